@@ -1,0 +1,143 @@
+// Shared helpers of the gfx950 kernels behind include/akb_raytrace.h.
+//
+// Every translation unit is compiled with -ffp-contract=off: the trace kernels reproduce numpy's
+// evaluation order operation by operation (each product and sum rounded on its own), which is
+// what makes them bit-identical to the reference's numpy expressions. Where an FMA is wanted
+// (Huygens complex accumulation, tolerance-checked) it is written explicitly.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string>
+
+#include "../../include/akb_raytrace.h"
+
+namespace akb {
+
+// thread-local last error, surfaced by akb_last_error()
+void set_error(const char* fmt, ...);
+void clear_error();
+
+#define AKB_HIP_CHECK(expr)                                                                  \
+    do {                                                                                     \
+        hipError_t _e = (expr);                                                              \
+        if (_e != hipSuccess) {                                                              \
+            ::akb::set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), __FILE__, \
+                             __LINE__);                                                      \
+            return AKB_E_HIP;                                                                \
+        }                                                                                    \
+    } while (0)
+
+#define AKB_REQUIRE(cond, msg)                                                    \
+    do {                                                                          \
+        if (!(cond)) {                                                            \
+            ::akb::set_error("invalid argument: %s (%s)", msg, #cond);            \
+            return AKB_E_INVALID;                                                 \
+        }                                                                         \
+    } while (0)
+
+// check the launch that was just issued
+inline int launch_status(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_error("launch of %s failed: %s", what, hipGetErrorString(e));
+        return AKB_E_HIP;
+    }
+    return AKB_OK;
+}
+
+constexpr int kBlock = 256;  // 4 waves of 64
+
+// Grid for a grid-stride elementwise kernel: enough workgroups to fill 256 CUs several times
+// over, capped so each thread still loops a few times on very large arrays.
+inline unsigned grid_for(int64_t n, int per_thread_min = 1) {
+    int64_t blocks = (n + (int64_t)kBlock * per_thread_min - 1) / ((int64_t)kBlock * per_thread_min);
+    if (blocks < 1) blocks = 1;
+    const int64_t cap = 256 * 16;  // 16 workgroups per CU
+    return (unsigned)(blocks > cap ? cap : blocks);
+}
+
+// 3-vector view of a (3, ld) SoA block with element increment inc (0 = broadcast)
+struct V3In {
+    const double* p;
+    int64_t ld;
+    int64_t inc;
+    __device__ __forceinline__ double x(int64_t i) const { return p[i * inc]; }
+    __device__ __forceinline__ double y(int64_t i) const { return p[ld + i * inc]; }
+    __device__ __forceinline__ double z(int64_t i) const { return p[2 * ld + i * inc]; }
+};
+struct V3Out {
+    double* p;
+    int64_t ld;
+    __device__ __forceinline__ void store(int64_t i, double x, double y, double z) const {
+        p[i] = x;
+        p[ld + i] = y;
+        p[2 * ld + i] = z;
+    }
+};
+
+struct Quadric {
+    double a, b, c, d, e, f, g, h, i, j;
+};
+
+inline Quadric quadric_from(const double* c) {
+    return Quadric{c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7], c[8], c[9]};
+}
+
+// ---- per-ray arithmetic, each in the reference's numpy association order ----
+
+// mirr_ray_intersection (EllipseRaytrace3D.py:23-43). Returns false when D <= 0 or NaN.
+__device__ __forceinline__ bool quadric_hit(const Quadric& Q, double l, double m, double n, double p,
+                                            double q, double r, bool negative, double& x, double& y,
+                                            double& z) {
+    const double A = Q.a * (l * l) + Q.b * (m * m) + Q.c * (n * n) + Q.d * m * l + Q.e * n * l +
+                     Q.f * m * n;
+    const double B = 2.0 * Q.a * p * l + 2.0 * Q.b * q * m + 2.0 * Q.c * r * n +
+                     Q.d * (p * m + q * l) + Q.e * (p * n + r * l) + Q.f * (r * m + q * n) +
+                     Q.g * l + Q.h * m + Q.i * n;
+    const double C = Q.a * (p * p) + Q.b * (q * q) + Q.c * (r * r) + Q.d * p * q + Q.e * p * r +
+                     Q.f * q * r + Q.g * p + Q.h * q + Q.i * r + Q.j;
+    const double D = B * B - 4.0 * A * C;
+    const double s = sqrt(D);
+    const double t = (negative ? (-B - s) : (-B + s)) / (2.0 * A);
+    x = t * l + p;
+    y = t * m + q;
+    z = t * n + r;
+    return D > 0.0;
+}
+
+// gradient of the quadric (norm_vector, EllipseRaytrace3D.py:66-68)
+__device__ __forceinline__ void quadric_grad(const Quadric& Q, double x, double y, double z, double& nx,
+                                             double& ny, double& nz) {
+    nx = 2.0 * Q.a * x + Q.d * y + Q.e * z + Q.g;
+    ny = 2.0 * Q.b * y + Q.d * x + Q.f * z + Q.h;
+    nz = 2.0 * Q.c * z + Q.e * x + Q.f * y + Q.i;
+}
+
+// np.linalg.norm(v, axis=0) for one column: sqrt((x*x + y*y) + z*z)
+__device__ __forceinline__ double norm3(double x, double y, double z) {
+    return sqrt(x * x + y * y + z * z);
+}
+
+// reflect_ray before normalisation (EllipseRaytrace3D.py:51-52)
+__device__ __forceinline__ void reflect_raw(double l, double m, double n, double nx, double ny,
+                                            double nz, double& rx, double& ry, double& rz) {
+    const double A = l * nx + m * ny + n * nz;
+    const double A2 = 2.0 * A;
+    rx = l - A2 * nx;
+    ry = m - A2 * ny;
+    rz = n - A2 * nz;
+}
+
+// plane_ray_intersection (EllipseRaytrace3D.py:150-155)
+__device__ __forceinline__ void plane_hit(double g, double h, double i, double j, double l, double m,
+                                          double n, double p, double q, double r, double& x,
+                                          double& y, double& z) {
+    const double t = -(g * p + h * q + i * r + j) / (g * l + h * m + i * n);
+    x = t * l + p;
+    y = t * m + q;
+    z = t * n + r;
+}
+
+}  // namespace akb

@@ -1,0 +1,186 @@
+// Huygens–Fresnel phase accumulation for gfx950 (the Wavecalc_raytrace_fromData hot loop).
+//
+//   u[i] = sum_j (u_j dS_j) * exp(-i k r_ij) / r_ij
+//   r_ij = sqrt(((x_i - x_j)^2 + (y_i - y_j)^2) + (z_i - z_j)^2)
+//
+// Reference: compute_u_parallel, Wavecalc_raytrace_fromData_CPU0402.py:71-85 (numba, one target
+// per prange iteration, vectorised over sources); the CuPy version materialises a B x M complex
+// matrix plus six temporaries per batch (Wavecalc_raytrace_fromData_GPU0402.py:112-120). Here
+// nothing is materialised: each lane owns kTPL targets and keeps their sums in registers while the
+// workgroup streams source tiles (x, y, z, Re u, Im u) through LDS, so HBM traffic is the source
+// set once per workgroup and the kernel is bound by FP64 VALU (sqrt, div, sincos per pair).
+//
+// r_ij is formed exactly as numpy forms it (no contraction), because k r ~ 7e10 rad: one ulp
+// of r moves the phase by ~1e-5 rad. The complex multiply-accumulate uses explicit FMAs
+// (tolerance-checked against the oracle, not bitwise: numpy's own sum order is pairwise).
+#include <math.h>
+
+#include "akb_common.h"
+
+namespace akb {
+
+constexpr int kHuyBlock = 256;
+constexpr int kHuyTile = 256;  // sources per LDS tile (5 doubles each = 10 KiB)
+constexpr int kTPL = 2;        // targets per lane
+
+__global__ void __launch_bounds__(kHuyBlock) k_huygens(const double* __restrict__ tx,
+                                                       const double* __restrict__ ty,
+                                                       const double* __restrict__ tz, int64_t n,
+                                                       const double* __restrict__ sx,
+                                                       const double* __restrict__ sy,
+                                                       const double* __restrict__ sz,
+                                                       const double* __restrict__ u, int64_t m,
+                                                       int64_t per_split, double negk,
+                                                       double* __restrict__ out) {
+    __shared__ double s_x[kHuyTile], s_y[kHuyTile], s_z[kHuyTile], s_ur[kHuyTile], s_ui[kHuyTile];
+    const int64_t base = (int64_t)blockIdx.x * (kHuyBlock * kTPL);
+    double px[kTPL], py[kTPL], pz[kTPL], ar[kTPL], ai[kTPL];
+#pragma unroll
+    for (int t = 0; t < kTPL; ++t) {
+        const int64_t i = base + threadIdx.x + t * kHuyBlock;
+        const bool ok = i < n;
+        px[t] = ok ? tx[i] : 0.0;
+        py[t] = ok ? ty[i] : 0.0;
+        pz[t] = ok ? tz[i] : 1.0e30;
+        ar[t] = 0.0;
+        ai[t] = 0.0;
+    }
+    // this workgroup's slice of the sources (blockIdx.y splits M so that small target sets
+    // still fill the 256 CUs; the partial sums are added in split order by k_huygens_reduce)
+    const int64_t jb = (int64_t)blockIdx.y * per_split;
+    const int64_t je = (jb + per_split) < m ? (jb + per_split) : m;
+    out += (int64_t)blockIdx.y * 2 * n;
+    for (int64_t j0 = jb; j0 < je; j0 += kHuyTile) {
+        const int cnt = (je - j0) < kHuyTile ? (int)(je - j0) : kHuyTile;
+        __syncthreads();
+        for (int s = threadIdx.x; s < cnt; s += kHuyBlock) {
+            const int64_t j = j0 + s;
+            s_x[s] = sx[j];
+            s_y[s] = sy[j];
+            s_z[s] = sz[j];
+            s_ur[s] = u[2 * j];
+            s_ui[s] = u[2 * j + 1];
+        }
+        __syncthreads();
+        for (int s = 0; s < cnt; ++s) {
+            const double xj = s_x[s], yj = s_y[s], zj = s_z[s], ur = s_ur[s], ui = s_ui[s];
+#pragma unroll
+            for (int t = 0; t < kTPL; ++t) {
+                const double dx = px[t] - xj;
+                const double dy = py[t] - yj;
+                const double dz = pz[t] - zj;
+                const double r = sqrt(dx * dx + dy * dy + dz * dz);
+                const double amp = 1.0 / r;
+                const double ph = negk * r;
+                double sn, cs;
+                sincos(ph, &sn, &cs);
+                const double fr = amp * cs;
+                const double fi = amp * sn;
+                ar[t] = __builtin_fma(fr, ur, __builtin_fma(-fi, ui, ar[t]));
+                ai[t] = __builtin_fma(fr, ui, __builtin_fma(fi, ur, ai[t]));
+            }
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < kTPL; ++t) {
+        const int64_t i = base + threadIdx.x + t * kHuyBlock;
+        if (i < n) {
+            out[2 * i] = ar[t];
+            out[2 * i + 1] = ai[t];
+        }
+    }
+}
+
+// out[i] = sum over splits, in split order
+__global__ void __launch_bounds__(kBlock) k_huygens_reduce(const double* part, int splits, int64_t n,
+                                                           double* out) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        double re = part[2 * i], im = part[2 * i + 1];
+        for (int s = 1; s < splits; ++s) {
+            re = re + part[(int64_t)s * 2 * n + 2 * i];
+            im = im + part[(int64_t)s * 2 * n + 2 * i + 1];
+        }
+        out[2 * i] = re;
+        out[2 * i + 1] = im;
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) k_scale_field(const double* u, const double* ds, int64_t m,
+                                                        double* out) {
+    for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < m;
+         j += (int64_t)gridDim.x * blockDim.x) {
+        // complex128 * float64 in numpy: (re*d - im*0, re*0 + im*d)
+        const double d = ds[j];
+        const double re = u[2 * j], im = u[2 * j + 1];
+        out[2 * j] = re * d - im * 0.0;
+        out[2 * j + 1] = re * 0.0 + im * d;
+    }
+}
+
+}  // namespace akb
+
+using namespace akb;
+
+// how many source splits a launch uses: enough workgroups to fill the chip (~8 per CU),
+// but at least kMinSplit sources per split
+static int huygens_splits(int64_t n, int64_t m) {
+    const int64_t per_block = (int64_t)kHuyBlock * kTPL;
+    const int64_t tblocks = (n + per_block - 1) / per_block;
+    const int64_t want = (2048 + tblocks - 1) / tblocks;
+    const int64_t kMinSplit = 1024;
+    int64_t maxs = (m + kMinSplit - 1) / kMinSplit;
+    if (maxs < 1) maxs = 1;
+    int64_t s = want < maxs ? want : maxs;
+    if (s > 65535) s = 65535;
+    return (int)(s < 1 ? 1 : s);
+}
+
+extern "C" {
+
+int64_t akb_huygens_work_bytes(int64_t n, int64_t m) {
+    if (n <= 0 || m <= 0) return 0;
+    const int s = huygens_splits(n, m);
+    return s > 1 ? (int64_t)s * 2 * n * (int64_t)sizeof(double) : 0;
+}
+
+int akb_huygens_f64(const double* tx, const double* ty, const double* tz, int64_t n,
+                    const double* sx, const double* sy, const double* sz, const double* u_re_im,
+                    int64_t m, double k, double* out_re_im, void* work, void* stream) {
+    clear_error();
+    AKB_REQUIRE(n >= 0 && m >= 0, "negative size");
+    if (n == 0) return AKB_OK;
+    AKB_REQUIRE(tx && ty && tz && out_re_im, "null target pointer");
+    hipStream_t s = (hipStream_t)stream;
+    if (m == 0) {
+        AKB_HIP_CHECK(hipMemsetAsync(out_re_im, 0, sizeof(double) * 2 * n, s));
+        return AKB_OK;
+    }
+    AKB_REQUIRE(sx && sy && sz && u_re_im, "null source pointer");
+    const int64_t per_block = (int64_t)kHuyBlock * kTPL;
+    const int64_t blocks = (n + per_block - 1) / per_block;
+    AKB_REQUIRE(blocks < (1LL << 31), "too many targets");
+    const int splits = huygens_splits(n, m);
+    AKB_REQUIRE(splits == 1 || work != nullptr, "work buffer required (akb_huygens_work_bytes)");
+    const int64_t per_split = (m + splits - 1) / splits;
+    double* dst = splits == 1 ? out_re_im : (double*)work;
+    // numpy's phase is (-k) * dist; negate the scalar once (exact)
+    k_huygens<<<dim3((unsigned)blocks, splits), kHuyBlock, 0, s>>>(tx, ty, tz, n, sx, sy, sz, u_re_im,
+                                                                   m, per_split, -k, dst);
+    int st = launch_status("k_huygens");
+    if (st || splits == 1) return st;
+    k_huygens_reduce<<<grid_for(n), kBlock, 0, s>>>(dst, splits, n, out_re_im);
+    return launch_status("k_huygens_reduce");
+}
+
+int akb_scale_field_f64(const double* u_re_im, const double* ds, int64_t m, double* out_re_im,
+                        void* stream) {
+    clear_error();
+    AKB_REQUIRE(m >= 0, "negative size");
+    if (m == 0) return AKB_OK;
+    AKB_REQUIRE(u_re_im && ds && out_re_im, "null pointer");
+    k_scale_field<<<grid_for(m), kBlock, 0, (hipStream_t)stream>>>(u_re_im, ds, m, out_re_im);
+    return launch_status("k_scale_field");
+}
+
+}  // extern "C"

@@ -1,0 +1,808 @@
+// Ray-trace kernels for gfx950: the reference's numpy primitives (one kernel each, the drop-in
+// stage API) and the fused mirror chain (device-resident API used by the AKB/KB pipelines).
+//
+// Layout: every ray quantity is struct-of-arrays float64, (3, ld) C-order, exactly the layout
+// of the reference's (3, N) numpy arrays (AKB_raytrace_20250312.py:2694-2717), so a wave's 64
+// lanes read 64 consecutive doubles of one row: fully coalesced 512-B segments per row.
+// Mirror coefficients travel in the kernel argument segment and are read with scalar loads
+// (wave-uniform, SGPR-resident), so the per-ray stream is only positions and directions.
+#include <math.h>
+
+#include <cstdarg>
+#include <mutex>
+
+#include "akb_common.h"
+
+namespace akb {
+
+static thread_local std::string g_last_error;
+
+void set_error(const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+}
+void clear_error() { g_last_error.clear(); }
+
+// ----------------------------------------------------------------------------------------------
+// stage kernels
+// ----------------------------------------------------------------------------------------------
+
+__global__ void __launch_bounds__(kBlock) k_isect(Quadric Q, V3In dir, V3In org, int negative,
+                                                  int64_t n, V3Out out, int32_t* flags) {
+    int fl = 0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        double x, y, z;
+        const bool ok = quadric_hit(Q, dir.x(i), dir.y(i), dir.z(i), org.x(i), org.y(i), org.z(i),
+                                    negative != 0, x, y, z);
+        if (!ok) fl |= AKB_FLAG_MISS;
+        out.store(i, x, y, z);
+    }
+    if (fl) atomicOr(flags, fl);
+}
+
+__global__ void __launch_bounds__(kBlock) k_normal(Quadric Q, V3In pt, int64_t n, V3Out out,
+                                                   int normalize, int32_t* flags) {
+    int fl = 0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        double nx, ny, nz;
+        quadric_grad(Q, pt.x(i), pt.y(i), pt.z(i), nx, ny, nz);
+        if (normalize) {
+            const double s = norm3(nx, ny, nz);
+            if (s == 0.0) fl |= AKB_FLAG_ZERO_NORMAL;
+            out.store(i, nx / s, ny / s, nz / s);
+        } else {
+            out.store(i, nx, ny, nz);
+        }
+    }
+    if (fl) atomicOr(flags, fl);
+}
+
+__global__ void __launch_bounds__(kBlock) k_reflect(V3In dir, V3In nrm, int64_t n, V3Out out,
+                                                    int normalize, int32_t* flags) {
+    int fl = 0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        double rx, ry, rz;
+        reflect_raw(dir.x(i), dir.y(i), dir.z(i), nrm.x(i), nrm.y(i), nrm.z(i), rx, ry, rz);
+        if (normalize) {
+            const double s = norm3(rx, ry, rz);
+            if (s == 0.0) fl |= AKB_FLAG_ZERO_REFLECT;
+            out.store(i, rx / s, ry / s, rz / s);
+        } else {
+            out.store(i, rx, ry, rz);
+        }
+    }
+    if (fl) atomicOr(flags, fl);
+}
+
+__global__ void __launch_bounds__(kBlock) k_normalize(V3In v, int64_t n, V3Out out, int32_t* flags) {
+    int fl = 0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const double x = v.x(i), y = v.y(i), z = v.z(i);
+        const double s = norm3(x, y, z);
+        if (s == 0.0) fl |= AKB_FLAG_ZERO_DIR;
+        out.store(i, x / s, y / s, z / s);
+    }
+    if (fl) atomicOr(flags, fl);
+}
+
+__global__ void __launch_bounds__(kBlock) k_plane(double g, double h, double ii, double j, V3In dir,
+                                                  V3In org, int64_t n, V3Out out) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        double x, y, z;
+        plane_hit(g, h, ii, j, dir.x(i), dir.y(i), dir.z(i), org.x(i), org.y(i), org.z(i), x, y, z);
+        out.store(i, x, y, z);
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) k_seglen(V3In a, V3In b, int64_t n, double* out) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        out[i] = norm3(b.x(i) - a.x(i), b.y(i) - a.y(i), b.z(i) - a.z(i));
+    }
+}
+
+struct Mat3 {
+    double m[9];
+};
+
+// R @ v for a 3x3 R in the order OpenBLAS dgemm forms it for the reference's (3,3) @ (3,N)
+// products (AKB_raytrace_20250312.py:929): r0*x, then fma(r1, y, .), then fma(r2, z, .)
+__device__ __forceinline__ void matvec(const Mat3& R, double x, double y, double z, double& ox,
+                                       double& oy, double& oz) {
+    ox = __builtin_fma(R.m[2], z, __builtin_fma(R.m[1], y, R.m[0] * x));
+    oy = __builtin_fma(R.m[5], z, __builtin_fma(R.m[4], y, R.m[3] * x));
+    oz = __builtin_fma(R.m[8], z, __builtin_fma(R.m[7], y, R.m[6] * x));
+}
+
+__global__ void __launch_bounds__(kBlock) k_rotate(Mat3 Ry, Mat3 Rz, double cx, double cy, double cz,
+                                                   int shift, V3In v, int64_t n, V3Out out) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        double x = v.x(i), y = v.y(i), z = v.z(i);
+        if (shift) {
+            x = x - cx;
+            y = y - cy;
+            z = z - cz;
+        }
+        double ax, ay, az, bx, by, bz;
+        matvec(Rz, x, y, z, ax, ay, az);
+        matvec(Ry, ax, ay, az, bx, by, bz);
+        if (shift) {
+            bx = bx + cx;
+            by = by + cy;
+            bz = bz + cz;
+        }
+        out.store(i, bx, by, bz);
+    }
+}
+
+__global__ void k_fill_nan(double* out, int64_t ld, int rows, int64_t n) {
+    const double qnan = __builtin_nan("");
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        for (int r = 0; r < rows; ++r) out[r * ld + i] = qnan;
+    }
+}
+
+// ----------------------------------------------------------------------------------------------
+// fused chain: K mirrors (+ detector plane + OPL) per ray, all intermediate state in registers
+// ----------------------------------------------------------------------------------------------
+
+struct ChainArgs {
+    int K;
+    int negmask;
+    Quadric q[AKB_MAX_MIRRORS];
+    double det[4];
+    const double* dir;
+    int64_t dir_ld, dir_inc;
+    const double* tan_h;
+    const double* tan_v;
+    int64_t n_h;
+    int64_t g0;  // global flat index of ray 0 of this launch
+    int64_t n;
+    const double* org;
+    int64_t org_ld, org_inc;
+    double src[3];
+    double* hits;
+    int64_t hits_ld;
+    double* last_hit;
+    int64_t last_hit_ld;
+    double* dir_out;
+    int64_t dir_out_ld;
+    double* det_out;
+    int64_t det_out_ld;
+    double* opl;
+    double* atan_h;
+    double* atan_v;
+    int64_t sh_begin, sh_end, sv_col;
+    double* samp_h;
+    double* samp_v;
+    int32_t* flags;
+};
+
+// Flag bit layout of the chain: mirror k uses bits 4k..4k+3 (MISS, ZERO_NORMAL, ZERO_REFLECT);
+// AKB_FLAG_CHAIN_DIR marks a zero-norm generated initial direction.
+
+template <bool kGrid, bool kOPL>
+__global__ void __launch_bounds__(kBlock) k_chain(ChainArgs a) {
+    int fl = 0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < a.n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t g = a.g0 + i;
+        double l, m, nn;
+        if (kGrid) {
+            // phai0[:, iv*n_h + ih] = (1, tan(p0h[ih]), tan(p0v[iv])) normalised (ref :2711-2717)
+            const int64_t iv = g / a.n_h;
+            const int64_t ih = g - iv * a.n_h;
+            const double th = a.tan_h[ih];
+            const double tv = a.tan_v[iv];
+            const double s = norm3(1.0, th, tv);
+            if (s == 0.0) fl |= AKB_FLAG_CHAIN_DIR;
+            l = 1.0 / s;
+            m = th / s;
+            nn = tv / s;
+        } else {
+            l = a.dir[i * a.dir_inc];
+            m = a.dir[a.dir_ld + i * a.dir_inc];
+            nn = a.dir[2 * a.dir_ld + i * a.dir_inc];
+        }
+        double p, q, r;
+        if (a.org) {
+            p = a.org[i * a.org_inc];
+            q = a.org[a.org_ld + i * a.org_inc];
+            r = a.org[2 * a.org_ld + i * a.org_inc];
+        } else {
+            p = a.src[0];
+            q = a.src[1];
+            r = a.src[2];
+        }
+        double opl = 0.0;
+#pragma unroll
+        for (int k = 0; k < AKB_MAX_MIRRORS; ++k) {
+            if (k >= a.K) break;
+            const Quadric& Q = a.q[k];
+            double x, y, z;
+            if (!quadric_hit(Q, l, m, nn, p, q, r, (a.negmask >> k) & 1, x, y, z))
+                fl |= AKB_FLAG_MISS << (4 * k);
+            if (kOPL) {
+                const double d = norm3(x - p, y - q, z - r);
+                opl = (k == 0) ? d : opl + d;
+            }
+            if (a.hits) {
+                double* h = a.hits + (int64_t)k * 3 * a.hits_ld;
+                h[i] = x;
+                h[a.hits_ld + i] = y;
+                h[2 * a.hits_ld + i] = z;
+            }
+            double nx, ny, nz;
+            quadric_grad(Q, x, y, z, nx, ny, nz);
+            const double sn = norm3(nx, ny, nz);
+            if (sn == 0.0) fl |= AKB_FLAG_ZERO_NORMAL << (4 * k);
+            nx = nx / sn;
+            ny = ny / sn;
+            nz = nz / sn;
+            double rx, ry, rz;
+            reflect_raw(l, m, nn, nx, ny, nz, rx, ry, rz);
+            const double sr = norm3(rx, ry, rz);
+            if (sr == 0.0) fl |= AKB_FLAG_ZERO_REFLECT << (4 * k);
+            l = rx / sr;
+            m = ry / sr;
+            nn = rz / sr;
+            p = x;
+            q = y;
+            r = z;
+        }
+        if (kOPL && a.opl) a.opl[i] = opl;
+        if (a.last_hit) {
+            a.last_hit[i] = p;
+            a.last_hit[a.last_hit_ld + i] = q;
+            a.last_hit[2 * a.last_hit_ld + i] = r;
+        }
+        if (a.dir_out) {
+            a.dir_out[i] = l;
+            a.dir_out[a.dir_out_ld + i] = m;
+            a.dir_out[2 * a.dir_out_ld + i] = nn;
+        }
+        if (a.det_out) {
+            double x, y, z;
+            plane_hit(a.det[0], a.det[1], a.det[2], a.det[3], l, m, nn, p, q, r, x, y, z);
+            a.det_out[i] = x;
+            a.det_out[a.det_out_ld + i] = y;
+            a.det_out[2 * a.det_out_ld + i] = z;
+        }
+        if (a.atan_h) a.atan_h[i] = atan(m / l);
+        if (a.atan_v) a.atan_v[i] = atan(nn / l);
+        // equal-angle resample samples: the slope ratios only; the host applies np.arctan so the
+        // resampled angle tables match the reference bit for bit (glibc atan, ref :2858-2859)
+        if (a.samp_h && g >= a.sh_begin && g < a.sh_end) a.samp_h[g - a.sh_begin] = m / l;
+        if (a.samp_v && kGrid) {
+            const int64_t iv = g / a.n_h;
+            if (g - iv * a.n_h == a.sv_col) a.samp_v[iv] = nn / l;
+        }
+    }
+    if (fl) atomicOr(a.flags, fl);
+}
+
+// ----------------------------------------------------------------------------------------------
+// tilt correction + detectors + OPL (ref AKB_raytrace_20250312.py:3583-3601, :3611-3633)
+// ----------------------------------------------------------------------------------------------
+
+struct TiltArgs {
+    Mat3 Ry, Rz;
+    double c[3];
+    double d1[4], d2[4];
+    const double* dir;
+    const double* pt;
+    const double* opl;
+    int64_t ld, n;
+    double* dir_rot;
+    double* pt_rot;
+    double* det1;
+    double* det2;
+    double* total1;
+    double* total2;
+};
+
+__global__ void __launch_bounds__(kBlock) k_tilt_opd(TiltArgs a) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < a.n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        double ax, ay, az;
+        double l, m, n;
+        matvec(a.Rz, a.dir[i], a.dir[a.ld + i], a.dir[2 * a.ld + i], ax, ay, az);
+        matvec(a.Ry, ax, ay, az, l, m, n);
+        double p, q, r;
+        matvec(a.Rz, a.pt[i] - a.c[0], a.pt[a.ld + i] - a.c[1], a.pt[2 * a.ld + i] - a.c[2], ax, ay,
+               az);
+        matvec(a.Ry, ax, ay, az, p, q, r);
+        p = p + a.c[0];
+        q = q + a.c[1];
+        r = r + a.c[2];
+        if (a.dir_rot) {
+            a.dir_rot[i] = l;
+            a.dir_rot[a.ld + i] = m;
+            a.dir_rot[2 * a.ld + i] = n;
+        }
+        if (a.pt_rot) {
+            a.pt_rot[i] = p;
+            a.pt_rot[a.ld + i] = q;
+            a.pt_rot[2 * a.ld + i] = r;
+        }
+        const double o = a.opl ? a.opl[i] : 0.0;
+        double x, y, z;
+        plane_hit(a.d1[0], a.d1[1], a.d1[2], a.d1[3], l, m, n, p, q, r, x, y, z);
+        if (a.det1) {
+            a.det1[i] = x;
+            a.det1[a.ld + i] = y;
+            a.det1[2 * a.ld + i] = z;
+        }
+        if (a.total1) a.total1[i] = o + norm3(x - p, y - q, z - r);
+        plane_hit(a.d2[0], a.d2[1], a.d2[2], a.d2[3], l, m, n, p, q, r, x, y, z);
+        if (a.det2) {
+            a.det2[i] = x;
+            a.det2[a.ld + i] = y;
+            a.det2[2 * a.ld + i] = z;
+        }
+        if (a.total2) a.total2[i] = o + norm3(x - p, y - q, z - r);
+    }
+}
+
+struct OpdArgs {
+    const double* t1;
+    double mean1;
+    const double* t2;
+    double mean2;
+    const double* det2;
+    int64_t ld, n;
+    double f[3];
+    double* e1;
+    double* e2;
+    double* sph;
+    double* wave;
+};
+
+__global__ void __launch_bounds__(kBlock) k_opd(OpdArgs a) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < a.n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        if (a.e1) a.e1[i] = (a.t1[i] - a.mean1) * 1e9;
+        double e2 = 0.0;
+        if (a.t2) e2 = (a.t2[i] - a.mean2) * 1e9;
+        if (a.e2) a.e2[i] = e2;
+        if (a.sph || a.wave) {
+            const double s =
+                norm3(a.det2[i] - a.f[0], a.det2[a.ld + i] - a.f[1], a.det2[2 * a.ld + i] - a.f[2]) * 1e9;
+            if (a.sph) a.sph[i] = s;
+            if (a.wave) a.wave[i] = e2 - s;
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------------------------
+// numpy-exact sum: np.add.reduce on a contiguous float64 row runs its inner loop on 8192-element
+// buffers, each summed by numpy's pairwise_sum (leaves of <= 128 elements with 8 accumulators,
+// split at n/2 rounded down to a multiple of 8), and adds the block results left to right.
+// One wave per 8192 block: lane 0 walks the split tree, the 64 lanes sum the leaves in
+// parallel, lane 0 combines them in tree order. A second kernel adds the blocks in order.
+// ----------------------------------------------------------------------------------------------
+
+constexpr int kPwBlock = 8192;
+constexpr int kPwMaxLeaves = 256;
+
+__device__ __forceinline__ int pw_split(int n) {
+    int n2 = n / 2;
+    return n2 - (n2 % 8);
+}
+
+__device__ __forceinline__ double pw_load(const double* a, int i, bool nan0, int& cnt) {
+    double v = a[i];
+    if (nan0) {
+        if (v != v) {
+            v = 0.0;
+        } else {
+            ++cnt;
+        }
+    } else {
+        ++cnt;
+    }
+    return v;
+}
+
+__device__ double pw_leaf(const double* a, int n, bool nan0, int& cnt) {
+    if (n < 8) {
+        double res = 0.0;
+        for (int i = 0; i < n; ++i) res = res + pw_load(a, i, nan0, cnt);
+        return res;
+    }
+    double r[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = pw_load(a, j, nan0, cnt);
+    int i = 8;
+    for (; i < n - (n % 8); i += 8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[j] = r[j] + pw_load(a, i + j, nan0, cnt);
+    }
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; ++i) res = res + pw_load(a, i, nan0, cnt);
+    return res;
+}
+
+__global__ void __launch_bounds__(64) k_pairwise_blocks(const double* x, int64_t ld, int64_t n,
+                                                        int nan0, double* block_sums,
+                                                        unsigned long long* counts, int nblocks) {
+    __shared__ int leaf_off[kPwMaxLeaves];
+    __shared__ int leaf_len[kPwMaxLeaves];
+    __shared__ double leaf_sum[kPwMaxLeaves];
+    __shared__ int n_leaves;
+    const int row = blockIdx.y;
+    const int blk = blockIdx.x;
+    const double* a = x + row * ld + (int64_t)blk * kPwBlock;
+    const int64_t rem = n - (int64_t)blk * kPwBlock;
+    const int len = rem < kPwBlock ? (int)rem : kPwBlock;
+    const int lane = threadIdx.x;
+
+    if (lane == 0) {
+        // depth-first walk of the split tree, recording leaves left to right
+        int st_off[16], st_len[16];
+        int sp = 0, nl = 0;
+        st_off[sp] = 0;
+        st_len[sp] = len;
+        ++sp;
+        while (sp > 0) {
+            --sp;
+            const int o = st_off[sp], l = st_len[sp];
+            if (l <= 128) {
+                leaf_off[nl] = o;
+                leaf_len[nl] = l;
+                ++nl;
+            } else {
+                const int l2 = pw_split(l);
+                // push right first so the left child is visited first
+                st_off[sp] = o + l2;
+                st_len[sp] = l - l2;
+                ++sp;
+                st_off[sp] = o;
+                st_len[sp] = l2;
+                ++sp;
+            }
+        }
+        n_leaves = nl;
+    }
+    __syncthreads();
+    int cnt = 0;
+    for (int li = lane; li < n_leaves; li += 64)
+        leaf_sum[li] = pw_leaf(a + leaf_off[li], leaf_len[li], nan0 != 0, cnt);
+    // count reduction across the wave
+    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_down(cnt, off);
+    __syncthreads();
+    if (lane == 0) {
+        // combine: post-order evaluation of the same tree
+        int st_len[16];
+        int st_state[16];
+        double st_left[16];
+        int sp = 0, li = 0;
+        double result = 0.0;
+        st_len[0] = len;
+        st_state[0] = 0;
+        sp = 1;
+        bool have = false;
+        while (sp > 0) {
+            const int t = sp - 1;
+            if (!have) {
+                if (st_len[t] <= 128) {
+                    result = leaf_sum[li++];
+                    have = true;
+                    --sp;
+                } else if (st_state[t] == 0) {
+                    st_state[t] = 1;
+                    st_len[sp] = pw_split(st_len[t]);
+                    st_state[sp] = 0;
+                    ++sp;
+                }
+            } else {
+                // `result` is the value of the child just finished, parent at t
+                if (st_state[t] == 1) {
+                    st_left[t] = result;
+                    st_state[t] = 2;
+                    have = false;
+                    st_len[sp] = st_len[t] - pw_split(st_len[t]);
+                    st_state[sp] = 0;
+                    ++sp;
+                } else {
+                    result = st_left[t] + result;
+                    --sp;
+                }
+            }
+        }
+        block_sums[row * nblocks + blk] = result;
+        atomicAdd(counts + row, (unsigned long long)cnt);
+    }
+}
+
+__global__ void k_pairwise_final(const double* block_sums, int nblocks, int rows, double* out) {
+    const int row = blockIdx.x * blockDim.x + threadIdx.x;
+    if (row >= rows) return;
+    double acc = block_sums[row * nblocks];
+    for (int b = 1; b < nblocks; ++b) acc = acc + block_sums[row * nblocks + b];
+    out[row] = acc;
+}
+
+}  // namespace akb
+
+// ==============================================================================================
+// C ABI
+// ==============================================================================================
+
+using namespace akb;
+
+static inline V3In v3in(const double* p, int64_t ld, int64_t inc) { return V3In{p, ld, inc}; }
+
+extern "C" {
+
+const char* akb_last_error(void) { return g_last_error.c_str(); }
+int akb_abi_version(void) { return AKB_ABI_VERSION; }
+int akb_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int akb_isect_f64(const double coeffs[10], const double* dir, int64_t dir_ld, int64_t dir_inc,
+                  const double* org, int64_t org_ld, int64_t org_inc, int negative, int64_t n,
+                  double* out, int64_t out_ld, int32_t* flags, void* stream) {
+    clear_error();
+    AKB_REQUIRE(coeffs && dir && org && out && flags, "null pointer");
+    AKB_REQUIRE(n >= 0, "n < 0");
+    if (n == 0) return AKB_OK;
+    k_isect<<<grid_for(n), kBlock, 0, (hipStream_t)stream>>>(
+        quadric_from(coeffs), v3in(dir, dir_ld, dir_inc), v3in(org, org_ld, org_inc), negative, n,
+        V3Out{out, out_ld}, flags);
+    return launch_status("k_isect");
+}
+
+int akb_normal_f64(const double coeffs[10], const double* pt, int64_t pt_ld, int64_t pt_inc, int64_t n,
+                   double* out, int64_t out_ld, int normalize, int32_t* flags, void* stream) {
+    clear_error();
+    AKB_REQUIRE(coeffs && pt && out && flags, "null pointer");
+    AKB_REQUIRE(n >= 0, "n < 0");
+    if (n == 0) return AKB_OK;
+    k_normal<<<grid_for(n), kBlock, 0, (hipStream_t)stream>>>(
+        quadric_from(coeffs), v3in(pt, pt_ld, pt_inc), n, V3Out{out, out_ld}, normalize, flags);
+    return launch_status("k_normal");
+}
+
+int akb_reflect_f64(const double* dir, int64_t dir_ld, int64_t dir_inc, const double* nrm,
+                    int64_t nrm_ld, int64_t nrm_inc, int64_t n, double* out, int64_t out_ld,
+                    int normalize, int32_t* flags, void* stream) {
+    clear_error();
+    AKB_REQUIRE(dir && nrm && out && flags, "null pointer");
+    AKB_REQUIRE(n >= 0, "n < 0");
+    if (n == 0) return AKB_OK;
+    k_reflect<<<grid_for(n), kBlock, 0, (hipStream_t)stream>>>(
+        v3in(dir, dir_ld, dir_inc), v3in(nrm, nrm_ld, nrm_inc), n, V3Out{out, out_ld}, normalize,
+        flags);
+    return launch_status("k_reflect");
+}
+
+int akb_normalize_f64(const double* v, int64_t v_ld, int64_t v_inc, int64_t n, double* out,
+                      int64_t out_ld, int32_t* flags, void* stream) {
+    clear_error();
+    AKB_REQUIRE(v && out && flags, "null pointer");
+    AKB_REQUIRE(n >= 0, "n < 0");
+    if (n == 0) return AKB_OK;
+    k_normalize<<<grid_for(n), kBlock, 0, (hipStream_t)stream>>>(v3in(v, v_ld, v_inc), n,
+                                                                 V3Out{out, out_ld}, flags);
+    return launch_status("k_normalize");
+}
+
+int akb_plane_isect_f64(const double ghij[4], const double* dir, int64_t dir_ld, int64_t dir_inc,
+                        const double* org, int64_t org_ld, int64_t org_inc, int64_t n, double* out,
+                        int64_t out_ld, void* stream) {
+    clear_error();
+    AKB_REQUIRE(ghij && dir && org && out, "null pointer");
+    AKB_REQUIRE(n >= 0, "n < 0");
+    if (n == 0) return AKB_OK;
+    k_plane<<<grid_for(n), kBlock, 0, (hipStream_t)stream>>>(
+        ghij[0], ghij[1], ghij[2], ghij[3], v3in(dir, dir_ld, dir_inc), v3in(org, org_ld, org_inc), n,
+        V3Out{out, out_ld});
+    return launch_status("k_plane");
+}
+
+int akb_seglen_f64(const double* a, int64_t a_ld, int64_t a_inc, const double* b, int64_t b_ld,
+                   int64_t b_inc, int64_t n, double* out, void* stream) {
+    clear_error();
+    AKB_REQUIRE(a && b && out, "null pointer");
+    AKB_REQUIRE(n >= 0, "n < 0");
+    if (n == 0) return AKB_OK;
+    k_seglen<<<grid_for(n), kBlock, 0, (hipStream_t)stream>>>(v3in(a, a_ld, a_inc),
+                                                              v3in(b, b_ld, b_inc), n, out);
+    return launch_status("k_seglen");
+}
+
+int akb_rotate_f64(const double ry[9], const double rz[9], const double center[3], const double* v,
+                   int64_t v_ld, int64_t v_inc, int64_t n, double* out, int64_t out_ld, void* stream) {
+    clear_error();
+    AKB_REQUIRE(ry && rz && v && out, "null pointer");
+    AKB_REQUIRE(n >= 0, "n < 0");
+    if (n == 0) return AKB_OK;
+    Mat3 Ry, Rz;
+    for (int k = 0; k < 9; ++k) {
+        Ry.m[k] = ry[k];
+        Rz.m[k] = rz[k];
+    }
+    const int shift = center != nullptr;
+    k_rotate<<<grid_for(n), kBlock, 0, (hipStream_t)stream>>>(
+        Ry, Rz, shift ? center[0] : 0.0, shift ? center[1] : 0.0, shift ? center[2] : 0.0, shift,
+        v3in(v, v_ld, v_inc), n, V3Out{out, out_ld});
+    return launch_status("k_rotate");
+}
+
+int akb_fill_nan_f64(double* out, int64_t ld, int rows, int64_t n, void* stream) {
+    clear_error();
+    AKB_REQUIRE(out && rows >= 0 && n >= 0, "bad fill arguments");
+    if (n == 0 || rows == 0) return AKB_OK;
+    k_fill_nan<<<grid_for(n), kBlock, 0, (hipStream_t)stream>>>(out, ld, rows, n);
+    return launch_status("k_fill_nan");
+}
+
+int akb_trace_chain_f64(const akb_chain_desc* d, void* stream) {
+    clear_error();
+    AKB_REQUIRE(d != nullptr, "null descriptor");
+    AKB_REQUIRE(d->n_mirrors >= 0 && d->n_mirrors <= AKB_MAX_MIRRORS, "n_mirrors out of range");
+    AKB_REQUIRE(d->n_rays >= 0, "n_rays < 0");
+    AKB_REQUIRE(d->flags != nullptr, "flags is null");
+    const bool grid = d->dir == nullptr;
+    if (grid) {
+        AKB_REQUIRE(d->tan_h && d->tan_v && d->n_h > 0 && d->n_v > 0, "grid tables missing");
+        AKB_REQUIRE(d->row0 >= 0 && d->row0 * d->n_h + d->n_rays <= d->n_h * d->n_v,
+                    "shard exceeds the ray grid");
+    }
+    if (d->samp_v) AKB_REQUIRE(grid && d->samp_v_col >= 0 && d->samp_v_col < d->n_h, "bad samp_v_col");
+    if (d->n_rays == 0) return AKB_OK;
+    ChainArgs a{};
+    a.K = d->n_mirrors;
+    a.negmask = 0;
+    for (int k = 0; k < d->n_mirrors; ++k) {
+        a.q[k] = quadric_from(d->coeffs[k]);
+        if (d->negative[k]) a.negmask |= 1 << k;
+    }
+    for (int k = 0; k < 4; ++k) a.det[k] = d->det_ghij[k];
+    a.dir = d->dir;
+    a.dir_ld = d->dir_ld;
+    a.dir_inc = d->dir_inc;
+    a.tan_h = d->tan_h;
+    a.tan_v = d->tan_v;
+    a.n_h = grid ? d->n_h : 1;
+    a.g0 = grid ? d->row0 * d->n_h : 0;
+    a.n = d->n_rays;
+    a.org = d->org;
+    a.org_ld = d->org_ld;
+    a.org_inc = d->org_inc;
+    for (int k = 0; k < 3; ++k) a.src[k] = d->src[k];
+    a.hits = d->hits;
+    a.hits_ld = d->hits_ld;
+    a.last_hit = d->last_hit;
+    a.last_hit_ld = d->last_hit_ld;
+    a.dir_out = d->dir_out;
+    a.dir_out_ld = d->dir_out_ld;
+    a.det_out = d->det_out;
+    a.det_out_ld = d->det_out_ld;
+    a.opl = d->opl;
+    a.atan_h = d->atan_h;
+    a.atan_v = d->atan_v;
+    a.sh_begin = d->samp_h ? d->samp_h_begin : 0;
+    a.sh_end = d->samp_h ? d->samp_h_end : 0;
+    a.sv_col = d->samp_v_col;
+    a.samp_h = d->samp_h;
+    a.samp_v = d->samp_v;
+    a.flags = d->flags;
+    const unsigned gsz = grid_for(d->n_rays);
+    hipStream_t s = (hipStream_t)stream;
+    if (grid) {
+        if (d->opl)
+            k_chain<true, true><<<gsz, kBlock, 0, s>>>(a);
+        else
+            k_chain<true, false><<<gsz, kBlock, 0, s>>>(a);
+    } else {
+        if (d->opl)
+            k_chain<false, true><<<gsz, kBlock, 0, s>>>(a);
+        else
+            k_chain<false, false><<<gsz, kBlock, 0, s>>>(a);
+    }
+    return launch_status("k_chain");
+}
+
+int akb_tilt_opd_f64(const double ry[9], const double rz[9], const double center[3],
+                     const double det1_ghij[4], const double det2_ghij[4], const double* dir,
+                     const double* pt, const double* opl, int64_t ld, int64_t n, double* dir_rot,
+                     double* pt_rot, double* det1, double* det2, double* total1, double* total2,
+                     void* stream) {
+    clear_error();
+    AKB_REQUIRE(ry && rz && center && det1_ghij && det2_ghij && dir && pt, "null pointer");
+    AKB_REQUIRE(n >= 0 && ld >= n, "bad sizes");
+    if (n == 0) return AKB_OK;
+    TiltArgs a{};
+    for (int k = 0; k < 9; ++k) {
+        a.Ry.m[k] = ry[k];
+        a.Rz.m[k] = rz[k];
+    }
+    for (int k = 0; k < 3; ++k) a.c[k] = center[k];
+    for (int k = 0; k < 4; ++k) {
+        a.d1[k] = det1_ghij[k];
+        a.d2[k] = det2_ghij[k];
+    }
+    a.dir = dir;
+    a.pt = pt;
+    a.opl = opl;
+    a.ld = ld;
+    a.n = n;
+    a.dir_rot = dir_rot;
+    a.pt_rot = pt_rot;
+    a.det1 = det1;
+    a.det2 = det2;
+    a.total1 = total1;
+    a.total2 = total2;
+    k_tilt_opd<<<grid_for(n), kBlock, 0, (hipStream_t)stream>>>(a);
+    return launch_status("k_tilt_opd");
+}
+
+int akb_opd_f64(const double* total1, double mean1, const double* total2, double mean2,
+                const double* det2, int64_t ld, const double mean_focus[3], int64_t n,
+                double* dist_err1, double* dist_err2, double* sph, double* wave, void* stream) {
+    clear_error();
+    AKB_REQUIRE(n >= 0, "n < 0");
+    AKB_REQUIRE(!dist_err1 || total1, "dist_err1 needs total1");
+    AKB_REQUIRE(!(dist_err2 || wave) || total2, "dist_err2/wave need total2");
+    AKB_REQUIRE(!(sph || wave) || (det2 && mean_focus), "sph/wave need det2 and mean_focus");
+    if (n == 0) return AKB_OK;
+    OpdArgs a{};
+    a.t1 = total1;
+    a.mean1 = mean1;
+    a.t2 = total2;
+    a.mean2 = mean2;
+    a.det2 = det2;
+    a.ld = ld;
+    a.n = n;
+    for (int k = 0; k < 3; ++k) a.f[k] = mean_focus ? mean_focus[k] : 0.0;
+    a.e1 = dist_err1;
+    a.e2 = dist_err2;
+    a.sph = sph;
+    a.wave = wave;
+    k_opd<<<grid_for(n), kBlock, 0, (hipStream_t)stream>>>(a);
+    return launch_status("k_opd");
+}
+
+int64_t akb_pairwise_work_bytes(int rows, int64_t n) {
+    const int64_t nb = n <= 0 ? 1 : (n + kPwBlock - 1) / kPwBlock;
+    return (int64_t)rows * nb * (int64_t)sizeof(double);
+}
+
+int akb_pairwise_sum_f64(const double* x, int64_t ld, int rows, int64_t n, int nan_to_zero,
+                         double* d_sum, int64_t* d_count, void* d_work, void* stream) {
+    clear_error();
+    AKB_REQUIRE(x && d_sum && d_count && d_work, "null pointer");
+    AKB_REQUIRE(rows > 0 && rows <= 65535 && n >= 0, "bad sizes");
+    hipStream_t s = (hipStream_t)stream;
+    AKB_HIP_CHECK(hipMemsetAsync(d_count, 0, sizeof(int64_t) * rows, s));
+    if (n == 0) {
+        AKB_HIP_CHECK(hipMemsetAsync(d_sum, 0, sizeof(double) * rows, s));
+        return AKB_OK;
+    }
+    const int nb = (int)((n + kPwBlock - 1) / kPwBlock);
+    double* bsum = (double*)d_work;
+    k_pairwise_blocks<<<dim3(nb, rows), 64, 0, s>>>(x, ld, n, nan_to_zero, bsum,
+                                                    (unsigned long long*)d_count, nb);
+    int st = launch_status("k_pairwise_blocks");
+    if (st) return st;
+    k_pairwise_final<<<(rows + 63) / 64, 64, 0, s>>>(bsum, nb, rows, d_sum);
+    return launch_status("k_pairwise_final");
+}
+
+}  // extern "C"

@@ -1,0 +1,207 @@
+/*
+ * akb_raytrace.h — C ABI of the MI355X-native AKB ray-trace / wavefront / PSF hot path.
+ *
+ * One shared library, akbraytracing_amd/lib/libakb_hip.so, built by hipcc for gfx950.
+ * Every entry point:
+ *   - takes plain pointers and sizes (no torch / numpy types),
+ *   - treats every array pointer as DEVICE memory unless the name says host,
+ *   - is stream-ordered on the hipStream_t passed as `void* stream` (NULL = default stream),
+ *   - returns 0 on success or a negative AKB_E* code; akb_last_error() gives the message
+ *     (thread-local, valid until the next call on the same thread). No C++ exception crosses it.
+ *
+ * Arrays of 3-vectors use the reference's struct-of-arrays layout: a (3, N) float64 C-order
+ * block, row k (x/y/z) at base + k*ld, element i at + i*inc. inc = 0 broadcasts one vector
+ * (the reference's `ray` of shape (3,)). ld = N, inc = 1 is the plain numpy (3, N) array.
+ *
+ * Reference interface each entry point replaces (file:line under Kakekakechan/AKBRaytracing):
+ *   akb_isect_f64        mirr_ray_intersection   EllipseRaytrace3D.py:18-45, AKB_raytrace_20250312.py:444-471
+ *   akb_normal_f64       norm_vector             EllipseRaytrace3D.py:61-71, AKB_raytrace_20250312.py:626-636
+ *   akb_reflect_f64      reflect_ray             EllipseRaytrace3D.py:47-55, AKB_raytrace_20250312.py:501-509
+ *   akb_normalize_f64    normalize_vector        EllipseRaytrace3D.py:57-59, AKB_raytrace_20250312.py:530-532
+ *   akb_plane_isect_f64  plane_ray_intersection  EllipseRaytrace3D.py:145-157, AKB_raytrace_20250312.py:873-885
+ *   akb_seglen_f64       np.linalg.norm(b-a, axis=0)  AKB_raytrace_20250312.py:2884-2897, :3623, :3630
+ *   akb_rotate_f64       rotate_vectors / rotate_points  AKB_raytrace_20250312.py:917-943
+ *   akb_trace_chain_f64  the pass-1 / pass-2 mirror chains of plot_result_debug
+ *                        AKB_raytrace_20250312.py:2694-2717 (ray grid), :2770-2845 (pass 1),
+ *                        :2881-2905 (pass 2 + OPL segments); KB_debug :10952-10997
+ *   akb_tilt_opd_f64     tilt correction + detector + OPL/OPD, AKB_raytrace_20250312.py:3583-3601, :3611-3677
+ *   akb_pairwise_sum_f64 np.sum / np.mean / np.nanmean as used at :3583-3591, :3626, :3633, :3674
+ *   akb_huygens_f64      compute_u_parallel / forward_propagation_*_batch
+ *                        Wavecalc_raytrace_fromData_CPU0402.py:71-124, ..._GPU0402.py:64-201
+ *   akb_psf_f64          compute_psf_fft         psf_fft.py:29-125 (FFT on rocFFT)
+ */
+#ifndef AKB_RAYTRACE_H
+#define AKB_RAYTRACE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AKB_ABI_VERSION 1
+
+/* status codes */
+#define AKB_OK 0
+#define AKB_E_INVALID (-1)   /* bad argument (shape, pointer, size) */
+#define AKB_E_HIP (-2)       /* HIP runtime error */
+#define AKB_E_FFT (-3)       /* rocFFT error */
+#define AKB_E_NOMEM (-4)     /* allocation failed */
+
+/* bits of the device int32 `flags` word written by the trace kernels */
+#define AKB_FLAG_MISS 0x1          /* some ray had discriminant D <= 0 (or NaN): ref :457 all-NaN rule */
+#define AKB_FLAG_ZERO_NORMAL 0x2   /* some surface normal had zero norm: ref :530-532 passthrough rule */
+#define AKB_FLAG_ZERO_REFLECT 0x4  /* some reflected direction had zero norm */
+#define AKB_FLAG_ZERO_DIR 0x8      /* some generated initial direction had zero norm */
+/* akb_trace_chain_f64 shifts the MISS/ZERO bits of mirror k by 4*k (k < 7); bit 28
+ * (AKB_FLAG_CHAIN_DIR) marks a zero-norm generated initial direction */
+#define AKB_FLAG_CHAIN_DIR (1 << 28)
+
+const char* akb_last_error(void);
+int akb_abi_version(void);
+/* number of visible HIP devices (0 on a host without GPU; never fails) */
+int akb_device_count(void);
+
+/* ---------------- stage primitives (drop-in boundary, one reference call each) ---------------- */
+
+/* mirr_ray_intersection: point = t*dir + org, t = (-B +- sqrt(B^2-4AC)) / (2A), minus root when
+ * negative != 0. Writes `out` for every ray and ORs AKB_FLAG_MISS into *flags if any D <= 0;
+ * the caller then replaces the whole output by NaN (reference :457-459). */
+int akb_isect_f64(const double coeffs[10], const double* dir, int64_t dir_ld, int64_t dir_inc,
+                  const double* org, int64_t org_ld, int64_t org_inc, int negative, int64_t n,
+                  double* out, int64_t out_ld, int32_t* flags, void* stream);
+
+/* norm_vector: gradient of the quadric at `pt`, normalised. normalize=1 writes the unit normal
+ * and ORs AKB_FLAG_ZERO_NORMAL if any norm == 0; normalize=0 writes the raw gradient (the
+ * reference's passthrough when any norm is zero). */
+int akb_normal_f64(const double coeffs[10], const double* pt, int64_t pt_ld, int64_t pt_inc, int64_t n,
+                   double* out, int64_t out_ld, int normalize, int32_t* flags, void* stream);
+
+/* reflect_ray: phai = dir - 2 (dir.N) N, normalised as akb_normal_f64 (AKB_FLAG_ZERO_REFLECT). */
+int akb_reflect_f64(const double* dir, int64_t dir_ld, int64_t dir_inc, const double* nrm,
+                    int64_t nrm_ld, int64_t nrm_inc, int64_t n, double* out, int64_t out_ld,
+                    int normalize, int32_t* flags, void* stream);
+
+/* normalize_vector: out = v / ||v|| ; ORs AKB_FLAG_ZERO_DIR if any ||v|| == 0 (caller keeps v). */
+int akb_normalize_f64(const double* v, int64_t v_ld, int64_t v_inc, int64_t n, double* out,
+                      int64_t out_ld, int32_t* flags, void* stream);
+
+/* plane_ray_intersection with plane g x + h y + i z + j = 0 (coeffs[6:10]); per-ray inf/NaN. */
+int akb_plane_isect_f64(const double ghij[4], const double* dir, int64_t dir_ld, int64_t dir_inc,
+                        const double* org, int64_t org_ld, int64_t org_inc, int64_t n, double* out,
+                        int64_t out_ld, void* stream);
+
+/* out[i] = sqrt(((bx-ax)^2 + (by-ay)^2) + (bz-az)^2) */
+int akb_seglen_f64(const double* a, int64_t a_ld, int64_t a_inc, const double* b, int64_t b_ld,
+                   int64_t b_inc, int64_t n, double* out, void* stream);
+
+/* out = Ry @ (Rz @ (v - c)) + c with c = center (host 3-vector, or NULL for rotate_vectors).
+ * ry, rz: host row-major 3x3 matrices. Each product row is fma(r2, v2, fma(r1, v1, r0*v0)),
+ * the order OpenBLAS dgemm uses for the reference's matmul. */
+int akb_rotate_f64(const double ry[9], const double rz[9], const double center[3], const double* v,
+                   int64_t v_ld, int64_t v_inc, int64_t n, double* out, int64_t out_ld, void* stream);
+
+/* fill rows x n of `out` (row stride ld) with quiet NaN */
+int akb_fill_nan_f64(double* out, int64_t ld, int rows, int64_t n, void* stream);
+
+/* ---------------- fused chain (device-resident API) ---------------- */
+
+#define AKB_MAX_MIRRORS 7
+
+typedef struct akb_chain_desc {
+    int32_t n_mirrors;                       /* K <= AKB_MAX_MIRRORS */
+    int32_t negative[AKB_MAX_MIRRORS];       /* minus root per mirror (ref :2820 H-hyperboloid) */
+    double coeffs[AKB_MAX_MIRRORS][10];      /* quadric a..j per mirror, in trace order */
+    double det_ghij[4];                      /* detector plane for det_out */
+    /* initial rays: either explicit (dir != NULL) or generated on the grid
+     * dir[:, iv*n_h + ih] = normalize(1, tan_h[ih], tan_v[iv])   (ref :2711-2717) */
+    const double* dir; int64_t dir_ld; int64_t dir_inc;
+    const double* tan_h; const double* tan_v; int64_t n_h; int64_t n_v;
+    int64_t row0;                            /* first V-row of this shard (multi-GPU) */
+    int64_t n_rays;                          /* rays in this launch */
+    const double* org; int64_t org_ld; int64_t org_inc; /* NULL => constant source src[] */
+    double src[3];
+    /* outputs (any may be NULL) */
+    double* hits; int64_t hits_ld;           /* K blocks of (3, hits_ld): mirror hit points */
+    double* last_hit; int64_t last_hit_ld;   /* (3, ld) point on the last mirror */
+    double* dir_out; int64_t dir_out_ld;     /* (3, ld) direction after the last mirror */
+    double* det_out; int64_t det_out_ld;     /* (3, ld) hit on det_ghij */
+    double* opl;                             /* (n): ((d01 + d12) + d23) + ... left to right */
+    double* atan_h; double* atan_v;          /* (n): arctan(Ry/Rx), arctan(Rz/Rx) of dir_out */
+    /* exit-slope samples for the equal-angle resample (ref :2849-2870); the caller applies
+     * np.arctan on the host so the resampled tables stay bit-identical to the reference */
+    int64_t samp_h_begin; int64_t samp_h_end; /* flat ray range -> samp_h[i - begin] = Ry/Rx */
+    int64_t samp_v_col;                       /* column ih -> samp_v[iv] = Rz/Rx */
+    double* samp_h; double* samp_v;
+    int32_t* flags;                           /* device int32, OR-ed */
+} akb_chain_desc;
+
+int akb_trace_chain_f64(const akb_chain_desc* desc, void* stream);
+
+/* tilt + detectors + OPL (ref :3583-3601, :3611-3633):
+ *   r' = Ry@(Rz@r), p' = Ry@(Rz@(p - c)) + c
+ *   det1 = plane(det1_ghij, r', p'), det2 = plane(det2_ghij, r', p')
+ *   total1 = opl + ||det1 - p'||, total2 = opl + ||det2 - p'||
+ * Any output may be NULL. */
+int akb_tilt_opd_f64(const double ry[9], const double rz[9], const double center[3],
+                     const double det1_ghij[4], const double det2_ghij[4], const double* dir,
+                     const double* pt, const double* opl, int64_t ld, int64_t n, double* dir_rot,
+                     double* pt_rot, double* det1, double* det2, double* total1, double* total2,
+                     void* stream);
+
+/* OPD maps (ref :3626, :3633, :3675-3677):
+ *   dist_err  = (total - mean_total) * 1e9
+ *   sph       = ||det2 - mean_focus|| * 1e9
+ *   wave      = dist_err2 - sph                                   (NULL outputs skipped) */
+int akb_opd_f64(const double* total1, double mean1, const double* total2, double mean2,
+                const double* det2, int64_t ld, const double mean_focus[3], int64_t n,
+                double* dist_err1, double* dist_err2, double* sph, double* wave, void* stream);
+
+/* numpy-exact reduction: for each of `rows` rows of length n (row stride ld),
+ * sum = the value np.sum gives (8192-element blocks, pairwise within a block, blocks added left
+ * to right), count = number of summed elements. nan_to_zero=1 reproduces np.nansum/np.nanmean
+ * (NaN -> 0, count excludes NaN). d_work: device scratch of akb_pairwise_work_bytes(rows, n).
+ * Results: d_sum[rows], d_count[rows] (device). */
+int64_t akb_pairwise_work_bytes(int rows, int64_t n);
+int akb_pairwise_sum_f64(const double* x, int64_t ld, int rows, int64_t n, int nan_to_zero,
+                         double* d_sum, int64_t* d_count, void* d_work, void* stream);
+
+/* ---------------- Huygens-Fresnel phase accumulation ---------------- */
+
+/* out[i] = sum_j u_j * exp(-i k r_ij) / r_ij,  r_ij = sqrt(((xi-xj)^2 + (yi-yj)^2) + (zi-zj)^2)
+ * u_j = u_re_im[2j] + i u_re_im[2j+1] already multiplied by dS_j (ref CPU0402 :102).
+ * out_re_im: interleaved complex128 (N). work: device scratch of akb_huygens_work_bytes(n, m)
+ * bytes (the sources are split over workgroups when the target set alone cannot fill the chip;
+ * the partial sums are added in split order, so results are run-to-run deterministic). */
+int64_t akb_huygens_work_bytes(int64_t n, int64_t m);
+int akb_huygens_f64(const double* tx, const double* ty, const double* tz, int64_t n,
+                    const double* sx, const double* sy, const double* sz, const double* u_re_im,
+                    int64_t m, double k, double* out_re_im, void* work, void* stream);
+/* u_out = u_in * ds (complex * real, ref CPU0402 :102 / GPU0402 :142) */
+int akb_scale_field_f64(const double* u_re_im, const double* ds, int64_t m, double* out_re_im,
+                        void* stream);
+
+/* ---------------- PSF by FFT (rocFFT) ---------------- */
+
+/* compute_psf_fft for a stack of `batch` wavelengths over one pupil:
+ *   opd, amp: (ny, nx) float64 device arrays (NaN/inf -> 0)
+ *   lambdas: host array of `batch` wavelengths
+ *   hann_wy (ny) / hann_wx (nx) / hann_max: separable window or NULL (ref psf_fft.py:20-27)
+ *   py = ny' * pad, px = nx' * pad with ny' = ny + ny%2 (ensure_even_size)
+ *   psf: (batch, py, px) normalised intensity; efield_re_im: (batch, py, px) complex or NULL
+ *   d_imax: device array of `batch` peak intensities before normalisation
+ *   work: device scratch of akb_psf_work_bytes(...) (pupil field + rocFFT work area) */
+int64_t akb_psf_work_bytes(int ny, int nx, int pad, int batch);
+int akb_psf_f64(const double* opd, const double* amp, int ny, int nx, int pad, int batch,
+                const double* lambdas, double dx, double dy, const double* hann_wy,
+                const double* hann_wx, double hann_max, double* psf, double* efield_re_im,
+                double* d_imax, void* work, void* stream);
+
+/* release cached rocFFT plans (also done at unload) */
+void akb_psf_release_plans(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* AKB_RAYTRACE_H */
