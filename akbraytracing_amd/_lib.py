@@ -1,0 +1,127 @@
+"""ctypes binding of libakb_hip.so (declarations mirror include/akb_raytrace.h one for one).
+
+The library is loaded lazily on first use. torch is imported first so the process uses torch's
+HIP runtime (libamdhip64.so.7 is matched by SONAME), which keeps the device pointers and stream
+handles that torch hands us valid inside the library.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+from . import build as _build
+
+_LIB = None
+
+c_i32 = ctypes.c_int32
+c_i64 = ctypes.c_int64
+c_int = ctypes.c_int
+c_dbl = ctypes.c_double
+c_vp = ctypes.c_void_p
+MAX_MIRRORS = 7
+
+FLAG_MISS = 0x1
+FLAG_ZERO_NORMAL = 0x2
+FLAG_ZERO_REFLECT = 0x4
+FLAG_ZERO_DIR = 0x8
+FLAG_CHAIN_DIR = 1 << 28
+
+# every symbol the header declares (tests check the library exports all of them)
+EXPORTS = [
+    "akb_last_error", "akb_abi_version", "akb_device_count",
+    "akb_isect_f64", "akb_normal_f64", "akb_reflect_f64", "akb_normalize_f64", "akb_plane_isect_f64",
+    "akb_seglen_f64", "akb_rotate_f64", "akb_fill_nan_f64",
+    "akb_trace_chain_f64", "akb_chain_desc_size", "akb_tilt_opd_f64", "akb_opd_f64",
+    "akb_pairwise_work_bytes", "akb_pairwise_sum_f64",
+    "akb_huygens_work_bytes", "akb_huygens_f64", "akb_scale_field_f64",
+    "akb_psf_work_bytes", "akb_psf_f64", "akb_psf_release_plans",
+]
+
+
+class ChainDesc(ctypes.Structure):
+    """akb_chain_desc"""
+    _fields_ = [
+        ("n_mirrors", c_i32),
+        ("negative", c_i32 * MAX_MIRRORS),
+        ("coeffs", (c_dbl * 10) * MAX_MIRRORS),
+        ("det_ghij", c_dbl * 4),
+        ("dir", c_vp), ("dir_ld", c_i64), ("dir_inc", c_i64),
+        ("tan_h", c_vp), ("tan_v", c_vp), ("n_h", c_i64), ("n_v", c_i64),
+        ("row0", c_i64),
+        ("n_rays", c_i64),
+        ("org", c_vp), ("org_ld", c_i64), ("org_inc", c_i64),
+        ("src", c_dbl * 3),
+        ("hits", c_vp), ("hits_ld", c_i64),
+        ("last_hit", c_vp), ("last_hit_ld", c_i64),
+        ("dir_out", c_vp), ("dir_out_ld", c_i64),
+        ("det_out", c_vp), ("det_out_ld", c_i64),
+        ("opl", c_vp),
+        ("atan_h", c_vp), ("atan_v", c_vp),
+        ("samp_h_begin", c_i64), ("samp_h_end", c_i64),
+        ("samp_v_col", c_i64),
+        ("samp_h", c_vp), ("samp_v", c_vp),
+        ("flags", c_vp),
+    ]
+
+
+class AKBError(RuntimeError):
+    pass
+
+
+def _declare(L):
+    v3 = [c_vp, c_i64, c_i64]
+    sig = {
+        "akb_last_error": ([], ctypes.c_char_p),
+        "akb_abi_version": ([], c_int),
+        "akb_device_count": ([], c_int),
+        "akb_isect_f64": ([c_vp] + v3 + v3 + [c_int, c_i64, c_vp, c_i64, c_vp, c_vp], c_int),
+        "akb_normal_f64": ([c_vp] + v3 + [c_i64, c_vp, c_i64, c_int, c_vp, c_vp], c_int),
+        "akb_reflect_f64": (v3 + v3 + [c_i64, c_vp, c_i64, c_int, c_vp, c_vp], c_int),
+        "akb_normalize_f64": (v3 + [c_i64, c_vp, c_i64, c_vp, c_vp], c_int),
+        "akb_plane_isect_f64": ([c_vp] + v3 + v3 + [c_i64, c_vp, c_i64, c_vp], c_int),
+        "akb_seglen_f64": (v3 + v3 + [c_i64, c_vp, c_vp], c_int),
+        "akb_rotate_f64": ([c_vp, c_vp, c_vp] + v3 + [c_i64, c_vp, c_i64, c_vp], c_int),
+        "akb_fill_nan_f64": ([c_vp, c_i64, c_int, c_i64, c_vp], c_int),
+        "akb_trace_chain_f64": ([ctypes.POINTER(ChainDesc), c_vp], c_int),
+        "akb_chain_desc_size": ([], c_i64),
+        "akb_tilt_opd_f64": ([c_vp] * 5 + [c_vp, c_vp, c_vp, c_i64, c_i64] + [c_vp] * 6 + [c_vp], c_int),
+        "akb_opd_f64": ([c_vp, c_dbl, c_vp, c_dbl, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp],
+                        c_int),
+        "akb_pairwise_work_bytes": ([c_int, c_i64], c_i64),
+        "akb_pairwise_sum_f64": ([c_vp, c_i64, c_int, c_i64, c_int, c_vp, c_vp, c_vp, c_vp], c_int),
+        "akb_huygens_work_bytes": ([c_i64, c_i64], c_i64),
+        "akb_huygens_f64": ([c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_dbl, c_vp, c_vp, c_vp],
+                            c_int),
+        "akb_scale_field_f64": ([c_vp, c_vp, c_i64, c_vp, c_vp], c_int),
+        "akb_psf_work_bytes": ([c_int, c_int, c_int, c_int], c_i64),
+        "akb_psf_f64": ([c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_dbl, c_dbl, c_vp, c_vp, c_dbl, c_vp,
+                         c_vp, c_vp, c_vp, c_vp], c_int),
+        "akb_psf_release_plans": ([], None),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+
+
+def lib():
+    """The loaded library. Raises (never falls back) when it is missing or cannot load."""
+    global _LIB
+    if _LIB is None:
+        path = _build.SO
+        if not os.path.exists(path):
+            raise AKBError(
+                f"{path} is missing: build the HIP extension first (python -m akbraytracing_amd.build "
+                "or __graft_entry__.build()); there is no CPU fallback")
+        L = ctypes.CDLL(path)
+        _declare(L)
+        if L.akb_chain_desc_size() != ctypes.sizeof(ChainDesc):
+            raise AKBError("akb_chain_desc layout mismatch between include/akb_raytrace.h and _lib.py")
+        _LIB = L
+    return _LIB
+
+
+def check(status):
+    if status != 0:
+        msg = lib().akb_last_error()
+        raise AKBError(f"libakb_hip error {status}: {msg.decode() if msg else ''}")

@@ -1,0 +1,52 @@
+"""Build libakb_hip.so (the C ABI of include/akb_raytrace.h) for gfx950 with hipcc, in-tree.
+
+    python -m akbraytracing_amd.build
+
+The library is compiled with -ffp-contract=off: the trace kernels depend on every product and
+sum being rounded separately, in numpy's order, to reproduce the reference bit for bit.
+"""
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIBDIR = os.path.join(PKG, "lib")
+SO = os.path.join(LIBDIR, "libakb_hip.so")
+SOURCES = ["akb_trace.hip", "akb_huygens.hip", "akb_psf.hip"]
+HEADERS = ["akb_common.h", os.path.join("..", "..", "include", "akb_raytrace.h")]
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+ARCH = os.environ.get("AKB_OFFLOAD_ARCH", "gfx950")
+
+
+def _newest(paths):
+    return max(os.path.getmtime(p) for p in paths)
+
+
+def needs_build():
+    if not os.path.exists(SO):
+        return True
+    deps = [os.path.join(CSRC, s) for s in SOURCES] + [os.path.join(CSRC, h) for h in HEADERS]
+    return _newest(deps) > os.path.getmtime(SO)
+
+
+def build(force=False, verbose=True):
+    if not force and not needs_build():
+        return SO
+    os.makedirs(LIBDIR, exist_ok=True)
+    hipcc = os.path.join(ROCM, "bin", "hipcc")
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
+           "-Wall", "-Wno-unused-function", "-o", SO + ".tmp"]
+    cmd += [os.path.join(CSRC, s) for s in SOURCES]
+    cmd += [f"-L{ROCM}/lib", "-lrocfft", f"-Wl,-rpath,{ROCM}/lib"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(SO + ".tmp", SO)
+    return SO
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)
+    print(SO)

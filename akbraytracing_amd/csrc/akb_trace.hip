@@ -226,10 +226,11 @@ __global__ void __launch_bounds__(kBlock) k_chain(ChainArgs a) {
             r = a.src[2];
         }
         double opl = 0.0;
-#pragma unroll
-        for (int k = 0; k < AKB_MAX_MIRRORS; ++k) {
-            if (k >= a.K) break;
-            const Quadric& Q = a.q[k];
+        // not unrolled: each iteration reads its mirror's 10 coefficients from the kernel
+        // argument segment with scalar loads (wave-uniform), keeping VGPR pressure low
+#pragma unroll 1
+        for (int k = 0; k < a.K; ++k) {
+            const Quadric Q = a.q[k];
             double x, y, z;
             if (!quadric_hit(Q, l, m, nn, p, q, r, (a.negmask >> k) & 1, x, y, z))
                 fl |= AKB_FLAG_MISS << (4 * k);
@@ -651,6 +652,8 @@ int akb_fill_nan_f64(double* out, int64_t ld, int rows, int64_t n, void* stream)
     k_fill_nan<<<grid_for(n), kBlock, 0, (hipStream_t)stream>>>(out, ld, rows, n);
     return launch_status("k_fill_nan");
 }
+
+int64_t akb_chain_desc_size(void) { return (int64_t)sizeof(akb_chain_desc); }
 
 int akb_trace_chain_f64(const akb_chain_desc* d, void* stream) {
     clear_error();

@@ -1,0 +1,57 @@
+"""Device plumbing: torch owns device memory and streams; the HIP library gets raw pointers.
+
+All hot-path data is float64 struct-of-arrays, (3, N) row-major, like the reference's arrays.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+
+F64 = torch.float64
+
+
+def require_gpu():
+    if not torch.cuda.is_available():
+        raise _lib.AKBError("no HIP device visible: the AKB hot path runs on MI355X only (no CPU fallback)")
+
+
+def device():
+    require_gpu()
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def stream_handle(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def ptr(t):
+    """Raw device pointer of a tensor (or None)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def to_dev(a, dev=None):
+    """numpy / torch array -> contiguous float64 device tensor."""
+    dev = dev or device()
+    if isinstance(a, torch.Tensor):
+        return a.to(device=dev, dtype=F64).contiguous()
+    arr = np.ascontiguousarray(np.asarray(a, dtype=np.float64))
+    return torch.from_numpy(arr).to(dev, non_blocking=False)
+
+
+def host_f64(values):
+    """ctypes double array on the host (coefficients, matrices, small vectors)."""
+    vals = [float(v) for v in values]
+    return (ctypes.c_double * len(vals))(*vals)
+
+
+def empty(shape, dev=None):
+    return torch.empty(shape, dtype=F64, device=dev or device())
+
+
+def flags_tensor(dev=None):
+    return torch.zeros(1, dtype=torch.int32, device=dev or device())

@@ -1,0 +1,109 @@
+"""One process per GPU over torch.distributed (backend "nccl" = RCCL on ROCm; "gloo" on CPU).
+
+The hot path shards without a data-path collective:
+  * ray trace: each rank owns a contiguous block of V-rows of the ray grid (Shard.split); the
+    only exchanges are the 2n resample samples (middle row / middle column picks), the flag
+    word, a handful of partial sums for the means, and the assembled pupil before the PSF
+    (SURVEY.md §5, §8(e));
+  * Huygens: targets are split across ranks, sources replicated, and the new field is
+    all-gathered so it can serve as the next stage's source set (Wavecalc _multi.py:136-138,
+    :228, as a collective instead of peer reads).
+
+The reference has no collectives at all (its multi-GPU code is CuPy device contexts + threads).
+"""
+import os
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def init_from_env(backend=None):
+    """Initialise the default group from RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT (torchrun)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group(backend=backend, rank=rank, world_size=world)
+    elif torch.cuda.is_available():
+        torch.cuda.set_device(local)
+    return rank, world, local
+
+
+class TorchComm:
+    """Communicator for RayWave over the default process group."""
+
+    def __init__(self, device=None):
+        self.world = dist.get_world_size() if dist.is_initialized() else 1
+        self.rank = dist.get_rank() if dist.is_initialized() else 0
+        self.device = device
+
+    def _dev(self, t):
+        return t if self.device is None else t.to(self.device)
+
+    def allreduce_sums(self, t):
+        if self.world > 1:
+            t = t.contiguous()
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return t
+
+    def allreduce_max(self, t):
+        if self.world > 1:
+            t = t.contiguous()
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return t
+
+    def gather_samples(self, samp_h, samp_v, shard, n):
+        """Each rank holds zeros outside its rows; one SUM all-reduce assembles both pick lists."""
+        if self.world == 1:
+            return samp_h, samp_v
+        buf = self._dev(torch.from_numpy(np.concatenate([samp_h, samp_v])))
+        buf = self.allreduce_sums(buf).cpu().numpy()
+        return buf[:samp_h.shape[0]], buf[samp_h.shape[0]:]
+
+    def sum_flags(self, f):
+        if self.world == 1:
+            return f
+        t = self._dev(torch.tensor([float(f)], dtype=torch.float64))
+        return int(self.allreduce_sums(t).item())
+
+    def barrier(self):
+        if self.world > 1:
+            dist.barrier()
+
+    def allgather_field(self, piece, counts):
+        """Concatenate per-rank 1-D pieces (lengths `counts`) in rank order on every rank."""
+        if self.world == 1:
+            return piece
+        mx = max(counts)
+        pad = torch.zeros(mx, dtype=piece.dtype, device=piece.device)
+        pad[:piece.shape[0]] = piece
+        bufs = [torch.empty_like(pad) for _ in range(self.world)]
+        if pad.is_complex():
+            real = [torch.view_as_real(b) for b in bufs]
+            dist.all_gather(real, torch.view_as_real(pad))
+        else:
+            dist.all_gather(bufs, pad)
+        return torch.cat([b[:c] for b, c in zip(bufs, counts)])
+
+
+def split_counts(n, world):
+    base, rem = divmod(n, world)
+    return [base + (1 if r < rem else 0) for r in range(world)]
+
+
+def propagate_sharded(tx, ty, tz, sx, sy, sz, u_ds, k, comm):
+    """Huygens stage with targets split over ranks (np.array_split order) and the result
+    all-gathered. tx.. are the FULL target arrays (device tensors) on every rank."""
+    from .wavecalc import propagate
+    n = int(tx.shape[0])
+    counts = split_counts(n, comm.world)
+    lo = sum(counts[:comm.rank])
+    hi = lo + counts[comm.rank]
+    piece = propagate(tx[lo:hi].contiguous(), ty[lo:hi].contiguous(), tz[lo:hi].contiguous(), sx, sy, sz, u_ds, k)
+    return comm.allgather_field(piece, counts)

@@ -1,0 +1,60 @@
+"""numpy-exact sums on the device.
+
+np.sum / np.mean / np.nanmean on a float64 row run numpy's pairwise summation inside 8192-element
+buffers and add the buffer results left to right; akb_pairwise_sum_f64 reproduces that order, so
+the means the drivers take (nanmean(arctan(...)) for the tilt, :3583-3588; mean(detcenter) :3590;
+nanmean(totalDist) :3626/:3633; nanmean(detcenter) :3674) come out bit-identical to the reference.
+"""
+import torch
+
+from . import _lib
+from . import device as D
+
+
+class RowSums:
+    """Reusable workspace for row reductions of a (rows, n) float64 device tensor."""
+
+    def __init__(self):
+        self._work = None
+
+    def __call__(self, x, nan=False, stream=None):
+        """x: (rows, n) or (n,) contiguous float64 device tensor -> (sums, counts) device tensors."""
+        L = _lib.lib()
+        if x.dim() == 1:
+            x = x.unsqueeze(0)
+        if not x.is_contiguous():
+            x = x.contiguous()
+        rows, n = x.shape
+        need = int(L.akb_pairwise_work_bytes(rows, n))
+        if self._work is None or self._work.numel() * 8 < need or self._work.device != x.device:
+            self._work = torch.empty(max(need // 8, 1), dtype=D.F64, device=x.device)
+        sums = torch.empty(rows, dtype=D.F64, device=x.device)
+        counts = torch.empty(rows, dtype=torch.int64, device=x.device)
+        _lib.check(L.akb_pairwise_sum_f64(D.ptr(x), n, rows, n, int(bool(nan)), D.ptr(sums), D.ptr(counts),
+                                          D.ptr(self._work), D.stream_handle(stream)))
+        return sums, counts
+
+
+_default = RowSums()
+
+
+def np_sum(x, nan=False):
+    """Device analogue of np.sum (nan=False) / np.nansum (nan=True) per row; returns (sums, counts)."""
+    return _default(x, nan=nan)
+
+
+def means_to_host(pairs):
+    """[(sums, counts), ...] device tensors -> list of numpy float64 means, one sync.
+    mean = sum / count in float64 (numpy's true_divide of the sum by the count)."""
+    import numpy as np
+    flat = [torch.cat([s, c.to(D.F64)]) for s, c in pairs]
+    host = torch.cat(flat).cpu().numpy() if flat else np.zeros(0)
+    out, off = [], 0
+    for s, _ in pairs:
+        r = s.shape[0]
+        sums = host[off:off + r]
+        cnts = host[off + r:off + 2 * r]
+        with np.errstate(invalid="ignore", divide="ignore"):
+            out.append(sums / cnts)
+        off += 2 * r
+    return out

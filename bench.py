@@ -1,0 +1,185 @@
+"""Benchmark: ray-surface intersections/s of the 4-mirror AKB wavefront hot path (+ PSF wall time).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload (BASELINE.json configs[2], "C3"): the 'ray_wave' path of plot_result_debug
+(AKB_raytrace_20250312.py:1326) on a 3163 x 3163 ray grid (1.0e7 rays) per GPU through the
+reference's Wolter III+I geometry (tests/golden/akb_geometry.json, recorded from the reference):
+pass 1 (4 mirrors), equal-angle resample, pass 2 (4 mirrors + OPL), tilt, two detector planes,
+OPD; then a 128 x 128 pupil padded x16 -> 2048^2 PSF on rocFFT. One step = all of it; its
+intersections are 2 passes x 4 mirrors x rays. Inputs (the two 1-D angle tables) are resident on
+the device before timing. Multi-GPU: weak scaling, each rank owns ~1e7 rays (contiguous V-rows of
+a grid of round(sqrt(N * 1e7))^2 rays); the PSF runs on rank 0.
+
+Prints one JSON line (rank 0). The dominant kernel's roofline uses HIP events on the stream it runs
+on; cpu_baseline times the oracle's C restatement (the "port") on this host on a bounded sample.
+"""
+import argparse
+import glob
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "ray-surface intersections/sec + PSF wall-time, 1e7-ray 4-mirror AKB, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X spec, MI355X_MICROARCH.md
+# bytes the pass-2 chain kernel must move per ray: it reads two L2-resident 1-D tables and
+# writes last hit (24) + exit direction (24) + detector hit (24) + OPL (8) + 2 arctans (16)
+PASS2_BYTES_PER_RAY = 96
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--rays", type=float, default=1.0e7, help="rays per GPU")
+    p.add_argument("--pupil", type=int, default=128)
+    p.add_argument("--pad", type=int, default=16)
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    return p.parse_args()
+
+
+def cpu_baseline(seconds):
+    """The oracle (C restatement, OpenMP, + numpy for the host steps) running the same ray_wave
+    pipeline on a 1001^2 grid, repeated for about `seconds`."""
+    import oracle
+    import oracle.pipeline as OPL
+    with open(os.path.join(ROOT, "tests", "golden", "akb_geometry.json")) as f:
+        g = json.load(f)
+    threads = oracle.max_threads()
+    n = 1001
+    OPL.akb_ray_wave(g, 65)  # load / warm
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        OPL.akb_ray_wave(g, n)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or reps >= 1000:
+            break
+    inter = 2 * len(g["mirrors"]) * n * n * reps
+    return {"value": inter / el, "unit": "intersections/s", "cores": threads, "kind": "port",
+            "sample": f"oracle ray_wave pipeline (C primitives, OpenMP {threads} threads, numpy means/interp1d) "
+                      f"on a {n}x{n} grid, {reps} reps in {el:.1f} s"}
+
+
+def read_traffic(launch_bytes):
+    """HBM bytes per pass-2 launch from the committed rocprofv3 --pmc summary, if present."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_pass2*.json")))
+    if not files:
+        return None
+    try:
+        with open(files[-1]) as f:
+            d = json.load(f)
+        return d.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    args = parse()
+    import torch
+    from akbraytracing_amd import build as B
+    from akbraytracing_amd import dist as AD
+    rank, world, local = AD.init_from_env()
+    if not os.path.exists(B.SO):
+        if rank == 0:
+            B.build()
+        AD.TorchComm().barrier()
+    from akbraytracing_amd.psf import psf_stack
+    from akbraytracing_amd.wavefront import RayWave, Shard, SystemGeometry
+
+    dev = torch.device("cuda", torch.cuda.current_device())
+    geom = SystemGeometry.load(os.path.join(ROOT, "tests", "golden", "akb_geometry.json"))
+    n = int(round(math.sqrt(args.rays * world)))
+    shard = Shard.split(n, world, rank)
+    comm = AD.TorchComm(dev)
+    rw = RayWave(geom, n, shard=shard, comm=comm)
+    lam = 13.5e-9  # EUV, AKB_raytrace_20250312.py:1161-1162 / :3614
+
+    psf_events = []
+
+    def step(timed):
+        rw.run()
+        opd, amp, dx, dy = rw.pupil(args.pupil)
+        if rank == 0:
+            if timed:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+            psf, _, _ = psf_stack(opd, amp, [lam], dx, dy, pad_factor=args.pad)
+            if timed:
+                e1.record()
+                psf_events.append((e0, e1))
+
+    for _ in range(args.warmup):
+        step(False)
+    rw.kernel_events = []
+    comm.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    comm.barrier()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device=dev)
+    t = comm.allreduce_max(t)
+    el = float(t.item())
+    inter_rank = rw.intersections_per_run() * args.steps
+    tot = torch.tensor([float(inter_rank)], dtype=torch.float64, device=dev)
+    total_inter = float(comm.allreduce_sums(tot).item())
+
+    if rank != 0:
+        return
+    k_ms = [a.elapsed_time(b) for a, b in rw.kernel_events]
+    k_avg = sum(k_ms) / len(k_ms)
+    psf_ms = sum(a.elapsed_time(b) for a, b in psf_events) / max(len(psf_events), 1)
+    launch_bytes = PASS2_BYTES_PER_RAY * rw.n_local
+    achieved = launch_bytes / (k_avg * 1e-3) / 1e9
+    out = {
+        "metric": METRIC,
+        "value": total_inter / el,
+        "unit": "intersections/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": el / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: deterministic ray grid through the reference's AKB geometry (recorded fixture)",
+        "config": {
+            "workload": "C3: 4-mirror AKB ray_wave trace (2 passes, tilt, OPD) + 2048^2 PSF on rocFFT",
+            "rays_per_gpu": rw.n_local, "grid": n, "mirrors": len(geom.mirrors),
+            "intersections_per_step": 2 * len(geom.mirrors) * n * n,
+            "psf": f"{args.pupil}^2 pupil x pad {args.pad} -> {args.pupil * args.pad}^2 complex128 FFT",
+            "parallelism": f"ray-row shards x{world}",
+        },
+        "psf_ms": psf_ms,
+        "pass2_kernel_ms": k_avg,
+        "roofline": {
+            "kernel": "k_chain<grid,opl> (pass 2)",
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": read_traffic(launch_bytes),
+            "algorithmic_bytes_per_launch": launch_bytes,
+        },
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

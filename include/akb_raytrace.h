@@ -137,6 +137,8 @@ typedef struct akb_chain_desc {
 } akb_chain_desc;
 
 int akb_trace_chain_f64(const akb_chain_desc* desc, void* stream);
+/* sizeof(akb_chain_desc), for bindings to check their struct layout */
+int64_t akb_chain_desc_size(void);
 
 /* tilt + detectors + OPL (ref :3583-3601, :3611-3633):
  *   r' = Ry@(Rz@r), p' = Ry@(Rz@(p - c)) + c

@@ -220,7 +220,7 @@ def np_sum(x, nan=False):
     return float(s), int(cnt.value)
 
 
-def huygens(tx, ty, tz, sx, sy, sz, u_times_ds, k):
+def huygens_c(tx, ty, tz, sx, sy, sz, u_times_ds, k):
     """compute_u_parallel (Wavecalc_raytrace_fromData_CPU0402.py:71-85), OpenMP over targets;
     u_times_ds is the already-scaled source field (:102). Speed baseline; tolerance-checked."""
     arrs = [np.ascontiguousarray(np.asarray(a, dtype=np.float64)) for a in (tx, ty, tz, sx, sy, sz)]
