@@ -134,12 +134,19 @@ __global__ void __launch_bounds__(kBlock) k_psf_inten(PsfIntenArgs a) {
         if (E) E[idx] = make_double2(re, im);
         m = (I > m || I != I) ? I : m;
     }
-    // wave max then one atomic per wave
+    // wave max, then workgroup max through LDS, then one atomic per workgroup (a per-wave
+    // atomic on one word serialises ~65k atomics for a 2048^2 plane)
+    __shared__ double wmax[kBlock / 64];
     for (int off = 32; off > 0; off >>= 1) {
         const double o = __shfl_down(m, off);
         m = (o > m || o != o) ? o : m;
     }
-    if ((threadIdx.x & 63) == 0) atomic_max_nonneg(a.imax + b, m);
+    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kBlock / 64; ++w) m = (wmax[w] > m || wmax[w] != wmax[w]) ? wmax[w] : m;
+        atomic_max_nonneg(a.imax + b, m);
+    }
 }
 
 __global__ void __launch_bounds__(kBlock) k_psf_norm(double* psf, double2* efield, const double* imax,

@@ -386,155 +386,6 @@ __global__ void __launch_bounds__(kBlock) k_opd(OpdArgs a) {
     }
 }
 
-// ----------------------------------------------------------------------------------------------
-// numpy-exact sum: np.add.reduce on a contiguous float64 row runs its inner loop on 8192-element
-// buffers, each summed by numpy's pairwise_sum (leaves of <= 128 elements with 8 accumulators,
-// split at n/2 rounded down to a multiple of 8), and adds the block results left to right.
-// One wave per 8192 block: lane 0 walks the split tree, the 64 lanes sum the leaves in
-// parallel, lane 0 combines them in tree order. A second kernel adds the blocks in order.
-// ----------------------------------------------------------------------------------------------
-
-constexpr int kPwBlock = 8192;
-constexpr int kPwMaxLeaves = 256;
-
-__device__ __forceinline__ int pw_split(int n) {
-    int n2 = n / 2;
-    return n2 - (n2 % 8);
-}
-
-__device__ __forceinline__ double pw_load(const double* a, int i, bool nan0, int& cnt) {
-    double v = a[i];
-    if (nan0) {
-        if (v != v) {
-            v = 0.0;
-        } else {
-            ++cnt;
-        }
-    } else {
-        ++cnt;
-    }
-    return v;
-}
-
-__device__ double pw_leaf(const double* a, int n, bool nan0, int& cnt) {
-    if (n < 8) {
-        double res = 0.0;
-        for (int i = 0; i < n; ++i) res = res + pw_load(a, i, nan0, cnt);
-        return res;
-    }
-    double r[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) r[j] = pw_load(a, j, nan0, cnt);
-    int i = 8;
-    for (; i < n - (n % 8); i += 8) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) r[j] = r[j] + pw_load(a, i + j, nan0, cnt);
-    }
-    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-    for (; i < n; ++i) res = res + pw_load(a, i, nan0, cnt);
-    return res;
-}
-
-__global__ void __launch_bounds__(64) k_pairwise_blocks(const double* x, int64_t ld, int64_t n,
-                                                        int nan0, double* block_sums,
-                                                        unsigned long long* counts, int nblocks) {
-    __shared__ int leaf_off[kPwMaxLeaves];
-    __shared__ int leaf_len[kPwMaxLeaves];
-    __shared__ double leaf_sum[kPwMaxLeaves];
-    __shared__ int n_leaves;
-    const int row = blockIdx.y;
-    const int blk = blockIdx.x;
-    const double* a = x + row * ld + (int64_t)blk * kPwBlock;
-    const int64_t rem = n - (int64_t)blk * kPwBlock;
-    const int len = rem < kPwBlock ? (int)rem : kPwBlock;
-    const int lane = threadIdx.x;
-
-    if (lane == 0) {
-        // depth-first walk of the split tree, recording leaves left to right
-        int st_off[16], st_len[16];
-        int sp = 0, nl = 0;
-        st_off[sp] = 0;
-        st_len[sp] = len;
-        ++sp;
-        while (sp > 0) {
-            --sp;
-            const int o = st_off[sp], l = st_len[sp];
-            if (l <= 128) {
-                leaf_off[nl] = o;
-                leaf_len[nl] = l;
-                ++nl;
-            } else {
-                const int l2 = pw_split(l);
-                // push right first so the left child is visited first
-                st_off[sp] = o + l2;
-                st_len[sp] = l - l2;
-                ++sp;
-                st_off[sp] = o;
-                st_len[sp] = l2;
-                ++sp;
-            }
-        }
-        n_leaves = nl;
-    }
-    __syncthreads();
-    int cnt = 0;
-    for (int li = lane; li < n_leaves; li += 64)
-        leaf_sum[li] = pw_leaf(a + leaf_off[li], leaf_len[li], nan0 != 0, cnt);
-    // count reduction across the wave
-    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_down(cnt, off);
-    __syncthreads();
-    if (lane == 0) {
-        // combine: post-order evaluation of the same tree
-        int st_len[16];
-        int st_state[16];
-        double st_left[16];
-        int sp = 0, li = 0;
-        double result = 0.0;
-        st_len[0] = len;
-        st_state[0] = 0;
-        sp = 1;
-        bool have = false;
-        while (sp > 0) {
-            const int t = sp - 1;
-            if (!have) {
-                if (st_len[t] <= 128) {
-                    result = leaf_sum[li++];
-                    have = true;
-                    --sp;
-                } else if (st_state[t] == 0) {
-                    st_state[t] = 1;
-                    st_len[sp] = pw_split(st_len[t]);
-                    st_state[sp] = 0;
-                    ++sp;
-                }
-            } else {
-                // `result` is the value of the child just finished, parent at t
-                if (st_state[t] == 1) {
-                    st_left[t] = result;
-                    st_state[t] = 2;
-                    have = false;
-                    st_len[sp] = st_len[t] - pw_split(st_len[t]);
-                    st_state[sp] = 0;
-                    ++sp;
-                } else {
-                    result = st_left[t] + result;
-                    --sp;
-                }
-            }
-        }
-        block_sums[row * nblocks + blk] = result;
-        atomicAdd(counts + row, (unsigned long long)cnt);
-    }
-}
-
-__global__ void k_pairwise_final(const double* block_sums, int nblocks, int rows, double* out) {
-    const int row = blockIdx.x * blockDim.x + threadIdx.x;
-    if (row >= rows) return;
-    double acc = block_sums[row * nblocks];
-    for (int b = 1; b < nblocks; ++b) acc = acc + block_sums[row * nblocks + b];
-    out[row] = acc;
-}
-
 }  // namespace akb
 
 // ==============================================================================================
@@ -780,32 +631,6 @@ int akb_opd_f64(const double* total1, double mean1, const double* total2, double
     a.wave = wave;
     k_opd<<<grid_for(n), kBlock, 0, (hipStream_t)stream>>>(a);
     return launch_status("k_opd");
-}
-
-int64_t akb_pairwise_work_bytes(int rows, int64_t n) {
-    const int64_t nb = n <= 0 ? 1 : (n + kPwBlock - 1) / kPwBlock;
-    return (int64_t)rows * nb * (int64_t)sizeof(double);
-}
-
-int akb_pairwise_sum_f64(const double* x, int64_t ld, int rows, int64_t n, int nan_to_zero,
-                         double* d_sum, int64_t* d_count, void* d_work, void* stream) {
-    clear_error();
-    AKB_REQUIRE(x && d_sum && d_count && d_work, "null pointer");
-    AKB_REQUIRE(rows > 0 && rows <= 65535 && n >= 0, "bad sizes");
-    hipStream_t s = (hipStream_t)stream;
-    AKB_HIP_CHECK(hipMemsetAsync(d_count, 0, sizeof(int64_t) * rows, s));
-    if (n == 0) {
-        AKB_HIP_CHECK(hipMemsetAsync(d_sum, 0, sizeof(double) * rows, s));
-        return AKB_OK;
-    }
-    const int nb = (int)((n + kPwBlock - 1) / kPwBlock);
-    double* bsum = (double*)d_work;
-    k_pairwise_blocks<<<dim3(nb, rows), 64, 0, s>>>(x, ld, n, nan_to_zero, bsum,
-                                                    (unsigned long long*)d_count, nb);
-    int st = launch_status("k_pairwise_blocks");
-    if (st) return st;
-    k_pairwise_final<<<(rows + 63) / 64, 64, 0, s>>>(bsum, nb, rows, d_sum);
-    return launch_status("k_pairwise_final");
 }
 
 }  // extern "C"

@@ -196,8 +196,11 @@ class RayWave:
         return hits[-1], r4, det, opl, atan
 
     # -------------------------------------------------------------- one run
-    def run(self, opd=True):
-        """Trace and reduce; returns a dict of device tensors (this shard's rays) and host means."""
+    def run(self, opd=True, keep_rotated=False, full=False):
+        """Trace and reduce; returns a dict of device tensors (this shard's rays) and host means.
+        keep_rotated: also return the tilted direction / last hit (dir_rot, pt_rot); full: also
+        return DistError (detector 1) and Sph. The default keeps what griddata consumes
+        (DistError2, Wave2, detcenter2) plus the reduction inputs."""
         samp_h, samp_v, flags1 = self._pass1()
         if flags1:
             raise _lib.AKBError(
@@ -230,19 +233,19 @@ class RayWave:
         out = dict(last_hit=last_hit, dir_out=dir_out, det_pre=det, opl=opl, theta_y=theta_y, theta_z=theta_z,
                    focus_apprx=focus, tan_h2=tan_h2, tan_v2=tan_v2, flags=(flags1, flags2))
         if opd:
-            out.update(self._tilt_opd(last_hit, dir_out, opl, theta_y, theta_z, focus))
+            out.update(self._tilt_opd(last_hit, dir_out, opl, theta_y, theta_z, focus, keep_rotated, full))
         self.last = out
         return out
 
-    def _tilt_opd(self, last_hit, dir_out, opl, theta_y, theta_z, focus):
+    def _tilt_opd(self, last_hit, dir_out, opl, theta_y, theta_z, focus, keep_rotated=False, full=False):
         L = _lib.lib()
         n = self.n_local
         ry, rz = P.rotation_matrices(-theta_y, -theta_z)
         det1 = torch.empty((3, n), dtype=D.F64, device=self.dev)
         det2 = torch.empty((3, n), dtype=D.F64, device=self.dev) if self.g.det2 is not None else None
         totals = torch.empty((2, n), dtype=D.F64, device=self.dev)
-        dir_rot = torch.empty((3, n), dtype=D.F64, device=self.dev)
-        pt_rot = torch.empty((3, n), dtype=D.F64, device=self.dev)
+        dir_rot = torch.empty((3, n), dtype=D.F64, device=self.dev) if keep_rotated else None
+        pt_rot = torch.empty((3, n), dtype=D.F64, device=self.dev) if keep_rotated else None
         d2 = self.g.det2 if self.g.det2 is not None else self.g.det1
         _lib.check(L.akb_tilt_opd_f64(D.host_f64(ry.ravel()), D.host_f64(rz.ravel()), D.host_f64(focus),
                                       D.host_f64(self.g.det1), D.host_f64(d2), D.ptr(dir_out), D.ptr(last_hit),
@@ -255,12 +258,12 @@ class RayWave:
         with np.errstate(invalid="ignore", divide="ignore"):
             mean_tot = host[0:2] / host[5:7]
             mean_focus = host[2:5] / host[7:10]
-        dist_err = torch.empty(n, dtype=D.F64, device=self.dev)
+        dist_err = torch.empty(n, dtype=D.F64, device=self.dev) if (full or det2 is None) else None
         res = dict(dir_rot=dir_rot, pt_rot=pt_rot, detcenter=det1, detcenter2=det2, total=totals[0],
                    total2=totals[1], mean_total=mean_tot, mean_focus=mean_focus, dist_err=dist_err)
         if det2 is not None:
             dist_err2 = torch.empty(n, dtype=D.F64, device=self.dev)
-            sph = torch.empty(n, dtype=D.F64, device=self.dev)
+            sph = torch.empty(n, dtype=D.F64, device=self.dev) if full else None
             wave2 = torch.empty(n, dtype=D.F64, device=self.dev)
             _lib.check(L.akb_opd_f64(D.ptr(totals), float(mean_tot[0]), D.ptr(totals[1]), float(mean_tot[1]),
                                      D.ptr(det2), n, D.host_f64(mean_focus), n, D.ptr(dist_err),
