@@ -55,12 +55,9 @@ __global__ void __launch_bounds__(kBlock) k_psf_pupil(PsfPupilArgs a) {
     const int b = blockIdx.z;
     const double kp = a.kphase[b];
     double2* F = a.field + (int64_t)b * g.py * g.px;
-    const int64_t total = (int64_t)g.py * g.px;
     const int hy = g.py / 2, hx = g.px / 2;
-    for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
-         idx += (int64_t)gridDim.x * blockDim.x) {
-        const int yo = (int)(idx / g.px);
-        const int xo = (int)(idx - (int64_t)yo * g.px);
+    for (int yo = blockIdx.y; yo < g.py; yo += gridDim.y)
+    for (int xo = blockIdx.x * blockDim.x + threadIdx.x; xo < g.px; xo += gridDim.x * blockDim.x) {
         // ifftshift for even lengths: out[i] = in[(i + n/2) % n]
         int ys = yo + hy;
         if (ys >= g.py) ys -= g.py;
@@ -116,10 +113,9 @@ __global__ void __launch_bounds__(kBlock) k_psf_inten(PsfIntenArgs a) {
     double2* E = a.efield ? a.efield + (int64_t)b * total : nullptr;
     const int hy = g.py / 2, hx = g.px / 2;
     double m = 0.0;
-    for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
-         idx += (int64_t)gridDim.x * blockDim.x) {
-        const int yo = (int)(idx / g.px);
-        const int xo = (int)(idx - (int64_t)yo * g.px);
+    for (int yo = blockIdx.y; yo < g.py; yo += gridDim.y)
+    for (int xo = blockIdx.x * blockDim.x + threadIdx.x; xo < g.px; xo += gridDim.x * blockDim.x) {
+        const int64_t idx = (int64_t)yo * g.px + xo;
         int ys = yo + hy;
         if (ys >= g.py) ys -= g.py;
         int xs = xo + hx;
@@ -257,8 +253,9 @@ int akb_psf_f64(const double* opd, const double* amp, int ny, int nx, int pad, i
     for (int b = 0; b < batch; ++b) pa.kphase[b] = (2.0 * M_PI / lambdas[b]);
     pa.field = field;
     const int64_t total = (int64_t)g.py * g.px;
-    const unsigned gx = grid_for(total, 4);
-    k_psf_pupil<<<dim3(gx, 1, batch), kBlock, 0, s>>>(pa);
+    const unsigned gx = (unsigned)((g.px + kBlock - 1) / kBlock);
+    const unsigned gy = (unsigned)(g.py < 4096 ? g.py : 4096);
+    k_psf_pupil<<<dim3(gx, gy, batch), kBlock, 0, s>>>(pa);
     if ((st = launch_status("k_psf_pupil"))) return st;
 
     rocfft_execution_info info = nullptr;
@@ -284,9 +281,9 @@ int akb_psf_f64(const double* opd, const double* amp, int ny, int nx, int pad, i
     ia.psf = psf;
     ia.efield = (double2*)efield_re_im;
     ia.imax = d_imax;
-    k_psf_inten<<<dim3(gx, 1, batch), kBlock, 0, s>>>(ia);
+    k_psf_inten<<<dim3(gx, gy, batch), kBlock, 0, s>>>(ia);
     if ((st = launch_status("k_psf_inten"))) return st;
-    k_psf_norm<<<dim3(gx, 1, batch), kBlock, 0, s>>>(psf, (double2*)efield_re_im, d_imax, total);
+    k_psf_norm<<<dim3(grid_for(total, 4), 1, batch), kBlock, 0, s>>>(psf, (double2*)efield_re_im, d_imax, total);
     return launch_status("k_psf_norm");
 }
 

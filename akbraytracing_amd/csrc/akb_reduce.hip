@@ -70,14 +70,29 @@ __global__ void __launch_bounds__(kPwThreads) k_pw_chunks(const double* __restri
     const int len = rem < kPwBuf ? (int)rem : kPwBuf;
 
     long long cnt = 0;
-    for (int i = tid; i < len; i += kPwThreads) {
-        double v = a[i];
-        if (nan0 && v != v) {
-            v = 0.0;
-        } else {
-            ++cnt;
+    // stage: 16 independent loads per thread in flight before the LDS stores (a full buffer is
+    // 32 loads per thread, two batches)
+    constexpr int kBatch = 16;
+    for (int i0 = tid; i0 < len; i0 += kPwThreads * kBatch) {
+        double v[kBatch];
+#pragma unroll
+        for (int k = 0; k < kBatch; ++k) {
+            const int i = i0 + k * kPwThreads;
+            v[k] = i < len ? a[i] : 0.0;
         }
-        s[(i >> 7) * kPwStride + (i & (kPwLeaf - 1))] = v;
+#pragma unroll
+        for (int k = 0; k < kBatch; ++k) {
+            const int i = i0 + k * kPwThreads;
+            if (i < len) {
+                double w = v[k];
+                if (nan0 && w != w) {
+                    w = 0.0;
+                } else {
+                    ++cnt;
+                }
+                s[(i >> 7) * kPwStride + (i & (kPwLeaf - 1))] = w;
+            }
+        }
     }
     for (int off = 32; off > 0; off >>= 1) cnt += __shfl_down(cnt, off);
     if ((tid & 63) == 0) wcnt[tid >> 6] = cnt;

@@ -92,6 +92,18 @@ def sample_plan(n):
     return round(n * (n - 1) / 2), round(n * (n + 1) / 2), col
 
 
+def sample_ownership(shard, n):
+    """Which resample picks a shard's rays supply: (mask over the middle-row range, mask over the
+    n rows of the middle column)."""
+    hb, he, _ = sample_plan(n)
+    lo, hi = shard.row0 * n, (shard.row0 + shard.rows) * n
+    own_h = np.zeros(he - hb, dtype=bool)
+    own_h[max(lo, hb) - hb:max(min(hi, he) - hb, 0)] = True
+    own_v = np.zeros(n, dtype=bool)
+    own_v[shard.row0:shard.row0 + shard.rows] = True
+    return own_h, own_v
+
+
 def resample(angle_h_sep, angle_v_sep, rand_h, rand_v):
     """:2861-2870 — interp1d of the launch angles onto equally spaced exit angles."""
     out_v = np.linspace(angle_v_sep[0], angle_v_sep[-1], len(angle_v_sep))
@@ -142,8 +154,6 @@ class RayWave:
     # -------------------------------------------------------------- passes
     def _pass1(self):
         hb, he, col = sample_plan(self.n)
-        lo = self.shard.row0 * self.n
-        hi = lo + self.n_local
         r = trace_chain(self.g.mirrors, tan_h=self.tan_h, tan_v=self.tan_v, row0=self.shard.row0,
                         n_rays=self.n_local, src=self.g.source, want=(), samples=(hb, he, col),
                         out=self._buf1)
@@ -155,10 +165,7 @@ class RayWave:
         samp_h = host[:he - hb]
         samp_v = host[he - hb:he - hb + self.n]
         flags = int(host[-1])
-        own_h = np.zeros(he - hb, dtype=bool)
-        own_h[max(lo, hb) - hb:max(min(hi, he) - hb, 0)] = True
-        own_v = np.zeros(self.n, dtype=bool)
-        own_v[self.shard.row0:self.shard.row0 + self.shard.rows] = True
+        own_h, own_v = sample_ownership(self.shard, self.n)
         samp_h = np.where(own_h, samp_h, 0.0)
         samp_v = np.where(own_v, samp_v, 0.0)
         samp_h, samp_v = self.comm.gather_samples(samp_h, samp_v, self.shard, self.n)

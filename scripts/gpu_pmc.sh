@@ -1,0 +1,22 @@
+#!/bin/bash
+# PMC passes (one counter group per run, kernel trace only, no sys/runtime trace) over a short
+# bench run, for the roofline's HBM traffic and the FP64 instruction mix.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 120 rocprofv3 -L > gpurun_out/counters.txt 2>&1
+rc=$?; echo "list exit $rc"; [ $rc -eq 0 ] || exit $rc
+F64=$(grep -oE "SQ_INSTS_VALU_(FMA|MUL|ADD|TRANS)_F64" gpurun_out/counters.txt | sort -u | tr '\n' ' ')
+echo "f64 counters: $F64"
+REGEX="${PMC_REGEX:-k_chain|k_tilt|k_opd|k_pw|k_psf|fft}"
+i=0
+for SET in "FETCH_SIZE" "WRITE_SIZE" "$F64" "GRBM_GUI_ACTIVE SQ_WAVES SQ_INSTS_VALU"; do
+  [ -n "$SET" ] || continue
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $SET --kernel-include-regex "$REGEX" --output-format csv \
+      -d gpurun_out/pmc_$i -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline \
+      > gpurun_out/pmc_$i.log 2>&1
+  rc=$?; echo "pmc set $i ($SET) exit $rc"
+  [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+done
+exit 0

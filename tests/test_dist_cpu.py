@@ -1,0 +1,90 @@
+"""The N > 1 path on CPU: world_size 2 over gloo (127.0.0.1). Each rank traces its V-row shard
+with the oracle's chain (the GPU kernels are covered by the gpu tests); the communicator must
+reassemble exactly what one process sees."""
+import json
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import GOLDEN
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, n, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle.pipeline as OPL
+        from akbraytracing_amd.dist import TorchComm, split_counts
+        from akbraytracing_amd.wavefront import Shard, sample_ownership, sample_plan
+        with open(os.path.join(GOLDEN, "akb_geometry.json")) as f:
+            g = json.load(f)
+        comm = TorchComm()
+        shard = Shard.split(n, world, rank)
+        rand_h, rand_v, tan_h, tan_v = OPL.angle_tables(g, n)
+        dirs = OPL.grid_dirs(tan_h, tan_v)
+        lo, hi = shard.row0 * n, (shard.row0 + shard.rows) * n
+        _, r4, _ = OPL.chain(g["mirrors"], dirs[:, lo:hi].copy(), np.zeros((3, hi - lo)))
+        # this rank's pieces of the resample picks, zero elsewhere (what RayWave._pass1 hands over)
+        hb, he, col = sample_plan(n)
+        sh = np.zeros(he - hb)
+        sv = np.zeros(n)
+        own_h, own_v = sample_ownership(shard, n)
+        g_idx = np.arange(lo, hi)
+        m = (g_idx >= hb) & (g_idx < he)
+        sh[g_idx[m] - hb] = r4[1, m] / r4[0, m]
+        cm = (g_idx % n) == col
+        sv[g_idx[cm] // n] = r4[2, cm] / r4[0, cm]
+        assert np.all(sh[~own_h] == 0) and np.all(sv[~own_v] == 0)
+        sh, sv = comm.gather_samples(sh, sv, shard, n)
+        # partial sums for the means: (sum, count) of this rank, summed across ranks
+        part = torch.tensor([np.sum(r4[0]), float(r4.shape[1])], dtype=torch.float64)
+        tot = comm.allreduce_sums(part).numpy()
+        mx = comm.allreduce_max(torch.tensor([float(np.max(r4[1]))], dtype=torch.float64)).numpy()
+        # Huygens-style field all-gather of uneven pieces
+        counts = split_counts(10, world)
+        piece = torch.arange(sum(counts[:rank]), sum(counts[:rank + 1]), dtype=torch.float64) * (1 + 1j)
+        field = comm.allgather_field(piece.to(torch.complex128), counts).numpy()
+        flags = comm.sum_flags(rank)
+        if rank == 0:
+            np.savez(os.path.join(out_dir, "r0.npz"), sh=sh, sv=sv, tot=tot, mx=mx, field=field,
+                     flags=np.array(flags))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n", [33, 34])
+def test_two_rank_shards_reassemble_single_process(tmp_path, n):
+    world = 2
+    mp.start_processes(_worker, args=(world, _free_port(), n, str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    r = np.load(os.path.join(tmp_path, "r0.npz"))
+    import oracle.pipeline as OPL
+    with open(os.path.join(GOLDEN, "akb_geometry.json")) as f:
+        g = json.load(f)
+    rand_h, rand_v, tan_h, tan_v = OPL.angle_tables(g, n)
+    _, r4, _ = OPL.chain(g["mirrors"], OPL.grid_dirs(tan_h, tan_v), np.zeros((3, n * n)))
+    _, v_idx, _, _, h_idx = OPL.sample_indices(n, n)
+    assert np.array_equal(r["sh"], r4[1, h_idx] / r4[0, h_idx])
+    assert np.array_equal(r["sv"], r4[2, v_idx] / r4[0, v_idx])
+    # resample from the gathered picks equals the single-process resample exactly
+    a = OPL.resample_from_angles(np.arctan(r["sh"]), np.arctan(r["sv"]), rand_h, rand_v)
+    b = OPL.resample_tables(r4, rand_h, rand_v, n, n)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+    assert r["tot"][1] == n * n
+    assert abs(r["tot"][0] / r["tot"][1] - np.mean(r4[0])) < 1e-15
+    assert r["mx"][0] == np.max(r4[1])
+    assert np.array_equal(r["field"], np.arange(10) * (1 + 1j))
+    assert int(r["flags"]) == 1

@@ -1,0 +1,181 @@
+"""Host-side logic and the C ABI boundary, without a GPU (no compute calls)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, golden_json
+
+
+def test_library_exports_every_header_symbol():
+    from akbraytracing_amd import _lib, build
+    build.build(verbose=False)
+    L = _lib.lib()
+    with open(os.path.join(ROOT, "include", "akb_raytrace.h")) as f:
+        hdr = f.read()
+    declared = set(re.findall(r"^\s*(?:const char\*|int64_t|int|void)\s+(akb_\w+)\s*\(", hdr, re.M))
+    assert declared == set(_lib.EXPORTS)
+    for sym in declared:
+        assert hasattr(L, sym), sym
+    raw = ctypes.CDLL(build.SO)
+    for sym in declared:
+        getattr(raw, sym)
+
+
+def test_abi_version_and_struct_layout():
+    from akbraytracing_amd import _lib
+    L = _lib.lib()
+    assert L.akb_abi_version() == 1
+    assert L.akb_chain_desc_size() == ctypes.sizeof(_lib.ChainDesc)
+    # no GPU in this container: device count is 0 and calls report errors instead of crashing
+    assert L.akb_device_count() >= 0
+
+
+def test_invalid_arguments_are_reported_not_crashed():
+    from akbraytracing_amd import _lib
+    L = _lib.lib()
+    st = L.akb_isect_f64(None, None, 0, 0, None, 0, 0, 0, 10, None, 0, None, None)
+    assert st == -1
+    assert b"null pointer" in L.akb_last_error()
+    with pytest.raises(_lib.AKBError):
+        _lib.check(st)
+    desc = _lib.ChainDesc()
+    desc.n_mirrors = 9
+    assert L.akb_trace_chain_f64(ctypes.byref(desc), None) == -1
+    assert L.akb_pairwise_work_bytes(3, 10_000_000) == 3 * 1221 * 16
+
+
+def test_header_comments_cite_reference_lines():
+    with open(os.path.join(ROOT, "include", "akb_raytrace.h")) as f:
+        hdr = f.read()
+    for ref in ("EllipseRaytrace3D.py:18-45", "psf_fft.py:29-125", "Wavecalc_raytrace_fromData_CPU0402.py:71-124"):
+        assert ref in hdr
+
+
+def test_geometry_and_sample_plan():
+    from akbraytracing_amd.wavefront import SystemGeometry, sample_plan, Shard
+    import oracle.pipeline as OPL
+    g = SystemGeometry.from_dict(golden_json("akb_geometry.json"))
+    assert len(g.mirrors) == 4 and [m.negative for m in g.mirrors] == [False, False, False, True]
+    assert len(g.det1) == 4 and g.det1[0] == 1.0
+    for n in (65, 64, 3163, 3164, 10000):
+        hb, he, col = sample_plan(n)
+        c2, v_idx, s2, e2, h_idx = OPL.sample_indices(n, n)
+        assert (hb, he, col) == (s2, e2, c2)
+        assert he - hb == n
+    for n, w in ((3163, 8), (65, 2), (10, 3), (8945, 8)):
+        shards = [Shard.split(n, w, r) for r in range(w)]
+        assert shards[0].row0 == 0
+        assert sum(s.rows for s in shards) == n
+        for a, b in zip(shards, shards[1:]):
+            assert a.row0 + a.rows == b.row0
+
+
+def test_angle_tables_match_reference_fixture():
+    from akbraytracing_amd.wavefront import SystemGeometry
+    from conftest import golden
+    g = SystemGeometry.from_dict(golden_json("akb_geometry.json"))
+    f = golden("akb_raywave_65.npz")
+    assert np.array_equal(g.angle_h.table(65), f["rand_h"])
+    assert np.array_equal(g.angle_v.table(65), f["rand_v"])
+    assert np.array_equal(np.tan(g.angle_h.table(65)), f["tan_h"])
+
+
+def test_resample_matches_oracle():
+    from akbraytracing_amd.wavefront import resample
+    import oracle.pipeline as OPL
+    rng = np.random.default_rng(1)
+    ah = np.sort(rng.random(33))
+    av = np.sort(rng.random(33))
+    rh, rv = np.linspace(0, 1, 33), np.linspace(-1, 0, 33)
+    a = resample(ah, av, rh, rv)
+    b = OPL.resample_from_angles(ah, av, rh, rv)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+def test_psf_host_helpers_match_reference_formulas():
+    from akbraytracing_amd import psf as G
+    import oracle.psf as OP
+    a = np.arange(12.0).reshape(3, 4)
+    padded, crop = G.ensure_even_size(a)
+    assert padded.shape == (4, 4) and crop == (slice(0, 3), slice(0, 4)) and padded[3].sum() == 0
+    same, none = G.ensure_even_size(np.ones((4, 6)))
+    assert none is None and same.shape == (4, 6)
+    wy, wx, m = G.hann_axes(9, 10)
+    w = np.outer(wy, wx)
+    assert m == w.max()
+    x, y = G.image_axes(64, 48, 5e-6, 4e-6, 13.5e-9, 1e-2)
+    _, xr, yr = OP.psf(np.zeros((24, 32)), np.ones((24, 32)), 13.5e-9, 5e-6, 1e-2, 2, dy=4e-6)
+    assert np.array_equal(x, xr) and np.array_equal(y, yr)
+    db = G.psf_to_db(np.array([1.0, 1e-3, 0.0]))
+    assert np.allclose(db, [0.0, -30.0, -60.0])
+
+
+def test_psf_argument_errors_before_any_device_work():
+    from akbraytracing_amd import psf as G
+    with pytest.raises(ValueError):
+        G._check_args((4, 4), (4, 5), 2, None)
+    with pytest.raises(ValueError):
+        G._check_args((4, 4), (4, 4), 0, None)
+    with pytest.raises(ValueError):
+        G._check_args((4, 4), (4, 4), 2.5, None)
+    with pytest.raises(ValueError):
+        G._check_args((4, 4), (4, 4), 2, "blackman")
+    G._check_args((4, 4), (4, 4), 3, "HANN")
+
+
+def test_install_rebinds_and_respects_option_mpmath():
+    import types
+    import akbraytracing_amd
+    from akbraytracing_amd import primitives as P
+    mod = types.ModuleType("driver")
+    mod.option_mpmath = True
+    orig = lambda *a, **k: "reference"  # noqa: E731
+    mod.mirr_ray_intersection = orig
+    mod.compute_psf_fft = orig
+    mod.unrelated = orig
+    names = akbraytracing_amd.install(mod)
+    assert set(names) == {"mirr_ray_intersection", "compute_psf_fft"}
+    assert mod.mirr_ray_intersection.__wrapped__ is orig
+    assert mod.unrelated is orig
+    # option_mpmath routes the mpmath-aware primitives to the reference's own branch
+    assert mod.mirr_ray_intersection(1, 2, 3) == "reference"
+    assert akbraytracing_amd.install(mod) == names  # idempotent
+    akbraytracing_amd.uninstall(mod)
+    assert mod.mirr_ray_intersection is orig and mod.compute_psf_fft is orig
+
+
+def test_product_path_fails_loudly_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from akbraytracing_amd import primitives as P, _lib
+    with pytest.raises(_lib.AKBError):
+        P.normalize_vector(np.ones((3, 4)))
+
+
+def test_product_package_never_imports_the_oracle():
+    pkg = os.path.join(ROOT, "akbraytracing_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for fn in files:
+            if fn.endswith(".py"):
+                with open(os.path.join(dirpath, fn)) as f:
+                    src = f.read()
+                assert not re.search(r"^\s*(import|from)\s+oracle", src, re.M), fn
+
+
+def test_dropin_psf_module_exports():
+    import importlib
+    import sys
+    import akbraytracing_amd
+    sys.path.insert(0, akbraytracing_amd.DROPIN_DIR)
+    try:
+        sys.modules.pop("psf_fft", None)
+        m = importlib.import_module("psf_fft")
+        assert m.compute_psf_fft.__module__ == "akbraytracing_amd.psf"
+        assert set(m.__all__) == {"compute_psf_fft", "psf_to_db", "ensure_even_size"}
+    finally:
+        sys.path.remove(akbraytracing_amd.DROPIN_DIR)
+        sys.modules.pop("psf_fft", None)
