@@ -19,6 +19,7 @@ c_int = ctypes.c_int
 c_dbl = ctypes.c_double
 c_vp = ctypes.c_void_p
 MAX_MIRRORS = 7
+ABI_VERSION = 2
 
 FLAG_MISS = 0x1
 FLAG_ZERO_NORMAL = 0x2
@@ -32,10 +33,19 @@ EXPORTS = [
     "akb_isect_f64", "akb_normal_f64", "akb_reflect_f64", "akb_normalize_f64", "akb_plane_isect_f64",
     "akb_seglen_f64", "akb_rotate_f64", "akb_fill_nan_f64",
     "akb_trace_chain_f64", "akb_chain_desc_size", "akb_tilt_opd_f64", "akb_opd_f64",
-    "akb_pairwise_work_bytes", "akb_pairwise_sum_f64",
+    "akb_pairwise_work_bytes", "akb_pairwise_sum_f64", "akb_pupil_sample_f64",
+    "akb_leaf_sink_bytes", "akb_leaf_sink_layout", "akb_leaf_finish_work_bytes", "akb_leaf_finish_f64",
     "akb_huygens_work_bytes", "akb_huygens_f64", "akb_scale_field_f64",
     "akb_psf_work_bytes", "akb_psf_f64", "akb_psf_release_plans",
 ]
+
+
+class LeafSink(ctypes.Structure):
+    """akb_leaf_sink"""
+    _fields_ = [
+        ("leaf_sum", c_vp), ("leaf_cnt", c_vp), ("tail", c_vp),
+        ("nq", c_i32), ("nan_mask", c_i32), ("n", c_i64),
+    ]
 
 
 class ChainDesc(ctypes.Structure):
@@ -61,6 +71,7 @@ class ChainDesc(ctypes.Structure):
         ("samp_v_col", c_i64),
         ("samp_h", c_vp), ("samp_v", c_vp),
         ("flags", c_vp),
+        ("sink", LeafSink),
     ]
 
 
@@ -84,9 +95,14 @@ def _declare(L):
         "akb_fill_nan_f64": ([c_vp, c_i64, c_int, c_i64, c_vp], c_int),
         "akb_trace_chain_f64": ([ctypes.POINTER(ChainDesc), c_vp], c_int),
         "akb_chain_desc_size": ([], c_i64),
-        "akb_tilt_opd_f64": ([c_vp] * 5 + [c_vp, c_vp, c_vp, c_i64, c_i64] + [c_vp] * 6 + [c_vp], c_int),
-        "akb_opd_f64": ([c_vp, c_dbl, c_vp, c_dbl, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp],
-                        c_int),
+        "akb_tilt_opd_f64": ([c_vp] * 5 + [c_vp, c_vp, c_vp, c_i64, c_i64] + [c_vp] * 6
+                             + [ctypes.POINTER(LeafSink), c_vp], c_int),
+        "akb_opd_f64": ([c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp], c_int),
+        "akb_pupil_sample_f64": ([c_vp, c_i64, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_vp], c_int),
+        "akb_leaf_sink_bytes": ([c_int, c_i64], c_i64),
+        "akb_leaf_sink_layout": ([c_vp, c_int, c_int, c_i64, ctypes.POINTER(LeafSink)], c_int),
+        "akb_leaf_finish_work_bytes": ([c_int, c_i64], c_i64),
+        "akb_leaf_finish_f64": ([ctypes.POINTER(LeafSink), c_vp, c_vp, c_vp, c_vp], c_int),
         "akb_pairwise_work_bytes": ([c_int, c_i64], c_i64),
         "akb_pairwise_sum_f64": ([c_vp, c_i64, c_int, c_i64, c_int, c_vp, c_vp, c_vp, c_vp], c_int),
         "akb_huygens_work_bytes": ([c_i64, c_i64], c_i64),
@@ -95,7 +111,7 @@ def _declare(L):
         "akb_scale_field_f64": ([c_vp, c_vp, c_i64, c_vp, c_vp], c_int),
         "akb_psf_work_bytes": ([c_int, c_int, c_int, c_int], c_i64),
         "akb_psf_f64": ([c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_dbl, c_dbl, c_vp, c_vp, c_dbl, c_vp,
-                         c_vp, c_vp, c_vp, c_vp], c_int),
+                         c_vp, c_vp, c_vp, c_vp, c_vp], c_int),
         "akb_psf_release_plans": ([], None),
     }
     for name, (args, res) in sig.items():
@@ -115,6 +131,8 @@ def lib():
                 "or __graft_entry__.build()); there is no CPU fallback")
         L = ctypes.CDLL(path)
         _declare(L)
+        if L.akb_abi_version() != ABI_VERSION:
+            raise AKBError(f"{path} has ABI {L.akb_abi_version()}, the bindings expect {ABI_VERSION}: rebuild")
         if L.akb_chain_desc_size() != ctypes.sizeof(ChainDesc):
             raise AKBError("akb_chain_desc layout mismatch between include/akb_raytrace.h and _lib.py")
         _LIB = L

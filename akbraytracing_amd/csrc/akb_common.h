@@ -141,3 +141,69 @@ __device__ __forceinline__ void plane_hit(double g, double h, double i, double j
 }
 
 }  // namespace akb
+
+namespace akb {
+
+// ---- numpy-order leaf sums fused into a producer (see akb_leaf_sink in the header) ----
+// A producer launched with 256-thread workgroups walks its rays in 256-ray segments (two numpy
+// leaves of 128); every thread hands over its ray's NQ quantities and the workgroup writes the
+// segment's leaf sums, or the raw values when the segment lies in the short last buffer.
+constexpr int kLeafSeg = 256;
+constexpr int kNpBuf = 8192;
+
+template <int NQ>
+struct LeafLds {
+    double v[NQ][kLeafSeg];
+};
+
+template <int NQ>
+__device__ __forceinline__ void leaf_sink_segment(const akb_leaf_sink& S, LeafLds<NQ>& L, int64_t seg0,
+                                                  const double (&v)[NQ], bool valid) {
+    const int tid = threadIdx.x;
+    const int64_t full = (S.n / kNpBuf) * kNpBuf;
+    if (seg0 >= full) {  // block-uniform: the short last buffer keeps raw values
+        if (valid) {
+            const int64_t t = seg0 + tid - full;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) S.tail[(int64_t)q * kNpBuf + t] = v[q];
+        }
+        return;
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) L.v[q][tid] = v[q];
+    __syncthreads();
+    if (tid < 16 * NQ) {
+        const int q = tid >> 4;
+        const int leaf = (tid >> 3) & 1;
+        const int j = tid & 7;
+        const bool nan0 = (S.nan_mask >> q) & 1;
+        const double* p = &L.v[q][leaf * 128 + j];
+        double x = p[0];
+        bool bad = nan0 && (x != x);
+        double r = bad ? 0.0 : x;
+        int c = bad ? 0 : 1;
+#pragma unroll
+        for (int row = 1; row < 16; ++row) {
+            x = p[row * 8];
+            bad = nan0 && (x != x);
+            r = r + (bad ? 0.0 : x);
+            c += bad ? 0 : 1;
+        }
+        // numpy's leaf: ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7))
+        r = r + __shfl_xor(r, 1);
+        r = r + __shfl_xor(r, 2);
+        r = r + __shfl_xor(r, 4);
+        c += __shfl_xor(c, 1);
+        c += __shfl_xor(c, 2);
+        c += __shfl_xor(c, 4);
+        if (j == 0) {
+            const int64_t nleaves = full / 128;
+            const int64_t li = seg0 / 128 + leaf;
+            S.leaf_sum[(int64_t)q * nleaves + li] = r;
+            S.leaf_cnt[(int64_t)q * nleaves + li] = c;
+        }
+    }
+    __syncthreads();
+}
+
+}  // namespace akb

@@ -68,8 +68,9 @@ __global__ void __launch_bounds__(kBlock) k_psf_pupil(PsfPupilArgs a) {
         double re = 0.0, im = 0.0;
         if (yy >= 0 && yy < g.ny && xx >= 0 && xx < g.nx) {
             const int64_t pi = (int64_t)yy * g.nx + xx;
-            double A = a.amp[pi];
             double o = a.opd[pi];
+            // amp == NULL: psf_calc's mask, 1 where the OPD is defined and 0 elsewhere (:1182-1188)
+            double A = a.amp ? a.amp[pi] : (isfinite(o) ? 1.0 : 0.0);
             if (!isfinite(A)) A = 0.0;
             if (!isfinite(o)) o = 0.0;
             const double ph = kp * o;
@@ -99,6 +100,7 @@ struct PsfIntenArgs {
     const double2* field;
     PsfGeom g;
     double dA;
+    const double* pitch;  // device [dx, dy] or NULL
     double* psf;
     double2* efield;
     double* imax;
@@ -112,6 +114,7 @@ __global__ void __launch_bounds__(kBlock) k_psf_inten(PsfIntenArgs a) {
     double* P = a.psf + (int64_t)b * total;
     double2* E = a.efield ? a.efield + (int64_t)b * total : nullptr;
     const int hy = g.py / 2, hx = g.px / 2;
+    const double dA = a.pitch ? a.pitch[0] * a.pitch[1] : a.dA;
     double m = 0.0;
     for (int yo = blockIdx.y; yo < g.py; yo += gridDim.y)
     for (int xo = blockIdx.x * blockDim.x + threadIdx.x; xo < g.px; xo += gridDim.x * blockDim.x) {
@@ -122,8 +125,8 @@ __global__ void __launch_bounds__(kBlock) k_psf_inten(PsfIntenArgs a) {
         if (xs >= g.px) xs -= g.px;
         const double2 f = F[(int64_t)ys * g.px + xs];
         // U_im = fftshift(F) * dA (complex * real as numpy)
-        const double re = f.x * a.dA - f.y * 0.0;
-        const double im = f.x * 0.0 + f.y * a.dA;
+        const double re = f.x * dA - f.y * 0.0;
+        const double im = f.x * 0.0 + f.y * dA;
         const double h = hypot(re, im);
         const double I = h * h;
         P[idx] = I;
@@ -229,9 +232,9 @@ int64_t akb_psf_work_bytes(int ny, int nx, int pad, int batch) {
 int akb_psf_f64(const double* opd, const double* amp, int ny, int nx, int pad, int batch,
                 const double* lambdas, double dx, double dy, const double* hann_wy,
                 const double* hann_wx, double hann_max, double* psf, double* efield_re_im,
-                double* d_imax, void* work, void* stream) {
+                double* d_imax, const double* d_pitch, void* work, void* stream) {
     clear_error();
-    AKB_REQUIRE(opd && amp && lambdas && psf && d_imax && work, "null pointer");
+    AKB_REQUIRE(opd && lambdas && psf && d_imax && work, "null pointer");
     AKB_REQUIRE(ny > 0 && nx > 0 && pad >= 1, "bad pupil size / pad");
     AKB_REQUIRE(batch >= 1 && batch <= 8, "batch must be 1..8");
     AKB_REQUIRE((hann_wy == nullptr) == (hann_wx == nullptr), "hann needs both axes");
@@ -254,7 +257,8 @@ int akb_psf_f64(const double* opd, const double* amp, int ny, int nx, int pad, i
     pa.field = field;
     const int64_t total = (int64_t)g.py * g.px;
     const unsigned gx = (unsigned)((g.px + kBlock - 1) / kBlock);
-    const unsigned gy = (unsigned)(g.py < 4096 ? g.py : 4096);
+    // rows per workgroup: ~1k workgroups in all, so the per-workgroup peak atomics stay few
+    const unsigned gy = (unsigned)(g.py < 128 ? g.py : 128);
     k_psf_pupil<<<dim3(gx, gy, batch), kBlock, 0, s>>>(pa);
     if ((st = launch_status("k_psf_pupil"))) return st;
 
@@ -278,6 +282,7 @@ int akb_psf_f64(const double* opd, const double* amp, int ny, int nx, int pad, i
     ia.field = field;
     ia.g = g;
     ia.dA = dx * dy;
+    ia.pitch = d_pitch;
     ia.psf = psf;
     ia.efield = (double2*)efield_re_im;
     ia.imax = d_imax;

@@ -54,8 +54,10 @@ __device__ double pw_leaf_lds(const double* s, int off, int n) {
     return res;
 }
 
+// part / part_cnt: row r, buffer c lands at [r * part_ld + part_col0 + c]
 __global__ void __launch_bounds__(kPwThreads) k_pw_chunks(const double* __restrict__ x, int64_t ld, int64_t n,
-                                                          int nan0, int nchunks, double* __restrict__ part,
+                                                          int nan_mask, int part_ld, int part_col0,
+                                                          double* __restrict__ part,
                                                           long long* __restrict__ part_cnt) {
     __shared__ double s[(kPwBuf / kPwLeaf) * kPwStride];
     __shared__ double leafv[kPwMaxLeaves];
@@ -68,6 +70,7 @@ __global__ void __launch_bounds__(kPwThreads) k_pw_chunks(const double* __restri
     const double* a = x + row * ld + (int64_t)c * kPwBuf;
     const int64_t rem = n - (int64_t)c * kPwBuf;
     const int len = rem < kPwBuf ? (int)rem : kPwBuf;
+    const bool nan0 = (nan_mask >> (row < 31 ? row : 31)) & 1;
 
     long long cnt = 0;
     // stage: 16 independent loads per thread in flight before the LDS stores (a full buffer is
@@ -192,10 +195,36 @@ __global__ void __launch_bounds__(kPwThreads) k_pw_chunks(const double* __restri
         }
     }
     if (tid == 0) {
-        part[(int64_t)row * nchunks + c] = result;
+        const int64_t o = (int64_t)row * part_ld + part_col0 + c;
+        part[o] = result;
         long long tc = 0;
         for (int w = 0; w < kPwThreads / 64; ++w) tc += wcnt[w];
-        part_cnt[(int64_t)row * nchunks + c] = tc;
+        part_cnt[o] = tc;
+    }
+}
+
+// full 8192-element buffers from producer leaf sums: one wave per (buffer, quantity); the six
+// xor-shuffles are numpy's split tree over the buffer's 64 leaves
+__global__ void __launch_bounds__(64) k_leaf_chunks(const double* __restrict__ leaf_sum,
+                                                    const int* __restrict__ leaf_cnt, int64_t nleaves,
+                                                    int part_ld, double* __restrict__ part,
+                                                    long long* __restrict__ part_cnt) {
+    const int q = blockIdx.y;
+    const int c = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int64_t li = (int64_t)q * nleaves + (int64_t)c * 64 + lane;
+    double v = leaf_sum[li];
+    long long k = leaf_cnt[li];
+    v = v + __shfl_xor(v, 1);
+    v = v + __shfl_xor(v, 2);
+    v = v + __shfl_xor(v, 4);
+    v = v + __shfl_xor(v, 8);
+    v = v + __shfl_xor(v, 16);
+    v = v + __shfl_xor(v, 32);
+    for (int off = 32; off > 0; off >>= 1) k += __shfl_down(k, off);
+    if (lane == 0) {
+        part[(int64_t)q * part_ld + c] = v;
+        part_cnt[(int64_t)q * part_ld + c] = k;
     }
 }
 
@@ -272,10 +301,69 @@ int akb_pairwise_sum_f64(const double* x, int64_t ld, int rows, int64_t n, int n
     const int nb = (int)nb64;
     double* part = (double*)d_work;
     long long* part_cnt = (long long*)(part + (int64_t)rows * nb);
-    k_pw_chunks<<<dim3(nb, rows), kPwThreads, 0, s>>>(x, ld, n, nan_to_zero, nb, part, part_cnt);
+    k_pw_chunks<<<dim3(nb, rows), kPwThreads, 0, s>>>(x, ld, n, nan_to_zero ? -1 : 0, nb, 0, part, part_cnt);
     int st = launch_status("k_pw_chunks");
     if (st) return st;
     k_pw_final<<<rows, kPwThreads, 0, s>>>(part, part_cnt, nb, d_sum, d_count);
+    return launch_status("k_pw_final");
+}
+
+int64_t akb_leaf_sink_bytes(int nq, int64_t n) {
+    if (nq <= 0 || n < 0) return 0;
+    const int64_t nleaves = (n / kPwBuf) * (kPwBuf / kPwLeaf);
+    const int64_t a = ((int64_t)nq * nleaves * 8 + 255) / 256 * 256;
+    const int64_t b = ((int64_t)nq * nleaves * 4 + 255) / 256 * 256;
+    return a + b + (int64_t)nq * kPwBuf * 8;
+}
+
+int akb_leaf_sink_layout(void* base, int nq, int nan_mask, int64_t n, akb_leaf_sink* out) {
+    clear_error();
+    AKB_REQUIRE(base && out && nq > 0 && nq <= 8 && n >= 0, "bad sink layout arguments");
+    const int64_t nleaves = (n / kPwBuf) * (kPwBuf / kPwLeaf);
+    const int64_t a = ((int64_t)nq * nleaves * 8 + 255) / 256 * 256;
+    const int64_t b = ((int64_t)nq * nleaves * 4 + 255) / 256 * 256;
+    out->leaf_sum = (double*)base;
+    out->leaf_cnt = (int32_t*)((char*)base + a);
+    out->tail = (double*)((char*)base + a + b);
+    out->nq = nq;
+    out->nan_mask = nan_mask;
+    out->n = n;
+    return AKB_OK;
+}
+
+int64_t akb_leaf_finish_work_bytes(int nq, int64_t n) {
+    const int64_t nb = n <= 0 ? 1 : (n + kPwBuf - 1) / kPwBuf;
+    return (int64_t)nq * nb * 16;
+}
+
+int akb_leaf_finish_f64(const akb_leaf_sink* sink, double* d_sum, int64_t* d_count, void* work, void* stream) {
+    clear_error();
+    AKB_REQUIRE(sink && d_sum && d_count && work, "null pointer");
+    AKB_REQUIRE(sink->nq > 0 && sink->nq <= 8 && sink->n >= 0, "bad sink");
+    hipStream_t s = (hipStream_t)stream;
+    const int nq = sink->nq;
+    if (sink->n == 0) {
+        AKB_HIP_CHECK(hipMemsetAsync(d_count, 0, sizeof(int64_t) * nq, s));
+        AKB_HIP_CHECK(hipMemsetAsync(d_sum, 0, sizeof(double) * nq, s));
+        return AKB_OK;
+    }
+    const int64_t nfull = sink->n / kPwBuf;
+    const int tail = (int)(sink->n - nfull * kPwBuf);
+    const int nb = (int)(nfull + (tail > 0 ? 1 : 0));
+    double* part = (double*)work;
+    long long* part_cnt = (long long*)(part + (int64_t)nq * nb);
+    int st;
+    if (nfull > 0) {
+        k_leaf_chunks<<<dim3((unsigned)nfull, nq), 64, 0, s>>>(sink->leaf_sum, sink->leaf_cnt,
+                                                                nfull * (kPwBuf / kPwLeaf), nb, part, part_cnt);
+        if ((st = launch_status("k_leaf_chunks"))) return st;
+    }
+    if (tail > 0) {
+        k_pw_chunks<<<dim3(1, nq), kPwThreads, 0, s>>>(sink->tail, kPwBuf, tail, sink->nan_mask, nb,
+                                                        (int)nfull, part, part_cnt);
+        if ((st = launch_status("k_pw_chunks(tail)"))) return st;
+    }
+    k_pw_final<<<nq, kPwThreads, 0, s>>>(part, part_cnt, nb, d_sum, d_count);
     return launch_status("k_pw_final");
 }
 

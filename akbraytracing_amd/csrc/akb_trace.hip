@@ -166,7 +166,9 @@ struct ChainArgs {
     int64_t dir_ld, dir_inc;
     const double* tan_h;
     const double* tan_v;
-    int64_t n_h;
+    uint32_t n_h;
+    uint32_t div_mul;  // Granlund-Montgomery magic for g / n_h with 32-bit g (see div_magic)
+    uint32_t div_shift;
     int64_t g0;  // global flat index of ray 0 of this launch
     int64_t n;
     const double* org;
@@ -187,108 +189,150 @@ struct ChainArgs {
     double* samp_h;
     double* samp_v;
     int32_t* flags;
+    akb_leaf_sink sink;
 };
 
-// Flag bit layout of the chain: mirror k uses bits 4k..4k+3 (MISS, ZERO_NORMAL, ZERO_REFLECT);
-// AKB_FLAG_CHAIN_DIR marks a zero-norm generated initial direction.
+// row / column of flat grid index g without a 64-bit division: q = (t + ((g - t) >> 1)) >> (s - 1)
+// with t = mulhi(g, m'), exact for every 32-bit g (Granlund & Montgomery 1994, fig. 4.1)
+__device__ __forceinline__ void grid_rc(const ChainArgs& a, int64_t g, int64_t& iv, int64_t& ih) {
+    const uint32_t g32 = (uint32_t)g;
+    uint32_t q;
+    if (a.n_h == 1) {
+        q = g32;
+    } else {
+        const uint32_t t = __umulhi(g32, a.div_mul);
+        q = (t + ((g32 - t) >> 1)) >> (a.div_shift - 1);
+    }
+    iv = (int64_t)q;
+    ih = g - iv * (int64_t)a.n_h;
+}
 
-template <bool kGrid, bool kOPL>
-__global__ void __launch_bounds__(kBlock) k_chain(ChainArgs a) {
-    int fl = 0;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < a.n;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t g = a.g0 + i;
-        double l, m, nn;
-        if (kGrid) {
-            // phai0[:, iv*n_h + ih] = (1, tan(p0h[ih]), tan(p0v[iv])) normalised (ref :2711-2717)
-            const int64_t iv = g / a.n_h;
-            const int64_t ih = g - iv * a.n_h;
-            const double th = a.tan_h[ih];
-            const double tv = a.tan_v[iv];
-            const double s = norm3(1.0, th, tv);
-            if (s == 0.0) fl |= AKB_FLAG_CHAIN_DIR;
-            l = 1.0 / s;
-            m = th / s;
-            nn = tv / s;
-        } else {
-            l = a.dir[i * a.dir_inc];
-            m = a.dir[a.dir_ld + i * a.dir_inc];
-            nn = a.dir[2 * a.dir_ld + i * a.dir_inc];
-        }
-        double p, q, r;
-        if (a.org) {
-            p = a.org[i * a.org_inc];
-            q = a.org[a.org_ld + i * a.org_inc];
-            r = a.org[2 * a.org_ld + i * a.org_inc];
-        } else {
-            p = a.src[0];
-            q = a.src[1];
-            r = a.src[2];
-        }
-        double opl = 0.0;
-        // not unrolled: each iteration reads its mirror's 10 coefficients from the kernel
-        // argument segment with scalar loads (wave-uniform), keeping VGPR pressure low
+// One ray through the chain. Writes the requested per-ray outputs and returns the sink quantities
+// (arctan of the exit slopes and the detector hit) in qv.
+template <bool kGrid, bool kOPL, bool kNeedQ>
+__device__ __forceinline__ void chain_ray(const ChainArgs& a, int64_t i, int& fl, double (&qv)[5]) {
+    const int64_t g = a.g0 + i;
+    double l, m, nn;
+    int64_t iv = 0, ih = 0;
+    if (kGrid) {
+        // phai0[:, iv*n_h + ih] = (1, tan(p0h[ih]), tan(p0v[iv])) normalised (ref :2711-2717)
+        grid_rc(a, g, iv, ih);
+        const double th = a.tan_h[ih];
+        const double tv = a.tan_v[iv];
+        const double s = norm3(1.0, th, tv);
+        if (s == 0.0) fl |= AKB_FLAG_CHAIN_DIR;
+        l = 1.0 / s;
+        m = th / s;
+        nn = tv / s;
+    } else {
+        l = a.dir[i * a.dir_inc];
+        m = a.dir[a.dir_ld + i * a.dir_inc];
+        nn = a.dir[2 * a.dir_ld + i * a.dir_inc];
+    }
+    double p, q, r;
+    if (a.org) {
+        p = a.org[i * a.org_inc];
+        q = a.org[a.org_ld + i * a.org_inc];
+        r = a.org[2 * a.org_ld + i * a.org_inc];
+    } else {
+        p = a.src[0];
+        q = a.src[1];
+        r = a.src[2];
+    }
+    double opl = 0.0;
+    // not unrolled: each iteration reads its mirror's 10 coefficients from the kernel
+    // argument segment with scalar loads (wave-uniform), keeping VGPR pressure low
 #pragma unroll 1
-        for (int k = 0; k < a.K; ++k) {
-            const Quadric Q = a.q[k];
-            double x, y, z;
-            if (!quadric_hit(Q, l, m, nn, p, q, r, (a.negmask >> k) & 1, x, y, z))
-                fl |= AKB_FLAG_MISS << (4 * k);
-            if (kOPL) {
-                const double d = norm3(x - p, y - q, z - r);
-                opl = (k == 0) ? d : opl + d;
-            }
-            if (a.hits) {
-                double* h = a.hits + (int64_t)k * 3 * a.hits_ld;
-                h[i] = x;
-                h[a.hits_ld + i] = y;
-                h[2 * a.hits_ld + i] = z;
-            }
-            double nx, ny, nz;
-            quadric_grad(Q, x, y, z, nx, ny, nz);
-            const double sn = norm3(nx, ny, nz);
-            if (sn == 0.0) fl |= AKB_FLAG_ZERO_NORMAL << (4 * k);
-            nx = nx / sn;
-            ny = ny / sn;
-            nz = nz / sn;
-            double rx, ry, rz;
-            reflect_raw(l, m, nn, nx, ny, nz, rx, ry, rz);
-            const double sr = norm3(rx, ry, rz);
-            if (sr == 0.0) fl |= AKB_FLAG_ZERO_REFLECT << (4 * k);
-            l = rx / sr;
-            m = ry / sr;
-            nn = rz / sr;
-            p = x;
-            q = y;
-            r = z;
+    for (int k = 0; k < a.K; ++k) {
+        const Quadric Q = a.q[k];
+        double x, y, z;
+        if (!quadric_hit(Q, l, m, nn, p, q, r, (a.negmask >> k) & 1, x, y, z)) fl |= AKB_FLAG_MISS << (4 * k);
+        if (kOPL) {
+            const double d = norm3(x - p, y - q, z - r);
+            opl = (k == 0) ? d : opl + d;
         }
-        if (kOPL && a.opl) a.opl[i] = opl;
-        if (a.last_hit) {
-            a.last_hit[i] = p;
-            a.last_hit[a.last_hit_ld + i] = q;
-            a.last_hit[2 * a.last_hit_ld + i] = r;
+        if (a.hits) {
+            double* h = a.hits + (int64_t)k * 3 * a.hits_ld;
+            h[i] = x;
+            h[a.hits_ld + i] = y;
+            h[2 * a.hits_ld + i] = z;
         }
-        if (a.dir_out) {
-            a.dir_out[i] = l;
-            a.dir_out[a.dir_out_ld + i] = m;
-            a.dir_out[2 * a.dir_out_ld + i] = nn;
-        }
+        double nx, ny, nz;
+        quadric_grad(Q, x, y, z, nx, ny, nz);
+        const double sn = norm3(nx, ny, nz);
+        if (sn == 0.0) fl |= AKB_FLAG_ZERO_NORMAL << (4 * k);
+        nx = nx / sn;
+        ny = ny / sn;
+        nz = nz / sn;
+        double rx, ry, rz;
+        reflect_raw(l, m, nn, nx, ny, nz, rx, ry, rz);
+        const double sr = norm3(rx, ry, rz);
+        if (sr == 0.0) fl |= AKB_FLAG_ZERO_REFLECT << (4 * k);
+        l = rx / sr;
+        m = ry / sr;
+        nn = rz / sr;
+        p = x;
+        q = y;
+        r = z;
+    }
+    if (kOPL && a.opl) a.opl[i] = opl;
+    if (a.last_hit) {
+        a.last_hit[i] = p;
+        a.last_hit[a.last_hit_ld + i] = q;
+        a.last_hit[2 * a.last_hit_ld + i] = r;
+    }
+    if (a.dir_out) {
+        a.dir_out[i] = l;
+        a.dir_out[a.dir_out_ld + i] = m;
+        a.dir_out[2 * a.dir_out_ld + i] = nn;
+    }
+    if (kNeedQ || a.det_out) {
+        double x, y, z;
+        plane_hit(a.det[0], a.det[1], a.det[2], a.det[3], l, m, nn, p, q, r, x, y, z);
         if (a.det_out) {
-            double x, y, z;
-            plane_hit(a.det[0], a.det[1], a.det[2], a.det[3], l, m, nn, p, q, r, x, y, z);
             a.det_out[i] = x;
             a.det_out[a.det_out_ld + i] = y;
             a.det_out[2 * a.det_out_ld + i] = z;
         }
-        if (a.atan_h) a.atan_h[i] = atan(m / l);
-        if (a.atan_v) a.atan_v[i] = atan(nn / l);
-        // equal-angle resample samples: the slope ratios only; the host applies np.arctan so the
-        // resampled angle tables match the reference bit for bit (glibc atan, ref :2858-2859)
-        if (a.samp_h && g >= a.sh_begin && g < a.sh_end) a.samp_h[g - a.sh_begin] = m / l;
-        if (a.samp_v && kGrid) {
-            const int64_t iv = g / a.n_h;
-            if (g - iv * a.n_h == a.sv_col) a.samp_v[iv] = nn / l;
-        }
+        qv[2] = x;
+        qv[3] = y;
+        qv[4] = z;
+    }
+    if (kNeedQ || a.atan_h || a.atan_v) {
+        qv[0] = atan(m / l);
+        qv[1] = atan(nn / l);
+        if (a.atan_h) a.atan_h[i] = qv[0];
+        if (a.atan_v) a.atan_v[i] = qv[1];
+    }
+    // equal-angle resample samples: the slope ratios only; the host applies np.arctan so the
+    // resampled angle tables match the reference bit for bit (glibc atan, ref :2858-2859)
+    if (a.samp_h && g >= a.sh_begin && g < a.sh_end) a.samp_h[g - a.sh_begin] = m / l;
+    if (a.samp_v && kGrid && ih == a.sv_col) a.samp_v[iv] = nn / l;
+}
+
+template <bool kGrid, bool kOPL>
+__global__ void __launch_bounds__(kBlock) k_chain(ChainArgs a) {
+    int fl = 0;
+    double qv[5];
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < a.n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        chain_ray<kGrid, kOPL, false>(a, i, fl, qv);
+    if (fl) atomicOr(a.flags, fl);
+}
+
+// the same, walking 256-ray segments and feeding the fused np.nanmean(arctan) / np.mean(det)
+// leaf sums (the tilt means, ref :3583-3591) instead of writing those five rows to HBM
+template <bool kGrid, bool kOPL>
+__global__ void __launch_bounds__(kBlock) k_chain_sink(ChainArgs a) {
+    __shared__ LeafLds<5> L;
+    int fl = 0;
+    const int64_t nseg = (a.n + kLeafSeg - 1) / kLeafSeg;
+    for (int64_t seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
+        const int64_t i = seg * kLeafSeg + threadIdx.x;
+        const bool valid = i < a.n;
+        double qv[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+        if (valid) chain_ray<kGrid, kOPL, true>(a, i, fl, qv);
+        leaf_sink_segment<5>(a.sink, L, seg * kLeafSeg, qv, valid);
     }
     if (fl) atomicOr(a.flags, fl);
 }
@@ -311,78 +355,158 @@ struct TiltArgs {
     double* det2;
     double* total1;
     double* total2;
+    akb_leaf_sink sink;
 };
 
-__global__ void __launch_bounds__(kBlock) k_tilt_opd(TiltArgs a) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < a.n;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        double ax, ay, az;
-        double l, m, n;
-        matvec(a.Rz, a.dir[i], a.dir[a.ld + i], a.dir[2 * a.ld + i], ax, ay, az);
-        matvec(a.Ry, ax, ay, az, l, m, n);
-        double p, q, r;
-        matvec(a.Rz, a.pt[i] - a.c[0], a.pt[a.ld + i] - a.c[1], a.pt[2 * a.ld + i] - a.c[2], ax, ay,
-               az);
-        matvec(a.Ry, ax, ay, az, p, q, r);
-        p = p + a.c[0];
-        q = q + a.c[1];
-        r = r + a.c[2];
-        if (a.dir_rot) {
-            a.dir_rot[i] = l;
-            a.dir_rot[a.ld + i] = m;
-            a.dir_rot[2 * a.ld + i] = n;
-        }
-        if (a.pt_rot) {
-            a.pt_rot[i] = p;
-            a.pt_rot[a.ld + i] = q;
-            a.pt_rot[2 * a.ld + i] = r;
-        }
-        const double o = a.opl ? a.opl[i] : 0.0;
-        double x, y, z;
-        plane_hit(a.d1[0], a.d1[1], a.d1[2], a.d1[3], l, m, n, p, q, r, x, y, z);
-        if (a.det1) {
-            a.det1[i] = x;
-            a.det1[a.ld + i] = y;
-            a.det1[2 * a.ld + i] = z;
-        }
-        if (a.total1) a.total1[i] = o + norm3(x - p, y - q, z - r);
-        plane_hit(a.d2[0], a.d2[1], a.d2[2], a.d2[3], l, m, n, p, q, r, x, y, z);
-        if (a.det2) {
-            a.det2[i] = x;
-            a.det2[a.ld + i] = y;
-            a.det2[2 * a.ld + i] = z;
-        }
-        if (a.total2) a.total2[i] = o + norm3(x - p, y - q, z - r);
+__device__ __forceinline__ void tilt_ray(const TiltArgs& a, int64_t i, double (&qv)[5]) {
+    double ax, ay, az;
+    double l, m, n;
+    matvec(a.Rz, a.dir[i], a.dir[a.ld + i], a.dir[2 * a.ld + i], ax, ay, az);
+    matvec(a.Ry, ax, ay, az, l, m, n);
+    double p, q, r;
+    matvec(a.Rz, a.pt[i] - a.c[0], a.pt[a.ld + i] - a.c[1], a.pt[2 * a.ld + i] - a.c[2], ax, ay, az);
+    matvec(a.Ry, ax, ay, az, p, q, r);
+    p = p + a.c[0];
+    q = q + a.c[1];
+    r = r + a.c[2];
+    if (a.dir_rot) {
+        a.dir_rot[i] = l;
+        a.dir_rot[a.ld + i] = m;
+        a.dir_rot[2 * a.ld + i] = n;
     }
+    if (a.pt_rot) {
+        a.pt_rot[i] = p;
+        a.pt_rot[a.ld + i] = q;
+        a.pt_rot[2 * a.ld + i] = r;
+    }
+    const double o = a.opl ? a.opl[i] : 0.0;
+    double x, y, z;
+    plane_hit(a.d1[0], a.d1[1], a.d1[2], a.d1[3], l, m, n, p, q, r, x, y, z);
+    if (a.det1) {
+        a.det1[i] = x;
+        a.det1[a.ld + i] = y;
+        a.det1[2 * a.ld + i] = z;
+    }
+    qv[0] = x;
+    qv[1] = y;
+    qv[2] = z;
+    qv[3] = o + norm3(x - p, y - q, z - r);
+    if (a.total1) a.total1[i] = qv[3];
+    plane_hit(a.d2[0], a.d2[1], a.d2[2], a.d2[3], l, m, n, p, q, r, x, y, z);
+    if (a.det2) {
+        a.det2[i] = x;
+        a.det2[a.ld + i] = y;
+        a.det2[2 * a.ld + i] = z;
+    }
+    qv[4] = o + norm3(x - p, y - q, z - r);
+    if (a.total2) a.total2[i] = qv[4];
+}
+
+__global__ void __launch_bounds__(kBlock) k_tilt_opd(TiltArgs a) {
+    double qv[5];
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < a.n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        tilt_ray(a, i, qv);
+}
+
+__global__ void __launch_bounds__(kBlock) k_tilt_opd_sink(TiltArgs a) {
+    __shared__ LeafLds<5> L;
+    const int64_t nseg = (a.n + kLeafSeg - 1) / kLeafSeg;
+    for (int64_t seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
+        const int64_t i = seg * kLeafSeg + threadIdx.x;
+        const bool valid = i < a.n;
+        double qv[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+        if (valid) tilt_ray(a, i, qv);
+        leaf_sink_segment<5>(a.sink, L, seg * kLeafSeg, qv, valid);
+    }
+}
+
+// ----------------------------------------------------------------------------------------------
+// OPD maps + pupil footprint (ref :3626, :3633, :3675-3677)
+// ----------------------------------------------------------------------------------------------
+
+// order-preserving uint64 key of a double (larger double -> larger key); 0 is below every key
+__device__ __forceinline__ unsigned long long order_key(double v) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ULL);
+}
+__device__ __forceinline__ double key_value(unsigned long long k) {
+    const unsigned long long b = (k >> 63) ? (k & 0x7fffffffffffffffULL) : ~k;
+    return __longlong_as_double((long long)b);
 }
 
 struct OpdArgs {
     const double* t1;
-    double mean1;
     const double* t2;
-    double mean2;
     const double* det2;
     int64_t ld, n;
-    double f[3];
+    const double* sum5;
+    const int64_t* cnt5;
     double* e1;
     double* e2;
     double* sph;
     double* wave;
+    unsigned long long* ext;
 };
 
 __global__ void __launch_bounds__(kBlock) k_opd(OpdArgs a) {
+    __shared__ double wext[kBlock / 64][4];
+    // np.nanmean results: sum / count in float64 (the reference's true_divide)
+    const double f0 = a.sum5[0] / (double)a.cnt5[0];
+    const double f1 = a.sum5[1] / (double)a.cnt5[1];
+    const double f2 = a.sum5[2] / (double)a.cnt5[2];
+    const double mean1 = a.sum5[3] / (double)a.cnt5[3];
+    const double mean2 = a.sum5[4] / (double)a.cnt5[4];
+    double e[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < a.n;
          i += (int64_t)gridDim.x * blockDim.x) {
-        if (a.e1) a.e1[i] = (a.t1[i] - a.mean1) * 1e9;
-        double e2 = 0.0;
-        if (a.t2) e2 = (a.t2[i] - a.mean2) * 1e9;
+        if (a.e1) a.e1[i] = (a.t1[i] - mean1) * 1e9;
+        const double e2 = (a.t2[i] - mean2) * 1e9;
         if (a.e2) a.e2[i] = e2;
+        const double y = a.det2[a.ld + i], z = a.det2[2 * a.ld + i];
         if (a.sph || a.wave) {
-            const double s =
-                norm3(a.det2[i] - a.f[0], a.det2[a.ld + i] - a.f[1], a.det2[2 * a.ld + i] - a.f[2]) * 1e9;
+            const double s = norm3(a.det2[i] - f0, y - f1, z - f2) * 1e9;
             if (a.sph) a.sph[i] = s;
             if (a.wave) a.wave[i] = e2 - s;
         }
+        if (a.ext) {  // fmax ignores NaN
+            e[0] = fmax(e[0], y);
+            e[1] = fmax(e[1], -y);
+            e[2] = fmax(e[2], z);
+            e[3] = fmax(e[3], -z);
+        }
+    }
+    if (a.ext) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            for (int off = 32; off > 0; off >>= 1) e[k] = fmax(e[k], __shfl_down(e[k], off));
+        if ((threadIdx.x & 63) == 0)
+            for (int k = 0; k < 4; ++k) wext[threadIdx.x >> 6][k] = e[k];
+        __syncthreads();
+        if (threadIdx.x < 4) {
+            double v = wext[0][threadIdx.x];
+            for (int w = 1; w < kBlock / 64; ++w) v = fmax(v, wext[w][threadIdx.x]);
+            atomicMax(a.ext + threadIdx.x, order_key(v));
+        }
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) k_pupil(const double* wave, int64_t row0, int64_t rows, int64_t n,
+                                                  int size, const unsigned long long* ext, double* opd,
+                                                  double* pitch) {
+    const int64_t total = (int64_t)size * size;
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < total;
+         k += (int64_t)gridDim.x * blockDim.x) {
+        const int ky = (int)(k / size), kx = (int)(k - (int64_t)ky * size);
+        const int64_t iv = ((int64_t)ky * (n - 1)) / (size - 1);
+        const int64_t ih = ((int64_t)kx * (n - 1)) / (size - 1);
+        double v = 0.0;
+        if (iv >= row0 && iv < row0 + rows) v = wave[(iv - row0) * n + ih] * 1e-9;
+        opd[k] = v;
+    }
+    if (pitch && blockIdx.x == 0 && threadIdx.x == 0) {
+        pitch[0] = (key_value(ext[0]) + key_value(ext[1])) / (double)(size - 1);
+        pitch[1] = (key_value(ext[2]) + key_value(ext[3])) / (double)(size - 1);
     }
 }
 
@@ -506,6 +630,20 @@ int akb_fill_nan_f64(double* out, int64_t ld, int rows, int64_t n, void* stream)
 
 int64_t akb_chain_desc_size(void) { return (int64_t)sizeof(akb_chain_desc); }
 
+// magic numbers for unsigned 32-bit division by d >= 2: l = ceil(log2 d),
+// m' = floor(2^32 (2^l - d) / d) + 1 (Granlund & Montgomery 1994, fig. 4.1)
+static void div_magic(uint32_t d, uint32_t* mul, uint32_t* shift) {
+    if (d <= 1) {
+        *mul = 0;
+        *shift = 0;
+        return;
+    }
+    uint32_t l = 0;
+    while ((1ULL << l) < d) ++l;
+    *mul = (uint32_t)((((1ULL << l) - d) << 32) / d + 1);
+    *shift = l;
+}
+
 int akb_trace_chain_f64(const akb_chain_desc* d, void* stream) {
     clear_error();
     AKB_REQUIRE(d != nullptr, "null descriptor");
@@ -517,8 +655,14 @@ int akb_trace_chain_f64(const akb_chain_desc* d, void* stream) {
         AKB_REQUIRE(d->tan_h && d->tan_v && d->n_h > 0 && d->n_v > 0, "grid tables missing");
         AKB_REQUIRE(d->row0 >= 0 && d->row0 * d->n_h + d->n_rays <= d->n_h * d->n_v,
                     "shard exceeds the ray grid");
+        AKB_REQUIRE(d->n_h * d->n_v < (1LL << 32), "ray grid beyond 2^32 rays");
     }
     if (d->samp_v) AKB_REQUIRE(grid && d->samp_v_col >= 0 && d->samp_v_col < d->n_h, "bad samp_v_col");
+    const bool sink = d->sink.nq > 0;
+    if (sink) {
+        AKB_REQUIRE(d->sink.nq == 5 && d->sink.n == d->n_rays && d->sink.leaf_sum && d->sink.leaf_cnt &&
+                        d->sink.tail, "chain sink must be a 5-quantity sink over n_rays");
+    }
     if (d->n_rays == 0) return AKB_OK;
     ChainArgs a{};
     a.K = d->n_mirrors;
@@ -533,7 +677,8 @@ int akb_trace_chain_f64(const akb_chain_desc* d, void* stream) {
     a.dir_inc = d->dir_inc;
     a.tan_h = d->tan_h;
     a.tan_v = d->tan_v;
-    a.n_h = grid ? d->n_h : 1;
+    a.n_h = grid ? (uint32_t)d->n_h : 1u;
+    div_magic(a.n_h, &a.div_mul, &a.div_shift);
     a.g0 = grid ? d->row0 * d->n_h : 0;
     a.n = d->n_rays;
     a.org = d->org;
@@ -557,8 +702,22 @@ int akb_trace_chain_f64(const akb_chain_desc* d, void* stream) {
     a.samp_h = d->samp_h;
     a.samp_v = d->samp_v;
     a.flags = d->flags;
-    const unsigned gsz = grid_for(d->n_rays);
+    a.sink = d->sink;
     hipStream_t s = (hipStream_t)stream;
+    const unsigned gsz = grid_for(d->n_rays);
+    if (sink) {
+        const int64_t nseg = (d->n_rays + kLeafSeg - 1) / kLeafSeg;
+        const unsigned gs = (unsigned)(nseg < 256 * 8 ? nseg : 256 * 8);
+        if (grid && d->opl)
+            k_chain_sink<true, true><<<gs, kBlock, 0, s>>>(a);
+        else if (grid)
+            k_chain_sink<true, false><<<gs, kBlock, 0, s>>>(a);
+        else if (d->opl)
+            k_chain_sink<false, true><<<gs, kBlock, 0, s>>>(a);
+        else
+            k_chain_sink<false, false><<<gs, kBlock, 0, s>>>(a);
+        return launch_status("k_chain_sink");
+    }
     if (grid) {
         if (d->opl)
             k_chain<true, true><<<gsz, kBlock, 0, s>>>(a);
@@ -577,10 +736,14 @@ int akb_tilt_opd_f64(const double ry[9], const double rz[9], const double center
                      const double det1_ghij[4], const double det2_ghij[4], const double* dir,
                      const double* pt, const double* opl, int64_t ld, int64_t n, double* dir_rot,
                      double* pt_rot, double* det1, double* det2, double* total1, double* total2,
-                     void* stream) {
+                     const akb_leaf_sink* sink, void* stream) {
     clear_error();
     AKB_REQUIRE(ry && rz && center && det1_ghij && det2_ghij && dir && pt, "null pointer");
     AKB_REQUIRE(n >= 0 && ld >= n, "bad sizes");
+    const bool use_sink = sink && sink->nq > 0;
+    if (use_sink)
+        AKB_REQUIRE(sink->nq == 5 && sink->n == n && sink->leaf_sum && sink->leaf_cnt && sink->tail,
+                    "tilt sink must be a 5-quantity sink over n");
     if (n == 0) return AKB_OK;
     TiltArgs a{};
     for (int k = 0; k < 9; ++k) {
@@ -603,34 +766,55 @@ int akb_tilt_opd_f64(const double ry[9], const double rz[9], const double center
     a.det2 = det2;
     a.total1 = total1;
     a.total2 = total2;
+    if (use_sink) {
+        a.sink = *sink;
+        const int64_t nseg = (n + kLeafSeg - 1) / kLeafSeg;
+        const unsigned gs = (unsigned)(nseg < 256 * 8 ? nseg : 256 * 8);
+        k_tilt_opd_sink<<<gs, kBlock, 0, (hipStream_t)stream>>>(a);
+        return launch_status("k_tilt_opd_sink");
+    }
     k_tilt_opd<<<grid_for(n), kBlock, 0, (hipStream_t)stream>>>(a);
     return launch_status("k_tilt_opd");
 }
 
-int akb_opd_f64(const double* total1, double mean1, const double* total2, double mean2,
-                const double* det2, int64_t ld, const double mean_focus[3], int64_t n,
-                double* dist_err1, double* dist_err2, double* sph, double* wave, void* stream) {
+int akb_opd_f64(const double* total1, const double* total2, const double* det2, int64_t ld, int64_t n,
+                const double* d_sum5, const int64_t* d_cnt5, double* dist_err1, double* dist_err2,
+                double* sph, double* wave, uint64_t* d_extent_keys, void* stream) {
     clear_error();
-    AKB_REQUIRE(n >= 0, "n < 0");
+    AKB_REQUIRE(n >= 0 && ld >= n, "bad sizes");
+    AKB_REQUIRE(total2 && det2 && d_sum5 && d_cnt5, "total2, det2 and the tilt means are required");
     AKB_REQUIRE(!dist_err1 || total1, "dist_err1 needs total1");
-    AKB_REQUIRE(!(dist_err2 || wave) || total2, "dist_err2/wave need total2");
-    AKB_REQUIRE(!(sph || wave) || (det2 && mean_focus), "sph/wave need det2 and mean_focus");
+    hipStream_t s = (hipStream_t)stream;
+    if (d_extent_keys) AKB_HIP_CHECK(hipMemsetAsync(d_extent_keys, 0, 4 * sizeof(uint64_t), s));
     if (n == 0) return AKB_OK;
     OpdArgs a{};
     a.t1 = total1;
-    a.mean1 = mean1;
     a.t2 = total2;
-    a.mean2 = mean2;
     a.det2 = det2;
     a.ld = ld;
     a.n = n;
-    for (int k = 0; k < 3; ++k) a.f[k] = mean_focus ? mean_focus[k] : 0.0;
+    a.sum5 = d_sum5;
+    a.cnt5 = d_cnt5;
     a.e1 = dist_err1;
     a.e2 = dist_err2;
     a.sph = sph;
     a.wave = wave;
-    k_opd<<<grid_for(n), kBlock, 0, (hipStream_t)stream>>>(a);
+    a.ext = (unsigned long long*)d_extent_keys;
+    const unsigned g = grid_for(n, 4) < 1024 ? grid_for(n, 4) : 1024;  // <= 4096 extent atomics
+    k_opd<<<g, kBlock, 0, s>>>(a);
     return launch_status("k_opd");
+}
+
+int akb_pupil_sample_f64(const double* wave, int64_t row0, int64_t rows, int64_t n, int size,
+                         const uint64_t* d_extent_keys, double* opd_m, double* d_pitch, void* stream) {
+    clear_error();
+    AKB_REQUIRE(wave && opd_m, "null pointer");
+    AKB_REQUIRE(size >= 2 && n >= 2 && row0 >= 0 && rows >= 0 && row0 + rows <= n, "bad sizes");
+    AKB_REQUIRE(!d_pitch || d_extent_keys, "pitch needs the extent keys");
+    const int64_t total = (int64_t)size * size;
+    k_pupil<<<grid_for(total), kBlock, 0, (hipStream_t)stream>>>(
+        wave, row0, rows, n, size, (const unsigned long long*)d_extent_keys, opd_m, d_pitch);
+    return launch_status("k_pupil");
 }
 
 }  // extern "C"

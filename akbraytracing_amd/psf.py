@@ -74,11 +74,13 @@ _ws = PsfWorkspace()
 
 
 def psf_stack(opd, amp, wavelengths, dx, dy=None, pad_factor=2, window=None, return_efield=False,
-              workspace=None, stream=None):
-    """Device API. opd, amp: (ny, nx) float64 device tensors. wavelengths: sequence of up to 8.
+              workspace=None, stream=None, pitch=None, out=None):
+    """Device API. opd, amp: (ny, nx) float64 device tensors (amp None: 1 where opd is finite,
+    psf_calc's mask). wavelengths: sequence of up to 8. pitch: optional device [dx, dy] tensor
+    replacing dx/dy (no host round trip). out: optional preallocated (B, py, px) psf tensor.
     Returns (psf (B, py, px), efield (B, py, px) complex128 or None, imax (B,) device tensor)."""
     L = _lib.lib()
-    _check_args(opd.shape, amp.shape, pad_factor, window)
+    _check_args(opd.shape, opd.shape if amp is None else amp.shape, pad_factor, window)
     dev = opd.device
     ny, nx = int(opd.shape[0]), int(opd.shape[1])
     pad = int(pad_factor)
@@ -87,7 +89,8 @@ def psf_stack(opd, amp, wavelengths, dx, dy=None, pad_factor=2, window=None, ret
     if not 1 <= B <= 8:
         raise ValueError("1..8 wavelengths per launch")
     py, px = (ny + ny % 2) * pad, (nx + nx % 2) * pad
-    psf = torch.empty((B, py, px), dtype=D.F64, device=dev)
+    psf = out if out is not None and tuple(out.shape) == (B, py, px) else torch.empty((B, py, px), dtype=D.F64,
+                                                                                         device=dev)
     ef = torch.empty((B, py, px), dtype=torch.complex128, device=dev) if return_efield else None
     imax = torch.empty(B, dtype=D.F64, device=dev)
     work = (workspace or _ws).get(ny, nx, pad, B, dev)
@@ -96,14 +99,14 @@ def psf_stack(opd, amp, wavelengths, dx, dy=None, pad_factor=2, window=None, ret
     if window is not None:
         hy, hx, wmax = hann_axes(ny, nx)
         wy, wx = D.to_dev(hy, dev), D.to_dev(hx, dev)
-    dxv = float(dx)
+    dxv = 0.0 if dx is None else float(dx)
     dyv = dxv if dy is None else float(dy)
     opd_c = opd.to(D.F64).contiguous()
-    amp_c = amp.to(D.F64).contiguous()
+    amp_c = None if amp is None else amp.to(D.F64).contiguous()
     _lib.check(L.akb_psf_f64(D.ptr(opd_c), D.ptr(amp_c), ny, nx, pad, B, D.host_f64(lams), dxv, dyv,
                              D.ptr(wy), D.ptr(wx), wmax, D.ptr(psf),
                              D.ptr(torch.view_as_real(ef)) if ef is not None else None, D.ptr(imax),
-                             D.ptr(work), D.stream_handle(stream)))
+                             D.ptr(pitch), D.ptr(work), D.stream_handle(stream)))
     return psf, ef, imax
 
 

@@ -58,3 +58,26 @@ def means_to_host(pairs):
             out.append(sums / cnts)
         off += 2 * r
     return out
+
+
+class LeafSink:
+    """Device buffers of an akb_leaf_sink: a producer kernel writes numpy pairwise leaf sums of
+    nq per-element quantities, finish() completes them to np.sum / np.nanmean results."""
+
+    def __init__(self, nq, n, nan_mask, dev):
+        L = _lib.lib()
+        self.nq, self.n = int(nq), int(n)
+        nbytes = max(int(L.akb_leaf_sink_bytes(nq, n)), 256)
+        self.buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        self.desc = _lib.LeafSink()
+        _lib.check(L.akb_leaf_sink_layout(D.ptr(self.buf), nq, int(nan_mask), n, self.desc))
+        wb = max(int(L.akb_leaf_finish_work_bytes(nq, n)), 16)
+        self.work = torch.empty(wb // 8 + 1, dtype=D.F64, device=dev)
+        self.sums = torch.empty(nq, dtype=D.F64, device=dev)
+        self.counts = torch.empty(nq, dtype=torch.int64, device=dev)
+
+    def finish(self, stream=None):
+        L = _lib.lib()
+        _lib.check(L.akb_leaf_finish_f64(self.desc, D.ptr(self.sums), D.ptr(self.counts), D.ptr(self.work),
+                                         D.stream_handle(stream)))
+        return self.sums, self.counts

@@ -62,7 +62,7 @@ def _fill_desc(desc, mirrors, det_ghij):
 
 
 def trace_chain(mirrors, *, tan_h=None, tan_v=None, row0=0, n_rays=None, dirs=None, src=(0.0, 0.0, 0.0),
-                det_ghij=None, want=("last_hit", "dir_out"), samples=None, out=None, stream=None):
+                det_ghij=None, want=("last_hit", "dir_out"), samples=None, out=None, sink=None, stream=None):
     """Run one fused chain launch.
 
     Rays: either the grid (tan_h, tan_v device tensors; rays row0*n_h .. + n_rays) or explicit
@@ -70,6 +70,8 @@ def trace_chain(mirrors, *, tan_h=None, tan_v=None, row0=0, n_rays=None, dirs=No
     want: subset of {"hits", "last_hit", "dir_out", "det", "opl", "atan"}.
     samples: (h_begin, h_end, v_col) flat-index range / column whose exit slopes to record.
     out: optional dict of preallocated tensors keyed like ChainOutputs fields (reused buffers).
+    sink: optional reduce.LeafSink(5, n_rays, nan_mask=0b00011) fed with (arctan(Ry/Rx),
+        arctan(Rz/Rx), det_x, det_y, det_z) — the tilt means without writing those rows.
     """
     L = _lib.lib()
     dev = D.device()
@@ -137,6 +139,10 @@ def trace_chain(mirrors, *, tan_h=None, tan_v=None, row0=0, n_rays=None, dirs=No
             res.samp_v = torch.full((tan_v.shape[0],), float("nan"), dtype=D.F64, device=dev)
             desc.samp_v, desc.samp_v_col = D.ptr(res.samp_v), vc
     desc.flags = D.ptr(res.flags)
+    if sink is not None:
+        if det_ghij is None:
+            raise ValueError("the chain sink reduces detector hits: give det_ghij")
+        desc.sink = sink.desc
     _lib.check(L.akb_trace_chain_f64(desc, D.stream_handle(stream)))
     res.extra["buffers"] = out
     return res

@@ -21,12 +21,11 @@ from dataclasses import dataclass, field
 
 import numpy as np
 import torch
-from scipy.interpolate import interp1d
 
 from . import _lib
 from . import device as D
 from . import primitives as P
-from .reduce import RowSums, means_to_host
+from .reduce import LeafSink, RowSums
 from .trace import Mirror, staged_chain, trace_chain
 
 
@@ -104,12 +103,22 @@ def sample_ownership(shard, n):
     return own_h, own_v
 
 
+def _interp1d_linear(x, y, x_new):
+    """scipy.interpolate.interp1d(x, y, kind='linear')(x_new) for 1-D float64 data: scipy sorts x
+    with a stable mergesort and delegates to np.interp (scipy 1.15 _call_linear_np)."""
+    ind = np.argsort(x, kind="mergesort")
+    xs, ys = x[ind], y[ind]
+    if np.any(x_new < xs[0]) or np.any(x_new > xs[-1]):
+        raise ValueError("A value in x_new is outside the interpolation range.")
+    return np.interp(x_new, xs, ys)
+
+
 def resample(angle_h_sep, angle_v_sep, rand_h, rand_v):
     """:2861-2870 — interp1d of the launch angles onto equally spaced exit angles."""
     out_v = np.linspace(angle_v_sep[0], angle_v_sep[-1], len(angle_v_sep))
     out_h = np.linspace(angle_h_sep[0], angle_h_sep[-1], len(angle_h_sep))
-    new_v = interp1d(angle_v_sep, rand_v, kind="linear")(out_v)
-    new_h = interp1d(angle_h_sep, rand_h, kind="linear")(out_h)
+    new_v = _interp1d_linear(np.asarray(angle_v_sep, dtype=np.float64), np.asarray(rand_v, dtype=np.float64), out_v)
+    new_h = _interp1d_linear(np.asarray(angle_h_sep, dtype=np.float64), np.asarray(rand_h, dtype=np.float64), out_h)
     return new_h, new_v
 
 
@@ -147,6 +156,14 @@ class RayWave:
         self.tan_v = torch.from_numpy(np.tan(self.rand_v)).to(self.dev)
         self.n_local = self.shard.rows * self.n
         self.sums = RowSums()
+        # fused numpy-order reductions: pass 2 -> (atan_h, atan_v, det x, y, z), nanmean for the
+        # arctans and plain mean for the detector (:3583-3590); tilt -> (det1 x, y, z, total1,
+        # total2), all nanmean (:3626, :3633, :3674)
+        self.sink2 = LeafSink(5, self.n_local, 0b00011, self.dev)
+        self.sink3 = LeafSink(5, self.n_local, 0b11111, self.dev)
+        self._ext = torch.zeros(4, dtype=torch.int64, device=self.dev)  # det2 extent keys (uint64 bits)
+        self._pitch = torch.zeros(2, dtype=D.F64, device=self.dev)
+        self._opd_buf = None
         self._buf1, self._buf2 = {}, {}
         self.last = {}
         self.kernel_events = None  # set to a list to time the pass-2 chain launch (bench.py)
@@ -172,14 +189,14 @@ class RayWave:
         flags = self.comm.sum_flags(flags)
         return samp_h, samp_v, flags
 
-    def _pass2(self, tan_h2, tan_v2):
+    def _pass2(self, tan_h2, tan_v2, want_rows=False):
         ev = None
         if self.kernel_events is not None:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
+        want = ("last_hit", "dir_out", "opl") + (("det", "atan") if want_rows else ())
         r = trace_chain(self.g.mirrors, tan_h=tan_h2, tan_v=tan_v2, row0=self.shard.row0, n_rays=self.n_local,
-                        src=self.g.source, det_ghij=self.g.det1,
-                        want=("last_hit", "dir_out", "det", "opl", "atan"), out=self._buf2)
+                        src=self.g.source, det_ghij=self.g.det1, want=want, out=self._buf2, sink=self.sink2)
         if ev is not None:
             ev[1].record()
             self.kernel_events.append(ev)
@@ -206,8 +223,11 @@ class RayWave:
     def run(self, opd=True, keep_rotated=False, full=False):
         """Trace and reduce; returns a dict of device tensors (this shard's rays) and host means.
         keep_rotated: also return the tilted direction / last hit (dir_rot, pt_rot); full: also
-        return DistError (detector 1) and Sph. The default keeps what griddata consumes
-        (DistError2, Wave2, detcenter2) plus the reduction inputs."""
+        return DistError (detector 1), Sph, detcenter and the pre-tilt rows. The default keeps what
+        griddata consumes (DistError2, Wave2, detcenter2) and reduces everything else on the fly.
+
+        Host round trips: two (the resample picks, and the tilt angles, whose rotation matrices are
+        formed with numpy's cos/sin exactly as the reference forms them)."""
         samp_h, samp_v, flags1 = self._pass1()
         if flags1:
             raise _lib.AKBError(
@@ -217,19 +237,18 @@ class RayWave:
             new_h, new_v = resample(np.arctan(samp_h), np.arctan(samp_v), self.rand_h, self.rand_v)
         else:
             new_h, new_v = self.rand_h, self.rand_v
-        tan_h2 = torch.from_numpy(np.tan(new_h)).to(self.dev)
-        tan_v2 = torch.from_numpy(np.tan(new_v)).to(self.dev)
-        r = self._pass2(tan_h2, tan_v2)
-        atan_s, atan_c = self.sums(r.atan, nan=True)
-        det_s, det_c = self.sums(r.det, nan=False)
-        red = torch.cat([atan_s, det_s, atan_c.to(D.F64), det_c.to(D.F64), r.flags.to(D.F64)])
-        red = self.comm.allreduce_sums(red)
+        tan_h2 = torch.from_numpy(np.tan(new_h)).to(self.dev, non_blocking=True)
+        tan_v2 = torch.from_numpy(np.tan(new_v)).to(self.dev, non_blocking=True)
+        r = self._pass2(tan_h2, tan_v2, want_rows=full)
+        sums, cnts = self.sink2.finish()
+        red = self.comm.allreduce_sums(torch.cat([sums, cnts.to(D.F64), r.flags.to(D.F64)]))
         host = red.cpu().numpy()
         flags2 = int(host[-1])
-        last_hit, dir_out, det, opl, atan = r.last_hit, r.dir_out, r.det, r.opl, r.atan
+        last_hit, dir_out, opl = r.last_hit, r.dir_out, r.opl
+        det_pre, atan = r.det, r.atan
         if flags2:
-            last_hit, dir_out, det, opl, atan = self._pass2_staged(tan_h2, tan_v2)
-            (atan_s, atan_c), (det_s, det_c) = self.sums(atan, nan=True), self.sums(det)
+            last_hit, dir_out, det_pre, opl, atan = self._pass2_staged(tan_h2, tan_v2)
+            (atan_s, atan_c), (det_s, det_c) = self.sums(atan, nan=True), self.sums(det_pre)
             red = self.comm.allreduce_sums(torch.cat([atan_s, det_s, atan_c.to(D.F64), det_c.to(D.F64)]))
             host = red.cpu().numpy()
         with np.errstate(invalid="ignore", divide="ignore"):
@@ -237,8 +256,10 @@ class RayWave:
             focus = host[2:5] / host[7:10]
         theta_y = -mean_atan[1]
         theta_z = mean_atan[0]
-        out = dict(last_hit=last_hit, dir_out=dir_out, det_pre=det, opl=opl, theta_y=theta_y, theta_z=theta_z,
+        out = dict(last_hit=last_hit, dir_out=dir_out, opl=opl, theta_y=theta_y, theta_z=theta_z,
                    focus_apprx=focus, tan_h2=tan_h2, tan_v2=tan_v2, flags=(flags1, flags2))
+        if full:
+            out.update(det_pre=det_pre, atan=atan)
         if opd:
             out.update(self._tilt_opd(last_hit, dir_out, opl, theta_y, theta_z, focus, keep_rotated, full))
         self.last = out
@@ -247,66 +268,71 @@ class RayWave:
     def _tilt_opd(self, last_hit, dir_out, opl, theta_y, theta_z, focus, keep_rotated=False, full=False):
         L = _lib.lib()
         n = self.n_local
+        dev = self.dev
         ry, rz = P.rotation_matrices(-theta_y, -theta_z)
-        det1 = torch.empty((3, n), dtype=D.F64, device=self.dev)
-        det2 = torch.empty((3, n), dtype=D.F64, device=self.dev) if self.g.det2 is not None else None
-        totals = torch.empty((2, n), dtype=D.F64, device=self.dev)
-        dir_rot = torch.empty((3, n), dtype=D.F64, device=self.dev) if keep_rotated else None
-        pt_rot = torch.empty((3, n), dtype=D.F64, device=self.dev) if keep_rotated else None
-        d2 = self.g.det2 if self.g.det2 is not None else self.g.det1
+        two = self.g.det2 is not None
+        det1 = torch.empty((3, n), dtype=D.F64, device=dev) if (full or not two) else None
+        det2 = torch.empty((3, n), dtype=D.F64, device=dev) if two else None
+        total1 = torch.empty(n, dtype=D.F64, device=dev) if (full or not two) else None
+        total2 = torch.empty(n, dtype=D.F64, device=dev)
+        dir_rot = torch.empty((3, n), dtype=D.F64, device=dev) if keep_rotated else None
+        pt_rot = torch.empty((3, n), dtype=D.F64, device=dev) if keep_rotated else None
+        d2 = self.g.det2 if two else self.g.det1
+        det2_buf = det2 if two else torch.empty((3, n), dtype=D.F64, device=dev)
         _lib.check(L.akb_tilt_opd_f64(D.host_f64(ry.ravel()), D.host_f64(rz.ravel()), D.host_f64(focus),
                                       D.host_f64(self.g.det1), D.host_f64(d2), D.ptr(dir_out), D.ptr(last_hit),
                                       D.ptr(opl), n, n, D.ptr(dir_rot), D.ptr(pt_rot), D.ptr(det1),
-                                      D.ptr(det2), D.ptr(totals), D.ptr(totals[1]), D.stream_handle()))
-        tot_s, tot_c = self.sums(totals, nan=True)
-        det_s, det_c = self.sums(det1, nan=True)
-        red = self.comm.allreduce_sums(torch.cat([tot_s, det_s, tot_c.to(D.F64), det_c.to(D.F64)]))
-        host = red.cpu().numpy()
-        with np.errstate(invalid="ignore", divide="ignore"):
-            mean_tot = host[0:2] / host[5:7]
-            mean_focus = host[2:5] / host[7:10]
-        dist_err = torch.empty(n, dtype=D.F64, device=self.dev) if (full or det2 is None) else None
-        res = dict(dir_rot=dir_rot, pt_rot=pt_rot, detcenter=det1, detcenter2=det2, total=totals[0],
-                   total2=totals[1], mean_total=mean_tot, mean_focus=mean_focus, dist_err=dist_err)
-        if det2 is not None:
-            dist_err2 = torch.empty(n, dtype=D.F64, device=self.dev)
-            sph = torch.empty(n, dtype=D.F64, device=self.dev) if full else None
-            wave2 = torch.empty(n, dtype=D.F64, device=self.dev)
-            _lib.check(L.akb_opd_f64(D.ptr(totals), float(mean_tot[0]), D.ptr(totals[1]), float(mean_tot[1]),
-                                     D.ptr(det2), n, D.host_f64(mean_focus), n, D.ptr(dist_err),
-                                     D.ptr(dist_err2), D.ptr(sph), D.ptr(wave2), D.stream_handle()))
-            res.update(dist_err2=dist_err2, sph=sph, wave2=wave2)
-        else:
-            _lib.check(L.akb_opd_f64(D.ptr(totals), float(mean_tot[0]), None, 0.0, None, n, None, n,
-                                     D.ptr(dist_err), None, None, None, D.stream_handle()))
+                                      D.ptr(det2_buf), D.ptr(total1), D.ptr(total2), self.sink3.desc,
+                                      D.stream_handle()))
+        sums, cnts = self.sink3.finish()
+        if self.comm.world > 1:  # cross-rank means: partial sums added over ranks (not numpy order)
+            red = self.comm.allreduce_sums(torch.cat([sums, cnts.to(D.F64)]))
+            sums = red[:5].contiguous()
+            cnts = red[5:].to(torch.int64).contiguous()
+        self._means5 = (sums, cnts)
+        dist_err = torch.empty(n, dtype=D.F64, device=dev) if total1 is not None else None
+        dist_err2 = torch.empty(n, dtype=D.F64, device=dev)
+        sph = torch.empty(n, dtype=D.F64, device=dev) if full else None
+        wave2 = torch.empty(n, dtype=D.F64, device=dev) if two else None
+        _lib.check(L.akb_opd_f64(D.ptr(total1), D.ptr(total2), D.ptr(det2_buf), n, n, D.ptr(sums), D.ptr(cnts),
+                                 D.ptr(dist_err), D.ptr(dist_err2), D.ptr(sph), D.ptr(wave2), D.ptr(self._ext),
+                                 D.stream_handle()))
+        res = dict(dir_rot=dir_rot, pt_rot=pt_rot, detcenter=det1, detcenter2=det2, total=total1, total2=total2,
+                   dist_err=dist_err, dist_err2=dist_err2, sph=sph, wave2=wave2)
         return res
 
+    def means(self):
+        """Host copies of the post-tilt means: (mean_total [detector 1, detector 2], mean_focus)."""
+        s, c = self._means5
+        h = torch.cat([s, c.to(D.F64)]).cpu().numpy()
+        m = h[:5] / h[5:]
+        return m[3:5], m[0:3]
+
     # -------------------------------------------------------------- pupil for the PSF
-    def pupil(self, size=128, out=None):
+    def pupil(self, size=128):
         """Wave2 (nm) sampled onto a size x size pupil in ray-index space (nearest ray), as OPD in
-        metres plus the binary amplitude, and the pitch of the detector-2 footprint.
+        metres, and the pupil pitch of the detector-2 footprint (device [dx, dy]).
 
         This stands in for griddata(cubic) + plane correction + rotate_with_nan of the driver
         (:3689-3710, psf_calc :1121-1188; SURVEY.md §8 rows f1/f4, not yet built): the ray grid is
-        a smooth deformed structured grid, so index-space sampling keeps the pupil's shape.
+        a smooth deformed structured grid, so index-space sampling keeps the pupil's shape. The
+        amplitude is psf_calc's mask (1 where the OPD is defined), formed inside the PSF kernel.
         Multi-GPU: each shard fills its rows and the pieces are summed over ranks."""
-        n = self.n
-        idx = torch.div(torch.arange(size, device=self.dev) * (n - 1), size - 1, rounding_mode="floor")
-        r0, rows = self.shard.row0, self.shard.rows
-        w = self.last["wave2"].view(rows, n)
-        mine = (idx >= r0) & (idx < r0 + rows)
-        opd = torch.zeros((size, size), dtype=D.F64, device=self.dev) if out is None else out.zero_()
-        sel = idx[mine] - r0
-        opd[mine] = w.index_select(0, sel).index_select(1, idx) * 1e-9
-        d2 = self.last["detcenter2"]
-        ext = torch.stack([torch.amax(d2[1]), -torch.amin(d2[1]), torch.amax(d2[2]), -torch.amin(d2[2])])
-        ext = self.comm.allreduce_max(ext) if self.comm.world > 1 else ext
-        opd = self.comm.allreduce_sums(opd) if self.comm.world > 1 else opd
-        amp = torch.isfinite(opd).to(D.F64)
-        e = ext.cpu().numpy()
-        dx = (e[0] + e[1]) / (size - 1)
-        dy = (e[2] + e[3]) / (size - 1)
-        return opd, amp, dx, dy
+        L = _lib.lib()
+        if self._opd_buf is None or self._opd_buf.shape[0] != size:
+            self._opd_buf = torch.empty((size, size), dtype=D.F64, device=self.dev)
+        ext = self._ext
+        if self.comm.world > 1:
+            # unsigned key order == signed order after flipping the top bit: MAX over ranks
+            flip = torch.tensor(-(1 << 63), dtype=torch.int64, device=self.dev)
+            ext = self.comm.allreduce_max(torch.bitwise_xor(ext, flip)).bitwise_xor(flip).contiguous()
+        _lib.check(L.akb_pupil_sample_f64(D.ptr(self.last["wave2"]), self.shard.row0, self.shard.rows, self.n,
+                                          size, D.ptr(ext), D.ptr(self._opd_buf), D.ptr(self._pitch),
+                                          D.stream_handle()))
+        opd = self._opd_buf
+        if self.comm.world > 1:
+            opd = self.comm.allreduce_sums(opd)
+        return opd, self._pitch
 
     # -------------------------------------------------------------- accounting
     def intersections_per_run(self):

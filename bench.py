@@ -30,8 +30,9 @@ sys.path.insert(0, ROOT)
 METRIC = "ray-surface intersections/sec + PSF wall-time, 1e7-ray 4-mirror AKB, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X spec, MI355X_MICROARCH.md
 # bytes the pass-2 chain kernel must move per ray: it reads two L2-resident 1-D tables and
-# writes last hit (24) + exit direction (24) + detector hit (24) + OPL (8) + 2 arctans (16)
-PASS2_BYTES_PER_RAY = 96
+# writes last hit (24) + exit direction (24) + OPL (8); the arctans and detector hits it also
+# forms are reduced in-kernel (numpy-order leaf sums, 5 x 8 B per 128 rays)
+PASS2_BYTES_PER_RAY = 56
 
 
 def parse():
@@ -105,15 +106,18 @@ def main():
     lam = 13.5e-9  # EUV, AKB_raytrace_20250312.py:1161-1162 / :3614
 
     psf_events = []
+    psf_out = {}
 
     def step(timed):
         rw.run()
-        opd, amp, dx, dy = rw.pupil(args.pupil)
+        opd, pitch = rw.pupil(args.pupil)
         if rank == 0:
             if timed:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-            psf, _, _ = psf_stack(opd, amp, [lam], dx, dy, pad_factor=args.pad)
+            psf, _, _ = psf_stack(opd, None, [lam], None, pitch=pitch, pad_factor=args.pad,
+                                  out=psf_out.get("psf"))
+            psf_out["psf"] = psf
             if timed:
                 e1.record()
                 psf_events.append((e0, e1))

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define AKB_ABI_VERSION 1
+#define AKB_ABI_VERSION 2
 
 /* status codes */
 #define AKB_OK 0
@@ -104,6 +104,30 @@ int akb_rotate_f64(const double ry[9], const double rz[9], const double center[3
 /* fill rows x n of `out` (row stride ld) with quiet NaN */
 int akb_fill_nan_f64(double* out, int64_t ld, int rows, int64_t n, void* stream);
 
+/* ---------------- numpy-order reductions fused into producer kernels ---------------- */
+
+/* A producer kernel that owns a leaf sink reduces up to 8 per-ray quantities on the fly, in
+ * numpy's summation order: for every full 8192-element buffer it writes the 64 pairwise leaf
+ * sums (128 consecutive elements, 8 accumulators each) and their non-NaN counts, and it copies
+ * the raw values of the short last buffer; akb_leaf_finish_f64 then completes np.sum /
+ * np.nanmean exactly as akb_pairwise_sum_f64 would on the materialised rows, without those rows
+ * ever reaching HBM. Lay one out with akb_leaf_sink_layout over akb_leaf_sink_bytes of memory. */
+typedef struct akb_leaf_sink {
+    double* leaf_sum;   /* [nq][n_full_leaves] */
+    int32_t* leaf_cnt;  /* [nq][n_full_leaves] */
+    double* tail;       /* [nq][8192] */
+    int32_t nq;         /* 0 disables the sink */
+    int32_t nan_mask;   /* bit q set: NaN -> 0 and not counted (np.nansum / np.nanmean) */
+    int64_t n;          /* elements reduced per quantity */
+} akb_leaf_sink;
+
+int64_t akb_leaf_sink_bytes(int nq, int64_t n);
+int akb_leaf_sink_layout(void* base, int nq, int nan_mask, int64_t n, akb_leaf_sink* out);
+int64_t akb_leaf_finish_work_bytes(int nq, int64_t n);
+/* d_sum[nq], d_count[nq] (device) */
+int akb_leaf_finish_f64(const akb_leaf_sink* sink, double* d_sum, int64_t* d_count, void* work,
+                        void* stream);
+
 /* ---------------- fused chain (device-resident API) ---------------- */
 
 #define AKB_MAX_MIRRORS 7
@@ -134,6 +158,8 @@ typedef struct akb_chain_desc {
     int64_t samp_v_col;                       /* column ih -> samp_v[iv] = Rz/Rx */
     double* samp_h; double* samp_v;
     int32_t* flags;                           /* device int32, OR-ed */
+    /* optional fused reduction of (atan_h, atan_v, det_x, det_y, det_z): sink.nq = 5 */
+    akb_leaf_sink sink;
 } akb_chain_desc;
 
 int akb_trace_chain_f64(const akb_chain_desc* desc, void* stream);
@@ -144,20 +170,32 @@ int64_t akb_chain_desc_size(void);
  *   r' = Ry@(Rz@r), p' = Ry@(Rz@(p - c)) + c
  *   det1 = plane(det1_ghij, r', p'), det2 = plane(det2_ghij, r', p')
  *   total1 = opl + ||det1 - p'||, total2 = opl + ||det2 - p'||
- * Any output may be NULL. */
+ * Any output may be NULL. sink (optional, nq = 5): fused np.nanmean of
+ * (det1_x, det1_y, det1_z, total1, total2). */
 int akb_tilt_opd_f64(const double ry[9], const double rz[9], const double center[3],
                      const double det1_ghij[4], const double det2_ghij[4], const double* dir,
                      const double* pt, const double* opl, int64_t ld, int64_t n, double* dir_rot,
                      double* pt_rot, double* det1, double* det2, double* total1, double* total2,
-                     void* stream);
+                     const akb_leaf_sink* sink, void* stream);
 
-/* OPD maps (ref :3626, :3633, :3675-3677):
+/* OPD maps (ref :3626, :3633, :3675-3677), with the means read from device memory as the tilt
+ * sink left them (d_sum5 / d_cnt5 = sums and counts of det1_x, det1_y, det1_z, total1, total2;
+ * mean = sum / count in float64):
  *   dist_err  = (total - mean_total) * 1e9
  *   sph       = ||det2 - mean_focus|| * 1e9
- *   wave      = dist_err2 - sph                                   (NULL outputs skipped) */
-int akb_opd_f64(const double* total1, double mean1, const double* total2, double mean2,
-                const double* det2, int64_t ld, const double mean_focus[3], int64_t n,
-                double* dist_err1, double* dist_err2, double* sph, double* wave, void* stream);
+ *   wave      = dist_err2 - sph                                   (NULL outputs skipped)
+ * d_extent_keys (optional, 4 x uint64, zero-initialised by this call): order-preserving keys of
+ * max(det2_y), -min(det2_y), max(det2_z), -min(det2_z) over non-NaN rays (pupil pitch). */
+int akb_opd_f64(const double* total1, const double* total2, const double* det2, int64_t ld, int64_t n,
+                const double* d_sum5, const int64_t* d_cnt5, double* dist_err1, double* dist_err2,
+                double* sph, double* wave, uint64_t* d_extent_keys, void* stream);
+
+/* Wave2 (nm) of a shard's rows sampled onto a size x size pupil in ray-index space (nearest ray,
+ * index (k * (n - 1)) // (size - 1)): opd_m[ky][kx] = wave[iv - row0][ih] * 1e-9 for the pupil rows
+ * this shard owns, 0 elsewhere (shards are summed across ranks). d_pitch (optional, device [2]):
+ * (max y - min y) / (size - 1), (max z - min z) / (size - 1) from akb_opd_f64's extent keys. */
+int akb_pupil_sample_f64(const double* wave, int64_t row0, int64_t rows, int64_t n, int size,
+                         const uint64_t* d_extent_keys, double* opd_m, double* d_pitch, void* stream);
 
 /* numpy-exact reduction: for each of `rows` rows of length n (row stride ld),
  * sum = the value np.sum gives (8192-element blocks, pairwise within a block, blocks added left
@@ -186,7 +224,9 @@ int akb_scale_field_f64(const double* u_re_im, const double* ds, int64_t m, doub
 /* ---------------- PSF by FFT (rocFFT) ---------------- */
 
 /* compute_psf_fft for a stack of `batch` wavelengths over one pupil:
- *   opd, amp: (ny, nx) float64 device arrays (NaN/inf -> 0)
+ *   opd, amp: (ny, nx) float64 device arrays (NaN/inf -> 0); amp may be NULL, meaning
+ *   amp = 1 where opd is finite and 0 elsewhere (psf_calc's mask, ref :1182-1188)
+ *   d_pitch: optional device [dx, dy]; when given it replaces dx, dy (pitch computed on device)
  *   lambdas: host array of `batch` wavelengths
  *   hann_wy (ny) / hann_wx (nx) / hann_max: separable window or NULL (ref psf_fft.py:20-27)
  *   py = ny' * pad, px = nx' * pad with ny' = ny + ny%2 (ensure_even_size)
@@ -197,7 +237,7 @@ int64_t akb_psf_work_bytes(int ny, int nx, int pad, int batch);
 int akb_psf_f64(const double* opd, const double* amp, int ny, int nx, int pad, int batch,
                 const double* lambdas, double dx, double dy, const double* hann_wy,
                 const double* hann_wx, double hann_max, double* psf, double* efield_re_im,
-                double* d_imax, void* work, void* stream);
+                double* d_imax, const double* d_pitch, void* work, void* stream);
 
 /* release cached rocFFT plans (also done at unload) */
 void akb_psf_release_plans(void);

@@ -207,7 +207,7 @@ def test_ray_wave_65_vs_reference(gpu):
     from akbraytracing_amd.wavefront import RayWave
     f = golden("akb_raywave_65.npz")
     rw = RayWave(_geom(), 65)
-    out = rw.run(keep_rotated=True)
+    out = rw.run(keep_rotated=True, full=True)
     assert out["flags"] == (0, 0)
     assert np.array_equal(out["tan_h2"].cpu().numpy(), OPL.akb_ray_wave(golden_json("akb_geometry.json"), 65)["tan_h2"])
     assert np.array_equal(out["last_hit"].cpu().numpy(), f["pass2_hits"][3])
@@ -227,11 +227,29 @@ def test_ray_wave_65_vs_reference(gpu):
     assert np.max(np.abs(out["wave2"].cpu().numpy() - f["wave2"])) <= 1e-4
 
 
+@pytest.mark.parametrize("n", [65, 128, 1001])
+def test_fused_means_equal_numpy_on_the_rows(gpu, n):
+    """The leaf sums fused into pass 2 and the tilt kernel give the same means numpy takes of the
+    rows they never write (n = 65: short last buffer only; 1001: full buffers + tail)."""
+    from akbraytracing_amd.wavefront import RayWave
+    rw = RayWave(_geom(), n)
+    out = rw.run(full=True)
+    at = out["atan"].cpu().numpy()
+    det = out["det_pre"].cpu().numpy()
+    assert out["theta_y"] == -np.nanmean(at[1]) and out["theta_z"] == np.nanmean(at[0])
+    assert np.array_equal(out["focus_apprx"], np.mean(det, axis=1))
+    mt, mf = rw.means()
+    assert mt[0] == np.nanmean(out["total"].cpu().numpy()) and mt[1] == np.nanmean(out["total2"].cpu().numpy())
+    assert np.array_equal(mf, np.nanmean(out["detcenter"].cpu().numpy(), axis=1))
+    e2 = out["dist_err2"].cpu().numpy()
+    assert np.array_equal(e2, (out["total2"].cpu().numpy() - mt[1]) * 1e9)
+
+
 def test_kb_wave_65_vs_reference(gpu):
     from akbraytracing_amd.wavefront import RayWave, SystemGeometry
     f = golden("kb_wave_65.npz")
     rw = RayWave(SystemGeometry.from_dict(golden_json("kb_geometry.json")), 65)
-    out = rw.run(opd=False)
+    out = rw.run(opd=False, full=True)
     assert np.array_equal(out["last_hit"].cpu().numpy(), f["pass2_hits"][1])
     assert np.array_equal(out["dir_out"].cpu().numpy(), f["pass2_refl"])
     assert np.array_equal(out["det_pre"].cpu().numpy(), f["pass2_det"])
@@ -381,6 +399,6 @@ def test_ray_wave_1e7_properties(gpu):
     # numpy's own mean of 1e7 values near 146 m is good to ~1e-13 m, i.e. ~1e-4 nm of OPD
     assert abs(np.nanmean(e)) < 1e-2
     t2 = out["total2"].cpu().numpy()
-    assert out["mean_total"][1] == np.nanmean(t2)
+    assert rw.means()[0][1] == np.nanmean(t2)
     # the OPD's spread at 1e7 rays stays within the 65^2 reference's order of magnitude (nm)
     assert 1e-4 < np.nanstd(w) < 1.0

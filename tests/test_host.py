@@ -27,7 +27,7 @@ def test_library_exports_every_header_symbol():
 def test_abi_version_and_struct_layout():
     from akbraytracing_amd import _lib
     L = _lib.lib()
-    assert L.akb_abi_version() == 1
+    assert L.akb_abi_version() == _lib.ABI_VERSION
     assert L.akb_chain_desc_size() == ctypes.sizeof(_lib.ChainDesc)
     # no GPU in this container: device count is 0 and calls report errors instead of crashing
     assert L.akb_device_count() >= 0
