@@ -61,8 +61,97 @@ def _fill_desc(desc, mirrors, det_ghij):
             desc.det_ghij[j] = float(det_ghij[j])
 
 
-def trace_chain(mirrors, *, tan_h=None, tan_v=None, row0=0, n_rays=None, dirs=None, src=(0.0, 0.0, 0.0),
-                det_ghij=None, want=("last_hit", "dir_out"), samples=None, out=None, sink=None, stream=None):
+class ChainLaunch:
+    """A prepared fused-chain launch: the descriptor and its device buffers are built once and
+    the launch can be repeated (the tables / source / sink contents may change between launches,
+    their addresses may not). trace_chain() is the one-shot form."""
+
+    def __init__(self, mirrors, *, tan_h=None, tan_v=None, row0=0, n_rays=None, dirs=None, src=(0.0, 0.0, 0.0),
+                 det_ghij=None, want=("last_hit", "dir_out"), samples=None, out=None, sink=None):
+        dev = D.device()
+        desc = _lib.ChainDesc()
+        _fill_desc(desc, mirrors, det_ghij)
+        self.keep = [tan_h, tan_v, dirs, sink]
+        if dirs is None:
+            n_h, n_v = tan_h.shape[0], tan_v.shape[0]
+            n = n_h * n_v - row0 * n_h if n_rays is None else n_rays
+            desc.dir = None
+            desc.tan_h, desc.tan_v = D.ptr(tan_h), D.ptr(tan_v)
+            desc.n_h, desc.n_v, desc.row0 = n_h, n_v, row0
+        else:
+            n = dirs.shape[1]
+            desc.dir, desc.dir_ld, desc.dir_inc = D.ptr(dirs), n, 1
+            desc.n_h, desc.n_v = 1, n
+        desc.n_rays = n
+        if isinstance(src, torch.Tensor) and src.dim() == 2:
+            desc.org, desc.org_ld, desc.org_inc = D.ptr(src), src.shape[1], 1
+            self.keep.append(src)
+        else:
+            desc.org = None
+            s = [float(x) for x in np.asarray(src, dtype=np.float64).ravel()[:3]]
+            for j in range(3):
+                desc.src[j] = s[j]
+        out = dict(out or {})
+        K = len(mirrors)
+
+        def buf(name, shape):
+            t = out.get(name)
+            if t is None or tuple(t.shape) != tuple(shape):
+                t = torch.empty(shape, dtype=D.F64, device=dev)
+            out[name] = t
+            return t
+
+        res = ChainOutputs(flags=torch.zeros(1, dtype=torch.int32, device=dev))
+        if "hits" in want:
+            res.hits = buf("hits", (K, 3, n))
+            desc.hits, desc.hits_ld = D.ptr(res.hits), n
+        if "last_hit" in want:
+            res.last_hit = buf("last_hit", (3, n))
+            desc.last_hit, desc.last_hit_ld = D.ptr(res.last_hit), n
+        if "dir_out" in want:
+            res.dir_out = buf("dir_out", (3, n))
+            desc.dir_out, desc.dir_out_ld = D.ptr(res.dir_out), n
+        if "det" in want:
+            if det_ghij is None:
+                raise ValueError("det requested without a detector plane")
+            res.det = buf("det", (3, n))
+            desc.det_out, desc.det_out_ld = D.ptr(res.det), n
+        if "opl" in want:
+            res.opl = buf("opl", (n,))
+            desc.opl = D.ptr(res.opl)
+        if "atan" in want:
+            res.atan = buf("atan", (2, n))
+            desc.atan_h = D.ptr(res.atan)
+            desc.atan_v = D.ptr(res.atan[1])
+        desc.samp_h_begin = desc.samp_h_end = 0
+        desc.samp_v_col = -1
+        if samples is not None:
+            hb, he, vc = samples
+            nh = max(he - hb, 0)
+            nv = tan_v.shape[0] if vc is not None else 0
+            # one buffer so the host reads both pick lists with one copy
+            res.extra["samples"] = torch.full((nh + nv,), float("nan"), dtype=D.F64, device=dev)
+            res.samp_h = res.extra["samples"][:nh]
+            desc.samp_h, desc.samp_h_begin, desc.samp_h_end = D.ptr(res.samp_h), hb, he
+            if vc is not None:
+                res.samp_v = res.extra["samples"][nh:]
+                desc.samp_v, desc.samp_v_col = D.ptr(res.samp_v), vc
+        desc.flags = D.ptr(res.flags)
+        if sink is not None:
+            if det_ghij is None:
+                raise ValueError("the chain sink reduces detector hits: give det_ghij")
+            desc.sink = sink.desc
+        res.extra["buffers"] = out
+        self.desc, self.res = desc, res
+
+    def launch(self, stream=None, reset_flags=True):
+        if reset_flags:
+            self.res.flags.zero_()
+        _lib.check(_lib.lib().akb_trace_chain_f64(self.desc, D.stream_handle(stream)))
+        return self.res
+
+
+def trace_chain(mirrors, *, stream=None, **kw):
     """Run one fused chain launch.
 
     Rays: either the grid (tan_h, tan_v device tensors; rays row0*n_h .. + n_rays) or explicit
@@ -73,79 +162,7 @@ def trace_chain(mirrors, *, tan_h=None, tan_v=None, row0=0, n_rays=None, dirs=No
     sink: optional reduce.LeafSink(5, n_rays, nan_mask=0b00011) fed with (arctan(Ry/Rx),
         arctan(Rz/Rx), det_x, det_y, det_z) — the tilt means without writing those rows.
     """
-    L = _lib.lib()
-    dev = D.device()
-    desc = _lib.ChainDesc()
-    _fill_desc(desc, mirrors, det_ghij)
-    keep = []  # keep tensors alive for the launch
-    if dirs is None:
-        n_h, n_v = tan_h.shape[0], tan_v.shape[0]
-        n = n_h * n_v - row0 * n_h if n_rays is None else n_rays
-        desc.dir = None
-        desc.tan_h, desc.tan_v = D.ptr(tan_h), D.ptr(tan_v)
-        desc.n_h, desc.n_v, desc.row0 = n_h, n_v, row0
-    else:
-        n = dirs.shape[1]
-        desc.dir, desc.dir_ld, desc.dir_inc = D.ptr(dirs), n, 1
-        desc.n_h, desc.n_v = 1, n
-    desc.n_rays = n
-    if isinstance(src, torch.Tensor) and src.dim() == 2:
-        desc.org, desc.org_ld, desc.org_inc = D.ptr(src), src.shape[1], 1
-        keep.append(src)
-    else:
-        desc.org = None
-        s = [float(x) for x in np.asarray(src, dtype=np.float64).ravel()[:3]]
-        for j in range(3):
-            desc.src[j] = s[j]
-    out = dict(out or {})
-    K = len(mirrors)
-
-    def buf(name, shape):
-        t = out.get(name)
-        if t is None or tuple(t.shape) != tuple(shape):
-            t = torch.empty(shape, dtype=D.F64, device=dev)
-        out[name] = t
-        return t
-
-    res = ChainOutputs(flags=torch.zeros(1, dtype=torch.int32, device=dev))
-    if "hits" in want:
-        res.hits = buf("hits", (K, 3, n))
-        desc.hits, desc.hits_ld = D.ptr(res.hits), n
-    if "last_hit" in want:
-        res.last_hit = buf("last_hit", (3, n))
-        desc.last_hit, desc.last_hit_ld = D.ptr(res.last_hit), n
-    if "dir_out" in want:
-        res.dir_out = buf("dir_out", (3, n))
-        desc.dir_out, desc.dir_out_ld = D.ptr(res.dir_out), n
-    if "det" in want:
-        if det_ghij is None:
-            raise ValueError("det requested without a detector plane")
-        res.det = buf("det", (3, n))
-        desc.det_out, desc.det_out_ld = D.ptr(res.det), n
-    if "opl" in want:
-        res.opl = buf("opl", (n,))
-        desc.opl = D.ptr(res.opl)
-    if "atan" in want:
-        res.atan = buf("atan", (2, n))
-        desc.atan_h = D.ptr(res.atan)
-        desc.atan_v = D.ptr(res.atan[1])
-    desc.samp_h_begin = desc.samp_h_end = 0
-    desc.samp_v_col = -1
-    if samples is not None:
-        hb, he, vc = samples
-        res.samp_h = torch.full((max(he - hb, 0),), float("nan"), dtype=D.F64, device=dev)
-        desc.samp_h, desc.samp_h_begin, desc.samp_h_end = D.ptr(res.samp_h), hb, he
-        if vc is not None:
-            res.samp_v = torch.full((tan_v.shape[0],), float("nan"), dtype=D.F64, device=dev)
-            desc.samp_v, desc.samp_v_col = D.ptr(res.samp_v), vc
-    desc.flags = D.ptr(res.flags)
-    if sink is not None:
-        if det_ghij is None:
-            raise ValueError("the chain sink reduces detector hits: give det_ghij")
-        desc.sink = sink.desc
-    _lib.check(L.akb_trace_chain_f64(desc, D.stream_handle(stream)))
-    res.extra["buffers"] = out
-    return res
+    return ChainLaunch(mirrors, **kw).launch(stream=stream, reset_flags=False)
 
 
 def staged_chain(mirrors, dirs, src, with_segments=False):

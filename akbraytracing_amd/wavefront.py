@@ -26,7 +26,7 @@ from . import _lib
 from . import device as D
 from . import primitives as P
 from .reduce import LeafSink, RowSums
-from .trace import Mirror, staged_chain, trace_chain
+from .trace import ChainLaunch, Mirror, staged_chain
 
 
 @dataclass
@@ -141,7 +141,10 @@ class LocalComm:
 
 
 class RayWave:
-    """Device-resident 'ray_wave' / 'wave' trace on an n x n grid (one shard of it)."""
+    """Device-resident 'ray_wave' / 'wave' trace on an n x n grid (one shard of it).
+
+    Every launch is prepared once (descriptors, device buffers, pinned host staging), so a run
+    costs two host round trips plus a handful of ctypes calls."""
 
     def __init__(self, geometry, n, shard=None, comm=None, resample_pass=True):
         self.g = geometry
@@ -164,43 +167,62 @@ class RayWave:
         self._ext = torch.zeros(4, dtype=torch.int64, device=self.dev)  # det2 extent keys (uint64 bits)
         self._pitch = torch.zeros(2, dtype=D.F64, device=self.dev)
         self._opd_buf = None
-        self._buf1, self._buf2 = {}, {}
         self.last = {}
         self.kernel_events = None  # set to a list to time the pass-2 chain launch (bench.py)
+        # prepared launches
+        self._plan = sample_plan(self.n)
+        hb, he, col = self._plan
+        self._tan2 = torch.empty(2 * self.n, dtype=D.F64, device=self.dev)  # pass-2 tables [h | v]
+        self._tan2_host = torch.empty(2 * self.n, dtype=D.F64, pin_memory=True)
+        self._p1 = ChainLaunch(self.g.mirrors, tan_h=self.tan_h, tan_v=self.tan_v, row0=self.shard.row0,
+                               n_rays=self.n_local, src=self.g.source, want=(), samples=(hb, he, col))
+        self._p2 = {}
+        nsamp = (he - hb) + self.n
+        self._x1_host = torch.empty(nsamp + 1, dtype=D.F64, pin_memory=True)
+        self._x2_host = torch.empty(11, dtype=D.F64, pin_memory=True)
+        self._x2_dev = torch.empty(11, dtype=D.F64, device=self.dev)
+        self._own = sample_ownership(self.shard, self.n)
+
+    def _pass2_launch(self, want_rows):
+        key = bool(want_rows)
+        if key not in self._p2:
+            want = ("last_hit", "dir_out", "opl") + (("det", "atan") if want_rows else ())
+            self._p2[key] = ChainLaunch(self.g.mirrors, tan_h=self._tan2[:self.n], tan_v=self._tan2[self.n:],
+                                        row0=self.shard.row0, n_rays=self.n_local, src=self.g.source,
+                                        det_ghij=self.g.det1, want=want, sink=self.sink2)
+        return self._p2[key]
 
     # -------------------------------------------------------------- passes
-    def _pass1(self):
-        hb, he, col = sample_plan(self.n)
-        r = trace_chain(self.g.mirrors, tan_h=self.tan_h, tan_v=self.tan_v, row0=self.shard.row0,
-                        n_rays=self.n_local, src=self.g.source, want=(), samples=(hb, he, col),
-                        out=self._buf1)
-        self._buf1 = r.extra["buffers"]
-        # this shard's pieces of the picks; NaN where another shard owns them
-        sh = r.samp_h
-        sv = r.samp_v
-        host = torch.cat([sh, sv, r.flags.to(D.F64)]).cpu().numpy()
-        samp_h = host[:he - hb]
-        samp_v = host[he - hb:he - hb + self.n]
+    def _pass1(self, overlap=None):
+        hb, he, col = self._plan
+        r = self._p1.launch()
+        x = self._x1_host
+        nh = he - hb
+        x[:nh + self.n].copy_(r.extra["samples"], non_blocking=True)
+        x[nh + self.n:].copy_(r.flags.to(D.F64), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        if overlap is not None:
+            overlap()  # independent device work queued behind the copy (runs while the host waits)
+        ev.synchronize()
+        host = x.numpy()
+        own_h, own_v = self._own
+        samp_h = np.where(own_h, host[:nh], 0.0)
+        samp_v = np.where(own_v, host[nh:nh + self.n], 0.0)
         flags = int(host[-1])
-        own_h, own_v = sample_ownership(self.shard, self.n)
-        samp_h = np.where(own_h, samp_h, 0.0)
-        samp_v = np.where(own_v, samp_v, 0.0)
         samp_h, samp_v = self.comm.gather_samples(samp_h, samp_v, self.shard, self.n)
         flags = self.comm.sum_flags(flags)
         return samp_h, samp_v, flags
 
-    def _pass2(self, tan_h2, tan_v2, want_rows=False):
+    def _pass2(self, want_rows=False):
         ev = None
         if self.kernel_events is not None:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
-        want = ("last_hit", "dir_out", "opl") + (("det", "atan") if want_rows else ())
-        r = trace_chain(self.g.mirrors, tan_h=tan_h2, tan_v=tan_v2, row0=self.shard.row0, n_rays=self.n_local,
-                        src=self.g.source, det_ghij=self.g.det1, want=want, out=self._buf2, sink=self.sink2)
+        r = self._pass2_launch(want_rows).launch()
         if ev is not None:
             ev[1].record()
             self.kernel_events.append(ev)
-        self._buf2 = r.extra["buffers"]
         return r
 
     def _pass2_staged(self, tan_h2, tan_v2):
@@ -220,15 +242,17 @@ class RayWave:
         return hits[-1], r4, det, opl, atan
 
     # -------------------------------------------------------------- one run
-    def run(self, opd=True, keep_rotated=False, full=False):
+    def run(self, opd=True, keep_rotated=False, full=False, overlap=None):
         """Trace and reduce; returns a dict of device tensors (this shard's rays) and host means.
         keep_rotated: also return the tilted direction / last hit (dir_rot, pt_rot); full: also
         return DistError (detector 1), Sph, detcenter and the pre-tilt rows. The default keeps what
         griddata consumes (DistError2, Wave2, detcenter2) and reduces everything else on the fly.
+        overlap: callable enqueuing independent device work (e.g. the previous step's PSF) that
+        runs while the host performs the resample.
 
         Host round trips: two (the resample picks, and the tilt angles, whose rotation matrices are
         formed with numpy's cos/sin exactly as the reference forms them)."""
-        samp_h, samp_v, flags1 = self._pass1()
+        samp_h, samp_v, flags1 = self._pass1(overlap)
         if flags1:
             raise _lib.AKBError(
                 f"pass 1 raised trace flags {flags1:#x} (a ray missed a mirror or a norm was zero): the "
@@ -237,17 +261,28 @@ class RayWave:
             new_h, new_v = resample(np.arctan(samp_h), np.arctan(samp_v), self.rand_h, self.rand_v)
         else:
             new_h, new_v = self.rand_h, self.rand_v
-        tan_h2 = torch.from_numpy(np.tan(new_h)).to(self.dev, non_blocking=True)
-        tan_v2 = torch.from_numpy(np.tan(new_v)).to(self.dev, non_blocking=True)
-        r = self._pass2(tan_h2, tan_v2, want_rows=full)
+        th = self._tan2_host.numpy()
+        np.tan(new_h, out=th[:self.n])
+        np.tan(new_v, out=th[self.n:])
+        self._tan2.copy_(self._tan2_host, non_blocking=True)
+        tan_h2, tan_v2 = self._tan2[:self.n], self._tan2[self.n:]
+        r = self._pass2(want_rows=full)
         sums, cnts = self.sink2.finish()
-        red = self.comm.allreduce_sums(torch.cat([sums, cnts.to(D.F64), r.flags.to(D.F64)]))
-        host = red.cpu().numpy()
+        x2 = self._x2_dev
+        x2[0:5].copy_(sums)
+        x2[5:10].copy_(cnts)
+        x2[10:11].copy_(r.flags)
+        red = self.comm.allreduce_sums(x2)
+        self._x2_host.copy_(red, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        ev.synchronize()
+        host = self._x2_host.numpy()
         flags2 = int(host[-1])
         last_hit, dir_out, opl = r.last_hit, r.dir_out, r.opl
         det_pre, atan = r.det, r.atan
         if flags2:
-            last_hit, dir_out, det_pre, opl, atan = self._pass2_staged(tan_h2, tan_v2)
+            last_hit, dir_out, det_pre, opl, atan = self._pass2_staged(tan_h2.clone(), tan_v2.clone())
             (atan_s, atan_c), (det_s, det_c) = self.sums(atan, nan=True), self.sums(det_pre)
             red = self.comm.allreduce_sums(torch.cat([atan_s, det_s, atan_c.to(D.F64), det_c.to(D.F64)]))
             host = red.cpu().numpy()

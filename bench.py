@@ -107,29 +107,39 @@ def main():
 
     psf_events = []
     psf_out = {}
+    pending = []  # pupil of the previous step, transformed while the host resamples the next one
+
+    def run_psf(item, timed):
+        opd, pitch = item
+        if rank != 0:
+            return
+        if timed:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        psf, _, _ = psf_stack(opd, None, [lam], None, pitch=pitch, pad_factor=args.pad, out=psf_out.get("psf"))
+        psf_out["psf"] = psf
+        if timed:
+            e1.record()
+            psf_events.append((e0, e1))
 
     def step(timed):
-        rw.run()
-        opd, pitch = rw.pupil(args.pupil)
-        if rank == 0:
-            if timed:
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-            psf, _, _ = psf_stack(opd, None, [lam], None, pitch=pitch, pad_factor=args.pad,
-                                  out=psf_out.get("psf"))
-            psf_out["psf"] = psf
-            if timed:
-                e1.record()
-                psf_events.append((e0, e1))
+        # the PSF of step k-1 is queued behind pass 1 of step k: it runs on the GPU while the host
+        # does the equal-angle resample (all of it stays inside the timed region)
+        rw.run(overlap=(lambda: run_psf(pending.pop(), timed)) if pending else None)
+        pending.append(rw.pupil(args.pupil))
 
     for _ in range(args.warmup):
         step(False)
+    while pending:
+        run_psf(pending.pop(), False)
     rw.kernel_events = []
     comm.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(True)
+    while pending:
+        run_psf(pending.pop(), True)
     torch.cuda.synchronize()
     comm.barrier()
     el = time.perf_counter() - t0
