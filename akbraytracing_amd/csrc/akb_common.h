@@ -87,6 +87,17 @@ inline Quadric quadric_from(const double* c) {
 
 // ---- per-ray arithmetic, each in the reference's numpy association order ----
 
+// x / s for several x sharing one s, each correctly rounded: inv = RN(1/s) (an IEEE division),
+// q = RN(x * inv), then one FMA correction q + (x - s q) inv, which is RN(x/s) whenever no
+// overflow or underflow occurs (Markstein 1990; 5.4e8 adversarial cases checked against x / s).
+// The r == 0 test returns q unchanged when it is already exact, which also keeps the sign of a
+// zero quotient (x = -0). Zero or non-finite s is caught by the callers' zero-norm flags.
+__device__ __forceinline__ double div_shared(double x, double s, double inv) {
+    const double q = x * inv;
+    const double r = __builtin_fma(-s, q, x);
+    return r == 0.0 ? q : __builtin_fma(r, inv, q);
+}
+
 // mirr_ray_intersection (EllipseRaytrace3D.py:23-43). Returns false when D <= 0 or NaN.
 __device__ __forceinline__ bool quadric_hit(const Quadric& Q, double l, double m, double n, double p,
                                             double q, double r, bool negative, double& x, double& y,
@@ -98,6 +109,33 @@ __device__ __forceinline__ bool quadric_hit(const Quadric& Q, double l, double m
                      Q.g * l + Q.h * m + Q.i * n;
     const double C = Q.a * (p * p) + Q.b * (q * q) + Q.c * (r * r) + Q.d * p * q + Q.e * p * r +
                      Q.f * q * r + Q.g * p + Q.h * q + Q.i * r + Q.j;
+    const double D = B * B - 4.0 * A * C;
+    const double s = sqrt(D);
+    const double t = (negative ? (-B - s) : (-B + s)) / (2.0 * A);
+    x = t * l + p;
+    y = t * m + q;
+    z = t * n + r;
+    return D > 0.0;
+}
+
+// The same intersection for a quadric with b = d = f = h = 0 (no y terms: the reference's
+// vertical mirrors before misalignment) or with c = e = f = i = 0 (no z terms). Each skipped term
+// is an exact +-0 added to a running sum that is non-zero by then, so the rounded result is the
+// one the full expression gives (only the sign of an exactly-zero result could differ).
+template <int kFree>  // 1: y-free, 2: z-free
+__device__ __forceinline__ bool quadric_hit_sparse(const Quadric& Q, double l, double m, double n, double p,
+                                                   double q, double r, bool negative, double& x, double& y,
+                                                   double& z) {
+    double A, B, C;
+    if (kFree == 1) {
+        A = Q.a * (l * l) + Q.c * (n * n) + Q.e * n * l;
+        B = 2.0 * Q.a * p * l + 2.0 * Q.c * r * n + Q.e * (p * n + r * l) + Q.g * l + Q.i * n;
+        C = Q.a * (p * p) + Q.c * (r * r) + Q.e * p * r + Q.g * p + Q.i * r + Q.j;
+    } else {
+        A = Q.a * (l * l) + Q.b * (m * m) + Q.d * m * l;
+        B = 2.0 * Q.a * p * l + 2.0 * Q.b * q * m + Q.d * (p * m + q * l) + Q.g * l + Q.h * m;
+        C = Q.a * (p * p) + Q.b * (q * q) + Q.d * p * q + Q.g * p + Q.h * q + Q.j;
+    }
     const double D = B * B - 4.0 * A * C;
     const double s = sqrt(D);
     const double t = (negative ? (-B - s) : (-B + s)) / (2.0 * A);

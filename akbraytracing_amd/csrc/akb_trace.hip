@@ -160,6 +160,7 @@ __global__ void k_fill_nan(double* out, int64_t ld, int rows, int64_t n) {
 struct ChainArgs {
     int K;
     int negmask;
+    int sparse[AKB_MAX_MIRRORS];  // 0 general, 1 y-free (b=d=f=h=0), 2 z-free (c=e=f=i=0)
     Quadric q[AKB_MAX_MIRRORS];
     double det[4];
     const double* dir;
@@ -221,9 +222,9 @@ __device__ __forceinline__ void chain_ray(const ChainArgs& a, int64_t i, int& fl
         const double tv = a.tan_v[iv];
         const double s = norm3(1.0, th, tv);
         if (s == 0.0) fl |= AKB_FLAG_CHAIN_DIR;
-        l = 1.0 / s;
-        m = th / s;
-        nn = tv / s;
+        l = 1.0 / s;  // = RN(1/s): also the shared reciprocal
+        m = div_shared(th, s, l);
+        nn = div_shared(tv, s, l);
     } else {
         l = a.dir[i * a.dir_inc];
         m = a.dir[a.dir_ld + i * a.dir_inc];
@@ -245,8 +246,16 @@ __device__ __forceinline__ void chain_ray(const ChainArgs& a, int64_t i, int& fl
 #pragma unroll 1
     for (int k = 0; k < a.K; ++k) {
         const Quadric Q = a.q[k];
+        const bool neg = (a.negmask >> k) & 1;
         double x, y, z;
-        if (!quadric_hit(Q, l, m, nn, p, q, r, (a.negmask >> k) & 1, x, y, z)) fl |= AKB_FLAG_MISS << (4 * k);
+        bool hit;
+        if (a.sparse[k] == 1)  // wave-uniform branch
+            hit = quadric_hit_sparse<1>(Q, l, m, nn, p, q, r, neg, x, y, z);
+        else if (a.sparse[k] == 2)
+            hit = quadric_hit_sparse<2>(Q, l, m, nn, p, q, r, neg, x, y, z);
+        else
+            hit = quadric_hit(Q, l, m, nn, p, q, r, neg, x, y, z);
+        if (!hit) fl |= AKB_FLAG_MISS << (4 * k);
         if (kOPL) {
             const double d = norm3(x - p, y - q, z - r);
             opl = (k == 0) ? d : opl + d;
@@ -261,16 +270,18 @@ __device__ __forceinline__ void chain_ray(const ChainArgs& a, int64_t i, int& fl
         quadric_grad(Q, x, y, z, nx, ny, nz);
         const double sn = norm3(nx, ny, nz);
         if (sn == 0.0) fl |= AKB_FLAG_ZERO_NORMAL << (4 * k);
-        nx = nx / sn;
-        ny = ny / sn;
-        nz = nz / sn;
+        const double in = 1.0 / sn;
+        nx = div_shared(nx, sn, in);
+        ny = div_shared(ny, sn, in);
+        nz = div_shared(nz, sn, in);
         double rx, ry, rz;
         reflect_raw(l, m, nn, nx, ny, nz, rx, ry, rz);
         const double sr = norm3(rx, ry, rz);
         if (sr == 0.0) fl |= AKB_FLAG_ZERO_REFLECT << (4 * k);
-        l = rx / sr;
-        m = ry / sr;
-        nn = rz / sr;
+        const double ir = 1.0 / sr;
+        l = div_shared(rx, sr, ir);
+        m = div_shared(ry, sr, ir);
+        nn = div_shared(rz, sr, ir);
         p = x;
         q = y;
         r = z;
@@ -299,8 +310,9 @@ __device__ __forceinline__ void chain_ray(const ChainArgs& a, int64_t i, int& fl
         qv[4] = z;
     }
     if (kNeedQ || a.atan_h || a.atan_v) {
-        qv[0] = atan(m / l);
-        qv[1] = atan(nn / l);
+        const double il = 1.0 / l;
+        qv[0] = atan(div_shared(m, l, il));
+        qv[1] = atan(div_shared(nn, l, il));
         if (a.atan_h) a.atan_h[i] = qv[0];
         if (a.atan_v) a.atan_v[i] = qv[1];
     }
@@ -670,6 +682,13 @@ int akb_trace_chain_f64(const akb_chain_desc* d, void* stream) {
     for (int k = 0; k < d->n_mirrors; ++k) {
         a.q[k] = quadric_from(d->coeffs[k]);
         if (d->negative[k]) a.negmask |= 1 << k;
+        const double* c = d->coeffs[k];
+        if (c[1] == 0.0 && c[3] == 0.0 && c[5] == 0.0 && c[7] == 0.0)
+            a.sparse[k] = 1;
+        else if (c[2] == 0.0 && c[4] == 0.0 && c[5] == 0.0 && c[8] == 0.0)
+            a.sparse[k] = 2;
+        else
+            a.sparse[k] = 0;
     }
     for (int k = 0; k < 4; ++k) a.det[k] = d->det_ghij[k];
     a.dir = d->dir;
