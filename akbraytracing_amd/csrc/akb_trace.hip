@@ -9,6 +9,7 @@
 #include <math.h>
 
 #include <cstdarg>
+#include <cstdlib>
 #include <mutex>
 
 #include "akb_common.h"
@@ -322,8 +323,8 @@ __device__ __forceinline__ void chain_ray(const ChainArgs& a, int64_t i, int& fl
     if (a.samp_v && kGrid && ih == a.sv_col) a.samp_v[iv] = nn / l;
 }
 
-template <bool kGrid, bool kOPL>
-__global__ void __launch_bounds__(kBlock) k_chain(ChainArgs a) {
+template <bool kGrid, bool kOPL, int kWaves>
+__global__ void __launch_bounds__(kBlock, kWaves) k_chain(ChainArgs a) {
     int fl = 0;
     double qv[5];
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < a.n;
@@ -334,8 +335,8 @@ __global__ void __launch_bounds__(kBlock) k_chain(ChainArgs a) {
 
 // the same, walking 256-ray segments and feeding the fused np.nanmean(arctan) / np.mean(det)
 // leaf sums (the tilt means, ref :3583-3591) instead of writing those five rows to HBM
-template <bool kGrid, bool kOPL>
-__global__ void __launch_bounds__(kBlock) k_chain_sink(ChainArgs a) {
+template <bool kGrid, bool kOPL, int kWaves>
+__global__ void __launch_bounds__(kBlock, kWaves) k_chain_sink(ChainArgs a) {
     __shared__ LeafLds<5> L;
     int fl = 0;
     const int64_t nseg = (a.n + kLeafSeg - 1) / kLeafSeg;
@@ -532,6 +533,37 @@ using namespace akb;
 
 static inline V3In v3in(const double* p, int64_t ld, int64_t inc) { return V3In{p, ld, inc}; }
 
+// occupancy variant of the chain kernels (minimum waves per SIMD the register allocator must
+// allow); AKB_CHAIN_WAVES in the environment selects one for A/B timing, default 4
+static int chain_waves() {
+    static int w = [] {
+        const char* e = getenv("AKB_CHAIN_WAVES");
+        const int v = e ? atoi(e) : 4;
+        return (v == 2 || v == 4 || v == 5 || v == 6 || v == 8) ? v : 4;
+    }();
+    return w;
+}
+
+template <bool kGrid, bool kOPL, bool kSink>
+static void launch_chain(int w, unsigned g, hipStream_t s, const ChainArgs& a) {
+#define AKB_CHAIN_CASE(W)                                                        \
+    case W:                                                                      \
+        if (kSink)                                                               \
+            k_chain_sink<kGrid, kOPL, W><<<g, kBlock, 0, s>>>(a);                \
+        else                                                                     \
+            k_chain<kGrid, kOPL, W><<<g, kBlock, 0, s>>>(a);                     \
+        break;
+    switch (w) {
+        AKB_CHAIN_CASE(2)
+        AKB_CHAIN_CASE(5)
+        AKB_CHAIN_CASE(6)
+        AKB_CHAIN_CASE(8)
+        default:
+            AKB_CHAIN_CASE(4)
+    }
+#undef AKB_CHAIN_CASE
+}
+
 extern "C" {
 
 const char* akb_last_error(void) { return g_last_error.c_str(); }
@@ -642,6 +674,8 @@ int akb_fill_nan_f64(double* out, int64_t ld, int rows, int64_t n, void* stream)
 
 int64_t akb_chain_desc_size(void) { return (int64_t)sizeof(akb_chain_desc); }
 
+
+
 // magic numbers for unsigned 32-bit division by d >= 2: l = ceil(log2 d),
 // m' = floor(2^32 (2^l - d) / d) + 1 (Granlund & Montgomery 1994, fig. 4.1)
 static void div_magic(uint32_t d, uint32_t* mul, uint32_t* shift) {
@@ -724,29 +758,30 @@ int akb_trace_chain_f64(const akb_chain_desc* d, void* stream) {
     a.sink = d->sink;
     hipStream_t s = (hipStream_t)stream;
     const unsigned gsz = grid_for(d->n_rays);
+    const int w = chain_waves();
     if (sink) {
         const int64_t nseg = (d->n_rays + kLeafSeg - 1) / kLeafSeg;
         const unsigned gs = (unsigned)(nseg < 256 * 8 ? nseg : 256 * 8);
         if (grid && d->opl)
-            k_chain_sink<true, true><<<gs, kBlock, 0, s>>>(a);
+            launch_chain<true, true, true>(w, gs, s, a);
         else if (grid)
-            k_chain_sink<true, false><<<gs, kBlock, 0, s>>>(a);
+            launch_chain<true, false, true>(w, gs, s, a);
         else if (d->opl)
-            k_chain_sink<false, true><<<gs, kBlock, 0, s>>>(a);
+            launch_chain<false, true, true>(w, gs, s, a);
         else
-            k_chain_sink<false, false><<<gs, kBlock, 0, s>>>(a);
+            launch_chain<false, false, true>(w, gs, s, a);
         return launch_status("k_chain_sink");
     }
     if (grid) {
         if (d->opl)
-            k_chain<true, true><<<gsz, kBlock, 0, s>>>(a);
+            launch_chain<true, true, false>(w, gsz, s, a);
         else
-            k_chain<true, false><<<gsz, kBlock, 0, s>>>(a);
+            launch_chain<true, false, false>(w, gsz, s, a);
     } else {
         if (d->opl)
-            k_chain<false, true><<<gsz, kBlock, 0, s>>>(a);
+            launch_chain<false, true, false>(w, gsz, s, a);
         else
-            k_chain<false, false><<<gsz, kBlock, 0, s>>>(a);
+            launch_chain<false, false, false>(w, gsz, s, a);
     }
     return launch_status("k_chain");
 }
