@@ -36,7 +36,7 @@ EXPORTS = [
     "akb_pairwise_work_bytes", "akb_pairwise_sum_f64", "akb_pupil_sample_f64",
     "akb_leaf_sink_bytes", "akb_leaf_sink_layout", "akb_leaf_finish_work_bytes", "akb_leaf_finish_f64",
     "akb_huygens_work_bytes", "akb_huygens_f64", "akb_scale_field_f64",
-    "akb_psf_work_bytes", "akb_psf_f64", "akb_psf_release_plans",
+    "akb_psf_work_bytes", "akb_psf_f64", "akb_psf_release_plans", "akb_selftest_arith_f64",
 ]
 
 
@@ -113,6 +113,7 @@ def _declare(L):
         "akb_psf_f64": ([c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_dbl, c_dbl, c_vp, c_vp, c_dbl, c_vp,
                          c_vp, c_vp, c_vp, c_vp, c_vp], c_int),
         "akb_psf_release_plans": ([], None),
+        "akb_selftest_arith_f64": ([c_vp, c_vp, c_i64, c_vp, c_vp], c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

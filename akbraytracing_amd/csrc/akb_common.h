@@ -98,6 +98,32 @@ __device__ __forceinline__ double div_shared(double x, double s, double inv) {
     return r == 0.0 ? q : __builtin_fma(r, inv, q);
 }
 
+// Correctly rounded square root without the tiny-input rescaling. hipcc's sqrt(double) on gfx950
+// scales inputs below 2^-767 by 2^256 (cmp, cndmask, ldexp in; cndmask, ldexp out; class test for
+// 0 / inf) around an rsq + Goldschmidt/Newton core. For inputs in [2^-767, 2^1000] the rescale is
+// the identity and the special cases cannot occur, so the core alone - the same instruction
+// sequence - gives the bit-identical result in fewer instructions. Everything else (zero,
+// negatives, NaN, inf, tiny or huge values: never produced by the trace's unit-vector norms,
+// discriminants and metre-scale segment lengths) takes sqrt() itself.
+__device__ __forceinline__ double sqrt_cr(double x) {
+    if (__builtin_expect(!(x >= 0x1p-767 && x <= 0x1p+1000), 0)) return sqrt(x);
+    const double r = __builtin_amdgcn_rsq(x);
+    double g = x * r;
+    double h = r * 0.5;
+    const double e = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, e, g);
+    const double d = __builtin_fma(-g, g, x);
+    h = __builtin_fma(h, e, h);
+    g = __builtin_fma(d, h, g);
+    const double d2 = __builtin_fma(-g, g, x);
+    return __builtin_fma(d2, h, g);
+}
+
+// np.linalg.norm(v, axis=0) for one column: sqrt((x*x + y*y) + z*z)
+__device__ __forceinline__ double norm3(double x, double y, double z) {
+    return sqrt_cr(x * x + y * y + z * z);
+}
+
 // mirr_ray_intersection (EllipseRaytrace3D.py:23-43). Returns false when D <= 0 or NaN.
 __device__ __forceinline__ bool quadric_hit(const Quadric& Q, double l, double m, double n, double p,
                                             double q, double r, bool negative, double& x, double& y,
@@ -110,7 +136,7 @@ __device__ __forceinline__ bool quadric_hit(const Quadric& Q, double l, double m
     const double C = Q.a * (p * p) + Q.b * (q * q) + Q.c * (r * r) + Q.d * p * q + Q.e * p * r +
                      Q.f * q * r + Q.g * p + Q.h * q + Q.i * r + Q.j;
     const double D = B * B - 4.0 * A * C;
-    const double s = sqrt(D);
+    const double s = sqrt_cr(D);
     const double t = (negative ? (-B - s) : (-B + s)) / (2.0 * A);
     x = t * l + p;
     y = t * m + q;
@@ -137,7 +163,7 @@ __device__ __forceinline__ bool quadric_hit_sparse(const Quadric& Q, double l, d
         C = Q.a * (p * p) + Q.b * (q * q) + Q.d * p * q + Q.g * p + Q.h * q + Q.j;
     }
     const double D = B * B - 4.0 * A * C;
-    const double s = sqrt(D);
+    const double s = sqrt_cr(D);
     const double t = (negative ? (-B - s) : (-B + s)) / (2.0 * A);
     x = t * l + p;
     y = t * m + q;
@@ -151,11 +177,6 @@ __device__ __forceinline__ void quadric_grad(const Quadric& Q, double x, double 
     nx = 2.0 * Q.a * x + Q.d * y + Q.e * z + Q.g;
     ny = 2.0 * Q.b * y + Q.d * x + Q.f * z + Q.h;
     nz = 2.0 * Q.c * z + Q.e * x + Q.f * y + Q.i;
-}
-
-// np.linalg.norm(v, axis=0) for one column: sqrt((x*x + y*y) + z*z)
-__device__ __forceinline__ double norm3(double x, double y, double z) {
-    return sqrt(x * x + y * y + z * z);
 }
 
 // reflect_ray before normalisation (EllipseRaytrace3D.py:51-52)

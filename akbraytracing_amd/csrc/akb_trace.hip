@@ -872,3 +872,24 @@ int akb_pupil_sample_f64(const double* wave, int64_t row0, int64_t rows, int64_t
 }
 
 }  // extern "C"
+
+// ---- diagnostics: the trace's arithmetic shortcuts against the plain operations ----
+namespace akb {
+__global__ void k_selftest(const double* a, const double* b, int64_t n, double* out) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const double x = a[i], s = b[i];
+        out[4 * i + 0] = sqrt_cr(x);
+        out[4 * i + 1] = sqrt(x);
+        out[4 * i + 2] = div_shared(x, s, 1.0 / s);
+        out[4 * i + 3] = x / s;
+    }
+}
+}  // namespace akb
+
+extern "C" int akb_selftest_arith_f64(const double* a, const double* b, int64_t n, double* out4, void* stream) {
+    akb::clear_error();
+    AKB_REQUIRE(a && b && out4 && n >= 0, "bad selftest arguments");
+    if (n == 0) return AKB_OK;
+    akb::k_selftest<<<akb::grid_for(n), akb::kBlock, 0, (hipStream_t)stream>>>(a, b, n, out4);
+    return akb::launch_status("k_selftest");
+}

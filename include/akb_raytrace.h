@@ -239,6 +239,10 @@ int akb_psf_f64(const double* opd, const double* amp, int ny, int nx, int pad, i
                 const double* hann_wx, double hann_max, double* psf, double* efield_re_im,
                 double* d_imax, const double* d_pitch, void* work, void* stream);
 
+/* diagnostics: out4[4i..4i+3] = (the trace's sqrt, sqrt, the trace's shared-reciprocal a/b, a/b)
+ * for n pairs (a[i], b[i]) — used by the tests to check the shortcuts bit for bit */
+int akb_selftest_arith_f64(const double* a, const double* b, int64_t n, double* out4, void* stream);
+
 /* release cached rocFFT plans (also done at unload) */
 void akb_psf_release_plans(void);
 

@@ -126,6 +126,30 @@ def test_rotations_match_reference_blas_order(gpu):
     assert np.array_equal(got_pt, f["rot_pt"])
 
 
+def test_arith_shortcuts_bitwise(gpu):
+    """The chain kernels' rescale-free sqrt and shared-reciprocal division equal sqrt() and a / b
+    bit for bit over a wide range (and fall back to them outside it)."""
+    from akbraytracing_amd import _lib, device as D
+    rng = np.random.default_rng(11)
+    n = 4_000_000
+    e = rng.integers(-760, 900, n).astype(np.float64)
+    a = rng.random(n) * 2.0 ** e
+    b = (rng.random(n) + 0.5) * 2.0 ** rng.integers(-40, 40, n)
+    special = np.array([0.0, -0.0, 1.0, 4.0, np.inf, -1.0, np.nan, 1e-300, 5e-324, 2.0 ** -767, 1e305])
+    a = np.concatenate([a, special])
+    b = np.concatenate([b, np.full(special.shape, 3.0)])
+    ta, tb = torch.from_numpy(a).to(gpu), torch.from_numpy(b).to(gpu)
+    out = torch.empty((a.shape[0], 4), dtype=torch.float64, device=gpu)
+    _lib.check(_lib.lib().akb_selftest_arith_f64(D.ptr(ta), D.ptr(tb), a.shape[0], D.ptr(out), D.stream_handle()))
+    o = out.cpu().numpy()
+    assert np.array_equal(o[:, 0].view(np.uint64), o[:, 1].view(np.uint64)) or \
+        np.array_equal(o[:, 0], o[:, 1], equal_nan=True)
+    assert np.array_equal(o[:, 0], np.sqrt(a), equal_nan=True)
+    fin = np.isfinite(a)
+    assert np.array_equal(o[fin, 2], o[fin, 3])
+    assert np.array_equal(o[fin, 3], (a / b)[fin])
+
+
 # ----------------------------------------------------------------------------- fused chain
 
 def _geom():
