@@ -19,7 +19,7 @@ c_int = ctypes.c_int
 c_dbl = ctypes.c_double
 c_vp = ctypes.c_void_p
 MAX_MIRRORS = 7
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 FLAG_MISS = 0x1
 FLAG_ZERO_NORMAL = 0x2
@@ -32,7 +32,8 @@ EXPORTS = [
     "akb_last_error", "akb_abi_version", "akb_device_count",
     "akb_isect_f64", "akb_normal_f64", "akb_reflect_f64", "akb_normalize_f64", "akb_plane_isect_f64",
     "akb_seglen_f64", "akb_rotate_f64", "akb_fill_nan_f64",
-    "akb_trace_chain_f64", "akb_chain_desc_size", "akb_tilt_opd_f64", "akb_opd_f64",
+    "akb_trace_chain_f64", "akb_chain_desc_size", "akb_tilt_opd_f64", "akb_tilt_params_f64",
+    "akb_tilt_opd_dev_f64", "akb_opd_f64", "akb_resample_f64",
     "akb_pairwise_work_bytes", "akb_pairwise_sum_f64", "akb_pupil_sample_f64",
     "akb_leaf_sink_bytes", "akb_leaf_sink_layout", "akb_leaf_finish_work_bytes", "akb_leaf_finish_f64",
     "akb_huygens_work_bytes", "akb_huygens_f64", "akb_scale_field_f64",
@@ -97,7 +98,12 @@ def _declare(L):
         "akb_chain_desc_size": ([], c_i64),
         "akb_tilt_opd_f64": ([c_vp] * 5 + [c_vp, c_vp, c_vp, c_i64, c_i64] + [c_vp] * 6
                              + [ctypes.POINTER(LeafSink), c_vp], c_int),
-        "akb_opd_f64": ([c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp], c_int),
+        "akb_tilt_params_f64": ([c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp], c_int),
+        "akb_tilt_opd_dev_f64": ([c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64] + [c_vp] * 6
+                                 + [ctypes.POINTER(LeafSink), c_vp], c_int),
+        "akb_opd_f64": ([c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp],
+                        c_int),
+        "akb_resample_f64": ([c_vp, c_vp, c_i64, c_vp], c_int),
         "akb_pupil_sample_f64": ([c_vp, c_i64, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_vp], c_int),
         "akb_leaf_sink_bytes": ([c_int, c_i64], c_i64),
         "akb_leaf_sink_layout": ([c_vp, c_int, c_int, c_i64, ctypes.POINTER(LeafSink)], c_int),

@@ -8,13 +8,14 @@
 // gives means bit-identical to the reference's (AKB_raytrace_20250312.py:3583-3591, :3626, :3633,
 // :3674), which keeps the tilt angles and the OPD reference point exact.
 //
-// k_pw_chunks: one 256-thread workgroup per 8192-element buffer. The buffer is staged through LDS
-// with coalesced loads (NaN -> 0 and the count happen here); leaves are laid out 136 doubles
-// apart so the (leaf, accumulator) reads of a half-wave hit 64 distinct banks. A full buffer is
-// always 64 leaves of 128: thread (leaf, j) runs accumulator j of its leaf, three xor-shuffles
-// form the leaf in numpy's order, and one wave's six xor-shuffles form the exact split tree over
-// the 64 leaves. The (at most one per row) short last buffer walks the generic split tree.
-// k_pw_final adds the buffer results of a row left to right.
+// k_pw_chunks: one 256-thread workgroup per full 8192-element buffer. The buffer is staged
+// through LDS with coalesced loads (NaN -> 0 and the count happen here); leaves are laid out 136
+// doubles apart so the (leaf, accumulator) reads of a half-wave hit 64 distinct banks. A full
+// buffer is always 64 leaves of 128: thread (leaf, j) runs accumulator j of its leaf, three
+// xor-shuffles form the leaf in numpy's order, and one wave's six xor-shuffles form the exact
+// split tree over the 64 leaves. k_leaf_chunks does the same from leaf sums a producer already
+// formed. k_pw_final finishes a row: the buffer results added left to right, then the short last
+// buffer's pairwise sum (its split tree built and combined level by level by one wave).
 #include "akb_common.h"
 
 namespace akb {
@@ -23,183 +24,179 @@ constexpr int kPwBuf = 8192;
 constexpr int kPwLeaf = 128;
 constexpr int kPwStride = 136;  // LDS doubles per leaf (128 + 8 padding)
 constexpr int kPwThreads = 256;
-constexpr int kPwMaxLeaves = 160;
+constexpr int kTreeLevels = 8;  // a short buffer (< 8192) has leaves down to depth 7, <= 64 per level
+constexpr int kFinalTile = 4096;
 
 __device__ __forceinline__ int pw_split(int n) {
     int n2 = n / 2;
     return n2 - (n2 % 8);
 }
 
-__device__ __forceinline__ double lds_at(const double* s, int idx) {
-    return s[(idx >> 7) * kPwStride + (idx & (kPwLeaf - 1))];
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// numpy pairwise leaf over staged elements [off, off + n)
-__device__ double pw_leaf_lds(const double* s, int off, int n) {
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(b & 0xffffffffLL), l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+__device__ __forceinline__ double nan_zero(double v, bool nan0, long long& cnt) {
+    if (nan0 && v != v) return 0.0;
+    ++cnt;
+    return v;
+}
+
+// numpy pairwise leaf (n <= 128) over staged values (NaN already replaced)
+__device__ double pw_leaf_lds(const double* a, int n) {
     if (n < 8) {
         double res = 0.0;
-        for (int i = 0; i < n; ++i) res = res + lds_at(s, off + i);
+        for (int i = 0; i < n; ++i) res = res + a[i];
         return res;
     }
     double r[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) r[j] = lds_at(s, off + j);
+    for (int j = 0; j < 8; ++j) r[j] = a[j];
     int i = 8;
     for (; i < n - (n % 8); i += 8) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) r[j] = r[j] + lds_at(s, off + i + j);
+        for (int j = 0; j < 8; ++j) r[j] = r[j] + a[i + j];
     }
     double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-    for (; i < n; ++i) res = res + lds_at(s, off + i);
+    for (; i < n; ++i) res = res + a[i];
     return res;
 }
 
-// part / part_cnt: row r, buffer c lands at [r * part_ld + part_col0 + c]
-__global__ void __launch_bounds__(kPwThreads) k_pw_chunks(const double* __restrict__ x, int64_t ld, int64_t n,
-                                                          int nan_mask, int part_ld, int part_col0,
-                                                          double* __restrict__ part,
+struct PwTree {
+    int off[kTreeLevels][64];
+    int len[kTreeLevels][64];
+    int child[kTreeLevels][64];
+    double val[kTreeLevels][64];
+};
+
+// numpy pairwise_sum of a[0..len), 0 < len < 8192, by one wave: the split tree is built top-down
+// one level per step (a node of more than 128 elements splits at pw_split(n) into left and right
+// children, placed in order by a ballot prefix count), each leaf is summed by one lane, and the
+// levels are combined bottom-up as left + right.
+__device__ double pw_tree_wave(PwTree& T, const double* a, int len) {
+    const int lane = threadIdx.x & 63;
+    if (lane == 0) {
+        T.off[0][0] = 0;
+        T.len[0][0] = len;
+    }
+    int nd[kTreeLevels];
+    nd[0] = 1;
+    int depth = 1;
+    wave_sync();
+#pragma unroll
+    for (int d = 0; d < kTreeLevels; ++d) {
+        if (d < depth) {
+            const bool act = lane < nd[d];
+            int o = 0, l = 0;
+            if (act) {
+                o = T.off[d][lane];
+                l = T.len[d][lane];
+            }
+            const bool split = act && l > kPwLeaf && d + 1 < kTreeLevels;
+            const unsigned long long m = __ballot(split);
+            if (split) {
+                const int pos = 2 * __popcll(m & ((1ull << lane) - 1ull));
+                const int l2 = pw_split(l);
+                if (d + 1 < kTreeLevels) {
+                    T.off[d + 1][pos] = o;
+                    T.len[d + 1][pos] = l2;
+                    T.off[d + 1][pos + 1] = o + l2;
+                    T.len[d + 1][pos + 1] = l - l2;
+                }
+                T.child[d][lane] = pos;
+            } else if (act) {
+                T.val[d][lane] = pw_leaf_lds(a + o, l);
+            }
+            if (m && d + 1 < kTreeLevels) {
+                nd[d + 1] = 2 * __popcll(m);
+                depth = d + 2;
+            }
+            wave_sync();
+        }
+    }
+#pragma unroll
+    for (int d = kTreeLevels - 2; d >= 0; --d) {
+        if (d + 1 < depth) {
+            if (lane < nd[d] && T.len[d][lane] > kPwLeaf) {
+                const int c = T.child[d][lane];
+                T.val[d][lane] = T.val[d + 1][c] + T.val[d + 1][c + 1];
+            }
+            wave_sync();
+        }
+    }
+    return T.val[0][0];
+}
+
+// part / part_cnt: row r, buffer c lands at [r * part_ld + c]; only full buffers come here
+__global__ void __launch_bounds__(kPwThreads) k_pw_chunks(const double* __restrict__ x, int64_t ld, int nan_mask,
+                                                          int part_ld, double* __restrict__ part,
                                                           long long* __restrict__ part_cnt) {
     __shared__ double s[(kPwBuf / kPwLeaf) * kPwStride];
-    __shared__ double leafv[kPwMaxLeaves];
-    __shared__ int leaf_off[kPwMaxLeaves], leaf_len[kPwMaxLeaves];
-    __shared__ int n_leaves;
+    __shared__ double leafv[kPwBuf / kPwLeaf];
     __shared__ long long wcnt[kPwThreads / 64];
     const int row = blockIdx.y;
     const int c = blockIdx.x;
     const int tid = threadIdx.x;
     const double* a = x + row * ld + (int64_t)c * kPwBuf;
-    const int64_t rem = n - (int64_t)c * kPwBuf;
-    const int len = rem < kPwBuf ? (int)rem : kPwBuf;
     const bool nan0 = (nan_mask >> (row < 31 ? row : 31)) & 1;
 
     long long cnt = 0;
-    // stage: 16 independent loads per thread in flight before the LDS stores (a full buffer is
-    // 32 loads per thread, two batches)
+    // stage: 16 independent loads per thread in flight before the LDS stores (32 loads per
+    // thread, two batches)
     constexpr int kBatch = 16;
-    for (int i0 = tid; i0 < len; i0 += kPwThreads * kBatch) {
+    for (int i0 = tid; i0 < kPwBuf; i0 += kPwThreads * kBatch) {
         double v[kBatch];
 #pragma unroll
-        for (int k = 0; k < kBatch; ++k) {
-            const int i = i0 + k * kPwThreads;
-            v[k] = i < len ? a[i] : 0.0;
-        }
+        for (int k = 0; k < kBatch; ++k) v[k] = a[i0 + k * kPwThreads];
 #pragma unroll
         for (int k = 0; k < kBatch; ++k) {
             const int i = i0 + k * kPwThreads;
-            if (i < len) {
-                double w = v[k];
-                if (nan0 && w != w) {
-                    w = 0.0;
-                } else {
-                    ++cnt;
-                }
-                s[(i >> 7) * kPwStride + (i & (kPwLeaf - 1))] = w;
-            }
+            s[(i >> 7) * kPwStride + (i & (kPwLeaf - 1))] = nan_zero(v[k], nan0, cnt);
         }
     }
     for (int off = 32; off > 0; off >>= 1) cnt += __shfl_down(cnt, off);
     if ((tid & 63) == 0) wcnt[tid >> 6] = cnt;
     __syncthreads();
 
-    double result;
-    if (len == kPwBuf) {
-        // 64 leaves x 8 accumulators = 512 sequences, two per thread
+    // 64 leaves x 8 accumulators = 512 sequences, two per thread
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int leaf = (tid >> 3) + 32 * h;
-            const int j = tid & 7;
-            const double* L = s + leaf * kPwStride + j;
-            double r = L[0];
+    for (int h = 0; h < 2; ++h) {
+        const int leaf = (tid >> 3) + 32 * h;
+        const int j = tid & 7;
+        const double* L = s + leaf * kPwStride + j;
+        double r = L[0];
 #pragma unroll
-            for (int row8 = 1; row8 < kPwLeaf / 8; ++row8) r = r + L[row8 * 8];
-            r = r + __shfl_xor(r, 1);
-            r = r + __shfl_xor(r, 2);
-            r = r + __shfl_xor(r, 4);
-            if (j == 0) leafv[leaf] = r;
-        }
-        __syncthreads();
-        if (tid < 64) {
-            double v = leafv[tid];
-            v = v + __shfl_xor(v, 1);
-            v = v + __shfl_xor(v, 2);
-            v = v + __shfl_xor(v, 4);
-            v = v + __shfl_xor(v, 8);
-            v = v + __shfl_xor(v, 16);
-            v = v + __shfl_xor(v, 32);
-            result = v;
-        }
-    } else {
-        // short last buffer: enumerate the split tree's leaves, sum them in parallel, combine
-        if (tid == 0) {
-            int st_off[16], st_len[16];
-            int sp = 1, nl = 0;
-            st_off[0] = 0;
-            st_len[0] = len;
-            while (sp > 0) {
-                --sp;
-                const int o = st_off[sp], l = st_len[sp];
-                if (l <= kPwLeaf) {
-                    leaf_off[nl] = o;
-                    leaf_len[nl] = l;
-                    ++nl;
-                } else {
-                    const int l2 = pw_split(l);
-                    st_off[sp] = o + l2;
-                    st_len[sp] = l - l2;
-                    ++sp;
-                    st_off[sp] = o;
-                    st_len[sp] = l2;
-                    ++sp;
-                }
-            }
-            n_leaves = nl;
-        }
-        __syncthreads();
-        for (int li = tid; li < n_leaves; li += kPwThreads) leafv[li] = pw_leaf_lds(s, leaf_off[li], leaf_len[li]);
-        __syncthreads();
-        if (tid == 0) {
-            // post-order evaluation of the same tree
-            int st_len[16], st_state[16];
-            double st_left[16];
-            int sp = 1, li = 0;
-            bool have = false;
-            double res = 0.0;
-            st_len[0] = len;
-            st_state[0] = 0;
-            while (sp > 0) {
-                const int t = sp - 1;
-                if (!have) {
-                    if (st_len[t] <= kPwLeaf) {
-                        res = leafv[li++];
-                        have = true;
-                        --sp;
-                    } else {
-                        st_state[t] = 1;
-                        st_len[sp] = pw_split(st_len[t]);
-                        st_state[sp] = 0;
-                        ++sp;
-                    }
-                } else if (st_state[t] == 1) {
-                    st_left[t] = res;
-                    st_state[t] = 2;
-                    have = false;
-                    st_len[sp] = st_len[t] - pw_split(st_len[t]);
-                    st_state[sp] = 0;
-                    ++sp;
-                } else {
-                    res = st_left[t] + res;
-                    --sp;
-                }
-            }
-            result = res;
-        }
+        for (int row8 = 1; row8 < kPwLeaf / 8; ++row8) r = r + L[row8 * 8];
+        r = r + __shfl_xor(r, 1);
+        r = r + __shfl_xor(r, 2);
+        r = r + __shfl_xor(r, 4);
+        if (j == 0) leafv[leaf] = r;
     }
-    if (tid == 0) {
-        const int64_t o = (int64_t)row * part_ld + part_col0 + c;
-        part[o] = result;
-        long long tc = 0;
-        for (int w = 0; w < kPwThreads / 64; ++w) tc += wcnt[w];
-        part_cnt[o] = tc;
+    __syncthreads();
+    if (tid < 64) {
+        double v = leafv[tid];
+        v = v + __shfl_xor(v, 1);
+        v = v + __shfl_xor(v, 2);
+        v = v + __shfl_xor(v, 4);
+        v = v + __shfl_xor(v, 8);
+        v = v + __shfl_xor(v, 16);
+        v = v + __shfl_xor(v, 32);
+        if (tid == 0) {
+            const int64_t o = (int64_t)row * part_ld + c;
+            part[o] = v;
+            long long tc = 0;
+            for (int w = 0; w < kPwThreads / 64; ++w) tc += wcnt[w];
+            part_cnt[o] = tc;
+        }
     }
 }
 
@@ -228,49 +225,89 @@ __global__ void __launch_bounds__(64) k_leaf_chunks(const double* __restrict__ l
     }
 }
 
-// one workgroup per row: buffer results added left to right (a single dependent chain, fed from
-// LDS eight values ahead), counts summed by all threads
+// One workgroup per row q: the row's nparts full-buffer sums (part[q * part_ld + c]) added left to
+// right by wave 0 (a single dependent chain fed lane by lane from an LDS tile), the short last
+// buffer tail[q * tail_ld + 0 .. tail_len) staged to LDS and summed pairwise by wave 1 meanwhile,
+// then added last.
 __global__ void __launch_bounds__(kPwThreads) k_pw_final(const double* __restrict__ part,
-                                                         const long long* __restrict__ part_cnt, int nchunks,
+                                                         const long long* __restrict__ part_cnt, int part_ld,
+                                                         int nparts, const double* __restrict__ tail,
+                                                         int64_t tail_ld, int tail_len, int nan_mask,
                                                          double* __restrict__ out, int64_t* __restrict__ cnt_out) {
-    constexpr int kTile = 4096;
-    __shared__ double t[kTile];
+    __shared__ double t[kFinalTile];
+    __shared__ double tl[kPwBuf];
+    __shared__ PwTree T;
     __shared__ long long wc[kPwThreads / 64];
-    const int row = blockIdx.x;
+    __shared__ double tail_sum;
+    const int q = blockIdx.x;
     const int tid = threadIdx.x;
-    const double* p = part + (int64_t)row * nchunks;
-    const long long* pc = part_cnt + (int64_t)row * nchunks;
+    const int w = tid >> 6, lane = tid & 63;
+    const bool nan0 = (nan_mask >> (q < 31 ? q : 31)) & 1;
+    const double* p = part + (int64_t)q * part_ld;
+    const long long* pc = part_cnt + (int64_t)q * part_ld;
     long long cnt = 0;
-    for (int i = tid; i < nchunks; i += kPwThreads) cnt += pc[i];
-    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_down(cnt, off);
-    if ((tid & 63) == 0) wc[tid >> 6] = cnt;
-    double acc = 0.0;
-    for (int base = 0; base < nchunks; base += kTile) {
-        const int m = (nchunks - base) < kTile ? (nchunks - base) : kTile;
-        __syncthreads();
-        for (int i = tid; i < m; i += kPwThreads) t[i] = p[base + i];
-        __syncthreads();
-        if (tid == 0) {
-            int i = 0;
-            if (base == 0) {
-                acc = t[0];
-                i = 1;
-            }
-            for (; i + 8 <= m; i += 8) {
-                double v[8];
+    for (int i = tid; i < nparts; i += kPwThreads) cnt += pc[i];
+    {  // stage the short buffer: NaN -> 0 and the count here
+        const double* a = tail + (int64_t)q * tail_ld;
+        constexpr int kBatch = 8;
+        for (int i0 = tid; i0 < tail_len; i0 += kPwThreads * kBatch) {
+            double v[kBatch];
 #pragma unroll
-                for (int k = 0; k < 8; ++k) v[k] = t[i + k];
-#pragma unroll
-                for (int k = 0; k < 8; ++k) acc = acc + v[k];
+            for (int k = 0; k < kBatch; ++k) {
+                const int i = i0 + k * kPwThreads;
+                v[k] = i < tail_len ? a[i] : 0.0;
             }
-            for (; i < m; ++i) acc = acc + t[i];
+#pragma unroll
+            for (int k = 0; k < kBatch; ++k) {
+                const int i = i0 + k * kPwThreads;
+                if (i < tail_len) tl[i] = nan_zero(v[k], nan0, cnt);
+            }
         }
     }
+    double acc = 0.0;
+    for (int base = 0; base == 0 || base < nparts; base += kFinalTile) {
+        const int m = nparts - base < kFinalTile ? nparts - base : kFinalTile;
+        if (base > 0) __syncthreads();
+        for (int i = tid; i < m; i += kPwThreads) t[i] = p[base + i];
+        __syncthreads();
+        if (w == 0 && m > 0) {
+            double cur = lane < m ? t[lane] : 0.0;
+            int j0 = 0;
+            if (base == 0) {
+                acc = readlane_f64(cur, 0);
+                j0 = 1;
+            }
+            for (int b = 0; b < m; b += 64) {
+                const double nxt = b + 64 + lane < m ? t[b + 64 + lane] : 0.0;
+                const int e = m - b < 64 ? m - b : 64;
+                if (e == 64 && j0 == 0) {  // straight-line: no branch between the dependent adds
+#pragma unroll
+                    for (int j = 0; j < 64; ++j) acc = acc + readlane_f64(cur, j);
+                } else if (e == 64) {
+#pragma unroll
+                    for (int j = 1; j < 64; ++j) acc = acc + readlane_f64(cur, j);
+                } else {
+                    for (int j = j0; j < e; ++j) acc = acc + readlane_f64(cur, j);
+                }
+                j0 = 0;
+                cur = nxt;
+            }
+        }
+        if (w == 1 && base == 0 && tail_len > 0) {
+            const double v = pw_tree_wave(T, tl, tail_len);
+            if (lane == 0) tail_sum = v;
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_down(cnt, off);
+    if (lane == 0) wc[w] = cnt;
+    __syncthreads();
     if (tid == 0) {
-        out[row] = acc;
+        double r = acc;
+        if (tail_len > 0) r = nparts > 0 ? acc + tail_sum : tail_sum;
+        out[q] = r;
         long long tc = 0;
-        for (int w = 0; w < kPwThreads / 64; ++w) tc += wc[w];
-        cnt_out[row] = tc;
+        for (int k = 0; k < kPwThreads / 64; ++k) tc += wc[k];
+        cnt_out[q] = tc;
     }
 }
 
@@ -299,12 +336,18 @@ int akb_pairwise_sum_f64(const double* x, int64_t ld, int rows, int64_t n, int n
     const int64_t nb64 = (n + kPwBuf - 1) / kPwBuf;
     AKB_REQUIRE(nb64 < (1LL << 31), "row too long");
     const int nb = (int)nb64;
+    const int64_t nfull = n / kPwBuf;
+    const int tail = (int)(n - nfull * kPwBuf);
     double* part = (double*)d_work;
     long long* part_cnt = (long long*)(part + (int64_t)rows * nb);
-    k_pw_chunks<<<dim3(nb, rows), kPwThreads, 0, s>>>(x, ld, n, nan_to_zero ? -1 : 0, nb, 0, part, part_cnt);
-    int st = launch_status("k_pw_chunks");
-    if (st) return st;
-    k_pw_final<<<rows, kPwThreads, 0, s>>>(part, part_cnt, nb, d_sum, d_count);
+    const int mask = nan_to_zero ? -1 : 0;
+    if (nfull > 0) {
+        k_pw_chunks<<<dim3((unsigned)nfull, rows), kPwThreads, 0, s>>>(x, ld, mask, nb, part, part_cnt);
+        int st = launch_status("k_pw_chunks");
+        if (st) return st;
+    }
+    k_pw_final<<<rows, kPwThreads, 0, s>>>(part, part_cnt, nb, (int)nfull, x + nfull * kPwBuf, ld, tail, mask,
+                                           d_sum, d_count);
     return launch_status("k_pw_final");
 }
 
@@ -352,18 +395,14 @@ int akb_leaf_finish_f64(const akb_leaf_sink* sink, double* d_sum, int64_t* d_cou
     const int nb = (int)(nfull + (tail > 0 ? 1 : 0));
     double* part = (double*)work;
     long long* part_cnt = (long long*)(part + (int64_t)nq * nb);
-    int st;
     if (nfull > 0) {
         k_leaf_chunks<<<dim3((unsigned)nfull, nq), 64, 0, s>>>(sink->leaf_sum, sink->leaf_cnt,
                                                                 nfull * (kPwBuf / kPwLeaf), nb, part, part_cnt);
-        if ((st = launch_status("k_leaf_chunks"))) return st;
+        int st = launch_status("k_leaf_chunks");
+        if (st) return st;
     }
-    if (tail > 0) {
-        k_pw_chunks<<<dim3(1, nq), kPwThreads, 0, s>>>(sink->tail, kPwBuf, tail, sink->nan_mask, nb,
-                                                        (int)nfull, part, part_cnt);
-        if ((st = launch_status("k_pw_chunks(tail)"))) return st;
-    }
-    k_pw_final<<<nq, kPwThreads, 0, s>>>(part, part_cnt, nb, d_sum, d_count);
+    k_pw_final<<<nq, kPwThreads, 0, s>>>(part, part_cnt, nb, (int)nfull, sink->tail, kPwBuf, tail,
+                                         sink->nan_mask, d_sum, d_count);
     return launch_status("k_pw_final");
 }
 

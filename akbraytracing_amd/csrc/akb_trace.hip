@@ -13,6 +13,7 @@
 #include <mutex>
 
 #include "akb_common.h"
+#include "akb_sincos.h"
 
 namespace akb {
 
@@ -354,9 +355,44 @@ __global__ void __launch_bounds__(kBlock, kWaves) k_chain_sink(ChainArgs a) {
 // tilt correction + detectors + OPL (ref AKB_raytrace_20250312.py:3583-3601, :3611-3633)
 // ----------------------------------------------------------------------------------------------
 
+// Parameter block of the tilt (ref :3583-3591 and rotate_vectors :917-927), formed on the device
+// from the pass-2 sums so no host round trip sits between pass 2 and the tilt:
+//   theta_y = -nanmean(arctan(Rz/Rx)), theta_z = nanmean(arctan(Ry/Rx)), focus = mean(det)
+//   Ry, Rz = rotation_matrices(-theta_y, -theta_z) with correctly rounded cos / sin
+// It also zeroes the words the next step accumulates into (pupil extent keys, trace flags that
+// were already copied out in stream order).
+constexpr int kTiltTheta = 0, kTiltRy = 2, kTiltRz = 11, kTiltFocus = 20;
+
+__global__ void k_tilt_params(const double* __restrict__ s5, const int64_t* __restrict__ c5, double* __restrict__ P,
+                              unsigned long long* keys, int32_t* clear, int nclear) {
+    const int lane = threadIdx.x;
+    // np.nanmean / np.mean: sum / count, an IEEE division (0 / 0 -> NaN as numpy's)
+    const double mh = s5[0] / (double)c5[0];
+    const double mv = s5[1] / (double)c5[1];
+    const double theta_y = -mv, theta_z = mh;
+    // lanes 0..3: sin(-theta_y), cos(-theta_y), sin(-theta_z), cos(-theta_z) side by side
+    double v = 0.0;
+    if (lane < 4) v = akb_sc::sin_cos_cr(lane < 2 ? -theta_y : -theta_z, lane & 1);
+    const double sy = __shfl(v, 0), cy = __shfl(v, 1), sz = __shfl(v, 2), cz = __shfl(v, 3);
+    if (lane == 0) {
+        P[kTiltTheta] = theta_y;
+        P[kTiltTheta + 1] = theta_z;
+        const double ry[9] = {cy, 0.0, sy, 0.0, 1.0, 0.0, -sy, 0.0, cy};
+        const double rz[9] = {cz, -sz, 0.0, sz, cz, 0.0, 0.0, 0.0, 1.0};
+        for (int k = 0; k < 9; ++k) {
+            P[kTiltRy + k] = ry[k];
+            P[kTiltRz + k] = rz[k];
+        }
+    }
+    if (lane >= 4 && lane < 7) P[kTiltFocus + lane - 4] = s5[2 + lane - 4] / (double)c5[2 + lane - 4];
+    if (keys && lane < 4) keys[lane] = 0ULL;
+    for (int i = lane; i < nclear; i += blockDim.x) clear[i] = 0;
+}
+
 struct TiltArgs {
     Mat3 Ry, Rz;
     double c[3];
+    const double* params;  // non-NULL: Ry, Rz, c from akb_tilt_params_f64's device block
     double d1[4], d2[4];
     const double* dir;
     const double* pt;
@@ -415,7 +451,21 @@ __device__ __forceinline__ void tilt_ray(const TiltArgs& a, int64_t i, double (&
     if (a.total2) a.total2[i] = qv[4];
 }
 
+// the rotation and centre from the device parameter block (uniform scalar loads)
+__device__ __forceinline__ void tilt_load_params(TiltArgs& a) {
+    if (!a.params) return;
+    const double* P = a.params;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        a.Ry.m[k] = P[kTiltRy + k];
+        a.Rz.m[k] = P[kTiltRz + k];
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) a.c[k] = P[kTiltFocus + k];
+}
+
 __global__ void __launch_bounds__(kBlock) k_tilt_opd(TiltArgs a) {
+    tilt_load_params(a);
     double qv[5];
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < a.n;
          i += (int64_t)gridDim.x * blockDim.x)
@@ -423,6 +473,7 @@ __global__ void __launch_bounds__(kBlock) k_tilt_opd(TiltArgs a) {
 }
 
 __global__ void __launch_bounds__(kBlock) k_tilt_opd_sink(TiltArgs a) {
+    tilt_load_params(a);
     __shared__ LeafLds<5> L;
     const int64_t nseg = (a.n + kLeafSeg - 1) / kLeafSeg;
     for (int64_t seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
@@ -786,25 +837,17 @@ int akb_trace_chain_f64(const akb_chain_desc* d, void* stream) {
     return launch_status("k_chain");
 }
 
-int akb_tilt_opd_f64(const double ry[9], const double rz[9], const double center[3],
-                     const double det1_ghij[4], const double det2_ghij[4], const double* dir,
-                     const double* pt, const double* opl, int64_t ld, int64_t n, double* dir_rot,
-                     double* pt_rot, double* det1, double* det2, double* total1, double* total2,
-                     const akb_leaf_sink* sink, void* stream) {
-    clear_error();
-    AKB_REQUIRE(ry && rz && center && det1_ghij && det2_ghij && dir && pt, "null pointer");
+static int launch_tilt(TiltArgs& a, const double det1_ghij[4], const double det2_ghij[4], const double* dir,
+                       const double* pt, const double* opl, int64_t ld, int64_t n, double* dir_rot, double* pt_rot,
+                       double* det1, double* det2, double* total1, double* total2, const akb_leaf_sink* sink,
+                       void* stream) {
+    AKB_REQUIRE(det1_ghij && det2_ghij && dir && pt, "null pointer");
     AKB_REQUIRE(n >= 0 && ld >= n, "bad sizes");
     const bool use_sink = sink && sink->nq > 0;
     if (use_sink)
         AKB_REQUIRE(sink->nq == 5 && sink->n == n && sink->leaf_sum && sink->leaf_cnt && sink->tail,
                     "tilt sink must be a 5-quantity sink over n");
     if (n == 0) return AKB_OK;
-    TiltArgs a{};
-    for (int k = 0; k < 9; ++k) {
-        a.Ry.m[k] = ry[k];
-        a.Rz.m[k] = rz[k];
-    }
-    for (int k = 0; k < 3; ++k) a.c[k] = center[k];
     for (int k = 0; k < 4; ++k) {
         a.d1[k] = det1_ghij[k];
         a.d2[k] = det2_ghij[k];
@@ -831,15 +874,55 @@ int akb_tilt_opd_f64(const double ry[9], const double rz[9], const double center
     return launch_status("k_tilt_opd");
 }
 
+int akb_tilt_opd_f64(const double ry[9], const double rz[9], const double center[3],
+                     const double det1_ghij[4], const double det2_ghij[4], const double* dir,
+                     const double* pt, const double* opl, int64_t ld, int64_t n, double* dir_rot,
+                     double* pt_rot, double* det1, double* det2, double* total1, double* total2,
+                     const akb_leaf_sink* sink, void* stream) {
+    clear_error();
+    AKB_REQUIRE(ry && rz && center, "null pointer");
+    TiltArgs a{};
+    for (int k = 0; k < 9; ++k) {
+        a.Ry.m[k] = ry[k];
+        a.Rz.m[k] = rz[k];
+    }
+    for (int k = 0; k < 3; ++k) a.c[k] = center[k];
+    a.params = nullptr;
+    return launch_tilt(a, det1_ghij, det2_ghij, dir, pt, opl, ld, n, dir_rot, pt_rot, det1, det2, total1, total2,
+                       sink, stream);
+}
+
+int akb_tilt_params_f64(const double* d_sum5, const int64_t* d_cnt5, double* d_params, uint64_t* d_extent_keys,
+                        int32_t* d_clear, int n_clear, void* stream) {
+    clear_error();
+    AKB_REQUIRE(d_sum5 && d_cnt5 && d_params, "null pointer");
+    AKB_REQUIRE(n_clear >= 0 && (n_clear == 0 || d_clear), "bad clear list");
+    k_tilt_params<<<1, 64, 0, (hipStream_t)stream>>>(d_sum5, d_cnt5, d_params, (unsigned long long*)d_extent_keys,
+                                                      d_clear, n_clear);
+    return launch_status("k_tilt_params");
+}
+
+int akb_tilt_opd_dev_f64(const double* d_params, const double det1_ghij[4], const double det2_ghij[4],
+                         const double* dir, const double* pt, const double* opl, int64_t ld, int64_t n,
+                         double* dir_rot, double* pt_rot, double* det1, double* det2, double* total1,
+                         double* total2, const akb_leaf_sink* sink, void* stream) {
+    clear_error();
+    AKB_REQUIRE(d_params, "null pointer");
+    TiltArgs a{};
+    a.params = d_params;
+    return launch_tilt(a, det1_ghij, det2_ghij, dir, pt, opl, ld, n, dir_rot, pt_rot, det1, det2, total1, total2,
+                       sink, stream);
+}
+
 int akb_opd_f64(const double* total1, const double* total2, const double* det2, int64_t ld, int64_t n,
                 const double* d_sum5, const int64_t* d_cnt5, double* dist_err1, double* dist_err2,
-                double* sph, double* wave, uint64_t* d_extent_keys, void* stream) {
+                double* sph, double* wave, uint64_t* d_extent_keys, int keys_zeroed, void* stream) {
     clear_error();
     AKB_REQUIRE(n >= 0 && ld >= n, "bad sizes");
     AKB_REQUIRE(total2 && det2 && d_sum5 && d_cnt5, "total2, det2 and the tilt means are required");
     AKB_REQUIRE(!dist_err1 || total1, "dist_err1 needs total1");
     hipStream_t s = (hipStream_t)stream;
-    if (d_extent_keys) AKB_HIP_CHECK(hipMemsetAsync(d_extent_keys, 0, 4 * sizeof(uint64_t), s));
+    if (d_extent_keys && !keys_zeroed) AKB_HIP_CHECK(hipMemsetAsync(d_extent_keys, 0, 4 * sizeof(uint64_t), s));
     if (n == 0) return AKB_OK;
     OpdArgs a{};
     a.t1 = total1;

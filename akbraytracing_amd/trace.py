@@ -67,7 +67,8 @@ class ChainLaunch:
     their addresses may not). trace_chain() is the one-shot form."""
 
     def __init__(self, mirrors, *, tan_h=None, tan_v=None, row0=0, n_rays=None, dirs=None, src=(0.0, 0.0, 0.0),
-                 det_ghij=None, want=("last_hit", "dir_out"), samples=None, out=None, sink=None):
+                 det_ghij=None, want=("last_hit", "dir_out"), samples=None, out=None, sink=None, flags=None,
+                 samples_buf=None):
         dev = D.device()
         desc = _lib.ChainDesc()
         _fill_desc(desc, mirrors, det_ghij)
@@ -101,7 +102,9 @@ class ChainLaunch:
             out[name] = t
             return t
 
-        res = ChainOutputs(flags=torch.zeros(1, dtype=torch.int32, device=dev))
+        if flags is None:
+            flags = torch.zeros(1, dtype=torch.int32, device=dev)
+        res = ChainOutputs(flags=flags)
         if "hits" in want:
             res.hits = buf("hits", (K, 3, n))
             desc.hits, desc.hits_ld = D.ptr(res.hits), n
@@ -130,7 +133,13 @@ class ChainLaunch:
             nh = max(he - hb, 0)
             nv = tan_v.shape[0] if vc is not None else 0
             # one buffer so the host reads both pick lists with one copy
-            res.extra["samples"] = torch.full((nh + nv,), float("nan"), dtype=D.F64, device=dev)
+            if samples_buf is not None:
+                if samples_buf.numel() != nh + nv or samples_buf.dtype != D.F64:
+                    raise ValueError("samples_buf must hold the middle-row range plus one column (float64)")
+                samples_buf.fill_(float("nan"))
+                res.extra["samples"] = samples_buf
+            else:
+                res.extra["samples"] = torch.full((nh + nv,), float("nan"), dtype=D.F64, device=dev)
             res.samp_h = res.extra["samples"][:nh]
             desc.samp_h, desc.samp_h_begin, desc.samp_h_end = D.ptr(res.samp_h), hb, he
             if vc is not None:
@@ -158,6 +167,8 @@ def trace_chain(mirrors, *, stream=None, **kw):
     `dirs` (3, n) device tensor. Source: a 3-vector (constant) or a (3, n) device tensor.
     want: subset of {"hits", "last_hit", "dir_out", "det", "opl", "atan"}.
     samples: (h_begin, h_end, v_col) flat-index range / column whose exit slopes to record.
+    flags / samples_buf: optional caller-owned int32 flag word and float64 pick buffer (RayWave
+        places the flag words right after the picks so one copy brings both to the host).
     out: optional dict of preallocated tensors keyed like ChainOutputs fields (reused buffers).
     sink: optional reduce.LeafSink(5, n_rays, nan_mask=0b00011) fed with (arctan(Ry/Rx),
         arctan(Rz/Rx), det_x, det_y, det_z) — the tilt means without writing those rows.

@@ -4,9 +4,9 @@ One call of RayWave.run() is what plot_result_debug(params, 'ray_wave') does bet
 its mirrors and calling griddata (AKB_raytrace_20250312.py:2675-3689), on an n x n ray grid:
 
   pass 1    fused chain over the grid, exit slopes of the middle row/column     :2770-2845
-  resample  np.arctan + scipy interp1d on the host (2n values)                  :2849-2879
+  resample  np.arctan + interp1d (restated in C) + np.tan on the host (2n values) :2849-2879
   pass 2    fused chain + OPL + pre-tilt detector + arctan of the exit slopes   :2881-2905
-  means     numpy-exact device sums -> theta_y, theta_z, focus_apprx            :3583-3591
+  means     numpy-exact device sums -> theta_y, theta_z, focus_apprx, R_y, R_z  :3583-3591, :917-927
   tilt      rotate direction / last hit (dgemm FMA order), detectors 1 and 2,
             totalDist, totalDist2                                               :3592-3633
   OPD       DistError2, Sph, Wave2 = DistError2 - Sph                           :3626-3677
@@ -103,23 +103,53 @@ def sample_ownership(shard, n):
     return own_h, own_v
 
 
-def _interp1d_linear(x, y, x_new):
-    """scipy.interpolate.interp1d(x, y, kind='linear')(x_new) for 1-D float64 data: scipy sorts x
-    with a stable mergesort and delegates to np.interp (scipy 1.15 _call_linear_np)."""
-    ind = np.argsort(x, kind="mergesort")
-    xs, ys = x[ind], y[ind]
-    if np.any(x_new < xs[0]) or np.any(x_new > xs[-1]):
-        raise ValueError("A value in x_new is outside the interpolation range.")
-    return np.interp(x_new, xs, ys)
+def resample_axis(angle_sep, rand, out=None):
+    """interp1d(angle_sep, rand, kind='linear')(np.linspace(angle_sep[0], angle_sep[-1], n)) — one
+    axis of :2861-2870, done by the library's host routine (numpy linspace / interp and scipy's
+    stable sort restated; ValueError out of range like interp1d)."""
+    x = np.ascontiguousarray(angle_sep, dtype=np.float64)
+    y = np.ascontiguousarray(rand, dtype=np.float64)
+    if x.ndim != 1 or x.shape != y.shape:
+        raise ValueError("resample needs two 1-D arrays of one length")
+    if out is None:
+        out = np.empty_like(x)
+    L = _lib.lib()
+    if L.akb_resample_f64(x.ctypes.data, y.ctypes.data, x.shape[0], out.ctypes.data) != 0:
+        raise ValueError(L.akb_last_error().decode())
+    return out
 
 
 def resample(angle_h_sep, angle_v_sep, rand_h, rand_v):
     """:2861-2870 — interp1d of the launch angles onto equally spaced exit angles."""
-    out_v = np.linspace(angle_v_sep[0], angle_v_sep[-1], len(angle_v_sep))
-    out_h = np.linspace(angle_h_sep[0], angle_h_sep[-1], len(angle_h_sep))
-    new_v = _interp1d_linear(np.asarray(angle_v_sep, dtype=np.float64), np.asarray(rand_v, dtype=np.float64), out_v)
-    new_h = _interp1d_linear(np.asarray(angle_h_sep, dtype=np.float64), np.asarray(rand_h, dtype=np.float64), out_h)
-    return new_h, new_v
+    return resample_axis(angle_h_sep, rand_h), resample_axis(angle_v_sep, rand_v)
+
+
+class RunResult(dict):
+    """RayWave.run()'s outputs. theta_y, theta_z and focus_apprx live in the device parameter
+    block of the tilt; they are copied to the host on first access (the run itself never waits
+    for them)."""
+    _LAZY = ("theta_y", "theta_z", "focus_apprx")
+
+    def __init__(self, *a, params=None, **k):
+        super().__init__(*a, **k)
+        self._params = params
+
+    def _resolve(self):
+        if self._params is not None:
+            h = self._params.cpu().numpy()
+            self._params = None
+            dict.update(self, theta_y=np.float64(h[0]), theta_z=np.float64(h[1]), focus_apprx=h[20:23].copy())
+
+    def __getitem__(self, k):
+        if k in self._LAZY:
+            self._resolve()
+        return dict.__getitem__(self, k)
+
+    def get(self, k, default=None):
+        return self[k] if k in self else default
+
+    def __contains__(self, k):
+        return (k in self._LAZY and self._params is not None) or dict.__contains__(self, k)
 
 
 class LocalComm:
@@ -143,8 +173,10 @@ class LocalComm:
 class RayWave:
     """Device-resident 'ray_wave' / 'wave' trace on an n x n grid (one shard of it).
 
-    Every launch is prepared once (descriptors, device buffers, pinned host staging), so a run
-    costs two host round trips plus a handful of ctypes calls."""
+    Every launch is prepared once (descriptors, device buffers, pinned host staging). A run
+    waits on the host once, for the resample picks of pass 1 (the resample itself is host work
+    by design, see resample_axis); pass 2, the tilt parameters, the tilt and the OPD are queued
+    back to back, and the run returns as soon as pass 2's flag word has reached the host."""
 
     def __init__(self, geometry, n, shard=None, comm=None, resample_pass=True):
         self.g = geometry
@@ -166,21 +198,26 @@ class RayWave:
         self.sink3 = LeafSink(5, self.n_local, 0b11111, self.dev)
         self._ext = torch.zeros(4, dtype=torch.int64, device=self.dev)  # det2 extent keys (uint64 bits)
         self._pitch = torch.zeros(2, dtype=D.F64, device=self.dev)
+        self._params = torch.zeros(23, dtype=D.F64, device=self.dev)  # akb_tilt_params_f64 block
         self._opd_buf = None
         self.last = {}
         self.kernel_events = None  # set to a list to time the pass-2 chain launch (bench.py)
-        # prepared launches
+        # prepared launches. The pick buffer ends with one double-sized slot holding the two
+        # trace flag words (pass 1, pass 2): one copy brings the picks and pass 1's flags to the
+        # host, an 8-byte copy brings pass 2's, and the tilt-parameter kernel zeroes both.
         self._plan = sample_plan(self.n)
         hb, he, col = self._plan
+        self._nsamp = (he - hb) + self.n
+        self._x1 = torch.zeros(self._nsamp + 1, dtype=D.F64, device=self.dev)
+        self._flags = self._x1[self._nsamp:].view(torch.int32)  # [pass 1, pass 2]
+        self._x1_host = torch.empty(self._nsamp + 1, dtype=D.F64, pin_memory=True)
+        self._f_host = torch.zeros(2, dtype=torch.int32, pin_memory=True)
         self._tan2 = torch.empty(2 * self.n, dtype=D.F64, device=self.dev)  # pass-2 tables [h | v]
         self._tan2_host = torch.empty(2 * self.n, dtype=D.F64, pin_memory=True)
         self._p1 = ChainLaunch(self.g.mirrors, tan_h=self.tan_h, tan_v=self.tan_v, row0=self.shard.row0,
-                               n_rays=self.n_local, src=self.g.source, want=(), samples=(hb, he, col))
+                               n_rays=self.n_local, src=self.g.source, want=(), samples=(hb, he, col),
+                               flags=self._flags[0:1], samples_buf=self._x1[:self._nsamp])
         self._p2 = {}
-        nsamp = (he - hb) + self.n
-        self._x1_host = torch.empty(nsamp + 1, dtype=D.F64, pin_memory=True)
-        self._x2_host = torch.empty(11, dtype=D.F64, pin_memory=True)
-        self._x2_dev = torch.empty(11, dtype=D.F64, device=self.dev)
         self._own = sample_ownership(self.shard, self.n)
 
     def _pass2_launch(self, want_rows):
@@ -189,29 +226,31 @@ class RayWave:
             want = ("last_hit", "dir_out", "opl") + (("det", "atan") if want_rows else ())
             self._p2[key] = ChainLaunch(self.g.mirrors, tan_h=self._tan2[:self.n], tan_v=self._tan2[self.n:],
                                         row0=self.shard.row0, n_rays=self.n_local, src=self.g.source,
-                                        det_ghij=self.g.det1, want=want, sink=self.sink2)
+                                        det_ghij=self.g.det1, want=want, sink=self.sink2, flags=self._flags[1:2])
         return self._p2[key]
 
     # -------------------------------------------------------------- passes
     def _pass1(self, overlap=None):
         hb, he, col = self._plan
-        r = self._p1.launch()
+        self._p1.launch(reset_flags=False)
         x = self._x1_host
-        nh = he - hb
-        x[:nh + self.n].copy_(r.extra["samples"], non_blocking=True)
-        x[nh + self.n:].copy_(r.flags.to(D.F64), non_blocking=True)
+        x.copy_(self._x1, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
         if overlap is not None:
             overlap()  # independent device work queued behind the copy (runs while the host waits)
         ev.synchronize()
         host = x.numpy()
-        own_h, own_v = self._own
-        samp_h = np.where(own_h, host[:nh], 0.0)
-        samp_v = np.where(own_v, host[nh:nh + self.n], 0.0)
-        flags = int(host[-1])
-        samp_h, samp_v = self.comm.gather_samples(samp_h, samp_v, self.shard, self.n)
-        flags = self.comm.sum_flags(flags)
+        nh = he - hb
+        flags = int(host[self._nsamp:].view(np.int32)[0])
+        if self.comm.world > 1:
+            own_h, own_v = self._own
+            samp_h = np.where(own_h, host[:nh], 0.0)
+            samp_v = np.where(own_v, host[nh:self._nsamp], 0.0)
+            samp_h, samp_v = self.comm.gather_samples(samp_h, samp_v, self.shard, self.n)
+            flags = self.comm.sum_flags(flags)
+        else:
+            samp_h, samp_v = host[:nh], host[nh:self._nsamp]
         return samp_h, samp_v, flags
 
     def _pass2(self, want_rows=False):
@@ -219,7 +258,7 @@ class RayWave:
         if self.kernel_events is not None:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
-        r = self._pass2_launch(want_rows).launch()
+        r = self._pass2_launch(want_rows).launch(reset_flags=False)
         if ev is not None:
             ev[1].record()
             self.kernel_events.append(ev)
@@ -243,68 +282,83 @@ class RayWave:
 
     # -------------------------------------------------------------- one run
     def run(self, opd=True, keep_rotated=False, full=False, overlap=None):
-        """Trace and reduce; returns a dict of device tensors (this shard's rays) and host means.
+        """Trace and reduce; returns a RunResult of device tensors (this shard's rays) and means.
         keep_rotated: also return the tilted direction / last hit (dir_rot, pt_rot); full: also
         return DistError (detector 1), Sph, detcenter and the pre-tilt rows. The default keeps what
         griddata consumes (DistError2, Wave2, detcenter2) and reduces everything else on the fly.
         overlap: callable enqueuing independent device work (e.g. the previous step's PSF) that
-        runs while the host performs the resample.
-
-        Host round trips: two (the resample picks, and the tilt angles, whose rotation matrices are
-        formed with numpy's cos/sin exactly as the reference forms them)."""
+        runs while the host performs the resample."""
+        L = _lib.lib()
+        stream = D.stream_handle()
         samp_h, samp_v, flags1 = self._pass1(overlap)
         if flags1:
+            self._flags.zero_()
             raise _lib.AKBError(
                 f"pass 1 raised trace flags {flags1:#x} (a ray missed a mirror or a norm was zero): the "
                 "reference returns all-NaN here and its interp1d resample fails on it")
-        if self.resample_pass:
-            new_h, new_v = resample(np.arctan(samp_h), np.arctan(samp_v), self.rand_h, self.rand_v)
-        else:
-            new_h, new_v = self.rand_h, self.rand_v
         th = self._tan2_host.numpy()
-        np.tan(new_h, out=th[:self.n])
-        np.tan(new_v, out=th[self.n:])
+        if self.resample_pass:
+            # np.arctan / np.tan stay numpy's (their SIMD kernels are what the reference runs)
+            np.tan(resample_axis(np.arctan(samp_h), self.rand_h), out=th[:self.n])
+            np.tan(resample_axis(np.arctan(samp_v), self.rand_v), out=th[self.n:])
+        else:
+            np.tan(self.rand_h, out=th[:self.n])
+            np.tan(self.rand_v, out=th[self.n:])
         self._tan2.copy_(self._tan2_host, non_blocking=True)
         tan_h2, tan_v2 = self._tan2[:self.n], self._tan2[self.n:]
         r = self._pass2(want_rows=full)
+        if self.comm.world > 1:
+            self.comm.allreduce_sums(self._flags[1:2])
+        self._f_host.copy_(self._flags, non_blocking=True)
+        ev2 = torch.cuda.Event()
+        ev2.record()
         sums, cnts = self.sink2.finish()
-        x2 = self._x2_dev
-        x2[0:5].copy_(sums)
-        x2[5:10].copy_(cnts)
-        x2[10:11].copy_(r.flags)
-        red = self.comm.allreduce_sums(x2)
-        self._x2_host.copy_(red, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
-        ev.synchronize()
-        host = self._x2_host.numpy()
-        flags2 = int(host[-1])
-        last_hit, dir_out, opl = r.last_hit, r.dir_out, r.opl
-        det_pre, atan = r.det, r.atan
+        if self.comm.world > 1:  # cross-rank means: partial sums added over ranks (not numpy order)
+            self.comm.allreduce_sums(sums)
+            self.comm.allreduce_sums(cnts)
+        _lib.check(L.akb_tilt_params_f64(D.ptr(sums), D.ptr(cnts), D.ptr(self._params), D.ptr(self._ext),
+                                         D.ptr(self._flags), 2, stream))
+        out = RunResult(last_hit=r.last_hit, dir_out=r.dir_out, opl=r.opl, tan_h2=tan_h2, tan_v2=tan_v2,
+                        params=self._params)
+        if full:
+            out.update(det_pre=r.det, atan=r.atan)
+        if opd:
+            out.update(self._tilt_opd(r.last_hit, r.dir_out, r.opl, keep_rotated, full))
+        ev2.synchronize()
+        flags2 = int(self._f_host[1])
         if flags2:
-            last_hit, dir_out, det_pre, opl, atan = self._pass2_staged(tan_h2.clone(), tan_v2.clone())
-            (atan_s, atan_c), (det_s, det_c) = self.sums(atan, nan=True), self.sums(det_pre)
-            red = self.comm.allreduce_sums(torch.cat([atan_s, det_s, atan_c.to(D.F64), det_c.to(D.F64)]))
-            host = red.cpu().numpy()
+            out = self._run_staged(out, tan_h2, tan_v2, opd, keep_rotated, full)
+        out["flags"] = (flags1, flags2)
+        self.last = out
+        return out
+
+    def _run_staged(self, fast, tan_h2, tan_v2, opd, keep_rotated, full):
+        """Pass 2 flagged a miss or a zero norm: redo it stage by stage (the reference's value
+        rules) and the tilt from host-formed matrices."""
+        torch.cuda.synchronize()
+        last_hit, dir_out, det_pre, opl, atan = self._pass2_staged(tan_h2.clone(), tan_v2.clone())
+        (atan_s, atan_c), (det_s, det_c) = self.sums(atan, nan=True), self.sums(det_pre)
+        red = self.comm.allreduce_sums(torch.cat([atan_s, det_s, atan_c.to(D.F64), det_c.to(D.F64)]))
+        host = red.cpu().numpy()
         with np.errstate(invalid="ignore", divide="ignore"):
             mean_atan = host[0:2] / host[5:7]
             focus = host[2:5] / host[7:10]
         theta_y = -mean_atan[1]
         theta_z = mean_atan[0]
-        out = dict(last_hit=last_hit, dir_out=dir_out, opl=opl, theta_y=theta_y, theta_z=theta_z,
-                   focus_apprx=focus, tan_h2=tan_h2, tan_v2=tan_v2, flags=(flags1, flags2))
+        out = RunResult(last_hit=last_hit, dir_out=dir_out, opl=opl, theta_y=theta_y, theta_z=theta_z,
+                        focus_apprx=focus, tan_h2=tan_h2, tan_v2=tan_v2)
         if full:
             out.update(det_pre=det_pre, atan=atan)
         if opd:
-            out.update(self._tilt_opd(last_hit, dir_out, opl, theta_y, theta_z, focus, keep_rotated, full))
-        self.last = out
+            ry, rz = P.rotation_matrices(-theta_y, -theta_z)
+            out.update(self._tilt_opd(last_hit, dir_out, opl, keep_rotated, full, host_tilt=(ry, rz, focus)))
         return out
 
-    def _tilt_opd(self, last_hit, dir_out, opl, theta_y, theta_z, focus, keep_rotated=False, full=False):
+    def _tilt_opd(self, last_hit, dir_out, opl, keep_rotated=False, full=False, host_tilt=None):
         L = _lib.lib()
         n = self.n_local
         dev = self.dev
-        ry, rz = P.rotation_matrices(-theta_y, -theta_z)
+        stream = D.stream_handle()
         two = self.g.det2 is not None
         det1 = torch.empty((3, n), dtype=D.F64, device=dev) if (full or not two) else None
         det2 = torch.empty((3, n), dtype=D.F64, device=dev) if two else None
@@ -314,16 +368,18 @@ class RayWave:
         pt_rot = torch.empty((3, n), dtype=D.F64, device=dev) if keep_rotated else None
         d2 = self.g.det2 if two else self.g.det1
         det2_buf = det2 if two else torch.empty((3, n), dtype=D.F64, device=dev)
-        _lib.check(L.akb_tilt_opd_f64(D.host_f64(ry.ravel()), D.host_f64(rz.ravel()), D.host_f64(focus),
-                                      D.host_f64(self.g.det1), D.host_f64(d2), D.ptr(dir_out), D.ptr(last_hit),
-                                      D.ptr(opl), n, n, D.ptr(dir_rot), D.ptr(pt_rot), D.ptr(det1),
-                                      D.ptr(det2_buf), D.ptr(total1), D.ptr(total2), self.sink3.desc,
-                                      D.stream_handle()))
+        outs = (D.ptr(dir_out), D.ptr(last_hit), D.ptr(opl), n, n, D.ptr(dir_rot), D.ptr(pt_rot), D.ptr(det1),
+                D.ptr(det2_buf), D.ptr(total1), D.ptr(total2), self.sink3.desc, stream)
+        if host_tilt is None:
+            _lib.check(L.akb_tilt_opd_dev_f64(D.ptr(self._params), D.host_f64(self.g.det1), D.host_f64(d2), *outs))
+        else:
+            ry, rz, focus = host_tilt
+            _lib.check(L.akb_tilt_opd_f64(D.host_f64(ry.ravel()), D.host_f64(rz.ravel()), D.host_f64(focus),
+                                          D.host_f64(self.g.det1), D.host_f64(d2), *outs))
         sums, cnts = self.sink3.finish()
-        if self.comm.world > 1:  # cross-rank means: partial sums added over ranks (not numpy order)
-            red = self.comm.allreduce_sums(torch.cat([sums, cnts.to(D.F64)]))
-            sums = red[:5].contiguous()
-            cnts = red[5:].to(torch.int64).contiguous()
+        if self.comm.world > 1:
+            self.comm.allreduce_sums(sums)
+            self.comm.allreduce_sums(cnts)
         self._means5 = (sums, cnts)
         dist_err = torch.empty(n, dtype=D.F64, device=dev) if total1 is not None else None
         dist_err2 = torch.empty(n, dtype=D.F64, device=dev)
@@ -331,7 +387,7 @@ class RayWave:
         wave2 = torch.empty(n, dtype=D.F64, device=dev) if two else None
         _lib.check(L.akb_opd_f64(D.ptr(total1), D.ptr(total2), D.ptr(det2_buf), n, n, D.ptr(sums), D.ptr(cnts),
                                  D.ptr(dist_err), D.ptr(dist_err2), D.ptr(sph), D.ptr(wave2), D.ptr(self._ext),
-                                 D.stream_handle()))
+                                 int(host_tilt is None), stream))
         res = dict(dir_rot=dir_rot, pt_rot=pt_rot, detcenter=det1, detcenter2=det2, total=total1, total2=total2,
                    dist_err=dist_err, dist_err2=dist_err2, sph=sph, wave2=wave2)
         return res

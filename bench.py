@@ -107,26 +107,41 @@ def main():
 
     psf_events = []
     psf_out = {}
-    pending = []  # pupil of the previous step, transformed while the host resamples the next one
+    pending = []  # pupil of the previous step, transformed while the next step traces
+    side = torch.cuda.Stream(device=dev)
+    state = {"psf_done": None}
 
     def run_psf(item, timed):
-        opd, pitch = item
+        """The PSF of a finished pupil on a side stream: it starts when the pupil is ready and
+        fills the GPU while the host resamples (and beside the next step's kernels)."""
+        opd, pitch, ready = item
         if rank != 0:
             return
-        if timed:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-        psf, _, _ = psf_stack(opd, None, [lam], None, pitch=pitch, pad_factor=args.pad, out=psf_out.get("psf"))
-        psf_out["psf"] = psf
-        if timed:
-            e1.record()
-            psf_events.append((e0, e1))
+        side.wait_event(ready)
+        with torch.cuda.stream(side):
+            if timed:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(side)
+            psf, _, _ = psf_stack(opd, None, [lam], None, pitch=pitch, pad_factor=args.pad,
+                                  out=psf_out.get("psf"))
+            psf_out["psf"] = psf
+            if timed:
+                e1.record(side)
+                psf_events.append((e0, e1))
+            done = torch.cuda.Event()
+            done.record(side)
+        state["psf_done"] = done
 
     def step(timed):
-        # the PSF of step k-1 is queued behind pass 1 of step k: it runs on the GPU while the host
-        # does the equal-angle resample (all of it stays inside the timed region)
+        # the PSF of step k-1 is queued right after pass 1 of step k (all inside the timed region)
         rw.run(overlap=(lambda: run_psf(pending.pop(), timed)) if pending else None)
-        pending.append(rw.pupil(args.pupil))
+        if state["psf_done"] is not None:  # the pupil buffer is reused: wait for its last reader
+            torch.cuda.current_stream().wait_event(state["psf_done"])
+            state["psf_done"] = None
+        opd, pitch = rw.pupil(args.pupil)
+        ready = torch.cuda.Event()
+        ready.record()
+        pending.append((opd, pitch, ready))
 
     for _ in range(args.warmup):
         step(False)

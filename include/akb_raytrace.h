@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define AKB_ABI_VERSION 2
+#define AKB_ABI_VERSION 3
 
 /* status codes */
 #define AKB_OK 0
@@ -178,17 +178,43 @@ int akb_tilt_opd_f64(const double ry[9], const double rz[9], const double center
                      double* pt_rot, double* det1, double* det2, double* total1, double* total2,
                      const akb_leaf_sink* sink, void* stream);
 
+/* The tilt parameters on the device (ref :3583-3591, rotate_vectors :917-927), so nothing waits
+ * on the host between pass 2 and the tilt. From the pass-2 sink's sums / counts of (arctan(Ry/Rx),
+ * arctan(Rz/Rx), det_x, det_y, det_z) it writes d_params[23]:
+ *   [0] theta_y = -nanmean(arctan(Rz/Rx))   [1] theta_z = nanmean(arctan(Ry/Rx))
+ *   [2..10] R_y, [11..19] R_z (row-major) of rotation_matrices(-theta_y, -theta_z), formed with
+ *           correctly rounded cos / sin (glibc's differ from those on ~0.13 % of arguments)
+ *   [20..22] focus_apprx = mean(det) (np.mean)
+ * and zeroes d_extent_keys[4] (optional) and d_clear[0..n_clear) (e.g. trace flag words already
+ * copied out in stream order) for the next step. */
+int akb_tilt_params_f64(const double* d_sum5, const int64_t* d_cnt5, double* d_params, uint64_t* d_extent_keys,
+                        int32_t* d_clear, int n_clear, void* stream);
+
+/* akb_tilt_opd_f64 with R_y, R_z and the centre read from akb_tilt_params_f64's device block. */
+int akb_tilt_opd_dev_f64(const double* d_params, const double det1_ghij[4], const double det2_ghij[4],
+                         const double* dir, const double* pt, const double* opl, int64_t ld, int64_t n,
+                         double* dir_rot, double* pt_rot, double* det1, double* det2, double* total1,
+                         double* total2, const akb_leaf_sink* sink, void* stream);
+
 /* OPD maps (ref :3626, :3633, :3675-3677), with the means read from device memory as the tilt
  * sink left them (d_sum5 / d_cnt5 = sums and counts of det1_x, det1_y, det1_z, total1, total2;
  * mean = sum / count in float64):
  *   dist_err  = (total - mean_total) * 1e9
  *   sph       = ||det2 - mean_focus|| * 1e9
  *   wave      = dist_err2 - sph                                   (NULL outputs skipped)
- * d_extent_keys (optional, 4 x uint64, zero-initialised by this call): order-preserving keys of
- * max(det2_y), -min(det2_y), max(det2_z), -min(det2_z) over non-NaN rays (pupil pitch). */
+ * d_extent_keys (optional, 4 x uint64): order-preserving keys of max(det2_y), -min(det2_y),
+ * max(det2_z), -min(det2_z) over non-NaN rays (pupil pitch), zero-initialised by this call unless
+ * keys_zeroed says the caller already zeroed them in stream order (akb_tilt_params_f64 does). */
 int akb_opd_f64(const double* total1, const double* total2, const double* det2, int64_t ld, int64_t n,
                 const double* d_sum5, const int64_t* d_cnt5, double* dist_err1, double* dist_err2,
-                double* sph, double* wave, uint64_t* d_extent_keys, void* stream);
+                double* sph, double* wave, uint64_t* d_extent_keys, int keys_zeroed, void* stream);
+
+/* Host function (no device work): the equal-angle resample between the two passes (ref
+ * :2861-2870, KB_debug :11020-11030) for one axis, numpy / scipy 1.15 bit for bit:
+ *   out = interp1d(angle_sep, rand, kind='linear')(np.linspace(angle_sep[0], angle_sep[-1], n))
+ * angle_sep = np.arctan of the pass-1 exit slopes (taken by the caller with numpy), rand = the
+ * pass-1 launch angles. AKB_E_INVALID with interp1d's message when a point is out of range. */
+int akb_resample_f64(const double* angle_sep, const double* rand, int64_t n, double* out);
 
 /* Wave2 (nm) of a shard's rows sampled onto a size x size pupil in ray-index space (nearest ray,
  * index (k * (n - 1)) // (size - 1)): opd_m[ky][kx] = wave[iv - row0][ih] * 1e-9 for the pupil rows

@@ -1,0 +1,15 @@
+"""Print one bench step's kernel timeline from a rocprofv3 kernel trace (gpurun_out/prof)."""
+import csv
+import sys
+
+path = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof/run_kernel_trace.csv"
+rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
+idx = [i for i, r in enumerate(rows) if "k_chain<" in r["Kernel_Name"] and "sink" not in r["Kernel_Name"]]
+i0, i1 = idx[-3], idx[-2]
+t0 = int(rows[i0]["Start_Timestamp"])
+prev = None
+for r in rows[i0:i1 + 1]:
+    s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+    gap = (s - prev) / 1e3 if prev else 0.0
+    print(f"{(s - t0) / 1e3:8.1f} {(e - s) / 1e3:7.1f} gap {gap:6.1f} q{r['Queue_Id']} {r['Kernel_Name'][:60]}")
+    prev = max(prev or 0, e)

@@ -225,6 +225,60 @@ def test_pairwise_sum_matches_numpy(gpu, n):
             assert np.array_equal(s[r] / c[r], np.nanmean(x[r]), equal_nan=True)
 
 
+def test_pairwise_sum_short_buffer_sweep(gpu):
+    """The last, short buffer's split tree (built level by level on the device) over many tail
+    lengths, behind two full buffers and alone."""
+    from akbraytracing_amd.reduce import np_sum
+    rng = np.random.default_rng(11)
+    tails = sorted(set([1, 2, 7, 8, 9, 15, 16, 17, 127, 128, 129, 135, 136, 255, 256, 257, 263, 264, 519, 1031,
+                        2055, 4103, 4104, 8190, 8191] + list(rng.integers(1, 8192, 40))))
+    for t in tails:
+        for n in (int(t), 2 * 8192 + int(t)):
+            x = 146.0 + rng.standard_normal((2, n)) * 1e-3
+            x[1, ::7] = np.nan
+            s, c = np_sum(torch.from_numpy(x).to(gpu), nan=True)
+            s, c = s.cpu().numpy(), c.cpu().numpy()
+            assert s[0] == np.sum(x[0]) and c[0] == n, (n, s[0] - np.sum(x[0]))
+            assert s[1] == np.nansum(x[1]) and c[1] == np.count_nonzero(~np.isnan(x[1])), n
+
+
+def test_tilt_params_on_device(gpu):
+    """akb_tilt_params_f64: the means are numpy's divisions bit for bit and R_y, R_z hold the
+    correctly rounded cos / sin (numpy's glibc values may differ by one ulp, rarely)."""
+    import mpmath
+    from akbraytracing_amd import _lib, device as D
+    from akbraytracing_amd.primitives import rotation_matrices
+    L = _lib.lib()
+    rng = np.random.default_rng(3)
+    mpmath.mp.prec = 200
+    worst = 0
+    for trial in range(64):
+        cnt = rng.integers(1, 10 ** 7, 5).astype(np.int64)
+        sums = (rng.standard_normal(5) * 1e-3 * cnt).astype(np.float64)
+        sums[2:] = rng.standard_normal(3) * 100.0 * cnt[2:]
+        s_d = torch.from_numpy(sums).to(gpu)
+        c_d = torch.from_numpy(cnt).to(gpu)
+        params = torch.empty(23, dtype=torch.float64, device=gpu)
+        keys = torch.full((4,), 7, dtype=torch.int64, device=gpu)
+        flags = torch.ones(2, dtype=torch.int32, device=gpu)
+        _lib.check(L.akb_tilt_params_f64(D.ptr(s_d), D.ptr(c_d), D.ptr(params), D.ptr(keys), D.ptr(flags), 2,
+                                         D.stream_handle()))
+        p = params.cpu().numpy()
+        assert keys.cpu().numpy().tolist() == [0, 0, 0, 0] and flags.cpu().numpy().tolist() == [0, 0]
+        mean = sums / cnt
+        theta_y, theta_z = -mean[1], mean[0]
+        assert p[0] == theta_y and p[1] == theta_z
+        assert np.array_equal(p[20:23], mean[2:5])
+        ry, rz = rotation_matrices(-theta_y, -theta_z)
+        cy, sy = float(mpmath.cos(mpmath.mpf(-theta_y))), float(mpmath.sin(mpmath.mpf(-theta_y)))
+        cz, sz = float(mpmath.cos(mpmath.mpf(-theta_z))), float(mpmath.sin(mpmath.mpf(-theta_z)))
+        assert np.array_equal(p[2:11], [cy, 0, sy, 0, 1, 0, -sy, 0, cy])
+        assert np.array_equal(p[11:20], [cz, -sz, 0, sz, cz, 0, 0, 0, 1])
+        ulp = np.abs(np.concatenate([p[2:11] - ry.ravel(), p[11:20] - rz.ravel()])) / np.spacing(1.0)
+        worst = max(worst, float(ulp.max()))
+    assert worst <= 1.0
+
+
 # ----------------------------------------------------------------------------- wavefront pipeline
 
 def test_ray_wave_65_vs_reference(gpu):
