@@ -288,7 +288,7 @@ int akb_psf_f64(const double* opd, const double* amp, int ny, int nx, int pad, i
     ia.imax = d_imax;
     k_psf_inten<<<dim3(gx, gy, batch), kBlock, 0, s>>>(ia);
     if ((st = launch_status("k_psf_inten"))) return st;
-    k_psf_norm<<<dim3(grid_for(total, 4), 1, batch), kBlock, 0, s>>>(psf, (double2*)efield_re_im, d_imax, total);
+    k_psf_norm<<<dim3(grid_for(total, 1, kStreamGridCap), 1, batch), kBlock, 0, s>>>(psf, (double2*)efield_re_im, d_imax, total);
     return launch_status("k_psf_norm");
 }
 

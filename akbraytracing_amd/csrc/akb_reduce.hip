@@ -246,7 +246,19 @@ __global__ void __launch_bounds__(kPwThreads) k_pw_final(const double* __restric
     const double* p = part + (int64_t)q * part_ld;
     const long long* pc = part_cnt + (int64_t)q * part_ld;
     long long cnt = 0;
-    for (int i = tid; i < nparts; i += kPwThreads) cnt += pc[i];
+    {  // all count loads in flight at once (a latency chain otherwise)
+        constexpr int kBatch = 8;
+        for (int i0 = tid; i0 < nparts; i0 += kPwThreads * kBatch) {
+            long long c[kBatch];
+#pragma unroll
+            for (int k = 0; k < kBatch; ++k) {
+                const int i = i0 + k * kPwThreads;
+                c[k] = i < nparts ? pc[i] : 0;
+            }
+#pragma unroll
+            for (int k = 0; k < kBatch; ++k) cnt += c[k];
+        }
+    }
     {  // stage the short buffer: NaN -> 0 and the count here
         const double* a = tail + (int64_t)q * tail_ld;
         constexpr int kBatch = 8;
@@ -268,30 +280,47 @@ __global__ void __launch_bounds__(kPwThreads) k_pw_final(const double* __restric
     for (int base = 0; base == 0 || base < nparts; base += kFinalTile) {
         const int m = nparts - base < kFinalTile ? nparts - base : kFinalTile;
         if (base > 0) __syncthreads();
-        for (int i = tid; i < m; i += kPwThreads) t[i] = p[base + i];
+        {
+            constexpr int kBatch = kFinalTile / kPwThreads;  // the whole tile in one batch
+            double v[kBatch];
+#pragma unroll
+            for (int k = 0; k < kBatch; ++k) {
+                const int i = tid + k * kPwThreads;
+                v[k] = i < m ? p[base + i] : 0.0;
+            }
+#pragma unroll
+            for (int k = 0; k < kBatch; ++k) {
+                const int i = tid + k * kPwThreads;
+                if (i < m) t[i] = v[k];
+            }
+        }
         __syncthreads();
-        if (w == 0 && m > 0) {
-            double cur = lane < m ? t[lane] : 0.0;
-            int j0 = 0;
+        if (w == 0 && lane == 0 && m > 0) {
+            // one lane walks the tile in order: 16 LDS reads in flight ahead of 16 dependent adds
+            int i = 0;
             if (base == 0) {
-                acc = readlane_f64(cur, 0);
-                j0 = 1;
+                acc = t[0];
+                i = 1;
             }
-            for (int b = 0; b < m; b += 64) {
-                const double nxt = b + 64 + lane < m ? t[b + 64 + lane] : 0.0;
-                const int e = m - b < 64 ? m - b : 64;
-                if (e == 64 && j0 == 0) {  // straight-line: no branch between the dependent adds
+            double v[16], u[16];
+            if (i + 16 <= m) {
 #pragma unroll
-                    for (int j = 0; j < 64; ++j) acc = acc + readlane_f64(cur, j);
-                } else if (e == 64) {
-#pragma unroll
-                    for (int j = 1; j < 64; ++j) acc = acc + readlane_f64(cur, j);
-                } else {
-                    for (int j = j0; j < e; ++j) acc = acc + readlane_f64(cur, j);
-                }
-                j0 = 0;
-                cur = nxt;
+                for (int k = 0; k < 16; ++k) v[k] = t[i + k];
             }
+            for (; i + 32 <= m; i += 16) {
+#pragma unroll
+                for (int k = 0; k < 16; ++k) u[k] = t[i + 16 + k];
+#pragma unroll
+                for (int k = 0; k < 16; ++k) acc = acc + v[k];
+#pragma unroll
+                for (int k = 0; k < 16; ++k) v[k] = u[k];
+            }
+            if (i + 16 <= m) {
+#pragma unroll
+                for (int k = 0; k < 16; ++k) acc = acc + v[k];
+                i += 16;
+            }
+            for (; i < m; ++i) acc = acc + t[i];
         }
         if (w == 1 && base == 0 && tail_len > 0) {
             const double v = pw_tree_wave(T, tl, tail_len);

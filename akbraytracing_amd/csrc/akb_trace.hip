@@ -407,13 +407,28 @@ struct TiltArgs {
     akb_leaf_sink sink;
 };
 
-__device__ __forceinline__ void tilt_ray(const TiltArgs& a, int64_t i, double (&qv)[5]) {
+// one ray's inputs (direction, last hit, OPL), loaded ahead of the arithmetic
+struct TiltIn {
+    double d[3], p[3], o;
+};
+
+__device__ __forceinline__ void tilt_load(const TiltArgs& a, int64_t i, TiltIn& t) {
+    t.d[0] = a.dir[i];
+    t.d[1] = a.dir[a.ld + i];
+    t.d[2] = a.dir[2 * a.ld + i];
+    t.p[0] = a.pt[i];
+    t.p[1] = a.pt[a.ld + i];
+    t.p[2] = a.pt[2 * a.ld + i];
+    t.o = a.opl ? a.opl[i] : 0.0;
+}
+
+__device__ __forceinline__ void tilt_ray(const TiltArgs& a, int64_t i, const TiltIn& t, double (&qv)[5]) {
     double ax, ay, az;
     double l, m, n;
-    matvec(a.Rz, a.dir[i], a.dir[a.ld + i], a.dir[2 * a.ld + i], ax, ay, az);
+    matvec(a.Rz, t.d[0], t.d[1], t.d[2], ax, ay, az);
     matvec(a.Ry, ax, ay, az, l, m, n);
     double p, q, r;
-    matvec(a.Rz, a.pt[i] - a.c[0], a.pt[a.ld + i] - a.c[1], a.pt[2 * a.ld + i] - a.c[2], ax, ay, az);
+    matvec(a.Rz, t.p[0] - a.c[0], t.p[1] - a.c[1], t.p[2] - a.c[2], ax, ay, az);
     matvec(a.Ry, ax, ay, az, p, q, r);
     p = p + a.c[0];
     q = q + a.c[1];
@@ -428,7 +443,7 @@ __device__ __forceinline__ void tilt_ray(const TiltArgs& a, int64_t i, double (&
         a.pt_rot[a.ld + i] = q;
         a.pt_rot[2 * a.ld + i] = r;
     }
-    const double o = a.opl ? a.opl[i] : 0.0;
+    const double o = t.o;
     double x, y, z;
     plane_hit(a.d1[0], a.d1[1], a.d1[2], a.d1[3], l, m, n, p, q, r, x, y, z);
     if (a.det1) {
@@ -467,21 +482,35 @@ __device__ __forceinline__ void tilt_load_params(TiltArgs& a) {
 __global__ void __launch_bounds__(kBlock) k_tilt_opd(TiltArgs a) {
     tilt_load_params(a);
     double qv[5];
+    TiltIn t;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < a.n;
-         i += (int64_t)gridDim.x * blockDim.x)
-        tilt_ray(a, i, qv);
+         i += (int64_t)gridDim.x * blockDim.x) {
+        tilt_load(a, i, t);
+        tilt_ray(a, i, t, qv);
+    }
 }
 
+// the next segment's inputs are loaded before this segment's arithmetic and leaf sums, so each
+// wave keeps its loads in flight across the sink's barriers
 __global__ void __launch_bounds__(kBlock) k_tilt_opd_sink(TiltArgs a) {
     tilt_load_params(a);
     __shared__ LeafLds<5> L;
     const int64_t nseg = (a.n + kLeafSeg - 1) / kLeafSeg;
-    for (int64_t seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
+    int64_t seg = blockIdx.x;
+    TiltIn cur{}, nxt{};
+    {
+        const int64_t i = seg * kLeafSeg + threadIdx.x;
+        if (seg < nseg && i < a.n) tilt_load(a, i, cur);
+    }
+    for (; seg < nseg; seg += gridDim.x) {
         const int64_t i = seg * kLeafSeg + threadIdx.x;
         const bool valid = i < a.n;
+        const int64_t j = (seg + gridDim.x) * kLeafSeg + threadIdx.x;
+        if (seg + gridDim.x < nseg && j < a.n) tilt_load(a, j, nxt);
         double qv[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-        if (valid) tilt_ray(a, i, qv);
+        if (valid) tilt_ray(a, i, cur, qv);
         leaf_sink_segment<5>(a.sink, L, seg * kLeafSeg, qv, valid);
+        cur = nxt;
     }
 }
 
@@ -550,7 +579,10 @@ __global__ void __launch_bounds__(kBlock) k_opd(OpdArgs a) {
         if (threadIdx.x < 4) {
             double v = wext[0][threadIdx.x];
             for (int w = 1; w < kBlock / 64; ++w) v = fmax(v, wext[w][threadIdx.x]);
-            atomicMax(a.ext + threadIdx.x, order_key(v));
+            const unsigned long long k = order_key(v);
+            // most workgroups hold no new extreme: skip their atomic (the max stays exact)
+            if (k > __hip_atomic_load(a.ext + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                atomicMax(a.ext + threadIdx.x, k);
         }
     }
 }
@@ -595,6 +627,27 @@ static int chain_waves() {
     return w;
 }
 
+// workgroups per chain launch (each walks 256-ray segments grid-stride); AKB_CHAIN_GRID in the
+// environment overrides the default for A/B timing
+static int64_t chain_grid_cap() {
+    static int64_t g = [] {
+        const char* e = getenv("AKB_CHAIN_GRID");
+        const long long v = e ? atoll(e) : 0;
+        return (int64_t)(v >= 256 ? v : 256 * 32);  // 8192: measured best for both passes
+    }();
+    return g;
+}
+
+// workgroup cap of the OPD kernel (AKB_OPD_GRID overrides, for A/B timing)
+static int64_t opd_grid_cap() {
+    static int64_t g = [] {
+        const char* e = getenv("AKB_OPD_GRID");
+        const long long v = e ? atoll(e) : 0;
+        return (int64_t)(v >= 256 ? v : 2048);  // measured best: the extent atomics grow with the grid
+    }();
+    return g;
+}
+
 template <bool kGrid, bool kOPL, bool kSink>
 static void launch_chain(int w, unsigned g, hipStream_t s, const ChainArgs& a) {
 #define AKB_CHAIN_CASE(W)                                                        \
@@ -632,7 +685,7 @@ int akb_isect_f64(const double coeffs[10], const double* dir, int64_t dir_ld, in
     AKB_REQUIRE(coeffs && dir && org && out && flags, "null pointer");
     AKB_REQUIRE(n >= 0, "n < 0");
     if (n == 0) return AKB_OK;
-    k_isect<<<grid_for(n), kBlock, 0, (hipStream_t)stream>>>(
+    k_isect<<<grid_for(n, 1, kStreamGridCap), kBlock, 0, (hipStream_t)stream>>>(
         quadric_from(coeffs), v3in(dir, dir_ld, dir_inc), v3in(org, org_ld, org_inc), negative, n,
         V3Out{out, out_ld}, flags);
     return launch_status("k_isect");
@@ -644,7 +697,7 @@ int akb_normal_f64(const double coeffs[10], const double* pt, int64_t pt_ld, int
     AKB_REQUIRE(coeffs && pt && out && flags, "null pointer");
     AKB_REQUIRE(n >= 0, "n < 0");
     if (n == 0) return AKB_OK;
-    k_normal<<<grid_for(n), kBlock, 0, (hipStream_t)stream>>>(
+    k_normal<<<grid_for(n, 1, kStreamGridCap), kBlock, 0, (hipStream_t)stream>>>(
         quadric_from(coeffs), v3in(pt, pt_ld, pt_inc), n, V3Out{out, out_ld}, normalize, flags);
     return launch_status("k_normal");
 }
@@ -656,7 +709,7 @@ int akb_reflect_f64(const double* dir, int64_t dir_ld, int64_t dir_inc, const do
     AKB_REQUIRE(dir && nrm && out && flags, "null pointer");
     AKB_REQUIRE(n >= 0, "n < 0");
     if (n == 0) return AKB_OK;
-    k_reflect<<<grid_for(n), kBlock, 0, (hipStream_t)stream>>>(
+    k_reflect<<<grid_for(n, 1, kStreamGridCap), kBlock, 0, (hipStream_t)stream>>>(
         v3in(dir, dir_ld, dir_inc), v3in(nrm, nrm_ld, nrm_inc), n, V3Out{out, out_ld}, normalize,
         flags);
     return launch_status("k_reflect");
@@ -668,7 +721,7 @@ int akb_normalize_f64(const double* v, int64_t v_ld, int64_t v_inc, int64_t n, d
     AKB_REQUIRE(v && out && flags, "null pointer");
     AKB_REQUIRE(n >= 0, "n < 0");
     if (n == 0) return AKB_OK;
-    k_normalize<<<grid_for(n), kBlock, 0, (hipStream_t)stream>>>(v3in(v, v_ld, v_inc), n,
+    k_normalize<<<grid_for(n, 1, kStreamGridCap), kBlock, 0, (hipStream_t)stream>>>(v3in(v, v_ld, v_inc), n,
                                                                  V3Out{out, out_ld}, flags);
     return launch_status("k_normalize");
 }
@@ -680,7 +733,7 @@ int akb_plane_isect_f64(const double ghij[4], const double* dir, int64_t dir_ld,
     AKB_REQUIRE(ghij && dir && org && out, "null pointer");
     AKB_REQUIRE(n >= 0, "n < 0");
     if (n == 0) return AKB_OK;
-    k_plane<<<grid_for(n), kBlock, 0, (hipStream_t)stream>>>(
+    k_plane<<<grid_for(n, 1, kStreamGridCap), kBlock, 0, (hipStream_t)stream>>>(
         ghij[0], ghij[1], ghij[2], ghij[3], v3in(dir, dir_ld, dir_inc), v3in(org, org_ld, org_inc), n,
         V3Out{out, out_ld});
     return launch_status("k_plane");
@@ -692,7 +745,7 @@ int akb_seglen_f64(const double* a, int64_t a_ld, int64_t a_inc, const double* b
     AKB_REQUIRE(a && b && out, "null pointer");
     AKB_REQUIRE(n >= 0, "n < 0");
     if (n == 0) return AKB_OK;
-    k_seglen<<<grid_for(n), kBlock, 0, (hipStream_t)stream>>>(v3in(a, a_ld, a_inc),
+    k_seglen<<<grid_for(n, 1, kStreamGridCap), kBlock, 0, (hipStream_t)stream>>>(v3in(a, a_ld, a_inc),
                                                               v3in(b, b_ld, b_inc), n, out);
     return launch_status("k_seglen");
 }
@@ -709,7 +762,7 @@ int akb_rotate_f64(const double ry[9], const double rz[9], const double center[3
         Rz.m[k] = rz[k];
     }
     const int shift = center != nullptr;
-    k_rotate<<<grid_for(n), kBlock, 0, (hipStream_t)stream>>>(
+    k_rotate<<<grid_for(n, 1, kStreamGridCap), kBlock, 0, (hipStream_t)stream>>>(
         Ry, Rz, shift ? center[0] : 0.0, shift ? center[1] : 0.0, shift ? center[2] : 0.0, shift,
         v3in(v, v_ld, v_inc), n, V3Out{out, out_ld});
     return launch_status("k_rotate");
@@ -719,7 +772,7 @@ int akb_fill_nan_f64(double* out, int64_t ld, int rows, int64_t n, void* stream)
     clear_error();
     AKB_REQUIRE(out && rows >= 0 && n >= 0, "bad fill arguments");
     if (n == 0 || rows == 0) return AKB_OK;
-    k_fill_nan<<<grid_for(n), kBlock, 0, (hipStream_t)stream>>>(out, ld, rows, n);
+    k_fill_nan<<<grid_for(n, 1, kStreamGridCap), kBlock, 0, (hipStream_t)stream>>>(out, ld, rows, n);
     return launch_status("k_fill_nan");
 }
 
@@ -808,11 +861,12 @@ int akb_trace_chain_f64(const akb_chain_desc* d, void* stream) {
     a.flags = d->flags;
     a.sink = d->sink;
     hipStream_t s = (hipStream_t)stream;
-    const unsigned gsz = grid_for(d->n_rays);
+    const int64_t gcap = chain_grid_cap();
+    const unsigned gsz = grid_for(d->n_rays, 1, gcap);
     const int w = chain_waves();
     if (sink) {
         const int64_t nseg = (d->n_rays + kLeafSeg - 1) / kLeafSeg;
-        const unsigned gs = (unsigned)(nseg < 256 * 8 ? nseg : 256 * 8);
+        const unsigned gs = (unsigned)(nseg < gcap ? nseg : gcap);
         if (grid && d->opl)
             launch_chain<true, true, true>(w, gs, s, a);
         else if (grid)
@@ -866,11 +920,11 @@ static int launch_tilt(TiltArgs& a, const double det1_ghij[4], const double det2
     if (use_sink) {
         a.sink = *sink;
         const int64_t nseg = (n + kLeafSeg - 1) / kLeafSeg;
-        const unsigned gs = (unsigned)(nseg < 256 * 8 ? nseg : 256 * 8);
+        const unsigned gs = (unsigned)(nseg < kStreamGridCap ? nseg : kStreamGridCap);
         k_tilt_opd_sink<<<gs, kBlock, 0, (hipStream_t)stream>>>(a);
         return launch_status("k_tilt_opd_sink");
     }
-    k_tilt_opd<<<grid_for(n), kBlock, 0, (hipStream_t)stream>>>(a);
+    k_tilt_opd<<<grid_for(n, 1, kStreamGridCap), kBlock, 0, (hipStream_t)stream>>>(a);
     return launch_status("k_tilt_opd");
 }
 
@@ -937,8 +991,7 @@ int akb_opd_f64(const double* total1, const double* total2, const double* det2, 
     a.sph = sph;
     a.wave = wave;
     a.ext = (unsigned long long*)d_extent_keys;
-    const unsigned g = grid_for(n, 4) < 1024 ? grid_for(n, 4) : 1024;  // <= 4096 extent atomics
-    k_opd<<<g, kBlock, 0, s>>>(a);
+    k_opd<<<grid_for(n, 1, opd_grid_cap()), kBlock, 0, s>>>(a);
     return launch_status("k_opd");
 }
 

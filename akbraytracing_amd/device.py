@@ -23,6 +23,9 @@ def device():
 
 
 def stream_handle(stream=None):
+    """hipStream_t of a torch stream (default: the current one); a handle passes through."""
+    if isinstance(stream, ctypes.c_void_p):
+        return stream
     s = stream if stream is not None else torch.cuda.current_stream()
     return ctypes.c_void_p(s.cuda_stream)
 

@@ -230,9 +230,9 @@ class RayWave:
         return self._p2[key]
 
     # -------------------------------------------------------------- passes
-    def _pass1(self, overlap=None):
+    def _pass1(self, overlap=None, stream=None):
         hb, he, col = self._plan
-        self._p1.launch(reset_flags=False)
+        self._p1.launch(stream=stream, reset_flags=False)
         x = self._x1_host
         x.copy_(self._x1, non_blocking=True)
         ev = torch.cuda.Event()
@@ -253,12 +253,12 @@ class RayWave:
             samp_h, samp_v = host[:nh], host[nh:self._nsamp]
         return samp_h, samp_v, flags
 
-    def _pass2(self, want_rows=False):
+    def _pass2(self, want_rows=False, stream=None):
         ev = None
         if self.kernel_events is not None:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
-        r = self._pass2_launch(want_rows).launch(reset_flags=False)
+        r = self._pass2_launch(want_rows).launch(stream=stream, reset_flags=False)
         if ev is not None:
             ev[1].record()
             self.kernel_events.append(ev)
@@ -290,7 +290,7 @@ class RayWave:
         runs while the host performs the resample."""
         L = _lib.lib()
         stream = D.stream_handle()
-        samp_h, samp_v, flags1 = self._pass1(overlap)
+        samp_h, samp_v, flags1 = self._pass1(overlap, stream)
         if flags1:
             self._flags.zero_()
             raise _lib.AKBError(
@@ -306,13 +306,13 @@ class RayWave:
             np.tan(self.rand_v, out=th[self.n:])
         self._tan2.copy_(self._tan2_host, non_blocking=True)
         tan_h2, tan_v2 = self._tan2[:self.n], self._tan2[self.n:]
-        r = self._pass2(want_rows=full)
+        r = self._pass2(want_rows=full, stream=stream)
         if self.comm.world > 1:
             self.comm.allreduce_sums(self._flags[1:2])
         self._f_host.copy_(self._flags, non_blocking=True)
         ev2 = torch.cuda.Event()
         ev2.record()
-        sums, cnts = self.sink2.finish()
+        sums, cnts = self.sink2.finish(stream)
         if self.comm.world > 1:  # cross-rank means: partial sums added over ranks (not numpy order)
             self.comm.allreduce_sums(sums)
             self.comm.allreduce_sums(cnts)
@@ -323,7 +323,7 @@ class RayWave:
         if full:
             out.update(det_pre=r.det, atan=r.atan)
         if opd:
-            out.update(self._tilt_opd(r.last_hit, r.dir_out, r.opl, keep_rotated, full))
+            out.update(self._tilt_opd(r.last_hit, r.dir_out, r.opl, keep_rotated, full, stream=stream))
         ev2.synchronize()
         flags2 = int(self._f_host[1])
         if flags2:
@@ -354,11 +354,11 @@ class RayWave:
             out.update(self._tilt_opd(last_hit, dir_out, opl, keep_rotated, full, host_tilt=(ry, rz, focus)))
         return out
 
-    def _tilt_opd(self, last_hit, dir_out, opl, keep_rotated=False, full=False, host_tilt=None):
+    def _tilt_opd(self, last_hit, dir_out, opl, keep_rotated=False, full=False, host_tilt=None, stream=None):
         L = _lib.lib()
         n = self.n_local
         dev = self.dev
-        stream = D.stream_handle()
+        stream = D.stream_handle(stream)
         two = self.g.det2 is not None
         det1 = torch.empty((3, n), dtype=D.F64, device=dev) if (full or not two) else None
         det2 = torch.empty((3, n), dtype=D.F64, device=dev) if two else None
@@ -376,7 +376,7 @@ class RayWave:
             ry, rz, focus = host_tilt
             _lib.check(L.akb_tilt_opd_f64(D.host_f64(ry.ravel()), D.host_f64(rz.ravel()), D.host_f64(focus),
                                           D.host_f64(self.g.det1), D.host_f64(d2), *outs))
-        sums, cnts = self.sink3.finish()
+        sums, cnts = self.sink3.finish(stream)
         if self.comm.world > 1:
             self.comm.allreduce_sums(sums)
             self.comm.allreduce_sums(cnts)

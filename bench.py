@@ -45,6 +45,9 @@ def parse():
     p.add_argument("--pad", type=int, default=16)
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--psf-start", choices=("pupil", "pass1"), default="pupil",
+                   help="side-stream PSF starts as soon as the previous pupil is ready, beside pass 1 "
+                        "(default; measured faster), or after this step's pass 1")
     return p.parse_args()
 
 
@@ -118,6 +121,10 @@ def main():
         if rank != 0:
             return
         side.wait_event(ready)
+        if args.psf_start == "pass1":  # called right after pass 1 and its copy were queued
+            after = torch.cuda.Event()
+            after.record()
+            side.wait_event(after)
         with torch.cuda.stream(side):
             if timed:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

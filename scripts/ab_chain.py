@@ -1,6 +1,7 @@
-"""A/B timing of the chain kernel variants (AKB_CHAIN_WAVES) on the bench geometry: pass-1 and
-pass-2 launches timed with HIP events, median of N launches. One variant per process (the variant
-is read once per process), all on the same GPU. Usage: python scripts/ab_chain.py [n] [reps]"""
+"""A/B timing of the chain kernel variants (AKB_CHAIN_WAVES occupancy, AKB_CHAIN_GRID workgroups)
+on the bench geometry: pass-1 and pass-2 launches timed with HIP events, median of N launches. One
+variant per process (variants are read once per process), all on the same GPU.
+Usage: python scripts/ab_chain.py [n] [reps] [waves|grid]"""
 import json
 import os
 import subprocess
@@ -27,7 +28,8 @@ def child(n, reps):
             b.record()
             b.synchronize()
             acc.append(a.elapsed_time(b))
-    print(json.dumps({"w": os.environ.get("AKB_CHAIN_WAVES", "4"), "pass1_ms": float(np.median(t1)),
+    print(json.dumps({"w": os.environ.get("AKB_CHAIN_WAVES", "4"), "grid": os.environ.get("AKB_CHAIN_GRID", "2048"),
+                      "pass1_ms": float(np.median(t1)),
                       "pass2_ms": float(np.median(t2)), "pass1_min": min(t1), "pass2_min": min(t2)}))
 
 
@@ -37,9 +39,12 @@ if __name__ == "__main__":
         sys.exit(0)
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 3163
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+    what = sys.argv[3] if len(sys.argv) > 3 else "waves"
+    variants = ([{"AKB_CHAIN_WAVES": str(w)} for w in (4, 2, 5, 6, 8)] if what == "waves" else
+                [{"AKB_CHAIN_GRID": str(g)} for g in (2048, 1024, 4096, 8192, 16384, 40000)])
     for rnd in range(2):
-        for w in (4, 2, 5, 6, 8):
-            env = dict(os.environ, AKB_CHAIN_WAVES=str(w))
+        for v in variants:
+            env = dict(os.environ, **v)
             r = subprocess.run([sys.executable, __file__, str(n), str(reps), "child"], env=env, capture_output=True,
                                text=True, timeout=300)
             print(r.stdout.strip() or r.stderr[-500:], flush=True)
