@@ -92,8 +92,11 @@ __global__ void __launch_bounds__(kBlock) k_psf_pupil(PsfPupilArgs a) {
 
 __device__ __forceinline__ void atomic_max_nonneg(double* addr, double v) {
     // non-negative doubles order like their bit patterns; NaN (0x7ff8...) orders above +inf,
-    // which reproduces numpy's NaN-propagating max
-    atomicMax((unsigned long long*)addr, (unsigned long long)__double_as_longlong(v));
+    // which reproduces numpy's NaN-propagating max. Thousands of workgroups meet on one word:
+    // only those holding a new maximum issue the atomic (a handful), the rest read and skip.
+    unsigned long long* a = (unsigned long long*)addr;
+    const unsigned long long k = (unsigned long long)__double_as_longlong(v);
+    if (k > __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(a, k);
 }
 
 struct PsfIntenArgs {
@@ -166,6 +169,355 @@ __global__ void __launch_bounds__(kBlock) k_psf_norm(double* psf, double2* efiel
     }
 }
 
+// ---- pruned transform: the padded plane is never built ----
+//
+// The padded field is zero outside the ey x ex pupil block, so with centred indices
+// a' = a - ey/2, b' = b - ex/2 and output indices ko, lo of the fftshift-ed plane
+//   F[ko][lo] = (-1)^((ey+ex)/2) e^{i pi ko/pad} e^{i pi lo/pad}
+//               * sum_a (-1)^a sum_b (-1)^b U0[a][b] W_px^(lo b) W_py^(ko a)
+// and with lo = pad j + r the inner sum is an ex-point DFT of U0[a][b] (-1)^b W_px^(r b) at j
+// (likewise for the columns). Rows pass: ey x pad FFTs of length ex -> H (ey x px, 4 MiB for a
+// 128^2 pupil at pad 16); column pass: px x pad FFTs of length ey, straight to |F dA|^2. The
+// column pass runs twice (peak, then the normalised write) instead of writing the unnormalised
+// plane and re-reading it: the only HBM traffic is the output itself. Each FFT is a four-step
+// split N = N1 N2 into in-register DFTs and one LDS exchange, twiddles of the pad split from a
+// W_P table in device memory.
+// Taken when ey and ex are powers of two in [8, 256]; rocFFT on the full plane otherwise.
+constexpr int kFftTile = 2048;  // complex points per workgroup
+
+__device__ __forceinline__ double2 cmul(double2 a, double2 b) {
+    return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+
+__global__ void __launch_bounds__(kBlock) k_psf_twiddle(double2* W, int P) {
+    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < P; t += gridDim.x * blockDim.x) {
+        double sn, cs;
+        sincospi(2.0 * (double)t / (double)P, &sn, &cs);
+        W[t] = make_double2(cs, -sn);  // exp(-2 pi i t / P)
+    }
+}
+
+// exp(-2 pi i k / 32), k < 16 (W_M^k = W_32^(k 32 / M) for M <= 32)
+constexpr double kW32re[16] = {0x1.0000000000000p+0,  0x1.f6297cff75cb0p-1,  0x1.d906bcf328d46p-1,
+                               0x1.a9b66290ea1a3p-1,  0x1.6a09e667f3bcdp-1,  0x1.1c73b39ae68c8p-1,
+                               0x1.87de2a6aea963p-2,  0x1.8f8b83c69a60bp-3,  0.0,
+                               -0x1.8f8b83c69a60bp-3, -0x1.87de2a6aea963p-2, -0x1.1c73b39ae68c8p-1,
+                               -0x1.6a09e667f3bcdp-1, -0x1.a9b66290ea1a3p-1, -0x1.d906bcf328d46p-1,
+                               -0x1.f6297cff75cb0p-1};
+constexpr double kW32im[16] = {0.0,                   -0x1.8f8b83c69a60bp-3, -0x1.87de2a6aea963p-2,
+                               -0x1.1c73b39ae68c8p-1, -0x1.6a09e667f3bcdp-1, -0x1.a9b66290ea1a3p-1,
+                               -0x1.d906bcf328d46p-1, -0x1.f6297cff75cb0p-1, -0x1.0000000000000p+0,
+                               -0x1.f6297cff75cb0p-1, -0x1.d906bcf328d46p-1, -0x1.a9b66290ea1a3p-1,
+                               -0x1.6a09e667f3bcdp-1, -0x1.1c73b39ae68c8p-1, -0x1.87de2a6aea963p-2,
+                               -0x1.8f8b83c69a60bp-3};
+
+constexpr int ilog2_c(int m) { return m <= 1 ? 0 : 1 + ilog2_c(m / 2); }
+constexpr int bitrev_c(int i, int bits) {
+    int r = 0;
+    for (int k = 0; k < bits; ++k) r |= ((i >> k) & 1) << (bits - 1 - k);
+    return r;
+}
+
+// in-register DFT of size M (power of two <= 32): v holds x[bitrev(i)] at i on entry (the caller
+// loads in that order) and X[k] at k on exit; radix-2 DIT, every index and twiddle resolved at
+// compile time, in place
+template <int M>
+__device__ __forceinline__ void dft_reg_br(double2 (&t)[M]) {
+#pragma unroll
+    for (int h = 1; h < M; h <<= 1) {  // half-length of the current butterflies
+#pragma unroll
+        for (int i = 0; i < M; i += 2 * h) {
+#pragma unroll
+            for (int k = 0; k < h; ++k) {
+                const double2 x = t[i + k];
+                double2 y = t[i + k + h];
+                if (k != 0) {
+                    if (2 * k == h) {
+                        y = make_double2(y.y, -y.x);  // * W^(len/4) = -i
+                    } else {
+                        const int wi = k * (16 / h);
+                        y = cmul(y, make_double2(kW32re[wi], kW32im[wi]));
+                    }
+                }
+                t[i + k] = make_double2(x.x + y.x, x.y + y.y);
+                t[i + k + h] = make_double2(x.x - y.x, x.y - y.y);
+            }
+        }
+    }
+}
+
+// C transforms of length N = N1 N2 per workgroup (C * N2 threads, column c fastest):
+//   step 1: thread (c, n2) takes x[n1 N2 + n2], n1 < N1, an N1-point DFT in registers, twiddle
+//           W_N^(n2 k1); LDS exchange
+//   step 2: thread (c, t2) runs the N2-point DFTs of k1 = t2 + s N2, giving X[k1 + N1 k2]
+// load(c, a) supplies input element a of transform c; store(c, j, value) consumes output j.
+template <int N>
+struct FftShape {
+    static constexpr int L = ilog2_c(N);
+    static constexpr int N1 = 1 << ((L + 1) / 2);
+    static constexpr int N2 = N / N1;
+    static constexpr int C0 = kFftTile / N < kBlock / N2 ? kFftTile / N : kBlock / N2;
+};
+
+template <int N, typename Load, typename Store>
+__device__ __forceinline__ void fft_block(int C, double2* Y, const double2* twN, Load load, Store store) {
+    constexpr int N1 = FftShape<N>::N1, N2 = FftShape<N>::N2;
+    constexpr int L1 = ilog2_c(N1), L2 = ilog2_c(N2);
+    const int tid = threadIdx.x;
+    const int c = tid % C, n2 = tid / C;
+    {
+        double2 v[N1];
+#pragma unroll
+        for (int i = 0; i < N1; ++i) v[i] = load(c, bitrev_c(i, L1) * N2 + n2);
+        dft_reg_br<N1>(v);
+#pragma unroll
+        for (int k1 = 0; k1 < N1; ++k1) {
+            const double2 w = k1 && n2 ? cmul(v[k1], twN[(n2 * k1) % N]) : v[k1];
+            Y[(k1 * N2 + n2) * C + c] = w;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < N1 / N2; ++s) {
+        const int k1 = n2 + s * N2;
+        double2 w[N2];
+#pragma unroll
+        for (int i = 0; i < N2; ++i) w[i] = Y[(k1 * N2 + bitrev_c(i, L2)) * C + c];
+        dft_reg_br<N2>(w);
+#pragma unroll
+        for (int k2 = 0; k2 < N2; ++k2) store(c, k1 + N1 * k2, w[k2]);
+    }
+}
+
+struct PsfFastArgs {
+    const double* opd;
+    const double* amp;
+    const double* wy;
+    const double* wx;
+    double wmax;
+    PsfGeom g;
+    double kphase[8];
+    const double2* Wx;  // W_px table
+    const double2* Wy;  // W_py table
+    double2* H;         // (batch, ey, px)
+    double dA;
+    const double* pitch;
+    double* psf;
+    double2* efield;
+    double* imax;
+};
+
+// row pass: workgroup (row a, chunk of r, batch) -> H[b][a][pad j + r], N = ex
+template <int N>
+__global__ void __launch_bounds__(kBlock) k_psf_rows(PsfFastArgs A) {
+    constexpr int C0 = FftShape<N>::C0;
+    __shared__ double2 Y[C0 * N];
+    __shared__ double2 u[N];
+    __shared__ double2 tw[N];
+    const PsfGeom g = A.g;
+    const int a = blockIdx.x, b = blockIdx.z;
+    const int pad = g.px / N;
+    const int r0 = blockIdx.y * C0;
+    if (a == 0 && blockIdx.y == 0 && threadIdx.x == 0) A.imax[b] = 0.0;  // column passes follow
+    for (int m = threadIdx.x; m < N; m += blockDim.x) {
+        tw[m] = A.Wx[(int64_t)m * pad];
+        // pupil row a with (-1)^col folded in (rows / cols past ny, nx: the even-size zero pad)
+        double re = 0.0, im = 0.0;
+        if (a < g.ny && m < g.nx) {
+            const int64_t pi = (int64_t)a * g.nx + m;
+            double o = A.opd[pi];
+            double amp = A.amp ? A.amp[pi] : (isfinite(o) ? 1.0 : 0.0);
+            if (!isfinite(amp)) amp = 0.0;
+            if (!isfinite(o)) o = 0.0;
+            double sn, cs;
+            sincos(A.kphase[b] * o, &sn, &cs);
+            re = amp * cs - 0.0 * sn;
+            im = amp * sn + 0.0 * cs;
+            if (A.wy) {
+                const double w = (A.wy[a] * A.wx[m]) / A.wmax;
+                const double x0 = re, y0 = im;
+                re = x0 * w - y0 * 0.0;
+                im = x0 * 0.0 + y0 * w;
+            }
+        }
+        if (m & 1) {
+            re = -re;
+            im = -im;
+        }
+        u[m] = make_double2(re, im);
+    }
+    __syncthreads();
+    double2* Hrow = A.H + ((int64_t)b * g.ny2 + a) * g.px;
+    fft_block<N>(
+        C0, Y, tw,
+        [&](int c, int m) {
+            const int r = r0 + c;
+            return r < pad ? cmul(u[m], A.Wx[r * m]) : make_double2(0.0, 0.0);
+        },
+        [&](int c, int j, double2 v) {
+            const int r = r0 + c;
+            if (r < pad) Hrow[(int64_t)pad * j + r] = v;
+        });
+}
+
+__device__ __forceinline__ double dmax_nan(double m, double v) { return (v > m || v != v) ? v : m; }
+
+// column pass: workgroup (column tile, r, batch), N = ey; kWrite = false: the peak only;
+// true: normalised intensity (and efield) at rows ko = pad j + r of the tile's columns
+template <int N, bool kWrite>
+__global__ void __launch_bounds__(kBlock) k_psf_cols(PsfFastArgs A, int C) {
+    constexpr int C0 = FftShape<N>::C0;
+    __shared__ double2 Y[C0 * N];
+    __shared__ double2 tw[N];
+    __shared__ double2 twr[N];  // (-1)^a W_py^(r a), the input twiddle of this workgroup's r
+    __shared__ double wm[kBlock / 64];
+    const PsfGeom g = A.g;
+    const int pad = g.py / N;
+    const int l0 = blockIdx.x * C, r = blockIdx.y, b = blockIdx.z;
+    for (int m = threadIdx.x; m < N; m += blockDim.x) {
+        tw[m] = A.Wy[(int64_t)m * pad];
+        const double2 w = A.Wy[r * m];
+        twr[m] = (m & 1) ? make_double2(-w.x, -w.y) : w;
+    }
+    __syncthreads();
+    const double2* Hb = A.H + (int64_t)b * N * g.px;
+    const double dA = A.pitch ? A.pitch[0] * A.pitch[1] : A.dA;
+    const double sgn = ((N / 2 + g.nx2 / 2) & 1) ? -1.0 : 1.0;
+    // |F dA|^2 does not need the unit-modulus phase factors: the peak and the write pass both
+    // take it from the raw transform; only the efield gets the phases and the sign
+    double scale = 1.0, sq = 1.0;
+    if (kWrite) {
+        const double imx = A.imax[b];
+        scale = imx > 0.0 ? 1.0 / imx : 1.0;
+        sq = sqrt(imx > 0.0 ? imx : 1.0);
+    }
+    double* P = A.psf + (int64_t)b * g.py * g.px;
+    double2* E = A.efield ? A.efield + (int64_t)b * g.py * g.px : nullptr;
+    double m = 0.0;
+    fft_block<N>(
+        C, Y, tw,
+        [&](int c, int a) { return cmul(Hb[(int64_t)a * g.px + l0 + c], twr[a]); },
+        [&](int c, int j, double2 f) {
+            const int ko = pad * j + r, lo = l0 + c;
+            const double re = f.x * dA, im = f.y * dA;
+            const double I = re * re + im * im;
+            if (kWrite) {
+                const int64_t idx = (int64_t)ko * g.px + lo;
+                P[idx] = I * scale;
+                if (E) {
+                    // e^{i pi ko / pad} = conj(W_py^(ko ey / 2)), likewise for lo; then the sign
+                    const double2 py_ph = A.Wy[((int64_t)ko * (N / 2)) % g.py];
+                    const double2 px_ph = A.Wx[((int64_t)lo * (g.nx2 / 2)) % g.px];
+                    double2 e = cmul(make_double2(re, im), make_double2(py_ph.x, -py_ph.y));
+                    e = cmul(e, make_double2(px_ph.x, -px_ph.y));
+                    E[idx] = make_double2(sgn * e.x / sq, sgn * e.y / sq);
+                }
+            } else {
+                m = dmax_nan(m, I);
+            }
+        });
+    if (!kWrite) {
+        for (int off = 32; off > 0; off >>= 1) m = dmax_nan(m, __shfl_down(m, off));
+        if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int w = 1; w < (int)(blockDim.x + 63) / 64; ++w) m = dmax_nan(m, wm[w]);
+            atomic_max_nonneg(A.imax + b, m);
+        }
+    }
+}
+
+template <int N>
+static int launch_psf_rows(const PsfFastArgs& fa, int batch, hipStream_t s) {
+    constexpr int C0 = FftShape<N>::C0;
+    const int pad = fa.g.px / N;
+    k_psf_rows<N><<<dim3(fa.g.ny2, (pad + C0 - 1) / C0, batch), C0 * FftShape<N>::N2, 0, s>>>(fa);
+    return launch_status("k_psf_rows");
+}
+
+template <int N>
+static int launch_psf_cols(const PsfFastArgs& fa, int batch, hipStream_t s) {
+    constexpr int C0 = FftShape<N>::C0;
+    const int C = C0 < fa.g.nx2 ? C0 : fa.g.nx2;
+    const dim3 grid(fa.g.px / C, fa.g.py / N, batch);
+    const unsigned threads = C * FftShape<N>::N2;
+    k_psf_cols<N, false><<<grid, threads, 0, s>>>(fa, C);
+    int st = launch_status("k_psf_cols(peak)");
+    if (st) return st;
+    k_psf_cols<N, true><<<grid, threads, 0, s>>>(fa, C);
+    return launch_status("k_psf_cols");
+}
+
+#define AKB_PSF_SIZES(X) X(8) X(16) X(32) X(64) X(128) X(256)
+
+static int psf_rows_dispatch(int n, const PsfFastArgs& fa, int batch, hipStream_t s) {
+    switch (n) {
+#define AKB_CASE(N) \
+    case N:         \
+        return launch_psf_rows<N>(fa, batch, s);
+        AKB_PSF_SIZES(AKB_CASE)
+#undef AKB_CASE
+    }
+    set_error("pruned PSF: unsupported row length %d", n);
+    return AKB_E_INVALID;
+}
+
+static int psf_cols_dispatch(int n, const PsfFastArgs& fa, int batch, hipStream_t s) {
+    switch (n) {
+#define AKB_CASE(N) \
+    case N:         \
+        return launch_psf_cols<N>(fa, batch, s);
+        AKB_PSF_SIZES(AKB_CASE)
+#undef AKB_CASE
+    }
+    set_error("pruned PSF: unsupported column length %d", n);
+    return AKB_E_INVALID;
+}
+
+static int ilog2_exact(int v) {
+    if (v <= 0 || (v & (v - 1))) return -1;
+    int l = 0;
+    while ((1 << l) < v) ++l;
+    return l;
+}
+
+static bool psf_fast_ok(const PsfGeom& g) {
+    if (getenv("AKB_PSF_ROCFFT")) return false;
+    const int ly = ilog2_exact(g.ny2), lx = ilog2_exact(g.nx2);
+    // up to 256: larger transforms hold 32-point register DFTs at one wave per SIMD and lose to
+    // rocFFT on the full plane (measured: 1024^2 pupil, pad 2: 193 vs 151 us)
+    return ly >= 3 && ly <= 8 && lx >= 3 && lx <= 8 && (int64_t)g.py * g.px < (1LL << 31);
+}
+
+static int64_t psf_fast_bytes(const PsfGeom& g, int batch) {
+    return ((int64_t)batch * g.ny2 * g.px * 16 + 255) / 256 * 256;
+}
+
+// W_P tables, built once per (device, P) and kept by the library (freed by akb_psf_release_plans)
+static std::mutex g_tw_mu;
+static std::map<std::pair<int, int>, double2*> g_tw;
+
+static int get_twiddles(int P, hipStream_t s, const double2** out) {
+    int dev = 0;
+    AKB_HIP_CHECK(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(g_tw_mu);
+    auto key = std::make_pair(dev, P);
+    auto it = g_tw.find(key);
+    if (it != g_tw.end()) {
+        *out = it->second;
+        return AKB_OK;
+    }
+    double2* W = nullptr;
+    AKB_HIP_CHECK(hipMalloc(&W, (size_t)P * sizeof(double2)));
+    k_psf_twiddle<<<(P + kBlock - 1) / kBlock, kBlock, 0, s>>>(W, P);
+    int st = launch_status("k_psf_twiddle");
+    if (st) return st;
+    AKB_HIP_CHECK(hipStreamSynchronize(s));  // other streams may use the table right away
+    g_tw[key] = W;
+    *out = W;
+    return AKB_OK;
+}
+
 // ---- rocFFT plan cache (thread-safe; the reference's _multi pattern runs one thread per GPU) ----
 
 struct PlanEntry {
@@ -222,6 +574,7 @@ extern "C" {
 int64_t akb_psf_work_bytes(int ny, int nx, int pad, int batch) {
     if (ny <= 0 || nx <= 0 || pad < 1 || batch < 1) return -1;
     const PsfGeom g = psf_geom(ny, nx, pad);
+    if (psf_fast_ok(g)) return psf_fast_bytes(g, batch);
     PlanEntry e;
     if (get_plan(g.py, g.px, batch, &e) != AKB_OK) return -1;
     const int64_t field = (int64_t)batch * g.py * g.px * 16;
@@ -239,10 +592,31 @@ int akb_psf_f64(const double* opd, const double* amp, int ny, int nx, int pad, i
     AKB_REQUIRE(batch >= 1 && batch <= 8, "batch must be 1..8");
     AKB_REQUIRE((hann_wy == nullptr) == (hann_wx == nullptr), "hann needs both axes");
     const PsfGeom g = psf_geom(ny, nx, pad);
-    PlanEntry e;
-    int st = get_plan(g.py, g.px, batch, &e);
-    if (st) return st;
     hipStream_t s = (hipStream_t)stream;
+    int st;
+    if (psf_fast_ok(g)) {
+        PsfFastArgs fa{};
+        fa.opd = opd;
+        fa.amp = amp;
+        fa.wy = hann_wy;
+        fa.wx = hann_wx;
+        fa.wmax = hann_max;
+        fa.g = g;
+        for (int b = 0; b < batch; ++b) fa.kphase[b] = (2.0 * M_PI / lambdas[b]);
+        fa.H = (double2*)work;
+        if ((st = get_twiddles(g.px, s, &fa.Wx))) return st;
+        if ((st = get_twiddles(g.py, s, &fa.Wy))) return st;
+        fa.dA = dx * dy;
+        fa.pitch = d_pitch;
+        fa.psf = psf;
+        fa.efield = (double2*)efield_re_im;
+        fa.imax = d_imax;
+        if ((st = psf_rows_dispatch(g.nx2, fa, batch, s))) return st;
+        return psf_cols_dispatch(g.ny2, fa, batch, s);
+    }
+    PlanEntry e;
+    st = get_plan(g.py, g.px, batch, &e);
+    if (st) return st;
     double2* field = (double2*)work;
     char* fft_work = (char*)work + (int64_t)batch * g.py * g.px * 16;
 
@@ -293,9 +667,14 @@ int akb_psf_f64(const double* opd, const double* amp, int ny, int nx, int pad, i
 }
 
 void akb_psf_release_plans(void) {
-    std::lock_guard<std::mutex> lk(g_plan_mu);
-    for (auto& kv : g_plans) rocfft_plan_destroy(kv.second.plan);
-    g_plans.clear();
+    {
+        std::lock_guard<std::mutex> lk(g_plan_mu);
+        for (auto& kv : g_plans) rocfft_plan_destroy(kv.second.plan);
+        g_plans.clear();
+    }
+    std::lock_guard<std::mutex> lk(g_tw_mu);
+    for (auto& kv : g_tw) (void)hipFree(kv.second);
+    g_tw.clear();
 }
 
 }  // extern "C"
