@@ -170,6 +170,18 @@ class LocalComm:
         return t
 
 
+@dataclass
+class _Front:
+    """What launch_front hands to launch_back."""
+    r: object
+    tan_h2: torch.Tensor
+    tan_v2: torch.Tensor
+    params: torch.Tensor
+    full: bool
+    stream: object
+    flags: tuple
+
+
 class RayWave:
     """Device-resident 'ray_wave' / 'wave' trace on an n x n grid (one shard of it).
 
@@ -198,7 +210,6 @@ class RayWave:
         self.sink3 = LeafSink(5, self.n_local, 0b11111, self.dev)
         self._ext = torch.zeros(4, dtype=torch.int64, device=self.dev)  # det2 extent keys (uint64 bits)
         self._pitch = torch.zeros(2, dtype=D.F64, device=self.dev)
-        self._params = torch.zeros(23, dtype=D.F64, device=self.dev)  # akb_tilt_params_f64 block
         self._opd_buf = None
         self.last = {}
         self.kernel_events = None  # set to a list to time the pass-2 chain launch (bench.py)
@@ -287,7 +298,17 @@ class RayWave:
         return DistError (detector 1), Sph, detcenter and the pre-tilt rows. The default keeps what
         griddata consumes (DistError2, Wave2, detcenter2) and reduces everything else on the fly.
         overlap: callable enqueuing independent device work (e.g. the previous step's PSF) that
-        runs while the host performs the resample."""
+        runs while the host performs the resample.
+
+        last_hit / dir_out / opl are the pass-2 launch's own buffers: the next run overwrites
+        them. A run is launch_back(launch_front()); a caller tracing several systems in a row can
+        pass the previous run's launch_back as this run's overlap, so its tilt and OPD fill the
+        GPU while the host resamples (bench.py does)."""
+        return self.launch_back(self.launch_front(full=full, overlap=overlap), opd=opd, keep_rotated=keep_rotated)
+
+    def launch_front(self, full=False, overlap=None):
+        """Pass 1, the resample (the run's one host wait), pass 2, its sums and the device tilt
+        parameters. Returns once pass 2's flag word is on the host; the rest stays queued."""
         L = _lib.lib()
         stream = D.stream_handle()
         samp_h, samp_v, flags1 = self._pass1(overlap, stream)
@@ -316,19 +337,27 @@ class RayWave:
         if self.comm.world > 1:  # cross-rank means: partial sums added over ranks (not numpy order)
             self.comm.allreduce_sums(sums)
             self.comm.allreduce_sums(cnts)
-        _lib.check(L.akb_tilt_params_f64(D.ptr(sums), D.ptr(cnts), D.ptr(self._params), D.ptr(self._ext),
+        params = torch.empty(23, dtype=D.F64, device=self.dev)  # this run's own block
+        _lib.check(L.akb_tilt_params_f64(D.ptr(sums), D.ptr(cnts), D.ptr(params), D.ptr(self._ext),
                                          D.ptr(self._flags), 2, stream))
-        out = RunResult(last_hit=r.last_hit, dir_out=r.dir_out, opl=r.opl, tan_h2=tan_h2, tan_v2=tan_v2,
-                        params=self._params)
-        if full:
-            out.update(det_pre=r.det, atan=r.atan)
-        if opd:
-            out.update(self._tilt_opd(r.last_hit, r.dir_out, r.opl, keep_rotated, full, stream=stream))
         ev2.synchronize()
-        flags2 = int(self._f_host[1])
-        if flags2:
-            out = self._run_staged(out, tan_h2, tan_v2, opd, keep_rotated, full)
-        out["flags"] = (flags1, flags2)
+        return _Front(r=r, tan_h2=tan_h2, tan_v2=tan_v2, params=params, full=full, stream=stream,
+                      flags=(flags1, int(self._f_host[1])))
+
+    def launch_back(self, f, opd=True, keep_rotated=False):
+        """Tilt, detectors and OPD of a launch_front (no host wait)."""
+        r = f.r
+        if f.flags[1]:
+            out = self._run_staged(None, f.tan_h2, f.tan_v2, opd, keep_rotated, f.full)
+        else:
+            out = RunResult(last_hit=r.last_hit, dir_out=r.dir_out, opl=r.opl, tan_h2=f.tan_h2, tan_v2=f.tan_v2,
+                            params=f.params)
+            if f.full:
+                out.update(det_pre=r.det, atan=r.atan)
+            if opd:
+                out.update(self._tilt_opd(r.last_hit, r.dir_out, r.opl, keep_rotated, f.full, params=f.params,
+                                          stream=f.stream))
+        out["flags"] = f.flags
         self.last = out
         return out
 
@@ -354,7 +383,8 @@ class RayWave:
             out.update(self._tilt_opd(last_hit, dir_out, opl, keep_rotated, full, host_tilt=(ry, rz, focus)))
         return out
 
-    def _tilt_opd(self, last_hit, dir_out, opl, keep_rotated=False, full=False, host_tilt=None, stream=None):
+    def _tilt_opd(self, last_hit, dir_out, opl, keep_rotated=False, full=False, host_tilt=None, params=None,
+                  stream=None):
         L = _lib.lib()
         n = self.n_local
         dev = self.dev
@@ -371,7 +401,7 @@ class RayWave:
         outs = (D.ptr(dir_out), D.ptr(last_hit), D.ptr(opl), n, n, D.ptr(dir_rot), D.ptr(pt_rot), D.ptr(det1),
                 D.ptr(det2_buf), D.ptr(total1), D.ptr(total2), self.sink3.desc, stream)
         if host_tilt is None:
-            _lib.check(L.akb_tilt_opd_dev_f64(D.ptr(self._params), D.host_f64(self.g.det1), D.host_f64(d2), *outs))
+            _lib.check(L.akb_tilt_opd_dev_f64(D.ptr(params), D.host_f64(self.g.det1), D.host_f64(d2), *outs))
         else:
             ry, rz, focus = host_tilt
             _lib.check(L.akb_tilt_opd_f64(D.host_f64(ry.ravel()), D.host_f64(rz.ravel()), D.host_f64(focus),

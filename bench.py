@@ -8,10 +8,14 @@ Workload (BASELINE.json configs[2], "C3"): the 'ray_wave' path of plot_result_de
 (AKB_raytrace_20250312.py:1326) on a 3163 x 3163 ray grid (1.0e7 rays) per GPU through the
 reference's Wolter III+I geometry (tests/golden/akb_geometry.json, recorded from the reference):
 pass 1 (4 mirrors), equal-angle resample, pass 2 (4 mirrors + OPL), tilt, two detector planes,
-OPD; then a 128 x 128 pupil padded x16 -> 2048^2 PSF on rocFFT. One step = all of it; its
-intersections are 2 passes x 4 mirrors x rays. Inputs (the two 1-D angle tables) are resident on
-the device before timing. Multi-GPU: weak scaling, each rank owns ~1e7 rays (contiguous V-rows of
-a grid of round(sqrt(N * 1e7))^2 rays); the PSF runs on rank 0.
+OPD; then a 128 x 128 pupil padded x16 -> 2048^2 PSF (pruned 2-D DFT: the padded plane is never
+built). One step = all of it; its intersections are 2 passes x 4 mirrors x rays. Steps are
+pipelined the way a caller tracing many systems would run them: step k's pass 1 is queued ahead
+of step k-1's tilt / OPD / pupil / PSF (RayWave.launch_front / launch_back), which hides the
+host's resample; every step still does all of its work inside the timed region. Inputs (the two
+1-D angle tables) are resident on the device before timing. Multi-GPU: weak scaling, each rank
+owns ~1e7 rays (contiguous V-rows of a grid of round(sqrt(N * 1e7))^2 rays); the PSF runs on
+rank 0.
 
 Prints one JSON line (rank 0). The dominant kernel's roofline uses HIP events on the stream it runs
 on; cpu_baseline times the oracle's C restatement (the "port") on this host on a bounded sample.
@@ -39,7 +43,7 @@ def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=3, help="at least 1 (fills the pipeline)")
     p.add_argument("--rays", type=float, default=1.0e7, help="rays per GPU")
     p.add_argument("--pupil", type=int, default=128)
     p.add_argument("--pad", type=int, default=16)
@@ -89,6 +93,7 @@ def read_traffic(launch_bytes):
 
 def main():
     args = parse()
+    args.warmup = max(args.warmup, 1)
     import torch
     from akbraytracing_amd import build as B
     from akbraytracing_amd import dist as AD
@@ -110,18 +115,17 @@ def main():
 
     psf_events = []
     psf_out = {}
-    pending = []  # pupil of the previous step, transformed while the next step traces
     side = torch.cuda.Stream(device=dev)
     state = {"psf_done": None}
+    fronts = []  # launched fronts (pass 1 .. tilt parameters) whose back half is still to queue
 
-    def run_psf(item, timed):
+    def run_psf(opd, pitch, ready, timed):
         """The PSF of a finished pupil on a side stream: it starts when the pupil is ready and
-        fills the GPU while the host resamples (and beside the next step's kernels)."""
-        opd, pitch, ready = item
+        shares the GPU with the next kernels of the main stream."""
         if rank != 0:
             return
         side.wait_event(ready)
-        if args.psf_start == "pass1":  # called right after pass 1 and its copy were queued
+        if args.psf_start == "pass1":
             after = torch.cuda.Event()
             after.record()
             side.wait_event(after)
@@ -139,32 +143,47 @@ def main():
             done.record(side)
         state["psf_done"] = done
 
-    def step(timed):
-        # the PSF of step k-1 is queued right after pass 1 of step k (all inside the timed region)
-        rw.run(overlap=(lambda: run_psf(pending.pop(), timed)) if pending else None)
+    def back(timed):
+        """Tilt, OPD and pupil of the oldest front, then its PSF."""
+        rw.launch_back(fronts.pop(0))
         if state["psf_done"] is not None:  # the pupil buffer is reused: wait for its last reader
             torch.cuda.current_stream().wait_event(state["psf_done"])
             state["psf_done"] = None
         opd, pitch = rw.pupil(args.pupil)
         ready = torch.cuda.Event()
         ready.record()
-        pending.append((opd, pitch, ready))
+        run_psf(opd, pitch, ready, timed)
+
+    def step(timed):
+        # pipelined: this step's pass 1 is queued first, the previous step's tilt / OPD / pupil /
+        # PSF right behind it, so the GPU works through them while the host does the resample;
+        # each step still traces, tilts, reduces and transforms one full grid
+        fronts.append(rw.launch_front(overlap=(lambda: back(timed)) if fronts else None))
 
     for _ in range(args.warmup):
         step(False)
-    while pending:
-        run_psf(pending.pop(), False)
     rw.kernel_events = []
     comm.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(True)
-    while pending:
-        run_psf(pending.pop(), True)
     torch.cuda.synchronize()
     comm.barrier()
     el = time.perf_counter() - t0
+    while fronts:  # the last front's back half (outside the timed region, like the first one's)
+        back(False)
+    torch.cuda.synchronize()
+    psf_alone_ms = None
+    if rank == 0:  # the PSF's own wall time, nothing beside it
+        opd, pitch = rw.pupil(args.pupil)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(10):
+            psf_stack(opd, None, [lam], None, pitch=pitch, pad_factor=args.pad, out=psf_out.get("psf"))
+        b.record()
+        b.synchronize()
+        psf_alone_ms = a.elapsed_time(b) / 10
     t = torch.tensor([el], dtype=torch.float64, device=dev)
     t = comm.allreduce_max(t)
     el = float(t.item())
@@ -193,13 +212,14 @@ def main():
         "dtype": "f64",
         "data": "synthetic: deterministic ray grid through the reference's AKB geometry (recorded fixture)",
         "config": {
-            "workload": "C3: 4-mirror AKB ray_wave trace (2 passes, tilt, OPD) + 2048^2 PSF on rocFFT",
+            "workload": "C3: 4-mirror AKB ray_wave trace (2 passes, tilt, OPD) + 2048^2 PSF",
             "rays_per_gpu": rw.n_local, "grid": n, "mirrors": len(geom.mirrors),
             "intersections_per_step": 2 * len(geom.mirrors) * n * n,
-            "psf": f"{args.pupil}^2 pupil x pad {args.pad} -> {args.pupil * args.pad}^2 complex128 FFT",
+            "psf": f"{args.pupil}^2 pupil x pad {args.pad} -> {args.pupil * args.pad}^2 complex128 DFT (pruned)",
             "parallelism": f"ray-row shards x{world}",
         },
         "psf_ms": psf_ms,
+        "psf_alone_ms": psf_alone_ms,
         "pass2_kernel_ms": k_avg,
         "roofline": {
             "kernel": "k_chain<grid,opl> (pass 2)",
