@@ -33,6 +33,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "ray-surface intersections/sec + PSF wall-time, 1e7-ray 4-mirror AKB, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X spec, MI355X_MICROARCH.md
+FP64_VALU_PEAK_TFS = 78.6  # MI355X FP64 vector peak (FMA counted as 2 flops)
 # bytes the pass-2 chain kernel must move per ray: it reads two L2-resident 1-D tables and
 # writes last hit (24) + exit direction (24) + OPL (8); the arctans and detector hits it also
 # forms are reduced in-kernel (numpy-order leaf sums, 5 x 8 B per 128 rays)
@@ -78,17 +79,16 @@ def cpu_baseline(seconds):
                       f"on a {n}x{n} grid, {reps} reps in {el:.1f} s"}
 
 
-def read_traffic(launch_bytes):
-    """HBM bytes per pass-2 launch from the committed rocprofv3 --pmc summary, if present."""
+def read_pmc():
+    """The pass-2 chain's rocprofv3 --pmc summary committed under profiles/ (newest), or {}."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_pass2*.json")))
     if not files:
-        return None
+        return {}
     try:
         with open(files[-1]) as f:
-            d = json.load(f)
-        return d.get("hbm_bytes_per_launch")
+            return json.load(f)
     except Exception:
-        return None
+        return {}
 
 
 def main():
@@ -198,6 +198,7 @@ def main():
     psf_ms = sum(a.elapsed_time(b) for a, b in psf_events) / max(len(psf_events), 1)
     launch_bytes = PASS2_BYTES_PER_RAY * rw.n_local
     achieved = launch_bytes / (k_avg * 1e-3) / 1e9
+    pmc = read_pmc()
     out = {
         "metric": METRIC,
         "value": total_inter / el,
@@ -228,8 +229,20 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": read_traffic(launch_bytes),
+            "traffic": pmc.get("hbm_bytes_per_launch"),
             "algorithmic_bytes_per_launch": launch_bytes,
+        },
+        # what actually bounds that kernel: FP64 vector issue. FP64 flops per
+        # launch from the committed PMC counts (FMA = 2) over this run's kernel time.
+        "roofline_fp64": {
+            "bound": "fp64-valu",
+            "achieved": (pmc["fp64_flops_per_launch"] / (k_avg * 1e-3) / 1e12) if pmc.get("fp64_flops_per_launch")
+            else None,
+            "peak": FP64_VALU_PEAK_TFS,
+            "unit": "TFLOP/s",
+            "frac": (pmc["fp64_flops_per_launch"] / (k_avg * 1e-3) / 1e12 / FP64_VALU_PEAK_TFS)
+            if pmc.get("fp64_flops_per_launch") else None,
+            "valu_busy_pct": pmc.get("valu_busy_pct"),
         },
     }
     if world == 1 and not args.no_cpu_baseline:

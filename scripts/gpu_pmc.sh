@@ -10,7 +10,9 @@ F64=$(grep -oE "SQ_INSTS_VALU_(FMA|MUL|ADD|TRANS)_F64" gpurun_out/counters.txt |
 echo "f64 counters: $F64"
 REGEX="${PMC_REGEX:-k_chain|k_tilt|k_opd|k_pw|k_psf|fft}"
 i=0
-for SET in "FETCH_SIZE" "WRITE_SIZE" "$F64" "GRBM_GUI_ACTIVE SQ_WAVES SQ_INSTS_VALU"; do
+for SET in "FETCH_SIZE" "WRITE_SIZE" "$F64" "GRBM_GUI_ACTIVE SQ_WAVES SQ_INSTS_VALU" \
+           "SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_SALU" \
+           "SQ_WAIT_INST_ANY SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR"; do
   [ -n "$SET" ] || continue
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $SET --kernel-include-regex "$REGEX" --output-format csv \

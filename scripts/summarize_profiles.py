@@ -18,7 +18,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "gpurun_out")
 DST = os.path.join(ROOT, "profiles")
-PASS2 = "akb::k_chain_sink<true, true>"
+PASS2 = "akb::k_chain_sink<true, true"
 
 
 def pmc_table():
@@ -67,6 +67,12 @@ def main(tag):
             "valu_wave_instructions_per_launch": d.get("SQ_INSTS_VALU"),
             "avg_duration_ns_kernel_trace": ns,
             "effective_clock_ghz": (d.get("GRBM_GUI_ACTIVE", 0) / 8 / ns) if ns else None,
+            # rocprof's VALUBusy: 100 * SQ_ACTIVE_INST_VALU / CU_NUM / GRBM_GUI_ACTIVE (per XCD)
+            "valu_busy_pct": (100.0 * d["SQ_ACTIVE_INST_VALU"] / 256 / (d["GRBM_GUI_ACTIVE"] / 8)
+                              if d.get("SQ_ACTIVE_INST_VALU") and d.get("GRBM_GUI_ACTIVE") else None),
+            "non_fp64_valu_wave_instructions_per_launch": (d.get("SQ_INSTS_VALU", 0) - f64_wave
+                                                           if d.get("SQ_INSTS_VALU") else None),
+            "int32_valu_wave_instructions_per_launch": d.get("SQ_INSTS_VALU_INT32"),
             "note": "FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM; WRITE_SIZE is uncalibrated for 8-B stores",
         }
         if ns:

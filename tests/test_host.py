@@ -95,6 +95,35 @@ def test_resample_matches_oracle():
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
 
 
+def test_resample_restatement_matches_scipy_interp1d():
+    """akb_resample_f64 (numpy linspace + scipy interp1d(kind='linear') restated in C) against
+    scipy itself: sorted, reversed, tied, unsorted and near-monotone angle samples, and the
+    out-of-range ValueError."""
+    import scipy.interpolate as si
+    from akbraytracing_amd.wavefront import resample_axis
+    rng = np.random.default_rng(5)
+    for t in range(1000):
+        n = int(rng.integers(1, 300))
+        kind = t % 5
+        x = np.sort(rng.standard_normal(n))
+        if kind == 1:
+            x = x[::-1].copy()
+        elif kind == 2:
+            x = np.round(x, 1)
+        elif kind == 3:
+            x = rng.standard_normal(n)
+        elif kind == 4:
+            x = np.tan(np.linspace(-0.01, 0.02, n)) * (1 + 1e-9 * rng.standard_normal(n))
+        y = rng.standard_normal(n)
+        try:
+            ref = si.interp1d(x, y, kind="linear")(np.linspace(x[0], x[-1], n))
+        except ValueError:
+            with pytest.raises(ValueError):
+                resample_axis(x, y)
+            continue
+        assert np.array_equal(resample_axis(x, y), ref, equal_nan=True), (t, n, kind)
+
+
 def test_psf_host_helpers_match_reference_formulas():
     from akbraytracing_amd import psf as G
     import oracle.psf as OP
