@@ -19,7 +19,7 @@ c_int = ctypes.c_int
 c_dbl = ctypes.c_double
 c_vp = ctypes.c_void_p
 MAX_MIRRORS = 7
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 FLAG_MISS = 0x1
 FLAG_ZERO_NORMAL = 0x2
@@ -73,6 +73,7 @@ class ChainDesc(ctypes.Structure):
         ("samp_h", c_vp), ("samp_v", c_vp),
         ("flags", c_vp),
         ("sink", LeafSink),
+        ("pert_h", c_vp), ("pert_v", c_vp), ("pert_terms", c_i32),
     ]
 
 

@@ -170,6 +170,7 @@ struct ChainArgs {
     const double* tan_h;
     const double* tan_v;
     uint32_t n_h;
+    uint32_t n_v;
     uint32_t div_mul;  // Granlund-Montgomery magic for g / n_h with 32-bit g (see div_magic)
     uint32_t div_shift;
     int64_t g0;  // global flat index of ray 0 of this launch
@@ -193,6 +194,9 @@ struct ChainArgs {
     double* samp_v;
     int32_t* flags;
     akb_leaf_sink sink;
+    const double* pert_h;  // (terms, n_h) / (terms, n_v) OPL perturbation tables or NULL
+    const double* pert_v;
+    int pert_terms;
 };
 
 // row / column of flat grid index g without a 64-bit division: q = (t + ((g - t) >> 1)) >> (s - 1)
@@ -287,6 +291,11 @@ __device__ __forceinline__ void chain_ray(const ChainArgs& a, int64_t i, int& fl
         p = x;
         q = y;
         r = z;
+    }
+    if (kOPL && kGrid && a.pert_h) {  // figure-error perturbation of the path (BASELINE config 5)
+        double d = 0.0;
+        for (int t = 0; t < a.pert_terms; ++t) d = __builtin_fma(a.pert_v[t * a.n_v + iv], a.pert_h[t * a.n_h + ih], d);
+        opl = opl + d;
     }
     if (kOPL && a.opl) a.opl[i] = opl;
     if (a.last_hit) {
@@ -808,6 +817,9 @@ int akb_trace_chain_f64(const akb_chain_desc* d, void* stream) {
         AKB_REQUIRE(d->n_h * d->n_v < (1LL << 32), "ray grid beyond 2^32 rays");
     }
     if (d->samp_v) AKB_REQUIRE(grid && d->samp_v_col >= 0 && d->samp_v_col < d->n_h, "bad samp_v_col");
+    if (d->pert_h)
+        AKB_REQUIRE(grid && d->pert_v && d->opl && d->pert_terms > 0 && d->pert_terms <= 8,
+                    "OPL perturbation needs grid rays, opl and 1..8 terms");
     const bool sink = d->sink.nq > 0;
     if (sink) {
         AKB_REQUIRE(d->sink.nq == 5 && d->sink.n == d->n_rays && d->sink.leaf_sum && d->sink.leaf_cnt &&
@@ -835,6 +847,7 @@ int akb_trace_chain_f64(const akb_chain_desc* d, void* stream) {
     a.tan_h = d->tan_h;
     a.tan_v = d->tan_v;
     a.n_h = grid ? (uint32_t)d->n_h : 1u;
+    a.n_v = grid ? (uint32_t)d->n_v : 1u;
     div_magic(a.n_h, &a.div_mul, &a.div_shift);
     a.g0 = grid ? d->row0 * d->n_h : 0;
     a.n = d->n_rays;
@@ -860,6 +873,9 @@ int akb_trace_chain_f64(const akb_chain_desc* d, void* stream) {
     a.samp_v = d->samp_v;
     a.flags = d->flags;
     a.sink = d->sink;
+    a.pert_h = d->pert_h;
+    a.pert_v = d->pert_v;
+    a.pert_terms = d->pert_h ? d->pert_terms : 0;
     hipStream_t s = (hipStream_t)stream;
     const int64_t gcap = chain_grid_cap();
     const unsigned gsz = grid_for(d->n_rays, 1, gcap);

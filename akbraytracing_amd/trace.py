@@ -68,7 +68,7 @@ class ChainLaunch:
 
     def __init__(self, mirrors, *, tan_h=None, tan_v=None, row0=0, n_rays=None, dirs=None, src=(0.0, 0.0, 0.0),
                  det_ghij=None, want=("last_hit", "dir_out"), samples=None, out=None, sink=None, flags=None,
-                 samples_buf=None):
+                 samples_buf=None, pert=None):
         dev = D.device()
         desc = _lib.ChainDesc()
         _fill_desc(desc, mirrors, det_ghij)
@@ -150,6 +150,14 @@ class ChainLaunch:
             if det_ghij is None:
                 raise ValueError("the chain sink reduces detector hits: give det_ghij")
             desc.sink = sink.desc
+        if pert is not None:
+            if dirs is not None or "opl" not in want:
+                raise ValueError("the OPL perturbation applies to grid rays with want containing 'opl'")
+            ph, pv = pert
+            if ph.shape[0] != pv.shape[0] or ph.shape[1] != desc.n_h or pv.shape[1] != desc.n_v:
+                raise ValueError("perturbation tables must be (terms, n_h) and (terms, n_v)")
+            desc.pert_h, desc.pert_v, desc.pert_terms = D.ptr(ph), D.ptr(pv), int(ph.shape[0])
+            self.keep += [ph, pv]
         res.extra["buffers"] = out
         self.desc, self.res = desc, res
 
@@ -169,6 +177,8 @@ def trace_chain(mirrors, *, stream=None, **kw):
     samples: (h_begin, h_end, v_col) flat-index range / column whose exit slopes to record.
     flags / samples_buf: optional caller-owned int32 flag word and float64 pick buffer (RayWave
         places the flag words right after the picks so one copy brings both to the host).
+    pert: optional (pert_h, pert_v) device tables of a legendre.LegendrePerturbation, added to
+        each grid ray's OPL (BASELINE config 5).
     out: optional dict of preallocated tensors keyed like ChainOutputs fields (reused buffers).
     sink: optional reduce.LeafSink(5, n_rays, nan_mask=0b00011) fed with (arctan(Ry/Rx),
         arctan(Rz/Rx), det_x, det_y, det_z) — the tilt means without writing those rows.

@@ -190,7 +190,9 @@ class RayWave:
     by design, see resample_axis); pass 2, the tilt parameters, the tilt and the OPD are queued
     back to back, and the run returns as soon as pass 2's flag word has reached the host."""
 
-    def __init__(self, geometry, n, shard=None, comm=None, resample_pass=True):
+    def __init__(self, geometry, n, shard=None, comm=None, resample_pass=True, perturbation=None):
+        """perturbation: optional legendre.LegendrePerturbation added to every ray's pass-2 optical
+        path (BASELINE config 5's figure-error model)."""
         self.g = geometry
         self.n = int(n)
         self.comm = comm or LocalComm()
@@ -230,6 +232,7 @@ class RayWave:
                                flags=self._flags[0:1], samples_buf=self._x1[:self._nsamp])
         self._p2 = {}
         self._own = sample_ownership(self.shard, self.n)
+        self._pert = perturbation.device_tables(self.n, self.n, self.dev) if perturbation is not None else None
 
     def _pass2_launch(self, want_rows):
         key = bool(want_rows)
@@ -237,7 +240,8 @@ class RayWave:
             want = ("last_hit", "dir_out", "opl") + (("det", "atan") if want_rows else ())
             self._p2[key] = ChainLaunch(self.g.mirrors, tan_h=self._tan2[:self.n], tan_v=self._tan2[self.n:],
                                         row0=self.shard.row0, n_rays=self.n_local, src=self.g.source,
-                                        det_ghij=self.g.det1, want=want, sink=self.sink2, flags=self._flags[1:2])
+                                        det_ghij=self.g.det1, want=want, sink=self.sink2, flags=self._flags[1:2],
+                                        pert=self._pert)
         return self._p2[key]
 
     # -------------------------------------------------------------- passes
@@ -287,6 +291,10 @@ class RayWave:
         opl = segs[0]
         for s in segs[1:]:
             opl = opl + s
+        if self._pert is not None:
+            ph, pv = self._pert
+            rows = pv[:, self.shard.row0:self.shard.row0 + self.shard.rows]
+            opl = opl + (rows.T @ ph).reshape(-1)
         det = P.plane_ray_intersection([0] * 6 + list(self.g.det1), r4, hits[-1])
         atan = torch.stack([torch.atan(r4[1] / r4[0]), torch.atan(r4[2] / r4[0])])
         return hits[-1], r4, det, opl, atan

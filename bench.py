@@ -50,6 +50,9 @@ def parse():
     p.add_argument("--pad", type=int, default=16)
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--config", choices=("c3", "c5"), default="c3",
+                   help="c3: BASELINE configs[2] (default, the headline); c5: configs[4], the Legendre "
+                        "figure-error OPL perturbation on every ray + a 3-wavelength PSF stack")
     p.add_argument("--psf-start", choices=("pupil", "pass1"), default="pupil",
                    help="side-stream PSF starts as soon as the previous pupil is ready, beside pass 1 "
                         "(default; measured faster), or after this step's pass 1")
@@ -110,8 +113,13 @@ def main():
     n = int(math.ceil(math.sqrt(args.rays * world)))  # 3163 at 1 GPU
     shard = Shard.split(n, world, rank)
     comm = AD.TorchComm(dev)
-    rw = RayWave(geom, n, shard=shard, comm=comm)
-    lam = 13.5e-9  # EUV, AKB_raytrace_20250312.py:1161-1162 / :3614
+    pert = None
+    lams = [13.5e-9]  # EUV, AKB_raytrace_20250312.py:1161-1162 / :3614
+    if args.config == "c5":
+        from akbraytracing_amd.legendre import LegendrePerturbation, config5_coefficients
+        pert = LegendrePerturbation(config5_coefficients(lams[0]))
+        lams = [13.5e-9, 1.35e-9, 1.35e-10]  # EUV, softXray, hardXray (:1161-1166)
+    rw = RayWave(geom, n, shard=shard, comm=comm, perturbation=pert)
 
     psf_events = []
     psf_out = {}
@@ -133,7 +141,7 @@ def main():
             if timed:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(side)
-            psf, _, _ = psf_stack(opd, None, [lam], None, pitch=pitch, pad_factor=args.pad,
+            psf, _, _ = psf_stack(opd, None, lams, None, pitch=pitch, pad_factor=args.pad,
                                   out=psf_out.get("psf"))
             psf_out["psf"] = psf
             if timed:
@@ -180,7 +188,7 @@ def main():
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
         for _ in range(10):
-            psf_stack(opd, None, [lam], None, pitch=pitch, pad_factor=args.pad, out=psf_out.get("psf"))
+            psf_stack(opd, None, lams, None, pitch=pitch, pad_factor=args.pad, out=psf_out.get("psf"))
         b.record()
         b.synchronize()
         psf_alone_ms = a.elapsed_time(b) / 10
@@ -213,10 +221,13 @@ def main():
         "dtype": "f64",
         "data": "synthetic: deterministic ray grid through the reference's AKB geometry (recorded fixture)",
         "config": {
-            "workload": "C3: 4-mirror AKB ray_wave trace (2 passes, tilt, OPD) + 2048^2 PSF",
+            "workload": ("C3: 4-mirror AKB ray_wave trace (2 passes, tilt, OPD) + 2048^2 PSF" if args.config == "c3"
+                         else "C5: 4-mirror AKB ray_wave trace with per-ray Legendre OPL perturbation + "
+                              "3-wavelength 2048^2 PSF stack"),
             "rays_per_gpu": rw.n_local, "grid": n, "mirrors": len(geom.mirrors),
             "intersections_per_step": 2 * len(geom.mirrors) * n * n,
-            "psf": f"{args.pupil}^2 pupil x pad {args.pad} -> {args.pupil * args.pad}^2 complex128 DFT (pruned)",
+            "psf": f"{args.pupil}^2 pupil x pad {args.pad} -> {len(lams)} x {args.pupil * args.pad}^2 complex128 "
+                   "DFT (pruned)",
             "parallelism": f"ray-row shards x{world}",
         },
         "psf_ms": psf_ms,

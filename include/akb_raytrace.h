@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define AKB_ABI_VERSION 3
+#define AKB_ABI_VERSION 4
 
 /* status codes */
 #define AKB_OK 0
@@ -160,6 +160,10 @@ typedef struct akb_chain_desc {
     int32_t* flags;                           /* device int32, OR-ed */
     /* optional fused reduction of (atan_h, atan_v, det_x, det_y, det_z): sink.nq = 5 */
     akb_leaf_sink sink;
+    /* optional per-ray OPL perturbation on the grid (BASELINE config 5, a figure-error model on a
+     * Legendre basis; grid rays only, needs opl): opl += sum_t pert_v[t][iv] * pert_h[t][ih] for
+     * t < pert_terms (<= 8), tables (pert_terms, n_v) and (pert_terms, n_h), row-major */
+    const double* pert_h; const double* pert_v; int32_t pert_terms;
 } akb_chain_desc;
 
 int akb_trace_chain_f64(const akb_chain_desc* desc, void* stream);

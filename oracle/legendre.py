@@ -29,3 +29,21 @@ def fit_multi(data, order):
         fits.append(c * Z)
         coefs.append(c)
     return np.array(fits), np.array(coefs)
+
+
+def config5_coefficients(wavelength_m=13.5e-9, order=5, seed=0):
+    """BASELINE config 5's figure-error coefficients: c = 0.01 lambda N(0, 1)
+    from numpy's default_rng(seed), one per (ny, nx) of orders(order)."""
+    return 0.01 * wavelength_m * np.random.default_rng(seed).standard_normal(len(orders(order)))
+
+
+def perturbation(n_h, n_v, coeffs, order=5):
+    """sum_k c_k Z_k on the n_v x n_h ray grid, Z_k the unit-norm component of match_legendre
+    (x = linspace(-1, 1) over ih, y over iv): the per-ray OPL perturbation of config 5."""
+    xs = np.linspace(-1, 1, n_h)
+    ys = np.linspace(-1, 1, n_v)
+    out = np.zeros((n_v, n_h))
+    for c, (ny, nx) in zip(coeffs, orders(order)):
+        Z = component(xs, ys, nx, ny)
+        out += c * (Z / np.sqrt(np.nansum(Z * Z)))
+    return out

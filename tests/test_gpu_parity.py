@@ -305,6 +305,24 @@ def test_ray_wave_65_vs_reference(gpu):
     assert np.max(np.abs(out["wave2"].cpu().numpy() - f["wave2"])) <= 1e-4
 
 
+def test_config5_legendre_opl_perturbation(gpu):
+    """BASELINE config 5: the chain adds the Legendre figure-error model to each ray's OPL (model
+    from oracle/legendre.py; the basis is pinned to legendre_fit by test_oracle_golden)."""
+    from akbraytracing_amd.legendre import LegendrePerturbation, config5_coefficients
+    from akbraytracing_amd.wavefront import RayWave
+    import oracle.legendre as OL
+    n = 65
+    for scale in (1.0, 1e6):  # the config's own size, and one far above the OPL's ulp
+        c = config5_coefficients() * scale
+        base = RayWave(_geom(), n).run(opd=False)
+        pert = RayWave(_geom(), n, perturbation=LegendrePerturbation(c)).run(opd=False)
+        want = OL.perturbation(n, n, c).reshape(-1)
+        got = (pert["opl"] - base["opl"]).cpu().numpy()
+        ulp = np.spacing(base["opl"].cpu().numpy())
+        assert np.all(np.abs(got - want) <= 1.01 * ulp + 1e-13 * np.abs(want))
+        assert torch.equal(pert["last_hit"], base["last_hit"])
+
+
 @pytest.mark.parametrize("n", [65, 128, 1001])
 def test_fused_means_equal_numpy_on_the_rows(gpu, n):
     """The leaf sums fused into pass 2 and the tilt kernel give the same means numpy takes of the
