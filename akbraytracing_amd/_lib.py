@@ -38,6 +38,7 @@ EXPORTS = [
     "akb_leaf_sink_bytes", "akb_leaf_sink_layout", "akb_leaf_finish_work_bytes", "akb_leaf_finish_f64",
     "akb_huygens_work_bytes", "akb_huygens_f64", "akb_scale_field_f64",
     "akb_psf_work_bytes", "akb_psf_f64", "akb_psf_release_plans", "akb_selftest_arith_f64",
+    "akb_first_valid_rows_f64", "akb_rotate_work_bytes", "akb_rotate_with_nan_f64",
 ]
 
 
@@ -121,6 +122,9 @@ def _declare(L):
                          c_vp, c_vp, c_vp, c_vp, c_vp], c_int),
         "akb_psf_release_plans": ([], None),
         "akb_selftest_arith_f64": ([c_vp, c_vp, c_i64, c_vp, c_vp], c_int),
+        "akb_first_valid_rows_f64": ([c_vp, c_int, c_int, c_vp, c_vp], c_int),
+        "akb_rotate_work_bytes": ([c_int, c_int], c_i64),
+        "akb_rotate_with_nan_f64": ([c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp], c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -269,6 +269,21 @@ int akb_psf_f64(const double* opd, const double* amp, int ny, int nx, int pad, i
                 const double* hann_wx, double hann_max, double* psf, double* efield_re_im,
                 double* d_imax, const double* d_pitch, void* work, void* stream);
 
+/* ---------------- psf_calc pupil preparation (ref AKB_raytrace_20250312.py:1121-1188) ---------------- */
+
+/* d_rows[c] = first row r with m[r][c] not NaN, -1 for an all-NaN column (the rotation
+ * estimate's min_indices, :1122-1128; the caller forms rot with np.arctan as the reference). */
+int akb_first_valid_rows_f64(const double* m, int ny, int nx, int32_t* d_rows, void* stream);
+
+/* rotate_with_nan(m, angle, order=3) of psf_calc (:1138-1156): scipy.ndimage.rotate (reshape
+ * False, mode 'constant', cubic B-spline) of the NaN-filled map and of its finite mask,
+ * rotated = filled' / max(mask', 1e-12), NaN where mask' < 0.5. rot = [[c, s], [-s, c]] with
+ * c = cosdg(angle), s = sindg(angle), offset = centre - rot @ centre (host-formed, as scipy
+ * forms them); opd_m (optional) = rotated * 1e-9. work: akb_rotate_work_bytes(ny, nx). */
+int64_t akb_rotate_work_bytes(int ny, int nx);
+int akb_rotate_with_nan_f64(const double* m, int ny, int nx, const double rot[4], const double offset[2],
+                            double* rotated, double* opd_m, void* work, void* stream);
+
 /* diagnostics: out4[4i..4i+3] = (the trace's sqrt, sqrt, the trace's shared-reciprocal a/b, a/b)
  * for n pairs (a[i], b[i]) — used by the tests to check the shortcuts bit for bit */
 int akb_selftest_arith_f64(const double* a, const double* b, int64_t n, double* out4, void* stream);

@@ -436,6 +436,42 @@ def test_psf_errors(gpu):
         G.compute_psf_fft(np.zeros((4, 4)), np.zeros((4, 4)), 1e-9, 1e-6, 1e-2, window="tukey")
 
 
+# ----------------------------------------------------------------------------- psf_calc
+
+def test_rotate_with_nan_vs_oracle(gpu):
+    from akbraytracing_amd import psfcalc as G
+    import oracle.psfcalc as PC
+    d = golden("scipy_rotate.npz")
+    for k in range(4):
+        img = d[f"k{k}_in"].copy()
+        img[d[f"k{k}_mask"] == 0] = np.nan
+        ang = float(d[f"k{k}_angle"])
+        got, opd = G.rotate_with_nan(torch.from_numpy(img).to(gpu), ang)
+        want = PC.rotate_with_nan(img, ang)
+        got = got.cpu().numpy()
+        assert np.array_equal(np.isnan(got), np.isnan(want))
+        assert np.nanmax(np.abs(got - want)) <= 1e-12 * max(1.0, np.nanmax(np.abs(want)))
+        assert np.array_equal(opd.cpu().numpy(), got * 1e-9, equal_nan=True)
+
+
+def test_psf_calc_vs_reference(gpu, tmp_path):
+    """The reference's psf_calc inputs from its 65x65 ray_wave run -> rotation, rotated pupil,
+    trimmed PSF and the saved .npy files."""
+    from akbraytracing_amd import psfcalc as G
+    f = golden("akb_psfcalc_65.npz")
+    r = G.psf_calc(f["psf_calc_in"], f["grid_H"], f["grid_V"], float(f["defocus"]), directory=str(tmp_path))
+    assert r["rot"] == f["rot"]
+    rot = r["rotated"].cpu().numpy()
+    assert np.array_equal(np.isnan(rot), np.isnan(f["rotated"]))
+    assert np.nanmax(np.abs(rot - f["rotated"])) <= 1e-12
+    t = r["psf_trimmed"].cpu().numpy()
+    assert t.shape == f["psf_trimmed"].shape
+    assert np.max(np.abs(t - f["psf_trimmed"])) <= 1e-10
+    assert np.array_equal(r["x_trimmed"], f["x_im"][f["trim_ix"]])
+    assert np.array_equal(np.load(tmp_path / "psf_x.npy"), f["x_im"])
+    assert np.load(tmp_path / "psf.npy").shape == (1056, 1056)
+
+
 # ----------------------------------------------------------------------------- Huygens
 
 def test_huygens_cases(gpu):

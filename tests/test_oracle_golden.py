@@ -158,3 +158,27 @@ def test_all_nan_and_passthrough_rules():
     # a zero vector: normalize_vector returns its input unchanged (ref :530-532)
     v = np.array([[0.0, 1.0], [0.0, 2.0], [0.0, 2.0]])
     assert O.normalize_vector(v) is v
+
+
+def test_oracle_rotate_matches_scipy_fixtures():
+    """oracle/psfcalc.rotate restates scipy.ndimage.rotate(order 3, constant, reshape False)."""
+    import oracle.psfcalc as PC
+    d = golden("scipy_rotate.npz")
+    for k in range(4):
+        ang = float(d[f"k{k}_angle"])
+        assert np.max(np.abs(PC.rotate(d[f"k{k}_in"], ang) - d[f"k{k}_out"])) <= 1e-13
+        assert np.max(np.abs(PC.rotate(d[f"k{k}_mask"], ang) - d[f"k{k}_mask_out"])) <= 1e-13
+
+
+def test_oracle_psf_calc_matches_reference():
+    """psf_calc of the reference's 65x65 ray_wave run: rotation estimate (exact), the rotated
+    map it handed compute_psf_fft (NaN pattern exact, values to 1e-15 nm) and the trimmed PSF."""
+    import oracle.psfcalc as PC
+    f = golden("akb_psfcalc_65.npz")
+    r = PC.psf_calc(f["psf_calc_in"], f["grid_H"], f["grid_V"], float(f["defocus"]))
+    assert r["rot"] == f["rot"]
+    assert np.array_equal(np.isnan(r["rotated"]), np.isnan(f["rotated"]))
+    assert np.nanmax(np.abs(r["rotated"] - f["rotated"])) <= 1e-15
+    assert r["psf_trimmed"].shape == f["psf_trimmed"].shape
+    assert np.max(np.abs(r["psf_trimmed"] - f["psf_trimmed"])) <= 1e-12
+    assert np.array_equal(r["x_im"], f["x_im"])
