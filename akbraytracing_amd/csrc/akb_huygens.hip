@@ -10,9 +10,13 @@
 // workgroup streams source tiles (x, y, z, Re u, Im u) through LDS, so HBM traffic is the source
 // set once per workgroup and the kernel is bound by FP64 VALU (sqrt, div, sincos per pair).
 //
-// r_ij is formed exactly as numpy forms it (no contraction), because k r ~ 7e10 rad: one ulp
-// of r moves the phase by ~1e-5 rad. The complex multiply-accumulate uses explicit FMAs
-// (tolerance-checked against the oracle, not bitwise: numpy's own sum order is pairwise).
+// r_ij is formed exactly as numpy forms it (no contraction, correctly rounded sqrt), because
+// k r ~ 7e10 rad: one ulp of r moves the phase by ~1e-5 rad. The phase -k r is reduced modulo
+// pi/2 by a five-piece Cody-Waite split (13-bit pieces: n pi/2 exact for |n| < 2^40, residual
+// 2^-65 rad) instead of the library's Payne-Hanek path, and sin / cos come from fdlibm's kernel
+// polynomials (< 1 ulp); 1/r is rcp + one Newton step (< 1 ulp). The complex multiply-accumulate
+// uses explicit FMAs. All of it is tolerance-checked against the oracle (numpy's own sum is
+// pairwise, so the field is not bitwise anyway).
 #include <math.h>
 
 #include "akb_common.h"
@@ -22,6 +26,55 @@ namespace akb {
 constexpr int kHuyBlock = 256;
 constexpr int kHuyTile = 256;  // sources per LDS tile (5 doubles each = 10 KiB)
 constexpr int kTPL = 2;        // targets per lane
+
+// correctly rounded sqrt for the pair distances without the library's tiny / huge-input paths:
+// sqrt_cr's core (akb_common.h) for x in [2^-767, 2^1000] — every distance between points metres
+// apart — and 0 for x = 0 (a target on a source, where the reference's amplitude is inf too);
+// anything else (never formed here) would come out NaN
+__device__ __forceinline__ double sqrt_core(double x) {
+    const double r = __builtin_amdgcn_rsq(x);
+    double g = x * r;
+    double h = r * 0.5;
+    const double e = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, e, g);
+    const double d = __builtin_fma(-g, g, x);
+    h = __builtin_fma(h, e, h);
+    g = __builtin_fma(d, h, g);
+    const double d2 = __builtin_fma(-g, g, x);
+    const double out = __builtin_fma(d2, h, g);
+    return x == 0.0 ? 0.0 : out;
+}
+
+// sin and cos of x for |x| < 2^40 pi/2 (the library call beyond)
+__device__ __forceinline__ void sincos_phase(double x, double& sn, double& cs) {
+    const double q = rint(x * 0x1.45f306dc9c883p-1);  // x * 2/pi
+    if (__builtin_expect(!(fabs(q) < 0x1p40), 0)) {
+        sincos(x, &sn, &cs);
+        return;
+    }
+    double f = __builtin_fma(-q, 0x1.9220000000000p+0, x);
+    f = __builtin_fma(-q, -0x1.2af0000000000p-18, f);
+    f = __builtin_fma(-q, 0x1.0b40000000000p-34, f);
+    f = __builtin_fma(-q, 0x1.8470000000000p-48, f);
+    f = __builtin_fma(-q, -0x1.9d9cceba3f91fp-62, f);
+    const double z = f * f;
+    // fdlibm __kernel_sin / __kernel_cos on [-pi/4, pi/4]
+    const double rs = __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, 0x1.5d93a5acfd57cp-33,
+                                    -0x1.ae5e68a2b9cebp-26), 0x1.71de357b1fe7dp-19), -0x1.a01a019c161d5p-13),
+                                    0x1.111111110f8a6p-7);
+    const double s0 = __builtin_fma(z * f, __builtin_fma(z, rs, -0x1.5555555555549p-3), f);
+    const double rc = z * __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, __builtin_fma(z,
+                                    -0x1.8fae9be8838d4p-37, 0x1.1ee9ebdb4b1c4p-29), -0x1.27e4f809c52adp-22),
+                                    0x1.a01a019cb1590p-16), -0x1.6c16c16c15177p-10), 0x1.555555555554cp-5);
+    const double hz = 0.5 * z;
+    const double w = 1.0 - hz;
+    const double c0 = w + (((1.0 - w) - hz) + z * rc);
+    const int k = (int)__builtin_fma(-4.0, floor(q * 0.25), q);  // q mod 4, exact for |q| < 2^40
+    const double a = (k & 1) ? c0 : s0;  // sin(x) = s0, c0, -s0, -c0 for k = 0..3
+    const double b = (k & 1) ? s0 : c0;  // cos(x) = c0, -s0, -c0, s0
+    sn = (k & 2) ? -a : a;
+    cs = ((k + 1) & 2) ? -b : b;
+}
 
 __global__ void __launch_bounds__(kHuyBlock) k_huygens(const double* __restrict__ tx,
                                                        const double* __restrict__ ty,
@@ -69,11 +122,12 @@ __global__ void __launch_bounds__(kHuyBlock) k_huygens(const double* __restrict_
                 const double dx = px[t] - xj;
                 const double dy = py[t] - yj;
                 const double dz = pz[t] - zj;
-                const double r = sqrt(dx * dx + dy * dy + dz * dz);
-                const double amp = 1.0 / r;
+                const double r = sqrt_core(dx * dx + dy * dy + dz * dz);
+                double amp = __builtin_amdgcn_rcp(r);
+                amp = __builtin_fma(amp, __builtin_fma(-r, amp, 1.0), amp);
                 const double ph = negk * r;
                 double sn, cs;
-                sincos(ph, &sn, &cs);
+                sincos_phase(ph, sn, cs);
                 const double fr = amp * cs;
                 const double fi = amp * sn;
                 ar[t] = __builtin_fma(fr, ur, __builtin_fma(-fi, ui, ar[t]));
