@@ -156,6 +156,43 @@ __global__ void k_fill_nan(double* out, int64_t ld, int rows, int64_t n) {
 }
 
 // ----------------------------------------------------------------------------------------------
+// focus sweeps (find_defocus, ref AKB_raytrace_20250312.py:9086-9170): one set of rays against P
+// detector planes x = -j_p at once. Pass A writes each plane's hit y and z rows; pass B, given the
+// numpy-order sums of pass A, writes (y - mean)^2 and (z - mean)^2 — np.std's two passes, the
+// sums in between by akb_pairwise_sum_f64 so the result is numpy's to the bit.
+// ----------------------------------------------------------------------------------------------
+
+__global__ void __launch_bounds__(kBlock) k_plane_sweep(const double* __restrict__ dir, const double* __restrict__ pt,
+                                                        int64_t ld, const int64_t* __restrict__ subset, int64_t m,
+                                                        const double* __restrict__ plane_j, int P,
+                                                        const double* __restrict__ sums, double n_div,
+                                                        double* __restrict__ rows) {
+    const int p = blockIdx.y;
+    const double j = plane_j[p];
+    double my = 0.0, mz = 0.0;
+    if (sums) {  // np.mean: true_divide(sum, n)
+        my = sums[2 * p] / n_div;
+        mz = sums[2 * p + 1] / n_div;
+    }
+    double* ry = rows + (int64_t)(2 * p) * m;
+    double* rz = ry + m;
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = subset ? subset[k] : k;
+        double x, y, z;
+        plane_hit(1.0, 0.0, 0.0, j, dir[i], dir[ld + i], dir[2 * ld + i], pt[i], pt[ld + i], pt[2 * ld + i], x, y, z);
+        (void)x;
+        if (sums) {
+            const double dy = y - my, dz = z - mz;
+            ry[k] = dy * dy;
+            rz[k] = dz * dz;
+        } else {
+            ry[k] = y;
+            rz[k] = z;
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------------------------
 // fused chain: K mirrors (+ detector plane + OPL) per ray, all intermediate state in registers
 // ----------------------------------------------------------------------------------------------
 
@@ -960,6 +997,20 @@ int akb_tilt_opd_f64(const double ry[9], const double rz[9], const double center
     a.params = nullptr;
     return launch_tilt(a, det1_ghij, det2_ghij, dir, pt, opl, ld, n, dir_rot, pt_rot, det1, det2, total1, total2,
                        sink, stream);
+}
+
+int akb_plane_sweep_rows_f64(const double* dir, const double* pt, int64_t ld, int64_t n, const int64_t* subset,
+                             int64_t m, const double* d_plane_j, int P, const double* d_sums, double* rows,
+                             void* stream) {
+    clear_error();
+    AKB_REQUIRE(dir && pt && d_plane_j && rows, "null pointer");
+    AKB_REQUIRE(n >= 0 && ld >= n && m >= 0 && (subset || m == n), "bad sizes");
+    AKB_REQUIRE(P > 0 && P <= 32767, "1..32767 planes");
+    if (m == 0) return AKB_OK;
+    const unsigned gx = grid_for(m, 1, kStreamGridCap / P > 0 ? kStreamGridCap / P : 1);
+    k_plane_sweep<<<dim3(gx, P), kBlock, 0, (hipStream_t)stream>>>(dir, pt, ld, subset, m, d_plane_j, P, d_sums,
+                                                                   (double)m, rows);
+    return launch_status("k_plane_sweep");
 }
 
 int akb_tilt_params_f64(const double* d_sum5, const int64_t* d_cnt5, double* d_params, uint64_t* d_extent_keys,

@@ -200,6 +200,16 @@ int akb_tilt_opd_dev_f64(const double* d_params, const double det1_ghij[4], cons
                          double* dir_rot, double* pt_rot, double* det1, double* det2, double* total1,
                          double* total2, const akb_leaf_sink* sink, void* stream);
 
+/* Focus sweep rows (find_defocus, ref :9086-9170): for P detector planes x = -d_plane_j[p]
+ * (coefficients g = 1, h = i = 0, j = d_plane_j[p], as coeffs_det[9] = -(s2f_middle + a)), the
+ * hits of rays `subset` (m indices into the n rays; NULL = all, m = n) of (dir, pt), (3, ld) each.
+ * d_sums == NULL: rows (2P, m) = [y_p0, z_p0, y_p1, ...]; else, with d_sums the pairwise sums of
+ * those rows (akb_pairwise_sum_f64), rows = [(y - mean)^2, (z - mean)^2, ...], mean = sum / m
+ * (np.std's two passes; sum the second rows again and divide by m for the variance). */
+int akb_plane_sweep_rows_f64(const double* dir, const double* pt, int64_t ld, int64_t n, const int64_t* subset,
+                             int64_t m, const double* d_plane_j, int P, const double* d_sums, double* rows,
+                             void* stream);
+
 /* OPD maps (ref :3626, :3633, :3675-3677), with the means read from device memory as the tilt
  * sink left them (d_sum5 / d_cnt5 = sums and counts of det1_x, det1_y, det1_z, total1, total2;
  * mean = sum / count in float64):

@@ -436,6 +436,34 @@ def test_psf_errors(gpu):
         G.compute_psf_fft(np.zeros((4, 4)), np.zeros((4, 4)), 1e-9, 1e-6, 1e-2, window="tukey")
 
 
+# ----------------------------------------------------------------------------- focus sweeps
+
+def test_find_defocus_vs_reference(gpu):
+    """find_defocus on the reference's own 65x65 pass-2 rays: the first loop's np.std sizes on
+    all 50 planes bit for bit, and the search's answer exactly."""
+    from akbraytracing_amd import focus as F
+    f = golden("akb_focus_65.npz")
+    s2f = float(f["s2f_middle"])
+    sw = F.PlaneSweep(f["reflect4"], f["points"])
+    a = np.linspace(-0.3, 0.3, 50)
+    size_h, size_v = sw.std(np.array([-(s2f + a[i]) for i in range(50)]))
+    assert np.array_equal(size_h, f["size_h0"]) and np.array_equal(size_v, f["size_v0"])
+    assert F.find_defocus(f["reflect4"], f["points"], s2f, 0.0, 65, sweep=sw) == f["best_a"]
+
+
+def test_plane_sweep_subset_vs_oracle(gpu):
+    """compare_sep-style thinned subsets (every ray_num-th ray, :9277-9280) against the oracle's
+    plane intersection + np.std."""
+    from akbraytracing_amd import focus as F
+    f = golden("akb_focus_65.npz")
+    sub = np.arange(4225)[32::65]
+    j = -(float(f["s2f_middle"]) + np.linspace(-0.01, 0.01, 7))
+    sh, sv = F.plane_std_sweep(f["reflect4"], f["points"], j, subset=sub)
+    for p in range(7):
+        det = O.plane_ray_intersection([0] * 6 + [1.0, 0.0, 0.0, j[p]], f["reflect4"][:, sub], f["points"][:, sub])
+        assert sh[p] == np.std(det[1]) and sv[p] == np.std(det[2])
+
+
 # ----------------------------------------------------------------------------- psf_calc
 
 def test_rotate_with_nan_vs_oracle(gpu):
