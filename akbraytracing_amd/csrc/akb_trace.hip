@@ -193,6 +193,52 @@ __global__ void __launch_bounds__(kBlock) k_plane_sweep(const double* __restrict
 }
 
 // ----------------------------------------------------------------------------------------------
+// calc_dS (ref AKB_raytrace_20250312.py:13418-13473): the area element of each point of a (V, H)
+// grid of mirror points = half the summed |cross| of its four neighbour triangles (right-up,
+// up-left, left-down, down-right); border points take the value of the nearest interior point
+// (the reference's edge and corner copies are exactly that clamp).
+// ----------------------------------------------------------------------------------------------
+
+__device__ __forceinline__ double tri_area(double x0, double y0, double z0, double x1, double y1, double z1,
+                                           double x2, double y2, double z2) {
+    const double ax = x1 - x0, ay = y1 - y0, az = z1 - z0;
+    const double bx = x2 - x0, by = y2 - y0, bz = z2 - z0;
+    const double cx = ay * bz - az * by;  // np.cross
+    const double cy = az * bx - ax * bz;
+    const double cz = ax * by - ay * bx;
+    // np.linalg.norm of a 3-vector goes to BLAS ddot: x0 x0, then fma(x1, x1, .), fma(x2, x2, .)
+    return sqrt(__builtin_fma(cz, cz, __builtin_fma(cy, cy, cx * cx))) / 2.0;
+}
+
+__global__ void __launch_bounds__(kBlock) k_calc_ds(const double* __restrict__ pts, int64_t ld, int V, int H,
+                                                    double* __restrict__ out) {
+    const int64_t total = (int64_t)V * H;
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < total; k += (int64_t)gridDim.x * blockDim.x) {
+        const int i0 = (int)(k / H), j0 = (int)(k - (int64_t)i0 * H);
+        const int i = i0 < 1 ? 1 : (i0 > V - 2 ? V - 2 : i0);
+        const int j = j0 < 1 ? 1 : (j0 > H - 2 ? H - 2 : j0);
+        auto P = [&](int a, int b, double& x, double& y, double& z) {
+            const int64_t c = (int64_t)a * H + b;
+            x = pts[c];
+            y = pts[ld + c];
+            z = pts[2 * ld + c];
+        };
+        double px, py, pz, rx, ry, rz, ux, uy, uz, lx, ly, lz, dx, dy, dz;
+        P(i, j, px, py, pz);
+        P(i, j + 1, rx, ry, rz);
+        P(i, j - 1, lx, ly, lz);
+        P(i - 1, j, ux, uy, uz);
+        P(i + 1, j, dx, dy, dz);
+        double s = 0.0;
+        s = s + tri_area(px, py, pz, rx, ry, rz, ux, uy, uz);
+        s = s + tri_area(px, py, pz, ux, uy, uz, lx, ly, lz);
+        s = s + tri_area(px, py, pz, lx, ly, lz, dx, dy, dz);
+        s = s + tri_area(px, py, pz, dx, dy, dz, rx, ry, rz);
+        out[k] = s;
+    }
+}
+
+// ----------------------------------------------------------------------------------------------
 // fused chain: K mirrors (+ detector plane + OPL) per ray, all intermediate state in registers
 // ----------------------------------------------------------------------------------------------
 
@@ -1011,6 +1057,15 @@ int akb_plane_sweep_rows_f64(const double* dir, const double* pt, int64_t ld, in
     k_plane_sweep<<<dim3(gx, P), kBlock, 0, (hipStream_t)stream>>>(dir, pt, ld, subset, m, d_plane_j, P, d_sums,
                                                                    (double)m, rows);
     return launch_status("k_plane_sweep");
+}
+
+int akb_calc_ds_f64(const double* points, int64_t ld, int V, int H, double* d_out, void* stream) {
+    clear_error();
+    AKB_REQUIRE(points && d_out, "null pointer");
+    AKB_REQUIRE(V >= 3 && H >= 3 && ld >= (int64_t)V * H, "calc_dS needs a grid of at least 3 x 3 points");
+    const int64_t n = (int64_t)V * H;
+    k_calc_ds<<<grid_for(n, 1, kStreamGridCap), kBlock, 0, (hipStream_t)stream>>>(points, ld, V, H, d_out);
+    return launch_status("k_calc_ds");
 }
 
 int akb_tilt_params_f64(const double* d_sum5, const int64_t* d_cnt5, double* d_params, uint64_t* d_extent_keys,

@@ -1,0 +1,203 @@
+"""The on-disk hand-off between the ray tracer and the wave calculation.
+
+saveWaveData (AKB_raytrace_20250312.py:13475-13764) writes, per traced system, a folder holding
+  points_source.npy                  the source point (3,)
+  points_M1.npy .. points_M4.npy     mirror hit points + area elements (4, N): x, y, z, dS,
+                                     dS from calc_dS (:13418-13473) on the (V, H) ray grid
+  points_gridImage.npy               an image-plane grid (3, H_f * V_f) around the focus
+  points_gridDefocus.npy             the same at the defocused plane (when defocusForWave != 0)
+  calculation_conditions.txt         params and grid sizes, "key: value" lines
+and the Wavecalc_raytrace_fromData scripts read it back (CPU0402.py:195-380), propagate source ->
+M1 -> M2 (-> M3 -> M4) -> image grids with the Huygens sum and save complex_data_<name>.npz
+(key 'data'). Here calc_dS runs on the device, the writers reproduce the file set and the
+conditions text, read_conditions parses it as the Wavecalc driver does, and run_wave_chain is
+that driver's propagation chain on the device (wavecalc.WaveField3D).
+"""
+import os
+
+import numpy as np
+import torch
+
+from . import _lib
+from . import device as D
+
+
+def calc_dS(points, ray_num_V, ray_num_H):
+    """Drop-in for calc_dS: area elements (V, H) of a (3, V*H) grid of points, on the device."""
+    L = _lib.lib()
+    as_torch = isinstance(points, torch.Tensor)
+    p = points.to(device=D.device(), dtype=D.F64).contiguous() if as_torch else D.to_dev(points)
+    V, H = int(ray_num_V), int(ray_num_H)
+    out = torch.empty((V, H), dtype=D.F64, device=p.device)
+    _lib.check(L.akb_calc_ds_f64(D.ptr(p), int(p.shape[1]), V, H, D.ptr(out), D.stream_handle()))
+    return out if as_torch else out.cpu().numpy()
+
+
+def downsample_array_3_n(array_3_n, ray_num_V, ray_num_H, downsample_h, downsample_v):
+    """downsample_array_3_n (:13336-13356): keep every 2nd column downsample_h // 2 times and
+    every 2nd row downsample_v // 2 times. Returns (array, size_v, size_h)."""
+    a = np.asarray(array_3_n)
+    x = a.reshape(3, ray_num_V, ray_num_H)
+    for _ in range(downsample_h // 2):
+        x = x[:, :, ::2]
+    for _ in range(downsample_v // 2):
+        x = x[:, ::2, :]
+    return np.ascontiguousarray(x.reshape(3, -1)), x.shape[1], x.shape[2]
+
+
+def _host(a):
+    return a.detach().cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a)
+
+
+def image_grid(detcenter, size_h, size_v, ysize, zsize):
+    """The points_gridImage grid of :13644-13662: size_h x size_v points spanning +-ysize, +-zsize
+    around the centre of the hits' y / z extent, at x = mean(hits x)."""
+    d = _host(detcenter)
+    y, z = d[1, :], d[2, :]
+    y_grid = np.linspace((np.min(y) + np.max(y)) / 2 - ysize, (np.min(y) + np.max(y)) / 2 + ysize, size_h)
+    z_grid = np.linspace((np.min(z) + np.max(z)) / 2 - zsize, (np.min(z) + np.max(z)) / 2 + zsize, size_v)
+    yy, zz = np.meshgrid(y_grid, z_grid)
+    yf, zf = yy.flatten(), zz.flatten()
+    xf = np.full_like(yf, fill_value=np.mean(d[0, :]))
+    return np.vstack([xf, yf, zf]), y_grid, z_grid
+
+
+def save_wave_data(directory, source, mirrors, ray_num_V, ray_num_H, detcenter, detcenter2=None, params=None,
+                   ysize=1e-6, zsize=1e-6, defocus_for_wave=0.0, option_AKB=True, option_HighNA=True,
+                   option_2mirror=False, option_avrgsplt=False, timestamp=""):
+    """The file set of saveWaveData (:13498-13764) without downsampling (odd grids with the
+    reference's downsample factors at 0). mirrors: [M1, M2(, M3, M4)] hit points (3, V*H) in the
+    reference's naming (M1 = first vertical hyperbola, M2 = horizontal hyperbola, M3 / M4 the
+    ellipses). Returns the paths written."""
+    os.makedirs(directory, exist_ok=True)
+    written = []
+
+    def save(name, arr):
+        path = os.path.join(directory, name)
+        np.save(path, arr)
+        written.append(path)
+
+    src = _host(source)
+    save("points_source.npy", src[:, 0] if src.ndim == 2 else src)
+    for k, m in enumerate(mirrors):
+        pts = _host(m)
+        ds = _host(calc_dS(torch.as_tensor(pts), ray_num_V, ray_num_H))
+        save(f"points_M{k + 1}.npy", np.vstack((pts, ds.flatten())))
+    grid, y_grid, z_grid = image_grid(detcenter, ray_num_H, ray_num_V, ysize, zsize)
+    save("points_gridImage.npy", grid)
+    if detcenter2 is not None and abs(defocus_for_wave) > 1e-9:
+        span = 2e-7 + defocus_for_wave * (0.082 if option_HighNA else 0.01) * 2
+        grid2, _, _ = image_grid(detcenter2, ray_num_H, ray_num_V, span, span)
+        save("points_gridDefocus.npy", grid2)
+    p = np.zeros(26) if params is None else np.asarray(params)
+    path = os.path.join(directory, "calculation_conditions.txt")
+    with open(path, "w") as f:
+        f.write("Conditions\n")
+        f.write("====================\n")
+        f.write(f"time: {timestamp}\n")
+        f.write(f"params 0-1: {p[0:2]}\n")
+        f.write(f"params 2-7: {p[2:8]}\n")
+        f.write(f"params 8-13: {p[8:14]}\n")
+        f.write(f"params 14-19: {p[14:20]}\n")
+        f.write(f"params 20-26: {p[20:26]}\n")
+        f.write(f"grid pitch_y: {y_grid[1] - y_grid[0]}\n")
+        f.write(f"grid pitch_z: {z_grid[1] - z_grid[0]}\n")
+        f.write(f"grid size_y: {np.max(y_grid) - np.min(y_grid)}\n")
+        f.write(f"grid size_z: {np.max(z_grid) - np.min(z_grid)}\n")
+        f.write(f"grid pix_y: {ray_num_H}\n")
+        f.write(f"grid pix_z: {ray_num_V}\n")
+        f.write(f"grid pix_H1: {ray_num_H}\n")
+        f.write(f"grid pix_V1: {ray_num_V}\n")
+        f.write(f"grid pix_H2: {ray_num_H}\n")
+        f.write(f"grid pix_V2: {ray_num_V}\n")
+        f.write(f"option_AKB: {option_AKB}\n")
+        f.write(f"option_HighNA: {option_HighNA}\n")
+        f.write(f"defocusForWave: {defocus_for_wave}\n")
+        f.write(f"calc both mirrors?: {option_2mirror}\n")
+        f.write(f"option_avrgsplt: {option_avrgsplt}\n")
+        f.write("====================\n")
+    written.append(path)
+    return written
+
+
+def read_conditions(folder):
+    """calculation_conditions.txt read as the Wavecalc driver reads it (CPU0402.py:208-236)."""
+    c = {}
+    with open(os.path.join(folder, "calculation_conditions.txt")) as f:
+        for line in f:
+            v = line.split(":")[1].strip() if ":" in line else ""
+            if "grid pix_y:" in line:
+                c["pix_y"] = c["ray_num_H1"] = c["ray_num_H2"] = int(v)
+            elif "grid pix_z:" in line:
+                c["pix_z"] = c["ray_num_V1"] = c["ray_num_V2"] = int(v)
+            elif "grid pix_H:" in line:
+                c["ray_num_H1"] = c["ray_num_V2"] = int(v)
+            elif "grid pix_V:" in line:
+                c["ray_num_V1"] = c["ray_num_H2"] = int(v)
+            elif "grid pix_H1:" in line:
+                c["ray_num_H1"] = int(v)
+            elif "grid pix_V1:" in line:
+                c["ray_num_V1"] = int(v)
+            elif "grid pix_H2:" in line:
+                c["ray_num_H2"] = int(v)
+            elif "grid pix_V2:" in line:
+                c["ray_num_V2"] = int(v)
+            elif "option_AKB:" in line:
+                c["option_AKB"] = v.lower() == "true"
+            elif "option_HighNA:" in line:
+                c["option_HighNA"] = v.lower() == "true"
+    return c
+
+
+def run_wave_chain(folder, out_dir=None, files=("points_source.npy", "points_M1.npy", "points_M2.npy",
+                                                "points_gridImage.npy", "points_gridDefocus.npy")):
+    """The Wavecalc_raytrace_fromData driver (CPU0402.py:186-380) on the device: source -> M1 ->
+    M2 (-> M3 -> M4) -> image grid (scaled x2 about its mean) and the second image grid, saving
+    complex_data_<name>.npz (key 'data') into out_dir. Returns {name: field (numpy complex128)}."""
+    from .wavecalc import WaveField3D
+    cond = read_conditions(folder)
+    akb = cond.get("option_AKB", True)
+    wl = 13.5e-9 if cond.get("option_HighNA", True) else 13.5e-9 * 1e-1
+    load = lambda name: np.load(os.path.join(folder, name))  # noqa: E731
+    source = load(files[0])
+    fields = {}
+
+    def store(name, u):
+        fields[name] = np.asarray(u)
+        if out_dir is not None:
+            os.makedirs(out_dir, exist_ok=True)
+            np.savez_compressed(os.path.join(out_dir, f"complex_data_{name}.npz"), data=fields[name])
+
+    src = WaveField3D(1, wl, 1, 1)
+    src.u[0] = 1.0
+    src.setdata(source.reshape(3, 1))
+    src.set_ds(np.ones(1))
+    chain = ["points_M1.npy", "points_M2.npy"] + (["points_M3.npy", "points_M4.npy"] if akb else [])
+    dims = [(cond["ray_num_H1"], cond["ray_num_V1"]), (cond["ray_num_H2"], cond["ray_num_V2"])] * 2
+    prev = src
+    for k, fname in enumerate(chain):
+        pts = load(fname)
+        f = WaveField3D(pts.shape[1], wl, *dims[k])
+        f.setdata(pts)
+        f.forward_propagation(prev)
+        f.set_ds(pts[3, :])
+        store(f"M{k + 1}", f.u)
+        prev = f
+    img = load(files[3]).copy()
+    mean = [np.mean(img[0, :]), np.mean(img[1, :]), np.mean(img[2, :])]
+    for r in range(3):
+        img[r, :] = (img[r, :] - mean[r]) * 2. + mean[r]
+    g = WaveField3D(img.shape[1], wl, cond["pix_y"], cond["pix_z"])
+    g.setdata(img)
+    g.forward_propagation(prev)
+    store("Image", g.u)
+    if os.path.exists(os.path.join(folder, files[4])):
+        img2 = load(files[4]).copy()
+        mean2 = [np.mean(img2[0, :]), np.mean(img2[1, :]), np.mean(img2[2, :])]
+        for r in range(3):
+            img2[r, :] = (img2[r, :] - mean2[r]) + mean2[r]
+        g2 = WaveField3D(img2.shape[1], wl, cond["pix_y"], cond["pix_z"])
+        g2.setdata(img2)
+        g2.forward_propagation(prev)
+        store("Image2", g2.u)
+    return fields

@@ -210,6 +210,11 @@ int akb_plane_sweep_rows_f64(const double* dir, const double* pt, int64_t ld, in
                              int64_t m, const double* d_plane_j, int P, const double* d_sums, double* rows,
                              void* stream);
 
+/* calc_dS (ref :13418-13473): area element of each point of a (V, H) grid of mirror points
+ * (points (3, ld), flat index iv * H + ih): half the summed |cross| of the four neighbour
+ * triangles, border points copied from the nearest interior point. V, H >= 3. */
+int akb_calc_ds_f64(const double* points, int64_t ld, int V, int H, double* d_out, void* stream);
+
 /* OPD maps (ref :3626, :3633, :3675-3677), with the means read from device memory as the tilt
  * sink left them (d_sum5 / d_cnt5 = sums and counts of det1_x, det1_y, det1_z, total1, total2;
  * mean = sum / count in float64):

@@ -65,6 +65,8 @@ def lib():
         L.oracle_huygens.restype = None
         L.oracle_max_threads.restype = ctypes.c_int
         L.oracle_set_threads.argtypes = [ctypes.c_int]
+        L.oracle_calc_ds.argtypes = [ctypes.c_void_p, _i64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        L.oracle_calc_ds.restype = None
         _lib = L
     return _lib
 
@@ -229,4 +231,12 @@ def huygens_c(tx, ty, tz, sx, sy, sz, u_times_ds, k):
     out = np.empty(n, dtype=np.complex128)
     lib().oracle_huygens(_ptr(arrs[0]), _ptr(arrs[1]), _ptr(arrs[2]), n, _ptr(arrs[3]), _ptr(arrs[4]),
                          _ptr(arrs[5]), _ptr(u), m, float(k), _ptr(out))
+    return out
+
+
+def calc_dS(points, V, H):
+    """calc_dS (AKB_raytrace_20250312.py:13418-13473) -> (V, H)."""
+    p = np.ascontiguousarray(points, dtype=np.float64)
+    out = np.empty((V, H))
+    lib().oracle_calc_ds(_ptr(p), p.shape[1], int(V), int(H), _ptr(out))
     return out

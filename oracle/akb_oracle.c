@@ -253,6 +253,39 @@ void oracle_huygens(const double* tx, const double* ty, const double* tz, int64_
     }
 }
 
+/* calc_dS (AKB_raytrace_20250312.py:13418-13473): the triangle norms are np.linalg.norm of a
+ * 3-vector, which numpy hands to BLAS ddot; OpenBLAS accumulates x0*x0, then fma(x1, x1, .),
+ * then fma(x2, x2, .) — restated with explicit fma() (measured: bit-identical on the fixture). */
+static double tri_area(const double* p, const double* a, const double* b) {
+    double e1[3], e2[3];
+    for (int k = 0; k < 3; ++k) {
+        e1[k] = a[k] - p[k];
+        e2[k] = b[k] - p[k];
+    }
+    const double c0 = e1[1] * e2[2] - e1[2] * e2[1];
+    const double c1 = e1[2] * e2[0] - e1[0] * e2[2];
+    const double c2 = e1[0] * e2[1] - e1[1] * e2[0];
+    return sqrt(fma(c2, c2, fma(c1, c1, c0 * c0))) / 2;
+}
+
+void oracle_calc_ds(const double* pts, int64_t ld, int V, int H, double* out) {
+    for (int i0 = 0; i0 < V; ++i0)
+        for (int j0 = 0; j0 < H; ++j0) {
+            const int i = i0 < 1 ? 1 : (i0 > V - 2 ? V - 2 : i0);
+            const int j = j0 < 1 ? 1 : (j0 > H - 2 ? H - 2 : j0);
+            double q[5][3];
+            const int ii[5] = {i, i, i - 1, i, i + 1}, jj[5] = {j, j + 1, j, j - 1, j};  /* p, right, up, left, down */
+            for (int t = 0; t < 5; ++t)
+                for (int k = 0; k < 3; ++k) q[t][k] = pts[k * ld + (int64_t)ii[t] * H + jj[t]];
+            double s = 0.0;
+            s += tri_area(q[0], q[1], q[2]);
+            s += tri_area(q[0], q[2], q[3]);
+            s += tri_area(q[0], q[3], q[4]);
+            s += tri_area(q[0], q[4], q[1]);
+            out[(int64_t)i0 * H + j0] = s;
+        }
+}
+
 int oracle_max_threads(void) {
 #ifdef _OPENMP
     return omp_get_max_threads();

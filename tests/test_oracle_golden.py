@@ -182,3 +182,11 @@ def test_oracle_psf_calc_matches_reference():
     assert r["psf_trimmed"].shape == f["psf_trimmed"].shape
     assert np.max(np.abs(r["psf_trimmed"] - f["psf_trimmed"])) <= 1e-12
     assert np.array_equal(r["x_im"], f["x_im"])
+
+
+def test_oracle_calc_ds_matches_reference():
+    """calc_dS on the four mirror grids of the reference's 65x65 run, bit for bit."""
+    f = golden("akb_raywave_65.npz")
+    d = golden("wavedata_65.npz")
+    for k in range(4):
+        assert np.array_equal(O.calc_dS(f["pass2_hits"][k], 65, 65), d["ds"][k])
