@@ -40,6 +40,7 @@ EXPORTS = [
     "akb_huygens_work_bytes", "akb_huygens_f64", "akb_scale_field_f64",
     "akb_psf_work_bytes", "akb_psf_f64", "akb_psf_release_plans", "akb_selftest_arith_f64",
     "akb_first_valid_rows_f64", "akb_rotate_work_bytes", "akb_rotate_with_nan_f64",
+    "akb_moments_work_bytes", "akb_map_moments_f64", "akb_plane_subtract_f64", "akb_legendre_rows_f64",
 ]
 
 
@@ -128,6 +129,11 @@ def _declare(L):
         "akb_first_valid_rows_f64": ([c_vp, c_int, c_int, c_vp, c_vp], c_int),
         "akb_rotate_work_bytes": ([c_int, c_int], c_i64),
         "akb_rotate_with_nan_f64": ([c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp], c_int),
+        "akb_moments_work_bytes": ([], c_i64),
+        "akb_map_moments_f64": ([c_vp, c_int, c_int, c_int, c_vp, c_dbl, c_int, c_dbl, c_vp, c_vp, c_vp], c_int),
+        "akb_plane_subtract_f64": ([c_vp, c_int, c_int, c_vp, c_vp, c_vp], c_int),
+        "akb_legendre_rows_f64": ([c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp],
+                                  c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

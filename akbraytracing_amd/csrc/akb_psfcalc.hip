@@ -111,6 +111,148 @@ __global__ void k_rotate_cubic(RotArgs a) {
     }
 }
 
+// ---- plane_correction_with_nan_and_outlier_filter (ref :9630-9693) and match_legendre (:59-73) ----
+//
+// Both are least-squares / projection steps over a 2-D map with NaNs. The device forms the sums
+// (per-workgroup partials in a fixed order, then one workgroup adds them in order: deterministic),
+// the host solves the 5 x 5 / 3 x 3 normal equations. Basis: 1, X, Y, X^2, Y^2 with X, Y the
+// column / row index centred and scaled to [-1, 1] (the same least-squares plane as the
+// reference's x, y indices, better conditioned).
+
+constexpr int kMomMax = 21;  // 15 (upper triangle of 5 x 5) + 5 (rhs) + 1 (count)
+
+struct MomArgs {
+    const double* z;
+    int ny, nx;
+    int nb;                 // basis size: 5 (quadratic) or 3 (plane)
+    const double* coef;     // NULL: all finite points; else keep |z - model(coef, 5 terms)| < thr
+    double thr;
+    int mode;               // 0: normal-equation sums; 1: residual sum; 2: residual sum of squares
+    double mean;            // mode 2: residual mean
+    double* part;           // (gridDim.x, kMomMax)
+};
+
+__device__ __forceinline__ void basis5(int i, int j, int ny, int nx, double (&f)[5]) {
+    const double X = nx > 1 ? (2.0 * j - (nx - 1)) / (double)(nx - 1) : 0.0;
+    const double Y = ny > 1 ? (2.0 * i - (ny - 1)) / (double)(ny - 1) : 0.0;
+    f[0] = 1.0;
+    f[1] = X;
+    f[2] = Y;
+    f[3] = X * X;
+    f[4] = Y * Y;
+}
+
+__global__ void __launch_bounds__(kBlock) k_moments(MomArgs a) {
+    __shared__ double red[kBlock / 64][kMomMax];
+    double acc[kMomMax];
+#pragma unroll
+    for (int q = 0; q < kMomMax; ++q) acc[q] = 0.0;
+    const int64_t total = (int64_t)a.ny * a.nx;
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < total; k += (int64_t)gridDim.x * blockDim.x) {
+        const double z = a.z[k];
+        if (z != z) continue;
+        const int i = (int)(k / a.nx), j = (int)(k - (int64_t)i * a.nx);
+        double f[5];
+        basis5(i, j, a.ny, a.nx, f);
+        double res = 0.0;
+        if (a.coef || a.mode > 0) {
+            double m = 0.0;
+            for (int t = 0; t < 5; ++t) m = __builtin_fma(a.coef[t], f[t], m);
+            res = z - m;
+            if (a.mode == 0 && !(fabs(res) < a.thr)) continue;
+        }
+        if (a.mode == 1) {
+            acc[0] += res;
+            acc[20] += 1.0;
+        } else if (a.mode == 2) {
+            const double d = res - a.mean;
+            acc[0] = __builtin_fma(d, d, acc[0]);
+            acc[20] += 1.0;
+        } else {
+            const bool quad = a.nb == 5;
+#pragma unroll
+            for (int r = 0; r < 5; ++r) {
+#pragma unroll
+                for (int c = r; c < 5; ++c) {
+                    const int q = r * 5 - r * (r - 1) / 2 + (c - r);  // upper-triangle slot
+                    if (quad || c < 3) acc[q] = __builtin_fma(f[r], f[c], acc[q]);
+                }
+                if (quad || r < 3) acc[15 + r] = __builtin_fma(f[r], z, acc[15 + r]);
+            }
+            acc[20] += 1.0;
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < kMomMax; ++q)
+        for (int off = 32; off > 0; off >>= 1) acc[q] += __shfl_down(acc[q], off);
+    if ((threadIdx.x & 63) == 0)
+        for (int q = 0; q < kMomMax; ++q) red[threadIdx.x >> 6][q] = acc[q];
+    __syncthreads();
+    if (threadIdx.x < kMomMax) {
+        double v = red[0][threadIdx.x];
+        for (int w = 1; w < kBlock / 64; ++w) v += red[w][threadIdx.x];
+        a.part[(int64_t)blockIdx.x * kMomMax + threadIdx.x] = v;
+    }
+}
+
+__global__ void k_moments_final(const double* part, int nparts, double* out) {
+    const int q = threadIdx.x;
+    if (q >= kMomMax) return;
+    double v = 0.0;
+    for (int b = 0; b < nparts; ++b) v += part[(int64_t)b * kMomMax + q];
+    out[q] = v;
+}
+
+// out = z - plane(coef, 3 terms); NaN where z is NaN
+__global__ void __launch_bounds__(kBlock) k_plane_subtract(const double* __restrict__ z, int ny, int nx,
+                                                           const double* __restrict__ coef, double* __restrict__ out) {
+    const int64_t total = (int64_t)ny * nx;
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < total; k += (int64_t)gridDim.x * blockDim.x) {
+        const int i = (int)(k / nx), j = (int)(k - (int64_t)i * nx);
+        double f[5];
+        basis5(i, j, ny, nx, f);
+        const double m = __builtin_fma(coef[2], f[2], __builtin_fma(coef[1], f[1], coef[0] * f[0]));
+        const double v = z[k];
+        out[k] = v != v ? v : v - m;
+    }
+}
+
+// match_legendre_multi (legendre_fit.py:59-92) on an n x n map. Z_k = outer(Py[ny_k], Px[nx_k])
+// (the product np.outer forms), then per k: s_k = nansum(Z*Z), Zn = Z / sqrt(s_k),
+// c_k = nansum(Zn * data), fit_k = c_k * Zn. This kernel writes the rows that numpy sums (mode 0:
+// Z*Z, mode 1: Zn*data) and the fits (mode 2); the sums themselves are akb_pairwise_sum_f64's, in
+// numpy's pairwise order, so the coefficients match the reference's bit for bit.
+struct LegArgs {
+    const double* data;
+    int n, K, order;
+    const double* px;   // (order, n): P_j(linspace(-1, 1, n)) for the columns
+    const double* py;   // (order, n): for the rows
+    const int* ord;     // (K, 2): (ny, nx)
+    const double* s;    // (K,) nansum(Z*Z)    modes 1, 2
+    const double* c;    // (K,) coefficients   mode 2
+    int mode;
+    double* out;        // (K, n*n)
+};
+
+__global__ void __launch_bounds__(kBlock) k_legendre_rows(LegArgs a) {
+    const int64_t nn = (int64_t)a.n * a.n, total = nn * a.K;
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+        const int k = (int)(t / nn);
+        const int64_t p = t - (int64_t)k * nn;
+        const int r = (int)(p / a.n), col = (int)(p - (int64_t)r * a.n);
+        const int ny = a.ord[2 * k], nx = a.ord[2 * k + 1];
+        const double z = a.py[(int64_t)ny * a.n + r] * a.px[(int64_t)nx * a.n + col];
+        double v;
+        if (a.mode == 0) {
+            v = z * z;
+        } else {
+            const double zn = z / sqrt_cr(a.s[k]);
+            v = a.mode == 1 ? zn * a.data[p] : a.c[k] * zn;
+        }
+        a.out[t] = v;
+    }
+}
+
 }  // namespace akb
 
 using namespace akb;
@@ -143,6 +285,45 @@ int akb_rotate_with_nan_f64(const double* m, int ny, int nx, const double rot[4]
     RotArgs a{coef, ny, nx, rot[0], rot[1], rot[2], rot[3], offset[0], offset[1], rotated, opd_m};
     k_rotate_cubic<<<grid_for(n), kBlock, 0, s>>>(a);
     return launch_status("k_rotate_cubic");
+}
+
+int64_t akb_moments_work_bytes(void) { return (int64_t)(512 * kMomMax + kMomMax) * 8; }
+
+int akb_map_moments_f64(const double* z, int ny, int nx, int nb, const double* d_coef, double thr, int mode,
+                        double mean, double* d_out, void* work, void* stream) {
+    clear_error();
+    AKB_REQUIRE(z && d_out && work && ny > 0 && nx > 0, "bad arguments");
+    AKB_REQUIRE(nb == 3 || nb == 5, "basis of 3 or 5 terms");
+    AKB_REQUIRE(mode >= 0 && mode <= 2 && (mode == 0 || d_coef), "bad mode");
+    hipStream_t s = (hipStream_t)stream;
+    MomArgs a{z, ny, nx, nb, d_coef, thr, mode, mean, (double*)work};
+    const int64_t n = (int64_t)ny * nx;
+    const unsigned g = grid_for(n, 4) < 512 ? grid_for(n, 4) : 512;
+    k_moments<<<g, kBlock, 0, s>>>(a);
+    int st = launch_status("k_moments");
+    if (st) return st;
+    k_moments_final<<<1, 64, 0, s>>>((double*)work, (int)g, d_out);
+    return launch_status("k_moments_final");
+}
+
+int akb_plane_subtract_f64(const double* z, int ny, int nx, const double* d_coef3, double* out, void* stream) {
+    clear_error();
+    AKB_REQUIRE(z && d_coef3 && out && ny > 0 && nx > 0, "bad arguments");
+    k_plane_subtract<<<grid_for((int64_t)ny * nx), kBlock, 0, (hipStream_t)stream>>>(z, ny, nx, d_coef3, out);
+    return launch_status("k_plane_subtract");
+}
+
+int akb_legendre_rows_f64(const double* data, int n, int K, int order, const double* px, const double* py,
+                          const int* ord, const double* s, const double* c, int mode, double* out, void* stream) {
+    clear_error();
+    AKB_REQUIRE(n > 0 && K > 0 && order > 0 && px && py && ord && out, "bad arguments");
+    AKB_REQUIRE(mode >= 0 && mode <= 2, "mode 0, 1 or 2");
+    AKB_REQUIRE(mode == 0 || s, "mode 1 / 2 need the norms");
+    AKB_REQUIRE(mode != 1 || data, "mode 1 needs the map");
+    AKB_REQUIRE(mode != 2 || c, "mode 2 needs the coefficients");
+    LegArgs a{data, n, K, order, px, py, ord, s, c, mode, out};
+    k_legendre_rows<<<grid_for((int64_t)n * n * K), kBlock, 0, (hipStream_t)stream>>>(a);
+    return launch_status("k_legendre_rows");
 }
 
 }  // extern "C"

@@ -1,0 +1,128 @@
+"""Pupil-map post-processing of the 'ray_wave' driver, device-backed.
+
+plane_correction_with_nan_and_outlier_filter (AKB_raytrace_20250312.py:9630-9693) removes the
+best plane from the gridded wavefront: a quadratic least-squares fit over the finite points, the
+residual's 3-sigma outliers dropped, a plane refit over the rest, the plane subtracted with the
+NaNs kept. The reference fits with scipy's curve_fit (Levenberg-Marquardt on the same linear
+models); the fits are linear least squares, so their solutions are the normal-equation
+solutions: the device forms the sums (akb_map_moments_f64), the host solves 5 x 5 and 3 x 3
+systems, the device subtracts (akb_plane_subtract_f64). Agreement with the reference is to the
+fit's rounding (~1e-13 of the map's range), not bit for bit: curve_fit's iterations stop at their
+own tolerance.
+
+match_legendre_multi (legendre_fit.py:75-92) projects a square map on unit-norm Legendre
+products: the rows numpy sums are formed on the device (akb_legendre_rows_f64) and summed in
+numpy's pairwise order (akb_pairwise_sum_f64), so the inner products are the reference's own.
+"""
+import numpy as np
+import torch
+from scipy.special import legendre
+
+from . import _lib
+from . import device as D
+from .reduce import RowSums
+
+_SLOT = {}
+for _r in range(5):
+    for _c in range(_r, 5):
+        _SLOT[(_r, _c)] = _r * 5 - _r * (_r - 1) // 2 + (_c - _r)
+
+
+def _as_dev(m):
+    if isinstance(m, torch.Tensor):
+        return m.to(device=D.device(), dtype=D.F64).contiguous()
+    return D.to_dev(np.ascontiguousarray(m, dtype=np.float64))
+
+
+def _normal_solve(mom, nb):
+    A = np.empty((nb, nb))
+    for r in range(nb):
+        for c in range(nb):
+            A[r, c] = mom[_SLOT[(min(r, c), max(r, c))]]
+    b = mom[15:15 + nb]
+    return np.linalg.solve(A, b)
+
+
+class _Moments:
+    def __init__(self, dev):
+        L = _lib.lib()
+        self.work = torch.empty(int(L.akb_moments_work_bytes()) // 8, dtype=D.F64, device=dev)
+        self.out = torch.empty(21, dtype=D.F64, device=dev)
+
+    def __call__(self, z, nb, coef=None, thr=0.0, mode=0, mean=0.0):
+        L = _lib.lib()
+        ny, nx = int(z.shape[0]), int(z.shape[1])
+        _lib.check(L.akb_map_moments_f64(D.ptr(z), ny, nx, nb, D.ptr(coef), float(thr), mode, float(mean),
+                                         D.ptr(self.out), D.ptr(self.work), D.stream_handle()))
+        return self.out.cpu().numpy()
+
+
+def plane_correction_with_nan_and_outlier_filter(data, sigma_threshold=3):
+    """Drop-in for the reference function: same arguments, same result (NaNs kept). A torch
+    input returns a device tensor, a numpy input a numpy array."""
+    as_torch = isinstance(data, torch.Tensor)
+    z = _as_dev(data)
+    if z.dim() != 2:
+        raise ValueError("data must be 2-D")
+    mom = _Moments(z.device)
+    m0 = mom(z, 5)
+    if m0[20] < 5:
+        # curve_fit refuses fewer points than parameters (:9667)
+        raise TypeError(f"Improper input: func (m=5) must not exceed the data count N={int(m0[20])}")
+    p1 = _normal_solve(m0, 5)
+    c1 = torch.from_numpy(p1).to(z.device)
+    cnt = mom(z, 5, c1, mode=1)
+    mean = cnt[0] / cnt[20]
+    ss = mom(z, 5, c1, mode=2, mean=mean)
+    sigma = np.sqrt(ss[0] / cnt[20])
+    m1 = mom(z, 3, c1, thr=sigma_threshold * sigma)
+    if m1[20] < 3:
+        raise TypeError(f"Improper input: func (m=3) must not exceed the data count N={int(m1[20])}")
+    p2 = torch.from_numpy(_normal_solve(m1, 3)).to(z.device)
+    out = torch.empty_like(z)
+    _lib.check(_lib.lib().akb_plane_subtract_f64(D.ptr(z), int(z.shape[0]), int(z.shape[1]), D.ptr(p2),
+                                                 D.ptr(out), D.stream_handle()))
+    return out if as_torch else out.cpu().numpy()
+
+
+def legendre_orders(order):
+    """(ny, nx) pairs in match_legendre_multi's order (legendre_fit.py:82-90)."""
+    return [(i - j, j) for i in range(order) for j in range(i + 1)]
+
+
+def match_legendre_multi(data, order):
+    """Drop-in for legendre_fit.match_legendre_multi: (fit_datas (K, n, n), inner_products (K,),
+    orders [(ny, nx), ...]). numpy in, numpy out; a torch input returns device tensors."""
+    as_torch = isinstance(data, torch.Tensor)
+    z = _as_dev(data)
+    n0, n1 = int(z.shape[0]), int(z.shape[1])
+    if n0 != n1:
+        # the reference's Z is (n1, n0) against data (n0, n1): numpy refuses the product
+        raise ValueError(f"operands could not be broadcast together with shapes ({n1},{n0}) ({n0},{n1})")
+    n, order = n0, int(order)
+    orders = legendre_orders(order)
+    K = len(orders)
+    x = np.linspace(-1, 1, n)
+    tab = np.stack([legendre(k)(x) for k in range(order)])  # scipy's poly1d values, as the reference
+    dev = z.device
+    pxy = torch.from_numpy(np.ascontiguousarray(tab)).to(dev)
+    ordt = torch.tensor(np.array(orders, dtype=np.int32).ravel(), device=dev)
+    rows = torch.empty((K, n * n), dtype=D.F64, device=dev)
+    L = _lib.lib()
+    sums = RowSums()
+
+    def run(mode, s=None, c=None):
+        _lib.check(L.akb_legendre_rows_f64(D.ptr(z), n, K, order, D.ptr(pxy), D.ptr(pxy), D.ptr(ordt), D.ptr(s),
+                                           D.ptr(c), mode, D.ptr(rows), D.stream_handle()))
+
+    run(0)
+    s, _ = sums(rows, nan=True)
+    s = s.clone()
+    run(1, s)
+    c, _ = sums(rows, nan=True)
+    c = c.clone()
+    run(2, s, c)
+    fits = rows.view(K, n, n)
+    if as_torch:
+        return fits, c, [tuple(o) for o in orders]
+    return fits.cpu().numpy(), c.cpu().numpy(), [tuple(o) for o in orders]

@@ -299,6 +299,31 @@ int64_t akb_rotate_work_bytes(int ny, int nx);
 int akb_rotate_with_nan_f64(const double* m, int ny, int nx, const double rot[4], const double offset[2],
                             double* rotated, double* opd_m, void* work, void* stream);
 
+/* ---------------- pupil-map post-processing (ref AKB_raytrace_20250312.py:9630-9693, legendre_fit.py:59-92) ---------------- */
+
+/* Sums for plane_correction_with_nan_and_outlier_filter (:9630) over the finite points of the
+ * (ny, nx) map z, basis f = (1, X, Y, X^2, Y^2) with X = (2j - (nx-1))/(nx-1), Y likewise
+ * (the reference's index coordinates, centred and scaled: the same least-squares fits).
+ *   mode 0: normal equations of an nb-term fit (nb 3 or 5): d_out[0..14] upper triangle of
+ *           sum f f^T (row-major, 5 x 5 slots), d_out[15..19] sum f z, d_out[20] count; with
+ *           d_coef (5 terms) only points with |z - f.coef| < thr count (the 3-sigma filter).
+ *   mode 1: d_out[0] = sum (z - f.coef), d_out[20] = count   (residual mean, :9672)
+ *   mode 2: d_out[0] = sum (z - f.coef - mean)^2             (np.std of the residual, :9675)
+ * The host solves the 5 x 5 / 3 x 3 systems. work: akb_moments_work_bytes(). Deterministic. */
+int64_t akb_moments_work_bytes(void);
+int akb_map_moments_f64(const double* z, int ny, int nx, int nb, const double* d_coef, double thr, int mode,
+                        double mean, double* d_out, void* work, void* stream);
+/* out = z - (c0 + c1 X + c2 Y), NaN kept (:9688-9691); d_coef3 on the device */
+int akb_plane_subtract_f64(const double* z, int ny, int nx, const double* d_coef3, double* out, void* stream);
+
+/* match_legendre_multi rows (legendre_fit.py:59-92) on an n x n map, K = order(order+1)/2
+ * components with (ny, nx) = ord[2k], ord[2k+1]; px / py (order, n) the Legendre polynomials on
+ * linspace(-1, 1, n) (host-evaluated with scipy.special.legendre, as the reference does).
+ * mode 0: out[k] = Z_k * Z_k;  mode 1: out[k] = Z_k / sqrt(s[k]) * data;  mode 2: out[k] = c[k] * Z_k / sqrt(s[k]).
+ * The nansums of modes 0 and 1 are akb_pairwise_sum_f64's rows (nan_mask 1). */
+int akb_legendre_rows_f64(const double* data, int n, int K, int order, const double* px, const double* py,
+                          const int* ord, const double* s, const double* c, int mode, double* out, void* stream);
+
 /* diagnostics: out4[4i..4i+3] = (the trace's sqrt, sqrt, the trace's shared-reciprocal a/b, a/b)
  * for n pairs (a[i], b[i]) — used by the tests to check the shortcuts bit for bit */
 int akb_selftest_arith_f64(const double* a, const double* b, int64_t n, double* out4, void* stream);

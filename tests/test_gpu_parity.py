@@ -541,6 +541,76 @@ def test_psf_calc_vs_reference(gpu, tmp_path):
     assert np.load(tmp_path / "psf.npy").shape == (1056, 1056)
 
 
+# ----------------------------------------------------------------------------- pupil map
+
+def test_plane_correction_vs_reference(gpu):
+    """plane_correction_with_nan_and_outlier_filter on the reference's 65x65 ray_wave map:
+    1e-12 of the map's range (curve_fit's own tolerance; observed ~4e-14 nm on 0.23 nm)."""
+    from akbraytracing_amd import pupilmap as PM
+    f = golden("akb_psfcalc_65.npz")
+    got = PM.plane_correction_with_nan_and_outlier_filter(f["plane_in"])
+    want = f["plane_out"]
+    assert np.array_equal(np.isnan(got), np.isnan(want))
+    assert np.nanmax(np.abs(got - want)) <= 1e-12 * (np.nanmax(want) - np.nanmin(want))
+
+
+@pytest.mark.parametrize("ny,nx", [(65, 65), (40, 97), (513, 511)])
+def test_plane_correction_vs_oracle(gpu, ny, nx):
+    """NaN border, a tilted quadratic, noise and injected outliers that the 3-sigma filter drops."""
+    from akbraytracing_amd import pupilmap as PM
+    import oracle.pupilmap as OPM
+    rng = np.random.default_rng(ny * 1000 + nx)
+    y, x = np.mgrid[0:ny, 0:nx].astype(np.float64)
+    m = 0.3 + 0.02 * x - 0.01 * y + 1e-4 * x * x + 3e-5 * y * y + 0.01 * rng.standard_normal((ny, nx))
+    m[((x - nx / 2) / (nx / 2)) ** 2 + ((y - ny / 2) / (ny / 2)) ** 2 > 0.9] = np.nan
+    idx = rng.choice(ny * nx, size=max(3, ny * nx // 200), replace=False)
+    m.flat[idx] += 0.5 * rng.choice([-1, 1], size=idx.size)
+    want = OPM.plane_correction_with_nan_and_outlier_filter(m)
+    got = PM.plane_correction_with_nan_and_outlier_filter(m)
+    assert np.array_equal(np.isnan(got), np.isnan(want))
+    assert np.nanmax(np.abs(got - want)) <= 1e-11 * (np.nanmax(want) - np.nanmin(want))
+    t = PM.plane_correction_with_nan_and_outlier_filter(torch.from_numpy(m).to(gpu))
+    assert t.is_cuda and np.array_equal(t.cpu().numpy(), got, equal_nan=True)
+
+
+def test_plane_correction_too_few_points(gpu):
+    from akbraytracing_amd import pupilmap as PM
+    m = np.full((8, 8), np.nan)
+    m[0, :3] = 1.0
+    with pytest.raises(TypeError):
+        PM.plane_correction_with_nan_and_outlier_filter(m)
+
+
+def test_match_legendre_multi_vs_reference(gpu):
+    """legendre_fit.match_legendre_multi on the 65x65 wave map: inner products and fits bit for
+    bit (numpy-order nansums on the device, scipy's Legendre values)."""
+    from akbraytracing_amd import pupilmap as PM
+    d = golden("legendre_cases.npz")
+    fits, coefs, orders = PM.match_legendre_multi(d["wave_map"], 5)
+    assert orders == [tuple(o) for o in d["orders"]]
+    assert np.array_equal(coefs, d["coefs"])
+    assert np.array_equal(fits, d["fit"])
+
+
+def test_match_legendre_multi_nan_and_nonsquare(gpu):
+    from akbraytracing_amd import pupilmap as PM
+    rng = np.random.default_rng(5)
+    m = rng.standard_normal((62, 62))
+    m[:3, :] = np.nan
+    m[10:20, 40:50] = np.nan
+    got_f, got_c, _ = PM.match_legendre_multi(m, 4)
+    from scipy.special import legendre
+    xs = np.linspace(-1, 1, 62)
+    for k, (ny, nx) in enumerate(PM.legendre_orders(4)):
+        Z = np.outer(legendre(ny)(xs), legendre(nx)(xs))
+        Z /= np.sqrt(np.nansum(Z * Z))
+        c = np.nansum(Z * m)
+        assert got_c[k] == c
+        assert np.array_equal(got_f[k], c * Z)
+    with pytest.raises(ValueError):
+        PM.match_legendre_multi(np.zeros((4, 5)), 3)
+
+
 # ----------------------------------------------------------------------------- Huygens
 
 def test_huygens_cases(gpu):

@@ -190,3 +190,14 @@ def test_oracle_calc_ds_matches_reference():
     d = golden("wavedata_65.npz")
     for k in range(4):
         assert np.array_equal(O.calc_dS(f["pass2_hits"][k], 65, 65), d["ds"][k])
+
+
+def test_plane_correction_oracle_vs_reference():
+    """oracle/pupilmap restates plane_correction_with_nan_and_outlier_filter (:9630) as lstsq;
+    the reference's own curve_fit output on its 65x65 ray_wave map pins it."""
+    import oracle.pupilmap as PM
+    f = golden("akb_psfcalc_65.npz")
+    got = PM.plane_correction_with_nan_and_outlier_filter(f["plane_in"])
+    want = f["plane_out"]
+    assert np.array_equal(np.isnan(got), np.isnan(want))
+    assert np.nanmax(np.abs(got - want)) <= 1e-12 * (np.nanmax(want) - np.nanmin(want))
