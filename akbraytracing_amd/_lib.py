@@ -41,6 +41,7 @@ EXPORTS = [
     "akb_psf_work_bytes", "akb_psf_f64", "akb_psf_release_plans", "akb_selftest_arith_f64",
     "akb_first_valid_rows_f64", "akb_rotate_work_bytes", "akb_rotate_with_nan_f64",
     "akb_moments_work_bytes", "akb_map_moments_f64", "akb_plane_subtract_f64", "akb_legendre_rows_f64",
+    "akb_gd_cells_f64", "akb_gd_pockets", "akb_gd_check_pockets", "akb_gd_grad_sweep_f64", "akb_gd_eval_f64",
 ]
 
 
@@ -134,6 +135,14 @@ def _declare(L):
         "akb_plane_subtract_f64": ([c_vp, c_int, c_int, c_vp, c_vp, c_vp], c_int),
         "akb_legendre_rows_f64": ([c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp],
                                   c_int),
+        "akb_gd_cells_f64": ([c_vp, c_vp, c_int, c_int, c_vp, c_dbl, c_vp, c_vp, c_vp, c_vp], c_int),
+        "akb_gd_pockets": ([c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp], c_int),
+        "akb_gd_check_pockets": ([c_vp, c_vp, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_dbl, c_vp, c_vp],
+                                 c_int),
+        "akb_gd_grad_sweep_f64": ([c_vp, c_vp, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
+                                   c_vp, c_vp, c_vp, c_vp], c_int),
+        "akb_gd_eval_f64": ([c_vp, c_vp, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int,
+                             c_vp, c_vp, c_int, c_vp, c_vp, c_vp], c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

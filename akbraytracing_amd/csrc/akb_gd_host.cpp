@@ -1,0 +1,183 @@
+// Host half of the structured Delaunay triangulation used by the device griddata (akb_griddata.hip).
+//
+// griddata(points, values, xi, method='cubic') (scipy 1.15, called at AKB_raytrace_20250312.py:3673
+// and :3689) triangulates the scattered points with qhull's Delaunay. The points here are the
+// detector hits of an n_v x n_h ray grid, a smoothly deformed lattice: its Delaunay triangulation
+// is every grid cell split by the diagonal that passes the in-circle test (the device does that)
+// plus the "pockets" between the grid's boundary ring and its convex hull. This file triangulates
+// the pockets: hull of the ring (Andrew's monotone chain, collinear and rounding-level collinear
+// points kept), then, for every
+// hull edge (p, q) that skips ring points, the Delaunay triangle on its inner side - the chain
+// point seeing (p, q) under the largest angle (its circumcircle holds no other chain point) - and
+// the same for the two sub-chains it leaves. The device checks the result is locally Delaunay
+// against the cell triangles it borders.
+#include <math.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "akb_common.h"
+
+namespace {
+
+struct Ring {
+    int nv, nh;
+    int64_t L;
+    int64_t vertex(int64_t r) const {  // ring position -> global vertex id (row-major iv * nh + ih)
+        r %= L;
+        const int64_t a = nh - 1, b = nv - 1;
+        if (r < a) return r;                                        // bottom row, ih = r
+        if (r < a + b) return (r - a) * nh + (nh - 1);              // right column, iv = r - a
+        if (r < 2 * a + b) return (int64_t)(nv - 1) * nh + (nh - 1 - (r - a - b));  // top row
+        return (int64_t)(nv - 1 - (r - 2 * a - b)) * nh;           // left column
+    }
+    bool corner(int64_t r) const {
+        r %= L;
+        const int64_t a = nh - 1, b = nv - 1;
+        return r == 0 || r == a || r == a + b || r == 2 * a + b;
+    }
+};
+
+double cross3(const double* x, const double* y, int64_t o, int64_t a, int64_t b) {
+    return (x[a] - x[o]) * (y[b] - y[o]) - (y[a] - y[o]) * (x[b] - x[o]);
+}
+
+// a strict right turn o -> a -> b, beyond rounding: qhull merges the slivers that rounding-level
+// bends of a straight boundary would make (sin of the bend below 1e-12 counts as straight)
+bool right_turn(const double* x, const double* y, int64_t o, int64_t a, int64_t b) {
+    const double c = cross3(x, y, o, a, b);
+    const double la = hypot(x[a] - x[o], y[a] - y[o]), lb = hypot(x[b] - x[o], y[b] - y[o]);
+    return c < -1e-12 * la * lb;
+}
+
+}  // namespace
+
+using namespace akb;
+
+extern "C" {
+
+int akb_gd_pockets(const double* rx, const double* ry, int nv, int nh, int cap, int32_t* n_out, int32_t* tri,
+                   int32_t* nbr, int32_t* edge_tri, int32_t* extra_ptr, int32_t* extra_idx) {
+    clear_error();
+    AKB_REQUIRE(rx && ry && n_out && tri && nbr && edge_tri && extra_ptr && extra_idx, "null pointer");
+    AKB_REQUIRE(nv >= 2 && nh >= 2, "grid of at least 2 x 2 points");
+    Ring R{nv, nh, 2 * (int64_t)(nh - 1) + 2 * (int64_t)(nv - 1)};
+    const int64_t L = R.L;
+    AKB_REQUIRE(cap >= L, "cap >= ring length");
+    const int64_t ncells = (int64_t)(nv - 1) * (nh - 1);
+    const int64_t base = 2 * ncells;
+    AKB_REQUIRE(base + cap < INT32_MAX, "grid too large for 32-bit triangle ids");
+
+    // convex hull of the ring points, collinear points kept (pop on a strict right turn only)
+    std::vector<int64_t> order(L);
+    for (int64_t i = 0; i < L; ++i) order[i] = i;
+    std::sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
+        return rx[a] < rx[b] || (rx[a] == rx[b] && ry[a] < ry[b]);
+    });
+    std::vector<char> on_hull(L, 0);
+    for (int pass = 0; pass < 2; ++pass) {
+        std::vector<int64_t> h;
+        for (int64_t k = 0; k < L; ++k) {
+            const int64_t i = pass == 0 ? order[k] : order[L - 1 - k];
+            while (h.size() >= 2 && right_turn(rx, ry, h[h.size() - 2], h.back(), i)) h.pop_back();
+            h.push_back(i);
+        }
+        for (int64_t i : h) on_hull[i] = 1;
+    }
+    std::vector<int64_t> hv;
+    for (int64_t i = 0; i < L; ++i)
+        if (on_hull[i]) hv.push_back(i);
+    AKB_REQUIRE(hv.size() >= 3, "degenerate point set (all boundary points collinear)");
+
+    for (int64_t e = 0; e < L; ++e) edge_tri[e] = -1;
+    std::vector<std::vector<int32_t>> extra(L);
+    int32_t n = 0;
+    struct Job {
+        int64_t p, q;
+        int32_t parent;  // pocket triangle on the other side of (p, q), -1 for a hull edge
+        int slot;        // which of the parent's nbr slots points back here
+    };
+    std::vector<Job> stack;
+    for (size_t k = 0; k < hv.size(); ++k) {
+        int64_t p = hv[k], q = hv[(k + 1) % hv.size()];
+        if (q <= p) q += L;
+        if (q - p >= 2) stack.push_back({p, q, -1, -1});
+    }
+    while (!stack.empty()) {
+        const Job J = stack.back();
+        stack.pop_back();
+        const int64_t p = J.p, q = J.q;
+        // the chain point seeing (p, q) under the largest angle: smallest cot = dot / |cross|
+        int64_t best = -1;
+        double best_cot = INFINITY;
+        const int64_t a = p % L, b = q % L;
+        for (int64_t m = p + 1; m < q; ++m) {
+            const int64_t c = m % L;
+            const double ux = rx[a] - rx[c], uy = ry[a] - ry[c];
+            const double vx = rx[b] - rx[c], vy = ry[b] - ry[c];
+            const double cr = fabs(ux * vy - uy * vx);
+            const double dt = ux * vx + uy * vy;
+            const double cot = cr > 0 ? dt / cr : (dt < 0 ? -INFINITY : INFINITY);
+            if (cot < best_cot) {
+                best_cot = cot;
+                best = m;
+            }
+        }
+        if (best < 0 || !(best_cot < INFINITY)) {
+            set_error("griddata: degenerate pocket between ring positions %lld and %lld", (long long)p, (long long)q);
+            return 2;
+        }
+        if (n >= cap) {
+            set_error("griddata: more pocket triangles than cap %d", cap);
+            return 2;
+        }
+        const int64_t m = best;
+        for (int64_t r = p + 1; r < q; ++r)
+            if (R.corner(r)) {
+                set_error("griddata: the convex hull cuts off a grid corner (ring position %lld); the grid is too "
+                          "distorted for the structured triangulation", (long long)(r % L));
+                return 2;
+            }
+        const int32_t id = n++;
+        tri[3 * id + 0] = (int32_t)R.vertex(p);
+        tri[3 * id + 1] = (int32_t)R.vertex(m);
+        tri[3 * id + 2] = (int32_t)R.vertex(q);
+        // opposite p: edge (m, q); opposite m: edge (q, p); opposite q: edge (p, m)
+        nbr[3 * id + 1] = J.parent < 0 ? -1 : (int32_t)(base + J.parent);
+        if (J.parent >= 0) nbr[3 * J.parent + J.slot] = (int32_t)(base + id);
+        if (q - m == 1) {
+            nbr[3 * id + 0] = -2 - (int32_t)(m % L);
+            edge_tri[m % L] = (int32_t)(base + id);
+        } else {
+            nbr[3 * id + 0] = -1;  // filled by the child
+            stack.push_back({m, q, id, 0});
+        }
+        if (m - p == 1) {
+            nbr[3 * id + 2] = -2 - (int32_t)(p % L);
+            edge_tri[p % L] = (int32_t)(base + id);
+        } else {
+            nbr[3 * id + 2] = -1;
+            stack.push_back({p, m, id, 2});
+        }
+        // the base chord (p, q) joins two ring points that are not grid neighbours
+        extra[a].push_back((int32_t)R.vertex(q));
+        extra[b].push_back((int32_t)R.vertex(p));
+    }
+    int64_t k = 0;
+    for (int64_t r = 0; r < L; ++r) {
+        extra_ptr[r] = (int32_t)k;
+        for (int32_t v : extra[r]) {
+            if (k >= 6 * (int64_t)cap) {
+                set_error("griddata: extra-neighbour list overflow");
+                return 2;
+            }
+            extra_idx[k++] = v;
+        }
+    }
+    extra_ptr[L] = (int32_t)k;
+    *n_out = n;
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,540 @@
+// griddata(points, values, (grid_H, grid_V), method='cubic') of the 'ray_wave' driver on the device
+// (AKB_raytrace_20250312.py:3673, :3689).
+//
+// scipy's cubic griddata is a Clough-Tocher interpolant on the Delaunay triangulation of the
+// points (CloughTocher2DInterpolator, scipy 1.15 interpolate/_interpnd): vertex gradients from
+// the global curvature-minimising estimate (estimate_gradients_2d_global: each vertex's gradient
+// minimises the summed squared second derivative of the edge cubics to its neighbours, solved by
+// repeated local 2 x 2 solves), then on each triangle the cubic Bezier patch of the Clough-Tocher
+// split, with the cross-boundary derivative taken along the direction to the neighbouring
+// triangle's centroid (affine invariant; -1/2 on hull edges), evaluated in extended barycentric
+// coordinates. NaN outside the convex hull.
+//
+// The points are the detector hits of the n_v x n_h ray grid (ray iv * n_h + ih), a smoothly
+// deformed lattice, so the Delaunay triangulation is structured: every cell split by the diagonal
+// that passes the in-circle test (k_gd_cells) plus the thin "pockets" between the grid's boundary
+// ring and its convex hull (akb_gd_pockets, host). k_gd_cells also checks the axis edges are
+// locally Delaunay and every cell is convex; a grid that fails is refused, not approximated.
+// Gradients: Jacobi sweeps of the same local solve until the largest relative change is below
+// tol (scipy runs Gauss-Seidel sweeps to 1e-6; both converge to the same fixed point, the
+// iteration matrix contracts by ~1/2 per sweep). Targets: each triangle claims the targets inside
+// it (atomicMin of the triangle id: deterministic on shared edges), then each target evaluates
+// its triangle's patch.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "akb_common.h"
+
+namespace akb {
+namespace {
+
+struct Grid {
+    const double* x;  // (n,) point x (detcenter2[1])
+    const double* y;  // (n,) point y (detcenter2[2])
+    int nv, nh;
+    const uint8_t* diag;  // (nv-1)(nh-1): 0 = split p00-p11, 1 = split p01-p10
+    // pockets
+    int npock;
+    const int32_t* ptri;   // (npock, 3) vertex ids
+    const int32_t* pnbr;   // (npock, 3) neighbour opposite vertex k: triangle id, -1 hull, <= -2 ring edge
+    const int32_t* edge_tri;  // (L) pocket triangle across ring edge e, -1 (hull edge)
+    const int32_t* xptr;   // (L + 1) extra neighbours of ring vertex r (pocket chords)
+    const int32_t* xidx;
+};
+
+__device__ __forceinline__ int64_t ncells(const Grid& g) { return (int64_t)(g.nv - 1) * (g.nh - 1); }
+
+__device__ __forceinline__ double orient(double ax, double ay, double bx, double by, double cx, double cy) {
+    return (bx - ax) * (cy - ay) - (by - ay) * (cx - ax);
+}
+
+// > 0 when d lies inside the circle through a, b, c (any orientation of a, b, c)
+__device__ __forceinline__ double incircle(double ax, double ay, double bx, double by, double cx, double cy,
+                                           double dx, double dy) {
+    const double adx = ax - dx, ady = ay - dy, bdx = bx - dx, bdy = by - dy, cdx = cx - dx, cdy = cy - dy;
+    const double A = adx * adx + ady * ady, B = bdx * bdx + bdy * bdy, C = cdx * cdx + cdy * cdy;
+    const double det = adx * (bdy * C - B * cdy) - ady * (bdx * C - B * cdx) + A * (bdx * cdy - bdy * cdx);
+    const double o = orient(ax, ay, bx, by, cx, cy);
+    return o > 0 ? det : -det;
+}
+
+// diagonal of cell (iv, ih): 0 (p00-p11) unless p10 lies inside the circle through p00, p01, p11
+__device__ int cell_diag(const Grid& g, int iv, int ih, double* viol) {
+    const int64_t i00 = (int64_t)iv * g.nh + ih, i01 = i00 + 1, i10 = i00 + g.nh, i11 = i10 + 1;
+    const double x0 = g.x[i00], y0 = g.y[i00];
+    const double bx = g.x[i01] - x0, by = g.y[i01] - y0;
+    const double cx = g.x[i11] - x0, cy = g.y[i11] - y0;
+    const double dx = g.x[i10] - x0, dy = g.y[i10] - y0;
+    const double ic = incircle(0.0, 0.0, bx, by, cx, cy, dx, dy);
+    int d = ic > 0 ? 1 : 0;
+    if (viol) {
+        // the chosen split must leave two triangles of the same orientation (a convex cell)
+        const double s = d == 0 ? orient(0, 0, bx, by, cx, cy) * orient(0, 0, cx, cy, dx, dy)
+                                : orient(0, 0, bx, by, dx, dy) * orient(bx, by, cx, cy, dx, dy);
+        *viol = s > 0 ? 0.0 : 1.0;
+    }
+    return d;
+}
+
+struct Tri {
+    int64_t v[3];
+};
+
+// triangle id -> vertices. Cell c = iv * (nh-1) + ih gives ids 2c, 2c + 1:
+//   diag 0: (p00, p01, p11), (p00, p11, p10);   diag 1: (p00, p01, p10), (p01, p11, p10)
+__device__ __forceinline__ Tri tri_verts(const Grid& g, int64_t t) {
+    Tri T;
+    const int64_t nc2 = 2 * ncells(g);
+    if (t >= nc2) {
+        const int64_t j = t - nc2;
+        T.v[0] = g.ptri[3 * j];
+        T.v[1] = g.ptri[3 * j + 1];
+        T.v[2] = g.ptri[3 * j + 2];
+        return T;
+    }
+    const int64_t c = t >> 1;
+    const int half = (int)(t & 1);
+    const int iv = (int)(c / (g.nh - 1)), ih = (int)(c - (int64_t)iv * (g.nh - 1));
+    const int64_t p00 = (int64_t)iv * g.nh + ih, p01 = p00 + 1, p10 = p00 + g.nh, p11 = p10 + 1;
+    if (g.diag[c] == 0) {
+        if (half == 0) { T.v[0] = p00; T.v[1] = p01; T.v[2] = p11; }
+        else { T.v[0] = p00; T.v[1] = p11; T.v[2] = p10; }
+    } else {
+        if (half == 0) { T.v[0] = p00; T.v[1] = p01; T.v[2] = p10; }
+        else { T.v[0] = p01; T.v[1] = p11; T.v[2] = p10; }
+    }
+    return T;
+}
+
+// ring edge index of a cell's boundary side (0 bottom, 1 right, 2 top, 3 left)
+__device__ __forceinline__ int64_t ring_edge(const Grid& g, int side, int iv, int ih) {
+    const int64_t a = g.nh - 1, b = g.nv - 1;
+    switch (side) {
+        case 0: return ih;
+        case 1: return a + iv;
+        case 2: return a + b + (g.nh - 2 - ih);
+        default: return 2 * a + b + (g.nv - 2 - iv);
+    }
+}
+
+// the cell triangle holding ring edge e
+__device__ __forceinline__ int64_t ring_edge_tri(const Grid& g, int64_t e) {
+    const int64_t a = g.nh - 1, b = g.nv - 1;
+    int iv, ih, side;
+    if (e < a) { iv = 0; ih = (int)e; side = 0; }
+    else if (e < a + b) { iv = (int)(e - a); ih = g.nh - 2; side = 1; }
+    else if (e < 2 * a + b) { iv = g.nv - 2; ih = (int)(g.nh - 2 - (e - a - b)); side = 2; }
+    else { iv = (int)(g.nv - 2 - (e - 2 * a - b)); ih = 0; side = 3; }
+    const int64_t c = (int64_t)iv * (g.nh - 1) + ih;
+    const int d = g.diag[c];
+    int half;
+    if (side == 0) half = 0;
+    else if (side == 2) half = 1;
+    else if (side == 1) half = d == 0 ? 0 : 1;
+    else half = d == 0 ? 1 : 0;
+    return 2 * c + half;
+}
+
+// neighbour of a cell triangle across its side: another cell's triangle, a pocket, or -1
+__device__ __forceinline__ int64_t across_side(const Grid& g, int side, int iv, int ih) {
+    if (side == 0) {
+        if (iv == 0) return g.edge_tri[ring_edge(g, 0, iv, ih)];
+        return 2 * ((int64_t)(iv - 1) * (g.nh - 1) + ih) + 1;  // its top edge: half 1
+    }
+    if (side == 2) {
+        if (iv == g.nv - 2) return g.edge_tri[ring_edge(g, 2, iv, ih)];
+        return 2 * ((int64_t)(iv + 1) * (g.nh - 1) + ih);      // its bottom edge: half 0
+    }
+    if (side == 1) {
+        if (ih == g.nh - 2) return g.edge_tri[ring_edge(g, 1, iv, ih)];
+        const int64_t c = (int64_t)iv * (g.nh - 1) + ih + 1;      // its left edge
+        return 2 * c + (g.diag[c] == 0 ? 1 : 0);
+    }
+    if (ih == 0) return g.edge_tri[ring_edge(g, 3, iv, ih)];
+    const int64_t c = (int64_t)iv * (g.nh - 1) + ih - 1;          // its right edge
+    return 2 * c + (g.diag[c] == 0 ? 0 : 1);
+}
+
+// neighbour triangle opposite vertex k of triangle t (-1: hull edge)
+__device__ int64_t tri_nbr(const Grid& g, int64_t t, int k) {
+    const int64_t nc2 = 2 * ncells(g);
+    if (t >= nc2) {
+        const int32_t v = g.pnbr[3 * (t - nc2) + k];
+        if (v >= -1) return v;
+        return ring_edge_tri(g, -2 - (int64_t)v);
+    }
+    const int64_t c = t >> 1;
+    const int half = (int)(t & 1);
+    const int iv = (int)(c / (g.nh - 1)), ih = (int)(c - (int64_t)iv * (g.nh - 1));
+    // side opposite vertex k per (diag, half); -1 = the cell's other triangle
+    //   d0 h0 (p00,p01,p11): right, diag, bottom     d0 h1 (p00,p11,p10): top, left, diag
+    //   d1 h0 (p00,p01,p10): diag, left, bottom      d1 h1 (p01,p11,p10): top, diag, right
+    // packed 3 bits per entry (side + 1), entry index (diag * 2 + half) * 3 + k
+    constexpr uint64_t kSide = (2ull << 0) | (0ull << 3) | (1ull << 6) | (3ull << 9) | (4ull << 12) | (0ull << 15) |
+                               (0ull << 18) | (4ull << 21) | (1ull << 24) | (3ull << 27) | (0ull << 30) | (2ull << 33);
+    const int side = (int)((kSide >> (3 * ((g.diag[c] * 2 + half) * 3 + k))) & 7u) - 1;
+    if (side < 0) return 2 * c + (1 - half);
+    return across_side(g, side, iv, ih);
+}
+
+// ------------------------------------------------------------------ triangulation + checks
+
+// flags: bit 0 a non-convex or degenerate cell, bit 1 an edge that is not locally Delaunay,
+// bit 2 a broken pocket adjacency, bits 3 / 4 cells of positive / negative orientation
+__global__ void __launch_bounds__(kBlock) k_gd_cells(Grid g, uint8_t* diag, double tol, unsigned* flags) {
+    const int64_t nc = ncells(g);
+    for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < nc; c += (int64_t)gridDim.x * blockDim.x) {
+        const int iv = (int)(c / (g.nh - 1)), ih = (int)(c - (int64_t)iv * (g.nh - 1));
+        double bad = 0.0;
+        const int d = cell_diag(g, iv, ih, &bad);
+        diag[c] = (uint8_t)d;
+        unsigned f = bad > 0 ? 1u : 0u;
+        {   // every cell must share the grid's orientation (bits 3 / 4 both set: a folded grid)
+            const int64_t q00 = (int64_t)iv * g.nh + ih;
+            const double o = orient(g.x[q00], g.y[q00], g.x[q00 + 1], g.y[q00 + 1], g.x[q00 + g.nh + 1], g.y[q00 + g.nh + 1]);
+            f |= o > 0 ? 8u : (o < 0 ? 16u : 1u);
+        }
+        const int64_t p00 = (int64_t)iv * g.nh + ih, p01 = p00 + 1, p10 = p00 + g.nh, p11 = p10 + 1;
+        // right edge p01-p11 against the next cell's left triangle
+        if (ih + 1 < g.nh - 1) {
+            const int dn = cell_diag(g, iv, ih + 1, nullptr);
+            const int64_t mine = d == 0 ? p00 : p10;           // opposite vertex of my right-edge triangle
+            const int64_t other = dn == 0 ? p11 + 1 : p01 + 1;  // opposite vertex of its left-edge triangle
+            const double x0 = g.x[p01], y0 = g.y[p01];
+            const double ax = g.x[mine] - x0, ay = g.y[mine] - y0, cx = g.x[p11] - x0, cy = g.y[p11] - y0;
+            const double ox = g.x[other] - x0, oy = g.y[other] - y0;
+            const double s = fmax(fmax(fabs(ax), fabs(ay)), fmax(fmax(fabs(cx), fabs(cy)), fmax(fabs(ox), fabs(oy))));
+            if (incircle(0.0, 0.0, ax, ay, cx, cy, ox, oy) > tol * s * s * s * s) f |= 2u;
+        }
+        // top edge p10-p11 against the next row's bottom triangle
+        if (iv + 1 < g.nv - 1) {
+            const int dn = cell_diag(g, iv + 1, ih, nullptr);
+            const int64_t mine = d == 0 ? p00 : p01;
+            const int64_t other = dn == 0 ? p11 + g.nh : p10 + g.nh;
+            const double x0 = g.x[p10], y0 = g.y[p10];
+            const double ax = g.x[mine] - x0, ay = g.y[mine] - y0, cx = g.x[p11] - x0, cy = g.y[p11] - y0;
+            const double ox = g.x[other] - x0, oy = g.y[other] - y0;
+            const double s = fmax(fmax(fabs(ax), fabs(ay)), fmax(fmax(fabs(cx), fabs(cy)), fmax(fabs(ox), fabs(oy))));
+            if (incircle(0.0, 0.0, ax, ay, cx, cy, ox, oy) > tol * s * s * s * s) f |= 2u;
+        }
+        atomicOr(flags, f);
+    }
+}
+
+// ring positions -> coordinates, for the host pocket builder
+__global__ void k_gd_ring(Grid g, double* rx, double* ry) {
+    const int64_t a = g.nh - 1, b = g.nv - 1, L = 2 * a + 2 * b;
+    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < L; r += (int64_t)gridDim.x * blockDim.x) {
+        int64_t v;
+        if (r < a) v = r;
+        else if (r < a + b) v = (r - a) * g.nh + (g.nh - 1);
+        else if (r < 2 * a + b) v = (int64_t)(g.nv - 1) * g.nh + (g.nh - 1 - (r - a - b));
+        else v = (int64_t)(g.nv - 1 - (r - 2 * a - b)) * g.nh;
+        rx[r] = g.x[v];
+        ry[r] = g.y[v];
+    }
+}
+
+// the pockets against the triangles they border: every pocket edge locally Delaunay (bit 1)
+__global__ void k_gd_check_pockets(Grid g, double tol, unsigned* flags) {
+    const int64_t nc2 = 2 * ncells(g);
+    for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < g.npock; j += (int64_t)gridDim.x * blockDim.x) {
+        const Tri T = tri_verts(g, nc2 + j);
+        for (int k = 0; k < 3; ++k) {
+            const int64_t n = tri_nbr(g, nc2 + j, k);
+            if (n < 0) continue;
+            const Tri N = tri_verts(g, n);
+            // the neighbour's vertex that is not on the shared edge
+            int64_t o = -1;
+            for (int q = 0; q < 3; ++q)
+                if (N.v[q] != T.v[(k + 1) % 3] && N.v[q] != T.v[(k + 2) % 3]) o = N.v[q];
+            if (o < 0) {
+                atomicOr(flags, 4u);
+                continue;
+            }
+            const double x0 = g.x[T.v[0]], y0 = g.y[T.v[0]];
+            const double bx = g.x[T.v[1]] - x0, by = g.y[T.v[1]] - y0, cx = g.x[T.v[2]] - x0, cy = g.y[T.v[2]] - y0;
+            const double ox = g.x[o] - x0, oy = g.y[o] - y0;
+            const double s = fmax(fmax(fabs(bx), fabs(by)), fmax(fmax(fabs(cx), fabs(cy)), fmax(fabs(ox), fabs(oy))));
+            if (incircle(0.0, 0.0, bx, by, cx, cy, ox, oy) > tol * s * s * s * s) atomicOr(flags, 2u);
+        }
+    }
+}
+
+// ------------------------------------------------------------------ gradients
+
+__device__ __forceinline__ int64_t ring_pos(const Grid& g, int iv, int ih) {
+    const int64_t a = g.nh - 1, b = g.nv - 1;
+    if (iv == 0) return ih;
+    if (ih == g.nh - 1) return a + iv;
+    if (iv == g.nv - 1) return a + b + (g.nh - 1 - ih);
+    if (ih == 0) return 2 * a + b + (g.nv - 1 - iv);
+    return -1;
+}
+
+struct GradAcc {
+    double q0 = 0, q1 = 0, q3 = 0, s0 = 0, s1 = 0;
+};
+
+__device__ __forceinline__ void grad_edge(GradAcc& A, double xi, double yi, double fi, double xj, double yj,
+                                          double fj, double gj0, double gj1) {
+    const double ex = xj - xi, ey = yj - yi;
+    const double L = sqrt(ex * ex + ey * ey);
+    const double L3 = L * L * L;
+    const double df2 = -ex * gj0 - ey * gj1;
+    A.q0 += 4 * ex * ex / L3;
+    A.q1 += 4 * ex * ey / L3;
+    A.q3 += 4 * ey * ey / L3;
+    const double w = 6 * (fi - fj) - 2 * df2;
+    A.s0 += w * ex / L3;
+    A.s1 += w * ey / L3;
+}
+
+// one Jacobi sweep: gout[i] from gin of the neighbours; the largest relative change -> chg
+__global__ void __launch_bounds__(kBlock) k_gd_grad(Grid g, const double* __restrict__ f,
+                                                    const double* __restrict__ gin, double* __restrict__ gout,
+                                                    unsigned long long* chg) {
+    const int64_t n = (int64_t)g.nv * g.nh;
+    double worst = 0.0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int iv = (int)(i / g.nh), ih = (int)(i - (int64_t)iv * g.nh);
+        const double xi = g.x[i], yi = g.y[i], fi = f[i];
+        GradAcc A;
+        auto edge = [&](int64_t j) { grad_edge(A, xi, yi, fi, g.x[j], g.y[j], f[j], gin[2 * j], gin[2 * j + 1]); };
+        if (ih > 0) edge(i - 1);
+        if (ih < g.nh - 1) edge(i + 1);
+        if (iv > 0) edge(i - g.nh);
+        if (iv < g.nv - 1) edge(i + g.nh);
+        // diagonals of the four cells around the vertex
+        if (iv > 0 && ih > 0 && g.diag[(int64_t)(iv - 1) * (g.nh - 1) + ih - 1] == 0) edge(i - g.nh - 1);
+        if (iv > 0 && ih < g.nh - 1 && g.diag[(int64_t)(iv - 1) * (g.nh - 1) + ih] == 1) edge(i - g.nh + 1);
+        if (iv < g.nv - 1 && ih > 0 && g.diag[(int64_t)iv * (g.nh - 1) + ih - 1] == 1) edge(i + g.nh - 1);
+        if (iv < g.nv - 1 && ih < g.nh - 1 && g.diag[(int64_t)iv * (g.nh - 1) + ih] == 0) edge(i + g.nh + 1);
+        const int64_t r = ring_pos(g, iv, ih);
+        if (r >= 0)
+            for (int32_t k = g.xptr[r]; k < g.xptr[r + 1]; ++k) edge(g.xidx[k]);
+        const double det = A.q0 * A.q3 - A.q1 * A.q1;
+        const double r0 = (A.q3 * A.s0 - A.q1 * A.s1) / det;
+        const double r1 = (-A.q1 * A.s0 + A.q0 * A.s1) / det;
+        const double c = fmax(fabs(gin[2 * i] + r0), fabs(gin[2 * i + 1] + r1)) / fmax(1.0, fmax(fabs(r0), fabs(r1)));
+        worst = fmax(worst, c);
+        gout[2 * i] = -r0;
+        gout[2 * i + 1] = -r1;
+    }
+    for (int off = 32; off > 0; off >>= 1) worst = fmax(worst, __shfl_down(worst, off));
+    if ((threadIdx.x & 63) == 0 && worst > 0) atomicMax(chg, (unsigned long long)__double_as_longlong(worst));
+}
+
+// ------------------------------------------------------------------ targets
+
+struct Targets {
+    const double* gx;  // (mx,) target x axis (grid_H row), ascending
+    const double* gy;  // (my,) target y axis (grid_V column), ascending
+    int mx, my;
+};
+
+__device__ __forceinline__ int lower_idx(const double* a, int n, double v) {  // first i with a[i] >= v
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int m = (lo + hi) >> 1;
+        if (a[m] < v) lo = m + 1;
+        else hi = m;
+    }
+    return lo;
+}
+
+// barycentric coordinates of (px, py) in triangle T (origin at its last vertex)
+__device__ __forceinline__ void bary(const Grid& g, const Tri& T, double px, double py, double (&b)[3]) {
+    const double x2 = g.x[T.v[2]], y2 = g.y[T.v[2]];
+    const double a00 = g.x[T.v[0]] - x2, a01 = g.x[T.v[1]] - x2;
+    const double a10 = g.y[T.v[0]] - y2, a11 = g.y[T.v[1]] - y2;
+    const double det = a00 * a11 - a01 * a10;
+    const double t00 = a11 / det, t01 = -a01 / det, t10 = -a10 / det, t11 = a00 / det;
+    const double dx = px - x2, dy = py - y2;
+    b[0] = t00 * dx + t01 * dy;
+    b[1] = t10 * dx + t11 * dy;
+    b[2] = 1.0 - b[0] - b[1];
+}
+
+constexpr double kInsideEps = 100 * 2.220446049250313e-16;
+
+__global__ void __launch_bounds__(kBlock) k_gd_claim(Grid g, Targets t, int* owner) {
+    const int64_t ntri = 2 * ncells(g) + g.npock;
+    for (int64_t id = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; id < ntri; id += (int64_t)gridDim.x * blockDim.x) {
+        const Tri T = tri_verts(g, id);
+        double xlo = g.x[T.v[0]], xhi = xlo, ylo = g.y[T.v[0]], yhi = ylo;
+        for (int k = 1; k < 3; ++k) {
+            xlo = fmin(xlo, g.x[T.v[k]]);
+            xhi = fmax(xhi, g.x[T.v[k]]);
+            ylo = fmin(ylo, g.y[T.v[k]]);
+            yhi = fmax(yhi, g.y[T.v[k]]);
+        }
+        const double padx = (xhi - xlo) * 1e-9, pady = (yhi - ylo) * 1e-9;
+        const int c0 = lower_idx(t.gx, t.mx, xlo - padx), c1 = lower_idx(t.gx, t.mx, xhi + padx);
+        const int r0 = lower_idx(t.gy, t.my, ylo - pady), r1 = lower_idx(t.gy, t.my, yhi + pady);
+        for (int r = r0; r < r1; ++r)
+            for (int c = c0; c < c1; ++c) {
+                double b[3];
+                bary(g, T, t.gx[c], t.gy[r], b);
+                if (b[0] >= -kInsideEps && b[1] >= -kInsideEps && b[2] >= -kInsideEps)
+                    atomicMin(&owner[(int64_t)r * t.mx + c], (int)id);
+            }
+    }
+}
+
+__device__ double clough_tocher(const Grid& g, int64_t tid, const Tri& T, const double* f, const double* grad,
+                                const double (&b)[3]) {
+    const double p0x = g.x[T.v[0]], p0y = g.y[T.v[0]];
+    const double p1x = g.x[T.v[1]], p1y = g.y[T.v[1]];
+    const double p2x = g.x[T.v[2]], p2y = g.y[T.v[2]];
+    const double e12x = p1x - p0x, e12y = p1y - p0y;
+    const double e23x = p2x - p1x, e23y = p2y - p1y;
+    const double e31x = p0x - p2x, e31y = p0y - p2y;
+    const double f1 = f[T.v[0]], f2 = f[T.v[1]], f3 = f[T.v[2]];
+    const double g0x = grad[2 * T.v[0]], g0y = grad[2 * T.v[0] + 1];
+    const double g1x = grad[2 * T.v[1]], g1y = grad[2 * T.v[1] + 1];
+    const double g2x = grad[2 * T.v[2]], g2y = grad[2 * T.v[2] + 1];
+    const double df12 = +(g0x * e12x + g0y * e12y);
+    const double df21 = -(g1x * e12x + g1y * e12y);
+    const double df23 = +(g1x * e23x + g1y * e23y);
+    const double df32 = -(g2x * e23x + g2y * e23y);
+    const double df31 = +(g2x * e31x + g2y * e31y);
+    const double df13 = -(g0x * e31x + g0y * e31y);
+    const double c3000 = f1, c2100 = (df12 + 3 * c3000) / 3, c2010 = (df13 + 3 * c3000) / 3;
+    const double c0300 = f2, c1200 = (df21 + 3 * c0300) / 3, c0210 = (df23 + 3 * c0300) / 3;
+    const double c0030 = f3, c1020 = (df31 + 3 * c0030) / 3, c0120 = (df32 + 3 * c0030) / 3;
+    const double c2001 = (c2100 + c2010 + c3000) / 3;
+    const double c0201 = (c1200 + c0300 + c0210) / 3;
+    const double c0021 = (c1020 + c0120 + c0030) / 3;
+    double gk[3];
+    for (int k = 0; k < 3; ++k) {
+        const int64_t n = tri_nbr(g, tid, k);
+        if (n < 0) {
+            gk[k] = -0.5;
+            continue;
+        }
+        const Tri N = tri_verts(g, n);
+        const double cx = (g.x[N.v[0]] + g.x[N.v[1]] + g.x[N.v[2]]) / 3;
+        const double cy = (g.y[N.v[0]] + g.y[N.v[1]] + g.y[N.v[2]]) / 3;
+        double c[3];
+        bary(g, T, cx, cy, c);
+        if (k == 0) gk[k] = (2 * c[2] + c[1] - 1) / (2 - 3 * c[2] - 3 * c[1]);
+        else if (k == 1) gk[k] = (2 * c[0] + c[2] - 1) / (2 - 3 * c[0] - 3 * c[2]);
+        else gk[k] = (2 * c[1] + c[0] - 1) / (2 - 3 * c[1] - 3 * c[0]);
+    }
+    const double c0111 = (gk[0] * (-c0300 + 3 * c0210 - 3 * c0120 + c0030) + (-c0300 + 2 * c0210 - c0120 + c0021 + c0201)) / 2;
+    const double c1011 = (gk[1] * (-c0030 + 3 * c1020 - 3 * c2010 + c3000) + (-c0030 + 2 * c1020 - c2010 + c2001 + c0021)) / 2;
+    const double c1101 = (gk[2] * (-c3000 + 3 * c2100 - 3 * c1200 + c0300) + (-c3000 + 2 * c2100 - c1200 + c2001 + c0201)) / 2;
+    const double c1002 = (c1101 + c1011 + c2001) / 3;
+    const double c0102 = (c1101 + c0111 + c0201) / 3;
+    const double c0012 = (c1011 + c0111 + c0021) / 3;
+    const double c0003 = (c1002 + c0102 + c0012) / 3;
+    const double mv = fmin(b[0], fmin(b[1], b[2]));
+    const double b1 = b[0] - mv, b2 = b[1] - mv, b3 = b[2] - mv, b4 = 3 * mv;
+    return b1 * b1 * b1 * c3000 + 3 * b1 * b1 * b2 * c2100 + 3 * b1 * b1 * b3 * c2010 + 3 * b1 * b1 * b4 * c2001 +
+           3 * b1 * b2 * b2 * c1200 + 6 * b1 * b2 * b4 * c1101 + 3 * b1 * b3 * b3 * c1020 + 6 * b1 * b3 * b4 * c1011 +
+           3 * b1 * b4 * b4 * c1002 + b2 * b2 * b2 * c0300 + 3 * b2 * b2 * b3 * c0210 + 3 * b2 * b2 * b4 * c0201 +
+           3 * b2 * b3 * b3 * c0120 + 6 * b2 * b3 * b4 * c0111 + 3 * b2 * b4 * b4 * c0102 + b3 * b3 * b3 * c0030 +
+           3 * b3 * b3 * b4 * c0021 + 3 * b3 * b4 * b4 * c0012 + b4 * b4 * b4 * c0003;
+}
+
+// nvals value sets share the triangulation: f / grad / out strided by n / 2n / mx*my
+__global__ void __launch_bounds__(kBlock) k_gd_eval(Grid g, Targets t, const int* __restrict__ owner,
+                                                    const double* f, const double* grad, int nvals, double* out) {
+    const int64_t m = (int64_t)t.mx * t.my, n = (int64_t)g.nv * g.nh;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+        const int o = owner[i];
+        if (o == INT32_MAX) {
+            for (int v = 0; v < nvals; ++v) out[v * m + i] = __builtin_nan("");
+            continue;
+        }
+        const int r = (int)(i / t.mx), c = (int)(i - (int64_t)r * t.mx);
+        const Tri T = tri_verts(g, o);
+        double b[3];
+        bary(g, T, t.gx[c], t.gy[r], b);
+        for (int v = 0; v < nvals; ++v) out[v * m + i] = clough_tocher(g, o, T, f + v * n, grad + 2 * v * n, b);
+    }
+}
+
+__global__ void k_fill_i32(int* p, int64_t n, int v) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = v;
+}
+
+}  // namespace
+}  // namespace akb
+
+using namespace akb;
+
+extern "C" {
+
+// pass 1: cell diagonals + local-Delaunay checks, ring coordinates for the host
+int akb_gd_cells_f64(const double* x, const double* y, int nv, int nh, uint8_t* diag, double tol, unsigned* d_flags,
+                     double* ring_x, double* ring_y, void* stream) {
+    clear_error();
+    AKB_REQUIRE(x && y && diag && d_flags && ring_x && ring_y, "null pointer");
+    AKB_REQUIRE(nv >= 2 && nh >= 2, "grid of at least 2 x 2 points");
+    hipStream_t s = (hipStream_t)stream;
+    Grid g{x, y, nv, nh, diag, 0, nullptr, nullptr, nullptr, nullptr, nullptr};
+    const int64_t nc = (int64_t)(nv - 1) * (nh - 1);
+    k_gd_cells<<<grid_for(nc, 1, kStreamGridCap), kBlock, 0, s>>>(g, diag, tol, d_flags);
+    int st = launch_status("k_gd_cells");
+    if (st) return st;
+    const int64_t L = 2 * (int64_t)(nh - 1) + 2 * (int64_t)(nv - 1);
+    k_gd_ring<<<grid_for(L), kBlock, 0, s>>>(g, ring_x, ring_y);
+    return launch_status("k_gd_ring");
+}
+
+int akb_gd_check_pockets(const double* x, const double* y, int nv, int nh, const uint8_t* diag, int npock,
+                         const int32_t* ptri, const int32_t* pnbr, const int32_t* edge_tri, double tol,
+                         unsigned* d_flags, void* stream) {
+    clear_error();
+    if (npock == 0) return 0;
+    Grid g{x, y, nv, nh, diag, npock, ptri, pnbr, edge_tri, nullptr, nullptr};
+    k_gd_check_pockets<<<grid_for(npock), kBlock, 0, (hipStream_t)stream>>>(g, tol, d_flags);
+    return launch_status("k_gd_check_pockets");
+}
+
+// one Jacobi sweep per value set; d_change: largest relative change (as ordered double bits,
+// zeroed by the caller), nvals value sets strided by n (values) and 2n (gradients)
+int akb_gd_grad_sweep_f64(const double* x, const double* y, int nv, int nh, const uint8_t* diag, int npock,
+                          const int32_t* ptri, const int32_t* pnbr, const int32_t* edge_tri, const int32_t* xptr,
+                          const int32_t* xidx, const double* f, int nvals, const double* gin, double* gout,
+                          unsigned long long* d_change, void* stream) {
+    clear_error();
+    AKB_REQUIRE(x && y && diag && f && gin && gout && d_change && nvals >= 1, "bad arguments");
+    Grid g{x, y, nv, nh, diag, npock, ptri, pnbr, edge_tri, xptr, xidx};
+    const int64_t n = (int64_t)nv * nh;
+    for (int v = 0; v < nvals; ++v) {
+        k_gd_grad<<<grid_for(n, 1, kStreamGridCap), kBlock, 0, (hipStream_t)stream>>>(g, f + v * n, gin + 2 * v * n,
+                                                                                   gout + 2 * v * n, d_change);
+        int st = launch_status("k_gd_grad");
+        if (st) return st;
+    }
+    return 0;
+}
+
+// targets: the meshgrid of gx (mx) x gy (my); owner: (my * mx) int32 scratch; out: (nvals, my, mx)
+int akb_gd_eval_f64(const double* x, const double* y, int nv, int nh, const uint8_t* diag, int npock,
+                    const int32_t* ptri, const int32_t* pnbr, const int32_t* edge_tri, const double* gx, int mx,
+                    const double* gy, int my, const double* f, const double* grad, int nvals, int* owner,
+                    double* out, void* stream) {
+    clear_error();
+    AKB_REQUIRE(x && y && diag && gx && gy && f && grad && owner && out && mx > 0 && my > 0 && nvals >= 1,
+                "bad arguments");
+    hipStream_t s = (hipStream_t)stream;
+    Grid g{x, y, nv, nh, diag, npock, ptri, pnbr, edge_tri, nullptr, nullptr};
+    Targets t{gx, gy, mx, my};
+    const int64_t m = (int64_t)mx * my;
+    k_fill_i32<<<grid_for(m, 4), kBlock, 0, s>>>(owner, m, INT32_MAX);
+    int st = launch_status("k_fill_i32");
+    if (st) return st;
+    const int64_t ntri = 2 * (int64_t)(nv - 1) * (nh - 1) + npock;
+    k_gd_claim<<<grid_for(ntri, 1, kStreamGridCap), kBlock, 0, s>>>(g, t, owner);
+    st = launch_status("k_gd_claim");
+    if (st) return st;
+    k_gd_eval<<<grid_for(m, 1, kStreamGridCap), kBlock, 0, s>>>(g, t, owner, f, grad, nvals, out);
+    return launch_status("k_gd_eval");
+}
+
+}  // extern "C"

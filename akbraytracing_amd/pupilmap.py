@@ -126,3 +126,28 @@ def match_legendre_multi(data, order):
     if as_torch:
         return fits, c, [tuple(o) for o in orders]
     return fits.cpu().numpy(), c.cpu().numpy(), [tuple(o) for o in orders]
+
+
+def wave_maps(detcenter2, dist_err2, wave2, ray_num_H, ray_num_V):
+    """The driver's gridding step (AKB_raytrace_20250312.py:3653-3696) on the device:
+    grid_H, grid_V = meshgrid(linspace(min, max) of the hits' y / z), matrixDistError2 and
+    matrixWave2 by cubic griddata (one triangulation for both), matrixWave2 -= nanmean, then both
+    plane-corrected. detcenter2 (3, n), dist_err2 / wave2 (n,) in ray order (n = V * H).
+    Returns a dict of device tensors (the grids as numpy)."""
+    from .griddata import CubicGrid
+    d2 = _as_dev(detcenter2)
+    y, z = d2[1].contiguous(), d2[2].contiguous()
+    ext = torch.stack([y.min(), y.max(), z.min(), z.max()]).cpu().numpy()
+    gx = np.linspace(ext[0], ext[1], int(ray_num_H))
+    gy = np.linspace(ext[2], ext[3], int(ray_num_V))
+    grid_H, grid_V = np.meshgrid(gx, gy)
+    cg = CubicGrid(y, z, int(ray_num_V), int(ray_num_H))
+    vals = torch.stack([_as_dev(dist_err2).reshape(-1), _as_dev(wave2).reshape(-1)])
+    maps = cg.interp(vals, gx, gy)
+    m_dist, m_wave = maps[0], maps[1]
+    s, c = RowSums()(m_wave.reshape(1, -1), nan=True)
+    m_wave = m_wave - (s / c.to(D.F64))[0]  # np.nanmean: nansum / count
+    return dict(grid_H=grid_H, grid_V=grid_V, matrixDistError2=m_dist, matrixWave2=m_wave,
+                matrixWave2_Corrected=plane_correction_with_nan_and_outlier_filter(m_wave),
+                matrixDistError2_Corrected=plane_correction_with_nan_and_outlier_filter(m_dist),
+                sweeps=cg.sweeps)

@@ -324,6 +324,32 @@ int akb_plane_subtract_f64(const double* z, int ny, int nx, const double* d_coef
 int akb_legendre_rows_f64(const double* data, int n, int K, int order, const double* px, const double* py,
                           const int* ord, const double* s, const double* c, int mode, double* out, void* stream);
 
+/* ---------------- griddata(method='cubic') on the ray grid (ref AKB_raytrace_20250312.py:3673, :3689) ----------------
+ * scipy's Clough-Tocher griddata for points that are the n_v x n_h ray grid's detector hits
+ * (x = detcenter2[1], y = detcenter2[2], ray iv * n_h + ih) onto the meshgrid of gx x gy.
+ * Triangulation: akb_gd_cells_f64 (cell diagonals by the in-circle test, checks; flags bit 0
+ * non-convex cell, bit 1 not locally Delaunay, bit 2 broken pocket adjacency, bits 3 and 4 both
+ * set = folded grid) -> akb_gd_pockets (HOST: the triangles between the boundary ring and the
+ * convex hull, ring coordinates from akb_gd_cells_f64; ids >= 2 (n_v-1)(n_h-1)) ->
+ * akb_gd_check_pockets. Gradients: akb_gd_grad_sweep_f64 (one Jacobi sweep of scipy's
+ * estimate_gradients_2d_global local solve, largest relative change atomically max-ed into
+ * *d_change as double bits) until converged. Values: akb_gd_eval_f64 (NaN outside the hull). */
+int akb_gd_cells_f64(const double* x, const double* y, int nv, int nh, uint8_t* diag, double tol, unsigned* d_flags,
+                     double* ring_x, double* ring_y, void* stream);
+int akb_gd_pockets(const double* ring_x, const double* ring_y, int nv, int nh, int cap, int32_t* n_out,
+                   int32_t* tri, int32_t* nbr, int32_t* edge_tri, int32_t* extra_ptr, int32_t* extra_idx);
+int akb_gd_check_pockets(const double* x, const double* y, int nv, int nh, const uint8_t* diag, int npock,
+                         const int32_t* ptri, const int32_t* pnbr, const int32_t* edge_tri, double tol,
+                         unsigned* d_flags, void* stream);
+int akb_gd_grad_sweep_f64(const double* x, const double* y, int nv, int nh, const uint8_t* diag, int npock,
+                          const int32_t* ptri, const int32_t* pnbr, const int32_t* edge_tri, const int32_t* xptr,
+                          const int32_t* xidx, const double* f, int nvals, const double* gin, double* gout,
+                          unsigned long long* d_change, void* stream);
+int akb_gd_eval_f64(const double* x, const double* y, int nv, int nh, const uint8_t* diag, int npock,
+                    const int32_t* ptri, const int32_t* pnbr, const int32_t* edge_tri, const double* gx, int mx,
+                    const double* gy, int my, const double* f, const double* grad, int nvals, int* owner,
+                    double* out, void* stream);
+
 /* diagnostics: out4[4i..4i+3] = (the trace's sqrt, sqrt, the trace's shared-reciprocal a/b, a/b)
  * for n pairs (a[i], b[i]) — used by the tests to check the shortcuts bit for bit */
 int akb_selftest_arith_f64(const double* a, const double* b, int64_t n, double* out4, void* stream);

@@ -611,6 +611,87 @@ def test_match_legendre_multi_nan_and_nonsquare(gpu):
         PM.match_legendre_multi(np.zeros((4, 5)), 3)
 
 
+# ----------------------------------------------------------------------------- griddata (f1)
+
+def _scale_tol(ref):
+    """1e-6 of the map's range, or 64 ulp of its largest magnitude (the 65x65 Wave2 carries a
+    ~1e7 nm offset, so rounding alone is ~1e-8 there)."""
+    return max(1e-6 * (np.nanmax(ref) - np.nanmin(ref)), 64 * np.spacing(np.nanmax(np.abs(ref))))
+
+
+def test_griddata_cubic_vs_reference(gpu):
+    """The driver's griddata(cubic) of Wave2 on its 65x65 detector hits (the reference's output):
+    same NaN mask (outside the hull), values to rounding."""
+    from akbraytracing_amd.griddata import griddata
+    f = golden("akb_raywave_65.npz")
+    g = golden("akb_psfcalc_65.npz")
+    d2 = f["detcenter2"]
+    got = griddata((d2[1, :], d2[2, :]), f["wave2"], (g["grid_H0"], g["grid_V0"]), method="cubic")
+    ref = g["griddata_wave2"]
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    assert np.nanmax(np.abs(got - ref)) <= _scale_tol(ref)
+
+
+def _lattice(nv, nh, seed):
+    u, v = np.meshgrid(np.linspace(-1, 1, nh), np.linspace(-1, 1, nv))
+    X = u * 1e-4 + 3e-6 * v ** 2 - 2e-6 * u * v + 1e-6 * v ** 3
+    Y = v * 1.3e-4 + 4e-6 * u ** 2 + 1e-6 * u ** 3
+    rng = np.random.default_rng(seed)
+    F = 0.3 * u ** 2 - 0.2 * u * v + 0.1 * np.sin(3 * v) + 1e-3 * rng.standard_normal(u.shape)
+    return X, Y, F
+
+
+@pytest.mark.parametrize("nv,nh", [(97, 113), (280, 300)])
+def test_griddata_cubic_vs_scipy(gpu, nv, nh):
+    """Deformed lattices with concave and convex edges vs scipy.interpolate.griddata itself."""
+    from scipy.interpolate import griddata as sp_griddata
+    from akbraytracing_amd.griddata import griddata
+    X, Y, F = _lattice(nv, nh, nv)
+    gx = np.linspace(X.min(), X.max(), nh)
+    gy = np.linspace(Y.min(), Y.max(), nv)
+    GH, GV = np.meshgrid(gx, gy)
+    want = sp_griddata((X.ravel(), Y.ravel()), F.ravel(), (GH, GV), method="cubic")
+    got = griddata((X.ravel(), Y.ravel()), F.ravel(), (GH, GV), method="cubic")
+    assert np.array_equal(np.isnan(got), np.isnan(want))
+    assert np.nanmax(np.abs(got - want)) <= _scale_tol(want)
+
+
+def test_griddata_batched_values_and_errors(gpu):
+    from akbraytracing_amd import _lib
+    from akbraytracing_amd.griddata import CubicGrid, griddata
+    X, Y, F = _lattice(40, 50, 1)
+    gx = np.linspace(X.min(), X.max(), 50)
+    gy = np.linspace(Y.min(), Y.max(), 40)
+    cg = CubicGrid(X.ravel(), Y.ravel(), 40, 50)
+    both = cg.interp(np.stack([F.ravel(), 2 * F.ravel()]), gx, gy).cpu().numpy()
+    one = cg.interp(F.ravel(), gx, gy).cpu().numpy()[0]
+    assert np.array_equal(both[0], one, equal_nan=True)
+    np.testing.assert_allclose(both[1], 2 * one, rtol=1e-12, atol=1e-15)
+    GH, GV = np.meshgrid(gx, gy)
+    with pytest.raises(NotImplementedError):
+        griddata((X.ravel(), Y.ravel()), F.ravel(), (GH, GV), method="linear")
+    Xf = X.copy()
+    Xf[:, 25:] = 2 * X[:, 25].reshape(-1, 1) - X[:, 25:]   # fold the lattice back on itself
+    with pytest.raises(_lib.AKBError):
+        CubicGrid(Xf.ravel(), Y.ravel(), 40, 50)
+
+
+def test_wave_maps_chain_vs_reference(gpu):
+    """detcenter2 / Wave2 of the reference's 65x65 ray_wave run -> grid, griddata, nanmean,
+    plane correction: the reference's plane_in / plane_out (= psf_calc's input)."""
+    from akbraytracing_amd import pupilmap as PM
+    f = golden("akb_raywave_65.npz")
+    g = golden("akb_psfcalc_65.npz")
+    r = PM.wave_maps(f["detcenter2"], f["dist_err2"], f["wave2"], 65, 65)
+    assert np.array_equal(r["grid_H"], g["grid_H0"]) and np.array_equal(r["grid_V"], g["grid_V0"])
+    w = r["matrixWave2"].cpu().numpy()
+    assert np.array_equal(np.isnan(w), np.isnan(g["plane_in"]))
+    rng_ = np.nanmax(g["plane_in"]) - np.nanmin(g["plane_in"])
+    assert np.nanmax(np.abs(w - g["plane_in"])) <= 1e-6 * rng_
+    c = r["matrixWave2_Corrected"].cpu().numpy()
+    assert np.nanmax(np.abs(c - g["plane_out"])) <= 1e-6 * rng_
+
+
 # ----------------------------------------------------------------------------- Huygens
 
 def test_huygens_cases(gpu):

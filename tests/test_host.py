@@ -208,3 +208,81 @@ def test_dropin_psf_module_exports():
     finally:
         sys.path.remove(akbraytracing_amd.DROPIN_DIR)
         sys.modules.pop("psf_fft", None)
+
+
+# ----------------------------------------------------------------------------- griddata triangulation
+
+def _cell_tris_np(X, Y):
+    """Cell split by the in-circle test (the rule k_gd_cells applies), as vertex triples."""
+    nv, nh = X.shape
+    x0, y0 = X[:-1, :-1], Y[:-1, :-1]
+    bx, by = X[:-1, 1:] - x0, Y[:-1, 1:] - y0
+    cx, cy = X[1:, 1:] - x0, Y[1:, 1:] - y0
+    dx, dy = X[1:, :-1] - x0, Y[1:, :-1] - y0
+    adx, ady, bdx, bdy, cdx, cdy = -dx, -dy, bx - dx, by - dy, cx - dx, cy - dy
+    A, B, C = adx * adx + ady * ady, bdx * bdx + bdy * bdy, cdx * cdx + cdy * cdy
+    det = adx * (bdy * C - B * cdy) - ady * (bdx * C - B * cdx) + A * (bdx * cdy - bdy * cdx)
+    o = bx * cy - by * cx
+    diag = np.where(o > 0, det, -det) > 0
+    iv, ih = np.meshgrid(np.arange(nv - 1), np.arange(nh - 1), indexing="ij")
+    p00 = iv * nh + ih
+    p01, p10, p11 = p00 + 1, p00 + nh, p00 + nh + 1
+    t0 = np.where(diag[..., None], np.stack([p00, p01, p10], -1), np.stack([p00, p01, p11], -1))
+    t1 = np.where(diag[..., None], np.stack([p01, p11, p10], -1), np.stack([p00, p11, p10], -1))
+    return np.concatenate([t0.reshape(-1, 3), t1.reshape(-1, 3)])
+
+
+def _ring_np(nv, nh):
+    return np.array([ih for ih in range(nh - 1)] + [iv * nh + nh - 1 for iv in range(nv - 1)] +
+                    [(nv - 1) * nh + ih for ih in range(nh - 1, 0, -1)] + [iv * nh for iv in range(nv - 1, 0, -1)])
+
+
+def _pockets(X, Y):
+    from akbraytracing_amd import _lib
+    L = _lib.lib()
+    nv, nh = X.shape
+    r = _ring_np(nv, nh)
+    rx, ry = np.ascontiguousarray(X.ravel()[r]), np.ascontiguousarray(Y.ravel()[r])
+    cap = len(r)
+    tri, nbr = np.zeros((cap, 3), np.int32), np.zeros((cap, 3), np.int32)
+    edge, xptr, xidx, n = np.zeros(cap, np.int32), np.zeros(cap + 1, np.int32), np.zeros(6 * cap, np.int32), np.zeros(1, np.int32)
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    _lib.check(L.akb_gd_pockets(p(rx), p(ry), nv, nh, cap, p(n), p(tri), p(nbr), p(edge), p(xptr), p(xidx)))
+    return tri[:n[0]], nbr[:n[0]], edge, xptr, xidx[:xptr[-1]]
+
+
+def _grids():
+    from conftest import golden
+    f = golden("akb_raywave_65.npz")
+    yield "ray_wave_65", f["detcenter2"][1].reshape(65, 65), f["detcenter2"][2].reshape(65, 65)
+    u, v = np.meshgrid(np.linspace(-1, 1, 300), np.linspace(-1, 1, 280))
+    yield "akb_like", u * 1e-4 + 3e-6 * v ** 2 - 2e-6 * u * v + 1e-6 * v ** 3, v * 1.3e-4 + 4e-6 * u ** 2 + 1e-6 * u ** 3
+    yield "skewed", u + 0.05 * v + 0.03 * (u + 0.3) ** 2, 0.8 * v - 0.04 * (v - 0.2) * u + 0.02 * u ** 3
+
+
+@pytest.mark.parametrize("case", ["ray_wave_65", "akb_like", "skewed"])
+def test_structured_triangulation_equals_qhull(case):
+    """Cells split by the in-circle test + akb_gd_pockets (host) = scipy's Delaunay (qhull),
+    triangle for triangle, on the reference's 65x65 detector hits and deformed lattices."""
+    from akbraytracing_amd import build
+    from scipy.spatial import Delaunay
+    build.build(verbose=False)
+    name, X, Y = next(g for g in _grids() if g[0] == case)
+    tri, nbr, edge, xptr, xidx = _pockets(X, Y)
+    ours = np.concatenate([_cell_tris_np(X, Y), tri])
+    P = np.stack([X.ravel(), Y.ravel()], 1)
+    q = Delaunay(P).simplices
+    assert len(ours) == len(q)
+    assert set(map(tuple, np.sort(ours, 1))) == set(map(tuple, np.sort(q, 1)))
+    # every pocket chord is listed from both ends, and every pocket edge on the ring is mapped
+    assert xptr[-1] == len(xidx) and len(xidx) % 2 == 0
+    assert np.count_nonzero(edge >= 0) == np.count_nonzero(nbr <= -2)
+
+
+def test_pockets_refuse_a_cut_corner():
+    from akbraytracing_amd import _lib
+    u, v = np.meshgrid(np.linspace(-1, 1, 20), np.linspace(-1, 1, 20))
+    X, Y = u.copy(), v.copy()
+    X[0, 0], Y[0, 0] = -0.5, -0.5   # the corner pulled inside the hull
+    with pytest.raises(_lib.AKBError):
+        _pockets(X, Y)
