@@ -140,7 +140,7 @@ def _declare(L):
         "akb_gd_check_pockets": ([c_vp, c_vp, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_dbl, c_vp, c_vp],
                                  c_int),
         "akb_gd_grad_sweep_f64": ([c_vp, c_vp, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
-                                   c_vp, c_vp, c_vp, c_vp], c_int),
+                                   c_vp, c_vp, c_vp, c_vp, c_vp], c_int),
         "akb_gd_eval_f64": ([c_vp, c_vp, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int,
                              c_vp, c_vp, c_int, c_vp, c_vp, c_vp], c_int),
     }

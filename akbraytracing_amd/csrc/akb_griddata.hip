@@ -184,6 +184,7 @@ __device__ int64_t tri_nbr(const Grid& g, int64_t t, int k) {
 // bit 2 a broken pocket adjacency, bits 3 / 4 cells of positive / negative orientation
 __global__ void __launch_bounds__(kBlock) k_gd_cells(Grid g, uint8_t* diag, double tol, unsigned* flags) {
     const int64_t nc = ncells(g);
+    unsigned acc = 0;
     for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < nc; c += (int64_t)gridDim.x * blockDim.x) {
         const int iv = (int)(c / (g.nh - 1)), ih = (int)(c - (int64_t)iv * (g.nh - 1));
         double bad = 0.0;
@@ -218,7 +219,13 @@ __global__ void __launch_bounds__(kBlock) k_gd_cells(Grid g, uint8_t* diag, doub
             const double s = fmax(fmax(fabs(ax), fabs(ay)), fmax(fmax(fabs(cx), fabs(cy)), fmax(fabs(ox), fabs(oy))));
             if (incircle(0.0, 0.0, ax, ay, cx, cy, ox, oy) > tol * s * s * s * s) f |= 2u;
         }
-        atomicOr(flags, f);
+        acc |= f;
+    }
+    // one atomic per wave, only for bits not yet set (every cell sets an orientation bit)
+    for (int off = 32; off > 0; off >>= 1) acc |= __shfl_down(acc, off);
+    if ((threadIdx.x & 63) == 0) {
+        const unsigned cur = __hip_atomic_load(flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((cur | acc) != cur) atomicOr(flags, acc);
     }
 }
 
@@ -277,53 +284,149 @@ struct GradAcc {
     double q0 = 0, q1 = 0, q3 = 0, s0 = 0, s1 = 0;
 };
 
-__device__ __forceinline__ void grad_edge(GradAcc& A, double xi, double yi, double fi, double xj, double yj,
-                                          double fj, double gj0, double gj1) {
-    const double ex = xj - xi, ey = yj - yi;
-    const double L = sqrt(ex * ex + ey * ey);
-    const double L3 = L * L * L;
-    const double df2 = -ex * gj0 - ey * gj1;
-    A.q0 += 4 * ex * ex / L3;
-    A.q1 += 4 * ex * ey / L3;
-    A.q3 += 4 * ey * ey / L3;
-    const double w = 6 * (fi - fj) - 2 * df2;
-    A.s0 += w * ex / L3;
-    A.s1 += w * ey / L3;
+// one edge (vertex i -> j) of the local problem, NV value sets
+template <int NV>
+__device__ __forceinline__ void grad_edge(const Grid& g, int64_t n, int64_t j, double xi, double yi,
+                                          const double (&fi)[NV], const double* __restrict__ f,
+                                          const double* __restrict__ gin, GradAcc (&A)[NV]) {
+    const double ex = g.x[j] - xi, ey = g.y[j] - yi;
+    // 1 / L^3 from the hardware reciprocal square root and one Newton step (relative error
+    // ~1e-16: this solve is converged to 1e-10, not reproduced bit for bit)
+    const double l2 = ex * ex + ey * ey;
+    double r = __builtin_amdgcn_rsq(l2);
+    r = r * __builtin_fma(-0.5 * l2 * r, r, 1.5);
+    const double r3 = r * r * r;
+    const double wx = ex * r3, wy = ey * r3;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const double df2 = -ex * gin[2 * (v * n + j)] - ey * gin[2 * (v * n + j) + 1];
+        A[v].q0 += 4 * ex * wx;
+        A[v].q1 += 4 * ex * wy;
+        A[v].q3 += 4 * ey * wy;
+        const double w = 6 * (fi[v] - f[v * n + j]) - 2 * df2;
+        A[v].s0 += w * wx;
+        A[v].s1 += w * wy;
+    }
 }
 
-// one Jacobi sweep: gout[i] from gin of the neighbours; the largest relative change -> chg
+// the 2 x 2 solve; returns the relative change (scipy's measure)
+__device__ __forceinline__ double grad_solve(const GradAcc& A, const double* gin, double* gout, int64_t o) {
+    const double inv = 1.0 / (A.q0 * A.q3 - A.q1 * A.q1);
+    const double r0 = (A.q3 * A.s0 - A.q1 * A.s1) * inv;
+    const double r1 = (-A.q1 * A.s0 + A.q0 * A.s1) * inv;
+    const double c = fmax(fabs(gin[o] + r0), fabs(gin[o + 1] + r1)) / fmax(1.0, fmax(fabs(r0), fabs(r1)));
+    gout[o] = -r0;
+    gout[o + 1] = -r1;
+    return c;
+}
+
+__device__ __forceinline__ void change_max(double worst, unsigned long long* chg) {
+    __shared__ double red[kBlock / 64];
+    for (int off = 32; off > 0; off >>= 1) worst = fmax(worst, __shfl_down(worst, off));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = worst;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kBlock / 64; ++w) worst = fmax(worst, red[w]);
+        const unsigned long long bits = (unsigned long long)__double_as_longlong(worst);
+        if (chg && worst > 0 && __hip_atomic_load(chg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < bits)
+            atomicMax(chg, bits);
+    }
+}
+
+// One Jacobi sweep for NV value sets sharing the geometry: gout[i] from gin of the grid
+// neighbours (4 axis + the diagonals of the 4 cells around i). Ring vertices also have pocket
+// chords - a hull vertex can fan out to thousands - so for them this kernel only stores the
+// grid-edge sums in ring_acc and k_gd_grad_ring adds the chords with a whole wave and solves.
+template <int NV>
 __global__ void __launch_bounds__(kBlock) k_gd_grad(Grid g, const double* __restrict__ f,
                                                     const double* __restrict__ gin, double* __restrict__ gout,
-                                                    unsigned long long* chg) {
+                                                    double* __restrict__ ring_acc, unsigned long long* chg) {
     const int64_t n = (int64_t)g.nv * g.nh;
     double worst = 0.0;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const int iv = (int)(i / g.nh), ih = (int)(i - (int64_t)iv * g.nh);
-        const double xi = g.x[i], yi = g.y[i], fi = f[i];
-        GradAcc A;
-        auto edge = [&](int64_t j) { grad_edge(A, xi, yi, fi, g.x[j], g.y[j], f[j], gin[2 * j], gin[2 * j + 1]); };
-        if (ih > 0) edge(i - 1);
-        if (ih < g.nh - 1) edge(i + 1);
-        if (iv > 0) edge(i - g.nh);
-        if (iv < g.nv - 1) edge(i + g.nh);
-        // diagonals of the four cells around the vertex
-        if (iv > 0 && ih > 0 && g.diag[(int64_t)(iv - 1) * (g.nh - 1) + ih - 1] == 0) edge(i - g.nh - 1);
-        if (iv > 0 && ih < g.nh - 1 && g.diag[(int64_t)(iv - 1) * (g.nh - 1) + ih] == 1) edge(i - g.nh + 1);
-        if (iv < g.nv - 1 && ih > 0 && g.diag[(int64_t)iv * (g.nh - 1) + ih - 1] == 1) edge(i + g.nh - 1);
-        if (iv < g.nv - 1 && ih < g.nh - 1 && g.diag[(int64_t)iv * (g.nh - 1) + ih] == 0) edge(i + g.nh + 1);
+        const double xi = g.x[i], yi = g.y[i];
+        double fi[NV];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) fi[v] = f[v * n + i];
+        GradAcc A[NV];
+        if (ih > 0) grad_edge<NV>(g, n, i - 1, xi, yi, fi, f, gin, A);
+        if (ih < g.nh - 1) grad_edge<NV>(g, n, i + 1, xi, yi, fi, f, gin, A);
+        if (iv > 0) grad_edge<NV>(g, n, i - g.nh, xi, yi, fi, f, gin, A);
+        if (iv < g.nv - 1) grad_edge<NV>(g, n, i + g.nh, xi, yi, fi, f, gin, A);
+        const int64_t c0 = (int64_t)iv * (g.nh - 1) + ih;  // cell with p00 = i
+        if (iv > 0 && ih > 0 && g.diag[c0 - g.nh] == 0) grad_edge<NV>(g, n, i - g.nh - 1, xi, yi, fi, f, gin, A);
+        if (iv > 0 && ih < g.nh - 1 && g.diag[c0 - (g.nh - 1)] == 1)
+            grad_edge<NV>(g, n, i - g.nh + 1, xi, yi, fi, f, gin, A);
+        if (iv < g.nv - 1 && ih > 0 && g.diag[c0 - 1] == 1) grad_edge<NV>(g, n, i + g.nh - 1, xi, yi, fi, f, gin, A);
+        if (iv < g.nv - 1 && ih < g.nh - 1 && g.diag[c0] == 0) grad_edge<NV>(g, n, i + g.nh + 1, xi, yi, fi, f, gin, A);
         const int64_t r = ring_pos(g, iv, ih);
-        if (r >= 0)
-            for (int32_t k = g.xptr[r]; k < g.xptr[r + 1]; ++k) edge(g.xidx[k]);
-        const double det = A.q0 * A.q3 - A.q1 * A.q1;
-        const double r0 = (A.q3 * A.s0 - A.q1 * A.s1) / det;
-        const double r1 = (-A.q1 * A.s0 + A.q0 * A.s1) / det;
-        const double c = fmax(fabs(gin[2 * i] + r0), fabs(gin[2 * i + 1] + r1)) / fmax(1.0, fmax(fabs(r0), fabs(r1)));
-        worst = fmax(worst, c);
-        gout[2 * i] = -r0;
-        gout[2 * i + 1] = -r1;
+        if (r >= 0) {
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                double* d = ring_acc + (r * NV + v) * 5;
+                d[0] = A[v].q0;
+                d[1] = A[v].q1;
+                d[2] = A[v].q3;
+                d[3] = A[v].s0;
+                d[4] = A[v].s1;
+            }
+            continue;
+        }
+#pragma unroll
+        for (int v = 0; v < NV; ++v) worst = fmax(worst, grad_solve(A[v], gin, gout, 2 * (v * n + i)));
     }
-    for (int off = 32; off > 0; off >>= 1) worst = fmax(worst, __shfl_down(worst, off));
-    if ((threadIdx.x & 63) == 0 && worst > 0) atomicMax(chg, (unsigned long long)__double_as_longlong(worst));
+    change_max(worst, chg);
+}
+
+// ring vertices: one wave each adds the pocket chords (lanes stride the chord list, fixed-order
+// wave reduction) to the grid-edge sums, then solves
+template <int NV>
+__global__ void __launch_bounds__(kBlock) k_gd_grad_ring(Grid g, const double* __restrict__ f,
+                                                         const double* __restrict__ gin, double* __restrict__ gout,
+                                                         const double* __restrict__ ring_acc, unsigned long long* chg) {
+    const int64_t n = (int64_t)g.nv * g.nh;
+    const int64_t a = g.nh - 1, b = g.nv - 1, L = 2 * a + 2 * b;
+    const int lane = threadIdx.x & 63;
+    double worst = 0.0;
+    for (int64_t r = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; r < L;
+         r += ((int64_t)gridDim.x * blockDim.x) >> 6) {
+        int64_t i;
+        if (r < a) i = r;
+        else if (r < a + b) i = (r - a) * g.nh + (g.nh - 1);
+        else if (r < 2 * a + b) i = (int64_t)(g.nv - 1) * g.nh + (g.nh - 1 - (r - a - b));
+        else i = (int64_t)(g.nv - 1 - (r - 2 * a - b)) * g.nh;
+        const double xi = g.x[i], yi = g.y[i];
+        double fi[NV];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) fi[v] = f[v * n + i];
+        GradAcc A[NV];
+        for (int32_t k = g.xptr[r] + lane; k < g.xptr[r + 1]; k += 64) grad_edge<NV>(g, n, g.xidx[k], xi, yi, fi, f, gin, A);
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            for (int off = 32; off > 0; off >>= 1) {
+                A[v].q0 += __shfl_down(A[v].q0, off);
+                A[v].q1 += __shfl_down(A[v].q1, off);
+                A[v].q3 += __shfl_down(A[v].q3, off);
+                A[v].s0 += __shfl_down(A[v].s0, off);
+                A[v].s1 += __shfl_down(A[v].s1, off);
+            }
+        }
+        if (lane == 0) {
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                const double* d = ring_acc + (r * NV + v) * 5;
+                GradAcc T;
+                T.q0 = d[0] + A[v].q0;
+                T.q1 = d[1] + A[v].q1;
+                T.q3 = d[2] + A[v].q3;
+                T.s0 = d[3] + A[v].s0;
+                T.s1 = d[4] + A[v].s1;
+                worst = fmax(worst, grad_solve(T, gin, gout, 2 * (v * n + i)));
+            }
+        }
+    }
+    change_max(worst, chg);
 }
 
 // ------------------------------------------------------------------ targets
@@ -359,27 +462,56 @@ __device__ __forceinline__ void bary(const Grid& g, const Tri& T, double px, dou
 
 constexpr double kInsideEps = 100 * 2.220446049250313e-16;
 
+// target index box of triangle T: columns [c0, c1), rows [r0, r1)
+__device__ __forceinline__ void tri_box(const Grid& g, const Targets& t, const Tri& T, int& c0, int& c1, int& r0,
+                                        int& r1) {
+    double xlo = g.x[T.v[0]], xhi = xlo, ylo = g.y[T.v[0]], yhi = ylo;
+    for (int k = 1; k < 3; ++k) {
+        xlo = fmin(xlo, g.x[T.v[k]]);
+        xhi = fmax(xhi, g.x[T.v[k]]);
+        ylo = fmin(ylo, g.y[T.v[k]]);
+        yhi = fmax(yhi, g.y[T.v[k]]);
+    }
+    const double padx = (xhi - xlo) * 1e-9, pady = (yhi - ylo) * 1e-9;
+    c0 = lower_idx(t.gx, t.mx, xlo - padx);
+    c1 = lower_idx(t.gx, t.mx, xhi + padx);
+    r0 = lower_idx(t.gy, t.my, ylo - pady);
+    r1 = lower_idx(t.gy, t.my, yhi + pady);
+}
+
+__device__ __forceinline__ void claim_one(const Grid& g, const Targets& t, const Tri& T, int id, int r, int c,
+                                          int* owner) {
+    double b[3];
+    bary(g, T, t.gx[c], t.gy[r], b);
+    if (b[0] >= -kInsideEps && b[1] >= -kInsideEps && b[2] >= -kInsideEps) atomicMin(&owner[(int64_t)r * t.mx + c], id);
+}
+
+// cell triangles (ids < 2 * ncells): one thread each, a box of a few targets
 __global__ void __launch_bounds__(kBlock) k_gd_claim(Grid g, Targets t, int* owner) {
-    const int64_t ntri = 2 * ncells(g) + g.npock;
+    const int64_t ntri = 2 * ncells(g);
     for (int64_t id = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; id < ntri; id += (int64_t)gridDim.x * blockDim.x) {
         const Tri T = tri_verts(g, id);
-        double xlo = g.x[T.v[0]], xhi = xlo, ylo = g.y[T.v[0]], yhi = ylo;
-        for (int k = 1; k < 3; ++k) {
-            xlo = fmin(xlo, g.x[T.v[k]]);
-            xhi = fmax(xhi, g.x[T.v[k]]);
-            ylo = fmin(ylo, g.y[T.v[k]]);
-            yhi = fmax(yhi, g.y[T.v[k]]);
-        }
-        const double padx = (xhi - xlo) * 1e-9, pady = (yhi - ylo) * 1e-9;
-        const int c0 = lower_idx(t.gx, t.mx, xlo - padx), c1 = lower_idx(t.gx, t.mx, xhi + padx);
-        const int r0 = lower_idx(t.gy, t.my, ylo - pady), r1 = lower_idx(t.gy, t.my, yhi + pady);
+        int c0, c1, r0, r1;
+        tri_box(g, t, T, c0, c1, r0, r1);
         for (int r = r0; r < r1; ++r)
-            for (int c = c0; c < c1; ++c) {
-                double b[3];
-                bary(g, T, t.gx[c], t.gy[r], b);
-                if (b[0] >= -kInsideEps && b[1] >= -kInsideEps && b[2] >= -kInsideEps)
-                    atomicMin(&owner[(int64_t)r * t.mx + c], (int)id);
-            }
+            for (int c = c0; c < c1; ++c) claim_one(g, t, T, (int)id, r, c, owner);
+    }
+}
+
+// pocket triangles: long slivers along the boundary whose boxes can hold thousands of targets,
+// so one workgroup per triangle, its threads striding the box
+__global__ void __launch_bounds__(kBlock) k_gd_claim_pockets(Grid g, Targets t, int* owner) {
+    const int64_t nc2 = 2 * ncells(g);
+    for (int64_t j = blockIdx.x; j < g.npock; j += gridDim.x) {
+        const Tri T = tri_verts(g, nc2 + j);
+        int c0, c1, r0, r1;
+        tri_box(g, t, T, c0, c1, r0, r1);
+        const int w = c1 - c0;
+        const int64_t m = (int64_t)w * (r1 - r0);
+        for (int64_t k = threadIdx.x; k < m; k += blockDim.x) {
+            const int r = r0 + (int)(k / w), c = c0 + (int)(k - (int64_t)(k / w) * w);
+            claim_one(g, t, T, (int)(nc2 + j), r, c, owner);
+        }
     }
 }
 
@@ -461,6 +593,21 @@ __global__ void k_fill_i32(int* p, int64_t n, int v) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = v;
 }
 
+// A/B knobs (environment, read once): workgroup cap of the sweep / claim launches, and the
+// per-sweep change reduction switched off (timing only)
+int64_t gd_grid_cap() {
+    static int64_t g = [] {
+        const char* e = getenv("AKB_GD_GRID");
+        const long long v = e ? atoll(e) : 0;
+        return (int64_t)(v >= 64 ? v : kStreamGridCap);
+    }();
+    return g;
+}
+bool gd_no_change() {
+    static bool b = getenv("AKB_GD_NOCHG") != nullptr;
+    return b;
+}
+
 }  // namespace
 }  // namespace akb
 
@@ -495,19 +642,32 @@ int akb_gd_check_pockets(const double* x, const double* y, int nv, int nh, const
     return launch_status("k_gd_check_pockets");
 }
 
-// one Jacobi sweep per value set; d_change: largest relative change (as ordered double bits,
-// zeroed by the caller), nvals value sets strided by n (values) and 2n (gradients)
+// one Jacobi sweep; d_change: largest relative change (as ordered double bits, zeroed by the
+// caller); nvals value sets strided by n (values) and 2n (gradients); ring_work: 10 L doubles
 int akb_gd_grad_sweep_f64(const double* x, const double* y, int nv, int nh, const uint8_t* diag, int npock,
                           const int32_t* ptri, const int32_t* pnbr, const int32_t* edge_tri, const int32_t* xptr,
                           const int32_t* xidx, const double* f, int nvals, const double* gin, double* gout,
-                          unsigned long long* d_change, void* stream) {
+                          double* ring_work, unsigned long long* d_change, void* stream) {
     clear_error();
-    AKB_REQUIRE(x && y && diag && f && gin && gout && d_change && nvals >= 1, "bad arguments");
+    AKB_REQUIRE(x && y && diag && f && gin && gout && ring_work && d_change && nvals >= 1, "bad arguments");
     Grid g{x, y, nv, nh, diag, npock, ptri, pnbr, edge_tri, xptr, xidx};
+    hipStream_t s = (hipStream_t)stream;
     const int64_t n = (int64_t)nv * nh;
-    for (int v = 0; v < nvals; ++v) {
-        k_gd_grad<<<grid_for(n, 1, kStreamGridCap), kBlock, 0, (hipStream_t)stream>>>(g, f + v * n, gin + 2 * v * n,
-                                                                                   gout + 2 * v * n, d_change);
+    const int64_t L = 2 * (int64_t)(nh - 1) + 2 * (int64_t)(nv - 1);
+    unsigned long long* chg = gd_no_change() ? nullptr : d_change;
+    const unsigned gr = grid_for(n, 1, gd_grid_cap());
+    const unsigned grr = grid_for(L * 64);
+    for (int v = 0; v < nvals; v += 2) {
+        const double* fv = f + v * n;
+        const double* gi = gin + 2 * v * n;
+        double* go = gout + 2 * v * n;
+        if (nvals - v >= 2) {
+            k_gd_grad<2><<<gr, kBlock, 0, s>>>(g, fv, gi, go, ring_work, chg);
+            k_gd_grad_ring<2><<<grr, kBlock, 0, s>>>(g, fv, gi, go, ring_work, chg);
+        } else {
+            k_gd_grad<1><<<gr, kBlock, 0, s>>>(g, fv, gi, go, ring_work, chg);
+            k_gd_grad_ring<1><<<grr, kBlock, 0, s>>>(g, fv, gi, go, ring_work, chg);
+        }
         int st = launch_status("k_gd_grad");
         if (st) return st;
     }
@@ -530,9 +690,14 @@ int akb_gd_eval_f64(const double* x, const double* y, int nv, int nh, const uint
     int st = launch_status("k_fill_i32");
     if (st) return st;
     const int64_t ntri = 2 * (int64_t)(nv - 1) * (nh - 1) + npock;
-    k_gd_claim<<<grid_for(ntri, 1, kStreamGridCap), kBlock, 0, s>>>(g, t, owner);
+    k_gd_claim<<<grid_for(ntri - npock, 1, gd_grid_cap()), kBlock, 0, s>>>(g, t, owner);
     st = launch_status("k_gd_claim");
     if (st) return st;
+    if (npock > 0) {
+        k_gd_claim_pockets<<<(unsigned)(npock < 16384 ? npock : 16384), kBlock, 0, s>>>(g, t, owner);
+        st = launch_status("k_gd_claim_pockets");
+        if (st) return st;
+    }
     k_gd_eval<<<grid_for(m, 1, kStreamGridCap), kBlock, 0, s>>>(g, t, owner, f, grad, nvals, out);
     return launch_status("k_gd_eval");
 }

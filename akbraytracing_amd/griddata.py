@@ -93,13 +93,15 @@ class CubicGrid:
         nvals = int(f.shape[0])
         g = [torch.zeros((nvals, self.nv * self.nh, 2), dtype=D.F64, device=self.dev) for _ in range(2)]
         change = torch.zeros(maxiter, dtype=torch.int64, device=self.dev)
+        ring = torch.empty(10 * self.L, dtype=D.F64, device=self.dev)
         s = D.stream_handle()
         cur, it = 0, 0
         while it < maxiter:
             stop = min(it + check_every, maxiter)
             for k in range(it, stop):
                 _lib.check(L.akb_gd_grad_sweep_f64(*self._tri_args(), D.ptr(self.xptr), D.ptr(self.xidx), D.ptr(f),
-                                                   nvals, D.ptr(g[cur]), D.ptr(g[1 - cur]), D.ptr(change[k:]), s))
+                                                   nvals, D.ptr(g[cur]), D.ptr(g[1 - cur]), D.ptr(ring),
+                                                   D.ptr(change[k:]), s))
                 cur = 1 - cur
             ch = change[it:stop].cpu().numpy().view(np.float64)
             done = np.nonzero(ch < tol)[0]

@@ -442,10 +442,11 @@ class RayWave:
         """Wave2 (nm) sampled onto a size x size pupil in ray-index space (nearest ray), as OPD in
         metres, and the pupil pitch of the detector-2 footprint (device [dx, dy]).
 
-        This stands in for griddata(cubic) + plane correction + rotate_with_nan of the driver
-        (:3689-3710, psf_calc :1121-1188; SURVEY.md §8 rows f1/f4, not yet built): the ray grid is
-        a smooth deformed structured grid, so index-space sampling keeps the pupil's shape. The
-        amplitude is psf_calc's mask (1 where the OPD is defined), formed inside the PSF kernel.
+        A fast stand-in for griddata(cubic) + plane correction + rotate_with_nan of the driver
+        (:3689-3710, psf_calc :1121-1188), used by the bench's PSF: the ray grid is a smooth
+        deformed structured grid, so index-space sampling keeps the pupil's shape. The faithful
+        chain is pupilmap.wave_maps + psfcalc.psf_calc. The amplitude is
+        psf_calc's mask (1 where the OPD is defined), formed inside the PSF kernel.
         Multi-GPU: each shard fills its rows and the pieces are summed over ranks."""
         L = _lib.lib()
         if self._opd_buf is None or self._opd_buf.shape[0] != size:

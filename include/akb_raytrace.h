@@ -333,7 +333,7 @@ int akb_legendre_rows_f64(const double* data, int n, int K, int order, const dou
  * convex hull, ring coordinates from akb_gd_cells_f64; ids >= 2 (n_v-1)(n_h-1)) ->
  * akb_gd_check_pockets. Gradients: akb_gd_grad_sweep_f64 (one Jacobi sweep of scipy's
  * estimate_gradients_2d_global local solve, largest relative change atomically max-ed into
- * *d_change as double bits) until converged. Values: akb_gd_eval_f64 (NaN outside the hull). */
+ * *d_change as double bits; ring_work: 10 * ring-length doubles) until converged. Values: akb_gd_eval_f64 (NaN outside the hull). */
 int akb_gd_cells_f64(const double* x, const double* y, int nv, int nh, uint8_t* diag, double tol, unsigned* d_flags,
                      double* ring_x, double* ring_y, void* stream);
 int akb_gd_pockets(const double* ring_x, const double* ring_y, int nv, int nh, int cap, int32_t* n_out,
@@ -344,7 +344,7 @@ int akb_gd_check_pockets(const double* x, const double* y, int nv, int nh, const
 int akb_gd_grad_sweep_f64(const double* x, const double* y, int nv, int nh, const uint8_t* diag, int npock,
                           const int32_t* ptri, const int32_t* pnbr, const int32_t* edge_tri, const int32_t* xptr,
                           const int32_t* xidx, const double* f, int nvals, const double* gin, double* gout,
-                          unsigned long long* d_change, void* stream);
+                          double* ring_work, unsigned long long* d_change, void* stream);
 int akb_gd_eval_f64(const double* x, const double* y, int nv, int nh, const uint8_t* diag, int npock,
                     const int32_t* ptri, const int32_t* pnbr, const int32_t* edge_tri, const double* gx, int mx,
                     const double* gy, int my, const double* f, const double* grad, int nvals, int* owner,

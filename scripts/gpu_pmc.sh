@@ -9,6 +9,8 @@ rc=$?; echo "list exit $rc"; [ $rc -eq 0 ] || exit $rc
 F64=$(grep -oE "SQ_INSTS_VALU_(FMA|MUL|ADD|TRANS)_F64" gpurun_out/counters.txt | sort -u | tr '\n' ' ')
 echo "f64 counters: $F64"
 REGEX="${PMC_REGEX:-k_chain|k_tilt|k_opd|k_pw|k_psf|fft}"
+CMD="${PMC_CMD:-python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline}"
+OUT="${PMC_OUT:-pmc}"
 i=0
 for SET in "FETCH_SIZE" "WRITE_SIZE" "$F64" "GRBM_GUI_ACTIVE SQ_WAVES SQ_INSTS_VALU" \
            "SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_SALU" \
@@ -16,8 +18,7 @@ for SET in "FETCH_SIZE" "WRITE_SIZE" "$F64" "GRBM_GUI_ACTIVE SQ_WAVES SQ_INSTS_V
   [ -n "$SET" ] || continue
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $SET --kernel-include-regex "$REGEX" --output-format csv \
-      -d gpurun_out/pmc_$i -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline \
-      > gpurun_out/pmc_$i.log 2>&1
+      -d gpurun_out/${OUT}_$i -o run -- $CMD > gpurun_out/${OUT}_$i.log 2>&1
   rc=$?; echo "pmc set $i ($SET) exit $rc"
   [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 done
