@@ -41,6 +41,7 @@ struct Grid {
     const int32_t* edge_tri;  // (L) pocket triangle across ring edge e, -1 (hull edge)
     const int32_t* xptr;   // (L + 1) extra neighbours of ring vertex r (pocket chords)
     const int32_t* xidx;
+    int no_xcd;  // 1: plain block order in the sweep (AKB_GD_NOXCD, A/B timing only)
 };
 
 __device__ __forceinline__ int64_t ncells(const Grid& g) { return (int64_t)(g.nv - 1) * (g.nh - 1); }
@@ -280,15 +281,21 @@ __device__ __forceinline__ int64_t ring_pos(const Grid& g, int iv, int ih) {
     return -1;
 }
 
+// sums of the local problem: Q (geometry only, shared by the value sets; the factor 4 applied at
+// the solve) and s per value set
+template <int NV>
 struct GradAcc {
-    double q0 = 0, q1 = 0, q3 = 0, s0 = 0, s1 = 0;
+    double q0 = 0, q1 = 0, q3 = 0;
+    double s0[NV] = {}, s1[NV] = {};
 };
+
+constexpr int64_t kGradChunk = 4 * kBlock;  // vertices per workgroup of a sweep
 
 // one edge (vertex i -> j) of the local problem, NV value sets
 template <int NV>
 __device__ __forceinline__ void grad_edge(const Grid& g, int64_t n, int64_t j, double xi, double yi,
                                           const double (&fi)[NV], const double* __restrict__ f,
-                                          const double* __restrict__ gin, GradAcc (&A)[NV]) {
+                                          const double* __restrict__ gin, GradAcc<NV>& A) {
     const double ex = g.x[j] - xi, ey = g.y[j] - yi;
     // 1 / L^3 from the hardware reciprocal square root and one Newton step (relative error
     // ~1e-16: this solve is converged to 1e-10, not reproduced bit for bit)
@@ -297,23 +304,26 @@ __device__ __forceinline__ void grad_edge(const Grid& g, int64_t n, int64_t j, d
     r = r * __builtin_fma(-0.5 * l2 * r, r, 1.5);
     const double r3 = r * r * r;
     const double wx = ex * r3, wy = ey * r3;
+    A.q0 = __builtin_fma(ex, wx, A.q0);
+    A.q1 = __builtin_fma(ex, wy, A.q1);
+    A.q3 = __builtin_fma(ey, wy, A.q3);
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
         const double df2 = -ex * gin[2 * (v * n + j)] - ey * gin[2 * (v * n + j) + 1];
-        A[v].q0 += 4 * ex * wx;
-        A[v].q1 += 4 * ex * wy;
-        A[v].q3 += 4 * ey * wy;
         const double w = 6 * (fi[v] - f[v * n + j]) - 2 * df2;
-        A[v].s0 += w * wx;
-        A[v].s1 += w * wy;
+        A.s0[v] = __builtin_fma(w, wx, A.s0[v]);
+        A.s1[v] = __builtin_fma(w, wy, A.s1[v]);
     }
 }
 
-// the 2 x 2 solve; returns the relative change (scipy's measure)
-__device__ __forceinline__ double grad_solve(const GradAcc& A, const double* gin, double* gout, int64_t o) {
-    const double inv = 1.0 / (A.q0 * A.q3 - A.q1 * A.q1);
-    const double r0 = (A.q3 * A.s0 - A.q1 * A.s1) * inv;
-    const double r1 = (-A.q1 * A.s0 + A.q0 * A.s1) * inv;
+// the 2 x 2 solve of value set v; returns the relative change (scipy's measure)
+template <int NV>
+__device__ __forceinline__ double grad_solve(const GradAcc<NV>& A, int v, const double* gin, double* gout,
+                                             int64_t o) {
+    const double q0 = 4 * A.q0, q1 = 4 * A.q1, q3 = 4 * A.q3;
+    const double inv = 1.0 / (q0 * q3 - q1 * q1);
+    const double r0 = (q3 * A.s0[v] - q1 * A.s1[v]) * inv;
+    const double r1 = (-q1 * A.s0[v] + q0 * A.s1[v]) * inv;
     const double c = fmax(fabs(gin[o] + r0), fabs(gin[o + 1] + r1)) / fmax(1.0, fmax(fabs(r0), fabs(r1)));
     gout[o] = -r0;
     gout[o + 1] = -r1;
@@ -343,13 +353,18 @@ __global__ void __launch_bounds__(kBlock) k_gd_grad(Grid g, const double* __rest
                                                     double* __restrict__ ring_acc, unsigned long long* chg) {
     const int64_t n = (int64_t)g.nv * g.nh;
     double worst = 0.0;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    // XCD-aware: the grid is a multiple of 8 and blocks b, b + 8, ... (one XCD, dealt round-robin)
+    // take consecutive chunks, so the rows above and below a chunk are read through the same L2
+    const int64_t per = gridDim.x / 8;
+    const int64_t chunk = g.no_xcd ? (int64_t)blockIdx.x : (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
+    const int64_t i0 = chunk * kGradChunk, i1 = i0 + kGradChunk < n ? i0 + kGradChunk : n;
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
         const int iv = (int)(i / g.nh), ih = (int)(i - (int64_t)iv * g.nh);
         const double xi = g.x[i], yi = g.y[i];
         double fi[NV];
 #pragma unroll
         for (int v = 0; v < NV; ++v) fi[v] = f[v * n + i];
-        GradAcc A[NV];
+        GradAcc<NV> A;
         if (ih > 0) grad_edge<NV>(g, n, i - 1, xi, yi, fi, f, gin, A);
         if (ih < g.nh - 1) grad_edge<NV>(g, n, i + 1, xi, yi, fi, f, gin, A);
         if (iv > 0) grad_edge<NV>(g, n, i - g.nh, xi, yi, fi, f, gin, A);
@@ -362,19 +377,19 @@ __global__ void __launch_bounds__(kBlock) k_gd_grad(Grid g, const double* __rest
         if (iv < g.nv - 1 && ih < g.nh - 1 && g.diag[c0] == 0) grad_edge<NV>(g, n, i + g.nh + 1, xi, yi, fi, f, gin, A);
         const int64_t r = ring_pos(g, iv, ih);
         if (r >= 0) {
+            double* d = ring_acc + r * (3 + 2 * NV);
+            d[0] = A.q0;
+            d[1] = A.q1;
+            d[2] = A.q3;
 #pragma unroll
             for (int v = 0; v < NV; ++v) {
-                double* d = ring_acc + (r * NV + v) * 5;
-                d[0] = A[v].q0;
-                d[1] = A[v].q1;
-                d[2] = A[v].q3;
-                d[3] = A[v].s0;
-                d[4] = A[v].s1;
+                d[3 + 2 * v] = A.s0[v];
+                d[4 + 2 * v] = A.s1[v];
             }
             continue;
         }
 #pragma unroll
-        for (int v = 0; v < NV; ++v) worst = fmax(worst, grad_solve(A[v], gin, gout, 2 * (v * n + i)));
+        for (int v = 0; v < NV; ++v) worst = fmax(worst, grad_solve<NV>(A, v, gin, gout, 2 * (v * n + i)));
     }
     change_max(worst, chg);
 }
@@ -400,30 +415,30 @@ __global__ void __launch_bounds__(kBlock) k_gd_grad_ring(Grid g, const double* _
         double fi[NV];
 #pragma unroll
         for (int v = 0; v < NV; ++v) fi[v] = f[v * n + i];
-        GradAcc A[NV];
+        GradAcc<NV> A;
         for (int32_t k = g.xptr[r] + lane; k < g.xptr[r + 1]; k += 64) grad_edge<NV>(g, n, g.xidx[k], xi, yi, fi, f, gin, A);
+        for (int off = 32; off > 0; off >>= 1) {
+            A.q0 += __shfl_down(A.q0, off);
+            A.q1 += __shfl_down(A.q1, off);
+            A.q3 += __shfl_down(A.q3, off);
 #pragma unroll
-        for (int v = 0; v < NV; ++v) {
-            for (int off = 32; off > 0; off >>= 1) {
-                A[v].q0 += __shfl_down(A[v].q0, off);
-                A[v].q1 += __shfl_down(A[v].q1, off);
-                A[v].q3 += __shfl_down(A[v].q3, off);
-                A[v].s0 += __shfl_down(A[v].s0, off);
-                A[v].s1 += __shfl_down(A[v].s1, off);
+            for (int v = 0; v < NV; ++v) {
+                A.s0[v] += __shfl_down(A.s0[v], off);
+                A.s1[v] += __shfl_down(A.s1[v], off);
             }
         }
         if (lane == 0) {
+            const double* d = ring_acc + r * (3 + 2 * NV);
+            A.q0 += d[0];
+            A.q1 += d[1];
+            A.q3 += d[2];
 #pragma unroll
             for (int v = 0; v < NV; ++v) {
-                const double* d = ring_acc + (r * NV + v) * 5;
-                GradAcc T;
-                T.q0 = d[0] + A[v].q0;
-                T.q1 = d[1] + A[v].q1;
-                T.q3 = d[2] + A[v].q3;
-                T.s0 = d[3] + A[v].s0;
-                T.s1 = d[4] + A[v].s1;
-                worst = fmax(worst, grad_solve(T, gin, gout, 2 * (v * n + i)));
+                A.s0[v] += d[3 + 2 * v];
+                A.s1[v] += d[4 + 2 * v];
             }
+#pragma unroll
+            for (int v = 0; v < NV; ++v) worst = fmax(worst, grad_solve<NV>(A, v, gin, gout, 2 * (v * n + i)));
         }
     }
     change_max(worst, chg);
@@ -603,6 +618,10 @@ int64_t gd_grid_cap() {
     }();
     return g;
 }
+int gd_no_xcd() {
+    static int b = getenv("AKB_GD_NOXCD") != nullptr ? 1 : 0;
+    return b;
+}
 bool gd_no_change() {
     static bool b = getenv("AKB_GD_NOCHG") != nullptr;
     return b;
@@ -650,12 +669,13 @@ int akb_gd_grad_sweep_f64(const double* x, const double* y, int nv, int nh, cons
                           double* ring_work, unsigned long long* d_change, void* stream) {
     clear_error();
     AKB_REQUIRE(x && y && diag && f && gin && gout && ring_work && d_change && nvals >= 1, "bad arguments");
-    Grid g{x, y, nv, nh, diag, npock, ptri, pnbr, edge_tri, xptr, xidx};
+    Grid g{x, y, nv, nh, diag, npock, ptri, pnbr, edge_tri, xptr, xidx, gd_no_xcd()};
     hipStream_t s = (hipStream_t)stream;
     const int64_t n = (int64_t)nv * nh;
     const int64_t L = 2 * (int64_t)(nh - 1) + 2 * (int64_t)(nv - 1);
     unsigned long long* chg = gd_no_change() ? nullptr : d_change;
-    const unsigned gr = grid_for(n, 1, gd_grid_cap());
+    const int64_t chunks = (n + kGradChunk - 1) / kGradChunk;
+    const unsigned gr = (unsigned)(8 * ((chunks + 7) / 8));  // a multiple of 8 for the XCD mapping
     const unsigned grr = grid_for(L * 64);
     for (int v = 0; v < nvals; v += 2) {
         const double* fv = f + v * n;
