@@ -14,12 +14,36 @@ import redirects every call site without editing the reference:
 Wavecalc scripts: install(W) rebinds forward_propagation_numpy_batch /
 forward_propagation_cupy_batch(_multi_gpu), used by their WaveField3D.forward_propagation.
 
+The driver's steps after the trace are rebound too: griddata (the module's
+`from scipy.interpolate import griddata`, :28), plane_correction_with_nan_and_outlier_filter,
+psf_calc (reading the module's live option_energy / option_AKB / directory_name as the reference
+does, :1161-1166, :1202-1214, :1271-1273), find_defocus and calc_dS. install(mod, names=[...])
+picks a subset; uninstall(mod) restores every original.
+
 The wrappers read the module's live `option_mpmath` flag (AKB_raytrace_20250312.py:92) at call
 time and hand the call to the original function when it is set (the mpmath branch, :399-443).
 """
 from . import primitives as _P
 from . import psf as _psf
 from . import wavecalc as _W
+
+
+def _lazy(modname, attr):
+    def call(*args, **kwargs):
+        import importlib
+        return getattr(importlib.import_module(f"{__package__}.{modname}"), attr)(*args, **kwargs)
+    return call
+
+
+def _psf_calc_for(mod):
+    """psf_calc with the module's globals, as the reference's psf_calc reads them."""
+    def psf_calc(matrixWave2_Corrected, grid_H, grid_V, defocusWave):
+        from .psfcalc import psf_calc as native
+        native(matrixWave2_Corrected, grid_H, grid_V, defocusWave,
+               option_energy=getattr(mod, "option_energy", "EUV"), option_AKB=getattr(mod, "option_AKB", True),
+               directory=getattr(mod, "directory_name", None))
+        return None  # the reference's psf_calc returns nothing; its results are the .npy files
+    return psf_calc
 
 _NATIVE = {
     "mirr_ray_intersection": _P.mirr_ray_intersection,
@@ -33,6 +57,11 @@ _NATIVE = {
     "forward_propagation_numpy_batch": _W.forward_propagation_numpy_batch,
     "forward_propagation_cupy_batch": _W.forward_propagation_cupy_batch,
     "forward_propagation_cupy_batch_multi_gpu": _W.forward_propagation_cupy_batch_multi_gpu,
+    "griddata": _lazy("griddata", "griddata"),
+    "plane_correction_with_nan_and_outlier_filter": _lazy("pupilmap", "plane_correction_with_nan_and_outlier_filter"),
+    "find_defocus": _lazy("focus", "find_defocus"),
+    "calc_dS": _lazy("wavedata", "calc_dS"),
+    "psf_calc": None,  # bound per module (_psf_calc_for)
 }
 # functions with an mpmath branch in the reference
 _MPMATH_AWARE = {"mirr_ray_intersection", "reflect_ray"}
@@ -60,7 +89,8 @@ def install(mod, names=None):
         if getattr(cur, "__akb_native__", False):
             done.append(name)
             continue
-        setattr(mod, name, _wrap(mod, name, cur, _NATIVE[name]))
+        native = _NATIVE[name] if _NATIVE[name] is not None else _psf_calc_for(mod)
+        setattr(mod, name, _wrap(mod, name, cur, native))
         done.append(name)
     return done
 

@@ -17,6 +17,7 @@ Multi-GPU: pass a Shard (contiguous V-rows of the grid) and a communicator (see 
 only exchanges are the 2n resample samples, a handful of means and the flag word.
 """
 import json
+import dataclasses
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -180,6 +181,7 @@ class _Front:
     full: bool
     stream: object
     flags: tuple
+    done: object = None  # event on the front's stream after its last kernel (the tilt parameters)
 
 
 class RayWave:
@@ -233,6 +235,9 @@ class RayWave:
         self._p2 = {}
         self._own = sample_ownership(self.shard, self.n)
         self._pert = perturbation.device_tables(self.n, self.n, self.dev) if perturbation is not None else None
+        # event after the last queued reader of the pass-2 buffers / extent keys (a back half
+        # and its pupil, possibly on another stream): the next pass 2 waits for it
+        self._back_done = None
 
     def _pass2_launch(self, want_rows):
         key = bool(want_rows)
@@ -335,6 +340,11 @@ class RayWave:
             np.tan(self.rand_v, out=th[self.n:])
         self._tan2.copy_(self._tan2_host, non_blocking=True)
         tan_h2, tan_v2 = self._tan2[:self.n], self._tan2[self.n:]
+        if self._back_done is not None:
+            # pass 2 rewrites the buffers a queued back half reads, and the tilt-parameter kernel
+            # behind it clears the extent keys that half's pupil reads
+            torch.cuda.current_stream().wait_event(self._back_done)
+            self._back_done = None
         r = self._pass2(want_rows=full, stream=stream)
         if self.comm.world > 1:
             self.comm.allreduce_sums(self._flags[1:2])
@@ -348,12 +358,30 @@ class RayWave:
         params = torch.empty(23, dtype=D.F64, device=self.dev)  # this run's own block
         _lib.check(L.akb_tilt_params_f64(D.ptr(sums), D.ptr(cnts), D.ptr(params), D.ptr(self._ext),
                                          D.ptr(self._flags), 2, stream))
+        done = torch.cuda.Event()
+        done.record()
         ev2.synchronize()
         return _Front(r=r, tan_h2=tan_h2, tan_v2=tan_v2, params=params, full=full, stream=stream,
-                      flags=(flags1, int(self._f_host[1])))
+                      flags=(flags1, int(self._f_host[1])), done=done)
 
-    def launch_back(self, f, opd=True, keep_rotated=False):
-        """Tilt, detectors and OPD of a launch_front (no host wait)."""
+    def launch_back(self, f, opd=True, keep_rotated=False, stream=None):
+        """Tilt, detectors and OPD of a launch_front (no host wait). stream: run them on that
+        stream instead of the front's - concurrently with the next launch_front's pass 1, which
+        is FP64-bound while this half is HBM-bound; the next pass 2 waits for it (and for a pupil
+        taken on the same stream)."""
+        if stream is None:
+            out = self._launch_back(f, opd, keep_rotated)
+        else:
+            stream.wait_event(f.done)
+            f.params.record_stream(stream)  # allocated on the front's stream, read here
+            with torch.cuda.stream(stream):
+                out = self._launch_back(dataclasses.replace(f, stream=None), opd, keep_rotated)
+        ev = torch.cuda.Event()
+        ev.record(stream if stream is not None else torch.cuda.current_stream())
+        self._back_done = ev
+        return out
+
+    def _launch_back(self, f, opd, keep_rotated):
         r = f.r
         if f.flags[1]:
             out = self._run_staged(None, f.tan_h2, f.tan_v2, opd, keep_rotated, f.full)
@@ -462,6 +490,9 @@ class RayWave:
         opd = self._opd_buf
         if self.comm.world > 1:
             opd = self.comm.allreduce_sums(opd)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._back_done = ev  # reads the extent keys the next tilt-parameter kernel clears
         return opd, self._pitch
 
     # -------------------------------------------------------------- accounting

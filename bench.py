@@ -12,7 +12,9 @@ OPD; then a 128 x 128 pupil padded x16 -> 2048^2 PSF (pruned 2-D DFT: the padded
 built). One step = all of it; its intersections are 2 passes x 4 mirrors x rays. Steps are
 pipelined the way a caller tracing many systems would run them: step k's pass 1 is queued ahead
 of step k-1's tilt / OPD / pupil / PSF (RayWave.launch_front / launch_back), which hides the
-host's resample; every step still does all of its work inside the timed region. Inputs (the two
+host's resample, and that back half runs on a second stream, concurrently with the FP64-bound
+pass 1 (it is HBM-bound); step k's pass 2 waits for it. Every step still does all of its work
+inside the timed region. Inputs (the two
 1-D angle tables) are resident on the device before timing. Multi-GPU: weak scaling, each rank
 owns ~1e7 rays (contiguous V-rows of a grid of round(sqrt(N * 1e7))^2 rays); the PSF runs on
 rank 0.
@@ -53,6 +55,9 @@ def parse():
     p.add_argument("--config", choices=("c3", "c5"), default="c3",
                    help="c3: BASELINE configs[2] (default, the headline); c5: configs[4], the Legendre "
                         "figure-error OPL perturbation on every ray + a 3-wavelength PSF stack")
+    p.add_argument("--back-stream", type=int, default=1,
+                   help="1: queue each step's tilt / OPD / pupil on a second stream, concurrent with the "
+                        "next step's FP64-bound pass 1 (0: behind it on one stream)")
     p.add_argument("--psf-start", choices=("pupil", "pass1"), default="pupil",
                    help="side-stream PSF starts as soon as the previous pupil is ready, beside pass 1 "
                         "(default; measured faster), or after this step's pass 1")
@@ -124,6 +129,7 @@ def main():
     psf_events = []
     psf_out = {}
     side = torch.cuda.Stream(device=dev)
+    back_stream = torch.cuda.Stream(device=dev)
     state = {"psf_done": None}
     fronts = []  # launched fronts (pass 1 .. tilt parameters) whose back half is still to queue
 
@@ -152,14 +158,18 @@ def main():
         state["psf_done"] = done
 
     def back(timed):
-        """Tilt, OPD and pupil of the oldest front, then its PSF."""
-        rw.launch_back(fronts.pop(0))
-        if state["psf_done"] is not None:  # the pupil buffer is reused: wait for its last reader
-            torch.cuda.current_stream().wait_event(state["psf_done"])
-            state["psf_done"] = None
-        opd, pitch = rw.pupil(args.pupil)
-        ready = torch.cuda.Event()
-        ready.record()
+        """Tilt, OPD and pupil of the oldest front (on the back stream, beside the next pass 1),
+        then its PSF."""
+        f = fronts.pop(0)
+        bs = back_stream if args.back_stream else torch.cuda.current_stream()
+        with torch.cuda.stream(bs):
+            rw.launch_back(f, stream=bs if args.back_stream else None)
+            if state["psf_done"] is not None:  # the pupil buffer is reused: wait for its last reader
+                bs.wait_event(state["psf_done"])
+                state["psf_done"] = None
+            opd, pitch = rw.pupil(args.pupil)
+            ready = torch.cuda.Event()
+            ready.record(bs)
         run_psf(opd, pitch, ready, timed)
 
     def step(timed):

@@ -305,6 +305,36 @@ def test_ray_wave_65_vs_reference(gpu):
     assert np.max(np.abs(out["wave2"].cpu().numpy() - f["wave2"])) <= 1e-4
 
 
+@pytest.mark.parametrize("n", [65, 1001])
+def test_two_stream_pipeline_equals_sequential_runs(gpu, n):
+    """bench.py's pipeline: each run's back half (tilt, OPD, pupil) on a second stream, beside
+    the next run's pass 1 - the same bits as run() one at a time, for every run in the chain."""
+    from akbraytracing_amd.wavefront import RayWave
+    rw = RayWave(_geom(), n)
+    seq = rw.run()
+    want = {k: seq[k].clone() for k in ("wave2", "dist_err2", "detcenter2")}
+    want_opd = rw.pupil(32)[0].clone()
+    bs = torch.cuda.Stream()
+    outs, opds = [], []
+
+    def back(front):
+        with torch.cuda.stream(bs):
+            outs.append(rw.launch_back(front, stream=bs))
+            opds.append(rw.pupil(32)[0].clone())
+
+    fronts = [rw.launch_front()]
+    for _ in range(3):
+        prev = fronts[-1]
+        fronts.append(rw.launch_front(overlap=lambda p=prev: back(p)))
+    back(fronts[-1])
+    torch.cuda.synchronize()
+    assert len(outs) == 4
+    for o, opd in zip(outs, opds):
+        for k, v in want.items():
+            assert torch.equal(o[k], v), k
+        assert torch.equal(opd, want_opd)
+
+
 def test_config5_legendre_opl_perturbation(gpu):
     """BASELINE config 5: the chain adds the Legendre figure-error model to each ray's OPL (model
     from oracle/legendre.py; the basis is pinned to legendre_fit by test_oracle_golden)."""
@@ -744,6 +774,34 @@ def test_install_on_a_driver_like_module(gpu):
     assert mod.mirr_ray_intersection(1, 2, 3) == "orig"
     akbraytracing_amd.uninstall(mod)
     assert mod.reflect_ray is O.reflect_ray
+
+
+def test_install_runs_the_ray_wave_post_trace_chain(gpu, tmp_path):
+    """The driver's :3653-3710 sequence through install()'d names: griddata x2, nanmean,
+    plane correction, psf_calc reading the module's option_energy / directory_name."""
+    import types
+    import akbraytracing_amd
+    from scipy.interpolate import griddata as sp_griddata
+    mod = types.ModuleType("fake_driver")
+    mod.griddata = sp_griddata
+    mod.plane_correction_with_nan_and_outlier_filter = lambda m: None
+    mod.psf_calc = lambda *a: None
+    mod.option_energy, mod.option_AKB, mod.directory_name = "EUV", True, str(tmp_path)
+    akbraytracing_amd.install(mod)
+    f = golden("akb_raywave_65.npz")
+    g = golden("akb_psfcalc_65.npz")
+    d2 = f["detcenter2"]
+    grid_H, grid_V = np.meshgrid(np.linspace(d2[1, :].min(), d2[1, :].max(), 65),
+                                 np.linspace(d2[2, :].min(), d2[2, :].max(), 65))
+    matrixWave2 = mod.griddata((d2[1, :], d2[2, :]), f["wave2"], (grid_H, grid_V), method="cubic")
+    matrixWave2 = matrixWave2 - np.nanmean(matrixWave2)
+    corrected = mod.plane_correction_with_nan_and_outlier_filter(matrixWave2)
+    rng_ = np.nanmax(g["plane_out"]) - np.nanmin(g["plane_out"])
+    assert np.nanmax(np.abs(corrected - g["plane_out"])) <= 1e-6 * rng_
+    assert mod.psf_calc(corrected, g["grid_H"], g["grid_V"], float(g["defocus"])) is None
+    assert np.load(tmp_path / "psf.npy").shape == (1056, 1056)
+    akbraytracing_amd.uninstall(mod)
+    assert mod.griddata is sp_griddata
 
 
 # ----------------------------------------------------------------------------- large sizes

@@ -176,6 +176,20 @@ def test_install_rebinds_and_respects_option_mpmath():
     assert mod.mirr_ray_intersection is orig and mod.compute_psf_fft is orig
 
 
+def test_install_covers_the_post_trace_steps():
+    import types
+    import akbraytracing_amd
+    mod = types.ModuleType("driver")
+    orig = lambda *a, **k: "reference"  # noqa: E731
+    post = ["griddata", "plane_correction_with_nan_and_outlier_filter", "psf_calc", "find_defocus", "calc_dS"]
+    for name in post:
+        setattr(mod, name, orig)
+    assert set(akbraytracing_amd.install(mod)) == set(post)
+    assert all(getattr(mod, n).__wrapped__ is orig for n in post)
+    akbraytracing_amd.uninstall(mod)
+    assert all(getattr(mod, n) is orig for n in post)
+
+
 def test_product_path_fails_loudly_without_gpu():
     import torch
     if torch.cuda.is_available():
