@@ -58,6 +58,8 @@ def parse():
     p.add_argument("--back-stream", type=int, default=1,
                    help="1: queue each step's tilt / OPD / pupil on a second stream, concurrent with the "
                         "next step's FP64-bound pass 1 (0: behind it on one stream)")
+    p.add_argument("--back-priority", type=int, default=0,
+                   help="torch stream priority of the back stream (lower = higher priority; 0 = normal)")
     p.add_argument("--psf-start", choices=("pupil", "pass1"), default="pupil",
                    help="side-stream PSF starts as soon as the previous pupil is ready, beside pass 1 "
                         "(default; measured faster), or after this step's pass 1")
@@ -129,7 +131,9 @@ def main():
     psf_events = []
     psf_out = {}
     side = torch.cuda.Stream(device=dev)
-    back_stream = torch.cuda.Stream(device=dev)
+    # --back-priority -1 lets the HBM-bound back half take CU slots ahead of the FP64-bound pass 1
+    # it overlaps; measured a wash (the host resample then lands on the critical path), so off
+    back_stream = torch.cuda.Stream(device=dev, priority=args.back_priority)
     state = {"psf_done": None}
     fronts = []  # launched fronts (pass 1 .. tilt parameters) whose back half is still to queue
 
