@@ -84,9 +84,24 @@ def cpu_baseline(seconds):
         if el >= seconds or reps >= 1000:
             break
     inter = 2 * len(g["mirrors"]) * n * n * reps
+    # the same pipeline on one thread (SURVEY.md §8(d) asks for both), a shorter sample
+    oracle.set_threads(1)
+    n1, reps1, t1 = 501, 0, time.perf_counter()
+    try:
+        while True:
+            OPL.akb_ray_wave(g, n1)
+            reps1 += 1
+            el1 = time.perf_counter() - t1
+            if el1 >= seconds / 4 or reps1 >= 1000:
+                break
+    finally:
+        oracle.set_threads(threads)
+    one = 2 * len(g["mirrors"]) * n1 * n1 * reps1 / el1
     return {"value": inter / el, "unit": "intersections/s", "cores": threads, "kind": "port",
             "sample": f"oracle ray_wave pipeline (C primitives, OpenMP {threads} threads, numpy means/interp1d) "
-                      f"on a {n}x{n} grid, {reps} reps in {el:.1f} s"}
+                      f"on a {n}x{n} grid, {reps} reps in {el:.1f} s",
+            "value_1thread": one,
+            "sample_1thread": f"same pipeline, 1 thread, {n1}x{n1} grid, {reps1} reps in {el1:.1f} s"}
 
 
 def read_pmc():
@@ -246,6 +261,9 @@ def main():
         },
         "psf_ms": psf_ms,
         "psf_alone_ms": psf_alone_ms,
+        # the PSF's compulsory HBM traffic is its output (the pupil is 128 KB): intensity planes
+        "psf_alone_output_gbs": (len(lams) * (args.pupil * args.pad) ** 2 * 8 / (psf_alone_ms * 1e-3) / 1e9
+                                 if psf_alone_ms else None),
         "pass2_kernel_ms": k_avg,
         "roofline": {
             "kernel": "k_chain<grid,opl> (pass 2)",
