@@ -25,9 +25,13 @@ def init_from_env(backend=None):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 and not dist.is_initialized():
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            # AKB_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share devices round-robin,
+            # collectives staged through the host); the default is RCCL, one rank per GPU
+            backend = os.environ.get("AKB_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         if backend == "nccl":
             torch.cuda.set_device(local)
+        elif torch.cuda.is_available():
+            torch.cuda.set_device(local % torch.cuda.device_count())
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group(backend=backend, rank=rank, world_size=world)
     elif torch.cuda.is_available():
@@ -42,20 +46,30 @@ class TorchComm:
         self.world = dist.get_world_size() if dist.is_initialized() else 1
         self.rank = dist.get_rank() if dist.is_initialized() else 0
         self.device = device
+        # gloo with device tensors (a rehearsal of the RCCL path): stage through host memory
+        self._stage = dist.is_initialized() and dist.get_backend() == "gloo"
 
     def _dev(self, t):
         return t if self.device is None else t.to(self.device)
 
+    def _all_reduce(self, t, op):
+        t = t.contiguous()
+        if self._stage and t.is_cuda:
+            h = t.cpu()
+            dist.all_reduce(h, op=op)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, op=op)
+        return t
+
     def allreduce_sums(self, t):
         if self.world > 1:
-            t = t.contiguous()
-            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            t = self._all_reduce(t, dist.ReduceOp.SUM)
         return t
 
     def allreduce_max(self, t):
         if self.world > 1:
-            t = t.contiguous()
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            t = self._all_reduce(t, dist.ReduceOp.MAX)
         return t
 
     def gather_samples(self, samp_h, samp_v, shard, n):
@@ -83,6 +97,8 @@ class TorchComm:
         mx = max(counts)
         pad = torch.zeros(mx, dtype=piece.dtype, device=piece.device)
         pad[:piece.shape[0]] = piece
+        if self._stage and pad.is_cuda:
+            return self.allgather_field(piece.cpu(), counts).to(piece.device)
         bufs = [torch.empty_like(pad) for _ in range(self.world)]
         if pad.is_complex():
             real = [torch.view_as_real(b) for b in bufs]

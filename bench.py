@@ -189,6 +189,7 @@ def main():
             opd, pitch = rw.pupil(args.pupil)
             ready = torch.cuda.Event()
             ready.record(bs)
+        state["pupil"] = (opd, pitch)
         run_psf(opd, pitch, ready, timed)
 
     def step(timed):
@@ -212,8 +213,8 @@ def main():
         back(False)
     torch.cuda.synchronize()
     psf_alone_ms = None
-    if rank == 0:  # the PSF's own wall time, nothing beside it
-        opd, pitch = rw.pupil(args.pupil)
+    if rank == 0:  # the PSF's own wall time, nothing beside it (the last pupil: rw.pupil is collective)
+        opd, pitch = state["pupil"]
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
         for _ in range(10):
