@@ -34,6 +34,7 @@ EXPORTS = [
     "akb_seglen_f64", "akb_rotate_f64", "akb_fill_nan_f64",
     "akb_trace_chain_f64", "akb_chain_desc_size", "akb_tilt_opd_f64", "akb_tilt_params_f64",
     "akb_tilt_opd_dev_f64", "akb_opd_f64", "akb_resample_f64", "akb_plane_sweep_rows_f64",
+    "akb_plane_sweep_sink_f64",
     "akb_calc_ds_f64",
     "akb_pairwise_work_bytes", "akb_pairwise_sum_f64", "akb_pupil_sample_f64",
     "akb_leaf_sink_bytes", "akb_leaf_sink_layout", "akb_leaf_finish_work_bytes", "akb_leaf_finish_f64",
@@ -111,6 +112,8 @@ def _declare(L):
         "akb_resample_f64": ([c_vp, c_vp, c_i64, c_vp], c_int),
         "akb_calc_ds_f64": ([c_vp, c_i64, c_int, c_int, c_vp, c_vp], c_int),
         "akb_plane_sweep_rows_f64": ([c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_int, c_vp, c_vp, c_vp], c_int),
+        "akb_plane_sweep_sink_f64": ([c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_int, c_vp,
+                                      ctypes.POINTER(LeafSink), c_vp], c_int),
         "akb_pupil_sample_f64": ([c_vp, c_i64, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_vp], c_int),
         "akb_leaf_sink_bytes": ([c_int, c_i64], c_i64),
         "akb_leaf_sink_layout": ([c_vp, c_int, c_int, c_i64, ctypes.POINTER(LeafSink)], c_int),

@@ -390,7 +390,7 @@ int64_t akb_leaf_sink_bytes(int nq, int64_t n) {
 
 int akb_leaf_sink_layout(void* base, int nq, int nan_mask, int64_t n, akb_leaf_sink* out) {
     clear_error();
-    AKB_REQUIRE(base && out && nq > 0 && nq <= 8 && n >= 0, "bad sink layout arguments");
+    AKB_REQUIRE(base && out && nq > 0 && nq <= 4096 && n >= 0, "bad sink layout arguments");
     const int64_t nleaves = (n / kPwBuf) * (kPwBuf / kPwLeaf);
     const int64_t a = ((int64_t)nq * nleaves * 8 + 255) / 256 * 256;
     const int64_t b = ((int64_t)nq * nleaves * 4 + 255) / 256 * 256;
@@ -411,7 +411,7 @@ int64_t akb_leaf_finish_work_bytes(int nq, int64_t n) {
 int akb_leaf_finish_f64(const akb_leaf_sink* sink, double* d_sum, int64_t* d_count, void* work, void* stream) {
     clear_error();
     AKB_REQUIRE(sink && d_sum && d_count && work, "null pointer");
-    AKB_REQUIRE(sink->nq > 0 && sink->nq <= 8 && sink->n >= 0, "bad sink");
+    AKB_REQUIRE(sink->nq > 0 && sink->nq <= 4096 && sink->n >= 0, "bad sink");
     hipStream_t s = (hipStream_t)stream;
     const int nq = sink->nq;
     if (sink->n == 0) {

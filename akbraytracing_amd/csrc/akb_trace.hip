@@ -192,6 +192,79 @@ __global__ void __launch_bounds__(kBlock) k_plane_sweep(const double* __restrict
     }
 }
 
+// The same sweep with np.std's two sums fused: each workgroup loads a 256-ray segment once and,
+// plane after plane, hands the segment's y / z (pass A) or squared deviations (pass B) to a leaf
+// sink of 2P quantities (plane p -> quantities 2p, 2p + 1). Nothing per plane reaches HBM but the
+// leaf sums, and the rays are read once per pass instead of once per plane.
+constexpr int kSweepGroup = 8;  // planes per leaf reduction round (16 quantities: every thread busy)
+
+__global__ void __launch_bounds__(kBlock) k_plane_sweep_sink(const double* __restrict__ dir,
+                                                             const double* __restrict__ pt, int64_t ld,
+                                                             const int64_t* __restrict__ subset, int64_t m,
+                                                             const double* __restrict__ plane_j, int P,
+                                                             const double* __restrict__ sums, double n_div,
+                                                             akb_leaf_sink sink) {
+    __shared__ LeafLds<2 * kSweepGroup> L;
+    extern __shared__ double mean[];  // pass B: the 2P means, divided once per workgroup
+    if (sums) {
+        for (int q = threadIdx.x; q < 2 * P; q += blockDim.x) mean[q] = sums[q] / n_div;  // np.mean: sum / n
+        __syncthreads();
+    }
+    const int64_t nseg = (m + kLeafSeg - 1) / kLeafSeg;
+    const int64_t nleaves = (sink.n / kNpBuf) * kNpBuf / 128;
+    for (int64_t seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
+        const int64_t k = seg * kLeafSeg + threadIdx.x;
+        const bool valid = k < m;
+        double l = 0.0, mm = 0.0, nn = 0.0, px = 0.0, py = 0.0, pz = 0.0;
+        if (valid) {
+            const int64_t i = subset ? subset[k] : k;
+            l = dir[i];
+            mm = dir[ld + i];
+            nn = dir[2 * ld + i];
+            px = pt[i];
+            py = pt[ld + i];
+            pz = pt[2 * ld + i];
+        }
+        // plane_hit's denominator (1 l + 0 m + 0 n) is the same for every plane: one IEEE
+        // reciprocal, then each plane's quotient by the shared-reciprocal correction (RN(x / s)
+        // exactly, div_shared); a zero / non-finite / tiny denominator takes the plain division
+        const double den = 1.0 * l + 0.0 * mm + 0.0 * nn;
+        const double inv = 1.0 / den;
+        const bool shared = fabs(den) >= 0x1p-900 && fabs(den) <= 0x1p+900;
+        for (int p0 = 0; p0 < P; p0 += kSweepGroup) {
+            double v[2 * kSweepGroup];
+#pragma unroll
+            for (int g = 0; g < kSweepGroup; ++g) {
+                const int p = p0 + g;
+                v[2 * g] = 0.0;
+                v[2 * g + 1] = 0.0;
+                if (valid && p < P) {
+                    const double num = -(1.0 * px + 0.0 * py + 0.0 * pz + plane_j[p]);
+                    const double an = fabs(num);
+                    const bool ok = shared && (num == 0.0 || (an >= 0x1p-900 && an <= 0x1p+900));
+                    const double t = ok ? div_shared(num, den, inv) : num / den;
+                    const double y = t * mm + py;
+                    const double z = t * nn + pz;
+                    if (sums) {
+                        const double dy = y - mean[2 * p], dz = z - mean[2 * p + 1];
+                        v[2 * g] = dy * dy;
+                        v[2 * g + 1] = dz * dz;
+                    } else {
+                        v[2 * g] = y;
+                        v[2 * g + 1] = z;
+                    }
+                }
+            }
+            // quantities 2 p0 .. 2 p0 + 15 (the sink is padded to a multiple of 16)
+            akb_leaf_sink S = sink;
+            S.leaf_sum += (int64_t)(2 * p0) * nleaves;
+            S.leaf_cnt += (int64_t)(2 * p0) * nleaves;
+            S.tail += (int64_t)(2 * p0) * kNpBuf;
+            leaf_sink_segment<2 * kSweepGroup>(S, L, seg * kLeafSeg, v, valid);
+        }
+    }
+}
+
 // ----------------------------------------------------------------------------------------------
 // calc_dS (ref AKB_raytrace_20250312.py:13418-13473): the area element of each point of a (V, H)
 // grid of mirror points = half the summed |cross| of its four neighbour triangles (right-up,
@@ -1057,6 +1130,25 @@ int akb_plane_sweep_rows_f64(const double* dir, const double* pt, int64_t ld, in
     k_plane_sweep<<<dim3(gx, P), kBlock, 0, (hipStream_t)stream>>>(dir, pt, ld, subset, m, d_plane_j, P, d_sums,
                                                                    (double)m, rows);
     return launch_status("k_plane_sweep");
+}
+
+int akb_plane_sweep_sink_f64(const double* dir, const double* pt, int64_t ld, int64_t n, const int64_t* subset,
+                             int64_t m, const double* d_plane_j, int P, const double* d_sums,
+                             const akb_leaf_sink* sink, void* stream) {
+    clear_error();
+    AKB_REQUIRE(dir && pt && d_plane_j && sink, "null pointer");
+    AKB_REQUIRE(n >= 0 && ld >= n && m >= 0 && (subset || m == n), "bad sizes");
+    AKB_REQUIRE(P > 0 && sink->nq >= 2 * P && sink->nq % (2 * kSweepGroup) == 0 && sink->n == m &&
+                    sink->nan_mask == 0,
+                "the sink must hold 2P quantities (padded to a multiple of 16) of m elements, no NaN skipping");
+    if (m == 0) return AKB_OK;
+    const int64_t nseg = (m + kLeafSeg - 1) / kLeafSeg;
+    const unsigned g = (unsigned)(nseg < kStreamGridCap ? nseg : kStreamGridCap);
+    AKB_REQUIRE(P <= 2048, "at most 2048 planes per sweep");
+    const size_t lds = d_sums ? (size_t)(2 * P) * sizeof(double) : 0;
+    k_plane_sweep_sink<<<g, kBlock, lds, (hipStream_t)stream>>>(dir, pt, ld, subset, m, d_plane_j, P, d_sums,
+                                                                (double)m, *sink);
+    return launch_status("k_plane_sweep_sink");
 }
 
 int akb_calc_ds_f64(const double* points, int64_t ld, int V, int H, double* d_out, void* stream) {

@@ -3,16 +3,18 @@
 find_defocus (AKB_raytrace_20250312.py:9086-9170) traces once and then intersects the same rays
 with 50 detector planes per loop, 10 loops, taking np.std of the hits' y and z on each plane and
 narrowing the range around the best one. plane_std_sweep does one such loop on the device for any
-number of planes at once: one kernel writes every plane's hit rows, numpy-order row sums give the
-means, a second kernel writes the squared deviations, and their sums give np.std exactly as the
-reference computes it (so the argmin, and find_defocus's answer, are the reference's own).
+number of planes at once: one kernel reads each ray once and feeds every plane's hit y / z to
+numpy-order leaf sums (the means), a second feeds the squared deviations (np.std's second pass),
+so np.std comes out exactly as the reference computes it (the argmin, and find_defocus's answer,
+are the reference's own) without writing a row per plane. PlaneSweep(fused=False) keeps the
+row-writing variant (akb_plane_sweep_rows_f64 + akb_pairwise_sum_f64) for comparison.
 """
 import numpy as np
 import torch
 
 from . import _lib
 from . import device as D
-from .reduce import RowSums
+from .reduce import LeafSink, RowSums
 
 
 def _dev3(a, dev):
@@ -23,7 +25,9 @@ def _dev3(a, dev):
 class PlaneSweep:
     """Rays (dir, pt: (3, n)) held on the device for repeated plane sweeps."""
 
-    def __init__(self, rays, points, subset=None):
+    def __init__(self, rays, points, subset=None, fused=True):
+        self.fused = bool(fused)
+        self._sinks = {}
         self.dev = D.device()
         self.dir = _dev3(rays, self.dev)
         self.pt = _dev3(points, self.dev)
@@ -37,6 +41,17 @@ class PlaneSweep:
         L = _lib.lib()
         j = torch.from_numpy(np.ascontiguousarray(plane_j, dtype=np.float64)).to(self.dev)
         P = int(j.shape[0])
+        if self.fused:
+            sink = self._sinks.get(P)
+            if sink is None:
+                sink = self._sinks[P] = LeafSink(-(-2 * P // 16) * 16, self.m, 0, self.dev)
+            args = (D.ptr(self.dir), D.ptr(self.pt), self.n, self.n, D.ptr(self.subset), self.m, D.ptr(j), P)
+            _lib.check(L.akb_plane_sweep_sink_f64(*args, None, sink.desc, D.stream_handle()))
+            s1 = sink.finish()[0][:2 * P].clone()
+            _lib.check(L.akb_plane_sweep_sink_f64(*args, D.ptr(s1), sink.desc, D.stream_handle()))
+            s2 = sink.finish()[0][:2 * P]
+            sd = np.sqrt(s2.cpu().numpy() / self.m)  # np.std: ret / rcount, then sqrt
+            return sd[0::2], sd[1::2]
         rows = torch.empty((2 * P, self.m), dtype=D.F64, device=self.dev)
         args = (D.ptr(self.dir), D.ptr(self.pt), self.n, self.n, D.ptr(self.subset), self.m, D.ptr(j), P)
         _lib.check(L.akb_plane_sweep_rows_f64(*args, None, D.ptr(rows), D.stream_handle()))

@@ -117,7 +117,7 @@ typedef struct akb_leaf_sink {
     int32_t* leaf_cnt;  /* [nq][n_full_leaves] */
     double* tail;       /* [nq][8192] */
     int32_t nq;         /* 0 disables the sink */
-    int32_t nan_mask;   /* bit q set: NaN -> 0 and not counted (np.nansum / np.nanmean) */
+    int32_t nan_mask;   /* bit q set: NaN -> 0 and not counted (np.nansum / np.nanmean); q >= 31 use bit 31 */
     int64_t n;          /* elements reduced per quantity */
 } akb_leaf_sink;
 
@@ -209,6 +209,13 @@ int akb_tilt_opd_dev_f64(const double* d_params, const double det1_ghij[4], cons
 int akb_plane_sweep_rows_f64(const double* dir, const double* pt, int64_t ld, int64_t n, const int64_t* subset,
                              int64_t m, const double* d_plane_j, int P, const double* d_sums, double* rows,
                              void* stream);
+/* The same two passes with np.std's sums fused (rays read once per pass, no rows written): plane p
+ * feeds quantities 2p (y or (y - mean)^2) and 2p + 1 (z ...) of `sink` (nq = 2P rounded up to a
+ * multiple of 16 - the extra quantities sum to 0 -, n = m, nan_mask 0); akb_leaf_finish_f64 then gives the numpy-order sums akb_pairwise_sum_f64 gives on
+ * the rows. Pass B: d_sums = pass A's 2P sums. */
+int akb_plane_sweep_sink_f64(const double* dir, const double* pt, int64_t ld, int64_t n, const int64_t* subset,
+                             int64_t m, const double* d_plane_j, int P, const double* d_sums,
+                             const akb_leaf_sink* sink, void* stream);
 
 /* calc_dS (ref :13418-13473): area element of each point of a (V, H) grid of mirror points
  * (points (3, ld), flat index iv * H + ih): half the summed |cross| of the four neighbour

@@ -494,6 +494,24 @@ def test_plane_sweep_subset_vs_oracle(gpu):
         assert sh[p] == np.std(det[1]) and sv[p] == np.std(det[2])
 
 
+@pytest.mark.parametrize("m", [1000, 8192, 100003])
+def test_plane_sweep_fused_equals_rows_and_numpy(gpu, m):
+    """The fused sweep (leaf sums, no rows) gives the row variant's and numpy's np.std bits, on
+    short, one-buffer and many-buffer + tail ray counts."""
+    from akbraytracing_amd import focus as F
+    rng = np.random.default_rng(m)
+    d = np.vstack([np.ones(m), 1e-3 * rng.standard_normal(m), 1e-3 * rng.standard_normal(m)])
+    d /= np.linalg.norm(d, axis=0)
+    p = np.vstack([145.0 + rng.random(m), 1e-4 * rng.standard_normal(m), 1e-4 * rng.standard_normal(m)])
+    j = -(146.0 + np.linspace(-0.3, 0.3, 9))
+    fused = F.PlaneSweep(d, p).std(j)
+    rows = F.PlaneSweep(d, p, fused=False).std(j)
+    assert np.array_equal(fused[0], rows[0]) and np.array_equal(fused[1], rows[1])
+    for k in (0, 4, 8):
+        det = O.plane_ray_intersection([0] * 6 + [1.0, 0.0, 0.0, j[k]], d, p)
+        assert fused[0][k] == np.std(det[1]) and fused[1][k] == np.std(det[2])
+
+
 # ----------------------------------------------------------------------------- wave data (f3)
 
 def test_calc_ds_vs_reference(gpu):
