@@ -127,6 +127,72 @@ __device__ __forceinline__ double norm3(double x, double y, double z) {
     return sqrt_cr(x * x + y * y + z * z);
 }
 
+// div_shared for a divisor known to be positive (a norm): the residual is formed with the opposite
+// sign, rn = RN(s q - x) = -RN(x - s q), so q - rn inv equals the corrected quotient for every
+// non-zero residual and, for a zero residual, keeps q together with the sign of a zero quotient
+// (x = +-0 gives rn = +0 and q - (+0) inv = q) without div_shared's compare and selects.
+// s < 0 would lose the sign of a +0 quotient: the callers' divisors are norms.
+__device__ __forceinline__ double div_pos(double x, double s, double inv) {
+    const double q = x * inv;
+    const double rn = __builtin_fma(s, q, -x);
+    return __builtin_fma(-rn, inv, q);
+}
+
+// s = np.linalg.norm of (x, y, z) and inv = RN(1 / s), sharing sqrt_cr's range test: for a squared
+// norm in [2^-767, 2^1000], s lies in [2^-384, 2^500], where hipcc's IEEE division 1 / s neither
+// scales its operands (v_div_scale) nor fixes its result up (v_div_fmas / v_div_fixup are the
+// identity), so the remaining rcp + two Newton steps + the final correction give its bits exactly
+// in 7 instead of 11 instructions. Outside the range both take the library operations.
+__device__ __forceinline__ void norm3_inv(double x, double y, double z, double& s, double& inv) {
+    const double v = x * x + y * y + z * z;
+    if (__builtin_expect(v >= 0x1p-767 && v <= 0x1p+1000, 1)) {
+        const double r = __builtin_amdgcn_rsq(v);
+        double g = v * r;
+        double h = r * 0.5;
+        const double e = __builtin_fma(-h, g, 0.5);
+        g = __builtin_fma(g, e, g);
+        const double d = __builtin_fma(-g, g, v);
+        h = __builtin_fma(h, e, h);
+        g = __builtin_fma(d, h, g);
+        const double d2 = __builtin_fma(-g, g, v);
+        s = __builtin_fma(d2, h, g);
+        double y0 = __builtin_amdgcn_rcp(s);
+        double e0 = __builtin_fma(-s, y0, 1.0);
+        y0 = __builtin_fma(y0, e0, y0);
+        e0 = __builtin_fma(-s, y0, 1.0);
+        y0 = __builtin_fma(y0, e0, y0);
+        const double r1 = __builtin_fma(-s, y0, 1.0);  // q = 1 * y0 = y0
+        inv = __builtin_fma(r1, y0, y0);
+    } else {
+        s = sqrt(v);
+        inv = 1.0 / s;
+    }
+}
+
+// np.arctan of an exit-ray slope (AKB_raytrace_20250312.py:2856-2857, :3583-3584). The slopes of a
+// focusing system are small (|x| ~ 1e-5 for the reference AKB), where the Taylor series
+// x - x^3/3 + ... + x^13/13 is exact to 2^-59 relative for |x| <= 2^-4 and x + (x z) P(z) rounds
+// to within 0.51 ulp: 8 instructions instead of OCML's range-reduced rational (~45, including an
+// IEEE division). Larger slopes take OCML's atan. Neither equals numpy's (glibc or its AVX-512
+// SIMD routine) bit for bit; the tilt stage's tolerance covers it.
+// OCML's atan out of line: its rational's constants then live only inside the call instead of
+// occupying registers across the whole trace loop
+__device__ __attribute__((noinline)) static double atan_lib(double x) { return atan(x); }
+
+__device__ __forceinline__ double atan_slope(double x) {
+    if (__builtin_expect(fabs(x) <= 0x1p-4, 1)) {
+        const double z = x * x;
+        double P = 1.0 / 13.0;
+        P = __builtin_fma(z, P, -1.0 / 11.0);
+        P = __builtin_fma(z, P, 1.0 / 9.0);
+        P = __builtin_fma(z, P, -1.0 / 7.0);
+        P = __builtin_fma(z, P, 1.0 / 5.0);
+        P = __builtin_fma(z, P, -1.0 / 3.0);
+        return __builtin_fma(x * z, P, x);
+    }
+    return atan_lib(x);
+}
+
 // mirr_ray_intersection (EllipseRaytrace3D.py:23-43). Returns false when D <= 0 or NaN.
 __device__ __forceinline__ bool quadric_hit(const Quadric& Q, double l, double m, double n, double p,
                                             double q, double r, bool negative, double& x, double& y,

@@ -8,6 +8,7 @@
 // (wave-uniform, SGPR-resident), so the per-ray stream is only positions and directions.
 #include <math.h>
 
+#include <cmath>
 #include <cstdarg>
 #include <cstdlib>
 #include <mutex>
@@ -315,11 +316,20 @@ __global__ void __launch_bounds__(kBlock) k_calc_ds(const double* __restrict__ p
 // fused chain: K mirrors (+ detector plane + OPL) per ray, all intermediate state in registers
 // ----------------------------------------------------------------------------------------------
 
+// a chain mirror: the quadric plus its doubled square coefficients (2a, 2b, 2c: exact, formed on the
+// host so the per-ray code does not recompute wave-uniform values on the vector ALU)
+struct CMirror {
+    double a, b, c, d, e, f, g, h, i, j, a2, b2, c2;
+};
+
+// mirror kinds: 0 general, 1 y-free (b = d = f = h = 0, h = +0.0), 2 z-free (c = e = f = i = 0, i = +0.0)
+constexpr int kKindGeneral = 0, kKindYFree = 1, kKindZFree = 2;
+
 struct ChainArgs {
     int K;
     int negmask;
-    int sparse[AKB_MAX_MIRRORS];  // 0 general, 1 y-free (b=d=f=h=0), 2 z-free (c=e=f=i=0)
-    Quadric q[AKB_MAX_MIRRORS];
+    int kind[AKB_MAX_MIRRORS];
+    CMirror q[AKB_MAX_MIRRORS];
     double det[4];
     const double* dir;
     int64_t dir_ld, dir_inc;
@@ -370,107 +380,186 @@ __device__ __forceinline__ void grid_rc(const ChainArgs& a, int64_t g, int64_t& 
     ih = g - iv * (int64_t)a.n_h;
 }
 
-// One ray through the chain. Writes the requested per-ray outputs and returns the sink quantities
-// (arctan of the exit slopes and the detector hit) in qv.
+// trace flags are raised per wave: the condition's lane mask lands in scalar registers and only a
+// wave that holds a flagged ray touches the flag word (no per-lane select / or in the common case)
+__device__ __forceinline__ void wave_flag(bool cond, int bit, int& fl) {
+    if (__ballot(cond)) fl |= bit;
+}
+
+struct Ray {
+    double l, m, n;  // direction
+    double p, q, r;  // origin / last hit
+};
+
+// One mirror of the chain in the reference's numpy association order: mirr_ray_intersection
+// (EllipseRaytrace3D.py:23-43), the segment length (AKB_raytrace_20250312.py:2884), norm_vector
+// (EllipseRaytrace3D.py:66-70) and reflect_ray (:51-54). A y-free (z-free) mirror skips the terms
+// whose coefficients are zero: each is an exact +-0 added to a sum that holds the other terms, the
+// gradient's y (z) component is exactly +0 (every term +-0, then + h = +0.0), its square adds +0 to
+// the norm, and the reflected y (z) component is m - 2A * (+0) = m: the results are the general
+// expression's bits (an exactly-zero partial sum could only change the sign of a zero).
+template <int kKind, bool kOPL>
+__device__ __forceinline__ void mirror_step(const CMirror& Q, bool neg, Ray& R, double& opl, bool first, int k,
+                                            int& fl, double* hits, int64_t hits_ld, int lane) {
+    const double l = R.l, m = R.m, n = R.n, p = R.p, q = R.q, r = R.r;
+    double A, B, C;
+    if (kKind == kKindYFree) {
+        A = Q.a * (l * l) + Q.c * (n * n) + Q.e * n * l;
+        B = Q.a2 * p * l + Q.c2 * r * n + Q.e * (p * n + r * l) + Q.g * l + Q.i * n;
+        C = Q.a * (p * p) + Q.c * (r * r) + Q.e * p * r + Q.g * p + Q.i * r + Q.j;
+    } else if (kKind == kKindZFree) {
+        A = Q.a * (l * l) + Q.b * (m * m) + Q.d * m * l;
+        B = Q.a2 * p * l + Q.b2 * q * m + Q.d * (p * m + q * l) + Q.g * l + Q.h * m;
+        C = Q.a * (p * p) + Q.b * (q * q) + Q.d * p * q + Q.g * p + Q.h * q + Q.j;
+    } else {
+        A = Q.a * (l * l) + Q.b * (m * m) + Q.c * (n * n) + Q.d * m * l + Q.e * n * l + Q.f * m * n;
+        B = Q.a2 * p * l + Q.b2 * q * m + Q.c2 * r * n + Q.d * (p * m + q * l) + Q.e * (p * n + r * l) +
+            Q.f * (r * m + q * n) + Q.g * l + Q.h * m + Q.i * n;
+        C = Q.a * (p * p) + Q.b * (q * q) + Q.c * (r * r) + Q.d * p * q + Q.e * p * r + Q.f * q * r + Q.g * p +
+            Q.h * q + Q.i * r + Q.j;
+    }
+    const double D = B * B - 4.0 * A * C;
+    wave_flag(!(D > 0.0), AKB_FLAG_MISS << (4 * k), fl);
+    const double sD = sqrt_cr(D);
+    const double t = (neg ? (-B - sD) : (-B + sD)) / (2.0 * A);
+    const double x = t * l + p, y = t * m + q, z = t * n + r;
+    if (kOPL) {
+        const double d = norm3(x - p, y - q, z - r);
+        opl = first ? d : opl + d;
+    }
+    if (hits) {  // hits: this segment's column 0 of mirror 0's x row (wave-uniform)
+        double* h = hits + (int64_t)k * 3 * hits_ld;
+        h[lane] = x;
+        (h + hits_ld)[lane] = y;
+        (h + 2 * hits_ld)[lane] = z;
+    }
+    // unit normal
+    double nx, ny = 0.0, nz = 0.0, sn, in;
+    if (kKind == kKindYFree) {
+        nx = Q.a2 * x + Q.e * z + Q.g;
+        nz = Q.c2 * z + Q.e * x + Q.i;
+        norm3_inv(nx, 0.0, nz, sn, in);
+    } else if (kKind == kKindZFree) {
+        nx = Q.a2 * x + Q.d * y + Q.g;
+        ny = Q.b2 * y + Q.d * x + Q.h;
+        norm3_inv(nx, ny, 0.0, sn, in);
+    } else {
+        nx = Q.a2 * x + Q.d * y + Q.e * z + Q.g;
+        ny = Q.b2 * y + Q.d * x + Q.f * z + Q.h;
+        nz = Q.c2 * z + Q.e * x + Q.f * y + Q.i;
+        norm3_inv(nx, ny, nz, sn, in);
+    }
+    wave_flag(sn == 0.0, AKB_FLAG_ZERO_NORMAL << (4 * k), fl);
+    nx = div_pos(nx, sn, in);
+    if (kKind != kKindYFree) ny = div_pos(ny, sn, in);
+    if (kKind != kKindZFree) nz = div_pos(nz, sn, in);
+    // reflection
+    double rx, ry, rz;
+    if (kKind == kKindYFree) {
+        const double A2 = 2.0 * (l * nx + n * nz);
+        rx = l - A2 * nx;
+        ry = m;
+        rz = n - A2 * nz;
+    } else if (kKind == kKindZFree) {
+        const double A2 = 2.0 * (l * nx + m * ny);
+        rx = l - A2 * nx;
+        ry = m - A2 * ny;
+        rz = n;
+    } else {
+        const double A2 = 2.0 * (l * nx + m * ny + n * nz);
+        rx = l - A2 * nx;
+        ry = m - A2 * ny;
+        rz = n - A2 * nz;
+    }
+    double sr, ir;
+    norm3_inv(rx, ry, rz, sr, ir);
+    wave_flag(sr == 0.0, AKB_FLAG_ZERO_REFLECT << (4 * k), fl);
+    R.l = div_pos(rx, sr, ir);
+    R.m = div_pos(ry, sr, ir);
+    R.n = div_pos(rz, sr, ir);
+    R.p = x;
+    R.q = y;
+    R.r = z;
+}
+
+// One ray through the chain: ray i = i0 + t of a segment starting at the wave-uniform i0, t the
+// lane's position in it, so every per-ray output row is addressed as a scalar base plus a 32-bit
+// lane offset (no per-row 64-bit vector addresses held across the loop). Writes the requested
+// per-ray outputs and returns the sink quantities (arctan of the exit slopes and the detector hit)
+// in qv.
 template <bool kGrid, bool kOPL, bool kNeedQ>
-__device__ __forceinline__ void chain_ray(const ChainArgs& a, int64_t i, int& fl, double (&qv)[5]) {
+__device__ __forceinline__ void chain_ray(const ChainArgs& a, int64_t i0, int t, int& fl, double (&qv)[5]) {
+    const int64_t i = i0 + t;
     const int64_t g = a.g0 + i;
-    double l, m, nn;
+    double* const hits = a.hits ? a.hits + i0 : nullptr;
+    Ray R;
     int64_t iv = 0, ih = 0;
     if (kGrid) {
         // phai0[:, iv*n_h + ih] = (1, tan(p0h[ih]), tan(p0v[iv])) normalised (ref :2711-2717)
         grid_rc(a, g, iv, ih);
         const double th = a.tan_h[ih];
         const double tv = a.tan_v[iv];
-        const double s = norm3(1.0, th, tv);
-        if (s == 0.0) fl |= AKB_FLAG_CHAIN_DIR;
-        l = 1.0 / s;  // = RN(1/s): also the shared reciprocal
-        m = div_shared(th, s, l);
-        nn = div_shared(tv, s, l);
+        double s, inv;
+        norm3_inv(1.0, th, tv, s, inv);
+        wave_flag(s == 0.0, AKB_FLAG_CHAIN_DIR, fl);
+        R.l = inv;  // = RN(1/s): also the shared reciprocal
+        R.m = div_pos(th, s, inv);
+        R.n = div_pos(tv, s, inv);
     } else {
-        l = a.dir[i * a.dir_inc];
-        m = a.dir[a.dir_ld + i * a.dir_inc];
-        nn = a.dir[2 * a.dir_ld + i * a.dir_inc];
+        R.l = a.dir[i * a.dir_inc];
+        R.m = a.dir[a.dir_ld + i * a.dir_inc];
+        R.n = a.dir[2 * a.dir_ld + i * a.dir_inc];
     }
-    double p, q, r;
     if (a.org) {
-        p = a.org[i * a.org_inc];
-        q = a.org[a.org_ld + i * a.org_inc];
-        r = a.org[2 * a.org_ld + i * a.org_inc];
+        R.p = a.org[i * a.org_inc];
+        R.q = a.org[a.org_ld + i * a.org_inc];
+        R.r = a.org[2 * a.org_ld + i * a.org_inc];
     } else {
-        p = a.src[0];
-        q = a.src[1];
-        r = a.src[2];
+        R.p = a.src[0];
+        R.q = a.src[1];
+        R.r = a.src[2];
     }
     double opl = 0.0;
-    // not unrolled: each iteration reads its mirror's 10 coefficients from the kernel
-    // argument segment with scalar loads (wave-uniform), keeping VGPR pressure low
+    // not unrolled: each iteration reads its mirror's coefficients from the kernel argument segment
+    // with scalar loads (wave-uniform), keeping VGPR pressure and code size low (a fully unrolled
+    // 4-mirror AKB kernel measured 12 % slower on MI355X)
 #pragma unroll 1
     for (int k = 0; k < a.K; ++k) {
-        const Quadric Q = a.q[k];
         const bool neg = (a.negmask >> k) & 1;
-        double x, y, z;
-        bool hit;
-        if (a.sparse[k] == 1)  // wave-uniform branch
-            hit = quadric_hit_sparse<1>(Q, l, m, nn, p, q, r, neg, x, y, z);
-        else if (a.sparse[k] == 2)
-            hit = quadric_hit_sparse<2>(Q, l, m, nn, p, q, r, neg, x, y, z);
+        if (a.kind[k] == kKindYFree)  // wave-uniform branch
+            mirror_step<kKindYFree, kOPL>(a.q[k], neg, R, opl, k == 0, k, fl, hits, a.hits_ld, t);
+        else if (a.kind[k] == kKindZFree)
+            mirror_step<kKindZFree, kOPL>(a.q[k], neg, R, opl, k == 0, k, fl, hits, a.hits_ld, t);
         else
-            hit = quadric_hit(Q, l, m, nn, p, q, r, neg, x, y, z);
-        if (!hit) fl |= AKB_FLAG_MISS << (4 * k);
-        if (kOPL) {
-            const double d = norm3(x - p, y - q, z - r);
-            opl = (k == 0) ? d : opl + d;
-        }
-        if (a.hits) {
-            double* h = a.hits + (int64_t)k * 3 * a.hits_ld;
-            h[i] = x;
-            h[a.hits_ld + i] = y;
-            h[2 * a.hits_ld + i] = z;
-        }
-        double nx, ny, nz;
-        quadric_grad(Q, x, y, z, nx, ny, nz);
-        const double sn = norm3(nx, ny, nz);
-        if (sn == 0.0) fl |= AKB_FLAG_ZERO_NORMAL << (4 * k);
-        const double in = 1.0 / sn;
-        nx = div_shared(nx, sn, in);
-        ny = div_shared(ny, sn, in);
-        nz = div_shared(nz, sn, in);
-        double rx, ry, rz;
-        reflect_raw(l, m, nn, nx, ny, nz, rx, ry, rz);
-        const double sr = norm3(rx, ry, rz);
-        if (sr == 0.0) fl |= AKB_FLAG_ZERO_REFLECT << (4 * k);
-        const double ir = 1.0 / sr;
-        l = div_shared(rx, sr, ir);
-        m = div_shared(ry, sr, ir);
-        nn = div_shared(rz, sr, ir);
-        p = x;
-        q = y;
-        r = z;
+            mirror_step<kKindGeneral, kOPL>(a.q[k], neg, R, opl, k == 0, k, fl, hits, a.hits_ld, t);
     }
+    const double l = R.l, m = R.m, nn = R.n, p = R.p, q = R.q, r = R.r;
     if (kOPL && kGrid && a.pert_h) {  // figure-error perturbation of the path (BASELINE config 5)
         double d = 0.0;
         for (int t = 0; t < a.pert_terms; ++t) d = __builtin_fma(a.pert_v[t * a.n_v + iv], a.pert_h[t * a.n_h + ih], d);
         opl = opl + d;
     }
-    if (kOPL && a.opl) a.opl[i] = opl;
+    if (kOPL && a.opl) (a.opl + i0)[t] = opl;
     if (a.last_hit) {
-        a.last_hit[i] = p;
-        a.last_hit[a.last_hit_ld + i] = q;
-        a.last_hit[2 * a.last_hit_ld + i] = r;
+        double* o = a.last_hit + i0;
+        o[t] = p;
+        (o + a.last_hit_ld)[t] = q;
+        (o + 2 * a.last_hit_ld)[t] = r;
     }
     if (a.dir_out) {
-        a.dir_out[i] = l;
-        a.dir_out[a.dir_out_ld + i] = m;
-        a.dir_out[2 * a.dir_out_ld + i] = nn;
+        double* o = a.dir_out + i0;
+        o[t] = l;
+        (o + a.dir_out_ld)[t] = m;
+        (o + 2 * a.dir_out_ld)[t] = nn;
     }
     if (kNeedQ || a.det_out) {
         double x, y, z;
         plane_hit(a.det[0], a.det[1], a.det[2], a.det[3], l, m, nn, p, q, r, x, y, z);
         if (a.det_out) {
-            a.det_out[i] = x;
-            a.det_out[a.det_out_ld + i] = y;
-            a.det_out[2 * a.det_out_ld + i] = z;
+            double* o = a.det_out + i0;
+            o[t] = x;
+            (o + a.det_out_ld)[t] = y;
+            (o + 2 * a.det_out_ld)[t] = z;
         }
         qv[2] = x;
         qv[3] = y;
@@ -478,10 +567,10 @@ __device__ __forceinline__ void chain_ray(const ChainArgs& a, int64_t i, int& fl
     }
     if (kNeedQ || a.atan_h || a.atan_v) {
         const double il = 1.0 / l;
-        qv[0] = atan(div_shared(m, l, il));
-        qv[1] = atan(div_shared(nn, l, il));
-        if (a.atan_h) a.atan_h[i] = qv[0];
-        if (a.atan_v) a.atan_v[i] = qv[1];
+        qv[0] = atan_slope(div_shared(m, l, il));
+        qv[1] = atan_slope(div_shared(nn, l, il));
+        if (a.atan_h) (a.atan_h + i0)[t] = qv[0];
+        if (a.atan_v) (a.atan_v + i0)[t] = qv[1];
     }
     // equal-angle resample samples: the slope ratios only; the host applies np.arctan so the
     // resampled angle tables match the reference bit for bit (glibc atan, ref :2858-2859)
@@ -493,9 +582,9 @@ template <bool kGrid, bool kOPL, int kWaves>
 __global__ void __launch_bounds__(kBlock, kWaves) k_chain(ChainArgs a) {
     int fl = 0;
     double qv[5];
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < a.n;
-         i += (int64_t)gridDim.x * blockDim.x)
-        chain_ray<kGrid, kOPL, false>(a, i, fl, qv);
+    const int t = threadIdx.x;
+    for (int64_t i0 = blockIdx.x * (int64_t)kBlock; i0 < a.n; i0 += (int64_t)gridDim.x * kBlock)
+        if (i0 + t < a.n) chain_ray<kGrid, kOPL, false>(a, i0, t, fl, qv);
     if (fl) atomicOr(a.flags, fl);
 }
 
@@ -510,7 +599,7 @@ __global__ void __launch_bounds__(kBlock, kWaves) k_chain_sink(ChainArgs a) {
         const int64_t i = seg * kLeafSeg + threadIdx.x;
         const bool valid = i < a.n;
         double qv[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-        if (valid) chain_ray<kGrid, kOPL, true>(a, i, fl, qv);
+        if (valid) chain_ray<kGrid, kOPL, true>(a, seg * kLeafSeg, threadIdx.x, fl, qv);
         leaf_sink_segment<5>(a.sink, L, seg * kLeafSeg, qv, valid);
     }
     if (fl) atomicOr(a.flags, fl);
@@ -787,7 +876,7 @@ static int chain_waves() {
     static int w = [] {
         const char* e = getenv("AKB_CHAIN_WAVES");
         const int v = e ? atoi(e) : 4;
-        return (v == 2 || v == 4 || v == 5 || v == 6 || v == 8) ? v : 4;
+        return (v == 2 || v == 4 || v == 8) ? v : 4;
     }();
     return w;
 }
@@ -824,8 +913,6 @@ static void launch_chain(int w, unsigned g, hipStream_t s, const ChainArgs& a) {
         break;
     switch (w) {
         AKB_CHAIN_CASE(2)
-        AKB_CHAIN_CASE(5)
-        AKB_CHAIN_CASE(6)
         AKB_CHAIN_CASE(8)
         default:
             AKB_CHAIN_CASE(4)
@@ -986,15 +1073,17 @@ int akb_trace_chain_f64(const akb_chain_desc* d, void* stream) {
     a.K = d->n_mirrors;
     a.negmask = 0;
     for (int k = 0; k < d->n_mirrors; ++k) {
-        a.q[k] = quadric_from(d->coeffs[k]);
-        if (d->negative[k]) a.negmask |= 1 << k;
         const double* c = d->coeffs[k];
-        if (c[1] == 0.0 && c[3] == 0.0 && c[5] == 0.0 && c[7] == 0.0)
-            a.sparse[k] = 1;
-        else if (c[2] == 0.0 && c[4] == 0.0 && c[5] == 0.0 && c[8] == 0.0)
-            a.sparse[k] = 2;
+        a.q[k] = CMirror{c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7], c[8], c[9],
+                         2.0 * c[0], 2.0 * c[1], 2.0 * c[2]};
+        if (d->negative[k]) a.negmask |= 1 << k;
+        // the sparse kinds need the constant term of the vanishing gradient component to be +0.0
+        if (c[1] == 0.0 && c[3] == 0.0 && c[5] == 0.0 && c[7] == 0.0 && !std::signbit(c[7]))
+            a.kind[k] = kKindYFree;
+        else if (c[2] == 0.0 && c[4] == 0.0 && c[5] == 0.0 && c[8] == 0.0 && !std::signbit(c[8]))
+            a.kind[k] = kKindZFree;
         else
-            a.sparse[k] = 0;
+            a.kind[k] = kKindGeneral;
     }
     for (int k = 0; k < 4; ++k) a.det[k] = d->det_ghij[k];
     a.dir = d->dir;
@@ -1225,21 +1314,36 @@ int akb_pupil_sample_f64(const double* wave, int64_t row0, int64_t rows, int64_t
 
 // ---- diagnostics: the trace's arithmetic shortcuts against the plain operations ----
 namespace akb {
+constexpr int kSelftestCols = AKB_SELFTEST_COLS;
+
+// out row i: sqrt_cr(a), sqrt(a), div_shared(a, b), a / b, div_pos(a, b), norm3_inv's s and inv of
+// (a, b, b), norm3 with 1.0 / norm3 of the same vector, atan_slope(a) and OCML's atan(a)
 __global__ void k_selftest(const double* a, const double* b, int64_t n, double* out) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const double x = a[i], s = b[i];
-        out[4 * i + 0] = sqrt_cr(x);
-        out[4 * i + 1] = sqrt(x);
-        out[4 * i + 2] = div_shared(x, s, 1.0 / s);
-        out[4 * i + 3] = x / s;
+        double* o = out + (int64_t)kSelftestCols * i;
+        o[0] = sqrt_cr(x);
+        o[1] = sqrt(x);
+        o[2] = div_shared(x, s, 1.0 / s);
+        o[3] = x / s;
+        o[4] = div_pos(x, s, 1.0 / s);
+        double nv, ninv;
+        norm3_inv(x, s, s, nv, ninv);
+        o[5] = nv;
+        o[6] = ninv;
+        const double v = x * x + s * s + s * s;
+        o[7] = sqrt(v);
+        o[8] = 1.0 / sqrt(v);
+        o[9] = atan_slope(x);
+        o[10] = atan(x);
     }
 }
 }  // namespace akb
 
-extern "C" int akb_selftest_arith_f64(const double* a, const double* b, int64_t n, double* out4, void* stream) {
+extern "C" int akb_selftest_arith_f64(const double* a, const double* b, int64_t n, double* out, void* stream) {
     akb::clear_error();
-    AKB_REQUIRE(a && b && out4 && n >= 0, "bad selftest arguments");
+    AKB_REQUIRE(a && b && out && n >= 0, "bad selftest arguments");
     if (n == 0) return AKB_OK;
-    akb::k_selftest<<<akb::grid_for(n), akb::kBlock, 0, (hipStream_t)stream>>>(a, b, n, out4);
+    akb::k_selftest<<<akb::grid_for(n), akb::kBlock, 0, (hipStream_t)stream>>>(a, b, n, out);
     return akb::launch_status("k_selftest");
 }

@@ -28,7 +28,7 @@ def child(n, reps):
             b.record()
             b.synchronize()
             acc.append(a.elapsed_time(b))
-    print(json.dumps({"w": os.environ.get("AKB_CHAIN_WAVES", "4"), "grid": os.environ.get("AKB_CHAIN_GRID", "2048"),
+    print(json.dumps({"w": os.environ.get("AKB_CHAIN_WAVES", "4"), "grid": os.environ.get("AKB_CHAIN_GRID", "8192"),
                       "pass1_ms": float(np.median(t1)),
                       "pass2_ms": float(np.median(t2)), "pass1_min": min(t1), "pass2_min": min(t2)}))
 
@@ -40,7 +40,7 @@ if __name__ == "__main__":
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 3163
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
     what = sys.argv[3] if len(sys.argv) > 3 else "waves"
-    variants = ([{"AKB_CHAIN_WAVES": str(w)} for w in (4, 2, 5, 6, 8)] if what == "waves" else
+    variants = ([{"AKB_CHAIN_WAVES": str(w)} for w in (4, 2, 8)] if what == "waves" else
                 [{"AKB_CHAIN_GRID": str(g)} for g in (2048, 1024, 4096, 8192, 16384, 40000)])
     for rnd in range(2):
         for v in variants:

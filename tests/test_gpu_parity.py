@@ -127,27 +127,60 @@ def test_rotations_match_reference_blas_order(gpu):
 
 
 def test_arith_shortcuts_bitwise(gpu):
-    """The chain kernels' rescale-free sqrt and shared-reciprocal division equal sqrt() and a / b
-    bit for bit over a wide range (and fall back to them outside it)."""
+    """The chain kernels' rescale-free sqrt, shared-reciprocal divisions and fused norm/reciprocal
+    equal sqrt(), a / b and 1 / sqrt() bit for bit (sign of zero included) over a wide range, and
+    fall back to them outside it."""
     from akbraytracing_amd import _lib, device as D
     rng = np.random.default_rng(11)
     n = 4_000_000
     e = rng.integers(-760, 900, n).astype(np.float64)
     a = rng.random(n) * 2.0 ** e
+    a[::3] *= -1.0
     b = (rng.random(n) + 0.5) * 2.0 ** rng.integers(-40, 40, n)
+    # norms at the edges of the fast path's range, all-ones and one-bit mantissas near 1
+    m = 200_000
+    edge_e = rng.choice(np.array([-768, -767, -766, -700, -2, -1, 0, 1, 998, 999, 1000]), m).astype(np.float64)
+    edge = (1.0 + rng.random(m)) * 2.0 ** edge_e
+    ones = np.array([np.nextafter(2.0 ** k, 0.0) for k in range(-300, 300)])
+    a = np.concatenate([a, np.sqrt(edge / 3.0), ones, 1.0 + ones])
+    b = np.concatenate([b, np.sqrt(edge / 3.0), ones, 1.0 + ones])
     special = np.array([0.0, -0.0, 1.0, 4.0, np.inf, -1.0, np.nan, 1e-300, 5e-324, 2.0 ** -767, 1e305])
     a = np.concatenate([a, special])
     b = np.concatenate([b, np.full(special.shape, 3.0)])
     ta, tb = torch.from_numpy(a).to(gpu), torch.from_numpy(b).to(gpu)
-    out = torch.empty((a.shape[0], 4), dtype=torch.float64, device=gpu)
+    cols = 11
+    out = torch.empty((a.shape[0], cols), dtype=torch.float64, device=gpu)
     _lib.check(_lib.lib().akb_selftest_arith_f64(D.ptr(ta), D.ptr(tb), a.shape[0], D.ptr(out), D.stream_handle()))
     o = out.cpu().numpy()
-    assert np.array_equal(o[:, 0].view(np.uint64), o[:, 1].view(np.uint64)) or \
-        np.array_equal(o[:, 0], o[:, 1], equal_nan=True)
+    bits = lambda v: v.view(np.uint64)
+    nan0 = np.isnan(o[:, 1])
+    assert np.array_equal(bits(o[~nan0, 0]), bits(o[~nan0, 1])) and np.isnan(o[nan0, 0]).all()
     assert np.array_equal(o[:, 0], np.sqrt(a), equal_nan=True)
     fin = np.isfinite(a)
-    assert np.array_equal(o[fin, 2], o[fin, 3])
-    assert np.array_equal(o[fin, 3], (a / b)[fin])
+    assert np.array_equal(bits(o[fin, 2]), bits(o[fin, 3]))
+    assert np.array_equal(bits(o[fin, 3]), bits((a / b)[fin]))
+    assert np.array_equal(bits(o[fin, 4]), bits(o[fin, 3]))          # positive divisors only
+    v = a * a + b * b + b * b
+    ok = np.isfinite(v) & (v > 0)
+    assert np.array_equal(bits(o[ok, 5]), bits(o[ok, 7]))
+    assert np.array_equal(bits(o[ok, 6]), bits(o[ok, 8]))
+    assert np.array_equal(bits(o[ok, 8]), bits(1.0 / np.sqrt(v[ok])))
+    # slope arctan: the library atan above 2^-4; below, within 1 ulp of the correctly rounded value
+    # (200-bit mpmath) and equal to it on nearly every argument
+    big = fin & (np.abs(a) > 2.0 ** -4)
+    assert np.array_equal(bits(o[big, 9]), bits(o[big, 10]))
+    import mpmath
+    mpmath.mp.prec = 200
+    xs = np.concatenate([(rng.random(4000) - 0.5) * 2.0 ** -3, (rng.random(4000) - 0.5) * 2e-4,
+                         (rng.random(2000) - 0.5) * 2.0 ** rng.integers(-60, -5, 2000), [0.0, -0.0, 2.0 ** -4]])
+    tx = torch.from_numpy(xs).to(gpu)
+    ox = torch.empty((xs.shape[0], cols), dtype=torch.float64, device=gpu)
+    _lib.check(_lib.lib().akb_selftest_arith_f64(D.ptr(tx), D.ptr(tx), xs.shape[0], D.ptr(ox), D.stream_handle()))
+    got = ox.cpu().numpy()[:, 9]
+    cr = np.array([float(mpmath.atan(mpmath.mpf(float(x)))) for x in xs])
+    ulp = np.spacing(np.abs(cr))
+    assert np.all(np.abs(got - cr) <= ulp) and np.array_equal(np.signbit(got), np.signbit(cr))
+    assert np.mean(got == cr) > 0.99
 
 
 # ----------------------------------------------------------------------------- fused chain
