@@ -306,16 +306,24 @@ __device__ __forceinline__ void leaf_sink_segment(const akb_leaf_sink& S, LeafLd
         const int j = tid & 7;
         const bool nan0 = (S.nan_mask >> q) & 1;
         const double* p = &L.v[q][leaf * 128 + j];
-        double x = p[0];
-        bool bad = nan0 && (x != x);
-        double r = bad ? 0.0 : x;
-        int c = bad ? 0 : 1;
+        // plain sum first: with no NaN among the 16 values it is np.nansum's sum, bit for bit;
+        // a NaN result (a NaN input, or inf - inf) re-sums with NaN skipped when the quantity is
+        // a nanmean one (for inf - inf that gives the same NaN)
+        double r = p[0];
 #pragma unroll
-        for (int row = 1; row < 16; ++row) {
-            x = p[row * 8];
-            bad = nan0 && (x != x);
-            r = r + (bad ? 0.0 : x);
-            c += bad ? 0 : 1;
+        for (int row = 1; row < 16; ++row) r = r + p[row * 8];
+        int c = 16;
+        if (nan0 && r != r) {
+            double x = p[0];
+            bool bad = x != x;
+            r = bad ? 0.0 : x;
+            c = bad ? 0 : 1;
+            for (int row = 1; row < 16; ++row) {
+                x = p[row * 8];
+                bad = x != x;
+                r = r + (bad ? 0.0 : x);
+                c += bad ? 0 : 1;
+            }
         }
         // numpy's leaf: ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7))
         r = r + __shfl_xor(r, 1);

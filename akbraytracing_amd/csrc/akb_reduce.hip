@@ -226,16 +226,20 @@ __global__ void __launch_bounds__(64) k_leaf_chunks(const double* __restrict__ l
 }
 
 // One workgroup per row q: the row's nparts full-buffer sums (part[q * part_ld + c]) added left to
-// right by wave 0 (a single dependent chain fed lane by lane from an LDS tile), the short last
-// buffer tail[q * tail_ld + 0 .. tail_len) staged to LDS and summed pairwise by wave 1 meanwhile,
-// then added last.
+// right by wave 0 (a single dependent chain fed lane by lane from an LDS tile of `tile` doubles),
+// the short last buffer tail[q * tail_ld + 0 .. tail_len) staged to LDS and summed pairwise by wave
+// 1 meanwhile, then added last. The LDS is sized to the row (dynamic: tile + tail_len doubles, 29
+// KB for a 1e7-element row instead of a fixed 96 KB), so the kernel finds room on a CU beside a
+// running trace kernel's workgroups instead of waiting for them to drain.
 __global__ void __launch_bounds__(kPwThreads) k_pw_final(const double* __restrict__ part,
                                                          const long long* __restrict__ part_cnt, int part_ld,
                                                          int nparts, const double* __restrict__ tail,
                                                          int64_t tail_ld, int tail_len, int nan_mask,
-                                                         double* __restrict__ out, int64_t* __restrict__ cnt_out) {
-    __shared__ double t[kFinalTile];
-    __shared__ double tl[kPwBuf];
+                                                         double* __restrict__ out, int64_t* __restrict__ cnt_out,
+                                                         int tile) {
+    extern __shared__ double dyn[];
+    double* const t = dyn;
+    double* const tl = dyn + tile;
     __shared__ PwTree T;
     __shared__ long long wc[kPwThreads / 64];
     __shared__ double tail_sum;
@@ -277,8 +281,8 @@ __global__ void __launch_bounds__(kPwThreads) k_pw_final(const double* __restric
         }
     }
     double acc = 0.0;
-    for (int base = 0; base == 0 || base < nparts; base += kFinalTile) {
-        const int m = nparts - base < kFinalTile ? nparts - base : kFinalTile;
+    for (int base = 0; base == 0 || base < nparts; base += tile) {
+        const int m = nparts - base < tile ? nparts - base : tile;
         if (base > 0) __syncthreads();
         {
             constexpr int kBatch = kFinalTile / kPwThreads;  // the whole tile in one batch
@@ -340,6 +344,10 @@ __global__ void __launch_bounds__(kPwThreads) k_pw_final(const double* __restric
     }
 }
 
+// k_pw_final's part tile (at most kFinalTile doubles) and dynamic LDS bytes
+static inline int final_tile(int nparts) { return nparts < 1 ? 1 : (nparts < kFinalTile ? nparts : kFinalTile); }
+static inline size_t final_lds(int tile, int tail_len) { return (size_t)(tile + (tail_len > 0 ? tail_len : 1)) * 8; }
+
 }  // namespace akb
 
 using namespace akb;
@@ -375,8 +383,9 @@ int akb_pairwise_sum_f64(const double* x, int64_t ld, int rows, int64_t n, int n
         int st = launch_status("k_pw_chunks");
         if (st) return st;
     }
-    k_pw_final<<<rows, kPwThreads, 0, s>>>(part, part_cnt, nb, (int)nfull, x + nfull * kPwBuf, ld, tail, mask,
-                                           d_sum, d_count);
+    const int tile = final_tile((int)nfull);
+    k_pw_final<<<rows, kPwThreads, final_lds(tile, tail), s>>>(part, part_cnt, nb, (int)nfull, x + nfull * kPwBuf,
+                                                              ld, tail, mask, d_sum, d_count, tile);
     return launch_status("k_pw_final");
 }
 
@@ -430,8 +439,9 @@ int akb_leaf_finish_f64(const akb_leaf_sink* sink, double* d_sum, int64_t* d_cou
         int st = launch_status("k_leaf_chunks");
         if (st) return st;
     }
-    k_pw_final<<<nq, kPwThreads, 0, s>>>(part, part_cnt, nb, (int)nfull, sink->tail, kPwBuf, tail,
-                                         sink->nan_mask, d_sum, d_count);
+    const int tile = final_tile((int)nfull);
+    k_pw_final<<<nq, kPwThreads, final_lds(tile, tail), s>>>(part, part_cnt, nb, (int)nfull, sink->tail, kPwBuf,
+                                                            tail, sink->nan_mask, d_sum, d_count, tile);
     return launch_status("k_pw_final");
 }
 

@@ -312,6 +312,53 @@ __global__ void __launch_bounds__(kBlock) k_calc_ds(const double* __restrict__ p
     }
 }
 
+// tilt correction inputs (defined ahead of the chain: the fused pass-1 + tilt kernel loads them
+// while it traces)
+struct TiltArgs {
+    Mat3 Ry, Rz;
+    double c[3];
+    const double* params;  // non-NULL: Ry, Rz, c from akb_tilt_params_f64's device block
+    double d1[4], d2[4];
+    const double* dir;
+    const double* pt;
+    const double* opl;
+    int64_t ld, n;
+    double* dir_rot;
+    double* pt_rot;
+    double* det1;
+    double* det2;
+    double* total1;
+    double* total2;
+    akb_leaf_sink sink;
+};
+
+// one ray's inputs (direction, last hit, OPL), loaded ahead of the arithmetic
+struct TiltIn {
+    double d[3], p[3], o;
+};
+
+// the same with the OPL row known to be present (no load under a branch: the fused kernel's wait
+// counts then stay exact across both paths)
+__device__ __forceinline__ void tilt_load_all(const TiltArgs& a, int64_t i, TiltIn& t) {
+    t.d[0] = a.dir[i];
+    t.d[1] = a.dir[a.ld + i];
+    t.d[2] = a.dir[2 * a.ld + i];
+    t.p[0] = a.pt[i];
+    t.p[1] = a.pt[a.ld + i];
+    t.p[2] = a.pt[2 * a.ld + i];
+    t.o = a.opl[i];
+}
+
+__device__ __forceinline__ void tilt_load(const TiltArgs& a, int64_t i, TiltIn& t) {
+    t.d[0] = a.dir[i];
+    t.d[1] = a.dir[a.ld + i];
+    t.d[2] = a.dir[2 * a.ld + i];
+    t.p[0] = a.pt[i];
+    t.p[1] = a.pt[a.ld + i];
+    t.p[2] = a.pt[2 * a.ld + i];
+    t.o = a.opl ? a.opl[i] : 0.0;
+}
+
 // ----------------------------------------------------------------------------------------------
 // fused chain: K mirrors (+ detector plane + OPL) per ray, all intermediate state in registers
 // ----------------------------------------------------------------------------------------------
@@ -339,7 +386,8 @@ struct ChainArgs {
     uint32_t n_v;
     uint32_t div_mul;  // Granlund-Montgomery magic for g / n_h with 32-bit g (see div_magic)
     uint32_t div_shift;
-    int64_t g0;  // global flat index of ray 0 of this launch
+    int64_t g0;        // global flat index of ray 0 of this launch
+    int64_t g_stride;  // flat-index step between consecutive rays (1; n_h walks a grid column)
     int64_t n;
     const double* org;
     int64_t org_ld, org_inc;
@@ -398,7 +446,7 @@ struct Ray {
 // gradient's y (z) component is exactly +0 (every term +-0, then + h = +0.0), its square adds +0 to
 // the norm, and the reflected y (z) component is m - 2A * (+0) = m: the results are the general
 // expression's bits (an exactly-zero partial sum could only change the sign of a zero).
-template <int kKind, bool kOPL>
+template <int kKind, bool kOPL, bool kHits>
 __device__ __forceinline__ void mirror_step(const CMirror& Q, bool neg, Ray& R, double& opl, bool first, int k,
                                             int& fl, double* hits, int64_t hits_ld, int lane) {
     const double l = R.l, m = R.m, n = R.n, p = R.p, q = R.q, r = R.r;
@@ -427,7 +475,11 @@ __device__ __forceinline__ void mirror_step(const CMirror& Q, bool neg, Ray& R, 
         const double d = norm3(x - p, y - q, z - r);
         opl = first ? d : opl + d;
     }
-    if (hits) {  // hits: this segment's column 0 of mirror 0's x row (wave-uniform)
+    // hits: this segment's column 0 of mirror 0's x row (wave-uniform). A compile-time switch: a
+    // vector store anywhere in the mirror loop makes the compiler drain every outstanding load
+    // before the loop (no separate store counter on gfx9), which would stall the fused kernel's
+    // in-flight tilt loads
+    if (kHits) {
         double* h = hits + (int64_t)k * 3 * hits_ld;
         h[lane] = x;
         (h + hits_ld)[lane] = y;
@@ -487,18 +539,43 @@ __device__ __forceinline__ void mirror_step(const CMirror& Q, bool neg, Ray& R, 
 // lane offset (no per-row 64-bit vector addresses held across the loop). Writes the requested
 // per-ray outputs and returns the sink quantities (arctan of the exit slopes and the detector hit)
 // in qv.
-template <bool kGrid, bool kOPL, bool kNeedQ>
-__device__ __forceinline__ void chain_ray(const ChainArgs& a, int64_t i0, int t, int& fl, double (&qv)[5]) {
+struct NoHook {
+    __device__ __forceinline__ void operator()() const {}
+};
+
+// grid position and direction-table entries of flat ray i of a launch
+__device__ __forceinline__ void ray_tables(const ChainArgs& a, int64_t i, int64_t& iv, int64_t& ih, double& th,
+                                           double& tv) {
+    grid_rc(a, a.g0 + i * a.g_stride, iv, ih);
+    th = a.tan_h[ih];
+    tv = a.tan_v[iv];
+}
+
+// One ray through the chain: ray i = i0 + t of a segment starting at the wave-uniform i0, t the
+// lane's position in it, so every per-ray output row is addressed as a scalar base plus a 32-bit
+// lane offset (no per-row 64-bit vector addresses held across the loop). Grid rays come with
+// their table entries th / tv (iv, ih: grid row and column). Writes the requested per-ray outputs
+// and returns the sink quantities (arctan of the exit slopes and the detector hit) in qv.
+//
+// post(): called after the mirror arithmetic and before any output store. The pipelined kernels
+// issue the next segment's loads there: gfx9 counts loads and stores on one in-order counter
+// (vmcnt), so loads issued after this segment's stores would make the next segment's first use
+// wait for those stores to reach memory; issued before them, they fly during the stores, the leaf
+// sums and (for the fused kernels) the next segment's mirror loop.
+// kLean: pass 1 of the fused kernel - only the resample picks and the flags leave the ray (no
+// optional output rows, no out-of-line atan call).
+// kPointSrc: rays start at the constant source (no origin loads, which would have to be waited
+// for - with everything issued before them - ahead of the mirror loop).
+template <bool kGrid, bool kOPL, bool kNeedQ, bool kHits = false, bool kLean = false, bool kPointSrc = kLean,
+          class Post = NoHook>
+__device__ __forceinline__ void chain_ray_tab(const ChainArgs& a, int64_t i0, int t, int64_t iv, int64_t ih,
+                                              double th, double tv, int& fl, double (&qv)[5], Post post = Post()) {
     const int64_t i = i0 + t;
-    const int64_t g = a.g0 + i;
-    double* const hits = a.hits ? a.hits + i0 : nullptr;
+    const int64_t g = a.g0 + i * a.g_stride;
+    double* const hits = kHits ? a.hits + i0 : nullptr;
     Ray R;
-    int64_t iv = 0, ih = 0;
     if (kGrid) {
         // phai0[:, iv*n_h + ih] = (1, tan(p0h[ih]), tan(p0v[iv])) normalised (ref :2711-2717)
-        grid_rc(a, g, iv, ih);
-        const double th = a.tan_h[ih];
-        const double tv = a.tan_v[iv];
         double s, inv;
         norm3_inv(1.0, th, tv, s, inv);
         wave_flag(s == 0.0, AKB_FLAG_CHAIN_DIR, fl);
@@ -510,7 +587,7 @@ __device__ __forceinline__ void chain_ray(const ChainArgs& a, int64_t i0, int t,
         R.m = a.dir[a.dir_ld + i * a.dir_inc];
         R.n = a.dir[2 * a.dir_ld + i * a.dir_inc];
     }
-    if (a.org) {
+    if (!kPointSrc && a.org) {
         R.p = a.org[i * a.org_inc];
         R.q = a.org[a.org_ld + i * a.org_inc];
         R.r = a.org[2 * a.org_ld + i * a.org_inc];
@@ -527,35 +604,36 @@ __device__ __forceinline__ void chain_ray(const ChainArgs& a, int64_t i0, int t,
     for (int k = 0; k < a.K; ++k) {
         const bool neg = (a.negmask >> k) & 1;
         if (a.kind[k] == kKindYFree)  // wave-uniform branch
-            mirror_step<kKindYFree, kOPL>(a.q[k], neg, R, opl, k == 0, k, fl, hits, a.hits_ld, t);
+            mirror_step<kKindYFree, kOPL, kHits>(a.q[k], neg, R, opl, k == 0, k, fl, hits, a.hits_ld, t);
         else if (a.kind[k] == kKindZFree)
-            mirror_step<kKindZFree, kOPL>(a.q[k], neg, R, opl, k == 0, k, fl, hits, a.hits_ld, t);
+            mirror_step<kKindZFree, kOPL, kHits>(a.q[k], neg, R, opl, k == 0, k, fl, hits, a.hits_ld, t);
         else
-            mirror_step<kKindGeneral, kOPL>(a.q[k], neg, R, opl, k == 0, k, fl, hits, a.hits_ld, t);
+            mirror_step<kKindGeneral, kOPL, kHits>(a.q[k], neg, R, opl, k == 0, k, fl, hits, a.hits_ld, t);
     }
     const double l = R.l, m = R.m, nn = R.n, p = R.p, q = R.q, r = R.r;
     if (kOPL && kGrid && a.pert_h) {  // figure-error perturbation of the path (BASELINE config 5)
         double d = 0.0;
-        for (int t = 0; t < a.pert_terms; ++t) d = __builtin_fma(a.pert_v[t * a.n_v + iv], a.pert_h[t * a.n_h + ih], d);
+        for (int k = 0; k < a.pert_terms; ++k) d = __builtin_fma(a.pert_v[k * a.n_v + iv], a.pert_h[k * a.n_h + ih], d);
         opl = opl + d;
     }
+    post();
     if (kOPL && a.opl) (a.opl + i0)[t] = opl;
-    if (a.last_hit) {
+    if (!kLean && a.last_hit) {
         double* o = a.last_hit + i0;
         o[t] = p;
         (o + a.last_hit_ld)[t] = q;
         (o + 2 * a.last_hit_ld)[t] = r;
     }
-    if (a.dir_out) {
+    if (!kLean && a.dir_out) {
         double* o = a.dir_out + i0;
         o[t] = l;
         (o + a.dir_out_ld)[t] = m;
         (o + 2 * a.dir_out_ld)[t] = nn;
     }
-    if (kNeedQ || a.det_out) {
+    if (kNeedQ || (!kLean && a.det_out)) {
         double x, y, z;
         plane_hit(a.det[0], a.det[1], a.det[2], a.det[3], l, m, nn, p, q, r, x, y, z);
-        if (a.det_out) {
+        if (!kLean && a.det_out) {
             double* o = a.det_out + i0;
             o[t] = x;
             (o + a.det_out_ld)[t] = y;
@@ -565,7 +643,7 @@ __device__ __forceinline__ void chain_ray(const ChainArgs& a, int64_t i0, int t,
         qv[3] = y;
         qv[4] = z;
     }
-    if (kNeedQ || a.atan_h || a.atan_v) {
+    if (kNeedQ || (!kLean && (a.atan_h || a.atan_v))) {
         const double il = 1.0 / l;
         qv[0] = atan_slope(div_shared(m, l, il));
         qv[1] = atan_slope(div_shared(nn, l, il));
@@ -578,28 +656,38 @@ __device__ __forceinline__ void chain_ray(const ChainArgs& a, int64_t i0, int t,
     if (a.samp_v && kGrid && ih == a.sv_col) a.samp_v[iv] = nn / l;
 }
 
-template <bool kGrid, bool kOPL, int kWaves>
+// the same, loading its own table entries (the unpipelined kernels)
+template <bool kGrid, bool kOPL, bool kNeedQ, bool kHits = false, bool kLean = false, bool kPointSrc = kLean>
+__device__ __forceinline__ void chain_ray(const ChainArgs& a, int64_t i0, int t, int& fl, double (&qv)[5]) {
+    int64_t iv = 0, ih = 0;
+    double th = 0.0, tv = 0.0;
+    if (kGrid) ray_tables(a, i0 + t, iv, ih, th, tv);
+    chain_ray_tab<kGrid, kOPL, kNeedQ, kHits, kLean, kPointSrc>(a, i0, t, iv, ih, th, tv, fl, qv);
+}
+
+template <bool kGrid, bool kOPL, int kWaves, bool kHits = false, bool kPointSrc = false>
 __global__ void __launch_bounds__(kBlock, kWaves) k_chain(ChainArgs a) {
     int fl = 0;
     double qv[5];
     const int t = threadIdx.x;
     for (int64_t i0 = blockIdx.x * (int64_t)kBlock; i0 < a.n; i0 += (int64_t)gridDim.x * kBlock)
-        if (i0 + t < a.n) chain_ray<kGrid, kOPL, false>(a, i0, t, fl, qv);
+        if (i0 + t < a.n) chain_ray<kGrid, kOPL, false, kHits, false, kPointSrc>(a, i0, t, fl, qv);
     if (fl) atomicOr(a.flags, fl);
 }
 
 // the same, walking 256-ray segments and feeding the fused np.nanmean(arctan) / np.mean(det)
 // leaf sums (the tilt means, ref :3583-3591) instead of writing those five rows to HBM
-template <bool kGrid, bool kOPL, int kWaves>
+// kPointSrc: grid rays from the point source (no origin loads)
+template <bool kGrid, bool kOPL, int kWaves, bool kPointSrc = false>
 __global__ void __launch_bounds__(kBlock, kWaves) k_chain_sink(ChainArgs a) {
     __shared__ LeafLds<5> L;
     int fl = 0;
+    const int t = threadIdx.x;
     const int64_t nseg = (a.n + kLeafSeg - 1) / kLeafSeg;
     for (int64_t seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
-        const int64_t i = seg * kLeafSeg + threadIdx.x;
-        const bool valid = i < a.n;
+        const bool valid = seg * kLeafSeg + t < a.n;
         double qv[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-        if (valid) chain_ray<kGrid, kOPL, true>(a, seg * kLeafSeg, threadIdx.x, fl, qv);
+        if (valid) chain_ray<kGrid, kOPL, true, false, false, kPointSrc>(a, seg * kLeafSeg, t, fl, qv);
         leaf_sink_segment<5>(a.sink, L, seg * kLeafSeg, qv, valid);
     }
     if (fl) atomicOr(a.flags, fl);
@@ -615,7 +703,7 @@ __global__ void __launch_bounds__(kBlock, kWaves) k_chain_sink(ChainArgs a) {
 //   Ry, Rz = rotation_matrices(-theta_y, -theta_z) with correctly rounded cos / sin
 // It also zeroes the words the next step accumulates into (pupil extent keys, trace flags that
 // were already copied out in stream order).
-constexpr int kTiltTheta = 0, kTiltRy = 2, kTiltRz = 11, kTiltFocus = 20;
+constexpr int kTiltTheta = 0, kTiltRy = 2, kTiltRz = 11, kTiltFocus = 20, kTiltSaved = 23;
 
 __global__ void k_tilt_params(const double* __restrict__ s5, const int64_t* __restrict__ c5, double* __restrict__ P,
                               unsigned long long* keys, int32_t* clear, int nclear) {
@@ -640,40 +728,11 @@ __global__ void k_tilt_params(const double* __restrict__ s5, const int64_t* __re
     }
     if (lane >= 4 && lane < 7) P[kTiltFocus + lane - 4] = s5[2 + lane - 4] / (double)c5[2 + lane - 4];
     if (keys && lane < 4) keys[lane] = 0ULL;
+    // the first (up to 4) words are kept in the block before they are cleared, so the host can
+    // read them from there whenever it likes (RayWave's trace flag words)
+    if (lane < 4) ((int32_t*)(P + kTiltSaved))[lane] = lane < nclear ? clear[lane] : 0;
+    __syncthreads();
     for (int i = lane; i < nclear; i += blockDim.x) clear[i] = 0;
-}
-
-struct TiltArgs {
-    Mat3 Ry, Rz;
-    double c[3];
-    const double* params;  // non-NULL: Ry, Rz, c from akb_tilt_params_f64's device block
-    double d1[4], d2[4];
-    const double* dir;
-    const double* pt;
-    const double* opl;
-    int64_t ld, n;
-    double* dir_rot;
-    double* pt_rot;
-    double* det1;
-    double* det2;
-    double* total1;
-    double* total2;
-    akb_leaf_sink sink;
-};
-
-// one ray's inputs (direction, last hit, OPL), loaded ahead of the arithmetic
-struct TiltIn {
-    double d[3], p[3], o;
-};
-
-__device__ __forceinline__ void tilt_load(const TiltArgs& a, int64_t i, TiltIn& t) {
-    t.d[0] = a.dir[i];
-    t.d[1] = a.dir[a.ld + i];
-    t.d[2] = a.dir[2 * a.ld + i];
-    t.p[0] = a.pt[i];
-    t.p[1] = a.pt[a.ld + i];
-    t.p[2] = a.pt[2 * a.ld + i];
-    t.o = a.opl ? a.opl[i] : 0.0;
 }
 
 __device__ __forceinline__ void tilt_ray(const TiltArgs& a, int64_t i, const TiltIn& t, double (&qv)[5]) {
@@ -718,6 +777,51 @@ __device__ __forceinline__ void tilt_ray(const TiltArgs& a, int64_t i, const Til
     }
     qv[4] = o + norm3(x - p, y - q, z - r);
     if (a.total2) a.total2[i] = qv[4];
+}
+
+// tilt_ray's arithmetic without its stores (the fused kernel computes before issuing the next
+// segment's loads and stores after): detector-2 hit and total OPL 2 in d2 / t2, the sink
+// quantities (detector-1 hit, total OPL 1, total OPL 2) in qv
+__device__ __forceinline__ void tilt_compute(const TiltArgs& a, const TiltIn& t, double (&d2)[3], double (&qv)[5]) {
+    double ax, ay, az;
+    double l, m, n;
+    matvec(a.Rz, t.d[0], t.d[1], t.d[2], ax, ay, az);
+    matvec(a.Ry, ax, ay, az, l, m, n);
+    double p, q, r;
+    matvec(a.Rz, t.p[0] - a.c[0], t.p[1] - a.c[1], t.p[2] - a.c[2], ax, ay, az);
+    matvec(a.Ry, ax, ay, az, p, q, r);
+    p = p + a.c[0];
+    q = q + a.c[1];
+    r = r + a.c[2];
+    double x, y, z;
+    plane_hit(a.d1[0], a.d1[1], a.d1[2], a.d1[3], l, m, n, p, q, r, x, y, z);
+    qv[0] = x;
+    qv[1] = y;
+    qv[2] = z;
+    qv[3] = t.o + norm3(x - p, y - q, z - r);
+    plane_hit(a.d2[0], a.d2[1], a.d2[2], a.d2[3], l, m, n, p, q, r, x, y, z);
+    d2[0] = x;
+    d2[1] = y;
+    d2[2] = z;
+    qv[4] = t.o + norm3(x - p, y - q, z - r);
+}
+
+__device__ __forceinline__ void tilt_store(const TiltArgs& a, int64_t i0, int t, const double (&d2)[3],
+                                           const double (&qv)[5]) {
+    if (a.det1) {
+        double* o = a.det1 + i0;
+        o[t] = qv[0];
+        (o + a.ld)[t] = qv[1];
+        (o + 2 * a.ld)[t] = qv[2];
+    }
+    if (a.total1) (a.total1 + i0)[t] = qv[3];
+    if (a.det2) {
+        double* o = a.det2 + i0;
+        o[t] = d2[0];
+        (o + a.ld)[t] = d2[1];
+        (o + 2 * a.ld)[t] = d2[2];
+    }
+    if (a.total2) (a.total2 + i0)[t] = qv[4];
 }
 
 // the rotation and centre from the device parameter block (uniform scalar loads)
@@ -766,6 +870,54 @@ __global__ void __launch_bounds__(kBlock) k_tilt_opd_sink(TiltArgs a) {
         leaf_sink_segment<5>(a.sink, L, seg * kLeafSeg, qv, valid);
         cur = nxt;
     }
+}
+
+// Pass 1 of one run fused with the tilt of the run before it (RayWave.launch_front(fuse=...)):
+// both walk the same shard in 256-ray segments. Each segment's tilt inputs (56 B per ray, written
+// by the previous run's pass 2) are loaded right after the ray's grid-table loads and arrive
+// while the FP64-bound mirror chain runs, so the tilt's HBM traffic hides behind pass 1's
+// arithmetic instead of competing with it for wave slots as a second kernel would.
+template <int kWaves>
+__global__ void __launch_bounds__(kBlock, kWaves) k_chain_tilt(ChainArgs a, TiltArgs b) {
+    tilt_load_params(b);
+    __shared__ LeafLds<5> L;
+    int fl = 0;
+    double qv[5];
+    const int t = threadIdx.x;
+    const int64_t nseg = (a.n + kLeafSeg - 1) / kLeafSeg;
+    int64_t seg = blockIdx.x;
+    // software pipeline: segment s's table entries and tilt inputs were loaded during segment
+    // s - gridDim's stores, leaf sums and mirror loop
+    int64_t iv = 0, ih = 0;
+    double th = 0.0, tv = 0.0;
+    TiltIn in;
+    if (seg < nseg && seg * kLeafSeg + t < a.n) {
+        ray_tables(a, seg * kLeafSeg + t, iv, ih, th, tv);
+        tilt_load_all(b, seg * kLeafSeg + t, in);
+    }
+    for (; seg < nseg; seg += gridDim.x) {
+        const int64_t i0 = seg * kLeafSeg;
+        const bool valid = i0 + t < a.n;
+        const int64_t nxt = (seg + gridDim.x) * kLeafSeg + t;
+        double d2[3], tq[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+        if (valid)
+            chain_ray_tab<true, false, false, false, true, true>(a, i0, t, iv, ih, th, tv, fl, qv, [&] {
+                tilt_compute(b, in, d2, tq);
+                if (nxt < a.n) {
+                    ray_tables(a, nxt, iv, ih, th, tv);
+                    tilt_load_all(b, nxt, in);
+                }
+            });
+        if (valid) {  // detector-2 rows only (detector 1 and the rotated rays are the full mode's)
+            double* o = b.det2 + i0;
+            o[t] = d2[0];
+            (o + b.ld)[t] = d2[1];
+            (o + 2 * b.ld)[t] = d2[2];
+            (b.total2 + i0)[t] = tq[4];
+        }
+        leaf_sink_segment<5>(b.sink, L, i0, tq, valid);
+    }
+    if (fl) atomicOr(a.flags, fl);
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -904,12 +1056,22 @@ static int64_t opd_grid_cap() {
 
 template <bool kGrid, bool kOPL, bool kSink>
 static void launch_chain(int w, unsigned g, hipStream_t s, const ChainArgs& a) {
+    if (!kSink && a.hits) {  // per-mirror hit rows (the stage-equivalent outputs): one variant
+        k_chain<kGrid, kOPL, 4, true><<<g, kBlock, 0, s>>>(a);
+        return;
+    }
+    // rays from the point source: the variant without origin loads (grid rays only)
+    const bool point = kGrid && a.org == nullptr;
 #define AKB_CHAIN_CASE(W)                                                        \
     case W:                                                                      \
-        if (kSink)                                                               \
-            k_chain_sink<kGrid, kOPL, W><<<g, kBlock, 0, s>>>(a);                \
+        if (kSink && point)                                                      \
+            k_chain_sink<kGrid, kOPL, W, kGrid><<<g, kBlock, 0, s>>>(a);         \
+        else if (kSink)                                                          \
+            k_chain_sink<kGrid, kOPL, W, false><<<g, kBlock, 0, s>>>(a);         \
+        else if (point)                                                          \
+            k_chain<kGrid, kOPL, W, false, kGrid><<<g, kBlock, 0, s>>>(a);       \
         else                                                                     \
-            k_chain<kGrid, kOPL, W><<<g, kBlock, 0, s>>>(a);                     \
+            k_chain<kGrid, kOPL, W, false, false><<<g, kBlock, 0, s>>>(a);       \
         break;
     switch (w) {
         AKB_CHAIN_CASE(2)
@@ -1046,8 +1208,10 @@ static void div_magic(uint32_t d, uint32_t* mul, uint32_t* shift) {
     *shift = l;
 }
 
-int akb_trace_chain_f64(const akb_chain_desc* d, void* stream) {
-    clear_error();
+// validate a chain descriptor and form the kernel arguments (AKB_OK, or an error with n_rays == 0
+// reported as AKB_OK and *empty set)
+static int chain_args_from(const akb_chain_desc* d, ChainArgs& a, bool& empty) {
+    empty = false;
     AKB_REQUIRE(d != nullptr, "null descriptor");
     AKB_REQUIRE(d->n_mirrors >= 0 && d->n_mirrors <= AKB_MAX_MIRRORS, "n_mirrors out of range");
     AKB_REQUIRE(d->n_rays >= 0, "n_rays < 0");
@@ -1067,9 +1231,13 @@ int akb_trace_chain_f64(const akb_chain_desc* d, void* stream) {
     if (sink) {
         AKB_REQUIRE(d->sink.nq == 5 && d->sink.n == d->n_rays && d->sink.leaf_sum && d->sink.leaf_cnt &&
                         d->sink.tail, "chain sink must be a 5-quantity sink over n_rays");
+        AKB_REQUIRE(d->hits == nullptr, "per-mirror hits are written by the chain without a sink");
     }
-    if (d->n_rays == 0) return AKB_OK;
-    ChainArgs a{};
+    a = ChainArgs{};
+    if (d->n_rays == 0) {
+        empty = true;
+        return AKB_OK;
+    }
     a.K = d->n_mirrors;
     a.negmask = 0;
     for (int k = 0; k < d->n_mirrors; ++k) {
@@ -1095,6 +1263,7 @@ int akb_trace_chain_f64(const akb_chain_desc* d, void* stream) {
     a.n_v = grid ? (uint32_t)d->n_v : 1u;
     div_magic(a.n_h, &a.div_mul, &a.div_shift);
     a.g0 = grid ? d->row0 * d->n_h : 0;
+    a.g_stride = 1;
     a.n = d->n_rays;
     a.org = d->org;
     a.org_ld = d->org_ld;
@@ -1121,6 +1290,17 @@ int akb_trace_chain_f64(const akb_chain_desc* d, void* stream) {
     a.pert_h = d->pert_h;
     a.pert_v = d->pert_v;
     a.pert_terms = d->pert_h ? d->pert_terms : 0;
+    return AKB_OK;
+}
+
+int akb_trace_chain_f64(const akb_chain_desc* d, void* stream) {
+    clear_error();
+    ChainArgs a;
+    bool empty;
+    const int st = chain_args_from(d, a, empty);
+    if (st != AKB_OK || empty) return st;
+    const bool grid = d->dir == nullptr;
+    const bool sink = d->sink.nq > 0;
     hipStream_t s = (hipStream_t)stream;
     const int64_t gcap = chain_grid_cap();
     const unsigned gsz = grid_for(d->n_rays, 1, gcap);
@@ -1152,17 +1332,16 @@ int akb_trace_chain_f64(const akb_chain_desc* d, void* stream) {
     return launch_status("k_chain");
 }
 
-static int launch_tilt(TiltArgs& a, const double det1_ghij[4], const double det2_ghij[4], const double* dir,
-                       const double* pt, const double* opl, int64_t ld, int64_t n, double* dir_rot, double* pt_rot,
-                       double* det1, double* det2, double* total1, double* total2, const akb_leaf_sink* sink,
-                       void* stream) {
+// validate a tilt's operands and fill its kernel arguments (the rotation comes from the caller)
+static int tilt_args_from(TiltArgs& a, const double det1_ghij[4], const double det2_ghij[4], const double* dir,
+                          const double* pt, const double* opl, int64_t ld, int64_t n, double* dir_rot, double* pt_rot,
+                          double* det1, double* det2, double* total1, double* total2, const akb_leaf_sink* sink) {
     AKB_REQUIRE(det1_ghij && det2_ghij && dir && pt, "null pointer");
     AKB_REQUIRE(n >= 0 && ld >= n, "bad sizes");
     const bool use_sink = sink && sink->nq > 0;
     if (use_sink)
         AKB_REQUIRE(sink->nq == 5 && sink->n == n && sink->leaf_sum && sink->leaf_cnt && sink->tail,
                     "tilt sink must be a 5-quantity sink over n");
-    if (n == 0) return AKB_OK;
     for (int k = 0; k < 4; ++k) {
         a.d1[k] = det1_ghij[k];
         a.d2[k] = det2_ghij[k];
@@ -1178,8 +1357,19 @@ static int launch_tilt(TiltArgs& a, const double det1_ghij[4], const double det2
     a.det2 = det2;
     a.total1 = total1;
     a.total2 = total2;
-    if (use_sink) {
-        a.sink = *sink;
+    if (use_sink) a.sink = *sink;
+    return AKB_OK;
+}
+
+static int launch_tilt(TiltArgs& a, const double det1_ghij[4], const double det2_ghij[4], const double* dir,
+                       const double* pt, const double* opl, int64_t ld, int64_t n, double* dir_rot, double* pt_rot,
+                       double* det1, double* det2, double* total1, double* total2, const akb_leaf_sink* sink,
+                       void* stream) {
+    const int st = tilt_args_from(a, det1_ghij, det2_ghij, dir, pt, opl, ld, n, dir_rot, pt_rot, det1, det2, total1,
+                                  total2, sink);
+    if (st != AKB_OK) return st;
+    if (n == 0) return AKB_OK;
+    if (sink && sink->nq > 0) {
         const int64_t nseg = (n + kLeafSeg - 1) / kLeafSeg;
         const unsigned gs = (unsigned)(nseg < kStreamGridCap ? nseg : kStreamGridCap);
         k_tilt_opd_sink<<<gs, kBlock, 0, (hipStream_t)stream>>>(a);
@@ -1269,6 +1459,86 @@ int akb_tilt_opd_dev_f64(const double* d_params, const double det1_ghij[4], cons
     a.params = d_params;
     return launch_tilt(a, det1_ghij, det2_ghij, dir, pt, opl, ld, n, dir_rot, pt_rot, det1, det2, total1, total2,
                        sink, stream);
+}
+
+int akb_trace_chain_samples_f64(const akb_chain_desc* d, void* stream) {
+    clear_error();
+    AKB_REQUIRE(d != nullptr, "null descriptor");
+    ChainArgs a;
+    bool empty;
+    const int st = chain_args_from(d, a, empty);
+    if (st != AKB_OK) return st;
+    AKB_REQUIRE(d->dir == nullptr && d->opl == nullptr && d->sink.nq == 0, "the picks come from grid rays of pass 1");
+    AKB_REQUIRE(d->samp_h || d->samp_v, "no picks requested");
+    const bool has_h = d->samp_h && d->samp_h_end > d->samp_h_begin;
+    if (has_h)
+        AKB_REQUIRE(d->samp_h_begin >= 0 && d->samp_h_end <= d->n_h * d->n_v, "pick range outside the grid");
+    // only the picks and the flags leave these rays
+    a.hits = a.last_hit = a.dir_out = a.det_out = a.opl = a.atan_h = a.atan_v = nullptr;
+    a.pert_h = a.pert_v = nullptr;
+    hipStream_t s = (hipStream_t)stream;
+    if (has_h) {  // the middle-row range: contiguous flat indices
+        ChainArgs r = a;
+        r.samp_v = nullptr;
+        r.g0 = d->samp_h_begin;
+        r.g_stride = 1;
+        r.n = d->samp_h_end - d->samp_h_begin;
+        k_chain<true, false, 4><<<grid_for(r.n), kBlock, 0, s>>>(r);
+        const int e = launch_status("k_chain (picks, row)");
+        if (e != AKB_OK) return e;
+    }
+    if (d->samp_v) {  // one grid column: flat indices col, col + n_h, ...
+        ChainArgs c = a;
+        c.samp_h = nullptr;
+        c.g0 = d->samp_v_col;
+        c.g_stride = d->n_h;
+        c.n = d->n_v;
+        k_chain<true, false, 4><<<grid_for(c.n), kBlock, 0, s>>>(c);
+        return launch_status("k_chain (picks, column)");
+    }
+    return AKB_OK;
+}
+
+int akb_chain_tilt_f64(const akb_chain_desc* d, const double* d_params, const double det1_ghij[4],
+                       const double det2_ghij[4], const double* dir, const double* pt, const double* opl, int64_t ld,
+                       int64_t n, double* dir_rot, double* pt_rot, double* det1, double* det2, double* total1,
+                       double* total2, const akb_leaf_sink* sink, void* stream) {
+    clear_error();
+    AKB_REQUIRE(d && d_params && sink, "null pointer");
+    ChainArgs a;
+    bool empty;
+    int st = chain_args_from(d, a, empty);
+    if (st != AKB_OK) return st;
+    AKB_REQUIRE(d->dir == nullptr && d->opl == nullptr && d->sink.nq == 0,
+                "the fused kernel runs pass 1: grid rays, no OPL, no sink of its own");
+    AKB_REQUIRE(d->n_rays == n, "the chain and the tilt must cover the same rays");
+    AKB_REQUIRE(opl != nullptr, "the fused tilt needs the pass-2 OPL row");
+    AKB_REQUIRE(d->org == nullptr, "the fused pass 1 traces from a point source");
+    AKB_REQUIRE(det2 && total2 && !det1 && !total1 && !dir_rot && !pt_rot,
+                "the fused tilt writes the detector-2 rows only (detector 1 / rotated rays: unfused)");
+    AKB_REQUIRE(!d->last_hit && !d->dir_out && !d->det_out && !d->atan_h && !d->atan_v && !d->hits,
+                "the fused pass 1 writes only the resample picks and the flags");
+    AKB_REQUIRE(sink->nq > 0, "the tilt needs its sink");
+    TiltArgs b{};
+    b.params = d_params;
+    st = tilt_args_from(b, det1_ghij, det2_ghij, dir, pt, opl, ld, n, dir_rot, pt_rot, det1, det2, total1, total2,
+                        sink);
+    if (st != AKB_OK || empty) return st;
+    const int64_t nseg = (n + kLeafSeg - 1) / kLeafSeg;
+    const int64_t gcap = chain_grid_cap();
+    const unsigned gs = (unsigned)(nseg < gcap ? nseg : gcap);
+    hipStream_t s = (hipStream_t)stream;
+    switch (chain_waves()) {
+        case 2:
+            k_chain_tilt<2><<<gs, kBlock, 0, s>>>(a, b);
+            break;
+        case 8:
+            k_chain_tilt<8><<<gs, kBlock, 0, s>>>(a, b);
+            break;
+        default:
+            k_chain_tilt<4><<<gs, kBlock, 0, s>>>(a, b);
+    }
+    return launch_status("k_chain_tilt");
 }
 
 int akb_opd_f64(const double* total1, const double* total2, const double* det2, int64_t ld, int64_t n,

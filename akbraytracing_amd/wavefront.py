@@ -180,8 +180,12 @@ class _Front:
     params: torch.Tensor
     full: bool
     stream: object
-    flags: tuple
+    flags: tuple = None  # (pass 1, pass 2) trace flag words once known (RayWave._resolve)
+    flag_ev: object = None  # event after the flag words' copy to the host
     done: object = None  # event on the front's stream after its last kernel (the tilt parameters)
+    slot: int = 0  # which of the two extent-key buffers this run's OPD / pupil use
+    tilt: dict = None  # tilt outputs, when the next front's pass 1 already tilted this run (fused)
+    tilted: object = None  # event after that fused kernel
 
 
 class RayWave:
@@ -212,73 +216,99 @@ class RayWave:
         # total2), all nanmean (:3626, :3633, :3674)
         self.sink2 = LeafSink(5, self.n_local, 0b00011, self.dev)
         self.sink3 = LeafSink(5, self.n_local, 0b11111, self.dev)
-        self._ext = torch.zeros(4, dtype=torch.int64, device=self.dev)  # det2 extent keys (uint64 bits)
+        # det2 extent keys (uint64 bits), two sets: run k's OPD / pupil read theirs while run k+1's
+        # tilt-parameter kernel clears the other one
+        self._ext = torch.zeros((2, 4), dtype=torch.int64, device=self.dev)
+        self._runs = 0
         self._pitch = torch.zeros(2, dtype=D.F64, device=self.dev)
         self._opd_buf = None
         self.last = {}
         self.kernel_events = None  # set to a list to time the pass-2 chain launch (bench.py)
-        # prepared launches. The pick buffer ends with one double-sized slot holding the two
-        # trace flag words (pass 1, pass 2): one copy brings the picks and pass 1's flags to the
-        # host, an 8-byte copy brings pass 2's, and the tilt-parameter kernel zeroes both.
+        # prepared launches. The resample picks come from a prepass that traces only the rays
+        # they read (akb_trace_chain_samples_f64, every rank all of them); the pick buffer ends
+        # with one double-sized slot holding that prepass's flag word, so one copy brings both to
+        # the host. The full pass 1 (this shard's rays, possibly fused with the previous run's
+        # tilt) then runs while the host resamples; its flag word and pass 2's ([pass 1, pass 2])
+        # reach the host in one 8-byte copy after pass 2, and the tilt-parameter kernel zeroes them.
         self._plan = sample_plan(self.n)
         hb, he, col = self._plan
         self._nsamp = (he - hb) + self.n
-        self._x1 = torch.zeros(self._nsamp + 1, dtype=D.F64, device=self.dev)
-        self._flags = self._x1[self._nsamp:].view(torch.int32)  # [pass 1, pass 2]
-        self._x1_host = torch.empty(self._nsamp + 1, dtype=D.F64, pin_memory=True)
-        self._f_host = torch.zeros(2, dtype=torch.int32, pin_memory=True)
-        self._tan2 = torch.empty(2 * self.n, dtype=D.F64, device=self.dev)  # pass-2 tables [h | v]
-        self._tan2_host = torch.empty(2 * self.n, dtype=D.F64, pin_memory=True)
+        # the picks, then four int32 flag words [pass 1, pass 2, prepass, unused]: one copy
+        # brings the picks and the prepass's word, and the tilt-parameter kernel clears all four
+        self._x1 = torch.zeros(self._nsamp + 2, dtype=D.F64, device=self.dev)
+        words = self._x1[self._nsamp:].view(torch.int32)
+        self._flags, self._sflag, self._words = words[0:2], words[2:3], words
+        self._x1_host = torch.empty(self._nsamp + 2, dtype=D.F64, pin_memory=True)
+        # per run slot (a run's front returns before its pass 2 ends, so the next run must not
+        # reuse them): the [pass 1, pass 2] flag words on the host and the pass-2 tables [h | v]
+        self._f_host = torch.zeros((2, 2), dtype=torch.int32, pin_memory=True)
+        self._tan2 = torch.empty((2, 2 * self.n), dtype=D.F64, device=self.dev)
+        self._tan2_host = torch.empty((2, 2 * self.n), dtype=D.F64, pin_memory=True)
+        self._ps = ChainLaunch(self.g.mirrors, tan_h=self.tan_h, tan_v=self.tan_v, row0=0, n_rays=self.n * self.n,
+                               src=self.g.source, want=(), samples=(hb, he, col), flags=self._sflag,
+                               samples_buf=self._x1[:self._nsamp])
         self._p1 = ChainLaunch(self.g.mirrors, tan_h=self.tan_h, tan_v=self.tan_v, row0=self.shard.row0,
-                               n_rays=self.n_local, src=self.g.source, want=(), samples=(hb, he, col),
-                               flags=self._flags[0:1], samples_buf=self._x1[:self._nsamp])
+                               n_rays=self.n_local, src=self.g.source, want=(), flags=self._flags[0:1])
         self._p2 = {}
-        self._own = sample_ownership(self.shard, self.n)
         self._pert = perturbation.device_tables(self.n, self.n, self.dev) if perturbation is not None else None
         # event after the last queued reader of the pass-2 buffers / extent keys (a back half
         # and its pupil, possibly on another stream): the next pass 2 waits for it
         self._back_done = None
+        # small host<->device copies (picks, pass-2 tables, flag words) run on their own stream,
+        # beside the kernels instead of between them
+        self._copy = torch.cuda.Stream(device=self.dev)
 
-    def _pass2_launch(self, want_rows):
-        key = bool(want_rows)
+    def _pass2_launch(self, want_rows, slot=0):
+        key = (bool(want_rows), slot)
         if key not in self._p2:
             want = ("last_hit", "dir_out", "opl") + (("det", "atan") if want_rows else ())
-            self._p2[key] = ChainLaunch(self.g.mirrors, tan_h=self._tan2[:self.n], tan_v=self._tan2[self.n:],
+            # both slots write the same output buffers (the next pass 2 may rewrite them once the
+            # fused tilt that reads them, queued ahead of it, is done)
+            out = self._p2[(key[0], 1 - slot)].res.extra["buffers"] if (key[0], 1 - slot) in self._p2 else None
+            t2 = self._tan2[slot]
+            self._p2[key] = ChainLaunch(self.g.mirrors, tan_h=t2[:self.n], tan_v=t2[self.n:], out=out,
                                         row0=self.shard.row0, n_rays=self.n_local, src=self.g.source,
                                         det_ghij=self.g.det1, want=want, sink=self.sink2, flags=self._flags[1:2],
                                         pert=self._pert)
         return self._p2[key]
 
     # -------------------------------------------------------------- passes
-    def _pass1(self, overlap=None, stream=None):
+    def _pass1(self, overlap=None, stream=None, fuse=None):
+        """The picks prepass and its copy to the host, then the full pass 1 (fused with fuse's
+        tilt when given) and `overlap`'s work queued behind it; the host waits for the picks only,
+        so the resample it does next overlaps the full trace. Returns the picks and the prepass's
+        flags (the full pass 1's are checked after pass 2)."""
         hb, he, col = self._plan
-        self._p1.launch(stream=stream, reset_flags=False)
+        _lib.check(_lib.lib().akb_trace_chain_samples_f64(self._ps.desc, stream))
+        picked = torch.cuda.Event()
+        picked.record()
         x = self._x1_host
-        x.copy_(self._x1, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
-        if overlap is not None:
-            overlap()  # independent device work queued behind the copy (runs while the host waits)
+        with torch.cuda.stream(self._copy):
+            self._copy.wait_event(picked)
+            x.copy_(self._x1, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self._copy)
+        if fuse is None:
+            self._p1.launch(stream=stream, reset_flags=False)
+        else:
+            self._fused_pass1(fuse, stream)
         ev.synchronize()
+        if overlap is not None:
+            # independent device work (the previous run's back half) queued behind pass 1, so it
+            # runs beside this run's pass 2; queued after the wait, when everything the previous
+            # run put on this stream - its pass-2 flag words included - has completed
+            overlap()
         host = x.numpy()
         nh = he - hb
         flags = int(host[self._nsamp:].view(np.int32)[0])
-        if self.comm.world > 1:
-            own_h, own_v = self._own
-            samp_h = np.where(own_h, host[:nh], 0.0)
-            samp_v = np.where(own_v, host[nh:self._nsamp], 0.0)
-            samp_h, samp_v = self.comm.gather_samples(samp_h, samp_v, self.shard, self.n)
-            flags = self.comm.sum_flags(flags)
-        else:
-            samp_h, samp_v = host[:nh], host[nh:self._nsamp]
-        return samp_h, samp_v, flags
+        return host[:nh].copy(), host[nh:self._nsamp].copy(), flags
 
-    def _pass2(self, want_rows=False, stream=None):
+    def _pass2(self, want_rows=False, stream=None, slot=0):
         ev = None
         if self.kernel_events is not None:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
-        r = self._pass2_launch(want_rows).launch(stream=stream, reset_flags=False)
+        r = self._pass2_launch(want_rows, slot).launch(stream=stream, reset_flags=False)
         if ev is not None:
             ev[1].record()
             self.kernel_events.append(ev)
@@ -319,18 +349,35 @@ class RayWave:
         GPU while the host resamples (bench.py does)."""
         return self.launch_back(self.launch_front(full=full, overlap=overlap), opd=opd, keep_rotated=keep_rotated)
 
-    def launch_front(self, full=False, overlap=None):
-        """Pass 1, the resample (the run's one host wait), pass 2, its sums and the device tilt
-        parameters. Returns once pass 2's flag word is on the host; the rest stays queued."""
+    def launch_front(self, full=False, overlap=None, fuse=None):
+        """The resample picks, pass 1, the resample (the run's one host wait, for the picks
+        only), pass 2, its sums and the device tilt parameters. Returns as soon as all of it is
+        queued; the trace flags are read when launch_back (or _resolve) needs them.
+
+        fuse: the previous run's front, not yet handed to launch_back: its tilt then runs inside
+        this run's pass-1 kernel (akb_chain_tilt_f64), its loads hidden behind the chain's
+        arithmetic, and its launch_back only finishes the tilt sums and forms the OPD (queue that
+        in `overlap`, called right after the host wait for the picks, so it runs beside this
+        run's pass 2). A fused OPD inside pass 2 measured slower (1.005 vs 0.974 ms per bench
+        step): its loads and registers cost the FP64-bound chain more than running beside it."""
         L = _lib.lib()
         stream = D.stream_handle()
-        samp_h, samp_v, flags1 = self._pass1(overlap, stream)
-        if flags1:
-            self._flags.zero_()
-            raise _lib.AKBError(
-                f"pass 1 raised trace flags {flags1:#x} (a ray missed a mirror or a norm was zero): the "
-                "reference returns all-NaN here and its interp1d resample fails on it")
-        th = self._tan2_host.numpy()
+        slot = self._runs % 2
+        self._runs += 1
+        if fuse is not None and fuse.tilt is not None:
+            fuse = None
+        # fused optimistically: should fuse's pass 2 turn out flagged, launch_back ignores the
+        # fused tilt and takes the staged path (its tables live in fuse's own slot)
+        if fuse is not None and self._back_done is not None:
+            # the fused tilt refills the tilt sink the previous back half finishes and reads
+            torch.cuda.current_stream().wait_event(self._back_done)
+            self._back_done = None
+        samp_h, samp_v, sflags = self._pass1(overlap, stream, fuse=fuse)
+        if sflags:
+            torch.cuda.synchronize()
+            self._words.zero_()
+            raise _lib.AKBError(self._pass1_error(sflags))
+        th = self._tan2_host[slot].numpy()
         if self.resample_pass:
             # np.arctan / np.tan stay numpy's (their SIMD kernels are what the reference runs)
             np.tan(resample_axis(np.arctan(samp_h), self.rand_h), out=th[:self.n])
@@ -338,31 +385,67 @@ class RayWave:
         else:
             np.tan(self.rand_h, out=th[:self.n])
             np.tan(self.rand_v, out=th[self.n:])
-        self._tan2.copy_(self._tan2_host, non_blocking=True)
-        tan_h2, tan_v2 = self._tan2[:self.n], self._tan2[self.n:]
-        if self._back_done is not None:
-            # pass 2 rewrites the buffers a queued back half reads, and the tilt-parameter kernel
-            # behind it clears the extent keys that half's pupil reads
+        with torch.cuda.stream(self._copy):
+            self._tan2[slot].copy_(self._tan2_host[slot], non_blocking=True)
+            tables = torch.cuda.Event()
+            tables.record(self._copy)
+        torch.cuda.current_stream().wait_event(tables)
+        tan_h2, tan_v2 = self._tan2[slot, :self.n], self._tan2[slot, self.n:]
+        if self._back_done is not None and fuse is None:
+            # pass 2 rewrites the buffers a queued (unfused) back half's tilt reads
             torch.cuda.current_stream().wait_event(self._back_done)
             self._back_done = None
-        r = self._pass2(want_rows=full, stream=stream)
+        r = self._pass2(want_rows=full, stream=stream, slot=slot)
         if self.comm.world > 1:
-            self.comm.allreduce_sums(self._flags[1:2])
-        self._f_host.copy_(self._flags, non_blocking=True)
-        ev2 = torch.cuda.Event()
-        ev2.record()
+            self.comm.allreduce_sums(self._flags)
         sums, cnts = self.sink2.finish(stream)
         if self.comm.world > 1:  # cross-rank means: partial sums added over ranks (not numpy order)
             self.comm.allreduce_sums(sums)
             self.comm.allreduce_sums(cnts)
-        params = torch.empty(23, dtype=D.F64, device=self.dev)  # this run's own block
-        _lib.check(L.akb_tilt_params_f64(D.ptr(sums), D.ptr(cnts), D.ptr(params), D.ptr(self._ext),
-                                         D.ptr(self._flags), 2, stream))
+        params = torch.empty(25, dtype=D.F64, device=self.dev)  # this run's own block
+        _lib.check(L.akb_tilt_params_f64(D.ptr(sums), D.ptr(cnts), D.ptr(params), D.ptr(self._ext[slot]),
+                                         D.ptr(self._words), 4, stream))
         done = torch.cuda.Event()
         done.record()
-        ev2.synchronize()
-        return _Front(r=r, tan_h2=tan_h2, tan_v2=tan_v2, params=params, full=full, stream=stream,
-                      flags=(flags1, int(self._f_host[1])), done=done)
+        # the flag words the parameter kernel kept (params[23:25]) to the host, beside the next run
+        with torch.cuda.stream(self._copy):
+            self._copy.wait_event(done)
+            self._f_host[slot].copy_(params[23:24].view(torch.int32), non_blocking=True)
+            ev2 = torch.cuda.Event()
+            ev2.record(self._copy)
+        params.record_stream(self._copy)
+        return _Front(r=r, tan_h2=tan_h2, tan_v2=tan_v2, params=params, full=full, stream=stream, flag_ev=ev2,
+                      done=done, slot=slot)
+
+    def _resolve(self, f):
+        """f's trace flags (waits for its pass 2 if still running); a flagged pass 1 raises."""
+        if f.flags is None:
+            f.flag_ev.synchronize()
+            h = self._f_host[f.slot]
+            f.flags = (int(h[0]), int(h[1]))
+        if f.flags[0]:  # the full pass 1 (its flag word arrives with pass 2's)
+            raise _lib.AKBError(self._pass1_error(f.flags[0]))
+        return f.flags
+
+    @staticmethod
+    def _pass1_error(flags):
+        return (f"pass 1 raised trace flags {flags:#x} (a ray missed a mirror or a norm was zero): the "
+                "reference returns all-NaN here and its interp1d resample fails on it")
+
+    def _fused_pass1(self, f, stream):
+        """This run's pass 1 and run f's tilt in one kernel (f's pass-2 buffers are still intact:
+        this run's pass 2 comes after it on the same stream)."""
+        L = _lib.lib()
+        tb = self._tilt_buffers(False, f.full)
+        r = f.r
+        n = self.n_local
+        _lib.check(L.akb_chain_tilt_f64(self._p1.desc, D.ptr(f.params), D.host_f64(self.g.det1),
+                                        D.host_f64(tb["d2"]), D.ptr(r.dir_out), D.ptr(r.last_hit), D.ptr(r.opl),
+                                        n, n, None, None, D.ptr(tb["det1"]), D.ptr(tb["det2_buf"]),
+                                        D.ptr(tb["total1"]), D.ptr(tb["total2"]), self.sink3.desc, stream))
+        ev = torch.cuda.Event()
+        ev.record()
+        f.tilt, f.tilted = tb, ev
 
     def launch_back(self, f, opd=True, keep_rotated=False, stream=None):
         """Tilt, detectors and OPD of a launch_front (no host wait). stream: run them on that
@@ -372,8 +455,11 @@ class RayWave:
         if stream is None:
             out = self._launch_back(f, opd, keep_rotated)
         else:
-            stream.wait_event(f.done)
+            stream.wait_event(f.tilted if f.tilt is not None else f.done)
             f.params.record_stream(stream)  # allocated on the front's stream, read here
+            for t in (f.tilt or {}).values():
+                if isinstance(t, torch.Tensor):
+                    t.record_stream(stream)
             with torch.cuda.stream(stream):
                 out = self._launch_back(dataclasses.replace(f, stream=None), opd, keep_rotated)
         ev = torch.cuda.Event()
@@ -383,21 +469,24 @@ class RayWave:
 
     def _launch_back(self, f, opd, keep_rotated):
         r = f.r
-        if f.flags[1]:
-            out = self._run_staged(None, f.tan_h2, f.tan_v2, opd, keep_rotated, f.full)
+        if self._resolve(f)[1]:  # a flagged pass 2: the staged path (a fused tilt is discarded)
+            out = self._run_staged(None, f.tan_h2, f.tan_v2, opd, keep_rotated, f.full, slot=f.slot)
         else:
             out = RunResult(last_hit=r.last_hit, dir_out=r.dir_out, opl=r.opl, tan_h2=f.tan_h2, tan_v2=f.tan_v2,
                             params=f.params)
             if f.full:
                 out.update(det_pre=r.det, atan=r.atan)
-            if opd:
+            if f.tilt is not None:  # tilted inside the next run's pass 1
+                out.update(self._opd_after_tilt(f.tilt, f.full, True, f.slot, f.stream))
+            elif opd:
                 out.update(self._tilt_opd(r.last_hit, r.dir_out, r.opl, keep_rotated, f.full, params=f.params,
-                                          stream=f.stream))
+                                          stream=f.stream, slot=f.slot))
         out["flags"] = f.flags
+        out["slot"] = f.slot
         self.last = out
         return out
 
-    def _run_staged(self, fast, tan_h2, tan_v2, opd, keep_rotated, full):
+    def _run_staged(self, fast, tan_h2, tan_v2, opd, keep_rotated, full, slot=0):
         """Pass 2 flagged a miss or a zero norm: redo it stage by stage (the reference's value
         rules) and the tilt from host-formed matrices."""
         torch.cuda.synchronize()
@@ -416,47 +505,58 @@ class RayWave:
             out.update(det_pre=det_pre, atan=atan)
         if opd:
             ry, rz = P.rotation_matrices(-theta_y, -theta_z)
-            out.update(self._tilt_opd(last_hit, dir_out, opl, keep_rotated, full, host_tilt=(ry, rz, focus)))
+            out.update(self._tilt_opd(last_hit, dir_out, opl, keep_rotated, full, host_tilt=(ry, rz, focus), slot=slot))
         return out
 
+    def _tilt_buffers(self, keep_rotated, full):
+        """Output tensors of one tilt (allocated on the current stream)."""
+        n, dev = self.n_local, self.dev
+        two = self.g.det2 is not None
+        e = lambda *shape: torch.empty(shape, dtype=D.F64, device=dev)
+        tb = dict(two=two, d2=self.g.det2 if two else self.g.det1,
+                  det1=e(3, n) if (full or not two) else None, det2=e(3, n) if two else None,
+                  total1=e(n) if (full or not two) else None, total2=e(n),
+                  dir_rot=e(3, n) if keep_rotated else None, pt_rot=e(3, n) if keep_rotated else None)
+        tb["det2_buf"] = tb["det2"] if two else e(3, n)
+        return tb
+
     def _tilt_opd(self, last_hit, dir_out, opl, keep_rotated=False, full=False, host_tilt=None, params=None,
-                  stream=None):
+                  stream=None, slot=0):
         L = _lib.lib()
         n = self.n_local
-        dev = self.dev
-        stream = D.stream_handle(stream)
-        two = self.g.det2 is not None
-        det1 = torch.empty((3, n), dtype=D.F64, device=dev) if (full or not two) else None
-        det2 = torch.empty((3, n), dtype=D.F64, device=dev) if two else None
-        total1 = torch.empty(n, dtype=D.F64, device=dev) if (full or not two) else None
-        total2 = torch.empty(n, dtype=D.F64, device=dev)
-        dir_rot = torch.empty((3, n), dtype=D.F64, device=dev) if keep_rotated else None
-        pt_rot = torch.empty((3, n), dtype=D.F64, device=dev) if keep_rotated else None
-        d2 = self.g.det2 if two else self.g.det1
-        det2_buf = det2 if two else torch.empty((3, n), dtype=D.F64, device=dev)
-        outs = (D.ptr(dir_out), D.ptr(last_hit), D.ptr(opl), n, n, D.ptr(dir_rot), D.ptr(pt_rot), D.ptr(det1),
-                D.ptr(det2_buf), D.ptr(total1), D.ptr(total2), self.sink3.desc, stream)
+        sh = D.stream_handle(stream)
+        tb = self._tilt_buffers(keep_rotated, full)
+        outs = (D.ptr(dir_out), D.ptr(last_hit), D.ptr(opl), n, n, D.ptr(tb["dir_rot"]), D.ptr(tb["pt_rot"]),
+                D.ptr(tb["det1"]), D.ptr(tb["det2_buf"]), D.ptr(tb["total1"]), D.ptr(tb["total2"]), self.sink3.desc,
+                sh)
         if host_tilt is None:
-            _lib.check(L.akb_tilt_opd_dev_f64(D.ptr(params), D.host_f64(self.g.det1), D.host_f64(d2), *outs))
+            _lib.check(L.akb_tilt_opd_dev_f64(D.ptr(params), D.host_f64(self.g.det1), D.host_f64(tb["d2"]), *outs))
         else:
             ry, rz, focus = host_tilt
             _lib.check(L.akb_tilt_opd_f64(D.host_f64(ry.ravel()), D.host_f64(rz.ravel()), D.host_f64(focus),
-                                          D.host_f64(self.g.det1), D.host_f64(d2), *outs))
-        sums, cnts = self.sink3.finish(stream)
+                                          D.host_f64(self.g.det1), D.host_f64(tb["d2"]), *outs))
+        return self._opd_after_tilt(tb, full, host_tilt is None, slot, stream)
+
+    def _opd_after_tilt(self, tb, full, keys_zeroed, slot, stream):
+        """The tilt sink's means, then DistError / Sph / Wave2 and the pupil extent keys."""
+        L = _lib.lib()
+        n, dev = self.n_local, self.dev
+        sh = D.stream_handle(stream)
+        sums, cnts = self.sink3.finish(sh)
         if self.comm.world > 1:
             self.comm.allreduce_sums(sums)
             self.comm.allreduce_sums(cnts)
         self._means5 = (sums, cnts)
+        total1 = tb["total1"]
         dist_err = torch.empty(n, dtype=D.F64, device=dev) if total1 is not None else None
         dist_err2 = torch.empty(n, dtype=D.F64, device=dev)
         sph = torch.empty(n, dtype=D.F64, device=dev) if full else None
-        wave2 = torch.empty(n, dtype=D.F64, device=dev) if two else None
-        _lib.check(L.akb_opd_f64(D.ptr(total1), D.ptr(total2), D.ptr(det2_buf), n, n, D.ptr(sums), D.ptr(cnts),
-                                 D.ptr(dist_err), D.ptr(dist_err2), D.ptr(sph), D.ptr(wave2), D.ptr(self._ext),
-                                 int(host_tilt is None), stream))
-        res = dict(dir_rot=dir_rot, pt_rot=pt_rot, detcenter=det1, detcenter2=det2, total=total1, total2=total2,
-                   dist_err=dist_err, dist_err2=dist_err2, sph=sph, wave2=wave2)
-        return res
+        wave2 = torch.empty(n, dtype=D.F64, device=dev) if tb["two"] else None
+        _lib.check(L.akb_opd_f64(D.ptr(total1), D.ptr(tb["total2"]), D.ptr(tb["det2_buf"]), n, n, D.ptr(sums),
+                                 D.ptr(cnts), D.ptr(dist_err), D.ptr(dist_err2), D.ptr(sph), D.ptr(wave2),
+                                 D.ptr(self._ext[slot]), int(bool(keys_zeroed)), sh))
+        return dict(dir_rot=tb["dir_rot"], pt_rot=tb["pt_rot"], detcenter=tb["det1"], detcenter2=tb["det2"],
+                    total=total1, total2=tb["total2"], dist_err=dist_err, dist_err2=dist_err2, sph=sph, wave2=wave2)
 
     def means(self):
         """Host copies of the post-tilt means: (mean_total [detector 1, detector 2], mean_focus)."""
@@ -479,7 +579,7 @@ class RayWave:
         L = _lib.lib()
         if self._opd_buf is None or self._opd_buf.shape[0] != size:
             self._opd_buf = torch.empty((size, size), dtype=D.F64, device=self.dev)
-        ext = self._ext
+        ext = self._ext[self.last.get("slot", 0)]
         if self.comm.world > 1:
             # unsigned key order == signed order after flipping the top bit: MAX over ranks
             flip = torch.tensor(-(1 << 63), dtype=torch.int64, device=self.dev)

@@ -13,8 +13,10 @@ built). One step = all of it; its intersections are 2 passes x 4 mirrors x rays.
 pipelined the way a caller tracing many systems would run them: step k's pass 1 is queued ahead
 of step k-1's tilt / OPD / pupil / PSF (RayWave.launch_front / launch_back), which hides the
 host's resample, and that back half runs on a second stream, concurrently with the FP64-bound
-pass 1 (it is HBM-bound); step k's pass 2 waits for it. Every step still does all of its work
-inside the timed region. Inputs (the two
+pass 1 (it is HBM-bound). By default (--fuse 1) step k-1's tilt runs inside step k's pass-1
+kernel, which hides its loads behind the chain's arithmetic, and only its OPD / pupil / PSF go to
+the back stream, where they fill the GPU during the host resample. Every step still does all of
+its work inside the timed region. Inputs (the two
 1-D angle tables) are resident on the device before timing. Multi-GPU: weak scaling, each rank
 owns ~1e7 rays (contiguous V-rows of a grid of round(sqrt(N * 1e7))^2 rays); the PSF runs on
 rank 0.
@@ -60,6 +62,10 @@ def parse():
                         "next step's FP64-bound pass 1 (0: behind it on one stream)")
     p.add_argument("--back-priority", type=int, default=0,
                    help="torch stream priority of the back stream (lower = higher priority; 0 = normal)")
+    p.add_argument("--fuse", type=int, default=1,
+                   help="1: each step's tilt runs inside the next step's pass-1 kernel (its loads hidden behind "
+                        "the chain's FP64 arithmetic), its OPD / pupil / PSF on the back stream during the host "
+                        "resample; 0: the tilt as its own kernel on the back stream beside pass 1")
     p.add_argument("--psf-start", choices=("pupil", "pass1"), default="pupil",
                    help="side-stream PSF starts as soon as the previous pupil is ready, beside pass 1 "
                         "(default; measured faster), or after this step's pass 1")
@@ -176,10 +182,10 @@ def main():
             done.record(side)
         state["psf_done"] = done
 
-    def back(timed):
-        """Tilt, OPD and pupil of the oldest front (on the back stream, beside the next pass 1),
-        then its PSF."""
-        f = fronts.pop(0)
+    def back(timed, f=None):
+        """Tilt (unless already fused into the next pass 1), OPD and pupil of the oldest front (on
+        the back stream, beside the next pass 1 / during the resample), then its PSF."""
+        f = f if f is not None else fronts.pop(0)
         bs = back_stream if args.back_stream else torch.cuda.current_stream()
         with torch.cuda.stream(bs):
             rw.launch_back(f, stream=bs if args.back_stream else None)
@@ -193,10 +199,15 @@ def main():
         run_psf(opd, pitch, ready, timed)
 
     def step(timed):
-        # pipelined: this step's pass 1 is queued first, the previous step's tilt / OPD / pupil /
-        # PSF right behind it, so the GPU works through them while the host does the resample;
-        # each step still traces, tilts, reduces and transforms one full grid
-        fronts.append(rw.launch_front(overlap=(lambda: back(timed)) if fronts else None))
+        # pipelined: this step's pass 1 is queued first (with --fuse, carrying the previous step's
+        # tilt), the previous step's OPD / pupil / PSF right behind it, so the GPU works through
+        # them while the host does the resample; each step still traces, tilts, reduces and
+        # transforms one full grid
+        if fronts and args.fuse:
+            prev = fronts.pop(0)
+            fronts.append(rw.launch_front(overlap=lambda: back(timed, prev), fuse=prev))
+        else:
+            fronts.append(rw.launch_front(overlap=(lambda: back(timed)) if fronts else None))
 
     for _ in range(args.warmup):
         step(False)

@@ -189,8 +189,9 @@ int akb_tilt_opd_f64(const double ry[9], const double rz[9], const double center
  *   [2..10] R_y, [11..19] R_z (row-major) of rotation_matrices(-theta_y, -theta_z), formed with
  *           correctly rounded cos / sin (glibc's differ from those on ~0.13 % of arguments)
  *   [20..22] focus_apprx = mean(det) (np.mean)
- * and zeroes d_extent_keys[4] (optional) and d_clear[0..n_clear) (e.g. trace flag words already
- * copied out in stream order) for the next step. */
+ *   [23..24] the first four int32 words of d_clear as they were (zero-padded)
+ * and zeroes d_extent_keys[4] (optional) and d_clear[0..n_clear) (e.g. the trace flag words, read
+ * back from [23..24]) for the next step. d_params holds 25 doubles. */
 int akb_tilt_params_f64(const double* d_sum5, const int64_t* d_cnt5, double* d_params, uint64_t* d_extent_keys,
                         int32_t* d_clear, int n_clear, void* stream);
 
@@ -199,6 +200,24 @@ int akb_tilt_opd_dev_f64(const double* d_params, const double det1_ghij[4], cons
                          const double* dir, const double* pt, const double* opl, int64_t ld, int64_t n,
                          double* dir_rot, double* pt_rot, double* det1, double* det2, double* total1,
                          double* total2, const akb_leaf_sink* sink, void* stream);
+
+/* The resample picks of a pass-1 descriptor alone: traces only the rays whose exit slopes the
+ * equal-angle resample reads (the middle-row range samp_h_begin..samp_h_end and grid column
+ * samp_v_col, ref AKB_raytrace_20250312.py:2849-2859) over the whole grid (row0 / n_rays ignored),
+ * writing samp_h / samp_v and ORing their flags. RayWave runs it ahead of the full pass 1 so the
+ * host resample overlaps the full trace (whose flags it checks after pass 2). */
+int akb_trace_chain_samples_f64(const akb_chain_desc* d, void* stream);
+
+/* Pass 1 of one run fused with the device-parameter tilt of the previous run (RayWave's pipelined
+ * mode): one launch traces the chain descriptor d (grid rays, no OPL, no sink: pass 1, ref
+ * AKB_raytrace_20250312.py:2805-2838) and applies akb_tilt_opd_dev_f64's tilt to the n rays of
+ * dir / pt / opl (the previous run's pass-2 outputs, ref :3583-3633) over the same shard. The
+ * tilt's loads overlap the chain's FP64 arithmetic inside each wave. Outputs and flags are those
+ * of the two calls; d->n_rays must equal n. */
+int akb_chain_tilt_f64(const akb_chain_desc* d, const double* d_params, const double det1_ghij[4],
+                       const double det2_ghij[4], const double* dir, const double* pt, const double* opl, int64_t ld,
+                       int64_t n, double* dir_rot, double* pt_rot, double* det1, double* det2, double* total1,
+                       double* total2, const akb_leaf_sink* sink, void* stream);
 
 /* Focus sweep rows (find_defocus, ref :9086-9170): for P detector planes x = -d_plane_j[p]
  * (coefficients g = 1, h = i = 0, j = d_plane_j[p], as coeffs_det[9] = -(s2f_middle + a)), the

@@ -1,10 +1,15 @@
-"""Print one bench step's kernel timeline from a rocprofv3 kernel trace (gpurun_out/prof)."""
+"""Print one bench step's kernel timeline from a rocprofv3 kernel trace (gpurun_out/prof).
+A step starts at a pass-1 launch (k_chain<true, false, ...> or the fused k_chain_tilt)."""
 import csv
 import sys
 
 path = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof/run_kernel_trace.csv"
 rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-idx = [i for i, r in enumerate(rows) if "k_chain<" in r["Kernel_Name"] and "sink" not in r["Kernel_Name"]]
+# the step's first kernel: the picks prepass (two short k_chain launches) or, without it, pass 1
+big = lambda r: int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) > 50_000
+idx = [i for i, r in enumerate(rows)
+       if "k_chain<true, false" in r["Kernel_Name"] and "sink" not in r["Kernel_Name"]
+       and not (i > 0 and "k_chain<true, false" in rows[i - 1]["Kernel_Name"] and not big(rows[i - 1]))]
 i0, i1 = idx[-3], idx[-2]
 t0 = int(rows[i0]["Start_Timestamp"])
 prev = None

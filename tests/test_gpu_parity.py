@@ -291,13 +291,14 @@ def test_tilt_params_on_device(gpu):
         sums[2:] = rng.standard_normal(3) * 100.0 * cnt[2:]
         s_d = torch.from_numpy(sums).to(gpu)
         c_d = torch.from_numpy(cnt).to(gpu)
-        params = torch.empty(23, dtype=torch.float64, device=gpu)
+        params = torch.empty(25, dtype=torch.float64, device=gpu)
         keys = torch.full((4,), 7, dtype=torch.int64, device=gpu)
-        flags = torch.ones(2, dtype=torch.int32, device=gpu)
+        flags = torch.tensor([trial, 5, -1], dtype=torch.int32, device=gpu)
         _lib.check(L.akb_tilt_params_f64(D.ptr(s_d), D.ptr(c_d), D.ptr(params), D.ptr(keys), D.ptr(flags), 2,
                                          D.stream_handle()))
         p = params.cpu().numpy()
-        assert keys.cpu().numpy().tolist() == [0, 0, 0, 0] and flags.cpu().numpy().tolist() == [0, 0]
+        assert keys.cpu().numpy().tolist() == [0, 0, 0, 0] and flags.cpu().numpy().tolist() == [0, 0, -1]
+        assert params[23:25].cpu().view(torch.int32).tolist() == [trial, 5, 0, 0]  # kept before the clear
         mean = sums / cnt
         theta_y, theta_z = -mean[1], mean[0]
         assert p[0] == theta_y and p[1] == theta_z
@@ -362,6 +363,37 @@ def test_two_stream_pipeline_equals_sequential_runs(gpu, n):
     back(fronts[-1])
     torch.cuda.synchronize()
     assert len(outs) == 4
+    for o, opd in zip(outs, opds):
+        for k, v in want.items():
+            assert torch.equal(o[k], v), k
+        assert torch.equal(opd, want_opd)
+
+
+@pytest.mark.parametrize("n", [65, 1001])
+def test_fused_pipeline_equals_sequential_runs(gpu, n):
+    """bench.py's default pipeline: each run's tilt inside the next run's pass-1 kernel
+    (akb_chain_tilt_f64), its OPD and pupil on a second stream during the next resample - the
+    same bits as run() one at a time."""
+    from akbraytracing_amd.wavefront import RayWave
+    rw = RayWave(_geom(), n)
+    seq = rw.run()
+    want = {k: seq[k].clone() for k in ("wave2", "dist_err2", "detcenter2")}
+    want_opd = rw.pupil(32)[0].clone()
+    bs = torch.cuda.Stream()
+    outs, opds, fused = [], [], []
+
+    def back(front):
+        fused.append(front.tilt is not None)
+        with torch.cuda.stream(bs):
+            outs.append(rw.launch_back(front, stream=bs))
+            opds.append(rw.pupil(32)[0].clone())
+
+    f = rw.launch_front()
+    for _ in range(3):
+        f = rw.launch_front(overlap=lambda p=f: back(p), fuse=f)
+    back(f)
+    torch.cuda.synchronize()
+    assert fused == [True, True, True, False]
     for o, opd in zip(outs, opds):
         for k, v in want.items():
             assert torch.equal(o[k], v), k
