@@ -400,6 +400,46 @@ def test_fused_pipeline_equals_sequential_runs(gpu, n):
         assert torch.equal(opd, want_opd)
 
 
+def test_ray_wave_pass1_miss_raises_after_pass2(gpu):
+    """A pass-1 miss outside the resample's pick rays (only the grid's corner rays miss a tiny
+    sphere) is found when the flag words come back after pass 2, and the run fails as the
+    reference's all-NaN rule makes it; a miss among the pick rays fails before pass 2."""
+    from akbraytracing_amd import _lib
+    from akbraytracing_amd.wavefront import RayWave, SystemGeometry
+    g = golden_json("akb_geometry.json")
+    x0, radius = 1.0, 2.5e-5  # corners (|angle| ~2.8e-5) miss, the middle row / column (<2.2e-5) hit
+    g = dict(g, mirrors=[{"coeffs": [1.0, 1.0, 1.0, 0.0, 0.0, 0.0, -2 * x0, 0.0, 0.0, x0 * x0 - radius ** 2],
+                          "negative": True}],
+             det1=[0.0] * 6 + [1.0, 0.0, 0.0, -0.5], det2=[0.0] * 6 + [1.0, 0.0, 0.0, -0.4])
+    rw = RayWave(SystemGeometry.from_dict(g), 65)
+    with pytest.raises(_lib.AKBError, match="pass 1"):
+        rw.run()
+    narrow = dict(g, mirrors=[dict(g["mirrors"][0], coeffs=g["mirrors"][0]["coeffs"][:9] + [x0 * x0 - 1e-5 ** 2])])
+    with pytest.raises(_lib.AKBError, match="pass 1"):
+        RayWave(SystemGeometry.from_dict(narrow), 65).run()
+
+
+def test_fused_pipeline_flagged_pass2_takes_staged_path(gpu):
+    """If a run's pass 2 turns out flagged after the next pass 1 already tilted it, launch_back
+    discards the fused tilt and redoes the run stage by stage (here the flag is forced on a clean
+    run, so the staged results must match the fused ones to the tilt stage's tolerance)."""
+    from akbraytracing_amd.wavefront import RayWave
+    rw = RayWave(_geom(), 65)
+    want = rw.run()
+    want = {k: want[k].clone() for k in ("wave2", "dist_err2")}
+    f = rw.launch_front()
+    nxt = rw.launch_front(fuse=f)
+    assert f.tilt is not None
+    rw._resolve(f)
+    f.flags = (0, 0x1)  # as if a ray of its pass 2 had missed
+    out = rw.launch_back(f)
+    torch.cuda.synchronize()
+    for k, v in want.items():
+        assert torch.max(torch.abs(out[k] - v)).item() <= 1e-4, k
+    rest = rw.launch_back(nxt)
+    assert torch.equal(rest["wave2"], want["wave2"])
+
+
 def test_config5_legendre_opl_perturbation(gpu):
     """BASELINE config 5: the chain adds the Legendre figure-error model to each ray's OPL (model
     from oracle/legendre.py; the basis is pinned to legendre_fit by test_oracle_golden)."""
