@@ -215,7 +215,9 @@ class RayWave:
         # arctans and plain mean for the detector (:3583-3590); tilt -> (det1 x, y, z, total1,
         # total2), all nanmean (:3626, :3633, :3674)
         self.sink2 = LeafSink(5, self.n_local, 0b00011, self.dev)
-        self.sink3 = LeafSink(5, self.n_local, 0b11111, self.dev)
+        # one tilt sink per run slot: run k's tilt (fused into run k+1's pass 1) fills one while
+        # run k-1's back half may still finish the other
+        self._sink3 = [LeafSink(5, self.n_local, 0b11111, self.dev) for _ in range(2)]
         # det2 extent keys (uint64 bits), two sets: run k's OPD / pupil read theirs while run k+1's
         # tilt-parameter kernel clears the other one
         self._ext = torch.zeros((2, 4), dtype=torch.int64, device=self.dev)
@@ -234,7 +236,8 @@ class RayWave:
         hb, he, col = self._plan
         self._nsamp = (he - hb) + self.n
         # the picks, then four int32 flag words [pass 1, pass 2, prepass, unused]: one copy
-        # brings the picks and the prepass's word, and the tilt-parameter kernel clears all four
+        # brings the picks and the prepass's word; the tilt-parameter kernel keeps and clears the
+        # first two, the prepass's is zeroed on its own stream ahead of each prepass
         self._x1 = torch.zeros(self._nsamp + 2, dtype=D.F64, device=self.dev)
         words = self._x1[self._nsamp:].view(torch.int32)
         self._flags, self._sflag, self._words = words[0:2], words[2:3], words
@@ -254,9 +257,11 @@ class RayWave:
         # event after the last queued reader of the pass-2 buffers / extent keys (a back half
         # and its pupil, possibly on another stream): the next pass 2 waits for it
         self._back_done = None
-        # small host<->device copies (picks, pass-2 tables, flag words) run on their own stream,
-        # beside the kernels instead of between them
-        self._copy = torch.cuda.Stream(device=self.dev)
+        # the picks prepass and the small host<->device copies (picks, pass-2 tables) run on their
+        # own stream, beside the trace kernels instead of between them; the flag words' copy on
+        # another (it waits for the run's tilt parameters, the prepass waits for nothing)
+        self._copy = torch.cuda.Stream(device=self.dev)  # (a high-priority copy stream measured 10 % slower)
+        self._flag_copy = torch.cuda.Stream(device=self.dev)
 
     def _pass2_launch(self, want_rows, slot=0):
         key = (bool(want_rows), slot)
@@ -279,12 +284,10 @@ class RayWave:
         so the resample it does next overlaps the full trace. Returns the picks and the prepass's
         flags (the full pass 1's are checked after pass 2)."""
         hb, he, col = self._plan
-        _lib.check(_lib.lib().akb_trace_chain_samples_f64(self._ps.desc, stream))
-        picked = torch.cuda.Event()
-        picked.record()
         x = self._x1_host
-        with torch.cuda.stream(self._copy):
-            self._copy.wait_event(picked)
+        with torch.cuda.stream(self._copy):  # the prepass reads only the constant grid tables
+            self._sflag.zero_()
+            _lib.check(_lib.lib().akb_trace_chain_samples_f64(self._ps.desc, D.stream_handle(self._copy)))
             x.copy_(self._x1, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(self._copy)
@@ -368,14 +371,14 @@ class RayWave:
             fuse = None
         # fused optimistically: should fuse's pass 2 turn out flagged, launch_back ignores the
         # fused tilt and takes the staged path (its tables live in fuse's own slot)
-        if fuse is not None and self._back_done is not None:
-            # the fused tilt refills the tilt sink the previous back half finishes and reads
-            torch.cuda.current_stream().wait_event(self._back_done)
+        prev_back = self._back_done if fuse is not None else None
+        if prev_back is not None:
             self._back_done = None
         samp_h, samp_v, sflags = self._pass1(overlap, stream, fuse=fuse)
         if sflags:
             torch.cuda.synchronize()
             self._words.zero_()
+            torch.cuda.synchronize()
             raise _lib.AKBError(self._pass1_error(sflags))
         th = self._tan2_host[slot].numpy()
         if self.resample_pass:
@@ -386,6 +389,13 @@ class RayWave:
             np.tan(self.rand_h, out=th[:self.n])
             np.tan(self.rand_v, out=th[self.n:])
         with torch.cuda.stream(self._copy):
+            if prev_back is not None:
+                # the back half queued before this run (two runs back: its tilt sums, OPD, pupil)
+                # ahead of this pass 2, through the tables' copy that pass 2 waits for anyway: this
+                # run's tilt-parameter kernel clears the extent keys of that run's slot, and the
+                # next fused pass 1 refills its tilt sink. Normally long done; the fused pass 1
+                # itself never waits for it.
+                self._copy.wait_event(prev_back)
             self._tan2[slot].copy_(self._tan2_host[slot], non_blocking=True)
             tables = torch.cuda.Event()
             tables.record(self._copy)
@@ -404,16 +414,16 @@ class RayWave:
             self.comm.allreduce_sums(cnts)
         params = torch.empty(25, dtype=D.F64, device=self.dev)  # this run's own block
         _lib.check(L.akb_tilt_params_f64(D.ptr(sums), D.ptr(cnts), D.ptr(params), D.ptr(self._ext[slot]),
-                                         D.ptr(self._words), 4, stream))
+                                         D.ptr(self._flags), 2, stream))
         done = torch.cuda.Event()
         done.record()
         # the flag words the parameter kernel kept (params[23:25]) to the host, beside the next run
-        with torch.cuda.stream(self._copy):
-            self._copy.wait_event(done)
+        with torch.cuda.stream(self._flag_copy):
+            self._flag_copy.wait_event(done)
             self._f_host[slot].copy_(params[23:24].view(torch.int32), non_blocking=True)
             ev2 = torch.cuda.Event()
-            ev2.record(self._copy)
-        params.record_stream(self._copy)
+            ev2.record(self._flag_copy)
+        params.record_stream(self._flag_copy)
         return _Front(r=r, tan_h2=tan_h2, tan_v2=tan_v2, params=params, full=full, stream=stream, flag_ev=ev2,
                       done=done, slot=slot)
 
@@ -442,7 +452,7 @@ class RayWave:
         _lib.check(L.akb_chain_tilt_f64(self._p1.desc, D.ptr(f.params), D.host_f64(self.g.det1),
                                         D.host_f64(tb["d2"]), D.ptr(r.dir_out), D.ptr(r.last_hit), D.ptr(r.opl),
                                         n, n, None, None, D.ptr(tb["det1"]), D.ptr(tb["det2_buf"]),
-                                        D.ptr(tb["total1"]), D.ptr(tb["total2"]), self.sink3.desc, stream))
+                                        D.ptr(tb["total1"]), D.ptr(tb["total2"]), self._sink3[f.slot].desc, stream))
         ev = torch.cuda.Event()
         ev.record()
         f.tilt, f.tilted = tb, ev
@@ -527,7 +537,8 @@ class RayWave:
         sh = D.stream_handle(stream)
         tb = self._tilt_buffers(keep_rotated, full)
         outs = (D.ptr(dir_out), D.ptr(last_hit), D.ptr(opl), n, n, D.ptr(tb["dir_rot"]), D.ptr(tb["pt_rot"]),
-                D.ptr(tb["det1"]), D.ptr(tb["det2_buf"]), D.ptr(tb["total1"]), D.ptr(tb["total2"]), self.sink3.desc,
+                D.ptr(tb["det1"]), D.ptr(tb["det2_buf"]), D.ptr(tb["total1"]), D.ptr(tb["total2"]),
+                self._sink3[slot].desc,
                 sh)
         if host_tilt is None:
             _lib.check(L.akb_tilt_opd_dev_f64(D.ptr(params), D.host_f64(self.g.det1), D.host_f64(tb["d2"]), *outs))
@@ -542,7 +553,7 @@ class RayWave:
         L = _lib.lib()
         n, dev = self.n_local, self.dev
         sh = D.stream_handle(stream)
-        sums, cnts = self.sink3.finish(sh)
+        sums, cnts = self._sink3[slot].finish(sh)
         if self.comm.world > 1:
             self.comm.allreduce_sums(sums)
             self.comm.allreduce_sums(cnts)

@@ -5,11 +5,11 @@ import sys
 
 path = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof/run_kernel_trace.csv"
 rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-# the step's first kernel: the picks prepass (two short k_chain launches) or, without it, pass 1
+# a step starts at its pass-1 kernel: the fused pass 1 + tilt, or (unfused) the long k_chain pass 1
 big = lambda r: int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) > 50_000
 idx = [i for i, r in enumerate(rows)
-       if "k_chain<true, false" in r["Kernel_Name"] and "sink" not in r["Kernel_Name"]
-       and not (i > 0 and "k_chain<true, false" in rows[i - 1]["Kernel_Name"] and not big(rows[i - 1]))]
+       if "k_chain_tilt" in r["Kernel_Name"]
+       or ("k_chain<true, false" in r["Kernel_Name"] and "sink" not in r["Kernel_Name"] and big(r))]
 i0, i1 = idx[-3], idx[-2]
 t0 = int(rows[i0]["Start_Timestamp"])
 prev = None
