@@ -367,7 +367,9 @@ class RayWave:
         stream = D.stream_handle()
         slot = self._runs % 2
         self._runs += 1
-        if fuse is not None and fuse.tilt is not None:
+        if fuse is not None and (fuse.tilt is not None or fuse.full or self.g.det2 is None):
+            # the fused kernel writes the detector-2 rows only: full runs and single-detector
+            # systems (KB) keep the tilt in their own back half
             fuse = None
         # fused optimistically: should fuse's pass 2 turn out flagged, launch_back ignores the
         # fused tilt and takes the staged path (its tables live in fuse's own slot)

@@ -400,6 +400,25 @@ def test_fused_pipeline_equals_sequential_runs(gpu, n):
         assert torch.equal(opd, want_opd)
 
 
+def test_fused_pipeline_falls_back_where_it_cannot_fuse(gpu):
+    """launch_front(fuse=...) on a single-detector system (KB) or a full run keeps the tilt in
+    the back half and still gives run()'s bits."""
+    from akbraytracing_amd.wavefront import RayWave, SystemGeometry
+    rw = RayWave(SystemGeometry.from_dict(golden_json("kb_geometry.json")), 65)
+    want = rw.run()["dist_err"].clone()
+    f = rw.launch_front()
+    g = rw.launch_front(fuse=f)
+    assert f.tilt is None
+    assert torch.equal(rw.launch_back(f)["dist_err"], want)
+    assert torch.equal(rw.launch_back(g)["dist_err"], want)
+    rw = RayWave(_geom(), 65)
+    want = rw.run(full=True)["sph"].clone()
+    f = rw.launch_front(full=True)
+    g = rw.launch_front(fuse=f)
+    assert f.tilt is None
+    assert torch.equal(rw.launch_back(f)["sph"], want)
+
+
 def test_ray_wave_pass1_miss_raises_after_pass2(gpu):
     """A pass-1 miss outside the resample's pick rays (only the grid's corner rays miss a tiny
     sphere) is found when the flag words come back after pass 2, and the run fails as the
