@@ -19,7 +19,7 @@ c_int = ctypes.c_int
 c_dbl = ctypes.c_double
 c_vp = ctypes.c_void_p
 MAX_MIRRORS = 7
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 FLAG_MISS = 0x1
 FLAG_ZERO_NORMAL = 0x2
@@ -79,6 +79,7 @@ class ChainDesc(ctypes.Structure):
         ("flags", c_vp),
         ("sink", LeafSink),
         ("pert_h", c_vp), ("pert_v", c_vp), ("pert_terms", c_i32),
+        ("copy_src", c_vp), ("copy_dst", c_vp), ("copy_n", c_i64),
     ]
 
 

@@ -411,7 +411,30 @@ struct ChainArgs {
     const double* pert_h;  // (terms, n_h) / (terms, n_v) OPL perturbation tables or NULL
     const double* pert_v;
     int pert_terms;
+    const double* cp_src;  // staging copy done by workgroup 0 (akb_chain_desc.copy_*)
+    double* cp_dst;
+    int64_t cp_n;
 };
+
+// the launch's staging copy (akb_chain_desc.copy_*), by workgroup 0 ahead of its rays: sixteen
+// loads in flight per thread (the source may be host memory across PCIe)
+__device__ __forceinline__ void stage_copy(const ChainArgs& a) {
+    if (a.cp_n <= 0 || blockIdx.x != 0) return;
+    constexpr int kB = 16;
+    for (int64_t i0 = threadIdx.x; i0 < a.cp_n; i0 += (int64_t)blockDim.x * kB) {
+        double v[kB];
+#pragma unroll
+        for (int k = 0; k < kB; ++k) {
+            const int64_t i = i0 + (int64_t)k * blockDim.x;
+            v[k] = i < a.cp_n ? __builtin_nontemporal_load(a.cp_src + i) : 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < kB; ++k) {
+            const int64_t i = i0 + (int64_t)k * blockDim.x;
+            if (i < a.cp_n) a.cp_dst[i] = v[k];
+        }
+    }
+}
 
 // row / column of flat grid index g without a 64-bit division: q = (t + ((g - t) >> 1)) >> (s - 1)
 // with t = mulhi(g, m'), exact for every 32-bit g (Granlund & Montgomery 1994, fig. 4.1)
@@ -667,6 +690,7 @@ __device__ __forceinline__ void chain_ray(const ChainArgs& a, int64_t i0, int t,
 
 template <bool kGrid, bool kOPL, int kWaves, bool kHits = false, bool kPointSrc = false>
 __global__ void __launch_bounds__(kBlock, kWaves) k_chain(ChainArgs a) {
+    stage_copy(a);
     int fl = 0;
     double qv[5];
     const int t = threadIdx.x;
@@ -680,6 +704,7 @@ __global__ void __launch_bounds__(kBlock, kWaves) k_chain(ChainArgs a) {
 // kPointSrc: grid rays from the point source (no origin loads)
 template <bool kGrid, bool kOPL, int kWaves, bool kPointSrc = false>
 __global__ void __launch_bounds__(kBlock, kWaves) k_chain_sink(ChainArgs a) {
+    stage_copy(a);
     __shared__ LeafLds<5> L;
     int fl = 0;
     const int t = threadIdx.x;
@@ -879,6 +904,7 @@ __global__ void __launch_bounds__(kBlock) k_tilt_opd_sink(TiltArgs a) {
 // arithmetic instead of competing with it for wave slots as a second kernel would.
 template <int kWaves>
 __global__ void __launch_bounds__(kBlock, kWaves) k_chain_tilt(ChainArgs a, TiltArgs b) {
+    stage_copy(a);
     tilt_load_params(b);
     __shared__ LeafLds<5> L;
     int fl = 0;
@@ -1290,6 +1316,10 @@ static int chain_args_from(const akb_chain_desc* d, ChainArgs& a, bool& empty) {
     a.pert_h = d->pert_h;
     a.pert_v = d->pert_v;
     a.pert_terms = d->pert_h ? d->pert_terms : 0;
+    AKB_REQUIRE(d->copy_n >= 0 && (d->copy_n == 0 || (d->copy_src && d->copy_dst)), "bad staging copy");
+    a.cp_src = d->copy_src;
+    a.cp_dst = d->copy_dst;
+    a.cp_n = d->copy_n;
     return AKB_OK;
 }
 
@@ -1475,6 +1505,7 @@ int akb_trace_chain_samples_f64(const akb_chain_desc* d, void* stream) {
         AKB_REQUIRE(d->samp_h_begin >= 0 && d->samp_h_end <= d->n_h * d->n_v, "pick range outside the grid");
     // only the picks and the flags leave these rays
     a.hits = a.last_hit = a.dir_out = a.det_out = a.opl = a.atan_h = a.atan_v = nullptr;
+    a.cp_n = 0;
     a.pert_h = a.pert_v = nullptr;
     hipStream_t s = (hipStream_t)stream;
     if (has_h) {  // the middle-row range: contiguous flat indices

@@ -241,7 +241,9 @@ class RayWave:
         self._x1 = torch.zeros(self._nsamp + 2, dtype=D.F64, device=self.dev)
         words = self._x1[self._nsamp:].view(torch.int32)
         self._flags, self._sflag, self._words = words[0:2], words[2:3], words
-        self._x1_host = torch.empty(self._nsamp + 2, dtype=D.F64, pin_memory=True)
+        self._x1_host = torch.empty((2, self._nsamp + 2), dtype=D.F64, pin_memory=True)
+        self._pick_buf = 0
+        self._next_picks = None  # (event, host buffer) of a prepass queued for the next run
         # per run slot (a run's front returns before its pass 2 ends, so the next run must not
         # reuse them): the [pass 1, pass 2] flag words on the host and the pass-2 tables [h | v]
         self._f_host = torch.zeros((2, 2), dtype=torch.int32, pin_memory=True)
@@ -278,33 +280,43 @@ class RayWave:
         return self._p2[key]
 
     # -------------------------------------------------------------- passes
-    def _pass1(self, overlap=None, stream=None, fuse=None):
-        """The picks prepass and its copy to the host, then the full pass 1 (fused with fuse's
-        tilt when given) and `overlap`'s work queued behind it; the host waits for the picks only,
-        so the resample it does next overlaps the full trace. Returns the picks and the prepass's
-        flags (the full pass 1's are checked after pass 2)."""
-        hb, he, col = self._plan
-        x = self._x1_host
-        with torch.cuda.stream(self._copy):  # the prepass reads only the constant grid tables
+    def _queue_picks(self):
+        """The picks prepass of the next run and its copy to the host, on the copy stream (it
+        reads only the constant grid tables, so it runs one run ahead, beside this run's
+        kernels); its host buffer alternates between runs."""
+        x = self._x1_host[self._pick_buf]
+        self._pick_buf ^= 1
+        with torch.cuda.stream(self._copy):
             self._sflag.zero_()
             _lib.check(_lib.lib().akb_trace_chain_samples_f64(self._ps.desc, D.stream_handle(self._copy)))
             x.copy_(self._x1, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(self._copy)
-        if fuse is None:
-            self._p1.launch(stream=stream, reset_flags=False)
-        else:
-            self._fused_pass1(fuse, stream)
+        self._next_picks = (ev, x)
+
+    def _take_picks(self):
+        """This run's picks and the prepass's flag word (waits for the prepass if still running)."""
+        if self._next_picks is None:
+            self._queue_picks()
+        ev, x = self._next_picks
+        self._next_picks = None
         ev.synchronize()
-        if overlap is not None:
-            # independent device work (the previous run's back half) queued behind pass 1, so it
-            # runs beside this run's pass 2; queued after the wait, when everything the previous
-            # run put on this stream - its pass-2 flag words included - has completed
-            overlap()
+        hb, he, _ = self._plan
         host = x.numpy()
         nh = he - hb
         flags = int(host[self._nsamp:].view(np.int32)[0])
         return host[:nh].copy(), host[nh:self._nsamp].copy(), flags
+
+    def _pass1(self, stream, fuse, slot):
+        """The full pass 1 (fused with fuse's tilt when given). Its workgroup 0 also stages this
+        run's resampled tables from pinned host memory to the device (akb_chain_desc.copy_*), so
+        pass 2 follows it with no copy or cross-stream wait in between."""
+        d = self._p1.desc
+        d.copy_src, d.copy_dst, d.copy_n = D.ptr(self._tan2_host[slot]), D.ptr(self._tan2[slot]), 2 * self.n
+        if fuse is None:
+            self._p1.launch(stream=stream, reset_flags=False)
+        else:
+            self._fused_pass1(fuse, stream)
 
     def _pass2(self, want_rows=False, stream=None, slot=0):
         ev = None
@@ -357,12 +369,17 @@ class RayWave:
         only), pass 2, its sums and the device tilt parameters. Returns as soon as all of it is
         queued; the trace flags are read when launch_back (or _resolve) needs them.
 
+        The picks come from a prepass queued one run ahead (on the copy stream, beside the
+        previous run's kernels); the host resamples, queues the next run's prepass, and pass 1
+        stages the new tables for pass 2 itself: the trace kernels follow each other on the stream
+        with nothing in between.
+
         fuse: the previous run's front, not yet handed to launch_back: its tilt then runs inside
         this run's pass-1 kernel (akb_chain_tilt_f64), its loads hidden behind the chain's
         arithmetic, and its launch_back only finishes the tilt sums and forms the OPD (queue that
-        in `overlap`, called right after the host wait for the picks, so it runs beside this
-        run's pass 2). A fused OPD inside pass 2 measured slower (1.005 vs 0.974 ms per bench
-        step): its loads and registers cost the FP64-bound chain more than running beside it."""
+        in `overlap`, called once pass 1 is queued, so it runs beside this run's pass 2). A fused
+        OPD inside pass 2 measured slower (1.005 vs 0.974 ms per bench step): its loads and
+        registers cost the FP64-bound chain more than running beside it."""
         L = _lib.lib()
         stream = D.stream_handle()
         slot = self._runs % 2
@@ -373,10 +390,7 @@ class RayWave:
             fuse = None
         # fused optimistically: should fuse's pass 2 turn out flagged, launch_back ignores the
         # fused tilt and takes the staged path (its tables live in fuse's own slot)
-        prev_back = self._back_done if fuse is not None else None
-        if prev_back is not None:
-            self._back_done = None
-        samp_h, samp_v, sflags = self._pass1(overlap, stream, fuse=fuse)
+        samp_h, samp_v, sflags = self._take_picks()
         if sflags:
             torch.cuda.synchronize()
             self._words.zero_()
@@ -390,18 +404,17 @@ class RayWave:
         else:
             np.tan(self.rand_h, out=th[:self.n])
             np.tan(self.rand_v, out=th[self.n:])
-        with torch.cuda.stream(self._copy):
-            if prev_back is not None:
-                # the back half queued before this run (two runs back: its tilt sums, OPD, pupil)
-                # ahead of this pass 2, through the tables' copy that pass 2 waits for anyway: this
-                # run's tilt-parameter kernel clears the extent keys of that run's slot, and the
-                # next fused pass 1 refills its tilt sink. Normally long done; the fused pass 1
-                # itself never waits for it.
-                self._copy.wait_event(prev_back)
-            self._tan2[slot].copy_(self._tan2_host[slot], non_blocking=True)
-            tables = torch.cuda.Event()
-            tables.record(self._copy)
-        torch.cuda.current_stream().wait_event(tables)
+        self._queue_picks()
+        if fuse is not None and self._back_done is not None:
+            # the back half queued before (its tilt sums, OPD, pupil; two runs back by the time the
+            # tilt-parameter kernel below clears that run's extent keys and the next fused pass 1
+            # refills its tilt sink): normally long done, and then no wait enters the stream
+            if not self._back_done.query():
+                torch.cuda.current_stream().wait_event(self._back_done)
+            self._back_done = None
+        self._pass1(stream, fuse, slot)
+        if overlap is not None:
+            overlap()  # e.g. the previous run's back half, beside this run's pass 2
         tan_h2, tan_v2 = self._tan2[slot, :self.n], self._tan2[slot, self.n:]
         if self._back_done is not None and fuse is None:
             # pass 2 rewrites the buffers a queued (unfused) back half's tilt reads

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define AKB_ABI_VERSION 4
+#define AKB_ABI_VERSION 5
 
 /* status codes */
 #define AKB_OK 0
@@ -164,6 +164,11 @@ typedef struct akb_chain_desc {
      * Legendre basis; grid rays only, needs opl): opl += sum_t pert_v[t][iv] * pert_h[t][ih] for
      * t < pert_terms (<= 8), tables (pert_terms, n_v) and (pert_terms, n_h), row-major */
     const double* pert_h; const double* pert_v; int32_t pert_terms;
+    /* optional staging copy done by the launch itself (not part of the trace): copy_n doubles from
+     * copy_src (e.g. pinned host memory the caller filled before the launch) to copy_dst (device
+     * memory a later launch on the stream reads) - RayWave hands the next pass 2 its resampled
+     * tables this way, with no copy packet between the two trace kernels */
+    const double* copy_src; double* copy_dst; int64_t copy_n;
 } akb_chain_desc;
 
 int akb_trace_chain_f64(const akb_chain_desc* desc, void* stream);
