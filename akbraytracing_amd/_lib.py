@@ -19,7 +19,7 @@ c_int = ctypes.c_int
 c_dbl = ctypes.c_double
 c_vp = ctypes.c_void_p
 MAX_MIRRORS = 7
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 FLAG_MISS = 0x1
 FLAG_ZERO_NORMAL = 0x2
@@ -33,7 +33,7 @@ EXPORTS = [
     "akb_isect_f64", "akb_normal_f64", "akb_reflect_f64", "akb_normalize_f64", "akb_plane_isect_f64",
     "akb_seglen_f64", "akb_rotate_f64", "akb_fill_nan_f64",
     "akb_trace_chain_f64", "akb_chain_desc_size", "akb_tilt_opd_f64", "akb_tilt_params_f64",
-    "akb_tilt_opd_dev_f64", "akb_chain_tilt_f64", "akb_trace_chain_samples_f64", "akb_opd_f64", "akb_resample_f64", "akb_plane_sweep_rows_f64",
+    "akb_tilt_opd_dev_f64", "akb_chain_tilt_f64", "akb_chain_tilt_opd_f64", "akb_trace_chain_samples_f64", "akb_opd_f64", "akb_resample_f64", "akb_plane_sweep_rows_f64",
     "akb_plane_sweep_sink_f64",
     "akb_calc_ds_f64",
     "akb_pairwise_work_bytes", "akb_pairwise_sum_f64", "akb_pupil_sample_f64",
@@ -111,6 +111,8 @@ def _declare(L):
         "akb_trace_chain_samples_f64": ([ctypes.POINTER(ChainDesc), c_vp], c_int),
         "akb_chain_tilt_f64": ([ctypes.POINTER(ChainDesc), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64]
                                + [c_vp] * 6 + [ctypes.POINTER(LeafSink), c_vp], c_int),
+        "akb_chain_tilt_opd_f64": ([ctypes.POINTER(ChainDesc), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
+                                    c_vp, c_vp, ctypes.POINTER(LeafSink)] + [c_vp] * 8, c_int),
         "akb_opd_f64": ([c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp],
                         c_int),
         "akb_resample_f64": ([c_vp, c_vp, c_i64, c_vp], c_int),

@@ -286,8 +286,7 @@ struct LeafLds {
 
 template <int NQ>
 __device__ __forceinline__ void leaf_sink_segment(const akb_leaf_sink& S, LeafLds<NQ>& L, int64_t seg0,
-                                                  const double (&v)[NQ], bool valid) {
-    const int tid = threadIdx.x;
+                                                  const double (&v)[NQ], bool valid, int tid) {
     const int64_t full = (S.n / kNpBuf) * kNpBuf;
     if (seg0 >= full) {  // block-uniform: the short last buffer keeps raw values
         if (valid) {
@@ -340,6 +339,11 @@ __device__ __forceinline__ void leaf_sink_segment(const akb_leaf_sink& S, LeafLd
         }
     }
     __syncthreads();
+}
+template <int NQ>
+__device__ __forceinline__ void leaf_sink_segment(const akb_leaf_sink& S, LeafLds<NQ>& L, int64_t seg0,
+                                                  const double (&v)[NQ], bool valid) {
+    leaf_sink_segment<NQ>(S, L, seg0, v, valid, (int)threadIdx.x);
 }
 
 }  // namespace akb

@@ -897,59 +897,6 @@ __global__ void __launch_bounds__(kBlock) k_tilt_opd_sink(TiltArgs a) {
     }
 }
 
-// Pass 1 of one run fused with the tilt of the run before it (RayWave.launch_front(fuse=...)):
-// both walk the same shard in 256-ray segments. Each segment's tilt inputs (56 B per ray, written
-// by the previous run's pass 2) are loaded right after the ray's grid-table loads and arrive
-// while the FP64-bound mirror chain runs, so the tilt's HBM traffic hides behind pass 1's
-// arithmetic instead of competing with it for wave slots as a second kernel would.
-template <int kWaves>
-__global__ void __launch_bounds__(kBlock, kWaves) k_chain_tilt(ChainArgs a, TiltArgs b) {
-    stage_copy(a);
-    tilt_load_params(b);
-    __shared__ LeafLds<5> L;
-    int fl = 0;
-    double qv[5];
-    const int t = threadIdx.x;
-    const int64_t nseg = (a.n + kLeafSeg - 1) / kLeafSeg;
-    int64_t seg = blockIdx.x;
-    // software pipeline: segment s's table entries and tilt inputs were loaded during segment
-    // s - gridDim's stores, leaf sums and mirror loop
-    int64_t iv = 0, ih = 0;
-    double th = 0.0, tv = 0.0;
-    TiltIn in;
-    if (seg < nseg && seg * kLeafSeg + t < a.n) {
-        ray_tables(a, seg * kLeafSeg + t, iv, ih, th, tv);
-        tilt_load_all(b, seg * kLeafSeg + t, in);
-    }
-    for (; seg < nseg; seg += gridDim.x) {
-        const int64_t i0 = seg * kLeafSeg;
-        const bool valid = i0 + t < a.n;
-        const int64_t nxt = (seg + gridDim.x) * kLeafSeg + t;
-        double d2[3], tq[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-        if (valid)
-            chain_ray_tab<true, false, false, false, true, true>(a, i0, t, iv, ih, th, tv, fl, qv, [&] {
-                tilt_compute(b, in, d2, tq);
-                if (nxt < a.n) {
-                    ray_tables(a, nxt, iv, ih, th, tv);
-                    tilt_load_all(b, nxt, in);
-                }
-            });
-        if (valid) {  // detector-2 rows only (detector 1 and the rotated rays are the full mode's)
-            double* o = b.det2 + i0;
-            o[t] = d2[0];
-            (o + b.ld)[t] = d2[1];
-            (o + 2 * b.ld)[t] = d2[2];
-            (b.total2 + i0)[t] = tq[4];
-        }
-        leaf_sink_segment<5>(b.sink, L, i0, tq, valid);
-    }
-    if (fl) atomicOr(a.flags, fl);
-}
-
-// ----------------------------------------------------------------------------------------------
-// OPD maps + pupil footprint (ref :3626, :3633, :3675-3677)
-// ----------------------------------------------------------------------------------------------
-
 // order-preserving uint64 key of a double (larger double -> larger key); 0 is below every key
 __device__ __forceinline__ unsigned long long order_key(double v) {
     const unsigned long long b = (unsigned long long)__double_as_longlong(v);
@@ -974,8 +921,139 @@ struct OpdArgs {
     unsigned long long* ext;
 };
 
-__global__ void __launch_bounds__(kBlock) k_opd(OpdArgs a) {
+// the fused kernel's OPD rows (akb_chain_tilt_opd_f64; ld / n are the tilt's)
+struct OpdRows {
+    const double* t2;
+    const double* det2;
+    double* e2;
+    double* wave;
+    unsigned long long* ext;
+    const double* sum5;
+    const int64_t* cnt5;
+};
+
+// one ray's OPD inputs (ref :3633, :3675-3677): total2 and the detector-2 point
+struct OpdIn {
+    double t2, x, y, z;
+};
+__device__ __forceinline__ void opd_load(const OpdRows& o, int64_t ld, int64_t i, OpdIn& v) {
+    v.t2 = o.t2[i];
+    v.x = o.det2[i];
+    v.y = o.det2[ld + i];
+    v.z = o.det2[2 * ld + i];
+}
+
+// the workgroup's four extents (max y, -y, z, -z) folded into the device keys (thread-uniform
+// call: every thread of the workgroup reaches it)
+__device__ __forceinline__ void extents_commit(double (&e)[4], unsigned long long* ext) {
     __shared__ double wext[kBlock / 64][4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        for (int off = 32; off > 0; off >>= 1) e[k] = fmax(e[k], __shfl_down(e[k], off));
+    if ((threadIdx.x & 63) == 0)
+        for (int k = 0; k < 4; ++k) wext[threadIdx.x >> 6][k] = e[k];
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        double v = wext[0][threadIdx.x];
+        for (int w = 1; w < kBlock / 64; ++w) v = fmax(v, wext[w][threadIdx.x]);
+        const unsigned long long k = order_key(v);
+        // most workgroups hold no new extreme: skip their atomic (the max stays exact)
+        if (k > __hip_atomic_load(ext + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            atomicMax(ext + threadIdx.x, k);
+    }
+}
+
+// Pass 1 of one run fused with the tilt of the run before it (RayWave.launch_front(fuse=...)):
+// both walk the same shard in 256-ray segments. Each segment's tilt inputs (56 B per ray, written
+// by the previous run's pass 2) are loaded right after the ray's grid-table loads and arrive
+// while the FP64-bound mirror chain runs, so the tilt's HBM traffic hides behind pass 1's
+// arithmetic instead of competing with it for wave slots as a second kernel would.
+//
+// kOPD: the same kernel also forms the OPD maps of the run before that one (o: its tilt outputs
+// and tilt sums, RayWave.launch_front(fuse_opd=...)), 48 B per ray more behind the same chain:
+// Wave2 = DistError2 - Sph, and the detector-2 extents for the pupil pitch.
+template <int kWaves, bool kOPD>
+__global__ void __launch_bounds__(kBlock, kWaves) k_chain_tilt(ChainArgs a, TiltArgs b, OpdRows o) {
+    stage_copy(a);
+    tilt_load_params(b);
+    // the OPD's means and each thread's running extents live in LDS, and its inputs are loaded
+    // for the current segment only (issued ahead of the tilt arithmetic, which hides part of their
+    // latency): nothing of the OPD is live across the mirror loop
+    __shared__ double om[kOPD ? 4 : 1];
+    __shared__ double oe[kOPD ? 4 : 1][kOPD ? kBlock : 1];
+    if constexpr (kOPD) {
+        if (threadIdx.x < 4) {  // np.nanmean results, as k_opd forms them: f0, f1, f2, mean2
+            const int q = threadIdx.x == 3 ? 4 : threadIdx.x;
+            om[threadIdx.x] = o.sum5[q] / (double)o.cnt5[q];
+        }
+        for (int k = 0; k < 4; ++k) oe[k][threadIdx.x] = -INFINITY;
+        __syncthreads();
+    }
+    __shared__ LeafLds<5> L;
+    int fl = 0;
+    double qv[5];
+    const int t = threadIdx.x;
+    const int64_t nseg = (a.n + kLeafSeg - 1) / kLeafSeg;
+    int64_t seg = blockIdx.x;
+    // software pipeline: segment s's table entries and tilt inputs were loaded during segment
+    // s - gridDim's stores, leaf sums and mirror loop
+    int64_t iv = 0, ih = 0;
+    double th = 0.0, tv = 0.0;
+    TiltIn in;
+    if (seg < nseg && seg * kLeafSeg + t < a.n) {
+        ray_tables(a, seg * kLeafSeg + t, iv, ih, th, tv);
+        tilt_load_all(b, seg * kLeafSeg + t, in);
+    }
+    for (; seg < nseg; seg += gridDim.x) {
+        // the thread index made opaque per segment: addresses derived from it are formed where
+        // they are used instead of being hoisted out of the loop and kept live (or spilled, and
+        // reloaded behind the prefetch loads) across the mirror chain
+        int t = threadIdx.x;
+        asm volatile("" : "+v"(t));
+        const int64_t i0 = seg * kLeafSeg;
+        const bool valid = i0 + t < a.n;
+        const int64_t nxt = (seg + gridDim.x) * kLeafSeg + t;
+        double d2[3], tq[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+        if (valid)
+            chain_ray_tab<true, false, false, false, true, true>(a, i0, t, iv, ih, th, tv, fl, qv, [&] {
+                OpdIn oin;
+                if constexpr (kOPD) opd_load(o, b.ld, i0 + t, oin);
+                tilt_compute(b, in, d2, tq);
+                if constexpr (kOPD) {  // k_opd's arithmetic, in its order
+                    const double oe2 = (oin.t2 - om[3]) * 1e9;
+                    (o.e2 + i0)[t] = oe2;
+                    (o.wave + i0)[t] = oe2 - norm3(oin.x - om[0], oin.y - om[1], oin.z - om[2]) * 1e9;
+                    oe[0][t] = fmax(oe[0][t], oin.y);
+                    oe[1][t] = fmax(oe[1][t], -oin.y);
+                    oe[2][t] = fmax(oe[2][t], oin.z);
+                    oe[3][t] = fmax(oe[3][t], -oin.z);
+                }
+                if (nxt < a.n) {
+                    ray_tables(a, nxt, iv, ih, th, tv);
+                    tilt_load_all(b, nxt, in);
+                }
+            });
+        if (valid) {  // detector-2 rows only (detector 1 and the rotated rays are the full mode's)
+            double* r = b.det2 + i0;
+            r[t] = d2[0];
+            (r + b.ld)[t] = d2[1];
+            (r + 2 * b.ld)[t] = d2[2];
+            (b.total2 + i0)[t] = tq[4];
+        }
+        leaf_sink_segment<5>(b.sink, L, i0, tq, valid, t);
+    }
+    if (fl) atomicOr(a.flags, fl);
+    if constexpr (kOPD) {
+        double e[4] = {oe[0][t], oe[1][t], oe[2][t], oe[3][t]};
+        extents_commit(e, o.ext);
+    }
+}
+
+// ----------------------------------------------------------------------------------------------
+// OPD maps + pupil footprint (ref :3626, :3633, :3675-3677)
+// ----------------------------------------------------------------------------------------------
+
+__global__ void __launch_bounds__(kBlock) k_opd(OpdArgs a) {
     // np.nanmean results: sum / count in float64 (the reference's true_divide)
     const double f0 = a.sum5[0] / (double)a.cnt5[0];
     const double f1 = a.sum5[1] / (double)a.cnt5[1];
@@ -1001,22 +1079,7 @@ __global__ void __launch_bounds__(kBlock) k_opd(OpdArgs a) {
             e[3] = fmax(e[3], -z);
         }
     }
-    if (a.ext) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            for (int off = 32; off > 0; off >>= 1) e[k] = fmax(e[k], __shfl_down(e[k], off));
-        if ((threadIdx.x & 63) == 0)
-            for (int k = 0; k < 4; ++k) wext[threadIdx.x >> 6][k] = e[k];
-        __syncthreads();
-        if (threadIdx.x < 4) {
-            double v = wext[0][threadIdx.x];
-            for (int w = 1; w < kBlock / 64; ++w) v = fmax(v, wext[w][threadIdx.x]);
-            const unsigned long long k = order_key(v);
-            // most workgroups hold no new extreme: skip their atomic (the max stays exact)
-            if (k > __hip_atomic_load(a.ext + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                atomicMax(a.ext + threadIdx.x, k);
-        }
-    }
+    if (a.ext) extents_commit(e, a.ext);
 }
 
 __global__ void __launch_bounds__(kBlock) k_pupil(const double* wave, int64_t row0, int64_t rows, int64_t n,
@@ -1530,11 +1593,10 @@ int akb_trace_chain_samples_f64(const akb_chain_desc* d, void* stream) {
     return AKB_OK;
 }
 
-int akb_chain_tilt_f64(const akb_chain_desc* d, const double* d_params, const double det1_ghij[4],
-                       const double det2_ghij[4], const double* dir, const double* pt, const double* opl, int64_t ld,
-                       int64_t n, double* dir_rot, double* pt_rot, double* det1, double* det2, double* total1,
-                       double* total2, const akb_leaf_sink* sink, void* stream) {
-    clear_error();
+static int chain_tilt(const akb_chain_desc* d, const double* d_params, const double det1_ghij[4],
+                      const double det2_ghij[4], const double* dir, const double* pt, const double* opl, int64_t ld,
+                      int64_t n, double* dir_rot, double* pt_rot, double* det1, double* det2, double* total1,
+                      double* total2, const akb_leaf_sink* sink, const OpdRows* o, void* stream) {
     AKB_REQUIRE(d && d_params && sink, "null pointer");
     ChainArgs a;
     bool empty;
@@ -1559,17 +1621,55 @@ int akb_chain_tilt_f64(const akb_chain_desc* d, const double* d_params, const do
     const int64_t gcap = chain_grid_cap();
     const unsigned gs = (unsigned)(nseg < gcap ? nseg : gcap);
     hipStream_t s = (hipStream_t)stream;
+    const OpdRows no{};
+#define AKB_CT(W)                                                  \
+    if (o)                                                         \
+        k_chain_tilt<W, true><<<gs, kBlock, 0, s>>>(a, b, *o);     \
+    else                                                           \
+        k_chain_tilt<W, false><<<gs, kBlock, 0, s>>>(a, b, no);
     switch (chain_waves()) {
         case 2:
-            k_chain_tilt<2><<<gs, kBlock, 0, s>>>(a, b);
+            AKB_CT(2)
             break;
         case 8:
-            k_chain_tilt<8><<<gs, kBlock, 0, s>>>(a, b);
+            AKB_CT(8)
             break;
         default:
-            k_chain_tilt<4><<<gs, kBlock, 0, s>>>(a, b);
+            AKB_CT(4)
     }
+#undef AKB_CT
     return launch_status("k_chain_tilt");
+}
+
+int akb_chain_tilt_f64(const akb_chain_desc* d, const double* d_params, const double det1_ghij[4],
+                       const double det2_ghij[4], const double* dir, const double* pt, const double* opl, int64_t ld,
+                       int64_t n, double* dir_rot, double* pt_rot, double* det1, double* det2, double* total1,
+                       double* total2, const akb_leaf_sink* sink, void* stream) {
+    clear_error();
+    return chain_tilt(d, d_params, det1_ghij, det2_ghij, dir, pt, opl, ld, n, dir_rot, pt_rot, det1, det2, total1,
+                      total2, sink, nullptr, stream);
+}
+
+int akb_chain_tilt_opd_f64(const akb_chain_desc* d, const double* d_params, const double det1_ghij[4],
+                           const double det2_ghij[4], const double* dir, const double* pt, const double* opl,
+                           int64_t ld, int64_t n, double* det2, double* total2, const akb_leaf_sink* sink,
+                           const double* opd_total2, const double* opd_det2, const double* d_sum5,
+                           const int64_t* d_cnt5, double* dist_err2, double* wave, uint64_t* d_extent_keys,
+                           void* stream) {
+    clear_error();
+    AKB_REQUIRE(opd_total2 && opd_det2 && d_sum5 && d_cnt5 && dist_err2 && wave && d_extent_keys,
+                "the fused OPD needs the earlier run's total2, det2 and tilt sums, and writes DistError2, "
+                "Wave2 and the extent keys");
+    OpdRows o{};
+    o.t2 = opd_total2;
+    o.det2 = opd_det2;
+    o.sum5 = d_sum5;
+    o.cnt5 = d_cnt5;
+    o.e2 = dist_err2;
+    o.wave = wave;
+    o.ext = (unsigned long long*)d_extent_keys;
+    return chain_tilt(d, d_params, det1_ghij, det2_ghij, dir, pt, opl, ld, n, nullptr, nullptr, nullptr, det2,
+                      nullptr, total2, sink, &o, stream);
 }
 
 int akb_opd_f64(const double* total1, const double* total2, const double* det2, int64_t ld, int64_t n,

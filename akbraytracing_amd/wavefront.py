@@ -183,9 +183,13 @@ class _Front:
     flags: tuple = None  # (pass 1, pass 2) trace flag words once known (RayWave._resolve)
     flag_ev: object = None  # event after the flag words' copy to the host
     done: object = None  # event on the front's stream after its last kernel (the tilt parameters)
-    slot: int = 0  # which of the two extent-key buffers this run's OPD / pupil use
+    slot: int = 0  # which of the per-run buffer sets (tables, extent keys, tilt sink) this run uses
     tilt: dict = None  # tilt outputs, when the next front's pass 1 already tilted this run (fused)
     tilted: object = None  # event after that fused kernel
+    fin: tuple = None  # (sums, counts) of the fused tilt's sink, finished on RayWave._fin
+    fin_ev: object = None  # event after that finish
+    opd: dict = None  # DistError2 / Wave2, when the front after next formed them in its pass 1
+    opd_ev: object = None  # event after that fused kernel
 
 
 class RayWave:
@@ -195,6 +199,8 @@ class RayWave:
     waits on the host once, for the resample picks of pass 1 (the resample itself is host work
     by design, see resample_axis); pass 2, the tilt parameters, the tilt and the OPD are queued
     back to back, and the run returns as soon as pass 2's flag word has reached the host."""
+
+    NSLOTS = 3  # runs in flight: k (front), k-1 (tilt fused into k), k-2 (OPD fused into k)
 
     def __init__(self, geometry, n, shard=None, comm=None, resample_pass=True, perturbation=None):
         """perturbation: optional legendre.LegendrePerturbation added to every ray's pass-2 optical
@@ -215,12 +221,13 @@ class RayWave:
         # arctans and plain mean for the detector (:3583-3590); tilt -> (det1 x, y, z, total1,
         # total2), all nanmean (:3626, :3633, :3674)
         self.sink2 = LeafSink(5, self.n_local, 0b00011, self.dev)
-        # one tilt sink per run slot: run k's tilt (fused into run k+1's pass 1) fills one while
-        # run k-1's back half may still finish the other
-        self._sink3 = [LeafSink(5, self.n_local, 0b11111, self.dev) for _ in range(2)]
-        # det2 extent keys (uint64 bits), two sets: run k's OPD / pupil read theirs while run k+1's
-        # tilt-parameter kernel clears the other one
-        self._ext = torch.zeros((2, 4), dtype=torch.int64, device=self.dev)
+        # per-run buffer sets ("slots", run k uses k % 3): run k's tilt is fused into run k+1's
+        # pass 1 and its OPD into run k+2's, so three runs are in flight at once. Each slot holds a
+        # tilt sink, the det2 extent keys (uint64 bits) its OPD folds and its pupil reads, the
+        # pass-2 tables and the flag words on the host
+        NS = self.NSLOTS
+        self._sink3 = [LeafSink(5, self.n_local, 0b11111, self.dev) for _ in range(NS)]
+        self._ext = torch.zeros((NS, 4), dtype=torch.int64, device=self.dev)
         self._runs = 0
         self._pitch = torch.zeros(2, dtype=D.F64, device=self.dev)
         self._opd_buf = None
@@ -246,9 +253,10 @@ class RayWave:
         self._next_picks = None  # (event, host buffer) of a prepass queued for the next run
         # per run slot (a run's front returns before its pass 2 ends, so the next run must not
         # reuse them): the [pass 1, pass 2] flag words on the host and the pass-2 tables [h | v]
-        self._f_host = torch.zeros((2, 2), dtype=torch.int32, pin_memory=True)
-        self._tan2 = torch.empty((2, 2 * self.n), dtype=D.F64, device=self.dev)
-        self._tan2_host = torch.empty((2, 2 * self.n), dtype=D.F64, pin_memory=True)
+        self._f_host = torch.zeros((NS, 2), dtype=torch.int32, pin_memory=True)
+        self._tan2 = torch.empty((NS, 2 * self.n), dtype=D.F64, device=self.dev)
+        self._tan2_host = torch.empty((NS, 2 * self.n), dtype=D.F64, pin_memory=True)
+        self._staged = [None] * NS  # event after the pass 1 that copied a slot's host tables
         self._ps = ChainLaunch(self.g.mirrors, tan_h=self.tan_h, tan_v=self.tan_v, row0=0, n_rays=self.n * self.n,
                                src=self.g.source, want=(), samples=(hb, he, col), flags=self._sflag,
                                samples_buf=self._x1[:self._nsamp])
@@ -264,14 +272,18 @@ class RayWave:
         # another (it waits for the run's tilt parameters, the prepass waits for nothing)
         self._copy = torch.cuda.Stream(device=self.dev)  # (a high-priority copy stream measured 10 % slower)
         self._flag_copy = torch.cuda.Stream(device=self.dev)
+        # a fused tilt's sums are finished here, beside the next pass 2 (the OPD fused into the
+        # pass 1 after that reads them)
+        self._fin = torch.cuda.Stream(device=self.dev)
 
     def _pass2_launch(self, want_rows, slot=0):
         key = (bool(want_rows), slot)
         if key not in self._p2:
             want = ("last_hit", "dir_out", "opl") + (("det", "atan") if want_rows else ())
-            # both slots write the same output buffers (the next pass 2 may rewrite them once the
+            # every slot writes the same output buffers (the next pass 2 may rewrite them once the
             # fused tilt that reads them, queued ahead of it, is done)
-            out = self._p2[(key[0], 1 - slot)].res.extra["buffers"] if (key[0], 1 - slot) in self._p2 else None
+            same = [v for (w, _), v in self._p2.items() if w == key[0]]
+            out = same[0].res.extra["buffers"] if same else None
             t2 = self._tan2[slot]
             self._p2[key] = ChainLaunch(self.g.mirrors, tan_h=t2[:self.n], tan_v=t2[self.n:], out=out,
                                         row0=self.shard.row0, n_rays=self.n_local, src=self.g.source,
@@ -307,16 +319,19 @@ class RayWave:
         flags = int(host[self._nsamp:].view(np.int32)[0])
         return host[:nh].copy(), host[nh:self._nsamp].copy(), flags
 
-    def _pass1(self, stream, fuse, slot):
-        """The full pass 1 (fused with fuse's tilt when given). Its workgroup 0 also stages this
-        run's resampled tables from pinned host memory to the device (akb_chain_desc.copy_*), so
-        pass 2 follows it with no copy or cross-stream wait in between."""
+    def _pass1(self, stream, fuse, slot, fuse_opd=None):
+        """The full pass 1 (fused with fuse's tilt, and fuse_opd's OPD, when given). Its workgroup
+        0 also stages this run's resampled tables from pinned host memory to the device
+        (akb_chain_desc.copy_*), so pass 2 follows it with no copy or cross-stream wait."""
         d = self._p1.desc
         d.copy_src, d.copy_dst, d.copy_n = D.ptr(self._tan2_host[slot]), D.ptr(self._tan2[slot]), 2 * self.n
         if fuse is None:
             self._p1.launch(stream=stream, reset_flags=False)
         else:
-            self._fused_pass1(fuse, stream)
+            self._fused_pass1(fuse, stream, fuse_opd)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._staged[slot] = ev
 
     def _pass2(self, want_rows=False, stream=None, slot=0):
         ev = None
@@ -364,7 +379,7 @@ class RayWave:
         GPU while the host resamples (bench.py does)."""
         return self.launch_back(self.launch_front(full=full, overlap=overlap), opd=opd, keep_rotated=keep_rotated)
 
-    def launch_front(self, full=False, overlap=None, fuse=None):
+    def launch_front(self, full=False, overlap=None, fuse=None, fuse_opd=None):
         """The resample picks, pass 1, the resample (the run's one host wait, for the picks
         only), pass 2, its sums and the device tilt parameters. Returns as soon as all of it is
         queued; the trace flags are read when launch_back (or _resolve) needs them.
@@ -376,18 +391,27 @@ class RayWave:
 
         fuse: the previous run's front, not yet handed to launch_back: its tilt then runs inside
         this run's pass-1 kernel (akb_chain_tilt_f64), its loads hidden behind the chain's
-        arithmetic, and its launch_back only finishes the tilt sums and forms the OPD (queue that
-        in `overlap`, called once pass 1 is queued, so it runs beside this run's pass 2). A fused
-        OPD inside pass 2 measured slower (1.005 vs 0.974 ms per bench step): its loads and
-        registers cost the FP64-bound chain more than running beside it."""
+        arithmetic, and its tilt sums are finished beside this run's pass 2. fuse_opd: the front
+        before that one (tilted inside the previous pass 1): its OPD maps are formed inside the same
+        kernel (akb_chain_tilt_opd_f64), and its launch_back then only assembles the result (queue
+        it in `overlap`, called once pass 1 is queued, so its pupil runs beside this run's pass 2).
+        Without fuse_opd, fuse's launch_back forms the OPD itself. A fused OPD inside pass 2
+        measured slower (1.005 vs 0.974 ms per bench step): its loads and registers cost the
+        FP64-bound chain more than running beside it; pass 1 keeps nothing of it across the chain."""
         L = _lib.lib()
         stream = D.stream_handle()
-        slot = self._runs % 2
+        slot = self._runs % self.NSLOTS
         self._runs += 1
         if fuse is not None and (fuse.tilt is not None or fuse.full or self.g.det2 is None):
             # the fused kernel writes the detector-2 rows only: full runs and single-detector
             # systems (KB) keep the tilt in their own back half
             fuse = None
+        if fuse_opd is not None and (fuse is None or fuse_opd.tilt is None or fuse_opd.opd is not None
+                                     or fuse_opd.fin_ev is None or any(self._flags_of(fuse_opd))):
+            # needs a fused tilt to ride on, fuse_opd's own fused tilt, and clean trace flags
+            # (a flagged run takes the staged path in its launch_back); its pass 2 ended two runs
+            # ago, so reading its flags waits for nothing
+            fuse_opd = None
         # fused optimistically: should fuse's pass 2 turn out flagged, launch_back ignores the
         # fused tilt and takes the staged path (its tables live in fuse's own slot)
         samp_h, samp_v, sflags = self._take_picks()
@@ -396,6 +420,9 @@ class RayWave:
             self._words.zero_()
             torch.cuda.synchronize()
             raise _lib.AKBError(self._pass1_error(sflags))
+        if self._staged[slot] is not None:  # the pass 1 that last copied this slot's host tables
+            self._staged[slot].synchronize()
+            self._staged[slot] = None
         th = self._tan2_host[slot].numpy()
         if self.resample_pass:
             # np.arctan / np.tan stay numpy's (their SIMD kernels are what the reference runs)
@@ -406,15 +433,19 @@ class RayWave:
             np.tan(self.rand_v, out=th[self.n:])
         self._queue_picks()
         if fuse is not None and self._back_done is not None:
-            # the back half queued before (its tilt sums, OPD, pupil; two runs back by the time the
-            # tilt-parameter kernel below clears that run's extent keys and the next fused pass 1
-            # refills its tilt sink): normally long done, and then no wait enters the stream
+            # the back half queued before (its OPD / pupil; its extent keys are cleared by a
+            # later tilt-parameter kernel and its tilt sink refilled by a later fused pass 1):
+            # normally long done, and then no wait enters the stream
             if not self._back_done.query():
                 torch.cuda.current_stream().wait_event(self._back_done)
             self._back_done = None
-        self._pass1(stream, fuse, slot)
+        if fuse_opd is not None and not fuse_opd.fin_ev.query():  # its tilt sums (normally done)
+            torch.cuda.current_stream().wait_event(fuse_opd.fin_ev)
+        self._pass1(stream, fuse, slot, fuse_opd)
+        if fuse is not None:
+            self._finish_tilt(fuse)
         if overlap is not None:
-            overlap()  # e.g. the previous run's back half, beside this run's pass 2
+            overlap()  # e.g. an earlier run's back half, beside this run's pass 2
         tan_h2, tan_v2 = self._tan2[slot, :self.n], self._tan2[slot, self.n:]
         if self._back_done is not None and fuse is None:
             # pass 2 rewrites the buffers a queued (unfused) back half's tilt reads
@@ -442,47 +473,86 @@ class RayWave:
         return _Front(r=r, tan_h2=tan_h2, tan_v2=tan_v2, params=params, full=full, stream=stream, flag_ev=ev2,
                       done=done, slot=slot)
 
-    def _resolve(self, f):
-        """f's trace flags (waits for its pass 2 if still running); a flagged pass 1 raises."""
+    def _flags_of(self, f):
+        """f's (pass 1, pass 2) trace flag words (waits for its pass 2 if still running)."""
         if f.flags is None:
             f.flag_ev.synchronize()
             h = self._f_host[f.slot]
             f.flags = (int(h[0]), int(h[1]))
-        if f.flags[0]:  # the full pass 1 (its flag word arrives with pass 2's)
-            raise _lib.AKBError(self._pass1_error(f.flags[0]))
         return f.flags
+
+    def _resolve(self, f):
+        """f's trace flags (waits for its pass 2 if still running); a flagged pass 1 raises."""
+        flags = self._flags_of(f)
+        if flags[0]:  # the full pass 1 (its flag word arrives with pass 2's)
+            raise _lib.AKBError(self._pass1_error(flags[0]))
+        return flags
 
     @staticmethod
     def _pass1_error(flags):
         return (f"pass 1 raised trace flags {flags:#x} (a ray missed a mirror or a norm was zero): the "
                 "reference returns all-NaN here and its interp1d resample fails on it")
 
-    def _fused_pass1(self, f, stream):
+    def _fused_pass1(self, f, stream, g=None):
         """This run's pass 1 and run f's tilt in one kernel (f's pass-2 buffers are still intact:
-        this run's pass 2 comes after it on the same stream)."""
+        this run's pass 2 comes after it on the same stream); with g (the run before f, tilted
+        by the previous pass 1, its sums finished) also g's DistError2 / Wave2 and extent keys."""
         L = _lib.lib()
         tb = self._tilt_buffers(False, f.full)
         r = f.r
         n = self.n_local
-        _lib.check(L.akb_chain_tilt_f64(self._p1.desc, D.ptr(f.params), D.host_f64(self.g.det1),
-                                        D.host_f64(tb["d2"]), D.ptr(r.dir_out), D.ptr(r.last_hit), D.ptr(r.opl),
-                                        n, n, None, None, D.ptr(tb["det1"]), D.ptr(tb["det2_buf"]),
-                                        D.ptr(tb["total1"]), D.ptr(tb["total2"]), self._sink3[f.slot].desc, stream))
+        if g is None:
+            _lib.check(L.akb_chain_tilt_f64(self._p1.desc, D.ptr(f.params), D.host_f64(self.g.det1),
+                                            D.host_f64(tb["d2"]), D.ptr(r.dir_out), D.ptr(r.last_hit),
+                                            D.ptr(r.opl), n, n, None, None, D.ptr(tb["det1"]),
+                                            D.ptr(tb["det2_buf"]), D.ptr(tb["total1"]), D.ptr(tb["total2"]),
+                                            self._sink3[f.slot].desc, stream))
+        else:
+            gt = g.tilt
+            sums, cnts = g.fin
+            opd = dict(dist_err2=torch.empty(n, dtype=D.F64, device=self.dev),
+                       wave2=torch.empty(n, dtype=D.F64, device=self.dev))
+            _lib.check(L.akb_chain_tilt_opd_f64(self._p1.desc, D.ptr(f.params), D.host_f64(self.g.det1),
+                                                D.host_f64(tb["d2"]), D.ptr(r.dir_out), D.ptr(r.last_hit),
+                                                D.ptr(r.opl), n, n, D.ptr(tb["det2_buf"]), D.ptr(tb["total2"]),
+                                                self._sink3[f.slot].desc, D.ptr(gt["total2"]),
+                                                D.ptr(gt["det2_buf"]), D.ptr(sums), D.ptr(cnts),
+                                                D.ptr(opd["dist_err2"]), D.ptr(opd["wave2"]),
+                                                D.ptr(self._ext[g.slot]), stream))
         ev = torch.cuda.Event()
         ev.record()
         f.tilt, f.tilted = tb, ev
+        if g is not None:
+            g.opd, g.opd_ev = opd, ev
+
+    def _finish_tilt(self, f):
+        """The sums of f's fused tilt (on the finish stream, beside the next pass 2)."""
+        with torch.cuda.stream(self._fin):
+            self._fin.wait_event(f.tilted)
+            sums, cnts = self._sink3[f.slot].finish(self._fin)
+            if self.comm.world > 1:
+                self.comm.allreduce_sums(sums)
+                self.comm.allreduce_sums(cnts)
+            ev = torch.cuda.Event()
+            ev.record(self._fin)
+        f.fin, f.fin_ev = (sums, cnts), ev
 
     def launch_back(self, f, opd=True, keep_rotated=False, stream=None):
         """Tilt, detectors and OPD of a launch_front (no host wait). stream: run them on that
         stream instead of the front's - concurrently with the next launch_front's pass 1, which
         is FP64-bound while this half is HBM-bound; the next pass 2 waits for it (and for a pupil
-        taken on the same stream)."""
+        taken on the same stream). A front whose tilt and OPD were fused into later pass-1
+        kernels only has its result assembled here."""
         if stream is None:
+            if f.opd is None and f.fin_ev is not None:
+                torch.cuda.current_stream().wait_event(f.fin_ev)
             out = self._launch_back(f, opd, keep_rotated)
         else:
-            stream.wait_event(f.tilted if f.tilt is not None else f.done)
+            stream.wait_event(f.opd_ev if f.opd is not None else f.tilted if f.tilt is not None else f.done)
+            if f.opd is None and f.fin_ev is not None:
+                stream.wait_event(f.fin_ev)
             f.params.record_stream(stream)  # allocated on the front's stream, read here
-            for t in (f.tilt or {}).values():
+            for t in list((f.tilt or {}).values()) + list((f.opd or {}).values()):
                 if isinstance(t, torch.Tensor):
                     t.record_stream(stream)
             with torch.cuda.stream(stream):
@@ -501,8 +571,13 @@ class RayWave:
                             params=f.params)
             if f.full:
                 out.update(det_pre=r.det, atan=r.atan)
-            if f.tilt is not None:  # tilted inside the next run's pass 1
-                out.update(self._opd_after_tilt(f.tilt, f.full, True, f.slot, f.stream))
+            if f.opd is not None:  # tilted and OPD-formed inside the two next runs' pass 1
+                tb = f.tilt
+                self._means5 = f.fin
+                out.update(dir_rot=None, pt_rot=None, detcenter=None, detcenter2=tb["det2"], total=None,
+                           total2=tb["total2"], dist_err=None, sph=None, **f.opd)
+            elif f.tilt is not None:  # tilted inside the next run's pass 1
+                out.update(self._opd_after_tilt(f.tilt, f.full, True, f.slot, f.stream, fin=f.fin))
             elif opd:
                 out.update(self._tilt_opd(r.last_hit, r.dir_out, r.opl, keep_rotated, f.full, params=f.params,
                                           stream=f.stream, slot=f.slot))
@@ -563,15 +638,19 @@ class RayWave:
                                           D.host_f64(self.g.det1), D.host_f64(tb["d2"]), *outs))
         return self._opd_after_tilt(tb, full, host_tilt is None, slot, stream)
 
-    def _opd_after_tilt(self, tb, full, keys_zeroed, slot, stream):
-        """The tilt sink's means, then DistError / Sph / Wave2 and the pupil extent keys."""
+    def _opd_after_tilt(self, tb, full, keys_zeroed, slot, stream, fin=None):
+        """The tilt sink's means (fin: already finished), then DistError / Sph / Wave2 and the
+        pupil extent keys."""
         L = _lib.lib()
         n, dev = self.n_local, self.dev
         sh = D.stream_handle(stream)
-        sums, cnts = self._sink3[slot].finish(sh)
-        if self.comm.world > 1:
-            self.comm.allreduce_sums(sums)
-            self.comm.allreduce_sums(cnts)
+        if fin is not None:
+            sums, cnts = fin
+        else:
+            sums, cnts = self._sink3[slot].finish(sh)
+            if self.comm.world > 1:
+                self.comm.allreduce_sums(sums)
+                self.comm.allreduce_sums(cnts)
         self._means5 = (sums, cnts)
         total1 = tb["total1"]
         dist_err = torch.empty(n, dtype=D.F64, device=dev) if total1 is not None else None

@@ -48,7 +48,7 @@ def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
-    p.add_argument("--warmup", type=int, default=3, help="at least 1 (fills the pipeline)")
+    p.add_argument("--warmup", type=int, default=3, help="at least 2 with --fuse 2 (fills the pipeline)")
     p.add_argument("--rays", type=float, default=1.0e7, help="rays per GPU")
     p.add_argument("--pupil", type=int, default=128)
     p.add_argument("--pad", type=int, default=16)
@@ -62,10 +62,11 @@ def parse():
                         "next step's FP64-bound pass 1 (0: behind it on one stream)")
     p.add_argument("--back-priority", type=int, default=0,
                    help="torch stream priority of the back stream (lower = higher priority; 0 = normal)")
-    p.add_argument("--fuse", type=int, default=1,
-                   help="1: each step's tilt runs inside the next step's pass-1 kernel (its loads hidden behind "
-                        "the chain's FP64 arithmetic), its OPD / pupil / PSF on the back stream during the host "
-                        "resample; 0: the tilt as its own kernel on the back stream beside pass 1")
+    p.add_argument("--fuse", type=int, default=2,
+                   help="2: step k's pass-1 kernel also tilts step k-1 and forms step k-2's OPD maps (their loads "
+                        "hidden behind the chain's FP64 arithmetic), step k-2's pupil / PSF on the back stream; "
+                        "1: the tilt only, the OPD on the back stream; 0: the tilt as its own kernel on the back "
+                        "stream beside pass 1")
     p.add_argument("--psf-start", choices=("pupil", "pass1"), default="pupil",
                    help="side-stream PSF starts as soon as the previous pupil is ready, beside pass 1 "
                         "(default; measured faster), or after this step's pass 1")
@@ -124,7 +125,7 @@ def read_pmc():
 
 def main():
     args = parse()
-    args.warmup = max(args.warmup, 1)
+    args.warmup = max(args.warmup, 2 if args.fuse >= 2 else 1)
     import torch
     from akbraytracing_amd import build as B
     from akbraytracing_amd import dist as AD
@@ -203,7 +204,12 @@ def main():
         # tilt), the previous step's OPD / pupil / PSF right behind it, so the GPU works through
         # them while the host does the resample; each step still traces, tilts, reduces and
         # transforms one full grid
-        if fronts and args.fuse:
+        if args.fuse >= 2 and len(fronts) == 2:  # two steps in flight: tilt k-1, OPD k-2
+            old = fronts.pop(0)
+            fronts.append(rw.launch_front(overlap=lambda: back(timed, old), fuse=fronts[-1], fuse_opd=old))
+        elif args.fuse >= 2 and len(fronts) == 1:  # filling the pipeline
+            fronts.append(rw.launch_front(fuse=fronts[0]))
+        elif fronts and args.fuse:
             prev = fronts.pop(0)
             fronts.append(rw.launch_front(overlap=lambda: back(timed, prev), fuse=prev))
         else:

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define AKB_ABI_VERSION 5
+#define AKB_ABI_VERSION 6
 
 /* status codes */
 #define AKB_OK 0
@@ -223,6 +223,18 @@ int akb_chain_tilt_f64(const akb_chain_desc* d, const double* d_params, const do
                        const double det2_ghij[4], const double* dir, const double* pt, const double* opl, int64_t ld,
                        int64_t n, double* dir_rot, double* pt_rot, double* det1, double* det2, double* total1,
                        double* total2, const akb_leaf_sink* sink, void* stream);
+/* akb_chain_tilt_f64 (detector-2 rows) that also forms the OPD maps of the run before the tilted
+ * one (akb_opd_f64 without detector 1 / Sph): from that run's opd_total2 (n) and opd_det2 (3, ld)
+ * and its tilt sums d_sum5 / d_cnt5, dist_err2 = (total2 - mean2) * 1e9, wave = dist_err2 - Sph,
+ * and its detector-2 extents max-folded into d_extent_keys (zeroed beforehand, e.g. by
+ * akb_tilt_params_f64). Same n and ld as the tilt. The chain's resample picks, the tilt and the
+ * OPD are those of the three separate calls. */
+int akb_chain_tilt_opd_f64(const akb_chain_desc* d, const double* d_params, const double det1_ghij[4],
+                           const double det2_ghij[4], const double* dir, const double* pt, const double* opl,
+                           int64_t ld, int64_t n, double* det2, double* total2, const akb_leaf_sink* sink,
+                           const double* opd_total2, const double* opd_det2, const double* d_sum5,
+                           const int64_t* d_cnt5, double* dist_err2, double* wave, uint64_t* d_extent_keys,
+                           void* stream);
 
 /* Focus sweep rows (find_defocus, ref :9086-9170): for P detector planes x = -d_plane_j[p]
  * (coefficients g = 1, h = i = 0, j = d_plane_j[p], as coeffs_det[9] = -(s2f_middle + a)), the

@@ -400,6 +400,46 @@ def test_fused_pipeline_equals_sequential_runs(gpu, n):
         assert torch.equal(opd, want_opd)
 
 
+@pytest.mark.parametrize("n", [65, 1001])
+def test_opd_fused_pipeline_equals_sequential_runs(gpu, n):
+    """bench.py's default pipeline (--fuse 2): run k's pass-1 kernel also tilts run k-1 and forms
+    run k-2's OPD maps and extent keys (akb_chain_tilt_opd_f64), k-1's tilt sums finished on a
+    stream of their own; k-2's launch_back and pupil go beside pass 2 - the same bits, pupil
+    pitch included, as run() one at a time. The two runs left in flight drain through the
+    tilt-only and the unfused back halves."""
+    from akbraytracing_amd.wavefront import RayWave
+    rw = RayWave(_geom(), n)
+    seq = rw.run()
+    want = {k: seq[k].clone() for k in ("wave2", "dist_err2", "detcenter2", "total2")}
+    want_opd, want_pitch = (t.clone() for t in rw.pupil(32))
+    want_means = rw.means()
+    bs = torch.cuda.Stream()
+    outs, pupils, kinds, means = [], [], [], []
+
+    def back(front):
+        kinds.append((front.tilt is not None, front.opd is not None))
+        with torch.cuda.stream(bs):
+            outs.append(rw.launch_back(front, stream=bs))
+            pupils.append(tuple(t.clone() for t in rw.pupil(32)))
+            means.append(rw.means())
+
+    fr = [rw.launch_front()]
+    fr.append(rw.launch_front(fuse=fr[0]))
+    for _ in range(4):
+        g = fr.pop(0)
+        fr.append(rw.launch_front(overlap=lambda p=g: back(p), fuse=fr[-1], fuse_opd=g))
+    for f in fr:
+        back(f)
+    torch.cuda.synchronize()
+    assert kinds == [(True, True)] * 4 + [(True, False), (False, False)]
+    for o, (opd, pitch), m in zip(outs, pupils, means):
+        for k, v in want.items():
+            assert torch.equal(o[k], v), k
+        assert torch.equal(opd, want_opd) and torch.equal(pitch, want_pitch)
+        for a, b in zip(m, want_means):
+            assert np.array_equal(a, b)
+
+
 def test_fused_pipeline_falls_back_where_it_cannot_fuse(gpu):
     """launch_front(fuse=...) on a single-detector system (KB) or a full run keeps the tilt in
     the back half and still gives run()'s bits."""
@@ -457,6 +497,18 @@ def test_fused_pipeline_flagged_pass2_takes_staged_path(gpu):
         assert torch.max(torch.abs(out[k] - v)).item() <= 1e-4, k
     rest = rw.launch_back(nxt)
     assert torch.equal(rest["wave2"], want["wave2"])
+    # the same two runs later: a flagged run is not OPD-fused into the pass 1 after next
+    f = rw.launch_front()
+    nxt = rw.launch_front(fuse=f)
+    rw._resolve(f)
+    f.flags = (0, 0x1)
+    last = rw.launch_front(fuse=nxt, fuse_opd=f)
+    assert f.opd is None and nxt.tilt is not None
+    out = rw.launch_back(f)
+    for k, v in want.items():
+        assert torch.max(torch.abs(out[k] - v)).item() <= 1e-4, k
+    for fr in (nxt, last):
+        assert torch.equal(rw.launch_back(fr)["wave2"], want["wave2"])
 
 
 def test_config5_legendre_opl_perturbation(gpu):
