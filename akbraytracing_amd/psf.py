@@ -25,8 +25,8 @@ def ensure_even_size(arr):
     py, px = ny % 2, nx % 2
     if not (py or px):
         return arr, None
-    out = np.zeros((ny + py, nx + px), dtype=np.result_type(arr.dtype, np.float64) if arr.dtype.kind in "iub"
-                   else arr.dtype)
+    # np.pad(arr, ..., mode="constant") as psf_fft.py:15: the input dtype is kept (int, bool too)
+    out = np.zeros((ny + py, nx + px), dtype=arr.dtype)
     out[:ny, :nx] = arr
     return out, (slice(0, ny), slice(0, nx))
 

@@ -6,13 +6,13 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 120 rocprofv3 -L > gpurun_out/counters.txt 2>&1
 rc=$?; echo "list exit $rc"; [ $rc -eq 0 ] || exit $rc
-F64=$(grep -oE "SQ_INSTS_VALU_(FMA|MUL|ADD|TRANS)_F64" gpurun_out/counters.txt | sort -u | tr '\n' ' ')
-echo "f64 counters: $F64"
 REGEX="${PMC_REGEX:-k_chain|k_tilt|k_opd|k_pw|k_psf|fft}"
 CMD="${PMC_CMD:-python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline}"
 OUT="${PMC_OUT:-pmc}"
 i=0
-for SET in "FETCH_SIZE" "WRITE_SIZE" "$F64" "GRBM_GUI_ACTIVE SQ_WAVES SQ_INSTS_VALU" \
+# each FP64 counter in a pass of its own: in one shared pass (r01d) FMA_F64 and MUL_F64 read identical
+for SET in "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU_FMA_F64" "SQ_INSTS_VALU_MUL_F64" \
+           "SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64" "GRBM_GUI_ACTIVE SQ_WAVES SQ_INSTS_VALU" \
            "SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_SALU" \
            "SQ_WAIT_INST_ANY SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR"; do
   [ -n "$SET" ] || continue

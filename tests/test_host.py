@@ -132,6 +132,11 @@ def test_psf_host_helpers_match_reference_formulas():
     assert padded.shape == (4, 4) and crop == (slice(0, 3), slice(0, 4)) and padded[3].sum() == 0
     same, none = G.ensure_even_size(np.ones((4, 6)))
     assert none is None and same.shape == (4, 6)
+    for dt in (np.int32, np.bool_, np.float32, np.complex128):  # np.pad keeps the dtype (psf_fft.py:15)
+        src = np.ones((3, 5), dtype=dt)
+        p, _ = G.ensure_even_size(src)
+        ref = np.pad(src, ((0, 1), (0, 1)), mode="constant", constant_values=0)
+        assert p.dtype == ref.dtype and np.array_equal(p, ref)
     wy, wx, m = G.hann_axes(9, 10)
     w = np.outer(wy, wx)
     assert m == w.max()
