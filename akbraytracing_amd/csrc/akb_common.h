@@ -169,6 +169,34 @@ __device__ __forceinline__ void norm3_inv(double x, double y, double z, double& 
     }
 }
 
+// norm3_inv for a vector whose squared norm is ~1 or NaN: a reflection r = l - 2 (l.n) n of a unit
+// direction l about a unit normal n has |r| = |l| = 1 up to rounding, so v = |r|^2 lies far inside
+// norm3_inv's range and its range test (two compares and the exec-mask juggling around the
+// library fallback) can go. v == 0 cannot occur for unit l and n, and if it does (it is returned
+// in `zero` for the caller's flag, where s and inv are NaN) the flag sends the ray to the staged
+// path, which applies the reference's value rule. A NaN input gives NaN as the checked form does.
+__device__ __forceinline__ void norm3_inv_unit(double x, double y, double z, double& s, double& inv, bool& zero) {
+    const double v = x * x + y * y + z * z;
+    zero = v == 0.0;
+    const double r = __builtin_amdgcn_rsq(v);
+    double g = v * r;
+    double h = r * 0.5;
+    const double e = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, e, g);
+    const double d = __builtin_fma(-g, g, v);
+    h = __builtin_fma(h, e, h);
+    g = __builtin_fma(d, h, g);
+    const double d2 = __builtin_fma(-g, g, v);
+    s = __builtin_fma(d2, h, g);
+    double y0 = __builtin_amdgcn_rcp(s);
+    double e0 = __builtin_fma(-s, y0, 1.0);
+    y0 = __builtin_fma(y0, e0, y0);
+    e0 = __builtin_fma(-s, y0, 1.0);
+    y0 = __builtin_fma(y0, e0, y0);
+    const double r1 = __builtin_fma(-s, y0, 1.0);
+    inv = __builtin_fma(r1, y0, y0);
+}
+
 // np.arctan of an exit-ray slope (AKB_raytrace_20250312.py:2856-2857, :3583-3584). The slopes of a
 // focusing system are small (|x| ~ 1e-5 for the reference AKB), where the Taylor series
 // x - x^3/3 + ... + x^13/13 is exact to 2^-59 relative for |x| <= 2^-4 and x + (x z) P(z) rounds

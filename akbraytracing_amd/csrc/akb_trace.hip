@@ -365,8 +365,10 @@ __device__ __forceinline__ void tilt_load(const TiltArgs& a, int64_t i, TiltIn& 
 
 // a chain mirror: the quadric plus its doubled square coefficients (2a, 2b, 2c: exact, formed on the
 // host so the per-ray code does not recompute wave-uniform values on the vector ALU)
+// sgn: +1.0, or -1.0 for a mirror traced with the minus root (negative=True): the root's sign as a
+// factor, sD * sgn, instead of both roots and a per-lane select (x + (-y) is x - y exactly)
 struct CMirror {
-    double a, b, c, d, e, f, g, h, i, j, a2, b2, c2;
+    double a, b, c, d, e, f, g, h, i, j, a2, b2, c2, sgn;
 };
 
 // mirror kinds: 0 general, 1 y-free (b = d = f = h = 0, h = +0.0), 2 z-free (c = e = f = i = 0, i = +0.0)
@@ -374,7 +376,6 @@ constexpr int kKindGeneral = 0, kKindYFree = 1, kKindZFree = 2;
 
 struct ChainArgs {
     int K;
-    int negmask;
     int kind[AKB_MAX_MIRRORS];
     CMirror q[AKB_MAX_MIRRORS];
     double det[4];
@@ -469,8 +470,10 @@ struct Ray {
 // gradient's y (z) component is exactly +0 (every term +-0, then + h = +0.0), its square adds +0 to
 // the norm, and the reflected y (z) component is m - 2A * (+0) = m: the results are the general
 // expression's bits (an exactly-zero partial sum could only change the sign of a zero).
-template <int kKind, bool kOPL, bool kHits>
-__device__ __forceinline__ void mirror_step(const CMirror& Q, bool neg, Ray& R, double& opl, bool first, int k,
+// kUnitIn: the incoming direction is a unit vector (grid rays, or any mirror after the first), so
+// the reflected direction's norm skips its range test (norm3_inv_unit).
+template <int kKind, bool kOPL, bool kHits, bool kUnitIn>
+__device__ __forceinline__ void mirror_step(const CMirror& Q, Ray& R, double& opl, int k,
                                             int& fl, double* hits, int64_t hits_ld, int lane) {
     const double l = R.l, m = R.m, n = R.n, p = R.p, q = R.q, r = R.r;
     double A, B, C;
@@ -492,12 +495,9 @@ __device__ __forceinline__ void mirror_step(const CMirror& Q, bool neg, Ray& R, 
     const double D = B * B - 4.0 * A * C;
     wave_flag(!(D > 0.0), AKB_FLAG_MISS << (4 * k), fl);
     const double sD = sqrt_cr(D);
-    const double t = (neg ? (-B - sD) : (-B + sD)) / (2.0 * A);
+    const double t = (-B + sD * Q.sgn) / (2.0 * A);  // (-B - sD) / (2A) for the minus root
     const double x = t * l + p, y = t * m + q, z = t * n + r;
-    if (kOPL) {
-        const double d = norm3(x - p, y - q, z - r);
-        opl = first ? d : opl + d;
-    }
+    if (kOPL) opl = opl + norm3(x - p, y - q, z - r);  // opl starts at +0.0: 0 + d is d exactly
     // hits: this segment's column 0 of mirror 0's x row (wave-uniform). A compile-time switch: a
     // vector store anywhere in the mirror loop makes the compiler drain every outstanding load
     // before the loop (no separate store counter on gfx9), which would stall the fused kernel's
@@ -547,8 +547,14 @@ __device__ __forceinline__ void mirror_step(const CMirror& Q, bool neg, Ray& R, 
         rz = n - A2 * nz;
     }
     double sr, ir;
-    norm3_inv(rx, ry, rz, sr, ir);
-    wave_flag(sr == 0.0, AKB_FLAG_ZERO_REFLECT << (4 * k), fl);
+    if (kUnitIn) {
+        bool zero;
+        norm3_inv_unit(rx, ry, rz, sr, ir, zero);
+        wave_flag(zero, AKB_FLAG_ZERO_REFLECT << (4 * k), fl);
+    } else {
+        norm3_inv(rx, ry, rz, sr, ir);
+        wave_flag(sr == 0.0, AKB_FLAG_ZERO_REFLECT << (4 * k), fl);
+    }
     R.l = div_pos(rx, sr, ir);
     R.m = div_pos(ry, sr, ir);
     R.n = div_pos(rz, sr, ir);
@@ -589,8 +595,11 @@ __device__ __forceinline__ void ray_tables(const ChainArgs& a, int64_t i, int64_
 // optional output rows, no out-of-line atan call).
 // kPointSrc: rays start at the constant source (no origin loads, which would have to be waited
 // for - with everything issued before them - ahead of the mirror loop).
+// kFixed: pass 2's output set, known at compile time - last hit, exit direction and OPL rows, no
+// detector / arctan rows, hits or picks - so none of the optional rows is tested per segment (their
+// tests' masks were what overflowed the scalar registers into VGPR lanes).
 template <bool kGrid, bool kOPL, bool kNeedQ, bool kHits = false, bool kLean = false, bool kPointSrc = kLean,
-          class Post = NoHook>
+          bool kFixed = false, class Post = NoHook>
 __device__ __forceinline__ void chain_ray_tab(const ChainArgs& a, int64_t i0, int t, int64_t iv, int64_t ih,
                                               double th, double tv, int& fl, double (&qv)[5], Post post = Post()) {
     const int64_t i = i0 + t;
@@ -625,13 +634,12 @@ __device__ __forceinline__ void chain_ray_tab(const ChainArgs& a, int64_t i0, in
     // 4-mirror AKB kernel measured 12 % slower on MI355X)
 #pragma unroll 1
     for (int k = 0; k < a.K; ++k) {
-        const bool neg = (a.negmask >> k) & 1;
         if (a.kind[k] == kKindYFree)  // wave-uniform branch
-            mirror_step<kKindYFree, kOPL, kHits>(a.q[k], neg, R, opl, k == 0, k, fl, hits, a.hits_ld, t);
+            mirror_step<kKindYFree, kOPL, kHits, kGrid>(a.q[k], R, opl, k, fl, hits, a.hits_ld, t);
         else if (a.kind[k] == kKindZFree)
-            mirror_step<kKindZFree, kOPL, kHits>(a.q[k], neg, R, opl, k == 0, k, fl, hits, a.hits_ld, t);
+            mirror_step<kKindZFree, kOPL, kHits, kGrid>(a.q[k], R, opl, k, fl, hits, a.hits_ld, t);
         else
-            mirror_step<kKindGeneral, kOPL, kHits>(a.q[k], neg, R, opl, k == 0, k, fl, hits, a.hits_ld, t);
+            mirror_step<kKindGeneral, kOPL, kHits, kGrid>(a.q[k], R, opl, k, fl, hits, a.hits_ld, t);
     }
     const double l = R.l, m = R.m, nn = R.n, p = R.p, q = R.q, r = R.r;
     if (kOPL && kGrid && a.pert_h) {  // figure-error perturbation of the path (BASELINE config 5)
@@ -640,23 +648,23 @@ __device__ __forceinline__ void chain_ray_tab(const ChainArgs& a, int64_t i0, in
         opl = opl + d;
     }
     post();
-    if (kOPL && a.opl) (a.opl + i0)[t] = opl;
-    if (!kLean && a.last_hit) {
+    if (kOPL && (kFixed || a.opl)) (a.opl + i0)[t] = opl;
+    if (!kLean && (kFixed || a.last_hit)) {
         double* o = a.last_hit + i0;
         o[t] = p;
         (o + a.last_hit_ld)[t] = q;
         (o + 2 * a.last_hit_ld)[t] = r;
     }
-    if (!kLean && a.dir_out) {
+    if (!kLean && (kFixed || a.dir_out)) {
         double* o = a.dir_out + i0;
         o[t] = l;
         (o + a.dir_out_ld)[t] = m;
         (o + 2 * a.dir_out_ld)[t] = nn;
     }
-    if (kNeedQ || (!kLean && a.det_out)) {
+    if (kNeedQ || (!kLean && !kFixed && a.det_out)) {
         double x, y, z;
         plane_hit(a.det[0], a.det[1], a.det[2], a.det[3], l, m, nn, p, q, r, x, y, z);
-        if (!kLean && a.det_out) {
+        if (!kLean && !kFixed && a.det_out) {
             double* o = a.det_out + i0;
             o[t] = x;
             (o + a.det_out_ld)[t] = y;
@@ -666,13 +674,14 @@ __device__ __forceinline__ void chain_ray_tab(const ChainArgs& a, int64_t i0, in
         qv[3] = y;
         qv[4] = z;
     }
-    if (kNeedQ || (!kLean && (a.atan_h || a.atan_v))) {
+    if (kNeedQ || (!kLean && !kFixed && (a.atan_h || a.atan_v))) {
         const double il = 1.0 / l;
         qv[0] = atan_slope(div_shared(m, l, il));
         qv[1] = atan_slope(div_shared(nn, l, il));
-        if (a.atan_h) (a.atan_h + i0)[t] = qv[0];
-        if (a.atan_v) (a.atan_v + i0)[t] = qv[1];
+        if (!kFixed && a.atan_h) (a.atan_h + i0)[t] = qv[0];
+        if (!kFixed && a.atan_v) (a.atan_v + i0)[t] = qv[1];
     }
+    if (kFixed) return;
     // equal-angle resample samples: the slope ratios only; the host applies np.arctan so the
     // resampled angle tables match the reference bit for bit (glibc atan, ref :2858-2859)
     if (a.samp_h && g >= a.sh_begin && g < a.sh_end) a.samp_h[g - a.sh_begin] = m / l;
@@ -680,12 +689,13 @@ __device__ __forceinline__ void chain_ray_tab(const ChainArgs& a, int64_t i0, in
 }
 
 // the same, loading its own table entries (the unpipelined kernels)
-template <bool kGrid, bool kOPL, bool kNeedQ, bool kHits = false, bool kLean = false, bool kPointSrc = kLean>
+template <bool kGrid, bool kOPL, bool kNeedQ, bool kHits = false, bool kLean = false, bool kPointSrc = kLean,
+          bool kFixed = false>
 __device__ __forceinline__ void chain_ray(const ChainArgs& a, int64_t i0, int t, int& fl, double (&qv)[5]) {
     int64_t iv = 0, ih = 0;
     double th = 0.0, tv = 0.0;
     if (kGrid) ray_tables(a, i0 + t, iv, ih, th, tv);
-    chain_ray_tab<kGrid, kOPL, kNeedQ, kHits, kLean, kPointSrc>(a, i0, t, iv, ih, th, tv, fl, qv);
+    chain_ray_tab<kGrid, kOPL, kNeedQ, kHits, kLean, kPointSrc, kFixed>(a, i0, t, iv, ih, th, tv, fl, qv);
 }
 
 template <bool kGrid, bool kOPL, int kWaves, bool kHits = false, bool kPointSrc = false>
@@ -702,7 +712,8 @@ __global__ void __launch_bounds__(kBlock, kWaves) k_chain(ChainArgs a) {
 // the same, walking 256-ray segments and feeding the fused np.nanmean(arctan) / np.mean(det)
 // leaf sums (the tilt means, ref :3583-3591) instead of writing those five rows to HBM
 // kPointSrc: grid rays from the point source (no origin loads)
-template <bool kGrid, bool kOPL, int kWaves, bool kPointSrc = false>
+// kFixed: pass 2 of RayWave (chain_ray_tab's fixed output set)
+template <bool kGrid, bool kOPL, int kWaves, bool kPointSrc = false, bool kFixed = false>
 __global__ void __launch_bounds__(kBlock, kWaves) k_chain_sink(ChainArgs a) {
     stage_copy(a);
     __shared__ LeafLds<5> L;
@@ -712,7 +723,7 @@ __global__ void __launch_bounds__(kBlock, kWaves) k_chain_sink(ChainArgs a) {
     for (int64_t seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
         const bool valid = seg * kLeafSeg + t < a.n;
         double qv[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-        if (valid) chain_ray<kGrid, kOPL, true, false, false, kPointSrc>(a, seg * kLeafSeg, t, fl, qv);
+        if (valid) chain_ray<kGrid, kOPL, true, false, false, kPointSrc, kFixed>(a, seg * kLeafSeg, t, fl, qv);
         leaf_sink_segment<5>(a.sink, L, seg * kLeafSeg, qv, valid);
     }
     if (fl) atomicOr(a.flags, fl);
@@ -1151,9 +1162,14 @@ static void launch_chain(int w, unsigned g, hipStream_t s, const ChainArgs& a) {
     }
     // rays from the point source: the variant without origin loads (grid rays only)
     const bool point = kGrid && a.org == nullptr;
+    // RayWave's pass 2: exactly the last hit, exit direction and OPL rows
+    const bool fixed = kGrid && kOPL && point && a.last_hit && a.dir_out && a.opl && !a.det_out && !a.atan_h &&
+                       !a.atan_v && !a.samp_h && !a.samp_v && !a.hits;
 #define AKB_CHAIN_CASE(W)                                                        \
     case W:                                                                      \
-        if (kSink && point)                                                      \
+        if (kSink && fixed)                                                      \
+            k_chain_sink<kGrid, kOPL, W, kGrid, kGrid && kOPL><<<g, kBlock, 0, s>>>(a); \
+        else if (kSink && point)                                                 \
             k_chain_sink<kGrid, kOPL, W, kGrid><<<g, kBlock, 0, s>>>(a);         \
         else if (kSink)                                                          \
             k_chain_sink<kGrid, kOPL, W, false><<<g, kBlock, 0, s>>>(a);         \
@@ -1328,12 +1344,10 @@ static int chain_args_from(const akb_chain_desc* d, ChainArgs& a, bool& empty) {
         return AKB_OK;
     }
     a.K = d->n_mirrors;
-    a.negmask = 0;
     for (int k = 0; k < d->n_mirrors; ++k) {
         const double* c = d->coeffs[k];
         a.q[k] = CMirror{c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7], c[8], c[9],
-                         2.0 * c[0], 2.0 * c[1], 2.0 * c[2]};
-        if (d->negative[k]) a.negmask |= 1 << k;
+                         2.0 * c[0], 2.0 * c[1], 2.0 * c[2], d->negative[k] ? -1.0 : 1.0};
         // the sparse kinds need the constant term of the vanishing gradient component to be +0.0
         if (c[1] == 0.0 && c[3] == 0.0 && c[5] == 0.0 && c[7] == 0.0 && !std::signbit(c[7]))
             a.kind[k] = kKindYFree;
