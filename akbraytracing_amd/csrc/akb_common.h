@@ -80,6 +80,14 @@ struct V3Out {
     }
 };
 
+// base[off / 8] for a byte offset that fits 32 bits: the access takes a scalar (wave-uniform) base
+// plus a 32-bit lane offset (global_load / global_store saddr form) instead of a per-lane 64-bit
+// address formed with 64-bit vector adds
+__device__ __forceinline__ double ld_off(const double* base, uint32_t off) {
+    return *(const double*)((const char*)base + off);
+}
+__device__ __forceinline__ void st_off(double* base, uint32_t off, double v) { *(double*)((char*)base + off) = v; }
+
 struct Quadric {
     double a, b, c, d, e, f, g, h, i, j;
 };
@@ -100,6 +108,30 @@ __device__ __forceinline__ double div_shared(double x, double s, double inv) {
     const double r = __builtin_fma(-s, q, x);
     return r == 0.0 ? q : __builtin_fma(r, inv, q);
 }
+
+// The in-range cores of sqrt_cr and norm3_inv below (no range test of their own).
+__device__ __forceinline__ double sqrt_core(double x) {
+    const double r = __builtin_amdgcn_rsq(x);
+    double g = x * r;
+    double h = r * 0.5;
+    const double e = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, e, g);
+    const double d = __builtin_fma(-g, g, x);
+    h = __builtin_fma(h, e, h);
+    g = __builtin_fma(d, h, g);
+    const double d2 = __builtin_fma(-g, g, x);
+    return __builtin_fma(d2, h, g);
+}
+__device__ __forceinline__ double rcp_core(double s) {
+    double y0 = __builtin_amdgcn_rcp(s);
+    double e0 = __builtin_fma(-s, y0, 1.0);
+    y0 = __builtin_fma(y0, e0, y0);
+    e0 = __builtin_fma(-s, y0, 1.0);
+    y0 = __builtin_fma(y0, e0, y0);
+    const double r1 = __builtin_fma(-s, y0, 1.0);  // q = 1 * y0 = y0
+    return __builtin_fma(r1, y0, y0);
+}
+__device__ __forceinline__ bool in_fast_range(double v) { return v >= 0x1p-767 && v <= 0x1p+1000; }
 
 // Correctly rounded square root without the tiny-input rescaling. hipcc's sqrt(double) on gfx950
 // scales inputs below 2^-767 by 2^256 (cmp, cndmask, ldexp in; cndmask, ldexp out; class test for
@@ -207,15 +239,24 @@ __device__ __forceinline__ void norm3_inv_unit(double x, double y, double z, dou
 // occupying registers across the whole trace loop
 __device__ __attribute__((noinline)) static double atan_lib(double x) { return atan(x); }
 
+// fma(a, b, c) as one VOP3 v_fma_f64 with every operand in a VGPR: for a loop-invariant c (a
+// polynomial coefficient) the compiler otherwise picks the two-address v_fmac_f64 and copies c into
+// the destination first, one v_mov_b64 per term
+__device__ __forceinline__ double fma3(double a, double b, double c) {
+    double r;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
 __device__ __forceinline__ double atan_slope(double x) {
     if (__builtin_expect(fabs(x) <= 0x1p-4, 1)) {
         const double z = x * x;
         double P = 1.0 / 13.0;
-        P = __builtin_fma(z, P, -1.0 / 11.0);
-        P = __builtin_fma(z, P, 1.0 / 9.0);
-        P = __builtin_fma(z, P, -1.0 / 7.0);
-        P = __builtin_fma(z, P, 1.0 / 5.0);
-        P = __builtin_fma(z, P, -1.0 / 3.0);
+        P = fma3(z, P, -1.0 / 11.0);
+        P = fma3(z, P, 1.0 / 9.0);
+        P = fma3(z, P, -1.0 / 7.0);
+        P = fma3(z, P, 1.0 / 5.0);
+        P = fma3(z, P, -1.0 / 3.0);
         return __builtin_fma(x * z, P, x);
     }
     return atan_lib(x);

@@ -31,17 +31,8 @@ constexpr int kTPL = 2;        // targets per lane
 // sqrt_cr's core (akb_common.h) for x in [2^-767, 2^1000] — every distance between points metres
 // apart — and 0 for x = 0 (a target on a source, where the reference's amplitude is inf too);
 // anything else (never formed here) would come out NaN
-__device__ __forceinline__ double sqrt_core(double x) {
-    const double r = __builtin_amdgcn_rsq(x);
-    double g = x * r;
-    double h = r * 0.5;
-    const double e = __builtin_fma(-h, g, 0.5);
-    g = __builtin_fma(g, e, g);
-    const double d = __builtin_fma(-g, g, x);
-    h = __builtin_fma(h, e, h);
-    g = __builtin_fma(d, h, g);
-    const double d2 = __builtin_fma(-g, g, x);
-    const double out = __builtin_fma(d2, h, g);
+__device__ __forceinline__ double sqrt_pair(double x) {
+    const double out = sqrt_core(x);
     return x == 0.0 ? 0.0 : out;
 }
 
@@ -122,7 +113,7 @@ __global__ void __launch_bounds__(kHuyBlock) k_huygens(const double* __restrict_
                 const double dx = px[t] - xj;
                 const double dy = py[t] - yj;
                 const double dz = pz[t] - zj;
-                const double r = sqrt_core(dx * dx + dy * dy + dz * dz);
+                const double r = sqrt_pair(dx * dx + dy * dy + dz * dz);
                 double amp = __builtin_amdgcn_rcp(r);
                 amp = __builtin_fma(amp, __builtin_fma(-r, amp, 1.0), amp);
                 const double ph = negk * r;

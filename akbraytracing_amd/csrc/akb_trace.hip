@@ -338,15 +338,18 @@ struct TiltIn {
 };
 
 // the same with the OPL row known to be present (no load under a branch: the fused kernel's wait
-// counts then stay exact across both paths)
-__device__ __forceinline__ void tilt_load_all(const TiltArgs& a, int64_t i, TiltIn& t) {
-    t.d[0] = a.dir[i];
-    t.d[1] = a.dir[a.ld + i];
-    t.d[2] = a.dir[2 * a.ld + i];
-    t.p[0] = a.pt[i];
-    t.p[1] = a.pt[a.ld + i];
-    t.p[2] = a.pt[2 * a.ld + i];
-    t.o = a.opl[i];
+// counts then stay exact across both paths), for ray i0 + off / 8 of a segment starting at the
+// wave-uniform i0: scalar row bases plus one 32-bit lane offset
+__device__ __forceinline__ void tilt_load_seg(const TiltArgs& a, int64_t i0, uint32_t off, TiltIn& t) {
+    const double* d = a.dir + i0;
+    const double* p = a.pt + i0;
+    t.d[0] = ld_off(d, off);
+    t.d[1] = ld_off(d + a.ld, off);
+    t.d[2] = ld_off(d + 2 * a.ld, off);
+    t.p[0] = ld_off(p, off);
+    t.p[1] = ld_off(p + a.ld, off);
+    t.p[2] = ld_off(p + 2 * a.ld, off);
+    t.o = ld_off(a.opl + i0, off);
 }
 
 __device__ __forceinline__ void tilt_load(const TiltArgs& a, int64_t i, TiltIn& t) {
@@ -439,7 +442,7 @@ __device__ __forceinline__ void stage_copy(const ChainArgs& a) {
 
 // row / column of flat grid index g without a 64-bit division: q = (t + ((g - t) >> 1)) >> (s - 1)
 // with t = mulhi(g, m'), exact for every 32-bit g (Granlund & Montgomery 1994, fig. 4.1)
-__device__ __forceinline__ void grid_rc(const ChainArgs& a, int64_t g, int64_t& iv, int64_t& ih) {
+__device__ __forceinline__ void grid_rc(const ChainArgs& a, int64_t g, uint32_t& iv, uint32_t& ih) {
     const uint32_t g32 = (uint32_t)g;
     uint32_t q;
     if (a.n_h == 1) {
@@ -448,14 +451,45 @@ __device__ __forceinline__ void grid_rc(const ChainArgs& a, int64_t g, int64_t& 
         const uint32_t t = __umulhi(g32, a.div_mul);
         q = (t + ((g32 - t) >> 1)) >> (a.div_shift - 1);
     }
-    iv = (int64_t)q;
-    ih = g - iv * (int64_t)a.n_h;
+    iv = q;
+    ih = g32 - q * a.n_h;  // exact: the grid holds fewer than 2^32 rays
 }
 
 // trace flags are raised per wave: the condition's lane mask lands in scalar registers and only a
 // wave that holds a flagged ray touches the flag word (no per-lane select / or in the common case)
 __device__ __forceinline__ void wave_flag(bool cond, int bit, int& fl) {
     if (__ballot(cond)) fl |= bit;
+}
+
+// sqrt_cr of a discriminant with the miss flag !(D > 0). Every lane takes the fast core; only a wave
+// holding a lane outside its range (a uniform branch) runs the library sqrt, selects it for those
+// lanes and evaluates the miss test - an input inside the range is positive, so a wave without such
+// a lane cannot miss, and the common case spends two compares on the range and none on the flag.
+__device__ __forceinline__ double sqrt_disc(double D, int bit, int& fl) {
+    const bool in = in_fast_range(D);
+    double s = sqrt_core(D);
+    if (__builtin_expect(__ballot(!in) != 0, 0)) {
+        const double sl = sqrt(D);
+        s = in ? s : sl;
+        wave_flag(!(D > 0.0), bit, fl);
+    }
+    return s;
+}
+
+// norm3_inv with its zero flag in the same form: a squared norm inside the fast range is positive
+__device__ __forceinline__ void norm3_inv_flag(double x, double y, double z, double& s, double& inv, int bit,
+                                               int& fl) {
+    const double v = x * x + y * y + z * z;
+    const bool in = in_fast_range(v);
+    s = sqrt_core(v);
+    inv = rcp_core(s);
+    if (__builtin_expect(__ballot(!in) != 0, 0)) {
+        const double sl = sqrt(v);
+        const double il = 1.0 / sl;
+        s = in ? s : sl;
+        inv = in ? inv : il;
+        wave_flag(s == 0.0, bit, fl);
+    }
 }
 
 struct Ray {
@@ -493,8 +527,7 @@ __device__ __forceinline__ void mirror_step(const CMirror& Q, Ray& R, double& op
             Q.h * q + Q.i * r + Q.j;
     }
     const double D = B * B - 4.0 * A * C;
-    wave_flag(!(D > 0.0), AKB_FLAG_MISS << (4 * k), fl);
-    const double sD = sqrt_cr(D);
+    const double sD = sqrt_disc(D, AKB_FLAG_MISS << (4 * k), fl);
     const double t = (-B + sD * Q.sgn) / (2.0 * A);  // (-B - sD) / (2A) for the minus root
     const double x = t * l + p, y = t * m + q, z = t * n + r;
     if (kOPL) opl = opl + norm3(x - p, y - q, z - r);  // opl starts at +0.0: 0 + d is d exactly
@@ -510,21 +543,21 @@ __device__ __forceinline__ void mirror_step(const CMirror& Q, Ray& R, double& op
     }
     // unit normal
     double nx, ny = 0.0, nz = 0.0, sn, in;
+    const int zbit = AKB_FLAG_ZERO_NORMAL << (4 * k);
     if (kKind == kKindYFree) {
         nx = Q.a2 * x + Q.e * z + Q.g;
         nz = Q.c2 * z + Q.e * x + Q.i;
-        norm3_inv(nx, 0.0, nz, sn, in);
+        norm3_inv_flag(nx, 0.0, nz, sn, in, zbit, fl);
     } else if (kKind == kKindZFree) {
         nx = Q.a2 * x + Q.d * y + Q.g;
         ny = Q.b2 * y + Q.d * x + Q.h;
-        norm3_inv(nx, ny, 0.0, sn, in);
+        norm3_inv_flag(nx, ny, 0.0, sn, in, zbit, fl);
     } else {
         nx = Q.a2 * x + Q.d * y + Q.e * z + Q.g;
         ny = Q.b2 * y + Q.d * x + Q.f * z + Q.h;
         nz = Q.c2 * z + Q.e * x + Q.f * y + Q.i;
-        norm3_inv(nx, ny, nz, sn, in);
+        norm3_inv_flag(nx, ny, nz, sn, in, zbit, fl);
     }
-    wave_flag(sn == 0.0, AKB_FLAG_ZERO_NORMAL << (4 * k), fl);
     nx = div_pos(nx, sn, in);
     if (kKind != kKindYFree) ny = div_pos(ny, sn, in);
     if (kKind != kKindZFree) nz = div_pos(nz, sn, in);
@@ -552,8 +585,7 @@ __device__ __forceinline__ void mirror_step(const CMirror& Q, Ray& R, double& op
         norm3_inv_unit(rx, ry, rz, sr, ir, zero);
         wave_flag(zero, AKB_FLAG_ZERO_REFLECT << (4 * k), fl);
     } else {
-        norm3_inv(rx, ry, rz, sr, ir);
-        wave_flag(sr == 0.0, AKB_FLAG_ZERO_REFLECT << (4 * k), fl);
+        norm3_inv_flag(rx, ry, rz, sr, ir, AKB_FLAG_ZERO_REFLECT << (4 * k), fl);
     }
     R.l = div_pos(rx, sr, ir);
     R.m = div_pos(ry, sr, ir);
@@ -573,11 +605,11 @@ struct NoHook {
 };
 
 // grid position and direction-table entries of flat ray i of a launch
-__device__ __forceinline__ void ray_tables(const ChainArgs& a, int64_t i, int64_t& iv, int64_t& ih, double& th,
+__device__ __forceinline__ void ray_tables(const ChainArgs& a, int64_t i, uint32_t& iv, uint32_t& ih, double& th,
                                            double& tv) {
     grid_rc(a, a.g0 + i * a.g_stride, iv, ih);
-    th = a.tan_h[ih];
-    tv = a.tan_v[iv];
+    th = ld_off(a.tan_h, ih << 3);  // the tables hold fewer than 2^29 entries (checked on the host)
+    tv = ld_off(a.tan_v, iv << 3);
 }
 
 // One ray through the chain: ray i = i0 + t of a segment starting at the wave-uniform i0, t the
@@ -600,7 +632,7 @@ __device__ __forceinline__ void ray_tables(const ChainArgs& a, int64_t i, int64_
 // tests' masks were what overflowed the scalar registers into VGPR lanes).
 template <bool kGrid, bool kOPL, bool kNeedQ, bool kHits = false, bool kLean = false, bool kPointSrc = kLean,
           bool kFixed = false, class Post = NoHook>
-__device__ __forceinline__ void chain_ray_tab(const ChainArgs& a, int64_t i0, int t, int64_t iv, int64_t ih,
+__device__ __forceinline__ void chain_ray_tab(const ChainArgs& a, int64_t i0, int t, uint32_t iv, uint32_t ih,
                                               double th, double tv, int& fl, double (&qv)[5], Post post = Post()) {
     const int64_t i = i0 + t;
     const int64_t g = a.g0 + i * a.g_stride;
@@ -609,8 +641,7 @@ __device__ __forceinline__ void chain_ray_tab(const ChainArgs& a, int64_t i0, in
     if (kGrid) {
         // phai0[:, iv*n_h + ih] = (1, tan(p0h[ih]), tan(p0v[iv])) normalised (ref :2711-2717)
         double s, inv;
-        norm3_inv(1.0, th, tv, s, inv);
-        wave_flag(s == 0.0, AKB_FLAG_CHAIN_DIR, fl);
+        norm3_inv_flag(1.0, th, tv, s, inv, AKB_FLAG_CHAIN_DIR, fl);
         R.l = inv;  // = RN(1/s): also the shared reciprocal
         R.m = div_pos(th, s, inv);
         R.n = div_pos(tv, s, inv);
@@ -644,22 +675,24 @@ __device__ __forceinline__ void chain_ray_tab(const ChainArgs& a, int64_t i0, in
     const double l = R.l, m = R.m, nn = R.n, p = R.p, q = R.q, r = R.r;
     if (kOPL && kGrid && a.pert_h) {  // figure-error perturbation of the path (BASELINE config 5)
         double d = 0.0;
-        for (int k = 0; k < a.pert_terms; ++k) d = __builtin_fma(a.pert_v[k * a.n_v + iv], a.pert_h[k * a.n_h + ih], d);
+        for (int k = 0; k < a.pert_terms; ++k)
+            d = __builtin_fma(a.pert_v[(int64_t)k * a.n_v + iv], a.pert_h[(int64_t)k * a.n_h + ih], d);
         opl = opl + d;
     }
     post();
-    if (kOPL && (kFixed || a.opl)) (a.opl + i0)[t] = opl;
+    const uint32_t off = (uint32_t)t << 3;
+    if (kOPL && (kFixed || a.opl)) st_off(a.opl + i0, off, opl);
     if (!kLean && (kFixed || a.last_hit)) {
         double* o = a.last_hit + i0;
-        o[t] = p;
-        (o + a.last_hit_ld)[t] = q;
-        (o + 2 * a.last_hit_ld)[t] = r;
+        st_off(o, off, p);
+        st_off(o + a.last_hit_ld, off, q);
+        st_off(o + 2 * a.last_hit_ld, off, r);
     }
     if (!kLean && (kFixed || a.dir_out)) {
         double* o = a.dir_out + i0;
-        o[t] = l;
-        (o + a.dir_out_ld)[t] = m;
-        (o + 2 * a.dir_out_ld)[t] = nn;
+        st_off(o, off, l);
+        st_off(o + a.dir_out_ld, off, m);
+        st_off(o + 2 * a.dir_out_ld, off, nn);
     }
     if (kNeedQ || (!kLean && !kFixed && a.det_out)) {
         double x, y, z;
@@ -692,7 +725,7 @@ __device__ __forceinline__ void chain_ray_tab(const ChainArgs& a, int64_t i0, in
 template <bool kGrid, bool kOPL, bool kNeedQ, bool kHits = false, bool kLean = false, bool kPointSrc = kLean,
           bool kFixed = false>
 __device__ __forceinline__ void chain_ray(const ChainArgs& a, int64_t i0, int t, int& fl, double (&qv)[5]) {
-    int64_t iv = 0, ih = 0;
+    uint32_t iv = 0, ih = 0;
     double th = 0.0, tv = 0.0;
     if (kGrid) ray_tables(a, i0 + t, iv, ih, th, tv);
     chain_ray_tab<kGrid, kOPL, kNeedQ, kHits, kLean, kPointSrc, kFixed>(a, i0, t, iv, ih, th, tv, fl, qv);
@@ -947,11 +980,12 @@ struct OpdRows {
 struct OpdIn {
     double t2, x, y, z;
 };
-__device__ __forceinline__ void opd_load(const OpdRows& o, int64_t ld, int64_t i, OpdIn& v) {
-    v.t2 = o.t2[i];
-    v.x = o.det2[i];
-    v.y = o.det2[ld + i];
-    v.z = o.det2[2 * ld + i];
+__device__ __forceinline__ void opd_load(const OpdRows& o, int64_t ld, int64_t i0, uint32_t off, OpdIn& v) {
+    const double* d = o.det2 + i0;
+    v.t2 = ld_off(o.t2 + i0, off);
+    v.x = ld_off(d, off);
+    v.y = ld_off(d + ld, off);
+    v.z = ld_off(d + 2 * ld, off);
 }
 
 // the workgroup's four extents (max y, -y, z, -z) folded into the device keys (thread-uniform
@@ -1008,12 +1042,12 @@ __global__ void __launch_bounds__(kBlock, kWaves) k_chain_tilt(ChainArgs a, Tilt
     int64_t seg = blockIdx.x;
     // software pipeline: segment s's table entries and tilt inputs were loaded during segment
     // s - gridDim's stores, leaf sums and mirror loop
-    int64_t iv = 0, ih = 0;
+    uint32_t iv = 0, ih = 0;
     double th = 0.0, tv = 0.0;
     TiltIn in;
     if (seg < nseg && seg * kLeafSeg + t < a.n) {
         ray_tables(a, seg * kLeafSeg + t, iv, ih, th, tv);
-        tilt_load_all(b, seg * kLeafSeg + t, in);
+        tilt_load_seg(b, seg * kLeafSeg, (uint32_t)t << 3, in);
     }
     for (; seg < nseg; seg += gridDim.x) {
         // the thread index made opaque per segment: addresses derived from it are formed where
@@ -1023,17 +1057,19 @@ __global__ void __launch_bounds__(kBlock, kWaves) k_chain_tilt(ChainArgs a, Tilt
         asm volatile("" : "+v"(t));
         const int64_t i0 = seg * kLeafSeg;
         const bool valid = i0 + t < a.n;
-        const int64_t nxt = (seg + gridDim.x) * kLeafSeg + t;
+        const int64_t n0 = (seg + gridDim.x) * kLeafSeg;  // the next segment (wave-uniform)
+        const int64_t nxt = n0 + t;
+        const uint32_t off = (uint32_t)t << 3;
         double d2[3], tq[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
         if (valid)
             chain_ray_tab<true, false, false, false, true, true>(a, i0, t, iv, ih, th, tv, fl, qv, [&] {
                 OpdIn oin;
-                if constexpr (kOPD) opd_load(o, b.ld, i0 + t, oin);
+                if constexpr (kOPD) opd_load(o, b.ld, i0, off, oin);
                 tilt_compute(b, in, d2, tq);
                 if constexpr (kOPD) {  // k_opd's arithmetic, in its order
                     const double oe2 = (oin.t2 - om[3]) * 1e9;
-                    (o.e2 + i0)[t] = oe2;
-                    (o.wave + i0)[t] = oe2 - norm3(oin.x - om[0], oin.y - om[1], oin.z - om[2]) * 1e9;
+                    st_off(o.e2 + i0, off, oe2);
+                    st_off(o.wave + i0, off, oe2 - norm3(oin.x - om[0], oin.y - om[1], oin.z - om[2]) * 1e9);
                     oe[0][t] = fmax(oe[0][t], oin.y);
                     oe[1][t] = fmax(oe[1][t], -oin.y);
                     oe[2][t] = fmax(oe[2][t], oin.z);
@@ -1041,15 +1077,15 @@ __global__ void __launch_bounds__(kBlock, kWaves) k_chain_tilt(ChainArgs a, Tilt
                 }
                 if (nxt < a.n) {
                     ray_tables(a, nxt, iv, ih, th, tv);
-                    tilt_load_all(b, nxt, in);
+                    tilt_load_seg(b, n0, off, in);
                 }
             });
         if (valid) {  // detector-2 rows only (detector 1 and the rotated rays are the full mode's)
             double* r = b.det2 + i0;
-            r[t] = d2[0];
-            (r + b.ld)[t] = d2[1];
-            (r + 2 * b.ld)[t] = d2[2];
-            (b.total2 + i0)[t] = tq[4];
+            st_off(r, off, d2[0]);
+            st_off(r + b.ld, off, d2[1]);
+            st_off(r + 2 * b.ld, off, d2[2]);
+            st_off(b.total2 + i0, off, tq[4]);
         }
         leaf_sink_segment<5>(b.sink, L, i0, tq, valid, t);
     }
@@ -1123,13 +1159,20 @@ using namespace akb;
 static inline V3In v3in(const double* p, int64_t ld, int64_t inc) { return V3In{p, ld, inc}; }
 
 // occupancy variant of the chain kernels (minimum waves per SIMD the register allocator must
-// allow); AKB_CHAIN_WAVES in the environment selects one for A/B timing, default 4
+// allow); AKB_CHAIN_WAVES in the environment selects one for A/B timing, default 4. RayWave's pass
+// 2 (the fixed-output sink variant) has its own knob, AKB_PASS2_WAVES, default 6 (measured in the
+// pipelined bench: 4 and 6 equal at 0.396 ms, 8 - 64 VGPRs and 160 B of spills - 0.407 ms)
+static int waves_from_env(const char* name, int dflt) {
+    const char* e = getenv(name);
+    const int v = e ? atoi(e) : dflt;
+    return (v == 2 || v == 4 || v == 6 || v == 8) ? v : dflt;
+}
 static int chain_waves() {
-    static int w = [] {
-        const char* e = getenv("AKB_CHAIN_WAVES");
-        const int v = e ? atoi(e) : 4;
-        return (v == 2 || v == 4 || v == 8) ? v : 4;
-    }();
+    static int w = waves_from_env("AKB_CHAIN_WAVES", 4);
+    return w;
+}
+static int pass2_waves() {
+    static int w = waves_from_env("AKB_PASS2_WAVES", 6);
     return w;
 }
 
@@ -1165,11 +1208,22 @@ static void launch_chain(int w, unsigned g, hipStream_t s, const ChainArgs& a) {
     // RayWave's pass 2: exactly the last hit, exit direction and OPL rows
     const bool fixed = kGrid && kOPL && point && a.last_hit && a.dir_out && a.opl && !a.det_out && !a.atan_h &&
                        !a.atan_v && !a.samp_h && !a.samp_v && !a.hits;
+    if (kSink && fixed) {
+        switch (pass2_waves()) {
+            case 4:
+                k_chain_sink<kGrid, kOPL, 4, kGrid, kGrid && kOPL><<<g, kBlock, 0, s>>>(a);
+                break;
+            case 6:
+                k_chain_sink<kGrid, kOPL, 6, kGrid, kGrid && kOPL><<<g, kBlock, 0, s>>>(a);
+                break;
+            default:
+                k_chain_sink<kGrid, kOPL, 8, kGrid, kGrid && kOPL><<<g, kBlock, 0, s>>>(a);
+        }
+        return;
+    }
 #define AKB_CHAIN_CASE(W)                                                        \
     case W:                                                                      \
-        if (kSink && fixed)                                                      \
-            k_chain_sink<kGrid, kOPL, W, kGrid, kGrid && kOPL><<<g, kBlock, 0, s>>>(a); \
-        else if (kSink && point)                                                 \
+        if (kSink && point)                                                      \
             k_chain_sink<kGrid, kOPL, W, kGrid><<<g, kBlock, 0, s>>>(a);         \
         else if (kSink)                                                          \
             k_chain_sink<kGrid, kOPL, W, false><<<g, kBlock, 0, s>>>(a);         \
@@ -1327,6 +1381,7 @@ static int chain_args_from(const akb_chain_desc* d, ChainArgs& a, bool& empty) {
         AKB_REQUIRE(d->row0 >= 0 && d->row0 * d->n_h + d->n_rays <= d->n_h * d->n_v,
                     "shard exceeds the ray grid");
         AKB_REQUIRE(d->n_h * d->n_v < (1LL << 32), "ray grid beyond 2^32 rays");
+        AKB_REQUIRE(d->n_h < (1LL << 29) && d->n_v < (1LL << 29), "angle tables beyond 2^29 entries");
     }
     if (d->samp_v) AKB_REQUIRE(grid && d->samp_v_col >= 0 && d->samp_v_col < d->n_h, "bad samp_v_col");
     if (d->pert_h)
@@ -1644,6 +1699,9 @@ static int chain_tilt(const akb_chain_desc* d, const double* d_params, const dou
     switch (chain_waves()) {
         case 2:
             AKB_CT(2)
+            break;
+        case 6:
+            AKB_CT(6)
             break;
         case 8:
             AKB_CT(8)
