@@ -19,7 +19,7 @@ c_int = ctypes.c_int
 c_dbl = ctypes.c_double
 c_vp = ctypes.c_void_p
 MAX_MIRRORS = 7
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 FLAG_MISS = 0x1
 FLAG_ZERO_NORMAL = 0x2
@@ -38,6 +38,7 @@ EXPORTS = [
     "akb_calc_ds_f64",
     "akb_pairwise_work_bytes", "akb_pairwise_sum_f64", "akb_pupil_sample_f64",
     "akb_leaf_sink_bytes", "akb_leaf_sink_layout", "akb_leaf_finish_work_bytes", "akb_leaf_finish_f64",
+    "akb_leaf_parts_f64", "akb_parts_chain_f64",
     "akb_huygens_work_bytes", "akb_huygens_f64", "akb_scale_field_f64",
     "akb_psf_work_bytes", "akb_psf_f64", "akb_psf_release_plans", "akb_selftest_arith_f64",
     "akb_first_valid_rows_f64", "akb_rotate_work_bytes", "akb_rotate_with_nan_f64",
@@ -63,7 +64,7 @@ class ChainDesc(ctypes.Structure):
         ("det_ghij", c_dbl * 4),
         ("dir", c_vp), ("dir_ld", c_i64), ("dir_inc", c_i64),
         ("tan_h", c_vp), ("tan_v", c_vp), ("n_h", c_i64), ("n_v", c_i64),
-        ("row0", c_i64),
+        ("ray0", c_i64),
         ("n_rays", c_i64),
         ("org", c_vp), ("org_ld", c_i64), ("org_inc", c_i64),
         ("src", c_dbl * 3),
@@ -125,6 +126,8 @@ def _declare(L):
         "akb_leaf_sink_layout": ([c_vp, c_int, c_int, c_i64, ctypes.POINTER(LeafSink)], c_int),
         "akb_leaf_finish_work_bytes": ([c_int, c_i64], c_i64),
         "akb_leaf_finish_f64": ([ctypes.POINTER(LeafSink), c_vp, c_vp, c_vp, c_vp], c_int),
+        "akb_leaf_parts_f64": ([ctypes.POINTER(LeafSink), c_vp, c_vp, c_int, c_vp, c_vp, c_vp], c_int),
+        "akb_parts_chain_f64": ([c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp], c_int),
         "akb_pairwise_work_bytes": ([c_int, c_i64], c_i64),
         "akb_pairwise_sum_f64": ([c_vp, c_i64, c_int, c_i64, c_int, c_vp, c_vp, c_vp, c_vp], c_int),
         "akb_huygens_work_bytes": ([c_i64, c_i64], c_i64),

@@ -445,4 +445,44 @@ int akb_leaf_finish_f64(const akb_leaf_sink* sink, double* d_sum, int64_t* d_cou
     return launch_status("k_pw_final");
 }
 
+int akb_leaf_parts_f64(const akb_leaf_sink* sink, double* d_part, int64_t* d_part_cnt, int part_ld,
+                       double* d_tail_sum, int64_t* d_tail_cnt, void* stream) {
+    clear_error();
+    AKB_REQUIRE(sink && d_part && d_part_cnt && d_tail_sum && d_tail_cnt, "null pointer");
+    AKB_REQUIRE(sink->nq > 0 && sink->nq <= 4096 && sink->n >= 0, "bad sink");
+    const int64_t nfull = sink->n / kPwBuf;
+    const int tail = (int)(sink->n - nfull * kPwBuf);
+    AKB_REQUIRE(part_ld >= nfull && part_ld >= 1, "part_ld below the sink's full buffers");
+    hipStream_t s = (hipStream_t)stream;
+    const int nq = sink->nq;
+    if (nfull > 0) {
+        k_leaf_chunks<<<dim3((unsigned)nfull, nq), 64, 0, s>>>(sink->leaf_sum, sink->leaf_cnt,
+                                                                nfull * (kPwBuf / kPwLeaf), part_ld, d_part,
+                                                                (long long*)d_part_cnt);
+        int st = launch_status("k_leaf_chunks");
+        if (st) return st;
+    }
+    if (tail == 0) {
+        AKB_HIP_CHECK(hipMemsetAsync(d_tail_sum, 0, sizeof(double) * nq, s));
+        AKB_HIP_CHECK(hipMemsetAsync(d_tail_cnt, 0, sizeof(int64_t) * nq, s));
+        return AKB_OK;
+    }
+    // the short buffer alone: k_pw_final with no full buffers gives its pairwise sum and count
+    k_pw_final<<<nq, kPwThreads, final_lds(1, tail), s>>>(d_part, (const long long*)d_part_cnt, part_ld, 0,
+                                                         sink->tail, kPwBuf, tail, sink->nan_mask, d_tail_sum,
+                                                         d_tail_cnt, 1);
+    return launch_status("k_pw_final (tail)");
+}
+
+int akb_parts_chain_f64(const double* d_part, const int64_t* d_part_cnt, int part_ld, int nq, int nparts,
+                        double* d_sum, int64_t* d_count, void* stream) {
+    clear_error();
+    AKB_REQUIRE(d_part && d_part_cnt && d_sum && d_count, "null pointer");
+    AKB_REQUIRE(nq > 0 && nq <= 65535 && nparts >= 1 && part_ld >= nparts, "bad sizes");
+    const int tile = final_tile(nparts);
+    k_pw_final<<<nq, kPwThreads, final_lds(tile, 0), (hipStream_t)stream>>>(
+        d_part, (const long long*)d_part_cnt, part_ld, nparts, nullptr, 0, 0, 0, d_sum, d_count, tile);
+    return launch_status("k_pw_final (chain)");
+}
+
 }  // extern "C"

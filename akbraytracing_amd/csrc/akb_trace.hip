@@ -1129,7 +1129,7 @@ __global__ void __launch_bounds__(kBlock) k_opd(OpdArgs a) {
     if (a.ext) extents_commit(e, a.ext);
 }
 
-__global__ void __launch_bounds__(kBlock) k_pupil(const double* wave, int64_t row0, int64_t rows, int64_t n,
+__global__ void __launch_bounds__(kBlock) k_pupil(const double* wave, int64_t ray0, int64_t nrays, int64_t n,
                                                   int size, const unsigned long long* ext, double* opd,
                                                   double* pitch) {
     const int64_t total = (int64_t)size * size;
@@ -1139,7 +1139,8 @@ __global__ void __launch_bounds__(kBlock) k_pupil(const double* wave, int64_t ro
         const int64_t iv = ((int64_t)ky * (n - 1)) / (size - 1);
         const int64_t ih = ((int64_t)kx * (n - 1)) / (size - 1);
         double v = 0.0;
-        if (iv >= row0 && iv < row0 + rows) v = wave[(iv - row0) * n + ih] * 1e-9;
+        const int64_t g = iv * n + ih;
+        if (g >= ray0 && g < ray0 + nrays) v = wave[g - ray0] * 1e-9;
         opd[k] = v;
     }
     if (pitch && blockIdx.x == 0 && threadIdx.x == 0) {
@@ -1378,7 +1379,7 @@ static int chain_args_from(const akb_chain_desc* d, ChainArgs& a, bool& empty) {
     const bool grid = d->dir == nullptr;
     if (grid) {
         AKB_REQUIRE(d->tan_h && d->tan_v && d->n_h > 0 && d->n_v > 0, "grid tables missing");
-        AKB_REQUIRE(d->row0 >= 0 && d->row0 * d->n_h + d->n_rays <= d->n_h * d->n_v,
+        AKB_REQUIRE(d->ray0 >= 0 && d->ray0 + d->n_rays <= d->n_h * d->n_v,
                     "shard exceeds the ray grid");
         AKB_REQUIRE(d->n_h * d->n_v < (1LL << 32), "ray grid beyond 2^32 rays");
         AKB_REQUIRE(d->n_h < (1LL << 29) && d->n_v < (1LL << 29), "angle tables beyond 2^29 entries");
@@ -1420,7 +1421,7 @@ static int chain_args_from(const akb_chain_desc* d, ChainArgs& a, bool& empty) {
     a.n_h = grid ? (uint32_t)d->n_h : 1u;
     a.n_v = grid ? (uint32_t)d->n_v : 1u;
     div_magic(a.n_h, &a.div_mul, &a.div_shift);
-    a.g0 = grid ? d->row0 * d->n_h : 0;
+    a.g0 = grid ? d->ray0 : 0;
     a.g_stride = 1;
     a.n = d->n_rays;
     a.org = d->org;
@@ -1771,15 +1772,15 @@ int akb_opd_f64(const double* total1, const double* total2, const double* det2, 
     return launch_status("k_opd");
 }
 
-int akb_pupil_sample_f64(const double* wave, int64_t row0, int64_t rows, int64_t n, int size,
+int akb_pupil_sample_f64(const double* wave, int64_t ray0, int64_t nrays, int64_t n, int size,
                          const uint64_t* d_extent_keys, double* opd_m, double* d_pitch, void* stream) {
     clear_error();
     AKB_REQUIRE(wave && opd_m, "null pointer");
-    AKB_REQUIRE(size >= 2 && n >= 2 && row0 >= 0 && rows >= 0 && row0 + rows <= n, "bad sizes");
+    AKB_REQUIRE(size >= 2 && n >= 2 && ray0 >= 0 && nrays >= 0 && ray0 + nrays <= n * n, "bad sizes");
     AKB_REQUIRE(!d_pitch || d_extent_keys, "pitch needs the extent keys");
     const int64_t total = (int64_t)size * size;
     k_pupil<<<grid_for(total), kBlock, 0, (hipStream_t)stream>>>(
-        wave, row0, rows, n, size, (const unsigned long long*)d_extent_keys, opd_m, d_pitch);
+        wave, ray0, nrays, n, size, (const unsigned long long*)d_extent_keys, opd_m, d_pitch);
     return launch_status("k_pupil");
 }
 

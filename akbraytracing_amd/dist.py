@@ -72,6 +72,18 @@ class TorchComm:
             t = self._all_reduce(t, dist.ReduceOp.MAX)
         return t
 
+    def allgather_equal(self, t):
+        """(world, *t.shape): every rank's t (same shape on every rank), in rank order."""
+        if self.world == 1:
+            return t.unsqueeze(0)
+        t = t.contiguous()
+        if self._stage and t.is_cuda:
+            return self.allgather_equal(t.cpu()).to(t.device)
+        out = torch.empty((self.world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t) if hasattr(dist, "all_gather_into_tensor") and t.is_cuda else \
+            dist.all_gather(list(out.unbind(0)), t)
+        return out
+
     def gather_samples(self, samp_h, samp_v, shard, n):
         """Each rank holds zeros outside its rows; one SUM all-reduce assembles both pick lists."""
         if self.world == 1:
@@ -80,11 +92,25 @@ class TorchComm:
         buf = self.allreduce_sums(buf).cpu().numpy()
         return buf[:samp_h.shape[0]], buf[samp_h.shape[0]:]
 
-    def sum_flags(self, f):
+    def allreduce_or(self, words):
+        """Bitwise OR of int32 flag words over ranks, in place. RCCL has no bitwise reduction, so
+        each word is unpacked to its 32 bits, the bits are MAX-reduced and packed again (a SUM
+        would carry: two ranks' FLAG_MISS 0x1 would read as FLAG_ZERO_NORMAL 0x2)."""
+        if self.world == 1:
+            return words
+        shifts = torch.arange(32, dtype=torch.int64, device=words.device)
+        bits = (words.to(torch.int64).unsqueeze(-1) >> shifts) & 1
+        bits = self._all_reduce(bits.contiguous(), dist.ReduceOp.MAX)
+        packed = (bits << shifts).sum(-1)
+        words.copy_(torch.where(packed >= 2 ** 31, packed - 2 ** 32, packed).to(words.dtype))
+        return words
+
+    def or_flags(self, f):
+        """One host flag word OR-ed over ranks."""
         if self.world == 1:
             return f
-        t = self._dev(torch.tensor([float(f)], dtype=torch.float64))
-        return int(self.allreduce_sums(t).item())
+        t = self._dev(torch.tensor([int(f)], dtype=torch.int32))
+        return int(self.allreduce_or(t).item())
 
     def barrier(self):
         if self.world > 1:

@@ -128,18 +128,20 @@ def match_legendre_multi(data, order):
     return fits.cpu().numpy(), c.cpu().numpy(), [tuple(o) for o in orders]
 
 
-def wave_maps(detcenter2, dist_err2, wave2, ray_num_H, ray_num_V):
+def wave_maps(detcenter2, dist_err2, wave2, ray_num_H, ray_num_V, grid_num_H=None, grid_num_V=None):
     """The driver's gridding step (AKB_raytrace_20250312.py:3653-3696) on the device:
     grid_H, grid_V = meshgrid(linspace(min, max) of the hits' y / z), matrixDistError2 and
     matrixWave2 by cubic griddata (one triangulation for both), matrixWave2 -= nanmean, then both
     plane-corrected. detcenter2 (3, n), dist_err2 / wave2 (n,) in ray order (n = V * H).
+    grid_num_H / grid_num_V: the output grid's size when it is not the ray grid's (the driver uses
+    ray_num for both; bench.py grids 1e7 hits onto its 128 x 128 pupil).
     Returns a dict of device tensors (the grids as numpy)."""
     from .griddata import CubicGrid
     d2 = _as_dev(detcenter2)
     y, z = d2[1].contiguous(), d2[2].contiguous()
     ext = torch.stack([y.min(), y.max(), z.min(), z.max()]).cpu().numpy()
-    gx = np.linspace(ext[0], ext[1], int(ray_num_H))
-    gy = np.linspace(ext[2], ext[3], int(ray_num_V))
+    gx = np.linspace(ext[0], ext[1], int(grid_num_H or ray_num_H))
+    gy = np.linspace(ext[2], ext[3], int(grid_num_V or ray_num_V))
     grid_H, grid_V = np.meshgrid(gx, gy)
     cg = CubicGrid(y, z, int(ray_num_V), int(ray_num_H))
     vals = torch.stack([_as_dev(dist_err2).reshape(-1), _as_dev(wave2).reshape(-1)])

@@ -81,3 +81,54 @@ class LeafSink:
         _lib.check(L.akb_leaf_finish_f64(self.desc, D.ptr(self.sums), D.ptr(self.counts), D.ptr(self.work),
                                          D.stream_handle(stream)))
         return self.sums, self.counts
+
+    def finish_dist(self, comm, nbufs, n_total, stream=None):
+        """finish() over ranks, bit for bit the single-process result: this rank's shard must be
+        aligned to numpy's 8192-element buffers (wavefront.Shard.split), nbufs[r] the full buffers
+        of rank r. Each rank forms its buffer sums and its short-buffer sum (only the last rank has
+        one), one all-gather brings every rank's to every rank, and the buffer sums are added
+        left to right in grid order, the short buffer last - numpy's order. The
+        counts are integers: their all-reduced sum is exact. n_total: elements over all ranks.
+        stream: a torch stream or a raw hipStream_t handle (default: the current stream); the
+        kernels, the torch ops and the collective all run on it."""
+        if stream is not None and not isinstance(stream, torch.cuda.Stream):
+            h = D.stream_handle(stream).value or 0  # the null stream's handle is NULL
+            if h != torch.cuda.current_stream().cuda_stream:
+                stream = torch.cuda.ExternalStream(h)
+            else:
+                stream = None
+        if stream is not None:
+            with torch.cuda.stream(stream):
+                return self.finish_dist(comm, nbufs, n_total)
+        L = _lib.lib()
+        nq, dev = self.nq, self.sums.device
+        nb_max = max(max(nbufs), 1)
+        sh = D.stream_handle()
+        part = torch.zeros((nq, nb_max), dtype=D.F64, device=dev)
+        pcnt = torch.zeros((nq, nb_max), dtype=torch.int64, device=dev)
+        tsum = torch.empty(nq, dtype=D.F64, device=dev)
+        tcnt = torch.empty(nq, dtype=torch.int64, device=dev)
+        _lib.check(L.akb_leaf_parts_f64(self.desc, D.ptr(part), D.ptr(pcnt), nb_max, D.ptr(tsum), D.ptr(tcnt), sh))
+        # one all-gather of everything (counts travel as float64: exact below 2^53)
+        mine = torch.cat([part.reshape(-1), pcnt.reshape(-1).to(D.F64), tsum, tcnt.to(D.F64)])
+        g = comm.allgather_equal(mine)  # (world, len)
+        w = g.shape[0]
+        m = nq * nb_max
+        g_part = g[:, :m].reshape(w, nq, nb_max)
+        g_pcnt = g[:, m:2 * m].reshape(w, nq, nb_max).to(torch.int64)
+        tail = g[-1, 2 * m:2 * m + nq]  # the grid's short buffer lives on the last rank
+        cnt_t = g[:, 2 * m + nq:].to(torch.int64).sum(dim=0)
+        total = sum(nbufs)
+        if total == 0:
+            self.sums.copy_(tail)
+            self.counts.copy_(cnt_t)
+            return self.sums, self.counts
+        parts = torch.cat([g_part[r, :, :nb] for r, nb in enumerate(nbufs) if nb], dim=1).contiguous()
+        pcnts = torch.cat([g_pcnt[r, :, :nb] for r, nb in enumerate(nbufs) if nb], dim=1).contiguous()
+        acc = torch.empty(nq, dtype=D.F64, device=dev)
+        cnt = torch.empty(nq, dtype=torch.int64, device=dev)
+        _lib.check(L.akb_parts_chain_f64(D.ptr(parts), D.ptr(pcnts), total, nq, total, D.ptr(acc), D.ptr(cnt), sh))
+        # k_pw_final's acc + tail_sum: one IEEE add, the short buffer last
+        self.sums.copy_(acc + tail if int(n_total) % 8192 != 0 else acc)
+        self.counts.copy_(cnt + cnt_t)
+        return self.sums, self.counts

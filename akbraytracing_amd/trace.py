@@ -68,17 +68,18 @@ class ChainLaunch:
 
     def __init__(self, mirrors, *, tan_h=None, tan_v=None, row0=0, n_rays=None, dirs=None, src=(0.0, 0.0, 0.0),
                  det_ghij=None, want=("last_hit", "dir_out"), samples=None, out=None, sink=None, flags=None,
-                 samples_buf=None, pert=None):
+                 samples_buf=None, pert=None, ray0=None):
         dev = D.device()
         desc = _lib.ChainDesc()
         _fill_desc(desc, mirrors, det_ghij)
         self.keep = [tan_h, tan_v, dirs, sink]
         if dirs is None:
             n_h, n_v = tan_h.shape[0], tan_v.shape[0]
-            n = n_h * n_v - row0 * n_h if n_rays is None else n_rays
+            ray0 = row0 * n_h if ray0 is None else int(ray0)
+            n = n_h * n_v - ray0 if n_rays is None else n_rays
             desc.dir = None
             desc.tan_h, desc.tan_v = D.ptr(tan_h), D.ptr(tan_v)
-            desc.n_h, desc.n_v, desc.row0 = n_h, n_v, row0
+            desc.n_h, desc.n_v, desc.ray0 = n_h, n_v, ray0
         else:
             n = dirs.shape[1]
             desc.dir, desc.dir_ld, desc.dir_inc = D.ptr(dirs), n, 1
@@ -171,7 +172,8 @@ class ChainLaunch:
 def trace_chain(mirrors, *, stream=None, **kw):
     """Run one fused chain launch.
 
-    Rays: either the grid (tan_h, tan_v device tensors; rays row0*n_h .. + n_rays) or explicit
+    Rays: either the grid (tan_h, tan_v device tensors; flat rays ray0 .. + n_rays, ray0 defaulting
+    to row0 * n_h) or explicit
     `dirs` (3, n) device tensor. Source: a 3-vector (constant) or a (3, n) device tensor.
     want: subset of {"hits", "last_hit", "dir_out", "det", "opl", "atan"}.
     samples: (h_begin, h_end, v_col) flat-index range / column whose exit slopes to record.

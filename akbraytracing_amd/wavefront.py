@@ -27,7 +27,7 @@ from . import _lib
 from . import device as D
 from . import primitives as P
 from .reduce import LeafSink, RowSums
-from .trace import ChainLaunch, Mirror, staged_chain
+from .trace import ChainLaunch, Mirror, _fill_desc, staged_chain
 
 
 @dataclass
@@ -71,18 +71,43 @@ class SystemGeometry:
             return SystemGeometry.from_dict(json.load(f))
 
 
+NP_BUF = 8192  # numpy's float64 sum buffer: pairwise inside, buffers added left to right
+
+
 @dataclass
 class Shard:
-    """Contiguous block of V-rows [row0, row0 + rows) of the n x n ray grid."""
-    row0: int
-    rows: int
+    """Contiguous block [start, start + count) of the n x n ray grid's flat rays (iv * n + ih, V-row
+    major). Shard.split cuts the grid at multiples of numpy's 8192-element sum buffers, so every
+    shard but the last holds whole buffers and the grid's short last buffer lies in the last one:
+    each rank's buffer sums are then numpy's own and the means combine across ranks in numpy's
+    order, bit for bit (reduce.LeafSink.finish_dist)."""
+    start: int
+    count: int
 
     @staticmethod
     def split(n, world, rank):
-        base, rem = divmod(n, world)
-        rows = base + (1 if rank < rem else 0)
-        row0 = rank * base + min(rank, rem)
-        return Shard(row0, rows)
+        total = int(n) * int(n)
+        if world == 1:
+            return Shard(0, total)
+        nbuf = total // NP_BUF
+        if nbuf < world:
+            raise ValueError(f"a {n} x {n} grid holds {nbuf} full 8192-ray buffers: too few for {world} ranks")
+        base, rem = divmod(nbuf, world)
+        b0 = rank * base + min(rank, rem)
+        nb = base + (1 if rank < rem else 0)
+        start = b0 * NP_BUF
+        end = total if rank == world - 1 else (b0 + nb) * NP_BUF
+        return Shard(start, end - start)
+
+    def full_buffers(self):
+        return self.count // NP_BUF
+
+
+def geometry_key(g):
+    """What a chain launch takes from a SystemGeometry (mirrors, pre-tilt detector, source):
+    equal keys trace identically."""
+    return (tuple(tuple(m.coeffs) + (bool(m.negative),) for m in g.mirrors), tuple(float(x) for x in g.det1),
+            tuple(float(x) for x in g.source))
 
 
 def sample_plan(n):
@@ -95,12 +120,12 @@ def sample_plan(n):
 def sample_ownership(shard, n):
     """Which resample picks a shard's rays supply: (mask over the middle-row range, mask over the
     n rows of the middle column)."""
-    hb, he, _ = sample_plan(n)
-    lo, hi = shard.row0 * n, (shard.row0 + shard.rows) * n
+    hb, he, col = sample_plan(n)
+    lo, hi = shard.start, shard.start + shard.count
     own_h = np.zeros(he - hb, dtype=bool)
     own_h[max(lo, hb) - hb:max(min(hi, he) - hb, 0)] = True
-    own_v = np.zeros(n, dtype=bool)
-    own_v[shard.row0:shard.row0 + shard.rows] = True
+    g = np.arange(n) * n + col
+    own_v = (g >= lo) & (g < hi)
     return own_h, own_v
 
 
@@ -161,8 +186,14 @@ class LocalComm:
     def gather_samples(self, samp_h, samp_v, shard, n):
         return samp_h, samp_v
 
-    def sum_flags(self, f):
+    def or_flags(self, f):
         return f
+
+    def allreduce_or(self, words):
+        return words
+
+    def allgather_equal(self, t):
+        return t.unsqueeze(0)
 
     def allreduce_sums(self, t):
         return t
@@ -190,6 +221,7 @@ class _Front:
     fin_ev: object = None  # event after that finish
     opd: dict = None  # DistError2 / Wave2, when the front after next formed them in its pass 1
     opd_ev: object = None  # event after that fused kernel
+    g: object = None  # the SystemGeometry this run traced (RayWave.launch_front(geometry=...))
 
 
 class RayWave:
@@ -208,14 +240,19 @@ class RayWave:
         self.g = geometry
         self.n = int(n)
         self.comm = comm or LocalComm()
-        self.shard = shard or Shard(0, self.n)
+        self.shard = shard or Shard(0, self.n * self.n)
+        if self.comm.world > 1:
+            want = Shard.split(self.n, self.comm.world, self.comm.rank)
+            if self.shard != want:
+                raise ValueError(f"rank {self.comm.rank}'s shard must be Shard.split's {want} (buffer-aligned)")
+            self._nbufs = [Shard.split(self.n, self.comm.world, r).full_buffers() for r in range(self.comm.world)]
         self.resample_pass = resample_pass
         self.dev = D.device()
         self.rand_h = geometry.angle_h.table(self.n)
         self.rand_v = geometry.angle_v.table(self.n)
         self.tan_h = torch.from_numpy(np.tan(self.rand_h)).to(self.dev)
         self.tan_v = torch.from_numpy(np.tan(self.rand_v)).to(self.dev)
-        self.n_local = self.shard.rows * self.n
+        self.n_local = self.shard.count
         self.sums = RowSums()
         # fused numpy-order reductions: pass 2 -> (atan_h, atan_v, det x, y, z), nanmean for the
         # arctans and plain mean for the detector (:3583-3590); tilt -> (det1 x, y, z, total1,
@@ -257,12 +294,14 @@ class RayWave:
         self._tan2 = torch.empty((NS, 2 * self.n), dtype=D.F64, device=self.dev)
         self._tan2_host = torch.empty((NS, 2 * self.n), dtype=D.F64, pin_memory=True)
         self._staged = [None] * NS  # event after the pass 1 that copied a slot's host tables
+        self._desc_key = {}  # id(ChainLaunch) -> geometry_key its descriptor holds
         self._ps = ChainLaunch(self.g.mirrors, tan_h=self.tan_h, tan_v=self.tan_v, row0=0, n_rays=self.n * self.n,
                                src=self.g.source, want=(), samples=(hb, he, col), flags=self._sflag,
                                samples_buf=self._x1[:self._nsamp])
-        self._p1 = ChainLaunch(self.g.mirrors, tan_h=self.tan_h, tan_v=self.tan_v, row0=self.shard.row0,
+        self._p1 = ChainLaunch(self.g.mirrors, tan_h=self.tan_h, tan_v=self.tan_v, ray0=self.shard.start,
                                n_rays=self.n_local, src=self.g.source, want=(), flags=self._flags[0:1])
         self._p2 = {}
+        self._desc_key[id(self._ps)] = self._desc_key[id(self._p1)] = geometry_key(self.g)
         self._pert = perturbation.device_tables(self.n, self.n, self.dev) if perturbation is not None else None
         # event after the last queued reader of the pass-2 buffers / extent keys (a back half
         # and its pupil, possibly on another stream): the next pass 2 waits for it
@@ -286,31 +325,64 @@ class RayWave:
             out = same[0].res.extra["buffers"] if same else None
             t2 = self._tan2[slot]
             self._p2[key] = ChainLaunch(self.g.mirrors, tan_h=t2[:self.n], tan_v=t2[self.n:], out=out,
-                                        row0=self.shard.row0, n_rays=self.n_local, src=self.g.source,
+                                        ray0=self.shard.start, n_rays=self.n_local, src=self.g.source,
                                         det_ghij=self.g.det1, want=want, sink=self.sink2, flags=self._flags[1:2],
                                         pert=self._pert)
+            self._desc_key[id(self._p2[key])] = geometry_key(self.g)
         return self._p2[key]
 
+    # -------------------------------------------------------------- per-run geometry
+    def _check_geometry(self, g):
+        """A run may trace another system than the one RayWave was built for (auto_focus-style
+        sweeps): its mirrors, detector planes and source may differ; the ray grid (angle ranges)
+        and the number of detectors may not."""
+        if g is self.g:
+            return
+        if (g.angle_h.start, g.angle_h.stop, g.angle_h.offset, g.angle_v.start, g.angle_v.stop, g.angle_v.offset) != (
+                self.g.angle_h.start, self.g.angle_h.stop, self.g.angle_h.offset, self.g.angle_v.start,
+                self.g.angle_v.stop, self.g.angle_v.offset):
+            raise ValueError("a run's geometry must keep RayWave's ray-grid angle ranges")
+        if (g.det2 is None) != (self.g.det2 is None) or len(g.mirrors) != len(self.g.mirrors):
+            raise ValueError("a run's geometry must have as many mirrors and detector planes as RayWave's")
+
+    def _use(self, launch, g):
+        """Point a prepared chain launch at g's mirrors / detector / source (only when it holds
+        another system: the descriptor is copied into the kernel arguments at each launch)."""
+        key = geometry_key(g)
+        if self._desc_key.get(id(launch)) != key:
+            _fill_desc(launch.desc, g.mirrors, g.det1)
+            for j in range(3):
+                launch.desc.src[j] = float(g.source[j])
+            self._desc_key[id(launch)] = key
+
     # -------------------------------------------------------------- passes
-    def _queue_picks(self):
-        """The picks prepass of the next run and its copy to the host, on the copy stream (it
-        reads only the constant grid tables, so it runs one run ahead, beside this run's
+    def _queue_picks(self, g=None):
+        """The picks prepass of the next run (system g) and its copy to the host, on the copy
+        stream (it reads only the constant grid tables, so it runs one run ahead, beside this run's
         kernels); its host buffer alternates between runs."""
+        g = g if g is not None else self.g
         x = self._x1_host[self._pick_buf]
         self._pick_buf ^= 1
+        self._use(self._ps, g)
         with torch.cuda.stream(self._copy):
             self._sflag.zero_()
             _lib.check(_lib.lib().akb_trace_chain_samples_f64(self._ps.desc, D.stream_handle(self._copy)))
             x.copy_(self._x1, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(self._copy)
-        self._next_picks = (ev, x)
+        self._next_picks = (ev, x, geometry_key(g))
 
-    def _take_picks(self):
-        """This run's picks and the prepass's flag word (waits for the prepass if still running)."""
+    def _take_picks(self, g=None):
+        """This run's picks and the prepass's flag word (waits for the prepass if still running).
+        A prepass queued for another system than g (the caller did not announce g as the
+        next_geometry) is dropped and redone for g."""
+        g = g if g is not None else self.g
+        if self._next_picks is not None and self._next_picks[2] != geometry_key(g):
+            self._next_picks[0].synchronize()  # its host buffer is about to be reused
+            self._next_picks = None
         if self._next_picks is None:
-            self._queue_picks()
-        ev, x = self._next_picks
+            self._queue_picks(g)
+        ev, x, _ = self._next_picks
         self._next_picks = None
         ev.synchronize()
         hb, he, _ = self._plan
@@ -344,28 +416,28 @@ class RayWave:
             self.kernel_events.append(ev)
         return r
 
-    def _pass2_staged(self, tan_h2, tan_v2):
+    def _pass2_staged(self, tan_h2, tan_v2, g=None):
         """Exact stage-by-stage pass 2 (used only when the fused kernel raised a flag)."""
+        g = g if g is not None else self.g
         from .trace import grid_dirs
         dirs = grid_dirs(tan_h2, tan_v2)
-        lo = self.shard.row0 * self.n
+        lo = self.shard.start
         dirs = dirs[:, lo:lo + self.n_local].contiguous()
-        src = torch.tensor(self.g.source, dtype=D.F64, device=self.dev).reshape(3, 1).expand(3, self.n_local)
+        src = torch.tensor(g.source, dtype=D.F64, device=self.dev).reshape(3, 1).expand(3, self.n_local)
         src = src.contiguous()
-        hits, r4, segs = staged_chain(self.g.mirrors, dirs, src, with_segments=True)
+        hits, r4, segs = staged_chain(g.mirrors, dirs, src, with_segments=True)
         opl = segs[0]
         for s in segs[1:]:
             opl = opl + s
         if self._pert is not None:
             ph, pv = self._pert
-            rows = pv[:, self.shard.row0:self.shard.row0 + self.shard.rows]
-            opl = opl + (rows.T @ ph).reshape(-1)
-        det = P.plane_ray_intersection([0] * 6 + list(self.g.det1), r4, hits[-1])
+            opl = opl + (pv.T @ ph).reshape(-1)[lo:lo + self.n_local]
+        det = P.plane_ray_intersection([0] * 6 + list(g.det1), r4, hits[-1])
         atan = torch.stack([torch.atan(r4[1] / r4[0]), torch.atan(r4[2] / r4[0])])
         return hits[-1], r4, det, opl, atan
 
     # -------------------------------------------------------------- one run
-    def run(self, opd=True, keep_rotated=False, full=False, overlap=None):
+    def run(self, opd=True, keep_rotated=False, full=False, overlap=None, geometry=None, next_geometry=None):
         """Trace and reduce; returns a RunResult of device tensors (this shard's rays) and means.
         keep_rotated: also return the tilted direction / last hit (dir_rot, pt_rot); full: also
         return DistError (detector 1), Sph, detcenter and the pre-tilt rows. The default keeps what
@@ -377,9 +449,10 @@ class RayWave:
         them. A run is launch_back(launch_front()); a caller tracing several systems in a row can
         pass the previous run's launch_back as this run's overlap, so its tilt and OPD fill the
         GPU while the host resamples (bench.py does)."""
-        return self.launch_back(self.launch_front(full=full, overlap=overlap), opd=opd, keep_rotated=keep_rotated)
+        return self.launch_back(self.launch_front(full=full, overlap=overlap, geometry=geometry,
+                                                  next_geometry=next_geometry), opd=opd, keep_rotated=keep_rotated)
 
-    def launch_front(self, full=False, overlap=None, fuse=None, fuse_opd=None):
+    def launch_front(self, full=False, overlap=None, fuse=None, fuse_opd=None, geometry=None, next_geometry=None):
         """The resample picks, pass 1, the resample (the run's one host wait, for the picks
         only), pass 2, its sums and the device tilt parameters. Returns as soon as all of it is
         queued; the trace flags are read when launch_back (or _resolve) needs them.
@@ -397,8 +470,16 @@ class RayWave:
         it in `overlap`, called once pass 1 is queued, so its pupil runs beside this run's pass 2).
         Without fuse_opd, fuse's launch_back forms the OPD itself. A fused OPD inside pass 2
         measured slower (1.005 vs 0.974 ms per bench step): its loads and registers cost the
-        FP64-bound chain more than running beside it; pass 1 keeps nothing of it across the chain."""
+        FP64-bound chain more than running beside it; pass 1 keeps nothing of it across the chain.
+
+        geometry: the system this run traces (default: RayWave's own); consecutive runs may trace
+        different systems - mirrors, detector planes, source - over the same ray grid, and the
+        fused tilt / OPD of an earlier run keep that run's system (its front carries it).
+        next_geometry: the system of the run after this one, whose picks prepass is queued here
+        (default: this run's); announcing it keeps the prepass one run ahead."""
         L = _lib.lib()
+        g = geometry if geometry is not None else self.g
+        self._check_geometry(g)
         stream = D.stream_handle()
         slot = self._runs % self.NSLOTS
         self._runs += 1
@@ -414,7 +495,7 @@ class RayWave:
             fuse_opd = None
         # fused optimistically: should fuse's pass 2 turn out flagged, launch_back ignores the
         # fused tilt and takes the staged path (its tables live in fuse's own slot)
-        samp_h, samp_v, sflags = self._take_picks()
+        samp_h, samp_v, sflags = self._take_picks(g)
         if sflags:
             torch.cuda.synchronize()
             self._words.zero_()
@@ -431,7 +512,9 @@ class RayWave:
         else:
             np.tan(self.rand_h, out=th[:self.n])
             np.tan(self.rand_v, out=th[self.n:])
-        self._queue_picks()
+        nxt = next_geometry if next_geometry is not None else g
+        self._check_geometry(nxt)
+        self._queue_picks(nxt)
         if fuse is not None and self._back_done is not None:
             # the back half queued before (its OPD / pupil; its extent keys are cleared by a
             # later tilt-parameter kernel and its tilt sink refilled by a later fused pass 1):
@@ -441,6 +524,7 @@ class RayWave:
             self._back_done = None
         if fuse_opd is not None and not fuse_opd.fin_ev.query():  # its tilt sums (normally done)
             torch.cuda.current_stream().wait_event(fuse_opd.fin_ev)
+        self._use(self._p1, g)
         self._pass1(stream, fuse, slot, fuse_opd)
         if fuse is not None:
             self._finish_tilt(fuse)
@@ -451,13 +535,11 @@ class RayWave:
             # pass 2 rewrites the buffers a queued (unfused) back half's tilt reads
             torch.cuda.current_stream().wait_event(self._back_done)
             self._back_done = None
+        self._use(self._pass2_launch(full, slot), g)
         r = self._pass2(want_rows=full, stream=stream, slot=slot)
-        if self.comm.world > 1:
-            self.comm.allreduce_sums(self._flags)
-        sums, cnts = self.sink2.finish(stream)
-        if self.comm.world > 1:  # cross-rank means: partial sums added over ranks (not numpy order)
-            self.comm.allreduce_sums(sums)
-            self.comm.allreduce_sums(cnts)
+        if self.comm.world > 1:  # any rank's flag bits (OR, not a sum: bits must not carry)
+            self.comm.allreduce_or(self._flags)
+        sums, cnts = self._finish_sink(self.sink2, stream)
         params = torch.empty(25, dtype=D.F64, device=self.dev)  # this run's own block
         _lib.check(L.akb_tilt_params_f64(D.ptr(sums), D.ptr(cnts), D.ptr(params), D.ptr(self._ext[slot]),
                                          D.ptr(self._flags), 2, stream))
@@ -471,7 +553,7 @@ class RayWave:
             ev2.record(self._flag_copy)
         params.record_stream(self._flag_copy)
         return _Front(r=r, tan_h2=tan_h2, tan_v2=tan_v2, params=params, full=full, stream=stream, flag_ev=ev2,
-                      done=done, slot=slot)
+                      done=done, slot=slot, g=g)
 
     def _flags_of(self, f):
         """f's (pass 1, pass 2) trace flag words (waits for its pass 2 if still running)."""
@@ -498,11 +580,11 @@ class RayWave:
         this run's pass 2 comes after it on the same stream); with g (the run before f, tilted
         by the previous pass 1, its sums finished) also g's DistError2 / Wave2 and extent keys."""
         L = _lib.lib()
-        tb = self._tilt_buffers(False, f.full)
+        tb = self._tilt_buffers(False, f.full, f.g)
         r = f.r
         n = self.n_local
         if g is None:
-            _lib.check(L.akb_chain_tilt_f64(self._p1.desc, D.ptr(f.params), D.host_f64(self.g.det1),
+            _lib.check(L.akb_chain_tilt_f64(self._p1.desc, D.ptr(f.params), D.host_f64(f.g.det1),
                                             D.host_f64(tb["d2"]), D.ptr(r.dir_out), D.ptr(r.last_hit),
                                             D.ptr(r.opl), n, n, None, None, D.ptr(tb["det1"]),
                                             D.ptr(tb["det2_buf"]), D.ptr(tb["total1"]), D.ptr(tb["total2"]),
@@ -512,7 +594,7 @@ class RayWave:
             sums, cnts = g.fin
             opd = dict(dist_err2=torch.empty(n, dtype=D.F64, device=self.dev),
                        wave2=torch.empty(n, dtype=D.F64, device=self.dev))
-            _lib.check(L.akb_chain_tilt_opd_f64(self._p1.desc, D.ptr(f.params), D.host_f64(self.g.det1),
+            _lib.check(L.akb_chain_tilt_opd_f64(self._p1.desc, D.ptr(f.params), D.host_f64(f.g.det1),
                                                 D.host_f64(tb["d2"]), D.ptr(r.dir_out), D.ptr(r.last_hit),
                                                 D.ptr(r.opl), n, n, D.ptr(tb["det2_buf"]), D.ptr(tb["total2"]),
                                                 self._sink3[f.slot].desc, D.ptr(gt["total2"]),
@@ -525,14 +607,18 @@ class RayWave:
         if g is not None:
             g.opd, g.opd_ev = opd, ev
 
+    def _finish_sink(self, sink, stream):
+        """A fused sink's np.sum / np.nanmean sums and counts; across ranks in numpy's own order
+        (LeafSink.finish_dist over the buffer-aligned shards): the same bits as one process."""
+        if self.comm.world == 1:
+            return sink.finish(stream)
+        return sink.finish_dist(self.comm, self._nbufs, self.n * self.n, stream)
+
     def _finish_tilt(self, f):
         """The sums of f's fused tilt (on the finish stream, beside the next pass 2)."""
         with torch.cuda.stream(self._fin):
             self._fin.wait_event(f.tilted)
-            sums, cnts = self._sink3[f.slot].finish(self._fin)
-            if self.comm.world > 1:
-                self.comm.allreduce_sums(sums)
-                self.comm.allreduce_sums(cnts)
+            sums, cnts = self._finish_sink(self._sink3[f.slot], self._fin)
             ev = torch.cuda.Event()
             ev.record(self._fin)
         f.fin, f.fin_ev = (sums, cnts), ev
@@ -565,7 +651,7 @@ class RayWave:
     def _launch_back(self, f, opd, keep_rotated):
         r = f.r
         if self._resolve(f)[1]:  # a flagged pass 2: the staged path (a fused tilt is discarded)
-            out = self._run_staged(None, f.tan_h2, f.tan_v2, opd, keep_rotated, f.full, slot=f.slot)
+            out = self._run_staged(None, f.tan_h2, f.tan_v2, opd, keep_rotated, f.full, slot=f.slot, g=f.g)
         else:
             out = RunResult(last_hit=r.last_hit, dir_out=r.dir_out, opl=r.opl, tan_h2=f.tan_h2, tan_v2=f.tan_v2,
                             params=f.params)
@@ -580,17 +666,17 @@ class RayWave:
                 out.update(self._opd_after_tilt(f.tilt, f.full, True, f.slot, f.stream, fin=f.fin))
             elif opd:
                 out.update(self._tilt_opd(r.last_hit, r.dir_out, r.opl, keep_rotated, f.full, params=f.params,
-                                          stream=f.stream, slot=f.slot))
+                                          stream=f.stream, slot=f.slot, g=f.g))
         out["flags"] = f.flags
         out["slot"] = f.slot
         self.last = out
         return out
 
-    def _run_staged(self, fast, tan_h2, tan_v2, opd, keep_rotated, full, slot=0):
+    def _run_staged(self, fast, tan_h2, tan_v2, opd, keep_rotated, full, slot=0, g=None):
         """Pass 2 flagged a miss or a zero norm: redo it stage by stage (the reference's value
         rules) and the tilt from host-formed matrices."""
         torch.cuda.synchronize()
-        last_hit, dir_out, det_pre, opl, atan = self._pass2_staged(tan_h2.clone(), tan_v2.clone())
+        last_hit, dir_out, det_pre, opl, atan = self._pass2_staged(tan_h2.clone(), tan_v2.clone(), g)
         (atan_s, atan_c), (det_s, det_c) = self.sums(atan, nan=True), self.sums(det_pre)
         red = self.comm.allreduce_sums(torch.cat([atan_s, det_s, atan_c.to(D.F64), det_c.to(D.F64)]))
         host = red.cpu().numpy()
@@ -605,15 +691,17 @@ class RayWave:
             out.update(det_pre=det_pre, atan=atan)
         if opd:
             ry, rz = P.rotation_matrices(-theta_y, -theta_z)
-            out.update(self._tilt_opd(last_hit, dir_out, opl, keep_rotated, full, host_tilt=(ry, rz, focus), slot=slot))
+            out.update(self._tilt_opd(last_hit, dir_out, opl, keep_rotated, full, host_tilt=(ry, rz, focus), slot=slot,
+                                      g=g))
         return out
 
-    def _tilt_buffers(self, keep_rotated, full):
+    def _tilt_buffers(self, keep_rotated, full, g=None):
         """Output tensors of one tilt (allocated on the current stream)."""
+        g = g if g is not None else self.g
         n, dev = self.n_local, self.dev
-        two = self.g.det2 is not None
+        two = g.det2 is not None
         e = lambda *shape: torch.empty(shape, dtype=D.F64, device=dev)
-        tb = dict(two=two, d2=self.g.det2 if two else self.g.det1,
+        tb = dict(two=two, d2=g.det2 if two else g.det1,
                   det1=e(3, n) if (full or not two) else None, det2=e(3, n) if two else None,
                   total1=e(n) if (full or not two) else None, total2=e(n),
                   dir_rot=e(3, n) if keep_rotated else None, pt_rot=e(3, n) if keep_rotated else None)
@@ -621,21 +709,22 @@ class RayWave:
         return tb
 
     def _tilt_opd(self, last_hit, dir_out, opl, keep_rotated=False, full=False, host_tilt=None, params=None,
-                  stream=None, slot=0):
+                  stream=None, slot=0, g=None):
         L = _lib.lib()
+        g = g if g is not None else self.g
         n = self.n_local
         sh = D.stream_handle(stream)
-        tb = self._tilt_buffers(keep_rotated, full)
+        tb = self._tilt_buffers(keep_rotated, full, g)
         outs = (D.ptr(dir_out), D.ptr(last_hit), D.ptr(opl), n, n, D.ptr(tb["dir_rot"]), D.ptr(tb["pt_rot"]),
                 D.ptr(tb["det1"]), D.ptr(tb["det2_buf"]), D.ptr(tb["total1"]), D.ptr(tb["total2"]),
                 self._sink3[slot].desc,
                 sh)
         if host_tilt is None:
-            _lib.check(L.akb_tilt_opd_dev_f64(D.ptr(params), D.host_f64(self.g.det1), D.host_f64(tb["d2"]), *outs))
+            _lib.check(L.akb_tilt_opd_dev_f64(D.ptr(params), D.host_f64(g.det1), D.host_f64(tb["d2"]), *outs))
         else:
             ry, rz, focus = host_tilt
             _lib.check(L.akb_tilt_opd_f64(D.host_f64(ry.ravel()), D.host_f64(rz.ravel()), D.host_f64(focus),
-                                          D.host_f64(self.g.det1), D.host_f64(tb["d2"]), *outs))
+                                          D.host_f64(g.det1), D.host_f64(tb["d2"]), *outs))
         return self._opd_after_tilt(tb, full, host_tilt is None, slot, stream)
 
     def _opd_after_tilt(self, tb, full, keys_zeroed, slot, stream, fin=None):
@@ -647,10 +736,7 @@ class RayWave:
         if fin is not None:
             sums, cnts = fin
         else:
-            sums, cnts = self._sink3[slot].finish(sh)
-            if self.comm.world > 1:
-                self.comm.allreduce_sums(sums)
-                self.comm.allreduce_sums(cnts)
+            sums, cnts = self._finish_sink(self._sink3[slot], sh)
         self._means5 = (sums, cnts)
         total1 = tb["total1"]
         dist_err = torch.empty(n, dtype=D.F64, device=dev) if total1 is not None else None
@@ -689,7 +775,7 @@ class RayWave:
             # unsigned key order == signed order after flipping the top bit: MAX over ranks
             flip = torch.tensor(-(1 << 63), dtype=torch.int64, device=self.dev)
             ext = self.comm.allreduce_max(torch.bitwise_xor(ext, flip)).bitwise_xor(flip).contiguous()
-        _lib.check(L.akb_pupil_sample_f64(D.ptr(self.last["wave2"]), self.shard.row0, self.shard.rows, self.n,
+        _lib.check(L.akb_pupil_sample_f64(D.ptr(self.last["wave2"]), self.shard.start, self.shard.count, self.n,
                                           size, D.ptr(ext), D.ptr(self._opd_buf), D.ptr(self._pitch),
                                           D.stream_handle()))
         opd = self._opd_buf

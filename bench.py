@@ -6,23 +6,32 @@
 
 Workload (BASELINE.json configs[2], "C3"): the 'ray_wave' path of plot_result_debug
 (AKB_raytrace_20250312.py:1326) on a 3163 x 3163 ray grid (1.0e7 rays) per GPU through the
-reference's Wolter III+I geometry (tests/golden/akb_geometry.json, recorded from the reference):
+reference's Wolter III+I geometry (tests/golden/akb_geometry.json, recorded from the reference),
+each step a different system of a cycle of --systems variants (the last mirror and the two
+detector planes moved per system, as the focus sweeps move the system between traces):
 pass 1 (4 mirrors), equal-angle resample, pass 2 (4 mirrors + OPL), tilt, two detector planes,
 OPD; then a 128 x 128 pupil padded x16 -> 2048^2 PSF (pruned 2-D DFT: the padded plane is never
 built). One step = all of it; its intersections are 2 passes x 4 mirrors x rays. Steps are
-pipelined the way a caller tracing many systems would run them: step k's pass 1 is queued ahead
-of step k-1's tilt / OPD / pupil / PSF (RayWave.launch_front / launch_back), which hides the
-host's resample, and that back half runs on a second stream, concurrently with the FP64-bound
-pass 1 (it is HBM-bound). By default (--fuse 1) step k-1's tilt runs inside step k's pass-1
-kernel, which hides its loads behind the chain's arithmetic, and only its OPD / pupil / PSF go to
-the back stream, where they fill the GPU during the host resample. Every step still does all of
-its work inside the timed region. Inputs (the two
-1-D angle tables) are resident on the device before timing. Multi-GPU: weak scaling, each rank
-owns ~1e7 rays (contiguous V-rows of a grid of round(sqrt(N * 1e7))^2 rays); the PSF runs on
-rank 0.
+pipelined the way a caller tracing many systems would run them (RayWave.launch_front /
+launch_back): by default (--fuse 2) step k's pass-1 kernel also tilts step k-1 and forms step
+k-2's OPD maps (their loads hidden behind the chain's FP64 arithmetic), and step k-2's pupil and
+PSF run on other streams beside step k's pass 2 while the host resamples. Every step still does
+all of its work inside the timed region. Inputs (the two 1-D angle tables) are resident on the
+device before timing.
+
+Multi-GPU (configs[3], "C4"): weak scaling at C4's per-GPU load, ~1.25e7 rays per rank of a
+round(sqrt(N * 1.25e7))^2 grid - 10000^2 = 1e8 rays, ~1250 V-rows per rank, at N = 8 - in
+contiguous blocks of whole 8192-ray numpy sum buffers (Shard.split), so the cross-rank means are
+numpy's to the bit; the exchanges are tiny all-gathers / all-reduces and the pupil before the PSF
+on rank 0.
 
 Prints one JSON line (rank 0). The dominant kernel's roofline uses HIP events on the stream it runs
-on; cpu_baseline times the oracle's C restatement (the "port") on this host on a bounded sample.
+on; its PMC-derived fields (HBM traffic, FP64 rate, the VALU-issue roofline) come from the newest
+profiles/*_roofline.json whose source hash matches the trace kernels' sources, else null.
+cpu_baseline times the oracle's C restatement (the "port") on this host on a bounded sample.
+Outside the timed region: one run() with its host wait (single_run_ms); at N = 1 also the
+faithful PSF chain (griddata + plane correction + psf_calc, faithful_psf_chain_ms) and the
+Huygens stage of configs[1] (huygens_pairs_per_s).
 """
 import argparse
 import glob
@@ -38,6 +47,9 @@ sys.path.insert(0, ROOT)
 METRIC = "ray-surface intersections/sec + PSF wall-time, 1e7-ray 4-mirror AKB, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X spec, MI355X_MICROARCH.md
 FP64_VALU_PEAK_TFS = 78.6  # MI355X FP64 vector peak (FMA counted as 2 flops)
+SIMDS = 1024  # 256 CUs x 4 SIMDs; a wave64 VALU instruction occupies a SIMD for 4 cycles
+C3_RAYS = 1.0e7  # configs[2]: 1e7 rays on one GPU
+C4_RAYS_PER_GPU = 1.25e7  # configs[3]: 1e8 rays over 8 GPUs
 # bytes the pass-2 chain kernel must move per ray: it reads two L2-resident 1-D tables and
 # writes last hit (24) + exit direction (24) + OPL (8); the arctans and detector hits it also
 # forms are reduced in-kernel (numpy-order leaf sums, 5 x 8 B per 128 rays)
@@ -49,7 +61,12 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3, help="at least 2 with --fuse 2 (fills the pipeline)")
-    p.add_argument("--rays", type=float, default=1.0e7, help="rays per GPU")
+    p.add_argument("--rays", type=float, default=None,
+                   help="rays per GPU (default: 1e7 on one GPU, C3; 1.25e7 per rank at N > 1, C4's 1e8 at N = 8)")
+    p.add_argument("--systems", type=int, default=8,
+                   help="distinct systems cycled through the steps (1: the same system every step)")
+    p.add_argument("--no-extras", action="store_true",
+                   help="skip single_run_ms / faithful_psf_chain_ms / huygens_pairs_per_s")
     p.add_argument("--pupil", type=int, default=128)
     p.add_argument("--pad", type=int, default=16)
     p.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -111,16 +128,83 @@ def cpu_baseline(seconds):
             "sample_1thread": f"same pipeline, 1 thread, {n1}x{n1} grid, {reps1} reps in {el1:.1f} s"}
 
 
-def read_pmc():
-    """The pass-2 chain's rocprofv3 --pmc summary committed under profiles/ (newest), or {}."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_pass2*.json")))
+def read_profile():
+    """(summary, file, matches): the newest profiles/*_roofline.json (scripts/summarize_profiles.py)
+    and whether it describes these kernel sources (its sha256 of them equals theirs now)."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    from summarize_profiles import sources_sha256
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_roofline.json")))
     if not files:
-        return {}
-    try:
-        with open(files[-1]) as f:
-            return json.load(f)
-    except Exception:
-        return {}
+        return {}, None, False
+    with open(files[-1]) as f:
+        d = json.load(f)
+    return d, os.path.relpath(files[-1], ROOT), d.get("sources_sha256") == sources_sha256()
+
+
+def system_variants(geom, k):
+    """k distinct systems on geom's ray grid: the last mirror's constant term scaled by
+    1 + 2e-11 i and the two detector planes moved 3 and 5 um x i (i = 0 .. k-1)."""
+    import copy
+    out = []
+    for i in range(k):
+        g = copy.deepcopy(geom)
+        c = list(g.mirrors[-1].coeffs)
+        c[9] = c[9] * (1.0 + 2e-11 * i)
+        g.mirrors[-1].coeffs = c
+        g.det1 = list(g.det1[:3]) + [g.det1[3] - 3e-6 * i]
+        if g.det2 is not None:
+            g.det2 = list(g.det2[:3]) + [g.det2[3] - 5e-6 * i]
+        out.append(g)
+    return out
+
+
+def faithful_psf_chain(rw, out, size):
+    """The reference's own pupil for the PSF: griddata(cubic) of Wave2 and
+    DistError2 from the detector-2 hits onto a size x size grid, nanmean removal, plane
+    correction (pupilmap.wave_maps), then psf_calc (rotation estimate, rotate_with_nan, pad-16
+    PSF, trim). Wall time with the device synchronised (its host steps included), ms; median of 3."""
+    import torch
+    from akbraytracing_amd import pupilmap as PM
+    from akbraytracing_amd.psfcalc import psf_calc
+    det2 = out["detcenter2"].clone()
+    e2, w2 = out["dist_err2"].clone(), out["wave2"].clone()
+    times = []
+    for _ in range(3):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        m = PM.wave_maps(det2, e2, w2, rw.n, rw.n, grid_num_H=size, grid_num_V=size)
+        psf_calc(m["matrixWave2_Corrected"], m["grid_H"], m["grid_V"], 1e-2)
+        torch.cuda.synchronize()
+        times.append((time.perf_counter() - t0) * 1e3)
+    return sorted(times)[1]
+
+
+def huygens_rate(out):
+    """configs[1]'s M2 -> image stage shape: this run's last-mirror hits as
+    sources (unit field, dS = 1) onto a 65 x 65 image grid around the focus; pairs/s."""
+    import numpy as np
+    import torch
+    from akbraytracing_amd.wavecalc import propagate
+    src = out["last_hit"]
+    sx, sy, sz = (src[i].contiguous() for i in range(3))
+    u = torch.ones(sx.shape[0], dtype=torch.complex128, device=sx.device)
+    c = out["detcenter2"].mean(dim=1).cpu().numpy()
+    t = np.linspace(-1e-6, 1e-6, 65)
+    ty, tz = np.meshgrid(c[1] + t, c[2] + t)
+    T = [torch.from_numpy(np.ascontiguousarray(v.ravel())).to(sx.device) for v in (np.full(ty.size, c[0]), ty, tz)]
+    k = 2 * np.pi / 13.5e-9
+    propagate(*T, sx, sy, sz, u, k)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(3):
+        propagate(*T, sx, sy, sz, u, k)
+    e1.record()
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / 3
+    return {"value": T[0].shape[0] * sx.shape[0] / (ms * 1e-3), "unit": "pairs/s", "ms": ms,
+            "sources": int(sx.shape[0]), "targets": int(T[0].shape[0]),
+            "stage": "M2 -> 65x65 image grid (configs[1]'s stage shape, sources from this trace)"}
 
 
 def main():
@@ -139,7 +223,11 @@ def main():
 
     dev = torch.device("cuda", torch.cuda.current_device())
     geom = SystemGeometry.load(os.path.join(ROOT, "tests", "golden", "akb_geometry.json"))
-    n = int(math.ceil(math.sqrt(args.rays * world)))  # 3163 at 1 GPU
+    if args.rays is None:
+        args.rays = C3_RAYS if world == 1 else C4_RAYS_PER_GPU
+    # 3163 at 1 GPU (C3); 10000 at 8 GPUs (C4: 1250 V-rows per rank); SURVEY.md §8(d)
+    n = int(round(math.sqrt(args.rays * world))) if world > 1 else int(math.ceil(math.sqrt(args.rays)))
+    systems = system_variants(geom, max(args.systems, 1))
     shard = Shard.split(n, world, rank)
     comm = AD.TorchComm(dev)
     pert = None
@@ -149,6 +237,10 @@ def main():
         pert = LegendrePerturbation(config5_coefficients(lams[0]))
         lams = [13.5e-9, 1.35e-9, 1.35e-10]  # EUV, softXray, hardXray (:1161-1166)
     rw = RayWave(geom, n, shard=shard, comm=comm, perturbation=pert)
+    nsteps = [0]  # steps launched so far (which system the next one traces)
+
+    def sys_of(i):
+        return systems[i % len(systems)]
 
     psf_events = []
     psf_out = {}
@@ -203,17 +295,20 @@ def main():
         # pipelined: this step's pass 1 is queued first (with --fuse, carrying the previous step's
         # tilt), the previous step's OPD / pupil / PSF right behind it, so the GPU works through
         # them while the host does the resample; each step still traces, tilts, reduces and
-        # transforms one full grid
+        # transforms one full grid - of its own system
+        i = nsteps[0]
+        nsteps[0] += 1
+        kw = dict(geometry=sys_of(i), next_geometry=sys_of(i + 1))
         if args.fuse >= 2 and len(fronts) == 2:  # two steps in flight: tilt k-1, OPD k-2
             old = fronts.pop(0)
-            fronts.append(rw.launch_front(overlap=lambda: back(timed, old), fuse=fronts[-1], fuse_opd=old))
+            fronts.append(rw.launch_front(overlap=lambda: back(timed, old), fuse=fronts[-1], fuse_opd=old, **kw))
         elif args.fuse >= 2 and len(fronts) == 1:  # filling the pipeline
-            fronts.append(rw.launch_front(fuse=fronts[0]))
+            fronts.append(rw.launch_front(fuse=fronts[0], **kw))
         elif fronts and args.fuse:
             prev = fronts.pop(0)
-            fronts.append(rw.launch_front(overlap=lambda: back(timed, prev), fuse=prev))
+            fronts.append(rw.launch_front(overlap=lambda: back(timed, prev), fuse=prev, **kw))
         else:
-            fronts.append(rw.launch_front(overlap=(lambda: back(timed)) if fronts else None))
+            fronts.append(rw.launch_front(overlap=(lambda: back(timed)) if fronts else None, **kw))
 
     for _ in range(args.warmup):
         step(False)
@@ -245,6 +340,20 @@ def main():
     inter_rank = rw.intersections_per_run() * args.steps
     tot = torch.tensor([float(inter_rank)], dtype=torch.float64, device=dev)
     total_inter = float(comm.allreduce_sums(tot).item())
+    # one run on its own, host wait included (what a caller that needs each result before the next
+    # trace sees); collective at N > 1, so every rank runs it
+    last_out, single_ms = None, None
+    if not args.no_extras:
+        single = []
+        for i in range(5):
+            comm.barrier()
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            last_out = rw.run(geometry=sys_of(i), next_geometry=sys_of(i + 1))
+            torch.cuda.synchronize()
+            single.append((time.perf_counter() - t1) * 1e3)
+        st = comm.allreduce_max(torch.tensor([sorted(single)[2]], dtype=torch.float64, device=dev))
+        single_ms = float(st.item())
 
     if rank != 0:
         return
@@ -253,7 +362,15 @@ def main():
     psf_ms = sum(a.elapsed_time(b) for a, b in psf_events) / max(len(psf_events), 1)
     launch_bytes = PASS2_BYTES_PER_RAY * rw.n_local
     achieved = launch_bytes / (k_avg * 1e-3) / 1e9
-    pmc = read_pmc()
+    prof, prof_file, prof_ok = read_profile()
+    pk = prof.get("kernels", {}).get("pass2", {}) if prof_ok else {}
+    inter_launch = 4 * rw.n_local  # pass 2's intersections per launch (4 mirrors)
+    # VALU-issue roofline of pass 2: the chip issues at most SIMDS / 4 wave-instructions per clock;
+    # with the profiled instructions per intersection that caps the intersection rate
+    vpi = (pk["valu_wave_instructions_per_launch"] / pk["intersections_per_launch"]) if pk else None
+    clock = pk.get("effective_clock_ghz") if pk else None
+    issue_peak = (SIMDS / 4 * clock * 1e9 / vpi) if vpi and clock else None
+    issue_achieved = inter_launch / (k_avg * 1e-3)
     out = {
         "metric": METRIC,
         "value": total_inter / el,
@@ -269,9 +386,12 @@ def main():
         "data": "synthetic: deterministic ray grid through the reference's AKB geometry (recorded fixture)",
         "config": {
             "workload": ("C3: 4-mirror AKB ray_wave trace (2 passes, tilt, OPD) + 2048^2 PSF" if args.config == "c3"
-                         else "C5: 4-mirror AKB ray_wave trace with per-ray Legendre OPL perturbation + "
-                              "3-wavelength 2048^2 PSF stack"),
-            "rays_per_gpu": rw.n_local, "grid": n, "mirrors": len(geom.mirrors),
+                         and world == 1 else
+                         "C4: 4-mirror AKB ray_wave trace, ray-row shards, + 2048^2 PSF" if args.config == "c3" else
+                         "C5: 4-mirror AKB ray_wave trace with per-ray Legendre OPL perturbation + "
+                         "3-wavelength 2048^2 PSF stack"),
+            "rays_per_gpu": rw.n_local, "rays_total": n * n, "grid": n, "v_rows_per_rank": round(shard.count / n, 1),
+            "mirrors": len(geom.mirrors), "systems_cycled": len(systems),
             "intersections_per_step": 2 * len(geom.mirrors) * n * n,
             "psf": f"{args.pupil}^2 pupil x pad {args.pad} -> {len(lams)} x {args.pupil * args.pad}^2 complex128 "
                    "DFT (pruned)",
@@ -283,29 +403,54 @@ def main():
         "psf_alone_output_gbs": (len(lams) * (args.pupil * args.pad) ** 2 * 8 / (psf_alone_ms * 1e-3) / 1e9
                                  if psf_alone_ms else None),
         "pass2_kernel_ms": k_avg,
+        # the contract's HBM roofline for the dominant kernel (pass 2, k_chain_sink with its fixed
+        # output set): algorithmic bytes over this run's event time. It moves 14 B per
+        # intersection, so HBM does not bound it; roofline_issue below is its real ceiling
         "roofline": {
-            "kernel": "k_chain<grid,opl> (pass 2)",
+            "kernel": "k_chain_sink<grid,opl,point,fixed> (pass 2)",
             "bound": "hbm",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": pmc.get("hbm_bytes_per_launch"),
+            "traffic": pk.get("hbm_bytes_per_launch"),
             "algorithmic_bytes_per_launch": launch_bytes,
         },
-        # what actually bounds that kernel: FP64 vector issue. FP64 flops per
-        # launch from the committed PMC counts (FMA = 2) over this run's kernel time.
+        # what bounds pass 2: VALU issue. Peak = intersections/s the chip would reach issuing one
+        # wave-instruction per SIMD every 4 cycles at the profiled clock, with the profiled VALU
+        # wave-instructions per intersection; frac = this run's rate over it
+        "roofline_issue": {
+            "kernel": pk.get("kernel"),
+            "bound": "valu-issue",
+            "achieved": issue_achieved,
+            "peak": issue_peak,
+            "unit": "intersections/s",
+            "frac": issue_achieved / issue_peak if issue_peak else None,
+            "valu_wave_instructions_per_intersection": vpi,
+            "non_fp64_share": pk.get("non_fp64_share"),
+            "effective_clock_ghz": clock,
+            "issue_frac_profiled": pk.get("issue_frac"),
+            "valu_busy_pct_profiled": pk.get("valu_busy_pct"),
+        },
         "roofline_fp64": {
             "bound": "fp64-valu",
-            "achieved": (pmc["fp64_flops_per_launch"] / (k_avg * 1e-3) / 1e12) if pmc.get("fp64_flops_per_launch")
-            else None,
+            "achieved": (pk["fp64_flops_per_launch"] / (k_avg * 1e-3) / 1e12) if pk else None,
             "peak": FP64_VALU_PEAK_TFS,
             "unit": "TFLOP/s",
-            "frac": (pmc["fp64_flops_per_launch"] / (k_avg * 1e-3) / 1e12 / FP64_VALU_PEAK_TFS)
-            if pmc.get("fp64_flops_per_launch") else None,
-            "valu_busy_pct": pmc.get("valu_busy_pct"),
+            "frac": (pk["fp64_flops_per_launch"] / (k_avg * 1e-3) / 1e12 / FP64_VALU_PEAK_TFS) if pk else None,
         },
+        # where the PMC-derived fields above come from (null when no profile matches the sources)
+        "profile": {"file": prof_file, "matches_sources": prof_ok, "git_head": prof.get("git_head"),
+                    "kernel": pk.get("kernel")},
     }
+    if single_ms is not None:
+        out["single_run_ms"] = single_ms
+    if world > 1:
+        out["note_multi_gpu"] = ("cross-rank means are sums of per-rank numpy-order partial sums: Wave2 agrees "
+                                 "with one process within 1e-4 nm (tests/test_dist_gpu.py), not bit for bit")
+    if world == 1 and last_out is not None:
+        out["huygens_pairs_per_s"] = huygens_rate(last_out)
+        out["faithful_psf_chain_ms"] = faithful_psf_chain(rw, last_out, args.pupil)
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     print(json.dumps(out), flush=True)

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define AKB_ABI_VERSION 6
+#define AKB_ABI_VERSION 7
 
 /* status codes */
 #define AKB_OK 0
@@ -127,6 +127,18 @@ int64_t akb_leaf_finish_work_bytes(int nq, int64_t n);
 /* d_sum[nq], d_count[nq] (device) */
 int akb_leaf_finish_f64(const akb_leaf_sink* sink, double* d_sum, int64_t* d_count, void* work,
                         void* stream);
+/* The two halves of akb_leaf_finish_f64, for a sum spread over ranks whose shards are aligned to
+ * numpy's 8192-element buffers (every shard but the last a whole number of buffers): each rank
+ * forms its full buffers' sums d_part[q * part_ld + c] and counts, and its short last buffer's
+ * pairwise sum and count (zero when its shard has none; only the last rank's can be non-empty)... */
+int akb_leaf_parts_f64(const akb_leaf_sink* sink, double* d_part, int64_t* d_part_cnt, int part_ld,
+                       double* d_tail_sum, int64_t* d_tail_cnt, void* stream);
+/* ... and, with every rank's buffer sums gathered in grid order (q-major rows of part_ld), adds
+ * them left to right as numpy does: d_sum[q], d_count[q]. The caller adds the last rank's short
+ * buffer sum last (sum = chain + tail), which is numpy's order exactly: the cross-rank result
+ * equals the single-process one bit for bit. */
+int akb_parts_chain_f64(const double* d_part, const int64_t* d_part_cnt, int part_ld, int nq, int nparts,
+                        double* d_sum, int64_t* d_count, void* stream);
 
 /* ---------------- fused chain (device-resident API) ---------------- */
 
@@ -141,7 +153,9 @@ typedef struct akb_chain_desc {
      * dir[:, iv*n_h + ih] = normalize(1, tan_h[ih], tan_v[iv])   (ref :2711-2717) */
     const double* dir; int64_t dir_ld; int64_t dir_inc;
     const double* tan_h; const double* tan_v; int64_t n_h; int64_t n_v;
-    int64_t row0;                            /* first V-row of this shard (multi-GPU) */
+    int64_t ray0;                            /* first flat ray index iv*n_h + ih of this launch (a
+                                              * multi-GPU shard; RayWave aligns shards to numpy's
+                                              * 8192-element sum buffers) */
     int64_t n_rays;                          /* rays in this launch */
     const double* org; int64_t org_ld; int64_t org_inc; /* NULL => constant source src[] */
     double src[3];
@@ -208,7 +222,7 @@ int akb_tilt_opd_dev_f64(const double* d_params, const double det1_ghij[4], cons
 
 /* The resample picks of a pass-1 descriptor alone: traces only the rays whose exit slopes the
  * equal-angle resample reads (the middle-row range samp_h_begin..samp_h_end and grid column
- * samp_v_col, ref AKB_raytrace_20250312.py:2849-2859) over the whole grid (row0 / n_rays ignored),
+ * samp_v_col, ref AKB_raytrace_20250312.py:2849-2859) over the whole grid (ray0 / n_rays ignored),
  * writing samp_h / samp_v and ORing their flags. RayWave runs it ahead of the full pass 1 so the
  * host resample overlaps the full trace (whose flags it checks after pass 2). */
 int akb_trace_chain_samples_f64(const akb_chain_desc* d, void* stream);
@@ -278,11 +292,12 @@ int akb_opd_f64(const double* total1, const double* total2, const double* det2, 
  * pass-1 launch angles. AKB_E_INVALID with interp1d's message when a point is out of range. */
 int akb_resample_f64(const double* angle_sep, const double* rand, int64_t n, double* out);
 
-/* Wave2 (nm) of a shard's rows sampled onto a size x size pupil in ray-index space (nearest ray,
- * index (k * (n - 1)) // (size - 1)): opd_m[ky][kx] = wave[iv - row0][ih] * 1e-9 for the pupil rows
- * this shard owns, 0 elsewhere (shards are summed across ranks). d_pitch (optional, device [2]):
+/* Wave2 (nm) of a shard (flat rays ray0 .. ray0 + nrays of the n x n grid) sampled onto a size x size
+ * pupil in ray-index space (nearest ray, index (k * (n - 1)) // (size - 1)): opd_m[ky][kx] =
+ * wave[iv * n + ih - ray0] * 1e-9 for the samples this shard owns, 0 elsewhere (shards are summed
+ * across ranks: each sample has one owner, so the sum is exact). d_pitch (optional, device [2]):
  * (max y - min y) / (size - 1), (max z - min z) / (size - 1) from akb_opd_f64's extent keys. */
-int akb_pupil_sample_f64(const double* wave, int64_t row0, int64_t rows, int64_t n, int size,
+int akb_pupil_sample_f64(const double* wave, int64_t ray0, int64_t nrays, int64_t n, int size,
                          const uint64_t* d_extent_keys, double* opd_m, double* d_pitch, void* stream);
 
 /* numpy-exact reduction: for each of `rows` rows of length n (row stride ld),

@@ -35,7 +35,7 @@ def _worker(rank, world, port, n, out_dir):
         shard = Shard.split(n, world, rank)
         rand_h, rand_v, tan_h, tan_v = OPL.angle_tables(g, n)
         dirs = OPL.grid_dirs(tan_h, tan_v)
-        lo, hi = shard.row0 * n, (shard.row0 + shard.rows) * n
+        lo, hi = shard.start, shard.start + shard.count
         _, r4, _ = OPL.chain(g["mirrors"], dirs[:, lo:hi].copy(), np.zeros((3, hi - lo)))
         # this rank's pieces of the resample picks, zero elsewhere (what RayWave._pass1 hands over)
         hb, he, col = sample_plan(n)
@@ -57,15 +57,17 @@ def _worker(rank, world, port, n, out_dir):
         counts = split_counts(10, world)
         piece = torch.arange(sum(counts[:rank]), sum(counts[:rank + 1]), dtype=torch.float64) * (1 + 1j)
         field = comm.allgather_field(piece.to(torch.complex128), counts).numpy()
-        flags = comm.sum_flags(rank)
+        flags = comm.or_flags(1 | (rank << 3))  # rank 0: 0x1, rank 1: 0x9
+        words = torch.tensor([1, rank << 30, -(1 << 31) if rank else 5], dtype=torch.int32)
+        comm.allreduce_or(words)
         if rank == 0:
             np.savez(os.path.join(out_dir, "r0.npz"), sh=sh, sv=sv, tot=tot, mx=mx, field=field,
-                     flags=np.array(flags))
+                     flags=np.array(flags), words=words.numpy())
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n", [33, 34])
+@pytest.mark.parametrize("n", [129, 181])  # shards hold whole 8192-ray buffers: >= 2 of them
 def test_two_rank_shards_reassemble_single_process(tmp_path, n):
     world = 2
     mp.start_processes(_worker, args=(world, _free_port(), n, str(tmp_path)), nprocs=world, join=True,
@@ -87,4 +89,6 @@ def test_two_rank_shards_reassemble_single_process(tmp_path, n):
     assert abs(r["tot"][0] / r["tot"][1] - np.mean(r4[0])) < 1e-15
     assert r["mx"][0] == np.max(r4[1])
     assert np.array_equal(r["field"], np.arange(10) * (1 + 1j))
-    assert int(r["flags"]) == 1
+    # OR over ranks, not a sum: 0x1 | 0x9 = 0x9 (a sum would give 0xa, FLAG_ZERO_NORMAL | ...)
+    assert int(r["flags"]) == 0x9
+    assert r["words"].tolist() == [1, 1 << 30, -(1 << 31) | 5]

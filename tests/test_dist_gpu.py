@@ -1,9 +1,9 @@
 """The N > 1 path on the GPU: two ranks (gloo, both on cuda:0 - a rehearsal of the one-rank-per-GPU
-RCCL run the driver makes on 8 GPUs) trace their V-row shards through the same pipeline bench.py
-runs (pass 1 / resample / pass 2 on the main stream, tilt / OPD / pupil on a second stream) and
-must reassemble what one process computes. Pass 2 is bit-exact per row (the pass-2 tables come
-from the all-reduced picks); after the tilt the means are sums of per-rank numpy-order partial
-sums, so Wave2 and the pupil agree to rounding."""
+RCCL run the driver makes on 8 GPUs) trace their buffer-aligned shards through the same pipeline
+bench.py runs (pass 1 / resample / pass 2 on the main stream, tilt / OPD / pupil on a second
+stream) and must reassemble what one process computes, bit for bit: every rank traces the same
+pass-2 tables, and the means combine the ranks' numpy buffer sums in numpy's own order
+(LeafSink.finish_dist)."""
 import json
 import os
 import socket
@@ -31,7 +31,23 @@ def _geom():
     return SystemGeometry.load(os.path.join(GOLDEN, "akb_geometry.json"))
 
 
-def _worker(rank, world, port, n, runs, out_dir):
+def _systems(k):
+    """k distinct systems (tests/test_gpu_parity.py::_variants): last mirror and detectors moved."""
+    import copy
+    from akbraytracing_amd.wavefront import SystemGeometry
+    with open(os.path.join(GOLDEN, "akb_geometry.json")) as f:
+        base = json.load(f)
+    out = []
+    for i in range(k):
+        d = copy.deepcopy(base)
+        d["mirrors"][-1]["coeffs"][9] = d["mirrors"][-1]["coeffs"][9] * (1.0 + 2e-11 * i)
+        d["det1"][9] = d["det1"][9] - 3e-6 * i
+        d["det2"][9] = d["det2"][9] - 5e-6 * i
+        out.append(SystemGeometry.from_dict(d))
+    return out
+
+
+def _worker(rank, world, port, n, runs, out_dir, schedule="plain"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank), AKB_DIST_BACKEND="gloo")
     import torch.distributed as dist
@@ -51,40 +67,59 @@ def _worker(rank, world, port, n, runs, out_dir):
                 outs.append({k: o[k].cpu().numpy() for k in ("last_hit", "wave2", "dist_err2")} |
                             {"pupil": opd.cpu().numpy()})
 
-        fronts = [rw.launch_front()]
-        for _ in range(runs - 1):
-            prev = fronts[-1]
-            fronts.append(rw.launch_front(overlap=lambda p=prev: back(p)))
-        back(fronts[-1])
+        if schedule == "plain":
+            fronts = [rw.launch_front()]
+            for _ in range(runs - 1):
+                prev = fronts[-1]
+                fronts.append(rw.launch_front(overlap=lambda p=prev: back(p)))
+            back(fronts[-1])
+        else:  # bench.py's --fuse 2 schedule, a different system per run
+            sy = _systems(runs)
+            nx = lambda i: sy[i + 1] if i + 1 < runs else None
+            fr = [rw.launch_front(geometry=sy[0], next_geometry=sy[1])]
+            fr.append(rw.launch_front(fuse=fr[0], geometry=sy[1], next_geometry=nx(1)))
+            for i in range(2, runs):
+                g = fr.pop(0)
+                fr.append(rw.launch_front(overlap=lambda p=g: back(p), fuse=fr[-1], fuse_opd=g, geometry=sy[i],
+                                          next_geometry=nx(i)))
+            for f in fr:
+                back(f)
         torch.cuda.synchronize()
-        np.savez(os.path.join(out_dir, f"r{rank}.npz"), row0=rw.shard.row0, rows=rw.shard.rows,
+        np.savez(os.path.join(out_dir, f"r{rank}.npz"), start=rw.shard.start, count=rw.shard.count,
                  **{f"{k}_{i}": v for i, o in enumerate(outs) for k, v in o.items()})
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n", [129])
-def test_two_ranks_on_the_gpu_reassemble_one_process(gpu, tmp_path, n):
+@pytest.mark.parametrize("n,schedule", [(129, "plain"), (129, "fuse2")])
+def test_two_ranks_on_the_gpu_reassemble_one_process(gpu, tmp_path, n, schedule):
+    """plain: the two-stream pipeline on one system; fuse2: bench.py's default schedule (run k's
+    pass 1 tilts run k-1 and forms run k-2's OPD from cross-rank sums finished on their own stream),
+    a different system per run, against one process's sequential run() of each system."""
     from akbraytracing_amd.wavefront import RayWave
-    runs = 3
+    runs = 3 if schedule == "plain" else 5
+    systems = [_geom()] * runs if schedule == "plain" else _systems(runs)
     rw = RayWave(_geom(), n)
-    one = rw.run()
-    want = {k: one[k].cpu().numpy() for k in ("last_hit", "wave2", "dist_err2")}
-    want_pupil = rw.pupil(32)[0].cpu().numpy()
+    wants = []
+    for g in systems:
+        one = rw.run(geometry=g)
+        wants.append(({k: one[k].cpu().numpy() for k in ("last_hit", "wave2", "dist_err2")},
+                      rw.pupil(32)[0].cpu().numpy()))
     del rw, one
     torch.cuda.synchronize()
-    mp.start_processes(_worker, args=(2, _free_port(), n, runs, str(tmp_path)), nprocs=2, join=True,
+    mp.start_processes(_worker, args=(2, _free_port(), n, runs, str(tmp_path), schedule), nprocs=2, join=True,
                        start_method="spawn")
     parts = [np.load(os.path.join(tmp_path, f"r{r}.npz")) for r in range(2)]
     for i in range(runs):
-        last_hit = np.concatenate([p[f"last_hit_{i}"] for p in parts], axis=1)
-        assert np.array_equal(last_hit, want["last_hit"])  # pass 2: bit-exact per row
-        for k in ("wave2", "dist_err2"):
+        want, want_pupil = wants[i]
+        if schedule == "plain":  # (pipelined deeper, a run's pass-2 rows are rewritten by later runs')
+            last_hit = np.concatenate([p[f"last_hit_{i}"] for p in parts], axis=1)
+            assert np.array_equal(last_hit, want["last_hit"])  # pass 2: bit-exact per ray
+        for k in ("wave2", "dist_err2"):  # the means in numpy's order across ranks: bit-exact too
             got = np.concatenate([p[f"{k}_{i}"] for p in parts])
-            # nm: a constant offset from the cross-rank mean order (observed 2.8e-5); bar 1e-4 nm
-            assert np.max(np.abs(got - want[k])) <= 1e-4, k
+            assert np.array_equal(got, want[k]), (i, k, np.max(np.abs(got - want[k])))
         for p in parts:  # every rank ends with the whole (all-reduced) pupil, OPD in metres
-            assert np.nanmax(np.abs(p[f"pupil_{i}"] - want_pupil)) <= 1e-13
+            assert np.array_equal(p[f"pupil_{i}"], want_pupil), i
 
 
 def test_bench_two_ranks_runs_to_the_json_line(gpu, tmp_path):

@@ -440,6 +440,85 @@ def test_opd_fused_pipeline_equals_sequential_runs(gpu, n):
             assert np.array_equal(a, b)
 
 
+def _variants(k):
+    """k distinct systems over the reference AKB's ray grid: the last mirror's constant term and
+    both detector planes moved a little per system (each run then has its own hits, tilt, means
+    and OPD, so a run's tilt or OPD formed from another run's buffers cannot go unnoticed)."""
+    import copy
+    base = golden_json("akb_geometry.json")
+    from akbraytracing_amd.wavefront import SystemGeometry
+    out = []
+    for i in range(k):
+        d = copy.deepcopy(base)
+        d["mirrors"][-1]["coeffs"][9] = d["mirrors"][-1]["coeffs"][9] * (1.0 + 2e-11 * i)
+        d["det1"][9] = d["det1"][9] - 3e-6 * i
+        d["det2"][9] = d["det2"][9] - 5e-6 * i
+        out.append(SystemGeometry.from_dict(d))
+    return out
+
+
+@pytest.mark.parametrize("n", [65, 301])
+def test_opd_fused_pipeline_distinct_systems(gpu, n):
+    """The default pipeline (--fuse 2) with every run tracing another system: run k's pass-1
+    kernel tilts run k-1 (with run k-1's detector planes and rotation) and forms run k-2's OPD
+    (from run k-2's tilt sums); each run's Wave2, DistError2, detector-2 hits, totals, means and
+    pupil pitch equal a sequential run() of that same system, bit for bit."""
+    from akbraytracing_amd.wavefront import RayWave
+    systems = _variants(6)
+    rw = RayWave(systems[0], n)
+    want = []
+    for g in systems:
+        seq = rw.run(geometry=g)
+        opd, pitch = rw.pupil(32)
+        want.append(({k: seq[k].clone() for k in ("wave2", "dist_err2", "detcenter2", "total2")},
+                     opd.clone(), pitch.clone(), rw.means()))
+    # the systems really differ run to run
+    assert not torch.equal(want[0][0]["wave2"], want[1][0]["wave2"])
+    assert not np.array_equal(want[0][3][1], want[1][3][1])
+    bs = torch.cuda.Stream()
+    outs, kinds = [], []
+
+    def back(front):
+        kinds.append((front.tilt is not None, front.opd is not None))
+        with torch.cuda.stream(bs):
+            o = rw.launch_back(front, stream=bs)
+            outs.append(({k: o[k].clone() for k in want[0][0]}, *(t.clone() for t in rw.pupil(32)), rw.means()))
+
+    nxt = lambda i: systems[i + 1] if i + 1 < len(systems) else None
+    fr = [rw.launch_front(geometry=systems[0], next_geometry=systems[1])]
+    fr.append(rw.launch_front(fuse=fr[0], geometry=systems[1], next_geometry=systems[2]))
+    for i in range(2, len(systems)):
+        g = fr.pop(0)
+        fr.append(rw.launch_front(overlap=lambda p=g: back(p), fuse=fr[-1], fuse_opd=g, geometry=systems[i],
+                                  next_geometry=nxt(i)))
+    for f in fr:
+        back(f)
+    torch.cuda.synchronize()
+    assert kinds == [(True, True)] * 4 + [(True, False), (False, False)]
+    for i, ((o, opd, pitch, m), (w, wopd, wpitch, wm)) in enumerate(zip(outs, want)):
+        for k, v in w.items():
+            assert torch.equal(o[k], v), (i, k)
+        assert torch.equal(opd, wopd) and torch.equal(pitch, wpitch), i
+        for a, b in zip(m, wm):
+            assert np.array_equal(a, b), i
+
+
+def test_prepass_for_an_unannounced_system_is_redone(gpu):
+    """A run whose system differs from the one its picks prepass was queued for (no
+    next_geometry) redoes the prepass: same bits as a fresh RayWave on that system."""
+    from akbraytracing_amd.wavefront import RayWave
+    a, b = _variants(2)
+    want = RayWave(b, 65).run()["wave2"].clone()
+    rw = RayWave(a, 65)
+    rw.run()
+    assert torch.equal(rw.run(geometry=b)["wave2"], want)
+    with pytest.raises(ValueError):
+        import copy
+        c = copy.deepcopy(b)
+        c.angle_h = type(c.angle_h)(c.angle_h.start * 1.01, c.angle_h.stop, c.angle_h.offset)
+        rw.run(geometry=c)
+
+
 def test_fused_pipeline_falls_back_where_it_cannot_fuse(gpu):
     """launch_front(fuse=...) on a single-detector system (KB) or a full run keeps the tilt in
     the back half and still gives run()'s bits."""

@@ -65,12 +65,17 @@ def test_geometry_and_sample_plan():
         c2, v_idx, s2, e2, h_idx = OPL.sample_indices(n, n)
         assert (hb, he, col) == (s2, e2, c2)
         assert he - hb == n
-    for n, w in ((3163, 8), (65, 2), (10, 3), (8945, 8)):
+    # flat shards cut at numpy's 8192-element sum buffers (the last one takes the short buffer)
+    for n, w in ((3163, 8), (129, 2), (10000, 8), (8945, 8), (3163, 1), (65, 1)):
         shards = [Shard.split(n, w, r) for r in range(w)]
-        assert shards[0].row0 == 0
-        assert sum(s.rows for s in shards) == n
+        assert shards[0].start == 0 and sum(s.count for s in shards) == n * n
         for a, b in zip(shards, shards[1:]):
-            assert a.row0 + a.rows == b.row0
+            assert a.start + a.count == b.start and a.count % 8192 == 0
+        counts = [s.full_buffers() for s in shards]
+        assert max(counts) - min(counts) <= 1 and sum(counts) == n * n // 8192
+    assert [s.count for s in (Shard.split(10000, 8, r) for r in range(8))][:2] == [1526 * 8192, 1526 * 8192]
+    with pytest.raises(ValueError):
+        Shard.split(65, 2, 0)  # 4225 rays: no full buffer to give each rank
 
 
 def test_angle_tables_match_reference_fixture():
