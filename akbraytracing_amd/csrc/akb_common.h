@@ -327,6 +327,19 @@ __device__ __forceinline__ void reflect_raw(double l, double m, double n, double
     rz = n - A2 * nz;
 }
 
+struct Mat3 {
+    double m[9];
+};
+
+// R @ v for a 3x3 R in the order OpenBLAS dgemm forms it for the reference's (3,3) @ (3,N)
+// products (AKB_raytrace_20250312.py:929): r0*x, then fma(r1, y, .), then fma(r2, z, .)
+__device__ __forceinline__ void matvec(const Mat3& R, double x, double y, double z, double& ox,
+                                       double& oy, double& oz) {
+    ox = __builtin_fma(R.m[2], z, __builtin_fma(R.m[1], y, R.m[0] * x));
+    oy = __builtin_fma(R.m[5], z, __builtin_fma(R.m[4], y, R.m[3] * x));
+    oz = __builtin_fma(R.m[8], z, __builtin_fma(R.m[7], y, R.m[6] * x));
+}
+
 // plane_ray_intersection (EllipseRaytrace3D.py:150-155)
 __device__ __forceinline__ void plane_hit(double g, double h, double i, double j, double l, double m,
                                           double n, double p, double q, double r, double& x,

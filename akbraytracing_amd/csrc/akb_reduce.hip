@@ -17,124 +17,14 @@
 // formed. k_pw_final finishes a row: the buffer results added left to right, then the short last
 // buffer's pairwise sum (its split tree built and combined level by level by one wave).
 #include "akb_common.h"
+#include "akb_pairwise.h"
 
 namespace akb {
 
 constexpr int kPwBuf = 8192;
-constexpr int kPwLeaf = 128;
 constexpr int kPwStride = 136;  // LDS doubles per leaf (128 + 8 padding)
 constexpr int kPwThreads = 256;
-constexpr int kTreeLevels = 8;  // a short buffer (< 8192) has leaves down to depth 7, <= 64 per level
 constexpr int kFinalTile = 4096;
-
-__device__ __forceinline__ int pw_split(int n) {
-    int n2 = n / 2;
-    return n2 - (n2 % 8);
-}
-
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-__device__ __forceinline__ double readlane_f64(double v, int l) {
-    const long long b = __double_as_longlong(v);
-    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(b & 0xffffffffLL), l);
-    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(b >> 32), l);
-    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
-}
-
-__device__ __forceinline__ double nan_zero(double v, bool nan0, long long& cnt) {
-    if (nan0 && v != v) return 0.0;
-    ++cnt;
-    return v;
-}
-
-// numpy pairwise leaf (n <= 128) over staged values (NaN already replaced)
-__device__ double pw_leaf_lds(const double* a, int n) {
-    if (n < 8) {
-        double res = 0.0;
-        for (int i = 0; i < n; ++i) res = res + a[i];
-        return res;
-    }
-    double r[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) r[j] = a[j];
-    int i = 8;
-    for (; i < n - (n % 8); i += 8) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) r[j] = r[j] + a[i + j];
-    }
-    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-    for (; i < n; ++i) res = res + a[i];
-    return res;
-}
-
-struct PwTree {
-    int off[kTreeLevels][64];
-    int len[kTreeLevels][64];
-    int child[kTreeLevels][64];
-    double val[kTreeLevels][64];
-};
-
-// numpy pairwise_sum of a[0..len), 0 < len < 8192, by one wave: the split tree is built top-down
-// one level per step (a node of more than 128 elements splits at pw_split(n) into left and right
-// children, placed in order by a ballot prefix count), each leaf is summed by one lane, and the
-// levels are combined bottom-up as left + right.
-__device__ double pw_tree_wave(PwTree& T, const double* a, int len) {
-    const int lane = threadIdx.x & 63;
-    if (lane == 0) {
-        T.off[0][0] = 0;
-        T.len[0][0] = len;
-    }
-    int nd[kTreeLevels];
-    nd[0] = 1;
-    int depth = 1;
-    wave_sync();
-#pragma unroll
-    for (int d = 0; d < kTreeLevels; ++d) {
-        if (d < depth) {
-            const bool act = lane < nd[d];
-            int o = 0, l = 0;
-            if (act) {
-                o = T.off[d][lane];
-                l = T.len[d][lane];
-            }
-            const bool split = act && l > kPwLeaf && d + 1 < kTreeLevels;
-            const unsigned long long m = __ballot(split);
-            if (split) {
-                const int pos = 2 * __popcll(m & ((1ull << lane) - 1ull));
-                const int l2 = pw_split(l);
-                if (d + 1 < kTreeLevels) {
-                    T.off[d + 1][pos] = o;
-                    T.len[d + 1][pos] = l2;
-                    T.off[d + 1][pos + 1] = o + l2;
-                    T.len[d + 1][pos + 1] = l - l2;
-                }
-                T.child[d][lane] = pos;
-            } else if (act) {
-                T.val[d][lane] = pw_leaf_lds(a + o, l);
-            }
-            if (m && d + 1 < kTreeLevels) {
-                nd[d + 1] = 2 * __popcll(m);
-                depth = d + 2;
-            }
-            wave_sync();
-        }
-    }
-#pragma unroll
-    for (int d = kTreeLevels - 2; d >= 0; --d) {
-        if (d + 1 < depth) {
-            if (lane < nd[d] && T.len[d][lane] > kPwLeaf) {
-                const int c = T.child[d][lane];
-                T.val[d][lane] = T.val[d + 1][c] + T.val[d + 1][c + 1];
-            }
-            wave_sync();
-        }
-    }
-    return T.val[0][0];
-}
 
 // part / part_cnt: row r, buffer c lands at [r * part_ld + c]; only full buffers come here
 __global__ void __launch_bounds__(kPwThreads) k_pw_chunks(const double* __restrict__ x, int64_t ld, int nan_mask,

@@ -11,7 +11,9 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdlib>
+#include <cstring>
 #include <mutex>
+#include <vector>
 
 #include "akb_common.h"
 #include "akb_sincos.h"
@@ -111,19 +113,6 @@ __global__ void __launch_bounds__(kBlock) k_seglen(V3In a, V3In b, int64_t n, do
          i += (int64_t)gridDim.x * blockDim.x) {
         out[i] = norm3(b.x(i) - a.x(i), b.y(i) - a.y(i), b.z(i) - a.z(i));
     }
-}
-
-struct Mat3 {
-    double m[9];
-};
-
-// R @ v for a 3x3 R in the order OpenBLAS dgemm forms it for the reference's (3,3) @ (3,N)
-// products (AKB_raytrace_20250312.py:929): r0*x, then fma(r1, y, .), then fma(r2, z, .)
-__device__ __forceinline__ void matvec(const Mat3& R, double x, double y, double z, double& ox,
-                                       double& oy, double& oz) {
-    ox = __builtin_fma(R.m[2], z, __builtin_fma(R.m[1], y, R.m[0] * x));
-    oy = __builtin_fma(R.m[5], z, __builtin_fma(R.m[4], y, R.m[3] * x));
-    oz = __builtin_fma(R.m[8], z, __builtin_fma(R.m[7], y, R.m[6] * x));
 }
 
 __global__ void __launch_bounds__(kBlock) k_rotate(Mat3 Ry, Mat3 Rz, double cx, double cy, double cz,
@@ -759,6 +748,21 @@ __global__ void __launch_bounds__(kBlock, kWaves) k_chain_sink(ChainArgs a) {
         if (valid) chain_ray<kGrid, kOPL, true, false, false, kPointSrc, kFixed>(a, seg * kLeafSeg, t, fl, qv);
         leaf_sink_segment<5>(a.sink, L, seg * kLeafSeg, qv, valid);
     }
+    if (fl) atomicOr(a.flags, fl);
+}
+
+// S independent grid systems in one launch: auto_focus_NA and calc_FoC trace many small systems
+// that differ in their mirrors, launch tables or source (ref AKB_raytrace_20250312.py:12776-12786,
+// :13780-13784). blockIdx.y picks the system; its kernel arguments sit in device memory at a
+// wave-uniform address, so every field is a scalar load, as from the argument segment.
+template <bool kOPL, bool kHits>
+__global__ void __launch_bounds__(kBlock) k_chain_batch(const ChainArgs* __restrict__ A) {
+    const ChainArgs& a = A[blockIdx.y];
+    int fl = 0;
+    double qv[5];
+    const int t = threadIdx.x;
+    for (int64_t i0 = blockIdx.x * (int64_t)kBlock; i0 < a.n; i0 += (int64_t)gridDim.x * kBlock)
+        if (i0 + t < a.n) chain_ray<true, kOPL, false, kHits, false, false>(a, i0, t, fl, qv);
     if (fl) atomicOr(a.flags, fl);
 }
 
@@ -1495,6 +1499,50 @@ int akb_trace_chain_f64(const akb_chain_desc* d, void* stream) {
     return launch_status("k_chain");
 }
 
+// Kernel arguments of a batched launch travel through pinned host memory: a small ring of slots,
+// each reused only after the event recorded behind its last copy has completed (the copy must not
+// read a slot the next call is refilling). One ring per device.
+namespace {
+struct ArgSlot {
+    void* host = nullptr;
+    size_t cap = 0;
+    hipEvent_t done = nullptr;
+};
+struct ArgRing {
+    static constexpr int kSlots = 8;
+    ArgSlot slot[kSlots];
+    int next = 0;
+};
+std::mutex g_ring_mu;
+ArgRing g_rings[64];
+}  // namespace
+
+// copy `bytes` of host data to a fresh stream-ordered device allocation (*d_out, freed by the
+// caller with hipFreeAsync on the same stream after its launch)
+static int stage_args(const void* src, size_t bytes, hipStream_t s, void** d_out) {
+    int dev = 0;
+    AKB_HIP_CHECK(hipGetDevice(&dev));
+    AKB_REQUIRE(dev >= 0 && dev < 64, "device index beyond 64");
+    std::lock_guard<std::mutex> lock(g_ring_mu);
+    ArgRing& R = g_rings[dev];
+    ArgSlot& S = R.slot[R.next];
+    R.next = (R.next + 1) % ArgRing::kSlots;
+    if (S.done) AKB_HIP_CHECK(hipEventSynchronize(S.done));
+    else AKB_HIP_CHECK(hipEventCreateWithFlags(&S.done, hipEventDisableTiming));
+    if (S.cap < bytes) {
+        if (S.host) AKB_HIP_CHECK(hipHostFree(S.host));
+        S.host = nullptr;
+        S.cap = 0;
+        AKB_HIP_CHECK(hipHostMalloc(&S.host, bytes, hipHostMallocDefault));
+        S.cap = bytes;
+    }
+    memcpy(S.host, src, bytes);
+    AKB_HIP_CHECK(hipMallocAsync(d_out, bytes, s));
+    AKB_HIP_CHECK(hipMemcpyAsync(*d_out, S.host, bytes, hipMemcpyHostToDevice, s));
+    AKB_HIP_CHECK(hipEventRecord(S.done, s));
+    return AKB_OK;
+}
+
 // validate a tilt's operands and fill its kernel arguments (the rotation comes from the caller)
 static int tilt_args_from(TiltArgs& a, const double det1_ghij[4], const double det2_ghij[4], const double* dir,
                           const double* pt, const double* opl, int64_t ld, int64_t n, double* dir_rot, double* pt_rot,
@@ -1622,6 +1670,47 @@ int akb_tilt_opd_dev_f64(const double* d_params, const double det1_ghij[4], cons
     a.params = d_params;
     return launch_tilt(a, det1_ghij, det2_ghij, dir, pt, opl, ld, n, dir_rot, pt_rot, det1, det2, total1, total2,
                        sink, stream);
+}
+
+int akb_trace_chain_batch_f64(const akb_chain_desc* descs, int n_sys, void* stream) {
+    clear_error();
+    AKB_REQUIRE(descs != nullptr && n_sys > 0 && n_sys <= 65535, "need 1..65535 descriptors");
+    std::vector<ChainArgs> args((size_t)n_sys);
+    int64_t nmax = 0;
+    for (int s = 0; s < n_sys; ++s) {
+        const akb_chain_desc* d = descs + s;
+        bool empty = false;
+        const int st = chain_args_from(d, args[s], empty);
+        if (st != AKB_OK) return st;
+        AKB_REQUIRE(d->dir == nullptr, "batched systems take grid rays (tan_h / tan_v)");
+        AKB_REQUIRE(d->sink.nq == 0 && d->samp_h == nullptr && d->samp_v == nullptr && d->copy_n == 0,
+                    "batched systems have no sink, resample picks or staging copy");
+        AKB_REQUIRE((d->opl != nullptr) == (descs[0].opl != nullptr) &&
+                        (d->hits != nullptr) == (descs[0].hits != nullptr),
+                    "every system of a batch asks for the same opl / hits rows");
+        if (empty) args[s].n = 0;
+        if (args[s].n > nmax) nmax = args[s].n;
+    }
+    if (nmax == 0) return AKB_OK;
+    hipStream_t s = (hipStream_t)stream;
+    void* d_args = nullptr;
+    int st = stage_args(args.data(), sizeof(ChainArgs) * args.size(), s, &d_args);
+    if (st != AKB_OK) return st;
+    const unsigned gx = grid_for(nmax, 1, 4096);
+    const dim3 grid(gx, (unsigned)n_sys);
+    const ChainArgs* A = (const ChainArgs*)d_args;
+    const bool opl = descs[0].opl != nullptr, hits = descs[0].hits != nullptr;
+    if (opl && hits)
+        k_chain_batch<true, true><<<grid, kBlock, 0, s>>>(A);
+    else if (opl)
+        k_chain_batch<true, false><<<grid, kBlock, 0, s>>>(A);
+    else if (hits)
+        k_chain_batch<false, true><<<grid, kBlock, 0, s>>>(A);
+    else
+        k_chain_batch<false, false><<<grid, kBlock, 0, s>>>(A);
+    st = launch_status("k_chain_batch");
+    AKB_HIP_CHECK(hipFreeAsync(d_args, s));
+    return st;
 }
 
 int akb_trace_chain_samples_f64(const akb_chain_desc* d, void* stream) {

@@ -29,6 +29,9 @@
  *   akb_huygens_f64      compute_u_parallel / forward_propagation_*_batch
  *                        Wavecalc_raytrace_fromData_CPU0402.py:71-124, ..._GPU0402.py:64-201
  *   akb_psf_f64          compute_psf_fft         psf_fft.py:29-125 (FFT on rocFFT)
+ *   akb_trace_chain_batch_f64 + akb_focus_eval_f64
+ *                        plot_result_debug(params, 'test') / auto_focus_NA's sweeps
+ *                        AKB_raytrace_20250312.py:2770-2847, :3565-3601, :12746-12895
  */
 #ifndef AKB_RAYTRACE_H
 #define AKB_RAYTRACE_H
@@ -39,7 +42,7 @@
 extern "C" {
 #endif
 
-#define AKB_ABI_VERSION 7
+#define AKB_ABI_VERSION 8
 
 /* status codes */
 #define AKB_OK 0
@@ -249,6 +252,26 @@ int akb_chain_tilt_opd_f64(const akb_chain_desc* d, const double* d_params, cons
                            const double* opd_total2, const double* opd_det2, const double* d_sum5,
                            const int64_t* d_cnt5, double* dist_err2, double* wave, uint64_t* d_extent_keys,
                            void* stream);
+
+/* S independent systems in one launch (auto_focus_NA / calc_FoC trace many small systems, ref
+ * AKB_raytrace_20250312.py:12776-12786, :13780-13784): descs[s] is an akb_trace_chain_f64 descriptor
+ * (host array) with grid rays, no sink, resample picks or staging copy, and every system asking for
+ * the same opl / hits rows. Each system's outputs and flag word are its own. */
+int akb_trace_chain_batch_f64(const akb_chain_desc* descs, int n_sys, void* stream);
+
+/* The focus evaluation of plot_result_debug's 'test' mode and auto_focus_NA's spot sizes (ref
+ * :2842-2847, :3565-3601, :12785-12786) for traced rays: system s has its exit directions and last
+ * hits at dir / pt + s * sys_ld ((3, n) rows each) and n_planes detector planes x = -j,
+ * d_plane_j[s * n_planes + p] (coeffs_det[9]). d_rot (device, (n_sys, 18): R_y then R_z of
+ * rotate_vectors, row-major) applies the tilt - det0 = plane(dir, pt), focus = np.mean(det0, axis=1),
+ * dir' = R_y@(R_z@dir), pt' = R_y@(R_z@(pt - focus)) + focus, det = plane(dir', pt') - or NULL for
+ * option_tilt=False (det = det0). d_std (n_sys * n_planes, 2) = np.std(det[2]), np.std(det[1]), every
+ * sum in numpy's order. det_out / dir_out (optional, (n_sys * n_planes, 3, n)): det and the
+ * (tilted) directions, the 'test' return's detcenter and angle. work: akb_focus_eval_work_bytes. */
+int64_t akb_focus_eval_work_bytes(int n_sys, int n_planes, int64_t n);
+int akb_focus_eval_f64(const double* dir, const double* pt, int64_t n, int64_t sys_ld, int n_sys, int n_planes,
+                       const double* d_plane_j, const double* d_rot, double* d_std, double* det_out, double* dir_out,
+                       void* work, void* stream);
 
 /* Focus sweep rows (find_defocus, ref :9086-9170): for P detector planes x = -d_plane_j[p]
  * (coefficients g = 1, h = i = 0, j = d_plane_j[p], as coeffs_det[9] = -(s2f_middle + a)), the
