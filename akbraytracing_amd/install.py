@@ -17,8 +17,11 @@ forward_propagation_cupy_batch(_multi_gpu), used by their WaveField3D.forward_pr
 The driver's steps after the trace are rebound too: griddata (the module's
 `from scipy.interpolate import griddata`, :28), plane_correction_with_nan_and_outlier_filter,
 psf_calc (reading the module's live option_energy / option_AKB / directory_name as the reference
-does, :1161-1166, :1202-1214, :1271-1273), find_defocus and calc_dS. install(mod, names=[...])
-picks a subset; uninstall(mod) restores every original.
+does, :1161-1166, :1202-1214, :1271-1273), find_defocus and calc_dS. plot_result_debug's 'test'
+mode and auto_focus_NA (:12746) run the batched device search (autofocus.py) for the live Wolter
+III+I AKB system; the reference's auto_focus_sep, calc_FoC and alignment loops reach them through
+the module globals. install(mod, names=[...]) picks a subset; uninstall(mod) restores every
+original.
 
 The wrappers read the module's live `option_mpmath` flag (AKB_raytrace_20250312.py:92) at call
 time and hand the call to the original function when it is set (the mpmath branch, :399-443).
@@ -45,6 +48,47 @@ def _psf_calc_for(mod):
         return None  # the reference's psf_calc returns nothing; its results are the .npy files
     return psf_calc
 
+def _akb_native_ok(mod):
+    """The batched focus search restates the Wolter III+I system of the live plot_result_debug
+    (:1325 `if option_wolter_3_1`) for option_AKB; anything else stays the reference's."""
+    return (getattr(mod, "option_AKB", False) and getattr(mod, "option_wolter_3_1", False)
+            and not getattr(mod, "option_mpmath", False))
+
+
+def _plot_result_debug_for(mod, original):
+    """plot_result_debug with its 'test' mode (the one auto_focus_NA and the alignment loops call
+    hundreds of times) on the device; every other mode runs the reference's own function, whose
+    primitives install() has rebound."""
+    def plot_result_debug(params, option, source_shift=[0., 0., 0.], option_tilt=True, option_legendre=False,
+                          angular_shift=[0., 0.], option_save=True):
+        if option == "test" and _akb_native_ok(mod) and list(angular_shift) == [0., 0.]:
+            from .autofocus import plot_result_test
+            return plot_result_test(params, source_shift, option_tilt, option_set=bool(getattr(mod, "option_set", False)))
+        return original(params, option, source_shift=source_shift, option_tilt=option_tilt,
+                        option_legendre=option_legendre, angular_shift=angular_shift, option_save=option_save)
+    return plot_result_debug
+
+
+def _auto_focus_for(mod, original):
+    """auto_focus_NA (:12746) with every sweep on the device, reading the module's live flags
+    (widesearch :98, option_set :94) as the reference does; KB systems, the mpmath branch and the
+    tandem variants run the reference's own function."""
+    def auto_focus_NA(num_adj_astg, initial_params, na_ratio_h, na_ratio_v, option, option_param,
+                      option_disp='ray', option_mode=False, source_shift0=[0., 0., 0.], option_legendre=False):
+        if not _akb_native_ok(mod):
+            return original(num_adj_astg, initial_params, na_ratio_h, na_ratio_v, option, option_param,
+                            option_disp=option_disp, option_mode=option_mode, source_shift0=source_shift0,
+                            option_legendre=option_legendre)
+        from .autofocus import auto_focus_NA as native
+        return native(num_adj_astg, initial_params, na_ratio_h, na_ratio_v, option, option_param,
+                      option_disp=option_disp, option_mode=option_mode, source_shift0=source_shift0,
+                      option_legendre=option_legendre, widesearch=bool(getattr(mod, "widesearch", False)),
+                      option_set=bool(getattr(mod, "option_set", False)), driver=mod)
+    return auto_focus_NA
+
+
+_PER_MODULE = {"plot_result_debug": _plot_result_debug_for, "auto_focus_NA": _auto_focus_for}
+
 _NATIVE = {
     "mirr_ray_intersection": _P.mirr_ray_intersection,
     "norm_vector": _P.norm_vector,
@@ -62,6 +106,8 @@ _NATIVE = {
     "find_defocus": _lazy("focus", "find_defocus"),
     "calc_dS": _lazy("wavedata", "calc_dS"),
     "psf_calc": None,  # bound per module (_psf_calc_for)
+    "plot_result_debug": None,  # bound per module (_PER_MODULE)
+    "auto_focus_NA": None,
 }
 # functions with an mpmath branch in the reference
 _MPMATH_AWARE = {"mirr_ray_intersection", "reflect_ray"}
@@ -87,6 +133,13 @@ def install(mod, names=None):
             continue
         cur = getattr(mod, name)
         if getattr(cur, "__akb_native__", False):
+            done.append(name)
+            continue
+        if name in _PER_MODULE:
+            w = _PER_MODULE[name](mod, cur)
+            w.__wrapped__ = cur
+            w.__akb_native__ = True
+            setattr(mod, name, w)
             done.append(name)
             continue
         native = _NATIVE[name] if _NATIVE[name] is not None else _psf_calc_for(mod)

@@ -245,3 +245,31 @@ def test_batched_trace_equals_single_launches(gpu):
         assert torch.equal(r.hits, ts.hits[s])
         assert torch.equal(r.dir_out, ts.dir[s])
         assert torch.equal(r.last_hit, ts.pt[s])
+
+
+@pytest.mark.gpu
+def test_install_rebinds_test_mode_and_auto_focus(gpu):
+    """install() on a driver-like module: plot_result_debug(params, 'test') and auto_focus_NA go to
+    the device for the Wolter III+I AKB system and to the module's own functions otherwise
+    (other modes, KB systems, mpmath)"""
+    import types
+    import akbraytracing_amd
+    f = golden(AF)
+    mod = types.ModuleType("fake_driver")
+    mod.option_AKB, mod.option_wolter_3_1, mod.option_mpmath = True, True, False
+    mod.option_set, mod.widesearch = True, False
+    seen = []
+    mod.plot_result_debug = lambda params, option, **kw: seen.append(option) or "orig"
+    mod.auto_focus_NA = lambda *a, **kw: seen.append("af") or "orig-af"
+    akbraytracing_amd.install(mod)
+    c = _case(f, 0)
+    r = mod.plot_result_debug(c["params"], "test")
+    assert np.array_equal(r[4], f["g0_detcenter"]) and not seen
+    assert mod.plot_result_debug(c["params"], "ray_wave") == "orig" and seen == ["ray_wave"]
+    p = f["af0_start"].copy()
+    ret = mod.auto_focus_NA(50, p, 1, 1, False, "")
+    assert np.array_equal(np.array(ret[:2]), f["af0_ret"]) and np.array_equal(p, f["af0_params_after"])
+    mod.option_AKB = False  # KB_debug systems: the reference's own loop
+    assert mod.auto_focus_NA(50, p, 1, 1, False, "") == "orig-af"
+    akbraytracing_amd.uninstall(mod)
+    assert mod.plot_result_debug(c["params"], "test") == "orig"

@@ -6,13 +6,15 @@ OCML atan instead of glibc atan, so the tilt angles may differ by an ulp: rotate
 held to a few ulp and the OPD to 1e-4 nm absolute. PSF intensity and Huygens
 fields: 1e-6 relative to the peak / max magnitude (BASELINE.json north_star), observed ~1e-12.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
 
 import oracle as O
 import oracle.pipeline as OPL
-from conftest import golden, golden_json
+from conftest import ROOT, golden, golden_json
 
 pytestmark = pytest.mark.gpu
 
@@ -1113,3 +1115,35 @@ def test_ray_wave_1e7_properties(gpu):
     assert rw.means()[0][1] == np.nanmean(t2)
     # the OPD's spread at 1e7 rays stays within the 65^2 reference's order of magnitude (nm)
     assert 1e-4 < np.nanstd(w) < 1.0
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+def test_psf_fft_example_at_its_own_size(gpu):
+    """psf_fft_example.py unmodified in substance: `from psf_fft import compute_psf_fft` resolving
+    to dropin/psf_fft.py, its 1024^2 pupil at pad_factor=16 -> 16384^2, against the reference's
+    own run (tests/golden/psf_example.npz: peak, 64^2 crop, 256^2 block sums, centre row / column,
+    total, axes). Tolerance: 1e-10 of the peak (rocFFT vs pocketfft rounding)."""
+    import importlib
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "akbraytracing_amd", "dropin"))
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    try:
+        sys.modules.pop("psf_fft", None)
+        psf_fft = importlib.import_module("psf_fft")
+        from make_golden_psf_example import example_inputs, summarize
+    finally:
+        sys.path.pop(0)
+        sys.path.pop(0)
+    assert psf_fft.__file__.startswith(os.path.join(ROOT, "akbraytracing_amd"))
+    opd, amp, wl, dx, f = example_inputs()
+    psf, x_im, y_im = psf_fft.compute_psf_fft(opd, amp, wl, dx, f, pad_factor=16, window=None)
+    got = summarize(psf, x_im, y_im)
+    del psf
+    ref = golden("psf_example.npz")
+    assert np.array_equal(got["shape"], ref["shape"]) and np.array_equal(got["peak"], ref["peak"])
+    assert np.array_equal(got["x_im_sub"], ref["x_im_sub"]) and np.array_equal(got["y_im_sub"], ref["y_im_sub"])
+    for k in ("crop", "row", "col"):
+        assert np.max(np.abs(got[k] - ref[k])) <= 1e-10, k
+    assert np.max(np.abs(got["blocks"] - ref["blocks"])) <= 1e-10 * 256 * 256
+    assert abs(got["total"] - ref["total"]) <= 1e-10 * ref["total"]
