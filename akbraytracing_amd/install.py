@@ -64,6 +64,11 @@ def _plot_result_debug_for(mod, original):
         if option == "test" and _akb_native_ok(mod) and list(angular_shift) == [0., 0.]:
             from .autofocus import plot_result_test
             return plot_result_test(params, source_shift, option_tilt, option_set=bool(getattr(mod, "option_set", False)))
+        if (option == "wave" and _akb_native_ok(mod) and list(angular_shift) == [0., 0.]
+                and getattr(mod, "option_rotate", True) and getattr(mod, "wave_num_H", 0) == getattr(mod, "wave_num_V", 1)):
+            from .wavedata import plot_result_wave
+            return plot_result_wave(params, mod.wave_num_H, defocus_for_wave=getattr(mod, "defocusForWave", 1e-3),
+                                    option_set=bool(getattr(mod, "option_set", False)), source_shift=source_shift)
         return original(params, option, source_shift=source_shift, option_tilt=option_tilt,
                         option_legendre=option_legendre, angular_shift=angular_shift, option_save=option_save)
     return plot_result_debug
@@ -87,7 +92,29 @@ def _auto_focus_for(mod, original):
     return auto_focus_NA
 
 
-_PER_MODULE = {"plot_result_debug": _plot_result_debug_for, "auto_focus_NA": _auto_focus_for}
+def _save_wave_for(mod, original):
+    """saveWaveData (:13475) with the 'wave' trace, calc_dS and the grids on the device, reading
+    the module's flags (wave_num_H / V, defocusForWave, downsample_*, option_HighNA, option_2mirror,
+    option_avrgsplt, option_set) as the reference does, and ending the process with sys.exit() as
+    it does (:13763). KB systems run the reference's own function."""
+    def saveWaveData(initial_params, ysize=1e-6, zsize=1e-6):
+        if not (_akb_native_ok(mod) and getattr(mod, "option_rotate", True)):
+            return original(initial_params, ysize=ysize, zsize=zsize)
+        import sys
+        from .wavedata import saveWaveData as native
+        g = lambda k, d: getattr(mod, k, d)  # noqa: E731
+        native(initial_params, ysize, zsize, ray_num_H=g("wave_num_H", 65), ray_num_V=g("wave_num_V", 65),
+               defocus_for_wave=g("defocusForWave", 1e-3),
+               downsample=tuple(g(k, 0) for k in ("downsample_h1", "downsample_v1", "downsample_h2", "downsample_v2",
+                                                  "downsample_h_f", "downsample_v_f")),
+               option_set=bool(g("option_set", False)), option_HighNA=g("option_HighNA", True),
+               option_2mirror=g("option_2mirror", True), option_avrgsplt=g("option_avrgsplt", False))
+        sys.exit()
+    return saveWaveData
+
+
+_PER_MODULE = {"plot_result_debug": _plot_result_debug_for, "auto_focus_NA": _auto_focus_for,
+               "saveWaveData": _save_wave_for}
 
 _NATIVE = {
     "mirr_ray_intersection": _P.mirr_ray_intersection,
@@ -108,6 +135,7 @@ _NATIVE = {
     "psf_calc": None,  # bound per module (_psf_calc_for)
     "plot_result_debug": None,  # bound per module (_PER_MODULE)
     "auto_focus_NA": None,
+    "saveWaveData": None,
 }
 # functions with an mpmath branch in the reference
 _MPMATH_AWARE = {"mirr_ray_intersection", "reflect_ray"}

@@ -64,11 +64,12 @@ def image_grid(detcenter, size_h, size_v, ysize, zsize):
 
 def save_wave_data(directory, source, mirrors, ray_num_V, ray_num_H, detcenter, detcenter2=None, params=None,
                    ysize=1e-6, zsize=1e-6, defocus_for_wave=0.0, option_AKB=True, option_HighNA=True,
-                   option_2mirror=False, option_avrgsplt=False, timestamp=""):
-    """The file set of saveWaveData (:13498-13764) without downsampling (odd grids with the
-    reference's downsample factors at 0). mirrors: [M1, M2(, M3, M4)] hit points (3, V*H) in the
-    reference's naming (M1 = first vertical hyperbola, M2 = horizontal hyperbola, M3 / M4 the
-    ellipses). Returns the paths written."""
+                   option_2mirror=False, option_avrgsplt=False, timestamp="", sizes=None):
+    """The file set of saveWaveData (:13506-13654). mirrors: [M1, M2(, M3, M4)] hit points
+    (3, V*H) in the reference's naming (M1 = first vertical hyperbola, M2 = horizontal hyperbola,
+    M3 / M4 the ellipses). sizes: ((v1, h1), (v2, h2), (vf, hf)) grid shapes of M1 / M3, M2 / M4
+    and the detector rows after downsample_array_3_n (default: all ray_num_V x ray_num_H).
+    Returns the paths written."""
     os.makedirs(directory, exist_ok=True)
     written = []
 
@@ -77,17 +78,22 @@ def save_wave_data(directory, source, mirrors, ray_num_V, ray_num_H, detcenter, 
         np.save(path, arr)
         written.append(path)
 
+    (v1, h1), (v2, h2), (vf, hf) = sizes or ((ray_num_V, ray_num_H),) * 3
     src = _host(source)
     save("points_source.npy", src[:, 0] if src.ndim == 2 else src)
     for k, m in enumerate(mirrors):
         pts = _host(m)
-        ds = _host(calc_dS(torch.as_tensor(pts), ray_num_V, ray_num_H))
+        v, h = (v1, h1) if k % 2 == 0 else (v2, h2)
+        ds = _host(calc_dS(torch.as_tensor(pts), v, h))
         save(f"points_M{k + 1}.npy", np.vstack((pts, ds.flatten())))
-    grid, y_grid, z_grid = image_grid(detcenter, ray_num_H, ray_num_V, ysize, zsize)
+    grid, y_grid, z_grid = image_grid(detcenter, hf, vf, ysize, zsize)
     save("points_gridImage.npy", grid)
-    if detcenter2 is not None and abs(defocus_for_wave) > 1e-9:
-        span = 2e-7 + defocus_for_wave * (0.082 if option_HighNA else 0.01) * 2
-        grid2, _, _ = image_grid(detcenter2, ray_num_H, ray_num_V, span, span)
+    if detcenter2 is not None and np.abs(defocus_for_wave) > 1e-9:
+        if option_HighNA:
+            span = 2e-7 + defocus_for_wave * 0.082 * 2
+        else:
+            span = 2e-7 + defocus_for_wave * 0.01 * 2
+        grid2, _, _ = image_grid(detcenter2, hf, vf, span, span)
         save("points_gridDefocus.npy", grid2)
     p = np.zeros(26) if params is None else np.asarray(params)
     path = os.path.join(directory, "calculation_conditions.txt")
@@ -104,12 +110,12 @@ def save_wave_data(directory, source, mirrors, ray_num_V, ray_num_H, detcenter, 
         f.write(f"grid pitch_z: {z_grid[1] - z_grid[0]}\n")
         f.write(f"grid size_y: {np.max(y_grid) - np.min(y_grid)}\n")
         f.write(f"grid size_z: {np.max(z_grid) - np.min(z_grid)}\n")
-        f.write(f"grid pix_y: {ray_num_H}\n")
-        f.write(f"grid pix_z: {ray_num_V}\n")
-        f.write(f"grid pix_H1: {ray_num_H}\n")
-        f.write(f"grid pix_V1: {ray_num_V}\n")
-        f.write(f"grid pix_H2: {ray_num_H}\n")
-        f.write(f"grid pix_V2: {ray_num_V}\n")
+        f.write(f"grid pix_y: {hf}\n")
+        f.write(f"grid pix_z: {vf}\n")
+        f.write(f"grid pix_H1: {h1}\n")
+        f.write(f"grid pix_V1: {v1}\n")
+        f.write(f"grid pix_H2: {h2}\n")
+        f.write(f"grid pix_V2: {v2}\n")
         f.write(f"option_AKB: {option_AKB}\n")
         f.write(f"option_HighNA: {option_HighNA}\n")
         f.write(f"defocusForWave: {defocus_for_wave}\n")
@@ -201,3 +207,120 @@ def run_wave_chain(folder, out_dir=None, files=("points_source.npy", "points_M1.
         g2.forward_propagation(prev)
         store("Image2", g2.u)
     return fields
+
+
+def plot_result_wave(params, ray_num, *, defocus_for_wave=1e-3, option_set=True, source_shift=(0.0, 0.0, 0.0),
+                     as_torch=False):
+    """plot_result_debug(params, 'wave') (AKB_raytrace_20250312.py:2675-2905, :3510-3561) on the
+    device for the AKB system built from params (geometry.build_akb), on a ray_num x ray_num grid:
+    pass 1, the equal-angle resample (host numpy arctan / tan and the C interp1d, as RayWave), pass
+    2 with every mirror's hits, then the 'wave' tilt - theta from np.mean (not nanmean) of the exit
+    slopes' arctan, every mirror grid and the source rotated about np.mean(detcenter, axis=1) -
+    the re-intersected detector and, when |defocus_for_wave| > 1e-9, the defocused one. Returns the
+    reference's tuple: (source, vmirr_hyp, hmirr_hyp, vmirr_ell, hmirr_ell, detcenter[, detcenter2],
+    ray_num_H, ray_num_V, vmirr_norm, hmirr_norm, vmirr2_norm, hmirr2_norm, vec0to1, vec1to2,
+    vec2to3, vec3to4), or np.inf where the reference returns np.inf."""
+    from . import geometry as G
+    from . import primitives as P
+    from .reduce import means_to_host, np_sum
+    from .trace import grid_dirs, staged_chain, trace_chain
+    from .wavefront import AngleRange, resample, sample_plan
+    b = G.build_akb(params, source_shift=source_shift, option_set=option_set)
+    if not isinstance(b, dict):
+        return b
+    n = int(ray_num)
+    dev = D.device()
+    mir = G.mirrors_of(b)
+    rand_h = AngleRange(**b["angle_h"]).table(n)
+    rand_v = AngleRange(**b["angle_v"]).table(n)
+    th = torch.from_numpy(np.tan(rand_h)).to(dev)
+    tv = torch.from_numpy(np.tan(rand_v)).to(dev)
+    hb, he, col = sample_plan(n)
+    r1 = trace_chain(mir, tan_h=th, tan_v=tv, src=b["source"], want=(), samples=(hb, he, col))
+    f1 = int(r1.flags.item())
+    if f1:
+        raise _lib.AKBError(f"pass 1 of the 'wave' trace flagged 0x{f1:x} (a miss or zero norm: the reference's "
+                            "all-NaN rays cannot be resampled)")
+    s = r1.extra["samples"].cpu().numpy()
+    rand_h2, rand_v2 = resample(np.arctan(s[:he - hb]), np.arctan(s[he - hb:]), rand_h, rand_v)
+    th2 = torch.from_numpy(np.tan(rand_h2)).to(dev)
+    tv2 = torch.from_numpy(np.tan(rand_v2)).to(dev)
+    det1 = b["det1"][6:10]
+    r2 = trace_chain(mir, tan_h=th2, tan_v=tv2, src=b["source"], want=("hits", "dir_out", "det"), det_ghij=det1)
+    N = n * n
+    if int(r2.flags.item()):
+        src = torch.tensor(b["source"], dtype=D.F64, device=dev).reshape(3, 1).expand(3, N).contiguous()
+        hits, refl, _ = staged_chain(mir, grid_dirs(th2, tv2), src)
+        hits = torch.stack(hits)
+        det = P.plane_ray_intersection(b["det1"], refl, hits[-1])
+    else:
+        hits, refl, det = r2.hits, r2.dir_out, r2.det
+    # theta from the exit slopes (:3516-3517), numpy on the host as the reference
+    ang = refl.cpu().numpy()
+    theta_y = -np.mean(np.arctan(ang[2, :] / ang[0, :]))
+    theta_z = np.mean(np.arctan(ang[1, :] / ang[0, :]))
+    (focus,) = means_to_host([np_sum(det)])  # np.mean(detcenter, axis=1), numpy's order on the device
+    source0 = torch.zeros((3, 1), dtype=D.F64, device=dev)
+    refl_rot = P.rotate_vectors(refl, -theta_y, -theta_z)
+    rot = [P.rotate_points(hits[k], focus, -theta_y, -theta_z) for k in range(4)]
+    src_rot = P.rotate_points(source0, focus, -theta_y, -theta_z)
+    vmirr_hyp, vmirr_ell, hmirr_ell, hmirr_hyp = rot
+    detcenter = P.plane_ray_intersection(b["det1"], refl_rot, hmirr_hyp)
+    vec0to1 = P.normalize_vector(vmirr_hyp - src_rot)
+    vec1to2 = P.normalize_vector(vmirr_ell - vmirr_hyp)
+    vec2to3 = P.normalize_vector(hmirr_ell - vmirr_ell)
+    vec3to4 = P.normalize_vector(hmirr_hyp - hmirr_ell)
+    vec4to5 = P.normalize_vector(detcenter - hmirr_hyp)
+    norms = [P.normalize_vector((-b_ + a_) / 2) for a_, b_ in
+             ((vec0to1, vec1to2), (vec1to2, vec2to3), (vec2to3, vec3to4), (vec3to4, vec4to5))]
+    out = [src_rot, vmirr_hyp, hmirr_hyp, vmirr_ell, hmirr_ell, detcenter]
+    if np.abs(defocus_for_wave) > 1e-9:
+        c2 = np.zeros(10)
+        c2[6] = 1
+        c2[9] = -(np.float64(b["s2f_middle"]) + np.float64(b["defocus"]) + defocus_for_wave)
+        out.append(P.plane_ray_intersection(c2, refl_rot, hmirr_hyp))
+    out += [n, n] + norms + [vec0to1, vec1to2, vec2to3, vec3to4]
+    if as_torch:
+        return tuple(out)
+    return tuple(x.cpu().numpy() if isinstance(x, torch.Tensor) else x for x in out)
+
+
+def saveWaveData(initial_params, ysize=1e-6, zsize=1e-6, *, ray_num_H=65, ray_num_V=None, directory=None,
+                 defocus_for_wave=1e-3, downsample=(0, 0, 0, 0, 0, 0), option_set=True, option_HighNA=True,
+                 option_2mirror=True, option_avrgsplt=False, timestamp=None):
+    """saveWaveData (AKB_raytrace_20250312.py:13475-13764) for the AKB system, without its final
+    sys.exit(): the 'wave' run (plot_result_wave), downsample_array_3_n of every grid when the grid
+    is odd (:13489-13497, factors (h1, v1, h2, v2, h_f, v_f) = the module's downsample_* flags), the
+    area elements on the device, and the file set into `directory` (default output_<timestamp>,
+    as the reference). Returns the directory. The module flags the reference reads (wave_num_H /
+    wave_num_V, defocusForWave, option_HighNA, option_2mirror, option_avrgsplt, option_set) are
+    keyword arguments here; install() passes the module's live values."""
+    from datetime import datetime
+    ray_num_V = ray_num_H if ray_num_V is None else ray_num_V
+    if ray_num_V != ray_num_H:
+        raise ValueError("the AKB 'wave' grid is square (ray_num = wave_num_H, :1890-1893)")
+    r = plot_result_wave(initial_params, ray_num_H, defocus_for_wave=defocus_for_wave, option_set=option_set)
+    if not isinstance(r, tuple):
+        raise TypeError("cannot unpack non-iterable float object")  # the reference unpacks np.inf
+    two = np.abs(defocus_for_wave) > 1e-9
+    source, vmirr_hyp, hmirr_hyp, vmirr_ell, hmirr_ell, detcenter = r[:6]
+    detcenter2 = r[6] if two else None
+    if ray_num_H % 2 != 1:
+        # the reference only sets the grid sizes inside its odd-grid branch
+        raise NameError("name 'size_v1' is not defined")
+    h1, v1, h2, v2, hf, vf = downsample
+    vmirr_hyp, size_v1, size_h1 = downsample_array_3_n(vmirr_hyp, ray_num_V, ray_num_H, h1, v1)
+    hmirr_hyp, size_v2, size_h2 = downsample_array_3_n(hmirr_hyp, ray_num_V, ray_num_H, h2, v2)
+    detcenter, size_v_f, size_h_f = downsample_array_3_n(detcenter, ray_num_V, ray_num_H, hf, vf)
+    vmirr_ell, _, _ = downsample_array_3_n(vmirr_ell, ray_num_V, ray_num_H, h1, v1)
+    hmirr_ell, _, _ = downsample_array_3_n(hmirr_ell, ray_num_V, ray_num_H, h2, v2)
+    if two:
+        detcenter2, _, _ = downsample_array_3_n(detcenter2, ray_num_V, ray_num_H, hf, vf)
+    timestamp = timestamp or datetime.now().strftime('%Y%m%d_%H%M%S')
+    directory = directory or f"output_{timestamp}"
+    save_wave_data(directory, source, [vmirr_hyp, hmirr_hyp, vmirr_ell, hmirr_ell], ray_num_V, ray_num_H,
+                   detcenter, detcenter2, params=initial_params, ysize=ysize, zsize=zsize,
+                   defocus_for_wave=defocus_for_wave, option_AKB=True, option_HighNA=option_HighNA,
+                   option_2mirror=option_2mirror, option_avrgsplt=option_avrgsplt, timestamp=timestamp,
+                   sizes=((size_v1, size_h1), (size_v2, size_h2), (size_v_f, size_h_f)))
+    return directory

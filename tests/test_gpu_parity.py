@@ -1147,3 +1147,25 @@ def test_psf_fft_example_at_its_own_size(gpu):
         assert np.max(np.abs(got[k] - ref[k])) <= 1e-10, k
     assert np.max(np.abs(got["blocks"] - ref["blocks"])) <= 1e-10 * 256 * 256
     assert abs(got["total"] - ref["total"]) <= 1e-10 * ref["total"]
+
+
+@pytest.mark.parametrize("run", ["plain", "thin"])
+def test_save_wave_data_files_vs_reference(gpu, tmp_path, run):
+    """saveWaveData (:13475-13764) end to end at the best-alignment params on a 33 x 33 grid: the
+    'wave' trace, the downsampling, calc_dS and the file writers give the reference's own files
+    (tests/golden/savewave_33.npz) - every array bit for bit, the conditions text byte for byte
+    (its time line set to the recorded one)."""
+    from akbraytracing_amd import wavedata as W
+    f = golden("savewave_33.npz")
+    text = str(f[f"{run}_conditions"])
+    stamp = [ln for ln in text.splitlines() if ln.startswith("time: ")][0][6:]
+    folder = W.saveWaveData(golden("akb_autofocus.npz")["g0_params"], ray_num_H=33, directory=str(tmp_path / run),
+                            defocus_for_wave=float(f["defocusForWave"]), downsample=tuple(f[f"{run}_downsample"]),
+                            timestamp=stamp)
+    for name in ("points_source", "points_M1", "points_M2", "points_M3", "points_M4", "points_gridImage",
+                 "points_gridDefocus"):
+        got = np.load(os.path.join(folder, name + ".npy"))
+        want = f[f"{run}_{name}"]
+        assert got.shape == want.shape and np.array_equal(got, want), name
+    with open(os.path.join(folder, "calculation_conditions.txt")) as fh:
+        assert fh.read() == text
