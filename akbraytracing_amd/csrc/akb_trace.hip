@@ -404,6 +404,7 @@ struct ChainArgs {
     const double* pert_h;  // (terms, n_h) / (terms, n_v) OPL perturbation tables or NULL
     const double* pert_v;
     int pert_terms;
+    int origin0;  // 1: point source at (+0, +0, +0) and mirror 0 with g != 0, j != 0 (mirror_step kOrigin)
     const double* cp_src;  // staging copy done by workgroup 0 (akb_chain_desc.copy_*)
     double* cp_dst;
     int64_t cp_n;
@@ -495,31 +496,77 @@ struct Ray {
 // expression's bits (an exactly-zero partial sum could only change the sign of a zero).
 // kUnitIn: the incoming direction is a unit vector (grid rays, or any mirror after the first), so
 // the reflected direction's norm skips its range test (norm3_inv_unit).
-template <int kKind, bool kOPL, bool kHits, bool kUnitIn>
+// kOrigin: the ray leaves the point (+0, +0, +0) (the first mirror of a point-source chain whose
+// source is the origin, ChainArgs.origin0): every term of B and C with a factor p, q or r is an
+// exact +-0, and a +-0 partial sum plus a non-zero term is that term exactly, so for g != 0 (and
+// l > 0, always so for grid rays) B = (g l + h m) + i n and for j != 0 C = j - the host checks both
+// conditions. The segment length's x - p is x itself.
+// kFlagsOnly: the last mirror of a pass whose only output is the flag word (the fused pass 1): the
+// miss and zero-normal tests need the hit and the gradient but nothing after them - the reflected
+// direction of a unit ray about a unit normal cannot have a zero norm, so its normalisation (and
+// the normal's) are skipped. The ray R is left as it came in.
+template <int kKind, bool kOPL, bool kHits, bool kUnitIn, bool kOrigin = false, bool kFlagsOnly = false>
 __device__ __forceinline__ void mirror_step(const CMirror& Q, Ray& R, double& opl, int k,
                                             int& fl, double* hits, int64_t hits_ld, int lane) {
     const double l = R.l, m = R.m, n = R.n, p = R.p, q = R.q, r = R.r;
     double A, B, C;
     if (kKind == kKindYFree) {
         A = Q.a * (l * l) + Q.c * (n * n) + Q.e * n * l;
-        B = Q.a2 * p * l + Q.c2 * r * n + Q.e * (p * n + r * l) + Q.g * l + Q.i * n;
-        C = Q.a * (p * p) + Q.c * (r * r) + Q.e * p * r + Q.g * p + Q.i * r + Q.j;
+        if (kOrigin) {
+            B = Q.g * l + Q.i * n;
+            C = Q.j;
+        } else {
+            B = Q.a2 * p * l + Q.c2 * r * n + Q.e * (p * n + r * l) + Q.g * l + Q.i * n;
+            C = Q.a * (p * p) + Q.c * (r * r) + Q.e * p * r + Q.g * p + Q.i * r + Q.j;
+        }
     } else if (kKind == kKindZFree) {
         A = Q.a * (l * l) + Q.b * (m * m) + Q.d * m * l;
-        B = Q.a2 * p * l + Q.b2 * q * m + Q.d * (p * m + q * l) + Q.g * l + Q.h * m;
-        C = Q.a * (p * p) + Q.b * (q * q) + Q.d * p * q + Q.g * p + Q.h * q + Q.j;
+        if (kOrigin) {
+            B = Q.g * l + Q.h * m;
+            C = Q.j;
+        } else {
+            B = Q.a2 * p * l + Q.b2 * q * m + Q.d * (p * m + q * l) + Q.g * l + Q.h * m;
+            C = Q.a * (p * p) + Q.b * (q * q) + Q.d * p * q + Q.g * p + Q.h * q + Q.j;
+        }
     } else {
         A = Q.a * (l * l) + Q.b * (m * m) + Q.c * (n * n) + Q.d * m * l + Q.e * n * l + Q.f * m * n;
-        B = Q.a2 * p * l + Q.b2 * q * m + Q.c2 * r * n + Q.d * (p * m + q * l) + Q.e * (p * n + r * l) +
-            Q.f * (r * m + q * n) + Q.g * l + Q.h * m + Q.i * n;
-        C = Q.a * (p * p) + Q.b * (q * q) + Q.c * (r * r) + Q.d * p * q + Q.e * p * r + Q.f * q * r + Q.g * p +
-            Q.h * q + Q.i * r + Q.j;
+        if (kOrigin) {
+            B = Q.g * l + Q.h * m + Q.i * n;
+            C = Q.j;
+        } else {
+            B = Q.a2 * p * l + Q.b2 * q * m + Q.c2 * r * n + Q.d * (p * m + q * l) + Q.e * (p * n + r * l) +
+                Q.f * (r * m + q * n) + Q.g * l + Q.h * m + Q.i * n;
+            C = Q.a * (p * p) + Q.b * (q * q) + Q.c * (r * r) + Q.d * p * q + Q.e * p * r + Q.f * q * r + Q.g * p +
+                Q.h * q + Q.i * r + Q.j;
+        }
     }
     const double D = B * B - 4.0 * A * C;
     const double sD = sqrt_disc(D, AKB_FLAG_MISS << (4 * k), fl);
     const double t = (-B + sD * Q.sgn) / (2.0 * A);  // (-B - sD) / (2A) for the minus root
     const double x = t * l + p, y = t * m + q, z = t * n + r;
-    if (kOPL) opl = opl + norm3(x - p, y - q, z - r);  // opl starts at +0.0: 0 + d is d exactly
+    if (kOPL) {  // opl starts at +0.0: 0 + d is d exactly
+        if (kOrigin)
+            opl = opl + norm3(x, y, z);
+        else
+            opl = opl + norm3(x - p, y - q, z - r);
+    }
+    if (kFlagsOnly) {
+        double nx, ny = 0.0, nz = 0.0;
+        if (kKind == kKindYFree) {
+            nx = Q.a2 * x + Q.e * z + Q.g;
+            nz = Q.c2 * z + Q.e * x + Q.i;
+        } else if (kKind == kKindZFree) {
+            nx = Q.a2 * x + Q.d * y + Q.g;
+            ny = Q.b2 * y + Q.d * x + Q.h;
+        } else {
+            nx = Q.a2 * x + Q.d * y + Q.e * z + Q.g;
+            ny = Q.b2 * y + Q.d * x + Q.f * z + Q.h;
+            nz = Q.c2 * z + Q.e * x + Q.f * y + Q.i;
+        }
+        // np.linalg.norm == 0 exactly when the sum of squares is 0
+        wave_flag(nx * nx + ny * ny + nz * nz == 0.0, AKB_FLAG_ZERO_NORMAL << (4 * k), fl);
+        return;
+    }
     // hits: this segment's column 0 of mirror 0's x row (wave-uniform). A compile-time switch: a
     // vector store anywhere in the mirror loop makes the compiler drain every outstanding load
     // before the loop (no separate store counter on gfx9), which would stall the fused kernel's
@@ -612,7 +659,7 @@ __device__ __forceinline__ void ray_tables(const ChainArgs& a, int64_t i, uint32
 // (vmcnt), so loads issued after this segment's stores would make the next segment's first use
 // wait for those stores to reach memory; issued before them, they fly during the stores, the leaf
 // sums and (for the fused kernels) the next segment's mirror loop.
-// kLean: pass 1 of the fused kernel - only the resample picks and the flags leave the ray (no
+// kLean: pass 1 of the fused kernel - only the flags leave the ray (the last mirror flags-only; no
 // optional output rows, no out-of-line atan call).
 // kPointSrc: rays start at the constant source (no origin loads, which would have to be waited
 // for - with everything issued before them - ahead of the mirror loop).
@@ -649,17 +696,49 @@ __device__ __forceinline__ void chain_ray_tab(const ChainArgs& a, int64_t i0, in
         R.r = a.src[2];
     }
     double opl = 0.0;
+    // the first mirror from the origin (a point source at +0, ChainArgs.origin0) and the last
+    // mirror of a flags-only pass take their reduced forms (mirror_step's kOrigin / kFlagsOnly)
+    int k0 = 0;
+    const int kend = kLean ? a.K - 1 : a.K;
+    if (kGrid && a.origin0) {  // wave-uniform (grid rays: l > 0)
+        if (kLean && a.K == 1) {
+            if (a.kind[0] == kKindYFree)
+                mirror_step<kKindYFree, kOPL, kHits, kGrid, true, true>(a.q[0], R, opl, 0, fl, hits, a.hits_ld, t);
+            else if (a.kind[0] == kKindZFree)
+                mirror_step<kKindZFree, kOPL, kHits, kGrid, true, true>(a.q[0], R, opl, 0, fl, hits, a.hits_ld, t);
+            else
+                mirror_step<kKindGeneral, kOPL, kHits, kGrid, true, true>(a.q[0], R, opl, 0, fl, hits, a.hits_ld, t);
+            k0 = 1;
+        } else {
+            if (a.kind[0] == kKindYFree)
+                mirror_step<kKindYFree, kOPL, kHits, kGrid, true>(a.q[0], R, opl, 0, fl, hits, a.hits_ld, t);
+            else if (a.kind[0] == kKindZFree)
+                mirror_step<kKindZFree, kOPL, kHits, kGrid, true>(a.q[0], R, opl, 0, fl, hits, a.hits_ld, t);
+            else
+                mirror_step<kKindGeneral, kOPL, kHits, kGrid, true>(a.q[0], R, opl, 0, fl, hits, a.hits_ld, t);
+            k0 = 1;
+        }
+    }
     // not unrolled: each iteration reads its mirror's coefficients from the kernel argument segment
     // with scalar loads (wave-uniform), keeping VGPR pressure and code size low (a fully unrolled
     // 4-mirror AKB kernel measured 12 % slower on MI355X)
 #pragma unroll 1
-    for (int k = 0; k < a.K; ++k) {
+    for (int k = k0; k < kend; ++k) {
         if (a.kind[k] == kKindYFree)  // wave-uniform branch
             mirror_step<kKindYFree, kOPL, kHits, kGrid>(a.q[k], R, opl, k, fl, hits, a.hits_ld, t);
         else if (a.kind[k] == kKindZFree)
             mirror_step<kKindZFree, kOPL, kHits, kGrid>(a.q[k], R, opl, k, fl, hits, a.hits_ld, t);
         else
             mirror_step<kKindGeneral, kOPL, kHits, kGrid>(a.q[k], R, opl, k, fl, hits, a.hits_ld, t);
+    }
+    if (kLean && kend >= k0) {  // the last mirror: its flags only
+        const int k = kend;
+        if (a.kind[k] == kKindYFree)
+            mirror_step<kKindYFree, kOPL, kHits, kGrid, false, true>(a.q[k], R, opl, k, fl, hits, a.hits_ld, t);
+        else if (a.kind[k] == kKindZFree)
+            mirror_step<kKindZFree, kOPL, kHits, kGrid, false, true>(a.q[k], R, opl, k, fl, hits, a.hits_ld, t);
+        else
+            mirror_step<kKindGeneral, kOPL, kHits, kGrid, false, true>(a.q[k], R, opl, k, fl, hits, a.hits_ld, t);
     }
     const double l = R.l, m = R.m, nn = R.n, p = R.p, q = R.q, r = R.r;
     if (kOPL && kGrid && a.pert_h) {  // figure-error perturbation of the path (BASELINE config 5)
@@ -1432,6 +1511,11 @@ static int chain_args_from(const akb_chain_desc* d, ChainArgs& a, bool& empty) {
     a.org_ld = d->org_ld;
     a.org_inc = d->org_inc;
     for (int k = 0; k < 3; ++k) a.src[k] = d->src[k];
+    // mirror_step's kOrigin conditions: the rays leave (+0, +0, +0), g of mirror 0 is far from
+    // underflow against l (l > 0 for grid rays) and j of mirror 0 is non-zero
+    a.origin0 = d->org == nullptr && d->n_mirrors > 0 && d->src[0] == 0.0 && d->src[1] == 0.0 && d->src[2] == 0.0 &&
+                !std::signbit(d->src[0]) && !std::signbit(d->src[1]) && !std::signbit(d->src[2]) &&
+                std::fabs(d->coeffs[0][6]) >= 0x1p-800 && std::isfinite(d->coeffs[0][6]) && d->coeffs[0][9] != 0.0;
     a.hits = d->hits;
     a.hits_ld = d->hits_ld;
     a.last_hit = d->last_hit;
@@ -1768,8 +1852,9 @@ static int chain_tilt(const akb_chain_desc* d, const double* d_params, const dou
     AKB_REQUIRE(d->org == nullptr, "the fused pass 1 traces from a point source");
     AKB_REQUIRE(det2 && total2 && !det1 && !total1 && !dir_rot && !pt_rot,
                 "the fused tilt writes the detector-2 rows only (detector 1 / rotated rays: unfused)");
-    AKB_REQUIRE(!d->last_hit && !d->dir_out && !d->det_out && !d->atan_h && !d->atan_v && !d->hits,
-                "the fused pass 1 writes only the resample picks and the flags");
+    AKB_REQUIRE(!d->last_hit && !d->dir_out && !d->det_out && !d->atan_h && !d->atan_v && !d->hits && !d->samp_h &&
+                    !d->samp_v,
+                "the fused pass 1 writes only the flags (its picks come from akb_trace_chain_samples_f64)");
     AKB_REQUIRE(sink->nq > 0, "the tilt needs its sink");
     TiltArgs b{};
     b.params = d_params;

@@ -312,12 +312,15 @@ def main():
 
     for _ in range(args.warmup):
         step(False)
-    rw.kernel_events = []
+    rw.kernel_events = [] if not os.environ.get("AKB_BENCH_NO_KEVENTS") else None
     comm.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    host_ms = []  # host time spent issuing each step (its waits included): is the host the limit?
     for _ in range(args.steps):
+        h0 = time.perf_counter()
         step(True)
+        host_ms.append((time.perf_counter() - h0) * 1e3)
     torch.cuda.synchronize()
     comm.barrier()
     el = time.perf_counter() - t0
@@ -357,7 +360,7 @@ def main():
 
     if rank != 0:
         return
-    k_ms = [a.elapsed_time(b) for a, b in rw.kernel_events]
+    k_ms = [a.elapsed_time(b) for a, b in rw.kernel_events] if rw.kernel_events else [float('nan')]
     k_avg = sum(k_ms) / len(k_ms)
     psf_ms = sum(a.elapsed_time(b) for a, b in psf_events) / max(len(psf_events), 1)
     launch_bytes = PASS2_BYTES_PER_RAY * rw.n_local
@@ -397,6 +400,7 @@ def main():
                    "DFT (pruned)",
             "parallelism": f"ray-row shards x{world}",
         },
+        "host_issue_ms_per_step": sorted(host_ms)[len(host_ms) // 2],
         "psf_ms": psf_ms,
         "psf_alone_ms": psf_alone_ms,
         # the PSF's compulsory HBM traffic is its output (the pupil is 128 KB): intensity planes
@@ -446,8 +450,9 @@ def main():
     if single_ms is not None:
         out["single_run_ms"] = single_ms
     if world > 1:
-        out["note_multi_gpu"] = ("cross-rank means are sums of per-rank numpy-order partial sums: Wave2 agrees "
-                                 "with one process within 1e-4 nm (tests/test_dist_gpu.py), not bit for bit")
+        out["note_multi_gpu"] = ("shards are aligned to numpy's 8192-element sum buffers and the ranks' buffer sums "
+                                 "are chained in numpy's order: N ranks give one process's bits "
+                                 "(tests/test_c4_gpu.py, tests/test_dist_gpu.py)")
     if world == 1 and last_out is not None:
         out["huygens_pairs_per_s"] = huygens_rate(last_out)
         out["faithful_psf_chain_ms"] = faithful_psf_chain(rw, last_out, args.pupil)

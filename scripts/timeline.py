@@ -10,7 +10,8 @@ big = lambda r: int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) > 50_000
 idx = [i for i, r in enumerate(rows)
        if "k_chain_tilt" in r["Kernel_Name"]
        or ("k_chain<true, false" in r["Kernel_Name"] and "sink" not in r["Kernel_Name"] and big(r))]
-i0, i1 = idx[-3], idx[-2]
+k = int(sys.argv[2]) if len(sys.argv) > 2 else len(idx) // 2
+i0, i1 = idx[k], idx[k + 1]
 t0 = int(rows[i0]["Start_Timestamp"])
 prev = None
 for r in rows[i0:i1 + 1]:

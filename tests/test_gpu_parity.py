@@ -1169,3 +1169,69 @@ def test_save_wave_data_files_vs_reference(gpu, tmp_path, run):
         assert got.shape == want.shape and np.array_equal(got, want), name
     with open(os.path.join(folder, "calculation_conditions.txt")) as fh:
         assert fh.read() == text
+
+
+def _subset_dirs(tan_h, tan_v, idx):
+    """the reference's phai0 columns idx (flat iv * n_h + ih) without the full grid"""
+    n_h = tan_h.shape[0]
+    phai0 = np.zeros((3, idx.shape[0]))
+    phai0[0] = 1.0
+    phai0[1] = tan_h[idx % n_h]
+    phai0[2] = tan_v[idx // n_h]
+    return O.normalize_vector(phai0)
+
+
+@pytest.mark.slow
+def test_kb_wave_3163_rows_vs_oracle(gpu):
+    """BASELINE config 2's trace (KB, 3163^2 = 1e7 rays, two passes): no flags, and pass 2's last
+    hit, exit direction and detector hit bit-exact to the oracle on the resample picks' rays and on
+    20 000 rays sampled over the whole grid (the oracle's pass 1 traced on the picks only)."""
+    from akbraytracing_amd.wavefront import RayWave, SystemGeometry
+    gd = golden_json("kb_geometry.json")
+    n = 3163
+    out = RayWave(SystemGeometry.from_dict(gd), n).run(opd=False, full=True)
+    assert out["flags"] == (0, 0)
+    rand_h, rand_v, tan_h, tan_v = OPL.angle_tables(gd, n)
+    col, v_idx, start, end, h_idx = OPL.sample_indices(n, n)
+    picks = np.concatenate([h_idx, v_idx])
+    _, r1, _ = OPL.chain(gd["mirrors"], _subset_dirs(tan_h, tan_v, picks), np.zeros((3, picks.shape[0])))
+    nh = h_idx.shape[0]
+    ah = np.arctan(r1[1, :nh] / r1[0, :nh])
+    av = np.arctan(r1[2, nh:] / r1[0, nh:])
+    new_h, new_v = OPL.resample_from_angles(ah, av, rand_h, rand_v)
+    th2, tv2 = np.tan(new_h), np.array([np.tan(x) for x in new_v])
+    rng = np.random.default_rng(11)
+    idx = np.unique(np.concatenate([picks, rng.integers(0, n * n, 20000)]))
+    hits, r2, _ = OPL.chain(gd["mirrors"], _subset_dirs(th2, tv2, idx), np.zeros((3, idx.shape[0])))
+    det = np.zeros(10)
+    det[6:10] = gd["det1"][6:10]
+    d2 = O.plane_ray_intersection(det, r2, hits[-1])
+    sel = torch.from_numpy(idx).to(gpu)
+    assert np.array_equal(out["last_hit"][:, sel].cpu().numpy(), hits[-1])
+    assert np.array_equal(out["dir_out"][:, sel].cpu().numpy(), r2)
+    assert np.array_equal(out["det_pre"][:, sel].cpu().numpy(), d2)
+
+
+@pytest.mark.slow
+def test_huygens_c2_stage_1e7_sources(gpu):
+    """BASELINE config 2's Huygens stage shape: the 1e7 last-mirror points of the KB 3163^2 run as
+    sources (synthetic dS and field) -> the 65 x 65 image grid (4225 targets): the device sum
+    against the oracle's C restatement on 64 sampled targets, <= 1e-9 of max |u| (the oracle walks
+    all 1e7 sources for each, so only a sample)."""
+    from akbraytracing_amd import wavecalc as W
+    from akbraytracing_amd.wavefront import RayWave, SystemGeometry
+    out = RayWave(SystemGeometry.from_dict(golden_json("kb_geometry.json")), 3163).run(opd=False, full=True)
+    pts = out["last_hit"].cpu().numpy()
+    det = out["det_pre"].cpu().numpy()
+    M = pts.shape[1]
+    rng = np.random.default_rng(21)
+    ds = 1e-12 * (1.0 + 0.1 * rng.random(M))
+    u = np.exp(1j * 2 * np.pi * rng.random(M))
+    foc = np.nanmean(det, axis=1)
+    gy, gz = np.meshgrid(np.linspace(-2e-7, 2e-7, 65), np.linspace(-2e-7, 2e-7, 65))
+    tx, ty, tz = np.full(4225, foc[0]), foc[1] + gy.ravel(), foc[2] + gz.ravel()
+    k = 2 * np.pi / 13.5e-9
+    got = W.forward_propagation_numpy_batch(tx, ty, tz, pts[0], pts[1], pts[2], u, k, ds)
+    pick = rng.choice(4225, 64, replace=False)
+    ref = O.huygens_c(tx[pick], ty[pick], tz[pick], pts[0], pts[1], pts[2], u * ds, k)
+    assert np.max(np.abs(got[pick] - ref)) <= 1e-9 * np.max(np.abs(ref))
