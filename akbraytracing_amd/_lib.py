@@ -19,7 +19,7 @@ c_int = ctypes.c_int
 c_dbl = ctypes.c_double
 c_vp = ctypes.c_void_p
 MAX_MIRRORS = 7
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 FLAG_MISS = 0x1
 FLAG_ZERO_NORMAL = 0x2
@@ -45,6 +45,7 @@ EXPORTS = [
     "akb_moments_work_bytes", "akb_map_moments_f64", "akb_plane_subtract_f64", "akb_legendre_rows_f64",
     "akb_gd_cells_f64", "akb_gd_pockets", "akb_gd_check_pockets", "akb_gd_grad_sweep_f64", "akb_gd_eval_f64",
     "akb_trace_chain_batch_f64", "akb_focus_eval_work_bytes", "akb_focus_eval_f64",
+    "akb_finish_params_work_bytes", "akb_finish_tilt_params_f64",
 ]
 
 
@@ -108,6 +109,8 @@ def _declare(L):
         "akb_tilt_opd_f64": ([c_vp] * 5 + [c_vp, c_vp, c_vp, c_i64, c_i64] + [c_vp] * 6
                              + [ctypes.POINTER(LeafSink), c_vp], c_int),
         "akb_tilt_params_f64": ([c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp], c_int),
+        "akb_finish_params_work_bytes": ([ctypes.POINTER(LeafSink)], c_i64),
+        "akb_finish_tilt_params_f64": ([ctypes.POINTER(LeafSink)] + [c_vp] * 5 + [c_int] + [c_vp] * 2, c_int),
         "akb_tilt_opd_dev_f64": ([c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64] + [c_vp] * 6
                                  + [ctypes.POINTER(LeafSink), c_vp], c_int),
         "akb_trace_chain_samples_f64": ([ctypes.POINTER(ChainDesc), c_vp], c_int),

@@ -38,22 +38,30 @@ __device__ __forceinline__ double nan_zero(double v, bool nan0, long long& cnt) 
 }
 
 // numpy pairwise leaf (n <= 128) over staged values (NaN already replaced)
+// kNan0: read NaN as 0 (np.nansum's values) - the caller counts the non-NaN elements
+template <bool kNan0 = false>
+__device__ __forceinline__ double pw_val(const double* a, int i) {
+    const double x = a[i];
+    return (kNan0 && x != x) ? 0.0 : x;
+}
+
+template <bool kNan0 = false>
 static __device__ double pw_leaf_lds(const double* a, int n) {
     if (n < 8) {
         double res = 0.0;
-        for (int i = 0; i < n; ++i) res = res + a[i];
+        for (int i = 0; i < n; ++i) res = res + pw_val<kNan0>(a, i);
         return res;
     }
     double r[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) r[j] = a[j];
+    for (int j = 0; j < 8; ++j) r[j] = pw_val<kNan0>(a, j);
     int i = 8;
     for (; i < n - (n % 8); i += 8) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) r[j] = r[j] + a[i + j];
+        for (int j = 0; j < 8; ++j) r[j] = r[j] + pw_val<kNan0>(a, i + j);
     }
     double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-    for (; i < n; ++i) res = res + a[i];
+    for (; i < n; ++i) res = res + pw_val<kNan0>(a, i);
     return res;
 }
 
@@ -68,6 +76,7 @@ struct PwTree {
 // one level per step (a node of more than 128 elements splits at pw_split(n) into left and right
 // children, placed in order by a ballot prefix count), each leaf is summed by one lane, and the
 // levels are combined bottom-up as left + right.
+template <bool kNan0 = false>
 static __device__ double pw_tree_wave(PwTree& T, const double* a, int len) {
     const int lane = threadIdx.x & 63;
     if (lane == 0) {
@@ -100,7 +109,7 @@ static __device__ double pw_tree_wave(PwTree& T, const double* a, int len) {
                 }
                 T.child[d][lane] = pos;
             } else if (act) {
-                T.val[d][lane] = pw_leaf_lds(a + o, l);
+                T.val[d][lane] = pw_leaf_lds<kNan0>(a + o, l);
             }
             if (m && d + 1 < kTreeLevels) {
                 nd[d + 1] = 2 * __popcll(m);

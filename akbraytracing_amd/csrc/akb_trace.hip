@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "akb_common.h"
+#include "akb_pairwise.h"
 #include "akb_sincos.h"
 
 namespace akb {
@@ -857,9 +858,18 @@ __global__ void __launch_bounds__(kBlock) k_chain_batch(const ChainArgs* __restr
 // were already copied out in stream order).
 constexpr int kTiltTheta = 0, kTiltRy = 2, kTiltRz = 11, kTiltFocus = 20, kTiltSaved = 23;
 
+// the parameter block from the five sums / counts, by one 64-lane wave (the whole of k_tilt_params,
+// and the last step of k_finish_params)
+__device__ __forceinline__ void tilt_params_wave(const double* s5, const int64_t* c5, double* P,
+                                                 unsigned long long* keys, int32_t* clear, int nclear, int lane);
+
 __global__ void k_tilt_params(const double* __restrict__ s5, const int64_t* __restrict__ c5, double* __restrict__ P,
                               unsigned long long* keys, int32_t* clear, int nclear) {
-    const int lane = threadIdx.x;
+    tilt_params_wave(s5, c5, P, keys, clear, nclear, threadIdx.x);
+}
+
+__device__ __forceinline__ void tilt_params_wave(const double* s5, const int64_t* c5, double* P,
+                                                 unsigned long long* keys, int32_t* clear, int nclear, int lane) {
     // np.nanmean / np.mean: sum / count, an IEEE division (0 / 0 -> NaN as numpy's)
     const double mh = s5[0] / (double)c5[0];
     const double mv = s5[1] / (double)c5[1];
@@ -884,7 +894,141 @@ __global__ void k_tilt_params(const double* __restrict__ s5, const int64_t* __re
     // read them from there whenever it likes (RayWave's trace flag words)
     if (lane < 4) ((int32_t*)(P + kTiltSaved))[lane] = lane < nclear ? clear[lane] : 0;
     __syncthreads();
-    for (int i = lane; i < nclear; i += blockDim.x) clear[i] = 0;
+    for (int i = lane; i < nclear; i += 64) clear[i] = 0;
+}
+
+// The pass-2 sink's finish and the tilt parameters in two launches instead of three
+// (akb_leaf_finish_f64's k_leaf_chunks + k_pw_final, then k_tilt_params): on the critical path of a
+// ray_wave run every kernel boundary costs ~10 us.
+// k_fin_buffers (256 threads): block (b, q) forms the sums of buffers b*kFinBPB .. +kFinBPB-1 of
+// quantity q from their 64 leaf sums each (numpy's tree over a buffer's leaves; a wave per buffer
+// group, all loads in flight together); the last block of each quantity instead stages the short
+// last buffer in LDS (NaN -> 0 for the nanmean rows) and forms its pairwise sum and count.
+// k_fin_params (one workgroup, wave q for quantity q): the buffer sums staged in LDS and added left
+// to right, the short buffer last - numpy's order - then wave 0 forms the parameter block. No
+// cross-workgroup hand-off inside a kernel, so no device-scope fences.
+constexpr int kFinBPB = 32;      // buffers per k_fin_buffers block (8 per wave)
+constexpr int kFinTile = 2048;   // buffer sums staged per LDS round and wave
+
+__global__ void __launch_bounds__(256) k_fin_buffers(akb_leaf_sink S, int64_t nfull, double* __restrict__ part,
+                                                     long long* __restrict__ part_cnt) {
+    extern __shared__ double tl[];  // the short buffer (its length in doubles)
+    __shared__ PwTree T;
+    const int q = blockIdx.y;
+    const int64_t blk = blockIdx.x;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t nb = (nfull + kFinBPB - 1) / kFinBPB;
+    double* const tsum = part + (int64_t)S.nq * nfull;
+    long long* const tcnt = part_cnt + (int64_t)S.nq * nfull;
+    if (blk < nb) {
+        constexpr int kPer = kFinBPB / 4;
+        const int64_t nleaves = nfull * (kNpBuf / 128);
+        double v[kPer];
+        int k[kPer];
+#pragma unroll
+        for (int b = 0; b < kPer; ++b) {
+            const int64_t c = blk * kFinBPB + w * kPer + b;
+            const int64_t li = (int64_t)q * nleaves + c * 64 + lane;
+            v[b] = c < nfull ? S.leaf_sum[li] : 0.0;
+            k[b] = c < nfull ? S.leaf_cnt[li] : 0;
+        }
+#pragma unroll
+        for (int b = 0; b < kPer; ++b) {
+            double x = v[b];
+            x = x + __shfl_xor(x, 1);
+            x = x + __shfl_xor(x, 2);
+            x = x + __shfl_xor(x, 4);
+            x = x + __shfl_xor(x, 8);
+            x = x + __shfl_xor(x, 16);
+            x = x + __shfl_xor(x, 32);
+            long long kk = k[b];
+            for (int off = 32; off > 0; off >>= 1) kk += __shfl_down(kk, off);
+            const int64_t c = blk * kFinBPB + w * kPer + b;
+            if (lane == 0 && c < nfull) {
+                part[(int64_t)q * nfull + c] = x;
+                part_cnt[(int64_t)q * nfull + c] = kk;
+            }
+        }
+        return;
+    }
+    // the short last buffer
+    const int tail = (int)(S.n - nfull * kNpBuf);
+    const bool nan0 = (S.nan_mask >> (q < 31 ? q : 31)) & 1;
+    const double* a = S.tail + (int64_t)q * kNpBuf;
+    long long cnt = 0;
+    for (int i = threadIdx.x; i < tail; i += 256) tl[i] = nan_zero(a[i], nan0, cnt);
+    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_down(cnt, off);
+    __shared__ long long wc[4];
+    if (lane == 0) wc[w] = cnt;
+    __syncthreads();
+    if (w == 0) {
+        const double v = tail > 0 ? pw_tree_wave(T, tl, tail) : 0.0;
+        if (lane == 0) {
+            tsum[q] = v;
+            tcnt[q] = wc[0] + wc[1] + wc[2] + wc[3];
+        }
+    }
+}
+
+__global__ void __launch_bounds__(320) k_fin_params(akb_leaf_sink S, int64_t nfull, const double* __restrict__ part,
+                                                    const long long* __restrict__ part_cnt, double* __restrict__ sum5,
+                                                    int64_t* __restrict__ cnt5, double* __restrict__ P,
+                                                    unsigned long long* keys, int32_t* clear, int nclear) {
+    __shared__ double tile[5][kFinTile];
+    __shared__ double s5[8];
+    __shared__ int64_t c5[8];
+    const int q = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int tail = (int)(S.n - nfull * kNpBuf);
+    long long cnt = 0;
+    double acc = 0.0;
+    const double* pq = part + (int64_t)q * nfull;
+    const long long* cq = part_cnt + (int64_t)q * nfull;
+    for (int64_t base = 0; base < nfull; base += kFinTile) {
+        const int m = (int)(nfull - base < kFinTile ? nfull - base : kFinTile);
+        constexpr int kB = kFinTile / 64;
+        double vb[kB];
+#pragma unroll
+        for (int r = 0; r < kB; ++r) {
+            const int i = lane + 64 * r;
+            vb[r] = i < m ? pq[base + i] : 0.0;
+            cnt += i < m ? cq[base + i] : 0;
+        }
+#pragma unroll
+        for (int r = 0; r < kB; ++r) {
+            const int i = lane + 64 * r;
+            if (i < m) tile[q][i] = vb[r];
+        }
+        wave_sync();
+        if (lane == 0) {  // 16 LDS reads in flight ahead of 16 dependent adds
+            int i = 0;
+            if (base == 0) {
+                acc = tile[q][0];
+                i = 1;
+            }
+            double u[16];
+            for (; i + 16 <= m; i += 16) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) u[r] = tile[q][i + r];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc = acc + u[r];
+            }
+            for (; i < m; ++i) acc = acc + tile[q][i];
+        }
+        wave_sync();
+    }
+    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_down(cnt, off);
+    if (lane == 0) {
+        const double* tsum = part + (int64_t)S.nq * nfull;
+        const long long* tcnt = part_cnt + (int64_t)S.nq * nfull;
+        const double sv = tail > 0 ? (nfull > 0 ? acc + tsum[q] : tsum[q]) : acc;
+        const long long cv = cnt + (tail > 0 ? tcnt[q] : 0);
+        s5[q] = sv;
+        c5[q] = cv;
+        sum5[q] = sv;
+        cnt5[q] = cv;
+    }
+    __syncthreads();
+    if (q == 0) tilt_params_wave(s5, c5, P, keys, clear, nclear, lane);
 }
 
 __device__ __forceinline__ void tilt_ray(const TiltArgs& a, int64_t i, const TiltIn& t, double (&qv)[5]) {
@@ -1742,6 +1886,36 @@ int akb_tilt_params_f64(const double* d_sum5, const int64_t* d_cnt5, double* d_p
     k_tilt_params<<<1, 64, 0, (hipStream_t)stream>>>(d_sum5, d_cnt5, d_params, (unsigned long long*)d_extent_keys,
                                                       d_clear, n_clear);
     return launch_status("k_tilt_params");
+}
+
+int64_t akb_finish_params_work_bytes(const akb_leaf_sink* sink) {
+    if (!sink || sink->nq <= 0 || sink->n < 0) return 0;
+    const int64_t nfull = sink->n / kNpBuf;
+    return (int64_t)sink->nq * (nfull + 1) * 16 + 64;
+}
+
+int akb_finish_tilt_params_f64(const akb_leaf_sink* sink, double* d_sum5, int64_t* d_cnt5, double* d_params,
+                               uint64_t* d_extent_keys, int32_t* d_clear, int n_clear, void* work, void* stream) {
+    clear_error();
+    AKB_REQUIRE(sink && d_sum5 && d_cnt5 && d_params && work, "null pointer");
+    AKB_REQUIRE(sink->nq == 5 && sink->n > 0, "the tilt's pass-2 sink: five quantities over n > 0 rays");
+    AKB_REQUIRE(n_clear >= 0 && (n_clear == 0 || d_clear), "bad clear list");
+    const int64_t nfull = sink->n / kNpBuf;
+    AKB_REQUIRE(nfull < (1LL << 31), "too many buffers");
+    double* part = (double*)work;
+    long long* part_cnt = (long long*)(part + (int64_t)sink->nq * (nfull + 1));
+    hipStream_t s = (hipStream_t)stream;
+    const int tail = (int)(sink->n - nfull * kNpBuf);
+    const int64_t nb = (nfull + kFinBPB - 1) / kFinBPB + (tail > 0 ? 1 : 0);
+    if (nb > 0) {
+        k_fin_buffers<<<dim3((unsigned)nb, (unsigned)sink->nq), 256, (size_t)(tail > 0 ? tail : 1) * 8, s>>>(
+            *sink, nfull, part, part_cnt);
+        int st = launch_status("k_fin_buffers");
+        if (st) return st;
+    }
+    k_fin_params<<<1, 320, 0, s>>>(*sink, nfull, part, part_cnt, d_sum5, d_cnt5, d_params,
+                                   (unsigned long long*)d_extent_keys, d_clear, n_clear);
+    return launch_status("k_fin_params");
 }
 
 int akb_tilt_opd_dev_f64(const double* d_params, const double det1_ghij[4], const double det2_ghij[4],

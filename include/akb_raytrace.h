@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define AKB_ABI_VERSION 8
+#define AKB_ABI_VERSION 9
 
 /* status codes */
 #define AKB_OK 0
@@ -216,6 +216,14 @@ int akb_tilt_opd_f64(const double ry[9], const double rz[9], const double center
  * back from [23..24]) for the next step. d_params holds 25 doubles. */
 int akb_tilt_params_f64(const double* d_sum5, const int64_t* d_cnt5, double* d_params, uint64_t* d_extent_keys,
                         int32_t* d_clear, int n_clear, void* stream);
+
+/* akb_leaf_finish_f64 + akb_tilt_params_f64 for the pass-2 sink in two small launches instead of
+ * three (nq = 5: arctan(Ry/Rx), arctan(Rz/Rx), det x, y, z; one process, sums over the whole sink):
+ * d_sum5 / d_cnt5 and the parameter block exactly as the two calls give them.
+ * work: akb_finish_params_work_bytes(sink). */
+int64_t akb_finish_params_work_bytes(const akb_leaf_sink* sink);
+int akb_finish_tilt_params_f64(const akb_leaf_sink* sink, double* d_sum5, int64_t* d_cnt5, double* d_params,
+                               uint64_t* d_extent_keys, int32_t* d_clear, int n_clear, void* work, void* stream);
 
 /* akb_tilt_opd_f64 with R_y, R_z and the centre read from akb_tilt_params_f64's device block. */
 int akb_tilt_opd_dev_f64(const double* d_params, const double det1_ghij[4], const double det2_ghij[4],

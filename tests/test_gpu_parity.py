@@ -1235,3 +1235,55 @@ def test_huygens_c2_stage_1e7_sources(gpu):
     pick = rng.choice(4225, 64, replace=False)
     ref = O.huygens_c(tx[pick], ty[pick], tz[pick], pts[0], pts[1], pts[2], u * ds, k)
     assert np.max(np.abs(got[pick] - ref)) <= 1e-9 * np.max(np.abs(ref))
+
+
+@pytest.mark.parametrize("n", [77, 8192, 3 * 8192 + 5, 2100 * 8192 + 2137])
+def test_finish_tilt_params_fused_equals_two_calls(gpu, n):
+    """akb_finish_tilt_params_f64 (one launch) = akb_leaf_finish_f64 + akb_tilt_params_f64: the
+    five sums / counts and the whole parameter block bit for bit, NaNs in the nanmean rows (full
+    buffers and the short one), a grid with more buffers than one LDS tile, two calls in a row."""
+    from akbraytracing_amd import _lib, device as D
+    from akbraytracing_amd.reduce import LeafSink
+    L = _lib.lib()
+    rng = np.random.default_rng(n)
+    sink = LeafSink(5, n, 0b00011, gpu)
+    nfull = n // 8192
+    nleaves = nfull * 64
+    tail = n - nfull * 8192
+    for rep in range(2):
+        ls = torch.from_numpy(rng.standard_normal(5 * max(nleaves, 1))[:5 * nleaves] * 1e-3).to(gpu)
+        lc = torch.from_numpy(rng.integers(120, 129, 5 * nleaves).astype(np.int32)).to(gpu)
+        tl = rng.standard_normal((5, 8192)) * 1e-3
+        tl[2:] += 146.0
+        if tail:
+            tl[0, rng.integers(0, tail, 3)] = np.nan
+        sink.buf.zero_()
+        base = sink.buf.data_ptr()
+        if nleaves:
+            ptr_s = sink.desc.leaf_sum - base
+            ptr_c = sink.desc.leaf_cnt - base
+            sink.buf[ptr_s:ptr_s + 8 * 5 * nleaves].view(torch.float64).copy_(ls)
+            sink.buf[ptr_c:ptr_c + 4 * 5 * nleaves].view(torch.int32).copy_(lc)
+        pt = sink.desc.tail - base
+        sink.buf[pt:pt + 8 * 5 * 8192].view(torch.float64).copy_(torch.from_numpy(tl.ravel()).to(gpu))
+        # reference: the two calls
+        s_ref, c_ref = (x.clone() for x in sink.finish())
+        p_ref = torch.empty(25, dtype=torch.float64, device=gpu)
+        keys = torch.full((4,), 7, dtype=torch.int64, device=gpu)
+        fl = torch.tensor([rep + 3, 9], dtype=torch.int32, device=gpu)
+        _lib.check(L.akb_tilt_params_f64(D.ptr(s_ref), D.ptr(c_ref), D.ptr(p_ref), D.ptr(keys), D.ptr(fl), 2,
+                                         D.stream_handle()))
+        # fused
+        work = torch.empty(int(L.akb_finish_params_work_bytes(sink.desc)) // 8 + 1, dtype=torch.float64, device=gpu)
+        s = torch.empty(5, dtype=torch.float64, device=gpu)
+        c = torch.empty(5, dtype=torch.int64, device=gpu)
+        p = torch.empty(25, dtype=torch.float64, device=gpu)
+        keys2 = torch.full((4,), 7, dtype=torch.int64, device=gpu)
+        fl2 = torch.tensor([rep + 3, 9], dtype=torch.int32, device=gpu)
+        for _ in range(2):
+            fl2.copy_(torch.tensor([rep + 3, 9], dtype=torch.int32))
+            _lib.check(L.akb_finish_tilt_params_f64(sink.desc, D.ptr(s), D.ptr(c), D.ptr(p), D.ptr(keys2),
+                                                    D.ptr(fl2), 2, D.ptr(work), D.stream_handle()))
+            assert torch.equal(s, s_ref) and torch.equal(c, c_ref)
+            assert torch.equal(p.view(torch.int64), p_ref.view(torch.int64))
+        assert keys2.cpu().tolist() == [0, 0, 0, 0] and fl2.cpu().tolist() == [0, 0]
