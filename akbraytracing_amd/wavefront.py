@@ -18,6 +18,7 @@ only exchanges are the 2n resample samples, a handful of means and the flag word
 """
 import json
 import dataclasses
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -232,7 +233,7 @@ class RayWave:
     by design, see resample_axis); pass 2, the tilt parameters, the tilt and the OPD are queued
     back to back, and the run returns as soon as pass 2's flag word has reached the host."""
 
-    NSLOTS = 3  # runs in flight: k (front), k-1 (tilt fused into k), k-2 (OPD fused into k)
+    NSLOTS = 4  # runs in flight: k (front), k-1 (its sums finishing), k-2 (tilt fused into k), k-3 (OPD fused into k)
 
     def __init__(self, geometry, n, shard=None, comm=None, resample_pass=True, perturbation=None):
         """perturbation: optional legendre.LegendrePerturbation added to every ray's pass-2 optical
@@ -257,11 +258,18 @@ class RayWave:
         # fused numpy-order reductions: pass 2 -> (atan_h, atan_v, det x, y, z), nanmean for the
         # arctans and plain mean for the detector (:3583-3590); tilt -> (det1 x, y, z, total1,
         # total2), all nanmean (:3626, :3633, :3674)
-        self.sink2 = LeafSink(5, self.n_local, 0b00011, self.dev)
-        # per-run buffer sets ("slots", run k uses k % 3): run k's tilt is fused into run k+1's
-        # pass 1 and its OPD into run k+2's, so three runs are in flight at once. Each slot holds a
-        # tilt sink, the det2 extent keys (uint64 bits) its OPD folds and its pupil reads, the
-        # pass-2 tables and the flag words on the host
+        # one per run slot: run k's sums finish (on their own stream) while run k+1's pass 1 and
+        # pass 2 run, and pass 2 of run k+1 refills its own slot's sink meanwhile
+        self._sink2 = [LeafSink(5, self.n_local, 0b00011, self.dev) for _ in range(self.NSLOTS)]
+        L = _lib.lib()
+        self._fin_work = [torch.empty(max(int(L.akb_finish_params_work_bytes(s.desc)) // 8 + 1, 2), dtype=D.F64,
+                                      device=self.dev) for s in self._sink2]
+        # per-run buffer sets ("slots", run k uses k % 4): a pipelined caller fuses run k's tilt
+        # into run k+2's pass 1 and its OPD into run k+3's, so that run k's pass-2 sums and tilt
+        # parameters (their own stream) finish beside run k+1's passes, off the chain of trace
+        # kernels; four runs are in flight at once. Each slot holds a pass-2 and a tilt sink, the
+        # det2 extent keys (uint64 bits) its OPD folds and its pupil reads, the pass-2 tables and
+        # output rows, and the flag words
         NS = self.NSLOTS
         self._sink3 = [LeafSink(5, self.n_local, 0b11111, self.dev) for _ in range(NS)]
         self._ext = torch.zeros((NS, 4), dtype=torch.int64, device=self.dev)
@@ -270,6 +278,7 @@ class RayWave:
         self._opd_buf = None
         self.last = {}
         self.kernel_events = None  # set to a list to time the pass-2 chain launch (bench.py)
+        self.host_waits = os.environ.get("AKB_HOST_WAITS", "1") != "0"  # see _wait
         # prepared launches. The resample picks come from a prepass that traces only the rays
         # they read (akb_trace_chain_samples_f64, every rank all of them); the pick buffer ends
         # with one double-sized slot holding that prepass's flag word, so one copy brings both to
@@ -284,50 +293,53 @@ class RayWave:
         # first two, the prepass's is zeroed on its own stream ahead of each prepass
         self._x1 = torch.zeros(self._nsamp + 2, dtype=D.F64, device=self.dev)
         words = self._x1[self._nsamp:].view(torch.int32)
-        self._flags, self._sflag, self._words = words[0:2], words[2:3], words
+        self._sflag, self._words = words[2:3], words
         self._x1_host = torch.empty((2, self._nsamp + 2), dtype=D.F64, pin_memory=True)
         self._pick_buf = 0
         self._next_picks = None  # (event, host buffer) of a prepass queued for the next run
         # per run slot (a run's front returns before its pass 2 ends, so the next run must not
         # reuse them): the [pass 1, pass 2] flag words on the host and the pass-2 tables [h | v]
         self._f_host = torch.zeros((NS, 2), dtype=torch.int32, pin_memory=True)
+        # the [pass 1, pass 2] trace flag words of each run slot (the tilt-parameter kernel of a
+        # run keeps and clears its slot's pair, beside the next run's passes)
+        self._flagw = torch.zeros((NS, 2), dtype=torch.int32, device=self.dev)
         self._tan2 = torch.empty((NS, 2 * self.n), dtype=D.F64, device=self.dev)
         self._tan2_host = torch.empty((NS, 2 * self.n), dtype=D.F64, pin_memory=True)
         self._staged = [None] * NS  # event after the pass 1 that copied a slot's host tables
+        # event after the tilt-parameter kernel of the run that last used a slot (it clears the
+        # slot's flag words and reads its sink): the slot's next pass 1 waits for it if needed
+        self._slot_done = [None] * NS
         self._desc_key = {}  # id(ChainLaunch) -> geometry_key its descriptor holds
         self._ps = ChainLaunch(self.g.mirrors, tan_h=self.tan_h, tan_v=self.tan_v, row0=0, n_rays=self.n * self.n,
                                src=self.g.source, want=(), samples=(hb, he, col), flags=self._sflag,
                                samples_buf=self._x1[:self._nsamp])
         self._p1 = ChainLaunch(self.g.mirrors, tan_h=self.tan_h, tan_v=self.tan_v, ray0=self.shard.start,
-                               n_rays=self.n_local, src=self.g.source, want=(), flags=self._flags[0:1])
+                               n_rays=self.n_local, src=self.g.source, want=(), flags=self._flagw[0, 0:1])
         self._p2 = {}
         self._desc_key[id(self._ps)] = self._desc_key[id(self._p1)] = geometry_key(self.g)
         self._pert = perturbation.device_tables(self.n, self.n, self.dev) if perturbation is not None else None
         # event after the last queued reader of the pass-2 buffers / extent keys (a back half
         # and its pupil, possibly on another stream): the next pass 2 waits for it
         self._back_done = None
-        # the picks prepass and the small host<->device copies (picks, pass-2 tables) run on their
-        # own stream, beside the trace kernels instead of between them; the flag words' copy on
-        # another (it waits for the run's tilt parameters, the prepass waits for nothing)
+        # two streams besides the caller's, each on a hardware queue of its own (a stream sharing
+        # a queue waits behind the other stream's kernels: the box gives a process 4 queues, so
+        # RayWave takes 2 and leaves one for a caller's back-half stream): the picks prepass and
+        # its copy to the host (beside the trace kernels, latency-bound: the next run's resample
+        # waits for it), and the finishes (a fused tilt's sums, each run's pass-2 sums and tilt
+        # parameters, the flag words' copy to the host), which overlap the next passes
         self._copy = torch.cuda.Stream(device=self.dev)  # (a high-priority copy stream measured 10 % slower)
-        self._flag_copy = torch.cuda.Stream(device=self.dev)
-        # a fused tilt's sums are finished here, beside the next pass 2 (the OPD fused into the
-        # pass 1 after that reads them)
         self._fin = torch.cuda.Stream(device=self.dev)
 
     def _pass2_launch(self, want_rows, slot=0):
         key = (bool(want_rows), slot)
         if key not in self._p2:
             want = ("last_hit", "dir_out", "opl") + (("det", "atan") if want_rows else ())
-            # every slot writes the same output buffers (the next pass 2 may rewrite them once the
-            # fused tilt that reads them, queued ahead of it, is done)
-            same = [v for (w, _), v in self._p2.items() if w == key[0]]
-            out = same[0].res.extra["buffers"] if same else None
+            # each slot writes its own output rows: run k's are tilted inside run k+2's pass 1
             t2 = self._tan2[slot]
-            self._p2[key] = ChainLaunch(self.g.mirrors, tan_h=t2[:self.n], tan_v=t2[self.n:], out=out,
+            self._p2[key] = ChainLaunch(self.g.mirrors, tan_h=t2[:self.n], tan_v=t2[self.n:],
                                         ray0=self.shard.start, n_rays=self.n_local, src=self.g.source,
-                                        det_ghij=self.g.det1, want=want, sink=self.sink2, flags=self._flags[1:2],
-                                        pert=self._pert)
+                                        det_ghij=self.g.det1, want=want, sink=self._sink2[slot],
+                                        flags=self._flagw[slot, 1:2], pert=self._pert)
             self._desc_key[id(self._p2[key])] = geometry_key(self.g)
         return self._p2[key]
 
@@ -397,6 +409,7 @@ class RayWave:
         (akb_chain_desc.copy_*), so pass 2 follows it with no copy or cross-stream wait."""
         d = self._p1.desc
         d.copy_src, d.copy_dst, d.copy_n = D.ptr(self._tan2_host[slot]), D.ptr(self._tan2[slot]), 2 * self.n
+        d.flags = D.ptr(self._flagw[slot, 0:1])
         if fuse is None:
             self._p1.launch(stream=stream, reset_flags=False)
         else:
@@ -499,6 +512,7 @@ class RayWave:
         if sflags:
             torch.cuda.synchronize()
             self._words.zero_()
+            self._flagw.zero_()
             torch.cuda.synchronize()
             raise _lib.AKBError(self._pass1_error(sflags))
         if self._staged[slot] is not None:  # the pass 1 that last copied this slot's host tables
@@ -519,11 +533,15 @@ class RayWave:
             # the back half queued before (its OPD / pupil; its extent keys are cleared by a
             # later tilt-parameter kernel and its tilt sink refilled by a later fused pass 1):
             # normally long done, and then no wait enters the stream
-            if not self._back_done.query():
-                torch.cuda.current_stream().wait_event(self._back_done)
+            self._wait(self._back_done)
             self._back_done = None
-        if fuse_opd is not None and not fuse_opd.fin_ev.query():  # its tilt sums (normally done)
-            torch.cuda.current_stream().wait_event(fuse_opd.fin_ev)
+        if fuse_opd is not None:  # its tilt sums
+            self._wait(fuse_opd.fin_ev)
+        if fuse is not None:  # its tilt parameters
+            self._wait(fuse.done)
+        if self._slot_done[slot] is not None:  # the slot's last tilt parameters (a pipelined caller waited)
+            self._wait(self._slot_done[slot])
+            self._slot_done[slot] = None
         self._use(self._p1, g)
         self._pass1(stream, fuse, slot, fuse_opd)
         if fuse is not None:
@@ -537,23 +555,48 @@ class RayWave:
             self._back_done = None
         self._use(self._pass2_launch(full, slot), g)
         r = self._pass2(want_rows=full, stream=stream, slot=slot)
-        if self.comm.world > 1:  # any rank's flag bits (OR, not a sum: bits must not carry)
-            self.comm.allreduce_or(self._flags)
-        sums, cnts = self._finish_sink(self.sink2, stream)
+        # this run's pass-2 sums and tilt parameters on their own stream: they overlap the next
+        # run's passes (the run is tilted two runs later, inside run k+2's pass 1)
+        p2done = torch.cuda.Event()
+        p2done.record()
         params = torch.empty(25, dtype=D.F64, device=self.dev)  # this run's own block
-        _lib.check(L.akb_tilt_params_f64(D.ptr(sums), D.ptr(cnts), D.ptr(params), D.ptr(self._ext[slot]),
-                                         D.ptr(self._flags), 2, stream))
-        done = torch.cuda.Event()
-        done.record()
-        # the flag words the parameter kernel kept (params[23:25]) to the host, beside the next run
-        with torch.cuda.stream(self._flag_copy):
-            self._flag_copy.wait_event(done)
+        with torch.cuda.stream(self._fin):
+            self._fin.wait_event(p2done)
+            ps = D.stream_handle(self._fin)
+            flags = self._flagw[slot]
+            if self.comm.world > 1:  # any rank's flag bits (OR, not a sum: bits must not carry)
+                self.comm.allreduce_or(flags)
+            if self.comm.world == 1:  # the sink's finish and the parameters in two small launches
+                s2 = self._sink2[slot]
+                _lib.check(L.akb_finish_tilt_params_f64(s2.desc, D.ptr(s2.sums), D.ptr(s2.counts), D.ptr(params),
+                                                        D.ptr(self._ext[slot]), D.ptr(flags), 2,
+                                                        D.ptr(self._fin_work[slot]), ps))
+            else:
+                sums, cnts = self._finish_sink(self._sink2[slot], ps)
+                _lib.check(L.akb_tilt_params_f64(D.ptr(sums), D.ptr(cnts), D.ptr(params), D.ptr(self._ext[slot]),
+                                                 D.ptr(flags), 2, ps))
+            done = torch.cuda.Event()
+            done.record(self._fin)
+            # the flag words the parameter kernel kept (params[23:25]) to the host
             self._f_host[slot].copy_(params[23:24].view(torch.int32), non_blocking=True)
             ev2 = torch.cuda.Event()
-            ev2.record(self._flag_copy)
-        params.record_stream(self._flag_copy)
+            ev2.record(self._fin)
+        self._slot_done[slot] = done
+        params.record_stream(self._fin)
         return _Front(r=r, tan_h2=tan_h2, tan_v2=tan_v2, params=params, full=full, stream=stream, flag_ev=ev2,
                       done=done, slot=slot, g=g)
+
+    def _wait(self, ev):
+        """Order the current stream after ev (an event of RayWave's other streams). host_waits:
+        wait for it on the host instead (a pipelined caller is runs ahead of the device, so the
+        wait costs the device nothing, while a cross-queue wait on the device puts a barrier
+        packet ahead of the next trace kernel); else a device-side wait when ev is still pending."""
+        if ev.query():
+            return
+        if self.host_waits:
+            ev.synchronize()
+        else:
+            torch.cuda.current_stream().wait_event(ev)
 
     def _flags_of(self, f):
         """f's (pass 1, pass 2) trace flag words (waits for its pass 2 if still running)."""
@@ -632,6 +675,8 @@ class RayWave:
         if stream is None:
             if f.opd is None and f.fin_ev is not None:
                 torch.cuda.current_stream().wait_event(f.fin_ev)
+            if f.tilt is None and not f.done.query():  # its tilt parameters (own stream)
+                torch.cuda.current_stream().wait_event(f.done)
             out = self._launch_back(f, opd, keep_rotated)
         else:
             stream.wait_event(f.opd_ev if f.opd is not None else f.tilted if f.tilt is not None else f.done)

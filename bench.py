@@ -13,9 +13,10 @@ pass 1 (4 mirrors), equal-angle resample, pass 2 (4 mirrors + OPL), tilt, two de
 OPD; then a 128 x 128 pupil padded x16 -> 2048^2 PSF (pruned 2-D DFT: the padded plane is never
 built). One step = all of it; its intersections are 2 passes x 4 mirrors x rays. Steps are
 pipelined the way a caller tracing many systems would run them (RayWave.launch_front /
-launch_back): by default (--fuse 2) step k's pass-1 kernel also tilts step k-1 and forms step
-k-2's OPD maps (their loads hidden behind the chain's FP64 arithmetic), and step k-2's pupil and
-PSF run on other streams beside step k's pass 2 while the host resamples. Every step still does
+launch_back): by default (--fuse 2) step k's pass-1 kernel also tilts step k-2 and forms step
+k-3's OPD maps (their loads hidden behind the chain's FP64 arithmetic), step k-1's pass-2 sums and
+tilt parameters finish on their own stream beside step k's passes, and step k-3's pupil and PSF
+run on other streams beside step k's pass 2 while the host resamples. Every step still does
 all of its work inside the timed region. Inputs (the two 1-D angle tables) are resident on the
 device before timing.
 
@@ -59,8 +60,10 @@ PASS2_BYTES_PER_RAY = 56
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=10)
-    p.add_argument("--warmup", type=int, default=3, help="at least 2 with --fuse 2 (fills the pipeline)")
+    # the device's clock settles over the first ~25 steps of a fresh process (step lengths fall
+    # from ~1.0 to ~0.8 ms, scripts/step_timeline.py): the default warm-up covers that
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=30, help="at least 3 with --fuse 2 (fills the pipeline)")
     p.add_argument("--rays", type=float, default=None,
                    help="rays per GPU (default: 1e7 on one GPU, C3; 1.25e7 per rank at N > 1, C4's 1e8 at N = 8)")
     p.add_argument("--systems", type=int, default=8,
@@ -80,8 +83,8 @@ def parse():
     p.add_argument("--back-priority", type=int, default=0,
                    help="torch stream priority of the back stream (lower = higher priority; 0 = normal)")
     p.add_argument("--fuse", type=int, default=2,
-                   help="2: step k's pass-1 kernel also tilts step k-1 and forms step k-2's OPD maps (their loads "
-                        "hidden behind the chain's FP64 arithmetic), step k-2's pupil / PSF on the back stream; "
+                   help="2: step k's pass-1 kernel also tilts step k-2 and forms step k-3's OPD maps (their loads "
+                        "hidden behind the chain's FP64 arithmetic), step k-3's pupil / PSF on the back stream; "
                         "1: the tilt only, the OPD on the back stream; 0: the tilt as its own kernel on the back "
                         "stream beside pass 1")
     p.add_argument("--psf-start", choices=("pupil", "pass1"), default="pupil",
@@ -209,7 +212,7 @@ def huygens_rate(out):
 
 def main():
     args = parse()
-    args.warmup = max(args.warmup, 2 if args.fuse >= 2 else 1)
+    args.warmup = max(args.warmup, 3 if args.fuse >= 2 else 1)
     import torch
     from akbraytracing_amd import build as B
     from akbraytracing_amd import dist as AD
@@ -244,7 +247,8 @@ def main():
 
     psf_events = []
     psf_out = {}
-    side = torch.cuda.Stream(device=dev)
+    # one stream for the back halves, pupils and PSFs (RayWave holds two more: with the caller's,
+    # four streams on the box's four hardware queues per process, none shared)
     # --back-priority -1 lets the HBM-bound back half take CU slots ahead of the FP64-bound pass 1
     # it overlaps; measured a wash (the host resample then lands on the critical path), so off
     back_stream = torch.cuda.Stream(device=dev, priority=args.back_priority)
@@ -252,10 +256,11 @@ def main():
     fronts = []  # launched fronts (pass 1 .. tilt parameters) whose back half is still to queue
 
     def run_psf(opd, pitch, ready, timed):
-        """The PSF of a finished pupil on a side stream: it starts when the pupil is ready and
-        shares the GPU with the next kernels of the main stream."""
+        """The PSF of a finished pupil on the back stream, right behind it: it shares the GPU with
+        the next kernels of the main stream."""
         if rank != 0:
             return
+        side = back_stream
         side.wait_event(ready)
         if args.psf_start == "pass1":
             after = torch.cuda.Event()
@@ -299,11 +304,13 @@ def main():
         i = nsteps[0]
         nsteps[0] += 1
         kw = dict(geometry=sys_of(i), next_geometry=sys_of(i + 1))
-        if args.fuse >= 2 and len(fronts) == 2:  # two steps in flight: tilt k-1, OPD k-2
+        if args.fuse >= 2 and len(fronts) == 3:  # three steps in flight: tilt k-2, OPD k-3
             old = fronts.pop(0)
-            fronts.append(rw.launch_front(overlap=lambda: back(timed, old), fuse=fronts[-1], fuse_opd=old, **kw))
-        elif args.fuse >= 2 and len(fronts) == 1:  # filling the pipeline
+            fronts.append(rw.launch_front(overlap=lambda: back(timed, old), fuse=fronts[0], fuse_opd=old, **kw))
+        elif args.fuse >= 2 and len(fronts) == 2:  # filling the pipeline
             fronts.append(rw.launch_front(fuse=fronts[0], **kw))
+        elif args.fuse >= 2:
+            fronts.append(rw.launch_front(**kw))
         elif fronts and args.fuse:
             prev = fronts.pop(0)
             fronts.append(rw.launch_front(overlap=lambda: back(timed, prev), fuse=prev, **kw))

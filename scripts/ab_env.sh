@@ -1,19 +1,12 @@
 #!/bin/bash
-# A/B of an environment knob by per-kernel rocprofv3 stats over a short bench run:
-#   bash scripts/ab_env.sh VAR "v1 v2 ..." KERNEL_REGEX
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-export TMPDIR=/tmp
-VAR=$1; VALS=$2; RE=$3
-for v in $VALS; do
-  env $VAR=$v timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/ab_$v -o run -- \
-      python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/ab_$v.json 2>/dev/null || exit $?
-  python3 - "$v" "$RE" <<'PY'
-import csv, json, sys
-v, rx = sys.argv[1], sys.argv[2]
-import re
-rows = list(csv.DictReader(open(f"gpurun_out/ab_{v}/run_kernel_stats.csv")))
-b = json.loads(open(f"gpurun_out/ab_{v}.json").read())
-out = {r["Name"][:40]: round(float(r["AverageNs"]) / 1e3, 1) for r in rows if re.search(rx, r["Name"])}
-print(v, round(b["ms_per_step"], 4), out, flush=True)
-PY
+# A/B of one environment variable over interleaved bench runs:
+#   bash scripts/ab_env.sh VAR "valA valB" [steps] [warmup]
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out
+var=$1; vals=$2; steps=${3:-200}; warm=${4:-30}
+for rep in 1 2; do
+  for v in $vals; do
+    env "$var=$v" timeout -k 10 200 python bench.py --steps $steps --warmup $warm --no-cpu-baseline --no-extras \
+        > gpurun_out/ab.json 2> gpurun_out/ab.err || { tail -5 gpurun_out/ab.err; exit 1; }
+    python -c "import json;d=json.load(open('gpurun_out/ab.json'));print('$var=$v ms/step', round(d['ms_per_step'],4), 'pass2', round(d['pass2_kernel_ms'],4), 'host', round(d['host_issue_ms_per_step'],4))"
+  done
 done

@@ -76,12 +76,14 @@ def _worker(rank, world, port, n, runs, out_dir, schedule="plain"):
         else:  # bench.py's --fuse 2 schedule, a different system per run
             sy = _systems(runs)
             nx = lambda i: sy[i + 1] if i + 1 < runs else None
-            fr = [rw.launch_front(geometry=sy[0], next_geometry=sy[1])]
-            fr.append(rw.launch_front(fuse=fr[0], geometry=sy[1], next_geometry=nx(1)))
-            for i in range(2, runs):
-                g = fr.pop(0)
-                fr.append(rw.launch_front(overlap=lambda p=g: back(p), fuse=fr[-1], fuse_opd=g, geometry=sy[i],
-                                          next_geometry=nx(i)))
+            fr = []
+            for i in range(runs):
+                kw = dict(geometry=sy[i], next_geometry=nx(i))
+                if len(fr) == 3:  # run i's pass 1 tilts run i-2 and forms run i-3's OPD
+                    g = fr.pop(0)
+                    fr.append(rw.launch_front(overlap=lambda p=g: back(p), fuse=fr[0], fuse_opd=g, **kw))
+                else:
+                    fr.append(rw.launch_front(fuse=fr[0] if len(fr) == 2 else None, **kw))
             for f in fr:
                 back(f)
         torch.cuda.synchronize()
@@ -94,10 +96,10 @@ def _worker(rank, world, port, n, runs, out_dir, schedule="plain"):
 @pytest.mark.parametrize("n,schedule", [(129, "plain"), (129, "fuse2")])
 def test_two_ranks_on_the_gpu_reassemble_one_process(gpu, tmp_path, n, schedule):
     """plain: the two-stream pipeline on one system; fuse2: bench.py's default schedule (run k's
-    pass 1 tilts run k-1 and forms run k-2's OPD from cross-rank sums finished on their own stream),
+    pass 1 tilts run k-2 and forms run k-3's OPD from cross-rank sums finished on their own stream),
     a different system per run, against one process's sequential run() of each system."""
     from akbraytracing_amd.wavefront import RayWave
-    runs = 3 if schedule == "plain" else 5
+    runs = 3 if schedule == "plain" else 6
     systems = [_geom()] * runs if schedule == "plain" else _systems(runs)
     rw = RayWave(_geom(), n)
     wants = []

@@ -402,13 +402,33 @@ def test_fused_pipeline_equals_sequential_runs(gpu, n):
         assert torch.equal(opd, want_opd)
 
 
+def _fused_pipeline(rw, back, lag, kws):
+    """Fronts pipelined as bench.py --fuse 2 does: run k's pass 1 tilts run k-lag and forms run
+    k-lag-1's OPD (lag 2 is bench.py's: run k-1's pass-2 sums and tilt parameters then finish
+    beside run k's passes); the runs left in flight drain through the tilt-only and unfused back
+    halves. kws: launch_front keywords of each run. Returns the expected back-half kinds."""
+    fr = []
+    for kw in kws:
+        if len(fr) == lag + 1:
+            g = fr.pop(0)
+            fr.append(rw.launch_front(overlap=lambda p=g: back(p), fuse=fr[0], fuse_opd=g, **kw))
+        elif len(fr) == lag:
+            fr.append(rw.launch_front(fuse=fr[0], **kw))
+        else:
+            fr.append(rw.launch_front(**kw))
+    for f in fr:
+        back(f)
+    return [(True, True)] * (len(kws) - lag - 1) + [(True, False)] + [(False, False)] * lag
+
+
+@pytest.mark.parametrize("lag", [1, 2])
 @pytest.mark.parametrize("n", [65, 1001])
-def test_opd_fused_pipeline_equals_sequential_runs(gpu, n):
-    """bench.py's default pipeline (--fuse 2): run k's pass-1 kernel also tilts run k-1 and forms
-    run k-2's OPD maps and extent keys (akb_chain_tilt_opd_f64), k-1's tilt sums finished on a
-    stream of their own; k-2's launch_back and pupil go beside pass 2 - the same bits, pupil
-    pitch included, as run() one at a time. The two runs left in flight drain through the
-    tilt-only and the unfused back halves."""
+def test_opd_fused_pipeline_equals_sequential_runs(gpu, n, lag):
+    """bench.py's default pipeline (--fuse 2): run k's pass-1 kernel also tilts run k-2 (or k-1)
+    and forms run k-3's (k-2's) OPD maps and extent keys (akb_chain_tilt_opd_f64), the tilt sums
+    finished on a stream of their own, each run's pass-2 sums and tilt parameters on another; the
+    OPD-formed run's launch_back and pupil go beside pass 2 - the same bits, pupil pitch
+    included, as run() one at a time."""
     from akbraytracing_amd.wavefront import RayWave
     rw = RayWave(_geom(), n)
     seq = rw.run()
@@ -425,15 +445,9 @@ def test_opd_fused_pipeline_equals_sequential_runs(gpu, n):
             pupils.append(tuple(t.clone() for t in rw.pupil(32)))
             means.append(rw.means())
 
-    fr = [rw.launch_front()]
-    fr.append(rw.launch_front(fuse=fr[0]))
-    for _ in range(4):
-        g = fr.pop(0)
-        fr.append(rw.launch_front(overlap=lambda p=g: back(p), fuse=fr[-1], fuse_opd=g))
-    for f in fr:
-        back(f)
+    want_kinds = _fused_pipeline(rw, back, lag, [{}] * (lag + 5))
     torch.cuda.synchronize()
-    assert kinds == [(True, True)] * 4 + [(True, False), (False, False)]
+    assert kinds == want_kinds
     for o, (opd, pitch), m in zip(outs, pupils, means):
         for k, v in want.items():
             assert torch.equal(o[k], v), k
@@ -459,14 +473,15 @@ def _variants(k):
     return out
 
 
+@pytest.mark.parametrize("lag", [1, 2])
 @pytest.mark.parametrize("n", [65, 301])
-def test_opd_fused_pipeline_distinct_systems(gpu, n):
+def test_opd_fused_pipeline_distinct_systems(gpu, n, lag):
     """The default pipeline (--fuse 2) with every run tracing another system: run k's pass-1
-    kernel tilts run k-1 (with run k-1's detector planes and rotation) and forms run k-2's OPD
-    (from run k-2's tilt sums); each run's Wave2, DistError2, detector-2 hits, totals, means and
-    pupil pitch equal a sequential run() of that same system, bit for bit."""
+    kernel tilts run k-lag (with that run's detector planes and rotation) and forms run
+    k-lag-1's OPD (from its tilt sums); each run's Wave2, DistError2, detector-2 hits, totals,
+    means and pupil pitch equal a sequential run() of that same system, bit for bit."""
     from akbraytracing_amd.wavefront import RayWave
-    systems = _variants(6)
+    systems = _variants(7)
     rw = RayWave(systems[0], n)
     want = []
     for g in systems:
@@ -486,17 +501,11 @@ def test_opd_fused_pipeline_distinct_systems(gpu, n):
             o = rw.launch_back(front, stream=bs)
             outs.append(({k: o[k].clone() for k in want[0][0]}, *(t.clone() for t in rw.pupil(32)), rw.means()))
 
-    nxt = lambda i: systems[i + 1] if i + 1 < len(systems) else None
-    fr = [rw.launch_front(geometry=systems[0], next_geometry=systems[1])]
-    fr.append(rw.launch_front(fuse=fr[0], geometry=systems[1], next_geometry=systems[2]))
-    for i in range(2, len(systems)):
-        g = fr.pop(0)
-        fr.append(rw.launch_front(overlap=lambda p=g: back(p), fuse=fr[-1], fuse_opd=g, geometry=systems[i],
-                                  next_geometry=nxt(i)))
-    for f in fr:
-        back(f)
+    kws = [dict(geometry=g, next_geometry=systems[i + 1] if i + 1 < len(systems) else None)
+           for i, g in enumerate(systems)]
+    want_kinds = _fused_pipeline(rw, back, lag, kws)
     torch.cuda.synchronize()
-    assert kinds == [(True, True)] * 4 + [(True, False), (False, False)]
+    assert kinds == want_kinds
     for i, ((o, opd, pitch, m), (w, wopd, wpitch, wm)) in enumerate(zip(outs, want)):
         for k, v in w.items():
             assert torch.equal(o[k], v), (i, k)
