@@ -30,14 +30,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "gpurun_out")
 DST = os.path.join(ROOT, "profiles")
 TRACE_SOURCES = ["akbraytracing_amd/csrc/akb_trace.hip", "akbraytracing_amd/csrc/akb_common.h",
-                 "include/akb_raytrace.h"]
+                 "akbraytracing_amd/csrc/akb_pairwise.h", "include/akb_raytrace.h"]
 # the kernels bench.py reports: (key, kernel-name prefix, algorithmic HBM bytes per ray, rays label)
 KERNELS = [
     ("pass2", "void akb::k_chain_sink<true, true", 56,
      "pass 2: 4 mirrors + OPL + detector + 2 arctan; writes last hit, exit direction, OPL (56 B/ray)"),
     ("pass1_fused", "void akb::k_chain_tilt<4, true>", 56 + 32 + 48,
-     "pass 1 of run k (4 mirrors) + tilt of run k-1 (reads 56 B, writes det2 + total2, 32 B) "
-     "+ OPD of run k-2 (reads 32 B, writes 16 B)"),
+     "pass 1 of run k (4 mirrors) + tilt of run k-2 (reads 56 B, writes det2 + total2, 32 B) "
+     "+ OPD of run k-3 (reads 32 B, writes 16 B)"),
 ]
 SIMDS = 1024  # 256 CUs x 4 SIMDs
 XCDS = 8
@@ -135,7 +135,7 @@ def main(tag):
     except Exception:
         head = None
     summary = {"tag": tag, "sources": TRACE_SOURCES, "sources_sha256": sources_sha256(), "git_head": head,
-               "command": os.environ.get("AKB_PROFILE_CMD", "python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline"),
+               "command": os.environ.get("AKB_PROFILE_CMD", "python3 bench.py --steps 20 --warmup 30 --no-cpu-baseline --no-extras"),
                "kernels": {}}
     for key, prefix, bpr, label in KERNELS:
         name = next((k for k in pmc if k.startswith(prefix)), None)
