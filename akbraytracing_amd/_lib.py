@@ -19,7 +19,7 @@ c_int = ctypes.c_int
 c_dbl = ctypes.c_double
 c_vp = ctypes.c_void_p
 MAX_MIRRORS = 7
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 FLAG_MISS = 0x1
 FLAG_ZERO_NORMAL = 0x2
@@ -46,6 +46,8 @@ EXPORTS = [
     "akb_gd_cells_f64", "akb_gd_pockets", "akb_gd_check_pockets", "akb_gd_grad_sweep_f64", "akb_gd_eval_f64",
     "akb_trace_chain_batch_f64", "akb_focus_eval_work_bytes", "akb_focus_eval_f64",
     "akb_finish_params_work_bytes", "akb_finish_tilt_params_f64",
+    "akb_valid_mask_u8", "akb_external_contours", "akb_approx_poly_dp", "akb_affine_from_points",
+    "akb_affine_invert", "akb_warp_affine_f64",
 ]
 
 
@@ -156,6 +158,12 @@ def _declare(L):
                                   c_int),
         "akb_gd_cells_f64": ([c_vp, c_vp, c_int, c_int, c_vp, c_dbl, c_vp, c_vp, c_vp, c_vp], c_int),
         "akb_gd_pockets": ([c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp], c_int),
+        "akb_valid_mask_u8": ([c_vp, c_int, c_int, c_vp, c_vp], c_int),
+        "akb_external_contours": ([c_vp, c_int, c_int, c_i64, c_vp, c_vp, c_i32, c_vp, c_vp], c_int),
+        "akb_approx_poly_dp": ([c_vp, c_i32, c_dbl, c_int, c_vp, c_vp], c_int),
+        "akb_affine_from_points": ([c_vp, c_vp, c_vp], c_int),
+        "akb_affine_invert": ([c_vp, c_vp], c_int),
+        "akb_warp_affine_f64": ([c_vp, c_int, c_int, c_vp, c_int, c_vp, c_vp], c_int),
         "akb_gd_check_pockets": ([c_vp, c_vp, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_dbl, c_vp, c_vp],
                                  c_int),
         "akb_gd_grad_sweep_f64": ([c_vp, c_vp, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,

@@ -15,7 +15,7 @@ CSRC = os.path.join(PKG, "csrc")
 LIBDIR = os.path.join(PKG, "lib")
 SO = os.path.join(LIBDIR, "libakb_hip.so")
 SOURCES = ["akb_trace.hip", "akb_reduce.hip", "akb_huygens.hip", "akb_psf.hip", "akb_psfcalc.hip", "akb_griddata.hip", "akb_focus.hip", "akb_host.cpp",
-           "akb_gd_host.cpp"]
+           "akb_gd_host.cpp", "akb_affine_host.cpp"]
 HEADERS = ["akb_common.h", "akb_sincos.h", "akb_pairwise.h", os.path.join("..", "..", "include", "akb_raytrace.h")]
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = os.environ.get("AKB_OFFLOAD_ARCH", "gfx950")

@@ -253,6 +253,84 @@ __global__ void __launch_bounds__(kBlock) k_legendre_rows(LegArgs a) {
     }
 }
 
+// ---- extract_affine_square_region's warps (AKB_raytrace_20250312.py:1109-1115), both in one pass:
+// cv2.warpAffine(nan_to_num(img), M, INTER_LINEAR) and cv2.warpAffine(mask, M, INTER_NEAREST) with
+// BORDER_CONSTANT 0, then NaN where the warped mask is 0. iM is M inverted as warpAffine inverts it
+// (akb_affine_invert). Source coordinates follow OpenCV's fixed point: the affine terms are scaled
+// by 2^10 and rounded to nearest even, INTER_LINEAR keeps 5 fractional bits (32 x 32 weight table,
+// weights (1 - f) / f products, exact), INTER_NEAREST rounds at 2^9; the bilinear sum is
+// v0 w0 + v1 w1 + v2 w2 + v3 w3 left to right, unfused, as OpenCV's double remap forms it.
+__device__ __forceinline__ int cv_round(double v) { return __double2int_rn(v); }
+__device__ __forceinline__ int sat_short(int v) { return v < -32768 ? -32768 : (v > 32767 ? 32767 : v); }
+__device__ __forceinline__ double nan_to_num(double v) {
+    if (v != v) return 0.0;
+    if (v == INFINITY) return 1.7976931348623157e308;
+    if (v == -INFINITY) return -1.7976931348623157e308;
+    return v;
+}
+
+struct WarpArgs {
+    const double* img;
+    int ny, nx;
+    double m0, m1, m2, m3, m4, m5;  // the inverse map: source = (m0 x + m1 y + m2, m3 x + m4 y + m5)
+    int side;
+    double* out;
+};
+
+__global__ void __launch_bounds__(256) k_warp_affine(WarpArgs a) {
+    const int64_t n = (int64_t)a.side * a.side;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int y = (int)(i / a.side), x = (int)(i - (int64_t)y * a.side);
+        const int xr = cv_round((a.m1 * y + a.m2) * 1024);
+        const int yr = cv_round((a.m4 * y + a.m5) * 1024);
+        const int adelta = cv_round(a.m0 * x * 1024), bdelta = cv_round(a.m3 * x * 1024);
+        // INTER_NEAREST mask
+        const int xn = sat_short((xr + 512 + adelta) >> 10), yn = sat_short((yr + 512 + bdelta) >> 10);
+        bool valid = false;
+        if ((unsigned)xn < (unsigned)a.nx && (unsigned)yn < (unsigned)a.ny) {
+            const double v = a.img[(int64_t)yn * a.nx + xn];
+            valid = v == v;
+        }
+        if (!valid) {
+            a.out[i] = NAN;
+            continue;
+        }
+        // INTER_LINEAR value
+        const int X = (xr + 16 + adelta) >> 5, Y = (yr + 16 + bdelta) >> 5;
+        const int sx = sat_short(X >> 5), sy = sat_short(Y >> 5);
+        const int fx = X & 31, fy = Y & 31;
+        const double ax = fx * (1.0 / 32), ay = fy * (1.0 / 32);
+        const double w0 = (1.0 - ay) * (1.0 - ax), w1 = (1.0 - ay) * ax, w2 = ay * (1.0 - ax), w3 = ay * ax;
+        double v0, v1, v2, v3;
+        if ((unsigned)sx < (unsigned)(a.nx - 1) && (unsigned)sy < (unsigned)(a.ny - 1)) {
+            const double* s = a.img + (int64_t)sy * a.nx + sx;
+            v0 = nan_to_num(s[0]);
+            v1 = nan_to_num(s[1]);
+            v2 = nan_to_num(s[a.nx]);
+            v3 = nan_to_num(s[a.nx + 1]);
+        } else if (sx >= a.nx || sx + 1 < 0 || sy >= a.ny || sy + 1 < 0) {
+            a.out[i] = 0.0;
+            continue;
+        } else {
+            const int x0 = sx >= 0 && sx < a.nx ? sx : -1, x1 = sx + 1 >= 0 && sx + 1 < a.nx ? sx + 1 : -1;
+            const int y0 = sy >= 0 && sy < a.ny ? sy : -1, y1 = sy + 1 >= 0 && sy + 1 < a.ny ? sy + 1 : -1;
+            v0 = x0 >= 0 && y0 >= 0 ? nan_to_num(a.img[(int64_t)y0 * a.nx + x0]) : 0.0;
+            v1 = x1 >= 0 && y0 >= 0 ? nan_to_num(a.img[(int64_t)y0 * a.nx + x1]) : 0.0;
+            v2 = x0 >= 0 && y1 >= 0 ? nan_to_num(a.img[(int64_t)y1 * a.nx + x0]) : 0.0;
+            v3 = x1 >= 0 && y1 >= 0 ? nan_to_num(a.img[(int64_t)y1 * a.nx + x1]) : 0.0;
+        }
+        a.out[i] = v0 * w0 + v1 * w1 + v2 * w2 + v3 * w3;
+    }
+}
+
+// mask = 255 where img is not NaN (extract_affine_square_region's valid_mask_uint8, :1063-1064)
+__global__ void __launch_bounds__(256) k_valid_mask(const double* __restrict__ img, int64_t n, uint8_t* __restrict__ m) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const double v = img[i];
+        m[i] = v == v ? 255 : 0;
+    }
+}
+
 }  // namespace akb
 
 using namespace akb;
@@ -324,6 +402,21 @@ int akb_legendre_rows_f64(const double* data, int n, int K, int order, const dou
     LegArgs a{data, n, K, order, px, py, ord, s, c, mode, out};
     k_legendre_rows<<<grid_for((int64_t)n * n * K), kBlock, 0, (hipStream_t)stream>>>(a);
     return launch_status("k_legendre_rows");
+}
+
+int akb_valid_mask_u8(const double* img, int ny, int nx, uint8_t* mask, void* stream) {
+    AKB_REQUIRE(img && mask && ny > 0 && nx > 0, "arguments");
+    const int64_t n = (int64_t)ny * nx;
+    akb::k_valid_mask<<<akb::grid_for(n, 4), 256, 0, (hipStream_t)stream>>>(img, n, mask);
+    return akb::launch_status("k_valid_mask");
+}
+
+int akb_warp_affine_f64(const double* img, int ny, int nx, const double* iM, int side, double* out, void* stream) {
+    AKB_REQUIRE(img && iM && out && ny > 0 && nx > 0 && side > 0, "arguments");
+    akb::WarpArgs a{img, ny, nx, iM[0], iM[1], iM[2], iM[3], iM[4], iM[5], side, out};
+    const int64_t n = (int64_t)side * side;
+    akb::k_warp_affine<<<akb::grid_for(n, 4), 256, 0, (hipStream_t)stream>>>(a);
+    return akb::launch_status("k_warp_affine");
 }
 
 }  // extern "C"

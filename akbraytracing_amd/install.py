@@ -132,6 +132,7 @@ _NATIVE = {
     "plane_correction_with_nan_and_outlier_filter": _lazy("pupilmap", "plane_correction_with_nan_and_outlier_filter"),
     "find_defocus": _lazy("focus", "find_defocus"),
     "calc_dS": _lazy("wavedata", "calc_dS"),
+    "extract_affine_square_region": _lazy("affine", "extract_affine_square_region"),
     "psf_calc": None,  # bound per module (_psf_calc_for)
     "plot_result_debug": None,  # bound per module (_PER_MODULE)
     "auto_focus_NA": None,

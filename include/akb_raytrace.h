@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define AKB_ABI_VERSION 9
+#define AKB_ABI_VERSION 10
 
 /* status codes */
 #define AKB_OK 0
@@ -412,6 +412,28 @@ int akb_plane_subtract_f64(const double* z, int ny, int nx, const double* d_coef
  * The nansums of modes 0 and 1 are akb_pairwise_sum_f64's rows (nan_mask 1). */
 int akb_legendre_rows_f64(const double* data, int n, int K, int order, const double* px, const double* py,
                           const int* ord, const double* s, const double* c, int mode, double* out, void* stream);
+
+/* ---------------- extract_affine_square_region (ref AKB_raytrace_20250312.py:1047-1119) ----------------
+ * The reference uses OpenCV (absent from this image: parity with cv2 unpinned; these restate the
+ * published algorithms as OpenCV 4.x implements them, see akb_affine_host.cpp).
+ * akb_valid_mask_u8: mask = 255 where img is not NaN, else 0 (device).
+ * akb_external_contours (HOST): cv2.findContours(mask, RETR_EXTERNAL, CHAIN_APPROX_SIMPLE) -
+ *   contour c is xy[2 offsets[c] .. 2 offsets[c+1]) as (x, y) pairs, in cv2's order; fails with
+ *   AKB_E_INVALID when the caller's capacities (cap points, ocap offsets) are too small, *n_xy and
+ *   *n_contours still set.
+ * akb_approx_poly_dp (HOST): cv2.approxPolyDP(src (count, 2) int32, eps, closed).
+ * akb_affine_from_points (HOST): cv2.getAffineTransform(src[3] float32 pairs, dst[3]) -> M (2 x 3).
+ * akb_affine_invert (HOST): M inverted as cv2.warpAffine does without WARP_INVERSE_MAP.
+ * akb_warp_affine_f64: out (side x side) = cv2.warpAffine(nan_to_num(img), M, INTER_LINEAR),
+ *   NaN where cv2.warpAffine(mask, M, INTER_NEAREST) == 0 (BORDER_CONSTANT 0); iM from
+ *   akb_affine_invert (host array, passed by value). */
+int akb_valid_mask_u8(const double* img, int ny, int nx, uint8_t* mask, void* stream);
+int akb_external_contours(const uint8_t* mask, int rows, int cols, int64_t cap, int32_t* xy, int64_t* n_xy,
+                          int32_t ocap, int32_t* offsets, int32_t* n_contours);
+int akb_approx_poly_dp(const int32_t* src, int32_t count, double eps, int closed, int32_t* dst, int32_t* n_out);
+int akb_affine_from_points(const float* src, const float* dst, double* M);
+int akb_affine_invert(const double* M, double* iM);
+int akb_warp_affine_f64(const double* img, int ny, int nx, const double* iM, int side, double* out, void* stream);
 
 /* ---------------- griddata(method='cubic') on the ray grid (ref AKB_raytrace_20250312.py:3673, :3689) ----------------
  * scipy's Clough-Tocher griddata for points that are the n_v x n_h ray grid's detector hits

@@ -2,7 +2,8 @@
 // restatement (SURVEY.md §5 "sanitizers"). Built and run by tests/test_sanitize.py:
 //
 //   hipcc -O1 -g -fsanitize=address,undefined -fno-gpu-sanitize  host_asan_driver.cpp
-//         akbraytracing_amd/csrc/akb_host.cpp akbraytracing_amd/csrc/akb_gd_host.cpp  (+ oracle C)
+//         akbraytracing_amd/csrc/akb_host.cpp akbraytracing_amd/csrc/akb_gd_host.cpp
+//         akbraytracing_amd/csrc/akb_affine_host.cpp  (+ oracle C)
 //
 // Host-only code (no kernel launches): the equal-angle resample (akb_resample_f64: numpy linspace
 // and interp restated, scipy's stable sort), the griddata pocket triangulation (akb_gd_pockets:
@@ -103,6 +104,46 @@ static int pocket_case(int nv, int nh, int warp, bool cut_corner) {
                           xidx.data());
 }
 
+// extract_affine_square_region's host steps (akb_affine_host.cpp) on random masks: contours into
+// exactly-sized buffers (a too-small capacity must be refused, not overrun), polygons of every
+// contour at several tolerances, the affine solve and inverse
+static int affine_cases() {
+    int contours = 0, refused = 0;
+    for (int t = 0; t < 300; ++t) {
+        const int rows = 1 + (int)(rng() % 40), cols = 1 + (int)(rng() % 40);
+        std::vector<uint8_t> m((size_t)rows * cols);
+        const int dens = (int)(rng() % 100);
+        for (auto& v : m) v = (int)(rng() % 100) < dens ? 255 : 0;
+        int64_t nxy = 0;
+        int32_t nc = 0;
+        int32_t probe_xy[2], probe_off[1];
+        if (akb_external_contours(m.data(), rows, cols, 0, probe_xy, &nxy, 0, probe_off, &nc) != 0) ++refused;
+        std::vector<int32_t> xy(2 * (size_t)(nxy > 0 ? nxy : 1)), offs((size_t)nc + 1);
+        if (akb_external_contours(m.data(), rows, cols, nxy, xy.data(), &nxy, nc + 1, offs.data(), &nc) != 0) return 0;
+        contours += nc;
+        for (int c = 0; c < nc; ++c) {
+            const int32_t k = offs[c + 1] - offs[c];
+            std::vector<int32_t> out(2 * (size_t)k);
+            int32_t nout = 0;
+            for (double eps : {0.0, 0.5, 2.0, 50.0})
+                if (akb_approx_poly_dp(xy.data() + 2 * (size_t)offs[c], k, eps, 1, out.data(), &nout) != 0 && k > 1)
+                    ++refused;  // coincident slice ends (a one-pixel-wide spur) are refused, as cv2 asserts
+        }
+    }
+    for (int t = 0; t < 200; ++t) {
+        float src[6], dst[6];
+        for (int i = 0; i < 6; ++i) {
+            src[i] = (float)unif(-50, 300);
+            dst[i] = (float)unif(-10, 260);
+        }
+        if (t % 50 == 0) src[4] = src[0], src[5] = src[1];  // repeated point: refused
+        double M[6], iM[6];
+        if (akb_affine_from_points(src, dst, M) == 0) akb_affine_invert(M, iM);
+    }
+    printf("affine: %d contours, %d refused\n", contours, refused);
+    return contours > 0;
+}
+
 static int oracle_cases() {
     const int64_t n = 1021;
     std::vector<double> d(3 * n), s(3 * n), out(3 * n), nrm(3 * n), ref(3 * n);
@@ -145,6 +186,7 @@ int main() {
     printf("pockets: cut corner -> %d (refused as expected: %s)\n", st, st != 0 ? "yes" : "no");
     if (st == 0) return 3;
     good &= oracle_cases();
+    good &= affine_cases();
     fflush(stdout);
     return good ? 0 : 1;
 }

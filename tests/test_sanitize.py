@@ -1,5 +1,6 @@
 """Sanitizer build of the host code: the library's host-side C++ (akb_host.cpp: the
-resample; akb_gd_host.cpp: the pocket triangulation with its fixed-capacity arrays) and the
+resample; akb_gd_host.cpp: the pocket triangulation with its fixed-capacity arrays;
+akb_affine_host.cpp: contours, polygons and the affine solve of extract_affine_square_region) and the
 oracle's C restatement, compiled with -fsanitize=address,undefined into a standalone driver
 (tests/sanitize/host_asan_driver.cpp) and run over random, ragged, NaN and degenerate inputs.
 GPU code is not sanitized (not available on this pool): the driver links host code only."""
@@ -28,7 +29,7 @@ def test_host_code_under_asan_and_ubsan(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     objs = [oobj]
     for src in (os.path.join(ROOT, "tests", "sanitize", "host_asan_driver.cpp"), os.path.join(csrc, "akb_host.cpp"),
-                os.path.join(csrc, "akb_gd_host.cpp")):
+                os.path.join(csrc, "akb_gd_host.cpp"), os.path.join(csrc, "akb_affine_host.cpp")):
         obj = str(tmp_path / (os.path.basename(src) + ".o"))
         r = subprocess.run([HIPCC, "-c", "--offload-arch=gfx950", "-std=c++17", "-fno-gpu-sanitize"] + san +
                            [src, "-o", obj], capture_output=True, text=True, timeout=600)
@@ -44,4 +45,4 @@ def test_host_code_under_asan_and_ubsan(tmp_path):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
     assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr, r.stderr[-4000:]
-    assert "resample:" in r.stdout and "cut corner" in r.stdout
+    assert "resample:" in r.stdout and "cut corner" in r.stdout and "affine:" in r.stdout
