@@ -330,6 +330,22 @@ __device__ __forceinline__ double grad_solve(const GradAcc<NV>& A, int v, const 
     return c;
 }
 
+template <int W>
+__device__ __forceinline__ void change_max_n(double worst, unsigned long long* chg) {
+    __shared__ double red[W / 64];
+    for (int off = 32; off > 0; off >>= 1) worst = fmax(worst, __shfl_down(worst, off));
+    if (W > 64) {
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = worst;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < W / 64; ++w) worst = fmax(worst, red[w]);
+        const unsigned long long bits = (unsigned long long)__double_as_longlong(worst);
+        if (chg && worst > 0 && __hip_atomic_load(chg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < bits)
+            atomicMax(chg, bits);
+    }
+}
+
 __device__ __forceinline__ void change_max(double worst, unsigned long long* chg) {
     __shared__ double red[kBlock / 64];
     for (int off = 32; off > 0; off >>= 1) worst = fmax(worst, __shfl_down(worst, off));
@@ -392,6 +408,167 @@ __global__ void __launch_bounds__(kBlock) k_gd_grad(Grid g, const double* __rest
         for (int v = 0; v < NV; ++v) worst = fmax(worst, grad_solve<NV>(A, v, gin, gout, 2 * (v * n + i)));
     }
     change_max(worst, chg);
+}
+
+// The same sweep with every vertex's data read from HBM once: a workgroup walks down a strip of
+// kStripW columns (plus one halo column each side) over kStripRows rows, holding three rows of
+// (x, y, f, g) in an LDS ring, the next row already in registers while the current one is solved
+// (its loads in flight across the row's arithmetic). The per-vertex edge order and arithmetic are
+// k_gd_grad's, so both give the same bits; the global version's eight-neighbour gathers (about 50
+// load instructions per vertex through the texture path) become LDS reads.
+constexpr int kStripRows = 32;
+
+template <int NV, int W>
+struct StripRow {  // one row of a strip in LDS: column c of the strip at [c + 1], halos at 0 / W + 1
+    double x[W + 2], y[W + 2];
+    double f[NV][W + 2];
+    double gx[NV][W + 2], gy[NV][W + 2];
+    uint8_t d[W + 2];  // the diagonal flags of the cell row below (cells (row, col - 1) at [col])
+};
+
+template <int NV>
+struct StripVals {
+    double x, y, f[NV], gx[NV], gy[NV];
+    int d;  // diag of cell (row, col) (0 outside the cells)
+};
+
+template <int NV>
+__device__ __forceinline__ void strip_load(const Grid& g, int64_t n, const double* __restrict__ f,
+                                           const double* __restrict__ gin, int64_t i, StripVals<NV>& v) {
+    v.x = g.x[i];
+    v.y = g.y[i];
+    const int iv = (int)(i / g.nh), ih = (int)(i - (int64_t)iv * g.nh);
+    v.d = (iv < g.nv - 1 && ih < g.nh - 1) ? g.diag[(int64_t)iv * (g.nh - 1) + ih] : 0;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        v.f[k] = f[k * n + i];
+        v.gx[k] = gin[2 * (k * n + i)];
+        v.gy[k] = gin[2 * (k * n + i) + 1];
+    }
+}
+
+template <int NV, int W>
+__device__ __forceinline__ void strip_store(StripRow<NV, W>& r, int c, const StripVals<NV>& v) {
+    r.x[c] = v.x;
+    r.y[c] = v.y;
+    r.d[c] = (uint8_t)v.d;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        r.f[k][c] = v.f[k];
+        r.gx[k][c] = v.gx[k];
+        r.gy[k][c] = v.gy[k];
+    }
+}
+
+// grad_edge with the neighbour's data from an LDS row
+template <int NV, int W>
+__device__ __forceinline__ void grad_edge_lds(const StripRow<NV, W>& r, int c, double xi, double yi,
+                                              const double (&fi)[NV], GradAcc<NV>& A) {
+    const double ex = r.x[c] - xi, ey = r.y[c] - yi;
+    const double l2 = ex * ex + ey * ey;
+    double rr = __builtin_amdgcn_rsq(l2);
+    rr = rr * __builtin_fma(-0.5 * l2 * rr, rr, 1.5);
+    const double r3 = rr * rr * rr;
+    const double wx = ex * r3, wy = ey * r3;
+    A.q0 = __builtin_fma(ex, wx, A.q0);
+    A.q1 = __builtin_fma(ex, wy, A.q1);
+    A.q3 = __builtin_fma(ey, wy, A.q3);
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const double df2 = -ex * r.gx[v][c] - ey * r.gy[v][c];
+        const double w = 6 * (fi[v] - r.f[v][c]) - 2 * df2;
+        A.s0[v] = __builtin_fma(w, wx, A.s0[v]);
+        A.s1[v] = __builtin_fma(w, wy, A.s1[v]);
+    }
+}
+
+template <int NV, int W>
+__global__ void __launch_bounds__(W) k_gd_grad_strip(Grid g, const double* __restrict__ f,
+                                                     const double* __restrict__ gin, double* __restrict__ gout,
+                                                     double* __restrict__ ring_acc, unsigned long long* chg) {
+    constexpr int kStripW = W;
+    __shared__ StripRow<NV, W> R[3];
+    const int64_t n = (int64_t)g.nv * g.nh;
+    const int nstrips = (g.nh + kStripW - 1) / kStripW;
+    const int strip = blockIdx.x % nstrips, chunk = blockIdx.x / nstrips;
+    const int c0 = strip * kStripW;
+    const int r0 = chunk * kStripRows;
+    const int r1 = r0 + kStripRows < g.nv ? r0 + kStripRows : g.nv;
+    const int t = threadIdx.x;
+    const int ih = c0 + t;
+    const bool col = ih < g.nh;
+    // halo columns: thread 0 the left one, thread 1 the right one (when they exist)
+    const int hcol = t == 0 ? c0 - 1 : c0 + kStripW;
+    const int hslot = t == 0 ? 0 : kStripW + 1;
+    const bool halo = t < 2 && hcol >= 0 && hcol < g.nh;
+    double worst = 0.0;
+    // rows iv + 1 and iv + 2 wait in two register sets (a and b, alternating) while row iv is solved
+    StripVals<NV> a, ah, b, bh;
+    auto load_row = [&](int rr, StripVals<NV>& v, StripVals<NV>& vh) {
+        if (col) strip_load<NV>(g, n, f, gin, (int64_t)rr * g.nh + ih, v);
+        if (halo) strip_load<NV>(g, n, f, gin, (int64_t)rr * g.nh + hcol, vh);
+    };
+    auto store_row = [&](int rr, const StripVals<NV>& v, const StripVals<NV>& vh) {
+        if (col) strip_store<NV, W>(R[rr % 3], t + 1, v);
+        if (halo) strip_store<NV, W>(R[rr % 3], hslot, vh);
+    };
+    // prologue: rows r0 - 1 and r0 into LDS, rows r0 + 1 and r0 + 2 into registers (a row k is
+    // needed while k <= r1: row r1 is the last row's lower neighbour)
+    for (int rr = r0 - 1; rr <= r0; ++rr) {
+        if (rr < 0) continue;
+        load_row(rr, a, ah);
+        store_row(rr, a, ah);
+    }
+    if (r0 + 1 < g.nv) load_row(r0 + 1, a, ah);
+    if (r0 + 2 < g.nv && r0 + 2 <= r1) load_row(r0 + 2, b, bh);
+    auto step = [&](int iv, StripVals<NV>& nx, StripVals<NV>& nh_) {
+        if (iv + 1 < g.nv) store_row(iv + 1, nx, nh_);  // row iv + 1: registers -> LDS
+        __syncthreads();
+        if (iv + 3 < g.nv && iv + 3 <= r1) load_row(iv + 3, nx, nh_);  // two rows ahead
+        if (col) {
+            const StripRow<NV, W>& up = R[(iv + 2) % 3];  // row iv - 1
+            const StripRow<NV, W>& cur = R[iv % 3];
+            const StripRow<NV, W>& dn = R[(iv + 1) % 3];
+            const int c = t + 1;
+            const int64_t i = (int64_t)iv * g.nh + ih;
+            const double xi = cur.x[c], yi = cur.y[c];
+            double fi[NV];
+#pragma unroll
+            for (int v = 0; v < NV; ++v) fi[v] = cur.f[v][c];
+            GradAcc<NV> A;
+            if (ih > 0) grad_edge_lds<NV, W>(cur, c - 1, xi, yi, fi, A);
+            if (ih < g.nh - 1) grad_edge_lds<NV, W>(cur, c + 1, xi, yi, fi, A);
+            if (iv > 0) grad_edge_lds<NV, W>(up, c, xi, yi, fi, A);
+            if (iv < g.nv - 1) grad_edge_lds<NV, W>(dn, c, xi, yi, fi, A);
+            // the four cells around i: (iv - 1, ih - 1), (iv - 1, ih), (iv, ih - 1), (iv, ih)
+            if (iv > 0 && ih > 0 && up.d[c - 1] == 0) grad_edge_lds<NV, W>(up, c - 1, xi, yi, fi, A);
+            if (iv > 0 && ih < g.nh - 1 && up.d[c] == 1) grad_edge_lds<NV, W>(up, c + 1, xi, yi, fi, A);
+            if (iv < g.nv - 1 && ih > 0 && cur.d[c - 1] == 1) grad_edge_lds<NV, W>(dn, c - 1, xi, yi, fi, A);
+            if (iv < g.nv - 1 && ih < g.nh - 1 && cur.d[c] == 0) grad_edge_lds<NV, W>(dn, c + 1, xi, yi, fi, A);
+            const int64_t r = ring_pos(g, iv, ih);
+            if (r >= 0) {
+                double* d = ring_acc + r * (3 + 2 * NV);
+                d[0] = A.q0;
+                d[1] = A.q1;
+                d[2] = A.q3;
+#pragma unroll
+                for (int v = 0; v < NV; ++v) {
+                    d[3 + 2 * v] = A.s0[v];
+                    d[4 + 2 * v] = A.s1[v];
+                }
+            } else {
+#pragma unroll
+                for (int v = 0; v < NV; ++v)
+                    worst = fmax(worst, grad_solve<NV>(A, v, gin, gout, 2 * (v * n + i)));
+            }
+        }
+        __syncthreads();  // the next step overwrites row iv - 1's slot
+    };
+    for (int iv = r0; iv < r1; iv += 2) {
+        step(iv, a, ah);
+        if (iv + 1 < r1) step(iv + 1, b, bh);
+    }
+    change_max_n<W>(worst, chg);
 }
 
 // ring vertices: one wave each adds the pocket chords (lanes stride the chord list, fixed-order
@@ -677,15 +854,36 @@ int akb_gd_grad_sweep_f64(const double* x, const double* y, int nv, int nh, cons
     const int64_t chunks = (n + kGradChunk - 1) / kGradChunk;
     const unsigned gr = (unsigned)(8 * ((chunks + 7) / 8));  // a multiple of 8 for the XCD mapping
     const unsigned grr = grid_for(L * 64);
+    // the LDS strip kernel, AKB_GD_STRIP columns wide (64 / 128 / 256; 0: the gather kernel; read
+    // per call: the tests compare them)
+    const char* se = getenv("AKB_GD_STRIP");
+    int strip = se ? atoi(se) : 128;
+    if (strip != 0 && strip != 64 && strip != 128 && strip != 256) strip = 128;
+    const unsigned gs =
+        strip ? (unsigned)(((nh + strip - 1) / strip) * ((nv + kStripRows - 1) / kStripRows)) : 0u;
     for (int v = 0; v < nvals; v += 2) {
         const double* fv = f + v * n;
         const double* gi = gin + 2 * v * n;
         double* go = gout + 2 * v * n;
         if (nvals - v >= 2) {
-            k_gd_grad<2><<<gr, kBlock, 0, s>>>(g, fv, gi, go, ring_work, chg);
+            if (strip == 64)
+                k_gd_grad_strip<2, 64><<<gs, 64, 0, s>>>(g, fv, gi, go, ring_work, chg);
+            else if (strip == 128)
+                k_gd_grad_strip<2, 128><<<gs, 128, 0, s>>>(g, fv, gi, go, ring_work, chg);
+            else if (strip == 256)
+                k_gd_grad_strip<2, 256><<<gs, 256, 0, s>>>(g, fv, gi, go, ring_work, chg);
+            else
+                k_gd_grad<2><<<gr, kBlock, 0, s>>>(g, fv, gi, go, ring_work, chg);
             k_gd_grad_ring<2><<<grr, kBlock, 0, s>>>(g, fv, gi, go, ring_work, chg);
         } else {
-            k_gd_grad<1><<<gr, kBlock, 0, s>>>(g, fv, gi, go, ring_work, chg);
+            if (strip == 64)
+                k_gd_grad_strip<1, 64><<<gs, 64, 0, s>>>(g, fv, gi, go, ring_work, chg);
+            else if (strip == 128)
+                k_gd_grad_strip<1, 128><<<gs, 128, 0, s>>>(g, fv, gi, go, ring_work, chg);
+            else if (strip == 256)
+                k_gd_grad_strip<1, 256><<<gs, 256, 0, s>>>(g, fv, gi, go, ring_work, chg);
+            else
+                k_gd_grad<1><<<gr, kBlock, 0, s>>>(g, fv, gi, go, ring_work, chg);
             k_gd_grad_ring<1><<<grr, kBlock, 0, s>>>(g, fv, gi, go, ring_work, chg);
         }
         int st = launch_status("k_gd_grad");

@@ -990,6 +990,29 @@ def test_griddata_batched_values_and_errors(gpu):
         CubicGrid(Xf.ravel(), Y.ravel(), 40, 50)
 
 
+@pytest.mark.parametrize("nv,nh,nvals", [(97, 113, 2), (300, 280, 1), (70, 530, 2), (33, 257, 2)])
+def test_gradient_sweep_strip_equals_gather(gpu, monkeypatch, nv, nh, nvals):
+    """The LDS strip sweeps (64, 128 or 256 columns wide) and the global-gather sweep (AKB_GD_STRIP=0) give the same
+    bits: every vertex's edges in the same order, the same arithmetic, the same change measure -
+    over sweeps from zero, random starting gradients and strips / row chunks that do not divide
+    the grid."""
+    from akbraytracing_amd.griddata import CubicGrid
+    X, Y, F = _lattice(nv, nh, nv + nh)
+    X = X * (nh / nv)  # square-ish cells for the wide grids (a triangulable lattice)
+    vals = np.stack([F.ravel(), np.cos(3 * F.ravel())])[:nvals]
+    out = {}
+    for mode in ("64", "128", "256", "0"):
+        monkeypatch.setenv("AKB_GD_STRIP", mode)
+        cg = CubicGrid(X.ravel(), Y.ravel(), nv, nh)
+        g = cg.gradients(vals, maxiter=5, check_every=5)  # five sweeps from zero
+        out[mode] = (g.cpu().numpy(), cg.sweeps)
+        g2 = cg.gradients(vals)  # to convergence
+        out[mode + "c"] = (g2.cpu().numpy(), cg.sweeps)
+    for w in ("64", "128", "256"):
+        assert np.array_equal(out[w][0], out["0"][0]) and out[w][1] == out["0"][1], w
+        assert np.array_equal(out[w + "c"][0], out["0c"][0]) and out[w + "c"][1] == out["0c"][1], w
+
+
 def test_wave_maps_chain_vs_reference(gpu):
     """detcenter2 / Wave2 of the reference's 65x65 ray_wave run -> grid, griddata, nanmean,
     plane correction: the reference's plane_in / plane_out (= psf_calc's input)."""
