@@ -327,8 +327,12 @@ class RayWave:
         # its copy to the host (beside the trace kernels, latency-bound: the next run's resample
         # waits for it), and the finishes (a fused tilt's sums, each run's pass-2 sums and tilt
         # parameters, the flag words' copy to the host), which overlap the next passes
-        self._copy = torch.cuda.Stream(device=self.dev)  # (a high-priority copy stream measured 10 % slower)
         self._fin = torch.cuda.Stream(device=self.dev)
+        # (a high-priority copy stream measured 10 % slower). With several ranks the collectives
+        # run on one more stream of their own (RCCL's): the picks then share the finish stream, so
+        # that the process still fits the box's four hardware queues (the picks are needed only
+        # by the next run's host resample, well after the finish kernels ahead of them)
+        self._copy = torch.cuda.Stream(device=self.dev) if self.comm.world == 1 else self._fin
 
     def _pass2_launch(self, want_rows, slot=0):
         key = (bool(want_rows), slot)
@@ -818,7 +822,8 @@ class RayWave:
         ext = self._ext[self.last.get("slot", 0)]
         if self.comm.world > 1:
             # unsigned key order == signed order after flipping the top bit: MAX over ranks
-            flip = torch.tensor(-(1 << 63), dtype=torch.int64, device=self.dev)
+            # (a Python-int operand: no host-to-device copy of a constant, which would wait for the stream)
+            flip = -(1 << 63)
             ext = self.comm.allreduce_max(torch.bitwise_xor(ext, flip)).bitwise_xor(flip).contiguous()
         _lib.check(L.akb_pupil_sample_f64(D.ptr(self.last["wave2"]), self.shard.start, self.shard.count, self.n,
                                           size, D.ptr(ext), D.ptr(self._opd_buf), D.ptr(self._pitch),
