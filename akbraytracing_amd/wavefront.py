@@ -416,10 +416,10 @@ class RayWave:
         d.flags = D.ptr(self._flagw[slot, 0:1])
         if fuse is None:
             self._p1.launch(stream=stream, reset_flags=False)
+            ev = torch.cuda.Event()
+            ev.record()
         else:
-            self._fused_pass1(fuse, stream, fuse_opd)
-        ev = torch.cuda.Event()
-        ev.record()
+            ev = self._fused_pass1(fuse, stream, fuse_opd)  # one event after the kernel serves both
         self._staged[slot] = ev
 
     def _pass2(self, want_rows=False, stream=None, slot=0):
@@ -653,6 +653,7 @@ class RayWave:
         f.tilt, f.tilted = tb, ev
         if g is not None:
             g.opd, g.opd_ev = opd, ev
+        return ev
 
     def _finish_sink(self, sink, stream):
         """A fused sink's np.sum / np.nanmean sums and counts; across ranks in numpy's own order

@@ -319,7 +319,7 @@ def main():
 
     for _ in range(args.warmup):
         step(False)
-    rw.kernel_events = [] if not os.environ.get("AKB_BENCH_NO_KEVENTS") else None
+    rw.kernel_events = [] if os.environ.get("AKB_BENCH_NO_KEVENTS", "0") == "0" else None
     comm.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
