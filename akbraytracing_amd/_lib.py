@@ -19,7 +19,7 @@ c_int = ctypes.c_int
 c_dbl = ctypes.c_double
 c_vp = ctypes.c_void_p
 MAX_MIRRORS = 7
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 FLAG_MISS = 0x1
 FLAG_ZERO_NORMAL = 0x2
@@ -44,7 +44,7 @@ EXPORTS = [
     "akb_first_valid_rows_f64", "akb_rotate_work_bytes", "akb_rotate_with_nan_f64",
     "akb_moments_work_bytes", "akb_map_moments_f64", "akb_plane_subtract_f64", "akb_legendre_rows_f64",
     "akb_gd_cells_f64", "akb_gd_pockets", "akb_gd_check_pockets", "akb_gd_grad_sweep_f64", "akb_gd_eval_f64",
-    "akb_trace_chain_batch_f64", "akb_focus_eval_work_bytes", "akb_focus_eval_f64",
+    "akb_trace_chain_batch_f64", "akb_focus_eval_work_bytes", "akb_focus_eval_f64", "akb_sep_search_f64",
     "akb_finish_params_work_bytes", "akb_finish_tilt_params_f64",
     "akb_valid_mask_u8", "akb_external_contours", "akb_approx_poly_dp", "akb_affine_from_points",
     "akb_affine_invert", "akb_warp_affine_f64",
@@ -119,6 +119,8 @@ def _declare(L):
         "akb_trace_chain_batch_f64": ([ctypes.POINTER(ChainDesc), c_int, c_vp], c_int),
         "akb_focus_eval_work_bytes": ([c_int, c_int, c_i64], c_i64),
         "akb_focus_eval_f64": ([c_vp, c_vp, c_i64, c_i64, c_int, c_int] + [c_vp] * 7, c_int),
+        "akb_sep_search_f64": ([c_vp, c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_dbl, c_dbl, c_int, c_int,
+                                c_dbl, c_dbl, c_vp, c_vp], c_int),
         "akb_chain_tilt_f64": ([ctypes.POINTER(ChainDesc), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64]
                                + [c_vp] * 6 + [ctypes.POINTER(LeafSink), c_vp], c_int),
         "akb_chain_tilt_opd_f64": ([ctypes.POINTER(ChainDesc), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,

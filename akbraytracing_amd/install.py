@@ -19,9 +19,9 @@ The driver's steps after the trace are rebound too: gridda
 psf_calc (reading the module's live option_energy / option_AKB / directory_name as the reference
 does, :1161-1166, :1202-1214, :1271-1273), find_defocus and calc_dS. plot_result_debug's 'test'
 mode and auto_focus_NA (:12746) run the batched device search (autofocus.py) for the live Wolter
-III+I AKB system; the reference's auto_focus_sep, calc_FoC and alignment loops reach them through
-the module globals. install(mod, names=[...]) picks a subset; uninstall(mod) restores every
-original.
+III+I AKB system, its 'sep' mode and compare_sep (:9267) the one-launch plane searches (sep.py);
+the reference's auto_focus_sep, calc_FoC and alignment loops reach them through the module globals.
+install(mod, names=[...]) picks a subset; uninstall(mod) restores every original.
 
 The wrappers read the module's live `option_mpmath` flag (AKB_raytrace_20250312.py:92) at call
 time and hand the call to the original function when it is set (the mpmath branch, :399-443).
@@ -57,13 +57,17 @@ def _akb_native_ok(mod):
 
 def _plot_result_debug_for(mod, original):
     """plot_result_debug with its 'test' mode (the one auto_focus_NA and the alignment loops call
-    hundreds of times) on the device; every other mode runs the reference's own function, whose
-    primitives install() has rebound."""
+    hundreds of times), its 'sep' mode (auto_focus_sep's, sep.py) and its 'wave' mode on the device;
+    every other mode runs the reference's own function, whose primitives install() has rebound."""
     def plot_result_debug(params, option, source_shift=[0., 0., 0.], option_tilt=True, option_legendre=False,
                           angular_shift=[0., 0.], option_save=True):
         if option == "test" and _akb_native_ok(mod) and list(angular_shift) == [0., 0.]:
             from .autofocus import plot_result_test
             return plot_result_test(params, source_shift, option_tilt, option_set=bool(getattr(mod, "option_set", False)))
+        if option == "sep" and _akb_native_ok(mod) and list(angular_shift) == [0., 0.]:
+            from .sep import plot_result_sep
+            return plot_result_sep(params, source_shift, option_tilt, option_set=bool(getattr(mod, "option_set", False)),
+                                   widesearch=bool(getattr(mod, "widesearch", False)))
         if (option == "wave" and _akb_native_ok(mod) and list(angular_shift) == [0., 0.]
                 and getattr(mod, "option_rotate", True) and getattr(mod, "wave_num_H", 0) == getattr(mod, "wave_num_V", 1)):
             from .wavedata import plot_result_wave
@@ -92,6 +96,15 @@ def _auto_focus_for(mod, original):
     return auto_focus_NA
 
 
+def _compare_sep_for(mod, original):
+    """compare_sep (:9267) with its twenty plane searches in one device launch (sep.py), reading the
+    module's live widesearch flag (:98) as the reference does."""
+    def compare_sep(rays, points, coeffs_det0, ray_num, region):
+        from .sep import compare_sep as native
+        return native(rays, points, coeffs_det0, ray_num, region, widesearch=bool(getattr(mod, "widesearch", False)))
+    return compare_sep
+
+
 def _save_wave_for(mod, original):
     """saveWaveData (:13475) with the 'wave' trace, calc_dS and the grids on the device, reading
     the module's flags (wave_num_H / V, defocusForWave, downsample_*, option_HighNA, option_2mirror,
@@ -114,7 +127,7 @@ def _save_wave_for(mod, original):
 
 
 _PER_MODULE = {"plot_result_debug": _plot_result_debug_for, "auto_focus_NA": _auto_focus_for,
-               "saveWaveData": _save_wave_for}
+               "saveWaveData": _save_wave_for, "compare_sep": _compare_sep_for}
 
 _NATIVE = {
     "mirr_ray_intersection": _P.mirr_ray_intersection,
@@ -137,6 +150,7 @@ _NATIVE = {
     "plot_result_debug": None,  # bound per module (_PER_MODULE)
     "auto_focus_NA": None,
     "saveWaveData": None,
+    "compare_sep": None,
 }
 # functions with an mpmath branch in the reference
 _MPMATH_AWARE = {"mirr_ray_intersection", "reflect_ray"}

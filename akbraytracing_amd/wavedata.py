@@ -209,6 +209,47 @@ def run_wave_chain(folder, out_dir=None, files=("points_source.npy", "points_M1.
     return fields
 
 
+def two_pass_trace(b, n, mode="wave"):
+    """The two-pass trace every resampled mode of plot_result_debug shares ('sep', 'wave', 'ray',
+    'ray_wave': :2694-2845 pass 1, :2849-2879 the equal-angle resample, :2881-2905 pass 2) for the
+    built system b on an n x n grid: pass 1 traces only the resample's picks' exit slopes (the
+    full pass 1 is still traced for its flags), the host resamples with numpy's arctan / tan and
+    the C interp1d, pass 2 keeps every mirror's hits, the exit directions and the detector hits on
+    coeffs_det = (g = 1, j = -(s2f_middle + defocus)). Returns device tensors (hits (4, 3, n^2),
+    exit directions, detcenter). A flagged pass 2 takes the drop-in primitives stage by stage,
+    which apply the reference's all-NaN / passthrough rules."""
+    from . import geometry as G
+    from . import primitives as P
+    from .trace import grid_dirs, staged_chain, trace_chain
+    from .wavefront import AngleRange, resample, sample_plan
+    dev = D.device()
+    mir = G.mirrors_of(b)
+    rand_h = AngleRange(**b["angle_h"]).table(n)
+    rand_v = AngleRange(**b["angle_v"]).table(n)
+    th = torch.from_numpy(np.tan(rand_h)).to(dev)
+    tv = torch.from_numpy(np.tan(rand_v)).to(dev)
+    hb, he, col = sample_plan(n)
+    r1 = trace_chain(mir, tan_h=th, tan_v=tv, src=b["source"], want=(), samples=(hb, he, col))
+    f1 = int(r1.flags.item())
+    if f1:
+        raise _lib.AKBError(f"pass 1 of the '{mode}' trace flagged 0x{f1:x} (a miss or zero norm: the reference's "
+                            "all-NaN rays cannot be resampled)")
+    s = r1.extra["samples"].cpu().numpy()
+    rand_h2, rand_v2 = resample(np.arctan(s[:he - hb]), np.arctan(s[he - hb:]), rand_h, rand_v)
+    th2 = torch.from_numpy(np.tan(rand_h2)).to(dev)
+    tv2 = torch.from_numpy(np.tan(rand_v2)).to(dev)
+    det1 = b["det1"][6:10]
+    r2 = trace_chain(mir, tan_h=th2, tan_v=tv2, src=b["source"], want=("hits", "dir_out", "det"), det_ghij=det1)
+    N = n * n
+    if int(r2.flags.item()):
+        src = torch.tensor(b["source"], dtype=D.F64, device=dev).reshape(3, 1).expand(3, N).contiguous()
+        hits, refl, _ = staged_chain(mir, grid_dirs(th2, tv2), src)
+        hits = torch.stack(hits)
+        det = P.plane_ray_intersection(b["det1"], refl, hits[-1])
+        return hits, refl, det
+    return r2.hits, r2.dir_out, r2.det
+
+
 def plot_result_wave(params, ray_num, *, defocus_for_wave=1e-3, option_set=True, source_shift=(0.0, 0.0, 0.0),
                      as_torch=False):
     """plot_result_debug(params, 'wave') (AKB_raytrace_20250312.py:2675-2905, :3510-3561) on the
@@ -223,38 +264,12 @@ def plot_result_wave(params, ray_num, *, defocus_for_wave=1e-3, option_set=True,
     from . import geometry as G
     from . import primitives as P
     from .reduce import means_to_host, np_sum
-    from .trace import grid_dirs, staged_chain, trace_chain
-    from .wavefront import AngleRange, resample, sample_plan
     b = G.build_akb(params, source_shift=source_shift, option_set=option_set)
     if not isinstance(b, dict):
         return b
     n = int(ray_num)
     dev = D.device()
-    mir = G.mirrors_of(b)
-    rand_h = AngleRange(**b["angle_h"]).table(n)
-    rand_v = AngleRange(**b["angle_v"]).table(n)
-    th = torch.from_numpy(np.tan(rand_h)).to(dev)
-    tv = torch.from_numpy(np.tan(rand_v)).to(dev)
-    hb, he, col = sample_plan(n)
-    r1 = trace_chain(mir, tan_h=th, tan_v=tv, src=b["source"], want=(), samples=(hb, he, col))
-    f1 = int(r1.flags.item())
-    if f1:
-        raise _lib.AKBError(f"pass 1 of the 'wave' trace flagged 0x{f1:x} (a miss or zero norm: the reference's "
-                            "all-NaN rays cannot be resampled)")
-    s = r1.extra["samples"].cpu().numpy()
-    rand_h2, rand_v2 = resample(np.arctan(s[:he - hb]), np.arctan(s[he - hb:]), rand_h, rand_v)
-    th2 = torch.from_numpy(np.tan(rand_h2)).to(dev)
-    tv2 = torch.from_numpy(np.tan(rand_v2)).to(dev)
-    det1 = b["det1"][6:10]
-    r2 = trace_chain(mir, tan_h=th2, tan_v=tv2, src=b["source"], want=("hits", "dir_out", "det"), det_ghij=det1)
-    N = n * n
-    if int(r2.flags.item()):
-        src = torch.tensor(b["source"], dtype=D.F64, device=dev).reshape(3, 1).expand(3, N).contiguous()
-        hits, refl, _ = staged_chain(mir, grid_dirs(th2, tv2), src)
-        hits = torch.stack(hits)
-        det = P.plane_ray_intersection(b["det1"], refl, hits[-1])
-    else:
-        hits, refl, det = r2.hits, r2.dir_out, r2.det
+    hits, refl, det = two_pass_trace(b, n, "wave")
     # theta from the exit slopes (:3516-3517), numpy on the host as the reference
     ang = refl.cpu().numpy()
     theta_y = -np.mean(np.arctan(ang[2, :] / ang[0, :]))

@@ -32,6 +32,8 @@
  *   akb_trace_chain_batch_f64 + akb_focus_eval_f64
  *                        plot_result_debug(params, 'test') / auto_focus_NA's sweeps
  *                        AKB_raytrace_20250312.py:2770-2847, :3565-3601, :12746-12895
+ *   akb_sep_search_f64   compare_sep / optimize_min_index of plot_result_debug(params, 'sep') and
+ *                        auto_focus_sep, AKB_raytrace_20250312.py:9174-9560, :3604-3606, :12897-13318
  */
 #ifndef AKB_RAYTRACE_H
 #define AKB_RAYTRACE_H
@@ -42,7 +44,7 @@
 extern "C" {
 #endif
 
-#define AKB_ABI_VERSION 10
+#define AKB_ABI_VERSION 11
 
 /* status codes */
 #define AKB_OK 0
@@ -280,6 +282,19 @@ int64_t akb_focus_eval_work_bytes(int n_sys, int n_planes, int64_t n);
 int akb_focus_eval_f64(const double* dir, const double* pt, int64_t n, int64_t sys_ld, int n_sys, int n_planes,
                        const double* d_plane_j, const double* d_rot, double* d_std, double* det_out, double* dir_out,
                        void* work, void* stream);
+
+/* compare_sep's plane searches (ref AKB_raytrace_20250312.py:9267-9560; optimize_min_index :9174-9217,
+ * create_func_to_minimize / create_evaluation_fn :9219-9265), all in one launch. Search q minimises
+ * sqrt(np.std(z)^2 + np.std(y)^2) of the hits of rays start[q] + i * step[q] (i < count[q], host arrays)
+ * of (dir, pt) ((3, ld) each, n rays) on the plane x = -a (coeffs_det[9] = a): num_steps points of
+ * np.linspace(x_min, x_max), first argmin (NaN first, as np.argmin), range * shrink about it, until
+ * tol > width > 1e-16 or max_attempts steps. d_out (device, (n_search, 4)): best_x, min_y, the last
+ * x evaluated (compare_sep leaves it in coeffs_det[9]) and the final width. n_search <= 32,
+ * num_steps <= 128. */
+int akb_sep_search_f64(const double* dir, const double* pt, int64_t ld, int64_t n, int n_search,
+                       const int64_t* h_start, const int64_t* h_step, const int64_t* h_count, double x_min,
+                       double x_max, int num_steps, int max_attempts, double shrink, double tol, double* d_out,
+                       void* stream);
 
 /* Focus sweep rows (find_defocus, ref :9086-9170): for P detector planes x = -d_plane_j[p]
  * (coefficients g = 1, h = i = 0, j = d_plane_j[p], as coeffs_det[9] = -(s2f_middle + a)), the
