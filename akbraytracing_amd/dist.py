@@ -149,3 +149,36 @@ def propagate_sharded(tx, ty, tz, sx, sy, sz, u_ds, k, comm):
     hi = lo + counts[comm.rank]
     piece = propagate(tx[lo:hi].contiguous(), ty[lo:hi].contiguous(), tz[lo:hi].contiguous(), sx, sy, sz, u_ds, k)
     return comm.allgather_field(piece, counts)
+
+
+def wavelength_shard(wavelengths, world, rank):
+    """SURVEY.md §8(e) PSF stack sharding: rank r transforms wavelengths[r::world] - one wavelength
+    per GPU for config 5's three at N >= 3, everything on rank 0 at N = 1, nothing on ranks beyond
+    the stack. Every rank holds the whole pupil (RayWave.pupil all-reduces it)."""
+    return list(wavelengths)[rank::world]
+
+
+def psf_stack_sharded(opd, wavelengths, comm, gather=False, **kw):
+    """psf_stack over this rank's wavelength_shard. Returns (psf (B_r, py, px) or None, the
+    wavelengths it holds); gather=True all-gathers the whole (B, py, px) stack in wavelength order
+    on every rank instead (B * py * px * 8 bytes over the links: an on-demand step, not per trace)."""
+    from .psf import psf_stack
+    lams = list(wavelengths)
+    mine = wavelength_shard(lams, comm.world, comm.rank)
+    psf = psf_stack(opd, None, mine, None, **kw)[0] if mine else None
+    if not gather or comm.world == 1:
+        return psf, mine
+    ny, nx = int(opd.shape[0]), int(opd.shape[1])
+    pad = int(kw.get("pad_factor", 2))
+    plane = ((ny + ny % 2) * pad) * ((nx + nx % 2) * pad)
+    counts = [len(wavelength_shard(lams, comm.world, r)) * plane for r in range(comm.world)]
+    piece = psf.reshape(-1) if psf is not None else torch.zeros(0, dtype=torch.float64, device=opd.device)
+    flat = comm.allgather_field(piece, counts)
+    py, px = (ny + ny % 2) * pad, (nx + nx % 2) * pad
+    out = torch.empty((len(lams), py, px), dtype=torch.float64, device=opd.device)
+    off = 0
+    for r in range(comm.world):
+        for j, _ in enumerate(wavelength_shard(lams, comm.world, r)):
+            out[r + j * comm.world] = flat[off:off + plane].reshape(py, px)
+            off += plane
+    return out, lams

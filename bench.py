@@ -255,10 +255,13 @@ def main():
     state = {"psf_done": None}
     fronts = []  # launched fronts (pass 1 .. tilt parameters) whose back half is still to queue
 
+    # the PSF stack is wavelength-sharded: rank r transforms lams[r::world]
+    my_lams = AD.wavelength_shard(lams, world, rank)
+
     def run_psf(opd, pitch, ready, timed):
         """The PSF of a finished pupil on the back stream, right behind it: it shares the GPU with
         the next kernels of the main stream."""
-        if rank != 0:
+        if not my_lams:
             return
         side = back_stream
         side.wait_event(ready)
@@ -270,7 +273,7 @@ def main():
             if timed:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(side)
-            psf, _, _ = psf_stack(opd, None, lams, None, pitch=pitch, pad_factor=args.pad,
+            psf, _, _ = psf_stack(opd, None, my_lams, None, pitch=pitch, pad_factor=args.pad,
                                   out=psf_out.get("psf"))
             psf_out["psf"] = psf
             if timed:
@@ -340,7 +343,7 @@ def main():
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
         for _ in range(10):
-            psf_stack(opd, None, lams, None, pitch=pitch, pad_factor=args.pad, out=psf_out.get("psf"))
+            psf_stack(opd, None, my_lams, None, pitch=pitch, pad_factor=args.pad, out=psf_out.get("psf"))
         b.record()
         b.synchronize()
         psf_alone_ms = a.elapsed_time(b) / 10
@@ -404,14 +407,15 @@ def main():
             "mirrors": len(geom.mirrors), "systems_cycled": len(systems),
             "intersections_per_step": 2 * len(geom.mirrors) * n * n,
             "psf": f"{args.pupil}^2 pupil x pad {args.pad} -> {len(lams)} x {args.pupil * args.pad}^2 complex128 "
-                   "DFT (pruned)",
+                   "DFT (pruned)" + (f", wavelength-sharded over {min(world, len(lams))} ranks" if world > 1 and
+                                     len(lams) > 1 else ""),
             "parallelism": f"ray-row shards x{world}",
         },
         "host_issue_ms_per_step": sorted(host_ms)[len(host_ms) // 2],
         "psf_ms": psf_ms,
         "psf_alone_ms": psf_alone_ms,
         # the PSF's compulsory HBM traffic is its output (the pupil is 128 KB): intensity planes
-        "psf_alone_output_gbs": (len(lams) * (args.pupil * args.pad) ** 2 * 8 / (psf_alone_ms * 1e-3) / 1e9
+        "psf_alone_output_gbs": (len(my_lams) * (args.pupil * args.pad) ** 2 * 8 / (psf_alone_ms * 1e-3) / 1e9
                                  if psf_alone_ms else None),
         "pass2_kernel_ms": k_avg,
         # the contract's HBM roofline for the dominant kernel (pass 2, k_chain_sink with its fixed

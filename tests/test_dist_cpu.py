@@ -92,3 +92,45 @@ def test_two_rank_shards_reassemble_single_process(tmp_path, n):
     # OR over ranks, not a sum: 0x1 | 0x9 = 0x9 (a sum would give 0xa, FLAG_ZERO_NORMAL | ...)
     assert int(r["flags"]) == 0x9
     assert r["words"].tolist() == [1, 1 << 30, -(1 << 31) | 5]
+
+
+def _psf_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import akbraytracing_amd.psf as PSF
+        from akbraytracing_amd.dist import TorchComm, psf_stack_sharded
+
+        def fake_stack(opd, amp, lams, dx, pad_factor=2, **kw):
+            # a stand-in transform (the kernel is a gpu test): plane b = opd tiled, times its wavelength
+            t = opd.repeat(pad_factor, pad_factor)
+            return torch.stack([t * lam for lam in lams]), None, None
+        PSF.psf_stack = fake_stack
+        opd = torch.arange(16, dtype=torch.float64).reshape(4, 4)
+        lams = [13.5e-9, 1.35e-9, 1.35e-10]
+        comm = TorchComm(torch.device("cpu"))
+        mine_psf, mine = psf_stack_sharded(opd, lams, comm, pad_factor=2)
+        full, order = psf_stack_sharded(opd, lams, comm, gather=True, pad_factor=2)
+        np.savez(os.path.join(out_dir, f"psf{rank}.npz"), mine=np.array(mine),
+                 mine_psf=mine_psf.numpy() if mine_psf is not None else np.zeros(0), full=full.numpy(),
+                 order=np.array(order))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_wavelength_sharded_psf_stack(tmp_path, world):
+    """SURVEY.md §8(e): the config-5 PSF stack, one wavelength per rank (lams[rank::world]); each
+    wavelength transformed exactly once, and the gathered stack in wavelength order on every rank"""
+    from akbraytracing_amd.dist import wavelength_shard
+    lams = [13.5e-9, 1.35e-9, 1.35e-10]
+    owned = sum((wavelength_shard(lams, world, r) for r in range(world)), [])
+    assert sorted(owned) == sorted(lams) and wavelength_shard(lams, 1, 0) == lams
+    mp.start_processes(_psf_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    want = np.stack([np.tile(np.arange(16.0).reshape(4, 4), (2, 2)) * lam for lam in lams])
+    for r in range(world):
+        d = np.load(os.path.join(tmp_path, f"psf{r}.npz"))
+        assert d["mine"].tolist() == lams[r::world]
+        assert np.array_equal(d["mine_psf"].reshape(-1), want[r::world].reshape(-1))
+        assert np.array_equal(d["full"], want) and d["order"].tolist() == lams
