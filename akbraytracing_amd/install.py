@@ -19,8 +19,10 @@ The driver's steps after the trace are rebound too: gridda
 psf_calc (reading the module's live option_energy / option_AKB / directory_name as the reference
 does, :1161-1166, :1202-1214, :1271-1273), find_defocus and calc_dS. plot_result_debug's 'test'
 mode and auto_focus_NA (:12746) run the batched device search (autofocus.py) for the live Wolter
-III+I AKB system, its 'sep' mode and compare_sep (:9267) the one-launch plane searches (sep.py);
-the reference's auto_focus_sep, calc_FoC and alignment loops reach them through the module globals.
+III+I AKB system, its 'sep' mode and compare_sep (:9267) the one-launch plane searches (sep.py),
+and its 'ray_wave' mode with option_legendre (the alignment loops' call) the whole chain from
+params to the Legendre fit (driver.py); the reference's auto_focus_sep, calc_FoC and alignment
+loops reach them through the module globals.
 install(mod, names=[...]) picks a subset; uninstall(mod) restores every original.
 
 The wrappers read the module's live `option_mpmath` flag (AKB_raytrace_20250312.py:92) at call
@@ -57,7 +59,8 @@ def _akb_native_ok(mod):
 
 def _plot_result_debug_for(mod, original):
     """plot_result_debug with its 'test' mode (the one auto_focus_NA and the alignment loops call
-    hundreds of times), its 'sep' mode (auto_focus_sep's, sep.py) and its 'wave' mode on the device;
+    hundreds of times), its 'sep' mode (auto_focus_sep's, sep.py), its 'wave' mode and its 'ray_wave'
+    mode with option_legendre (the alignment loops', driver.py) on the device;
     every other mode runs the reference's own function, whose primitives install() has rebound."""
     def plot_result_debug(params, option, source_shift=[0., 0., 0.], option_tilt=True, option_legendre=False,
                           angular_shift=[0., 0.], option_save=True):
@@ -68,6 +71,16 @@ def _plot_result_debug_for(mod, original):
             from .sep import plot_result_sep
             return plot_result_sep(params, source_shift, option_tilt, option_set=bool(getattr(mod, "option_set", False)),
                                    widesearch=bool(getattr(mod, "widesearch", False)))
+        if (option == "ray_wave" and option_legendre and option_save and option_tilt and _akb_native_ok(mod)
+                and list(angular_shift) == [0., 0.] and getattr(mod, "wave_num_H", 0) == getattr(mod, "wave_num_V", 1)):
+            # the alignment loops' call: the whole chain on the device (driver.py); the plotting
+            # run (option_legendre=False) stays the reference's
+            from .driver import plot_result_ray_wave
+            return plot_result_ray_wave(params, mod.wave_num_H, source_shift=source_shift,
+                                        option_set=bool(getattr(mod, "option_set", False)),
+                                        option_HighNA=getattr(mod, "option_HighNA", True),
+                                        option_energy=getattr(mod, "option_energy", "EUV"), option_AKB=True,
+                                        directory=getattr(mod, "directory_name", None))
         if (option == "wave" and _akb_native_ok(mod) and list(angular_shift) == [0., 0.]
                 and getattr(mod, "option_rotate", True) and getattr(mod, "wave_num_H", 0) == getattr(mod, "wave_num_V", 1)):
             from .wavedata import plot_result_wave
