@@ -482,7 +482,12 @@ __device__ __forceinline__ void grad_edge_lds(const StripRow<NV, W>& r, int c, d
     }
 }
 
-template <int NV, int W>
+// kGS: a line Gauss-Seidel sweep instead of Jacobi - once row iv is solved, its new gradients
+// replace the old ones in the LDS ring, so row iv + 1 sees its upper neighbours' new values (the
+// way scipy's Gauss-Seidel sweep sees its earlier vertices'); left / right neighbours, the rows
+// outside the chunk, the halo columns and the ring vertices keep the old values. Same local solve,
+// same fixed point, ~1/3 fewer sweeps; deterministic (no value depends on workgroup timing).
+template <int NV, int W, bool kGS = false>
 __global__ void __launch_bounds__(W) k_gd_grad_strip(Grid g, const double* __restrict__ f,
                                                      const double* __restrict__ gin, double* __restrict__ gout,
                                                      double* __restrict__ ring_acc, unsigned long long* chg) {
@@ -521,6 +526,8 @@ __global__ void __launch_bounds__(W) k_gd_grad_strip(Grid g, const double* __res
     }
     if (r0 + 1 < g.nv) load_row(r0 + 1, a, ah);
     if (r0 + 2 < g.nv && r0 + 2 <= r1) load_row(r0 + 2, b, bh);
+    double ngx[NV], ngy[NV];
+    bool solved = false;
     auto step = [&](int iv, StripVals<NV>& nx, StripVals<NV>& nh_) {
         if (iv + 1 < g.nv) store_row(iv + 1, nx, nh_);  // row iv + 1: registers -> LDS
         __syncthreads();
@@ -558,11 +565,27 @@ __global__ void __launch_bounds__(W) k_gd_grad_strip(Grid g, const double* __res
                 }
             } else {
 #pragma unroll
-                for (int v = 0; v < NV; ++v)
-                    worst = fmax(worst, grad_solve<NV>(A, v, gin, gout, 2 * (v * n + i)));
+                for (int v = 0; v < NV; ++v) {
+                    const int64_t o = 2 * (v * n + i);
+                    worst = fmax(worst, grad_solve<NV>(A, v, gin, gout, o));
+                    if (kGS) {
+                        ngx[v] = gout[o];
+                        ngy[v] = gout[o + 1];
+                    }
+                }
+                solved = kGS;
             }
         }
         __syncthreads();  // the next step overwrites row iv - 1's slot
+        if (kGS && solved) {  // row iv's new gradients, for row iv + 1 (read after the next sync)
+            StripRow<NV, W>& cur = R[iv % 3];
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                cur.gx[v][t + 1] = ngx[v];
+                cur.gy[v][t + 1] = ngy[v];
+            }
+            solved = false;
+        }
     };
     for (int iv = r0; iv < r1; iv += 2) {
         step(iv, a, ah);
@@ -859,6 +882,9 @@ int akb_gd_grad_sweep_f64(const double* x, const double* y, int nv, int nh, cons
     const char* se = getenv("AKB_GD_STRIP");
     int strip = se ? atoi(se) : 128;
     if (strip != 0 && strip != 64 && strip != 128 && strip != 256) strip = 128;
+    // the strip sweeps as line Gauss-Seidel (AKB_GD_GS=0: Jacobi, the gather kernel's bits)
+    const char* ge = getenv("AKB_GD_GS");
+    const bool gs_sweep = !(ge && ge[0] == '0');
     const unsigned gs =
         strip ? (unsigned)(((nh + strip - 1) / strip) * ((nv + kStripRows - 1) / kStripRows)) : 0u;
     for (int v = 0; v < nvals; v += 2) {
@@ -867,21 +893,27 @@ int akb_gd_grad_sweep_f64(const double* x, const double* y, int nv, int nh, cons
         double* go = gout + 2 * v * n;
         if (nvals - v >= 2) {
             if (strip == 64)
-                k_gd_grad_strip<2, 64><<<gs, 64, 0, s>>>(g, fv, gi, go, ring_work, chg);
+                gs_sweep ? k_gd_grad_strip<2, 64, true><<<gs, 64, 0, s>>>(g, fv, gi, go, ring_work, chg)
+                         : k_gd_grad_strip<2, 64><<<gs, 64, 0, s>>>(g, fv, gi, go, ring_work, chg);
             else if (strip == 128)
-                k_gd_grad_strip<2, 128><<<gs, 128, 0, s>>>(g, fv, gi, go, ring_work, chg);
+                gs_sweep ? k_gd_grad_strip<2, 128, true><<<gs, 128, 0, s>>>(g, fv, gi, go, ring_work, chg)
+                         : k_gd_grad_strip<2, 128><<<gs, 128, 0, s>>>(g, fv, gi, go, ring_work, chg);
             else if (strip == 256)
-                k_gd_grad_strip<2, 256><<<gs, 256, 0, s>>>(g, fv, gi, go, ring_work, chg);
+                gs_sweep ? k_gd_grad_strip<2, 256, true><<<gs, 256, 0, s>>>(g, fv, gi, go, ring_work, chg)
+                         : k_gd_grad_strip<2, 256><<<gs, 256, 0, s>>>(g, fv, gi, go, ring_work, chg);
             else
                 k_gd_grad<2><<<gr, kBlock, 0, s>>>(g, fv, gi, go, ring_work, chg);
             k_gd_grad_ring<2><<<grr, kBlock, 0, s>>>(g, fv, gi, go, ring_work, chg);
         } else {
             if (strip == 64)
-                k_gd_grad_strip<1, 64><<<gs, 64, 0, s>>>(g, fv, gi, go, ring_work, chg);
+                gs_sweep ? k_gd_grad_strip<1, 64, true><<<gs, 64, 0, s>>>(g, fv, gi, go, ring_work, chg)
+                         : k_gd_grad_strip<1, 64><<<gs, 64, 0, s>>>(g, fv, gi, go, ring_work, chg);
             else if (strip == 128)
-                k_gd_grad_strip<1, 128><<<gs, 128, 0, s>>>(g, fv, gi, go, ring_work, chg);
+                gs_sweep ? k_gd_grad_strip<1, 128, true><<<gs, 128, 0, s>>>(g, fv, gi, go, ring_work, chg)
+                         : k_gd_grad_strip<1, 128><<<gs, 128, 0, s>>>(g, fv, gi, go, ring_work, chg);
             else if (strip == 256)
-                k_gd_grad_strip<1, 256><<<gs, 256, 0, s>>>(g, fv, gi, go, ring_work, chg);
+                gs_sweep ? k_gd_grad_strip<1, 256, true><<<gs, 256, 0, s>>>(g, fv, gi, go, ring_work, chg)
+                         : k_gd_grad_strip<1, 256><<<gs, 256, 0, s>>>(g, fv, gi, go, ring_work, chg);
             else
                 k_gd_grad<1><<<gr, kBlock, 0, s>>>(g, fv, gi, go, ring_work, chg);
             k_gd_grad_ring<1><<<grr, kBlock, 0, s>>>(g, fv, gi, go, ring_work, chg);

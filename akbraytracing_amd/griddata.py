@@ -9,10 +9,11 @@ scipy answers with a Clough-Tocher interpolant on the points' Delaunay triangula
 are the ray grid's hits, a smoothly deformed n_v x n_h lattice, so CubicGrid builds that
 triangulation structurally (akb_griddata.hip: cell diagonals by the in-circle test, the hull
 pockets on the host, local-Delaunay checks that refuse a grid where this would not be qhull's
-answer), estimates the vertex gradients by Jacobi sweeps of scipy's own local solve until they
-stop changing, and evaluates the patches on the device. Agreement with scipy is to rounding on
-the reference's 65 x 65 run (tests/test_gpu_parity.py), not bit for bit: qhull's co-circular
-tie-breaks and scipy's Gauss-Seidel stopping point are not reproduced.
+answer), estimates the vertex gradients by sweeps of scipy's own local solve until they stop
+changing (line Gauss-Seidel in LDS strips: each row sees its upper neighbours' new values), and
+evaluates the patches on the device. Agreement with scipy is to rounding on the reference's
+65 x 65 run (tests/test_gpu_parity.py), not bit for bit: qhull's co-circular tie-breaks and
+scipy's Gauss-Seidel stopping point (1e-6; these sweeps run to 1e-10) are not reproduced.
 """
 import numpy as np
 import torch
@@ -85,8 +86,10 @@ class CubicGrid:
         return (D.ptr(self.x), D.ptr(self.y), self.nv, self.nh, D.ptr(self.diag), self.npock, D.ptr(self.ptri),
                 D.ptr(self.pnbr), D.ptr(self.edge_tri))
 
-    def gradients(self, values, tol=1e-10, maxiter=400, check_every=8):
-        """estimate_gradients_2d_global for (nvals, n) values: (nvals, n, 2) device tensor."""
+    def gradients(self, values, tol=1e-10, maxiter=400, check_every=8, adaptive=True):
+        """estimate_gradients_2d_global for (nvals, n) values: (nvals, n, 2) device tensor. The sweeps
+        stop after the first batch holding one whose largest relative change is below tol; with
+        adaptive, batches after the first are sized from the observed decay rate."""
         L = _lib.lib()
         f = _dev(values, self.dev)
         f = f.reshape(-1, self.nv * self.nh).contiguous()
@@ -95,9 +98,10 @@ class CubicGrid:
         change = torch.zeros(maxiter, dtype=torch.int64, device=self.dev)
         ring = torch.empty(10 * self.L, dtype=D.F64, device=self.dev)
         s = D.stream_handle()
-        cur, it = 0, 0
+        cur, it, batch = 0, 0, check_every
+        hist = []
         while it < maxiter:
-            stop = min(it + check_every, maxiter)
+            stop = min(it + batch, maxiter)
             for k in range(it, stop):
                 _lib.check(L.akb_gd_grad_sweep_f64(*self._tri_args(), D.ptr(self.xptr), D.ptr(self.xidx), D.ptr(f),
                                                    nvals, D.ptr(g[cur]), D.ptr(g[1 - cur]), D.ptr(ring),
@@ -108,6 +112,14 @@ class CubicGrid:
             it = stop
             if done.size:
                 break
+            # the change decays geometrically: queue about as many sweeps as the observed rate says
+            # remain (the host checks once per batch; a batch overshoots by at most one sweep then)
+            hist.extend(ch.tolist())
+            batch = check_every
+            if adaptive and len(hist) >= 4 and hist[-1] > 0 and hist[-4] > hist[-1]:
+                rate = (hist[-1] / hist[-4]) ** (1.0 / 3.0)
+                need = int(np.ceil(np.log(tol / hist[-1]) / np.log(rate)))
+                batch = int(min(max(need, 1), check_every))
         self.sweeps = it
         return g[cur]
 
