@@ -183,7 +183,8 @@ def lib():
     """The loaded library. Raises (never falls back) when it is missing or cannot load."""
     global _LIB
     if _LIB is None:
-        path = _build.SO
+        # AKB_LIB: another build of the same ABI (A/B timing of kernel variants); default the in-tree one
+        path = os.environ.get("AKB_LIB") or _build.SO
         if not os.path.exists(path):
             raise AKBError(
                 f"{path} is missing: build the HIP extension first (python -m akbraytracing_amd.build "

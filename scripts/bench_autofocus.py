@@ -4,7 +4,8 @@
 
 auto_focus_NA from the reference's best-alignment params (1800 'test' traces in the reference,
 ~17.5 s in the build container), its pieces (system build, one trace, one 100-plane sweep), a
-batched trace of 256 systems, and calc_FoC on a 5 x 5 source grid (25 FoC searches).
+batched trace of 256 systems, calc_FoC on a 5 x 5 source grid (25 FoC searches), the 'sep'
+mode and auto_focus_sep ('abrr' and 'matrix').
 """
 import argparse
 import json
@@ -81,6 +82,19 @@ def main():
     res["auto_focus_NA_reference_s"] = 17.46  # the reference, same call, build container (1 core)
     t, out = wall(lambda: AF.calc_FoC(p0.copy(), range_h=[-5e-3, 5e-3, 5], range_v=[-5e-3, 5e-3, 5]))
     res["calc_FoC_5x5_ms"] = t * 1e3
+    # the 'sep' analysis (two-pass 53^2 trace, tilt, compare_sep's twenty searches in one launch)
+    # and auto_focus_sep; the reference, same calls, build container (1 core): 2.0-2.3 s and 13.9 s
+    from akbraytracing_amd import sep as S
+    S.plot_result_sep(p0.copy(), verbose=False)
+    t, _ = wall(lambda: S.plot_result_sep(p0.copy(), verbose=False), reps=5)
+    res["sep_mode_ms"] = t * 1e3
+    res["sep_mode_reference_s"] = 2.1
+    t, _ = wall(lambda: S.auto_focus_sep(p0.copy(), 9, 21, -2e-5, 2e-5, option="abrr", verbose=False), reps=3)
+    res["auto_focus_sep_abrr_ms"] = t * 1e3
+    res["auto_focus_sep_abrr_reference_s"] = 13.9
+    t, _ = wall(lambda: S.auto_focus_sep(p0.copy(), 9, 21, -2e-5, 2e-5, option="matrix", option_eval="9",
+                                         verbose=False))
+    res["auto_focus_sep_matrix_ms"] = t * 1e3
     print(json.dumps(res, indent=1))
     if args.out:
         with open(args.out, "w") as f:
