@@ -29,6 +29,8 @@
 namespace akb {
 namespace {
 
+constexpr int kStripRowsDefault = 32;
+
 struct Grid {
     const double* x;  // (n,) point x (detcenter2[1])
     const double* y;  // (n,) point y (detcenter2[2])
@@ -42,6 +44,7 @@ struct Grid {
     const int32_t* xptr;   // (L + 1) extra neighbours of ring vertex r (pocket chords)
     const int32_t* xidx;
     int no_xcd;  // 1: plain block order in the sweep (AKB_GD_NOXCD, A/B timing only)
+    int strip_rows = kStripRowsDefault;  // rows per strip workgroup (AKB_GD_ROWS, A/B timing)
 };
 
 __device__ __forceinline__ int64_t ncells(const Grid& g) { return (int64_t)(g.nv - 1) * (g.nh - 1); }
@@ -411,12 +414,11 @@ __global__ void __launch_bounds__(kBlock) k_gd_grad(Grid g, const double* __rest
 }
 
 // The same sweep with every vertex's data read from HBM once: a workgroup walks down a strip of
-// kStripW columns (plus one halo column each side) over kStripRows rows, holding three rows of
+// kStripW columns (plus one halo column each side) over strip_rows rows (default 32), holding three rows of
 // (x, y, f, g) in an LDS ring, the next row already in registers while the current one is solved
 // (its loads in flight across the row's arithmetic). The per-vertex edge order and arithmetic are
 // k_gd_grad's, so both give the same bits; the global version's eight-neighbour gathers (about 50
 // load instructions per vertex through the texture path) become LDS reads.
-constexpr int kStripRows = 32;
 
 template <int NV, int W>
 struct StripRow {  // one row of a strip in LDS: column c of the strip at [c + 1], halos at 0 / W + 1
@@ -497,8 +499,8 @@ __global__ void __launch_bounds__(W) k_gd_grad_strip(Grid g, const double* __res
     const int nstrips = (g.nh + kStripW - 1) / kStripW;
     const int strip = blockIdx.x % nstrips, chunk = blockIdx.x / nstrips;
     const int c0 = strip * kStripW;
-    const int r0 = chunk * kStripRows;
-    const int r1 = r0 + kStripRows < g.nv ? r0 + kStripRows : g.nv;
+    const int r0 = chunk * g.strip_rows;
+    const int r1 = r0 + g.strip_rows < g.nv ? r0 + g.strip_rows : g.nv;
     const int t = threadIdx.x;
     const int ih = c0 + t;
     const bool col = ih < g.nh;
@@ -870,6 +872,11 @@ int akb_gd_grad_sweep_f64(const double* x, const double* y, int nv, int nh, cons
     clear_error();
     AKB_REQUIRE(x && y && diag && f && gin && gout && ring_work && d_change && nvals >= 1, "bad arguments");
     Grid g{x, y, nv, nh, diag, npock, ptri, pnbr, edge_tri, xptr, xidx, gd_no_xcd()};
+    {
+        const char* re = getenv("AKB_GD_ROWS");
+        const int rows = re ? atoi(re) : 0;
+        if (rows >= 4 && rows <= 256) g.strip_rows = rows;
+    }
     hipStream_t s = (hipStream_t)stream;
     const int64_t n = (int64_t)nv * nh;
     const int64_t L = 2 * (int64_t)(nh - 1) + 2 * (int64_t)(nv - 1);
@@ -880,13 +887,15 @@ int akb_gd_grad_sweep_f64(const double* x, const double* y, int nv, int nh, cons
     // the LDS strip kernel, AKB_GD_STRIP columns wide (64 / 128 / 256; 0: the gather kernel; read
     // per call: the tests compare them)
     const char* se = getenv("AKB_GD_STRIP");
-    int strip = se ? atoi(se) : 128;
-    if (strip != 0 && strip != 64 && strip != 128 && strip != 256) strip = 128;
+    // 256 by default: 11.9 vs 12.5 / 12.8 ms of sweeps for 128 / 64 on the C3 hits (the row chunk,
+    // 8 ... 64 rows, moves it by < 5 %: the strips are LDS-occupancy bound at 3 waves per SIMD)
+    int strip = se ? atoi(se) : 256;
+    if (strip != 0 && strip != 64 && strip != 128 && strip != 256) strip = 256;
     // the strip sweeps as line Gauss-Seidel (AKB_GD_GS=0: Jacobi, the gather kernel's bits)
     const char* ge = getenv("AKB_GD_GS");
     const bool gs_sweep = !(ge && ge[0] == '0');
     const unsigned gs =
-        strip ? (unsigned)(((nh + strip - 1) / strip) * ((nv + kStripRows - 1) / kStripRows)) : 0u;
+        strip ? (unsigned)(((nh + strip - 1) / strip) * ((nv + g.strip_rows - 1) / g.strip_rows)) : 0u;
     for (int v = 0; v < nvals; v += 2) {
         const double* fv = f + v * n;
         const double* gi = gin + 2 * v * n;
