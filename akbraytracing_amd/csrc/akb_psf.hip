@@ -448,7 +448,7 @@ static int launch_psf_cols(const PsfFastArgs& fa, int batch, hipStream_t s) {
     return launch_status("k_psf_cols");
 }
 
-#define AKB_PSF_SIZES(X) X(8) X(16) X(32) X(64) X(128) X(256)
+#define AKB_PSF_SIZES(X) X(8) X(16) X(32) X(64) X(128) X(256) X(512) X(1024)
 
 static int psf_rows_dispatch(int n, const PsfFastArgs& fa, int batch, hipStream_t s) {
     switch (n) {
@@ -484,9 +484,12 @@ static int ilog2_exact(int v) {
 static bool psf_fast_ok(const PsfGeom& g) {
     if (getenv("AKB_PSF_ROCFFT")) return false;
     const int ly = ilog2_exact(g.ny2), lx = ilog2_exact(g.nx2);
-    // up to 256: larger transforms hold 32-point register DFTs at one wave per SIMD and lose to
-    // rocFFT on the full plane (measured: 1024^2 pupil, pad 2: 193 vs 151 us)
-    return ly >= 3 && ly <= 8 && lx >= 3 && lx <= 8 && (int64_t)g.py * g.px < (1LL << 31);
+    // up to 256 at any pad; 512 / 1024 only at pad >= 8, where the padded plane rocFFT would
+    // transform is 64x the pupil or more (their 32-point register DFTs run at one wave per SIMD
+    // and lose to rocFFT on a small plane: 1024^2 pupil, pad 2: 193 vs 151 us)
+    const int pad = g.px / g.nx2;
+    const int lmax = pad >= 8 ? 10 : 8;
+    return ly >= 3 && ly <= lmax && lx >= 3 && lx <= lmax && (int64_t)g.py * g.px < (1LL << 31);
 }
 
 static int64_t psf_fast_bytes(const PsfGeom& g, int batch) {

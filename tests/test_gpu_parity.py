@@ -696,7 +696,8 @@ def test_psf_stack_equals_single(gpu):
 
 @pytest.mark.parametrize("ny,nx,pad,win,eff", [(128, 128, 16, False, False), (64, 32, 4, True, True),
                                                (15, 16, 3, False, True), (8, 8, 1, False, False),
-                                               (256, 8, 2, True, False), (32, 256, 5, False, True)])
+                                               (256, 8, 2, True, False), (32, 256, 5, False, True),
+                                               (512, 512, 8, False, True), (1024, 32, 8, True, False)])
 def test_psf_pruned_transform(gpu, ny, nx, pad, win, eff, monkeypatch):
     """Power-of-two pupils take the pruned transform (the padded plane is never built): against
     the oracle (numpy fft2 on the padded plane) and against the rocFFT path on the same input."""
