@@ -251,16 +251,76 @@ __device__ __forceinline__ void dft_reg_br(double2 (&t)[M]) {
 //           W_N^(n2 k1); LDS exchange
 //   step 2: thread (c, t2) runs the N2-point DFTs of k1 = t2 + s N2, giving X[k1 + N1 k2]
 // load(c, a) supplies input element a of transform c; store(c, j, value) consumes output j.
+// N <= 256: two stages (N1 x N2, N1 <= 16 complex values per thread). N = 512 / 1024: three
+// stages (fft_block3: NA = 8 / 16 in registers, then the remaining 64-point transforms as 8 x 8),
+// so no thread holds more than 16 complex values - a 32-point register DFT needs ~290 VGPRs and
+// runs one wave per SIMD.
 template <int N>
 struct FftShape {
     static constexpr int L = ilog2_c(N);
-    static constexpr int N1 = 1 << ((L + 1) / 2);
-    static constexpr int N2 = N / N1;
+    static constexpr bool k3 = N >= 512;
+    static constexpr int NA = N >= 1024 ? 16 : 8;  // first stage of the three-stage split
+    static constexpr int N1 = k3 ? NA : 1 << ((L + 1) / 2);
+    static constexpr int N2 = N / N1;  // threads per transform (both splits)
     static constexpr int C0 = kFftTile / N < kBlock / N2 ? kFftTile / N : kBlock / N2;
 };
 
+// three stages for N = NA * M, M = 64 = 8 x 8: stage A, thread (c, m) takes x[nA M + m], an
+// NA-point DFT, twiddle W_N^(m kA) -> Y[kA][m]; stage B1, for each kA the 64-point transform's
+// first 8-point DFTs over m = mb1 8 + mb2 (in place in Y[kA], twiddle W_64^(mb2 kb1)); stage B2,
+// the second 8-point DFTs give Z_kA[kb1 + 8 kb2] = X[kA + NA (kb1 + 8 kb2)].
 template <int N, typename Load, typename Store>
-__device__ __forceinline__ void fft_block(int C, double2* Y, const double2* twN, Load load, Store store) {
+__device__ __forceinline__ void fft_block3(int C, double2* Y, const double2* twN, Load load, Store store) {
+    constexpr int NA = FftShape<N>::NA, M = N / NA, MB = 8;
+    static_assert(M == MB * MB, "three-stage split: N / NA must be 64");
+    constexpr int LA = ilog2_c(NA), LB = ilog2_c(MB);
+    const int tid = threadIdx.x;
+    const int c = tid % C, p = tid / C;  // p < M: this thread's task in each stage
+    {
+        const int m = p;
+        double2 v[NA];
+#pragma unroll
+        for (int i = 0; i < NA; ++i) v[i] = load(c, bitrev_c(i, LA) * M + m);
+        dft_reg_br<NA>(v);
+#pragma unroll
+        for (int kA = 0; kA < NA; ++kA) {
+            const double2 w = kA && m ? cmul(v[kA], twN[(m * kA) % N]) : v[kA];
+            Y[(kA * M + m) * C + c] = w;
+        }
+    }
+    __syncthreads();
+    // stage B1: NA * 8 tasks (kA, mb2) over M threads
+#pragma unroll
+    for (int s = 0; s < NA * MB / M; ++s) {
+        const int task = p + s * M;
+        const int kA = task / MB, mb2 = task % MB;
+        double2 w[MB];
+#pragma unroll
+        for (int i = 0; i < MB; ++i) w[i] = Y[(kA * M + bitrev_c(i, LB) * MB + mb2) * C + c];
+        dft_reg_br<MB>(w);
+#pragma unroll
+        for (int kb1 = 0; kb1 < MB; ++kb1) {
+            const double2 t = kb1 && mb2 ? cmul(w[kb1], twN[(NA * mb2 * kb1) % N]) : w[kb1];
+            Y[(kA * M + kb1 * MB + mb2) * C + c] = t;
+        }
+    }
+    __syncthreads();
+    // stage B2: NA * 8 tasks (kA, kb1)
+#pragma unroll
+    for (int s = 0; s < NA * MB / M; ++s) {
+        const int task = p + s * M;
+        const int kA = task / MB, kb1 = task % MB;
+        double2 u[MB];
+#pragma unroll
+        for (int i = 0; i < MB; ++i) u[i] = Y[(kA * M + kb1 * MB + bitrev_c(i, LB)) * C + c];
+        dft_reg_br<MB>(u);
+#pragma unroll
+        for (int kb2 = 0; kb2 < MB; ++kb2) store(c, kA + NA * (kb1 + MB * kb2), u[kb2]);
+    }
+}
+
+template <int N, typename Load, typename Store>
+__device__ __forceinline__ void fft_block2(int C, double2* Y, const double2* twN, Load load, Store store) {
     constexpr int N1 = FftShape<N>::N1, N2 = FftShape<N>::N2;
     constexpr int L1 = ilog2_c(N1), L2 = ilog2_c(N2);
     const int tid = threadIdx.x;
@@ -289,6 +349,14 @@ __device__ __forceinline__ void fft_block(int C, double2* Y, const double2* twN,
     }
 }
 
+template <int N, typename Load, typename Store>
+__device__ __forceinline__ void fft_block(int C, double2* Y, const double2* twN, Load load, Store store) {
+    if constexpr (FftShape<N>::k3)
+        fft_block3<N>(C, Y, twN, load, store);
+    else
+        fft_block2<N>(C, Y, twN, load, store);
+}
+
 struct PsfFastArgs {
     const double* opd;
     const double* amp;
@@ -299,7 +367,8 @@ struct PsfFastArgs {
     double kphase[8];
     const double2* Wx;  // W_px table
     const double2* Wy;  // W_py table
-    double2* H;         // (batch, ey, px)
+    double2* H;         // (batch, ey, px), or (batch, px, ey) when hT (column length >= 512)
+    int hT;
     double dA;
     const double* pitch;
     double* psf;
@@ -348,6 +417,9 @@ __global__ void __launch_bounds__(kBlock) k_psf_rows(PsfFastArgs A) {
     }
     __syncthreads();
     double2* Hrow = A.H + ((int64_t)b * g.ny2 + a) * g.px;
+    // transposed H for long columns: the column pass then reads each column contiguously (its
+    // 32 reads of H are what the scattered write here pays for once)
+    double2* Ht = A.H + (int64_t)b * g.ny2 * g.px + a;
     fft_block<N>(
         C0, Y, tw,
         [&](int c, int m) {
@@ -356,7 +428,12 @@ __global__ void __launch_bounds__(kBlock) k_psf_rows(PsfFastArgs A) {
         },
         [&](int c, int j, double2 v) {
             const int r = r0 + c;
-            if (r < pad) Hrow[(int64_t)pad * j + r] = v;
+            if (r < pad) {
+                if (A.hT)
+                    Ht[((int64_t)pad * j + r) * g.ny2] = v;
+                else
+                    Hrow[(int64_t)pad * j + r] = v;
+            }
         });
 }
 
@@ -396,7 +473,10 @@ __global__ void __launch_bounds__(kBlock) k_psf_cols(PsfFastArgs A, int C) {
     double m = 0.0;
     fft_block<N>(
         C, Y, tw,
-        [&](int c, int a) { return cmul(Hb[(int64_t)a * g.px + l0 + c], twr[a]); },
+        [&](int c, int a) {
+            const int64_t h = FftShape<N>::k3 ? (int64_t)(l0 + c) * N + a : (int64_t)a * g.px + l0 + c;
+            return cmul(Hb[h], twr[a]);
+        },
         [&](int c, int j, double2 f) {
             const int ko = pad * j + r, lo = l0 + c;
             const double re = f.x * dA, im = f.y * dA;
@@ -607,6 +687,7 @@ int akb_psf_f64(const double* opd, const double* amp, int ny, int nx, int pad, i
         fa.g = g;
         for (int b = 0; b < batch; ++b) fa.kphase[b] = (2.0 * M_PI / lambdas[b]);
         fa.H = (double2*)work;
+        fa.hT = g.ny2 >= 512;  // FftShape<N>::k3 of the column pass
         if ((st = get_twiddles(g.px, s, &fa.Wx))) return st;
         if ((st = get_twiddles(g.py, s, &fa.Wy))) return st;
         fa.dA = dx * dy;
