@@ -21,6 +21,11 @@ Here a sweep is:
 so the spot sizes, the argmins auto_focus_NA takes over them and its answer are the reference's
 bit for bit (tests/golden/akb_autofocus.npz). A flagged trace (a miss or zero norm) takes the
 drop-in primitives stage by stage, which apply the reference's all-NaN / passthrough rules.
+
+KB_debug(params, na_ratio_h, na_ratio_v, 'test') (:9742-12726) - the KB pair auto_focus_NA sweeps
+when option_AKB is False - is kb_test: geometry.build_kb's two ellipses through the same batched
+trace and evaluation, tilted always and by np.mean (not nanmean) of the exit angles
+(tests/golden/kb_build.npz).
 """
 import numpy as np
 import torch
@@ -44,8 +49,11 @@ class TracedSystems:
     """S systems traced on an n x n grid: exit directions and last hits (S, 3, n^2) on the device,
     their tilt rotations (S, 18) and detector-plane offsets s2f_middle."""
 
-    def __init__(self, builts, ray_num=53, want_hits=False, tilt=True):
+    def __init__(self, builts, ray_num=53, want_hits=False, tilt=True, theta_mean="nanmean"):
         L = _lib.lib()
+        if theta_mean not in ("nanmean", "mean"):
+            raise ValueError("theta_mean is 'nanmean' (plot_result_debug) or 'mean' (KB_debug)")
+        self.theta_mean = theta_mean
         self.dev = D.device()
         self.builts = list(builts)
         S = len(self.builts)
@@ -110,17 +118,21 @@ class TracedSystems:
 
     def _rotations(self):
         """theta_y = -nanmean(arctan(angle[2]/angle[0])), theta_z = nanmean(arctan(angle[1]/angle[0]))
-        (:3583-3588) and rotate_vectors' R_y(-theta_y), R_z(-theta_z) (:917-927), per system."""
+        (:3583-3588; np.mean in KB_debug, :11705-11706) and rotate_vectors' R_y(-theta_y),
+        R_z(-theta_z) (:917-927), per system."""
+        mean = np.nanmean if self.theta_mean == "nanmean" else np.mean
         ang = self.dir.cpu().numpy()
         rot = np.empty((self.S, 18), dtype=np.float64)
+        self.thetas = np.empty((self.S, 2), dtype=np.float64)
         with np.errstate(invalid="ignore", divide="ignore"):
             import warnings
             with warnings.catch_warnings():
                 warnings.simplefilter("ignore", RuntimeWarning)  # an all-NaN system: nanmean warns, gives NaN
                 for s in range(self.S):
                     a = ang[s]
-                    theta_y = -np.nanmean(np.arctan(a[2, :] / a[0, :]))
-                    theta_z = np.nanmean(np.arctan(a[1, :] / a[0, :]))
+                    theta_y = -mean(np.arctan(a[2, :] / a[0, :]))
+                    theta_z = mean(np.arctan(a[1, :] / a[0, :]))
+                    self.thetas[s] = theta_y, theta_z
                     ry, rz = P.rotation_matrices(-theta_y, -theta_z)
                     rot[s, :9] = ry.ravel()
                     rot[s, 9:] = rz.ravel()
@@ -182,24 +194,58 @@ def plot_result_test(params, source_shift=(0.0, 0.0, 0.0), option_tilt=True, *, 
     return tuple(x.cpu().numpy() for x in out)
 
 
-class _SystemCache:
-    """Built and traced systems keyed by what they depend on (params[1:], source shift, flags)."""
+def kb_test(params, source_shift=(0.0, 0.0, 0.0), *, designparams=None, ray_num=53, as_torch=False):
+    """KB_debug(params, na_ratio_h, na_ratio_v, 'test') (:9742-12726; the NA ratios are unused):
+    the KB pair of geometry.build_kb traced once, the detector hits tilted by the np.mean exit
+    angles (always: the mode sets option_tilt = True, :11703-11717). Returns (vmirr_hyp, tilted
+    hmirr_hyp, tilted detcenter, tilted angle) as numpy (3, n^2) arrays, or np.inf where the
+    reference returns np.inf."""
+    b = G.build_kb(params, source_shift=source_shift, designparams=designparams)
+    if not isinstance(b, dict):
+        return b
+    ts = TracedSystems([b], ray_num=ray_num, want_hits=True, tilt=True, theta_mean="mean")
+    _, _, det, ang = ts.evaluate(np.array([b["defocus"]]), want_rows=True)
+    # the H hits rotated about the untilted spot's mean (:11708-11709), as rotate_points does
+    det1 = np.array(b["det1"], dtype=np.float64)
+    det0 = P.plane_ray_intersection(det1, ts.dir[0], ts.pt[0])
+    focus = np.mean(det0.cpu().numpy(), axis=1)
+    theta_y, theta_z = ts.thetas[0]
+    h_rot = P.rotate_points(ts.hits[0, 1], focus, -theta_y, -theta_z)
+    out = (ts.hits[0, 0], h_rot, det[0, 0], ang[0, 0])
+    if as_torch:
+        return out
+    return tuple(x.cpu().numpy() for x in out)
 
-    def __init__(self, option_set, ray_num):
-        self.option_set, self.ray_num = option_set, ray_num
+
+class _SystemCache:
+    """Built and traced systems keyed by what they depend on (params[1:], source shift, flags).
+    system 'kb' builds KB_debug's pair (geometry.build_kb: no source shift - auto_focus_NA calls
+    KB_debug without one - and always tilted by the np.mean angles)."""
+
+    def __init__(self, option_set, ray_num, system="akb", kb_design=None):
+        if system not in ("akb", "kb"):
+            raise ValueError("system is 'akb' or 'kb'")
+        self.option_set, self.ray_num, self.system = option_set, ray_num, system
+        self.kb_design = kb_design
         self._c = {}
 
     def get(self, params, source_shift, tilt):
+        kb = self.system == "kb"
+        if kb:
+            source_shift, tilt = (0.0, 0.0, 0.0), True
         key = (tuple(float(x) for x in np.asarray(params, dtype=np.float64)[1:]),
                tuple(float(x) for x in source_shift), bool(tilt))
         ts = self._c.get(key)
         if ts is None:
-            b = G.build_akb(params, source_shift=source_shift, option_set=self.option_set)
+            if kb:
+                b = G.build_kb(params, designparams=self.kb_design)
+            else:
+                b = G.build_akb(params, source_shift=source_shift, option_set=self.option_set)
             if not isinstance(b, dict):
-                # the reference's plot_result_debug returns np.inf here and auto_focus_NA's
-                # unpacking of it raises
+                # the reference's plot_result_debug / KB_debug returns np.inf here and
+                # auto_focus_NA's unpacking of it raises
                 raise TypeError("cannot unpack non-iterable float object")
-            ts = TracedSystems([b], ray_num=self.ray_num, tilt=tilt)
+            ts = TracedSystems([b], ray_num=self.ray_num, tilt=tilt, theta_mean="mean" if kb else "nanmean")
             if len(self._c) > 64:
                 self._c.clear()
             self._c[key] = ts
@@ -208,15 +254,18 @@ class _SystemCache:
 
 def auto_focus_NA(num_adj_astg, initial_params, na_ratio_h, na_ratio_v, option, option_param, option_disp='ray',
                   option_mode=False, source_shift0=[0., 0., 0.], option_legendre=False, *, widesearch=False,
-                  option_set=True, driver=None, verbose=True, cache=None):
+                  option_set=True, option_AKB=True, kb_design=None, driver=None, verbose=True, cache=None):
     """auto_focus_NA (AKB_raytrace_20250312.py:12746-12895) for the AKB system (option_AKB): the same
     ranges, steps, attempts, astigmatism updates and stopping rule, with every 100-value sweep of
     params[0] one device evaluation. initial_params is updated in place as the reference does.
 
-    widesearch / option_set: the reference's module flags (:98, :94). driver: the reference module,
-    used only for what follows the search when `option` or `option_legendre` asks for a display
-    or 'ray_wave' run (those call its own plot_result_debug; without a driver they raise)."""
-    cache = cache or _SystemCache(option_set, 53)
+    widesearch / option_set / option_AKB: the reference's module flags (:98, :94, :80). With
+    option_AKB False the sweeps trace KB_debug's pair (kb_test's system: no source shift, always
+    tilted by the np.mean angles, :12784; kb_design: the module's KBdesign_7params, :100).
+    driver: the reference module, used only for what follows the search when `option` or
+    `option_legendre` asks for a display or 'ray_wave' run (those call its own plot_result_debug /
+    KB_debug; without a driver they raise)."""
+    cache = cache or _SystemCache(option_set, 53, "akb" if option_AKB else "kb", kb_design)
     if widesearch:
         a_min, a_max = -1 + initial_params[0].copy(), 1 + initial_params[0].copy()
         shrink_factor, num_adj_astg, max_attempts = 0.1, 300, 17
@@ -275,11 +324,19 @@ def auto_focus_NA(num_adj_astg, initial_params, na_ratio_h, na_ratio_v, option, 
             raise NotImplementedError("the display / 'ray_wave' follow-up runs the reference's plot_result_debug: "
                                       "pass driver=<the AKB_raytrace module>")
         if option_legendre:
+            if not option_AKB:
+                return driver.KB_debug(initial_params, na_ratio_h, na_ratio_v, 'ray_wave', option_legendre=True,
+                                       source_shift=source_shift0)
             return driver.plot_result_debug(initial_params, 'ray_wave', option_legendre=True, source_shift=source_shift0)
-        if option_disp == 'ray_wave':
+        if not option_AKB:
+            r = driver.KB_debug(initial_params, na_ratio_h, na_ratio_v, option_disp)
+            if option_disp == 'ray_wave':
+                return r
+        elif option_disp == 'ray_wave':
             return driver.plot_result_debug(initial_params, option_disp, source_shift=source_shift0)
-        kw = dict(option_tilt=False) if foc else {}
-        driver.plot_result_debug(initial_params, option_disp, source_shift=source_shift0, **kw)
+        else:
+            kw = dict(option_tilt=False) if foc else {}
+            driver.plot_result_debug(initial_params, option_disp, source_shift=source_shift0, **kw)
     if option_param == 'D':
         return np.min(distance_)
     return size_v_param, size_h_param, initial_params

@@ -411,3 +411,210 @@ def build_akb(params, *, source_shift=(0.0, 0.0, 0.0), option_set=True, prims=No
 def mirrors_of(built):
     """The trace-order Mirror list of a build_akb result."""
     return [Mirror(m["coeffs"], m["negative"]) for m in built["mirrors"]]
+
+
+# ---------------------------------------------------------------- the KB pair (KB_debug)
+
+# KBdesign_7params (AKB_raytrace_20250312.py:100): l1h, l2h, inc_h, mlen_h, wd_v, inc_v, mlen_v
+KB_DESIGN_7PARAMS = (np.float64(146.), np.float64(0.21), np.float64(0.16742), np.float64(0.180), np.float64(0.030),
+                     np.float64(0.15525), np.float64(0.05))
+
+
+def rotate_x(coeffs, theta, center):
+    """:669-693"""
+    a, b, c, d, e, f, g, h, i, j = shift_z(shift_y(shift_x(coeffs, -center[0]), -center[1]), -center[2])
+    Cos, Sin = np.cos(theta), np.sin(theta)
+    out = [a, b * Cos**2 + c * Sin**2 - f * Sin * Cos, b * Sin**2 + c * Cos**2 + f * Sin * Cos, d * Cos - e * Sin,
+           d * Sin + e * Cos, b * np.sin(2 * theta) - c * np.sin(2 * theta) + f * np.cos(2 * theta), g,
+           h * Cos - i * Sin, h * Sin + i * Cos, j]
+    return shift_z(shift_y(shift_x(out, center[0]), center[1]), center[2])
+
+
+def rotate_y(coeffs, theta, center):
+    """:695-719"""
+    a, b, c, d, e, f, g, h, i, j = shift_z(shift_y(shift_x(coeffs, -center[0]), -center[1]), -center[2])
+    Cos, Sin = np.cos(theta), np.sin(theta)
+    out = [a * Cos**2 + c * Sin**2 + e * Sin * Cos, b, a * Sin**2 + c * Cos**2 - e * Sin * Cos, d * Cos + f * Sin,
+           -a * np.sin(2 * theta) + c * np.sin(2 * theta) + e * np.cos(2 * theta), -d * Sin + f * Cos,
+           g * Cos + i * Sin, h, i * Cos - g * Sin, j]
+    return shift_z(shift_y(shift_x(out, center[0]), center[1]), center[2])
+
+
+def rotate_z(coeffs, theta, center):
+    """:721-745"""
+    a, b, c, d, e, f, g, h, i, j = shift_z(shift_y(shift_x(coeffs, -center[0]), -center[1]), -center[2])
+    Cos, Sin = np.cos(theta), np.sin(theta)
+    out = [a * Cos**2 + b * Sin**2 - d * Sin * Cos, b * Cos**2 + a * Sin**2 + d * Sin * Cos, c,
+           a * np.sin(2 * theta) - b * np.sin(2 * theta) + d * np.cos(2 * theta), e * Cos - f * Sin,
+           e * Sin + f * Cos, g * Cos - h * Sin, g * Sin + h * Cos, i, j]
+    return shift_z(shift_y(shift_x(out, center[0]), center[1]), center[2])
+
+
+def ell_define(l1, inc, l2):
+    """Ell_define (:272-281)"""
+    sita1 = np.arctan(l2 * np.sin(2. * inc) / (l1 + l2 * np.cos(2. * inc)))
+    a_ell = (l1 + l2) / 2.
+    b_ell = np.sqrt(l1 * l2 * np.sin(inc) ** 2)
+    sita3 = np.arcsin(l1 * np.sin(sita1) / l2)
+    return a_ell, b_ell, sita1, sita3
+
+
+def kb_define(l1h, l2h, inc_h, mlen_h, wd_v, inc_v, mlen_v):
+    """KB_define (:297-336): the two ellipses of a KB pair sharing one focus; the V ellipse's source
+    distance found by the reference's fixed-point iteration. Returns the reference's tuple."""
+    a_h, b_h, sita1h, sita3h = ell_define(l1h, inc_h, l2h)
+    s2f_h = np.sqrt(a_h**2. - b_h**2.) * 2.
+    xh_s = l1h * np.cos(sita1h) - mlen_h / 2.
+    xh_e = l1h * np.cos(sita1h) + mlen_h / 2.
+    yh_s = _calc_y_ell(a_h, b_h, xh_s)
+    yh_e = _calc_y_ell(a_h, b_h, xh_e)
+    accept_h = np.abs(yh_e - yh_s)
+    NA_h = np.sin(np.abs(np.arctan(yh_e / (s2f_h - xh_e)) - np.arctan(yh_s / (s2f_h - xh_s)))) / 2.
+    l1v = l1h + (l2h - wd_v - mlen_v / 2.)
+    l2v = wd_v + mlen_v / 2.
+    while True:
+        a_v, b_v, sita1v, sita3v = ell_define(l1v, inc_v, l2v)
+        s2f_v = np.sqrt(a_v**2. - b_v**2.) * 2.
+        diff = s2f_h - s2f_v
+        if np.abs(diff) < 1e-9:
+            break
+        l1v += diff * 0.9
+    xv_s = l1v * np.cos(sita1v) - mlen_v / 2.
+    xv_e = l1v * np.cos(sita1v) + mlen_v / 2.
+    yv_s = _calc_y_ell(a_v, b_v, xv_s)
+    yv_e = _calc_y_ell(a_v, b_v, xv_e)
+    accept_v = np.abs(yv_e - yv_s)
+    NA_v = np.sin(np.abs(np.arctan(yv_e / (s2f_v - xv_e)) - np.arctan(yv_s / (s2f_v - xv_s)))) / 2.
+    gap = xv_s - xh_e
+    return a_h, b_h, a_v, b_v, l1v, l2v, [xh_s, xh_e, yh_s, yh_e, sita1h, sita3h, accept_h, NA_h, xv_s, xv_e, yv_s,
+                                          yv_e, sita1v, sita3v, accept_v, NA_v, s2f_h, diff, gap]
+
+
+def _ell_theta5(a, org, theta1):
+    """theta5 of KB_debug's print_optical_design (:10463-10493), the only output it uses."""
+    l4 = ((org)**2 - 2 * org * a * np.cos(theta1) + a**2) / (a - org * np.cos(theta1))
+    return np.arcsin((2 * a - l4) * np.sin(theta1) / l4)
+
+
+def build_kb(params, *, source_shift=(0.0, 0.0, 0.0), designparams=None, prims=None, name=None):
+    """KB_debug's system for params (26 floats) with its live flags (optKBdesign False,
+    option_HighNA True, option_axial / option_alignment / optin_axialrotation /
+    optionLocalRotation True, optionLocalRotationonlyAll False: :9742-10935): the V and H
+    ellipses of KB_define from KBdesign_7params (or designparams), aligned on five centre rays,
+    then params' misalignments (pitch / roll / yaw of the V mirror about its centre ray's hit, of the
+    H mirror about its local axes through its corner rays' mean hit; decenters). Returns a dict
+    with the SystemGeometry fields (two mirrors, det1, launch-angle ranges, source) plus
+    s2f_middle and defocus, or np.inf where the reference returns np.inf."""
+    if prims is None:
+        from . import primitives as prims
+    p = [np.float64(x) for x in np.asarray(params, dtype=np.float64).ravel()]
+    if len(p) != 26:
+        raise ValueError("params must hold 26 values")
+    (defocus, astigH,
+     pitch_hyp_v, roll_hyp_v, yaw_hyp_v, decX_hyp_v, decY_hyp_v, decZ_hyp_v,
+     pitch_hyp_h, roll_hyp_h, yaw_hyp_h, decX_hyp_h, decY_hyp_h, decZ_hyp_h) = p[:14]
+    l1h, l2h, inc_h, mlen_h, wd_v, inc_v, mlen_v = (KB_DESIGN_7PARAMS if designparams is None
+                                                     else [np.float64(x) for x in designparams])
+    a_h, b_h, a_v, b_v, l1v, l2v, rest = kb_define(l1h, l2h, inc_h, mlen_h, wd_v, inc_v, mlen_v)
+    xh_s, xh_e, yh_s, yh_e, sita1h, sita3h, _, _, xv_s, xv_e, yv_s, yv_e, sita1v = rest[:13]
+    a_hyp_v, b_hyp_v, a_hyp_h, b_hyp_h = a_h, b_h, a_v, b_v
+    org_hyp_v = np.sqrt(a_hyp_v**2 - b_hyp_v**2)
+    org_hyp_h = np.sqrt(a_hyp_h**2 - b_hyp_h**2)
+    y1_v, x1_v, y2_v, x2_v = yh_s, xh_s, yh_e, xh_e
+    y1_h, x1_h, y2_h, x2_h = yv_s, xv_s, yv_e, xv_e
+    theta1_v, theta1_h = sita1h, sita1v
+
+    # V mirror (:10432-10447)
+    axis_x, axis_y, axis_z = np.float64([1., 0., 0.]), np.float64([0., 1., 0.]), np.float64([0., 0., 1.])
+    hyp_v = np.zeros(10)
+    hyp_v[0] = 1 / a_hyp_v**2
+    hyp_v[2] = 1 / b_hyp_v**2
+    hyp_v[9] = -1.
+    hyp_v = shift_x(hyp_v, org_hyp_v)
+    hyp_v, R = rotate_general_axis(hyp_v, axis_y, theta1_v, [0., 0., 0.])
+    axis_x, axis_y, axis_z = rotatematrix(R, axis_x, axis_y, axis_z)
+
+    # the five alignment rays (:10458-10609): the centre and four corners
+    at1h, at2h = np.arctan(y1_h / x1_h), np.arctan(y2_h / x2_h)
+    at1v, at2v = np.arctan(y1_v / x1_v), np.arctan(y2_v / x2_v)
+    theta_cntr_h = (at2h + at1h) / 2.
+    theta_cntr_v = (at2v + at1v) / 2.
+    theta5_v1 = _ell_theta5(a_hyp_v, org_hyp_v, at1v)
+    theta5_v2 = _ell_theta5(a_hyp_v, org_hyp_v, at2v)
+    omega_V = ((at1v + at2v) + theta5_v1 + theta5_v2) / 2
+    ts1h, ts2h = at1h - theta_cntr_h, at2h - theta_cntr_h
+    ts1v, ts2v = at1v - theta_cntr_v, at2v - theta_cntr_v
+    bufray = np.zeros((3, 5))
+    bufray[0, :] = 1.
+    bufray[1, 0], bufray[2, 0] = np.tan(theta1_h), np.tan(theta1_v)
+    bufray[1, 1], bufray[2, 1] = np.tan(ts1h), np.tan(ts1v)
+    bufray[1, 2], bufray[2, 2] = np.tan(ts2h), np.tan(ts1v)
+    bufray[1, 3], bufray[2, 3] = np.tan(ts2h), np.tan(ts1v)
+    bufray[1, 4], bufray[2, 4] = np.tan(ts2h), np.tan(ts2v)
+    source = np.zeros((3, 5))
+    bufray = prims.normalize_vector(bufray)
+    center_hyp_v = prims.mirr_ray_intersection(hyp_v, bufray, source)
+    if not np.isreal(center_hyp_v).all():
+        return np.inf
+    refl1 = prims.reflect_ray(bufray, prims.norm_vector(hyp_v, center_hyp_v))
+
+    # H mirror (:10808-10847)
+    hyp_h = np.zeros(10)
+    hyp_h[0] = 1 / a_hyp_h**2
+    hyp_h[1] = 1 / b_hyp_h**2
+    hyp_h[9] = -1.
+    hyp_h = shift_x(hyp_h, org_hyp_h + astigH)
+    ax2, ay2, az2 = np.float64([1., 0., 0.]), np.float64([0., 1., 0.]), np.float64([0., 0., 1.])
+    ay_g, az_g = np.float64([0., 1., 0.]), np.float64([0., 0., 1.])
+    hyp_h, R = rotate_general_axis(hyp_h, az_g, -theta1_h, [0, 0, 0])
+    ax2, ay2, az2 = rotatematrix(R, ax2, ay2, az2)
+    center_hyp_h = prims.mirr_ray_intersection(hyp_h, refl1, center_hyp_v)
+    if not np.isreal(center_hyp_h).all():
+        return np.inf
+    hyp_h, R = rotate_general_axis(hyp_h, ay_g, omega_V, _col_mean(center_hyp_h))
+    ax2, ay2, az2 = rotatematrix(R, ax2, ay2, az2)
+    center_hyp_h = prims.mirr_ray_intersection(hyp_h, refl1, center_hyp_v)
+
+    s2f_middle = (2 * org_hyp_h + 2 * org_hyp_v) / 2  # (s2f_H + s2f_V) / 2, :10862-10866
+
+    # misalignments (:10898-10934)
+    cv = center_hyp_v[:, 0]
+    if pitch_hyp_v != 0:
+        hyp_v = rotate_y(hyp_v, pitch_hyp_v, cv)
+    if roll_hyp_v != 0:
+        hyp_v = rotate_x(hyp_v, roll_hyp_v, cv)
+    if yaw_hyp_v != 0:
+        hyp_v = rotate_z(hyp_v, yaw_hyp_v, cv)
+    ch = _col_mean(center_hyp_h)
+    if pitch_hyp_h != 0:
+        hyp_h, _ = rotate_general_axis(hyp_h, ay2, pitch_hyp_h, ch)
+    if yaw_hyp_h != 0:
+        hyp_h, _ = rotate_general_axis(hyp_h, az2, yaw_hyp_h, ch)
+    if roll_hyp_h != 0:
+        hyp_h, _ = rotate_general_axis(hyp_h, ax2, roll_hyp_h, ch)
+    for s, f in ((decX_hyp_v, shift_x), (decY_hyp_v, shift_y), (decZ_hyp_v, shift_z)):
+        if s != 0:
+            hyp_v = f(hyp_v, s)
+    for s, f in ((decX_hyp_h, shift_x), (decY_hyp_h, shift_y), (decZ_hyp_h, shift_z)):
+        if s != 0:
+            hyp_h = f(hyp_h, s)
+
+    # launch grid (:10948-10956): angles from the shifted source, centred on the unshifted edges'
+    ss = [np.float64(x) for x in source_shift]
+    det1 = np.zeros(10)
+    det1[6] = 1.
+    det1[9] = -(s2f_middle + defocus)
+    return BuiltSystem(
+        name=name or "KB_debug pair (KB_define of KBdesign_7params, built from params)",
+        mirrors=[dict(coeffs=[float(x) for x in hyp_v], negative=False),
+                 dict(coeffs=[float(x) for x in hyp_h], negative=False)],
+        det1=[float(x) for x in det1],
+        angle_h=dict(start=float(np.arctan((y1_h - ss[1]) / (x1_h - ss[0]))),
+                     stop=float(np.arctan((y2_h - ss[1]) / (x2_h - ss[0]))), offset=float(np.mean([at1h, at2h]))),
+        angle_v=dict(start=float(np.arctan((y1_v - ss[2]) / (x1_v - ss[0]))),
+                     stop=float(np.arctan((y2_v - ss[2]) / (x2_v - ss[0]))), offset=float(np.mean([at1v, at2v]))),
+        source=[0.0 + ss[0], 0.0 + ss[1], 0.0 + ss[2]],
+        s2f_middle=float(s2f_middle), defocus=float(defocus),
+        meta=dict(params=[float(x) for x in p], design=[float(x) for x in (l1h, l2h, inc_h, mlen_h, wd_v, inc_v,
+                                                                          mlen_v)]),
+    )

@@ -57,6 +57,30 @@ def _akb_native_ok(mod):
             and not getattr(mod, "option_mpmath", False))
 
 
+def _kb_native_ok(mod):
+    """KB_debug's pair as build_kb restates it: option_AKB False, the KB_define design branch
+    (optKBdesign False, :65, :9748) with option_HighNA (:83, :9938) and both mirrors traced
+    (option_2mirror, :66)."""
+    return (not getattr(mod, "option_AKB", True) and not getattr(mod, "optKBdesign", False)
+            and getattr(mod, "option_HighNA", True) and getattr(mod, "option_2mirror", True)
+            and not getattr(mod, "option_mpmath", False))
+
+
+def _kb_debug_for(mod, original):
+    """KB_debug (:9742) with its 'test' mode (auto_focus_NA's, called hundreds of times for a KB
+    system) on the device (autofocus.kb_test, with the module's live KBdesign_7params :100);
+    every other mode runs the reference's own function."""
+    def KB_debug(params, na_ratio_h, na_ratio_v, option, option_legendre=False, source_shift=[0., 0., 0.],
+                 option_save=True, designparams=None):
+        if option == "test" and _kb_native_ok(mod):
+            from .autofocus import kb_test
+            dp = designparams if designparams is not None else getattr(mod, "KBdesign_7params", None)
+            return kb_test(params, source_shift, designparams=dp)
+        return original(params, na_ratio_h, na_ratio_v, option, option_legendre=option_legendre,
+                        source_shift=source_shift, option_save=option_save, designparams=designparams)
+    return KB_debug
+
+
 def _plot_result_debug_for(mod, original):
     """plot_result_debug with its 'test' mode (the one auto_focus_NA and the alignment loops call
     hundreds of times), its 'sep' mode (auto_focus_sep's, sep.py), its 'wave' mode and its 'ray_wave'
@@ -93,11 +117,13 @@ def _plot_result_debug_for(mod, original):
 
 def _auto_focus_for(mod, original):
     """auto_focus_NA (:12746) with every sweep on the device, reading the module's live flags
-    (widesearch :98, option_set :94) as the reference does; KB systems, the mpmath branch and the
-    tandem variants run the reference's own function."""
+    (widesearch :98, option_set :94, option_AKB :80) as the reference does: the Wolter III+I
+    system's sweeps or KB_debug's pair's; the mpmath branch and other systems run the reference's
+    own function."""
     def auto_focus_NA(num_adj_astg, initial_params, na_ratio_h, na_ratio_v, option, option_param,
                       option_disp='ray', option_mode=False, source_shift0=[0., 0., 0.], option_legendre=False):
-        if not _akb_native_ok(mod):
+        kb = _kb_native_ok(mod)
+        if not (_akb_native_ok(mod) or kb):
             return original(num_adj_astg, initial_params, na_ratio_h, na_ratio_v, option, option_param,
                             option_disp=option_disp, option_mode=option_mode, source_shift0=source_shift0,
                             option_legendre=option_legendre)
@@ -105,7 +131,8 @@ def _auto_focus_for(mod, original):
         return native(num_adj_astg, initial_params, na_ratio_h, na_ratio_v, option, option_param,
                       option_disp=option_disp, option_mode=option_mode, source_shift0=source_shift0,
                       option_legendre=option_legendre, widesearch=bool(getattr(mod, "widesearch", False)),
-                      option_set=bool(getattr(mod, "option_set", False)), driver=mod)
+                      option_set=bool(getattr(mod, "option_set", False)), option_AKB=not kb,
+                      kb_design=getattr(mod, "KBdesign_7params", None), driver=mod)
     return auto_focus_NA
 
 
@@ -139,7 +166,7 @@ def _save_wave_for(mod, original):
     return saveWaveData
 
 
-_PER_MODULE = {"plot_result_debug": _plot_result_debug_for, "auto_focus_NA": _auto_focus_for,
+_PER_MODULE = {"plot_result_debug": _plot_result_debug_for, "auto_focus_NA": _auto_focus_for, "KB_debug": _kb_debug_for,
                "saveWaveData": _save_wave_for, "compare_sep": _compare_sep_for}
 
 _NATIVE = {
@@ -161,6 +188,7 @@ _NATIVE = {
     "extract_affine_square_region": _lazy("affine", "extract_affine_square_region"),
     "psf_calc": None,  # bound per module (_psf_calc_for)
     "plot_result_debug": None,  # bound per module (_PER_MODULE)
+    "KB_debug": None,
     "auto_focus_NA": None,
     "saveWaveData": None,
     "compare_sep": None,

@@ -5,7 +5,8 @@
 auto_focus_NA from the reference's best-alignment params (1800 'test' traces in the reference,
 ~17.5 s in the build container), its pieces (system build, one trace, one 100-plane sweep), a
 batched trace of 256 systems, calc_FoC on a 5 x 5 source grid (25 FoC searches), the 'sep'
-mode and auto_focus_sep ('abrr' and 'matrix').
+mode and auto_focus_sep ('abrr' and 'matrix'), and auto_focus_NA on KB_debug's pair (option_AKB
+False: 1800 KB 'test' traces in the reference, 5.3 s on one core of the build container).
 """
 import argparse
 import json
@@ -95,6 +96,16 @@ def main():
     t, _ = wall(lambda: S.auto_focus_sep(p0.copy(), 9, 21, -2e-5, 2e-5, option="matrix", option_eval="9",
                                          verbose=False))
     res["auto_focus_sep_matrix_ms"] = t * 1e3
+    # KB_debug's pair (option_AKB False)
+    pk = np.zeros(26)
+    pk[0], pk[1] = 2e-3, -1e-4
+    AF.auto_focus_NA(50, pk.copy(), 1, 1, False, "", option_AKB=False, verbose=False)
+    t, _ = wall(lambda: AF.kb_test(np.zeros(26)), reps=20)
+    res["kb_test_mode_ms"] = t * 1e3
+    res["kb_test_mode_reference_ms"] = 2.21
+    t, _ = wall(lambda: AF.auto_focus_NA(50, pk.copy(), 1, 1, False, "", option_AKB=False, verbose=False), reps=3)
+    res["kb_auto_focus_NA_ms"] = t * 1e3
+    res["kb_auto_focus_NA_reference_s"] = 5.28
     print(json.dumps(res, indent=1))
     if args.out:
         with open(args.out, "w") as f:

@@ -251,7 +251,7 @@ def test_batched_trace_equals_single_launches(gpu):
 def test_install_rebinds_test_mode_and_auto_focus(gpu):
     """install() on a driver-like module: plot_result_debug(params, 'test') and auto_focus_NA go to
     the device for the Wolter III+I AKB system and to the module's own functions otherwise
-    (other modes, KB systems, mpmath)"""
+    (other modes, systems not restated, mpmath); KB_debug's pair: tests/test_kb.py"""
     import types
     import akbraytracing_amd
     f = golden(AF)
@@ -269,7 +269,7 @@ def test_install_rebinds_test_mode_and_auto_focus(gpu):
     p = f["af0_start"].copy()
     ret = mod.auto_focus_NA(50, p, 1, 1, False, "")
     assert np.array_equal(np.array(ret[:2]), f["af0_ret"]) and np.array_equal(p, f["af0_params_after"])
-    mod.option_AKB = False  # KB_debug systems: the reference's own loop
+    mod.option_AKB, mod.optKBdesign = False, True  # a KB design branch not restated: the reference's own loop
     assert mod.auto_focus_NA(50, p, 1, 1, False, "") == "orig-af"
     akbraytracing_amd.uninstall(mod)
     assert mod.plot_result_debug(c["params"], "test") == "orig"
