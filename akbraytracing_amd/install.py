@@ -68,14 +68,23 @@ def _kb_native_ok(mod):
 
 def _kb_debug_for(mod, original):
     """KB_debug (:9742) with its 'test' mode (auto_focus_NA's, called hundreds of times for a KB
-    system) on the device (autofocus.kb_test, with the module's live KBdesign_7params :100);
-    every other mode runs the reference's own function."""
+    system; autofocus.kb_test) and its 'ray_wave' mode (driver.kb_ray_wave) on the device, with the
+    module's live KBdesign_7params (:100); every other mode runs the reference's own function."""
     def KB_debug(params, na_ratio_h, na_ratio_v, option, option_legendre=False, source_shift=[0., 0., 0.],
                  option_save=True, designparams=None):
+        dp = designparams if designparams is not None else getattr(mod, "KBdesign_7params", None)
         if option == "test" and _kb_native_ok(mod):
             from .autofocus import kb_test
-            dp = designparams if designparams is not None else getattr(mod, "KBdesign_7params", None)
             return kb_test(params, source_shift, designparams=dp)
+        if (option == "ray_wave" and option_save and _kb_native_ok(mod)
+                and getattr(mod, "wave_num_H", 0) == getattr(mod, "wave_num_V", 1)):
+            # the whole mode on the device (driver.kb_ray_wave), its figures not drawn
+            from .driver import kb_ray_wave
+            return kb_ray_wave(params, mod.wave_num_H, source_shift=source_shift, designparams=dp,
+                               option_HighNA=getattr(mod, "option_HighNA", True),
+                               option_energy=getattr(mod, "option_energy", "EUV"),
+                               widesearch=bool(getattr(mod, "widesearch", False)), option_legendre=option_legendre,
+                               directory=getattr(mod, "directory_name", None))
         return original(params, na_ratio_h, na_ratio_v, option, option_legendre=option_legendre,
                         source_shift=source_shift, option_save=option_save, designparams=designparams)
     return KB_debug

@@ -180,3 +180,79 @@ def test_install_routes_kb_debug_and_kb_auto_focus(gpu):
     finally:
         akbraytracing_amd.uninstall(mod)
     assert mod.KB_debug(f["k0_params"], 1, 1, "test") == "orig-kb"
+
+
+def test_kb_ray_wave_conditions():
+    from akbraytracing_amd.driver import kb_ray_wave_conditions
+    assert kb_ray_wave_conditions() == (1e-4, 13.5)
+    assert kb_ray_wave_conditions(True, "hardXray", True) == (1e-1, 0.135)
+    assert kb_ray_wave_conditions(False, "hardXray") == (1e-5, 1.35)
+    with pytest.raises(ValueError):
+        kb_ray_wave_conditions(True, "visible")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("c", [0, 1, 2])
+def test_kb_ray_wave_vs_reference(gpu, tmp_path, c):
+    """KB_debug(params, 1, 1, 'ray_wave', option_legendre=True) on the device: the griddata points
+    and values, the corrected map psf_calc receives (tests/golden/kb_raywave.npz, recorded from the
+    reference), then the rectification (256 x 256) and Legendre fit against the oracle's
+    composition on the reference's own map; the files the mode writes"""
+    import oracle.affine as OA
+    import oracle.legendre as OLg
+    from akbraytracing_amd.driver import kb_ray_wave
+    g = golden("kb_raywave.npz")
+    n = int(g[f"c{c}_n"])
+    out_dir = tmp_path / "out"
+    r = kb_ray_wave(g[f"c{c}_params"], n, directory=str(out_dir), workdir=str(tmp_path), verbose=False, as_dict=True)
+    run = r["run"]
+    det2 = run["detcenter2"].cpu().numpy()[1:3]
+    want = g[f"c{c}_det2"]
+    # the tilt's angles are the reference's to an ulp of arctan (DESIGN a7)
+    assert np.max(np.abs(det2 - want)) <= 1e-12 * np.max(np.ptp(want, axis=1))
+    w = run["wave2"].cpu().numpy()
+    ref_w = g[f"c{c}_wave2"]
+    assert np.max(np.abs(w - ref_w)) <= 1e-6 * np.ptp(ref_w)
+    corr = r["maps"]["matrixWave2_Corrected"].cpu().numpy()
+    ref = g[f"c{c}_plane_out"]
+    assert np.array_equal(np.isnan(corr), np.isnan(ref))
+    assert np.nanmax(np.abs(corr - ref)) <= 1e-6 * (np.nanmax(ref) - np.nanmin(ref))
+    # past psf_calc: cv2's step is unpinned (absent here); the oracle's composition on the
+    # reference's map
+    rect = OA.extract_affine_square_region(ref / 13.5, target_size=256)
+    assert r["rectified_img"].shape == (256, 256)
+    assert np.array_equal(np.isnan(r["rectified_img"]), np.isnan(rect))
+    assert np.nanmax(np.abs(r["rectified_img"] - rect)) <= 1e-6 * np.nanmax(np.abs(rect))
+    fits, ip = OLg.fit_multi(rect[1:-2, 1:-2], 5)
+    assert np.max(np.abs(r["inner_products"] - ip)) <= 1e-6 * np.max(np.abs(ip))
+    for name in ("psf.npy", "matrixWave2_Corrected(lambda).txt", "rectified_img.txt", "inner_products.txt",
+                 "orders.txt", "pvs.txt", "fit_sum.txt", "pv.txt"):
+        assert (out_dir / name).exists(), name
+    assert (tmp_path / "matrixWave2(nm).txt").exists()
+    # pvs.txt is written before the last entry is set (:11866, :11878)
+    saved = np.loadtxt(out_dir / "pvs.txt")
+    assert saved[-1] == 0.0 and np.array_equal(saved[:-1], r["pvs"][:-1])
+    assert r["pvs"][-1] == np.nanstd(corr / 13.5) * 6 * np.sign(np.sum(r["inner_products"]))
+
+
+@pytest.mark.gpu
+def test_install_routes_kb_ray_wave(gpu, tmp_path, monkeypatch):
+    import types
+    import akbraytracing_amd
+    monkeypatch.chdir(tmp_path)
+    g = golden("kb_raywave.npz")
+    mod = types.ModuleType("fake_driver")
+    mod.option_AKB, mod.option_mpmath, mod.option_HighNA, mod.option_energy = False, False, True, "EUV"
+    mod.wave_num_H = mod.wave_num_V = 33
+    mod.directory_name = str(tmp_path / "d")
+    seen = []
+    mod.KB_debug = lambda params, na_h, na_v, option, **kw: seen.append(option) or "orig-kb"
+    akbraytracing_amd.install(mod)
+    try:
+        ip, orders, pvs = mod.KB_debug(g["c2_params"], 1, 1, "ray_wave", option_legendre=True)
+        assert not seen and len(ip) == 15 and len(pvs) == 16
+        pv = mod.KB_debug(g["c2_params"], 1, 1, "ray_wave")
+        assert np.isfinite(pv) and (tmp_path / "d" / "optical_params.txt").exists()
+        assert mod.KB_debug(g["c2_params"], 1, 1, "ray_wave", option_save=False) == "orig-kb"
+    finally:
+        akbraytracing_amd.uninstall(mod)
