@@ -20,6 +20,11 @@ run on other streams beside step k's pass 2 while the host resamples. Every step
 all of its work inside the timed region. Inputs (the two 1-D angle tables) are resident on the
 device before timing.
 
+--config c2 (configs[1]): the same pipeline through KB_debug's pair at params = 0
+(geometry.build_kb, bit-exact vs the reference's builds; the second plane at the module's
+defocusForWave = 1e-3, :89, as its 'wave' mode places it, :11694-11698): 2 passes x 2 mirrors per
+ray; huygens_pairs_per_s is that config's M2 -> image stage.
+
 Multi-GPU (configs[3], "C4"): weak scaling at C4's per-GPU load, ~1.25e7 rays per rank of a
 round(sqrt(N * 1.25e7))^2 grid - 10000^2 = 1e8 rays, ~1250 V-rows per rank, at N = 8 - in
 contiguous blocks of whole 8192-ray numpy sum buffers (Shard.split), so the cross-rank means are
@@ -74,9 +79,10 @@ def parse():
     p.add_argument("--pad", type=int, default=16)
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--config", choices=("c3", "c5"), default="c3",
+    p.add_argument("--config", choices=("c2", "c3", "c5"), default="c3",
                    help="c3: BASELINE configs[2] (default, the headline); c5: configs[4], the Legendre "
-                        "figure-error OPL perturbation on every ray + a 3-wavelength PSF stack")
+                        "figure-error OPL perturbation on every ray + a 3-wavelength PSF stack; c2: configs[1], "
+                        "the KB pair")
     p.add_argument("--back-stream", type=int, default=1,
                    help="1: queue each step's tilt / OPD / pupil on a second stream, concurrent with the "
                         "next step's FP64-bound pass 1 (0: behind it on one stream)")
@@ -93,13 +99,26 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(seconds):
+def geometry_dict(config):
+    """The traced system as a dict: the recorded AKB fixture (c3, c5) or KB_debug's pair built
+    from params = 0 with its 'wave'-mode second plane (c2)."""
+    if config != "c2":
+        with open(os.path.join(ROOT, "tests", "golden", "akb_geometry.json")) as f:
+            return json.load(f)
+    import numpy as np
+    from akbraytracing_amd import geometry as G
+    b = G.build_kb(np.zeros(26))
+    det2 = np.zeros(10)
+    det2[6] = 1
+    det2[9] = -(np.float64(b["s2f_middle"]) + np.float64(b["defocus"]) + 1e-3)
+    return dict(b, det2=[float(x) for x in det2], defocus_wave_m=1e-3)
+
+
+def cpu_baseline(seconds, g):
     """The oracle (C restatement, OpenMP, + numpy for the host steps) running the same ray_wave
     pipeline on a 1001^2 grid, repeated for about `seconds`."""
     import oracle
     import oracle.pipeline as OPL
-    with open(os.path.join(ROOT, "tests", "golden", "akb_geometry.json")) as f:
-        g = json.load(f)
     threads = oracle.max_threads()
     n = 1001
     OPL.akb_ray_wave(g, 65)  # load / warm
@@ -225,7 +244,8 @@ def main():
     from akbraytracing_amd.wavefront import RayWave, Shard, SystemGeometry
 
     dev = torch.device("cuda", torch.cuda.current_device())
-    geom = SystemGeometry.load(os.path.join(ROOT, "tests", "golden", "akb_geometry.json"))
+    gdict = geometry_dict(args.config)
+    geom = SystemGeometry.from_dict(gdict)
     if args.rays is None:
         args.rays = C3_RAYS if world == 1 else C4_RAYS_PER_GPU
     # 3163 at 1 GPU (C3); 10000 at 8 GPUs (C4: 1250 V-rows per rank); SURVEY.md §8(d)
@@ -376,8 +396,9 @@ def main():
     launch_bytes = PASS2_BYTES_PER_RAY * rw.n_local
     achieved = launch_bytes / (k_avg * 1e-3) / 1e9
     prof, prof_file, prof_ok = read_profile()
-    pk = prof.get("kernels", {}).get("pass2", {}) if prof_ok else {}
-    inter_launch = 4 * rw.n_local  # pass 2's intersections per launch (4 mirrors)
+    # the profile describes the 4-mirror pass-2 kernel (C3's): no PMC fields for the KB pair
+    pk = prof.get("kernels", {}).get("pass2", {}) if prof_ok and args.config != "c2" else {}
+    inter_launch = len(geom.mirrors) * rw.n_local  # pass 2's intersections per launch
     # VALU-issue roofline of pass 2: the chip issues at most SIMDS / 4 wave-instructions per clock;
     # with the profiled instructions per intersection that caps the intersection rate
     vpi = (pk["valu_wave_instructions_per_launch"] / pk["intersections_per_launch"]) if pk else None
@@ -396,9 +417,12 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic: deterministic ray grid through the reference's AKB geometry (recorded fixture)",
+        "data": "synthetic: deterministic ray grid through the reference's "
+                + ("KB" if args.config == "c2" else "AKB") + " geometry (recorded fixture)",
         "config": {
-            "workload": ("C3: 4-mirror AKB ray_wave trace (2 passes, tilt, OPD) + 2048^2 PSF" if args.config == "c3"
+            "workload": ("C2: 2-mirror KB ray trace (2 passes, tilt, OPD) + 2048^2 PSF"
+                         + (", ray-row shards" if world > 1 else "") if args.config == "c2" else
+                         "C3: 4-mirror AKB ray_wave trace (2 passes, tilt, OPD) + 2048^2 PSF" if args.config == "c3"
                          and world == 1 else
                          "C4: 4-mirror AKB ray_wave trace, ray-row shards, + 2048^2 PSF" if args.config == "c3" else
                          "C5: 4-mirror AKB ray_wave trace with per-ray Legendre OPL perturbation + "
@@ -468,7 +492,7 @@ def main():
         out["huygens_pairs_per_s"] = huygens_rate(last_out)
         out["faithful_psf_chain_ms"] = faithful_psf_chain(rw, last_out, args.pupil)
     if world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, gdict)
     print(json.dumps(out), flush=True)
 
 

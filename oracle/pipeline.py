@@ -99,7 +99,8 @@ def tilt(refl, last_hit, det_pre, det_ghij):
 
 def akb_ray_wave(geom, n, source=None):
     """The 'ray_wave' hot path of the Wolter 3-1 plot_result_debug on an n x n grid, up to the
-    griddata inputs (:3689). Returns a dict of the intermediate arrays."""
+    griddata inputs (:3689); with a 2-mirror geometry KB_debug's 'wave' trace and OPD (:11629-11700).
+    Returns a dict of the intermediate arrays."""
     src = np.zeros((3, n * n)) if source is None else source
     mirrors = geom["mirrors"]
     det1 = np.zeros(10)
@@ -118,10 +119,13 @@ def akb_ray_wave(geom, n, source=None):
     r4r, p4r, det, (ty, tz, fa) = tilt(r4, hits[-1], det_pre, geom["det1"][6:10])
     det_2 = O.plane_ray_intersection(det2, r4r, p4r)
     d4 = O.seglen(p4r, det)
-    total = segs[0] + segs[1] + segs[2] + segs[3] + d4
+    mirr = segs[0]
+    for sg in segs[1:]:  # left to right, as the drivers write dist0to1 + dist1to2 + ... (K = 4 or 2)
+        mirr = mirr + sg
+    total = mirr + d4
     dist_err = (total - np.nanmean(total)) * 1e9
     d4b = O.seglen(p4r, det_2)
-    total2 = segs[0] + segs[1] + segs[2] + segs[3] + d4b
+    total2 = mirr + d4b
     dist_err2 = (total2 - np.nanmean(total2)) * 1e9
     mean_focus = np.nanmean(det, axis=1)
     sph = O.seglen(np.broadcast_to(mean_focus[:, None], det_2.shape).copy(), det_2) * 1e9

@@ -256,3 +256,24 @@ def test_install_routes_kb_ray_wave(gpu, tmp_path, monkeypatch):
         assert mod.KB_debug(g["c2_params"], 1, 1, "ray_wave", option_save=False) == "orig-kb"
     finally:
         akbraytracing_amd.uninstall(mod)
+
+
+@pytest.mark.gpu
+def test_kb_c2_pipeline_vs_oracle(gpu):
+    """bench.py --config c2's system (KB_debug's pair at params = 0, second plane at defocusForWave)
+    through RayWave - pass 1, resample, pass 2, tilt, OPD - against the oracle's pipeline on the
+    same geometry: resampled tables bitwise, the hits and OPD to the tilt's ulp"""
+    import oracle.pipeline as OPL
+    import bench
+    from akbraytracing_amd.wavefront import RayWave, SystemGeometry
+    g = bench.geometry_dict("c2")
+    ref = OPL.akb_ray_wave(g, 65)
+    out = RayWave(SystemGeometry.from_dict(g), 65).run(keep_rotated=True, full=True)
+    assert out["flags"] == (0, 0)
+    assert np.array_equal(out["tan_h2"].cpu().numpy(), ref["tan_h2"])
+    assert np.array_equal(out["last_hit"].cpu().numpy(), ref["hits"][-1])
+    for key in ("detcenter", "detcenter2"):
+        got, want = out[key].cpu().numpy(), ref[key]
+        assert np.max(np.abs(got - want)) <= 64 * np.max(np.spacing(np.abs(want))), key
+    for key in ("dist_err2", "wave2"):
+        assert np.max(np.abs(out[key].cpu().numpy() - ref[key])) <= 1e-4, key
