@@ -68,7 +68,8 @@ def _kb_native_ok(mod):
 
 def _kb_debug_for(mod, original):
     """KB_debug (:9742) with its 'test' mode (auto_focus_NA's, called hundreds of times for a KB
-    system; autofocus.kb_test) and its 'ray_wave' mode (driver.kb_ray_wave) on the device, with the
+    system; autofocus.kb_test), its 'sep' mode (auto_focus_sep's; sep.kb_sep) and its 'ray_wave'
+    mode (driver.kb_ray_wave) on the device, with the
     module's live KBdesign_7params (:100); every other mode runs the reference's own function."""
     def KB_debug(params, na_ratio_h, na_ratio_v, option, option_legendre=False, source_shift=[0., 0., 0.],
                  option_save=True, designparams=None):
@@ -76,6 +77,9 @@ def _kb_debug_for(mod, original):
         if option == "test" and _kb_native_ok(mod):
             from .autofocus import kb_test
             return kb_test(params, source_shift, designparams=dp)
+        if option == "sep" and _kb_native_ok(mod):
+            from .sep import kb_sep
+            return kb_sep(params, source_shift, designparams=dp, widesearch=bool(getattr(mod, "widesearch", False)))
         if (option == "ray_wave" and option_save and _kb_native_ok(mod)
                 and getattr(mod, "wave_num_H", 0) == getattr(mod, "wave_num_V", 1)):
             # the whole mode on the device (driver.kb_ray_wave), its figures not drawn

@@ -113,24 +113,42 @@ def plot_result_sep(params, source_shift=(0.0, 0.0, 0.0), option_tilt=True, *, o
     system built from params (geometry.build_akb): compare_sep's twelve outputs, or np.inf where the
     reference returns np.inf."""
     from . import geometry as G
-    from .reduce import means_to_host, np_sum
-    from .wavedata import two_pass_trace
     b = G.build_akb(params, source_shift=source_shift, option_set=option_set)
     if not isinstance(b, dict):
         return b
-    n = int(ray_num)
-    hits, refl, det = two_pass_trace(b, n, "sep")
     if not option_tilt:
         # the reference reaches compare_sep with reflect4_rotated unbound (:3605)
         raise UnboundLocalError("local variable 'reflect4_rotated' referenced before assignment")
+    return _sep_of_built(b, int(ray_num), np.nanmean, widesearch, verbose)
+
+
+def kb_sep(params, source_shift=(0.0, 0.0, 0.0), *, designparams=None, widesearch=False, ray_num=53,
+           verbose=True):
+    """KB_debug(params, na_ratio_h, na_ratio_v, 'sep') (:9742; reset_p0's resample :11001-11054,
+    the np.mean tilt :11703-11717, compare_sep :11719-11721) for the KB pair of geometry.build_kb:
+    compare_sep's twelve outputs, or np.inf where the reference returns np.inf."""
+    from . import geometry as G
+    b = G.build_kb(params, source_shift=source_shift, designparams=designparams)
+    if not isinstance(b, dict):
+        return b
+    return _sep_of_built(b, int(ray_num), np.mean, widesearch, verbose)
+
+
+def _sep_of_built(b, n, mean, widesearch, verbose):
+    """The two-pass trace, the tilt by mean(arctan) of the exit slopes (np.nanmean in
+    plot_result_debug, np.mean in KB_debug), the rotation about np.mean(detcenter) and compare_sep
+    on the plane x = s2f_middle + defocus."""
+    from .reduce import means_to_host, np_sum
+    from .wavedata import two_pass_trace
+    hits, refl, det = two_pass_trace(b, n, "sep")
     ang = refl.cpu().numpy()
     import warnings
     with warnings.catch_warnings():
         warnings.simplefilter("ignore", RuntimeWarning)  # nanmean of an all-NaN trace warns, gives NaN
-        theta_y = -np.nanmean(np.arctan(ang[2, :] / ang[0, :]))
-        theta_z = np.nanmean(np.arctan(ang[1, :] / ang[0, :]))
+        theta_y = -mean(np.arctan(ang[2, :] / ang[0, :]))
+        theta_z = mean(np.arctan(ang[1, :] / ang[0, :]))
     refl_rot = P.rotate_vectors(refl, -theta_y, -theta_z)
-    (focus,) = means_to_host([np_sum(det)])  # np.mean(detcenter, axis=1) (:3591)
+    (focus,) = means_to_host([np_sum(det)])  # np.mean(detcenter, axis=1) (:3591, :11708)
     pts_rot = P.rotate_points(hits[-1], focus, -theta_y, -theta_z)
     coeffs_det = np.zeros(10)
     coeffs_det[6] = 1
@@ -184,26 +202,29 @@ def _linearfit(a, b, verbose):
 
 
 def auto_focus_sep(initial_params0, adj_param1, adj_param2, la, ua, option='none', option_eval=None, *,
-                   widesearch=False, option_set=True, verbose=True):
-    """auto_focus_sep (:12897-13318) for the AKB system (option_AKB): auto_focus_NA and the 'sep'
-    analysis on the device for each of the five values of params[adj_param1] = params[adj_param2],
-    the reference's measures, and its returns ('abrr': the measure vector of one 'sep' run of the
-    focused params; 'matrix': the fitted slopes / intercepts per option_eval; otherwise None).
-    The reference's figures ('matrix') are not drawn."""
+                   widesearch=False, option_set=True, option_AKB=True, kb_design=None, verbose=True):
+    """auto_focus_sep (:12897-13318): auto_focus_NA and the 'sep' analysis on the device for each of
+    the five values of params[adj_param1] = params[adj_param2], the reference's measures, and its
+    returns ('abrr': the measure vector of one 'sep' run of the focused params; 'matrix': the fitted
+    slopes / intercepts per option_eval; otherwise None). option_AKB False: KB_debug's pair
+    (auto_focus_NA's KB sweeps, kb_sep; the KB measure set a0, a2, a4 by default, :12978, :13158;
+    kb_design: the module's KBdesign_7params). The reference's figures ('matrix') are not drawn."""
     from .autofocus import _SystemCache, auto_focus_NA
-    cache = _SystemCache(option_set, 53)
+    cache = _SystemCache(option_set, 53, "akb" if option_AKB else "kb", kb_design)
 
     def focus(p):
         return auto_focus_NA(50, p, 1, 1, False, '', widesearch=widesearch, option_set=option_set,
-                             verbose=verbose, cache=cache)
+                             option_AKB=option_AKB, kb_design=kb_design, verbose=verbose, cache=cache)
 
     def sep(p):
+        if not option_AKB:
+            return kb_sep(p, designparams=kb_design, widesearch=widesearch, verbose=verbose)
         return plot_result_sep(p, option_set=option_set, widesearch=widesearch, verbose=verbose)
 
     if option == 'abrr':
         _, _, initial_params = focus(initial_params0)
         m = _abrr(sep(initial_params))
-        keys = _ABRR_SETS.get(option_eval, _ABRR_SETS["9"]).split()
+        keys = _ABRR_SETS.get(option_eval, _ABRR_SETS["9" if option_AKB else "KB"]).split()
         return np.array([m[k] for k in keys])
 
     initial_params = initial_params0.copy()
@@ -219,10 +240,10 @@ def auto_focus_sep(initial_params0, adj_param1, adj_param2, la, ua, option='none
         size_v_param[j], size_h_param[j], initial_params = focus(initial_params)
         steps.append(sep(initial_params))
         astig[j] = initial_params[1]
-    return sep_summary(a_param, size_h_param, steps, option, option_eval, verbose)
+    return sep_summary(a_param, size_h_param, steps, option, option_eval, verbose, option_AKB=option_AKB)
 
 
-def sep_summary(a_param, size_h_param, steps, option='none', option_eval=None, verbose=True):
+def sep_summary(a_param, size_h_param, steps, option='none', option_eval=None, verbose=True, option_AKB=True):
     """What auto_focus_sep forms from its five 'sep' results (:13029-13316): the coma / focus-length
     measures, the printed argmins, and for option='matrix' the scikit-learn line fits, returned per
     option_eval (None otherwise). Host numpy, as the reference."""
@@ -285,5 +306,7 @@ def sep_summary(a_param, size_h_param, steps, option='none', option_eval=None, v
         return np.array([m0, m1, m2, m3, m4, m8, m9])
     if option_eval == 'MinimizeH':
         return a_param[np.argmin(size_h_param)]
+    if not option_AKB:
+        return np.array([m0, m2, m4])
     return np.array([m0, m1, m2, m3, m4, m6, m7, m8, m9])
 
