@@ -68,8 +68,9 @@ def _kb_native_ok(mod):
 
 def _kb_debug_for(mod, original):
     """KB_debug (:9742) with its 'test' mode (auto_focus_NA's, called hundreds of times for a KB
-    system; autofocus.kb_test), its 'sep' mode (auto_focus_sep's; sep.kb_sep) and its 'ray_wave'
-    mode (driver.kb_ray_wave) on the device, with the
+    system; autofocus.kb_test), its 'sep' mode (auto_focus_sep's; sep.kb_sep), its 'wave' mode
+    (saveWaveData's; wavedata.kb_wave) and its 'ray_wave' mode (driver.kb_ray_wave) on the device,
+    with the
     module's live KBdesign_7params (:100); every other mode runs the reference's own function."""
     def KB_debug(params, na_ratio_h, na_ratio_v, option, option_legendre=False, source_shift=[0., 0., 0.],
                  option_save=True, designparams=None):
@@ -77,6 +78,12 @@ def _kb_debug_for(mod, original):
         if option == "test" and _kb_native_ok(mod):
             from .autofocus import kb_test
             return kb_test(params, source_shift, designparams=dp)
+        if (option == "wave" and _kb_native_ok(mod) and getattr(mod, "option_rotate", True)
+                and not getattr(mod, "option_avrgsplt", False)
+                and getattr(mod, "wave_num_H", 0) == getattr(mod, "wave_num_V", 1)):
+            from .wavedata import kb_wave
+            return kb_wave(params, mod.wave_num_H, defocus_for_wave=getattr(mod, "defocusForWave", 1e-3),
+                           source_shift=source_shift, designparams=dp)
         if option == "sep" and _kb_native_ok(mod):
             from .sep import kb_sep
             return kb_sep(params, source_shift, designparams=dp, widesearch=bool(getattr(mod, "widesearch", False)))
@@ -162,9 +169,10 @@ def _save_wave_for(mod, original):
     """saveWaveData (:13475) with the 'wave' trace, calc_dS and the grids on the device, reading
     the module's flags (wave_num_H / V, defocusForWave, downsample_*, option_HighNA, option_2mirror,
     option_avrgsplt, option_set) as the reference does, and ending the process with sys.exit() as
-    it does (:13763). KB systems run the reference's own function."""
+    it does (:13763); KB_debug's pair (option_AKB False) through wavedata.kb_wave."""
     def saveWaveData(initial_params, ysize=1e-6, zsize=1e-6):
-        if not (_akb_native_ok(mod) and getattr(mod, "option_rotate", True)):
+        kb = _kb_native_ok(mod) and not getattr(mod, "option_avrgsplt", False)
+        if not ((_akb_native_ok(mod) or kb) and getattr(mod, "option_rotate", True)):
             return original(initial_params, ysize=ysize, zsize=zsize)
         import sys
         from .wavedata import saveWaveData as native
@@ -174,7 +182,8 @@ def _save_wave_for(mod, original):
                downsample=tuple(g(k, 0) for k in ("downsample_h1", "downsample_v1", "downsample_h2", "downsample_v2",
                                                   "downsample_h_f", "downsample_v_f")),
                option_set=bool(g("option_set", False)), option_HighNA=g("option_HighNA", True),
-               option_2mirror=g("option_2mirror", True), option_avrgsplt=g("option_avrgsplt", False))
+               option_2mirror=g("option_2mirror", True), option_avrgsplt=g("option_avrgsplt", False),
+               option_AKB=not kb, kb_design=g("KBdesign_7params", None))
         sys.exit()
     return saveWaveData
 

@@ -300,26 +300,81 @@ def plot_result_wave(params, ray_num, *, defocus_for_wave=1e-3, option_set=True,
     return tuple(x.cpu().numpy() if isinstance(x, torch.Tensor) else x for x in out)
 
 
+def kb_wave(params, ray_num, *, defocus_for_wave=1e-3, source_shift=(0.0, 0.0, 0.0), designparams=None,
+            as_torch=False):
+    """KB_debug(params, na_ratio_h, na_ratio_v, 'wave') (AKB_raytrace_20250312.py:10948-11054,
+    :11629-11701; option_rotate True, option_avrgsplt False) on the device for the KB pair of
+    geometry.build_kb on a ray_num x ray_num grid: pass 1, reset_p0's equal-angle resample, pass 2,
+    the np.mean tilt, both mirror grids and the (unshifted) source rotated about
+    np.mean(detcenter, axis=1), the re-intersected detector and, when |defocus_for_wave| > 1e-9, the
+    defocused one. Returns the reference's tuple: (source, vmirr_hyp, hmirr_hyp, detcenter[,
+    detcenter2], ray_num_H, ray_num_V, vmirr_norm, hmirr_norm, vec0to1, vec1to2), or np.inf where
+    the reference returns np.inf."""
+    from . import geometry as G
+    from . import primitives as P
+    from .reduce import means_to_host, np_sum
+    b = G.build_kb(params, source_shift=source_shift, designparams=designparams)
+    if not isinstance(b, dict):
+        return b
+    n = int(ray_num)
+    dev = D.device()
+    hits, refl, det = two_pass_trace(b, n, "wave")
+    ang = refl.cpu().numpy()
+    theta_y = -np.mean(np.arctan(ang[2, :] / ang[0, :]))  # :11634-11635
+    theta_z = np.mean(np.arctan(ang[1, :] / ang[0, :]))
+    (focus,) = means_to_host([np_sum(det)])  # np.mean(detcenter, axis=1) of pass 2's hits (:11639)
+    source0 = torch.zeros((3, 1), dtype=D.F64, device=dev)
+    refl_rot = P.rotate_vectors(refl, -theta_y, -theta_z)
+    hmirr = P.rotate_points(hits[1], focus, -theta_y, -theta_z)
+    src_rot = P.rotate_points(source0, focus, -theta_y, -theta_z)
+    vmirr = P.rotate_points(hits[0], focus, -theta_y, -theta_z)
+    detcenter = P.plane_ray_intersection(b["det1"], refl_rot, hmirr)  # :11683-11686
+    vec0to1 = P.normalize_vector(vmirr - src_rot)
+    vec1to2 = P.normalize_vector(hmirr - vmirr)
+    vec2to3 = P.normalize_vector(detcenter - hmirr)
+    vmirr_norm = P.normalize_vector((-vec1to2 + vec0to1) / 2)
+    hmirr_norm = P.normalize_vector((-vec2to3 + vec1to2) / 2)
+    out = [src_rot, vmirr, hmirr, detcenter]
+    if np.abs(defocus_for_wave) > 1e-9:
+        c2 = np.zeros(10)
+        c2[6] = 1
+        c2[9] = -(np.float64(b["s2f_middle"]) + np.float64(b["defocus"]) + defocus_for_wave)
+        out.append(P.plane_ray_intersection(c2, refl_rot, hmirr))
+    out += [n, n, vmirr_norm, hmirr_norm, vec0to1, vec1to2]
+    if as_torch:
+        return tuple(out)
+    return tuple(x.cpu().numpy() if isinstance(x, torch.Tensor) else x for x in out)
+
+
 def saveWaveData(initial_params, ysize=1e-6, zsize=1e-6, *, ray_num_H=65, ray_num_V=None, directory=None,
                  defocus_for_wave=1e-3, downsample=(0, 0, 0, 0, 0, 0), option_set=True, option_HighNA=True,
-                 option_2mirror=True, option_avrgsplt=False, timestamp=None):
+                 option_2mirror=True, option_avrgsplt=False, timestamp=None, option_AKB=True, kb_design=None):
     """saveWaveData (AKB_raytrace_20250312.py:13475-13764) for the AKB system, without its final
     sys.exit(): the 'wave' run (plot_result_wave), downsample_array_3_n of every grid when the grid
     is odd (:13489-13497, factors (h1, v1, h2, v2, h_f, v_f) = the module's downsample_* flags), the
     area elements on the device, and the file set into `directory` (default output_<timestamp>,
     as the reference). Returns the directory. The module flags the reference reads (wave_num_H /
     wave_num_V, defocusForWave, option_HighNA, option_2mirror, option_avrgsplt, option_set) are
-    keyword arguments here; install() passes the module's live values."""
+    keyword arguments here; install() passes the module's live values. option_AKB False: KB_debug's
+    pair (kb_wave; kb_design = the module's KBdesign_7params) and its two-mirror file set."""
     from datetime import datetime
     ray_num_V = ray_num_H if ray_num_V is None else ray_num_V
     if ray_num_V != ray_num_H:
-        raise ValueError("the AKB 'wave' grid is square (ray_num = wave_num_H, :1890-1893)")
-    r = plot_result_wave(initial_params, ray_num_H, defocus_for_wave=defocus_for_wave, option_set=option_set)
+        raise ValueError("the 'wave' grid is square (ray_num = wave_num_H, :1890-1893, :10412-10415)")
+    two = np.abs(defocus_for_wave) > 1e-9
+    if option_AKB:
+        r = plot_result_wave(initial_params, ray_num_H, defocus_for_wave=defocus_for_wave, option_set=option_set)
+    else:
+        r = kb_wave(initial_params, ray_num_H, defocus_for_wave=defocus_for_wave, designparams=kb_design)
     if not isinstance(r, tuple):
         raise TypeError("cannot unpack non-iterable float object")  # the reference unpacks np.inf
-    two = np.abs(defocus_for_wave) > 1e-9
-    source, vmirr_hyp, hmirr_hyp, vmirr_ell, hmirr_ell, detcenter = r[:6]
-    detcenter2 = r[6] if two else None
+    if option_AKB:
+        source, vmirr_hyp, hmirr_hyp, vmirr_ell, hmirr_ell, detcenter = r[:6]
+        detcenter2 = r[6] if two else None
+    else:
+        source, vmirr_hyp, hmirr_hyp, detcenter = r[:4]
+        vmirr_ell = hmirr_ell = None
+        detcenter2 = r[4] if two else None
     if ray_num_H % 2 != 1:
         # the reference only sets the grid sizes inside its odd-grid branch
         raise NameError("name 'size_v1' is not defined")
@@ -327,15 +382,17 @@ def saveWaveData(initial_params, ysize=1e-6, zsize=1e-6, *, ray_num_H=65, ray_nu
     vmirr_hyp, size_v1, size_h1 = downsample_array_3_n(vmirr_hyp, ray_num_V, ray_num_H, h1, v1)
     hmirr_hyp, size_v2, size_h2 = downsample_array_3_n(hmirr_hyp, ray_num_V, ray_num_H, h2, v2)
     detcenter, size_v_f, size_h_f = downsample_array_3_n(detcenter, ray_num_V, ray_num_H, hf, vf)
-    vmirr_ell, _, _ = downsample_array_3_n(vmirr_ell, ray_num_V, ray_num_H, h1, v1)
-    hmirr_ell, _, _ = downsample_array_3_n(hmirr_ell, ray_num_V, ray_num_H, h2, v2)
+    if option_AKB:
+        vmirr_ell, _, _ = downsample_array_3_n(vmirr_ell, ray_num_V, ray_num_H, h1, v1)
+        hmirr_ell, _, _ = downsample_array_3_n(hmirr_ell, ray_num_V, ray_num_H, h2, v2)
     if two:
         detcenter2, _, _ = downsample_array_3_n(detcenter2, ray_num_V, ray_num_H, hf, vf)
     timestamp = timestamp or datetime.now().strftime('%Y%m%d_%H%M%S')
     directory = directory or f"output_{timestamp}"
-    save_wave_data(directory, source, [vmirr_hyp, hmirr_hyp, vmirr_ell, hmirr_ell], ray_num_V, ray_num_H,
+    mirrors = [vmirr_hyp, hmirr_hyp] + ([vmirr_ell, hmirr_ell] if option_AKB else [])
+    save_wave_data(directory, source, mirrors, ray_num_V, ray_num_H,
                    detcenter, detcenter2, params=initial_params, ysize=ysize, zsize=zsize,
-                   defocus_for_wave=defocus_for_wave, option_AKB=True, option_HighNA=option_HighNA,
+                   defocus_for_wave=defocus_for_wave, option_AKB=bool(option_AKB), option_HighNA=option_HighNA,
                    option_2mirror=option_2mirror, option_avrgsplt=option_avrgsplt, timestamp=timestamp,
                    sizes=((size_v1, size_h1), (size_v2, size_h2), (size_v_f, size_h_f)))
     return directory

@@ -277,3 +277,60 @@ def test_kb_c2_pipeline_vs_oracle(gpu):
         assert np.max(np.abs(got - want)) <= 64 * np.max(np.spacing(np.abs(want))), key
     for key in ("dist_err2", "wave2"):
         assert np.max(np.abs(out[key].cpu().numpy() - ref[key])) <= 1e-4, key
+
+
+@pytest.mark.gpu
+def test_kb_wave_mode_bitwise_vs_reference(gpu):
+    """KB_debug(params, 1, 1, 'wave') at 33 x 33: the rotated source, mirror grids, both detector
+    planes, the mirror normals and the segment directions, bit for bit
+    (tests/golden/kb_savewave_33.npz)"""
+    from akbraytracing_amd.wavedata import kb_wave
+    f = golden("kb_savewave_33.npz")
+    r = kb_wave(f["params"], 33, defocus_for_wave=float(f["defocusForWave"]))
+    names = ("source", "vmirr_hyp", "hmirr_hyp", "detcenter", "detcenter2", "ray_num_H", "ray_num_V", "vmirr_norm",
+             "hmirr_norm", "vec0to1", "vec1to2")
+    assert len(r) == len(names)
+    for name, got in zip(names, r):
+        assert np.array_equal(np.asarray(got), f[f"w_{name}"]), name
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("run", ["plain", "thin"])
+def test_kb_save_wave_data_files_vs_reference(gpu, tmp_path, run):
+    """saveWaveData with option_AKB False (:13483-13487): KB 'wave', downsampling, calc_dS and the
+    two-mirror file set - every array bit for bit, the conditions text byte for byte"""
+    import os
+    from akbraytracing_amd import wavedata as W
+    f = golden("kb_savewave_33.npz")
+    text = str(f[f"{run}_conditions"])
+    stamp = [ln for ln in text.splitlines() if ln.startswith("time: ")][0][6:]
+    folder = W.saveWaveData(f["params"], ray_num_H=33, directory=str(tmp_path / run),
+                            defocus_for_wave=float(f["defocusForWave"]), downsample=tuple(f[f"{run}_downsample"]),
+                            timestamp=stamp, option_AKB=False)
+    for name in ("points_source", "points_M1", "points_M2", "points_gridImage", "points_gridDefocus"):
+        got = np.load(os.path.join(folder, name + ".npy"))
+        want = f[f"{run}_{name}"]
+        assert got.shape == want.shape and np.array_equal(got, want), name
+    assert not os.path.exists(os.path.join(folder, "points_M3.npy"))
+    with open(os.path.join(folder, "calculation_conditions.txt")) as fh:
+        assert fh.read() == text
+
+
+@pytest.mark.gpu
+def test_install_routes_kb_wave(gpu):
+    import types
+    import akbraytracing_amd
+    f = golden("kb_savewave_33.npz")
+    mod = types.ModuleType("fake_driver")
+    mod.option_AKB, mod.option_mpmath, mod.option_rotate, mod.option_avrgsplt = False, False, True, False
+    mod.wave_num_H = mod.wave_num_V = 33
+    mod.defocusForWave = float(f["defocusForWave"])
+    mod.KB_debug = lambda *a, **kw: "orig-kb"
+    akbraytracing_amd.install(mod)
+    try:
+        r = mod.KB_debug(f["params"], 1, 1, "wave")
+        assert np.array_equal(r[4], f["w_detcenter2"])
+        mod.option_avrgsplt = True  # the split-average variant is not restated
+        assert mod.KB_debug(f["params"], 1, 1, "wave") == "orig-kb"
+    finally:
+        akbraytracing_amd.uninstall(mod)
