@@ -14,7 +14,8 @@
 // k r ~ 7e10 rad: one ulp of r moves the phase by ~1e-5 rad. The phase -k r is reduced modulo
 // pi/2 by a five-piece Cody-Waite split (13-bit pieces: n pi/2 exact for |n| < 2^40, residual
 // 2^-65 rad) instead of the library's Payne-Hanek path, and sin / cos come from fdlibm's kernel
-// polynomials (< 1 ulp); 1/r is rcp + one Newton step (< 1 ulp). The complex multiply-accumulate
+// polynomials (< 1 ulp), the quadrant from the rounding shifter's low bits; 1/r comes from the
+// distance's own rsq after one Newton step (~1e-13 relative). The complex multiply-accumulate
 // uses explicit FMAs. All of it is tolerance-checked against the oracle (numpy's own sum is
 // pairwise, so the field is not bitwise anyway).
 #include <math.h>
@@ -25,24 +26,42 @@ namespace akb {
 
 constexpr int kHuyBlock = 256;
 constexpr int kHuyTile = 256;  // sources per LDS tile (5 doubles each = 10 KiB)
-constexpr int kTPL = 2;        // targets per lane
+#ifndef AKB_HUY_TPL
+#define AKB_HUY_TPL 2
+#endif
+constexpr int kTPL = AKB_HUY_TPL;  // targets per lane
 
-// correctly rounded sqrt for the pair distances without the library's tiny / huge-input paths:
-// sqrt_cr's core (akb_common.h) for x in [2^-767, 2^1000] — every distance between points metres
-// apart — and 0 for x = 0 (a target on a source, where the reference's amplitude is inf too);
-// anything else (never formed here) would come out NaN
-__device__ __forceinline__ double sqrt_pair(double x) {
-    const double out = sqrt_core(x);
-    return x == 0.0 ? 0.0 : out;
+// Pair distance and half its reciprocal from one rsq: r = sqrt(x) correctly rounded (sqrt_core's
+// sequence, akb_common.h, exact for x in [2^-767, 2^1000] - every distance between points metres
+// apart) and h ~ 0.5 / r after one Newton step (relative error ~1e-13, one-signed; the factor 2 is
+// applied to the sums once at the end, exactly). x = 0 (a target on a source, where the
+// reference's amplitude is inf too) gives r = 0.
+__device__ __forceinline__ void dist_half_inv(double x, double& r, double& h) {
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y;
+    h = y * 0.5;
+    const double e = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, e, g);
+    const double d = __builtin_fma(-g, g, x);
+    h = __builtin_fma(h, e, h);
+    g = __builtin_fma(d, h, g);
+    const double d2 = __builtin_fma(-g, g, x);
+    const double out = __builtin_fma(d2, h, g);
+    r = x == 0.0 ? 0.0 : out;
+}
+
+constexpr double kShift = 0x1.8p52;  // t = x 2/pi + 1.5 2^52 holds rint(x 2/pi) in its low mantissa bits
+
+// phases beyond the fast range (|x 2/pi| >= 2^40; never formed by points metres apart at EUV k):
+// the library's sincos, out of line so its Payne-Hanek registers stay out of the loop
+__device__ __attribute__((noinline)) void sincos_slow(double x, double& sn, double& cs) {
+    sincos(x, &sn, &cs);
 }
 
 // sin and cos of x for |x| < 2^40 pi/2 (the library call beyond)
 __device__ __forceinline__ void sincos_phase(double x, double& sn, double& cs) {
-    const double q = rint(x * 0x1.45f306dc9c883p-1);  // x * 2/pi
-    if (__builtin_expect(!(fabs(q) < 0x1p40), 0)) {
-        sincos(x, &sn, &cs);
-        return;
-    }
+    const double t = __builtin_fma(x, 0x1.45f306dc9c883p-1, kShift);  // rint(x * 2/pi) + shift
+    const double q = t - kShift;
     double f = __builtin_fma(-q, 0x1.9220000000000p+0, x);
     f = __builtin_fma(-q, -0x1.2af0000000000p-18, f);
     f = __builtin_fma(-q, 0x1.0b40000000000p-34, f);
@@ -60,11 +79,15 @@ __device__ __forceinline__ void sincos_phase(double x, double& sn, double& cs) {
     const double hz = 0.5 * z;
     const double w = 1.0 - hz;
     const double c0 = w + (((1.0 - w) - hz) + z * rc);
-    const int k = (int)__builtin_fma(-4.0, floor(q * 0.25), q);  // q mod 4, exact for |q| < 2^40
-    const double a = (k & 1) ? c0 : s0;  // sin(x) = s0, c0, -s0, -c0 for k = 0..3
-    const double b = (k & 1) ? s0 : c0;  // cos(x) = c0, -s0, -c0, s0
-    sn = (k & 2) ? -a : a;
-    cs = ((k + 1) & 2) ? -b : b;
+    // q mod 4 = the shifter's low mantissa bits (2^51 + q, and 2^51 = 0 mod 4, negative q too)
+    const unsigned k = (unsigned)__double2loint(t);
+    const bool odd = k & 1u;
+    const double a = odd ? c0 : s0;  // sin(x) = s0, c0, -s0, -c0 for k = 0..3
+    const double b = odd ? s0 : c0;  // cos(x) = c0, -s0, -c0, s0
+    // the quadrant's signs as sign-bit flips of the high words (no compares or selects)
+    sn = __hiloint2double(__double2hiint(a) ^ (int)((k << 30) & 0x80000000u), __double2loint(a));
+    cs = __hiloint2double(__double2hiint(b) ^ (int)(((k + 1u) << 30) & 0x80000000u), __double2loint(b));
+    if (__builtin_expect(!(fabs(q) < 0x1p40), 0)) sincos_slow(x, sn, cs);
 }
 
 __global__ void __launch_bounds__(kHuyBlock) k_huygens(const double* __restrict__ tx,
@@ -113,9 +136,8 @@ __global__ void __launch_bounds__(kHuyBlock) k_huygens(const double* __restrict_
                 const double dx = px[t] - xj;
                 const double dy = py[t] - yj;
                 const double dz = pz[t] - zj;
-                const double r = sqrt_pair(dx * dx + dy * dy + dz * dz);
-                double amp = __builtin_amdgcn_rcp(r);
-                amp = __builtin_fma(amp, __builtin_fma(-r, amp, 1.0), amp);
+                double r, amp;  // amp = 1 / (2 r)
+                dist_half_inv(dx * dx + dy * dy + dz * dz, r, amp);
                 const double ph = negk * r;
                 double sn, cs;
                 sincos_phase(ph, sn, cs);
@@ -130,8 +152,8 @@ __global__ void __launch_bounds__(kHuyBlock) k_huygens(const double* __restrict_
     for (int t = 0; t < kTPL; ++t) {
         const int64_t i = base + threadIdx.x + t * kHuyBlock;
         if (i < n) {
-            out[2 * i] = ar[t];
-            out[2 * i + 1] = ai[t];
+            out[2 * i] = 2.0 * ar[t];  // the 1 / (2 r) amplitudes' factor 2, exact
+            out[2 * i + 1] = 2.0 * ai[t];
         }
     }
 }
@@ -167,12 +189,39 @@ __global__ void __launch_bounds__(kBlock) k_scale_field(const double* u, const d
 
 using namespace akb;
 
-// how many source splits a launch uses: enough workgroups to fill the chip (~8 per CU),
-// but at least kMinSplit sources per split
+// workgroups of k_huygens the device holds at once (CUs x resident workgroups per CU), 0 if the
+// runtime cannot say (no device)
+static int huygens_slots() {
+    static int cached = -1;
+    if (cached < 0) {
+        int dev = 0, cus = 0, per_cu = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_huygens, kHuyBlock, 0) == hipSuccess)
+            cached = cus * per_cu;
+        else {
+            (void)hipGetLastError();
+            cached = 0;
+        }
+    }
+    return cached;
+}
+
+#ifndef AKB_HUY_ROUNDS
+#define AKB_HUY_ROUNDS 64
+#endif
+// how many source splits a launch uses: a whole number of rounds of resident workgroups
+// (splits x target blocks = kRounds x the device's slots; measured on the C2 stage: 2052
+// workgroups over 1280 slots, 1.6 rounds, 170.7 ms; 1 round 200 ms, 2 rounds 174, 4 142, 8 125,
+// 16 118, 64 113.6 ms: finer pieces even out the workgroups' finishing times), at least kMinSplit
+// sources per split
 static int huygens_splits(int64_t n, int64_t m) {
+    constexpr int64_t kRounds = AKB_HUY_ROUNDS;
     const int64_t per_block = (int64_t)kHuyBlock * kTPL;
     const int64_t tblocks = (n + per_block - 1) / per_block;
-    const int64_t want = (2048 + tblocks - 1) / tblocks;
+    const int slots = huygens_slots();
+    const int64_t want = slots > 0 ? (kRounds * slots >= tblocks ? kRounds * slots / tblocks : 1)
+                                   : (2048 + tblocks - 1) / tblocks;
     const int64_t kMinSplit = 1024;
     int64_t maxs = (m + kMinSplit - 1) / kMinSplit;
     if (maxs < 1) maxs = 1;
