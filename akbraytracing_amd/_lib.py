@@ -19,7 +19,7 @@ c_int = ctypes.c_int
 c_dbl = ctypes.c_double
 c_vp = ctypes.c_void_p
 MAX_MIRRORS = 7
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 FLAG_MISS = 0x1
 FLAG_ZERO_NORMAL = 0x2
@@ -29,7 +29,7 @@ FLAG_CHAIN_DIR = 1 << 28
 
 # every symbol the header declares (tests check the library exports all of them)
 EXPORTS = [
-    "akb_last_error", "akb_abi_version", "akb_device_count",
+    "akb_last_error", "akb_abi_version", "akb_sources_hash", "akb_device_count",
     "akb_isect_f64", "akb_normal_f64", "akb_reflect_f64", "akb_normalize_f64", "akb_plane_isect_f64",
     "akb_seglen_f64", "akb_rotate_f64", "akb_fill_nan_f64",
     "akb_trace_chain_f64", "akb_chain_desc_size", "akb_tilt_opd_f64", "akb_tilt_params_f64",
@@ -97,6 +97,7 @@ def _declare(L):
     sig = {
         "akb_last_error": ([], ctypes.c_char_p),
         "akb_abi_version": ([], c_int),
+        "akb_sources_hash": ([], ctypes.c_char_p),
         "akb_device_count": ([], c_int),
         "akb_isect_f64": ([c_vp] + v3 + v3 + [c_int, c_i64, c_vp, c_i64, c_vp, c_vp], c_int),
         "akb_normal_f64": ([c_vp] + v3 + [c_i64, c_vp, c_i64, c_int, c_vp, c_vp], c_int),
@@ -193,10 +194,23 @@ def lib():
         _declare(L)
         if L.akb_abi_version() != ABI_VERSION:
             raise AKBError(f"{path} has ABI {L.akb_abi_version()}, the bindings expect {ABI_VERSION}: rebuild")
+        if not os.environ.get("AKB_LIB") and os.path.isdir(_build.CSRC):
+            # provenance: the library must be the build of this tree's sources (a prebuilt .so
+            # shipped beside edited sources is refused, not silently run)
+            want = _build.sources_hash()
+            got = L.akb_sources_hash().decode()
+            if got != want:
+                raise AKBError(f"{path} was built from sources {got[:16]}, the tree's hash {want[:16]}: rebuild "
+                               "(python -m akbraytracing_amd.build)")
         if L.akb_chain_desc_size() != ctypes.sizeof(ChainDesc):
             raise AKBError("akb_chain_desc layout mismatch between include/akb_raytrace.h and _lib.py")
         _LIB = L
     return _LIB
+
+
+def sources_hash():
+    """the akb_sources_hash() of the loaded library"""
+    return lib().akb_sources_hash().decode()
 
 
 def check(status):

@@ -5,6 +5,7 @@
 The library is compiled with -ffp-contract=off: the trace kernels depend on every product and
 sum being rounded separately, in numpy's order, to reproduce the reference bit for bit.
 """
+import hashlib
 import os
 import subprocess
 import sys
@@ -19,6 +20,17 @@ SOURCES = ["akb_trace.hip", "akb_reduce.hip", "akb_huygens.hip", "akb_psf.hip", 
 HEADERS = ["akb_common.h", "akb_sincos.h", "akb_pairwise.h", os.path.join("..", "..", "include", "akb_raytrace.h")]
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = os.environ.get("AKB_OFFLOAD_ARCH", "gfx950")
+
+
+def sources_hash(csrc=CSRC):
+    """sha256 over every compiled source and included header (fixed order, name + bytes). It is
+    compiled into the library (akb_sources_hash) and compared by _lib.lib() at load time."""
+    h = hashlib.sha256()
+    for rel in SOURCES + HEADERS:
+        h.update(os.path.basename(rel).encode() + b"\0")
+        with open(os.path.join(csrc, rel), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
 
 
 def _newest(paths):
@@ -38,7 +50,7 @@ def build(force=False, verbose=True):
     os.makedirs(LIBDIR, exist_ok=True)
     hipcc = os.path.join(ROCM, "bin", "hipcc")
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-function", "-o", SO + ".tmp"]
+           "-Wall", "-Wno-unused-function", f'-DAKB_SOURCES_HASH="{sources_hash()}"', "-o", SO + ".tmp"]
     cmd += [os.path.join(CSRC, s) for s in SOURCES]
     cmd += [f"-L{ROCM}/lib", "-lrocfft", f"-Wl,-rpath,{ROCM}/lib"]
     if verbose:

@@ -1473,6 +1473,10 @@ extern "C" {
 
 const char* akb_last_error(void) { return g_last_error.c_str(); }
 int akb_abi_version(void) { return AKB_ABI_VERSION; }
+#ifndef AKB_SOURCES_HASH
+#define AKB_SOURCES_HASH "unknown"
+#endif
+const char* akb_sources_hash(void) { return AKB_SOURCES_HASH; }
 int akb_device_count(void) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;

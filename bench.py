@@ -229,6 +229,11 @@ def huygens_rate(out):
             "stage": "M2 -> 65x65 image grid (configs[1]'s stage shape, sources from this trace)"}
 
 
+def _lib_hash():
+    from akbraytracing_amd import _lib
+    return _lib.sources_hash()
+
+
 def main():
     args = parse()
     args.warmup = max(args.warmup, 3 if args.fuse >= 2 else 1)
@@ -481,6 +486,9 @@ def main():
         # where the PMC-derived fields above come from (null when no profile matches the sources)
         "profile": {"file": prof_file, "matches_sources": prof_ok, "git_head": prof.get("git_head"),
                     "kernel": pk.get("kernel")},
+        # provenance: sha256 of the kernel sources compiled into the loaded libakb_hip.so (the
+        # loader refuses a library whose hash differs from this tree's, akbraytracing_amd/_lib.py)
+        "lib_sources_hash": _lib_hash(),
     }
     if single_ms is not None:
         out["single_run_ms"] = single_ms

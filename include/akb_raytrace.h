@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define AKB_ABI_VERSION 11
+#define AKB_ABI_VERSION 12
 
 /* status codes */
 #define AKB_OK 0
@@ -64,6 +64,10 @@ extern "C" {
 
 const char* akb_last_error(void);
 int akb_abi_version(void);
+/* sha256 (hex) of the sources this library was compiled from: every csrc/ file the build compiles
+ * or includes plus this header, as akbraytracing_amd/build.py:sources_hash() forms it. The Python
+ * binding refuses a library whose hash differs from the tree's (a stale prebuilt .so). */
+const char* akb_sources_hash(void);
 /* number of visible HIP devices (0 on a host without GPU; never fails) */
 int akb_device_count(void);
 

@@ -33,6 +33,22 @@ def test_abi_version_and_struct_layout():
     assert L.akb_device_count() >= 0
 
 
+def test_library_carries_the_tree_sources_hash(tmp_path):
+    """Provenance: the loaded library's akb_sources_hash() is the tree's, and a source edit changes
+    the tree's hash (so _lib.lib() would refuse the stale library)."""
+    import shutil
+    from akbraytracing_amd import _lib, build
+    assert _lib.sources_hash() == build.sources_hash()
+    csrc = tmp_path / "pkg" / "csrc"  # the header sits at csrc/../../include, as in the tree
+    shutil.copytree(build.CSRC, csrc)
+    os.makedirs(tmp_path / "include")
+    shutil.copy(os.path.join(ROOT, "include", "akb_raytrace.h"), tmp_path / "include")
+    assert build.sources_hash(str(csrc)) == build.sources_hash()
+    with open(csrc / "akb_trace.hip", "a") as f:
+        f.write("\n// edit\n")
+    assert build.sources_hash(str(csrc)) != build.sources_hash()
+
+
 def test_invalid_arguments_are_reported_not_crashed():
     from akbraytracing_amd import _lib
     L = _lib.lib()
