@@ -45,13 +45,27 @@ def needs_build():
 
 
 def build(force=False, verbose=True):
+    """Compile each source to an object in parallel (hipcc -c), then link the shared library."""
     if not force and not needs_build():
         return SO
     os.makedirs(LIBDIR, exist_ok=True)
+    objdir = os.path.join(LIBDIR, "obj")
+    os.makedirs(objdir, exist_ok=True)
     hipcc = os.path.join(ROCM, "bin", "hipcc")
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-function", f'-DAKB_SOURCES_HASH="{sources_hash()}"', "-o", SO + ".tmp"]
-    cmd += [os.path.join(CSRC, s) for s in SOURCES]
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-Wall",
+             "-Wno-unused-function", f'-DAKB_SOURCES_HASH="{sources_hash()}"']
+    jobs, objs = [], []
+    for src in SOURCES:
+        obj = os.path.join(objdir, os.path.splitext(src)[0] + ".o")
+        objs.append(obj)
+        cmd = [hipcc] + flags + ["-c", os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        jobs.append((src, subprocess.Popen(cmd)))
+    failed = [src for src, p in jobs if p.wait() != 0]
+    if failed:
+        raise subprocess.CalledProcessError(1, f"hipcc -c {' '.join(failed)}")
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", SO + ".tmp"] + objs
     cmd += [f"-L{ROCM}/lib", "-lrocfft", f"-Wl,-rpath,{ROCM}/lib"]
     if verbose:
         print(" ".join(cmd), flush=True)

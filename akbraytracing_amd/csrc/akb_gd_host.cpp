@@ -12,9 +12,13 @@
 // the same for the two sub-chains it leaves. The device checks the result is locally Delaunay
 // against the cell triangles it borders.
 #include <math.h>
+#include <stdlib.h>
 #include <stdint.h>
 
 #include <algorithm>
+#include <functional>
+#include <thread>
+#include <utility>
 #include <vector>
 
 #include "akb_common.h"
@@ -47,8 +51,9 @@ double cross3(const double* x, const double* y, int64_t o, int64_t a, int64_t b)
 // bends of a straight boundary would make (sin of the bend below 1e-12 counts as straight)
 bool right_turn(const double* x, const double* y, int64_t o, int64_t a, int64_t b) {
     const double c = cross3(x, y, o, a, b);
-    const double la = hypot(x[a] - x[o], y[a] - y[o]), lb = hypot(x[b] - x[o], y[b] - y[o]);
-    return c < -1e-12 * la * lb;
+    if (!(c < 0)) return false;
+    const double ax = x[a] - x[o], ay = y[a] - y[o], bx = x[b] - x[o], by = y[b] - y[o];
+    return c < -1e-12 * sqrt((ax * ax + ay * ay) * (bx * bx + by * by));
 }
 
 }  // namespace
@@ -91,91 +96,138 @@ int akb_gd_pockets(const double* rx, const double* ry, int nv, int nh, int cap, 
     AKB_REQUIRE(hv.size() >= 3, "degenerate point set (all boundary points collinear)");
 
     for (int64_t e = 0; e < L; ++e) edge_tri[e] = -1;
-    std::vector<std::vector<int32_t>> extra(L);
-    int32_t n = 0;
-    struct Job {
+    // the ring twice over, so a pocket's chain p .. q (q < p + L) is one contiguous index range
+    std::vector<double> X(2 * L), Y(2 * L);
+    for (int64_t i = 0; i < 2 * L; ++i) {
+        X[i] = rx[i < L ? i : i - L];
+        Y[i] = ry[i < L ? i : i - L];
+    }
+    // the pockets, one per hull edge that skips ring points. They are independent (disjoint chains
+    // and ring edges), so the large ones run on their own threads; triangle ids and chord order are
+    // those of one LIFO walk over all of them (the last hull edge's pocket first), whatever ran where.
+    struct Pocket {
         int64_t p, q;
-        int32_t parent;  // pocket triangle on the other side of (p, q), -1 for a hull edge
-        int slot;        // which of the parent's nbr slots points back here
+        int32_t id0;  // its first triangle id
+        std::vector<std::pair<int64_t, int32_t>> chords;  // (ring position, the other end's vertex id)
+        int err = 0;
+        int64_t err_p = 0, err_q = 0;
     };
-    std::vector<Job> stack;
+    std::vector<Pocket> pockets;
     for (size_t k = 0; k < hv.size(); ++k) {
         int64_t p = hv[k], q = hv[(k + 1) % hv.size()];
         if (q <= p) q += L;
-        if (q - p >= 2) stack.push_back({p, q, -1, -1});
-    }
-    while (!stack.empty()) {
-        const Job J = stack.back();
-        stack.pop_back();
-        const int64_t p = J.p, q = J.q;
-        // the chain point seeing (p, q) under the largest angle: smallest cot = dot / |cross|
-        int64_t best = -1;
-        double best_cot = INFINITY;
-        const int64_t a = p % L, b = q % L;
-        for (int64_t m = p + 1; m < q; ++m) {
-            const int64_t c = m % L;
-            const double ux = rx[a] - rx[c], uy = ry[a] - ry[c];
-            const double vx = rx[b] - rx[c], vy = ry[b] - ry[c];
-            const double cr = fabs(ux * vy - uy * vx);
-            const double dt = ux * vx + uy * vy;
-            const double cot = cr > 0 ? dt / cr : (dt < 0 ? -INFINITY : INFINITY);
-            if (cot < best_cot) {
-                best_cot = cot;
-                best = m;
-            }
-        }
-        if (best < 0 || !(best_cot < INFINITY)) {
-            set_error("griddata: degenerate pocket between ring positions %lld and %lld", (long long)p, (long long)q);
-            return 2;
-        }
-        if (n >= cap) {
-            set_error("griddata: more pocket triangles than cap %d", cap);
-            return 2;
-        }
-        const int64_t m = best;
+        if (q - p < 2) continue;
+        // a hull edge that skips a grid corner: the structured triangulation does not apply
         for (int64_t r = p + 1; r < q; ++r)
             if (R.corner(r)) {
                 set_error("griddata: the convex hull cuts off a grid corner (ring position %lld); the grid is too "
                           "distorted for the structured triangulation", (long long)(r % L));
                 return 2;
             }
-        const int32_t id = n++;
-        tri[3 * id + 0] = (int32_t)R.vertex(p);
-        tri[3 * id + 1] = (int32_t)R.vertex(m);
-        tri[3 * id + 2] = (int32_t)R.vertex(q);
-        // opposite p: edge (m, q); opposite m: edge (q, p); opposite q: edge (p, m)
-        nbr[3 * id + 1] = J.parent < 0 ? -1 : (int32_t)(base + J.parent);
-        if (J.parent >= 0) nbr[3 * J.parent + J.slot] = (int32_t)(base + id);
-        if (q - m == 1) {
-            nbr[3 * id + 0] = -2 - (int32_t)(m % L);
-            edge_tri[m % L] = (int32_t)(base + id);
-        } else {
-            nbr[3 * id + 0] = -1;  // filled by the child
-            stack.push_back({m, q, id, 0});
-        }
-        if (m - p == 1) {
-            nbr[3 * id + 2] = -2 - (int32_t)(p % L);
-            edge_tri[p % L] = (int32_t)(base + id);
-        } else {
-            nbr[3 * id + 2] = -1;
-            stack.push_back({p, m, id, 2});
-        }
-        // the base chord (p, q) joins two ring points that are not grid neighbours
-        extra[a].push_back((int32_t)R.vertex(q));
-        extra[b].push_back((int32_t)R.vertex(p));
+        pockets.push_back({p, q, 0, {}});
     }
-    int64_t k = 0;
-    for (int64_t r = 0; r < L; ++r) {
-        extra_ptr[r] = (int32_t)k;
-        for (int32_t v : extra[r]) {
-            if (k >= 6 * (int64_t)cap) {
-                set_error("griddata: extra-neighbour list overflow");
-                return 2;
+    int32_t total = 0;
+    for (size_t k = pockets.size(); k-- > 0;) {  // the LIFO walk's order: the last pocket first
+        pockets[k].id0 = total;
+        total += (int32_t)(pockets[k].q - pockets[k].p - 1);  // a pocket of m chain points: m - 2 triangles
+    }
+    if (total > cap) {
+        set_error("griddata: more pocket triangles than cap %d", cap);
+        return 2;
+    }
+    auto fill = [&](Pocket& P) {
+        struct Job {
+            int64_t p, q;
+            int32_t parent;  // pocket triangle on the other side of (p, q), -1 for a hull edge
+            int slot;        // which of the parent's nbr slots points back here
+        };
+        std::vector<Job> stack{{P.p, P.q, -1, -1}};
+        int32_t n = P.id0;
+        P.chords.reserve(2 * (size_t)(P.q - P.p));
+        while (!stack.empty()) {
+            const Job J = stack.back();
+            stack.pop_back();
+            const int64_t p = J.p, q = J.q;
+            // the chain point seeing (p, q) under the largest angle: smallest cot = dot / |cross|
+            int64_t best = -1;
+            double best_cot = INFINITY;
+            const int64_t a = p % L, b = q % L;
+            const double ax = X[p], ay = Y[p], bx = X[q], by = Y[q];
+            for (int64_t m = p + 1; m < q; ++m) {
+                const double ux = ax - X[m], uy = ay - Y[m];
+                const double vx = bx - X[m], vy = by - Y[m];
+                const double cr = fabs(ux * vy - uy * vx);
+                const double dt = ux * vx + uy * vy;
+                const double cot = cr > 0 ? dt / cr : (dt < 0 ? -INFINITY : INFINITY);
+                if (cot < best_cot) {
+                    best_cot = cot;
+                    best = m;
+                }
             }
-            extra_idx[k++] = v;
+            if (best < 0 || !(best_cot < INFINITY)) {
+                P.err = 1;
+                P.err_p = p;
+                P.err_q = q;
+                return;
+            }
+            const int64_t m = best;
+            const int32_t id = n++;
+            tri[3 * id + 0] = (int32_t)R.vertex(p);
+            tri[3 * id + 1] = (int32_t)R.vertex(m);
+            tri[3 * id + 2] = (int32_t)R.vertex(q);
+            // opposite p: edge (m, q); opposite m: edge (q, p); opposite q: edge (p, m)
+            nbr[3 * id + 1] = J.parent < 0 ? -1 : (int32_t)(base + J.parent);
+            if (J.parent >= 0) nbr[3 * J.parent + J.slot] = (int32_t)(base + id);
+            if (q - m == 1) {
+                nbr[3 * id + 0] = -2 - (int32_t)(m % L);
+                edge_tri[m % L] = (int32_t)(base + id);
+            } else {
+                nbr[3 * id + 0] = -1;  // filled by the child
+                stack.push_back({m, q, id, 0});
+            }
+            if (m - p == 1) {
+                nbr[3 * id + 2] = -2 - (int32_t)(p % L);
+                edge_tri[p % L] = (int32_t)(base + id);
+            } else {
+                nbr[3 * id + 2] = -1;
+                stack.push_back({p, m, id, 2});
+            }
+            // the base chord (p, q) joins two ring points that are not grid neighbours
+            P.chords.push_back({a, (int32_t)R.vertex(q)});
+            P.chords.push_back({b, (int32_t)R.vertex(p)});
         }
+    };
+    {
+        static const bool serial = getenv("AKB_GD_SERIAL_POCKETS") != nullptr;  // A/B
+        std::vector<std::thread> threads;
+        for (auto& P : pockets)
+            if (!serial && P.q - P.p >= 512) threads.emplace_back(fill, std::ref(P));
+        for (auto& P : pockets)
+            if (serial || P.q - P.p < 512) fill(P);
+        for (auto& t : threads) t.join();
     }
-    extra_ptr[L] = (int32_t)k;
+    std::vector<std::pair<int64_t, int32_t>> chords;
+    chords.reserve(2 * (size_t)L);
+    for (size_t k = pockets.size(); k-- > 0;) {
+        const Pocket& P = pockets[k];
+        if (P.err) {
+            set_error("griddata: degenerate pocket between ring positions %lld and %lld", (long long)P.err_p,
+                      (long long)P.err_q);
+            return 2;
+        }
+        chords.insert(chords.end(), P.chords.begin(), P.chords.end());
+    }
+    const int32_t n = total;
+    if ((int64_t)chords.size() > 6 * (int64_t)cap) {
+        set_error("griddata: extra-neighbour list overflow");
+        return 2;
+    }
+    // counting sort by ring position, stable: each vertex's chords in the order they were made
+    for (int64_t r = 0; r <= L; ++r) extra_ptr[r] = 0;
+    for (const auto& c : chords) ++extra_ptr[c.first + 1];
+    for (int64_t r = 0; r < L; ++r) extra_ptr[r + 1] += extra_ptr[r];
+    std::vector<int32_t> next(extra_ptr, extra_ptr + L);
+    for (const auto& c : chords) extra_idx[next[c.first]++] = c.second;
     *n_out = n;
     return 0;
 }

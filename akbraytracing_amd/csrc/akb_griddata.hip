@@ -185,7 +185,8 @@ __device__ int64_t tri_nbr(const Grid& g, int64_t t, int k) {
 // ------------------------------------------------------------------ triangulation + checks
 
 // flags: bit 0 a non-convex or degenerate cell, bit 1 an edge that is not locally Delaunay,
-// bit 2 a broken pocket adjacency, bits 3 / 4 cells of positive / negative orientation
+// bit 2 a broken pocket adjacency, bits 3 / 4 cells of positive / negative orientation, bit 5 a
+// non-finite point
 __global__ void __launch_bounds__(kBlock) k_gd_cells(Grid g, uint8_t* diag, double tol, unsigned* flags) {
     const int64_t nc = ncells(g);
     unsigned acc = 0;
@@ -195,6 +196,10 @@ __global__ void __launch_bounds__(kBlock) k_gd_cells(Grid g, uint8_t* diag, doub
         const int d = cell_diag(g, iv, ih, &bad);
         diag[c] = (uint8_t)d;
         unsigned f = bad > 0 ? 1u : 0u;
+        {   // bit 5: a non-finite point (a ray that missed); the ring kernel covers the last row / column
+            const int64_t q = (int64_t)iv * g.nh + ih;
+            if (!isfinite(g.x[q]) || !isfinite(g.y[q])) f |= 32u;
+        }
         {   // every cell must share the grid's orientation (bits 3 / 4 both set: a folded grid)
             const int64_t q00 = (int64_t)iv * g.nh + ih;
             const double o = orient(g.x[q00], g.y[q00], g.x[q00 + 1], g.y[q00 + 1], g.x[q00 + g.nh + 1], g.y[q00 + g.nh + 1]);
@@ -233,8 +238,8 @@ __global__ void __launch_bounds__(kBlock) k_gd_cells(Grid g, uint8_t* diag, doub
     }
 }
 
-// ring positions -> coordinates, for the host pocket builder
-__global__ void k_gd_ring(Grid g, double* rx, double* ry) {
+// ring positions -> coordinates, for the host pocket builder (bit 5 of flags: a non-finite one)
+__global__ void k_gd_ring(Grid g, double* rx, double* ry, unsigned* flags) {
     const int64_t a = g.nh - 1, b = g.nv - 1, L = 2 * a + 2 * b;
     for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < L; r += (int64_t)gridDim.x * blockDim.x) {
         int64_t v;
@@ -244,6 +249,7 @@ __global__ void k_gd_ring(Grid g, double* rx, double* ry) {
         else v = (int64_t)(g.nv - 1 - (r - 2 * a - b)) * g.nh;
         rx[r] = g.x[v];
         ry[r] = g.y[v];
+        if (!isfinite(rx[r]) || !isfinite(ry[r])) atomicOr(flags, 32u);
     }
 }
 
@@ -319,17 +325,36 @@ __device__ __forceinline__ void grad_edge(const Grid& g, int64_t n, int64_t j, d
     }
 }
 
-// the 2 x 2 solve of value set v; returns the relative change (scipy's measure)
+// Chebyshev semi-iteration on top of the Jacobi sweep (gprev != nullptr): the new gradient is
+// omega * (y - g_prev) + g_prev with y the Jacobi solve's value, which contracts the error by
+// ~0.27 per sweep instead of Jacobi's ~1/2 (the iteration matrix's spectrum lies in [-1/2, 1/2]:
+// the local problem is block diagonally dominant by a factor 2)
+struct Cheb {
+    const double* gprev;  // the iterate before gin (nullptr: a plain sweep, unless zero_prev)
+    double omega;
+    int zero_prev = 0;    // the previous iterate is zero (a Chebyshev step from x_0 = 0)
+};
+
+// the 2 x 2 solve of value set v; returns the relative change of the Jacobi step (scipy's measure)
 template <int NV>
 __device__ __forceinline__ double grad_solve(const GradAcc<NV>& A, int v, const double* gin, double* gout,
-                                             int64_t o) {
+                                             int64_t o, const Cheb& ch) {
     const double q0 = 4 * A.q0, q1 = 4 * A.q1, q3 = 4 * A.q3;
     const double inv = 1.0 / (q0 * q3 - q1 * q1);
     const double r0 = (q3 * A.s0[v] - q1 * A.s1[v]) * inv;
     const double r1 = (-q1 * A.s0[v] + q0 * A.s1[v]) * inv;
     const double c = fmax(fabs(gin[o] + r0), fabs(gin[o + 1] + r1)) / fmax(1.0, fmax(fabs(r0), fabs(r1)));
-    gout[o] = -r0;
-    gout[o + 1] = -r1;
+    if (ch.gprev) {
+        const double p0 = ch.gprev[o], p1 = ch.gprev[o + 1];
+        gout[o] = ch.omega * (-r0 - p0) + p0;
+        gout[o + 1] = ch.omega * (-r1 - p1) + p1;
+    } else if (ch.zero_prev) {
+        gout[o] = ch.omega * (-r0 - 0.0) + 0.0;
+        gout[o + 1] = ch.omega * (-r1 - 0.0) + 0.0;
+    } else {
+        gout[o] = -r0;
+        gout[o + 1] = -r1;
+    }
     return c;
 }
 
@@ -369,7 +394,7 @@ __device__ __forceinline__ void change_max(double worst, unsigned long long* chg
 template <int NV>
 __global__ void __launch_bounds__(kBlock) k_gd_grad(Grid g, const double* __restrict__ f,
                                                     const double* __restrict__ gin, double* __restrict__ gout,
-                                                    double* __restrict__ ring_acc, unsigned long long* chg) {
+                                                    double* __restrict__ ring_acc, unsigned long long* chg, Cheb ch) {
     const int64_t n = (int64_t)g.nv * g.nh;
     double worst = 0.0;
     // XCD-aware: the grid is a multiple of 8 and blocks b, b + 8, ... (one XCD, dealt round-robin)
@@ -408,7 +433,7 @@ __global__ void __launch_bounds__(kBlock) k_gd_grad(Grid g, const double* __rest
             continue;
         }
 #pragma unroll
-        for (int v = 0; v < NV; ++v) worst = fmax(worst, grad_solve<NV>(A, v, gin, gout, 2 * (v * n + i)));
+        for (int v = 0; v < NV; ++v) worst = fmax(worst, grad_solve<NV>(A, v, gin, gout, 2 * (v * n + i), ch));
     }
     change_max(worst, chg);
 }
@@ -492,7 +517,7 @@ __device__ __forceinline__ void grad_edge_lds(const StripRow<NV, W>& r, int c, d
 template <int NV, int W, bool kGS = false>
 __global__ void __launch_bounds__(W) k_gd_grad_strip(Grid g, const double* __restrict__ f,
                                                      const double* __restrict__ gin, double* __restrict__ gout,
-                                                     double* __restrict__ ring_acc, unsigned long long* chg) {
+                                                     double* __restrict__ ring_acc, unsigned long long* chg, Cheb ch) {
     constexpr int kStripW = W;
     __shared__ StripRow<NV, W> R[3];
     const int64_t n = (int64_t)g.nv * g.nh;
@@ -569,7 +594,7 @@ __global__ void __launch_bounds__(W) k_gd_grad_strip(Grid g, const double* __res
 #pragma unroll
                 for (int v = 0; v < NV; ++v) {
                     const int64_t o = 2 * (v * n + i);
-                    worst = fmax(worst, grad_solve<NV>(A, v, gin, gout, o));
+                    worst = fmax(worst, grad_solve<NV>(A, v, gin, gout, o, ch));
                     if (kGS) {
                         ngx[v] = gout[o];
                         ngy[v] = gout[o + 1];
@@ -601,7 +626,8 @@ __global__ void __launch_bounds__(W) k_gd_grad_strip(Grid g, const double* __res
 template <int NV>
 __global__ void __launch_bounds__(kBlock) k_gd_grad_ring(Grid g, const double* __restrict__ f,
                                                          const double* __restrict__ gin, double* __restrict__ gout,
-                                                         const double* __restrict__ ring_acc, unsigned long long* chg) {
+                                                         const double* __restrict__ ring_acc, unsigned long long* chg,
+                                                         Cheb ch) {
     const int64_t n = (int64_t)g.nv * g.nh;
     const int64_t a = g.nh - 1, b = g.nv - 1, L = 2 * a + 2 * b;
     const int lane = threadIdx.x & 63;
@@ -640,10 +666,398 @@ __global__ void __launch_bounds__(kBlock) k_gd_grad_ring(Grid g, const double* _
                 A.s1[v] += d[4 + 2 * v];
             }
 #pragma unroll
-            for (int v = 0; v < NV; ++v) worst = fmax(worst, grad_solve<NV>(A, v, gin, gout, 2 * (v * n + i)));
+            for (int v = 0; v < NV; ++v) worst = fmax(worst, grad_solve<NV>(A, v, gin, gout, 2 * (v * n + i), ch));
         }
     }
     change_max(worst, chg);
+}
+
+// ------------------------------------------------------------------ register sweeps (two per launch)
+//
+// k_gd_sweeps: each wave owns a strip of columns (one lane per column, the two outer lanes on each
+// side are halo) and walks down a chunk of rows; the rows it works on sit in registers and the
+// left / right neighbours come from the adjacent lanes (DPP wave shifts), so there is no LDS and
+// no barrier. kK = 2 does two Chebyshev sweeps per launch, the second one row behind the first
+// (wavefront temporal blocking): the first sweep's values are formed one column and one row into
+// the halo so the second has its neighbours, and only x, y, f and the two gradient sets of the
+// rows are read from HBM once per two sweeps. Ring vertices take their pocket chords from
+// k_gd_ring_chords (x_k, before the launch); in the second sweep they only store their grid-edge
+// sums and k_gd_grad_ring adds the chords of x_{k+1} and solves after the launch. Per vertex the
+// edge order and arithmetic are k_gd_grad's, so kK sweeps here give the bits of kK sweeps there.
+
+// lane l gets lane l - 1's value (DPP wave_shr:1; lane 0 keeps its own) / lane l + 1's (wave_shl:1)
+__device__ __forceinline__ int lane_prev_i(int v) { return __builtin_amdgcn_update_dpp(v, v, 0x138, 0xf, 0xf, false); }
+__device__ __forceinline__ int lane_next_i(int v) { return __builtin_amdgcn_update_dpp(v, v, 0x130, 0xf, 0xf, false); }
+// (the cell flags are loaded per lane rather than shifted: an int shifted this way read the
+// neighbour on the wrong side at a flag change on the MI355X, tests/test_gpu_parity.py's 300 x 280
+// lattice; the doubles' shifts are checked bit for bit against the LDS kernels there)
+// doubles: one v_mov_b32_dpp per half with bound_ctrl (lane 0 / lane 63 read 0: halo lanes)
+__device__ __forceinline__ double lane_prev(double v) {
+    return __hiloint2double(__builtin_amdgcn_mov_dpp(__double2hiint(v), 0x138, 0xf, 0xf, true),
+                            __builtin_amdgcn_mov_dpp(__double2loint(v), 0x138, 0xf, 0xf, true));
+}
+__device__ __forceinline__ double lane_next(double v) {
+    return __hiloint2double(__builtin_amdgcn_mov_dpp(__double2hiint(v), 0x130, 0xf, 0xf, true),
+                            __builtin_amdgcn_mov_dpp(__double2loint(v), 0x130, 0xf, 0xf, true));
+}
+
+template <int NV>
+struct RV {  // one vertex of a row: position, values, gradients, diagonal flags of cells (row, col), (row, col - 1)
+    double x, y, f[NV], gx[NV], gy[NV];
+    int d, dl;
+};
+
+template <int NV, bool kNext>
+__device__ __forceinline__ RV<NV> rv_shift(const RV<NV>& r) {
+    RV<NV> o;
+    o.x = kNext ? lane_next(r.x) : lane_prev(r.x);
+    o.y = kNext ? lane_next(r.y) : lane_prev(r.y);
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        o.f[v] = kNext ? lane_next(r.f[v]) : lane_prev(r.f[v]);
+        o.gx[v] = kNext ? lane_next(r.gx[v]) : lane_prev(r.gx[v]);
+        o.gy[v] = kNext ? lane_next(r.gy[v]) : lane_prev(r.gy[v]);
+    }
+    o.d = o.dl = 0;  // the flags are loaded per lane (RV::dl), never shifted
+    return o;
+}
+
+// grad_edge with the neighbour in registers
+template <int NV>
+__device__ __forceinline__ void edge_rv(const RV<NV>& o, double xi, double yi, const double (&fi)[NV],
+                                        GradAcc<NV>& A) {
+    const double ex = o.x - xi, ey = o.y - yi;
+    const double l2 = ex * ex + ey * ey;
+    double rr = __builtin_amdgcn_rsq(l2);
+    rr = rr * __builtin_fma(-0.5 * l2 * rr, rr, 1.5);
+    const double r3 = rr * rr * rr;
+    const double wx = ex * r3, wy = ey * r3;
+    A.q0 = __builtin_fma(ex, wx, A.q0);
+    A.q1 = __builtin_fma(ex, wy, A.q1);
+    A.q3 = __builtin_fma(ey, wy, A.q3);
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const double df2 = -ex * o.gx[v] - ey * o.gy[v];
+        const double w = 6 * (fi[v] - o.f[v]) - 2 * df2;
+        A.s0[v] = __builtin_fma(w, wx, A.s0[v]);
+        A.s1[v] = __builtin_fma(w, wy, A.s1[v]);
+    }
+}
+
+// the grid-edge sums of the vertex in row `cur` (wave-uniform control flow: the lane shifts run in
+// every lane; only the shifts some lane of the wave needs are made)
+template <int NV>
+__device__ __forceinline__ GradAcc<NV> vertex_sums(const RV<NV>& up, const RV<NV>& cur, const RV<NV>& dn,
+                                                   bool hl, bool hr, bool hu, bool hd) {
+    // which diagonals exist: cells (iv - 1, ih - 1), (iv - 1, ih), (iv, ih - 1), (iv, ih)
+    const bool ul = hu && hl && up.dl == 0, ur = hu && hr && up.d == 1;
+    const bool dl = hd && hl && cur.dl == 1, dr = hd && hr && cur.d == 0;
+    GradAcc<NV> A;
+    // one shifted neighbour live at a time, the edges in k_gd_grad's order
+    {
+        const RV<NV> L = rv_shift<NV, false>(cur);
+        if (hl) edge_rv<NV>(L, cur.x, cur.y, cur.f, A);
+    }
+    {
+        const RV<NV> R = rv_shift<NV, true>(cur);
+        if (hr) edge_rv<NV>(R, cur.x, cur.y, cur.f, A);
+    }
+    if (hu) edge_rv<NV>(up, cur.x, cur.y, cur.f, A);
+    if (hd) edge_rv<NV>(dn, cur.x, cur.y, cur.f, A);
+    if (__any(ul)) {
+        const RV<NV> N = rv_shift<NV, false>(up);
+        if (ul) edge_rv<NV>(N, cur.x, cur.y, cur.f, A);
+    }
+    if (__any(ur)) {
+        const RV<NV> N = rv_shift<NV, true>(up);
+        if (ur) edge_rv<NV>(N, cur.x, cur.y, cur.f, A);
+    }
+    if (__any(dl)) {
+        const RV<NV> N = rv_shift<NV, false>(dn);
+        if (dl) edge_rv<NV>(N, cur.x, cur.y, cur.f, A);
+    }
+    if (__any(dr)) {
+        const RV<NV> N = rv_shift<NV, true>(dn);
+        if (dr) edge_rv<NV>(N, cur.x, cur.y, cur.f, A);
+    }
+    return A;
+}
+
+// grad_solve on registers: y = -Q^-1 s, the change against the current value (gi), then the
+// Chebyshev combination with the previous iterate (p; plain: y itself)
+template <int NV>
+__device__ __forceinline__ double solve_rv(const GradAcc<NV>& A, int v, double gix, double giy, bool plain,
+                                           double omega, double px, double py, double& ox, double& oy) {
+    const double q0 = 4 * A.q0, q1 = 4 * A.q1, q3 = 4 * A.q3;
+    const double inv = 1.0 / (q0 * q3 - q1 * q1);  // the same for every v: CSE'd across the unrolled calls
+    const double r0 = (q3 * A.s0[v] - q1 * A.s1[v]) * inv;
+    const double r1 = (-q1 * A.s0[v] + q0 * A.s1[v]) * inv;
+    const double c = fmax(fabs(gix + r0), fabs(giy + r1)) / fmax(1.0, fmax(fabs(r0), fabs(r1)));
+    if (plain) {
+        ox = -r0;
+        oy = -r1;
+    } else {
+        ox = omega * (-r0 - px) + px;
+        oy = omega * (-r1 - py) + py;
+    }
+    return c;
+}
+
+template <int NV>
+struct SweepArgs {
+    const double* f;       // (NV, n) values
+    const double* gin;     // (NV, n, 2) x_k, nullptr = zeros
+    const double* gprev;   // (NV, n, 2) x_{k-1} for the first sweep's Chebyshev step, nullptr = plain
+    double om1, om2;       // the two sweeps' weights
+    double* gout1;         // x_{k+1}
+    double* gout2;         // x_{k+2} (kK = 2)
+    const double* chords;  // (L, 3 + 2 NV) pocket-chord sums of x_k (k_gd_ring_chords)
+    double* ring_acc;      // (L, 3 + 2 NV) grid-edge sums of x_{k+1} at ring vertices (kK = 2)
+    unsigned long long* chg;  // [2]: largest relative change of each sweep
+    int rows;              // rows per wave
+};
+
+template <int NV, int kK, int kWaves, int kDepth = 1>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves)))
+k_gd_sweeps(Grid g, SweepArgs<NV> a) {
+    constexpr int kHalo = kK;             // halo lanes on each side
+    constexpr int kOwn = 64 - 2 * kHalo;  // columns a wave owns
+    const int64_t n = (int64_t)g.nv * g.nh;
+    const int lane = threadIdx.x & 63;
+    const int wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
+    const int nstrips = (g.nh + kOwn - 1) / kOwn;
+    const int nchunks = (g.nv + a.rows - 1) / a.rows;
+    double worst1 = 0.0, worst2 = 0.0;
+    if (wave < nstrips * nchunks) {
+        const int strip = wave % nstrips, chunk = wave / nstrips;
+        const int ih = strip * kOwn + lane - kHalo;
+        const bool col = ih >= 0 && ih < g.nh;
+        const bool own = col && lane >= kHalo && lane < 64 - kHalo;
+        const int r0 = chunk * a.rows, r1 = min(r0 + a.rows, g.nv);
+        const bool hl = ih > 0, hr = ih < g.nh - 1;
+        // geometry (x, y, f, d) and x_k of row rr; x_{k-1} of row rr
+        auto load = [&](int rr, RV<NV>& r) {
+            r.x = r.y = 0.0;
+            r.d = r.dl = 0;
+#pragma unroll
+            for (int v = 0; v < NV; ++v) r.f[v] = r.gx[v] = r.gy[v] = 0.0;
+            if (!col || rr < 0 || rr >= g.nv) return;
+            const int64_t i = (int64_t)rr * g.nh + ih;
+            r.x = g.x[i];
+            r.y = g.y[i];
+            const int64_t c = (int64_t)rr * (g.nh - 1) + ih;
+            r.d = (rr < g.nv - 1 && ih < g.nh - 1) ? g.diag[c] : 0;
+            r.dl = (rr < g.nv - 1 && ih > 0) ? g.diag[c - 1] : 0;
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                r.f[v] = a.f[v * n + i];
+                if (a.gin) {
+                    r.gx[v] = a.gin[2 * (v * n + i)];
+                    r.gy[v] = a.gin[2 * (v * n + i) + 1];
+                }
+            }
+        };
+        auto load_prev = [&](int rr, double (&px)[NV], double (&py)[NV]) {
+#pragma unroll
+            for (int v = 0; v < NV; ++v) px[v] = py[v] = 0.0;
+            if (!a.gprev || !col || rr < 0 || rr >= g.nv) return;
+            const int64_t i = (int64_t)rr * g.nh + ih;
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                px[v] = a.gprev[2 * (v * n + i)];
+                py[v] = a.gprev[2 * (v * n + i) + 1];
+            }
+        };
+        // sweep 1 of row i (rows up / cur / dn) -> s (x_{k+1} of row i, NV x 2)
+        auto sweep1 = [&](int i, const RV<NV>& up, const RV<NV>& cur, const RV<NV>& dn, const double (&px)[NV],
+                          const double (&py)[NV], RV<NV>& s) {
+            s = cur;  // geometry and values carry over; gradients replaced below
+            GradAcc<NV> A = vertex_sums<NV>(up, cur, dn, hl, hr, i > 0, i < g.nv - 1);
+            if (!col || i < 0 || i >= g.nv) return;
+            const int64_t r = ring_pos(g, i, ih);
+            if (r >= 0) {  // pocket chords of x_k (commutative sum: the bits of k_gd_grad_ring's order)
+                const double* c = a.chords + r * (3 + 2 * NV);
+                A.q0 = c[0] + A.q0;
+                A.q1 = c[1] + A.q1;
+                A.q3 = c[2] + A.q3;
+#pragma unroll
+                for (int v = 0; v < NV; ++v) {
+                    A.s0[v] = c[3 + 2 * v] + A.s0[v];
+                    A.s1[v] = c[4 + 2 * v] + A.s1[v];
+                }
+            }
+            const bool mine = own && i >= r0 && i < r1;
+            const int64_t o = (int64_t)i * g.nh + ih;
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                double ox, oy;
+                const double ch = solve_rv<NV>(A, v, cur.gx[v], cur.gy[v], a.gprev == nullptr, a.om1, px[v], py[v],
+                                               ox, oy);
+                s.gx[v] = ox;
+                s.gy[v] = oy;
+                if (mine) {
+                    worst1 = fmax(worst1, ch);
+                    a.gout1[2 * (v * n + o)] = ox;
+                    a.gout1[2 * (v * n + o) + 1] = oy;
+                }
+            }
+        };
+        RV<NV> G0, G1, G2, G3;  // x_k rows i - 2 .. i + 1 (kK = 2) / i - 1 .. i + 1 (kK = 1: G1 .. G3)
+        RV<NV> S0, S1, S2;      // x_{k+1} rows i - 2 .. i
+        double px[NV], py[NV], qx[NV], qy[NV];
+        const int first = kK == 2 ? r0 - 1 : r0;  // rows of sweep 1
+        const int last = kK == 2 ? r1 : r1 - 1;
+        load(first - 2, G0);
+        load(first - 1, G1);
+        load(first, G2);
+        load(first + 1, G3);
+        load_prev(first, px, py);
+        S0 = G0;
+        S1 = G1;
+        // rows i + 2 (and, kDepth = 2, i + 3) in flight across row i's arithmetic: the VGPR budget
+        // of two waves per SIMD holds a second prefetched row
+        RV<NV> P;
+        double sx[NV], sy[NV];
+        if (kDepth == 2) {
+            load(first + 2, P);
+            load_prev(first + 1, sx, sy);
+        }
+        for (int i = first; i <= last; ++i) {
+            RV<NV> N;
+            if (kDepth == 2) {
+                N = P;
+#pragma unroll
+                for (int v = 0; v < NV; ++v) {
+                    qx[v] = sx[v];
+                    qy[v] = sy[v];
+                }
+                load(i + 3, P);
+                load_prev(i + 2, sx, sy);
+            } else {
+                load(i + 2, N);
+                load_prev(i + 1, qx, qy);
+            }
+            sweep1(i, G1, G2, G3, px, py, S2);
+            if (kK == 2 && i - 1 >= r0 && i - 1 < r1) {
+                // sweep 2 of row i - 1 from the x_{k+1} rows S0 (i - 2), S1 (i - 1), S2 (i)
+                const int iv = i - 1;
+                GradAcc<NV> A = vertex_sums<NV>(S0, S1, S2, hl, hr, iv > 0, iv < g.nv - 1);
+                if (own) {
+                    const int64_t o = (int64_t)iv * g.nh + ih;
+                    const int64_t r = ring_pos(g, iv, ih);
+                    if (r >= 0) {  // k_gd_grad_ring adds the chords of x_{k+1} and solves
+                        double* d = a.ring_acc + r * (3 + 2 * NV);
+                        d[0] = A.q0;
+                        d[1] = A.q1;
+                        d[2] = A.q3;
+#pragma unroll
+                        for (int v = 0; v < NV; ++v) {
+                            d[3 + 2 * v] = A.s0[v];
+                            d[4 + 2 * v] = A.s1[v];
+                        }
+                    } else {
+#pragma unroll
+                        for (int v = 0; v < NV; ++v) {
+                            double ox, oy;
+                            // Chebyshev against x_k of row i - 1 (G1)
+                            worst2 = fmax(worst2, solve_rv<NV>(A, v, S1.gx[v], S1.gy[v], false, a.om2, G1.gx[v],
+                                                               G1.gy[v], ox, oy));
+                            a.gout2[2 * (v * n + o)] = ox;
+                            a.gout2[2 * (v * n + o) + 1] = oy;
+                        }
+                    }
+                }
+            }
+            G0 = G1;
+            G1 = G2;
+            G2 = G3;
+            G3 = N;
+            S0 = S1;
+            S1 = S2;
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                px[v] = qx[v];
+                py[v] = qy[v];
+            }
+        }
+    }
+    // the two sweeps' largest changes: wave reduction, one atomic per wave
+    for (int off = 32; off > 0; off >>= 1) {
+        worst1 = fmax(worst1, __shfl_down(worst1, off));
+        worst2 = fmax(worst2, __shfl_down(worst2, off));
+    }
+    if (lane == 0 && a.chg) {
+        const unsigned long long b1 = (unsigned long long)__double_as_longlong(worst1);
+        if (worst1 > 0 && __hip_atomic_load(&a.chg[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < b1)
+            atomicMax(&a.chg[0], b1);
+        const unsigned long long b2 = (unsigned long long)__double_as_longlong(worst2);
+        if (kK == 2 && worst2 > 0 && __hip_atomic_load(&a.chg[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < b2)
+            atomicMax(&a.chg[1], b2);
+    }
+}
+
+// pocket-chord sums of every ring vertex from gradients gin (nullptr = zeros): one wave per ring
+// vertex, lanes striding its chord list, the fixed-order wave reduction of k_gd_grad_ring
+template <int NV>
+__global__ void __launch_bounds__(kBlock) k_gd_ring_chords(Grid g, const double* __restrict__ f,
+                                                           const double* __restrict__ gin, double* __restrict__ out) {
+    const int64_t n = (int64_t)g.nv * g.nh;
+    const int64_t a = g.nh - 1, b = g.nv - 1, L = 2 * a + 2 * b;
+    const int lane = threadIdx.x & 63;
+    for (int64_t r = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; r < L;
+         r += ((int64_t)gridDim.x * blockDim.x) >> 6) {
+        int64_t i;
+        if (r < a) i = r;
+        else if (r < a + b) i = (r - a) * g.nh + (g.nh - 1);
+        else if (r < 2 * a + b) i = (int64_t)(g.nv - 1) * g.nh + (g.nh - 1 - (r - a - b));
+        else i = (int64_t)(g.nv - 1 - (r - 2 * a - b)) * g.nh;
+        const double xi = g.x[i], yi = g.y[i];
+        double fi[NV];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) fi[v] = f[v * n + i];
+        GradAcc<NV> A;
+        for (int32_t k = g.xptr[r] + lane; k < g.xptr[r + 1]; k += 64) {
+            const int64_t j = g.xidx[k];
+            const double ex = g.x[j] - xi, ey = g.y[j] - yi;
+            const double l2 = ex * ex + ey * ey;
+            double rr = __builtin_amdgcn_rsq(l2);
+            rr = rr * __builtin_fma(-0.5 * l2 * rr, rr, 1.5);
+            const double r3 = rr * rr * rr;
+            const double wx = ex * r3, wy = ey * r3;
+            A.q0 = __builtin_fma(ex, wx, A.q0);
+            A.q1 = __builtin_fma(ex, wy, A.q1);
+            A.q3 = __builtin_fma(ey, wy, A.q3);
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                const double gx = gin ? gin[2 * (v * n + j)] : 0.0, gy = gin ? gin[2 * (v * n + j) + 1] : 0.0;
+                const double df2 = -ex * gx - ey * gy;
+                const double w = 6 * (fi[v] - f[v * n + j]) - 2 * df2;
+                A.s0[v] = __builtin_fma(w, wx, A.s0[v]);
+                A.s1[v] = __builtin_fma(w, wy, A.s1[v]);
+            }
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+            A.q0 += __shfl_down(A.q0, off);
+            A.q1 += __shfl_down(A.q1, off);
+            A.q3 += __shfl_down(A.q3, off);
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                A.s0[v] += __shfl_down(A.s0[v], off);
+                A.s1[v] += __shfl_down(A.s1[v], off);
+            }
+        }
+        if (lane == 0) {
+            double* d = out + r * (3 + 2 * NV);
+            d[0] = A.q0;
+            d[1] = A.q1;
+            d[2] = A.q3;
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                d[3 + 2 * v] = A.s0[v];
+                d[4 + 2 * v] = A.s1[v];
+            }
+        }
+    }
 }
 
 // ------------------------------------------------------------------ targets
@@ -653,6 +1067,12 @@ struct Targets {
     const double* gy;  // (my,) target y axis (grid_V column), ascending
     int mx, my;
 };
+
+// (m - 1) / (a[m-1] - a[0]): the inverse step of a linspace axis (0 for one point)
+__device__ __forceinline__ double inv_step(const double* a, int m) {
+    const double d = a[m - 1] - a[0];
+    return m > 1 && d > 0 ? (m - 1) / d : 0.0;
+}
 
 __device__ __forceinline__ int lower_idx(const double* a, int n, double v) {  // first i with a[i] >= v
     int lo = 0, hi = n;
@@ -712,6 +1132,57 @@ __global__ void __launch_bounds__(kBlock) k_gd_claim(Grid g, Targets t, int* own
         tri_box(g, t, T, c0, c1, r0, r1);
         for (int r = r0; r < r1; ++r)
             for (int c = c0; c < c1; ++c) claim_one(g, t, T, (int)id, r, c, owner);
+    }
+}
+
+// cell triangles, one thread per cell: the targets are sparse against the cells (a 128^2 pupil
+// grid over 1e7 hits), so the cell's target index box is first estimated from the linspace axes
+// (widened by one index each way) and almost every thread stops there; the candidates are then
+// held to each triangle's exact box and barycentric test, so the claims are k_gd_claim's
+// candidate index range of the targets of an ascending linspace axis a (m points) in [lo, hi):
+// the real-valued indices of lo and hi from the axis's own step, widened by 1e-6 of an index (the
+// axis values sit within a few ulp of a0 + c * step); empty when no integer falls between them
+__device__ __forceinline__ bool axis_range(const double* a, int m, double inv_step, double lo, double hi, int& c0,
+                                           int& c1) {
+    const double a0 = a[0];
+    const double e0 = (lo - a0) * inv_step - 1e-6, e1 = (hi - a0) * inv_step + 1e-6;
+    if (!(e1 >= 0.0) || !(e0 <= (double)(m - 1))) return false;
+    const double f0 = ceil(fmax(e0, 0.0)), f1 = floor(fmin(e1, (double)(m - 1)));
+    if (f0 > f1) return false;
+    c0 = (int)f0;
+    c1 = (int)f1 + 1;
+    return true;
+}
+
+__global__ void __launch_bounds__(kBlock) k_gd_claim_cells(Grid g, Targets t, int* owner) {
+    const int64_t nc = ncells(g);
+    const double inv_dx = inv_step(t.gx, t.mx), inv_dy = inv_step(t.gy, t.my);
+    for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < nc; c += (int64_t)gridDim.x * blockDim.x) {
+        const int iv = (int)(c / (g.nh - 1)), ih = (int)(c - (int64_t)iv * (g.nh - 1));
+        const int64_t p00 = (int64_t)iv * g.nh + ih;
+        const double xa = g.x[p00], xb = g.x[p00 + 1], xc = g.x[p00 + g.nh], xd = g.x[p00 + g.nh + 1];
+        const double ya = g.y[p00], yb = g.y[p00 + 1], yc = g.y[p00 + g.nh], yd = g.y[p00 + g.nh + 1];
+        const double xlo = fmin(fmin(xa, xb), fmin(xc, xd)), xhi = fmax(fmax(xa, xb), fmax(xc, xd));
+        const double ylo = fmin(fmin(ya, yb), fmin(yc, yd)), yhi = fmax(fmax(ya, yb), fmax(yc, yd));
+        const double padx = (xhi - xlo) * 1e-9, pady = (yhi - ylo) * 1e-9;
+        int c0, c1, r0, r1;
+        if (!axis_range(t.gx, t.mx, inv_dx, xlo - padx, xhi + padx, c0, c1)) continue;
+        if (!axis_range(t.gy, t.my, inv_dy, ylo - pady, yhi + pady, r0, r1)) continue;
+        // the exact box within the estimate: targets with lo <= coordinate < hi (as lower_idx gives)
+        while (c0 < c1 && t.gx[c0] < xlo - padx) ++c0;
+        while (c1 > c0 && t.gx[c1 - 1] >= xhi + padx) --c1;
+        if (c0 >= c1) continue;
+        while (r0 < r1 && t.gy[r0] < ylo - pady) ++r0;
+        while (r1 > r0 && t.gy[r1 - 1] >= yhi + pady) --r1;
+        if (r0 >= r1) continue;
+        for (int half = 0; half < 2; ++half) {
+            const int64_t id = 2 * c + half;
+            const Tri T = tri_verts(g, id);
+            int tc0, tc1, tr0, tr1;
+            tri_box(g, t, T, tc0, tc1, tr0, tr1);
+            for (int r = max(r0, tr0); r < min(r1, tr1); ++r)
+                for (int cc = max(c0, tc0); cc < min(c1, tc1); ++cc) claim_one(g, t, T, (int)id, r, cc, owner);
+        }
     }
 }
 
@@ -849,7 +1320,7 @@ int akb_gd_cells_f64(const double* x, const double* y, int nv, int nh, uint8_t* 
     int st = launch_status("k_gd_cells");
     if (st) return st;
     const int64_t L = 2 * (int64_t)(nh - 1) + 2 * (int64_t)(nv - 1);
-    k_gd_ring<<<grid_for(L), kBlock, 0, s>>>(g, ring_x, ring_y);
+    k_gd_ring<<<grid_for(L), kBlock, 0, s>>>(g, ring_x, ring_y, d_flags);
     return launch_status("k_gd_ring");
 }
 
@@ -864,13 +1335,16 @@ int akb_gd_check_pockets(const double* x, const double* y, int nv, int nh, const
 }
 
 // one Jacobi sweep; d_change: largest relative change (as ordered double bits, zeroed by the
-// caller); nvals value sets strided by n (values) and 2n (gradients); ring_work: 10 L doubles
+// caller); nvals value sets strided by n (values) and 2n (gradients); ring_work: 10 L doubles.
+// gprev != NULL: Chebyshev step, gout = omega * (jacobi(gin) - gprev) + gprev (a Jacobi sweep
+// then, whatever AKB_GD_GS says); gprev == NULL with omega == 0: a plain Jacobi sweep
 int akb_gd_grad_sweep_f64(const double* x, const double* y, int nv, int nh, const uint8_t* diag, int npock,
                           const int32_t* ptri, const int32_t* pnbr, const int32_t* edge_tri, const int32_t* xptr,
-                          const int32_t* xidx, const double* f, int nvals, const double* gin, double* gout,
-                          double* ring_work, unsigned long long* d_change, void* stream) {
+                          const int32_t* xidx, const double* f, int nvals, const double* gin, const double* gprev,
+                          double omega, double* gout, double* ring_work, unsigned long long* d_change, void* stream) {
     clear_error();
     AKB_REQUIRE(x && y && diag && f && gin && gout && ring_work && d_change && nvals >= 1, "bad arguments");
+    AKB_REQUIRE(!gprev || (omega > 0 && omega < 2), "Chebyshev weight outside (0, 2)");
     Grid g{x, y, nv, nh, diag, npock, ptri, pnbr, edge_tri, xptr, xidx, gd_no_xcd()};
     {
         const char* re = getenv("AKB_GD_ROWS");
@@ -893,41 +1367,111 @@ int akb_gd_grad_sweep_f64(const double* x, const double* y, int nv, int nh, cons
     if (strip != 0 && strip != 64 && strip != 128 && strip != 256) strip = 256;
     // the strip sweeps as line Gauss-Seidel (AKB_GD_GS=0: Jacobi, the gather kernel's bits)
     const char* ge = getenv("AKB_GD_GS");
-    const bool gs_sweep = !(ge && ge[0] == '0');
+    // Gauss-Seidel only for a plain sweep that asks for it (omega >= 1): Chebyshev iterations pass
+    // omega = 0 for their plain first sweep, which must be the Jacobi one
+    const bool gs_sweep = !(ge && ge[0] == '0') && !gprev && omega > 0;
     const unsigned gs =
         strip ? (unsigned)(((nh + strip - 1) / strip) * ((nv + g.strip_rows - 1) / g.strip_rows)) : 0u;
     for (int v = 0; v < nvals; v += 2) {
         const double* fv = f + v * n;
         const double* gi = gin + 2 * v * n;
         double* go = gout + 2 * v * n;
+        const Cheb ch{gprev ? gprev + 2 * v * n : nullptr, omega};
         if (nvals - v >= 2) {
             if (strip == 64)
-                gs_sweep ? k_gd_grad_strip<2, 64, true><<<gs, 64, 0, s>>>(g, fv, gi, go, ring_work, chg)
-                         : k_gd_grad_strip<2, 64><<<gs, 64, 0, s>>>(g, fv, gi, go, ring_work, chg);
+                gs_sweep ? k_gd_grad_strip<2, 64, true><<<gs, 64, 0, s>>>(g, fv, gi, go, ring_work, chg, ch)
+                         : k_gd_grad_strip<2, 64><<<gs, 64, 0, s>>>(g, fv, gi, go, ring_work, chg, ch);
             else if (strip == 128)
-                gs_sweep ? k_gd_grad_strip<2, 128, true><<<gs, 128, 0, s>>>(g, fv, gi, go, ring_work, chg)
-                         : k_gd_grad_strip<2, 128><<<gs, 128, 0, s>>>(g, fv, gi, go, ring_work, chg);
+                gs_sweep ? k_gd_grad_strip<2, 128, true><<<gs, 128, 0, s>>>(g, fv, gi, go, ring_work, chg, ch)
+                         : k_gd_grad_strip<2, 128><<<gs, 128, 0, s>>>(g, fv, gi, go, ring_work, chg, ch);
             else if (strip == 256)
-                gs_sweep ? k_gd_grad_strip<2, 256, true><<<gs, 256, 0, s>>>(g, fv, gi, go, ring_work, chg)
-                         : k_gd_grad_strip<2, 256><<<gs, 256, 0, s>>>(g, fv, gi, go, ring_work, chg);
+                gs_sweep ? k_gd_grad_strip<2, 256, true><<<gs, 256, 0, s>>>(g, fv, gi, go, ring_work, chg, ch)
+                         : k_gd_grad_strip<2, 256><<<gs, 256, 0, s>>>(g, fv, gi, go, ring_work, chg, ch);
             else
-                k_gd_grad<2><<<gr, kBlock, 0, s>>>(g, fv, gi, go, ring_work, chg);
-            k_gd_grad_ring<2><<<grr, kBlock, 0, s>>>(g, fv, gi, go, ring_work, chg);
+                k_gd_grad<2><<<gr, kBlock, 0, s>>>(g, fv, gi, go, ring_work, chg, ch);
+            k_gd_grad_ring<2><<<grr, kBlock, 0, s>>>(g, fv, gi, go, ring_work, chg, ch);
         } else {
             if (strip == 64)
-                gs_sweep ? k_gd_grad_strip<1, 64, true><<<gs, 64, 0, s>>>(g, fv, gi, go, ring_work, chg)
-                         : k_gd_grad_strip<1, 64><<<gs, 64, 0, s>>>(g, fv, gi, go, ring_work, chg);
+                gs_sweep ? k_gd_grad_strip<1, 64, true><<<gs, 64, 0, s>>>(g, fv, gi, go, ring_work, chg, ch)
+                         : k_gd_grad_strip<1, 64><<<gs, 64, 0, s>>>(g, fv, gi, go, ring_work, chg, ch);
             else if (strip == 128)
-                gs_sweep ? k_gd_grad_strip<1, 128, true><<<gs, 128, 0, s>>>(g, fv, gi, go, ring_work, chg)
-                         : k_gd_grad_strip<1, 128><<<gs, 128, 0, s>>>(g, fv, gi, go, ring_work, chg);
+                gs_sweep ? k_gd_grad_strip<1, 128, true><<<gs, 128, 0, s>>>(g, fv, gi, go, ring_work, chg, ch)
+                         : k_gd_grad_strip<1, 128><<<gs, 128, 0, s>>>(g, fv, gi, go, ring_work, chg, ch);
             else if (strip == 256)
-                gs_sweep ? k_gd_grad_strip<1, 256, true><<<gs, 256, 0, s>>>(g, fv, gi, go, ring_work, chg)
-                         : k_gd_grad_strip<1, 256><<<gs, 256, 0, s>>>(g, fv, gi, go, ring_work, chg);
+                gs_sweep ? k_gd_grad_strip<1, 256, true><<<gs, 256, 0, s>>>(g, fv, gi, go, ring_work, chg, ch)
+                         : k_gd_grad_strip<1, 256><<<gs, 256, 0, s>>>(g, fv, gi, go, ring_work, chg, ch);
             else
-                k_gd_grad<1><<<gr, kBlock, 0, s>>>(g, fv, gi, go, ring_work, chg);
-            k_gd_grad_ring<1><<<grr, kBlock, 0, s>>>(g, fv, gi, go, ring_work, chg);
+                k_gd_grad<1><<<gr, kBlock, 0, s>>>(g, fv, gi, go, ring_work, chg, ch);
+            k_gd_grad_ring<1><<<grr, kBlock, 0, s>>>(g, fv, gi, go, ring_work, chg, ch);
         }
         int st = launch_status("k_gd_grad");
+        if (st) return st;
+    }
+    return 0;
+}
+
+// kk = 1 or 2 Jacobi sweeps in one launch of the register kernel, each a Chebyshev step (om1, om2;
+// gprev == NULL: the first is a plain sweep; gin == NULL: x_k = 0). gout1 = x_{k+1}, gout2 =
+// x_{k+2}; d_change[0], [1]: the sweeps' largest relative changes; ring_work: 14 L doubles.
+int akb_gd_grad_sweeps_f64(const double* x, const double* y, int nv, int nh, const uint8_t* diag, int npock,
+                           const int32_t* ptri, const int32_t* pnbr, const int32_t* edge_tri, const int32_t* xptr,
+                           const int32_t* xidx, const double* f, int nvals, const double* gin, const double* gprev,
+                           double om1, double om2, int kk, double* gout1, double* gout2, double* ring_work,
+                           unsigned long long* d_change, void* stream) {
+    clear_error();
+    AKB_REQUIRE(x && y && diag && f && gout1 && ring_work && d_change && nvals >= 1, "bad arguments");
+    AKB_REQUIRE(kk == 1 || (kk == 2 && gout2), "kk must be 1, or 2 with gout2");
+    AKB_REQUIRE(!gprev || (om1 > 0 && om1 < 2), "Chebyshev weight outside (0, 2)");
+    AKB_REQUIRE(kk == 1 || (om2 > 0 && om2 < 2), "Chebyshev weight outside (0, 2)");
+    Grid g{x, y, nv, nh, diag, npock, ptri, pnbr, edge_tri, xptr, xidx, gd_no_xcd()};
+    int rows = 24;  // rows per wave (AKB_GD_ROWS): 24 at 3 waves per SIMD measured best on the C3 hits
+    {
+        const char* re = getenv("AKB_GD_ROWS");
+        const int v = re ? atoi(re) : 0;
+        if (v >= 4 && v <= 1024) rows = v;
+    }
+    // the two-value two-sweep kernel's occupancy variant (AKB_GD_OCC, A/B): 3 waves per SIMD by
+    // default (168 VGPRs, 12 B of scratch: 4.75 vs 5.3 ms for the C3 hits' solve at 2 waves)
+    const char* oe = getenv("AKB_GD_OCC");
+    const int occ = oe ? atoi(oe) : 3;
+    hipStream_t s = (hipStream_t)stream;
+    const int64_t n = (int64_t)nv * nh;
+    const int64_t L = 2 * (int64_t)(nh - 1) + 2 * (int64_t)(nv - 1);
+    unsigned long long* chg = gd_no_change() ? nullptr : d_change;
+    const unsigned grr = grid_for(L * 64);
+    const int own = 64 - 2 * kk;
+    const int64_t waves = (int64_t)((nh + own - 1) / own) * ((nv + rows - 1) / rows);
+    const unsigned gw = (unsigned)((waves + 3) / 4);
+    for (int v = 0; v < nvals; v += 2) {
+        const int nv2 = nvals - v >= 2 ? 2 : 1;
+        const double* fv = f + v * n;
+        const double* gi = gin ? gin + 2 * v * n : nullptr;
+        double* o1 = gout1 + 2 * v * n;
+        double* o2 = gout2 ? gout2 + 2 * v * n : nullptr;
+        double* chords = ring_work;
+        double* acc = ring_work + 7 * L;
+        if (nv2 == 2) {
+            k_gd_ring_chords<2><<<grr, kBlock, 0, s>>>(g, fv, gi, chords);
+            SweepArgs<2> a{fv, gi, gprev ? gprev + 2 * v * n : nullptr, om1, om2, o1, o2, chords, acc, chg, rows};
+            if (kk == 2 && occ == 2) k_gd_sweeps<2, 2, 1, 2><<<gw, 256, 0, s>>>(g, a);
+            else if (kk == 2 && occ == 5) k_gd_sweeps<2, 2, 3, 2><<<gw, 256, 0, s>>>(g, a);
+            else if (kk == 2 && occ == 3) k_gd_sweeps<2, 2, 3><<<gw, 256, 0, s>>>(g, a);
+            else if (kk == 2 && occ == 4) k_gd_sweeps<2, 2, 4><<<gw, 256, 0, s>>>(g, a);
+            else if (kk == 2) k_gd_sweeps<2, 2, 1><<<gw, 256, 0, s>>>(g, a);
+            else k_gd_sweeps<2, 1, 1><<<gw, 256, 0, s>>>(g, a);
+            if (kk == 2)
+                k_gd_grad_ring<2><<<grr, kBlock, 0, s>>>(g, fv, o1, o2, acc, chg ? chg + 1 : nullptr,
+                                                         Cheb{gi, om2, gi ? 0 : 1});
+        } else {
+            k_gd_ring_chords<1><<<grr, kBlock, 0, s>>>(g, fv, gi, chords);
+            SweepArgs<1> a{fv, gi, gprev ? gprev + 2 * v * n : nullptr, om1, om2, o1, o2, chords, acc, chg, rows};
+            if (kk == 2) k_gd_sweeps<1, 2, 1><<<gw, 256, 0, s>>>(g, a);
+            else k_gd_sweeps<1, 1, 1><<<gw, 256, 0, s>>>(g, a);
+            if (kk == 2)
+                k_gd_grad_ring<1><<<grr, kBlock, 0, s>>>(g, fv, o1, o2, acc, chg ? chg + 1 : nullptr,
+                                                         Cheb{gi, om2, gi ? 0 : 1});
+        }
+        int st = launch_status("k_gd_sweeps");
         if (st) return st;
     }
     return 0;
@@ -949,7 +1493,10 @@ int akb_gd_eval_f64(const double* x, const double* y, int nv, int nh, const uint
     int st = launch_status("k_fill_i32");
     if (st) return st;
     const int64_t ntri = 2 * (int64_t)(nv - 1) * (nh - 1) + npock;
-    k_gd_claim<<<grid_for(ntri - npock, 1, gd_grid_cap()), kBlock, 0, s>>>(g, t, owner);
+    if (getenv("AKB_GD_CLAIM_TRI"))  // the per-triangle claim (A/B and the tests' cross-check)
+        k_gd_claim<<<grid_for(ntri - npock, 1, gd_grid_cap()), kBlock, 0, s>>>(g, t, owner);
+    else
+        k_gd_claim_cells<<<grid_for((ntri - npock) / 2, 1, kStreamGridCap), kBlock, 0, s>>>(g, t, owner);
     st = launch_status("k_gd_claim");
     if (st) return st;
     if (npock > 0) {

@@ -44,17 +44,49 @@ def _normal_solve(mom, nb):
 
 
 class _Moments:
-    def __init__(self, dev):
-        L = _lib.lib()
-        self.work = torch.empty(int(L.akb_moments_work_bytes()) // 8, dtype=D.F64, device=dev)
-        self.out = torch.empty(21, dtype=D.F64, device=dev)
+    """akb_map_moments_f64 over k maps at once: one launch per map, one host copy for all of them."""
 
-    def __call__(self, z, nb, coef=None, thr=0.0, mode=0, mean=0.0):
+    def __init__(self, dev, k=1):
         L = _lib.lib()
-        ny, nx = int(z.shape[0]), int(z.shape[1])
-        _lib.check(L.akb_map_moments_f64(D.ptr(z), ny, nx, nb, D.ptr(coef), float(thr), mode, float(mean),
-                                         D.ptr(self.out), D.ptr(self.work), D.stream_handle()))
-        return self.out.cpu().numpy()
+        self.k = k
+        self.work = torch.empty((k, int(L.akb_moments_work_bytes()) // 8), dtype=D.F64, device=dev)
+        self.out = torch.empty((k, 21), dtype=D.F64, device=dev)
+
+    def __call__(self, zs, nb, coefs=None, thr=None, mode=0, means=None):
+        L = _lib.lib()
+        for j, z in enumerate(zs):
+            ny, nx = int(z.shape[0]), int(z.shape[1])
+            _lib.check(L.akb_map_moments_f64(D.ptr(z), ny, nx, nb, D.ptr(coefs[j] if coefs else None),
+                                             float(thr[j] if thr else 0.0), mode, float(means[j] if means else 0.0),
+                                             D.ptr(self.out[j]), D.ptr(self.work[j]), D.stream_handle()))
+        return self.out[:len(zs)].cpu().numpy()
+
+
+def _plane_corrections(zs, sigma_threshold=3):
+    """plane_correction_with_nan_and_outlier_filter of each map in zs (device tensors), in lockstep so
+    each of the four stages costs one host copy for all the maps."""
+    mom = _Moments(zs[0].device, len(zs))
+    m0 = mom(zs, 5)
+    for m in m0:
+        if m[20] < 5:
+            # curve_fit refuses fewer points than parameters (:9667)
+            raise TypeError(f"Improper input: func (m=5) must not exceed the data count N={int(m[20])}")
+    c1 = [torch.from_numpy(_normal_solve(m, 5)).to(zs[0].device) for m in m0]
+    cnt = mom(zs, 5, c1, mode=1)
+    means = [c[0] / c[20] for c in cnt]
+    ss = mom(zs, 5, c1, mode=2, means=means)
+    thr = [sigma_threshold * np.sqrt(v[0] / c[20]) for v, c in zip(ss, cnt)]
+    m1 = mom(zs, 3, c1, thr=thr)
+    outs = []
+    for z, m in zip(zs, m1):
+        if m[20] < 3:
+            raise TypeError(f"Improper input: func (m=3) must not exceed the data count N={int(m[20])}")
+        p2 = torch.from_numpy(_normal_solve(m, 3)).to(z.device)
+        out = torch.empty_like(z)
+        _lib.check(_lib.lib().akb_plane_subtract_f64(D.ptr(z), int(z.shape[0]), int(z.shape[1]), D.ptr(p2),
+                                                     D.ptr(out), D.stream_handle()))
+        outs.append(out)
+    return outs
 
 
 def plane_correction_with_nan_and_outlier_filter(data, sigma_threshold=3):
@@ -64,24 +96,7 @@ def plane_correction_with_nan_and_outlier_filter(data, sigma_threshold=3):
     z = _as_dev(data)
     if z.dim() != 2:
         raise ValueError("data must be 2-D")
-    mom = _Moments(z.device)
-    m0 = mom(z, 5)
-    if m0[20] < 5:
-        # curve_fit refuses fewer points than parameters (:9667)
-        raise TypeError(f"Improper input: func (m=5) must not exceed the data count N={int(m0[20])}")
-    p1 = _normal_solve(m0, 5)
-    c1 = torch.from_numpy(p1).to(z.device)
-    cnt = mom(z, 5, c1, mode=1)
-    mean = cnt[0] / cnt[20]
-    ss = mom(z, 5, c1, mode=2, mean=mean)
-    sigma = np.sqrt(ss[0] / cnt[20])
-    m1 = mom(z, 3, c1, thr=sigma_threshold * sigma)
-    if m1[20] < 3:
-        raise TypeError(f"Improper input: func (m=3) must not exceed the data count N={int(m1[20])}")
-    p2 = torch.from_numpy(_normal_solve(m1, 3)).to(z.device)
-    out = torch.empty_like(z)
-    _lib.check(_lib.lib().akb_plane_subtract_f64(D.ptr(z), int(z.shape[0]), int(z.shape[1]), D.ptr(p2),
-                                                 D.ptr(out), D.stream_handle()))
+    out = _plane_corrections([z], sigma_threshold)[0]
     return out if as_torch else out.cpu().numpy()
 
 
@@ -139,17 +154,35 @@ def wave_maps(detcenter2, dist_err2, wave2, ray_num_H, ray_num_V, grid_num_H=Non
     from .griddata import CubicGrid
     d2 = _as_dev(detcenter2)
     y, z = d2[1].contiguous(), d2[2].contiguous()
-    ext = torch.stack([y.min(), y.max(), z.min(), z.max()]).cpu().numpy()
+    cg = CubicGrid(y, z, int(ray_num_V), int(ray_num_H))
+    ext = cg.extent  # min / max of the hits' y and z (on the lattice's boundary ring, exactly)
     gx = np.linspace(ext[0], ext[1], int(grid_num_H or ray_num_H))
     gy = np.linspace(ext[2], ext[3], int(grid_num_V or ray_num_V))
     grid_H, grid_V = np.meshgrid(gx, gy)
-    cg = CubicGrid(y, z, int(ray_num_V), int(ray_num_H))
     vals = torch.stack([_as_dev(dist_err2).reshape(-1), _as_dev(wave2).reshape(-1)])
     maps = cg.interp(vals, gx, gy)
     m_dist, m_wave = maps[0], maps[1]
     s, c = RowSums()(m_wave.reshape(1, -1), nan=True)
     m_wave = m_wave - (s / c.to(D.F64))[0]  # np.nanmean: nansum / count
+    w_c, d_c = _plane_corrections([m_wave.contiguous(), m_dist.contiguous()])
     return dict(grid_H=grid_H, grid_V=grid_V, matrixDistError2=m_dist, matrixWave2=m_wave,
-                matrixWave2_Corrected=plane_correction_with_nan_and_outlier_filter(m_wave),
-                matrixDistError2_Corrected=plane_correction_with_nan_and_outlier_filter(m_dist),
-                sweeps=cg.sweeps)
+                matrixWave2_Corrected=w_c, matrixDistError2_Corrected=d_c, sweeps=cg.sweeps)
+
+
+def wave_pupil(detcenter2, wave2, ray_num_H, ray_num_V, grid_num_H=None, grid_num_V=None):
+    """The PSF's half of the driver's gridding step (AKB_raytrace_20250312.py:3653-3696): grid,
+    griddata(cubic) of Wave2, minus its nanmean, plane-corrected - matrixWave2_Corrected, the map
+    psf_calc transforms (:3698-3700). The same arithmetic as wave_maps' Wave2 (one value set on the
+    triangulation instead of two); matrixDistError2, the driver's other map, feeds no PSF.
+    Returns (matrixWave2_Corrected device tensor, grid_H, grid_V, gradient sweeps)."""
+    from .griddata import CubicGrid
+    d2 = _as_dev(detcenter2)
+    cg = CubicGrid(d2[1].contiguous(), d2[2].contiguous(), int(ray_num_V), int(ray_num_H))
+    ext = cg.extent
+    gx = np.linspace(ext[0], ext[1], int(grid_num_H or ray_num_H))
+    gy = np.linspace(ext[2], ext[3], int(grid_num_V or ray_num_V))
+    grid_H, grid_V = np.meshgrid(gx, gy)
+    m_wave = cg.interp(_as_dev(wave2).reshape(1, -1), gx, gy)[0]
+    s, c = RowSums()(m_wave.reshape(1, -1), nan=True)
+    m_wave = m_wave - (s / c.to(D.F64))[0]
+    return _plane_corrections([m_wave.contiguous()])[0], grid_H, grid_V, cg.sweeps

@@ -76,6 +76,8 @@ def parse():
     p.add_argument("--no-extras", action="store_true",
                    help="skip single_run_ms / faithful_psf_chain_ms / huygens_pairs_per_s")
     p.add_argument("--pupil", type=int, default=128)
+    p.add_argument("--faithful-steps", type=int, default=10,
+                   help="steps of the trace + faithful-PSF loop reported as faithful_step (outside the timed region)")
     p.add_argument("--pad", type=int, default=16)
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -180,25 +182,42 @@ def system_variants(geom, k):
     return out
 
 
-def faithful_psf_chain(rw, out, size):
-    """The reference's own pupil for the PSF: griddata(cubic) of Wave2 and
-    DistError2 from the detector-2 hits onto a size x size grid, nanmean removal, plane
-    correction (pupilmap.wave_maps), then psf_calc (rotation estimate, rotate_with_nan, pad-16
-    PSF, trim). Wall time with the device synchronised (its host steps included), ms; median of 3."""
+def faithful_psf(out, n, size):
+    """The reference's own PSF of one trace: griddata(cubic) of Wave2 from the
+    detector-2 hits onto a size x size grid, nanmean removal, plane correction (pupilmap.wave_pupil),
+    then psf_calc (rotation estimate, rotate_with_nan, pad-16 PSF, trim)."""
+    from akbraytracing_amd import pupilmap as PM
+    from akbraytracing_amd.psfcalc import psf_calc
+    m, gh, gv, _ = PM.wave_pupil(out["detcenter2"], out["wave2"], n, n, grid_num_H=size, grid_num_V=size)
+    return psf_calc(m, gh, gv, 1e-2)
+
+
+def faithful_psf_chain(rw, out, size, reps=5):
+    """Wall time (ms, device synchronised, host steps included; median of reps) of faithful_psf on
+    the last step's trace, and of the driver's whole gridding step (pupilmap.wave_maps: DistError2's
+    map too, which feeds no PSF) + psf_calc."""
     import torch
     from akbraytracing_amd import pupilmap as PM
     from akbraytracing_amd.psfcalc import psf_calc
     det2 = out["detcenter2"].clone()
     e2, w2 = out["dist_err2"].clone(), out["wave2"].clone()
-    times = []
-    for _ in range(3):
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
+    src = dict(detcenter2=det2, wave2=w2)
+
+    def timed(f):
+        times = []
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            f()
+            torch.cuda.synchronize()
+            times.append((time.perf_counter() - t0) * 1e3)
+        return sorted(times)[reps // 2]
+
+    def both():
         m = PM.wave_maps(det2, e2, w2, rw.n, rw.n, grid_num_H=size, grid_num_V=size)
         psf_calc(m["matrixWave2_Corrected"], m["grid_H"], m["grid_V"], 1e-2)
-        torch.cuda.synchronize()
-        times.append((time.perf_counter() - t0) * 1e3)
-    return sorted(times)[1]
+
+    return timed(lambda: faithful_psf(src, rw.n, size)), timed(both)
 
 
 def huygens_rate(out):
@@ -393,6 +412,25 @@ def main():
         st = comm.allreduce_max(torch.tensor([sorted(single)[2]], dtype=torch.float64, device=dev))
         single_ms = float(st.item())
 
+    # steps with the reference's own PSF: each step traces a system (run(): pass 1, resample, pass 2,
+    # tilt, OPD) and forms its faithful PSF (faithful_psf), nothing overlapped across steps
+    faithful_steps = None
+    if world == 1 and not args.no_extras:
+        ft = []
+        for i in range(args.faithful_steps + 2):
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            o = rw.run(geometry=sys_of(i), next_geometry=sys_of(i + 1))
+            faithful_psf(o, rw.n, args.pupil)
+            torch.cuda.synchronize()
+            if i >= 2:
+                ft.append((time.perf_counter() - t1) * 1e3)
+        ms = sorted(ft)[len(ft) // 2]
+        faithful_steps = {"ms_per_step": ms, "steps": len(ft),
+                          "intersections_per_s": rw.intersections_per_run() / (ms * 1e-3),
+                          "what": "run() (trace, resample, tilt, OPD) + griddata(cubic) of Wave2 -> nanmean -> plane "
+                                  f"correction -> psf_calc on the {args.pupil}^2 grid, one system per step, median"}
+
     if rank != 0:
         return
     k_ms = [a.elapsed_time(b) for a, b in rw.kernel_events] if rw.kernel_events else [float('nan')]
@@ -498,7 +536,13 @@ def main():
                                  "(tests/test_c4_gpu.py, tests/test_dist_gpu.py)")
     if world == 1 and last_out is not None:
         out["huygens_pairs_per_s"] = huygens_rate(last_out)
-        out["faithful_psf_chain_ms"] = faithful_psf_chain(rw, last_out, args.pupil)
+        chain_ms, maps_ms = faithful_psf_chain(rw, last_out, args.pupil)
+        # the PSF of the reference's own pupil: griddata(cubic) -> nanmean -> plane correction ->
+        # psf_calc on this trace's 1e7 detector-2 hits
+        out["faithful_psf_chain_ms"] = chain_ms
+        out["faithful_wave_maps_psf_ms"] = maps_ms
+        if faithful_steps is not None:
+            out["faithful_step"] = faithful_steps
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, gdict)
     print(json.dumps(out), flush=True)

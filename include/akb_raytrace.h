@@ -462,8 +462,11 @@ int akb_warp_affine_f64(const double* img, int ny, int nx, const double* iM, int
  * set = folded grid) -> akb_gd_pockets (HOST: the triangles between the boundary ring and the
  * convex hull, ring coordinates from akb_gd_cells_f64; ids >= 2 (n_v-1)(n_h-1)) ->
  * akb_gd_check_pockets. Gradients: akb_gd_grad_sweep_f64 (one Jacobi sweep of scipy's
- * estimate_gradients_2d_global local solve, largest relative change atomically max-ed into
- * *d_change as double bits; ring_work: 10 * ring-length doubles) until converged. Values: akb_gd_eval_f64 (NaN outside the hull). */
+ * estimate_gradients_2d_global local solve, largest relative change of that Jacobi step
+ * atomically max-ed into *d_change as double bits; ring_work: 10 * ring-length doubles; with
+ * gprev != NULL a Chebyshev step, gout = omega * (jacobi(gin) - gprev) + gprev; gprev == NULL:
+ * a plain sweep, line Gauss-Seidel unless AKB_GD_GS=0 or omega == 0) until converged.
+ * Values: akb_gd_eval_f64 (NaN outside the hull). */
 int akb_gd_cells_f64(const double* x, const double* y, int nv, int nh, uint8_t* diag, double tol, unsigned* d_flags,
                      double* ring_x, double* ring_y, void* stream);
 int akb_gd_pockets(const double* ring_x, const double* ring_y, int nv, int nh, int cap, int32_t* n_out,
@@ -473,8 +476,17 @@ int akb_gd_check_pockets(const double* x, const double* y, int nv, int nh, const
                          unsigned* d_flags, void* stream);
 int akb_gd_grad_sweep_f64(const double* x, const double* y, int nv, int nh, const uint8_t* diag, int npock,
                           const int32_t* ptri, const int32_t* pnbr, const int32_t* edge_tri, const int32_t* xptr,
-                          const int32_t* xidx, const double* f, int nvals, const double* gin, double* gout,
-                          double* ring_work, unsigned long long* d_change, void* stream);
+                          const int32_t* xidx, const double* f, int nvals, const double* gin, const double* gprev,
+                          double omega, double* gout, double* ring_work, unsigned long long* d_change, void* stream);
+/* kk = 1 or 2 sweeps in one launch (register kernel, wave-shift neighbours, the second sweep one row
+ * behind the first): gout1 = x_{k+1}, gout2 = x_{k+2} from gin = x_k (NULL: zeros) and gprev =
+ * x_{k-1} (NULL: the first sweep is plain), Chebyshev weights om1, om2; the same bits as kk calls of
+ * akb_gd_grad_sweep_f64. d_change[0..kk-1]: the sweeps' changes; ring_work: 14 * ring-length doubles. */
+int akb_gd_grad_sweeps_f64(const double* x, const double* y, int nv, int nh, const uint8_t* diag, int npock,
+                           const int32_t* ptri, const int32_t* pnbr, const int32_t* edge_tri, const int32_t* xptr,
+                           const int32_t* xidx, const double* f, int nvals, const double* gin, const double* gprev,
+                           double om1, double om2, int kk, double* gout1, double* gout2, double* ring_work,
+                           unsigned long long* d_change, void* stream);
 int akb_gd_eval_f64(const double* x, const double* y, int nv, int nh, const uint8_t* diag, int npock,
                     const int32_t* ptri, const int32_t* pnbr, const int32_t* edge_tri, const double* gx, int mx,
                     const double* gy, int my, const double* f, const double* grad, int nvals, int* owner,

@@ -971,6 +971,22 @@ def test_griddata_cubic_vs_scipy(gpu, nv, nh):
     assert np.nanmax(np.abs(got - want)) <= _scale_tol(want)
 
 
+@pytest.mark.parametrize("nv,nh,m", [(97, 113, 40), (280, 300, 128), (300, 280, 7), (33, 257, 300)])
+def test_griddata_cell_claim_equals_triangle_claim(gpu, monkeypatch, nv, nh, m):
+    """The per-cell claim kernel (index boxes estimated from the linspace axes) claims exactly the
+    targets the per-triangle kernel does: the same values and NaN mask, bit for bit."""
+    from akbraytracing_amd.griddata import CubicGrid
+    X, Y, F = _lattice(nv, nh, nv * 7 + nh)
+    X = X * (nh / nv)  # square-ish cells for the wide grids (a triangulable lattice)
+    gx = np.linspace(X.min(), X.max(), m)
+    gy = np.linspace(Y.min() - 1e-6, Y.max(), m + 3)  # some targets outside the hull
+    cg = CubicGrid(X.ravel(), Y.ravel(), nv, nh)
+    got = cg.interp(F.ravel(), gx, gy).cpu().numpy()
+    monkeypatch.setenv("AKB_GD_CLAIM_TRI", "1")
+    want = cg.interp(F.ravel(), gx, gy).cpu().numpy()
+    assert np.array_equal(got, want, equal_nan=True)
+
+
 def test_griddata_batched_values_and_errors(gpu):
     from akbraytracing_amd import _lib
     from akbraytracing_amd.griddata import CubicGrid, griddata
@@ -1006,13 +1022,26 @@ def test_gradient_sweep_strip_equals_gather(gpu, monkeypatch, nv, nh, nvals):
     for mode in ("64", "128", "256", "0"):
         monkeypatch.setenv("AKB_GD_STRIP", mode)
         cg = CubicGrid(X.ravel(), Y.ravel(), nv, nh)
-        g = cg.gradients(vals, maxiter=5, check_every=5)  # five sweeps from zero
+        g = cg.gradients(vals, maxiter=5, check_every=5, method="sweep")  # five sweeps from zero
         out[mode] = (g.cpu().numpy(), cg.sweeps)
-        g2 = cg.gradients(vals)  # to convergence
+        g2 = cg.gradients(vals, tol=1e-10, method="sweep")  # to convergence
+        # Chebyshev, one sweep per launch of this kernel (5 sweeps)
+        out[mode + "x"] = (cg.gradients(vals, maxiter=5, check_every=5, method="chebyshev-strip").cpu().numpy(),
+                           cg.sweeps)
         out[mode + "c"] = (g2.cpu().numpy(), cg.sweeps)
     for w in ("64", "128", "256"):
         assert np.array_equal(out[w][0], out["0"][0]) and out[w][1] == out["0"][1], w
         assert np.array_equal(out[w + "c"][0], out["0c"][0]) and out[w + "c"][1] == out["0c"][1], w
+        assert np.array_equal(out[w + "x"][0], out["0x"][0]), w
+    # the register kernel's two sweeps per launch: the same bits (2 + 2 + 1 launches, and 3 + 2 in
+    # two batches, row chunks that do not divide the grid)
+    cg = CubicGrid(X.ravel(), Y.ravel(), nv, nh)
+    assert np.array_equal(cg.gradients(vals, maxiter=5, check_every=5).cpu().numpy(), out["0x"][0])
+    assert np.array_equal(cg.gradients(vals, maxiter=5, check_every=3, adaptive=False).cpu().numpy(), out["0x"][0])
+    for rows in ("4", "7", "32"):
+        monkeypatch.setenv("AKB_GD_ROWS", rows)
+        cg = CubicGrid(X.ravel(), Y.ravel(), nv, nh)
+        assert np.array_equal(cg.gradients(vals, maxiter=5, check_every=5).cpu().numpy(), out["0x"][0]), rows
 
 
 @pytest.mark.parametrize("nv,nh", [(97, 113), (300, 280), (33, 257)])
@@ -1028,13 +1057,20 @@ def test_gradient_sweep_line_gauss_seidel(gpu, monkeypatch, nv, nh):
     for gs in ("0", "1", "1"):
         monkeypatch.setenv("AKB_GD_GS", gs)
         cg = CubicGrid(X.ravel(), Y.ravel(), nv, nh)
-        g = cg.gradients(vals, check_every=1).cpu().numpy()
+        g = cg.gradients(vals, tol=1e-10, check_every=1, method="sweep").cpu().numpy()
         res.setdefault(gs, []).append((g, cg.sweeps))
     (gj, sj), = res["0"]
     (g1, s1), (g2, s2) = res["1"]
     assert np.array_equal(g1, g2) and s1 == s2
     assert s1 < sj, (s1, sj)
     assert np.max(np.abs(g1 - gj)) <= 1e-8 * np.max(np.abs(gj))
+    # Chebyshev-accelerated Jacobi: the same fixed point, in fewer sweeps than either, deterministic
+    cg = CubicGrid(X.ravel(), Y.ravel(), nv, nh)
+    gc = cg.gradients(vals, tol=1e-10, check_every=1).cpu().numpy()
+    sc = cg.sweeps
+    assert np.array_equal(gc, cg.gradients(vals, tol=1e-10, check_every=1).cpu().numpy())
+    assert sc < s1, (sc, s1)
+    assert np.max(np.abs(gc - gj)) <= 1e-8 * np.max(np.abs(gj))
 
 
 def test_wave_maps_chain_vs_reference(gpu):
