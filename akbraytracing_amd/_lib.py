@@ -39,7 +39,7 @@ EXPORTS = [
     "akb_pairwise_work_bytes", "akb_pairwise_sum_f64", "akb_pupil_sample_f64",
     "akb_leaf_sink_bytes", "akb_leaf_sink_layout", "akb_leaf_finish_work_bytes", "akb_leaf_finish_f64",
     "akb_leaf_parts_f64", "akb_parts_chain_f64",
-    "akb_huygens_work_bytes", "akb_huygens_f64", "akb_scale_field_f64",
+    "akb_huygens_splits", "akb_huygens_work_bytes", "akb_huygens_f64", "akb_scale_field_f64",
     "akb_psf_work_bytes", "akb_psf_f64", "akb_psf_release_plans", "akb_selftest_arith_f64",
     "akb_first_valid_rows_f64", "akb_rotate_work_bytes", "akb_rotate_with_nan_f64",
     "akb_moments_work_bytes", "akb_map_moments_f64", "akb_plane_subtract_f64", "akb_legendre_rows_f64",
@@ -143,9 +143,10 @@ def _declare(L):
         "akb_parts_chain_f64": ([c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp], c_int),
         "akb_pairwise_work_bytes": ([c_int, c_i64], c_i64),
         "akb_pairwise_sum_f64": ([c_vp, c_i64, c_int, c_i64, c_int, c_vp, c_vp, c_vp, c_vp], c_int),
-        "akb_huygens_work_bytes": ([c_i64, c_i64], c_i64),
-        "akb_huygens_f64": ([c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_dbl, c_vp, c_vp, c_vp],
-                            c_int),
+        "akb_huygens_splits": ([c_i64, c_i64], c_int),
+        "akb_huygens_work_bytes": ([c_i64, c_i64, c_int], c_i64),
+        "akb_huygens_f64": ([c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_dbl, c_vp, c_int, c_vp,
+                             c_vp], c_int),
         "akb_scale_field_f64": ([c_vp, c_vp, c_i64, c_vp, c_vp], c_int),
         "akb_psf_work_bytes": ([c_int, c_int, c_int, c_int], c_i64),
         "akb_psf_f64": ([c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_dbl, c_dbl, c_vp, c_vp, c_dbl, c_vp,

@@ -191,31 +191,34 @@ __global__ void __launch_bounds__(kBlock) k_scale_field(const double* u, const d
 using namespace akb;
 
 // workgroups of k_huygens the device holds at once (CUs x resident workgroups per CU), 0 if the
-// runtime cannot say (no device)
+// runtime cannot say (no device); a function-local static, initialised once and thread-safely
 static int huygens_slots() {
-    static int cached = -1;
-    if (cached < 0) {
+    static const int cached = [] {
         int dev = 0, cus = 0, per_cu = 0;
         if (hipGetDevice(&dev) == hipSuccess &&
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
             hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_huygens, kHuyBlock, 0) == hipSuccess)
-            cached = cus * per_cu;
-        else {
-            (void)hipGetLastError();
-            cached = 0;
-        }
-    }
+            return cus * per_cu;
+        (void)hipGetLastError();
+        return 0;
+    }();
     return cached;
 }
 
 #ifndef AKB_HUY_ROUNDS
 #define AKB_HUY_ROUNDS 64
 #endif
+// split partials are capped at this much scratch (2 doubles per target per split): 512 MiB holds
+// 7943 splits of the C2 stage's 4225 targets, ~53 rounds
+constexpr int64_t kHuyScratchBytes = 512ll << 20;
+
 // how many source splits a launch uses: a whole number of rounds of resident workgroups
 // (splits x target blocks = kRounds x the device's slots; measured on the C2 stage: 2052
 // workgroups over 1280 slots, 1.6 rounds, 170.7 ms; 1 round 200 ms, 2 rounds 174, 4 142, 8 125,
 // 16 118, 64 113.6 ms: finer pieces even out the workgroups' finishing times), at least kMinSplit
-// sources per split
+// sources per split, and partials within kHuyScratchBytes. The count depends on the device (its
+// slots) and on n: a target-sharded caller passes the whole problem's count to every piece
+// (akb_huygens_splits) so each target's sum is the same whatever the sharding.
 static int huygens_splits(int64_t n, int64_t m) {
     constexpr int64_t kRounds = AKB_HUY_ROUNDS;
     const int64_t per_block = (int64_t)kHuyBlock * kTPL;
@@ -227,23 +230,30 @@ static int huygens_splits(int64_t n, int64_t m) {
     int64_t maxs = (m + kMinSplit - 1) / kMinSplit;
     if (maxs < 1) maxs = 1;
     int64_t s = want < maxs ? want : maxs;
+    const int64_t cap = n > 0 ? kHuyScratchBytes / (2 * n * (int64_t)sizeof(double)) : s;
+    if (s > cap) s = cap;
     if (s > 65535) s = 65535;
     return (int)(s < 1 ? 1 : s);
 }
 
+static int64_t huygens_work_bytes(int64_t n, int splits) {
+    if (n <= 0 || splits <= 1) return 0;
+    const int64_t chunks = (splits + kRedChunk - 1) / kRedChunk;
+    return ((int64_t)splits + (chunks > 1 ? chunks : 0)) * 2 * n * (int64_t)sizeof(double);
+}
+
 extern "C" {
 
-int64_t akb_huygens_work_bytes(int64_t n, int64_t m) {
+int akb_huygens_splits(int64_t n, int64_t m) { return n > 0 && m > 0 ? huygens_splits(n, m) : 1; }
+
+int64_t akb_huygens_work_bytes(int64_t n, int64_t m, int splits) {
     if (n <= 0 || m <= 0) return 0;
-    const int s = huygens_splits(n, m);
-    if (s <= 1) return 0;
-    const int64_t chunks = (s + kRedChunk - 1) / kRedChunk;
-    return ((int64_t)s + (chunks > 1 ? chunks : 0)) * 2 * n * (int64_t)sizeof(double);
+    return huygens_work_bytes(n, splits > 0 ? splits : huygens_splits(n, m));
 }
 
 int akb_huygens_f64(const double* tx, const double* ty, const double* tz, int64_t n,
                     const double* sx, const double* sy, const double* sz, const double* u_re_im,
-                    int64_t m, double k, double* out_re_im, void* work, void* stream) {
+                    int64_t m, double k, double* out_re_im, int splits, void* work, void* stream) {
     clear_error();
     AKB_REQUIRE(n >= 0 && m >= 0, "negative size");
     if (n == 0) return AKB_OK;
@@ -257,7 +267,8 @@ int akb_huygens_f64(const double* tx, const double* ty, const double* tz, int64_
     const int64_t per_block = (int64_t)kHuyBlock * kTPL;
     const int64_t blocks = (n + per_block - 1) / per_block;
     AKB_REQUIRE(blocks < (1LL << 31), "too many targets");
-    const int splits = huygens_splits(n, m);
+    if (splits <= 0) splits = huygens_splits(n, m);
+    AKB_REQUIRE(splits <= 65535, "at most 65535 source splits");
     AKB_REQUIRE(splits == 1 || work != nullptr, "work buffer required (akb_huygens_work_bytes)");
     const int64_t per_split = (m + splits - 1) / splits;
     double* dst = splits == 1 ? out_re_im : (double*)work;

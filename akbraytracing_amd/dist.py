@@ -139,15 +139,24 @@ def split_counts(n, world):
     return [base + (1 if r < rem else 0) for r in range(world)]
 
 
-def propagate_sharded(tx, ty, tz, sx, sy, sz, u_ds, k, comm):
+def propagate_sharded(tx, ty, tz, sx, sy, sz, u_ds, k, comm, propagate=None, splits=None):
     """Huygens stage with targets split over ranks (np.array_split order) and the result
-    all-gathered. tx.. are the FULL target arrays (device tensors) on every rank."""
-    from .wavecalc import propagate
+    all-gathered. tx.. are the FULL target arrays (device tensors) on every rank. Every rank sums
+    its sources in the whole problem's split order (splits: that count, default the library's for
+    the full sizes), so the gathered field is the one-process field bit for bit. propagate: the
+    per-rank kernel call (default wavecalc.propagate)."""
+    from . import wavecalc as W
     n = int(tx.shape[0])
+    if propagate is None:
+        propagate = W.propagate
+        if splits is None:
+            splits = W.splits_for(n, int(sx.shape[0]))
     counts = split_counts(n, comm.world)
     lo = sum(counts[:comm.rank])
     hi = lo + counts[comm.rank]
-    piece = propagate(tx[lo:hi].contiguous(), ty[lo:hi].contiguous(), tz[lo:hi].contiguous(), sx, sy, sz, u_ds, k)
+    kw = {} if splits is None else {"splits": splits}
+    piece = propagate(tx[lo:hi].contiguous(), ty[lo:hi].contiguous(), tz[lo:hi].contiguous(), sx, sy, sz, u_ds, k,
+                      **kw)
     return comm.allgather_field(piece, counts)
 
 

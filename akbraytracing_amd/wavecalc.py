@@ -30,20 +30,32 @@ def _field_dev(u, dev):
     return torch.from_numpy(np.ascontiguousarray(np.asarray(u, dtype=np.complex128))).to(dev)
 
 
-def propagate(tx, ty, tz, sx, sy, sz, u_ds, k, stream=None, work=None):
+_WORK = {}  # device -> the split partials' scratch, reused across calls (up to ~516 MiB)
+
+
+def splits_for(n, m):
+    """The source-split count the library picks for n targets and m sources (on this device)."""
+    return int(_lib.lib().akb_huygens_splits(int(n), int(m)))
+
+
+def propagate(tx, ty, tz, sx, sy, sz, u_ds, k, stream=None, work=None, splits=0):
     """Device API: all arguments float64 / complex128 device tensors (u_ds already times dS).
-    Returns the (N,) complex128 device tensor of target fields."""
+    splits: the source-split count (0: the library's for these sizes; a target-sharded caller
+    passes splits_for(whole target count, m) so every target's sum is the unsharded one, bit for
+    bit). Returns the (N,) complex128 device tensor of target fields."""
     L = _lib.lib()
     dev = tx.device
     n, m = int(tx.shape[0]), int(sx.shape[0])
     out = torch.empty(n, dtype=torch.complex128, device=dev)
-    need = int(L.akb_huygens_work_bytes(n, m))
+    need = int(L.akb_huygens_work_bytes(n, m, int(splits)))
     if need > 0 and (work is None or work.numel() * 8 < need):
-        work = torch.empty(need // 8 + 1, dtype=D.F64, device=dev)
+        work = _WORK.get(dev)
+        if work is None or work.numel() * 8 < need:
+            work = _WORK[dev] = torch.empty(need // 8 + 1, dtype=D.F64, device=dev)
     ur = torch.view_as_real(u_ds)
     _lib.check(L.akb_huygens_f64(D.ptr(tx), D.ptr(ty), D.ptr(tz), n, D.ptr(sx), D.ptr(sy), D.ptr(sz), D.ptr(ur), m,
-                                 float(k), D.ptr(torch.view_as_real(out)), D.ptr(work) if need > 0 else None,
-                                 D.stream_handle(stream)))
+                                 float(k), D.ptr(torch.view_as_real(out)), int(splits),
+                                 D.ptr(work) if need > 0 else None, D.stream_handle(stream)))
     return out
 
 
@@ -88,6 +100,10 @@ def forward_propagation_cupy_batch_multi_gpu(x, y, z, u_back_x, u_back_y, u_back
     pieces = [np.array_split(a, len(devs)) for a in x_np]
     results = [None] * len(devs)
     errors = []
+    # every piece sums its sources in the whole problem's split order: the concatenated field is
+    # the one-device field bit for bit
+    with torch.cuda.device(devs[0]):
+        splits = splits_for(x_np[0].shape[0], np.shape(u_back_u)[0])
 
     def work(i, dev_id):
         try:
@@ -95,7 +111,7 @@ def forward_propagation_cupy_batch_multi_gpu(x, y, z, u_back_x, u_back_y, u_back
                 dev = torch.device("cuda", dev_id)
                 _, tx, ty, tz, sx, sy, sz, u = _prepare(pieces[0][i], pieces[1][i], pieces[2][i], u_back_x,
                                                         u_back_y, u_back_z, u_back_u, ds, dev)
-                results[i] = propagate(tx, ty, tz, sx, sy, sz, u, k).cpu().numpy()
+                results[i] = propagate(tx, ty, tz, sx, sy, sz, u, k, splits=splits).cpu().numpy()
         except Exception as e:  # surfaced after join
             errors.append(e)
 

@@ -155,11 +155,27 @@ def read_conditions(folder):
     return c
 
 
+def load_npz_data(filename):
+    """load_npz_data (CPU0402.py:173-187): the 'data' array of an .npz, or None when the file does not
+    exist. Loaded without pickle (numpy's default)."""
+    if os.path.exists(filename):
+        with np.load(filename) as data:
+            return data["data"]
+    return None
+
+
 def run_wave_chain(folder, out_dir=None, files=("points_source.npy", "points_M1.npy", "points_M2.npy",
-                                                "points_gridImage.npy", "points_gridDefocus.npy")):
+                                                "points_gridImage.npy", "points_gridDefocus.npy"), resume_dir=".",
+                   resumed=None):
     """The Wavecalc_raytrace_fromData driver (CPU0402.py:186-380) on the device: source -> M1 ->
     M2 (-> M3 -> M4) -> image grid (scaled x2 about its mean) and the second image grid, saving
-    complex_data_<name>.npz (key 'data') into out_dir. Returns {name: field (numpy complex128)}."""
+    complex_data_<name>.npz (key 'data') into out_dir. Returns {name: field (numpy complex128)}.
+
+    Stage resume, as the driver does (:261-269, :281-290, and M3 / M4): a mirror stage whose
+    complex_data_M<k>.npz is found in resume_dir (the driver looks in the working directory, the
+    default here) takes that field instead of propagating, and it is not written again; None
+    switches resuming off (resumed, a list, receives the names of the stages taken from files). The
+    image stages are always computed."""
     from .wavecalc import WaveField3D
     cond = read_conditions(folder)
     akb = cond.get("option_AKB", True)
@@ -181,13 +197,22 @@ def run_wave_chain(folder, out_dir=None, files=("points_source.npy", "points_M1.
     chain = ["points_M1.npy", "points_M2.npy"] + (["points_M3.npy", "points_M4.npy"] if akb else [])
     dims = [(cond["ray_num_H1"], cond["ray_num_V1"]), (cond["ray_num_H2"], cond["ray_num_V2"])] * 2
     prev = src
+    resumed = [] if resumed is None else resumed
     for k, fname in enumerate(chain):
         pts = load(fname)
         f = WaveField3D(pts.shape[1], wl, *dims[k])
         f.setdata(pts)
-        f.forward_propagation(prev)
+        data = load_npz_data(os.path.join(resume_dir, f"complex_data_M{k + 1}.npz")) if resume_dir is not None else None
+        if data is not None:
+            if data.shape != (pts.shape[1],):
+                raise ValueError(f"complex_data_M{k + 1}.npz holds {data.shape} values for {pts.shape[1]} points")
+            f.u = np.asarray(data, dtype=np.complex128)
+            fields[f"M{k + 1}"] = f.u
+            resumed.append(f"M{k + 1}")
+        else:
+            f.forward_propagation(prev)
+            store(f"M{k + 1}", f.u)
         f.set_ds(pts[3, :])
-        store(f"M{k + 1}", f.u)
         prev = f
     img = load(files[3]).copy()
     mean = [np.mean(img[0, :]), np.mean(img[1, :]), np.mean(img[2, :])]

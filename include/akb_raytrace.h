@@ -363,13 +363,21 @@ int akb_pairwise_sum_f64(const double* x, int64_t ld, int rows, int64_t n, int n
 
 /* out[i] = sum_j u_j * exp(-i k r_ij) / r_ij,  r_ij = sqrt(((xi-xj)^2 + (yi-yj)^2) + (zi-zj)^2)
  * u_j = u_re_im[2j] + i u_re_im[2j+1] already multiplied by dS_j (ref CPU0402 :102).
- * out_re_im: interleaved complex128 (N). work: device scratch of akb_huygens_work_bytes(n, m)
- * bytes (the sources are split over workgroups when the target set alone cannot fill the chip;
- * the partial sums are added in split order, so results are run-to-run deterministic). */
-int64_t akb_huygens_work_bytes(int64_t n, int64_t m);
+ * out_re_im: interleaved complex128 (N).
+ * splits: how many contiguous source ranges the sum is split over (0: the library's choice,
+ * akb_huygens_splits). A target's sum is each range's partial (sources in order) and then the
+ * partials summed in two ordered levels - chunks of 128 ranges, then the chunks - so it depends
+ * only on m and the split count: run-to-run deterministic, and the same for any subset of targets
+ * given the same split count (a target-sharded caller passes the whole problem's count). The
+ * library's count depends on the device (its resident workgroups) and on n; it is capped so the
+ * partials fit in 512 MiB.
+ * work: device scratch of akb_huygens_work_bytes(n, m, splits) bytes: 16 n (splits + ceil(splits /
+ * 128)) when splits > 1, at most ~516 MiB for the library's count (0 bytes for one split). */
+int akb_huygens_splits(int64_t n, int64_t m);
+int64_t akb_huygens_work_bytes(int64_t n, int64_t m, int splits);
 int akb_huygens_f64(const double* tx, const double* ty, const double* tz, int64_t n,
                     const double* sx, const double* sy, const double* sz, const double* u_re_im,
-                    int64_t m, double k, double* out_re_im, void* work, void* stream);
+                    int64_t m, double k, double* out_re_im, int splits, void* work, void* stream);
 /* u_out = u_in * ds (complex * real, ref CPU0402 :102 / GPU0402 :142) */
 int akb_scale_field_f64(const double* u_re_im, const double* ds, int64_t m, double* out_re_im,
                         void* stream);

@@ -134,3 +134,45 @@ def test_wavelength_sharded_psf_stack(tmp_path, world):
         assert d["mine"].tolist() == lams[r::world]
         assert np.array_equal(d["mine_psf"].reshape(-1), want[r::world].reshape(-1))
         assert np.array_equal(d["full"], want) and d["order"].tolist() == lams
+
+
+def _huygens_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle as O
+        from akbraytracing_amd.dist import TorchComm, propagate_sharded
+
+        def oracle_propagate(tx, ty, tz, sx, sy, sz, u, k):
+            # the per-rank kernel's stand-in (the HIP kernel is a gpu test): the oracle's C sum
+            return torch.from_numpy(O.huygens_c(tx.numpy(), ty.numpy(), tz.numpy(), sx.numpy(), sy.numpy(),
+                                                sz.numpy(), u.numpy(), k))
+
+        rng = np.random.default_rng(5)
+        n, m = 101, 700  # 101 targets: uneven pieces over 2 and 3 ranks
+        T = [torch.from_numpy(rng.random(n) * 1e-6 + o) for o in (1.0, 0.0, 0.0)]
+        S = [torch.from_numpy(rng.random(m) * 1e-3) for _ in range(3)]
+        u = torch.from_numpy(np.exp(2j * np.pi * rng.random(m)) * (1 + rng.random(m)))
+        got = propagate_sharded(*T, *S, u, 2 * np.pi / 13.5e-9, TorchComm(), propagate=oracle_propagate)
+        np.savez(os.path.join(out_dir, f"h{rank}.npz"), got=got.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_huygens_target_sharding_reassembles_one_process(tmp_path, world):
+    """dist.propagate_sharded (the _multi script's target split, :123-229): targets
+    in np.array_split pieces over the ranks, sources replicated, the field all-gathered in rank
+    order on every rank - the one-process field, value for value (each target's sum is independent
+    of the others; the HIP kernel's split order is pinned by tests/test_dist_gpu.py)."""
+    import oracle as O
+    mp.start_processes(_huygens_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    rng = np.random.default_rng(5)
+    n, m = 101, 700
+    T = [rng.random(n) * 1e-6 + o for o in (1.0, 0.0, 0.0)]
+    S = [rng.random(m) * 1e-3 for _ in range(3)]
+    u = np.exp(2j * np.pi * rng.random(m)) * (1 + rng.random(m))
+    want = O.huygens_c(*T, *S, u, 2 * np.pi / 13.5e-9)
+    for r in range(world):
+        assert np.array_equal(np.load(os.path.join(tmp_path, f"h{r}.npz"))["got"], want), r

@@ -139,3 +139,62 @@ def test_bench_two_ranks_runs_to_the_json_line(gpu, tmp_path):
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
     out = json.loads(line)
     assert out["n_gpus"] == 2 and out["value"] > 0
+
+
+def _huygens_field(n, m, seed=3):
+    rng = np.random.default_rng(seed)
+    T = [rng.random(n) * 2e-6 + o for o in (1.0, 0.0, 0.0)]
+    S = [rng.random(m) * 1e-3 for _ in range(3)]
+    u = np.exp(2j * np.pi * rng.random(m)) * (1 + rng.random(m))
+    return T, S, u
+
+
+def _huygens_rank(rank, world, port, n, m, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), AKB_DIST_BACKEND="gloo")
+    import torch.distributed as dist
+    from akbraytracing_amd import dist as AD
+    AD.init_from_env()
+    try:
+        dev = torch.device("cuda", torch.cuda.current_device())
+        T, S, u = _huygens_field(n, m)
+        td = [torch.from_numpy(a).to(dev) for a in T]
+        sd = [torch.from_numpy(a).to(dev) for a in S]
+        got = AD.propagate_sharded(*td, *sd, torch.from_numpy(u).to(dev), 2 * np.pi / 13.5e-9, AD.TorchComm(dev))
+        np.savez(os.path.join(out_dir, f"h{rank}.npz"), got=got.cpu().numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_huygens_sharded_over_ranks_is_one_process_bitwise(gpu, tmp_path, world):
+    """dist.propagate_sharded through the HIP kernel (ranks over gloo on the one GPU): every rank
+    sums its targets' sources in the whole problem's split order (wavecalc.splits_for), so the
+    gathered field equals one process's propagate bit for bit - a split count > 1 here (4225
+    targets cannot fill the chip alone)."""
+    from akbraytracing_amd import wavecalc as W
+    n, m = 4225, 300_000
+    T, S, u = _huygens_field(n, m)
+    assert W.splits_for(n, m) > 1
+    want = W.propagate(*(torch.from_numpy(a).to(gpu) for a in T), *(torch.from_numpy(a).to(gpu) for a in S),
+                       torch.from_numpy(u).to(gpu), 2 * np.pi / 13.5e-9).cpu().numpy()
+    torch.cuda.synchronize()
+    mp.start_processes(_huygens_rank, args=(world, _free_port(), n, m, str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    for r in range(world):
+        assert np.array_equal(np.load(os.path.join(tmp_path, f"h{r}.npz"))["got"], want), r
+
+
+def test_huygens_multi_gpu_threads_equal_one_device(gpu):
+    """forward_propagation_cupy_batch_multi_gpu (the _multi script's thread per device, :123-229)
+    with the device list [0, 0] (two host threads, one GPU): the concatenated pieces are the
+    one-device field bit for bit, and the reference's dS scaling is applied on both paths."""
+    from akbraytracing_amd import wavecalc as W
+    n, m = 5001, 200_000
+    T, S, u = _huygens_field(n, m, seed=9)
+    ds = np.random.default_rng(1).random(m) * 1e-12 + 1e-12
+    k = 2 * np.pi / 13.5e-9
+    one = W.forward_propagation_numpy_batch(*T, *S, u, k, ds)
+    two = W.forward_propagation_cupy_batch_multi_gpu(*T, *S, u, k, ds, devices=[0, 0])
+    three = W.forward_propagation_cupy_batch_multi_gpu(*T, *S, u, k, ds, devices=[0, 0, 0])
+    assert np.array_equal(two, one) and np.array_equal(three, one)
