@@ -116,6 +116,24 @@ class TorchComm:
         if self.world > 1:
             dist.barrier()
 
+    def gather_field(self, piece, counts, root=0):
+        """Concatenate per-rank 1-D pieces (lengths `counts`) in rank order on `root` (None on the
+        other ranks): one gather, each rank's piece crossing the links once."""
+        if self.world == 1:
+            return piece
+        if self._stage and piece.is_cuda:
+            got = self.gather_field(piece.cpu(), counts, root)
+            return got.to(piece.device) if got is not None else None
+        mx = max(counts)
+        pad = torch.zeros(mx, dtype=piece.dtype, device=piece.device)
+        pad[:piece.shape[0]] = piece
+        real = (lambda t: torch.view_as_real(t)) if pad.is_complex() else (lambda t: t)
+        bufs = [torch.empty_like(pad) for _ in range(self.world)] if self.rank == root else None
+        dist.gather(real(pad), gather_list=[real(b) for b in bufs] if bufs is not None else None, dst=root)
+        if self.rank != root:
+            return None
+        return torch.cat([b[:c] for b, c in zip(bufs, counts)])
+
     def allgather_field(self, piece, counts):
         """Concatenate per-rank 1-D pieces (lengths `counts`) in rank order on every rank."""
         if self.world == 1:
@@ -132,6 +150,33 @@ class TorchComm:
         else:
             dist.all_gather(bufs, pad)
         return torch.cat([b[:c] for b, c in zip(bufs, counts)])
+
+
+def gather_to_root(comm, pieces, counts, root=0):
+    """Concatenate each rank's 1-D pieces (a list of same-length tensors per rank; rank r holds
+    counts[r] elements) in rank order on `root` only: a list of full tensors there, None elsewhere.
+    SURVEY.md §8(e)'s route for the global griddata step: the (y, z, Wave2) triples of every shard
+    meet on one rank (24 B per ray: 2.4 GB at configs[3]'s 1e8 rays). gloo: staged through host
+    memory."""
+    if comm.world == 1:
+        return list(pieces)
+    out = [comm.gather_field(p, counts, root) for p in pieces]
+    return out if comm.rank == root else None
+
+
+def wave_pupil_sharded(rw, out, size, comm, root=0):
+    """The faithful pupil (pupilmap.wave_pupil) of a ray-sharded trace: each rank hands its rows of
+    detcenter2 (y, z) and Wave2 to `root` (gather_to_root), which grids the whole n x n lattice.
+    Returns wave_pupil's tuple on root, None elsewhere."""
+    from .pupilmap import wave_pupil
+    counts = [int(c) for c in comm.allgather_equal(
+        torch.tensor([rw.shard.count], dtype=torch.int64, device=out["wave2"].device)).reshape(-1).tolist()]
+    d2 = out["detcenter2"]
+    got = gather_to_root(comm, [d2[1].contiguous(), d2[2].contiguous(), out["wave2"].contiguous()], counts, root)
+    if got is None:
+        return None
+    y, z, w = got
+    return wave_pupil((y, z), w, rw.n, rw.n, grid_num_H=size, grid_num_V=size)
 
 
 def split_counts(n, world):

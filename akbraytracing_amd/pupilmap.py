@@ -174,10 +174,15 @@ def wave_pupil(detcenter2, wave2, ray_num_H, ray_num_V, grid_num_H=None, grid_nu
     griddata(cubic) of Wave2, minus its nanmean, plane-corrected - matrixWave2_Corrected, the map
     psf_calc transforms (:3698-3700). The same arithmetic as wave_maps' Wave2 (one value set on the
     triangulation instead of two); matrixDistError2, the driver's other map, feeds no PSF.
+    detcenter2 may also be the pair (y, z) of its rows 1 and 2.
     Returns (matrixWave2_Corrected device tensor, grid_H, grid_V, gradient sweeps)."""
     from .griddata import CubicGrid
-    d2 = _as_dev(detcenter2)
-    cg = CubicGrid(d2[1].contiguous(), d2[2].contiguous(), int(ray_num_V), int(ray_num_H))
+    if isinstance(detcenter2, (tuple, list)):
+        y, z = (_as_dev(a).reshape(-1) for a in detcenter2)
+    else:
+        d2 = _as_dev(detcenter2)
+        y, z = d2[1].contiguous(), d2[2].contiguous()
+    cg = CubicGrid(y, z, int(ray_num_V), int(ray_num_H))
     ext = cg.extent
     gx = np.linspace(ext[0], ext[1], int(grid_num_H or ray_num_H))
     gy = np.linspace(ext[2], ext[3], int(grid_num_V or ray_num_V))

@@ -431,6 +431,25 @@ def main():
                           "what": "run() (trace, resample, tilt, OPD) + griddata(cubic) of Wave2 -> nanmean -> plane "
                                   f"correction -> psf_calc on the {args.pupil}^2 grid, one system per step, median"}
 
+    # N > 1: the faithful PSF through SURVEY.md §8(e)'s route - every rank's (y, z, Wave2) rows
+    # gathered to rank 0, which grids the whole lattice and forms the PSF (collective; wall time
+    # between barriers, median of 3)
+    faithful_dist_ms = None
+    if world > 1 and last_out is not None:
+        from akbraytracing_amd.psfcalc import psf_calc
+        ft = []
+        for _ in range(3):
+            comm.barrier()
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            got = AD.wave_pupil_sharded(rw, last_out, args.pupil, comm)
+            if got is not None:
+                psf_calc(got[0], got[1], got[2], 1e-2)
+            torch.cuda.synchronize()
+            comm.barrier()
+            ft.append((time.perf_counter() - t1) * 1e3)
+        faithful_dist_ms = sorted(ft)[1]
+
     if rank != 0:
         return
     k_ms = [a.elapsed_time(b) for a, b in rw.kernel_events] if rw.kernel_events else [float('nan')]
@@ -530,6 +549,10 @@ def main():
     }
     if single_ms is not None:
         out["single_run_ms"] = single_ms
+    if faithful_dist_ms is not None:
+        out["faithful_psf_chain_ms"] = faithful_dist_ms
+        out["faithful_psf_route"] = (f"(y, z, Wave2) rows of the {world} ray shards gathered to rank 0 (24 B per ray), "
+                                     "griddata cubic -> nanmean -> plane correction -> psf_calc there")
     if world > 1:
         out["note_multi_gpu"] = ("shards are aligned to numpy's 8192-element sum buffers and the ranks' buffer sums "
                                  "are chained in numpy's order: N ranks give one process's bits "

@@ -176,3 +176,33 @@ def test_huygens_target_sharding_reassembles_one_process(tmp_path, world):
     want = O.huygens_c(*T, *S, u, 2 * np.pi / 13.5e-9)
     for r in range(world):
         assert np.array_equal(np.load(os.path.join(tmp_path, f"h{r}.npz"))["got"], want), r
+
+
+def _gather_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from akbraytracing_amd.dist import TorchComm, gather_to_root
+        counts = [5, 3, 4][:world]
+        lo = sum(counts[:rank])
+        a = torch.arange(lo, lo + counts[rank], dtype=torch.float64)
+        c = a.to(torch.complex128) * (1 - 2j)
+        got = gather_to_root(TorchComm(), [a, c], counts, root=1)
+        np.savez(os.path.join(out_dir, f"g{rank}.npz"), none=np.array(got is None),
+                 **({"a": got[0].numpy(), "c": got[1].numpy()} if got is not None else {}))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_to_root_in_rank_order(tmp_path):
+    """dist.gather_to_root (the faithful pupil's N > 1 route): uneven pieces, float and complex,
+    concatenated in rank order on the root only."""
+    world = 3
+    mp.start_processes(_gather_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    for r in range(world):
+        d = np.load(os.path.join(tmp_path, f"g{r}.npz"))
+        if r == 1:
+            assert np.array_equal(d["a"], np.arange(12.0)) and np.array_equal(d["c"], np.arange(12.0) * (1 - 2j))
+        else:
+            assert bool(d["none"])

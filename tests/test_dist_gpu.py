@@ -198,3 +198,39 @@ def test_huygens_multi_gpu_threads_equal_one_device(gpu):
     two = W.forward_propagation_cupy_batch_multi_gpu(*T, *S, u, k, ds, devices=[0, 0])
     three = W.forward_propagation_cupy_batch_multi_gpu(*T, *S, u, k, ds, devices=[0, 0, 0])
     assert np.array_equal(two, one) and np.array_equal(three, one)
+
+
+def _pupil_rank(rank, world, port, n, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), AKB_DIST_BACKEND="gloo")
+    import torch.distributed as dist
+    from akbraytracing_amd import dist as AD
+    from akbraytracing_amd.wavefront import RayWave, Shard
+    AD.init_from_env()
+    try:
+        dev = torch.device("cuda", torch.cuda.current_device())
+        rw = RayWave(_geom(), n, shard=Shard.split(n, world, rank), comm=AD.TorchComm(dev))
+        out = rw.run()
+        got = AD.wave_pupil_sharded(rw, out, 64, AD.TorchComm(dev))
+        if rank == 0:
+            np.save(os.path.join(out_dir, "pupil.npy"), got[0].cpu().numpy())
+        else:
+            assert got is None
+    finally:
+        dist.destroy_process_group()
+
+
+def test_faithful_pupil_gathered_from_eight_ranks(gpu, tmp_path):
+    """SURVEY.md §8(e)'s route for the global griddata step: eight ranks (gloo, all on cuda:0) trace
+    their shards of a 301 x 301 grid and hand their (y, z, Wave2) rows to rank 0, which grids the
+    whole lattice - the one-process faithful pupil bit for bit (the sharded trace is bit-exact per
+    ray, and the gather restores ray order)."""
+    from akbraytracing_amd.pupilmap import wave_pupil
+    from akbraytracing_amd.wavefront import RayWave
+    n = 301
+    out = RayWave(_geom(), n).run()
+    want = wave_pupil(out["detcenter2"], out["wave2"], n, n, grid_num_H=64, grid_num_V=64)[0].cpu().numpy()
+    torch.cuda.synchronize()
+    mp.start_processes(_pupil_rank, args=(8, _free_port(), n, str(tmp_path)), nprocs=8, join=True,
+                       start_method="spawn")
+    assert np.array_equal(np.load(os.path.join(tmp_path, "pupil.npy")), want, equal_nan=True)
