@@ -44,16 +44,18 @@ def needs_build():
     return _newest(deps) > os.path.getmtime(SO)
 
 
-def build(force=False, verbose=True):
-    """Compile each source to an object in parallel (hipcc -c), then link the shared library."""
-    if not force and not needs_build():
+def build(force=False, verbose=True, out=None, defines=()):
+    """Compile each source to an object in parallel (hipcc -c), then link the shared library.
+    out / defines: an A/B variant (another path, extra -D flags; loaded through AKB_LIB)."""
+    if out is None and not force and not needs_build():
         return SO
     os.makedirs(LIBDIR, exist_ok=True)
-    objdir = os.path.join(LIBDIR, "obj")
+    tag = "" if out is None else "_" + os.path.splitext(os.path.basename(out))[0]
+    objdir = os.path.join(LIBDIR, "obj" + tag)
     os.makedirs(objdir, exist_ok=True)
     hipcc = os.path.join(ROCM, "bin", "hipcc")
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-Wall",
-             "-Wno-unused-function", f'-DAKB_SOURCES_HASH="{sources_hash()}"']
+             "-Wno-unused-function", f'-DAKB_SOURCES_HASH="{sources_hash()}"'] + [f"-D{d}" for d in defines]
     jobs, objs = [], []
     for src in SOURCES:
         obj = os.path.join(objdir, os.path.splitext(src)[0] + ".o")
@@ -65,13 +67,14 @@ def build(force=False, verbose=True):
     failed = [src for src, p in jobs if p.wait() != 0]
     if failed:
         raise subprocess.CalledProcessError(1, f"hipcc -c {' '.join(failed)}")
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", SO + ".tmp"] + objs
+    target = SO if out is None else out
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", target + ".tmp"] + objs
     cmd += [f"-L{ROCM}/lib", "-lrocfft", f"-Wl,-rpath,{ROCM}/lib"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(SO + ".tmp", SO)
-    return SO
+    os.replace(target + ".tmp", target)
+    return target
 
 
 if __name__ == "__main__":

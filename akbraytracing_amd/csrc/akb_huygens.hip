@@ -53,13 +53,12 @@ __device__ __forceinline__ void dist_half_inv(double x, double& r, double& h) {
 constexpr double kShift = 0x1.8p52;  // t = x 2/pi + 1.5 2^52 holds rint(x 2/pi) in its low mantissa bits
 
 // phases beyond the fast range (|x 2/pi| >= 2^40; never formed by points metres apart at EUV k):
-// the library's sincos, out of line so its Payne-Hanek registers stay out of the loop
-__device__ __attribute__((noinline)) void sincos_slow(double x, double& sn, double& cs) {
-    sincos(x, &sn, &cs);
-}
+// the library's sincos (its Payne-Hanek reduction), used only by the fix-up loop after the main one
+__device__ __forceinline__ void sincos_slow(double x, double& sn, double& cs) { sincos(x, &sn, &cs); }
 
-// sin and cos of x for |x| < 2^40 pi/2 (the library call beyond)
-__device__ __forceinline__ void sincos_phase(double x, double& sn, double& cs) {
+// sin and cos of x for |x| < 2^40 pi/2; returns false (values unusable) beyond, where the caller
+// takes the library's sincos instead
+__device__ __forceinline__ bool sincos_phase_fast(double x, double& sn, double& cs) {
     const double t = __builtin_fma(x, 0x1.45f306dc9c883p-1, kShift);  // rint(x * 2/pi) + shift
     const double q = t - kShift;
     double f = __builtin_fma(-q, 0x1.9220000000000p+0, x);
@@ -87,7 +86,30 @@ __device__ __forceinline__ void sincos_phase(double x, double& sn, double& cs) {
     // the quadrant's signs as sign-bit flips of the high words (no compares or selects)
     sn = __hiloint2double(__double2hiint(a) ^ (int)((k << 30) & 0x80000000u), __double2loint(a));
     cs = __hiloint2double(__double2hiint(b) ^ (int)(((k + 1u) << 30) & 0x80000000u), __double2loint(b));
-    if (__builtin_expect(!(fabs(q) < 0x1p40), 0)) sincos_slow(x, sn, cs);
+    return fabs(q) < 0x1p40;
+}
+
+// one pair's contribution: the distance, 1 / (2 r), the phase -k r and its sincos, the complex
+// multiply-accumulate; returns false when the phase left the fast range (the sums then are
+// recomputed by the caller's slow loop)
+template <bool kSlow>
+__device__ __forceinline__ bool pair_add(double px, double py, double pz, double xj, double yj, double zj,
+                                         double ur, double ui, double negk, double& ar, double& ai) {
+    const double dx = px - xj;
+    const double dy = py - yj;
+    const double dz = pz - zj;
+    double r, amp;  // amp = 1 / (2 r)
+    dist_half_inv(dx * dx + dy * dy + dz * dz, r, amp);
+    const double ph = negk * r;
+    double sn, cs;
+    bool ok = true;
+    if (kSlow) sincos_slow(ph, sn, cs);
+    else ok = sincos_phase_fast(ph, sn, cs);
+    const double fr = amp * cs;
+    const double fi = amp * sn;
+    ar = __builtin_fma(fr, ur, __builtin_fma(-fi, ui, ar));
+    ai = __builtin_fma(fr, ui, __builtin_fma(fi, ur, ai));
+    return ok;
 }
 
 __global__ void __launch_bounds__(kHuyBlock) k_huygens(const double* __restrict__ tx,
@@ -106,9 +128,10 @@ __global__ void __launch_bounds__(kHuyBlock) k_huygens(const double* __restrict_
     for (int t = 0; t < kTPL; ++t) {
         const int64_t i = base + threadIdx.x + t * kHuyBlock;
         const bool ok = i < n;
+        // a lane's slots past the last target sit at the origin: finite pairs, sums never written
         px[t] = ok ? tx[i] : 0.0;
         py[t] = ok ? ty[i] : 0.0;
-        pz[t] = ok ? tz[i] : 1.0e30;
+        pz[t] = ok ? tz[i] : 0.0;
         ar[t] = 0.0;
         ai[t] = 0.0;
     }
@@ -117,6 +140,9 @@ __global__ void __launch_bounds__(kHuyBlock) k_huygens(const double* __restrict_
     const int64_t jb = (int64_t)blockIdx.y * per_split;
     const int64_t je = (jb + per_split) < m ? (jb + per_split) : m;
     out += (int64_t)blockIdx.y * 2 * n;
+    bool fast[kTPL];  // every pair of target t stayed in the fast phase range
+#pragma unroll
+    for (int t = 0; t < kTPL; ++t) fast[t] = true;
     for (int64_t j0 = jb; j0 < je; j0 += kHuyTile) {
         const int cnt = (je - j0) < kHuyTile ? (int)(je - j0) : kHuyTile;
         __syncthreads();
@@ -132,20 +158,19 @@ __global__ void __launch_bounds__(kHuyBlock) k_huygens(const double* __restrict_
         for (int s = 0; s < cnt; ++s) {
             const double xj = s_x[s], yj = s_y[s], zj = s_z[s], ur = s_ur[s], ui = s_ui[s];
 #pragma unroll
-            for (int t = 0; t < kTPL; ++t) {
-                const double dx = px[t] - xj;
-                const double dy = py[t] - yj;
-                const double dz = pz[t] - zj;
-                double r, amp;  // amp = 1 / (2 r)
-                dist_half_inv(dx * dx + dy * dy + dz * dz, r, amp);
-                const double ph = negk * r;
-                double sn, cs;
-                sincos_phase(ph, sn, cs);
-                const double fr = amp * cs;
-                const double fi = amp * sn;
-                ar[t] = __builtin_fma(fr, ur, __builtin_fma(-fi, ui, ar[t]));
-                ai[t] = __builtin_fma(fr, ui, __builtin_fma(fi, ur, ai[t]));
-            }
+            for (int t = 0; t < kTPL; ++t)
+                fast[t] &= pair_add<false>(px[t], py[t], pz[t], xj, yj, zj, ur, ui, negk, ar[t], ai[t]);
+        }
+    }
+    // a phase beyond the fast reduction's range (|k r| >= 2^40 pi/2: points ~4 km apart at EUV k,
+    // never in the reference's geometries): that target's sum again with the library's sincos. Kept
+    // out of the loop above so its pair arithmetic carries no branch and no call.
+#pragma unroll
+    for (int t = 0; t < kTPL; ++t) {
+        if (__builtin_expect(!fast[t], 0)) {
+            ar[t] = ai[t] = 0.0;
+            for (int64_t j = jb; j < je; ++j)
+                pair_add<true>(px[t], py[t], pz[t], sx[j], sy[j], sz[j], u[2 * j], u[2 * j + 1], negk, ar[t], ai[t]);
         }
     }
 #pragma unroll
