@@ -243,9 +243,29 @@ def huygens_rate(out):
     e1.record()
     e1.synchronize()
     ms = e0.elapsed_time(e1) / 3
-    return {"value": T[0].shape[0] * sx.shape[0] / (ms * 1e-3), "unit": "pairs/s", "ms": ms,
-            "sources": int(sx.shape[0]), "targets": int(T[0].shape[0]),
-            "stage": "M2 -> 65x65 image grid (configs[1]'s stage shape, sources from this trace)"}
+    rate = T[0].shape[0] * sx.shape[0] / (ms * 1e-3)
+    res = {"value": rate, "unit": "pairs/s", "ms": ms, "sources": int(sx.shape[0]), "targets": int(T[0].shape[0]),
+           "stage": "M2 -> 65x65 image grid (configs[1]'s stage shape, sources from this trace)"}
+    # its roofline: VALU issue (FP64 sqrt / reciprocal / sincos per pair, sources from LDS) with the
+    # instruction mix of the committed PMC summary (scripts/summarize_huygens.py) while it describes
+    # this kernel source
+    import hashlib
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_huygens.json")))
+    src = os.path.join(ROOT, "akbraytracing_amd", "csrc", "akb_huygens.hip")
+    prof = json.load(open(files[-1])) if files else {}
+    ok = prof.get("sources_sha256") == hashlib.sha256(open(src, "rb").read()).hexdigest()
+    if ok:
+        lane_ops = prof["valu_lane_ops_per_pair"]
+        peak = SIMDS / 4 * prof["effective_clock_ghz"] * 1e9 * 64 / lane_ops
+        res["roofline"] = {"bound": "valu-issue", "achieved": rate, "peak": peak, "unit": "pairs/s",
+                           "frac": rate / peak, "valu_lane_ops_per_pair": lane_ops,
+                           "fp64_lane_ops_per_pair": prof["fp64_lane_ops_per_pair"],
+                           "non_fp64_share": prof["non_fp64_share"],
+                           "fp64_frac_of_peak_profiled": prof["fp64_frac_of_peak"],
+                           "issue_frac_profiled": prof["issue_frac"],
+                           "effective_clock_ghz": prof["effective_clock_ghz"]}
+    res["profile"] = {"file": os.path.relpath(files[-1], ROOT) if files else None, "matches_sources": ok}
+    return res
 
 
 def _lib_hash():

@@ -31,8 +31,10 @@ def main(tag, sources=10004569, targets=4225):
     tr = [r for r in csv.DictReader(open(os.path.join(SRC, "hprof", "run_kernel_trace.csv")))
           if r["Kernel_Name"].startswith("akb::k_huygens(")]
     gsz = lambda r: int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])  # noqa: E731
-    small = min(gsz(r) for r in tr)
-    td = sorted(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in tr if gsz(r) == small)
+    dur = lambda r: int(r["End_Timestamp"]) - int(r["Start_Timestamp"])  # noqa: E731
+    # the M2 -> image launches: the longest ones (split over sources; the source -> M1 stage is short)
+    shape = gsz(max(tr, key=dur))
+    td = sorted(dur(r) for r in tr if gsz(r) == shape)
     trace_ns = float(td[len(td) // 2])
     # per counter: values of the big launches (grid of the M2 -> image shape: the largest VALU count)
     vals = collections.defaultdict(list)
@@ -42,8 +44,8 @@ def main(tag, sources=10004569, targets=4225):
         if not os.path.exists(f):
             continue
         rows = [r for r in csv.DictReader(open(f)) if r["Kernel_Name"].startswith("akb::k_huygens(")]
-        grids = collections.Counter(r["Grid_Size"] for r in rows)
-        big = min(grids, key=int)  # the few-target stage: fewest work-items (split over sources)
+        # the M2 -> image launch: the longest dispatch of the pass
+        big = max(rows, key=lambda r: int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))["Grid_Size"]
         for r in rows:
             if r["Grid_Size"] == big:
                 vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
@@ -57,8 +59,11 @@ def main(tag, sources=10004569, targets=4225):
     flops = 64 * (f64["add"] + f64["mul"] + f64["trans"] + 2 * f64["fma"])
     cycles = med["GRBM_GUI_ACTIVE"] / XCDS
     pmc_ns = sorted(durs)[len(durs) // 2]
+    import hashlib
+    src = os.path.join(ROOT, "akbraytracing_amd", "csrc", "akb_huygens.hip")
     out = {
         "tag": tag,
+        "sources_sha256": hashlib.sha256(open(src, "rb").read()).hexdigest(),
         "command": "python3 scripts/bench_huygens.py --reps 2 (kernel trace); --reps 1 per PMC pass",
         "kernel": "akb::k_huygens (M2 -> 65x65 image grid: 1e7 sources, 4225 targets, split over sources)",
         "sources": sources, "targets": targets, "pairs_per_launch": pairs,
