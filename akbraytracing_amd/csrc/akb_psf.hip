@@ -8,6 +8,7 @@
 // The transform is HBM-bound (a 2048^2 complex128 plane is 64 MiB); the pre/post kernels are
 // single streaming passes.
 #include <math.h>
+#include <string.h>
 #include <rocfft/rocfft.h>
 
 #include <map>
@@ -221,7 +222,12 @@ constexpr int bitrev_c(int i, int bits) {
 // in-register DFT of size M (power of two <= 32): v holds x[bitrev(i)] at i on entry (the caller
 // loads in that order) and X[k] at k on exit; radix-2 DIT, every index and twiddle resolved at
 // compile time, in place
-template <int M>
+// a * b with fused multiply-adds (the line transforms: their bar is 1e-10 of the peak, not bits)
+__device__ __forceinline__ double2 cmulf(double2 a, double2 b) {
+    return make_double2(fma(a.x, b.x, -(a.y * b.y)), fma(a.x, b.y, a.y * b.x));
+}
+
+template <int M, bool kFma = false>
 __device__ __forceinline__ void dft_reg_br(double2 (&t)[M]) {
 #pragma unroll
     for (int h = 1; h < M; h <<= 1) {  // half-length of the current butterflies
@@ -236,7 +242,8 @@ __device__ __forceinline__ void dft_reg_br(double2 (&t)[M]) {
                         y = make_double2(y.y, -y.x);  // * W^(len/4) = -i
                     } else {
                         const int wi = k * (16 / h);
-                        y = cmul(y, make_double2(kW32re[wi], kW32im[wi]));
+                        const double2 w = make_double2(kW32re[wi], kW32im[wi]);
+                        y = kFma ? cmulf(y, w) : cmul(y, w);
                     }
                 }
                 t[i + k] = make_double2(x.x + y.x, x.y + y.y);
@@ -528,6 +535,360 @@ static int launch_psf_cols(const PsfFastArgs& fa, int batch, hipStream_t s) {
     return launch_status("k_psf_cols");
 }
 
+// ---- line transforms (pad 8 / 16): whole output rows per store ----
+//
+// The same F[ko][lo] (up to its unit-modulus phases) in two passes of one kernel family:
+//   pass 1, pupil columns: G[b][ko] = sum_a (-1)^a U0[a][b] W_py^(ko a)   (b < ex; G is ex x py,
+//                          contiguous in ko)
+//   pass 2, plane rows:    X[ko][lo] = sum_b (-1)^b G[b][ko] W_px^(lo b),   psf = |X dA|^2 / Imax
+// Each line is a P = N PAD-point transform of N inputs, decimated in time so that every thread
+// ends with whole output columns j (lanes consecutive in j, so each store instruction of pass 2
+// writes 64 consecutive doubles of one psf row):
+//   X[j + N r] = sum_{s<PAD} W_PAD^(s r) (W_P^(s j) Y_s[j])                       stage 2
+//   Y_s[t + PAD u] = sum_{q<Q} (g[PAD q + s] W_N^(q t)) W_Q^(q u),  Q = N / PAD     stage 1
+// Stage 1 runs SIG values of s at a time through LDS: Q <= SIG, whole Q-point DFTs per thread;
+// Q = SIG Q2 (N >= 256 at pad 16), a SIG x Q2 four-step with one more exchange. Thread j gathers
+// its Y_s[j], applies W_P^(s j) (powers of one table entry) and runs the PAD-point DFT in
+// registers. Pass 2 runs twice: the peak, then the normalised write (its only HBM traffic is the
+// output and one read of G). Workgroups are persistent over lines, prefetching the next line's
+// inputs, and walk an XCD's share of the lines contiguously (pass 2's reads of G are 16-byte
+// pieces of 128-byte lines shared by 8 neighbouring rows).
+enum { kLinePupil = 0, kLinePeak = 1, kLineWrite = 2, kLineWriteE = 3 };
+
+template <int N, int PAD>
+struct LineShape {
+    static constexpr int SIG = 8;
+    static constexpr int CH = PAD / SIG;
+    static constexpr int Q = N / PAD;
+    static constexpr bool kFour = Q > SIG;
+    static constexpr int Q2 = kFour ? Q / SIG : 1;
+    static constexpr int LINES = N >= 256 ? 1 : 256 / N;
+    static constexpr int kThreads = N * LINES;
+    static constexpr int TS = SIG * PAD;  // stage-1 tasks (s, t) per chunk and line
+    static constexpr int kTab = kFour ? Q2 * PAD + SIG * PAD + Q2 * SIG : Q * PAD;
+    static_assert(Q >= 1 && Q2 <= SIG && PAD % SIG == 0, "line transform shape");
+};
+
+struct PsfLineArgs {
+    const double* opd;
+    const double* amp;
+    const double* wy;
+    const double* wx;
+    double wmax;
+    double kphase[8];
+    PsfGeom g;
+    const double2* Wx;  // W_px table
+    const double2* Wy;  // W_py table
+    double2* G;         // (batch, ex, py)
+    double dA;
+    const double* pitch;
+    double* psf;
+    double2* efield;
+    double* imax;
+    int ngroups;  // line groups (LINES lines each) per batch entry
+};
+
+template <int N, int PAD, int MODE>
+__global__ void __launch_bounds__((LineShape<N, PAD>::kThreads)) k_psf_line(PsfLineArgs A) {
+    using S = LineShape<N, PAD>;
+    constexpr int SIG = S::SIG, Q = S::Q, Q2 = S::Q2, LINES = S::LINES, TS = S::TS;
+    constexpr int LQ = ilog2_c(Q), LS = ilog2_c(SIG), LQ2 = ilog2_c(Q2);
+    __shared__ double2 Yc[LINES * SIG * N];
+    __shared__ double2 gl[LINES * N];
+    __shared__ double2 tab[S::kTab];
+    __shared__ double wm[S::kThreads / 64];
+    const PsfGeom g = A.g;
+    const int b = blockIdx.y;
+    const double2* WP = MODE == kLinePupil ? A.Wy : A.Wx;
+    const int nl = MODE == kLinePupil ? g.nx2 : g.py;
+    const int line = threadIdx.x / N, i = threadIdx.x % N;
+    // twiddle tables, W_N^m = W_P^(PAD m): kFour: TA[q2][t] = W_N^(q2 t), TB[q1][t] = W_N^(q1 Q2 t),
+    // TQ[q2][k1] = W_Q^(q2 k1); else T2[q][t] = W_N^(q t)
+    double2* TA = tab;
+    double2* TB = tab + Q2 * PAD;
+    double2* TQ = tab + Q2 * PAD + SIG * PAD;
+    for (int e = threadIdx.x; e < S::kTab; e += S::kThreads) {
+        int m;
+        if (S::kFour) {
+            if (e < Q2 * PAD)
+                m = (e / PAD) * (e % PAD);
+            else if (e < Q2 * PAD + SIG * PAD)
+                m = ((e - Q2 * PAD) / PAD) * Q2 * ((e - Q2 * PAD) % PAD);
+            else
+                m = PAD * ((e - Q2 * PAD - SIG * PAD) / SIG) * ((e - Q2 * PAD - SIG * PAD) % SIG);
+        } else {
+            m = (e / PAD) * (e % PAD);
+        }
+        tab[e] = WP[(int64_t)PAD * m];
+    }
+    if (MODE == kLinePupil && blockIdx.x == 0 && threadIdx.x == 0) A.imax[b] = 0.0;  // pass 2 follows
+    const double dA = A.pitch ? A.pitch[0] * A.pitch[1] : A.dA;
+    double scale = 1.0, sq = 1.0;
+    if (MODE >= kLineWrite) {
+        const double imx = A.imax[b];
+        scale = imx > 0.0 ? 1.0 / imx : 1.0;
+        sq = sqrt(imx > 0.0 ? imx : 1.0);
+    }
+    const double sgn = ((g.ny2 / 2 + g.nx2 / 2) & 1) ? -1.0 : 1.0;
+
+    // this workgroup's line groups: an XCD's contiguous share, slot-strided within it
+    const int ngr = A.ngroups, nwg = gridDim.x;
+    int base = 0, slot = blockIdx.x, nslot = nwg, R = ngr;
+    if ((nwg & 7) == 0) {
+        R = (ngr + 7) / 8;
+        base = (blockIdx.x & 7) * R;
+        slot = blockIdx.x >> 3;
+        nslot = nwg >> 3;
+    }
+    auto group_at = [&](int k) {
+        const int o = slot + k * nslot;
+        const int gi = base + o;
+        return (o < R && gi < ngr) ? gi : -1;
+    };
+    // inputs: pass 1, (opd, amp) of pupil element (a = i, column = line); pass 2, G[x = i][ko = line]
+    auto fetch = [&](int grp) {
+        double2 r = make_double2(0.0, 0.0);
+        const int L = grp * LINES + line;
+        if (grp < 0 || L >= nl) return r;
+        if (MODE == kLinePupil) {
+            if (i < g.ny && L < g.nx) {
+                const int64_t pi = (int64_t)i * g.nx + L;
+                r.x = A.opd[pi];
+                r.y = A.amp ? A.amp[pi] : (isfinite(r.x) ? 1.0 : 0.0);
+            }
+        } else {
+            r = A.G[((int64_t)b * g.nx2 + i) * g.py + L];
+        }
+        return r;
+    };
+    auto input = [&](double2 r, int L) {
+        double re = r.x, im = r.y;
+        if (MODE == kLinePupil) {
+            re = 0.0;
+            im = 0.0;
+            if (i < g.ny && L < g.nx) {
+                double o = r.x, amp = r.y;
+                if (!isfinite(amp)) amp = 0.0;
+                if (!isfinite(o)) o = 0.0;
+                double sn, cs;
+                sincos(A.kphase[b] * o, &sn, &cs);
+                re = amp * cs - 0.0 * sn;
+                im = amp * sn + 0.0 * cs;
+                if (A.wy) {
+                    const double w = (A.wy[i] * A.wx[L]) / A.wmax;
+                    const double x0 = re, y0 = im;
+                    re = x0 * w - y0 * 0.0;
+                    im = x0 * 0.0 + y0 * w;
+                }
+            }
+        }
+        if (i & 1) {
+            re = -re;
+            im = -im;
+        }
+        return make_double2(re, im);
+    };
+
+    double m = 0.0;
+    int grp = group_at(0);
+    double2 pre = fetch(grp);
+    for (int k = 0; grp >= 0; ++k) {
+        const int L = grp * LINES + line;
+        const int next = group_at(k + 1);
+        __syncthreads();  // the previous group is done with gl / Yc (and the tables are in)
+        gl[line * N + i] = input(pre, L);
+        pre = fetch(next);
+        __syncthreads();
+        double2 v[PAD];
+        const double2 w1 = WP[i];  // W_P^j
+        const double2 wch = S::CH == 1 ? w1 : cmulf(w1, w1);
+        double2* Yl = Yc + line * SIG * N;
+        const double2* gll = gl + line * N;
+#pragma unroll
+        for (int c = 0; c < S::CH; ++c) {
+            if constexpr (!S::kFour) {
+#pragma unroll
+                for (int kk = 0; kk < SIG / Q; ++kk) {
+                    const int T = i + kk * N;
+                    const int s_l = T / PAD, t = T % PAD, s = S::CH * s_l + c;
+                    double2 w[Q];
+#pragma unroll
+                    for (int ii = 0; ii < Q; ++ii) {
+                        const int q = bitrev_c(ii, LQ);
+                        const double2 x = gll[PAD * q + s];
+                        w[ii] = q ? cmulf(x, tab[q * PAD + t]) : x;
+                    }
+                    dft_reg_br<Q, true>(w);
+#pragma unroll
+                    for (int u = 0; u < Q; ++u) Yl[s_l * N + t + PAD * u] = w[u];
+                }
+            } else {
+                {
+                    const int task = i % TS, q2 = i / TS;
+                    const int s_l = task / PAD, t = task % PAD, s = S::CH * s_l + c;
+                    double2 w[SIG];
+#pragma unroll
+                    for (int ii = 0; ii < SIG; ++ii) {
+                        const int q1 = bitrev_c(ii, LS);
+                        const double2 x = gll[PAD * (q1 * Q2 + q2) + s];
+                        w[ii] = q1 ? cmulf(x, TB[q1 * PAD + t]) : x;
+                    }
+                    dft_reg_br<SIG, true>(w);
+                    const double2 wa = TA[q2 * PAD + t];
+#pragma unroll
+                    for (int k1 = 0; k1 < SIG; ++k1) {
+                        const double2 tw = k1 ? cmulf(wa, TQ[q2 * SIG + k1]) : wa;
+                        Yl[(k1 * Q2 + q2) * TS + task] = cmulf(w[k1], tw);
+                    }
+                }
+                __syncthreads();
+                {
+                    const int task = i % TS, kg = i / TS;
+                    const int s_l = task / PAD, t = task % PAD;
+                    double2 w[SIG / Q2][Q2];
+#pragma unroll
+                    for (int e = 0; e < SIG / Q2; ++e) {
+                        const int k1 = kg + Q2 * e;
+#pragma unroll
+                        for (int ii = 0; ii < Q2; ++ii) w[e][ii] = Yl[(k1 * Q2 + bitrev_c(ii, LQ2)) * TS + task];
+                    }
+                    __syncthreads();
+#pragma unroll
+                    for (int e = 0; e < SIG / Q2; ++e) {
+                        dft_reg_br<Q2, true>(w[e]);
+                        const int k1 = kg + Q2 * e;
+#pragma unroll
+                        for (int k2 = 0; k2 < Q2; ++k2) Yl[s_l * N + t + PAD * (k1 + SIG * k2)] = w[e][k2];
+                    }
+                }
+            }
+            __syncthreads();
+            // stage 2 of this chunk's s = CH s' + c: W_P^(s j) as powers of W_P^(CH j) (at most
+            // SIG - 1 roundings), the SIG-point DFT over s'
+            double2 a[SIG];
+            {
+                double2 p = c ? w1 : make_double2(1.0, 0.0);
+#pragma unroll
+                for (int s_l = 0; s_l < SIG; ++s_l) {
+                    const double2 y = Yl[s_l * N + i];
+                    a[bitrev_c(s_l, LS)] = (c == 0 && s_l == 0) ? y : cmulf(y, p);
+                    if (s_l + 1 < SIG) p = (c == 0 && s_l == 0) ? wch : cmulf(p, wch);
+                }
+            }
+            dft_reg_br<SIG, true>(a);
+            if (c + 1 < S::CH) __syncthreads();
+            if constexpr (S::CH == 1) {
+#pragma unroll
+                for (int r = 0; r < SIG; ++r) v[r] = a[r];
+            } else {
+                // PAD = 2 SIG: X[r] = A0[r] + W_PAD^r A1[r], X[r + SIG] = A0[r] - W_PAD^r A1[r]
+                if (c == 0) {
+#pragma unroll
+                    for (int r = 0; r < SIG; ++r) v[r] = a[r];
+                } else {
+#pragma unroll
+                    for (int r = 0; r < SIG; ++r) {
+                        const int wi = r * (32 / PAD);
+                        const double2 t = r ? cmulf(a[r], make_double2(kW32re[wi], kW32im[wi])) : a[r];
+                        const double2 x0 = v[r];
+                        v[r] = make_double2(x0.x + t.x, x0.y + t.y);
+                        v[r + SIG] = make_double2(x0.x - t.x, x0.y - t.y);
+                    }
+                }
+            }
+        }
+        if (L < nl) {
+            if (MODE == kLinePupil) {
+                double2* Gl = A.G + ((int64_t)b * g.nx2 + L) * g.py + i;
+#pragma unroll
+                for (int r = 0; r < PAD; ++r) Gl[(int64_t)N * r] = v[r];
+            } else {
+                double* Pr = A.psf + ((int64_t)b * g.py + L) * g.px + i;
+                double2* Er = A.efield + ((int64_t)b * g.py + L) * g.px + i;
+#pragma unroll
+                for (int r = 0; r < PAD; ++r) {
+                    const double re = v[r].x * dA, im = v[r].y * dA;
+                    const double I = fma(re, re, im * im);
+                    if (MODE == kLinePeak) {
+                        m = dmax_nan(m, I);
+                    } else {
+                        Pr[N * r] = I * scale;
+                        if (MODE == kLineWriteE) {
+                            const int lo = i + N * r;
+                            const double2 py_ph = A.Wy[((int64_t)L * (g.ny2 / 2)) % g.py];
+                            const double2 px_ph = A.Wx[((int64_t)lo * (g.nx2 / 2)) % g.px];
+                            double2 e = cmul(make_double2(re, im), make_double2(py_ph.x, -py_ph.y));
+                            e = cmul(e, make_double2(px_ph.x, -px_ph.y));
+                            Er[N * r] = make_double2(sgn * e.x / sq, sgn * e.y / sq);
+                        }
+                    }
+                }
+            }
+        }
+        grp = next;
+    }
+    if (MODE == kLinePeak) {
+        for (int off = 32; off > 0; off >>= 1) m = dmax_nan(m, __shfl_down(m, off));
+        if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int w = 1; w < S::kThreads / 64; ++w) m = dmax_nan(m, wm[w]);
+            atomic_max_nonneg(A.imax + b, m);
+        }
+    }
+}
+
+// persistent workgroups per pass: the resident count (LDS / threads) x 256 CUs, a multiple of 8
+template <int N, int PAD>
+static int line_wgs(int ngroups) {
+    using S = LineShape<N, PAD>;
+    const int lds = (int)sizeof(double2) * (S::LINES * S::SIG * N + S::LINES * N + S::kTab);
+    int per_cu = (160 * 1024) / lds;
+    const int by_threads = 2048 / S::kThreads;
+    if (per_cu > by_threads) per_cu = by_threads;
+    if (per_cu < 1) per_cu = 1;
+    int w = 256 * per_cu;
+    if (const char* e = getenv("AKB_PSF_LINE_WGS")) w = atoi(e) > 0 ? atoi(e) : w;
+    if (ngroups < w) w = ngroups >= 8 ? ngroups / 8 * 8 : ngroups;
+    return w;
+}
+
+template <int N, int PAD, int MODE>
+static int launch_psf_line(PsfLineArgs fa, int nlines, int batch, hipStream_t s) {
+    using S = LineShape<N, PAD>;
+    fa.ngroups = (nlines + S::LINES - 1) / S::LINES;
+    k_psf_line<N, PAD, MODE><<<dim3(line_wgs<N, PAD>(fa.ngroups), batch), S::kThreads, 0, s>>>(fa);
+    return launch_status(MODE == kLinePupil ? "k_psf_line(pupil)" : MODE == kLinePeak ? "k_psf_line(peak)" : "k_psf_line(write)");
+}
+
+// pad 16: lines of 16..1024; pad 8: 8..512 (Q = N / PAD <= 64)
+#define AKB_LINE_SHAPES(X) \
+    X(16, 16) X(32, 16) X(64, 16) X(128, 16) X(256, 16) X(512, 16) X(1024, 16) \
+    X(8, 8) X(16, 8) X(32, 8) X(64, 8) X(128, 8) X(256, 8) X(512, 8)
+
+static bool psf_line_ok(const PsfGeom& g, int pad) {
+    if (getenv("AKB_PSF_ROCFFT")) return false;
+    if (const char* e = getenv("AKB_PSF_PATH"))
+        if (strcmp(e, "cols") == 0) return false;
+    auto ok = [&](int n) {
+#define AKB_CASE(NN, PP) if (n == NN && pad == PP) return true;
+        AKB_LINE_SHAPES(AKB_CASE)
+#undef AKB_CASE
+        return false;
+    };
+    return ok(g.ny2) && ok(g.nx2) && (int64_t)g.py * g.px < (1LL << 31);
+}
+
+template <int MODE>
+static int psf_line_dispatch(int n, int pad, const PsfLineArgs& fa, int nlines, int batch, hipStream_t s) {
+#define AKB_CASE(NN, PP) \
+    if (n == NN && pad == PP) return launch_psf_line<NN, PP, MODE>(fa, nlines, batch, s);
+    AKB_LINE_SHAPES(AKB_CASE)
+#undef AKB_CASE
+    set_error("line PSF: unsupported line %d at pad %d", n, pad);
+    return AKB_E_INVALID;
+}
+
 #define AKB_PSF_SIZES(X) X(8) X(16) X(32) X(64) X(128) X(256) X(512) X(1024)
 
 static int psf_rows_dispatch(int n, const PsfFastArgs& fa, int batch, hipStream_t s) {
@@ -657,7 +1018,7 @@ extern "C" {
 int64_t akb_psf_work_bytes(int ny, int nx, int pad, int batch) {
     if (ny <= 0 || nx <= 0 || pad < 1 || batch < 1) return -1;
     const PsfGeom g = psf_geom(ny, nx, pad);
-    if (psf_fast_ok(g)) return psf_fast_bytes(g, batch);
+    if (psf_line_ok(g, pad) || psf_fast_ok(g)) return psf_fast_bytes(g, batch);  // G: ex x py, H: ey x px
     PlanEntry e;
     if (get_plan(g.py, g.px, batch, &e) != AKB_OK) return -1;
     const int64_t field = (int64_t)batch * g.py * g.px * 16;
@@ -677,6 +1038,28 @@ int akb_psf_f64(const double* opd, const double* amp, int ny, int nx, int pad, i
     const PsfGeom g = psf_geom(ny, nx, pad);
     hipStream_t s = (hipStream_t)stream;
     int st;
+    if (psf_line_ok(g, pad)) {
+        PsfLineArgs la{};
+        la.opd = opd;
+        la.amp = amp;
+        la.wy = hann_wy;
+        la.wx = hann_wx;
+        la.wmax = hann_max;
+        la.g = g;
+        for (int b = 0; b < batch; ++b) la.kphase[b] = (2.0 * M_PI / lambdas[b]);
+        la.G = (double2*)work;
+        if ((st = get_twiddles(g.px, s, &la.Wx))) return st;
+        if ((st = get_twiddles(g.py, s, &la.Wy))) return st;
+        la.dA = dx * dy;
+        la.pitch = d_pitch;
+        la.psf = psf;
+        la.efield = (double2*)efield_re_im;
+        la.imax = d_imax;
+        if ((st = psf_line_dispatch<kLinePupil>(g.ny2, pad, la, g.nx2, batch, s))) return st;
+        if ((st = psf_line_dispatch<kLinePeak>(g.nx2, pad, la, g.py, batch, s))) return st;
+        if (la.efield) return psf_line_dispatch<kLineWriteE>(g.nx2, pad, la, g.py, batch, s);
+        return psf_line_dispatch<kLineWrite>(g.nx2, pad, la, g.py, batch, s);
+    }
     if (psf_fast_ok(g)) {
         PsfFastArgs fa{};
         fa.opd = opd;

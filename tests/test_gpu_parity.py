@@ -697,10 +697,14 @@ def test_psf_stack_equals_single(gpu):
 @pytest.mark.parametrize("ny,nx,pad,win,eff", [(128, 128, 16, False, False), (64, 32, 4, True, True),
                                                (15, 16, 3, False, True), (8, 8, 1, False, False),
                                                (256, 8, 2, True, False), (32, 256, 5, False, True),
-                                               (512, 512, 8, False, True), (1024, 32, 8, True, False)])
+                                               (512, 512, 8, False, True), (1024, 32, 8, True, False),
+                                               (15, 16, 16, False, True), (16, 8, 8, True, True),
+                                               (256, 64, 16, True, True), (64, 512, 16, False, False),
+                                               (1024, 16, 16, False, True), (127, 1024, 16, True, False)])
 def test_psf_pruned_transform(gpu, ny, nx, pad, win, eff, monkeypatch):
     """Power-of-two pupils take the pruned transform (the padded plane is never built): against
-    the oracle (numpy fft2 on the padded plane) and against the rocFFT path on the same input."""
+    the oracle (numpy fft2 on the padded plane), the rocFFT path on the same input and, at pad 8
+    / 16 (the line transforms), the column-pass transform."""
     from akbraytracing_amd import psf as G
     import oracle.psf as OP
     rng = np.random.default_rng(ny * 7 + nx)
@@ -717,6 +721,11 @@ def test_psf_pruned_transform(gpu, ny, nx, pad, win, eff, monkeypatch):
     if eff:
         e = fast[1][0].cpu().numpy()
         assert np.max(np.abs(e - ref[3])) <= 1e-10 * np.max(np.abs(ref[3]))
+    if pad in (8, 16):
+        monkeypatch.setenv("AKB_PSF_PATH", "cols")
+        cols = G.psf_stack(o, None, [lam], dx, dy, pad_factor=pad, window="hann" if win else None,
+                           workspace=G.PsfWorkspace())
+        assert np.max(np.abs(cols[0][0].cpu().numpy() - got)) <= 1e-12
     monkeypatch.setenv("AKB_PSF_ROCFFT", "1")
     slow = G.psf_stack(o, None, [lam], dx, dy, pad_factor=pad, window="hann" if win else None,
                        workspace=G.PsfWorkspace())
