@@ -14,6 +14,7 @@
 #include <map>
 #include <mutex>
 #include <tuple>
+#include <type_traits>
 
 #include "akb_common.h"
 
@@ -553,7 +554,62 @@ static int launch_psf_cols(const PsfFastArgs& fa, int batch, hipStream_t s) {
 // output and one read of G). Workgroups are persistent over lines, prefetching the next line's
 // inputs, and walk an XCD's share of the lines contiguously (pass 2's reads of G are 16-byte
 // pieces of 128-byte lines shared by 8 neighbouring rows).
-enum { kLinePupil = 0, kLinePeak = 1, kLineWrite = 2, kLineWriteE = 3 };
+enum { kLinePupil = 0, kLinePeak = 1, kLineWrite = 2, kLineWriteE = 3, kLinePeak32 = 4 };
+#ifndef AKB_PSF_NT
+#define AKB_PSF_NT 1  // nontemporal psf stores (the stream must not evict G's lines): 0 for A/B
+#endif
+// The peak: kLinePeak32 runs pass 2 in fp32 (half the LDS bytes, twice the VALU rate) for each
+// row's max of |F|^2; the rows within kPeakSlack of the fp32 peak (the fp32 transform's error is
+// ~1e-6 of the peak, its worst-case bound ~1e-3 at 1024-point lines) are re-run in fp64
+// (kLinePeak over that list), which gives the exact max. Non-finite or zero peaks, or more than a
+// quarter of the rows within the slack, take the fp64 pass over every row. Planes of 2^24 points
+// and up (AKB_PSF_PEAK=f32 / f64 forces either way).
+constexpr float kPeakSlack = 0.0625f;
+
+template <typename R>
+struct Cx;
+template <>
+struct Cx<double> {
+    using T = double2;
+    __device__ static double2 mk(double x, double y) { return make_double2(x, y); }
+};
+template <>
+struct Cx<float> {
+    using T = float2;
+    __device__ static float2 mk(float x, float y) { return make_float2(x, y); }
+};
+
+template <typename R>
+__device__ __forceinline__ typename Cx<R>::T cmul_r(typename Cx<R>::T a, typename Cx<R>::T b) {
+    return Cx<R>::mk(fma(a.x, b.x, -(a.y * b.y)), fma(a.x, b.y, a.y * b.x));
+}
+
+// dft_reg_br with fused multiply-adds in precision R
+template <int M, typename R>
+__device__ __forceinline__ void dft_br(typename Cx<R>::T (&t)[M]) {
+    using V = typename Cx<R>::T;
+#pragma unroll
+    for (int h = 1; h < M; h <<= 1) {
+#pragma unroll
+        for (int i = 0; i < M; i += 2 * h) {
+#pragma unroll
+            for (int k = 0; k < h; ++k) {
+                const V x = t[i + k];
+                V y = t[i + k + h];
+                if (k != 0) {
+                    if (2 * k == h) {
+                        y = Cx<R>::mk(y.y, -y.x);
+                    } else {
+                        const int wi = k * (16 / h);
+                        y = cmul_r<R>(y, Cx<R>::mk((R)kW32re[wi], (R)kW32im[wi]));
+                    }
+                }
+                t[i + k] = Cx<R>::mk(x.x + y.x, x.y + y.y);
+                t[i + k + h] = Cx<R>::mk(x.x - y.x, x.y - y.y);
+            }
+        }
+    }
+}
 
 template <int N, int PAD>
 struct LineShape {
@@ -584,29 +640,50 @@ struct PsfLineArgs {
     const double* pitch;
     double* psf;
     double2* efield;
-    double* imax;
-    int ngroups;  // line groups (LINES lines each) per batch entry
+    double* imax;        // Imax = max |F dA|^2 per batch entry (written by the write pass)
+    double* umax;        // max |F|^2 per batch entry (workspace; pass 1 zeroes it)
+    unsigned* umax32;    // fp32 peak pass: max |F|^2 (float bits) per batch entry
+    float* rowmax32;     // fp32 peak pass: (batch, py) row maxima
+    int* cand;           // (batch, py) rows for the fp64 peak pass
+    int* cand_n;         // per batch entry: their count, or -1 for every row
+    int ngroups;         // line groups (LINES lines each) per batch entry
 };
 
 template <int N, int PAD, int MODE>
 __global__ void __launch_bounds__((LineShape<N, PAD>::kThreads)) k_psf_line(PsfLineArgs A) {
     using S = LineShape<N, PAD>;
+    using R = typename std::conditional<MODE == kLinePeak32, float, double>::type;
+    using V = typename Cx<R>::T;
     constexpr int SIG = S::SIG, Q = S::Q, Q2 = S::Q2, LINES = S::LINES, TS = S::TS;
     constexpr int LQ = ilog2_c(Q), LS = ilog2_c(SIG), LQ2 = ilog2_c(Q2);
-    __shared__ double2 Yc[LINES * SIG * N];
-    __shared__ double2 gl[LINES * N];
-    __shared__ double2 tab[S::kTab];
+    __shared__ V Yc[LINES * SIG * N];
+    __shared__ V gl[LINES * N];
+    __shared__ V tab[S::kTab];
     __shared__ double wm[S::kThreads / 64];
     const PsfGeom g = A.g;
     const int b = blockIdx.y;
     const double2* WP = MODE == kLinePupil ? A.Wy : A.Wx;
-    const int nl = MODE == kLinePupil ? g.nx2 : g.py;
     const int line = threadIdx.x / N, i = threadIdx.x % N;
-    // twiddle tables, W_N^m = W_P^(PAD m): kFour: TA[q2][t] = W_N^(q2 t), TB[q1][t] = W_N^(q1 Q2 t),
-    // TQ[q2][k1] = W_Q^(q2 k1); else T2[q][t] = W_N^(q t)
-    double2* TA = tab;
-    double2* TB = tab + Q2 * PAD;
-    double2* TQ = tab + Q2 * PAD + SIG * PAD;
+    const int t = i % PAD, q2 = i / TS;
+    // lines of this pass: pupil columns (pass 1), psf rows, or the fp64 peak pass's row list
+    int nl = MODE == kLinePupil ? g.nx2 : g.py;
+    const int* rows = nullptr;
+    if (MODE == kLinePeak && A.cand) {
+        const int cn = A.cand_n[b];
+        if (cn >= 0) {
+            nl = cn;
+            rows = A.cand + (int64_t)b * g.py;
+        }
+    }
+    if (MODE == kLinePupil && blockIdx.x == 0 && threadIdx.x == 0) {
+        A.umax[b] = 0.0;  // pass 2 follows
+        A.umax32[b] = 0u;
+    }
+    // stage-1 twiddles, W_N^m = W_P^(PAD m): four-step, TA[q2][t] = W_N^(q2 t),
+    // TB[q1][t] = W_N^(q1 Q2 t), TQ[q2][k1] = W_Q^(q2 k1); one-step, T2[q][t] = W_N^(q t)
+    V* TA = tab;
+    V* TB = tab + Q2 * PAD;
+    V* TQ = tab + Q2 * PAD + SIG * PAD;
     for (int e = threadIdx.x; e < S::kTab; e += S::kThreads) {
         int m;
         if (S::kFour) {
@@ -619,37 +696,45 @@ __global__ void __launch_bounds__((LineShape<N, PAD>::kThreads)) k_psf_line(PsfL
         } else {
             m = (e / PAD) * (e % PAD);
         }
-        tab[e] = WP[(int64_t)PAD * m];
+        const double2 w = WP[(int64_t)PAD * m];
+        tab[e] = Cx<R>::mk((R)w.x, (R)w.y);
     }
-    if (MODE == kLinePupil && blockIdx.x == 0 && threadIdx.x == 0) A.imax[b] = 0.0;  // pass 2 follows
     const double dA = A.pitch ? A.pitch[0] * A.pitch[1] : A.dA;
+    // psf = |F dA|^2 / Imax = |F|^2 / max |F|^2 (unnormalised |F dA|^2 when Imax is not > 0, as
+    // psf_fft.py:120-122); Imax itself goes to the caller's imax
     double scale = 1.0, sq = 1.0;
-    if (MODE >= kLineWrite) {
-        const double imx = A.imax[b];
-        scale = imx > 0.0 ? 1.0 / imx : 1.0;
+    if (MODE == kLineWrite || MODE == kLineWriteE) {
+        const double um = A.umax[b];
+        const double imx = um * dA * dA;
+        scale = imx > 0.0 ? 1.0 / um : dA * dA;
         sq = sqrt(imx > 0.0 ? imx : 1.0);
+        if (blockIdx.x == 0 && threadIdx.x == 0) A.imax[b] = imx;
     }
     const double sgn = ((g.ny2 / 2 + g.nx2 / 2) & 1) ? -1.0 : 1.0;
 
     // this workgroup's line groups: an XCD's contiguous share, slot-strided within it
-    const int ngr = A.ngroups, nwg = gridDim.x;
-    int base = 0, slot = blockIdx.x, nslot = nwg, R = ngr;
+    const int ngr = rows ? (nl + LINES - 1) / LINES : A.ngroups, nwg = gridDim.x;
+    int base = 0, slot = blockIdx.x, nslot = nwg, RR = ngr;
     if ((nwg & 7) == 0) {
-        R = (ngr + 7) / 8;
-        base = (blockIdx.x & 7) * R;
+        RR = (ngr + 7) / 8;
+        base = (blockIdx.x & 7) * RR;
         slot = blockIdx.x >> 3;
         nslot = nwg >> 3;
     }
     auto group_at = [&](int k) {
         const int o = slot + k * nslot;
         const int gi = base + o;
-        return (o < R && gi < ngr) ? gi : -1;
+        return (o < RR && gi < ngr) ? gi : -1;
+    };
+    auto line_of = [&](int grp) {  // -1: none
+        const int idx = grp * LINES + line;
+        if (grp < 0 || idx >= nl) return -1;
+        return rows ? rows[idx] : idx;
     };
     // inputs: pass 1, (opd, amp) of pupil element (a = i, column = line); pass 2, G[x = i][ko = line]
-    auto fetch = [&](int grp) {
+    auto fetch = [&](int L) {
         double2 r = make_double2(0.0, 0.0);
-        const int L = grp * LINES + line;
-        if (grp < 0 || L >= nl) return r;
+        if (L < 0) return r;
         if (MODE == kLinePupil) {
             if (i < g.ny && L < g.nx) {
                 const int64_t pi = (int64_t)i * g.nx + L;
@@ -666,7 +751,7 @@ __global__ void __launch_bounds__((LineShape<N, PAD>::kThreads)) k_psf_line(PsfL
         if (MODE == kLinePupil) {
             re = 0.0;
             im = 0.0;
-            if (i < g.ny && L < g.nx) {
+            if (L >= 0 && i < g.ny && L < g.nx) {
                 double o = r.x, amp = r.y;
                 if (!isfinite(amp)) amp = 0.0;
                 if (!isfinite(o)) o = 0.0;
@@ -686,66 +771,65 @@ __global__ void __launch_bounds__((LineShape<N, PAD>::kThreads)) k_psf_line(PsfL
             re = -re;
             im = -im;
         }
-        return make_double2(re, im);
+        return Cx<R>::mk((R)re, (R)im);
     };
 
-    double m = 0.0;
+    double m = 0.0, nan_sum = 0.0;
+    unsigned m32 = 0u;
     int grp = group_at(0);
-    double2 pre = fetch(grp);
+    double2 pre = fetch(line_of(grp));
     for (int k = 0; grp >= 0; ++k) {
-        const int L = grp * LINES + line;
+        const int L = line_of(grp);
         const int next = group_at(k + 1);
-        __syncthreads();  // the previous group is done with gl / Yc (and the tables are in)
+        __syncthreads();  // the previous group is done with gl / Yc / wm (and the tables are in)
         gl[line * N + i] = input(pre, L);
-        pre = fetch(next);
+        pre = fetch(line_of(next));
         __syncthreads();
-        double2 v[PAD];
-        const double2 w1 = WP[i];  // W_P^j
-        const double2 wch = S::CH == 1 ? w1 : cmulf(w1, w1);
-        double2* Yl = Yc + line * SIG * N;
-        const double2* gll = gl + line * N;
+        V v[PAD];
+        const double2 w1d = WP[i];  // W_P^j (reloaded per line: fewer registers held across it)
+        const V w1 = Cx<R>::mk((R)w1d.x, (R)w1d.y);
+        const V wch = S::CH == 1 ? w1 : cmul_r<R>(w1, w1);
+        V* Yl = Yc + line * SIG * N;
+        const V* gll = gl + line * N;
 #pragma unroll
         for (int c = 0; c < S::CH; ++c) {
             if constexpr (!S::kFour) {
 #pragma unroll
                 for (int kk = 0; kk < SIG / Q; ++kk) {
-                    const int T = i + kk * N;
-                    const int s_l = T / PAD, t = T % PAD, s = S::CH * s_l + c;
-                    double2 w[Q];
+                    const int s_l = (i + kk * N) / PAD, s = S::CH * s_l + c;
+                    V w[Q];
 #pragma unroll
-                    for (int ii = 0; ii < Q; ++ii) {
-                        const int q = bitrev_c(ii, LQ);
-                        const double2 x = gll[PAD * q + s];
-                        w[ii] = q ? cmulf(x, tab[q * PAD + t]) : x;
+                    for (int q = 0; q < Q; ++q) {
+                        const V x = gll[PAD * q + s];
+                        w[bitrev_c(q, LQ)] = q ? cmul_r<R>(x, tab[q * PAD + t]) : x;
                     }
-                    dft_reg_br<Q, true>(w);
+                    dft_br<Q, R>(w);
 #pragma unroll
                     for (int u = 0; u < Q; ++u) Yl[s_l * N + t + PAD * u] = w[u];
                 }
             } else {
                 {
-                    const int task = i % TS, q2 = i / TS;
-                    const int s_l = task / PAD, t = task % PAD, s = S::CH * s_l + c;
-                    double2 w[SIG];
+                    const int task = i % TS;
+                    const int s_l = task / PAD, s = S::CH * s_l + c;
+                    V w[SIG];
 #pragma unroll
-                    for (int ii = 0; ii < SIG; ++ii) {
-                        const int q1 = bitrev_c(ii, LS);
-                        const double2 x = gll[PAD * (q1 * Q2 + q2) + s];
-                        w[ii] = q1 ? cmulf(x, TB[q1 * PAD + t]) : x;
+                    for (int q1 = 0; q1 < SIG; ++q1) {
+                        const V x = gll[PAD * (q1 * Q2 + q2) + s];
+                        w[bitrev_c(q1, LS)] = q1 ? cmul_r<R>(x, TB[q1 * PAD + t]) : x;
                     }
-                    dft_reg_br<SIG, true>(w);
-                    const double2 wa = TA[q2 * PAD + t];
+                    dft_br<SIG, R>(w);
+                    const V tw0 = TA[q2 * PAD + t];  // W_N^(q2 t) W_Q^(q2 k1)
 #pragma unroll
                     for (int k1 = 0; k1 < SIG; ++k1) {
-                        const double2 tw = k1 ? cmulf(wa, TQ[q2 * SIG + k1]) : wa;
-                        Yl[(k1 * Q2 + q2) * TS + task] = cmulf(w[k1], tw);
+                        const V tw = k1 ? cmul_r<R>(tw0, TQ[q2 * SIG + k1]) : tw0;
+                        Yl[(k1 * Q2 + q2) * TS + task] = cmul_r<R>(w[k1], tw);
                     }
                 }
                 __syncthreads();
                 {
                     const int task = i % TS, kg = i / TS;
-                    const int s_l = task / PAD, t = task % PAD;
-                    double2 w[SIG / Q2][Q2];
+                    const int s_l = task / PAD;
+                    V w[SIG / Q2][Q2];
 #pragma unroll
                     for (int e = 0; e < SIG / Q2; ++e) {
                         const int k1 = kg + Q2 * e;
@@ -755,7 +839,7 @@ __global__ void __launch_bounds__((LineShape<N, PAD>::kThreads)) k_psf_line(PsfL
                     __syncthreads();
 #pragma unroll
                     for (int e = 0; e < SIG / Q2; ++e) {
-                        dft_reg_br<Q2, true>(w[e]);
+                        dft_br<Q2, R>(w[e]);
                         const int k1 = kg + Q2 * e;
 #pragma unroll
                         for (int k2 = 0; k2 < Q2; ++k2) Yl[s_l * N + t + PAD * (k1 + SIG * k2)] = w[e][k2];
@@ -765,17 +849,17 @@ __global__ void __launch_bounds__((LineShape<N, PAD>::kThreads)) k_psf_line(PsfL
             __syncthreads();
             // stage 2 of this chunk's s = CH s' + c: W_P^(s j) as powers of W_P^(CH j) (at most
             // SIG - 1 roundings), the SIG-point DFT over s'
-            double2 a[SIG];
+            V a[SIG];
             {
-                double2 p = c ? w1 : make_double2(1.0, 0.0);
+                V p = c ? w1 : Cx<R>::mk((R)1, (R)0);
 #pragma unroll
                 for (int s_l = 0; s_l < SIG; ++s_l) {
-                    const double2 y = Yl[s_l * N + i];
-                    a[bitrev_c(s_l, LS)] = (c == 0 && s_l == 0) ? y : cmulf(y, p);
-                    if (s_l + 1 < SIG) p = (c == 0 && s_l == 0) ? wch : cmulf(p, wch);
+                    const V y = Yl[s_l * N + i];
+                    a[bitrev_c(s_l, LS)] = (c == 0 && s_l == 0) ? y : cmul_r<R>(y, p);
+                    if (s_l + 1 < SIG) p = (c == 0 && s_l == 0) ? wch : cmul_r<R>(p, wch);
                 }
             }
-            dft_reg_br<SIG, true>(a);
+            dft_br<SIG, R>(a);
             if (c + 1 < S::CH) __syncthreads();
             if constexpr (S::CH == 1) {
 #pragma unroll
@@ -789,60 +873,116 @@ __global__ void __launch_bounds__((LineShape<N, PAD>::kThreads)) k_psf_line(PsfL
 #pragma unroll
                     for (int r = 0; r < SIG; ++r) {
                         const int wi = r * (32 / PAD);
-                        const double2 t = r ? cmulf(a[r], make_double2(kW32re[wi], kW32im[wi])) : a[r];
-                        const double2 x0 = v[r];
-                        v[r] = make_double2(x0.x + t.x, x0.y + t.y);
-                        v[r + SIG] = make_double2(x0.x - t.x, x0.y - t.y);
+                        const V tt = r ? cmul_r<R>(a[r], Cx<R>::mk((R)kW32re[wi], (R)kW32im[wi])) : a[r];
+                        const V x0 = v[r];
+                        v[r] = Cx<R>::mk(x0.x + tt.x, x0.y + tt.y);
+                        v[r + SIG] = Cx<R>::mk(x0.x - tt.x, x0.y - tt.y);
                     }
                 }
             }
         }
-        if (L < nl) {
-            if (MODE == kLinePupil) {
+        if constexpr (MODE == kLinePupil) {
+            if (L >= 0) {
                 double2* Gl = A.G + ((int64_t)b * g.nx2 + L) * g.py + i;
 #pragma unroll
                 for (int r = 0; r < PAD; ++r) Gl[(int64_t)N * r] = v[r];
-            } else {
-                double* Pr = A.psf + ((int64_t)b * g.py + L) * g.px + i;
-                double2* Er = A.efield + ((int64_t)b * g.py + L) * g.px + i;
+            }
+        } else if constexpr (MODE == kLinePeak32) {
+            // this row's max (uint order of non-negative floats is numeric, NaN above +inf)
+            unsigned mr = 0u;
 #pragma unroll
-                for (int r = 0; r < PAD; ++r) {
-                    const double re = v[r].x * dA, im = v[r].y * dA;
-                    const double I = fma(re, re, im * im);
-                    if (MODE == kLinePeak) {
-                        m = dmax_nan(m, I);
-                    } else {
-                        Pr[N * r] = I * scale;
-                        if (MODE == kLineWriteE) {
-                            const int lo = i + N * r;
-                            const double2 py_ph = A.Wy[((int64_t)L * (g.ny2 / 2)) % g.py];
-                            const double2 px_ph = A.Wx[((int64_t)lo * (g.nx2 / 2)) % g.px];
-                            double2 e = cmul(make_double2(re, im), make_double2(py_ph.x, -py_ph.y));
-                            e = cmul(e, make_double2(px_ph.x, -px_ph.y));
-                            Er[N * r] = make_double2(sgn * e.x / sq, sgn * e.y / sq);
-                        }
+            for (int r = 0; r < PAD; ++r) {
+                const float U = fmaf(v[r].x, v[r].x, v[r].y * v[r].y);
+                mr = max(mr, __float_as_uint(U));
+            }
+            constexpr int W = N < 64 ? N : 64;
+#pragma unroll
+            for (int off = 1; off < W; off <<= 1) mr = max(mr, (unsigned)__shfl_xor((int)mr, off));
+            if (N > 64) {
+                if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = (double)__uint_as_float(mr);
+                __syncthreads();
+                if (i == 0)
+                    for (int w = 1; w < N / 64; ++w) mr = max(mr, __float_as_uint((float)wm[(threadIdx.x >> 6) + w]));
+            }
+            if (i == 0 && L >= 0) {
+                A.rowmax32[(int64_t)b * g.py + L] = __uint_as_float(mr);
+                m32 = max(m32, mr);
+            }
+        } else {
+          if (L >= 0) {
+            double* Pr = A.psf + ((int64_t)b * g.py + L) * g.px + i;
+            double2* Er = A.efield + ((int64_t)b * g.py + L) * g.px + i;
+#pragma unroll
+            for (int r = 0; r < PAD; ++r) {
+                const double U = fma(v[r].x, v[r].x, v[r].y * v[r].y);
+                if (MODE == kLinePeak) {
+                    m = fmax(m, U);
+                    nan_sum += U;  // NaN iff some U is NaN (U >= 0): numpy's max propagates it
+                } else {
+                    if (AKB_PSF_NT)
+                        __builtin_nontemporal_store(U * scale, Pr + N * r);
+                    else
+                        Pr[N * r] = U * scale;
+                    if (MODE == kLineWriteE) {
+                        const double re = v[r].x * dA, im = v[r].y * dA;
+                        const int lo = i + N * r;
+                        const double2 py_ph = A.Wy[((int64_t)L * (g.ny2 / 2)) % g.py];
+                        const double2 px_ph = A.Wx[((int64_t)lo * (g.nx2 / 2)) % g.px];
+                        double2 e = cmul(make_double2(re, im), make_double2(py_ph.x, -py_ph.y));
+                        e = cmul(e, make_double2(px_ph.x, -px_ph.y));
+                        Er[N * r] = make_double2(sgn * e.x / sq, sgn * e.y / sq);
                     }
                 }
             }
+          }
         }
         grp = next;
     }
     if (MODE == kLinePeak) {
+        if (nan_sum != nan_sum) m = nan_sum;
         for (int off = 32; off > 0; off >>= 1) m = dmax_nan(m, __shfl_down(m, off));
+        __syncthreads();
         if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
         __syncthreads();
         if (threadIdx.x == 0) {
             for (int w = 1; w < S::kThreads / 64; ++w) m = dmax_nan(m, wm[w]);
-            atomic_max_nonneg(A.imax + b, m);
+            atomic_max_nonneg(A.umax + b, m);
         }
+    } else if (MODE == kLinePeak32) {
+        // thousands of workgroups meet on one word: only a new maximum issues the atomic
+        if (m32 > __hip_atomic_load(A.umax32 + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(A.umax32 + b, m32);
     }
 }
 
+// the fp64 peak pass's rows: those whose fp32 max is within kPeakSlack of the fp32 peak (one
+// workgroup per batch entry; -1 = every row)
+__global__ void __launch_bounds__(1024) k_psf_peak_rows(PsfLineArgs A, int limit) {
+    __shared__ int cnt;
+    const int b = blockIdx.x, py = A.g.py;
+    const float M = __uint_as_float(A.umax32[b]);
+    const bool all = !(M > 0.0f) || !isfinite(M);
+    const float thr = M * (1.0f - kPeakSlack);
+    if (threadIdx.x == 0) cnt = 0;
+    __syncthreads();
+    if (!all) {
+        const float* rm = A.rowmax32 + (int64_t)b * py;
+        int* cd = A.cand + (int64_t)b * py;
+        for (int r = threadIdx.x; r < py; r += blockDim.x) {
+            if (rm[r] >= thr) {
+                const int k = atomicAdd(&cnt, 1);
+                if (k < limit) cd[k] = r;
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) A.cand_n[b] = (all || cnt > limit) ? -1 : cnt;
+}
+
 // persistent workgroups per pass: the resident count (LDS / threads) x 256 CUs, a multiple of 8
-template <int N, int PAD>
+template <int N, int PAD, typename R>
 static int line_wgs(int ngroups) {
     using S = LineShape<N, PAD>;
-    const int lds = (int)sizeof(double2) * (S::LINES * S::SIG * N + S::LINES * N + S::kTab);
+    const int lds = (int)(2 * sizeof(R)) * (S::LINES * S::SIG * N + S::LINES * N + S::kTab);
     int per_cu = (160 * 1024) / lds;
     const int by_threads = 2048 / S::kThreads;
     if (per_cu > by_threads) per_cu = by_threads;
@@ -856,9 +996,13 @@ static int line_wgs(int ngroups) {
 template <int N, int PAD, int MODE>
 static int launch_psf_line(PsfLineArgs fa, int nlines, int batch, hipStream_t s) {
     using S = LineShape<N, PAD>;
+    using R = typename std::conditional<MODE == kLinePeak32, float, double>::type;
     fa.ngroups = (nlines + S::LINES - 1) / S::LINES;
-    k_psf_line<N, PAD, MODE><<<dim3(line_wgs<N, PAD>(fa.ngroups), batch), S::kThreads, 0, s>>>(fa);
-    return launch_status(MODE == kLinePupil ? "k_psf_line(pupil)" : MODE == kLinePeak ? "k_psf_line(peak)" : "k_psf_line(write)");
+    k_psf_line<N, PAD, MODE><<<dim3(line_wgs<N, PAD, R>(fa.ngroups), batch), S::kThreads, 0, s>>>(fa);
+    return launch_status(MODE == kLinePupil  ? "k_psf_line(pupil)"
+                         : MODE == kLinePeak32 ? "k_psf_line(peak32)"
+                         : MODE == kLinePeak   ? "k_psf_line(peak)"
+                                               : "k_psf_line(write)");
 }
 
 // pad 16: lines of 16..1024; pad 8: 8..512 (Q = N / PAD <= 64)
@@ -935,6 +1079,11 @@ static bool psf_fast_ok(const PsfGeom& g) {
 
 static int64_t psf_fast_bytes(const PsfGeom& g, int batch) {
     return ((int64_t)batch * g.ny2 * g.px * 16 + 255) / 256 * 256;
+}
+
+// one 4-byte value per psf row and batch entry (fp32 row maxima, then the fp64 peak pass's rows)
+static int64_t psf_line_rows_bytes(const PsfGeom& g, int batch) {
+    return ((int64_t)batch * g.py * 4 + 255) / 256 * 256;
 }
 
 // W_P tables, built once per (device, P) and kept by the library (freed by akb_psf_release_plans)
@@ -1018,7 +1167,8 @@ extern "C" {
 int64_t akb_psf_work_bytes(int ny, int nx, int pad, int batch) {
     if (ny <= 0 || nx <= 0 || pad < 1 || batch < 1) return -1;
     const PsfGeom g = psf_geom(ny, nx, pad);
-    if (psf_line_ok(g, pad) || psf_fast_ok(g)) return psf_fast_bytes(g, batch);  // G: ex x py, H: ey x px
+    if (psf_line_ok(g, pad)) return psf_fast_bytes(g, batch) + 256 + 2 * psf_line_rows_bytes(g, batch);  // G, peaks, rows
+    if (psf_fast_ok(g)) return psf_fast_bytes(g, batch);             // H (ey x px)
     PlanEntry e;
     if (get_plan(g.py, g.px, batch, &e) != AKB_OK) return -1;
     const int64_t field = (int64_t)batch * g.py * g.px * 16;
@@ -1047,7 +1197,13 @@ int akb_psf_f64(const double* opd, const double* amp, int ny, int nx, int pad, i
         la.wmax = hann_max;
         la.g = g;
         for (int b = 0; b < batch; ++b) la.kphase[b] = (2.0 * M_PI / lambdas[b]);
+        char* tail = (char*)work + psf_fast_bytes(g, batch);
         la.G = (double2*)work;
+        la.umax = (double*)tail;
+        la.umax32 = (unsigned*)(tail + 64);
+        la.cand_n = (int*)(tail + 128);
+        la.rowmax32 = (float*)(tail + 256);
+        la.cand = (int*)(tail + 256 + psf_line_rows_bytes(g, batch));
         if ((st = get_twiddles(g.px, s, &la.Wx))) return st;
         if ((st = get_twiddles(g.py, s, &la.Wy))) return st;
         la.dA = dx * dy;
@@ -1056,6 +1212,17 @@ int akb_psf_f64(const double* opd, const double* amp, int ny, int nx, int pad, i
         la.efield = (double2*)efield_re_im;
         la.imax = d_imax;
         if ((st = psf_line_dispatch<kLinePupil>(g.ny2, pad, la, g.nx2, batch, s))) return st;
+        // the fp32 peak pass pays off on large planes (16384^2: 0.91 -> 0.58 ms with its row
+        // re-run); below 2^24 points the fp64 pass alone is faster (2048^2: 14 us vs 29 us + 11)
+        const char* pk = getenv("AKB_PSF_PEAK");
+        const bool peak32 = pk ? strcmp(pk, "f32") == 0 : (int64_t)g.py * g.px >= (1LL << 24);
+        if (peak32) {
+            if ((st = psf_line_dispatch<kLinePeak32>(g.nx2, pad, la, g.py, batch, s))) return st;
+            k_psf_peak_rows<<<batch, 1024, 0, s>>>(la, g.py / 4);
+            if ((st = launch_status("k_psf_peak_rows"))) return st;
+        } else {
+            la.cand = nullptr;
+        }
         if ((st = psf_line_dispatch<kLinePeak>(g.nx2, pad, la, g.py, batch, s))) return st;
         if (la.efield) return psf_line_dispatch<kLineWriteE>(g.nx2, pad, la, g.py, batch, s);
         return psf_line_dispatch<kLineWrite>(g.nx2, pad, la, g.py, batch, s);

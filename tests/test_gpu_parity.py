@@ -722,6 +722,13 @@ def test_psf_pruned_transform(gpu, ny, nx, pad, win, eff, monkeypatch):
         e = fast[1][0].cpu().numpy()
         assert np.max(np.abs(e - ref[3])) <= 1e-10 * np.max(np.abs(ref[3]))
     if pad in (8, 16):
+        # the fp32 peak pass only picks the rows of the exact fp64 one: identical bits either way
+        for mode in ("f64", "f32"):
+            monkeypatch.setenv("AKB_PSF_PEAK", mode)
+            alt = G.psf_stack(o, None, [lam], dx, dy, pad_factor=pad, window="hann" if win else None,
+                              workspace=G.PsfWorkspace())
+            assert torch.equal(alt[0][0], fast[0][0])
+        monkeypatch.delenv("AKB_PSF_PEAK")
         monkeypatch.setenv("AKB_PSF_PATH", "cols")
         cols = G.psf_stack(o, None, [lam], dx, dy, pad_factor=pad, window="hann" if win else None,
                            workspace=G.PsfWorkspace())
@@ -730,6 +737,36 @@ def test_psf_pruned_transform(gpu, ny, nx, pad, win, eff, monkeypatch):
     slow = G.psf_stack(o, None, [lam], dx, dy, pad_factor=pad, window="hann" if win else None,
                        workspace=G.PsfWorkspace())
     assert np.max(np.abs(slow[0][0].cpu().numpy() - got)) <= 1e-12
+
+
+@pytest.mark.parametrize("case", ["point", "zero", "nan"])
+def test_psf_line_peak_edges(gpu, case, monkeypatch):
+    """The line transforms' peak at its edges: one lit pixel (a flat |F|: every row ties the fp32
+    peak, so the fp64 pass runs over all rows), a dark pupil (Imax = 0: the unnormalised plane) and
+    an infinite amplitude (NaN in the plane: numpy's max propagates it) - against the oracle and
+    against the fp64-only peak."""
+    from akbraytracing_amd import psf as G
+    import oracle.psf as OP
+    n, pad = 64, 16
+    opd = np.zeros((n, n))
+    amp = np.zeros((n, n))
+    if case == "point":
+        amp[17, 40] = 0.75
+    elif case == "nan":
+        amp[:] = 1.0
+        amp[5, 9] = np.inf
+    o, a = torch.from_numpy(opd).to(gpu), torch.from_numpy(amp).to(gpu)
+    got = G.psf_stack(o, a, [13.5e-9], 5e-6, 5e-6, pad_factor=pad)[0][0].cpu().numpy()
+    with np.errstate(invalid="ignore"):
+        ref = OP.psf(opd, amp, 13.5e-9, 5e-6, 1e-2, pad)[0]
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    fin = np.isfinite(ref)
+    if fin.any():
+        assert np.max(np.abs(got[fin] - ref[fin])) <= 1e-10 * max(1.0, np.max(np.abs(ref[fin])))
+    for mode in ("f64", "f32"):
+        monkeypatch.setenv("AKB_PSF_PEAK", mode)
+        alt = G.psf_stack(o, a, [13.5e-9], 5e-6, 5e-6, pad_factor=pad)[0][0].cpu().numpy()
+        assert np.array_equal(alt, got, equal_nan=True)
 
 
 def test_psf_errors(gpu):
