@@ -133,6 +133,38 @@ __device__ __forceinline__ double rcp_core(double s) {
 }
 __device__ __forceinline__ bool in_fast_range(double v) { return v >= 0x1p-767 && v <= 0x1p+1000; }
 
+// x / d as hipcc's IEEE division computes it, without its operand scaling: hipcc emits
+// v_div_scale (both operands), rcp + two Newton steps, the quotient and its residual, v_div_fmas
+// and v_div_fixup. For |x| and |d| in [2^-300, 2^300] the scaling is the identity (exponent
+// difference < 768, no operand, reciprocal or quotient near the denormals, numerator exponent
+// far above 53), v_div_fmas is a plain FMA and v_div_fixup returns its input, so the core below
+// gives the same bits in 8 instead of 12 instructions (checked bitwise by k_selftest).
+__device__ __forceinline__ bool in_div_range(double v) {
+    const double a = fabs(v);
+    return a >= 0x1p-300 && a <= 0x1p+300;
+}
+__device__ __forceinline__ double div_core(double x, double d) {
+    double y = __builtin_amdgcn_rcp(d);
+    double e = __builtin_fma(-d, y, 1.0);
+    y = __builtin_fma(y, e, y);
+    e = __builtin_fma(-d, y, 1.0);
+    y = __builtin_fma(y, e, y);
+    const double q = x * y;
+    const double r = __builtin_fma(-d, q, x);
+    return __builtin_fma(r, y, q);
+}
+// every lane takes the core; a wave holding a lane outside the range (a uniform branch) computes
+// the library quotient and selects it for those lanes
+__device__ __forceinline__ double div_w(double x, double d) {
+    const bool in = in_div_range(x) && in_div_range(d);
+    double q = div_core(x, d);
+    if (__builtin_expect(__ballot(!in) != 0, 0)) {
+        const double ql = x / d;
+        q = in ? q : ql;
+    }
+    return q;
+}
+
 // Correctly rounded square root without the tiny-input rescaling. hipcc's sqrt(double) on gfx950
 // scales inputs below 2^-767 by 2^256 (cmp, cndmask, ldexp in; cndmask, ldexp out; class test for
 // 0 / inf) around an rsq + Goldschmidt/Newton core. For inputs in [2^-767, 2^1000] the rescale is
@@ -140,8 +172,11 @@ __device__ __forceinline__ bool in_fast_range(double v) { return v >= 0x1p-767 &
 // sequence - gives the bit-identical result in fewer instructions. Everything else (zero,
 // negatives, NaN, inf, tiny or huge values: never produced by the trace's unit-vector norms,
 // discriminants and metre-scale segment lengths) takes sqrt() itself.
+// The range test is wave-wide: every lane takes the core and only a wave holding a lane outside
+// the range (a uniform branch) runs the library sqrt and selects it for those lanes - a per-lane
+// branch would be if-converted into the library's scaling selects on every lane.
 __device__ __forceinline__ double sqrt_cr(double x) {
-    if (__builtin_expect(!(x >= 0x1p-767 && x <= 0x1p+1000), 0)) return sqrt(x);
+    const bool in = in_fast_range(x);
     const double r = __builtin_amdgcn_rsq(x);
     double g = x * r;
     double h = r * 0.5;
@@ -151,7 +186,12 @@ __device__ __forceinline__ double sqrt_cr(double x) {
     h = __builtin_fma(h, e, h);
     g = __builtin_fma(d, h, g);
     const double d2 = __builtin_fma(-g, g, x);
-    return __builtin_fma(d2, h, g);
+    double s = __builtin_fma(d2, h, g);
+    if (__builtin_expect(__ballot(!in) != 0, 0)) {
+        const double sl = sqrt(x);
+        s = in ? s : sl;
+    }
+    return s;
 }
 
 // np.linalg.norm(v, axis=0) for one column: sqrt((x*x + y*y) + z*z)
@@ -344,7 +384,7 @@ __device__ __forceinline__ void matvec(const Mat3& R, double x, double y, double
 __device__ __forceinline__ void plane_hit(double g, double h, double i, double j, double l, double m,
                                           double n, double p, double q, double r, double& x,
                                           double& y, double& z) {
-    const double t = -(g * p + h * q + i * r + j) / (g * l + h * m + i * n);
+    const double t = div_w(-(g * p + h * q + i * r + j), g * l + h * m + i * n);
     x = t * l + p;
     y = t * m + q;
     z = t * n + r;

@@ -543,7 +543,7 @@ __device__ __forceinline__ void mirror_step(const CMirror& Q, Ray& R, double& op
     }
     const double D = B * B - 4.0 * A * C;
     const double sD = sqrt_disc(D, AKB_FLAG_MISS << (4 * k), fl);
-    const double t = (-B + sD * Q.sgn) / (2.0 * A);  // (-B - sD) / (2A) for the minus root
+    const double t = div_w(-B + sD * Q.sgn, 2.0 * A);  // (-B - sD) / (2A) for the minus root
     const double x = t * l + p, y = t * m + q, z = t * n + r;
     if (kOPL) {  // opl starts at +0.0: 0 + d is d exactly
         if (kOrigin)
@@ -777,7 +777,7 @@ __device__ __forceinline__ void chain_ray_tab(const ChainArgs& a, int64_t i0, in
         qv[4] = z;
     }
     if (kNeedQ || (!kLean && !kFixed && (a.atan_h || a.atan_v))) {
-        const double il = 1.0 / l;
+        const double il = div_w(1.0, l);
         qv[0] = atan_slope(div_shared(m, l, il));
         qv[1] = atan_slope(div_shared(nn, l, il));
         if (!kFixed && a.atan_h) (a.atan_h + i0)[t] = qv[0];
@@ -1388,8 +1388,9 @@ static inline V3In v3in(const double* p, int64_t ld, int64_t inc) { return V3In{
 
 // occupancy variant of the chain kernels (minimum waves per SIMD the register allocator must
 // allow); AKB_CHAIN_WAVES in the environment selects one for A/B timing, default 4. RayWave's pass
-// 2 (the fixed-output sink variant) has its own knob, AKB_PASS2_WAVES, default 6 (measured in the
-// pipelined bench: 4 and 6 equal at 0.396 ms, 8 - 64 VGPRs and 160 B of spills - 0.407 ms)
+// 2 (the fixed-output sink variant) has its own knob, AKB_PASS2_WAVES, default 4: 89 VGPRs and no
+// scratch (6 waves: 80 VGPRs and 8 spilled; both 0.358 ms in the 100 / 30-step bench after the
+// wave-guarded division and sqrt; 8 - 64 VGPRs and 160 B of spills - measured slower)
 static int waves_from_env(const char* name, int dflt) {
     const char* e = getenv(name);
     const int v = e ? atoi(e) : dflt;
@@ -1400,7 +1401,7 @@ static int chain_waves() {
     return w;
 }
 static int pass2_waves() {
-    static int w = waves_from_env("AKB_PASS2_WAVES", 6);
+    static int w = waves_from_env("AKB_PASS2_WAVES", 4);
     return w;
 }
 
@@ -2143,7 +2144,8 @@ namespace akb {
 constexpr int kSelftestCols = AKB_SELFTEST_COLS;
 
 // out row i: sqrt_cr(a), sqrt(a), div_shared(a, b), a / b, div_pos(a, b), norm3_inv's s and inv of
-// (a, b, b), norm3 with 1.0 / norm3 of the same vector, atan_slope(a) and OCML's atan(a)
+// (a, b, b), norm3 with 1.0 / norm3 of the same vector, atan_slope(a), OCML's atan(a), div_w(a, b)
+// and div_w(1, b)
 __global__ void k_selftest(const double* a, const double* b, int64_t n, double* out) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const double x = a[i], s = b[i];
@@ -2162,6 +2164,8 @@ __global__ void k_selftest(const double* a, const double* b, int64_t n, double* 
         o[8] = 1.0 / sqrt(v);
         o[9] = atan_slope(x);
         o[10] = atan(x);
+        o[11] = div_w(x, s);
+        o[12] = div_w(1.0, s);
     }
 }
 }  // namespace akb

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define AKB_ABI_VERSION 12
+#define AKB_ABI_VERSION 13
 
 /* status codes */
 #define AKB_OK 0
@@ -500,11 +500,12 @@ int akb_gd_eval_f64(const double* x, const double* y, int nv, int nh, const uint
                     const double* gy, int my, const double* f, const double* grad, int nvals, int* owner,
                     double* out, void* stream);
 
-/* diagnostics: out[11i..11i+10] = (the trace's sqrt, sqrt, the trace's shared-reciprocal a/b, a/b,
+/* diagnostics: out[13i..13i+12] = (the trace's sqrt, sqrt, the trace's shared-reciprocal a/b, a/b,
  * the positive-divisor a/b, the trace's norm and reciprocal norm of (a, b, b), sqrt and 1/sqrt of
- * that squared norm, the trace's slope arctan of a, the library atan of a) for n pairs (a[i], b[i])
- * — used by the tests to check the shortcuts bit for bit (the arctan to its stated accuracy) */
-#define AKB_SELFTEST_COLS 11
+ * that squared norm, the trace's slope arctan of a, the library atan of a, the trace's a/b and
+ * 1/b) for n pairs (a[i], b[i]) — used by the tests to check the shortcuts bit for bit (the
+ * arctan to its stated accuracy) */
+#define AKB_SELFTEST_COLS 13
 int akb_selftest_arith_f64(const double* a, const double* b, int64_t n, double* out, void* stream);
 
 /* release cached rocFFT plans (also done at unload) */

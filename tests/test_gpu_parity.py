@@ -150,7 +150,7 @@ def test_arith_shortcuts_bitwise(gpu):
     a = np.concatenate([a, special])
     b = np.concatenate([b, np.full(special.shape, 3.0)])
     ta, tb = torch.from_numpy(a).to(gpu), torch.from_numpy(b).to(gpu)
-    cols = 11
+    cols = 13
     out = torch.empty((a.shape[0], cols), dtype=torch.float64, device=gpu)
     _lib.check(_lib.lib().akb_selftest_arith_f64(D.ptr(ta), D.ptr(tb), a.shape[0], D.ptr(out), D.stream_handle()))
     o = out.cpu().numpy()
@@ -167,6 +167,33 @@ def test_arith_shortcuts_bitwise(gpu):
     assert np.array_equal(bits(o[ok, 5]), bits(o[ok, 7]))
     assert np.array_equal(bits(o[ok, 6]), bits(o[ok, 8]))
     assert np.array_equal(bits(o[ok, 8]), bits(1.0 / np.sqrt(v[ok])))
+    # the trace's division (core in [2^-300, 2^300], library outside) equals a / b and 1 / b
+    with np.errstate(all="ignore"):
+        assert np.array_equal(o[:, 11], a / b, equal_nan=True) and np.array_equal(bits(o[fin, 11]), bits((a / b)[fin]))
+        assert np.array_equal(bits(o[:, 12]), bits(1.0 / b))
+    # and over the whole exponent range, signs, zeros, infinities and NaN, as both operands
+    n2 = 2_000_000
+    a2 = (rng.random(n2) + 0.5) * 2.0 ** rng.integers(-1074, 1023, n2).astype(np.float64)
+    b2 = (rng.random(n2) + 0.5) * 2.0 ** rng.integers(-1074, 1023, n2).astype(np.float64)
+    a2[::2] *= -1.0
+    b2[::3] *= -1.0
+    mid = rng.random(n2) < 0.5  # half inside the core's range, near its edges
+    a2[mid] = (rng.random(mid.sum()) + 0.5) * 2.0 ** rng.integers(-302, 302, mid.sum()).astype(np.float64)
+    b2[mid] = (rng.random(mid.sum()) + 0.5) * 2.0 ** rng.integers(-302, 302, mid.sum()).astype(np.float64)
+    sp = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 5e-324, 2.0 ** -300, 2.0 ** 300, 1.0, -1.0])
+    a2 = np.concatenate([a2, np.repeat(sp, sp.size)])
+    b2 = np.concatenate([b2, np.tile(sp, sp.size)])
+    t2a, t2b = torch.from_numpy(a2).to(gpu), torch.from_numpy(b2).to(gpu)
+    out2 = torch.empty((a2.shape[0], cols), dtype=torch.float64, device=gpu)
+    _lib.check(_lib.lib().akb_selftest_arith_f64(D.ptr(t2a), D.ptr(t2b), a2.shape[0], D.ptr(out2), D.stream_handle()))
+    o2 = out2.cpu().numpy()
+    with np.errstate(all="ignore"):
+        q = a2 / b2
+        nanq = np.isnan(q)
+        assert np.array_equal(np.isnan(o2[:, 11]), nanq) and np.array_equal(bits(o2[~nanq, 11]), bits(q[~nanq]))
+        r = 1.0 / b2
+        nanr = np.isnan(r)
+        assert np.array_equal(np.isnan(o2[:, 12]), nanr) and np.array_equal(bits(o2[~nanr, 12]), bits(r[~nanr]))
     # slope arctan: the library atan above 2^-4; below, within 1 ulp of the correctly rounded value
     # (200-bit mpmath) and equal to it on nearly every argument
     big = fin & (np.abs(a) > 2.0 ** -4)
