@@ -434,7 +434,9 @@ __device__ __forceinline__ void leaf_sink_segment(const akb_leaf_sink& S, LeafLd
 #pragma unroll
         for (int row = 1; row < 16; ++row) r = r + p[row * 8];
         int c = 16;
-        if (nan0 && r != r) {
+        // wave-uniform: a per-lane branch is if-converted into 16 compares and 40 selects per
+        // segment on every lane
+        if (__builtin_expect(__ballot(nan0 && r != r) != 0, 0) && nan0 && r != r) {
             double x = p[0];
             bool bad = x != x;
             r = bad ? 0.0 : x;
