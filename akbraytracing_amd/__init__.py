@@ -18,8 +18,8 @@ import os as _os
 import torch as _torch  # noqa: F401  (loads torch's HIP runtime before libakb_hip.so)
 
 from ._lib import AKBError, lib  # noqa: F401
-from .install import install, uninstall  # noqa: F401
+from .install import NATIVE_NAMES, install, uninstall  # noqa: F401
 
 DROPIN_DIR = _os.path.join(_os.path.dirname(_os.path.abspath(__file__)), "dropin")
 
-__all__ = ["install", "uninstall", "lib", "AKBError", "DROPIN_DIR"]
+__all__ = ["install", "uninstall", "NATIVE_NAMES", "lib", "AKBError", "DROPIN_DIR"]

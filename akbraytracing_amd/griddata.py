@@ -9,11 +9,12 @@ scipy answers with a Clough-Tocher interpolant on the points' Delaunay triangula
 are the ray grid's hits, a smoothly deformed n_v x n_h lattice, so CubicGrid builds that
 triangulation structurally (akb_griddata.hip: cell diagonals by the in-circle test, the hull
 pockets on the host, local-Delaunay checks that refuse a grid where this would not be qhull's
-answer), estimates the vertex gradients by sweeps of scipy's own local solve until they stop
-changing (line Gauss-Seidel in LDS strips: each row sees its upper neighbours' new values), and
-evaluates the patches on the device. Agreement with scipy is to rounding on the reference's
-65 x 65 run (tests/test_gpu_parity.py), not bit for bit: qhull's co-circular tie-breaks and
-scipy's Gauss-Seidel iterates are not reproduced: both iterations converge to the same fixed point,
+answer), estimates the vertex gradients by Jacobi sweeps of scipy's own local solve with
+Chebyshev semi-iteration (a register-resident strip kernel, two sweeps per launch) until they stop
+changing, and evaluates the patches on the device. Agreement with scipy is to rounding on the
+reference's 65 x 65 run (tests/test_gpu_parity.py) and within 1e-6 of the range at 1001^2 /
+3163^2 (tests/test_fullsize_gpu.py), not bit for bit: qhull's near-cocircular picks and scipy's
+Gauss-Seidel iterates are not reproduced - both iterations converge to the same fixed point,
 scipy's stopping at a largest relative change of 1e-6, ours at GRADIENT_TOL (within ~1e-8 of the
 map's range of that point).
 """

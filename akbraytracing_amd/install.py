@@ -215,6 +215,8 @@ _NATIVE = {
     "saveWaveData": None,
     "compare_sep": None,
 }
+# every name install() can rebind (pass a subset as `names`)
+NATIVE_NAMES = tuple(_NATIVE)
 # functions with an mpmath branch in the reference
 _MPMATH_AWARE = {"mirr_ray_intersection", "reflect_ray"}
 
@@ -231,8 +233,13 @@ def _wrap(mod, name, original, native):
 
 
 def install(mod, names=None):
-    """Rebind `names` (default: every hot-path name the module defines) in `mod`.
-    Returns the list of rebound names. uninstall(mod) restores the originals."""
+    """Rebind `names` (default: every hot-path name the module defines, NATIVE_NAMES) in `mod`.
+    Returns the list of rebound names. uninstall(mod) restores the originals.
+
+    Parity unpinned: extract_affine_square_region (AKB_raytrace_20250312.py:1047-1119) restates
+    OpenCV's findContours / approxPolyDP / warpAffine; cv2 is not importable here and the reference
+    holds no recorded output of it, so it is checked only against oracle/affine.py and closed forms.
+    Leave it out of `names` to keep the reference's cv2 step."""
     done = []
     for name in (names or _NATIVE):
         if name not in _NATIVE or not hasattr(mod, name):

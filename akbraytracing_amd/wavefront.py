@@ -87,12 +87,17 @@ class Shard:
 
     @staticmethod
     def split(n, world, rank):
+        """Rank `rank`'s contiguous range of whole 8192-ray numpy sum buffers (the last rank takes the
+        short tail buffer too), so N ranks' per-buffer sums chain into one process's bits. A grid
+        needs at least 8192 * world rays to split (the reference's 33^2 / 65^2 grids run on one
+        rank): below that this raises ValueError, before any RayWave is built."""
         total = int(n) * int(n)
         if world == 1:
             return Shard(0, total)
         nbuf = total // NP_BUF
         if nbuf < world:
-            raise ValueError(f"a {n} x {n} grid holds {nbuf} full 8192-ray buffers: too few for {world} ranks")
+            raise ValueError(f"a {n} x {n} grid holds {nbuf} full 8192-ray buffers: too few for {world} ranks "
+                             f"(row shards need at least {NP_BUF * world} rays; trace it on one rank)")
         base, rem = divmod(nbuf, world)
         b0 = rank * base + min(rank, rem)
         nb = base + (1 if rank < rem else 0)
