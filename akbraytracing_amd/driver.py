@@ -39,13 +39,15 @@ def ray_wave_conditions(option_HighNA=True):
 
 def plot_result_ray_wave(params, ray_num, *, source_shift=(0.0, 0.0, 0.0), option_set=True, option_HighNA=True,
                          option_energy="EUV", option_AKB=True, directory=None, workdir=None, verbose=True,
-                         as_dict=False):
-    """The 'ray_wave' mode with option_legendre=True and option_save=True for the AKB system built
-    from params on a ray_num x ray_num grid. Returns (inner_products, orders, pvs) as the reference
-    (:3775), or np.inf where the reference returns np.inf (an unbuildable system). directory: the
-    module's directory_name (psf_calc's and the txt / csv outputs); workdir: where the reference's
-    cwd-relative 'matrixWave2(nm).txt' goes (default: the current directory). as_dict: also
-    return the intermediate maps (device tensors)."""
+                         as_dict=False, option_legendre=True):
+    """The 'ray_wave' mode with option_save=True for the AKB system built from params on a
+    ray_num x ray_num grid. With option_legendre (the alignment loops' call) returns
+    (inner_products, orders, pvs) as the reference (:3775); without it (the plotting run) writes the
+    run's conditions file optical_params.txt (:3803-3834) and returns np.nanstd(map / lambda) * 6
+    (:3913) - its figures are not drawn. np.inf where the reference returns np.inf (an unbuildable
+    system). directory: the module's directory_name (psf_calc's and the txt / csv outputs);
+    workdir: where the reference's cwd-relative 'matrixWave2(nm).txt' goes (default: the current
+    directory). as_dict: also return the intermediate maps (device tensors)."""
     from . import geometry as G
     from .affine import extract_affine_square_region
     from .psfcalc import psf_calc
@@ -92,11 +94,22 @@ def plot_result_ray_wave(params, ray_num, *, source_shift=(0.0, 0.0, 0.0), optio
         pvs[i] = (np.nanmax(fit_datas[i]) - np.nanmin(fit_datas[i])) * np.sign(inner_products[i])
     np.savetxt(os.path.join(out_dir, 'inner_products.csv'), inner_products, delimiter=',')
     np.savetxt(os.path.join(out_dir, 'orders.csv'), orders, delimiter=',')
-    pvs[-1] = np.nanstd(wave_lambda) * 6 * np.sign(np.sum(inner_products))
+    pv6 = np.nanstd(wave_lambda) * 6
+    if option_legendre:
+        pvs[-1] = pv6 * np.sign(np.sum(inner_products))
+    else:  # the plotting run: its conditions file (:3803-3834), then it returns the 6-sigma (:3913)
+        p = np.asarray(params, dtype=np.float64).ravel()
+        with open(os.path.join(out_dir, 'optical_params.txt'), 'w') as f:
+            f.write("input\n")
+            f.write("====================\n")
+            for i in range(26):
+                f.write(f"params[{i}]: {p[i]}\n")
     if as_dict:
         return dict(inner_products=inner_products, orders=orders, pvs=pvs, maps=m, run=run, psf=psf,
-                    rectified_img=rectified_img, fit_datas=fit_datas, grid_H=grid_H, grid_V=grid_V)
-    return inner_products, orders, pvs
+                    rectified_img=rectified_img, fit_datas=fit_datas, grid_H=grid_H, grid_V=grid_V, pv=pv6)
+    if option_legendre:
+        return inner_products, orders, pvs
+    return pv6
 
 
 

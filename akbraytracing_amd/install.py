@@ -104,8 +104,9 @@ def _kb_debug_for(mod, original):
 def _plot_result_debug_for(mod, original):
     """plot_result_debug with its 'test' mode (the one auto_focus_NA and the alignment loops call
     hundreds of times), its 'sep' mode (auto_focus_sep's, sep.py), its 'wave' mode and its 'ray_wave'
-    mode with option_legendre (the alignment loops', driver.py) on the device;
-    every other mode runs the reference's own function, whose primitives install() has rebound."""
+    mode (driver.py: with option_legendre the alignment loops' call, without it the plotting run -
+    the same device chain and files, its figures not drawn) on the device; every other mode runs the
+    reference's own function, whose primitives install() has rebound."""
     def plot_result_debug(params, option, source_shift=[0., 0., 0.], option_tilt=True, option_legendre=False,
                           angular_shift=[0., 0.], option_save=True):
         if option == "test" and _akb_native_ok(mod) and list(angular_shift) == [0., 0.]:
@@ -115,16 +116,17 @@ def _plot_result_debug_for(mod, original):
             from .sep import plot_result_sep
             return plot_result_sep(params, source_shift, option_tilt, option_set=bool(getattr(mod, "option_set", False)),
                                    widesearch=bool(getattr(mod, "widesearch", False)))
-        if (option == "ray_wave" and option_legendre and option_save and option_tilt and _akb_native_ok(mod)
+        if (option == "ray_wave" and option_save and option_tilt and _akb_native_ok(mod)
                 and list(angular_shift) == [0., 0.] and getattr(mod, "wave_num_H", 0) == getattr(mod, "wave_num_V", 1)):
-            # the alignment loops' call: the whole chain on the device (driver.py); the plotting
-            # run (option_legendre=False) stays the reference's
+            # the whole chain on the device (driver.py): the alignment loops' call (option_legendre)
+            # and the live __main__ plotting run (:14603-14611; its figures not drawn)
             from .driver import plot_result_ray_wave
             return plot_result_ray_wave(params, mod.wave_num_H, source_shift=source_shift,
                                         option_set=bool(getattr(mod, "option_set", False)),
                                         option_HighNA=getattr(mod, "option_HighNA", True),
                                         option_energy=getattr(mod, "option_energy", "EUV"), option_AKB=True,
-                                        directory=getattr(mod, "directory_name", None))
+                                        directory=getattr(mod, "directory_name", None),
+                                        option_legendre=bool(option_legendre))
         if (option == "wave" and _akb_native_ok(mod) and list(angular_shift) == [0., 0.]
                 and getattr(mod, "option_rotate", True) and getattr(mod, "wave_num_H", 0) == getattr(mod, "wave_num_V", 1)):
             from .wavedata import plot_result_wave

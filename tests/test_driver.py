@@ -67,9 +67,28 @@ def test_ray_wave_mode_end_to_end(gpu, tmp_path):
 
 
 @pytest.mark.gpu
+def test_ray_wave_plotting_run(gpu, tmp_path):
+    """The live __main__ call without option_legendre (:14603-14611): the same chain, the
+    conditions file, and the reference's return value np.nanstd(map / lambda) * 6 (:3913)."""
+    from akbraytracing_amd.driver import plot_result_ray_wave
+    g = golden("akb_psfcalc_65.npz")
+    out_dir = tmp_path / "out"
+    pv = plot_result_ray_wave(_best_params(), 65, directory=str(out_dir), workdir=str(tmp_path), verbose=False,
+                              option_legendre=False)
+    ref = np.nanstd(g["plane_out"] / 13.5) * 6
+    assert abs(pv - ref) <= 1e-6 * ref
+    lines = (out_dir / "optical_params.txt").read_text().splitlines()
+    assert lines[:2] == ["input", "===================="] and len(lines) == 28
+    assert lines[2] == f"params[0]: {np.float64(_best_params()[0])}"
+    for name in ("matrixWave2_Corrected(lambda).txt", "rectified_img.txt", "inner_products.csv", "orders.csv"):
+        assert (out_dir / name).exists(), name
+
+
+@pytest.mark.gpu
 def test_install_routes_ray_wave_legendre(gpu, tmp_path, monkeypatch):
     """install(): plot_result_debug(params, 'ray_wave', option_legendre=True) runs the device chain
-    with the module's live flags; without option_legendre (the plotting run) the reference's own."""
+    with the module's live flags, and so does the plotting run without option_legendre (its figures
+    not drawn); option_save=False (no files) stays the reference's own."""
     import types
     import akbraytracing_amd
     monkeypatch.chdir(tmp_path)
@@ -85,6 +104,10 @@ def test_install_routes_ray_wave_legendre(gpu, tmp_path, monkeypatch):
         ip, orders, pvs = mod.plot_result_debug(_best_params(), "ray_wave", option_legendre=True)
         assert not seen and len(ip) == 15 and len(pvs) == 16
         assert os.path.exists(os.path.join(mod.directory_name, "inner_products.csv"))
-        assert mod.plot_result_debug(_best_params(), "ray_wave") == "orig" and seen == [("ray_wave", False)]
+        pv = mod.plot_result_debug(_best_params(), "ray_wave")
+        assert not seen and np.isfinite(pv) and pv > 0
+        assert os.path.exists(os.path.join(mod.directory_name, "optical_params.txt"))
+        assert mod.plot_result_debug(_best_params(), "ray_wave", option_save=False) == "orig"
+        assert seen == [("ray_wave", False)]
     finally:
         akbraytracing_amd.uninstall(mod)
