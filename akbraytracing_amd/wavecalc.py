@@ -30,7 +30,10 @@ def _field_dev(u, dev):
     return torch.from_numpy(np.ascontiguousarray(np.asarray(u, dtype=np.complex128))).to(dev)
 
 
-_WORK = {}  # device -> the split partials' scratch, reused across calls (up to ~516 MiB)
+# the split partials' scratch (up to ~516 MiB), reused across calls: one per host thread and
+# device - the _multi pattern's threads may share a device, and one call queues three kernels
+# (the pair sum and the two reduce levels) that must not interleave with another thread's on it
+_WORK = threading.local()
 
 
 def splits_for(n, m):
@@ -49,9 +52,10 @@ def propagate(tx, ty, tz, sx, sy, sz, u_ds, k, stream=None, work=None, splits=0)
     out = torch.empty(n, dtype=torch.complex128, device=dev)
     need = int(L.akb_huygens_work_bytes(n, m, int(splits)))
     if need > 0 and (work is None or work.numel() * 8 < need):
-        work = _WORK.get(dev)
+        cache = _WORK.__dict__.setdefault("by_device", {})
+        work = cache.get(dev)
         if work is None or work.numel() * 8 < need:
-            work = _WORK[dev] = torch.empty(need // 8 + 1, dtype=D.F64, device=dev)
+            work = cache[dev] = torch.empty(need // 8 + 1, dtype=D.F64, device=dev)
     ur = torch.view_as_real(u_ds)
     _lib.check(L.akb_huygens_f64(D.ptr(tx), D.ptr(ty), D.ptr(tz), n, D.ptr(sx), D.ptr(sy), D.ptr(sz), D.ptr(ur), m,
                                  float(k), D.ptr(torch.view_as_real(out)), int(splits),
