@@ -372,7 +372,8 @@ int akb_pairwise_sum_f64(const double* x, int64_t ld, int rows, int64_t n, int n
  * library's count depends on the device (its resident workgroups) and on n; it is capped so the
  * partials fit in 512 MiB.
  * work: device scratch of akb_huygens_work_bytes(n, m, splits) bytes: 16 n (splits + ceil(splits /
- * 128)) when splits > 1, at most ~516 MiB for the library's count (0 bytes for one split). */
+ * 128)) when splits > 1, at most ~516 MiB for the library's count (0 bytes for one split). One call
+ * queues three kernels that use it: concurrent calls need their own work buffers. */
 int akb_huygens_splits(int64_t n, int64_t m);
 int64_t akb_huygens_work_bytes(int64_t n, int64_t m, int splits);
 int akb_huygens_f64(const double* tx, const double* ty, const double* tz, int64_t n,

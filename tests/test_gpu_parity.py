@@ -766,6 +766,30 @@ def test_psf_pruned_transform(gpu, ny, nx, pad, win, eff, monkeypatch):
     assert np.max(np.abs(slow[0][0].cpu().numpy() - got)) <= 1e-12
 
 
+@pytest.mark.parametrize("n", [128, 512])
+def test_psf_line_stack_equals_single(gpu, n):
+    """The line transforms batched over wavelengths (one launch per pass for the stack; at 512^2 x
+    pad 16 = 8192^2 the fp32 peak route with its per-row re-run) equal one wavelength at a time,
+    bit for bit, and the oracle at 128^2."""
+    from akbraytracing_amd import psf as G
+    rng = np.random.default_rng(n)
+    opd = rng.standard_normal((n, n)) * 3e-9
+    opd[rng.random((n, n)) < 0.03] = np.nan
+    o = torch.from_numpy(opd).to(gpu)
+    lams = [13.5e-9, 1.35e-9, 6.7e-9]
+    st, _, imax = G.psf_stack(o, None, lams, 5e-6, 4e-6, pad_factor=16)
+    for b, lam in enumerate(lams):
+        one, _, im1 = G.psf_stack(o, None, [lam], 5e-6, 4e-6, pad_factor=16)
+        assert torch.equal(st[b], one[0]) and torch.equal(imax[b:b + 1], im1)
+        del one
+    if n == 128:
+        import oracle.psf as OP
+        amp = np.where(np.isfinite(opd), 1.0, 0.0)
+        for b, lam in enumerate(lams):
+            ref = OP.psf(opd, amp, lam, 5e-6, 1e-2, 16, dy=4e-6)[0]
+            assert np.max(np.abs(st[b].cpu().numpy() - ref)) <= 1e-10
+
+
 @pytest.mark.parametrize("case", ["point", "zero", "nan"])
 def test_psf_line_peak_edges(gpu, case, monkeypatch):
     """The line transforms' peak at its edges: one lit pixel (a flat |F|: every row ties the fp32
