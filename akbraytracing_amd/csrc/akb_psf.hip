@@ -558,12 +558,12 @@ enum { kLinePupil = 0, kLinePeak = 1, kLineWrite = 2, kLineWriteE = 3, kLinePeak
 #ifndef AKB_PSF_NT
 #define AKB_PSF_NT 1  // nontemporal psf stores (the stream must not evict G's lines): 0 for A/B
 #endif
-// The peak: kLinePeak32 runs pass 2 in fp32 (half the LDS bytes, twice the VALU rate) for each
+// The peak, fp32 route (AKB_PSF_PEAK=f32; the row-bound route below replaced it as the default on
+// large planes): kLinePeak32 runs pass 2 in fp32 (half the LDS bytes, twice the VALU rate) for each
 // row's max of |F|^2; the rows within kPeakSlack of the fp32 peak (the fp32 transform's error is
 // ~1e-6 of the peak, its worst-case bound ~1e-3 at 1024-point lines) are re-run in fp64
 // (kLinePeak over that list), which gives the exact max. Non-finite or zero peaks, or more than a
-// quarter of the rows within the slack, take the fp64 pass over every row. Planes of 2^24 points
-// and up (AKB_PSF_PEAK=f32 / f64 forces either way).
+// quarter of the rows within the slack, take the fp64 pass over every row.
 constexpr float kPeakSlack = 0.0625f;
 
 template <typename R>
@@ -646,6 +646,8 @@ struct PsfLineArgs {
     float* rowmax32;     // fp32 peak pass: (batch, py) row maxima
     int* cand;           // (batch, py) rows for the fp64 peak pass
     int* cand_n;         // per batch entry: their count, or -1 for every row
+    double* ubound;      // row-bound route: (batch, py) bounds B[ko] >= max_lo |F[ko][lo]|^2
+    double* ubmax;       // row-bound route: per batch entry max B, NaN when the route is off
     int ngroups;         // line groups (LINES lines each) per batch entry
 };
 
@@ -679,6 +681,22 @@ __global__ void __launch_bounds__((LineShape<N, PAD>::kThreads)) k_psf_line(PsfL
         A.umax[b] = 0.0;  // pass 2 follows
         A.umax32[b] = 0u;
     }
+    // this workgroup's line groups: an XCD's contiguous share, slot-strided within it
+    const int ngr = rows ? (nl + LINES - 1) / LINES : A.ngroups, nwg = gridDim.x;
+    int base = 0, slot = blockIdx.x, nslot = nwg, RR = ngr;
+    if ((nwg & 7) == 0) {
+        RR = (ngr + 7) / 8;
+        base = (blockIdx.x & 7) * RR;
+        slot = blockIdx.x >> 3;
+        nslot = nwg >> 3;
+    }
+    auto group_at = [&](int k) {
+        const int o = slot + k * nslot;
+        const int gi = base + o;
+        return (o < RR && gi < ngr) ? gi : -1;
+    };
+    // a workgroup without lines (the peak rounds' short row lists) leaves before its tables
+    if (group_at(0) < 0) return;
     // stage-1 twiddles, W_N^m = W_P^(PAD m): four-step, TA[q2][t] = W_N^(q2 t),
     // TB[q1][t] = W_N^(q1 Q2 t), TQ[q2][k1] = W_Q^(q2 k1); one-step, T2[q][t] = W_N^(q t)
     V* TA = tab;
@@ -712,20 +730,6 @@ __global__ void __launch_bounds__((LineShape<N, PAD>::kThreads)) k_psf_line(PsfL
     }
     const double sgn = ((g.ny2 / 2 + g.nx2 / 2) & 1) ? -1.0 : 1.0;
 
-    // this workgroup's line groups: an XCD's contiguous share, slot-strided within it
-    const int ngr = rows ? (nl + LINES - 1) / LINES : A.ngroups, nwg = gridDim.x;
-    int base = 0, slot = blockIdx.x, nslot = nwg, RR = ngr;
-    if ((nwg & 7) == 0) {
-        RR = (ngr + 7) / 8;
-        base = (blockIdx.x & 7) * RR;
-        slot = blockIdx.x >> 3;
-        nslot = nwg >> 3;
-    }
-    auto group_at = [&](int k) {
-        const int o = slot + k * nslot;
-        const int gi = base + o;
-        return (o < RR && gi < ngr) ? gi : -1;
-    };
     auto line_of = [&](int grp) {  // -1: none
         const int idx = grp * LINES + line;
         if (grp < 0 || idx >= nl) return -1;
@@ -978,6 +982,95 @@ __global__ void __launch_bounds__(1024) k_psf_peak_rows(PsfLineArgs A, int limit
     if (threadIdx.x == 0) A.cand_n[b] = (all || cnt > limit) ? -1 : cnt;
 }
 
+// The row-bound route to the peak (the default). Pass 2 computes row ko of F as
+// X[lo] = sum_x (-1)^x G[x][ko] W^(lo x), so |X[lo]| <= sum_x |G[x][ko]| for every lo: B[ko], that
+// sum squared times 1 + 2^-20, bounds every |F|^2 the kernel computes for the row (the rounding of
+// a line transform and of the sum are ~1e-13 of it), and no row whose bound lies below some
+// computed |F|^2 holds the peak. Round 1 runs the fp64 peak pass over the rows with B >= B_max / 2
+// (a focused PSF's peak row is among them: its coherent sum reaches B); round 2 over the rest with
+// B >= round 1's max M1. Every row that could hold the peak is in one of the rounds, each row's
+// values are the write pass's bits, so the max is the all-rows pass's max exactly. A non-finite or
+// zero B_max (NaN or infinite field, dark pupil) turns the route off: round 1 takes every row.
+// Measured on the example's 1024^2 pupil: 1 of 16384 rows; ~2.5 % with 3 waves of aberration.
+constexpr double kBoundMargin = 1.0 + 0x1p-20;
+constexpr double kBoundTheta = 0.5;
+
+// B per row: one workgroup per 64 rows and batch entry, sixteen waves over the pupil columns,
+// summed in a fixed order
+__global__ void __launch_bounds__(1024) k_psf_rowbound(PsfLineArgs A) {
+    __shared__ double red[16][64];
+    const PsfGeom g = A.g;
+    const int b = blockIdx.y;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int ko = blockIdx.x * 64 + lane;
+    double s = 0.0;
+    if (ko < g.py) {
+        const double2* Gp = A.G + (int64_t)b * g.nx2 * g.py + ko;
+#pragma unroll 4
+        for (int x = w; x < g.nx2; x += 16) {
+            const double2 v = Gp[(int64_t)x * g.py];
+            s += sqrt(fma(v.x, v.x, v.y * v.y));
+        }
+    }
+    red[w][lane] = s;
+    __syncthreads();
+    if (w == 0 && ko < g.py) {
+        double t = red[0][lane];
+        for (int k = 1; k < 16; ++k) t += red[k][lane];
+        A.ubound[(int64_t)b * g.py + ko] = (t * t) * kBoundMargin;
+    }
+}
+
+// B_max and round 1's rows (one workgroup per batch entry)
+__global__ void __launch_bounds__(1024) k_psf_bound_rows1(PsfLineArgs A) {
+    __shared__ double wmx[16];
+    __shared__ int cnt;
+    const int b = blockIdx.x, py = A.g.py;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const double* ub = A.ubound + (int64_t)b * py;
+    double m = 0.0;
+    for (int r = threadIdx.x; r < py; r += blockDim.x) m = dmax_nan(m, ub[r]);
+    for (int off = 32; off > 0; off >>= 1) m = dmax_nan(m, __shfl_down(m, off));
+    if (lane == 0) wmx[w] = m;
+    if (threadIdx.x == 0) cnt = 0;
+    __syncthreads();
+    m = wmx[0];
+    for (int k = 1; k < 16; ++k) m = dmax_nan(m, wmx[k]);
+    const bool on = isfinite(m) && m > 0.0;
+    if (on) {
+        const double thr = m * kBoundTheta;
+        int* cd = A.cand + (int64_t)b * py;
+        for (int r = threadIdx.x; r < py; r += blockDim.x)
+            if (ub[r] >= thr) cd[atomicAdd(&cnt, 1)] = r;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        A.ubmax[b] = on ? m : __builtin_nan("");
+        A.cand_n[b] = on ? cnt : -1;
+    }
+}
+
+// round 2's rows: B below round 1's threshold but not below its max M1 (none when the route is
+// off; a NaN M1 is already the answer)
+__global__ void __launch_bounds__(1024) k_psf_bound_rows2(PsfLineArgs A) {
+    __shared__ int cnt;
+    const int b = blockIdx.x, py = A.g.py;
+    const double M = A.ubmax[b], m1 = A.umax[b];
+    if (threadIdx.x == 0) cnt = 0;
+    __syncthreads();
+    if (M == M) {
+        const double thr = M * kBoundTheta;
+        const double* ub = A.ubound + (int64_t)b * py;
+        int* cd = A.cand + (int64_t)b * py;
+        for (int r = threadIdx.x; r < py; r += blockDim.x) {
+            const double u = ub[r];
+            if (u < thr && u >= m1) cd[atomicAdd(&cnt, 1)] = r;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) A.cand_n[b] = cnt;
+}
+
 // persistent workgroups per pass: the resident count (LDS / threads) x 256 CUs, a multiple of 8
 template <int N, int PAD, typename R>
 static int line_wgs(int ngroups) {
@@ -1167,7 +1260,7 @@ extern "C" {
 int64_t akb_psf_work_bytes(int ny, int nx, int pad, int batch) {
     if (ny <= 0 || nx <= 0 || pad < 1 || batch < 1) return -1;
     const PsfGeom g = psf_geom(ny, nx, pad);
-    if (psf_line_ok(g, pad)) return psf_fast_bytes(g, batch) + 256 + 2 * psf_line_rows_bytes(g, batch);  // G, peaks, rows
+    if (psf_line_ok(g, pad)) return psf_fast_bytes(g, batch) + 256 + 4 * psf_line_rows_bytes(g, batch);  // G, peaks, rows, bounds
     if (psf_fast_ok(g)) return psf_fast_bytes(g, batch);             // H (ey x px)
     PlanEntry e;
     if (get_plan(g.py, g.px, batch, &e) != AKB_OK) return -1;
@@ -1204,6 +1297,8 @@ int akb_psf_f64(const double* opd, const double* amp, int ny, int nx, int pad, i
         la.cand_n = (int*)(tail + 128);
         la.rowmax32 = (float*)(tail + 256);
         la.cand = (int*)(tail + 256 + psf_line_rows_bytes(g, batch));
+        la.ubmax = (double*)(tail + 160);
+        la.ubound = (double*)(tail + 256 + 2 * psf_line_rows_bytes(g, batch));
         if ((st = get_twiddles(g.px, s, &la.Wx))) return st;
         if ((st = get_twiddles(g.py, s, &la.Wy))) return st;
         la.dA = dx * dy;
@@ -1212,11 +1307,23 @@ int akb_psf_f64(const double* opd, const double* amp, int ny, int nx, int pad, i
         la.efield = (double2*)efield_re_im;
         la.imax = d_imax;
         if ((st = psf_line_dispatch<kLinePupil>(g.ny2, pad, la, g.nx2, batch, s))) return st;
-        // the fp32 peak pass pays off on large planes (16384^2: 0.91 -> 0.58 ms with its row
-        // re-run); below 2^24 points the fp64 pass alone is faster (2048^2: 14 us vs 29 us + 11)
+        // the peak (same bits on every route): on planes of 2^24 points and up the row-bound
+        // rounds (16384^2: 46 us of bounds + 2 x 12 us of rounds instead of a 0.91 ms fp64 pass or
+        // the fp32 pass + re-run's 0.58 ms), below it the fp64 pass over every row (2048^2: 13 us,
+        // against ~25 us for the bound route's four short launches). AKB_PSF_PEAK = bound / f32 /
+        // f64 forces a route.
         const char* pk = getenv("AKB_PSF_PEAK");
-        const bool peak32 = pk ? strcmp(pk, "f32") == 0 : (int64_t)g.py * g.px >= (1LL << 24);
-        if (peak32) {
+        const bool peak32 = pk && strcmp(pk, "f32") == 0;
+        const bool bound = pk ? strcmp(pk, "bound") == 0 : (int64_t)g.py * g.px >= (1LL << 24);
+        if (bound) {
+            k_psf_rowbound<<<dim3((g.py + 63) / 64, batch), 1024, 0, s>>>(la);
+            if ((st = launch_status("k_psf_rowbound"))) return st;
+            k_psf_bound_rows1<<<batch, 1024, 0, s>>>(la);
+            if ((st = launch_status("k_psf_bound_rows1"))) return st;
+            if ((st = psf_line_dispatch<kLinePeak>(g.nx2, pad, la, g.py, batch, s))) return st;
+            k_psf_bound_rows2<<<batch, 1024, 0, s>>>(la);
+            if ((st = launch_status("k_psf_bound_rows2"))) return st;
+        } else if (peak32) {
             if ((st = psf_line_dispatch<kLinePeak32>(g.nx2, pad, la, g.py, batch, s))) return st;
             k_psf_peak_rows<<<batch, 1024, 0, s>>>(la, g.py / 4);
             if ((st = launch_status("k_psf_peak_rows"))) return st;

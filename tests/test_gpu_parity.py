@@ -749,8 +749,9 @@ def test_psf_pruned_transform(gpu, ny, nx, pad, win, eff, monkeypatch):
         e = fast[1][0].cpu().numpy()
         assert np.max(np.abs(e - ref[3])) <= 1e-10 * np.max(np.abs(ref[3]))
     if pad in (8, 16):
-        # the fp32 peak pass only picks the rows of the exact fp64 one: identical bits either way
-        for mode in ("f64", "f32"):
+        # the row-bound rounds (default) and the fp32 peak pass only pick the rows of the exact
+        # fp64 one: identical bits on every route
+        for mode in ("f64", "f32", "bound"):
             monkeypatch.setenv("AKB_PSF_PEAK", mode)
             alt = G.psf_stack(o, None, [lam], dx, dy, pad_factor=pad, window="hann" if win else None,
                               workspace=G.PsfWorkspace())
@@ -769,7 +770,7 @@ def test_psf_pruned_transform(gpu, ny, nx, pad, win, eff, monkeypatch):
 @pytest.mark.parametrize("n", [128, 512])
 def test_psf_line_stack_equals_single(gpu, n):
     """The line transforms batched over wavelengths (one launch per pass for the stack; at 512^2 x
-    pad 16 = 8192^2 the fp32 peak route with its per-row re-run) equal one wavelength at a time,
+    pad 16 = 8192^2 the row-bound peak route, per batch entry) equal one wavelength at a time,
     bit for bit, and the oracle at 128^2."""
     from akbraytracing_amd import psf as G
     rng = np.random.default_rng(n)
@@ -814,10 +815,35 @@ def test_psf_line_peak_edges(gpu, case, monkeypatch):
     fin = np.isfinite(ref)
     if fin.any():
         assert np.max(np.abs(got[fin] - ref[fin])) <= 1e-10 * max(1.0, np.max(np.abs(ref[fin])))
-    for mode in ("f64", "f32"):
+    for mode in ("f64", "f32", "bound"):  # bound: a dark or NaN plane turns it off
         monkeypatch.setenv("AKB_PSF_PEAK", mode)
         alt = G.psf_stack(o, a, [13.5e-9], 5e-6, 5e-6, pad_factor=pad)[0][0].cpu().numpy()
         assert np.array_equal(alt, got, equal_nan=True)
+
+
+@pytest.mark.parametrize("n", [128, 256])
+@pytest.mark.parametrize("waves", [0.0, 0.3, 1.0, 3.0])
+def test_psf_line_bound_rounds(gpu, n, waves, monkeypatch):
+    """The row-bound peak (akb_psf.hip k_psf_rowbound): from a flat wavefront (the peak row alone
+    in round 1) to three waves of aberration (peak / max bound ~0.28, so round 2 runs rows under
+    round 1's threshold) - the same bits as the fp64 pass over every row, and the oracle."""
+    from akbraytracing_amd import psf as G
+    import oracle.psf as OP
+    lam = 13.5e-9
+    y, x = np.mgrid[-1:1:n * 1j, -1:1:n * 1j]
+    r2 = x * x + y * y
+    ph = waves * (0.7 * (2 * r2 - 1) + 1.5 * x * y + 0.4 * (3 * r2 - 2) * x + 0.3 * np.sin(7 * x + 3 * y))
+    opd = np.where(r2 <= 1.0, ph * lam, np.nan)
+    o = torch.from_numpy(opd).to(gpu)
+    monkeypatch.setenv("AKB_PSF_PEAK", "bound")  # the default from 4096^2 up
+    got, _, imax = G.psf_stack(o, None, [lam], 5e-6, 5e-6, pad_factor=16)
+    monkeypatch.setenv("AKB_PSF_PEAK", "f64")
+    alt, _, imax64 = G.psf_stack(o, None, [lam], 5e-6, 5e-6, pad_factor=16, workspace=G.PsfWorkspace())
+    assert torch.equal(alt, got) and torch.equal(imax, imax64)
+    if n == 128:
+        amp = np.where(np.isfinite(opd), 1.0, 0.0)
+        ref = OP.psf(opd, amp, lam, 5e-6, 1e-2, 16)[0]
+        assert np.max(np.abs(got[0].cpu().numpy() - ref)) <= 1e-10
 
 
 def test_psf_errors(gpu):
