@@ -69,6 +69,11 @@ def parse():
     # from ~1.0 to ~0.8 ms, scripts/step_timeline.py): the default warm-up covers that
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=30, help="at least 3 with --fuse 2 (fills the pipeline)")
+    # a fresh process's device clock settles over ~0.3 s of load: the driver's 20 steps after 5
+    # warm-up steps measured 0.89 ms per step without a ramp, 0.80 with it (100 / 30: 0.78);
+    # the timed steps are the same either way, and the JSON line reports the ramp
+    p.add_argument("--ramp-ms", type=float, default=300.0,
+                   help="device clock ramp before the warm-up: untimed steps for this long (reported)")
     p.add_argument("--rays", type=float, default=None,
                    help="rays per GPU (default: 1e7 on one GPU, C3; 1.25e7 per rank at N > 1, C4's 1e8 at N = 8)")
     p.add_argument("--systems", type=int, default=8,
@@ -384,6 +389,15 @@ def main():
         else:
             fronts.append(rw.launch_front(overlap=(lambda: back(timed)) if fronts else None, **kw))
 
+    ramp_steps = 0
+    if args.ramp_ms > 0:
+        torch.cuda.synchronize()
+        r0 = time.perf_counter()
+        while (time.perf_counter() - r0) * 1e3 < args.ramp_ms:
+            step(False)
+            ramp_steps += 1
+            if ramp_steps % 8 == 0:
+                torch.cuda.synchronize()
     for _ in range(args.warmup):
         step(False)
     rw.kernel_events = [] if os.environ.get("AKB_BENCH_NO_KEVENTS", "0") == "0" else None
@@ -494,6 +508,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "clock_ramp": {"ms": args.ramp_ms, "untimed_steps": ramp_steps},
         "ms_per_step": el / args.steps * 1e3,
         "higher_is_better": True,
         "scaling": "weak",
