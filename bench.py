@@ -393,11 +393,15 @@ def main():
     if args.ramp_ms > 0:
         torch.cuda.synchronize()
         r0 = time.perf_counter()
-        while (time.perf_counter() - r0) * 1e3 < args.ramp_ms:
-            step(False)
-            ramp_steps += 1
-            if ramp_steps % 8 == 0:
-                torch.cuda.synchronize()
+        while True:  # in chunks of 8 steps, every rank going on while any rank's time is short
+            for _ in range(8):
+                step(False)
+            ramp_steps += 8
+            torch.cuda.synchronize()
+            more = torch.tensor([float((time.perf_counter() - r0) * 1e3 < args.ramp_ms)],
+                                dtype=torch.float64, device=dev)
+            if float(comm.allreduce_max(more).item()) == 0.0:
+                break
     for _ in range(args.warmup):
         step(False)
     rw.kernel_events = [] if os.environ.get("AKB_BENCH_NO_KEVENTS", "0") == "0" else None
