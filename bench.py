@@ -40,6 +40,7 @@ faithful PSF chain (griddata + plane correction + psf_calc, faithful_psf_chain_m
 Huygens stage of configs[1] (huygens_pairs_per_s).
 """
 import argparse
+import ctypes
 import glob
 import json
 import math
@@ -273,6 +274,95 @@ def huygens_rate(out):
     return res
 
 
+def stage_api(rw, geom, dev, reps=5):
+    """The drop-in stage API (SURVEY.md §8(d)'s HBM-bound mode): the reference's per-mirror calls
+    on device-resident (3, N) rows of the bench's grid - mirr_ray_intersection, the segment norm,
+    norm_vector, reflect_ray per mirror, then plane_ray_intersection (AKB_raytrace_20250312.py:
+    2881-2905) - through the C ABI, each kernel timed over `reps` back-to-back calls with HIP events
+    on the current stream. Algorithmic bytes per ray: the rows a call reads and writes."""
+    import torch
+    from akbraytracing_amd import _lib
+    from akbraytracing_amd import device as D
+    L = _lib.lib()
+    n = rw.n * rw.n
+    th, tv = rw.tan_h, rw.tan_v
+    ih = torch.arange(n, device=dev) % rw.n
+    iv = torch.arange(n, device=dev) // rw.n
+    raw = torch.stack([torch.ones(n, dtype=torch.float64, device=dev), th[ih], tv[iv]]).contiguous()
+    del ih, iv
+    flags = torch.zeros(1, dtype=torch.int32, device=dev)
+    sh = D.stream_handle()
+    P = D.ptr
+
+    def cf(c):
+        return (ctypes.c_double * 10)(*[float(x) for x in c])
+
+    def plane4(p):
+        return (ctypes.c_double * 4)(*[float(x) for x in p])
+
+    def timed(fn):
+        fn()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(reps):
+            fn()
+        b.record()
+        b.synchronize()
+        return a.elapsed_time(b) / reps
+
+    res = {}
+    d = torch.empty_like(raw)
+    res["normalize_vector"] = (timed(lambda: _lib.check(L.akb_normalize_f64(P(raw), n, 1, n, P(d), n, P(flags), sh))), 48)
+    o = torch.zeros_like(raw)  # the point source, as (3, N) rows
+    hit = torch.empty_like(raw)
+    nrm = torch.empty_like(raw)
+    d2 = torch.empty_like(raw)
+    seg = torch.empty(n, dtype=torch.float64, device=dev)
+    per = {"mirr_ray_intersection": [], "segment_length": [], "norm_vector": [], "reflect_ray": []}
+    torch.cuda.synchronize()
+    c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    chain_ms = 0.0
+    for m in geom.mirrors:
+        q = cf(m.coeffs)
+        neg = int(bool(m.negative))
+        calls = [
+            ("mirr_ray_intersection", lambda: _lib.check(L.akb_isect_f64(q, P(d), n, 1, P(o), n, 1, neg, n, P(hit), n, P(flags), sh))),
+            ("segment_length", lambda: _lib.check(L.akb_seglen_f64(P(o), n, 1, P(hit), n, 1, n, P(seg), sh))),
+            ("norm_vector", lambda: _lib.check(L.akb_normal_f64(q, P(hit), n, 1, n, P(nrm), n, 1, P(flags), sh))),
+            ("reflect_ray", lambda: _lib.check(L.akb_reflect_f64(P(d), n, 1, P(nrm), n, 1, n, P(d2), n, 1, P(flags), sh))),
+        ]
+        c0.record()
+        for _, fn in calls:  # the mirror once, in the reference's order (the chain's own time)
+            fn()
+        c1.record()
+        c1.synchronize()
+        chain_ms += c0.elapsed_time(c1)
+        for name, fn in calls:
+            per[name].append(timed(fn))
+        d, d2 = d2, d
+        o, hit = hit, o
+    pl = plane4(geom.det2 or geom.det1)
+    res["plane_ray_intersection"] = (timed(lambda: _lib.check(L.akb_plane_isect_f64(pl, P(d), n, 1, P(o), n, 1, n, P(hit), n, sh))), 72)
+    nbytes = {"mirr_ray_intersection": 72, "segment_length": 56, "norm_vector": 48, "reflect_ray": 72}
+    for k, v in per.items():
+        res[k] = (sum(v) / len(v), nbytes[k])
+    out = {}
+    for k, (ms, b) in res.items():
+        gbs = b * n / (ms * 1e-3) / 1e9
+        out[k] = {"ms": ms, "bytes_per_ray": b, "gbs": gbs, "frac_of_hbm": gbs / 8000.0}
+    k = len(geom.mirrors)
+    out["chain"] = {"ms": chain_ms, "rays": n, "mirrors": k,
+                    "intersections_per_s": k * n / (chain_ms * 1e-3),
+                    "bytes_per_intersection": 248,
+                    "gbs": 248 * k * n / (chain_ms * 1e-3) / 1e9,
+                    "what": "per mirror: intersection, segment norm, normal, reflection as separate calls"}
+    out["rays"] = n
+    # the device's streaming ceiling for the same traffic: a (3, N) float64 copy (48 B per ray)
+    cms = timed(lambda: d2.copy_(d))
+    out["copy_3xN_f64"] = {"ms": cms, "gbs": 48 * n / (cms * 1e-3) / 1e9}
+    return out
+
+
 def _lib_hash():
     from akbraytracing_amd import _lib
     return _lib.sources_hash()
@@ -488,6 +578,10 @@ def main():
             ft.append((time.perf_counter() - t1) * 1e3)
         faithful_dist_ms = sorted(ft)[1]
 
+    stage = None
+    if world == 1 and not args.no_extras:
+        stage = stage_api(rw, geom, dev)
+
     if rank != 0:
         return
     k_ms = [a.elapsed_time(b) for a, b in rw.kernel_events] if rw.kernel_events else [float('nan')]
@@ -605,6 +699,8 @@ def main():
         out["faithful_wave_maps_psf_ms"] = maps_ms
         if faithful_steps is not None:
             out["faithful_step"] = faithful_steps
+        if stage is not None:
+            out["stage_api"] = stage
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, gdict)
     print(json.dumps(out), flush=True)
