@@ -394,7 +394,12 @@ int akb_scale_field_f64(const double* u_re_im, const double* ds, int64_t m, doub
  *   py = ny' * pad, px = nx' * pad with ny' = ny + ny%2 (ensure_even_size)
  *   psf: (batch, py, px) normalised intensity; efield_re_im: (batch, py, px) complex or NULL
  *   d_imax: device array of `batch` peak intensities before normalisation
- *   work: device scratch of akb_psf_work_bytes(...) (pupil field + rocFFT work area) */
+ *   work: device scratch of akb_psf_work_bytes(...): for power-of-two pupils at pad 8 / 16 the
+ *   line transforms' column-pass plane G (batch x nx' x py complex) plus per-row peak bookkeeping
+ *   (row bounds, candidate rows: 16 bytes per psf row and batch entry); for other power-of-two
+ *   pupils the pruned transform's plane; otherwise the padded field + rocFFT's work area.
+ *   The peak max |F|^2 is exact on every route (AKB_PSF_PEAK = bound / f32 / f64 picks how its
+ *   rows are searched; same bits). */
 int64_t akb_psf_work_bytes(int ny, int nx, int pad, int batch);
 int akb_psf_f64(const double* opd, const double* amp, int ny, int nx, int pad, int batch,
                 const double* lambdas, double dx, double dy, const double* hann_wy,
