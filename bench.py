@@ -509,7 +509,7 @@ def main():
     while fronts:  # the last front's back half (outside the timed region, like the first one's)
         back(False)
     torch.cuda.synchronize()
-    psf_alone_ms = None
+    psf_alone_ms = psf_device_ms = None
     if rank == 0:  # the PSF's own wall time, nothing beside it (the last pupil: rw.pupil is collective)
         opd, pitch = state["pupil"]
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -519,6 +519,19 @@ def main():
         b.record()
         b.synchronize()
         psf_alone_ms = a.elapsed_time(b) / 10
+        # the same ten calls with the device held back by a spin kernel while the host queues them:
+        # the device's own time per transform (measured: 32.8 vs 33.5 us wall at 2048^2 - the host
+        # keeps ahead of the three launches per call)
+        if hasattr(torch.cuda, "_sleep"):
+            torch.cuda.synchronize()
+            torch.cuda._sleep(20_000_000)
+            a2, b2 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a2.record()
+            for _ in range(10):
+                psf_stack(opd, None, my_lams, None, pitch=pitch, pad_factor=args.pad, out=psf_out.get("psf"))
+            b2.record()
+            b2.synchronize()
+            psf_device_ms = a2.elapsed_time(b2) / 10
     t = torch.tensor([el], dtype=torch.float64, device=dev)
     t = comm.allreduce_max(t)
     el = float(t.item())
@@ -633,6 +646,7 @@ def main():
         "host_issue_ms_per_step": sorted(host_ms)[len(host_ms) // 2],
         "psf_ms": psf_ms,
         "psf_alone_ms": psf_alone_ms,
+        "psf_device_ms": psf_device_ms,
         # the PSF's compulsory HBM traffic is its output (the pupil is 128 KB): intensity planes
         "psf_alone_output_gbs": (len(my_lams) * (args.pupil * args.pad) ** 2 * 8 / (psf_alone_ms * 1e-3) / 1e9
                                  if psf_alone_ms else None),
