@@ -1154,8 +1154,24 @@ __device__ __forceinline__ bool axis_range(const double* a, int m, double inv_st
     return true;
 }
 
+// whether axis a (m points, ascending) is a linspace: strictly increasing and every point within
+// 1e-6 of an index of a0 + i * step (axis_range's widening); one value per thread of the workgroup
+__device__ __forceinline__ bool axis_uniform_part(const double* a, int m, int i) {
+    if (i >= m || m < 2) return true;
+    const double step = (a[m - 1] - a[0]) / (m - 1);
+    if (!(step > 0)) return false;
+    if (i > 0 && !(a[i] > a[i - 1])) return false;
+    return fabs((a[i] - a[0]) / step - i) <= 1e-7;
+}
+
 __global__ void __launch_bounds__(kBlock) k_gd_claim_cells(Grid g, Targets t, int* owner) {
     const int64_t nc = ncells(g);
+    // the index-box estimate below needs evenly spaced axes (np.linspace, the driver's); any other
+    // ascending axis takes the exact binary search (lower_idx) of the per-triangle claim
+    bool ok = true;
+    for (int i = threadIdx.x; i < t.mx || i < t.my; i += blockDim.x)
+        ok = ok && axis_uniform_part(t.gx, t.mx, i) && axis_uniform_part(t.gy, t.my, i);
+    const bool uniform = __syncthreads_and(ok) != 0;
     const double inv_dx = inv_step(t.gx, t.mx), inv_dy = inv_step(t.gy, t.my);
     for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < nc; c += (int64_t)gridDim.x * blockDim.x) {
         const int iv = (int)(c / (g.nh - 1)), ih = (int)(c - (int64_t)iv * (g.nh - 1));
@@ -1166,8 +1182,16 @@ __global__ void __launch_bounds__(kBlock) k_gd_claim_cells(Grid g, Targets t, in
         const double ylo = fmin(fmin(ya, yb), fmin(yc, yd)), yhi = fmax(fmax(ya, yb), fmax(yc, yd));
         const double padx = (xhi - xlo) * 1e-9, pady = (yhi - ylo) * 1e-9;
         int c0, c1, r0, r1;
-        if (!axis_range(t.gx, t.mx, inv_dx, xlo - padx, xhi + padx, c0, c1)) continue;
-        if (!axis_range(t.gy, t.my, inv_dy, ylo - pady, yhi + pady, r0, r1)) continue;
+        if (uniform) {
+            if (!axis_range(t.gx, t.mx, inv_dx, xlo - padx, xhi + padx, c0, c1)) continue;
+            if (!axis_range(t.gy, t.my, inv_dy, ylo - pady, yhi + pady, r0, r1)) continue;
+        } else {
+            c0 = lower_idx(t.gx, t.mx, xlo - padx);
+            c1 = lower_idx(t.gx, t.mx, xhi + padx);
+            r0 = lower_idx(t.gy, t.my, ylo - pady);
+            r1 = lower_idx(t.gy, t.my, yhi + pady);
+            if (c0 >= c1 || r0 >= r1) continue;
+        }
         // the exact box within the estimate: targets with lo <= coordinate < hi (as lower_idx gives)
         while (c0 < c1 && t.gx[c0] < xlo - padx) ++c0;
         while (c1 > c0 && t.gx[c1 - 1] >= xhi + padx) --c1;

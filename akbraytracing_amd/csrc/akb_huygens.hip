@@ -86,7 +86,9 @@ __device__ __forceinline__ bool sincos_phase_fast(double x, double& sn, double& 
     // the quadrant's signs as sign-bit flips of the high words (no compares or selects)
     sn = __hiloint2double(__double2hiint(a) ^ (int)((k << 30) & 0x80000000u), __double2loint(a));
     cs = __hiloint2double(__double2hiint(b) ^ (int)(((k + 1u) << 30) & 0x80000000u), __double2loint(b));
-    return fabs(q) < 0x1p40;
+    // a NaN phase stays on the fast path (its sums are NaN whatever runs them); only a phase
+    // outside the Cody-Waite range sends its target to the fix-up loop
+    return !(fabs(q) >= 0x1p40);
 }
 
 // one pair's contribution: the distance, 1 / (2 r), the phase -k r and its sincos, the complex

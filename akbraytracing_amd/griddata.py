@@ -14,9 +14,8 @@ Chebyshev semi-iteration (a register-resident strip kernel, two sweeps per launc
 changing, and evaluates the patches on the device. Agreement with scipy is to rounding on the
 reference's 65 x 65 run (tests/test_gpu_parity.py) and within 1e-6 of the range at 1001^2 /
 3163^2 (tests/test_fullsize_gpu.py), not bit for bit: qhull's near-cocircular picks and scipy's
-Gauss-Seidel iterates are not reproduced - both iterations converge to the same fixed point,
-scipy's stopping at a largest relative change of 1e-6, ours at GRADIENT_TOL (within ~1e-8 of the
-map's range of that point).
+Gauss-Seidel iterates are not reproduced - both iterations converge to the same fixed point and
+both stop at a largest relative change of 1e-6 (GRADIENT_TOL).
 """
 import numpy as np
 import torch
@@ -27,12 +26,11 @@ from . import device as D
 _F_NONCONVEX, _F_NOT_DELAUNAY, _F_POCKET, _F_POS, _F_NEG, _F_NONFINITE = 1, 2, 4, 8, 16, 32
 
 # Stopping tolerance of the gradient iteration: the largest relative change of a Jacobi step
-# (scipy's measure; scipy stops at 1e-6). Its iterates and ours differ, so neither point is the
-# other's: what parity needs is the interpolated values near the common fixed point. At 1e-4 the
-# gridded values are within ~1e-8 of the map's range of the fixed point (1001^2 hits onto the
-# 128^2 pupil: 1.2e-8 of the Wave2 range at the sweep where the change falls below 1e-4, DESIGN.md
-# §7.1), 100x inside the 1e-6 parity bar (tests/test_fullsize_gpu.py) - and ~6 sweeps fewer.
-GRADIENT_TOL = 1e-4
+# (scipy's measure) below scipy's own tolerance, 1e-6. Its iterates and ours differ, so neither
+# point is the other's: what parity needs is the interpolated values near the common fixed point,
+# and stopping where scipy stops keeps that distance at scipy's own on every lattice (coarse grids
+# included; tests/test_gpu_parity.py::test_griddata_default_tol_margin).
+GRADIENT_TOL = 1e-6
 
 
 def _dev(a, dev, dtype=D.F64):
@@ -45,7 +43,11 @@ class CubicGrid:
     """The triangulation of an n_v x n_h grid of points (x, y: (n_v * n_h,) row-major), reused for
     any number of value sets and target grids."""
 
-    def __init__(self, x, y, n_v, n_h, delaunay_tol=1e-10):
+    def __init__(self, x, y, n_v, n_h, delaunay_tol=1e-10, diag_override=None):
+        """diag_override: (cells, splits) - flat cell indices iv * (n_h - 1) + ih and the split each
+        takes (0: p00-p11, 1: p01-p10) in place of the exact in-circle one, e.g. qhull's own picks in
+        near-cocircular cells (tests/golden/akb_qhull_full.npz); the triangulation then is that one,
+        and the sweeps, claims and patches follow it."""
         L = _lib.lib()
         self.dev = D.device()
         self.nv, self.nh = int(n_v), int(n_h)
@@ -65,6 +67,13 @@ class CubicGrid:
         _lib.check(L.akb_gd_cells_f64(D.ptr(self.x), D.ptr(self.y), self.nv, self.nh, D.ptr(self.diag),
                                       float(delaunay_tol), D.ptr(flags), D.ptr(ringbuf[:self.L]),
                                       D.ptr(ringbuf[self.L:2 * self.L]), s))
+        if diag_override is not None:
+            cells, splits = (np.asarray(a).reshape(-1) for a in diag_override)
+            if cells.size:
+                if cells.min() < 0 or cells.max() >= self.diag.numel() or not np.isin(splits, (0, 1)).all():
+                    raise ValueError("diag_override: cell index out of range or a split other than 0 / 1")
+                self.diag[torch.from_numpy(cells.astype(np.int64)).to(self.dev)] = \
+                    torch.from_numpy(splits.astype(np.uint8)).to(self.dev)
         rb = ringbuf.cpu().numpy()
         f = int(rb[2 * self.L:].view(np.int32)[0])
         if f & _F_NONFINITE:
@@ -99,15 +108,19 @@ class CubicGrid:
                                           self.npock, D.ptr(self.ptri), D.ptr(self.pnbr), D.ptr(self.edge_tri),
                                           float(delaunay_tol), D.ptr(self._status), s))
         self._checked = False
+        self._bad = False
         self.sweeps = 0
 
     def _check_status(self, word=None):
         """Raise if the pocket check flagged the triangulation (word: its value, already on the host)."""
         if self._checked:
+            if self._bad:  # a flagged triangulation stays refused on every later call
+                raise _lib.AKBError("griddata: the grid is too distorted for the structured Delaunay triangulation")
             return
         f = int(self._status.item()) if word is None else int(word)
         self._checked = True
-        if f & (_F_NOT_DELAUNAY | _F_POCKET):
+        self._bad = bool(f & (_F_NOT_DELAUNAY | _F_POCKET))
+        if self._bad:
             raise _lib.AKBError("griddata: the grid is too distorted for the structured Delaunay triangulation")
 
     def _tri_args(self):
@@ -130,6 +143,8 @@ class CubicGrid:
           "sweep"            plain sweeps (line Gauss-Seidel in the LDS strips, Jacobi with AKB_GD_GS=0)"""
         import os
         L = _lib.lib()
+        if self._checked:
+            self._check_status()  # re-raises for a triangulation the pocket check flagged
         method = method or os.environ.get("AKB_GD_ITER", "chebyshev")
         if method not in ("chebyshev", "chebyshev-strip", "sweep"):
             raise ValueError(f"unknown gradient iteration {method!r}")

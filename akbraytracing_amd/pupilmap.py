@@ -143,18 +143,19 @@ def match_legendre_multi(data, order):
     return fits.cpu().numpy(), c.cpu().numpy(), [tuple(o) for o in orders]
 
 
-def wave_maps(detcenter2, dist_err2, wave2, ray_num_H, ray_num_V, grid_num_H=None, grid_num_V=None):
+def wave_maps(detcenter2, dist_err2, wave2, ray_num_H, ray_num_V, grid_num_H=None, grid_num_V=None, **grid_kw):
     """The driver's gridding step (AKB_raytrace_20250312.py:3653-3696) on the device:
     grid_H, grid_V = meshgrid(linspace(min, max) of the hits' y / z), matrixDistError2 and
     matrixWave2 by cubic griddata (one triangulation for both), matrixWave2 -= nanmean, then both
     plane-corrected. detcenter2 (3, n), dist_err2 / wave2 (n,) in ray order (n = V * H).
     grid_num_H / grid_num_V: the output grid's size when it is not the ray grid's (the driver uses
     ray_num for both; bench.py grids 1e7 hits onto its 128 x 128 pupil).
+    grid_kw: passed to CubicGrid (diag_override).
     Returns a dict of device tensors (the grids as numpy)."""
     from .griddata import CubicGrid
     d2 = _as_dev(detcenter2)
     y, z = d2[1].contiguous(), d2[2].contiguous()
-    cg = CubicGrid(y, z, int(ray_num_V), int(ray_num_H))
+    cg = CubicGrid(y, z, int(ray_num_V), int(ray_num_H), **grid_kw)
     ext = cg.extent  # min / max of the hits' y and z (on the lattice's boundary ring, exactly)
     gx = np.linspace(ext[0], ext[1], int(grid_num_H or ray_num_H))
     gy = np.linspace(ext[2], ext[3], int(grid_num_V or ray_num_V))
@@ -169,7 +170,7 @@ def wave_maps(detcenter2, dist_err2, wave2, ray_num_H, ray_num_V, grid_num_H=Non
                 matrixWave2_Corrected=w_c, matrixDistError2_Corrected=d_c, sweeps=cg.sweeps)
 
 
-def wave_pupil(detcenter2, wave2, ray_num_H, ray_num_V, grid_num_H=None, grid_num_V=None):
+def wave_pupil(detcenter2, wave2, ray_num_H, ray_num_V, grid_num_H=None, grid_num_V=None, **grid_kw):
     """The PSF's half of the driver's gridding step (AKB_raytrace_20250312.py:3653-3696): grid,
     griddata(cubic) of Wave2, minus its nanmean, plane-corrected - matrixWave2_Corrected, the map
     psf_calc transforms (:3698-3700). The same arithmetic as wave_maps' Wave2 (one value set on the
@@ -182,7 +183,7 @@ def wave_pupil(detcenter2, wave2, ray_num_H, ray_num_V, grid_num_H=None, grid_nu
     else:
         d2 = _as_dev(detcenter2)
         y, z = d2[1].contiguous(), d2[2].contiguous()
-    cg = CubicGrid(y, z, int(ray_num_V), int(ray_num_H))
+    cg = CubicGrid(y, z, int(ray_num_V), int(ray_num_H), **grid_kw)
     ext = cg.extent
     gx = np.linspace(ext[0], ext[1], int(grid_num_H or ray_num_H))
     gy = np.linspace(ext[2], ext[3], int(grid_num_V or ray_num_V))

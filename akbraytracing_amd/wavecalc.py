@@ -52,10 +52,13 @@ def propagate(tx, ty, tz, sx, sy, sz, u_ds, k, stream=None, work=None, splits=0)
     out = torch.empty(n, dtype=torch.complex128, device=dev)
     need = int(L.akb_huygens_work_bytes(n, m, int(splits)))
     if need > 0 and (work is None or work.numel() * 8 < need):
-        cache = _WORK.__dict__.setdefault("by_device", {})
-        work = cache.get(dev)
+        # keyed by (device, stream): calls on two streams of one thread may overlap on the device,
+        # so they must not share the split partials
+        cache = _WORK.__dict__.setdefault("by_stream", {})
+        key = (dev, D.stream_handle(stream).value)
+        work = cache.get(key)
         if work is None or work.numel() * 8 < need:
-            work = cache[dev] = torch.empty(need // 8 + 1, dtype=D.F64, device=dev)
+            work = cache[key] = torch.empty(need // 8 + 1, dtype=D.F64, device=dev)
     ur = torch.view_as_real(u_ds)
     _lib.check(L.akb_huygens_f64(D.ptr(tx), D.ptr(ty), D.ptr(tz), n, D.ptr(sx), D.ptr(sy), D.ptr(sz), D.ptr(ur), m,
                                  float(k), D.ptr(torch.view_as_real(out)), int(splits),

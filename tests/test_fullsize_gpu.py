@@ -11,8 +11,10 @@ detector hits within 64 ulp of their row scale (the per-ray OCML arctan of the t
 §3); DistError2 and Wave2 within 1e-4 nm; the gridded and plane-corrected maps within 1e-6 of their
 range, with the same NaN mask, except next to the near-cocircular cells where qhull's roundoff
 model (on coordinates ~2 cm from the origin) picked the other diagonal than the exact in-circle
-test - there scipy's answer is itself an artefact of that pick and the bar is 1e-2 of the range
+test - there scipy's answer is itself an artefact of that pick and the bar is 3e-3 of the range
 (2 % of the targets at 1001^2, 5.5 % at 3163^2; the fixture marks them, make_golden_raywave_full.py:qhull_ambiguity).
+With qhull's own picks imposed (akb_qhull_full.npz) every target is within 1e-6 of the range and the
+PSF within 1e-6 of its peak; end to end with the exact picks the PSF is within 1e-6 too.
 """
 import numpy as np
 import pytest
@@ -36,11 +38,12 @@ def _run(n):
     return rw, rw.run(full=True)
 
 
-def _map_check(got, want, amb, what, bar=1e-6):
+def _map_check(got, want, amb, what, bar=1e-6, amb_bar=3e-3):
     """`bar` of the range wherever qhull's triangulation is the exact Delaunay one around the
     target; at targets near a near-cocircular cell qhull split the other way (amb) scipy's own answer
-    depends on that roundoff-driven pick, so those are held to 1e-2 of the range (and must stay a
-    small minority)."""
+    depends on that roundoff-driven pick, so those are held to amb_bar of the range - the measured
+    deviation (2.6e-3 at 1001^2, 2.3e-4 at 3163^2) - and must stay a small minority.
+    test_faithful_pupil_on_qhull_triangulation imposes qhull's picks and holds every target to `bar`."""
     got = got.cpu().numpy() if isinstance(got, torch.Tensor) else got
     assert np.array_equal(np.isnan(got), np.isnan(want)), what
     rng = np.nanmax(want) - np.nanmin(want)
@@ -49,7 +52,7 @@ def _map_check(got, want, amb, what, bar=1e-6):
     print(f"{what}: max |diff| {err:.3e} = {err / rng:.2e} of the range {rng:.4g}; at the {int(amb.sum())} "
           f"targets near qhull's other diagonals {err_amb / rng:.2e}")
     assert err <= bar * rng, what
-    assert err_amb <= 1e-2 * rng, what
+    assert err_amb <= amb_bar * rng, what
 
 
 @pytest.mark.parametrize("n", [1001, pytest.param(3163, marks=pytest.mark.slow)])
@@ -102,3 +105,116 @@ def test_faithful_pupil_full_size_vs_reference(gpu, n):
     # range at 1e-2 of the targets) move the whole corrected map by ~1e-6 of the range
     _map_check(r["matrixWave2_Corrected"], f[f"n{n}_map_wave_c"], amb, "matrixWave2_Corrected", bar=1e-5)
     _map_check(r["matrixDistError2_Corrected"], f[f"n{n}_map_dist_c"], amb, "matrixDistError2_Corrected", bar=1e-5)
+
+
+def _driver_grids(gx, gy):
+    """grid_H, grid_V as the driver hands them to psf_calc: meshgrid, then minus their means (:3698)."""
+    GH, GV = np.meshgrid(gx, gy)
+    return GH - np.mean(GH), GV - np.mean(GV)
+
+
+def _psf_crop(r, f, n):
+    iy0, iy1, ix0, ix1 = (int(v) for v in f[f"n{n}_psf_win"])
+    return r["psf"][iy0:iy1, ix0:ix1].cpu().numpy()
+
+
+@pytest.mark.parametrize("n", [1001, 3163])
+def test_psf_calc_full_size_on_reference_map(gpu, n):
+    """The PSF stage at full size: the device psf_calc on the reference's own plane-corrected 128^2 map
+    of its n^2 run against the reference's own psf_calc of that map (akb_psf_full.npz): rotation
+    estimate exact, rotated map to 1e-12 of its range, the trimmed PSF to 1e-10 of the peak."""
+    from akbraytracing_amd.psfcalc import psf_calc
+    full = golden("akb_raywave_full.npz")
+    f = golden("akb_psf_full.npz")
+    GH, GV = _driver_grids(full[f"n{n}_gx"], full[f"n{n}_gy"])
+    r = psf_calc(full[f"n{n}_map_wave_c"], GH, GV, 1e-2)
+    assert r["rot"] == f[f"n{n}_rot"]
+    rot = r["rotated"].cpu().numpy()
+    want = f[f"n{n}_rotated"]
+    assert np.array_equal(np.isnan(rot), np.isnan(want))
+    assert np.nanmax(np.abs(rot - want)) <= 1e-12 * (np.nanmax(want) - np.nanmin(want))
+    assert np.array_equal(r["x_im"], f[f"n{n}_x_im"]) and np.array_equal(r["y_im"], f[f"n{n}_y_im"])
+    got = _psf_crop(r, f, n)
+    assert r["psf_trimmed"].shape == got.shape == f[f"n{n}_psf_crop"].shape
+    assert np.max(np.abs(got - f[f"n{n}_psf_crop"])) <= 1e-10
+    P = r["psf"].cpu().numpy()
+    st = f[f"n{n}_psf_stats"]
+    assert abs(P.sum() - st[0]) <= 1e-10 * st[0]
+    assert tuple(np.unravel_index(np.argmax(P), P.shape)) == (int(st[1]), int(st[2]))
+
+
+def _qhull_override(n):
+    q = golden("akb_qhull_full.npz")
+    cells, qd = q[f"n{n}_flip_cells"], q[f"n{n}_flip_qd"]
+    keep = qd >= 0
+    return (cells[keep], qd[keep]), cells[~keep]
+
+
+def _near_cells(cells, n, gx, gy, hits_y, hits_z, radius=3):
+    """(128, 128) mask of targets whose lattice cell lies within `radius` cells of one of `cells`
+    (located by the nearest hit of each target: the lattice is smooth, so its index is the cell's)."""
+    mask = np.zeros((gy.size, gx.size), bool)
+    if cells.size == 0:
+        return mask
+    iv, ih = np.divmod(cells, n - 1)
+    Y, Z = hits_y.reshape(n, n), hits_z.reshape(n, n)
+    for a, b in zip(iv, ih):
+        y0, y1 = Y[max(a - radius, 0):a + radius + 2, max(b - radius, 0):b + radius + 2].min(), \
+            Y[max(a - radius, 0):a + radius + 2, max(b - radius, 0):b + radius + 2].max()
+        z0, z1 = Z[max(a - radius, 0):a + radius + 2, max(b - radius, 0):b + radius + 2].min(), \
+            Z[max(a - radius, 0):a + radius + 2, max(b - radius, 0):b + radius + 2].max()
+        mask |= (gx[None, :] >= y0) & (gx[None, :] <= y1) & (gy[:, None] >= z0) & (gy[:, None] <= z1)
+    return mask
+
+
+@pytest.mark.parametrize("n", [1001, pytest.param(3163, marks=pytest.mark.slow)])
+def test_faithful_pupil_on_qhull_triangulation(gpu, n):
+    """The whole gap between the device's gridding and scipy's at full size is qhull's near-cocircular
+    picks: with qhull's own diagonals imposed on the device's structured triangulation
+    (akb_qhull_full.npz), the device's gridded maps equal the reference's to 1e-6 of their range at
+    every target (only targets next to a cell qhull did not split along a diagonal at all are left
+    out), the plane-corrected Wave2 map too, and the PSF the device forms from that map equals the
+    reference's PSF to the north star's 1e-6 of its peak."""
+    from akbraytracing_amd import pupilmap as PM
+    from akbraytracing_amd.psfcalc import psf_calc
+    f = golden("akb_raywave_full.npz")
+    fp = golden("akb_psf_full.npz")
+    _, out = _run(n)
+    over, odd = _qhull_override(n)
+    gx, gy = f[f"n{n}_gx"], f[f"n{n}_gy"]
+    det2 = out["detcenter2"]
+    skip = _near_cells(odd, n, gx, gy, det2[1].cpu().numpy(), det2[2].cpu().numpy())
+    print(f"qhull picks imposed: {over[0].size}; cells split otherwise: {odd.size}; targets skipped: {int(skip.sum())}")
+    assert skip.mean() <= 0.01
+    r = PM.wave_maps(det2, out["dist_err2"], out["wave2"], n, n, grid_num_H=128, grid_num_V=128, diag_override=over)
+    _map_check(r["matrixWave2"], f[f"n{n}_map_wave"], skip, "matrixWave2 (qhull's triangulation)")
+    _map_check(r["matrixDistError2"], f[f"n{n}_map_dist"], skip, "matrixDistError2 (qhull's triangulation)")
+    if not skip.any():
+        _map_check(r["matrixWave2_Corrected"], f[f"n{n}_map_wave_c"], skip, "matrixWave2_Corrected (qhull's)")
+        GH, GV = _driver_grids(r["grid_H"][0], r["grid_V"][:, 0])
+        p = psf_calc(r["matrixWave2_Corrected"], GH, GV, 1e-2)
+        got, want = _psf_crop(p, fp, n), fp[f"n{n}_psf_crop"]
+        d = float(np.max(np.abs(got - want)))
+        print(f"PSF on qhull's triangulation: max |dI| / Imax = {d:.3e}")
+        assert d <= 1e-6
+
+
+@pytest.mark.parametrize("n", [1001, pytest.param(3163, marks=pytest.mark.slow)])
+def test_faithful_psf_end_to_end_vs_reference(gpu, n):
+    """End to end at the bench's sizes: the device's own trace -> griddata(cubic) -> nanmean removal ->
+    plane correction -> psf_calc, against the reference's PSF of its own run (akb_psf_full.npz). The
+    device takes the exact in-circle diagonal where qhull's roundoff took the other one
+    (test_faithful_pupil_on_qhull_triangulation shows that is the whole gap); the deviation that
+    leaves in the PSF is measured here and held to the bar DESIGN.md §3 states."""
+    from akbraytracing_amd import pupilmap as PM
+    from akbraytracing_amd.psfcalc import psf_calc
+    fp = golden("akb_psf_full.npz")
+    _, out = _run(n)
+    m, gh, gv, _ = PM.wave_pupil(out["detcenter2"], out["wave2"], n, n, grid_num_H=128, grid_num_V=128)
+    GH, GV = _driver_grids(gh[0], gv[:, 0])
+    p = psf_calc(m, GH, GV, 1e-2)
+    assert p["rot"] == fp[f"n{n}_rot"]
+    got, want = _psf_crop(p, fp, n), fp[f"n{n}_psf_crop"]
+    d = float(np.max(np.abs(got - want)))
+    print(f"n={n}: end-to-end PSF max |dI| / Imax = {d:.3e}")
+    assert d <= 1e-6  # the north star's PSF bar (measured 3.4e-7 at 1001^2, 2.8e-7 at 3163^2)

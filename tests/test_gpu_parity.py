@@ -106,16 +106,24 @@ def test_torch_inputs_stay_on_device(gpu):
     assert np.array_equal(out.cpu().numpy(), d["c00_mirr_ray_intersection_out"])
 
 
-def test_ellipse_config1(gpu):
+@pytest.mark.parametrize("fixture", ["ellipse_33.npz", "ellipse_317.npz"])
+def test_ellipse_config1(gpu, fixture):
+    """BASELINE configs[0] (C1): EllipseRaytrace3D's __main__ ellipse - calc_reflect and the three
+    PlanePoints planes (position, position -+ delta, EllipseRaytrace3D.py:241-262) - bit for bit vs
+    the reference's own run, at 33^2 and at C1's own 317^2 (1.0e5 rays)."""
     from akbraytracing_amd import primitives as P
-    d = golden("ellipse_33.npz")
+    d = golden(fixture)
     src = np.zeros_like(d["dir"])
     pts = P.mirr_ray_intersection(d["coeffs"], d["dir"], src)
-    refl = P.reflect_ray(d["dir"], P.norm_vector(d["coeffs"], pts))
+    nrm = P.norm_vector(d["coeffs"], pts)
+    refl = P.reflect_ray(d["dir"], nrm)
     assert np.array_equal(pts, d["points"]) and np.array_equal(refl, d["reflect"])
-    c = np.zeros(10)
-    c[6], c[9] = 1.0, -float(d["plane_pos"])
-    assert np.array_equal(P.plane_ray_intersection(c, refl, pts), d["det0"])
+    assert np.array_equal(nrm, d["normal"])
+    pos, delta = float(d["plane_pos"]), float(d["plane_delta"])
+    for key, c9 in (("det0", -pos), ("det1", -pos + delta), ("det2", -pos - delta)):
+        c = np.zeros(10)
+        c[6], c[9] = 1.0, c9
+        assert np.array_equal(P.plane_ray_intersection(c, refl, pts), d[key]), key
 
 
 def test_rotations_match_reference_blas_order(gpu):
@@ -1110,6 +1118,81 @@ def test_griddata_cell_claim_equals_triangle_claim(gpu, monkeypatch, nv, nh, m):
     assert np.array_equal(got, want, equal_nan=True)
 
 
+@pytest.mark.parametrize("kind", ["geometric", "jittered", "repeated"])
+def test_griddata_nonuniform_axes(gpu, monkeypatch, kind):
+    """Target axes that are ascending but not evenly spaced take the binary-search claim inside the
+    per-cell kernel: the same claims as the per-triangle kernel, and scipy's values."""
+    from scipy.interpolate import griddata as sp_griddata
+    from akbraytracing_amd.griddata import CubicGrid, griddata
+    nv, nh = 97, 113
+    X, Y, F = _lattice(nv, nh, 11)
+    lo, hi = X.min(), X.max()
+    if kind == "geometric":
+        gx = lo + (hi - lo) * (np.geomspace(1, 50, 60) - 1) / 49
+    elif kind == "jittered":
+        gx = np.sort(np.linspace(lo, hi, 60) + np.random.default_rng(3).uniform(-0.3, 0.3, 60) * (hi - lo) / 59)
+    else:
+        gx = np.repeat(np.linspace(lo, hi, 30), 2)
+    gy = np.linspace(Y.min(), Y.max(), 45)
+    cg = CubicGrid(X.ravel(), Y.ravel(), nv, nh)
+    got = cg.interp(F.ravel(), gx, gy).cpu().numpy()[0]
+    monkeypatch.setenv("AKB_GD_CLAIM_TRI", "1")
+    assert np.array_equal(got, cg.interp(F.ravel(), gx, gy).cpu().numpy()[0], equal_nan=True)
+    monkeypatch.delenv("AKB_GD_CLAIM_TRI")
+    GH, GV = np.meshgrid(gx, gy)
+    want = sp_griddata((X.ravel(), Y.ravel()), F.ravel(), (GH, GV), method="cubic")
+    assert np.array_equal(np.isnan(got), np.isnan(want))
+    assert np.isfinite(got).mean() > 0.8
+    assert np.nanmax(np.abs(got - want)) <= _scale_tol(want)
+    assert np.array_equal(griddata((X.ravel(), Y.ravel()), F.ravel(), (GH, GV), grid_shape=(nv, nh)), got, equal_nan=True)
+
+
+def test_griddata_default_tol_margin(gpu):
+    """At the default stopping tolerance (scipy's 1e-6) the gridded values sit within 1e-6 of the range
+    of scipy's on a coarse grid (the 65x65 reference run) and on a strongly distorted lattice, with
+    margin: the values move by far less than the bar between the default and a 1e-12 solve."""
+    from scipy.interpolate import griddata as sp_griddata
+    from akbraytracing_amd.griddata import GRADIENT_TOL, CubicGrid
+    assert GRADIENT_TOL <= 1e-6
+    f = golden("akb_raywave_65.npz")
+    g = golden("akb_psfcalc_65.npz")
+    d2 = f["detcenter2"]
+    gx, gy = g["grid_H0"][0], g["grid_V0"][:, 0]
+    cases = [(d2[1], d2[2], f["wave2"], 65, 65, g["griddata_wave2"])]
+    nv, nh = 61, 67
+    u, v = np.meshgrid(np.linspace(-1, 1, nh), np.linspace(-1, 1, nv))
+    X = u * 1e-4 + 2.5e-5 * v ** 2 - 1.5e-5 * u * v
+    Y = v * 1.1e-4 + 2e-5 * u ** 2 + 1e-5 * u ** 3
+    F = np.sin(2.5 * u) * np.cos(1.7 * v) + 0.4 * u * v
+    GH, GV = np.meshgrid(np.linspace(X.min(), X.max(), 50), np.linspace(Y.min(), Y.max(), 50))
+    cases.append((X.ravel(), Y.ravel(), F.ravel(), nv, nh,
+                  sp_griddata((X.ravel(), Y.ravel()), F.ravel(), (GH, GV), method="cubic")))
+    for i, (x, y, val, a, b, ref) in enumerate(cases):
+        ax, ay = (gx, gy) if i == 0 else (GH[0], GV[:, 0])
+        cg = CubicGrid(x, y, a, b)
+        got = cg.interp(val, ax, ay).cpu().numpy()[0]
+        tight = cg.interp(val, ax, ay, tol=1e-12).cpu().numpy()[0]
+        rng_ = np.nanmax(ref) - np.nanmin(ref)
+        assert np.array_equal(np.isnan(got), np.isnan(ref)), i
+        assert np.nanmax(np.abs(got - ref)) <= _scale_tol(ref), i
+        # the default's own distance from the converged map: 10x inside the bar
+        assert np.nanmax(np.abs(got - tight)) <= 0.1 * max(1e-6 * rng_, 64 * np.spacing(np.nanmax(np.abs(ref)))), i
+
+
+def test_griddata_flagged_triangulation_stays_refused(gpu):
+    """A triangulation the pocket check flags is refused on the first gradient call and on every later
+    one (the failing status is kept, not only the fact that it was read)."""
+    from akbraytracing_amd import _lib
+    from akbraytracing_amd.griddata import CubicGrid
+    X, Y, F = _lattice(40, 50, 2)
+    cg = CubicGrid(X.ravel(), Y.ravel(), 40, 50)
+    cg._status.fill_(2)  # as k_gd_check_pockets raises bit 1 (an edge that is not locally Delaunay)
+    gx, gy = np.linspace(X.min(), X.max(), 9), np.linspace(Y.min(), Y.max(), 7)
+    for _ in range(3):
+        with pytest.raises(_lib.AKBError):
+            cg.interp(F.ravel(), gx, gy)
+
+
 def test_griddata_batched_values_and_errors(gpu):
     from akbraytracing_amd import _lib
     from akbraytracing_amd.griddata import CubicGrid, griddata
@@ -1243,6 +1326,61 @@ def test_huygens_source_split_and_wavefield(gpu):
     dst.setdata(np.vstack([tx, ty, tz]))
     dst.forward_propagation(src)
     assert np.max(np.abs(dst.u - ref)) <= 1e-9 * np.max(np.abs(ref))
+
+
+def _huygens_split_case(m=400_000, n=37, seed=9):
+    rng = np.random.default_rng(seed)
+    s = [torch.from_numpy(rng.random(m) * 1e-3).cuda() for _ in range(3)]
+    t = [torch.from_numpy(rng.random(n) * 1e-3).cuda() for _ in range(2)]
+    t.append(torch.from_numpy(0.05 + rng.random(n) * 1e-3).cuda())
+    u = torch.from_numpy(rng.standard_normal(m) + 1j * rng.standard_normal(m)).cuda()
+    return t, s, u, 2 * np.pi / 13.5e-9
+
+
+def test_huygens_nan_source_stays_fast(gpu):
+    """One NaN source coordinate: every target's sum is NaN (numpy's), and the call costs about what a
+    finite one does - a NaN phase stays on the fast sincos path instead of sending every target of its
+    split to the library fix-up loop."""
+    import time
+    from akbraytracing_amd.wavecalc import propagate
+    t, s, u, k = _huygens_split_case()
+    clean = propagate(*t, *s, u, k)
+    s_nan = [a.clone() for a in s]
+    s_nan[1][12345] = float("nan")
+
+    def timed(src):
+        propagate(*t, *src, u, k)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(5):
+            out = propagate(*t, *src, u, k)
+        torch.cuda.synchronize()
+        return out, (time.perf_counter() - t0) / 5
+
+    out, t_nan = timed(s_nan)
+    _, t_ok = timed(s)
+    assert torch.isnan(out.real).all() and torch.isnan(out.imag).all()
+    assert torch.isfinite(clean.real).all()
+    assert t_nan <= 2.0 * t_ok + 2e-3, (t_nan, t_ok)
+
+
+def test_huygens_two_streams_do_not_share_scratch(gpu):
+    """propagate on two streams of one thread, queued back to back so their kernels may overlap: each
+    result equals the same call run alone (the split partials' scratch is per stream)."""
+    from akbraytracing_amd.wavecalc import propagate
+    t, s, u, k = _huygens_split_case(seed=10)
+    t2 = [a.flip(0).contiguous() for a in t]
+    want_a = propagate(*t, *s, u, k)
+    want_b = propagate(*t2, *s, u, k)
+    torch.cuda.synchronize()
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    for _ in range(3):
+        with torch.cuda.stream(sa):
+            got_a = propagate(*t, *s, u, k, stream=sa)
+        with torch.cuda.stream(sb):
+            got_b = propagate(*t2, *s, u, k, stream=sb)
+        torch.cuda.synchronize()
+        assert torch.equal(got_a, want_a) and torch.equal(got_b, want_b)
 
 
 # ----------------------------------------------------------------------------- install

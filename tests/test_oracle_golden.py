@@ -30,8 +30,10 @@ def test_primitives_bitwise_vs_reference():
     assert n == 28
 
 
-def test_ellipse_chain_bitwise():
-    d = golden("ellipse_33.npz")
+@pytest.mark.parametrize("fixture", ["ellipse_33.npz", "ellipse_317.npz"])
+def test_ellipse_chain_bitwise(fixture):
+    """C1 (BASELINE configs[0]) at 33^2 and at its own 317^2: the oracle equals the reference's run."""
+    d = golden(fixture)
     src = np.zeros_like(d["dir"])
     pts = O.mirr_ray_intersection(d["coeffs"], d["dir"], src)
     nrm = O.norm_vector(d["coeffs"], pts)
@@ -182,6 +184,24 @@ def test_oracle_psf_calc_matches_reference():
     assert r["psf_trimmed"].shape == f["psf_trimmed"].shape
     assert np.max(np.abs(r["psf_trimmed"] - f["psf_trimmed"])) <= 1e-12
     assert np.array_equal(r["x_im"], f["x_im"])
+
+
+@pytest.mark.parametrize("n", [1001, 3163])
+def test_oracle_psf_calc_full_size_matches_reference(n):
+    """psf_calc at the bench's sizes: the reference's own call on its own plane-corrected 128^2 map
+    of the n^2 trace (akb_psf_full.npz, make_golden_full_extra.py psf): rotation estimate exact, the
+    rotated map to 1e-15 nm, the trimmed 2048^2 PSF to 1e-12 of its peak."""
+    import oracle.psfcalc as PC
+    full = golden("akb_raywave_full.npz")
+    f = golden("akb_psf_full.npz")
+    GH, GV = np.meshgrid(full[f"n{n}_gx"], full[f"n{n}_gy"])
+    r = PC.psf_calc(full[f"n{n}_map_wave_c"], GH - np.mean(GH), GV - np.mean(GV), 1e-2)
+    assert r["rot"] == f[f"n{n}_rot"]
+    assert np.array_equal(np.isnan(r["rotated"]), np.isnan(f[f"n{n}_rotated"]))
+    assert np.nanmax(np.abs(r["rotated"] - f[f"n{n}_rotated"])) <= 1e-15 * max(1.0, np.nanmax(np.abs(r["rotated"])))
+    assert r["psf_trimmed"].shape == f[f"n{n}_psf_crop"].shape
+    assert np.max(np.abs(r["psf_trimmed"] - f[f"n{n}_psf_crop"])) <= 1e-12
+    assert np.array_equal(r["x_im"], f[f"n{n}_x_im"]) and np.array_equal(r["y_im"], f[f"n{n}_y_im"])
 
 
 def test_oracle_calc_ds_matches_reference():
