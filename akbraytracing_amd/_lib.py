@@ -41,10 +41,10 @@ EXPORTS = [
     "akb_leaf_parts_f64", "akb_parts_chain_f64",
     "akb_huygens_splits", "akb_huygens_work_bytes", "akb_huygens_f64", "akb_scale_field_f64",
     "akb_psf_work_bytes", "akb_psf_f64", "akb_psf_release_plans", "akb_selftest_arith_f64",
-    "akb_first_valid_rows_f64", "akb_rotate_work_bytes", "akb_rotate_with_nan_f64",
+    "akb_first_valid_rows_f64", "akb_rotate_work_bytes", "akb_rotate_with_nan_f64", "akb_pupil_post_f64",
     "akb_moments_work_bytes", "akb_map_moments_f64", "akb_plane_subtract_f64", "akb_legendre_rows_f64",
     "akb_gd_cells_f64", "akb_gd_pockets", "akb_gd_check_pockets", "akb_gd_grad_sweep_f64", "akb_gd_grad_sweeps_f64",
-    "akb_gd_eval_f64",
+    "akb_gd_eval_f64", "akb_gd_cone_work_bytes", "akb_gd_cone_eval_f64", "akb_gd_axes_f64",
     "akb_trace_chain_batch_f64", "akb_focus_eval_work_bytes", "akb_focus_eval_f64", "akb_sep_search_f64",
     "akb_finish_params_work_bytes", "akb_finish_tilt_params_f64",
     "akb_valid_mask_u8", "akb_external_contours", "akb_approx_poly_dp", "akb_affine_from_points",
@@ -156,6 +156,7 @@ def _declare(L):
         "akb_first_valid_rows_f64": ([c_vp, c_int, c_int, c_vp, c_vp], c_int),
         "akb_rotate_work_bytes": ([c_int, c_int], c_i64),
         "akb_rotate_with_nan_f64": ([c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp], c_int),
+        "akb_pupil_post_f64": ([c_vp, c_int, c_int, c_dbl, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp], c_int),
         "akb_moments_work_bytes": ([], c_i64),
         "akb_map_moments_f64": ([c_vp, c_int, c_int, c_int, c_vp, c_dbl, c_int, c_dbl, c_vp, c_vp, c_vp], c_int),
         "akb_plane_subtract_f64": ([c_vp, c_int, c_int, c_vp, c_vp, c_vp], c_int),
@@ -177,6 +178,10 @@ def _declare(L):
                                     c_vp, c_vp, c_dbl, c_dbl, c_int, c_vp, c_vp, c_vp, c_vp, c_vp], c_int),
         "akb_gd_eval_f64": ([c_vp, c_vp, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int,
                              c_vp, c_vp, c_int, c_vp, c_vp, c_vp], c_int),
+        "akb_gd_cone_work_bytes": ([c_int, c_int, c_int, c_int, c_int], c_i64),
+        "akb_gd_axes_f64": ([c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp], c_int),
+        "akb_gd_cone_eval_f64": ([c_vp, c_vp, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
+                                  c_vp, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp], c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -15,6 +15,8 @@
 #include <stdlib.h>
 #include <stdint.h>
 
+#include <immintrin.h>
+
 #include <algorithm>
 #include <functional>
 #include <thread>
@@ -56,6 +58,96 @@ bool right_turn(const double* x, const double* y, int64_t o, int64_t a, int64_t 
     return c < -1e-12 * sqrt((ax * ax + ay * ay) * (bx * bx + by * by));
 }
 
+// cot of the angle under which chain point m sees (p, q), for m in (p, q), into tmp[m - p - 1]:
+// each value is the same IEEE expression as a scalar loop's (no contraction: -ffp-contract=off),
+// so the vector widths below only change the speed
+__attribute__((always_inline)) inline void cot_scan_body(const double* X, const double* Y, int64_t p, int64_t q,
+                                                          double* tmp) {
+    const double ax = X[p], ay = Y[p], bx = X[q], by = Y[q];
+    const int64_t len = q - p - 1;
+    const double* xs = X + p + 1;
+    const double* ys = Y + p + 1;
+#pragma clang loop vectorize(enable) interleave(enable)
+    for (int64_t k = 0; k < len; ++k) {
+        const double ux = ax - xs[k], uy = ay - ys[k];
+        const double vx = bx - xs[k], vy = by - ys[k];
+        const double cr = fabs(ux * vy - uy * vx);
+        const double dt = ux * vx + uy * vy;
+        const double qt = dt / cr;
+        tmp[k] = cr > 0 ? qt : (dt < 0 ? -INFINITY : INFINITY);
+    }
+}
+__attribute__((target("avx512f,avx512dq"))) void cot_scan_avx512(const double* X, const double* Y, int64_t p, int64_t q,
+                                                                 double* tmp) {
+    cot_scan_body(X, Y, p, q, tmp);
+}
+__attribute__((target("avx2"))) void cot_scan_avx2(const double* X, const double* Y, int64_t p, int64_t q, double* tmp) {
+    cot_scan_body(X, Y, p, q, tmp);
+}
+void cot_scan_base(const double* X, const double* Y, int64_t p, int64_t q, double* tmp) {
+    cot_scan_body(X, Y, p, q, tmp);
+}
+
+// first index of the smallest of tmp[0, len) under '<' (the scalar scan's pick), 8 lanes at a time:
+// each lane keeps its own first minimum, then the lanes' minima are merged value first, index second
+__attribute__((target("avx512f,avx512dq"))) int64_t first_min_avx512(const double* tmp, int64_t len, double& mn_out) {
+    __m512d mn = _mm512_set1_pd(INFINITY);
+    __m512i at = _mm512_set1_epi64(-1);
+    __m512i idx = _mm512_setr_epi64(0, 1, 2, 3, 4, 5, 6, 7);
+    const __m512i eight = _mm512_set1_epi64(8);
+    int64_t k = 0;
+    for (; k + 8 <= len; k += 8) {
+        const __m512d v = _mm512_loadu_pd(tmp + k);
+        const __mmask8 lt = _mm512_cmp_pd_mask(v, mn, _CMP_LT_OQ);
+        mn = _mm512_mask_mov_pd(mn, lt, v);
+        at = _mm512_mask_mov_epi64(at, lt, idx);
+        idx = _mm512_add_epi64(idx, eight);
+    }
+    alignas(64) double m8[8];
+    alignas(64) int64_t a8[8];
+    _mm512_store_pd(m8, mn);
+    _mm512_store_si512((__m512i*)a8, at);
+    double best = INFINITY;
+    int64_t pos = -1;
+    for (int l = 0; l < 8; ++l)
+        if (a8[l] >= 0 && (m8[l] < best || (m8[l] == best && a8[l] < pos))) {
+            best = m8[l];
+            pos = a8[l];
+        }
+    for (; k < len; ++k)
+        if (tmp[k] < best) {
+            best = tmp[k];
+            pos = k;
+        }
+    mn_out = best;
+    return pos;
+}
+
+int64_t first_min_base(const double* tmp, int64_t len, double& mn_out) {
+    double mn = INFINITY;
+    int64_t at = -1;
+    for (int64_t k = 0; k < len; ++k)
+        if (tmp[k] < mn) {
+            mn = tmp[k];
+            at = k;
+        }
+    mn_out = mn;
+    return at;
+}
+
+// the first m in (p, q) with the smallest cot (a strict '<' scan's pick); best_cot receives it
+int64_t best_chain_point(const double* X, const double* Y, int64_t p, int64_t q, double* tmp, double& best_cot) {
+    static const int isa = __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512dq") ? 2
+                           : __builtin_cpu_supports("avx2")                                       ? 1
+                                                                                                  : 0;
+    if (isa == 2) cot_scan_avx512(X, Y, p, q, tmp);
+    else if (isa == 1) cot_scan_avx2(X, Y, p, q, tmp);
+    else cot_scan_base(X, Y, p, q, tmp);
+    const int64_t len = q - p - 1;
+    const int64_t at = isa == 2 ? first_min_avx512(tmp, len, best_cot) : first_min_base(tmp, len, best_cot);
+    return at < 0 ? -1 : p + 1 + at;
+}
+
 }  // namespace
 
 using namespace akb;
@@ -74,12 +166,50 @@ int akb_gd_pockets(const double* rx, const double* ry, int nv, int nh, int cap, 
     const int64_t base = 2 * ncells;
     AKB_REQUIRE(base + cap < INT32_MAX, "grid too large for 32-bit triangle ids");
 
-    // convex hull of the ring points, collinear points kept (pop on a strict right turn only)
+    // convex hull of the ring points, collinear points kept (pop on a strict right turn only);
+    // sorted as (x, y, index) records (the comparisons read neighbouring memory, not the ring)
+    struct Key {
+        double x, y;
+        int64_t i;
+    };
+    std::vector<Key> keys(L);
+    for (int64_t i = 0; i < L; ++i) keys[i] = {rx[i], ry[i], i};
+    const auto less = [](const Key& a, const Key& b) {
+        return a.x < b.x || (a.x == b.x && (a.y < b.y || (a.y == b.y && a.i < b.i)));
+    };
+    // a lattice's boundary ring is a few monotone runs in this (total) order - four for the C3
+    // ring - so a natural merge sort is O(L): strictly descending runs reversed, runs merged in
+    // pairs. The order is total (the index breaks ties), so the result is std::sort's exactly.
+    {
+        std::vector<std::pair<size_t, size_t>> runs;
+        for (size_t i = 0; i < (size_t)L && runs.size() <= 64;) {
+            size_t j = i + 1;
+            if (j < (size_t)L && less(keys[j], keys[i])) {
+                while (j < (size_t)L && less(keys[j], keys[j - 1])) ++j;
+                std::reverse(keys.begin() + i, keys.begin() + j);
+            } else {
+                while (j < (size_t)L && !less(keys[j], keys[j - 1])) ++j;
+            }
+            runs.push_back({i, j});
+            i = j;
+        }
+        if (runs.size() > 64) {
+            std::sort(keys.begin(), keys.end(), less);
+        } else {
+            while (runs.size() > 1) {
+                std::vector<std::pair<size_t, size_t>> next;
+                for (size_t r = 0; r + 1 < runs.size(); r += 2) {
+                    std::inplace_merge(keys.begin() + runs[r].first, keys.begin() + runs[r].second,
+                                       keys.begin() + runs[r + 1].second, less);
+                    next.push_back({runs[r].first, runs[r + 1].second});
+                }
+                if (runs.size() % 2) next.push_back(runs.back());
+                runs.swap(next);
+            }
+        }
+    }
     std::vector<int64_t> order(L);
-    for (int64_t i = 0; i < L; ++i) order[i] = i;
-    std::sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
-        return rx[a] < rx[b] || (rx[a] == rx[b] && ry[a] < ry[b]);
-    });
+    for (int64_t i = 0; i < L; ++i) order[i] = keys[i].i;
     std::vector<char> on_hull(L, 0);
     for (int pass = 0; pass < 2; ++pass) {
         std::vector<int64_t> h;
@@ -142,28 +272,17 @@ int akb_gd_pockets(const double* rx, const double* ry, int nv, int nh, int cap, 
             int slot;        // which of the parent's nbr slots points back here
         };
         std::vector<Job> stack{{P.p, P.q, -1, -1}};
+        std::vector<double> cot((size_t)(P.q - P.p));
         int32_t n = P.id0;
         P.chords.reserve(2 * (size_t)(P.q - P.p));
         while (!stack.empty()) {
             const Job J = stack.back();
             stack.pop_back();
             const int64_t p = J.p, q = J.q;
-            // the chain point seeing (p, q) under the largest angle: smallest cot = dot / |cross|
-            int64_t best = -1;
-            double best_cot = INFINITY;
+            // the chain point seeing (p, q) under the largest angle: the first smallest cot = dot / |cross|
             const int64_t a = p % L, b = q % L;
-            const double ax = X[p], ay = Y[p], bx = X[q], by = Y[q];
-            for (int64_t m = p + 1; m < q; ++m) {
-                const double ux = ax - X[m], uy = ay - Y[m];
-                const double vx = bx - X[m], vy = by - Y[m];
-                const double cr = fabs(ux * vy - uy * vx);
-                const double dt = ux * vx + uy * vy;
-                const double cot = cr > 0 ? dt / cr : (dt < 0 ? -INFINITY : INFINITY);
-                if (cot < best_cot) {
-                    best_cot = cot;
-                    best = m;
-                }
-            }
+            double best_cot = INFINITY;
+            const int64_t best = best_chain_point(X.data(), Y.data(), p, q, cot.data(), best_cot);
             if (best < 0 || !(best_cot < INFINITY)) {
                 P.err = 1;
                 P.err_p = p;

@@ -24,6 +24,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "akb_common.h"
 
 namespace akb {
@@ -1060,6 +1062,429 @@ __global__ void __launch_bounds__(kBlock) k_gd_ring_chords(Grid g, const double*
     }
 }
 
+// ------------------------------------------------------------------ cone solve (fixed K sweeps)
+//
+// After K Chebyshev sweeps from x_0 = 0 a vertex's gradient depends only on the vertices within K
+// hops of it (each sweep reads the 1-hop neighbours' previous iterate and the vertex's own
+// iterate before that). The interpolated values need the gradients at the vertices of the
+// triangles that hold targets only, so for a 128^2 target grid over a 1e7-point lattice the global
+// iteration's x_K there is formed from small patches instead of K passes over the whole lattice:
+//   * interior targets (their cell more than K + 1 cells from the lattice boundary): one workgroup
+//     per target cell holds the (2K + 4)^2 box around the cell in LDS and runs the K sweeps on the
+//     shrinking square that still influences the cell (x_j on the vertices within K + 1 - j of it);
+//   * the rest (cells near the boundary, pocket triangles): the ring's pocket chords couple vertices
+//     far along a side, so those run the global iteration on the boundary band (depth <= 2K + 2,
+//     one launch per sweep, the chords in the ring kernel), valid to depth K + 3 after K sweeps.
+// Per vertex the edge order and arithmetic are k_gd_grad's / k_gd_grad_ring's, so the result at
+// every target vertex is the global iteration's K-sweep value bit for bit
+// (tests/test_gpu_parity.py::test_gradient_cone_equals_global_sweeps).
+
+constexpr int kConeMaxK = 14;                    // patch box side 2K + 4 <= 32
+constexpr int kConeBox = 2 * kConeMaxK + 4;
+
+// grad_edge on values: neighbour (xj, yj), its values fj and previous gradients (gxj, gyj)
+template <int NV>
+__device__ __forceinline__ void edge_vals(double xj, double yj, const double (&fj)[NV], const double (&gxj)[NV],
+                                          const double (&gyj)[NV], double xi, double yi, const double (&fi)[NV],
+                                          GradAcc<NV>& A) {
+    const double ex = xj - xi, ey = yj - yi;
+    const double l2 = ex * ex + ey * ey;
+    double r = __builtin_amdgcn_rsq(l2);
+    r = r * __builtin_fma(-0.5 * l2 * r, r, 1.5);
+    const double r3 = r * r * r;
+    const double wx = ex * r3, wy = ey * r3;
+    A.q0 = __builtin_fma(ex, wx, A.q0);
+    A.q1 = __builtin_fma(ex, wy, A.q1);
+    A.q3 = __builtin_fma(ey, wy, A.q3);
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const double df2 = -ex * gxj[v] - ey * gyj[v];
+        const double w = 6 * (fi[v] - fj[v]) - 2 * df2;
+        A.s0[v] = __builtin_fma(w, wx, A.s0[v]);
+        A.s1[v] = __builtin_fma(w, wy, A.s1[v]);
+    }
+}
+
+// sweep j's weight and predecessor form: j = 1 plain, j = 2 against x_0 = 0, later against x_{j-2}
+struct ConeStep {
+    int mode;  // 0 plain, 1 zero predecessor, 2 predecessor x_{j-2}
+    double omega;
+};
+
+// grad_solve on values: returns scipy's change measure; (ox, oy) = the new gradient
+template <int NV>
+__device__ __forceinline__ double solve_vals(const GradAcc<NV>& A, int v, double gix, double giy, const ConeStep& st,
+                                             double px, double py, double& ox, double& oy) {
+    const double q0 = 4 * A.q0, q1 = 4 * A.q1, q3 = 4 * A.q3;
+    const double inv = 1.0 / (q0 * q3 - q1 * q1);
+    const double r0 = (q3 * A.s0[v] - q1 * A.s1[v]) * inv;
+    const double r1 = (-q1 * A.s0[v] + q0 * A.s1[v]) * inv;
+    const double c = fmax(fabs(gix + r0), fabs(giy + r1)) / fmax(1.0, fmax(fabs(r0), fabs(r1)));
+    if (st.mode == 2) {
+        ox = st.omega * (-r0 - px) + px;
+        oy = st.omega * (-r1 - py) + py;
+    } else if (st.mode == 1) {
+        ox = st.omega * (-r0 - 0.0) + 0.0;
+        oy = st.omega * (-r1 - 0.0) + 0.0;
+    } else {
+        ox = -r0;
+        oy = -r1;
+    }
+    return c;
+}
+
+// the boundary band: vertices with min(iv, ih, nv - 1 - iv, nh - 1 - ih) <= D, enumerated as the
+// top rows, the bottom rows, then the left / right column pieces of the rows between
+struct BandMap {
+    int nv, nh, D;
+    int rows_top, rows_bot, mid0, mid1, cols;  // full rows [0, rows_top), [nv - rows_bot, nv); side columns
+    int64_t n_top, n_bot, n_mid, total;
+};
+
+inline BandMap band_map(int nv, int nh, int D) {
+    BandMap b{nv, nh, D, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    b.rows_top = std::min(D + 1, nv);
+    b.rows_bot = std::min(D + 1, nv - b.rows_top);
+    b.mid0 = b.rows_top;
+    b.mid1 = nv - b.rows_bot;
+    b.cols = std::min(D + 1, nh / 2);
+    const bool full_mid = 2 * (D + 1) >= nh;
+    b.n_top = (int64_t)b.rows_top * nh;
+    b.n_bot = (int64_t)b.rows_bot * nh;
+    b.n_mid = (int64_t)(b.mid1 - b.mid0) * (full_mid ? nh : 2 * b.cols);
+    if (full_mid) b.cols = -1;
+    b.total = b.n_top + b.n_bot + b.n_mid;
+    return b;
+}
+
+__device__ __forceinline__ int64_t band_vertex(const BandMap& b, int64_t k) {
+    if (k < b.n_top) return k;
+    k -= b.n_top;
+    if (k < b.n_bot) return (int64_t)(b.nv - b.rows_bot) * b.nh + k;
+    k -= b.n_bot;
+    if (b.cols < 0) return (int64_t)b.mid0 * b.nh + k;
+    const int w = 2 * b.cols;
+    const int r = b.mid0 + (int)(k / w), c = (int)(k - (int64_t)(k / w) * w);
+    return (int64_t)r * b.nh + (c < b.cols ? c : b.nh - 2 * b.cols + c);
+}
+
+template <int NV>
+struct ConeBand {
+    const double* f;   // (NV, n)
+    const double* gin;    // x_{j-1} (NV, n, 2) or nullptr (x_0 = 0)
+    const double* gprev;  // x_{j-2} (mode 2)
+    double* gout;         // x_j
+    double* ring_acc;     // (L, 3 + 2 NV): ring vertices' grid-edge sums, solved by k_gd_cone_ring
+    ConeStep st;
+    const int* needed;    // device flag: some target needs the band (else the launch returns at once)
+};
+
+// one sweep of the band (k_gd_grad's per-vertex body; nothing reads outside the lattice)
+template <int NV>
+__global__ void __launch_bounds__(kBlock) k_gd_cone_band(Grid g, BandMap bm, ConeBand<NV> a) {
+    if (!*a.needed) return;
+    const int64_t n = (int64_t)g.nv * g.nh;
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < bm.total;
+         k += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = band_vertex(bm, k);
+        const int iv = (int)(i / g.nh), ih = (int)(i - (int64_t)iv * g.nh);
+        const double xi = g.x[i], yi = g.y[i];
+        double fi[NV];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) fi[v] = a.f[v * n + i];
+        GradAcc<NV> A;
+        auto edge = [&](int64_t j) {
+            double fj[NV], gxj[NV], gyj[NV];
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                fj[v] = a.f[v * n + j];
+                gxj[v] = a.gin ? a.gin[2 * (v * n + j)] : 0.0;
+                gyj[v] = a.gin ? a.gin[2 * (v * n + j) + 1] : 0.0;
+            }
+            edge_vals<NV>(g.x[j], g.y[j], fj, gxj, gyj, xi, yi, fi, A);
+        };
+        if (ih > 0) edge(i - 1);
+        if (ih < g.nh - 1) edge(i + 1);
+        if (iv > 0) edge(i - g.nh);
+        if (iv < g.nv - 1) edge(i + g.nh);
+        const int64_t c0 = (int64_t)iv * (g.nh - 1) + ih;
+        if (iv > 0 && ih > 0 && g.diag[c0 - g.nh] == 0) edge(i - g.nh - 1);
+        if (iv > 0 && ih < g.nh - 1 && g.diag[c0 - (g.nh - 1)] == 1) edge(i - g.nh + 1);
+        if (iv < g.nv - 1 && ih > 0 && g.diag[c0 - 1] == 1) edge(i + g.nh - 1);
+        if (iv < g.nv - 1 && ih < g.nh - 1 && g.diag[c0] == 0) edge(i + g.nh + 1);
+        const int64_t r = ring_pos(g, iv, ih);
+        if (r >= 0) {
+            double* d = a.ring_acc + r * (3 + 2 * NV);
+            d[0] = A.q0;
+            d[1] = A.q1;
+            d[2] = A.q3;
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                d[3 + 2 * v] = A.s0[v];
+                d[4 + 2 * v] = A.s1[v];
+            }
+            continue;
+        }
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            const int64_t o = 2 * (v * n + i);
+            const double gix = a.gin ? a.gin[o] : 0.0, giy = a.gin ? a.gin[o + 1] : 0.0;
+            const double px = a.st.mode == 2 ? a.gprev[o] : 0.0, py = a.st.mode == 2 ? a.gprev[o + 1] : 0.0;
+            double ox, oy;
+            solve_vals<NV>(A, v, gix, giy, a.st, px, py, ox, oy);
+            a.gout[o] = ox;
+            a.gout[o + 1] = oy;
+        }
+    }
+}
+
+// the ring vertices of a band sweep: pocket chords (a wave per ring vertex, k_gd_grad_ring's fixed
+// reduction order), then the grid-edge sums the band kernel left, then the solve
+template <int NV>
+__global__ void __launch_bounds__(kBlock) k_gd_cone_ring(Grid g, ConeBand<NV> a) {
+    if (!*a.needed) return;
+    const int64_t n = (int64_t)g.nv * g.nh;
+    const int64_t ra = g.nh - 1, rb = g.nv - 1, L = 2 * ra + 2 * rb;
+    const int lane = threadIdx.x & 63;
+    for (int64_t r = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; r < L;
+         r += ((int64_t)gridDim.x * blockDim.x) >> 6) {
+        int64_t i;
+        if (r < ra) i = r;
+        else if (r < ra + rb) i = (r - ra) * g.nh + (g.nh - 1);
+        else if (r < 2 * ra + rb) i = (int64_t)(g.nv - 1) * g.nh + (g.nh - 1 - (r - ra - rb));
+        else i = (int64_t)(g.nv - 1 - (r - 2 * ra - rb)) * g.nh;
+        const double xi = g.x[i], yi = g.y[i];
+        double fi[NV];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) fi[v] = a.f[v * n + i];
+        GradAcc<NV> A;
+        for (int32_t k = g.xptr[r] + lane; k < g.xptr[r + 1]; k += 64) {
+            const int64_t j = g.xidx[k];
+            double fj[NV], gxj[NV], gyj[NV];
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                fj[v] = a.f[v * n + j];
+                gxj[v] = a.gin ? a.gin[2 * (v * n + j)] : 0.0;
+                gyj[v] = a.gin ? a.gin[2 * (v * n + j) + 1] : 0.0;
+            }
+            edge_vals<NV>(g.x[j], g.y[j], fj, gxj, gyj, xi, yi, fi, A);
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+            A.q0 += __shfl_down(A.q0, off);
+            A.q1 += __shfl_down(A.q1, off);
+            A.q3 += __shfl_down(A.q3, off);
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                A.s0[v] += __shfl_down(A.s0[v], off);
+                A.s1[v] += __shfl_down(A.s1[v], off);
+            }
+        }
+        if (lane == 0) {
+            const double* d = a.ring_acc + r * (3 + 2 * NV);
+            A.q0 += d[0];
+            A.q1 += d[1];
+            A.q3 += d[2];
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                A.s0[v] += d[3 + 2 * v];
+                A.s1[v] += d[4 + 2 * v];
+            }
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                const int64_t o = 2 * (v * n + i);
+                const double gix = a.gin ? a.gin[o] : 0.0, giy = a.gin ? a.gin[o + 1] : 0.0;
+                const double px = a.st.mode == 2 ? a.gprev[o] : 0.0, py = a.st.mode == 2 ? a.gprev[o + 1] : 0.0;
+                double ox, oy;
+                solve_vals<NV>(A, v, gix, giy, a.st, px, py, ox, oy);
+                a.gout[o] = ox;
+                a.gout[o + 1] = oy;
+            }
+        }
+    }
+}
+
+template <int NV>
+struct ConePatch {
+    const double* f;           // (NV, n)
+    const int64_t* cells;      // interior target cells (duplicates allowed)
+    const int* count;          // how many (device)
+    int K;
+    ConeStep st[kConeMaxK + 1];  // st[j] for sweep j = 1 .. K
+    double* gout;              // x_K (NV, n, 2): the cells' four corners are written
+    unsigned long long* chg;   // largest change measure of one more sweep at the corners (or nullptr)
+};
+
+// one workgroup per interior target cell: the (2K + 4)^2 box around it in LDS, K sweeps on the
+// shrinking square that influences the cell, the corners' x_K to global memory
+template <int NV>
+__global__ void __launch_bounds__(256) k_gd_cone_patch(Grid g, ConePatch<NV> a) {
+    constexpr int B2 = kConeBox * kConeBox;
+    __shared__ double sx[B2], sy[B2], sf[NV][B2];
+    __shared__ double sg[3][NV][B2][2];  // x_{j-2}, x_{j-1}, x_j rotating
+    __shared__ uint8_t sd[B2];
+    const int64_t n = (int64_t)g.nv * g.nh;
+    const int K = a.K, W = 2 * K + 4;
+    for (int pid = blockIdx.x; pid < *a.count; pid += gridDim.x) {
+        const int64_t cell = a.cells[pid];
+        const int iv0 = (int)(cell / (g.nh - 1)), ih0 = (int)(cell - (int64_t)iv0 * (g.nh - 1));
+        const int R0 = iv0 - (K + 1), C0 = ih0 - (K + 1);
+        __syncthreads();  // the previous cell's reads are done
+        for (int idx = threadIdx.x; idx < W * W; idx += blockDim.x) {
+            const int r = idx / W, c = idx - (idx / W) * W;
+            const int64_t i = (int64_t)(R0 + r) * g.nh + (C0 + c);
+            sx[idx] = g.x[i];
+            sy[idx] = g.y[i];
+#pragma unroll
+            for (int v = 0; v < NV; ++v) sf[v][idx] = a.f[v * n + i];
+            sd[idx] = (r < W - 1 && c < W - 1) ? g.diag[(int64_t)(R0 + r) * (g.nh - 1) + (C0 + c)] : 0;
+        }
+        __syncthreads();
+        // the sums of box vertex b from iterate buffer `in` (nullptr role: x_0 = 0)
+        auto sums = [&](int b, int in) {
+            GradAcc<NV> A;
+            double fi[NV];
+#pragma unroll
+            for (int v = 0; v < NV; ++v) fi[v] = sf[v][b];
+            const double xi = sx[b], yi = sy[b];
+            auto edge = [&](int j) {
+                double fj[NV], gxj[NV], gyj[NV];
+#pragma unroll
+                for (int v = 0; v < NV; ++v) {
+                    fj[v] = sf[v][j];
+                    gxj[v] = in < 0 ? 0.0 : sg[in][v][j][0];
+                    gyj[v] = in < 0 ? 0.0 : sg[in][v][j][1];
+                }
+                edge_vals<NV>(sx[j], sy[j], fj, gxj, gyj, xi, yi, fi, A);
+            };
+            // k_gd_grad's order: left, right, down (iv - 1), up (iv + 1), then the diagonals
+            edge(b - 1);
+            edge(b + 1);
+            edge(b - W);
+            edge(b + W);
+            if (sd[b - W - 1] == 0) edge(b - W - 1);
+            if (sd[b - W] == 1) edge(b - W + 1);
+            if (sd[b - 1] == 1) edge(b + W - 1);
+            if (sd[b] == 0) edge(b + W + 1);
+            return A;
+        };
+        for (int j = 1; j <= K; ++j) {
+            const int half = K + 1 - j, side = 2 * half + 2, off = (K + 1) - half;
+            const int in = j == 1 ? -1 : (j - 1) % 3, out = j % 3, prev = (j + 1) % 3;  // x_{j-1}, x_j, x_{j-2}
+            const ConeStep st = a.st[j];
+            for (int idx = threadIdx.x; idx < side * side; idx += blockDim.x) {
+                const int b = (off + idx / side) * W + off + (idx - (idx / side) * side);
+                const GradAcc<NV> A = sums(b, in);
+#pragma unroll
+                for (int v = 0; v < NV; ++v) {
+                    const double gix = in < 0 ? 0.0 : sg[in][v][b][0], giy = in < 0 ? 0.0 : sg[in][v][b][1];
+                    const double px = st.mode == 2 ? sg[prev][v][b][0] : 0.0;
+                    const double py = st.mode == 2 ? sg[prev][v][b][1] : 0.0;
+                    double ox, oy;
+                    solve_vals<NV>(A, v, gix, giy, st, px, py, ox, oy);
+                    sg[out][v][b][0] = ox;
+                    sg[out][v][b][1] = oy;
+                }
+            }
+            __syncthreads();
+        }
+        // the cell's corners: x_K out, and the change one more (plain-measured) sweep would make
+        double worst = 0.0;
+        if (threadIdx.x < 4) {
+            const int cr = K + 1 + (threadIdx.x >> 1), cc = K + 1 + (threadIdx.x & 1);
+            const int b = cr * W + cc, fin = K % 3;
+            const int64_t i = (int64_t)(R0 + cr) * g.nh + (C0 + cc);
+            const GradAcc<NV> A = sums(b, fin);
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                const double gx = sg[fin][v][b][0], gy = sg[fin][v][b][1];
+                a.gout[2 * (v * n + i)] = gx;
+                a.gout[2 * (v * n + i) + 1] = gy;
+                double ox, oy;
+                worst = fmax(worst, solve_vals<NV>(A, v, gx, gy, ConeStep{0, 1.0}, 0.0, 0.0, ox, oy));
+            }
+        }
+        if (a.chg && threadIdx.x < 64) {
+            for (int off = 2; off > 0; off >>= 1) worst = fmax(worst, __shfl_down(worst, off));
+            if (threadIdx.x == 0 && worst > 0) atomicMax(a.chg, (unsigned long long)__double_as_longlong(worst));
+        }
+    }
+}
+
+// targets -> interior target cells (the patch list) and whether any target needs the band
+__global__ void __launch_bounds__(kBlock) k_gd_cone_targets(Grid g, const int* __restrict__ owner, int64_t m, int K,
+                                                             int64_t* cells, int* count, int* band) {
+    const int64_t nc2 = 2 * ncells(g);
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < m; t += (int64_t)gridDim.x * blockDim.x) {
+        const int o = owner[t];
+        if (o == INT32_MAX) continue;
+        bool interior = false;
+        int64_t c = -1;
+        if (o < nc2) {
+            c = o >> 1;
+            const int iv = (int)(c / (g.nh - 1)), ih = (int)(c - (int64_t)iv * (g.nh - 1));
+            // the box rows iv - K - 1 .. iv + K + 2 clear of the ring rows / columns
+            interior = iv - K - 1 >= 1 && iv + K + 2 <= g.nv - 2 && ih - K - 1 >= 1 && ih + K + 2 <= g.nh - 2;
+        }
+        if (interior) cells[atomicAdd(count, 1)] = c;
+        else atomicOr(band, 1);
+    }
+}
+
+// the driver's target grid axes from the lattice's extent (its extremes lie on the boundary ring):
+// np.linspace(min, max, m) of the ring's x and y - i * step + start, the last point the stop
+// (numpy 2.x's linspace arithmetic) - one workgroup
+__global__ void __launch_bounds__(kBlock) k_gd_axes(const double* __restrict__ rx, const double* __restrict__ ry,
+                                                     int64_t L, int mx, int my, double* gx, double* gy, double* ext) {
+    __shared__ double red[4][kBlock / 64];
+    double lo_x = INFINITY, hi_x = -INFINITY, lo_y = INFINITY, hi_y = -INFINITY;
+    for (int64_t r = threadIdx.x; r < L; r += blockDim.x) {
+        lo_x = fmin(lo_x, rx[r]);
+        hi_x = fmax(hi_x, rx[r]);
+        lo_y = fmin(lo_y, ry[r]);
+        hi_y = fmax(hi_y, ry[r]);
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        lo_x = fmin(lo_x, __shfl_down(lo_x, off));
+        hi_x = fmax(hi_x, __shfl_down(hi_x, off));
+        lo_y = fmin(lo_y, __shfl_down(lo_y, off));
+        hi_y = fmax(hi_y, __shfl_down(hi_y, off));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = lo_x;
+        red[1][threadIdx.x >> 6] = hi_x;
+        red[2][threadIdx.x >> 6] = lo_y;
+        red[3][threadIdx.x >> 6] = hi_y;
+    }
+    __syncthreads();
+    double e[4];
+    for (int q = 0; q < 4; ++q) {
+        e[q] = red[q][0];
+        for (int w = 1; w < kBlock / 64; ++w) e[q] = (q & 1) ? fmax(e[q], red[q][w]) : fmin(e[q], red[q][w]);
+    }
+    if (threadIdx.x == 0 && ext) {
+        for (int q = 0; q < 4; ++q) ext[q] = e[q];
+        // the pupil pitch psf_calc takes (:1176-1177): one step of each axis (before the driver's
+        // mean subtraction, which can move it by an ulp; the normalised PSF does not depend on it)
+        ext[4] = mx > 1 ? fabs((e[1] - e[0]) / (double)(mx - 1)) : 0.0;
+        ext[5] = my > 1 ? fabs((e[3] - e[2]) / (double)(my - 1)) : 0.0;
+    }
+    auto lin = [&](double a0, double a1, int m, double* out) {
+        if (m == 1) {
+            if (threadIdx.x == 0) out[0] = a0;
+            return;
+        }
+        const double step = (a1 - a0) / (double)(m - 1);
+        for (int i = threadIdx.x; i < m; i += blockDim.x) {
+            double v;
+            if (step == 0) v = (double)i / (double)(m - 1) * (a1 - a0) + a0;  // numpy's zero-step branch
+            else v = (double)i * step + a0;
+            out[i] = i == m - 1 ? a1 : v;
+        }
+    };
+    lin(e[0], e[1], mx, gx);
+    lin(e[2], e[3], my, gy);
+}
+
 // ------------------------------------------------------------------ targets
 
 struct Targets {
@@ -1530,6 +1955,102 @@ int akb_gd_eval_f64(const double* x, const double* y, int nv, int nh, const uint
     }
     k_gd_eval<<<grid_for(m, 1, kStreamGridCap), kBlock, 0, s>>>(g, t, owner, f, grad, nvals, out);
     return launch_status("k_gd_eval");
+}
+
+int akb_gd_axes_f64(const double* ring_x, const double* ring_y, int64_t L, int mx, int my, double* gx, double* gy,
+                    double* d_extent, void* stream) {
+    clear_error();
+    AKB_REQUIRE(ring_x && ring_y && gx && gy && L > 0 && mx > 0 && my > 0, "bad arguments");
+    k_gd_axes<<<1, kBlock, 0, (hipStream_t)stream>>>(ring_x, ring_y, L, mx, my, gx, gy, d_extent);
+    return launch_status("k_gd_axes");
+}
+
+// ---- cone solve: claims, the fixed-K gradient iteration restricted to what the targets read,
+// the patches; one call, no host synchronisation
+
+int64_t akb_gd_cone_work_bytes(int nv, int nh, int mx, int my, int nvals) {
+    if (nv < 2 || nh < 2 || mx < 1 || my < 1 || nvals < 1) return -1;
+    const int64_t n = (int64_t)nv * nh, L = 2 * (int64_t)(nh - 1) + 2 * (int64_t)(nv - 1);
+    const int nv2 = nvals >= 2 ? 2 : 1;
+    const int64_t m = (int64_t)mx * my;
+    return 3 * (int64_t)nv2 * n * 2 * 8 + L * 7 * 8 + m * 8 + 64;
+}
+
+int akb_gd_cone_eval_f64(const double* x, const double* y, int nv, int nh, const uint8_t* diag, int npock,
+                         const int32_t* ptri, const int32_t* pnbr, const int32_t* edge_tri, const int32_t* xptr,
+                         const int32_t* xidx, const double* gx, int mx, const double* gy, int my, const double* f,
+                         int nvals, int K, const double* omegas, void* work, int* owner, double* out,
+                         unsigned long long* d_change, void* stream) {
+    clear_error();
+    AKB_REQUIRE(x && y && diag && gx && gy && f && omegas && work && owner && out && mx > 0 && my > 0 && nvals >= 1,
+                "bad arguments");
+    AKB_REQUIRE(K >= 1 && K <= kConeMaxK, "K sweeps in 1 .. 14");
+    AKB_REQUIRE(nv >= 2 && nh >= 2, "grid of at least 2 x 2 points");
+    for (int j = 2; j <= K; ++j) AKB_REQUIRE(omegas[j - 1] > 0 && omegas[j - 1] < 2, "Chebyshev weight outside (0, 2)");
+    hipStream_t s = (hipStream_t)stream;
+    Grid g{x, y, nv, nh, diag, npock, ptri, pnbr, edge_tri, xptr, xidx};
+    Targets t{gx, gy, mx, my};
+    const int64_t n = (int64_t)nv * nh, m = (int64_t)mx * my;
+    const int64_t L = 2 * (int64_t)(nh - 1) + 2 * (int64_t)(nv - 1);
+    const int nv2 = nvals >= 2 ? 2 : 1;
+    double* gb[3];
+    for (int k = 0; k < 3; ++k) gb[k] = (double*)work + (int64_t)k * nv2 * n * 2;
+    double* ring_acc = (double*)work + 3 * (int64_t)nv2 * n * 2;
+    int64_t* cells = (int64_t*)(ring_acc + L * 7);
+    int* count = (int*)(cells + m);
+    int* band = count + 1;
+    // claims (akb_gd_eval_f64's)
+    k_fill_i32<<<grid_for(m, 4), kBlock, 0, s>>>(owner, m, INT32_MAX);
+    int st = launch_status("k_fill_i32");
+    if (st) return st;
+    const int64_t ntri = 2 * (int64_t)(nv - 1) * (nh - 1) + npock;
+    k_gd_claim_cells<<<grid_for((ntri - npock) / 2, 1, kStreamGridCap), kBlock, 0, s>>>(g, t, owner);
+    if ((st = launch_status("k_gd_claim"))) return st;
+    if (npock > 0) {
+        k_gd_claim_pockets<<<(unsigned)(npock < 16384 ? npock : 16384), kBlock, 0, s>>>(g, t, owner);
+        if ((st = launch_status("k_gd_claim_pockets"))) return st;
+    }
+    if (hipMemsetAsync(count, 0, 2 * sizeof(int), s) != hipSuccess) return launch_status("hipMemsetAsync");
+    k_gd_cone_targets<<<grid_for(m, 1), kBlock, 0, s>>>(g, owner, m, K, cells, count, band);
+    if ((st = launch_status("k_gd_cone_targets"))) return st;
+    // the boundary band: depth <= 2K + 2 (x_K valid to depth K + 3 >= every band target's corners)
+    const BandMap bm = band_map(nv, nh, 2 * K + 2);
+    ConeStep steps[kConeMaxK + 1];
+    steps[0] = ConeStep{0, 1.0};
+    for (int j = 1; j <= K; ++j)
+        steps[j] = j == 1 ? ConeStep{0, 1.0} : j == 2 ? ConeStep{1, omegas[1]} : ConeStep{2, omegas[j - 1]};
+    const unsigned pg = (unsigned)(m < 8192 ? m : 8192);
+    for (int v0 = 0; v0 < nvals; v0 += 2) {
+        const int nvv = nvals - v0 >= 2 ? 2 : 1;
+        const double* fv = f + v0 * n;
+        for (int j = 1; j <= K; ++j) {
+            const double* gin = j == 1 ? nullptr : gb[(j - 1) % 3];
+            const double* gprev = j >= 3 ? gb[(j + 1) % 3] : nullptr;
+            if (nvv == 2) {
+                ConeBand<2> a{fv, gin, gprev, gb[j % 3], ring_acc, steps[j], band};
+                k_gd_cone_band<2><<<grid_for(bm.total, 1, kStreamGridCap), kBlock, 0, s>>>(g, bm, a);
+                k_gd_cone_ring<2><<<grid_for(L * 64), kBlock, 0, s>>>(g, a);
+            } else {
+                ConeBand<1> a{fv, gin, gprev, gb[j % 3], ring_acc, steps[j], band};
+                k_gd_cone_band<1><<<grid_for(bm.total, 1, kStreamGridCap), kBlock, 0, s>>>(g, bm, a);
+                k_gd_cone_ring<1><<<grid_for(L * 64), kBlock, 0, s>>>(g, a);
+            }
+            if ((st = launch_status("k_gd_cone_band"))) return st;
+        }
+        if (nvv == 2) {
+            ConePatch<2> a{fv, cells, count, K, {}, gb[K % 3], d_change};
+            for (int j = 0; j <= K; ++j) a.st[j] = steps[j];
+            k_gd_cone_patch<2><<<pg, 256, 0, s>>>(g, a);
+        } else {
+            ConePatch<1> a{fv, cells, count, K, {}, gb[K % 3], d_change};
+            for (int j = 0; j <= K; ++j) a.st[j] = steps[j];
+            k_gd_cone_patch<1><<<pg, 256, 0, s>>>(g, a);
+        }
+        if ((st = launch_status("k_gd_cone_patch"))) return st;
+        k_gd_eval<<<grid_for(m, 1, kStreamGridCap), kBlock, 0, s>>>(g, t, owner, fv, gb[K % 3], nvv, out + v0 * m);
+        if ((st = launch_status("k_gd_eval"))) return st;
+    }
+    return 0;
 }
 
 }  // extern "C"

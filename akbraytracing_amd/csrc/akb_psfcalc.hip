@@ -8,6 +8,7 @@
 // its boundary rules). The maps are small (65^2 .. 1k^2): one thread per line for the recursive
 // prefilter, one thread per output pixel for the interpolation, both arrays at once.
 #include "akb_common.h"
+#include "akb_pairwise.h"
 
 namespace akb {
 
@@ -31,15 +32,7 @@ __global__ void k_nan_split(const double* __restrict__ m, int64_t n, double* __r
 
 // scipy spline_filter1d(order 3) along each line of one axis: gain 6, mirror-symmetric causal
 // initialisation, causal pass, anti-causal initialisation and pass (the order of oracle/psfcalc.py)
-__global__ void k_spline_lines(double* __restrict__ coef, int ny, int nx, int axis) {
-    // blockIdx.y: which array (map, mask); one thread per line
-    const int line = blockIdx.x * blockDim.x + threadIdx.x;
-    const int nlines = axis == 0 ? nx : ny;
-    if (line >= nlines) return;
-    double* base = coef + (int64_t)blockIdx.y * ny * nx;
-    const int n = axis == 0 ? ny : nx;
-    const int64_t s = axis == 0 ? nx : 1;
-    double* c = base + (axis == 0 ? line : (int64_t)line * nx);
+__device__ void spline_line(double* c, int n, int64_t s) {
     const double z = sqrt(3.0) - 2.0;
     const double gain = (1.0 - z) * (1.0 - 1.0 / z);
     for (int i = 0; i < n; ++i) c[i * s] = c[i * s] * gain;
@@ -55,6 +48,15 @@ __global__ void k_spline_lines(double* __restrict__ coef, int ny, int nx, int ax
     for (int i = 1; i < n; ++i) c[i * s] += z * c[(i - 1) * s];
     c[(n - 1) * s] = (z * c[(n - 2) * s] + c[(n - 1) * s]) * z / (z * z - 1.0);
     for (int i = n - 2; i >= 0; --i) c[i * s] = z * (c[(i + 1) * s] - c[i * s]);
+}
+
+__global__ void k_spline_lines(double* __restrict__ coef, int ny, int nx, int axis) {
+    // blockIdx.y: which array (map, mask); one thread per line
+    const int line = blockIdx.x * blockDim.x + threadIdx.x;
+    const int nlines = axis == 0 ? nx : ny;
+    if (line >= nlines) return;
+    double* base = coef + (int64_t)blockIdx.y * ny * nx;
+    spline_line(base + (axis == 0 ? line : (int64_t)line * nx), axis == 0 ? ny : nx, axis == 0 ? nx : 1);
 }
 
 __device__ __forceinline__ int mirror_index(int i, int n) {
@@ -80,9 +82,9 @@ struct RotArgs {
     double* opd_m;    // rotated * 1e-9 (or NULL)
 };
 
-__global__ void k_rotate_cubic(RotArgs a) {
+__device__ __forceinline__ void rotate_pixel(const RotArgs& a, int64_t k) {
     const int64_t total = (int64_t)a.ny * a.nx;
-    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < total; k += (int64_t)gridDim.x * blockDim.x) {
+    {
         const int i = (int)(k / a.nx), j = (int)(k - (int64_t)i * a.nx);
         const double y = a.m00 * i + a.m01 * j + a.off0;
         const double x = a.m10 * i + a.m11 * j + a.off1;
@@ -109,6 +111,12 @@ __global__ void k_rotate_cubic(RotArgs a) {
         a.rotated[k] = r;
         if (a.opd_m) a.opd_m[k] = r * 1e-9;
     }
+}
+
+__global__ void k_rotate_cubic(RotArgs a) {
+    const int64_t total = (int64_t)a.ny * a.nx;
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < total; k += (int64_t)gridDim.x * blockDim.x)
+        rotate_pixel(a, k);
 }
 
 // ---- plane_correction_with_nan_and_outlier_filter (ref :9630-9693) and match_legendre (:59-73) ----
@@ -214,6 +222,299 @@ __global__ void __launch_bounds__(kBlock) k_plane_subtract(const double* __restr
         const double m = __builtin_fma(coef[2], f[2], __builtin_fma(coef[1], f[1], coef[0] * f[0]));
         const double v = z[k];
         out[k] = v != v ? v : v - m;
+    }
+}
+
+// ---- the pupil's whole post-processing in one workgroup (no host round trip) ----
+//
+// The driver's chain from the gridded Wave2 map to compute_psf_fft's input
+// (AKB_raytrace_20250312.py:3690-3700, :9630-9693, :1121-1188): matrixWave2 -= np.nanmean,
+// plane_correction_with_nan_and_outlier_filter (the moments and normal-equation solves of
+// pupilmap._plane_corrections, on the device), psf_calc's rotation estimate, and rotate_with_nan
+// (order 3) with scipy.ndimage.rotate's matrix from cephes' cosdg / sindg. One 1024-thread
+// workgroup does it all for maps of up to 65536 points (the pipelined 128^2 pupil): each step is a
+// workgroup pass over the map in L2 with a fixed-order reduction, so a pipelined caller queues the
+// PSF behind it with no host synchronisation. The nanmean is numpy's (pairwise over 8192-element
+// buffers, left to right); the moments' association differs from k_moments (rounding-level
+// differences, tests hold the maps to 1e-12 of the range).
+
+// cephes sindg / cosdg (degrees; the functions scipy.ndimage.rotate calls for its matrix, scipy
+// 1.15 special/xsf/cephes/sindg.h): octant reduction in degrees, then the cephes minimax polynomials
+// on [0, pi/4]; every product and sum rounded on its own, as the host library evaluates them.
+__device__ __constant__ double kSinCof[6] = {1.58962301572218447952E-10, -2.50507477628503540135E-8,
+                                             2.75573136213856773549E-6,  -1.98412698295895384658E-4,
+                                             8.33333333332211858862E-3,  -1.66666666666666307295E-1};
+__device__ __constant__ double kCosCof[7] = {1.13678171382044553091E-11, -2.08758833757683644217E-9,
+                                             2.75573155429816611547E-7,  -2.48015872936186303776E-5,
+                                             1.38888888888806666760E-3,  -4.16666666666666348141E-2,
+                                             4.99999999999999999798E-1};
+
+__device__ __forceinline__ double horner(double x, const double* c, int deg) {
+    double r = c[0];
+    for (int i = 1; i <= deg; ++i) r = r * x + c[i];
+    return r;
+}
+
+// octant of |x| degrees (cephes' reduction): returns j in 0..3 and sets y to the multiple of 45
+// taken off, flipping *neg for the octants 4..7
+__device__ __forceinline__ int deg_octant(double x, double& y, bool& flip) {
+    y = floor(x / 45.0);
+    double z = ldexp(y, -4);
+    z = floor(z);
+    z = y - ldexp(z, 4);
+    int j = (int)z;
+    if (j & 1) {
+        j += 1;
+        y += 1.0;
+    }
+    j &= 7;
+    flip = j > 3;
+    return flip ? j - 4 : j;
+}
+
+__device__ double sin_deg(double x) {
+    bool neg = x < 0;
+    if (neg) x = -x;
+    if (x > 1.0e14) return 0.0;
+    double y;
+    bool flip;
+    const int j = deg_octant(x, y, flip);
+    if (flip) neg = !neg;
+    double z = x - y * 45.0;
+    z = z * 1.74532925199432957692E-2;
+    const double zz = z * z;
+    double r = (j == 1 || j == 2) ? 1.0 - zz * horner(zz, kCosCof, 6) : z + z * (zz * horner(zz, kSinCof, 5));
+    return neg ? -r : r;
+}
+
+__device__ double cos_deg(double x) {
+    if (x < 0) x = -x;
+    if (x > 1.0e14) return 0.0;
+    double y;
+    bool flip;
+    const int j = deg_octant(x, y, flip);
+    bool neg = flip;
+    if (j > 1) neg = !neg;
+    double z = x - y * 45.0;
+    z = z * 1.74532925199432957692E-2;
+    const double zz = z * z;
+    double r = (j == 1 || j == 2) ? z + z * (zz * horner(zz, kSinCof, 5)) : 1.0 - zz * horner(zz, kCosCof, 6);
+    return neg ? -r : r;
+}
+
+// A x = b by Gaussian elimination with partial pivoting (the largest magnitude in the column,
+// the first on ties, as LAPACK's dgetf2 picks); A row-major n x n, solution in b. false: singular.
+__device__ bool solve_small(double* A, double* b, int n) {
+    for (int k = 0; k < n; ++k) {
+        int p = k;
+        for (int i = k + 1; i < n; ++i)
+            if (fabs(A[i * n + k]) > fabs(A[p * n + k])) p = i;
+        if (A[p * n + k] == 0.0) return false;
+        if (p != k) {
+            for (int j = 0; j < n; ++j) {
+                const double t = A[k * n + j];
+                A[k * n + j] = A[p * n + j];
+                A[p * n + j] = t;
+            }
+            const double t = b[k];
+            b[k] = b[p];
+            b[p] = t;
+        }
+        for (int i = k + 1; i < n; ++i) {
+            const double l = A[i * n + k] / A[k * n + k];
+            for (int j = k; j < n; ++j) A[i * n + j] = A[i * n + j] - l * A[k * n + j];
+            b[i] = b[i] - l * b[k];
+        }
+    }
+    for (int k = n - 1; k >= 0; --k) {
+        double v = b[k];
+        for (int j = k + 1; j < n; ++j) v = v - A[k * n + j] * b[j];
+        b[k] = v / A[k * n + k];
+    }
+    return true;
+}
+
+constexpr int kPostThreads = 1024;
+constexpr int64_t kPostMax = 65536;  // map points the one-workgroup post handles
+
+struct PostArgs {
+    const double* m;     // (ny, nx) gridded map (NaN outside the hull)
+    int ny, nx;
+    double sigma;        // the outlier filter's threshold in standard deviations (3)
+    double* corrected;   // matrixWave2_Corrected
+    double* rotated;     // psf_calc's rotated map (nm, NaN outside)
+    double* opd;         // rotated * 1e-9 (the PSF's opd_m)
+    double* coef;        // work: (2, ny, nx) prefilter coefficients
+    double* params;      // out, kPostParams doubles (layout in akb_raytrace.h)
+};
+
+// fixed-order workgroup sum of q values per thread (wave shuffles, then the waves in order)
+template <int Q>
+__device__ __forceinline__ void block_sum(double (&acc)[Q], double (*red)[Q]) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int q = 0; q < Q; ++q)
+        for (int off = 32; off > 0; off >>= 1) acc[q] += __shfl_down(acc[q], off);
+    if (lane == 0)
+#pragma unroll
+        for (int q = 0; q < Q; ++q) red[w][q] = acc[q];
+    __syncthreads();
+    if (threadIdx.x < Q) {
+        double v = red[0][threadIdx.x];
+        for (int k = 1; k < kPostThreads / 64; ++k) v += red[k][threadIdx.x];
+        red[0][threadIdx.x] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < Q; ++q) acc[q] = red[0][q];
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
+    __shared__ PwTree trees[8];
+    __shared__ double bufsum[8];
+    __shared__ double red[kPostThreads / 64][kMomMax];
+    __shared__ double sys[32];
+    __shared__ int sflag;
+    const int64_t total = (int64_t)a.ny * a.nx;
+    const int tid = threadIdx.x, w = tid >> 6;
+    double* P = a.params;
+    // np.nanmean: numpy's pairwise sum of the NaN-zeroed map, one wave per 8192-element buffer
+    const int nbuf = (int)((total + 8191) / 8192);
+    if (w < nbuf) {
+        const int64_t b0 = (int64_t)w * 8192;
+        const int len = (int)(total - b0 < 8192 ? total - b0 : 8192);
+        const double v = pw_tree_wave<true>(trees[w], a.m + b0, len);
+        if ((tid & 63) == 0) bufsum[w] = v;
+    }
+    double cnt[1] = {0.0};
+    for (int64_t k = tid; k < total; k += kPostThreads) cnt[0] += a.m[k] == a.m[k] ? 1.0 : 0.0;
+    block_sum<1>(cnt, (double(*)[1])red);
+    double tot = 0.0;
+    for (int b = 0; b < nbuf; ++b) tot = tot + bufsum[b];
+    const double mean = tot / cnt[0];
+    // matrixWave2 - nanmean, into `corrected` (the plane correction's input)
+    for (int64_t k = tid; k < total; k += kPostThreads) a.corrected[k] = a.m[k] - mean;
+    __syncthreads();
+    // plane_correction_with_nan_and_outlier_filter: the four moment passes of k_moments
+    auto moments = [&](int nb, const double* cf, double thr, int mode, double mu, double (&acc)[kMomMax]) {
+#pragma unroll
+        for (int q = 0; q < kMomMax; ++q) acc[q] = 0.0;
+        for (int64_t k = tid; k < total; k += kPostThreads) {
+            const double z = a.corrected[k];
+            if (z != z) continue;
+            const int i = (int)(k / a.nx), j = (int)(k - (int64_t)i * a.nx);
+            double f[5];
+            basis5(i, j, a.ny, a.nx, f);
+            double res = 0.0;
+            if (cf || mode > 0) {
+                double mm = 0.0;
+                for (int t = 0; t < 5; ++t) mm = __builtin_fma(cf[t], f[t], mm);
+                res = z - mm;
+                if (mode == 0 && !(fabs(res) < thr)) continue;
+            }
+            if (mode == 1) {
+                acc[0] += res;
+                acc[20] += 1.0;
+            } else if (mode == 2) {
+                const double d = res - mu;
+                acc[0] = __builtin_fma(d, d, acc[0]);
+                acc[20] += 1.0;
+            } else {
+#pragma unroll
+                for (int r = 0; r < 5; ++r) {
+#pragma unroll
+                    for (int c = r; c < 5; ++c) {
+                        const int q = r * 5 - r * (r - 1) / 2 + (c - r);
+                        if (nb == 5 || c < 3) acc[q] = __builtin_fma(f[r], f[c], acc[q]);
+                    }
+                    if (nb == 5 || r < 3) acc[15 + r] = __builtin_fma(f[r], z, acc[15 + r]);
+                }
+                acc[20] += 1.0;
+            }
+        }
+        block_sum<kMomMax>(acc, red);
+    };
+    // the normal equations of nb terms from the moment slots (pupilmap._normal_solve) into sys[25..]
+    auto normal_solve = [&](const double (&mom)[kMomMax], int nb, int at) {
+        if (tid == 0) {
+            double A[25], b[5];
+            for (int r = 0; r < nb; ++r) {
+                for (int c = 0; c < nb; ++c) {
+                    const int lo = r < c ? r : c, hi = r < c ? c : r;
+                    A[r * nb + c] = mom[lo * 5 - lo * (lo - 1) / 2 + (hi - lo)];
+                }
+                b[r] = mom[15 + r];
+            }
+            if (!solve_small(A, b, nb)) sflag |= 2;
+            for (int r = 0; r < nb; ++r) sys[at + r] = b[r];
+        }
+        __syncthreads();
+    };
+    if (tid == 0) sflag = 0;
+    double acc[kMomMax];
+    moments(5, nullptr, 0.0, 0, 0.0, acc);
+    if (tid == 0 && acc[20] < 5) sflag |= 1;  // curve_fit refuses fewer points than parameters
+    normal_solve(acc, 5, 0);                  // c1 = sys[0..5)
+    moments(5, sys, 0.0, 1, 0.0, acc);
+    const double n1 = acc[20], mu = acc[0] / acc[20];
+    moments(5, sys, 0.0, 2, mu, acc);
+    const double thr = a.sigma * sqrt(acc[0] / n1);
+    moments(3, sys, thr, 0, 0.0, acc);
+    if (tid == 0 && acc[20] < 3) sflag |= 1;
+    normal_solve(acc, 3, 8);                  // p2 = sys[8..11)
+    for (int64_t k = tid; k < total; k += kPostThreads) {
+        const int i = (int)(k / a.nx), j = (int)(k - (int64_t)i * a.nx);
+        double f[5];
+        basis5(i, j, a.ny, a.nx, f);
+        const double pl = __builtin_fma(sys[10], f[2], __builtin_fma(sys[9], f[1], sys[8] * f[0]));
+        const double v = a.corrected[k];
+        a.corrected[k] = v != v ? v : v - pl;
+    }
+    __syncthreads();
+    // psf_calc's rotation estimate (:1122-1132): the first valid row of columns nx / 4 and 3 nx / 4
+    if (tid == 0) {
+        const int c1 = a.nx / 4, c3 = a.nx * 3 / 4;
+        int r1 = 0, r3 = 0;
+        while (r1 < a.ny && a.corrected[(int64_t)r1 * a.nx + c1] != a.corrected[(int64_t)r1 * a.nx + c1]) ++r1;
+        while (r3 < a.ny && a.corrected[(int64_t)r3 * a.nx + c3] != a.corrected[(int64_t)r3 * a.nx + c3]) ++r3;
+        const double q = (r1 < a.ny && r3 < a.ny) ? (double)(r1 - r3) / (double)(c1 - c3) : __builtin_nan("");
+        const double rot = atan(q);
+        const double deg = rot * (180.0 / 3.14159265358979323846);
+        const double cs = cos_deg(deg), sn = sin_deg(deg);
+        const double cy = (a.ny - 1) / 2.0, cx = (a.nx - 1) / 2.0;
+        sys[16] = rot;
+        sys[17] = deg;
+        sys[18] = cs;
+        sys[19] = sn;
+        sys[20] = cy - (cs * cy + sn * cx);
+        sys[21] = cx - (-sn * cy + cs * cx);
+    }
+    __syncthreads();
+    // rotate_with_nan(order 3): NaN split, the B-spline prefilter along both axes, the rotation
+    for (int64_t k = tid; k < total; k += kPostThreads) {
+        const double v = a.corrected[k];
+        const bool nan = v != v;
+        a.coef[k] = nan ? 0.0 : v;
+        a.coef[total + k] = nan ? 0.0 : 1.0;
+    }
+    __syncthreads();
+    for (int l = tid; l < 2 * a.nx; l += kPostThreads)
+        spline_line(a.coef + (int64_t)(l / a.nx) * total + (l % a.nx), a.ny, a.nx);
+    __syncthreads();
+    for (int l = tid; l < 2 * a.ny; l += kPostThreads)
+        spline_line(a.coef + (int64_t)(l / a.ny) * total + (int64_t)(l % a.ny) * a.nx, a.nx, 1);
+    __syncthreads();
+    RotArgs ra{a.coef, a.ny, a.nx, sys[18], sys[19], -sys[19], sys[18], sys[20], sys[21], a.rotated, a.opd};
+    for (int64_t k = tid; k < total; k += kPostThreads) rotate_pixel(ra, k);
+    if (tid == 0) {
+        P[0] = mean;
+        P[1] = cnt[0];
+        for (int q = 0; q < 5; ++q) P[2 + q] = sys[q];
+        for (int q = 0; q < 3; ++q) P[7 + q] = sys[8 + q];
+        P[10] = thr;
+        for (int q = 0; q < 6; ++q) P[11 + q] = sys[16 + q];
+        P[17] = (double)sflag;
     }
 }
 
@@ -389,6 +690,16 @@ int akb_plane_subtract_f64(const double* z, int ny, int nx, const double* d_coef
     AKB_REQUIRE(z && d_coef3 && out && ny > 0 && nx > 0, "bad arguments");
     k_plane_subtract<<<grid_for((int64_t)ny * nx), kBlock, 0, (hipStream_t)stream>>>(z, ny, nx, d_coef3, out);
     return launch_status("k_plane_subtract");
+}
+
+int akb_pupil_post_f64(const double* map, int ny, int nx, double sigma, double* corrected, double* rotated,
+                       double* opd, void* work, double* d_params, void* stream) {
+    clear_error();
+    AKB_REQUIRE(map && corrected && rotated && opd && work && d_params && ny > 1 && nx > 1, "bad arguments");
+    AKB_REQUIRE((int64_t)ny * nx <= kPostMax, "the one-workgroup post handles maps of up to 65536 points");
+    PostArgs a{map, ny, nx, sigma, corrected, rotated, opd, (double*)work, d_params};
+    k_pupil_post<<<1, kPostThreads, 0, (hipStream_t)stream>>>(a);
+    return launch_status("k_pupil_post");
 }
 
 int akb_legendre_rows_f64(const double* data, int n, int K, int order, const double* px, const double* py,

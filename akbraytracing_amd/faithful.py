@@ -1,0 +1,226 @@
+"""The reference's own PSF of a traced run, pipelined on the device.
+
+plot_result_debug's 'ray_wave' step after the trace (AKB_raytrace_20250312.py:3653-3700):
+
+    grid_H, grid_V = meshgrid(linspace(min, max) of detcenter2[1], [2])        :3654-3657
+    matrixWave2 = griddata((y, z), Wave2, (grid_H, grid_V), 'cubic')            :3689
+    matrixWave2 -= nanmean(matrixWave2);  plane_correction_...(matrixWave2)     :3690, :3693
+    psf_calc(matrixWave2_Corrected, grid_H, grid_V, defocusWave)                :3698-3700
+
+FaithfulPupil runs it for run after run without a host wait on the queuing thread:
+
+  begin(y, z)   on the caller's stream: the cell diagonals and checks (akb_gd_cells_f64), the
+                boundary ring to pinned host memory; a worker thread then builds the hull pockets
+                (akb_gd_pockets, host C++ - the only host step, off the GIL);
+  finish(t, f)  once that ticket's pockets are built: the pocket arrays to the device, their
+                local-Delaunay check, the target axes from the ring (akb_gd_axes_f64), griddata by
+                the cone solve (akb_gd_cone_eval_f64: claims, CONE_SWEEPS Chebyshev sweeps formed
+                only where the targets read them, the Clough-Tocher patches), the nanmean removal,
+                plane correction, rotation estimate and rotate_with_nan in one workgroup
+                (akb_pupil_post_f64), and the pad-16 PSF (akb_psf_f64). All on the stream, no host
+                synchronisation; errors the reference would raise surface in Ticket.check().
+
+The host-synchronous drop-ins (griddata.griddata, pupilmap.wave_pupil, psfcalc.psf_calc) stay the
+API for single calls; tests/test_faithful_gpu.py holds this pipeline to them and to the
+reference's own PSF.
+"""
+import concurrent.futures
+
+import numpy as np
+import torch
+
+from . import _lib
+from . import device as D
+from .griddata import CONE_SWEEPS, _F_NEG, _F_NONCONVEX, _F_NONFINITE, _F_NOT_DELAUNAY, _F_POCKET, _F_POS
+from .griddata import chebyshev_weights
+from .psf import psf_stack
+from .pupilmap import pupil_post, pupil_post_check
+
+EUV = 13.5e-9  # option_energy 'EUV' (:1161-1162)
+
+
+class Ticket:
+    """One run in the pipeline: its slot, the tensors it reads, the pocket job, then its results."""
+
+    __slots__ = ("slot", "y", "z", "f", "job", "npock", "result", "h2d", "status", "finished")
+
+    def ready(self):
+        return self.job.done()
+
+    def check(self):
+        """Raise as the host chain would (waits for the device): non-finite hits, a lattice that is
+        not a convex unfolded grid, pockets that are not locally Delaunay, too few points for the
+        plane fits."""
+        self.job.result()
+        st = int(self.status.item())
+        if st & (_F_NOT_DELAUNAY | _F_POCKET):
+            raise _lib.AKBError("griddata: the grid is too distorted for the structured Delaunay triangulation")
+        if self.result is not None:
+            pupil_post_check(self.result["params"])
+
+
+class FaithfulPupil:
+    """The faithful pupil and PSF of runs traced on an n_v x n_h ray grid (see the module doc).
+    size: the pupil grid (the bench's 128); pad: psf_calc's pad factor (16); slots: runs between
+    begin and finish; workers: pocket builders running at once."""
+
+    def __init__(self, n_v, n_h, size=128, pad=16, wavelengths=(EUV,), sweeps=CONE_SWEEPS, slots=6, workers=4,
+                 delaunay_tol=1e-10):
+        L = _lib.lib()
+        self.dev = D.device()
+        self.nv, self.nh = int(n_v), int(n_h)
+        self.size, self.pad, self.sweeps = int(size), int(pad), int(sweeps)
+        self.lams = [float(w) for w in wavelengths]
+        self.tol = float(delaunay_tol)
+        self.L = 2 * (self.nh - 1) + 2 * (self.nv - 1)
+        nc = (self.nv - 1) * (self.nh - 1)
+        Lr = self.L
+        cap = Lr
+        # pocket arrays in one int32 block: tri (3 cap) | nbr (3 cap) | edge (L) | xptr (L + 1) | xidx (6 cap) | npk
+        self._o = dict(tri=0, nbr=3 * cap, edge=6 * cap, xptr=6 * cap + Lr, xidx=6 * cap + 2 * Lr + 1)
+        self._o["npk"] = self._o["xidx"] + 6 * cap
+        self._pk_len = self._o["npk"] + 1
+        self.slots = []
+        for _ in range(int(slots)):
+            self.slots.append(dict(
+                diag=torch.empty(nc, dtype=torch.uint8, device=self.dev),
+                ring=torch.zeros(2 * Lr + 1, dtype=D.F64, device=self.dev),
+                ring_host=torch.empty(2 * Lr + 1, dtype=D.F64, pin_memory=True),
+                pk_host=torch.zeros(self._pk_len, dtype=torch.int32, pin_memory=True),
+                pk=torch.zeros(self._pk_len, dtype=torch.int32, device=self.dev),
+                status=torch.zeros(1, dtype=torch.int64, device=self.dev),
+                last=None))
+        self._next = 0
+        m = self.size * self.size
+        self.work = torch.empty(int(L.akb_gd_cone_work_bytes(self.nv, self.nh, self.size, self.size, 1)) // 8 + 1,
+                                dtype=D.F64, device=self.dev)
+        self.owner = torch.empty(m, dtype=torch.int32, device=self.dev)
+        self.axes = torch.empty(2 * self.size + 6, dtype=D.F64, device=self.dev)  # gx | gy | extent | pitch
+        self.map = torch.empty((1, self.size, self.size), dtype=D.F64, device=self.dev)
+        self.change = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        self.post = {}
+        self.psf = None
+        self._omegas = D.host_f64(chebyshev_weights(max(self.sweeps, 1)))
+        self.pool = concurrent.futures.ThreadPoolExecutor(max_workers=int(workers), thread_name_prefix="akb-pockets")
+
+    # ------------------------------------------------------------------ stage 1
+    def begin(self, y, z, f, stream=None):
+        """Queue the cell pass of one run's detector hits (y, z: (n,) device rows, e.g. detcenter2[1],
+        [2]; f: its Wave2) on `stream` and start its pocket job. Returns a Ticket."""
+        L = _lib.lib()
+        s = self.slots[self._next]
+        self._next = (self._next + 1) % len(self.slots)
+        if s["last"] is not None:  # the slot's previous run must be through its finish (pinned buffers)
+            prev = s["last"]
+            if not prev.finished:
+                raise RuntimeError("FaithfulPupil: more runs begun than slots before a finish")
+            if prev.h2d is not None:
+                prev.h2d.synchronize()
+        sh = D.stream_handle(stream)
+        Lr = self.L
+        ring = s["ring"]
+        flags = ring.view(torch.int32)[4 * Lr:4 * Lr + 1]
+        st = torch.cuda.current_stream() if stream is None else stream
+        for a in (y, z, f):  # read on this stream now and in finish: not to be reused before
+            a.record_stream(st)
+        with torch.cuda.stream(st):
+            flags.zero_()
+            _lib.check(L.akb_gd_cells_f64(D.ptr(y), D.ptr(z), self.nv, self.nh, D.ptr(s["diag"]), self.tol,
+                                          D.ptr(flags), D.ptr(ring[:Lr]), D.ptr(ring[Lr:2 * Lr]), sh))
+            s["ring_host"].copy_(ring, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(st)
+        t = Ticket()
+        t.slot, t.y, t.z, t.f = s, y, z, f
+        t.npock, t.result, t.h2d, t.status, t.finished = None, None, None, s["status"], False
+        t.job = self.pool.submit(self._pockets, s, ev)
+        s["last"] = t
+        return t
+
+    def _pockets(self, s, ev):
+        """Worker thread: wait for the ring on the host, check the cell flags, build the pockets."""
+        ev.synchronize()
+        L = _lib.lib()
+        Lr = self.L
+        rb = s["ring_host"].numpy()
+        fl = int(rb[2 * Lr:].view(np.int32)[0])
+        if fl & _F_NONFINITE:
+            raise ValueError("griddata: non-finite point coordinates (a ray that missed)")
+        if fl & _F_NONCONVEX or (fl & _F_POS and fl & _F_NEG):
+            raise _lib.AKBError("griddata: the points do not form a convex, unfolded lattice")
+        if fl & _F_NOT_DELAUNAY:
+            raise _lib.AKBError("griddata: the grid is too distorted for the structured Delaunay triangulation")
+        buf = s["pk_host"].numpy()
+        o = self._o
+        hp = lambda k: buf[o[k]:].ctypes.data_as(_lib.c_vp)  # noqa: E731
+        _lib.check(L.akb_gd_pockets(rb[:Lr].ctypes.data_as(_lib.c_vp), rb[Lr:2 * Lr].ctypes.data_as(_lib.c_vp),
+                                    self.nv, self.nh, Lr, hp("npk"), hp("tri"), hp("nbr"), hp("edge"), hp("xptr"),
+                                    hp("xidx")))
+        return int(buf[o["npk"]])
+
+    # ------------------------------------------------------------------ stage 2
+    def finish(self, t, stream=None, events=None):
+        """Queue the rest of ticket t's chain on `stream` (waits for its pocket job on the host -
+        normally long done). Returns dict(psf (B, P, P) device, map, corrected, rotated, params);
+        the buffers are reused by the next finish on the stream. events: optional (start, end)
+        timing events recorded around the device work."""
+        L = _lib.lib()
+        t.npock = t.job.result()
+        s = t.slot
+        st = torch.cuda.current_stream() if stream is None else stream
+        sh = D.stream_handle(st)
+        o, Lr = self._o, self.L
+        with torch.cuda.stream(st):
+            if events is not None:
+                events[0].record(st)
+            s["pk"].copy_(s["pk_host"], non_blocking=True)
+            t.h2d = torch.cuda.Event()
+            t.h2d.record(st)
+            pk = s["pk"]
+            k = max(t.npock, 1)
+            ptri, pnbr = pk[o["tri"]:o["tri"] + 3 * k], pk[o["nbr"]:o["nbr"] + 3 * k]
+            edge, xptr, xidx = pk[o["edge"]:o["edge"] + Lr], pk[o["xptr"]:o["xptr"] + Lr + 1], pk[o["xidx"]:]
+            tri = (D.ptr(t.y), D.ptr(t.z), self.nv, self.nh, D.ptr(s["diag"]), t.npock, D.ptr(ptri), D.ptr(pnbr),
+                   D.ptr(edge))
+            s["status"].zero_()
+            _lib.check(L.akb_gd_check_pockets(*tri, self.tol, D.ptr(s["status"]), sh))
+            m = self.size
+            gx, gy = self.axes[:m], self.axes[m:2 * m]
+            ring = s["ring"]
+            _lib.check(L.akb_gd_axes_f64(D.ptr(ring[:Lr]), D.ptr(ring[Lr:2 * Lr]), Lr, m, m, D.ptr(gx), D.ptr(gy),
+                                         D.ptr(self.axes[2 * m:]), sh))
+            self.change.zero_()
+            _lib.check(L.akb_gd_cone_eval_f64(*tri, D.ptr(xptr), D.ptr(xidx), D.ptr(gx), m, D.ptr(gy), m,
+                                              D.ptr(t.f), 1, self.sweeps, self._omegas, D.ptr(self.work),
+                                              D.ptr(self.owner), D.ptr(self.map), D.ptr(self.change), sh))
+            post = pupil_post(self.map[0], out=self.post, stream=st)
+            self.post = post
+            psf, _, _ = psf_stack(post["opd"], None, self.lams, None, pad_factor=self.pad, stream=st, out=self.psf,
+                                  pitch=self.axes[2 * m + 4:2 * m + 6])
+            self.psf = psf
+            if events is not None:
+                events[1].record(st)
+        t.result = dict(psf=psf, map=self.map[0], corrected=post["corrected"], rotated=post["rotated"],
+                        params=post["params"], axes=self.axes, change=self.change)
+        t.y = t.z = t.f = None
+        t.finished = True
+        return t.result
+
+    def run(self, y, z, f, stream=None):
+        """begin + finish of one run (the pocket job waited for at once)."""
+        return self.finish(self.begin(y, z, f, stream), stream)
+
+    def close(self):
+        self.pool.shutdown(wait=True)
+
+
+def image_axes_of(result, pad=16, wavelength=EUV, defocus=1e-2):
+    """x_im, y_im of psf_calc for a finished result (host): the pupil pitch after the driver's
+    grid_H -= mean (:3698) from the device axes."""
+    from .psf import image_axes
+    a = result["axes"].cpu().numpy()
+    m = (a.size - 6) // 2
+    gh, gv = np.meshgrid(a[:m], a[m:2 * m])
+    gh, gv = gh - np.mean(gh), gv - np.mean(gv)
+    dx, dy = np.abs(gh[0, 1] - gh[0, 0]), np.abs(gv[1, 0] - gv[0, 0])
+    return image_axes(m * pad, m * pad, dx, dy, wavelength, defocus)

@@ -32,6 +32,23 @@ _F_NONCONVEX, _F_NOT_DELAUNAY, _F_POCKET, _F_POS, _F_NEG, _F_NONFINITE = 1, 2, 4
 # included; tests/test_gpu_parity.py::test_griddata_default_tol_margin).
 GRADIENT_TOL = 1e-6
 
+# Fixed sweep count of the cone solve (interp_cone): the Chebyshev iteration contracts by ~0.27 a
+# sweep, so after 14 sweeps from zero the gradients sit within ~1e-8 of their scale of the fixed
+# point, and the interpolated values within ~1e-8 of the map's range (1001^2 C3 hits onto the 128^2
+# pupil: 1.7e-7 after 12 sweeps; tests/test_gpu_parity.py::test_gradient_cone_on_the_c3_hits,
+# DESIGN.md §7.1). 14 is the patch kernel's largest (its (2K + 4)^2 box fills 32^2 in LDS).
+CONE_SWEEPS = 14
+
+
+def chebyshev_weights(count, rho=0.5):
+    """omegas[k]: the weight of the sweep that reads x_k (omegas[0] unused: a plain first sweep),
+    Chebyshev semi-iteration for a Jacobi spectrum in [-rho, rho]."""
+    rho2 = rho * rho
+    om = [1.0]
+    for k in range(1, count + 1):
+        om.append(2.0 / (2.0 - rho2) if k == 1 else 1.0 / (1.0 - rho2 * om[-1] / 4.0))
+    return om
+
 
 def _dev(a, dev, dtype=D.F64):
     if isinstance(a, torch.Tensor):
@@ -154,10 +171,8 @@ class CubicGrid:
         shape = (nvals, self.nv * self.nh, 2)
         change = torch.zeros(maxiter + 1, dtype=torch.int64, device=self.dev)
         s = D.stream_handle()
-        rho2 = float(os.environ.get("AKB_GD_RHO", "0.5")) ** 2  # spectral radius 1/2 (A/B knob), squared
-        omegas = [1.0]
-        for k in range(1, maxiter + 1):
-            omegas.append(2.0 / (2.0 - rho2) if k == 1 else 1.0 / (1.0 - rho2 * omegas[-1] / 4.0))
+        # spectral radius 1/2 (AKB_GD_RHO: an A/B knob)
+        omegas = chebyshev_weights(maxiter, float(os.environ.get("AKB_GD_RHO", "0.5")))
         if method == "chebyshev":
             # iterate k in g[k % 4] (a launch reads x_k, x_{k-1} and writes x_{k+1}, x_{k+2}); x_0 = 0
             g = [torch.empty(shape, dtype=D.F64, device=self.dev) for _ in range(4)]
@@ -246,6 +261,33 @@ class CubicGrid:
         out = torch.empty((nvals, my, mx), dtype=D.F64, device=self.dev)
         _lib.check(L.akb_gd_eval_f64(*self._tri_args(), D.ptr(gx), mx, D.ptr(gy), my, D.ptr(f), D.ptr(grad), nvals,
                                      D.ptr(owner), D.ptr(out), D.stream_handle()))
+        return out
+
+    def interp_cone(self, values, gx, gy, sweeps=CONE_SWEEPS, stream=None):
+        """interp with the gradients of exactly `sweeps` Chebyshev sweeps from zero, formed only where
+        the targets read them (akb_gd_cone_eval_f64: a patch per interior target cell, the boundary
+        band globally). Equal bit for bit to interp on gradients(maxiter=sweeps, tol=0); one launch
+        sequence, no host synchronisation. self.cone_change: the change one more sweep would make
+        at the interior target cells' corners (device, scipy's measure as ordered double bits)."""
+        L = _lib.lib()
+        if not self._checked:
+            self._check_status()
+        f = _dev(values, self.dev).reshape(-1, self.nv * self.nh).contiguous()
+        gx = _dev(gx, self.dev).reshape(-1)
+        gy = _dev(gy, self.dev).reshape(-1)
+        mx, my = int(gx.numel()), int(gy.numel())
+        nvals = int(f.shape[0])
+        need = int(L.akb_gd_cone_work_bytes(self.nv, self.nh, mx, my, nvals))
+        work = torch.empty(need // 8 + 1, dtype=D.F64, device=self.dev)
+        owner = torch.empty(mx * my, dtype=torch.int32, device=self.dev)
+        out = torch.empty((nvals, my, mx), dtype=D.F64, device=self.dev)
+        self.cone_change = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        om = chebyshev_weights(max(int(sweeps), 1))
+        _lib.check(L.akb_gd_cone_eval_f64(*self._tri_args(), D.ptr(self.xptr), D.ptr(self.xidx), D.ptr(gx), mx,
+                                          D.ptr(gy), my, D.ptr(f), nvals, int(sweeps), D.host_f64(om), D.ptr(work),
+                                          D.ptr(owner), D.ptr(out), D.ptr(self.cone_change),
+                                          D.stream_handle(stream)))
+        self.sweeps = int(sweeps)
         return out
 
 

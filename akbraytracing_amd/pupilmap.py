@@ -192,3 +192,41 @@ def wave_pupil(detcenter2, wave2, ray_num_H, ray_num_V, grid_num_H=None, grid_nu
     s, c = RowSums()(m_wave.reshape(1, -1), nan=True)
     m_wave = m_wave - (s / c.to(D.F64))[0]
     return _plane_corrections([m_wave.contiguous()])[0], grid_H, grid_V, cg.sweeps
+
+
+POST_PARAMS = 18  # akb_pupil_post_f64's parameter block (include/akb_raytrace.h)
+
+
+def pupil_post(m, sigma_threshold=3, out=None, stream=None):
+    """The driver's chain from a gridded Wave2 map to compute_psf_fft's input in one device launch,
+    no host round trip (akb_pupil_post_f64): matrixWave2 - nanmean -> plane correction ->
+    psf_calc's rotation estimate and rotate_with_nan (:3690-3700, :9630-9693, :1121-1188).
+    m: (ny, nx) device map, ny * nx <= 65536. out: optional dict of preallocated buffers.
+    Returns dict(corrected, rotated, opd, params) of device tensors; params[17] holds error flags
+    (bit 0: too few points for the fits, bit 1: a singular normal system), read by the caller when
+    it can wait (pupil_post_check)."""
+    L = _lib.lib()
+    m = _as_dev(m)
+    ny, nx = int(m.shape[0]), int(m.shape[1])
+    o = out if out is not None else {}
+    for k in ("corrected", "rotated", "opd"):
+        if k not in o or tuple(o[k].shape) != (ny, nx):
+            o[k] = torch.empty((ny, nx), dtype=D.F64, device=m.device)
+    if "work" not in o or o["work"].numel() < 2 * ny * nx:
+        o["work"] = torch.empty(2 * ny * nx, dtype=D.F64, device=m.device)
+    if "params" not in o:
+        o["params"] = torch.empty(POST_PARAMS, dtype=D.F64, device=m.device)
+    _lib.check(L.akb_pupil_post_f64(D.ptr(m), ny, nx, float(sigma_threshold), D.ptr(o["corrected"]),
+                                    D.ptr(o["rotated"]), D.ptr(o["opd"]), D.ptr(o["work"]), D.ptr(o["params"]),
+                                    D.stream_handle(stream)))
+    return o
+
+
+def pupil_post_check(params):
+    """Raise as the host chain would for a pupil_post parameter block (host copy or device tensor)."""
+    p = params.cpu().numpy() if isinstance(params, torch.Tensor) else np.asarray(params)
+    flags = int(p[17])
+    if flags & 1:
+        raise TypeError(f"Improper input: the plane fit needs more finite points (N={int(p[1])})")
+    if flags & 2:
+        raise np.linalg.LinAlgError("Singular matrix")

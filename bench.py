@@ -101,6 +101,14 @@ def parse():
                         "hidden behind the chain's FP64 arithmetic), step k-3's pupil / PSF on the back stream; "
                         "1: the tilt only, the OPD on the back stream; 0: the tilt as its own kernel on the back "
                         "stream beside pass 1")
+    p.add_argument("--pupil-mode", choices=("faithful", "standin"), default="faithful",
+                   help="faithful (default): each step's PSF is the reference's own - griddata(cubic) of Wave2 "
+                        "(cone solve), nanmean removal, plane correction, psf_calc - pipelined on the back stream "
+                        "(akbraytracing_amd/faithful.py); standin: RayWave.pupil's ray-index sampler (rounds 1-3)")
+    p.add_argument("--faithful-lag", type=int, default=3,
+                   help="faithful runs whose pocket jobs may be in flight before a step waits for the oldest")
+    p.add_argument("--no-ramp-form", action="store_true",
+                   help="skip the timed steps before the clock ramp (ms_per_step_no_ramp)")
     p.add_argument("--psf-start", choices=("pupil", "pass1"), default="pupil",
                    help="side-stream PSF starts as soon as the previous pupil is ready, beside pass 1 "
                         "(default; measured faster), or after this step's pass 1")
@@ -442,10 +450,43 @@ def main():
             done.record(side)
         state["psf_done"] = done
 
+    faithful = args.pupil_mode == "faithful" and world == 1
+    fp = None
+    tickets = []
+    fp_events = []
+    if faithful:
+        from akbraytracing_amd.faithful import FaithfulPupil
+        fp = FaithfulPupil(n, n, size=args.pupil, pad=args.pad, wavelengths=my_lams,
+                           slots=args.faithful_lag + 3)
+
+    def faithful_back(timed, f):
+        """The reference's pupil and PSF of the oldest front: its tilt and OPD were fused into later
+        passes 1, so its rows are final; the cell pass and the pocket job start now, and the runs
+        whose pockets are built (or the oldest, once --faithful-lag are in flight) finish on the
+        back stream - griddata, plane correction, psf_calc, PSF - beside the next passes."""
+        bs = back_stream
+        with torch.cuda.stream(bs):
+            out = rw.launch_back(f, stream=bs)
+            d2 = out["detcenter2"]
+            if timed:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(bs)
+            tickets.append(fp.begin(d2[1], d2[2], out["wave2"], stream=bs))
+            if timed:
+                e1.record(bs)
+                fp_events.append(("begin", e0, e1))
+            while tickets and (tickets[0].ready() or len(tickets) > args.faithful_lag):
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if timed else None
+                fp.finish(tickets.pop(0), stream=bs, events=ev)
+                if timed:
+                    fp_events.append(("finish", ev[0], ev[1]))
+
     def back(timed, f=None):
         """Tilt (unless already fused into the next pass 1), OPD and pupil of the oldest front (on
         the back stream, beside the next pass 1 / during the resample), then its PSF."""
         f = f if f is not None else fronts.pop(0)
+        if faithful:
+            return faithful_back(timed, f)
         bs = back_stream if args.back_stream else torch.cuda.current_stream()
         with torch.cuda.stream(bs):
             rw.launch_back(f, stream=bs if args.back_stream else None)
@@ -479,6 +520,31 @@ def main():
         else:
             fronts.append(rw.launch_front(overlap=(lambda: back(timed)) if fronts else None, **kw))
 
+    def timed_steps(k):
+        comm.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        hm = []
+        for _ in range(k):
+            h0 = time.perf_counter()
+            step(True)
+            hm.append((time.perf_counter() - h0) * 1e3)
+        torch.cuda.synchronize()
+        comm.barrier()
+        return time.perf_counter() - t0, hm
+
+    # the driver's form without the clock ramp, in the same process: W warm-up steps, K timed
+    no_ramp_ms = None
+    if args.ramp_ms > 0 and not args.no_ramp_form:
+        for _ in range(args.warmup):
+            step(False)
+        el0, _ = timed_steps(args.steps)
+        t = comm.allreduce_max(torch.tensor([el0], dtype=torch.float64, device=dev))
+        no_ramp_ms = float(t.item()) / args.steps * 1e3
+        rw.kernel_events = None
+        fp_events.clear()
+        psf_events.clear()
+
     ramp_steps = 0
     if args.ramp_ms > 0:
         torch.cuda.synchronize()
@@ -495,23 +561,23 @@ def main():
     for _ in range(args.warmup):
         step(False)
     rw.kernel_events = [] if os.environ.get("AKB_BENCH_NO_KEVENTS", "0") == "0" else None
-    comm.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    host_ms = []  # host time spent issuing each step (its waits included): is the host the limit?
-    for _ in range(args.steps):
-        h0 = time.perf_counter()
-        step(True)
-        host_ms.append((time.perf_counter() - h0) * 1e3)
-    torch.cuda.synchronize()
-    comm.barrier()
-    el = time.perf_counter() - t0
+    fp_events.clear()
+    # host_ms: host time spent issuing each step (its waits included): is the host the limit?
+    el, host_ms = timed_steps(args.steps)
     while fronts:  # the last front's back half (outside the timed region, like the first one's)
         back(False)
+    while tickets:
+        fp.finish(tickets.pop(0), stream=back_stream)
     torch.cuda.synchronize()
+    faithful_checked = None
+    if faithful:  # every run's error words (the reference's raises), read now that nothing waits on them
+        for sl in fp.slots:
+            if sl["last"] is not None:
+                sl["last"].check()
+        faithful_checked = sum(1 for sl in fp.slots if sl["last"] is not None)
     psf_alone_ms = psf_device_ms = None
     if rank == 0:  # the PSF's own wall time, nothing beside it (the last pupil: rw.pupil is collective)
-        opd, pitch = state["pupil"]
+        opd, pitch = (fp.post["opd"], None) if faithful else state["pupil"]
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
         for _ in range(10):
@@ -553,10 +619,11 @@ def main():
         st = comm.allreduce_max(torch.tensor([sorted(single)[2]], dtype=torch.float64, device=dev))
         single_ms = float(st.item())
 
-    # steps with the reference's own PSF: each step traces a system (run(): pass 1, resample, pass 2,
-    # tilt, OPD) and forms its faithful PSF (faithful_psf), nothing overlapped across steps
+    # steps with the reference's own PSF through the host-synchronous drop-ins: each step traces a
+    # system (run()) and forms its faithful PSF (faithful_psf: wave_pupil + psf_calc), nothing
+    # overlapped across steps (the pipelined faithful steps are the timed region itself)
     faithful_steps = None
-    if world == 1 and not args.no_extras:
+    if world == 1 and not args.no_extras and not faithful:
         ft = []
         for i in range(args.faithful_steps + 2):
             torch.cuda.synchronize()
@@ -600,6 +667,10 @@ def main():
     k_ms = [a.elapsed_time(b) for a, b in rw.kernel_events] if rw.kernel_events else [float('nan')]
     k_avg = sum(k_ms) / len(k_ms)
     psf_ms = sum(a.elapsed_time(b) for a, b in psf_events) / max(len(psf_events), 1)
+    # the faithful chain's device time per step on the back stream (cell pass + finish), and the
+    # finishes alone (griddata, plane correction, psf_calc, PSF), sharing the GPU with the passes
+    fp_begin = [a.elapsed_time(b) for k, a, b in fp_events if k == "begin"]
+    fp_fin = [a.elapsed_time(b) for k, a, b in fp_events if k == "finish"]
     launch_bytes = PASS2_BYTES_PER_RAY * rw.n_local
     achieved = launch_bytes / (k_avg * 1e-3) / 1e9
     prof, prof_file, prof_ok = read_profile()
@@ -621,6 +692,10 @@ def main():
         "warmup": args.warmup,
         "clock_ramp": {"ms": args.ramp_ms, "untimed_steps": ramp_steps},
         "ms_per_step": el / args.steps * 1e3,
+        # the same K steps timed in this process after the W warm-up steps alone, before the clock
+        # ramp: the driver's plain W / K form (null with --no-ramp-form or --ramp-ms 0)
+        "ms_per_step_no_ramp": no_ramp_ms,
+        "untimed_steps_before_timing": (args.warmup + (args.warmup + args.steps if no_ramp_ms else 0) + ramp_steps),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -630,6 +705,9 @@ def main():
         "config": {
             "workload": ("C2: 2-mirror KB ray trace (2 passes, tilt, OPD) + 2048^2 PSF"
                          + (", ray-row shards" if world > 1 else "") if args.config == "c2" else
+                         "C3: 4-mirror AKB ray_wave trace (2 passes, tilt, OPD) + the reference's pupil (griddata "
+                         "cubic, nanmean, plane correction, psf_calc) + 2048^2 PSF" if args.config == "c3"
+                         and world == 1 and faithful else
                          "C3: 4-mirror AKB ray_wave trace (2 passes, tilt, OPD) + 2048^2 PSF" if args.config == "c3"
                          and world == 1 else
                          "C4: 4-mirror AKB ray_wave trace, ray-row shards, + 2048^2 PSF" if args.config == "c3" else
@@ -644,7 +722,14 @@ def main():
             "parallelism": f"ray-row shards x{world}",
         },
         "host_issue_ms_per_step": sorted(host_ms)[len(host_ms) // 2],
-        "psf_ms": psf_ms,
+        "pupil": ("faithful: each step's PSF from the reference's own pupil - griddata(cubic) of Wave2 on the "
+                  f"{n}^2 hits (cone solve, {fp.sweeps} Chebyshev sweeps), nanmean removal, plane correction, "
+                  "psf_calc (rotation, rotate_with_nan, pad 16) - pipelined on the back stream "
+                  f"(akbraytracing_amd/faithful.py; {faithful_checked} runs' error words checked)" if faithful else
+                  "stand-in: RayWave.pupil's ray-index sampler (up to 0.098 nm from the reference's Clough-Tocher)"),
+        "faithful_chain_ms": ((sum(fp_begin) + sum(fp_fin)) / max(len(fp_fin), 1)) if fp_fin else None,
+        "faithful_finish_ms": (sum(fp_fin) / len(fp_fin)) if fp_fin else None,
+        "psf_ms": psf_ms if psf_events else None,
         "psf_alone_ms": psf_alone_ms,
         "psf_device_ms": psf_device_ms,
         # the PSF's compulsory HBM traffic is its output (the pupil is 128 KB): intensity planes
@@ -711,6 +796,18 @@ def main():
         # psf_calc on this trace's 1e7 detector-2 hits
         out["faithful_psf_chain_ms"] = chain_ms
         out["faithful_wave_maps_psf_ms"] = maps_ms
+        if fp is not None:
+            # one run's pipelined chain on its own (begin + pocket job + finish, device synchronised):
+            # its latency, not its share of a step
+            d2 = last_out["detcenter2"]
+            ft = []
+            for _ in range(5):
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                fp.run(d2[1], d2[2], last_out["wave2"])
+                torch.cuda.synchronize()
+                ft.append((time.perf_counter() - t1) * 1e3)
+            out["faithful_pipelined_single_ms"] = sorted(ft)[2]
         if faithful_steps is not None:
             out["faithful_step"] = faithful_steps
         if stage is not None:

@@ -423,6 +423,18 @@ int akb_rotate_with_nan_f64(const double* m, int ny, int nx, const double rot[4]
 
 /* ---------------- pupil-map post-processing (ref AKB_raytrace_20250312.py:9630-9693, legendre_fit.py:59-92) ---------------- */
 
+/* The driver's whole chain from a gridded Wave2 map (ny * nx <= 65536) to compute_psf_fft's input
+ * in one workgroup, no host round trip (AKB_raytrace_20250312.py:3690-3700, :9630-9693,
+ * :1121-1188): corrected = plane_correction_with_nan_and_outlier_filter(map - nanmean(map), sigma),
+ * psf_calc's rotation estimate, rotated = rotate_with_nan(corrected, degrees(rot), order 3)
+ * (cephes cosdg / sindg for scipy.ndimage.rotate's matrix), opd = rotated * 1e-9. work: 2 ny nx
+ * doubles. d_params (18 doubles): nanmean, finite count, the quadratic fit (5), the plane (3), the
+ * outlier threshold, rot, its degrees, cos, sin, the rotation's offset (2), error flags (bit 0: too
+ * few points for curve_fit, bit 1: a singular normal system). Replaces pupilmap._plane_corrections
+ * + psfcalc.rotation_estimate / rotate_with_nan where a pipelined caller cannot wait on the host. */
+int akb_pupil_post_f64(const double* map, int ny, int nx, double sigma, double* corrected, double* rotated,
+                       double* opd, void* work, double* d_params, void* stream);
+
 /* Sums for plane_correction_with_nan_and_outlier_filter (:9630) over the finite points of the
  * (ny, nx) map z, basis f = (1, X, Y, X^2, Y^2) with X = (2j - (nx-1))/(nx-1), Y likewise
  * (the reference's index coordinates, centred and scaled: the same least-squares fits).
@@ -505,6 +517,29 @@ int akb_gd_eval_f64(const double* x, const double* y, int nv, int nh, const uint
                     const int32_t* ptri, const int32_t* pnbr, const int32_t* edge_tri, const double* gx, int mx,
                     const double* gy, int my, const double* f, const double* grad, int nvals, int* owner,
                     double* out, void* stream);
+
+/* The same interpolation with the gradients of exactly K Chebyshev sweeps (1 <= K <= 14, omegas[j]
+ * the weight of sweep j + 1 as CubicGrid.gradients forms them), computed only where the targets
+ * read them: per interior target cell a (2K + 4)^2 patch in LDS, the global iteration on the
+ * boundary band (depth 2K + 2, pocket chords included) for the rest. The values equal
+ * akb_gd_eval_f64 on the global iteration's K-sweep gradients bit for bit; one call, no host
+ * synchronisation. work: akb_gd_cone_work_bytes; d_change (or NULL): the largest change measure
+ * (scipy's, as ordered double bits, atomic max) one more sweep would make at the interior target
+ * cells' corners. Replaces the gradient loop of scipy's estimate_gradients_2d_global
+ * (scipy/interpolate/_interpnd.pyx) where the driver's griddata (AKB_raytrace_20250312.py:3689)
+ * feeds a fixed-size pupil. */
+int64_t akb_gd_cone_work_bytes(int nv, int nh, int mx, int my, int nvals);
+/* The driver's target axes (AKB_raytrace_20250312.py:3654-3657): gx = np.linspace(min, max, mx) of
+ * the lattice's x (its extremes lie on the boundary ring akb_gd_cells_f64 returns), gy likewise of
+ * y; d_extent (or NULL, 6 doubles): [min x, max x, min y, max y, x step, y step] (the steps: the
+ * pupil pitch psf_calc hands compute_psf_fft, :1176-1177). One workgroup, device-resident. */
+int akb_gd_axes_f64(const double* ring_x, const double* ring_y, int64_t L, int mx, int my, double* gx, double* gy,
+                    double* d_extent, void* stream);
+int akb_gd_cone_eval_f64(const double* x, const double* y, int nv, int nh, const uint8_t* diag, int npock,
+                         const int32_t* ptri, const int32_t* pnbr, const int32_t* edge_tri, const int32_t* xptr,
+                         const int32_t* xidx, const double* gx, int mx, const double* gy, int my, const double* f,
+                         int nvals, int K, const double* omegas, void* work, int* owner, double* out,
+                         unsigned long long* d_change, void* stream);
 
 /* diagnostics: out[13i..13i+12] = (the trace's sqrt, sqrt, the trace's shared-reciprocal a/b, a/b,
  * the positive-divisor a/b, the trace's norm and reciprocal norm of (a, b, b), sqrt and 1/sqrt of

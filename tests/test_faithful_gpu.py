@@ -1,0 +1,112 @@
+"""The pipelined faithful PSF (akbraytracing_amd/faithful.py) against the host-synchronous drop-in
+chain and against the reference's own PSF (MI355X).
+
+Bars: the cone gridding is the global iteration's fixed-K result (bit for bit, test_gpu_parity);
+against the converged chain (pupilmap.wave_pupil at scipy's tolerance + psfcalc.psf_calc) the maps
+agree to 3e-8 of their range (the fixed sweep count's distance from the fixed point) and the PSF to
+1e-7 of its peak; against the reference's PSF of its own run (akb_psf_full.npz) to the north star's
+1e-6 of the peak.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden, golden_json
+
+pytestmark = pytest.mark.gpu
+
+
+def _trace(n):
+    from akbraytracing_amd.wavefront import RayWave, SystemGeometry
+    return RayWave(SystemGeometry.from_dict(golden_json("akb_geometry.json")), n).run()
+
+
+def _crop(psf, fp, n):
+    iy0, iy1, ix0, ix1 = (int(v) for v in fp[f"n{n}_psf_win"])
+    return psf[iy0:iy1, ix0:ix1]
+
+
+@pytest.mark.parametrize("n", [1001, pytest.param(3163, marks=pytest.mark.slow)])
+def test_faithful_pipeline_vs_host_chain_and_reference(gpu, n):
+    from akbraytracing_amd import pupilmap as PM
+    from akbraytracing_amd.faithful import FaithfulPupil, image_axes_of
+    from akbraytracing_amd.psfcalc import psf_calc
+    out = _trace(n)
+    d2 = out["detcenter2"]
+    y, z, w2 = d2[1], d2[2], out["wave2"]
+    fp_ = FaithfulPupil(n, n)
+    r = fp_.run(y, z, w2)
+    t = fp_.slots[0]["last"]
+    t.check()
+    torch.cuda.synchronize()
+    # the host chain at scipy's tolerance
+    m, gh, gv, _ = PM.wave_pupil(d2, w2, n, n, grid_num_H=128, grid_num_V=128)
+    a = r["axes"].cpu().numpy()
+    assert np.array_equal(a[:128], gh[0]) and np.array_equal(a[128:256], gv[:, 0])
+    want_c = m.cpu().numpy()
+    got_c = r["corrected"].cpu().numpy()
+    rng_ = np.nanmax(want_c) - np.nanmin(want_c)
+    assert np.array_equal(np.isnan(got_c), np.isnan(want_c))
+    e_map = np.nanmax(np.abs(got_c - want_c)) / rng_
+    GH, GV = gh - np.mean(gh), gv - np.mean(gv)
+    host = psf_calc(m, GH, GV, 1e-2)
+    P = r["psf"][0].cpu().numpy()
+    e_psf = float(np.max(np.abs(P - host["psf"].cpu().numpy())))
+    x_im, y_im = image_axes_of(r)
+    assert np.array_equal(x_im, host["x_im"]) and np.array_equal(y_im, host["y_im"])
+    fp = golden("akb_psf_full.npz")
+    e_ref = float(np.max(np.abs(_crop(P, fp, n) - fp[f"n{n}_psf_crop"])))
+    ch = np.array([int(r["change"].item())]).view(np.float64)[0]
+    print(f"n={n}: pipelined vs host chain: corrected map {e_map:.2e} of the range, PSF {e_psf:.2e} of the peak; "
+          f"vs the reference's PSF {e_ref:.2e}; change at the target corners {ch:.2e}")
+    assert e_map <= 3e-8
+    assert e_psf <= 1e-7
+    assert e_ref <= 1e-6
+    fp_.close()
+
+
+def test_faithful_pipeline_in_flight_runs_equal_one_at_a_time(gpu):
+    """Runs begun several at a time (tickets finished in order, pocket jobs on worker threads) give
+    each run's own PSF bit for bit, as when each is begun and finished alone."""
+    import copy
+    from akbraytracing_amd.faithful import FaithfulPupil
+    from akbraytracing_amd.wavefront import RayWave, SystemGeometry
+    n = 401
+    g = SystemGeometry.from_dict(golden_json("akb_geometry.json"))
+    outs = []
+    for i in range(4):
+        gi = copy.deepcopy(g)
+        gi.det2 = list(gi.det2[:3]) + [gi.det2[3] - 5e-6 * i]
+        o = RayWave(gi, n).run()
+        outs.append((o["detcenter2"][1].clone(), o["detcenter2"][2].clone(), o["wave2"].clone()))
+    fp_ = FaithfulPupil(n, n, slots=3)
+    alone = []
+    for y, z, w in outs:
+        alone.append(fp_.run(y, z, w)["psf"].clone())
+    s = torch.cuda.Stream()
+    tickets, got = [], []
+    with torch.cuda.stream(s):
+        for y, z, w in outs:
+            tickets.append(fp_.begin(y, z, w, stream=s))
+            if len(tickets) == 3:
+                got.append(fp_.finish(tickets.pop(0), stream=s)["psf"].clone())
+        while tickets:
+            got.append(fp_.finish(tickets.pop(0), stream=s)["psf"].clone())
+    torch.cuda.synchronize()
+    for a, b in zip(alone, got):
+        assert torch.equal(a, b)
+    assert not torch.equal(alone[0], alone[3])
+    fp_.close()
+
+
+def test_faithful_pipeline_raises_for_a_missed_ray(gpu):
+    from akbraytracing_amd.faithful import FaithfulPupil
+    n = 65
+    out = _trace(n)
+    y = out["detcenter2"][1].clone()
+    y[n * 10 + 5] = float("nan")
+    fp_ = FaithfulPupil(n, n, slots=2)
+    t = fp_.begin(y, out["detcenter2"][2], out["wave2"])
+    with pytest.raises(ValueError):
+        fp_.finish(t)
+    fp_.close()
