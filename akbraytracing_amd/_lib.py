@@ -45,6 +45,7 @@ EXPORTS = [
     "akb_moments_work_bytes", "akb_map_moments_f64", "akb_plane_subtract_f64", "akb_legendre_rows_f64",
     "akb_gd_cells_f64", "akb_gd_pockets", "akb_gd_check_pockets", "akb_gd_grad_sweep_f64", "akb_gd_grad_sweeps_f64",
     "akb_gd_eval_f64", "akb_gd_cone_work_bytes", "akb_gd_cone_eval_f64", "akb_gd_axes_f64",
+    "akb_gd_claims_f64", "akb_gd_cone_part_f64", "akb_gd_part_finish_f64", "akb_gd_ring_f64", "akb_gd_cells_window_f64",
     "akb_trace_chain_batch_f64", "akb_focus_eval_work_bytes", "akb_focus_eval_f64", "akb_sep_search_f64",
     "akb_finish_params_work_bytes", "akb_finish_tilt_params_f64",
     "akb_valid_mask_u8", "akb_external_contours", "akb_approx_poly_dp", "akb_affine_from_points",
@@ -180,6 +181,14 @@ def _declare(L):
                              c_vp, c_vp, c_int, c_vp, c_vp, c_vp], c_int),
         "akb_gd_cone_work_bytes": ([c_int, c_int, c_int, c_int, c_int], c_i64),
         "akb_gd_axes_f64": ([c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp], c_int),
+        "akb_gd_claims_f64": ([c_vp, c_vp, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp,
+                               c_int, c_vp, c_int, c_vp, c_vp], c_int),
+        "akb_gd_cone_part_f64": ([c_vp, c_vp, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
+                                  c_int, c_vp, c_int, c_vp, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                  c_vp, c_vp], c_int),
+        "akb_gd_part_finish_f64": ([c_vp, c_vp, c_i64, c_int, c_vp], c_int),
+        "akb_gd_ring_f64": ([c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp], c_int),
+        "akb_gd_cells_window_f64": ([c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_dbl, c_vp, c_vp], c_int),
         "akb_gd_cone_eval_f64": ([c_vp, c_vp, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
                                   c_vp, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp], c_int),
     }

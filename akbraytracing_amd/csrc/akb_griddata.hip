@@ -47,7 +47,16 @@ struct Grid {
     const int32_t* xidx;
     int no_xcd;  // 1: plain block order in the sweep (AKB_GD_NOXCD, A/B timing only)
     int strip_rows = kStripRowsDefault;  // rows per strip workgroup (AKB_GD_ROWS, A/B timing)
+    // cell rows [row0, row1) the cell pass and the claims visit (a rank's window of a sharded
+    // lattice: x, y, diag are then "virtual" global arrays of which only the window's rows, plus
+    // two vertex rows below and above, are backed); row1 < 0: every row
+    int row0 = 0, row1 = -1;
 };
+
+__device__ __forceinline__ int64_t win_cell0(const Grid& g) { return (int64_t)g.row0 * (g.nh - 1); }
+__device__ __forceinline__ int64_t win_cell1(const Grid& g) {
+    return (int64_t)(g.row1 < 0 ? g.nv - 1 : g.row1) * (g.nh - 1);
+}
 
 __device__ __forceinline__ int64_t ncells(const Grid& g) { return (int64_t)(g.nv - 1) * (g.nh - 1); }
 
@@ -190,9 +199,10 @@ __device__ int64_t tri_nbr(const Grid& g, int64_t t, int k) {
 // bit 2 a broken pocket adjacency, bits 3 / 4 cells of positive / negative orientation, bit 5 a
 // non-finite point
 __global__ void __launch_bounds__(kBlock) k_gd_cells(Grid g, uint8_t* diag, double tol, unsigned* flags) {
-    const int64_t nc = ncells(g);
+    const int64_t nc = win_cell1(g);
     unsigned acc = 0;
-    for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < nc; c += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t c = win_cell0(g) + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < nc;
+         c += (int64_t)gridDim.x * blockDim.x) {
         const int iv = (int)(c / (g.nh - 1)), ih = (int)(c - (int64_t)iv * (g.nh - 1));
         double bad = 0.0;
         const int d = cell_diag(g, iv, ih, &bad);
@@ -1485,6 +1495,39 @@ __global__ void __launch_bounds__(kBlock) k_gd_axes(const double* __restrict__ r
     lin(e[2], e[3], my, gy);
 }
 
+// a sharded lattice's targets: this rank forms the interior targets whose cell's p00 lies in its
+// rays [own0, own1); the band owner forms every band and pocket target. assigned[t] = 1 for the
+// targets formed here; the interior ones' cells go to the patch list
+__global__ void __launch_bounds__(kBlock) k_gd_cone_assign(Grid g, const int* __restrict__ owner, int64_t m, int K,
+                                                            int64_t own0, int64_t own1, int band_on, int64_t* cells,
+                                                            int* count, int* band, uint8_t* assigned) {
+    const int64_t nc2 = 2 * ncells(g);
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < m; t += (int64_t)gridDim.x * blockDim.x) {
+        const int o = owner[t];
+        uint8_t mine = 0;
+        if (o != INT32_MAX) {
+            bool interior = false;
+            int64_t c = -1, p00 = -1;
+            if (o < nc2) {
+                c = o >> 1;
+                const int iv = (int)(c / (g.nh - 1)), ih = (int)(c - (int64_t)iv * (g.nh - 1));
+                interior = iv - K - 1 >= 1 && iv + K + 2 <= g.nv - 2 && ih - K - 1 >= 1 && ih + K + 2 <= g.nh - 2;
+                p00 = (int64_t)iv * g.nh + ih;
+            }
+            if (interior) {
+                if (p00 >= own0 && p00 < own1) {
+                    cells[atomicAdd(count, 1)] = c;
+                    mine = 1;
+                }
+            } else if (band_on) {
+                atomicOr(band, 1);
+                mine = 1;
+            }
+        }
+        assigned[t] = mine;
+    }
+}
+
 // ------------------------------------------------------------------ targets
 
 struct Targets {
@@ -1590,7 +1633,6 @@ __device__ __forceinline__ bool axis_uniform_part(const double* a, int m, int i)
 }
 
 __global__ void __launch_bounds__(kBlock) k_gd_claim_cells(Grid g, Targets t, int* owner) {
-    const int64_t nc = ncells(g);
     // the index-box estimate below needs evenly spaced axes (np.linspace, the driver's); any other
     // ascending axis takes the exact binary search (lower_idx) of the per-triangle claim
     bool ok = true;
@@ -1598,7 +1640,8 @@ __global__ void __launch_bounds__(kBlock) k_gd_claim_cells(Grid g, Targets t, in
         ok = ok && axis_uniform_part(t.gx, t.mx, i) && axis_uniform_part(t.gy, t.my, i);
     const bool uniform = __syncthreads_and(ok) != 0;
     const double inv_dx = inv_step(t.gx, t.mx), inv_dy = inv_step(t.gy, t.my);
-    for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < nc; c += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t c = win_cell0(g) + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < win_cell1(g);
+         c += (int64_t)gridDim.x * blockDim.x) {
         const int iv = (int)(c / (g.nh - 1)), ih = (int)(c - (int64_t)iv * (g.nh - 1));
         const int64_t p00 = (int64_t)iv * g.nh + ih;
         const double xa = g.x[p00], xb = g.x[p00 + 1], xc = g.x[p00 + g.nh], xd = g.x[p00 + g.nh + 1];
@@ -1724,6 +1767,35 @@ __global__ void __launch_bounds__(kBlock) k_gd_eval(Grid g, Targets t, const int
         bary(g, T, t.gx[c], t.gy[r], b);
         for (int v = 0; v < nvals; ++v) out[v * m + i] = clough_tocher(g, o, T, f + v * n, grad + 2 * v * n, b);
     }
+}
+
+// k_gd_eval for the targets a rank forms (assigned): value and count, zeros elsewhere, so the
+// ranks' pieces add up to the map (a SUM reduction; count 0: outside the hull, NaN)
+__global__ void __launch_bounds__(kBlock) k_gd_eval_part(Grid g, Targets t, const int* __restrict__ owner,
+                                                         const uint8_t* __restrict__ assigned, const double* f,
+                                                         const double* grad, int nvals, double* out, double* cnt) {
+    const int64_t m = (int64_t)t.mx * t.my, n = (int64_t)g.nv * g.nh;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+        if (!assigned[i]) {
+            for (int v = 0; v < nvals; ++v) out[v * m + i] = 0.0;
+            cnt[i] = 0.0;
+            continue;
+        }
+        const int o = owner[i];
+        const int r = (int)(i / t.mx), c = (int)(i - (int64_t)r * t.mx);
+        const Tri T = tri_verts(g, o);
+        double b[3];
+        bary(g, T, t.gx[c], t.gy[r], b);
+        for (int v = 0; v < nvals; ++v) out[v * m + i] = clough_tocher(g, o, T, f + v * n, grad + 2 * v * n, b);
+        cnt[i] = 1.0;
+    }
+}
+
+// the assembled pieces: value where some rank formed it, NaN elsewhere (outside the hull)
+__global__ void k_gd_part_finish(double* out, const double* cnt, int64_t m, int nvals) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x)
+        if (!(cnt[i] > 0))
+            for (int v = 0; v < nvals; ++v) out[v * m + i] = __builtin_nan("");
 }
 
 __global__ void k_fill_i32(int* p, int64_t n, int v) {
@@ -1973,8 +2045,97 @@ int64_t akb_gd_cone_work_bytes(int nv, int nh, int mx, int my, int nvals) {
     const int64_t n = (int64_t)nv * nh, L = 2 * (int64_t)(nh - 1) + 2 * (int64_t)(nv - 1);
     const int nv2 = nvals >= 2 ? 2 : 1;
     const int64_t m = (int64_t)mx * my;
-    return 3 * (int64_t)nv2 * n * 2 * 8 + L * 7 * 8 + m * 8 + 64;
+    return 3 * (int64_t)nv2 * n * 2 * 8 + L * 7 * 8 + m * 8 + m + 64;
 }
+
+namespace {
+
+// the cone solve's claims: owner filled with INT32_MAX, then the window's cells (and the pockets)
+int cone_claims(const Grid& g, const Targets& t, int with_pockets, int* owner, hipStream_t s) {
+    const int64_t m = (int64_t)t.mx * t.my;
+    k_fill_i32<<<grid_for(m, 4), kBlock, 0, s>>>(owner, m, INT32_MAX);
+    int st = launch_status("k_fill_i32");
+    if (st) return st;
+    const int64_t wc = (int64_t)((g.row1 < 0 ? g.nv - 1 : g.row1) - g.row0) * (g.nh - 1);
+    if (wc > 0) {
+        k_gd_claim_cells<<<grid_for(wc, 1, kStreamGridCap), kBlock, 0, s>>>(g, t, owner);
+        if ((st = launch_status("k_gd_claim"))) return st;
+    }
+    if (with_pockets && g.npock > 0) {
+        k_gd_claim_pockets<<<(unsigned)(g.npock < 16384 ? g.npock : 16384), kBlock, 0, s>>>(g, t, owner);
+        if ((st = launch_status("k_gd_claim_pockets"))) return st;
+    }
+    return 0;
+}
+
+// the targets this call forms (own0 .. own1, band_on), their gradients, their values: out / cnt
+// as k_gd_eval_part writes them (cnt == nullptr: k_gd_eval's NaN for unclaimed targets)
+int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int band_on, const double* f, int nvals,
+              int K, const double* omegas, void* work, const int* owner, double* out, double* cnt,
+              unsigned long long* d_change, hipStream_t s) {
+    const int64_t n = (int64_t)g.nv * g.nh, m = (int64_t)t.mx * t.my;
+    const int64_t L = 2 * (int64_t)(g.nh - 1) + 2 * (int64_t)(g.nv - 1);
+    const int nv2 = nvals >= 2 ? 2 : 1;
+    double* gb[3];
+    for (int k = 0; k < 3; ++k) gb[k] = (double*)work + (int64_t)k * nv2 * n * 2;
+    double* ring_acc = (double*)work + 3 * (int64_t)nv2 * n * 2;
+    int64_t* cells = (int64_t*)(ring_acc + L * 7);
+    uint8_t* assigned = (uint8_t*)(cells + m);
+    int* count = (int*)(((uintptr_t)(assigned + m) + 7) & ~(uintptr_t)7);
+    int* band = count + 1;
+    if (hipMemsetAsync(count, 0, 2 * sizeof(int), s) != hipSuccess) return launch_status("hipMemsetAsync");
+    k_gd_cone_assign<<<grid_for(m, 1), kBlock, 0, s>>>(g, owner, m, K, own0, own1, band_on, cells, count, band,
+                                                      assigned);
+    int st = launch_status("k_gd_cone_assign");
+    if (st) return st;
+    // the boundary band: depth <= 2K + 2 (x_K valid to depth K + 3 >= every band target's corners)
+    const BandMap bm = band_map(g.nv, g.nh, 2 * K + 2);
+    ConeStep steps[kConeMaxK + 1];
+    steps[0] = ConeStep{0, 1.0};
+    for (int j = 1; j <= K; ++j)
+        steps[j] = j == 1 ? ConeStep{0, 1.0} : j == 2 ? ConeStep{1, omegas[1]} : ConeStep{2, omegas[j - 1]};
+    const unsigned pg = (unsigned)(m < 8192 ? m : 8192);
+    for (int v0 = 0; v0 < nvals; v0 += 2) {
+        const int nvv = nvals - v0 >= 2 ? 2 : 1;
+        const double* fv = f + v0 * n;
+        if (band_on) {
+            for (int j = 1; j <= K; ++j) {
+                const double* gin = j == 1 ? nullptr : gb[(j - 1) % 3];
+                const double* gprev = j >= 3 ? gb[(j + 1) % 3] : nullptr;
+                if (nvv == 2) {
+                    ConeBand<2> a{fv, gin, gprev, gb[j % 3], ring_acc, steps[j], band};
+                    k_gd_cone_band<2><<<grid_for(bm.total, 1, kStreamGridCap), kBlock, 0, s>>>(g, bm, a);
+                    k_gd_cone_ring<2><<<grid_for(L * 64), kBlock, 0, s>>>(g, a);
+                } else {
+                    ConeBand<1> a{fv, gin, gprev, gb[j % 3], ring_acc, steps[j], band};
+                    k_gd_cone_band<1><<<grid_for(bm.total, 1, kStreamGridCap), kBlock, 0, s>>>(g, bm, a);
+                    k_gd_cone_ring<1><<<grid_for(L * 64), kBlock, 0, s>>>(g, a);
+                }
+                if ((st = launch_status("k_gd_cone_band"))) return st;
+            }
+        }
+        if (nvv == 2) {
+            ConePatch<2> a{fv, cells, count, K, {}, gb[K % 3], d_change};
+            for (int j = 0; j <= K; ++j) a.st[j] = steps[j];
+            k_gd_cone_patch<2><<<pg, 256, 0, s>>>(g, a);
+        } else {
+            ConePatch<1> a{fv, cells, count, K, {}, gb[K % 3], d_change};
+            for (int j = 0; j <= K; ++j) a.st[j] = steps[j];
+            k_gd_cone_patch<1><<<pg, 256, 0, s>>>(g, a);
+        }
+        if ((st = launch_status("k_gd_cone_patch"))) return st;
+        if (cnt)
+            k_gd_eval_part<<<grid_for(m, 1, kStreamGridCap), kBlock, 0, s>>>(g, t, owner, assigned, fv, gb[K % 3], nvv,
+                                                                              out + v0 * m, cnt);
+        else
+            k_gd_eval<<<grid_for(m, 1, kStreamGridCap), kBlock, 0, s>>>(g, t, owner, fv, gb[K % 3], nvv,
+                                                                         out + v0 * m);
+        if ((st = launch_status("k_gd_eval"))) return st;
+    }
+    return 0;
+}
+
+}  // namespace
 
 int akb_gd_cone_eval_f64(const double* x, const double* y, int nv, int nh, const uint8_t* diag, int npock,
                          const int32_t* ptri, const int32_t* pnbr, const int32_t* edge_tri, const int32_t* xptr,
@@ -1990,67 +2151,70 @@ int akb_gd_cone_eval_f64(const double* x, const double* y, int nv, int nh, const
     hipStream_t s = (hipStream_t)stream;
     Grid g{x, y, nv, nh, diag, npock, ptri, pnbr, edge_tri, xptr, xidx};
     Targets t{gx, gy, mx, my};
-    const int64_t n = (int64_t)nv * nh, m = (int64_t)mx * my;
-    const int64_t L = 2 * (int64_t)(nh - 1) + 2 * (int64_t)(nv - 1);
-    const int nv2 = nvals >= 2 ? 2 : 1;
-    double* gb[3];
-    for (int k = 0; k < 3; ++k) gb[k] = (double*)work + (int64_t)k * nv2 * n * 2;
-    double* ring_acc = (double*)work + 3 * (int64_t)nv2 * n * 2;
-    int64_t* cells = (int64_t*)(ring_acc + L * 7);
-    int* count = (int*)(cells + m);
-    int* band = count + 1;
-    // claims (akb_gd_eval_f64's)
-    k_fill_i32<<<grid_for(m, 4), kBlock, 0, s>>>(owner, m, INT32_MAX);
-    int st = launch_status("k_fill_i32");
+    int st = cone_claims(g, t, 1, owner, s);
     if (st) return st;
-    const int64_t ntri = 2 * (int64_t)(nv - 1) * (nh - 1) + npock;
-    k_gd_claim_cells<<<grid_for((ntri - npock) / 2, 1, kStreamGridCap), kBlock, 0, s>>>(g, t, owner);
-    if ((st = launch_status("k_gd_claim"))) return st;
-    if (npock > 0) {
-        k_gd_claim_pockets<<<(unsigned)(npock < 16384 ? npock : 16384), kBlock, 0, s>>>(g, t, owner);
-        if ((st = launch_status("k_gd_claim_pockets"))) return st;
-    }
-    if (hipMemsetAsync(count, 0, 2 * sizeof(int), s) != hipSuccess) return launch_status("hipMemsetAsync");
-    k_gd_cone_targets<<<grid_for(m, 1), kBlock, 0, s>>>(g, owner, m, K, cells, count, band);
-    if ((st = launch_status("k_gd_cone_targets"))) return st;
-    // the boundary band: depth <= 2K + 2 (x_K valid to depth K + 3 >= every band target's corners)
-    const BandMap bm = band_map(nv, nh, 2 * K + 2);
-    ConeStep steps[kConeMaxK + 1];
-    steps[0] = ConeStep{0, 1.0};
-    for (int j = 1; j <= K; ++j)
-        steps[j] = j == 1 ? ConeStep{0, 1.0} : j == 2 ? ConeStep{1, omegas[1]} : ConeStep{2, omegas[j - 1]};
-    const unsigned pg = (unsigned)(m < 8192 ? m : 8192);
-    for (int v0 = 0; v0 < nvals; v0 += 2) {
-        const int nvv = nvals - v0 >= 2 ? 2 : 1;
-        const double* fv = f + v0 * n;
-        for (int j = 1; j <= K; ++j) {
-            const double* gin = j == 1 ? nullptr : gb[(j - 1) % 3];
-            const double* gprev = j >= 3 ? gb[(j + 1) % 3] : nullptr;
-            if (nvv == 2) {
-                ConeBand<2> a{fv, gin, gprev, gb[j % 3], ring_acc, steps[j], band};
-                k_gd_cone_band<2><<<grid_for(bm.total, 1, kStreamGridCap), kBlock, 0, s>>>(g, bm, a);
-                k_gd_cone_ring<2><<<grid_for(L * 64), kBlock, 0, s>>>(g, a);
-            } else {
-                ConeBand<1> a{fv, gin, gprev, gb[j % 3], ring_acc, steps[j], band};
-                k_gd_cone_band<1><<<grid_for(bm.total, 1, kStreamGridCap), kBlock, 0, s>>>(g, bm, a);
-                k_gd_cone_ring<1><<<grid_for(L * 64), kBlock, 0, s>>>(g, a);
-            }
-            if ((st = launch_status("k_gd_cone_band"))) return st;
-        }
-        if (nvv == 2) {
-            ConePatch<2> a{fv, cells, count, K, {}, gb[K % 3], d_change};
-            for (int j = 0; j <= K; ++j) a.st[j] = steps[j];
-            k_gd_cone_patch<2><<<pg, 256, 0, s>>>(g, a);
-        } else {
-            ConePatch<1> a{fv, cells, count, K, {}, gb[K % 3], d_change};
-            for (int j = 0; j <= K; ++j) a.st[j] = steps[j];
-            k_gd_cone_patch<1><<<pg, 256, 0, s>>>(g, a);
-        }
-        if ((st = launch_status("k_gd_cone_patch"))) return st;
-        k_gd_eval<<<grid_for(m, 1, kStreamGridCap), kBlock, 0, s>>>(g, t, owner, fv, gb[K % 3], nvv, out + v0 * m);
-        if ((st = launch_status("k_gd_eval"))) return st;
-    }
-    return 0;
+    return cone_part(g, t, 0, (int64_t)nv * nh, 1, f, nvals, K, omegas, work, owner, out, nullptr, d_change, s);
+}
+
+int akb_gd_claims_f64(const double* x, const double* y, int nv, int nh, const uint8_t* diag, int npock,
+                      const int32_t* ptri, const int32_t* pnbr, const int32_t* edge_tri, int row0, int row1,
+                      int with_pockets, const double* gx, int mx, const double* gy, int my, int* owner, void* stream) {
+    clear_error();
+    AKB_REQUIRE(x && y && diag && gx && gy && owner && mx > 0 && my > 0, "bad arguments");
+    AKB_REQUIRE(nv >= 2 && nh >= 2 && row0 >= 0 && row1 <= nv - 1 && (row1 < 0 || row0 <= row1), "bad window");
+    AKB_REQUIRE(!with_pockets || npock == 0 || (ptri && pnbr && edge_tri), "pockets needed");
+    Grid g{x, y, nv, nh, diag, npock, ptri, pnbr, edge_tri, nullptr, nullptr};
+    g.row0 = row0;
+    g.row1 = row1;
+    return cone_claims(g, Targets{gx, gy, mx, my}, with_pockets, owner, (hipStream_t)stream);
+}
+
+int akb_gd_cone_part_f64(const double* x, const double* y, int nv, int nh, const uint8_t* diag, int npock,
+                         const int32_t* ptri, const int32_t* pnbr, const int32_t* edge_tri, const int32_t* xptr,
+                         const int32_t* xidx, int64_t own0, int64_t own1, int band_on, const double* gx, int mx,
+                         const double* gy, int my, const double* f, int nvals, int K, const double* omegas, void* work,
+                         const int* owner, double* out, double* cnt, unsigned long long* d_change, void* stream) {
+    clear_error();
+    AKB_REQUIRE(x && y && diag && gx && gy && f && omegas && work && owner && out && cnt && mx > 0 && my > 0,
+                "bad arguments");
+    AKB_REQUIRE(nvals >= 1 && nvals <= 2, "one or two value sets");
+    AKB_REQUIRE(K >= 1 && K <= kConeMaxK, "K sweeps in 1 .. 14");
+    AKB_REQUIRE(!band_on || (xptr && xidx && (npock == 0 || (ptri && pnbr && edge_tri))), "the band needs the pockets");
+    for (int j = 2; j <= K; ++j) AKB_REQUIRE(omegas[j - 1] > 0 && omegas[j - 1] < 2, "Chebyshev weight outside (0, 2)");
+    Grid g{x, y, nv, nh, diag, npock, ptri, pnbr, edge_tri, xptr, xidx};
+    return cone_part(g, Targets{gx, gy, mx, my}, own0, own1, band_on, f, nvals, K, omegas, work, owner, out, cnt,
+                     d_change, (hipStream_t)stream);
+}
+
+int akb_gd_part_finish_f64(double* out, const double* cnt, int64_t m, int nvals, void* stream) {
+    clear_error();
+    AKB_REQUIRE(out && cnt && m > 0 && nvals >= 1, "bad arguments");
+    k_gd_part_finish<<<grid_for(m), kBlock, 0, (hipStream_t)stream>>>(out, cnt, m, nvals);
+    return launch_status("k_gd_part_finish");
+}
+
+int akb_gd_ring_f64(const double* x, const double* y, int nv, int nh, double* ring_x, double* ring_y, unsigned* d_flags,
+                    void* stream) {
+    clear_error();
+    AKB_REQUIRE(x && y && ring_x && ring_y && d_flags && nv >= 2 && nh >= 2, "bad arguments");
+    Grid g{x, y, nv, nh, nullptr, 0, nullptr, nullptr, nullptr, nullptr, nullptr};
+    const int64_t L = 2 * (int64_t)(nh - 1) + 2 * (int64_t)(nv - 1);
+    k_gd_ring<<<grid_for(L), kBlock, 0, (hipStream_t)stream>>>(g, ring_x, ring_y, d_flags);
+    return launch_status("k_gd_ring");
+}
+
+int akb_gd_cells_window_f64(const double* x, const double* y, int nv, int nh, int row0, int row1, uint8_t* diag,
+                            double tol, unsigned* d_flags, void* stream) {
+    clear_error();
+    AKB_REQUIRE(x && y && diag && d_flags && nv >= 2 && nh >= 2 && row0 >= 0 && row0 <= row1 && row1 <= nv - 1,
+                "bad arguments");
+    Grid g{x, y, nv, nh, diag, 0, nullptr, nullptr, nullptr, nullptr, nullptr};
+    g.row0 = row0;
+    g.row1 = row1;
+    const int64_t wc = (int64_t)(row1 - row0) * (nh - 1);
+    if (wc == 0) return 0;
+    k_gd_cells<<<grid_for(wc, 1, kStreamGridCap), kBlock, 0, (hipStream_t)stream>>>(g, diag, tol, d_flags);
+    return launch_status("k_gd_cells");
 }
 
 }  // extern "C"

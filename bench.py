@@ -450,14 +450,20 @@ def main():
             done.record(side)
         state["psf_done"] = done
 
-    faithful = args.pupil_mode == "faithful" and world == 1
+    faithful = args.pupil_mode == "faithful"
     fp = None
     tickets = []
     fp_events = []
-    if faithful:
+    if faithful and world == 1:
         from akbraytracing_amd.faithful import FaithfulPupil
         fp = FaithfulPupil(n, n, size=args.pupil, pad=args.pad, wavelengths=my_lams,
                            slots=args.faithful_lag + 3)
+    elif faithful:
+        # N > 1: the pupil sharded with the rays (halo rows + the boundary band to rank 0, no gather
+        # of the hits: faithful_dist.py); rank 0 forms the map, the plane correction and the stack
+        from akbraytracing_amd.faithful_dist import ShardedFaithfulPupil
+        fp = ShardedFaithfulPupil(n, comm, size=args.pupil, pad=args.pad, wavelengths=lams,
+                                  slots=args.faithful_lag + 2)
 
     def faithful_back(timed, f):
         """The reference's pupil and PSF of the oldest front: its tilt and OPD were fused into later
@@ -475,7 +481,8 @@ def main():
             if timed:
                 e1.record(bs)
                 fp_events.append(("begin", e0, e1))
-            while tickets and (tickets[0].ready() or len(tickets) > args.faithful_lag):
+            # N > 1: every rank finishes the same runs (collectives), so by count alone
+            while tickets and ((world == 1 and tickets[0].ready()) or len(tickets) > args.faithful_lag):
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if timed else None
                 fp.finish(tickets.pop(0), stream=bs, events=ev)
                 if timed:
@@ -573,7 +580,7 @@ def main():
     if faithful:  # every run's error words (the reference's raises), read now that nothing waits on them
         for sl in fp.slots:
             if sl["last"] is not None:
-                sl["last"].check()
+                fp.check(sl["last"]) if world > 1 else sl["last"].check()
         faithful_checked = sum(1 for sl in fp.slots if sl["last"] is not None)
     psf_alone_ms = psf_device_ms = None
     if rank == 0:  # the PSF's own wall time, nothing beside it (the last pupil: rw.pupil is collective)
@@ -639,20 +646,17 @@ def main():
                           "what": "run() (trace, resample, tilt, OPD) + griddata(cubic) of Wave2 -> nanmean -> plane "
                                   f"correction -> psf_calc on the {args.pupil}^2 grid, one system per step, median"}
 
-    # N > 1: the faithful PSF through SURVEY.md §8(e)'s route - every rank's (y, z, Wave2) rows
-    # gathered to rank 0, which grids the whole lattice and forms the PSF (collective; wall time
-    # between barriers, median of 3)
+    # N > 1: one faithful pupil + PSF on its own through the sharded route (halo rows + band to rank
+    # 0, no gather of the hits; collective: wall time between barriers, median of 3)
     faithful_dist_ms = None
-    if world > 1 and last_out is not None:
-        from akbraytracing_amd.psfcalc import psf_calc
+    if world > 1 and last_out is not None and faithful:
         ft = []
+        d2 = last_out["detcenter2"]
         for _ in range(3):
             comm.barrier()
             torch.cuda.synchronize()
             t1 = time.perf_counter()
-            got = AD.wave_pupil_sharded(rw, last_out, args.pupil, comm)
-            if got is not None:
-                psf_calc(got[0], got[1], got[2], 1e-2)
+            fp.run(d2[1], d2[2], last_out["wave2"])
             torch.cuda.synchronize()
             comm.barrier()
             ft.append((time.perf_counter() - t1) * 1e3)
@@ -710,6 +714,9 @@ def main():
                          and world == 1 and faithful else
                          "C3: 4-mirror AKB ray_wave trace (2 passes, tilt, OPD) + 2048^2 PSF" if args.config == "c3"
                          and world == 1 else
+                         "C4: 4-mirror AKB ray_wave trace, ray-row shards, + the reference's pupil (griddata cubic, "
+                         "nanmean, plane correction, psf_calc) sharded with the rays + 2048^2 PSF"
+                         if args.config == "c3" and faithful else
                          "C4: 4-mirror AKB ray_wave trace, ray-row shards, + 2048^2 PSF" if args.config == "c3" else
                          "C5: 4-mirror AKB ray_wave trace with per-ray Legendre OPL perturbation + "
                          "3-wavelength 2048^2 PSF stack"),
@@ -723,9 +730,12 @@ def main():
         },
         "host_issue_ms_per_step": sorted(host_ms)[len(host_ms) // 2],
         "pupil": ("faithful: each step's PSF from the reference's own pupil - griddata(cubic) of Wave2 on the "
-                  f"{n}^2 hits (cone solve, {fp.sweeps} Chebyshev sweeps), nanmean removal, plane correction, "
-                  "psf_calc (rotation, rotate_with_nan, pad 16) - pipelined on the back stream "
-                  f"(akbraytracing_amd/faithful.py; {faithful_checked} runs' error words checked)" if faithful else
+                  f"{n}^2 hits (cone solve, {fp.K if world > 1 else fp.sweeps} Chebyshev sweeps), nanmean removal, "
+                  "plane correction, psf_calc (rotation, rotate_with_nan, pad 16) - pipelined on the back stream "
+                  + (f"(akbraytracing_amd/faithful.py; {faithful_checked} runs' error words checked)" if world == 1 else
+                     f"(akbraytracing_amd/faithful_dist.py: each rank grids its own rows, halo of {fp.K + 3} rows "
+                     f"from its neighbours, the boundary band ({sum(fp.plan.band_count(r) for r in range(world))} "
+                     f"hits) to rank 0; {faithful_checked} runs' error words checked)") if faithful else
                   "stand-in: RayWave.pupil's ray-index sampler (up to 0.098 nm from the reference's Clough-Tocher)"),
         "faithful_chain_ms": ((sum(fp_begin) + sum(fp_fin)) / max(len(fp_fin), 1)) if fp_fin else None,
         "faithful_finish_ms": (sum(fp_fin) / len(fp_fin)) if fp_fin else None,
@@ -783,8 +793,8 @@ def main():
         out["single_run_ms"] = single_ms
     if faithful_dist_ms is not None:
         out["faithful_psf_chain_ms"] = faithful_dist_ms
-        out["faithful_psf_route"] = (f"(y, z, Wave2) rows of the {world} ray shards gathered to rank 0 (24 B per ray), "
-                                     "griddata cubic -> nanmean -> plane correction -> psf_calc there")
+        out["faithful_psf_route"] = (f"sharded over the {world} ray shards (faithful_dist.py): halo rows and the "
+                                     "boundary band move, not the hits; one run alone, between barriers")
     if world > 1:
         out["note_multi_gpu"] = ("shards are aligned to numpy's 8192-element sum buffers and the ranks' buffer sums "
                                  "are chained in numpy's order: N ranks give one process's bits "

@@ -541,6 +541,35 @@ int akb_gd_cone_eval_f64(const double* x, const double* y, int nv, int nh, const
                          int nvals, int K, const double* omegas, void* work, int* owner, double* out,
                          unsigned long long* d_change, void* stream);
 
+/* The cone solve of a lattice sharded over ranks (row-block shards of the flat ray index; each
+ * rank passes x, y, diag as "virtual" global arrays of which only its rows plus K + 3 halo rows are
+ * backed - pointer minus row0 * nh - and the band owner passes full arrays with the boundary band
+ * filled):
+ *   akb_gd_cells_window_f64: the cell pass over cell rows [row0, row1) (no ring);
+ *   akb_gd_ring_f64: the boundary ring's coordinates (the band owner, for the host pockets);
+ *   akb_gd_claims_f64: owner[] = INT32_MAX, then the claims of the cells in rows [row0, row1)
+ *     (row1 < 0: all) and, with with_pockets, of the pocket triangles; a MIN all-reduce of the
+ *     ranks' owners gives the one-process owners (the same atomicMin over all triangles);
+ *   akb_gd_cone_part_f64: with that global owner, the targets this rank forms - interior cells
+ *     whose p00 lies in its rays [own0, own1), and with band_on every band / pocket target - their
+ *     gradients and values: out (nvals, my, mx) and cnt (my, mx) hold value / 1 there, 0 elsewhere,
+ *     so a SUM reduction of the ranks' pieces assembles the map;
+ *   akb_gd_part_finish_f64: NaN where the reduced cnt is 0 (outside the hull).
+ * Every target value is the one-process akb_gd_cone_eval_f64's bit for bit. */
+int akb_gd_cells_window_f64(const double* x, const double* y, int nv, int nh, int row0, int row1, uint8_t* diag,
+                            double tol, unsigned* d_flags, void* stream);
+int akb_gd_ring_f64(const double* x, const double* y, int nv, int nh, double* ring_x, double* ring_y, unsigned* d_flags,
+                    void* stream);
+int akb_gd_claims_f64(const double* x, const double* y, int nv, int nh, const uint8_t* diag, int npock,
+                      const int32_t* ptri, const int32_t* pnbr, const int32_t* edge_tri, int row0, int row1,
+                      int with_pockets, const double* gx, int mx, const double* gy, int my, int* owner, void* stream);
+int akb_gd_cone_part_f64(const double* x, const double* y, int nv, int nh, const uint8_t* diag, int npock,
+                         const int32_t* ptri, const int32_t* pnbr, const int32_t* edge_tri, const int32_t* xptr,
+                         const int32_t* xidx, int64_t own0, int64_t own1, int band_on, const double* gx, int mx,
+                         const double* gy, int my, const double* f, int nvals, int K, const double* omegas, void* work,
+                         const int* owner, double* out, double* cnt, unsigned long long* d_change, void* stream);
+int akb_gd_part_finish_f64(double* out, const double* cnt, int64_t m, int nvals, void* stream);
+
 /* diagnostics: out[13i..13i+12] = (the trace's sqrt, sqrt, the trace's shared-reciprocal a/b, a/b,
  * the positive-divisor a/b, the trace's norm and reciprocal norm of (a, b, b), sqrt and 1/sqrt of
  * that squared norm, the trace's slope arctan of a, the library atan of a, the trace's a/b and

@@ -4,9 +4,10 @@ cuda:0), each tracing its shard (Shard.split: 1525-1526 whole 8192-ray buffers, 
 combining the means through the communicator. Everything must come out bit-exact: pass 2 (every
 rank traces the same pass-2 tables), and Wave2 after the tilt, whose means combine the ranks'
 numpy buffer sums in numpy's order (LeafSink.finish_dist); the trace flags clean.
-Then the faithful pupil (griddata cubic -> nanmean -> plane correction onto the 128^2 grid) of the
-1e8 hits on one GPU, and through SURVEY.md §8(e)'s N > 1 route (dist.wave_pupil_sharded: the
-ranks' (y, z, Wave2) rows gathered to rank 0): the same map bit for bit.
+Then the faithful pupil and PSF (griddata cubic -> nanmean -> plane correction -> psf_calc) of the
+1e8 hits on one GPU (faithful.FaithfulPupil), and sharded over the eight ranks without gathering the
+hits (faithful_dist.ShardedFaithfulPupil: halo rows to the neighbours, the boundary band to rank
+0): the same map, pupil and PSF bit for bit.
 AKB_raytrace_20250312.py:2694-2717 (the grid), :3653-3696 (the gridding), SURVEY.md §8(d) C4."""
 import json
 import os
@@ -77,11 +78,16 @@ def _worker(rank, world, port, n, ref_dir):
                "blocks_equal": int(np.sum(sums == ref_sums)),
                "wave2_max_diff_nm": float(np.max(np.abs(wave - ref_wave[lo:hi]))),
                "wave2_nan": int(np.isnan(wave).sum())}
-        # the faithful pupil of the sharded trace: every rank's (y, z, Wave2) rows to rank 0, which
-        # grids the whole 1e8-hit lattice; the unsharded map's bits
-        pup = AD.wave_pupil_sharded(rw, out, 128, AD.TorchComm(dev))
+        # the faithful pupil and PSF of the sharded trace: no gather of the hits (faithful_dist.py)
+        from test_faithful_dist_gpu import save_result
+        from akbraytracing_amd.faithful_dist import ShardedFaithfulPupil
+        sp = ShardedFaithfulPupil(n, AD.TorchComm(dev), slots=1)
+        r, _ = sp.run(out["detcenter2"][1], out["detcenter2"][2], out["wave2"])
         if rank == 0:
-            np.save(os.path.join(ref_dir, "pupil_8ranks.npy"), pup[0].cpu().numpy())
+            save_result(os.path.join(ref_dir, "faithful_8ranks.npz"), r)
+        res["halo_rows"] = sp.plan.rows[1] - sp.plan.rows[0]
+        res["band_vertices"] = sp.plan.band_count(rank)
+        sp.close()
         with open(os.path.join(ref_dir, f"rank{rank}.json"), "w") as f:
             json.dump(res, f)
         dist.barrier()
@@ -100,19 +106,22 @@ def test_c4_1e8_rays_unsharded_and_eight_ranks(gpu, tmp_path):
     wave = out["wave2"].cpu().numpy()
     assert not np.isnan(wave).any()
     np.save(os.path.join(tmp_path, "wave2.npy"), wave)
-    # the faithful pupil of 1e8 hits on one GPU (griddata cubic -> nanmean -> plane correction)
+    # the faithful pupil and PSF of 1e8 hits on one GPU
     import time
-    from akbraytracing_amd.pupilmap import wave_pupil
+    from akbraytracing_amd.faithful import FaithfulPupil
+    from test_faithful_dist_gpu import KEYS, assert_same
+    fp = FaithfulPupil(N, N, slots=2)
     for _ in range(2):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        pupil, gh, gv, sweeps = wave_pupil(out["detcenter2"], out["wave2"], N, N, grid_num_H=128, grid_num_V=128)
+        want = fp.run(out["detcenter2"][1], out["detcenter2"][2], out["wave2"])
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t0) * 1e3
-    print(f"C4 faithful pupil (1e8 hits -> 128^2): {ms:.1f} ms, {sweeps} gradient sweeps")
-    pupil = pupil.cpu().numpy()
-    assert np.isfinite(pupil).sum() > 0.5 * pupil.size
-    del rw, out, wave
+    print(f"C4 faithful pupil + PSF (1e8 hits -> 128^2 -> 2048^2), one process: {ms:.1f} ms")
+    want = {k: want[k].clone() for k in KEYS}
+    fp.close()
+    assert np.isfinite(want["map"].cpu().numpy()).sum() > 0.5 * 128 * 128
+    del rw, out, wave, fp
     torch.cuda.empty_cache()
     mp.start_processes(_worker, args=(WORLD, _free_port(), N, str(tmp_path)), nprocs=WORLD, join=True,
                        start_method="spawn")
@@ -124,4 +133,4 @@ def test_c4_1e8_rays_unsharded_and_eight_ranks(gpu, tmp_path):
         assert r["blocks_equal"] == r["blocks"], r  # pass 2 and Wave2 bit-exact, block by block
         assert r["wave2_nan"] == 0
         assert r["wave2_max_diff_nm"] == 0.0, r
-    assert np.array_equal(np.load(os.path.join(tmp_path, "pupil_8ranks.npy")), pupil, equal_nan=True)
+    assert_same(os.path.join(tmp_path, "faithful_8ranks.npz"), want)
