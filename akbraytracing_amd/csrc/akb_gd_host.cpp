@@ -148,6 +148,40 @@ int64_t best_chain_point(const double* X, const double* Y, int64_t p, int64_t q,
     return at < 0 ? -1 : p + 1 + at;
 }
 
+struct Key {
+    double x, y;
+    int64_t i;
+};
+inline bool key_less(const Key& a, const Key& b) {
+    return a.x < b.x || (a.x == b.x && (a.y < b.y || (a.y == b.y && a.i < b.i)));
+}
+struct Job {
+    int64_t p, q;
+    int32_t parent;  // pocket triangle on the other side of (p, q), -1 for a hull edge
+    int slot;        // which of the parent's nbr slots points back here
+};
+struct Pocket {
+    int64_t p, q;
+    int32_t id0;  // its first triangle id
+    int err;
+    int64_t err_p, err_q;
+};
+struct Workspace {
+    std::vector<Key> keys, keys2;
+    std::vector<std::pair<size_t, size_t>> runs, runs2;
+    std::vector<char> on_hull;
+    std::vector<int64_t> h, hv;
+    std::vector<double> X, Y, cot;
+    std::vector<Pocket> pockets;
+    std::vector<Job> stack;
+    std::vector<std::pair<int64_t, int32_t>> chords;
+    std::vector<int32_t> next;
+};
+Workspace& workspace() {
+    thread_local Workspace w;
+    return w;
+}
+
 }  // namespace
 
 using namespace akb;
@@ -166,83 +200,91 @@ int akb_gd_pockets(const double* rx, const double* ry, int nv, int nh, int cap, 
     const int64_t base = 2 * ncells;
     AKB_REQUIRE(base + cap < INT32_MAX, "grid too large for 32-bit triangle ids");
 
+    // every buffer below lives in a per-thread workspace: a call runs in a few ms, and fresh
+    // allocations of these sizes (mmap'd by malloc) cost it their page faults every time
+    Workspace& w = workspace();
     // convex hull of the ring points, collinear points kept (pop on a strict right turn only);
     // sorted as (x, y, index) records (the comparisons read neighbouring memory, not the ring)
-    struct Key {
-        double x, y;
-        int64_t i;
-    };
-    std::vector<Key> keys(L);
+    std::vector<Key>& keys = w.keys;
+    keys.resize(L);
     for (int64_t i = 0; i < L; ++i) keys[i] = {rx[i], ry[i], i};
-    const auto less = [](const Key& a, const Key& b) {
-        return a.x < b.x || (a.x == b.x && (a.y < b.y || (a.y == b.y && a.i < b.i)));
-    };
     // a lattice's boundary ring is a few monotone runs in this (total) order - four for the C3
     // ring - so a natural merge sort is O(L): strictly descending runs reversed, runs merged in
     // pairs. The order is total (the index breaks ties), so the result is std::sort's exactly.
     {
-        std::vector<std::pair<size_t, size_t>> runs;
+        auto& runs = w.runs;
+        runs.clear();
         for (size_t i = 0; i < (size_t)L && runs.size() <= 64;) {
             size_t j = i + 1;
-            if (j < (size_t)L && less(keys[j], keys[i])) {
-                while (j < (size_t)L && less(keys[j], keys[j - 1])) ++j;
+            if (j < (size_t)L && key_less(keys[j], keys[i])) {
+                while (j < (size_t)L && key_less(keys[j], keys[j - 1])) ++j;
                 std::reverse(keys.begin() + i, keys.begin() + j);
             } else {
-                while (j < (size_t)L && !less(keys[j], keys[j - 1])) ++j;
+                while (j < (size_t)L && !key_less(keys[j], keys[j - 1])) ++j;
             }
             runs.push_back({i, j});
             i = j;
         }
         if (runs.size() > 64) {
-            std::sort(keys.begin(), keys.end(), less);
+            std::sort(keys.begin(), keys.end(), key_less);
         } else {
-            while (runs.size() > 1) {
-                std::vector<std::pair<size_t, size_t>> next;
-                for (size_t r = 0; r + 1 < runs.size(); r += 2) {
-                    std::inplace_merge(keys.begin() + runs[r].first, keys.begin() + runs[r].second,
-                                       keys.begin() + runs[r + 1].second, less);
-                    next.push_back({runs[r].first, runs[r + 1].second});
+            std::vector<Key>& tmp = w.keys2;
+            tmp.resize(L);
+            while (runs.size() > 1) {  // pairwise merges, ping-pong between the two buffers
+                auto& next = w.runs2;
+                next.clear();
+                for (size_t r = 0; r < runs.size(); r += 2) {
+                    if (r + 1 < runs.size()) {
+                        std::merge(keys.begin() + runs[r].first, keys.begin() + runs[r].second,
+                                   keys.begin() + runs[r + 1].first, keys.begin() + runs[r + 1].second,
+                                   tmp.begin() + runs[r].first, key_less);
+                        next.push_back({runs[r].first, runs[r + 1].second});
+                    } else {
+                        std::copy(keys.begin() + runs[r].first, keys.begin() + runs[r].second,
+                                  tmp.begin() + runs[r].first);
+                        next.push_back(runs[r]);
+                    }
                 }
-                if (runs.size() % 2) next.push_back(runs.back());
+                keys.swap(tmp);
                 runs.swap(next);
             }
         }
     }
-    std::vector<int64_t> order(L);
-    for (int64_t i = 0; i < L; ++i) order[i] = keys[i].i;
-    std::vector<char> on_hull(L, 0);
+    std::vector<char>& on_hull = w.on_hull;
+    on_hull.assign(L, 0);
     for (int pass = 0; pass < 2; ++pass) {
-        std::vector<int64_t> h;
+        std::vector<int64_t>& h = w.h;
+        h.clear();
         for (int64_t k = 0; k < L; ++k) {
-            const int64_t i = pass == 0 ? order[k] : order[L - 1 - k];
+            const int64_t i = pass == 0 ? keys[k].i : keys[L - 1 - k].i;
             while (h.size() >= 2 && right_turn(rx, ry, h[h.size() - 2], h.back(), i)) h.pop_back();
             h.push_back(i);
         }
         for (int64_t i : h) on_hull[i] = 1;
     }
-    std::vector<int64_t> hv;
+    std::vector<int64_t>& hv = w.hv;
+    hv.clear();
     for (int64_t i = 0; i < L; ++i)
         if (on_hull[i]) hv.push_back(i);
     AKB_REQUIRE(hv.size() >= 3, "degenerate point set (all boundary points collinear)");
 
     for (int64_t e = 0; e < L; ++e) edge_tri[e] = -1;
     // the ring twice over, so a pocket's chain p .. q (q < p + L) is one contiguous index range
-    std::vector<double> X(2 * L), Y(2 * L);
+    std::vector<double>& X = w.X;
+    std::vector<double>& Y = w.Y;
+    X.resize(2 * L);
+    Y.resize(2 * L);
     for (int64_t i = 0; i < 2 * L; ++i) {
         X[i] = rx[i < L ? i : i - L];
         Y[i] = ry[i < L ? i : i - L];
     }
     // the pockets, one per hull edge that skips ring points. They are independent (disjoint chains
-    // and ring edges), so the large ones run on their own threads; triangle ids and chord order are
-    // those of one LIFO walk over all of them (the last hull edge's pocket first), whatever ran where.
-    struct Pocket {
-        int64_t p, q;
-        int32_t id0;  // its first triangle id
-        std::vector<std::pair<int64_t, int32_t>> chords;  // (ring position, the other end's vertex id)
-        int err = 0;
-        int64_t err_p = 0, err_q = 0;
-    };
-    std::vector<Pocket> pockets;
+    // and ring edges); triangle ids and chord order are those of one LIFO walk over all of them
+    // (the last hull edge's pocket first). One thread walks them in that order (a call is one job of
+    // the caller's pool); AKB_GD_POCKET_THREADS=1 gives the large ones threads of their own, with
+    // the same result
+    std::vector<Pocket>& pockets = w.pockets;
+    pockets.clear();
     for (size_t k = 0; k < hv.size(); ++k) {
         int64_t p = hv[k], q = hv[(k + 1) % hv.size()];
         if (q <= p) q += L;
@@ -254,7 +296,7 @@ int akb_gd_pockets(const double* rx, const double* ry, int nv, int nh, int cap, 
                           "distorted for the structured triangulation", (long long)(r % L));
                 return 2;
             }
-        pockets.push_back({p, q, 0, {}});
+        pockets.push_back({p, q, 0, 0, 0, 0});
     }
     int32_t total = 0;
     for (size_t k = pockets.size(); k-- > 0;) {  // the LIFO walk's order: the last pocket first
@@ -265,22 +307,19 @@ int akb_gd_pockets(const double* rx, const double* ry, int nv, int nh, int cap, 
         set_error("griddata: more pocket triangles than cap %d", cap);
         return 2;
     }
-    auto fill = [&](Pocket& P) {
-        struct Job {
-            int64_t p, q;
-            int32_t parent;  // pocket triangle on the other side of (p, q), -1 for a hull edge
-            int slot;        // which of the parent's nbr slots points back here
-        };
-        std::vector<Job> stack{{P.p, P.q, -1, -1}};
-        std::vector<double> cot((size_t)(P.q - P.p));
+    // chords: two per pocket triangle, at 2 (id - id0) within the pocket's block of the list
+    std::vector<std::pair<int64_t, int32_t>>& chords = w.chords;
+    chords.resize(2 * (size_t)total);
+    auto fill = [&](Pocket& P, std::vector<Job>& stack, std::vector<double>& cot) {
+        stack.clear();
+        stack.push_back({P.p, P.q, -1, -1});
+        cot.resize((size_t)(P.q - P.p));
         int32_t n = P.id0;
-        P.chords.reserve(2 * (size_t)(P.q - P.p));
         while (!stack.empty()) {
             const Job J = stack.back();
             stack.pop_back();
             const int64_t p = J.p, q = J.q;
             // the chain point seeing (p, q) under the largest angle: the first smallest cot = dot / |cross|
-            const int64_t a = p % L, b = q % L;
             double best_cot = INFINITY;
             const int64_t best = best_chain_point(X.data(), Y.data(), p, q, cot.data(), best_cot);
             if (best < 0 || !(best_cot < INFINITY)) {
@@ -291,9 +330,10 @@ int akb_gd_pockets(const double* rx, const double* ry, int nv, int nh, int cap, 
             }
             const int64_t m = best;
             const int32_t id = n++;
-            tri[3 * id + 0] = (int32_t)R.vertex(p);
-            tri[3 * id + 1] = (int32_t)R.vertex(m);
-            tri[3 * id + 2] = (int32_t)R.vertex(q);
+            const int32_t vp = (int32_t)R.vertex(p), vm = (int32_t)R.vertex(m), vq = (int32_t)R.vertex(q);
+            tri[3 * id + 0] = vp;
+            tri[3 * id + 1] = vm;
+            tri[3 * id + 2] = vq;
             // opposite p: edge (m, q); opposite m: edge (q, p); opposite q: edge (p, m)
             nbr[3 * id + 1] = J.parent < 0 ? -1 : (int32_t)(base + J.parent);
             if (J.parent >= 0) nbr[3 * J.parent + J.slot] = (int32_t)(base + id);
@@ -312,21 +352,31 @@ int akb_gd_pockets(const double* rx, const double* ry, int nv, int nh, int cap, 
                 stack.push_back({p, m, id, 2});
             }
             // the base chord (p, q) joins two ring points that are not grid neighbours
-            P.chords.push_back({a, (int32_t)R.vertex(q)});
-            P.chords.push_back({b, (int32_t)R.vertex(p)});
+            chords[2 * (size_t)id] = {p % L, vq};
+            chords[2 * (size_t)id + 1] = {q % L, vp};
         }
     };
     {
-        static const bool serial = getenv("AKB_GD_SERIAL_POCKETS") != nullptr;  // A/B
+        static const bool threaded = getenv("AKB_GD_POCKET_THREADS") != nullptr;
         std::vector<std::thread> threads;
+        std::vector<std::vector<Job>> stacks;
+        std::vector<std::vector<double>> cots;
+        if (threaded) {
+            size_t big = 0;
+            for (auto& P : pockets) big += P.q - P.p >= 512;
+            stacks.resize(big);
+            cots.resize(big);
+            size_t k = 0;
+            for (auto& P : pockets)
+                if (P.q - P.p >= 512) {
+                    threads.emplace_back(fill, std::ref(P), std::ref(stacks[k]), std::ref(cots[k]));
+                    ++k;
+                }
+        }
         for (auto& P : pockets)
-            if (!serial && P.q - P.p >= 512) threads.emplace_back(fill, std::ref(P));
-        for (auto& P : pockets)
-            if (serial || P.q - P.p < 512) fill(P);
+            if (!threaded || P.q - P.p < 512) fill(P, w.stack, w.cot);
         for (auto& t : threads) t.join();
     }
-    std::vector<std::pair<int64_t, int32_t>> chords;
-    chords.reserve(2 * (size_t)L);
     for (size_t k = pockets.size(); k-- > 0;) {
         const Pocket& P = pockets[k];
         if (P.err) {
@@ -334,7 +384,6 @@ int akb_gd_pockets(const double* rx, const double* ry, int nv, int nh, int cap, 
                       (long long)P.err_q);
             return 2;
         }
-        chords.insert(chords.end(), P.chords.begin(), P.chords.end());
     }
     const int32_t n = total;
     if ((int64_t)chords.size() > 6 * (int64_t)cap) {
@@ -345,7 +394,8 @@ int akb_gd_pockets(const double* rx, const double* ry, int nv, int nh, int cap, 
     for (int64_t r = 0; r <= L; ++r) extra_ptr[r] = 0;
     for (const auto& c : chords) ++extra_ptr[c.first + 1];
     for (int64_t r = 0; r < L; ++r) extra_ptr[r + 1] += extra_ptr[r];
-    std::vector<int32_t> next(extra_ptr, extra_ptr + L);
+    std::vector<int32_t>& next = w.next;
+    next.assign(extra_ptr, extra_ptr + L);
     for (const auto& c : chords) extra_idx[next[c.first]++] = c.second;
     *n_out = n;
     return 0;

@@ -42,7 +42,7 @@ EUV = 13.5e-9  # option_energy 'EUV' (:1161-1162)
 class Ticket:
     """One run in the pipeline: its slot, the tensors it reads, the pocket job, then its results."""
 
-    __slots__ = ("slot", "y", "z", "f", "job", "npock", "result", "h2d", "status", "finished")
+    __slots__ = ("slot", "y", "z", "f", "job", "npock", "result", "h2d", "status", "finished", "done")
 
     def ready(self):
         return self.job.done()
@@ -100,6 +100,7 @@ class FaithfulPupil:
         self.change = torch.zeros(1, dtype=torch.int64, device=self.dev)
         self.post = {}
         self.psf = None
+        self._done = None  # the latest finish's end (finishes share work / map / pupil / psf buffers)
         self._omegas = D.host_f64(chebyshev_weights(max(self.sweeps, 1)))
         self.pool = concurrent.futures.ThreadPoolExecutor(max_workers=int(workers), thread_name_prefix="akb-pockets")
 
@@ -121,6 +122,8 @@ class FaithfulPupil:
         ring = s["ring"]
         flags = ring.view(torch.int32)[4 * Lr:4 * Lr + 1]
         st = torch.cuda.current_stream() if stream is None else stream
+        if s["last"] is not None and s["last"].done is not None:  # the slot's last reader, on any stream
+            st.wait_event(s["last"].done)
         for a in (y, z, f):  # read on this stream now and in finish: not to be reused before
             a.record_stream(st)
         with torch.cuda.stream(st):
@@ -132,7 +135,7 @@ class FaithfulPupil:
             ev.record(st)
         t = Ticket()
         t.slot, t.y, t.z, t.f = s, y, z, f
-        t.npock, t.result, t.h2d, t.status, t.finished = None, None, None, s["status"], False
+        t.npock, t.result, t.h2d, t.status, t.finished, t.done = None, None, None, s["status"], False, None
         t.job = self.pool.submit(self._pockets, s, ev)
         s["last"] = t
         return t
@@ -171,6 +174,8 @@ class FaithfulPupil:
         sh = D.stream_handle(st)
         o, Lr = self._o, self.L
         with torch.cuda.stream(st):
+            if self._done is not None:  # the shared buffers' last finish, on any stream
+                st.wait_event(self._done)
             if events is not None:
                 events[0].record(st)
             s["pk"].copy_(s["pk_host"], non_blocking=True)
@@ -200,6 +205,9 @@ class FaithfulPupil:
             self.psf = psf
             if events is not None:
                 events[1].record(st)
+            t.done = torch.cuda.Event()
+            t.done.record(st)
+            self._done = t.done
         t.result = dict(psf=psf, map=self.map[0], corrected=post["corrected"], rotated=post["rotated"],
                         params=post["params"], axes=self.axes, change=self.change)
         t.y = t.z = t.f = None

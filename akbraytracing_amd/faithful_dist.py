@@ -261,7 +261,7 @@ def _all_reduce_min(comm, t, group=None):
 # ---------------------------------------------------------------------- the pipeline
 
 class DistTicket:
-    __slots__ = ("slot", "job", "npock", "err", "result", "h2d", "finished")
+    __slots__ = ("slot", "job", "npock", "err", "result", "h2d", "finished", "done")
 
     def ready(self):
         return self.job.done()
@@ -323,6 +323,7 @@ class ShardedFaithfulPupil:
         self.pool = concurrent.futures.ThreadPoolExecutor(max_workers=int(workers), thread_name_prefix="akb-pk") \
             if p.is_root else None
         self.flags_all = 0
+        self._done = None  # the latest finish's end (finishes share work / owner / map / psf buffers)
 
     @staticmethod
     def _v(t, elems_off):
@@ -352,8 +353,10 @@ class ShardedFaithfulPupil:
         sh = D.stream_handle(st)
         win, diag = s["win"], s["diag"]
         t = DistTicket()
-        t.slot, t.npock, t.err, t.result, t.h2d, t.finished = s, 0, None, None, None, False
+        t.slot, t.npock, t.err, t.result, t.h2d, t.finished, t.done = s, 0, None, None, None, False, None
         with torch.cuda.stream(st):
+            if s["last"] is not None and s["last"].done is not None:  # the slot's last reader
+                st.wait_event(s["last"].done)
             for a in (y, z, f):  # read on this stream (the trace allocated them on its own)
                 a.record_stream(st)
             exchange_halo(p, self.comm, torch.stack([y, z, f]), win, self.group)
@@ -425,6 +428,8 @@ class ShardedFaithfulPupil:
         mm = m * m
         red = self.red
         with torch.cuda.stream(st):
+            if self._done is not None:  # the shared buffers' last finish, on any stream
+                st.wait_event(self._done)
             if events is not None:
                 events[0].record(st)
             if p.is_root:
@@ -468,6 +473,9 @@ class ShardedFaithfulPupil:
                            params=post["params"], axes=self.axes, change=self.change)
             if events is not None:
                 events[1].record(st)
+            t.done = torch.cuda.Event()
+            t.done.record(st)
+            self._done = t.done
         t.result = res
         t.finished = True
         return res

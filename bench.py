@@ -105,8 +105,9 @@ def parse():
                    help="faithful (default): each step's PSF is the reference's own - griddata(cubic) of Wave2 "
                         "(cone solve), nanmean removal, plane correction, psf_calc - pipelined on the back stream "
                         "(akbraytracing_amd/faithful.py); standin: RayWave.pupil's ray-index sampler (rounds 1-3)")
-    p.add_argument("--faithful-lag", type=int, default=3,
-                   help="faithful runs whose pocket jobs may be in flight before a step waits for the oldest")
+    p.add_argument("--faithful-lag", type=int, default=None,
+                   help="faithful runs whose pocket jobs may be in flight before a step waits for the oldest "
+                        "(default 3; 6 at N > 1, where the band owner builds configs[3]'s 40k-point ring)")
     p.add_argument("--no-ramp-form", action="store_true",
                    help="skip the timed steps before the clock ramp (ms_per_step_no_ramp)")
     p.add_argument("--psf-start", choices=("pupil", "pass1"), default="pupil",
@@ -451,6 +452,8 @@ def main():
         state["psf_done"] = done
 
     faithful = args.pupil_mode == "faithful"
+    if args.faithful_lag is None:
+        args.faithful_lag = 3 if world == 1 else 6
     fp = None
     tickets = []
     fp_events = []
@@ -463,7 +466,7 @@ def main():
         # of the hits: faithful_dist.py); rank 0 forms the map, the plane correction and the stack
         from akbraytracing_amd.faithful_dist import ShardedFaithfulPupil
         fp = ShardedFaithfulPupil(n, comm, size=args.pupil, pad=args.pad, wavelengths=lams,
-                                  slots=args.faithful_lag + 2)
+                                  slots=args.faithful_lag + 2, workers=4)
 
     def faithful_back(timed, f):
         """The reference's pupil and PSF of the oldest front: its tilt and OPD were fused into later
