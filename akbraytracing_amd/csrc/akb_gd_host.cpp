@@ -77,10 +77,6 @@ __attribute__((always_inline)) inline void cot_scan_body(const double* X, const 
         tmp[k] = cr > 0 ? qt : (dt < 0 ? -INFINITY : INFINITY);
     }
 }
-__attribute__((target("avx512f,avx512dq"))) void cot_scan_avx512(const double* X, const double* Y, int64_t p, int64_t q,
-                                                                 double* tmp) {
-    cot_scan_body(X, Y, p, q, tmp);
-}
 __attribute__((target("avx2"))) void cot_scan_avx2(const double* X, const double* Y, int64_t p, int64_t q, double* tmp) {
     cot_scan_body(X, Y, p, q, tmp);
 }
@@ -88,16 +84,46 @@ void cot_scan_base(const double* X, const double* Y, int64_t p, int64_t q, doubl
     cot_scan_body(X, Y, p, q, tmp);
 }
 
-// first index of the smallest of tmp[0, len) under '<' (the scalar scan's pick), 8 lanes at a time:
-// each lane keeps its own first minimum, then the lanes' minima are merged value first, index second
-__attribute__((target("avx512f,avx512dq"))) int64_t first_min_avx512(const double* tmp, int64_t len, double& mn_out) {
-    __m512d mn = _mm512_set1_pd(INFINITY);
+int64_t first_min_base(const double* tmp, int64_t len, double& mn_out) {
+    double mn = INFINITY;
+    int64_t at = -1;
+    for (int64_t k = 0; k < len; ++k)
+        if (tmp[k] < mn) {
+            mn = tmp[k];
+            at = k;
+        }
+    mn_out = mn;
+    return at;
+}
+
+// cot_scan + first_min in one pass (AVX-512): the same cot bits per point (the expression above
+// with explicit, uncontracted vector operations), each lane keeping its first minimum, the lanes
+// merged value first, index second, the tail scalar - the strict '<' scan's pick
+__attribute__((target("avx512f,avx512dq"))) int64_t best_avx512(const double* X, const double* Y, int64_t p, int64_t q,
+                                                               double& mn_out) {
+    const double ax = X[p], ay = Y[p], bx = X[q], by = Y[q];
+    const int64_t len = q - p - 1;
+    const double* xs = X + p + 1;
+    const double* ys = Y + p + 1;
+    const __m512d vax = _mm512_set1_pd(ax), vay = _mm512_set1_pd(ay), vbx = _mm512_set1_pd(bx),
+                  vby = _mm512_set1_pd(by);
+    const __m512d zero = _mm512_setzero_pd(), pinf = _mm512_set1_pd(INFINITY), ninf = _mm512_set1_pd(-INFINITY);
+    __m512d mn = pinf;
     __m512i at = _mm512_set1_epi64(-1);
     __m512i idx = _mm512_setr_epi64(0, 1, 2, 3, 4, 5, 6, 7);
     const __m512i eight = _mm512_set1_epi64(8);
     int64_t k = 0;
     for (; k + 8 <= len; k += 8) {
-        const __m512d v = _mm512_loadu_pd(tmp + k);
+        const __m512d x = _mm512_loadu_pd(xs + k), y = _mm512_loadu_pd(ys + k);
+        const __m512d ux = _mm512_sub_pd(vax, x), uy = _mm512_sub_pd(vay, y);
+        const __m512d vx = _mm512_sub_pd(vbx, x), vy = _mm512_sub_pd(vby, y);
+        const __m512d cr = _mm512_abs_pd(_mm512_sub_pd(_mm512_mul_pd(ux, vy), _mm512_mul_pd(uy, vx)));
+        const __m512d dt = _mm512_add_pd(_mm512_mul_pd(ux, vx), _mm512_mul_pd(uy, vy));
+        const __m512d qt = _mm512_div_pd(dt, cr);
+        // cr > 0 ? qt : (dt < 0 ? -inf : inf)
+        const __mmask8 pos = _mm512_cmp_pd_mask(cr, zero, _CMP_GT_OQ);
+        const __mmask8 neg = _mm512_cmp_pd_mask(dt, zero, _CMP_LT_OQ);
+        const __m512d v = _mm512_mask_mov_pd(_mm512_mask_mov_pd(pinf, neg, ninf), pos, qt);
         const __mmask8 lt = _mm512_cmp_pd_mask(v, mn, _CMP_LT_OQ);
         mn = _mm512_mask_mov_pd(mn, lt, v);
         at = _mm512_mask_mov_epi64(at, lt, idx);
@@ -114,37 +140,36 @@ __attribute__((target("avx512f,avx512dq"))) int64_t first_min_avx512(const doubl
             best = m8[l];
             pos = a8[l];
         }
-    for (; k < len; ++k)
-        if (tmp[k] < best) {
-            best = tmp[k];
+    for (; k < len; ++k) {
+        const double ux = ax - xs[k], uy = ay - ys[k];
+        const double vx = bx - xs[k], vy = by - ys[k];
+        const double cr = fabs(ux * vy - uy * vx);
+        const double dt = ux * vx + uy * vy;
+        const double qt = dt / cr;
+        const double c = cr > 0 ? qt : (dt < 0 ? -INFINITY : INFINITY);
+        if (c < best) {
+            best = c;
             pos = k;
         }
+    }
     mn_out = best;
     return pos;
 }
 
-int64_t first_min_base(const double* tmp, int64_t len, double& mn_out) {
-    double mn = INFINITY;
-    int64_t at = -1;
-    for (int64_t k = 0; k < len; ++k)
-        if (tmp[k] < mn) {
-            mn = tmp[k];
-            at = k;
-        }
-    mn_out = mn;
-    return at;
-}
-
 // the first m in (p, q) with the smallest cot (a strict '<' scan's pick); best_cot receives it
 int64_t best_chain_point(const double* X, const double* Y, int64_t p, int64_t q, double* tmp, double& best_cot) {
-    static const int isa = __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512dq") ? 2
+    static const int isa = getenv("AKB_GD_NO_AVX512") ? 1  // A/B: the two-pass AVX2 scan
+                           : __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512dq") ? 2
                            : __builtin_cpu_supports("avx2")                                       ? 1
                                                                                                   : 0;
-    if (isa == 2) cot_scan_avx512(X, Y, p, q, tmp);
-    else if (isa == 1) cot_scan_avx2(X, Y, p, q, tmp);
+    if (isa == 2) {
+        const int64_t at = best_avx512(X, Y, p, q, best_cot);
+        return at < 0 ? -1 : p + 1 + at;
+    }
+    if (isa == 1) cot_scan_avx2(X, Y, p, q, tmp);
     else cot_scan_base(X, Y, p, q, tmp);
     const int64_t len = q - p - 1;
-    const int64_t at = isa == 2 ? first_min_avx512(tmp, len, best_cot) : first_min_base(tmp, len, best_cot);
+    const int64_t at = first_min_base(tmp, len, best_cot);
     return at < 0 ? -1 : p + 1 + at;
 }
 
