@@ -106,6 +106,14 @@ def kernel_summary(name, d, pmc_ns, trace_ns, bytes_per_ray, n_rays, label):
                           if d.get("SQ_ACTIVE_INST_VALU") and cycles else None),
         "issue_cycles_min": (valu * 4 / SIMDS) if valu else None,
         "issue_frac": (valu * 4 / SIMDS / cycles) if valu and cycles else None,
+        # the stall diagnosis: share of wave cycles spent waiting (s_waitcnt and dependencies), and
+        # the VMEM instructions in flight per wave cycle (SQ_INST_LEVEL_VMEM accumulates the level)
+        "wait_any_frac": (d["SQ_WAIT_ANY"] / d["SQ_WAVE_CYCLES"]
+                          if d.get("SQ_WAIT_ANY") is not None and d.get("SQ_WAVE_CYCLES") else None),
+        "wait_inst_any_frac": (d["SQ_WAIT_INST_ANY"] / d["SQ_WAVE_CYCLES"]
+                               if d.get("SQ_WAIT_INST_ANY") is not None and d.get("SQ_WAVE_CYCLES") else None),
+        "vmem_level_per_wave_cycle": (d["SQ_INST_LEVEL_VMEM"] / d["SQ_WAVE_CYCLES"]
+                                      if d.get("SQ_INST_LEVEL_VMEM") is not None and d.get("SQ_WAVE_CYCLES") else None),
     }
     if pmc_ns:
         out["fp64_tflops_pmc_run"] = out["fp64_flops_per_launch"] / pmc_ns / 1e3
