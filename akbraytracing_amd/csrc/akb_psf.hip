@@ -648,8 +648,26 @@ struct PsfLineArgs {
     int* cand_n;         // per batch entry: their count, or -1 for every row
     double* ubound;      // row-bound route: (batch, py) bounds B[ko] >= max_lo |F[ko][lo]|^2
     double* ubmax;       // row-bound route: per batch entry max B, NaN when the route is off
+    double* bpart;       // select route: (batch, npart, py) sum over a pass-1 workgroup's columns of |G|
+    double2* spart;      // select route: (batch, npart, 32) its columns' part of F at the kSel samples
+    int npart;           // select route: pass 1's workgroup count
     int ngroups;         // line groups (LINES lines each) per batch entry
 };
+
+// The select route to the peak (the default below 2^24 points). Pass 1 also leaves, per workgroup,
+// the sums over its pupil columns x of |G[x][ko]| for every row and of (-1)^x G[x][ko] W^(lo x) at
+// a 5 x 5 grid of samples around the plane's centre (ko = py/2 - 2 .. py/2 + 2, lo likewise: the
+// pupil's zero frequency, where a focused PSF peaks). The peak pass sums those parts in a fixed
+// order in every workgroup: B[ko] = (sum_x |G[x][ko]|)^2 (1 + 2^-20) bounds every |F|^2 it computes
+// in row ko (the row-bound argument below), and each sample S gives M_low = (|S| - d)^2 (1 - 2^-30)
+// with d = 2^-30 sum_x |G[x][ko]|, below the |F|^2 the pass computes at that sample (both sums'
+// roundings are ~1e-13 of sum_x |G|), so below the max. A row with B < M_low cannot hold the max:
+// each workgroup transforms only its rows with B >= M_low (the peak row among them), all rows when
+// M_low is not a positive finite number (dark, NaN or infinite field). The max is therefore the
+// all-rows pass's exactly, with no launch beyond the three passes.
+constexpr int kSel = 25;
+constexpr int kSelRows = 256;
+constexpr double kBoundMarginSel = 1.0 + 0x1p-20;
 
 template <int N, int PAD, int MODE>
 __global__ void __launch_bounds__((LineShape<N, PAD>::kThreads)) k_psf_line(PsfLineArgs A) {
@@ -662,8 +680,18 @@ __global__ void __launch_bounds__((LineShape<N, PAD>::kThreads)) k_psf_line(PsfL
     __shared__ V gl[LINES * N];
     __shared__ V tab[S::kTab];
     __shared__ double wm[S::kThreads / 64];
+    // select route (pass 1 of planes up to 4096 rows: per-workgroup row sums; the peak pass: its rows)
+    constexpr int BS = (MODE == kLinePupil && N * PAD <= 4096) ? N * PAD : 1;
+    constexpr bool kSelPeak = MODE == kLinePeak;
+    __shared__ double Bsum[BS];
+    __shared__ double2 Gs[MODE == kLinePupil ? LINES : 1][5];
+    __shared__ int Lc[MODE == kLinePupil ? LINES : 1];
+    __shared__ int lrows[kSelPeak ? kSelRows : 1];
+    __shared__ int lcount;
+    __shared__ double msel;
     const PsfGeom g = A.g;
     const int b = blockIdx.y;
+    const bool sel1 = BS > 1 && A.bpart != nullptr;  // pass 1 leaves the select route's parts
     const double2* WP = MODE == kLinePupil ? A.Wy : A.Wx;
     const int line = threadIdx.x / N, i = threadIdx.x % N;
     const int t = i % PAD, q2 = i / TS;
@@ -682,7 +710,8 @@ __global__ void __launch_bounds__((LineShape<N, PAD>::kThreads)) k_psf_line(PsfL
         A.umax32[b] = 0u;
     }
     // this workgroup's line groups: an XCD's contiguous share, slot-strided within it
-    const int ngr = rows ? (nl + LINES - 1) / LINES : A.ngroups, nwg = gridDim.x;
+    int ngr = rows ? (nl + LINES - 1) / LINES : A.ngroups;
+    const int nwg = gridDim.x;
     int base = 0, slot = blockIdx.x, nslot = nwg, RR = ngr;
     if ((nwg & 7) == 0) {
         RR = (ngr + 7) / 8;
@@ -693,8 +722,64 @@ __global__ void __launch_bounds__((LineShape<N, PAD>::kThreads)) k_psf_line(PsfL
     auto group_at = [&](int k) {
         const int o = slot + k * nslot;
         const int gi = base + o;
-        return (o < RR && gi < ngr) ? gi : -1;
+        return (o < RR && gi < (rows ? (nl + LINES - 1) / LINES : ngr)) ? gi : -1;
     };
+    double2 sacc = make_double2(0.0, 0.0);
+    if (sel1) {
+        for (int k = threadIdx.x; k < BS; k += S::kThreads) Bsum[k] = 0.0;
+        if (group_at(0) < 0) {  // no columns here: its parts are zero
+            double* bp = A.bpart + ((int64_t)b * A.npart + blockIdx.x) * g.py;
+            for (int k = threadIdx.x; k < g.py; k += S::kThreads) bp[k] = 0.0;
+            if (threadIdx.x < kSel) A.spart[((int64_t)b * A.npart + blockIdx.x) * 32 + threadIdx.x] = sacc;
+            return;
+        }
+    }
+    if (kSelPeak && A.bpart && !rows) {
+        // M_low from the samples (threads 0 .. kSel - 1 of wave 0), parts summed in workgroup order
+        double mk = 0.0;
+        if (threadIdx.x < kSel) {
+            double2 sv = make_double2(0.0, 0.0);
+            double bs = 0.0;
+            const int ko = g.py / 2 - 2 + threadIdx.x / 5;
+            for (int w = 0; w < A.npart; ++w) {
+                const double2 t = A.spart[((int64_t)b * A.npart + w) * 32 + threadIdx.x];
+                sv.x += t.x;
+                sv.y += t.y;
+                bs += A.bpart[((int64_t)b * A.npart + w) * g.py + ko];
+            }
+            const double as = sqrt(fma(sv.x, sv.x, sv.y * sv.y)), dl = bs * 0x1p-30;
+            mk = as > dl ? ((as - dl) * (as - dl)) * (1.0 - 0x1p-30) : (as == as && dl == dl ? 0.0 : as + dl);
+        }
+        if (threadIdx.x < 64) {
+            for (int off = 32; off > 0; off >>= 1) mk = dmax_nan(mk, __shfl_down(mk, off));
+            if (threadIdx.x == 0) {
+                msel = mk;
+                lcount = 0;
+            }
+        }
+        __syncthreads();
+        const double M = msel;
+        const bool all = !(M > 0.0) || !isfinite(M);
+        // this workgroup's rows (the all-rows pass's assignment): keep those with B >= M_low
+        int nmine = 0;
+        for (int k = 0; group_at(k) >= 0; ++k) nmine += LINES;
+        if (!all && nmine <= kSelRows) {
+            for (int e = threadIdx.x; e < nmine; e += S::kThreads) {
+                const int row = group_at(e / LINES) * LINES + e % LINES;
+                if (row >= nl) continue;
+                double bs = 0.0;
+                for (int w = 0; w < A.npart; ++w) bs += A.bpart[((int64_t)b * A.npart + w) * g.py + row];
+                if (!((bs * bs) * kBoundMarginSel < M)) lrows[atomicAdd(&lcount, 1)] = row;
+            }
+            __syncthreads();
+            nl = lcount;
+            rows = lrows;
+            base = 0;
+            slot = 0;
+            nslot = 1;
+            RR = (nl + LINES - 1) / LINES;
+        }
+    }
     // a workgroup without lines (the peak rounds' short row lists) leaves before its tables
     if (group_at(0) < 0) return;
     // stage-1 twiddles, W_N^m = W_P^(PAD m): four-step, TA[q2][t] = W_N^(q2 t),
@@ -891,6 +976,37 @@ __global__ void __launch_bounds__((LineShape<N, PAD>::kThreads)) k_psf_line(PsfL
 #pragma unroll
                 for (int r = 0; r < PAD; ++r) Gl[(int64_t)N * r] = v[r];
             }
+            if constexpr (BS > 1) {
+                if (sel1) {
+                    // |G| into the row sums, one line after the other (a fixed order); the sample
+                    // rows' values to LDS
+                    for (int ln = 0; ln < LINES; ++ln) {
+                        __syncthreads();
+                        if (line == ln && L >= 0) {
+#pragma unroll
+                            for (int r = 0; r < PAD; ++r) Bsum[i + N * r] += sqrt(fma(v[r].x, v[r].x, v[r].y * v[r].y));
+                        }
+                    }
+                    if (i == 0) Lc[line] = L;
+#pragma unroll
+                    for (int r = 0; r < PAD; ++r) {
+                        const int d = i + N * r - (N * PAD / 2 - 2);
+                        if (d >= 0 && d < 5) Gs[line][d] = L >= 0 ? v[r] : make_double2(0.0, 0.0);
+                    }
+                    __syncthreads();
+                    if (threadIdx.x < kSel) {  // sample (ko = py/2 - 2 + k / 5, lo = px/2 - 2 + k % 5)
+                        const int dk = threadIdx.x / 5, lo = g.px / 2 - 2 + threadIdx.x % 5;
+                        for (int ln = 0; ln < LINES; ++ln) {
+                            const int x = Lc[ln];
+                            if (x < 0) continue;
+                            double2 t = cmul(Gs[ln][dk], A.Wx[((int64_t)lo * x) % g.px]);
+                            if (x & 1) t = make_double2(-t.x, -t.y);
+                            sacc.x += t.x;
+                            sacc.y += t.y;
+                        }
+                    }
+                }
+            }
         } else if constexpr (MODE == kLinePeak32) {
             // this row's max (uint order of non-negative floats is numeric, NaN above +inf)
             unsigned mr = 0u;
@@ -941,6 +1057,14 @@ __global__ void __launch_bounds__((LineShape<N, PAD>::kThreads)) k_psf_line(PsfL
           }
         }
         grp = next;
+    }
+    if constexpr (BS > 1) {
+        if (sel1) {
+            __syncthreads();
+            double* bp = A.bpart + ((int64_t)b * A.npart + blockIdx.x) * g.py;
+            for (int k = threadIdx.x; k < g.py; k += S::kThreads) bp[k] = Bsum[k];
+            if (threadIdx.x < kSel) A.spart[((int64_t)b * A.npart + blockIdx.x) * 32 + threadIdx.x] = sacc;
+        }
     }
     if (MODE == kLinePeak) {
         if (nan_sum != nan_sum) m = nan_sum;
@@ -1098,6 +1222,13 @@ static int launch_psf_line(PsfLineArgs fa, int nlines, int batch, hipStream_t s)
                                                : "k_psf_line(write)");
 }
 
+// pass 1's workgroup count for a pupil of n-point columns at this pad (the select route's parts)
+template <int N, int PAD>
+static int pupil_pass_wgs(int nlines) {
+    using S = LineShape<N, PAD>;
+    return line_wgs<N, PAD, double>((nlines + S::LINES - 1) / S::LINES);
+}
+
 // pad 16: lines of 16..1024; pad 8: 8..512 (Q = N / PAD <= 64)
 #define AKB_LINE_SHAPES(X) \
     X(16, 16) X(32, 16) X(64, 16) X(128, 16) X(256, 16) X(512, 16) X(1024, 16) \
@@ -1124,6 +1255,14 @@ static int psf_line_dispatch(int n, int pad, const PsfLineArgs& fa, int nlines, 
 #undef AKB_CASE
     set_error("line PSF: unsupported line %d at pad %d", n, pad);
     return AKB_E_INVALID;
+}
+
+static int psf_line_pupil_wgs(int n, int pad, int nlines) {
+#define AKB_CASE(NN, PP) \
+    if (n == NN && pad == PP) return pupil_pass_wgs<NN, PP>(nlines);
+    AKB_LINE_SHAPES(AKB_CASE)
+#undef AKB_CASE
+    return -1;
 }
 
 #define AKB_PSF_SIZES(X) X(8) X(16) X(32) X(64) X(128) X(256) X(512) X(1024)
@@ -1177,6 +1316,13 @@ static int64_t psf_fast_bytes(const PsfGeom& g, int batch) {
 // one 4-byte value per psf row and batch entry (fp32 row maxima, then the fp64 peak pass's rows)
 static int64_t psf_line_rows_bytes(const PsfGeom& g, int batch) {
     return ((int64_t)batch * g.py * 4 + 255) / 256 * 256;
+}
+
+// the select route's per-workgroup parts (pass 1 has at most one workgroup per pupil column)
+static bool psf_sel_ok(const PsfGeom& g) { return g.py <= 4096 && g.px <= 4096; }
+static int64_t psf_sel_bytes(const PsfGeom& g, int batch) {
+    if (!psf_sel_ok(g)) return 0;
+    return (((int64_t)batch * g.nx2 * g.py * 8 + 255) / 256 * 256) + (int64_t)batch * g.nx2 * 32 * 16;
 }
 
 // W_P tables, built once per (device, P) and kept by the library (freed by akb_psf_release_plans)
@@ -1260,7 +1406,8 @@ extern "C" {
 int64_t akb_psf_work_bytes(int ny, int nx, int pad, int batch) {
     if (ny <= 0 || nx <= 0 || pad < 1 || batch < 1) return -1;
     const PsfGeom g = psf_geom(ny, nx, pad);
-    if (psf_line_ok(g, pad)) return psf_fast_bytes(g, batch) + 256 + 4 * psf_line_rows_bytes(g, batch);  // G, peaks, rows, bounds
+    if (psf_line_ok(g, pad))  // G, peaks, rows, bounds, the select route's parts
+        return psf_fast_bytes(g, batch) + 256 + 4 * psf_line_rows_bytes(g, batch) + psf_sel_bytes(g, batch);
     if (psf_fast_ok(g)) return psf_fast_bytes(g, batch);             // H (ey x px)
     PlanEntry e;
     if (get_plan(g.py, g.px, batch, &e) != AKB_OK) return -1;
@@ -1306,15 +1453,24 @@ int akb_psf_f64(const double* opd, const double* amp, int ny, int nx, int pad, i
         la.psf = psf;
         la.efield = (double2*)efield_re_im;
         la.imax = d_imax;
-        if ((st = psf_line_dispatch<kLinePupil>(g.ny2, pad, la, g.nx2, batch, s))) return st;
         // the peak (same bits on every route): on planes of 2^24 points and up the row-bound
         // rounds (16384^2: 46 us of bounds + 2 x 12 us of rounds instead of a 0.91 ms fp64 pass or
-        // the fp32 pass + re-run's 0.58 ms), below it the fp64 pass over every row (2048^2: 13 us,
-        // against ~25 us for the bound route's four short launches). AKB_PSF_PEAK = bound / f32 /
-        // f64 forces a route.
+        // the fp32 pass + re-run's 0.58 ms); below it the select route (pass 1 leaves the row
+        // bounds and the centre samples, the peak pass transforms only the rows that can hold the
+        // max: no launch beyond the three passes). AKB_PSF_PEAK = select / bound / f32 / f64 (every
+        // row) forces a route.
         const char* pk = getenv("AKB_PSF_PEAK");
         const bool peak32 = pk && strcmp(pk, "f32") == 0;
         const bool bound = pk ? strcmp(pk, "bound") == 0 : (int64_t)g.py * g.px >= (1LL << 24);
+        const bool select = psf_sel_ok(g) && (pk ? strcmp(pk, "select") == 0 : !bound);
+        if (select) {
+            char* sp = tail + 256 + 4 * psf_line_rows_bytes(g, batch);
+            la.bpart = (double*)sp;
+            la.spart = (double2*)(sp + ((int64_t)batch * g.nx2 * g.py * 8 + 255) / 256 * 256);
+            la.npart = psf_line_pupil_wgs(g.ny2, pad, g.nx2);
+            AKB_REQUIRE(la.npart >= 1 && la.npart <= g.nx2, "select route: pass-1 workgroups");
+        }
+        if ((st = psf_line_dispatch<kLinePupil>(g.ny2, pad, la, g.nx2, batch, s))) return st;
         if (bound) {
             k_psf_rowbound<<<dim3((g.py + 63) / 64, batch), 1024, 0, s>>>(la);
             if ((st = launch_status("k_psf_rowbound"))) return st;

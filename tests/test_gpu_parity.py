@@ -757,9 +757,9 @@ def test_psf_pruned_transform(gpu, ny, nx, pad, win, eff, monkeypatch):
         e = fast[1][0].cpu().numpy()
         assert np.max(np.abs(e - ref[3])) <= 1e-10 * np.max(np.abs(ref[3]))
     if pad in (8, 16):
-        # the row-bound rounds (default) and the fp32 peak pass only pick the rows of the exact
-        # fp64 one: identical bits on every route
-        for mode in ("f64", "f32", "bound"):
+        # the select route (default below 2^24 points), the row-bound rounds (default above) and
+        # the fp32 peak pass only pick the rows of the exact fp64 one: identical bits on every route
+        for mode in ("f64", "f32", "bound", "select"):
             monkeypatch.setenv("AKB_PSF_PEAK", mode)
             alt = G.psf_stack(o, None, [lam], dx, dy, pad_factor=pad, window="hann" if win else None,
                               workspace=G.PsfWorkspace())
@@ -823,7 +823,7 @@ def test_psf_line_peak_edges(gpu, case, monkeypatch):
     fin = np.isfinite(ref)
     if fin.any():
         assert np.max(np.abs(got[fin] - ref[fin])) <= 1e-10 * max(1.0, np.max(np.abs(ref[fin])))
-    for mode in ("f64", "f32", "bound"):  # bound: a dark or NaN plane turns it off
+    for mode in ("f64", "f32", "bound", "select"):  # bound / select: a dark or NaN plane turns them off
         monkeypatch.setenv("AKB_PSF_PEAK", mode)
         alt = G.psf_stack(o, a, [13.5e-9], 5e-6, 5e-6, pad_factor=pad)[0][0].cpu().numpy()
         assert np.array_equal(alt, got, equal_nan=True)
@@ -832,9 +832,10 @@ def test_psf_line_peak_edges(gpu, case, monkeypatch):
 @pytest.mark.parametrize("n", [128, 256])
 @pytest.mark.parametrize("waves", [0.0, 0.3, 1.0, 3.0])
 def test_psf_line_bound_rounds(gpu, n, waves, monkeypatch):
-    """The row-bound peak (akb_psf.hip k_psf_rowbound): from a flat wavefront (the peak row alone
-    in round 1) to three waves of aberration (peak / max bound ~0.28, so round 2 runs rows under
-    round 1's threshold) - the same bits as the fp64 pass over every row, and the oracle."""
+    """The row-bound peak (akb_psf.hip k_psf_rowbound) and the select route (pass-1 row sums and
+    centre samples): from a flat wavefront (the peak row alone in round 1) to three waves of
+    aberration (peak / max bound ~0.28, so round 2 runs rows under round 1's threshold) - the same
+    bits as the fp64 pass over every row, and the oracle."""
     from akbraytracing_amd import psf as G
     import oracle.psf as OP
     lam = 13.5e-9
@@ -848,6 +849,11 @@ def test_psf_line_bound_rounds(gpu, n, waves, monkeypatch):
     monkeypatch.setenv("AKB_PSF_PEAK", "f64")
     alt, _, imax64 = G.psf_stack(o, None, [lam], 5e-6, 5e-6, pad_factor=16, workspace=G.PsfWorkspace())
     assert torch.equal(alt, got) and torch.equal(imax, imax64)
+    # the select route (the default below 2^24 points): the rows whose bound reaches the centre
+    # samples' lower bound - few when focused, more as the aberration moves the peak off centre
+    monkeypatch.setenv("AKB_PSF_PEAK", "select")
+    sel, _, imaxs = G.psf_stack(o, None, [lam], 5e-6, 5e-6, pad_factor=16, workspace=G.PsfWorkspace())
+    assert torch.equal(sel, got) and torch.equal(imaxs, imax64)
     if n == 128:
         amp = np.where(np.isfinite(opd), 1.0, 0.0)
         ref = OP.psf(opd, amp, lam, 5e-6, 1e-2, 16)[0]
