@@ -162,11 +162,11 @@ class FaithfulPupil:
         return int(buf[o["npk"]])
 
     # ------------------------------------------------------------------ stage 2
-    def finish(self, t, stream=None, events=None):
+    def finish(self, t, stream=None, events=None, psf_events=None):
         """Queue the rest of ticket t's chain on `stream` (waits for its pocket job on the host -
         normally long done). Returns dict(psf (B, P, P) device, map, corrected, rotated, params);
         the buffers are reused by the next finish on the stream. events: optional (start, end)
-        timing events recorded around the device work."""
+        timing events recorded around the device work; psf_events: the same around the PSF alone."""
         L = _lib.lib()
         t.npock = t.job.result()
         s = t.slot
@@ -200,8 +200,12 @@ class FaithfulPupil:
                                               D.ptr(self.owner), D.ptr(self.map), D.ptr(self.change), sh))
             post = pupil_post(self.map[0], out=self.post, stream=st)
             self.post = post
+            if psf_events is not None:
+                psf_events[0].record(st)
             psf, _, _ = psf_stack(post["opd"], None, self.lams, None, pad_factor=self.pad, stream=st, out=self.psf,
                                   pitch=self.axes[2 * m + 4:2 * m + 6])
+            if psf_events is not None:
+                psf_events[1].record(st)
             self.psf = psf
             if events is not None:
                 events[1].record(st)

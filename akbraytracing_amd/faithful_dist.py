@@ -407,9 +407,10 @@ class ShardedFaithfulPupil:
             return 0, e
 
     # ------------------------------------------------------------------ stage 2
-    def finish(self, t, stream=None, events=None):
+    def finish(self, t, stream=None, events=None, psf_events=None):
         """Queue the rest of t's chain. Returns dict(psf, map, corrected, rotated, params, axes,
-        change) on the band owner, None elsewhere. events: optional (start, end) timing events."""
+        change) on the band owner, None elsewhere. events / psf_events: optional (start, end)
+        timing events around the device work / the PSF alone (band owner)."""
         from . import _lib
         from . import device as D
         from .psf import psf_stack
@@ -466,8 +467,12 @@ class ShardedFaithfulPupil:
                 _lib.check(L.akb_gd_part_finish_f64(D.ptr(self.map), D.ptr(red[mm:2 * mm]), mm, 1, sh))
                 post = pupil_post(self.map[0], out=self.post, stream=st)
                 self.post = post
+                if psf_events is not None:
+                    psf_events[0].record(st)
                 psf, _, _ = psf_stack(post["opd"], None, self.lams, None, pad_factor=self.pad, stream=st,
                                       out=self.psf, pitch=self.axes[2 * m + 4:2 * m + 6])
+                if psf_events is not None:
+                    psf_events[1].record(st)
                 self.psf = psf
                 res = dict(psf=psf, map=self.map[0], corrected=post["corrected"], rotated=post["rotated"],
                            params=post["params"], axes=self.axes, change=self.change)

@@ -487,9 +487,13 @@ def main():
             # N > 1: every rank finishes the same runs (collectives), so by count alone
             while tickets and ((world == 1 and tickets[0].ready()) or len(tickets) > args.faithful_lag):
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if timed else None
-                fp.finish(tickets.pop(0), stream=bs, events=ev)
+                pe = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) \
+                    if timed and rank == 0 else None
+                fp.finish(tickets.pop(0), stream=bs, events=ev, psf_events=pe)
                 if timed:
                     fp_events.append(("finish", ev[0], ev[1]))
+                if pe is not None:
+                    psf_events.append(pe)
 
     def back(timed, f=None):
         """Tilt (unless already fused into the next pass 1), OPD and pupil of the oldest front (on
@@ -572,6 +576,7 @@ def main():
         step(False)
     rw.kernel_events = [] if os.environ.get("AKB_BENCH_NO_KEVENTS", "0") == "0" else None
     fp_events.clear()
+    psf_events.clear()
     # host_ms: host time spent issuing each step (its waits included): is the host the limit?
     el, host_ms = timed_steps(args.steps)
     while fronts:  # the last front's back half (outside the timed region, like the first one's)
