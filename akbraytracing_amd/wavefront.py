@@ -165,10 +165,19 @@ class RunResult(dict):
     def __init__(self, *a, params=None, **k):
         super().__init__(*a, **k)
         self._params = params
+        self._host = None
+
+    def tilt_params(self):
+        """Host copy of the tilt's device parameter block: theta_y, theta_z, R_y (3 x 3, row-major),
+        R_z, the focus estimate, the flag words (akb_tilt_params_f64); None for a run that took
+        the staged path (host-formed matrices)."""
+        if self._host is None and self._params is not None:
+            self._host = self._params.cpu().numpy()
+        return self._host
 
     def _resolve(self):
-        if self._params is not None:
-            h = self._params.cpu().numpy()
+        h = self.tilt_params()
+        if h is not None and "theta_y" not in dict.keys(self):
             self._params = None
             dict.update(self, theta_y=np.float64(h[0]), theta_z=np.float64(h[1]), focus_apprx=h[20:23].copy())
 

@@ -106,7 +106,8 @@ def _check_config(n, perturbation=None, k=20000):
         want = OL.perturbation(n, n, perturbation.coeffs).reshape(-1)[idx]
         assert np.all(np.abs((got_opl - opl) - want) <= 1.01 * np.spacing(opl) + 1e-13 * np.abs(want))
         opl = got_opl  # the tilt / OPD below from the device's perturbed path length
-    params = out["params"].cpu().numpy()
+    params = out.tilt_params()
+    assert params is not None
     det2, e2, w2 = _oracle_opd(g, last_hit, dir_out, opl, params, rw.means())
     assert np.array_equal(out["detcenter2"][:, ti].cpu().numpy(), det2)
     assert np.array_equal(out["dist_err2"][ti].cpu().numpy(), e2)
