@@ -1313,6 +1313,116 @@ __global__ void __launch_bounds__(kBlock) k_gd_cone_ring(Grid g, ConeBand<NV> a)
     }
 }
 
+// one sweep of the band in one launch: the band's vertices off the ring (k_gd_cone_band's body) in
+// the first `nb` workgroups, then a wave per ring vertex - the pocket chords reduced over the
+// wave, then the vertex's grid edges (lane 0, k_gd_cone_band's order), added to the chord sums in
+// that order as k_gd_cone_ring adds the band kernel's partial sums - then the solve. Both halves
+// read x_{j-1} / x_{j-2} only, so one launch per sweep gives k_gd_cone_band + k_gd_cone_ring's bits.
+template <int NV>
+__global__ void __launch_bounds__(kBlock) k_gd_cone_sweep(Grid g, BandMap bm, ConeBand<NV> a, int nbw) {
+    if (!*a.needed) return;
+    const int64_t n = (int64_t)g.nv * g.nh;
+    // the grid-edge sums of vertex i (k_gd_cone_band's edge order)
+    auto grid_sums = [&](int64_t i, int iv, int ih, double xi, double yi, const double (&fi)[NV], GradAcc<NV>& A) {
+        auto edge = [&](int64_t j) {
+            double fj[NV], gxj[NV], gyj[NV];
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                fj[v] = a.f[v * n + j];
+                gxj[v] = a.gin ? a.gin[2 * (v * n + j)] : 0.0;
+                gyj[v] = a.gin ? a.gin[2 * (v * n + j) + 1] : 0.0;
+            }
+            edge_vals<NV>(g.x[j], g.y[j], fj, gxj, gyj, xi, yi, fi, A);
+        };
+        if (ih > 0) edge(i - 1);
+        if (ih < g.nh - 1) edge(i + 1);
+        if (iv > 0) edge(i - g.nh);
+        if (iv < g.nv - 1) edge(i + g.nh);
+        const int64_t c0 = (int64_t)iv * (g.nh - 1) + ih;
+        if (iv > 0 && ih > 0 && g.diag[c0 - g.nh] == 0) edge(i - g.nh - 1);
+        if (iv > 0 && ih < g.nh - 1 && g.diag[c0 - (g.nh - 1)] == 1) edge(i - g.nh + 1);
+        if (iv < g.nv - 1 && ih > 0 && g.diag[c0 - 1] == 1) edge(i + g.nh - 1);
+        if (iv < g.nv - 1 && ih < g.nh - 1 && g.diag[c0] == 0) edge(i + g.nh + 1);
+    };
+    auto solve_store = [&](int64_t i, const GradAcc<NV>& A) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            const int64_t o = 2 * (v * n + i);
+            const double gix = a.gin ? a.gin[o] : 0.0, giy = a.gin ? a.gin[o + 1] : 0.0;
+            const double px = a.st.mode == 2 ? a.gprev[o] : 0.0, py = a.st.mode == 2 ? a.gprev[o + 1] : 0.0;
+            double ox, oy;
+            solve_vals<NV>(A, v, gix, giy, a.st, px, py, ox, oy);
+            a.gout[o] = ox;
+            a.gout[o + 1] = oy;
+        }
+    };
+    if ((int)blockIdx.x < nbw) {
+        for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < bm.total; k += (int64_t)nbw * blockDim.x) {
+            const int64_t i = band_vertex(bm, k);
+            const int iv = (int)(i / g.nh), ih = (int)(i - (int64_t)iv * g.nh);
+            if (ring_pos(g, iv, ih) >= 0) continue;  // the ring's waves below
+            const double xi = g.x[i], yi = g.y[i];
+            double fi[NV];
+#pragma unroll
+            for (int v = 0; v < NV; ++v) fi[v] = a.f[v * n + i];
+            GradAcc<NV> A;
+            grid_sums(i, iv, ih, xi, yi, fi, A);
+            solve_store(i, A);
+        }
+        return;
+    }
+    const int64_t ra = g.nh - 1, rb = g.nv - 1, L = 2 * ra + 2 * rb;
+    const int lane = threadIdx.x & 63;
+    const int64_t nwave = ((int64_t)(gridDim.x - nbw) * blockDim.x) >> 6;
+    for (int64_t r = (((int64_t)blockIdx.x - nbw) * blockDim.x + threadIdx.x) >> 6; r < L; r += nwave) {
+        int64_t i;
+        if (r < ra) i = r;
+        else if (r < ra + rb) i = (r - ra) * g.nh + (g.nh - 1);
+        else if (r < 2 * ra + rb) i = (int64_t)(g.nv - 1) * g.nh + (g.nh - 1 - (r - ra - rb));
+        else i = (int64_t)(g.nv - 1 - (r - 2 * ra - rb)) * g.nh;
+        const double xi = g.x[i], yi = g.y[i];
+        double fi[NV];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) fi[v] = a.f[v * n + i];
+        GradAcc<NV> A;
+        for (int32_t k = g.xptr[r] + lane; k < g.xptr[r + 1]; k += 64) {
+            const int64_t j = g.xidx[k];
+            double fj[NV], gxj[NV], gyj[NV];
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                fj[v] = a.f[v * n + j];
+                gxj[v] = a.gin ? a.gin[2 * (v * n + j)] : 0.0;
+                gyj[v] = a.gin ? a.gin[2 * (v * n + j) + 1] : 0.0;
+            }
+            edge_vals<NV>(g.x[j], g.y[j], fj, gxj, gyj, xi, yi, fi, A);
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+            A.q0 += __shfl_down(A.q0, off);
+            A.q1 += __shfl_down(A.q1, off);
+            A.q3 += __shfl_down(A.q3, off);
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                A.s0[v] += __shfl_down(A.s0[v], off);
+                A.s1[v] += __shfl_down(A.s1[v], off);
+            }
+        }
+        if (lane == 0) {
+            const int iv = (int)(i / g.nh), ih = (int)(i - (int64_t)iv * g.nh);
+            GradAcc<NV> G;
+            grid_sums(i, iv, ih, xi, yi, fi, G);
+            A.q0 += G.q0;
+            A.q1 += G.q1;
+            A.q3 += G.q3;
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                A.s0[v] += G.s0[v];
+                A.s1[v] += G.s1[v];
+            }
+            solve_store(i, A);
+        }
+    }
+}
+
 template <int NV>
 struct ConePatch {
     const double* f;           // (NV, n)
@@ -1416,6 +1526,142 @@ __global__ void __launch_bounds__(256) k_gd_cone_patch(Grid g, ConePatch<NV> a) 
         if (a.chg && threadIdx.x < 64) {
             for (int off = 2; off > 0; off >>= 1) worst = fmax(worst, __shfl_down(worst, off));
             if (threadIdx.x == 0 && worst > 0) atomicMax(a.chg, (unsigned long long)__double_as_longlong(worst));
+        }
+    }
+}
+
+// k_gd_cone_patch with one thread per box vertex (one value set): the edge geometry of a vertex -
+// (ex, ey), r^-3 and 6 (f_i - f_j) per edge, the local 2 x 2 system and its reciprocal
+// determinant - does not change between sweeps, so each thread forms its own once per cell, in
+// k_gd_grad's expressions and edge order, and keeps it in registers; a sweep then costs per edge
+// one LDS read of the neighbour's iterate and nine operations (against the full edge_vals: a
+// reciprocal square root and ~25 operations, five LDS reads). The box has pitch 32 (thread =
+// row * 32 + column); x_j overwrites x_{j-2} in place (a vertex reads its own predecessor only),
+// so two iterate buffers suffice. The arithmetic is edge_vals / solve_vals' exactly: x_K at the
+// corners equals k_gd_cone_patch's, bit for bit.
+__global__ void __launch_bounds__(1024) k_gd_cone_patch1(Grid g, ConePatch<1> a) {
+    constexpr int P = 32;
+    static_assert(kConeBox <= P, "box pitch");
+    __shared__ double sx[P * P], sy[P * P], sf[P * P];
+    __shared__ double2 sg[2][P * P];
+    __shared__ uint8_t sd[P * P];
+    const int64_t n = (int64_t)g.nv * g.nh;
+    const int K = a.K, W = 2 * K + 4;
+    const int t = threadIdx.x, r = t / P, c = t - (t / P) * P;
+    const bool inbox = r < W && c < W;
+    const bool mine = r >= 1 && r < W - 1 && c >= 1 && c < W - 1;  // active in some sweep
+    for (int pid = blockIdx.x; pid < *a.count; pid += gridDim.x) {
+        const int64_t cell = a.cells[pid];
+        const int iv0 = (int)(cell / (g.nh - 1)), ih0 = (int)(cell - (int64_t)iv0 * (g.nh - 1));
+        const int R0 = iv0 - (K + 1), C0 = ih0 - (K + 1);
+        __syncthreads();  // the previous cell's reads are done
+        if (inbox) {
+            const int64_t i = (int64_t)(R0 + r) * g.nh + (C0 + c);
+            sx[t] = g.x[i];
+            sy[t] = g.y[i];
+            sf[t] = a.f[i];
+            sd[t] = (r < W - 1 && c < W - 1) ? g.diag[(int64_t)(R0 + r) * (g.nh - 1) + (C0 + c)] : 0;
+        }
+        __syncthreads();
+        // this vertex's edges in k_gd_grad's order: left, right, down, up, then the diagonals
+        int nb[8];
+        unsigned em = 0;
+        double ex[8], ey[8], r3[8], c6[8];
+        double q0 = 0.0, q1 = 0.0, q3 = 0.0, inv = 0.0;
+        if (mine) {
+            nb[0] = t - 1;
+            nb[1] = t + 1;
+            nb[2] = t - P;
+            nb[3] = t + P;
+            nb[4] = t - P - 1;
+            nb[5] = t - P + 1;
+            nb[6] = t + P - 1;
+            nb[7] = t + P + 1;
+            em = 0x0fu | (sd[t - P - 1] == 0 ? 0x10u : 0u) | (sd[t - P] == 1 ? 0x20u : 0u) |
+                 (sd[t - 1] == 1 ? 0x40u : 0u) | (sd[t] == 0 ? 0x80u : 0u);
+            const double xi = sx[t], yi = sy[t], fi = sf[t];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                ex[k] = ey[k] = r3[k] = c6[k] = 0.0;
+                if (!(em & (1u << k))) continue;
+                const int j = nb[k];
+                const double exk = sx[j] - xi, eyk = sy[j] - yi;
+                const double l2 = exk * exk + eyk * eyk;
+                double rr = __builtin_amdgcn_rsq(l2);
+                rr = rr * __builtin_fma(-0.5 * l2 * rr, rr, 1.5);
+                const double r3k = rr * rr * rr;
+                const double wx = exk * r3k, wy = eyk * r3k;
+                q0 = __builtin_fma(exk, wx, q0);
+                q1 = __builtin_fma(exk, wy, q1);
+                q3 = __builtin_fma(eyk, wy, q3);
+                ex[k] = exk;
+                ey[k] = eyk;
+                r3[k] = r3k;
+                c6[k] = 6 * (fi - sf[j]);
+            }
+            q0 = 4 * q0;
+            q1 = 4 * q1;
+            q3 = 4 * q3;
+            inv = 1.0 / (q0 * q3 - q1 * q1);
+        }
+        // the sums of one sweep from iterate buffer `in` (in < 0: x_0 = 0), solve_vals' solve
+        auto sweep_r = [&](int in, double& r0, double& r1) {
+            double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                if (!(em & (1u << k))) continue;
+                double gxj = 0.0, gyj = 0.0;
+                if (in >= 0) {
+                    const double2 gj = sg[in][nb[k]];
+                    gxj = gj.x;
+                    gyj = gj.y;
+                }
+                const double df2 = -ex[k] * gxj - ey[k] * gyj;
+                const double w = c6[k] - 2 * df2;
+                const double wx = ex[k] * r3[k], wy = ey[k] * r3[k];
+                s0 = __builtin_fma(w, wx, s0);
+                s1 = __builtin_fma(w, wy, s1);
+            }
+            r0 = (q3 * s0 - q1 * s1) * inv;
+            r1 = (-q1 * s0 + q0 * s1) * inv;
+        };
+        for (int j = 1; j <= K; ++j) {
+            const int side = 2 * (K + 1 - j) + 2, off = j;
+            if (mine && r >= off && r < off + side && c >= off && c < off + side) {
+                const int in = j == 1 ? -1 : ((j - 1) & 1), out = j & 1;
+                const ConeStep st = a.st[j];
+                double r0, r1;
+                sweep_r(in, r0, r1);
+                double ox, oy;
+                if (st.mode == 2) {
+                    const double2 pv = sg[out][t];  // x_{j-2}, overwritten below
+                    ox = st.omega * (-r0 - pv.x) + pv.x;
+                    oy = st.omega * (-r1 - pv.y) + pv.y;
+                } else if (st.mode == 1) {
+                    ox = st.omega * (-r0 - 0.0) + 0.0;
+                    oy = st.omega * (-r1 - 0.0) + 0.0;
+                } else {
+                    ox = -r0;
+                    oy = -r1;
+                }
+                sg[out][t] = make_double2(ox, oy);
+            }
+            __syncthreads();
+        }
+        // the cell's corners: x_K out, and the change one more (plain-measured) sweep would make
+        const bool corner = (r == K + 1 || r == K + 2) && (c == K + 1 || c == K + 2);
+        if (corner) {
+            const int fin = K & 1;
+            const double2 gk = sg[fin][t];
+            const int64_t i = (int64_t)(R0 + r) * g.nh + (C0 + c);
+            a.gout[2 * i] = gk.x;
+            a.gout[2 * i + 1] = gk.y;
+            if (a.chg) {
+                double r0, r1;
+                sweep_r(fin, r0, r1);
+                const double cm = fmax(fabs(gk.x + r0), fabs(gk.y + r1)) / fmax(1.0, fmax(fabs(r0), fabs(r1)));
+                if (cm > 0) atomicMax(a.chg, (unsigned long long)__double_as_longlong(cm));
+            }
         }
     }
 }
@@ -1816,6 +2062,14 @@ int gd_no_xcd() {
     static int b = getenv("AKB_GD_NOXCD") != nullptr ? 1 : 0;
     return b;
 }
+bool gd_band_split() {  // A/B: the band sweep as two launches (band, then ring)
+    static bool b = getenv("AKB_GD_BAND_SPLIT") != nullptr;
+    return b;
+}
+bool gd_patch_v1() {  // A/B: the 256-thread patch kernel for one value set
+    static bool b = getenv("AKB_GD_PATCH_V1") != nullptr;
+    return b;
+}
 bool gd_no_change() {
     static bool b = getenv("AKB_GD_NOCHG") != nullptr;
     return b;
@@ -2102,14 +2356,23 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
             for (int j = 1; j <= K; ++j) {
                 const double* gin = j == 1 ? nullptr : gb[(j - 1) % 3];
                 const double* gprev = j >= 3 ? gb[(j + 1) % 3] : nullptr;
+                const unsigned nbw = grid_for(bm.total, 1, kStreamGridCap), nrw = grid_for(L * 64);
                 if (nvv == 2) {
                     ConeBand<2> a{fv, gin, gprev, gb[j % 3], ring_acc, steps[j], band};
-                    k_gd_cone_band<2><<<grid_for(bm.total, 1, kStreamGridCap), kBlock, 0, s>>>(g, bm, a);
-                    k_gd_cone_ring<2><<<grid_for(L * 64), kBlock, 0, s>>>(g, a);
+                    if (gd_band_split()) {
+                        k_gd_cone_band<2><<<nbw, kBlock, 0, s>>>(g, bm, a);
+                        k_gd_cone_ring<2><<<nrw, kBlock, 0, s>>>(g, a);
+                    } else {
+                        k_gd_cone_sweep<2><<<nbw + nrw, kBlock, 0, s>>>(g, bm, a, (int)nbw);
+                    }
                 } else {
                     ConeBand<1> a{fv, gin, gprev, gb[j % 3], ring_acc, steps[j], band};
-                    k_gd_cone_band<1><<<grid_for(bm.total, 1, kStreamGridCap), kBlock, 0, s>>>(g, bm, a);
-                    k_gd_cone_ring<1><<<grid_for(L * 64), kBlock, 0, s>>>(g, a);
+                    if (gd_band_split()) {
+                        k_gd_cone_band<1><<<nbw, kBlock, 0, s>>>(g, bm, a);
+                        k_gd_cone_ring<1><<<nrw, kBlock, 0, s>>>(g, a);
+                    } else {
+                        k_gd_cone_sweep<1><<<nbw + nrw, kBlock, 0, s>>>(g, bm, a, (int)nbw);
+                    }
                 }
                 if ((st = launch_status("k_gd_cone_band"))) return st;
             }
@@ -2121,7 +2384,10 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
         } else {
             ConePatch<1> a{fv, cells, count, K, {}, gb[K % 3], d_change};
             for (int j = 0; j <= K; ++j) a.st[j] = steps[j];
-            k_gd_cone_patch<1><<<pg, 256, 0, s>>>(g, a);
+            if (gd_patch_v1())
+                k_gd_cone_patch<1><<<pg, 256, 0, s>>>(g, a);
+            else
+                k_gd_cone_patch1<<<pg, 1024, 0, s>>>(g, a);
         }
         if ((st = launch_status("k_gd_cone_patch"))) return st;
         if (cnt)

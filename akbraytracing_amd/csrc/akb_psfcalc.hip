@@ -370,9 +370,17 @@ __device__ __forceinline__ void block_sum(double (&acc)[Q], double (*red)[Q]) {
     __syncthreads();
 }
 
+// the B-spline prefilter runs in LDS for maps of up to 128 x 128 (a padded pitch nx + 1 spreads
+// the row lines over the banks): its lines are sequential recursions, and through L2 each step
+// would wait for a load
+constexpr int kSplineLds = 128 * 129;
+
 __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
-    __shared__ PwTree trees[8];
+    __shared__ double smem[kSplineLds];  // the nanmean's trees, later one prefilter array
+    static_assert(8 * sizeof(PwTree) <= sizeof(smem), "nanmean trees in the prefilter buffer");
+    PwTree* trees = reinterpret_cast<PwTree*>(smem);
     __shared__ double bufsum[8];
+    __shared__ int firstrow[2];
     __shared__ double red[kPostThreads / 64][kMomMax];
     __shared__ double sys[32];
     __shared__ int sflag;
@@ -473,11 +481,21 @@ __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
     }
     __syncthreads();
     // psf_calc's rotation estimate (:1122-1132): the first valid row of columns nx / 4 and 3 nx / 4
+    // (every row tested at once, the smallest kept)
+    if (tid < 2) firstrow[tid] = a.ny;
+    __syncthreads();
+    {
+        const int c1 = a.nx / 4, c3 = a.nx * 3 / 4;
+        for (int r = tid; r < 2 * a.ny; r += kPostThreads) {
+            const int row = r >> 1, c = (r & 1) ? c3 : c1;
+            const double v = a.corrected[(int64_t)row * a.nx + c];
+            if (v == v) atomicMin(&firstrow[r & 1], row);
+        }
+    }
+    __syncthreads();
     if (tid == 0) {
         const int c1 = a.nx / 4, c3 = a.nx * 3 / 4;
-        int r1 = 0, r3 = 0;
-        while (r1 < a.ny && a.corrected[(int64_t)r1 * a.nx + c1] != a.corrected[(int64_t)r1 * a.nx + c1]) ++r1;
-        while (r3 < a.ny && a.corrected[(int64_t)r3 * a.nx + c3] != a.corrected[(int64_t)r3 * a.nx + c3]) ++r3;
+        const int r1 = firstrow[0], r3 = firstrow[1];
         const double q = (r1 < a.ny && r3 < a.ny) ? (double)(r1 - r3) / (double)(c1 - c3) : __builtin_nan("");
         const double rot = atan(q);
         const double deg = rot * (180.0 / 3.14159265358979323846);
@@ -492,19 +510,42 @@ __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
     }
     __syncthreads();
     // rotate_with_nan(order 3): NaN split, the B-spline prefilter along both axes, the rotation
-    for (int64_t k = tid; k < total; k += kPostThreads) {
-        const double v = a.corrected[k];
-        const bool nan = v != v;
-        a.coef[k] = nan ? 0.0 : v;
-        a.coef[total + k] = nan ? 0.0 : 1.0;
+    const int pitch = a.nx + 1;
+    if ((int64_t)a.ny * pitch <= kSplineLds) {
+        for (int arr = 0; arr < 2; ++arr) {  // the NaN-filled map, then its finite mask
+            for (int64_t k = tid; k < total; k += kPostThreads) {
+                const double v = a.corrected[k];
+                const bool nan = v != v;
+                const int i = (int)(k / a.nx), j = (int)(k - (int64_t)i * a.nx);
+                smem[i * pitch + j] = nan ? 0.0 : (arr == 0 ? v : 1.0);
+            }
+            __syncthreads();
+            for (int l = tid; l < a.nx; l += kPostThreads) spline_line(smem + l, a.ny, pitch);
+            __syncthreads();
+            for (int l = tid; l < a.ny; l += kPostThreads) spline_line(smem + (int64_t)l * pitch, a.nx, 1);
+            __syncthreads();
+            double* out = a.coef + (int64_t)arr * total;
+            for (int64_t k = tid; k < total; k += kPostThreads) {
+                const int i = (int)(k / a.nx), j = (int)(k - (int64_t)i * a.nx);
+                out[k] = smem[i * pitch + j];
+            }
+            __syncthreads();
+        }
+    } else {
+        for (int64_t k = tid; k < total; k += kPostThreads) {
+            const double v = a.corrected[k];
+            const bool nan = v != v;
+            a.coef[k] = nan ? 0.0 : v;
+            a.coef[total + k] = nan ? 0.0 : 1.0;
+        }
+        __syncthreads();
+        for (int l = tid; l < 2 * a.nx; l += kPostThreads)
+            spline_line(a.coef + (int64_t)(l / a.nx) * total + (l % a.nx), a.ny, a.nx);
+        __syncthreads();
+        for (int l = tid; l < 2 * a.ny; l += kPostThreads)
+            spline_line(a.coef + (int64_t)(l / a.ny) * total + (int64_t)(l % a.ny) * a.nx, a.nx, 1);
+        __syncthreads();
     }
-    __syncthreads();
-    for (int l = tid; l < 2 * a.nx; l += kPostThreads)
-        spline_line(a.coef + (int64_t)(l / a.nx) * total + (l % a.nx), a.ny, a.nx);
-    __syncthreads();
-    for (int l = tid; l < 2 * a.ny; l += kPostThreads)
-        spline_line(a.coef + (int64_t)(l / a.ny) * total + (int64_t)(l % a.ny) * a.nx, a.nx, 1);
-    __syncthreads();
     RotArgs ra{a.coef, a.ny, a.nx, sys[18], sys[19], -sys[19], sys[18], sys[20], sys[21], a.rotated, a.opd};
     for (int64_t k = tid; k < total; k += kPostThreads) rotate_pixel(ra, k);
     if (tid == 0) {
