@@ -250,6 +250,104 @@ __global__ void __launch_bounds__(kBlock) k_gd_cells(Grid g, uint8_t* diag, doub
     }
 }
 
+// k_gd_cells on 16 x 16 tiles of the window's cells, one workgroup each: the tile's 18 x 18
+// vertices in LDS (its cells, the next row's and column's), each of its 17 x 17 cells' diagonal
+// formed once (cell_diag's arithmetic on the same values), then each cell's checks from LDS. Per
+// cell: ~1.3 vertex loads and ~3 in-circle tests instead of ~10 and 5. Same diagonals and flags.
+constexpr int kCellTile = 16;
+__global__ void __launch_bounds__(kCellTile * kCellTile) k_gd_cells_tiled(Grid g, uint8_t* diag, double tol,
+                                                                        unsigned* flags) {
+    constexpr int T = kCellTile, V = T + 2;
+    __shared__ double vx[V * V], vy[V * V];
+    __shared__ uint8_t sdg[(T + 1) * (T + 1)];
+    const int r_lo = g.row0, r_hi = g.row1 < 0 ? g.nv - 1 : g.row1;  // window cell rows [r_lo, r_hi)
+    const int tiles_h = (g.nh - 1 + T - 1) / T;
+    const int64_t ntiles = (int64_t)((r_hi - r_lo + T - 1) / T) * tiles_h;
+    unsigned acc = 0;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int tv = (int)(tile / tiles_h), th = (int)(tile - (int64_t)tv * tiles_h);
+        const int iv0 = r_lo + tv * T, ih0 = th * T;
+        __syncthreads();
+        for (int k = threadIdx.x; k < V * V; k += blockDim.x) {
+            const int rr = k / V, cc = k - (k / V) * V;
+            const int iv = iv0 + rr, ih = ih0 + cc;
+            double x = 0.0, y = 0.0;
+            if (iv < g.nv && ih < g.nh && iv <= r_hi + 1) {
+                const int64_t q = (int64_t)iv * g.nh + ih;
+                x = g.x[q];
+                y = g.y[q];
+            }
+            vx[k] = x;
+            vy[k] = y;
+        }
+        __syncthreads();
+        // the diagonals of the tile's cells and of the next row / column (cell_diag's arithmetic)
+        auto diag_of = [&](int rr, int cc, double* viol) {
+            const int k00 = rr * V + cc, k01 = k00 + 1, k10 = k00 + V, k11 = k10 + 1;
+            const double x0 = vx[k00], y0 = vy[k00];
+            const double bx = vx[k01] - x0, by = vy[k01] - y0;
+            const double cx = vx[k11] - x0, cy = vy[k11] - y0;
+            const double dx = vx[k10] - x0, dy = vy[k10] - y0;
+            const double ic = incircle(0.0, 0.0, bx, by, cx, cy, dx, dy);
+            const int d = ic > 0 ? 1 : 0;
+            if (viol) {
+                const double sgn = d == 0 ? orient(0, 0, bx, by, cx, cy) * orient(0, 0, cx, cy, dx, dy)
+                                          : orient(0, 0, bx, by, dx, dy) * orient(bx, by, cx, cy, dx, dy);
+                *viol = sgn > 0 ? 0.0 : 1.0;
+            }
+            return d;
+        };
+        double bad = 0.0;
+        const int rr = threadIdx.x / T, cc = threadIdx.x - (threadIdx.x / T) * T;
+        const int iv = iv0 + rr, ih = ih0 + cc;
+        const bool own = iv < r_hi && ih < g.nh - 1;
+        const int d = own ? diag_of(rr, cc, &bad) : 0;
+        sdg[rr * (T + 1) + cc] = (uint8_t)d;
+        if (threadIdx.x < 2 * T + 1) {  // the next row (T + 1 cells) and column (T cells)
+            const int r2 = threadIdx.x <= T ? T : (int)threadIdx.x - (T + 1);
+            const int c2 = threadIdx.x <= T ? (int)threadIdx.x : T;
+            const int jv = iv0 + r2, jh = ih0 + c2;
+            sdg[r2 * (T + 1) + c2] =
+                (jv < g.nv - 1 && jh < g.nh - 1 && jv <= r_hi) ? (uint8_t)diag_of(r2, c2, nullptr) : (uint8_t)0;
+        }
+        __syncthreads();
+        if (!own) continue;
+        const int64_t c = (int64_t)iv * (g.nh - 1) + ih;
+        diag[c] = (uint8_t)d;
+        unsigned f = bad > 0 ? 1u : 0u;
+        const int k00 = rr * V + cc, k01 = k00 + 1, k10 = k00 + V, k11 = k10 + 1;
+        if (!isfinite(vx[k00]) || !isfinite(vy[k00])) f |= 32u;
+        {
+            const double o = orient(vx[k00], vy[k00], vx[k01], vy[k01], vx[k11], vy[k11]);
+            f |= o > 0 ? 8u : (o < 0 ? 16u : 1u);
+        }
+        if (ih + 1 < g.nh - 1) {  // right edge p01-p11 against the next cell's left triangle
+            const int dn = sdg[rr * (T + 1) + cc + 1];
+            const int mine = d == 0 ? k00 : k10, other = dn == 0 ? k11 + 1 : k01 + 1;
+            const double x0 = vx[k01], y0 = vy[k01];
+            const double ax = vx[mine] - x0, ay = vy[mine] - y0, cx = vx[k11] - x0, cy = vy[k11] - y0;
+            const double ox = vx[other] - x0, oy = vy[other] - y0;
+            const double sc = fmax(fmax(fabs(ax), fabs(ay)), fmax(fmax(fabs(cx), fabs(cy)), fmax(fabs(ox), fabs(oy))));
+            if (incircle(0.0, 0.0, ax, ay, cx, cy, ox, oy) > tol * sc * sc * sc * sc) f |= 2u;
+        }
+        if (iv + 1 < g.nv - 1) {  // top edge p10-p11 against the next row's bottom triangle
+            const int dn = sdg[(rr + 1) * (T + 1) + cc];
+            const int mine = d == 0 ? k00 : k01, other = dn == 0 ? k11 + V : k10 + V;
+            const double x0 = vx[k10], y0 = vy[k10];
+            const double ax = vx[mine] - x0, ay = vy[mine] - y0, cx = vx[k11] - x0, cy = vy[k11] - y0;
+            const double ox = vx[other] - x0, oy = vy[other] - y0;
+            const double sc = fmax(fmax(fabs(ax), fabs(ay)), fmax(fmax(fabs(cx), fabs(cy)), fmax(fabs(ox), fabs(oy))));
+            if (incircle(0.0, 0.0, ax, ay, cx, cy, ox, oy) > tol * sc * sc * sc * sc) f |= 2u;
+        }
+        acc |= f;
+    }
+    for (int off = 32; off > 0; off >>= 1) acc |= __shfl_down(acc, off);
+    if ((threadIdx.x & 63) == 0) {
+        const unsigned cur = __hip_atomic_load(flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((cur | acc) != cur) atomicOr(flags, acc);
+    }
+}
+
 // ring positions -> coordinates, for the host pocket builder (bit 5 of flags: a non-finite one)
 __global__ void k_gd_ring(Grid g, double* rx, double* ry, unsigned* flags) {
     const int64_t a = g.nh - 1, b = g.nv - 1, L = 2 * a + 2 * b;
@@ -1545,7 +1643,6 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch1(Grid g, ConePatch<1> a)
     __shared__ double sx[P * P], sy[P * P], sf[P * P];
     __shared__ double2 sg[2][P * P];
     __shared__ uint8_t sd[P * P];
-    const int64_t n = (int64_t)g.nv * g.nh;
     const int K = a.K, W = 2 * K + 4;
     const int t = threadIdx.x, r = t / P, c = t - (t / P) * P;
     const bool inbox = r < W && c < W;
@@ -1878,49 +1975,114 @@ __device__ __forceinline__ bool axis_uniform_part(const double* a, int m, int i)
     return fabs((a[i] - a[0]) / step - i) <= 1e-7;
 }
 
-__global__ void __launch_bounds__(kBlock) k_gd_claim_cells(Grid g, Targets t, int* owner) {
-    // the index-box estimate below needs evenly spaced axes (np.linspace, the driver's); any other
+// one cell's claims (its two triangles' targets)
+__device__ __forceinline__ void claim_cell(const Grid& g, const Targets& t, int64_t c, bool uniform, double inv_dx,
+                                           double inv_dy, int* owner) {
+    const int iv = (int)(c / (g.nh - 1)), ih = (int)(c - (int64_t)iv * (g.nh - 1));
+    const int64_t p00 = (int64_t)iv * g.nh + ih;
+    const double xa = g.x[p00], xb = g.x[p00 + 1], xc = g.x[p00 + g.nh], xd = g.x[p00 + g.nh + 1];
+    const double ya = g.y[p00], yb = g.y[p00 + 1], yc = g.y[p00 + g.nh], yd = g.y[p00 + g.nh + 1];
+    const double xlo = fmin(fmin(xa, xb), fmin(xc, xd)), xhi = fmax(fmax(xa, xb), fmax(xc, xd));
+    const double ylo = fmin(fmin(ya, yb), fmin(yc, yd)), yhi = fmax(fmax(ya, yb), fmax(yc, yd));
+    const double padx = (xhi - xlo) * 1e-9, pady = (yhi - ylo) * 1e-9;
+    int c0, c1, r0, r1;
+    if (uniform) {
+        if (!axis_range(t.gx, t.mx, inv_dx, xlo - padx, xhi + padx, c0, c1)) return;
+        if (!axis_range(t.gy, t.my, inv_dy, ylo - pady, yhi + pady, r0, r1)) return;
+    } else {
+        c0 = lower_idx(t.gx, t.mx, xlo - padx);
+        c1 = lower_idx(t.gx, t.mx, xhi + padx);
+        r0 = lower_idx(t.gy, t.my, ylo - pady);
+        r1 = lower_idx(t.gy, t.my, yhi + pady);
+        if (c0 >= c1 || r0 >= r1) return;
+    }
+    // the exact box within the estimate: targets with lo <= coordinate < hi (as lower_idx gives)
+    while (c0 < c1 && t.gx[c0] < xlo - padx) ++c0;
+    while (c1 > c0 && t.gx[c1 - 1] >= xhi + padx) --c1;
+    if (c0 >= c1) return;
+    while (r0 < r1 && t.gy[r0] < ylo - pady) ++r0;
+    while (r1 > r0 && t.gy[r1 - 1] >= yhi + pady) --r1;
+    if (r0 >= r1) return;
+    for (int half = 0; half < 2; ++half) {
+        const int64_t id = 2 * c + half;
+        const Tri T = tri_verts(g, id);
+        int tc0, tc1, tr0, tr1;
+        tri_box(g, t, T, tc0, tc1, tr0, tr1);
+        for (int r = max(r0, tr0); r < min(r1, tr1); ++r)
+            for (int cc = max(c0, tc0); cc < min(c1, tc1); ++cc) claim_one(g, t, T, (int)id, r, cc, owner);
+    }
+}
+
+// the claim kernels' axis test: whether both axes are linspaces (workgroup-wide; every thread)
+__device__ __forceinline__ bool axes_uniform(const Targets& t) {
+    // the index-box estimate needs evenly spaced axes (np.linspace, the driver's); any other
     // ascending axis takes the exact binary search (lower_idx) of the per-triangle claim
     bool ok = true;
     for (int i = threadIdx.x; i < t.mx || i < t.my; i += blockDim.x)
         ok = ok && axis_uniform_part(t.gx, t.mx, i) && axis_uniform_part(t.gy, t.my, i);
-    const bool uniform = __syncthreads_and(ok) != 0;
+    return __syncthreads_and(ok) != 0;
+}
+
+__global__ void __launch_bounds__(kBlock) k_gd_claim_cells(Grid g, Targets t, int* owner) {
+    const bool uniform = axes_uniform(t);
     const double inv_dx = inv_step(t.gx, t.mx), inv_dy = inv_step(t.gy, t.my);
     for (int64_t c = win_cell0(g) + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < win_cell1(g);
-         c += (int64_t)gridDim.x * blockDim.x) {
-        const int iv = (int)(c / (g.nh - 1)), ih = (int)(c - (int64_t)iv * (g.nh - 1));
-        const int64_t p00 = (int64_t)iv * g.nh + ih;
-        const double xa = g.x[p00], xb = g.x[p00 + 1], xc = g.x[p00 + g.nh], xd = g.x[p00 + g.nh + 1];
-        const double ya = g.y[p00], yb = g.y[p00 + 1], yc = g.y[p00 + g.nh], yd = g.y[p00 + g.nh + 1];
-        const double xlo = fmin(fmin(xa, xb), fmin(xc, xd)), xhi = fmax(fmax(xa, xb), fmax(xc, xd));
-        const double ylo = fmin(fmin(ya, yb), fmin(yc, yd)), yhi = fmax(fmax(ya, yb), fmax(yc, yd));
-        const double padx = (xhi - xlo) * 1e-9, pady = (yhi - ylo) * 1e-9;
-        int c0, c1, r0, r1;
-        if (uniform) {
-            if (!axis_range(t.gx, t.mx, inv_dx, xlo - padx, xhi + padx, c0, c1)) continue;
-            if (!axis_range(t.gy, t.my, inv_dy, ylo - pady, yhi + pady, r0, r1)) continue;
-        } else {
-            c0 = lower_idx(t.gx, t.mx, xlo - padx);
-            c1 = lower_idx(t.gx, t.mx, xhi + padx);
-            r0 = lower_idx(t.gy, t.my, ylo - pady);
-            r1 = lower_idx(t.gy, t.my, yhi + pady);
-            if (c0 >= c1 || r0 >= r1) continue;
+         c += (int64_t)gridDim.x * blockDim.x)
+        claim_cell(g, t, c, uniform, inv_dx, inv_dy, owner);
+}
+
+// k_gd_claim_cells by 8 x 8 blocks of the window's cells, a wave each: the bounding box of the
+// block's 9 x 9 vertices (a superset of each of its cells' boxes, so of their candidate targets)
+// tested first, and only a block with a candidate target claims cell by cell. The targets are
+// sparse against the cells (a 128^2 grid over 1e7 cells: ~85 % of the blocks hold none), so most
+// cells are settled by one 81-vertex load per block. Same claims as k_gd_claim_cells.
+__global__ void __launch_bounds__(kBlock) k_gd_claim_blocks(Grid g, Targets t, int* owner) {
+    const bool uniform = axes_uniform(t);
+    const double inv_dx = inv_step(t.gx, t.mx), inv_dy = inv_step(t.gy, t.my);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int r_lo = g.row0, r_hi = g.row1 < 0 ? g.nv - 1 : g.row1;
+    const int bh = (g.nh - 1 + 7) / 8;
+    const int64_t nblk = (int64_t)((r_hi - r_lo + 7) / 8) * bh;
+    for (int64_t blk = (int64_t)blockIdx.x * nw + wv; blk < nblk; blk += (int64_t)gridDim.x * nw) {
+        const int bv = (int)(blk / bh), bc = (int)(blk - (int64_t)bv * bh);
+        const int iv0 = r_lo + bv * 8, ih0 = bc * 8;
+        const int nr = min(8, r_hi - iv0), nc = min(8, g.nh - 1 - ih0);  // cells; vertices one more
+        double xlo = INFINITY, xhi = -INFINITY, ylo = INFINITY, yhi = -INFINITY;
+        bool nonfinite = false;
+        for (int k = lane; k < (nr + 1) * (nc + 1); k += 64) {
+            const int vr = k / (nc + 1), vc = k - (k / (nc + 1)) * (nc + 1);
+            const int64_t q = (int64_t)(iv0 + vr) * g.nh + (ih0 + vc);
+            const double x = g.x[q], y = g.y[q];
+            nonfinite = nonfinite || !isfinite(x) || !isfinite(y);
+            xlo = fmin(xlo, x);
+            xhi = fmax(xhi, x);
+            ylo = fmin(ylo, y);
+            yhi = fmax(yhi, y);
         }
-        // the exact box within the estimate: targets with lo <= coordinate < hi (as lower_idx gives)
-        while (c0 < c1 && t.gx[c0] < xlo - padx) ++c0;
-        while (c1 > c0 && t.gx[c1 - 1] >= xhi + padx) --c1;
-        if (c0 >= c1) continue;
-        while (r0 < r1 && t.gy[r0] < ylo - pady) ++r0;
-        while (r1 > r0 && t.gy[r1 - 1] >= yhi + pady) --r1;
-        if (r0 >= r1) continue;
-        for (int half = 0; half < 2; ++half) {
-            const int64_t id = 2 * c + half;
-            const Tri T = tri_verts(g, id);
-            int tc0, tc1, tr0, tr1;
-            tri_box(g, t, T, tc0, tc1, tr0, tr1);
-            for (int r = max(r0, tr0); r < min(r1, tr1); ++r)
-                for (int cc = max(c0, tc0); cc < min(c1, tc1); ++cc) claim_one(g, t, T, (int)id, r, cc, owner);
+        for (int off = 32; off > 0; off >>= 1) {
+            xlo = fmin(xlo, __shfl_xor(xlo, off));
+            xhi = fmax(xhi, __shfl_xor(xhi, off));
+            ylo = fmin(ylo, __shfl_xor(ylo, off));
+            yhi = fmax(yhi, __shfl_xor(yhi, off));
         }
+        // a non-finite vertex (a run that raises): its cells as k_gd_claim_cells would see them
+        const bool any_nf = __any(nonfinite);
+        if (!any_nf) {
+            const double padx = (xhi - xlo) * 1e-9, pady = (yhi - ylo) * 1e-9;
+            int c0, c1, r0, r1;
+            bool hit;
+            if (uniform) {
+                hit = axis_range(t.gx, t.mx, inv_dx, xlo - padx, xhi + padx, c0, c1) &&
+                      axis_range(t.gy, t.my, inv_dy, ylo - pady, yhi + pady, r0, r1);
+            } else {
+                hit = lower_idx(t.gx, t.mx, xlo - padx) < lower_idx(t.gx, t.mx, xhi + padx) &&
+                      lower_idx(t.gy, t.my, ylo - pady) < lower_idx(t.gy, t.my, yhi + pady);
+            }
+            if (!hit) continue;
+        }
+        const int rr = lane >> 3, cc = lane & 7;
+        if (rr < nr && cc < nc) claim_cell(g, t, (int64_t)(iv0 + rr) * (g.nh - 1) + (ih0 + cc), uniform, inv_dx, inv_dy,
+                                           owner);
     }
 }
 
@@ -2062,8 +2224,30 @@ int gd_no_xcd() {
     static int b = getenv("AKB_GD_NOXCD") != nullptr ? 1 : 0;
     return b;
 }
-bool gd_band_split() {  // A/B: the band sweep as two launches (band, then ring)
-    static bool b = getenv("AKB_GD_BAND_SPLIT") != nullptr;
+bool gd_claim_v1() {  // A/B: the per-cell claim kernel
+    static bool b = getenv("AKB_GD_CLAIM_V1") != nullptr;
+    return b;
+}
+bool gd_cells_v1() {  // A/B: the per-cell (untiled) cell pass
+    static bool b = getenv("AKB_GD_CELLS_V1") != nullptr;
+    return b;
+}
+// the cell pass over the window's `rows` cell rows
+int launch_cells(const Grid& g, uint8_t* diag, double tol, unsigned* d_flags, int rows, hipStream_t s) {
+    const int64_t wc = (int64_t)rows * (g.nh - 1);
+    if (gd_cells_v1()) {
+        k_gd_cells<<<grid_for(wc, 1, kStreamGridCap), kBlock, 0, s>>>(g, diag, tol, d_flags);
+    } else {
+        const int64_t tiles = (int64_t)((rows + kCellTile - 1) / kCellTile) * ((g.nh - 1 + kCellTile - 1) / kCellTile);
+        k_gd_cells_tiled<<<(unsigned)(tiles < 4096 ? tiles : 4096), kCellTile * kCellTile, 0, s>>>(g, diag, tol,
+                                                                                                    d_flags);
+    }
+    return launch_status("k_gd_cells");
+}
+bool gd_band_split() {  // the band sweep as two launches (band, then ring); AKB_GD_BAND_MERGED: one
+    // (measured slower: 37 us vs 16 + 13 per sweep beside the passes - the ring's grid edges then
+    // wait behind its chord reduction on one lane)
+    static bool b = getenv("AKB_GD_BAND_MERGED") == nullptr;
     return b;
 }
 bool gd_patch_v1() {  // A/B: the 256-thread patch kernel for one value set
@@ -2090,9 +2274,7 @@ int akb_gd_cells_f64(const double* x, const double* y, int nv, int nh, uint8_t* 
     AKB_REQUIRE(nv >= 2 && nh >= 2, "grid of at least 2 x 2 points");
     hipStream_t s = (hipStream_t)stream;
     Grid g{x, y, nv, nh, diag, 0, nullptr, nullptr, nullptr, nullptr, nullptr};
-    const int64_t nc = (int64_t)(nv - 1) * (nh - 1);
-    k_gd_cells<<<grid_for(nc, 1, kStreamGridCap), kBlock, 0, s>>>(g, diag, tol, d_flags);
-    int st = launch_status("k_gd_cells");
+    int st = launch_cells(g, diag, tol, d_flags, nv - 1, s);
     if (st) return st;
     const int64_t L = 2 * (int64_t)(nh - 1) + 2 * (int64_t)(nv - 1);
     k_gd_ring<<<grid_for(L), kBlock, 0, s>>>(g, ring_x, ring_y, d_flags);
@@ -2270,8 +2452,10 @@ int akb_gd_eval_f64(const double* x, const double* y, int nv, int nh, const uint
     const int64_t ntri = 2 * (int64_t)(nv - 1) * (nh - 1) + npock;
     if (getenv("AKB_GD_CLAIM_TRI"))  // the per-triangle claim (A/B and the tests' cross-check)
         k_gd_claim<<<grid_for(ntri - npock, 1, gd_grid_cap()), kBlock, 0, s>>>(g, t, owner);
-    else
+    else if (gd_claim_v1())
         k_gd_claim_cells<<<grid_for((ntri - npock) / 2, 1, kStreamGridCap), kBlock, 0, s>>>(g, t, owner);
+    else
+        k_gd_claim_blocks<<<grid_for((ntri - npock) / 32 + 1, 1, kStreamGridCap), kBlock, 0, s>>>(g, t, owner);
     st = launch_status("k_gd_claim");
     if (st) return st;
     if (npock > 0) {
@@ -2312,7 +2496,10 @@ int cone_claims(const Grid& g, const Targets& t, int with_pockets, int* owner, h
     if (st) return st;
     const int64_t wc = (int64_t)((g.row1 < 0 ? g.nv - 1 : g.row1) - g.row0) * (g.nh - 1);
     if (wc > 0) {
-        k_gd_claim_cells<<<grid_for(wc, 1, kStreamGridCap), kBlock, 0, s>>>(g, t, owner);
+        if (gd_claim_v1())
+            k_gd_claim_cells<<<grid_for(wc, 1, kStreamGridCap), kBlock, 0, s>>>(g, t, owner);
+        else
+            k_gd_claim_blocks<<<grid_for(wc / 16 + 1, 1, kStreamGridCap), kBlock, 0, s>>>(g, t, owner);
         if ((st = launch_status("k_gd_claim"))) return st;
     }
     if (with_pockets && g.npock > 0) {
@@ -2479,8 +2666,7 @@ int akb_gd_cells_window_f64(const double* x, const double* y, int nv, int nh, in
     g.row1 = row1;
     const int64_t wc = (int64_t)(row1 - row0) * (nh - 1);
     if (wc == 0) return 0;
-    k_gd_cells<<<grid_for(wc, 1, kStreamGridCap), kBlock, 0, (hipStream_t)stream>>>(g, diag, tol, d_flags);
-    return launch_status("k_gd_cells");
+    return launch_cells(g, diag, tol, d_flags, row1 - row0, (hipStream_t)stream);
 }
 
 }  // extern "C"
