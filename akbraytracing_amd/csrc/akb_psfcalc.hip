@@ -119,6 +119,15 @@ __global__ void k_rotate_cubic(RotArgs a) {
         rotate_pixel(a, k);
 }
 
+// rotate_with_nan's interpolation after k_pupil_post: scipy.ndimage.rotate's matrix and offsets
+// from its parameter block (cos, sin, offsets at [13 .. 17), akb_raytrace.h)
+__global__ void k_rotate_post(const double* coef, int ny, int nx, const double* P, double* rotated, double* opd) {
+    const RotArgs ra{coef, ny, nx, P[13], P[14], -P[14], P[13], P[15], P[16], rotated, opd};
+    const int64_t total = (int64_t)ny * nx;
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < total; k += (int64_t)gridDim.x * blockDim.x)
+        rotate_pixel(ra, k);
+}
+
 // ---- plane_correction_with_nan_and_outlier_filter (ref :9630-9693) and match_legendre (:59-73) ----
 //
 // Both are least-squares / projection steps over a 2-D map with NaNs. The device forms the sums
@@ -401,15 +410,19 @@ __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
     double tot = 0.0;
     for (int b = 0; b < nbuf; ++b) tot = tot + bufsum[b];
     const double mean = tot / cnt[0];
-    // matrixWave2 - nanmean, into `corrected` (the plane correction's input)
-    for (int64_t k = tid; k < total; k += kPostThreads) a.corrected[k] = a.m[k] - mean;
+    // matrixWave2 - nanmean, the plane correction's input: in LDS when it fits (the trees are done
+    // with; the moment passes then read it there), else in `corrected`
+    const bool in_lds = total <= kSplineLds;
+    double* cm = in_lds ? smem : a.corrected;
+    __syncthreads();
+    for (int64_t k = tid; k < total; k += kPostThreads) cm[k] = a.m[k] - mean;
     __syncthreads();
     // plane_correction_with_nan_and_outlier_filter: the four moment passes of k_moments
     auto moments = [&](int nb, const double* cf, double thr, int mode, double mu, double (&acc)[kMomMax]) {
 #pragma unroll
         for (int q = 0; q < kMomMax; ++q) acc[q] = 0.0;
         for (int64_t k = tid; k < total; k += kPostThreads) {
-            const double z = a.corrected[k];
+            const double z = cm[k];
             if (z != z) continue;
             const int i = (int)(k / a.nx), j = (int)(k - (int64_t)i * a.nx);
             double f[5];
@@ -476,8 +489,10 @@ __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
         double f[5];
         basis5(i, j, a.ny, a.nx, f);
         const double pl = __builtin_fma(sys[10], f[2], __builtin_fma(sys[9], f[1], sys[8] * f[0]));
-        const double v = a.corrected[k];
-        a.corrected[k] = v != v ? v : v - pl;
+        const double v = cm[k];
+        const double o = v != v ? v : v - pl;
+        cm[k] = o;
+        if (in_lds) a.corrected[k] = o;
     }
     __syncthreads();
     // psf_calc's rotation estimate (:1122-1132): the first valid row of columns nx / 4 and 3 nx / 4
@@ -488,7 +503,7 @@ __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
         const int c1 = a.nx / 4, c3 = a.nx * 3 / 4;
         for (int r = tid; r < 2 * a.ny; r += kPostThreads) {
             const int row = r >> 1, c = (r & 1) ? c3 : c1;
-            const double v = a.corrected[(int64_t)row * a.nx + c];
+            const double v = cm[(int64_t)row * a.nx + c];
             if (v == v) atomicMin(&firstrow[r & 1], row);
         }
     }
@@ -511,6 +526,7 @@ __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
     __syncthreads();
     // rotate_with_nan(order 3): NaN split, the B-spline prefilter along both axes, the rotation
     const int pitch = a.nx + 1;
+    __syncthreads();  // the rotation estimate's reads of cm are done
     if ((int64_t)a.ny * pitch <= kSplineLds) {
         for (int arr = 0; arr < 2; ++arr) {  // the NaN-filled map, then its finite mask
             for (int64_t k = tid; k < total; k += kPostThreads) {
@@ -546,8 +562,7 @@ __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
             spline_line(a.coef + (int64_t)(l / a.ny) * total + (int64_t)(l % a.ny) * a.nx, a.nx, 1);
         __syncthreads();
     }
-    RotArgs ra{a.coef, a.ny, a.nx, sys[18], sys[19], -sys[19], sys[18], sys[20], sys[21], a.rotated, a.opd};
-    for (int64_t k = tid; k < total; k += kPostThreads) rotate_pixel(ra, k);
+    // the rotation itself: k_rotate_post, across the GPU
     if (tid == 0) {
         P[0] = mean;
         P[1] = cnt[0];
@@ -740,7 +755,12 @@ int akb_pupil_post_f64(const double* map, int ny, int nx, double sigma, double* 
     AKB_REQUIRE((int64_t)ny * nx <= kPostMax, "the one-workgroup post handles maps of up to 65536 points");
     PostArgs a{map, ny, nx, sigma, corrected, rotated, opd, (double*)work, d_params};
     k_pupil_post<<<1, kPostThreads, 0, (hipStream_t)stream>>>(a);
-    return launch_status("k_pupil_post");
+    int st = launch_status("k_pupil_post");
+    if (st) return st;
+    const int64_t total = (int64_t)ny * nx;
+    k_rotate_post<<<grid_for(total, 4, 128), kBlock, 0, (hipStream_t)stream>>>((const double*)work, ny, nx, d_params,
+                                                                             rotated, opd);
+    return launch_status("k_rotate_post");
 }
 
 int akb_legendre_rows_f64(const double* data, int n, int K, int order, const double* px, const double* py,

@@ -10,15 +10,15 @@ timeout -k 10 700 python -u -m pytest tests/test_gpu_parity.py tests/test_faithf
   > gpurun_out/r04f_pytest.log 2>&1
 rc=$?; tail -6 gpurun_out/r04f_pytest.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof6 -o run -- \
-    python3 scripts/micro_faithful.py --out gpurun_out/mf_new.npz > gpurun_out/r04f_micro.log 2>&1
+    python3 scripts/micro_faithful.py --out /tmp/mf_new.npz > gpurun_out/r04f_micro.log 2>&1
 rc=$?; tail -2 gpurun_out/r04f_micro.log; fatal $rc && exit $rc; [ $rc -eq 0 ] || exit $rc
-head -16 gpurun_out/prof6/run_kernel_stats.csv | cut -d, -f1-4 | cut -c1-140
+python3 scripts/kstats.py gpurun_out/prof6/run_kernel_stats.csv; rm -f gpurun_out/prof6/run_kernel_trace.csv
 AKB_GD_CELLS_V1=1 AKB_GD_CLAIM_V1=1 AKB_GD_PATCH_V1=1 timeout -k 10 300 python3 scripts/micro_faithful.py --reps 5 \
-    --out gpurun_out/mf_old.npz > gpurun_out/r04f_micro_old.log 2>&1
+    --out /tmp/mf_old.npz > gpurun_out/r04f_micro_old.log 2>&1
 rc=$?; tail -1 gpurun_out/r04f_micro_old.log; fatal $rc && exit $rc
 python3 -c "
 import numpy as np
-a, b = np.load('gpurun_out/mf_new.npz'), np.load('gpurun_out/mf_old.npz')
+a, b = np.load('/tmp/mf_new.npz'), np.load('/tmp/mf_old.npz')
 print('new == old:', {k: bool(np.array_equal(a[k], b[k], equal_nan=True)) for k in a.files})"
 timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-extras > gpurun_out/r04f_bench.json 2> gpurun_out/r04f_bench.err
 rc=$?; tail -c 600 gpurun_out/r04f_bench.json; exit $rc
