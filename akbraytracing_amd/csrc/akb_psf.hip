@@ -1462,7 +1462,7 @@ int akb_psf_f64(const double* opd, const double* amp, int ny, int nx, int pad, i
         const char* pk = getenv("AKB_PSF_PEAK");
         const bool peak32 = pk && strcmp(pk, "f32") == 0;
         const bool bound = pk ? strcmp(pk, "bound") == 0 : (int64_t)g.py * g.px >= (1LL << 24);
-        const bool select = psf_sel_ok(g) && pk && strcmp(pk, "select") == 0;  // opt-in until measured
+        const bool select = psf_sel_ok(g) && (pk ? strcmp(pk, "select") == 0 : !bound);
         if (select) {
             char* sp = tail + 256 + 4 * psf_line_rows_bytes(g, batch);
             la.bpart = (double*)sp;
