@@ -105,6 +105,8 @@ def parse():
                    help="faithful (default): each step's PSF is the reference's own - griddata(cubic) of Wave2 "
                         "(cone solve), nanmean removal, plane correction, psf_calc - pipelined on the back stream "
                         "(akbraytracing_amd/faithful.py); standin: RayWave.pupil's ray-index sampler (rounds 1-3)")
+    p.add_argument("--cone-sweeps", type=int, default=None,
+                   help="Chebyshev sweeps of the faithful pupil's cone solve (default griddata.CONE_SWEEPS)")
     p.add_argument("--faithful-lag", type=int, default=None,
                    help="faithful runs whose pocket jobs may be in flight before a step waits for the oldest "
                         "(default 3; 6 at N > 1, where the band owner builds configs[3]'s 40k-point ring)")
@@ -460,13 +462,14 @@ def main():
     if faithful and world == 1:
         from akbraytracing_amd.faithful import FaithfulPupil
         fp = FaithfulPupil(n, n, size=args.pupil, pad=args.pad, wavelengths=my_lams,
-                           slots=args.faithful_lag + 3)
+                           slots=args.faithful_lag + 3, **({"sweeps": args.cone_sweeps} if args.cone_sweeps else {}))
     elif faithful:
         # N > 1: the pupil sharded with the rays (halo rows + the boundary band to rank 0, no gather
         # of the hits: faithful_dist.py); rank 0 forms the map, the plane correction and the stack
         from akbraytracing_amd.faithful_dist import ShardedFaithfulPupil
         fp = ShardedFaithfulPupil(n, comm, size=args.pupil, pad=args.pad, wavelengths=lams,
-                                  slots=args.faithful_lag + 2, workers=4)
+                                  slots=args.faithful_lag + 2, workers=4,
+                                  **({"sweeps": args.cone_sweeps} if args.cone_sweeps else {}))
 
     def faithful_back(timed, f):
         """The reference's pupil and PSF of the oldest front: its tilt and OPD were fused into later
