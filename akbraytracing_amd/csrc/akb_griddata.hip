@@ -2006,10 +2006,26 @@ __device__ __forceinline__ void claim_cell(const Grid& g, const Targets& t, int6
     for (int half = 0; half < 2; ++half) {
         const int64_t id = 2 * c + half;
         const Tri T = tri_verts(g, id);
-        int tc0, tc1, tr0, tr1;
-        tri_box(g, t, T, tc0, tc1, tr0, tr1);
-        for (int r = max(r0, tr0); r < min(r1, tr1); ++r)
-            for (int cc = max(c0, tc0); cc < min(c1, tc1); ++cc) claim_one(g, t, T, (int)id, r, cc, owner);
+        // tri_box within the cell's box: the triangle's padded range lies inside the cell's, so its
+        // lower_idx bounds lie in [c0, c1] / [r0, r1] and a scan from the cell's bounds finds them
+        // (the binary searches over the whole axis were the kernel's longest dependent chains)
+        double txlo = g.x[T.v[0]], txhi = txlo, tylo = g.y[T.v[0]], tyhi = tylo;
+        for (int k = 1; k < 3; ++k) {
+            txlo = fmin(txlo, g.x[T.v[k]]);
+            txhi = fmax(txhi, g.x[T.v[k]]);
+            tylo = fmin(tylo, g.y[T.v[k]]);
+            tyhi = fmax(tyhi, g.y[T.v[k]]);
+        }
+        const double tpx = (txhi - txlo) * 1e-9, tpy = (tyhi - tylo) * 1e-9;
+        int tc0 = c0, tr0 = r0;
+        while (tc0 < c1 && t.gx[tc0] < txlo - tpx) ++tc0;
+        int tc1 = tc0;
+        while (tc1 < c1 && t.gx[tc1] < txhi + tpx) ++tc1;
+        while (tr0 < r1 && t.gy[tr0] < tylo - tpy) ++tr0;
+        int tr1 = tr0;
+        while (tr1 < r1 && t.gy[tr1] < tyhi + tpy) ++tr1;
+        for (int r = tr0; r < tr1; ++r)
+            for (int cc = tc0; cc < tc1; ++cc) claim_one(g, t, T, (int)id, r, cc, owner);
     }
 }
 

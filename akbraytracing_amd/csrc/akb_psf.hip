@@ -687,6 +687,7 @@ __global__ void __launch_bounds__((LineShape<N, PAD>::kThreads)) k_psf_line(PsfL
     __shared__ double2 Gs[MODE == kLinePupil ? LINES : 1][5];
     __shared__ int Lc[MODE == kLinePupil ? LINES : 1];
     __shared__ int lrows[kSelPeak ? kSelRows : 1];
+    __shared__ double ssum[kSelPeak ? 3 * kSel + kSelRows : 1];  // samples (re, im, sum |G|), row bounds
     __shared__ int lcount;
     __shared__ double msel;
     const PsfGeom g = A.g;
@@ -735,41 +736,50 @@ __global__ void __launch_bounds__((LineShape<N, PAD>::kThreads)) k_psf_line(PsfL
         }
     }
     if (kSelPeak && A.bpart && !rows) {
-        // M_low from the samples (threads 0 .. kSel - 1 of wave 0), parts summed in workgroup order
+        // M_low from the samples and the bounds of this workgroup's rows: the workgroups' parts
+        // summed by all threads at once (LDS atomics: any order gives a valid bound, the margins
+        // cover the rounding; a long per-thread chain of L2 loads would be the kernel's critical path)
+        const int np = A.npart;
+        const int64_t pb = (int64_t)b * np;
+        int nmine = 0;
+        for (int k = 0; group_at(k) >= 0; ++k) nmine += LINES;
+        const bool fits = nmine <= kSelRows;
+        for (int e = threadIdx.x; e < 3 * kSel + kSelRows; e += S::kThreads) ssum[e] = 0.0;
+        if (threadIdx.x == 0) lcount = 0;
+        __syncthreads();
+        for (int e = threadIdx.x; e < kSel * np; e += S::kThreads) {
+            const int k = e % kSel, w = e / kSel;
+            const double2 tv = A.spart[(pb + w) * 32 + k];
+            atomicAdd(&ssum[k], tv.x);
+            atomicAdd(&ssum[kSel + k], tv.y);
+            atomicAdd(&ssum[2 * kSel + k], A.bpart[(pb + w) * g.py + g.py / 2 - 2 + k / 5]);
+        }
+        if (fits)
+            for (int e = threadIdx.x; e < nmine * np; e += S::kThreads) {
+                const int q = e / np, w = e - (e / np) * np;
+                const int row = group_at(q / LINES) * LINES + q % LINES;
+                if (row < nl) atomicAdd(&ssum[3 * kSel + q], A.bpart[(pb + w) * g.py + row]);
+            }
+        __syncthreads();
         double mk = 0.0;
         if (threadIdx.x < kSel) {
-            double2 sv = make_double2(0.0, 0.0);
-            double bs = 0.0;
-            const int ko = g.py / 2 - 2 + threadIdx.x / 5;
-            for (int w = 0; w < A.npart; ++w) {
-                const double2 t = A.spart[((int64_t)b * A.npart + w) * 32 + threadIdx.x];
-                sv.x += t.x;
-                sv.y += t.y;
-                bs += A.bpart[((int64_t)b * A.npart + w) * g.py + ko];
-            }
-            const double as = sqrt(fma(sv.x, sv.x, sv.y * sv.y)), dl = bs * 0x1p-30;
+            const double sx = ssum[threadIdx.x], sy = ssum[kSel + threadIdx.x], bs = ssum[2 * kSel + threadIdx.x];
+            const double as = sqrt(fma(sx, sx, sy * sy)), dl = bs * 0x1p-30;
             mk = as > dl ? ((as - dl) * (as - dl)) * (1.0 - 0x1p-30) : (as == as && dl == dl ? 0.0 : as + dl);
         }
         if (threadIdx.x < 64) {
             for (int off = 32; off > 0; off >>= 1) mk = dmax_nan(mk, __shfl_down(mk, off));
-            if (threadIdx.x == 0) {
-                msel = mk;
-                lcount = 0;
-            }
+            if (threadIdx.x == 0) msel = mk;
         }
         __syncthreads();
         const double M = msel;
         const bool all = !(M > 0.0) || !isfinite(M);
         // this workgroup's rows (the all-rows pass's assignment): keep those with B >= M_low
-        int nmine = 0;
-        for (int k = 0; group_at(k) >= 0; ++k) nmine += LINES;
-        if (!all && nmine <= kSelRows) {
-            for (int e = threadIdx.x; e < nmine; e += S::kThreads) {
-                const int row = group_at(e / LINES) * LINES + e % LINES;
-                if (row >= nl) continue;
-                double bs = 0.0;
-                for (int w = 0; w < A.npart; ++w) bs += A.bpart[((int64_t)b * A.npart + w) * g.py + row];
-                if (!((bs * bs) * kBoundMarginSel < M)) lrows[atomicAdd(&lcount, 1)] = row;
+        if (!all && fits) {
+            for (int q = threadIdx.x; q < nmine; q += S::kThreads) {
+                const int row = group_at(q / LINES) * LINES + q % LINES;
+                const double bs = ssum[3 * kSel + q];
+                if (row < nl && !((bs * bs) * kBoundMarginSel < M)) lrows[atomicAdd(&lcount, 1)] = row;
             }
             __syncthreads();
             nl = lcount;

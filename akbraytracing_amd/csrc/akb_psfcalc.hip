@@ -379,10 +379,39 @@ __device__ __forceinline__ void block_sum(double (&acc)[Q], double (*red)[Q]) {
     __syncthreads();
 }
 
-// the B-spline prefilter runs in LDS for maps of up to 128 x 128 (a padded pitch nx + 1 spreads
-// the row lines over the banks): its lines are sequential recursions, and through L2 each step
-// would wait for a load
+// LDS of the post: the nanmean's trees, then the map for the moment passes (maps of up to 16512
+// points; larger ones are read from `corrected`)
 constexpr int kSplineLds = 128 * 129;
+
+// spline_filter1d along one axis in LDS: a workgroup of 64 threads takes 64 lines of one array
+// (blockIdx.y: map, mask) - a line is a sequential recursion, so through L2 each step would wait
+// for a load; in LDS (pitch lines + 1 against bank conflicts) it waits for LDS only. Lines of up to
+// 256 points; spline_line's arithmetic.
+constexpr int kSplineLines = 64, kSplineMaxLen = 256;
+__global__ void __launch_bounds__(kSplineLines) k_spline_block(double* __restrict__ coef, int ny, int nx, int axis) {
+    __shared__ double buf[kSplineMaxLen * (kSplineLines + 1)];
+    const int nlines = axis == 0 ? nx : ny, len = axis == 0 ? ny : nx;
+    const int l0 = blockIdx.x * kSplineLines, nl = min(kSplineLines, nlines - l0);
+    double* base = coef + (int64_t)blockIdx.y * ny * nx;
+    const int P = kSplineLines + 1;  // buf[i * P + l]: point i of line l
+    for (int e = threadIdx.x; e < len * nl; e += blockDim.x) {
+        int i, l;
+        if (axis == 0) { i = e / nl; l = e - (e / nl) * nl; }  // columns: read along rows (coalesced)
+        else { l = e / len; i = e - (e / len) * len; }         // rows: read along the row
+        const int64_t gi = axis == 0 ? (int64_t)i * nx + (l0 + l) : (int64_t)(l0 + l) * nx + i;
+        buf[i * P + l] = base[gi];
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < nl) spline_line(buf + threadIdx.x, len, P);
+    __syncthreads();
+    for (int e = threadIdx.x; e < len * nl; e += blockDim.x) {
+        int i, l;
+        if (axis == 0) { i = e / nl; l = e - (e / nl) * nl; }
+        else { l = e / len; i = e - (e / len) * len; }
+        const int64_t gi = axis == 0 ? (int64_t)i * nx + (l0 + l) : (int64_t)(l0 + l) * nx + i;
+        base[gi] = buf[i * P + l];
+    }
+}
 
 __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
     __shared__ double smem[kSplineLds];  // the nanmean's trees, later one prefilter array
@@ -524,43 +553,14 @@ __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
         sys[21] = cx - (-sn * cy + cs * cx);
     }
     __syncthreads();
-    // rotate_with_nan(order 3): NaN split, the B-spline prefilter along both axes, the rotation
-    const int pitch = a.nx + 1;
-    __syncthreads();  // the rotation estimate's reads of cm are done
-    if ((int64_t)a.ny * pitch <= kSplineLds) {
-        for (int arr = 0; arr < 2; ++arr) {  // the NaN-filled map, then its finite mask
-            for (int64_t k = tid; k < total; k += kPostThreads) {
-                const double v = a.corrected[k];
-                const bool nan = v != v;
-                const int i = (int)(k / a.nx), j = (int)(k - (int64_t)i * a.nx);
-                smem[i * pitch + j] = nan ? 0.0 : (arr == 0 ? v : 1.0);
-            }
-            __syncthreads();
-            for (int l = tid; l < a.nx; l += kPostThreads) spline_line(smem + l, a.ny, pitch);
-            __syncthreads();
-            for (int l = tid; l < a.ny; l += kPostThreads) spline_line(smem + (int64_t)l * pitch, a.nx, 1);
-            __syncthreads();
-            double* out = a.coef + (int64_t)arr * total;
-            for (int64_t k = tid; k < total; k += kPostThreads) {
-                const int i = (int)(k / a.nx), j = (int)(k - (int64_t)i * a.nx);
-                out[k] = smem[i * pitch + j];
-            }
-            __syncthreads();
-        }
-    } else {
-        for (int64_t k = tid; k < total; k += kPostThreads) {
-            const double v = a.corrected[k];
-            const bool nan = v != v;
-            a.coef[k] = nan ? 0.0 : v;
-            a.coef[total + k] = nan ? 0.0 : 1.0;
-        }
-        __syncthreads();
-        for (int l = tid; l < 2 * a.nx; l += kPostThreads)
-            spline_line(a.coef + (int64_t)(l / a.nx) * total + (l % a.nx), a.ny, a.nx);
-        __syncthreads();
-        for (int l = tid; l < 2 * a.ny; l += kPostThreads)
-            spline_line(a.coef + (int64_t)(l / a.ny) * total + (int64_t)(l % a.ny) * a.nx, a.nx, 1);
-        __syncthreads();
+    // rotate_with_nan(order 3): the NaN split here; the B-spline prefilter (k_spline_block, its
+    // lines spread over workgroups) and the rotation (k_rotate_post) follow as their own launches
+    __syncthreads();
+    for (int64_t k = tid; k < total; k += kPostThreads) {
+        const double v = a.corrected[k];
+        const bool nan = v != v;
+        a.coef[k] = nan ? 0.0 : v;
+        a.coef[total + k] = nan ? 0.0 : 1.0;
     }
     // the rotation itself: k_rotate_post, across the GPU
     if (tid == 0) {
@@ -758,6 +758,15 @@ int akb_pupil_post_f64(const double* map, int ny, int nx, double sigma, double* 
     int st = launch_status("k_pupil_post");
     if (st) return st;
     const int64_t total = (int64_t)ny * nx;
+    for (int axis = 0; axis < 2; ++axis) {
+        const int nlines = axis == 0 ? nx : ny, len = axis == 0 ? ny : nx;
+        if (len <= kSplineMaxLen)
+            k_spline_block<<<dim3((nlines + kSplineLines - 1) / kSplineLines, 2), kSplineLines, 0,
+                             (hipStream_t)stream>>>((double*)work, ny, nx, axis);
+        else
+            k_spline_lines<<<dim3((nlines + 63) / 64, 2), 64, 0, (hipStream_t)stream>>>((double*)work, ny, nx, axis);
+        if ((st = launch_status("k_spline"))) return st;
+    }
     k_rotate_post<<<grid_for(total, 4, 128), kBlock, 0, (hipStream_t)stream>>>((const double*)work, ny, nx, d_params,
                                                                              rotated, opd);
     return launch_status("k_rotate_post");
