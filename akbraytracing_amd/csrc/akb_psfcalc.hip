@@ -149,6 +149,19 @@ struct MomArgs {
     double* part;           // (gridDim.x, kMomMax)
 };
 
+// basis5 from per-axis tables (the same X, Y values; tables only for axes of up to kPostBasisMax)
+constexpr int kPostBasisMax = 1024;
+__device__ __forceinline__ void basis5_tab(const double* bX, const double* bY, int i, int j, int ny, int nx,
+                                           double (&f)[5]) {
+    const double X = nx <= kPostBasisMax && ny <= kPostBasisMax ? bX[j] : (nx > 1 ? (2.0 * j - (nx - 1)) / (double)(nx - 1) : 0.0);
+    const double Y = nx <= kPostBasisMax && ny <= kPostBasisMax ? bY[i] : (ny > 1 ? (2.0 * i - (ny - 1)) / (double)(ny - 1) : 0.0);
+    f[0] = 1.0;
+    f[1] = X;
+    f[2] = Y;
+    f[3] = X * X;
+    f[4] = Y * Y;
+}
+
 __device__ __forceinline__ void basis5(int i, int j, int ny, int nx, double (&f)[5]) {
     const double X = nx > 1 ? (2.0 * j - (nx - 1)) / (double)(nx - 1) : 0.0;
     const double Y = ny > 1 ? (2.0 * i - (ny - 1)) / (double)(ny - 1) : 0.0;
@@ -387,8 +400,8 @@ constexpr int kSplineLds = 128 * 129;
 // (blockIdx.y: map, mask) - a line is a sequential recursion, so through L2 each step would wait
 // for a load; in LDS (pitch lines + 1 against bank conflicts) it waits for LDS only. Lines of up to
 // 256 points; spline_line's arithmetic.
-constexpr int kSplineLines = 64, kSplineMaxLen = 256;
-__global__ void __launch_bounds__(kSplineLines) k_spline_block(double* __restrict__ coef, int ny, int nx, int axis) {
+constexpr int kSplineLines = 64, kSplineMaxLen = 256, kSplineThreads = 256;
+__global__ void __launch_bounds__(kSplineThreads) k_spline_block(double* __restrict__ coef, int ny, int nx, int axis) {
     __shared__ double buf[kSplineMaxLen * (kSplineLines + 1)];
     const int nlines = axis == 0 ? nx : ny, len = axis == 0 ? ny : nx;
     const int l0 = blockIdx.x * kSplineLines, nl = min(kSplineLines, nlines - l0);
@@ -422,9 +435,17 @@ __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
     __shared__ double red[kPostThreads / 64][kMomMax];
     __shared__ double sys[32];
     __shared__ int sflag;
+    // basis5's X (per column) and Y (per row), each division once (the moment passes and the plane
+    // subtraction would repeat two divisions per point each)
+    __shared__ double bX[kPostBasisMax], bY[kPostBasisMax];
     const int64_t total = (int64_t)a.ny * a.nx;
     const int tid = threadIdx.x, w = tid >> 6;
     double* P = a.params;
+    const bool tab = a.nx <= kPostBasisMax && a.ny <= kPostBasisMax;
+    if (tab) {
+        for (int j = tid; j < a.nx; j += kPostThreads) bX[j] = a.nx > 1 ? (2.0 * j - (a.nx - 1)) / (double)(a.nx - 1) : 0.0;
+        for (int i = tid; i < a.ny; i += kPostThreads) bY[i] = a.ny > 1 ? (2.0 * i - (a.ny - 1)) / (double)(a.ny - 1) : 0.0;
+    }
     // np.nanmean: numpy's pairwise sum of the NaN-zeroed map, one wave per 8192-element buffer
     const int nbuf = (int)((total + 8191) / 8192);
     if (w < nbuf) {
@@ -453,9 +474,9 @@ __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
         for (int64_t k = tid; k < total; k += kPostThreads) {
             const double z = cm[k];
             if (z != z) continue;
-            const int i = (int)(k / a.nx), j = (int)(k - (int64_t)i * a.nx);
+            const int i = (int)k / a.nx, j = (int)k - ((int)k / a.nx) * a.nx;
             double f[5];
-            basis5(i, j, a.ny, a.nx, f);
+            basis5_tab(bX, bY, i, j, a.ny, a.nx, f);
             double res = 0.0;
             if (cf || mode > 0) {
                 double mm = 0.0;
@@ -514,9 +535,9 @@ __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
     if (tid == 0 && acc[20] < 3) sflag |= 1;
     normal_solve(acc, 3, 8);                  // p2 = sys[8..11)
     for (int64_t k = tid; k < total; k += kPostThreads) {
-        const int i = (int)(k / a.nx), j = (int)(k - (int64_t)i * a.nx);
+        const int i = (int)k / a.nx, j = (int)k - ((int)k / a.nx) * a.nx;
         double f[5];
-        basis5(i, j, a.ny, a.nx, f);
+        basis5_tab(bX, bY, i, j, a.ny, a.nx, f);
         const double pl = __builtin_fma(sys[10], f[2], __builtin_fma(sys[9], f[1], sys[8] * f[0]));
         const double v = cm[k];
         const double o = v != v ? v : v - pl;
@@ -761,7 +782,7 @@ int akb_pupil_post_f64(const double* map, int ny, int nx, double sigma, double* 
     for (int axis = 0; axis < 2; ++axis) {
         const int nlines = axis == 0 ? nx : ny, len = axis == 0 ? ny : nx;
         if (len <= kSplineMaxLen)
-            k_spline_block<<<dim3((nlines + kSplineLines - 1) / kSplineLines, 2), kSplineLines, 0,
+            k_spline_block<<<dim3((nlines + kSplineLines - 1) / kSplineLines, 2), kSplineThreads, 0,
                              (hipStream_t)stream>>>((double*)work, ny, nx, axis);
         else
             k_spline_lines<<<dim3((nlines + 63) / 64, 2), 64, 0, (hipStream_t)stream>>>((double*)work, ny, nx, axis);
