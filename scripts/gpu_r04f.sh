@@ -22,12 +22,12 @@ a, b = np.load('/tmp/mf_new.npz'), np.load('/tmp/mf_old.npz')
 print('new == old:', {k: bool(np.array_equal(a[k], b[k], equal_nan=True)) for k in a.files})"
 timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-extras > gpurun_out/r04f_bench.json 2> gpurun_out/r04f_bench.err
 rc=$?; fatal $rc && exit $rc
-timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-extras --cone-sweeps 12 \
-    > gpurun_out/r04f_bench12.json 2> gpurun_out/r04f_bench12.err
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-extras --cone-sweeps 14 \
+    > gpurun_out/r04f_bench14.json 2> gpurun_out/r04f_bench14.err
 rc2=$?
 python3 -c "
 import json
-for f in ('gpurun_out/r04f_bench.json', 'gpurun_out/r04f_bench12.json'):
+for f in ('gpurun_out/r04f_bench.json', 'gpurun_out/r04f_bench14.json'):
     try:
         d = json.loads([l for l in open(f) if l.startswith('{')][-1])
         print(f, {k: d.get(k) for k in ('value', 'ms_per_step', 'ms_per_step_no_ramp', 'faithful_chain_ms', 'faithful_finish_ms', 'psf_ms', 'host_issue_ms_per_step')})
