@@ -19,7 +19,7 @@ c_int = ctypes.c_int
 c_dbl = ctypes.c_double
 c_vp = ctypes.c_void_p
 MAX_MIRRORS = 7
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 FLAG_MISS = 0x1
 FLAG_ZERO_NORMAL = 0x2
@@ -182,7 +182,7 @@ def _declare(L):
         "akb_gd_cone_work_bytes": ([c_int, c_int, c_int, c_int, c_int], c_i64),
         "akb_gd_axes_f64": ([c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp], c_int),
         "akb_gd_claims_f64": ([c_vp, c_vp, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp,
-                               c_int, c_vp, c_int, c_vp, c_vp], c_int),
+                               c_int, c_vp, c_int, c_vp, c_vp, c_vp], c_int),
         "akb_gd_cone_part_f64": ([c_vp, c_vp, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
                                   c_int, c_vp, c_int, c_vp, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
                                   c_vp, c_vp], c_int),

@@ -1633,8 +1633,8 @@ __global__ void __launch_bounds__(256) k_gd_cone_patch(Grid g, ConePatch<NV> a) 
 // determinant - does not change between sweeps, so each thread forms its own once per cell, in
 // k_gd_grad's expressions and edge order, and keeps it in registers; a sweep then costs per edge
 // one LDS read of the neighbour's iterate and nine operations (against the full edge_vals: a
-// reciprocal square root and ~25 operations, five LDS reads). The box has pitch 32 (thread =
-// row * 32 + column); x_j overwrites x_{j-2} in place (a vertex reads its own predecessor only),
+// reciprocal square root and ~25 operations, five LDS reads). The box has pitch 32; threads take
+// its vertices in order of depth; x_j overwrites x_{j-2} in place (a vertex reads its own predecessor only),
 // so two iterate buffers suffice. The arithmetic is edge_vals / solve_vals' exactly: x_K at the
 // corners equals k_gd_cone_patch's, bit for bit.
 __global__ void __launch_bounds__(1024) k_gd_cone_patch1(Grid g, ConePatch<1> a) {
@@ -1644,20 +1644,43 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch1(Grid g, ConePatch<1> a)
     __shared__ double2 sg[2][P * P];
     __shared__ uint8_t sd[P * P];
     const int K = a.K, W = 2 * K + 4;
-    const int t = threadIdx.x, r = t / P, c = t - (t / P) * P;
-    const bool inbox = r < W && c < W;
-    const bool mine = r >= 1 && r < W - 1 && c >= 1 && c < W - 1;  // active in some sweep
+    const int t = threadIdx.x;
+    // this thread's vertex, in order of depth from the box's centre outwards: vertex (r, c) of depth
+    // d = min(r, c, W-1-r, W-1-c) takes part in sweeps 1 .. d, so sweep j's vertices are a prefix of
+    // the threads - its waves are full, the rest idle (row-major lanes would run each sweep's
+    // shrinking square at ~half occupancy). The four innermost are the cell's corners.
+    int r = -1, c = -1, dep = 0;
+    {
+        int rem = t;
+        for (int d = W / 2 - 1; d >= 1; --d) {
+            const int s1 = W - 2 * d - 1, cnt = 4 * s1;
+            if (rem < cnt) {
+                if (rem < s1) { r = d; c = d + rem; }
+                else if (rem < 2 * s1) { r = d + (rem - s1); c = d + s1; }
+                else if (rem < 3 * s1) { r = d + s1; c = d + s1 - (rem - 2 * s1); }
+                else { r = d + s1 - (rem - 3 * s1); c = d; }
+                dep = d;
+                break;
+            }
+            rem -= cnt;
+        }
+    }
+    const bool mine = dep >= 1;
+    const int b = mine ? r * P + c : 0;
     for (int pid = blockIdx.x; pid < *a.count; pid += gridDim.x) {
         const int64_t cell = a.cells[pid];
         const int iv0 = (int)(cell / (g.nh - 1)), ih0 = (int)(cell - (int64_t)iv0 * (g.nh - 1));
         const int R0 = iv0 - (K + 1), C0 = ih0 - (K + 1);
         __syncthreads();  // the previous cell's reads are done
-        if (inbox) {
-            const int64_t i = (int64_t)(R0 + r) * g.nh + (C0 + c);
-            sx[t] = g.x[i];
-            sy[t] = g.y[i];
-            sf[t] = a.f[i];
-            sd[t] = (r < W - 1 && c < W - 1) ? g.diag[(int64_t)(R0 + r) * (g.nh - 1) + (C0 + c)] : 0;
+        {
+            const int lr = t / P, lc = t - (t / P) * P;  // the box load, row-major (coalesced)
+            if (lr < W && lc < W) {
+                const int64_t i = (int64_t)(R0 + lr) * g.nh + (C0 + lc);
+                sx[t] = g.x[i];
+                sy[t] = g.y[i];
+                sf[t] = a.f[i];
+                sd[t] = (lr < W - 1 && lc < W - 1) ? g.diag[(int64_t)(R0 + lr) * (g.nh - 1) + (C0 + lc)] : 0;
+            }
         }
         __syncthreads();
         // this vertex's edges in k_gd_grad's order: left, right, down, up, then the diagonals
@@ -1666,17 +1689,17 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch1(Grid g, ConePatch<1> a)
         double ex[8], ey[8], r3[8], c6[8];
         double q0 = 0.0, q1 = 0.0, q3 = 0.0, inv = 0.0;
         if (mine) {
-            nb[0] = t - 1;
-            nb[1] = t + 1;
-            nb[2] = t - P;
-            nb[3] = t + P;
-            nb[4] = t - P - 1;
-            nb[5] = t - P + 1;
-            nb[6] = t + P - 1;
-            nb[7] = t + P + 1;
-            em = 0x0fu | (sd[t - P - 1] == 0 ? 0x10u : 0u) | (sd[t - P] == 1 ? 0x20u : 0u) |
-                 (sd[t - 1] == 1 ? 0x40u : 0u) | (sd[t] == 0 ? 0x80u : 0u);
-            const double xi = sx[t], yi = sy[t], fi = sf[t];
+            nb[0] = b - 1;
+            nb[1] = b + 1;
+            nb[2] = b - P;
+            nb[3] = b + P;
+            nb[4] = b - P - 1;
+            nb[5] = b - P + 1;
+            nb[6] = b + P - 1;
+            nb[7] = b + P + 1;
+            em = 0x0fu | (sd[b - P - 1] == 0 ? 0x10u : 0u) | (sd[b - P] == 1 ? 0x20u : 0u) |
+                 (sd[b - 1] == 1 ? 0x40u : 0u) | (sd[b] == 0 ? 0x80u : 0u);
+            const double xi = sx[b], yi = sy[b], fi = sf[b];
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 ex[k] = ey[k] = r3[k] = c6[k] = 0.0;
@@ -1723,15 +1746,14 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch1(Grid g, ConePatch<1> a)
             r1 = (-q1 * s0 + q0 * s1) * inv;
         };
         for (int j = 1; j <= K; ++j) {
-            const int side = 2 * (K + 1 - j) + 2, off = j;
-            if (mine && r >= off && r < off + side && c >= off && c < off + side) {
+            if (dep >= j) {  // the square [j, W - 1 - j]^2 (depth >= j)
                 const int in = j == 1 ? -1 : ((j - 1) & 1), out = j & 1;
                 const ConeStep st = a.st[j];
                 double r0, r1;
                 sweep_r(in, r0, r1);
                 double ox, oy;
                 if (st.mode == 2) {
-                    const double2 pv = sg[out][t];  // x_{j-2}, overwritten below
+                    const double2 pv = sg[out][b];  // x_{j-2}, overwritten below
                     ox = st.omega * (-r0 - pv.x) + pv.x;
                     oy = st.omega * (-r1 - pv.y) + pv.y;
                 } else if (st.mode == 1) {
@@ -1741,15 +1763,15 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch1(Grid g, ConePatch<1> a)
                     ox = -r0;
                     oy = -r1;
                 }
-                sg[out][t] = make_double2(ox, oy);
+                sg[out][b] = make_double2(ox, oy);
             }
             __syncthreads();
         }
-        // the cell's corners: x_K out, and the change one more (plain-measured) sweep would make
-        const bool corner = (r == K + 1 || r == K + 2) && (c == K + 1 || c == K + 2);
-        if (corner) {
+        // the cell's corners (the innermost ring): x_K out, and the change one more (plain-measured)
+        // sweep would make
+        if (dep == K + 1) {
             const int fin = K & 1;
-            const double2 gk = sg[fin][t];
+            const double2 gk = sg[fin][b];
             const int64_t i = (int64_t)(R0 + r) * g.nh + (C0 + c);
             a.gout[2 * i] = gk.x;
             a.gout[2 * i + 1] = gk.y;
@@ -2096,6 +2118,78 @@ __global__ void __launch_bounds__(kBlock) k_gd_claim_blocks(Grid g, Targets t, i
             }
             if (!hit) continue;
         }
+        const int rr = lane >> 3, cc = lane & 7;
+        if (rr < nr && cc < nc) claim_cell(g, t, (int64_t)(iv0 + rr) * (g.nh - 1) + (ih0 + cc), uniform, inv_dx, inv_dy,
+                                           owner);
+    }
+}
+
+// The claims in two launches (the cone solve's, with scratch): k_gd_claim_scan - one thread per
+// 8 x 8 block of the window's cells, the bounding box of its 9 x 9 vertices tested against the
+// target axes (a superset of its cells' candidate targets; a non-finite vertex marks the block) -
+// then k_gd_claim_hit, a wave per marked block claiming cell by cell. The scan holds few registers,
+// so the whole GPU's worth of blocks is in flight at once (k_gd_claim_blocks' waves, sized for the
+// per-cell claims, walk ~40 blocks each, one load latency after another). Same claims.
+__device__ __forceinline__ void claim_block_dims(const Grid& g, int64_t& nblk, int& bh, int& r_lo, int& r_hi) {
+    r_lo = g.row0;
+    r_hi = g.row1 < 0 ? g.nv - 1 : g.row1;
+    bh = (g.nh - 1 + 7) / 8;
+    nblk = (int64_t)((r_hi - r_lo + 7) / 8) * bh;
+}
+
+__global__ void __launch_bounds__(kBlock) k_gd_claim_scan(Grid g, Targets t, uint8_t* hit) {
+    const bool uniform = axes_uniform(t);
+    const double inv_dx = inv_step(t.gx, t.mx), inv_dy = inv_step(t.gy, t.my);
+    int64_t nblk;
+    int bh, r_lo, r_hi;
+    claim_block_dims(g, nblk, bh, r_lo, r_hi);
+    for (int64_t blk = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; blk < nblk;
+         blk += (int64_t)gridDim.x * blockDim.x) {
+        const int bv = (int)(blk / bh), bc = (int)(blk - (int64_t)bv * bh);
+        const int iv0 = r_lo + bv * 8, ih0 = bc * 8;
+        const int nr = min(8, r_hi - iv0), nc = min(8, g.nh - 1 - ih0);
+        double xlo = INFINITY, xhi = -INFINITY, ylo = INFINITY, yhi = -INFINITY;
+        bool nonfinite = false;
+        for (int vr = 0; vr <= nr; ++vr) {
+            const int64_t q0 = (int64_t)(iv0 + vr) * g.nh + ih0;
+            for (int vc = 0; vc <= nc; ++vc) {
+                const double x = g.x[q0 + vc], y = g.y[q0 + vc];
+                nonfinite = nonfinite || !isfinite(x) || !isfinite(y);
+                xlo = fmin(xlo, x);
+                xhi = fmax(xhi, x);
+                ylo = fmin(ylo, y);
+                yhi = fmax(yhi, y);
+            }
+        }
+        bool h = nonfinite;
+        if (!h) {
+            const double padx = (xhi - xlo) * 1e-9, pady = (yhi - ylo) * 1e-9;
+            int c0, c1, r0, r1;
+            if (uniform) {
+                h = axis_range(t.gx, t.mx, inv_dx, xlo - padx, xhi + padx, c0, c1) &&
+                    axis_range(t.gy, t.my, inv_dy, ylo - pady, yhi + pady, r0, r1);
+            } else {
+                h = lower_idx(t.gx, t.mx, xlo - padx) < lower_idx(t.gx, t.mx, xhi + padx) &&
+                    lower_idx(t.gy, t.my, ylo - pady) < lower_idx(t.gy, t.my, yhi + pady);
+            }
+        }
+        hit[blk] = h ? 1 : 0;
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) k_gd_claim_hit(Grid g, Targets t, const uint8_t* __restrict__ hit,
+                                                         int* owner) {
+    const bool uniform = axes_uniform(t);
+    const double inv_dx = inv_step(t.gx, t.mx), inv_dy = inv_step(t.gy, t.my);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    int64_t nblk;
+    int bh, r_lo, r_hi;
+    claim_block_dims(g, nblk, bh, r_lo, r_hi);
+    for (int64_t blk = (int64_t)blockIdx.x * nw + wv; blk < nblk; blk += (int64_t)gridDim.x * nw) {
+        if (!hit[blk]) continue;
+        const int bv = (int)(blk / bh), bc = (int)(blk - (int64_t)bv * bh);
+        const int iv0 = r_lo + bv * 8, ih0 = bc * 8;
+        const int nr = min(8, r_hi - iv0), nc = min(8, g.nh - 1 - ih0);
         const int rr = lane >> 3, cc = lane & 7;
         if (rr < nr && cc < nc) claim_cell(g, t, (int64_t)(iv0 + rr) * (g.nh - 1) + (ih0 + cc), uniform, inv_dx, inv_dy,
                                            owner);
@@ -2494,28 +2588,42 @@ int akb_gd_axes_f64(const double* ring_x, const double* ring_y, int64_t L, int m
 // ---- cone solve: claims, the fixed-K gradient iteration restricted to what the targets read,
 // the patches; one call, no host synchronisation
 
-int64_t akb_gd_cone_work_bytes(int nv, int nh, int mx, int my, int nvals) {
-    if (nv < 2 || nh < 2 || mx < 1 || my < 1 || nvals < 1) return -1;
+// the claims' block flags, at the end of the cone work buffer
+static int64_t claim_scratch_bytes(int nv, int nh) {
+    return ((int64_t)((nv - 1 + 7) / 8) * ((nh - 1 + 7) / 8) + 63) / 64 * 64;
+}
+static int64_t claim_scratch_offset(int nv, int nh, int mx, int my, int nvals) {
     const int64_t n = (int64_t)nv * nh, L = 2 * (int64_t)(nh - 1) + 2 * (int64_t)(nv - 1);
     const int nv2 = nvals >= 2 ? 2 : 1;
     const int64_t m = (int64_t)mx * my;
-    return 3 * (int64_t)nv2 * n * 2 * 8 + L * 7 * 8 + m * 8 + m + 64;
+    return (3 * (int64_t)nv2 * n * 2 * 8 + L * 7 * 8 + m * 8 + m + 64 + 63) / 64 * 64;
+}
+
+int64_t akb_gd_cone_work_bytes(int nv, int nh, int mx, int my, int nvals) {
+    if (nv < 2 || nh < 2 || mx < 1 || my < 1 || nvals < 1) return -1;
+    return claim_scratch_offset(nv, nh, mx, my, nvals) + claim_scratch_bytes(nv, nh);
 }
 
 namespace {
 
 // the cone solve's claims: owner filled with INT32_MAX, then the window's cells (and the pockets)
-int cone_claims(const Grid& g, const Targets& t, int with_pockets, int* owner, hipStream_t s) {
+int cone_claims(const Grid& g, const Targets& t, int with_pockets, int* owner, hipStream_t s, uint8_t* scratch = nullptr) {
     const int64_t m = (int64_t)t.mx * t.my;
     k_fill_i32<<<grid_for(m, 4), kBlock, 0, s>>>(owner, m, INT32_MAX);
     int st = launch_status("k_fill_i32");
     if (st) return st;
     const int64_t wc = (int64_t)((g.row1 < 0 ? g.nv - 1 : g.row1) - g.row0) * (g.nh - 1);
     if (wc > 0) {
-        if (gd_claim_v1())
+        if (gd_claim_v1()) {
             k_gd_claim_cells<<<grid_for(wc, 1, kStreamGridCap), kBlock, 0, s>>>(g, t, owner);
-        else
+        } else if (scratch) {
+            const int64_t nblk = (int64_t)(((g.row1 < 0 ? g.nv - 1 : g.row1) - g.row0 + 7) / 8) * ((g.nh - 1 + 7) / 8);
+            k_gd_claim_scan<<<grid_for(nblk, 1, kStreamGridCap), kBlock, 0, s>>>(g, t, scratch);
+            if ((st = launch_status("k_gd_claim_scan"))) return st;
+            k_gd_claim_hit<<<grid_for(nblk * 16, 1, kStreamGridCap), kBlock, 0, s>>>(g, t, scratch, owner);
+        } else {
             k_gd_claim_blocks<<<grid_for(wc / 16 + 1, 1, kStreamGridCap), kBlock, 0, s>>>(g, t, owner);
+        }
         if ((st = launch_status("k_gd_claim"))) return st;
     }
     if (with_pockets && g.npock > 0) {
@@ -2620,14 +2728,15 @@ int akb_gd_cone_eval_f64(const double* x, const double* y, int nv, int nh, const
     hipStream_t s = (hipStream_t)stream;
     Grid g{x, y, nv, nh, diag, npock, ptri, pnbr, edge_tri, xptr, xidx};
     Targets t{gx, gy, mx, my};
-    int st = cone_claims(g, t, 1, owner, s);
+    int st = cone_claims(g, t, 1, owner, s, (uint8_t*)work + claim_scratch_offset(nv, nh, mx, my, nvals));
     if (st) return st;
     return cone_part(g, t, 0, (int64_t)nv * nh, 1, f, nvals, K, omegas, work, owner, out, nullptr, d_change, s);
 }
 
 int akb_gd_claims_f64(const double* x, const double* y, int nv, int nh, const uint8_t* diag, int npock,
                       const int32_t* ptri, const int32_t* pnbr, const int32_t* edge_tri, int row0, int row1,
-                      int with_pockets, const double* gx, int mx, const double* gy, int my, int* owner, void* stream) {
+                      int with_pockets, const double* gx, int mx, const double* gy, int my, int* owner, void* work,
+                      void* stream) {
     clear_error();
     AKB_REQUIRE(x && y && diag && gx && gy && owner && mx > 0 && my > 0, "bad arguments");
     AKB_REQUIRE(nv >= 2 && nh >= 2 && row0 >= 0 && row1 <= nv - 1 && (row1 < 0 || row0 <= row1), "bad window");
@@ -2635,7 +2744,8 @@ int akb_gd_claims_f64(const double* x, const double* y, int nv, int nh, const ui
     Grid g{x, y, nv, nh, diag, npock, ptri, pnbr, edge_tri, nullptr, nullptr};
     g.row0 = row0;
     g.row1 = row1;
-    return cone_claims(g, Targets{gx, gy, mx, my}, with_pockets, owner, (hipStream_t)stream);
+    return cone_claims(g, Targets{gx, gy, mx, my}, with_pockets, owner, (hipStream_t)stream,
+                       work ? (uint8_t*)work + claim_scratch_offset(nv, nh, mx, my, 1) : nullptr);
 }
 
 int akb_gd_cone_part_f64(const double* x, const double* y, int nv, int nh, const uint8_t* diag, int npock,

@@ -450,7 +450,7 @@ class ShardedFaithfulPupil:
                 pock, chords = (0, None, None, None), (None, None)
             _broadcast(self.comm, self.axes, p.root, self.group)
             _lib.check(L.akb_gd_claims_f64(vx, vy, n, n, vd, *pock, p.claim[0], p.claim[1], int(p.is_root),
-                                           D.ptr(gx), m, D.ptr(gy), m, D.ptr(self.owner), sh))
+                                           D.ptr(gx), m, D.ptr(gy), m, D.ptr(self.owner), D.ptr(self.work), sh))
             _all_reduce_min(self.comm, self.owner, self.group)
             self.change.zero_()
             _lib.check(L.akb_gd_cone_part_f64(vx, vy, n, n, vd, *pock, *chords, p.own[0], p.own[1], int(p.is_root),

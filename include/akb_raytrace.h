@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define AKB_ABI_VERSION 13
+#define AKB_ABI_VERSION 14
 
 /* status codes */
 #define AKB_OK 0
@@ -549,7 +549,8 @@ int akb_gd_cone_eval_f64(const double* x, const double* y, int nv, int nh, const
  *   akb_gd_ring_f64: the boundary ring's coordinates (the band owner, for the host pockets);
  *   akb_gd_claims_f64: owner[] = INT32_MAX, then the claims of the cells in rows [row0, row1)
  *     (row1 < 0: all) and, with with_pockets, of the pocket triangles; a MIN all-reduce of the
- *     ranks' owners gives the one-process owners (the same atomicMin over all triangles);
+ *     ranks' owners gives the one-process owners (the same atomicMin over all triangles); work
+ *     (or NULL): an akb_gd_cone_work_bytes(nv, nh, mx, my, 1) buffer for the block scan's flags;
  *   akb_gd_cone_part_f64: with that global owner, the targets this rank forms - interior cells
  *     whose p00 lies in its rays [own0, own1), and with band_on every band / pocket target - their
  *     gradients and values: out (nvals, my, mx) and cnt (my, mx) hold value / 1 there, 0 elsewhere,
@@ -562,7 +563,8 @@ int akb_gd_ring_f64(const double* x, const double* y, int nv, int nh, double* ri
                     void* stream);
 int akb_gd_claims_f64(const double* x, const double* y, int nv, int nh, const uint8_t* diag, int npock,
                       const int32_t* ptri, const int32_t* pnbr, const int32_t* edge_tri, int row0, int row1,
-                      int with_pockets, const double* gx, int mx, const double* gy, int my, int* owner, void* stream);
+                      int with_pockets, const double* gx, int mx, const double* gy, int my, int* owner, void* work,
+                      void* stream);
 int akb_gd_cone_part_f64(const double* x, const double* y, int nv, int nh, const uint8_t* diag, int npock,
                          const int32_t* ptri, const int32_t* pnbr, const int32_t* edge_tri, const int32_t* xptr,
                          const int32_t* xidx, int64_t own0, int64_t own1, int band_on, const double* gx, int mx,
