@@ -1637,12 +1637,12 @@ __global__ void __launch_bounds__(256) k_gd_cone_patch(Grid g, ConePatch<NV> a) 
 // its vertices in order of depth; x_j overwrites x_{j-2} in place (a vertex reads its own predecessor only),
 // so two iterate buffers suffice. The arithmetic is edge_vals / solve_vals' exactly: x_K at the
 // corners equals k_gd_cone_patch's, bit for bit.
-__global__ void __launch_bounds__(1024) k_gd_cone_patch1(Grid g, ConePatch<1> a) {
-    constexpr int P = 32;
-    static_assert(kConeBox <= P, "box pitch");
-    __shared__ double sx[P * P], sy[P * P], sf[P * P];
-    __shared__ double2 sg[2][P * P];
-    __shared__ uint8_t sd[P * P];
+__global__ void __launch_bounds__(1024) k_gd_cone_patch1(Grid g, ConePatch<1> a, int rowmajor) {
+    constexpr int P = 33;  // LDS pitch: a column of the box steps 2 banks per row, not 0
+    static_assert(kConeBox < P, "box pitch");
+    __shared__ double sx[P * 32], sy[P * 32], sf[P * 32];
+    __shared__ double2 sg[2][P * 32];
+    __shared__ uint8_t sd[P * 32];
     const int K = a.K, W = 2 * K + 4;
     const int t = threadIdx.x;
     // this thread's vertex, in order of depth from the box's centre outwards: vertex (r, c) of depth
@@ -1650,7 +1650,12 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch1(Grid g, ConePatch<1> a)
     // the threads - its waves are full, the rest idle (row-major lanes would run each sweep's
     // shrinking square at ~half occupancy). The four innermost are the cell's corners.
     int r = -1, c = -1, dep = 0;
-    {
+    if (rowmajor) {  // A/B: lanes along the box's rows
+        r = t / 32;
+        c = t - (t / 32) * 32;
+        dep = (r < W && c < W) ? min(min(r, c), min(W - 1 - r, W - 1 - c)) : 0;
+        if (dep > K + 1) dep = K + 1;
+    } else {
         int rem = t;
         for (int d = W / 2 - 1; d >= 1; --d) {
             const int s1 = W - 2 * d - 1, cnt = 4 * s1;
@@ -1673,13 +1678,14 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch1(Grid g, ConePatch<1> a)
         const int R0 = iv0 - (K + 1), C0 = ih0 - (K + 1);
         __syncthreads();  // the previous cell's reads are done
         {
-            const int lr = t / P, lc = t - (t / P) * P;  // the box load, row-major (coalesced)
+            const int lr = t / 32, lc = t - (t / 32) * 32;  // the box load, row-major (coalesced)
             if (lr < W && lc < W) {
                 const int64_t i = (int64_t)(R0 + lr) * g.nh + (C0 + lc);
-                sx[t] = g.x[i];
-                sy[t] = g.y[i];
-                sf[t] = a.f[i];
-                sd[t] = (lr < W - 1 && lc < W - 1) ? g.diag[(int64_t)(R0 + lr) * (g.nh - 1) + (C0 + lc)] : 0;
+                const int q = lr * P + lc;
+                sx[q] = g.x[i];
+                sy[q] = g.y[i];
+                sf[q] = a.f[i];
+                sd[q] = (lr < W - 1 && lc < W - 1) ? g.diag[(int64_t)(R0 + lr) * (g.nh - 1) + (C0 + lc)] : 0;
             }
         }
         __syncthreads();
@@ -2360,6 +2366,10 @@ bool gd_band_split() {  // the band sweep as two launches (band, then ring); AKB
     static bool b = getenv("AKB_GD_BAND_MERGED") == nullptr;
     return b;
 }
+bool gd_patch_rowmajor() {  // A/B: the register patch kernel's lanes along rows (not by depth)
+    static bool b = getenv("AKB_GD_PATCH_ROWMAJOR") != nullptr;
+    return b;
+}
 bool gd_patch_v1() {  // A/B: the 256-thread patch kernel for one value set
     static bool b = getenv("AKB_GD_PATCH_V1") != nullptr;
     return b;
@@ -2698,7 +2708,7 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
             if (gd_patch_v1())
                 k_gd_cone_patch<1><<<pg, 256, 0, s>>>(g, a);
             else
-                k_gd_cone_patch1<<<pg, 1024, 0, s>>>(g, a);
+                k_gd_cone_patch1<<<pg, 1024, 0, s>>>(g, a, gd_patch_rowmajor() ? 1 : 0);
         }
         if ((st = launch_status("k_gd_cone_patch"))) return st;
         if (cnt)

@@ -13,6 +13,10 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
     python3 scripts/micro_faithful.py --out /tmp/mf_new.npz > gpurun_out/r04f_micro.log 2>&1
 rc=$?; tail -2 gpurun_out/r04f_micro.log; fatal $rc && exit $rc; [ $rc -eq 0 ] || exit $rc
 python3 scripts/kstats.py gpurun_out/prof6/run_kernel_stats.csv; rm -f gpurun_out/prof6/run_kernel_trace.csv
+AKB_GD_PATCH_ROWMAJOR=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof7 -o run -- \
+    python3 scripts/micro_faithful.py --reps 10 > gpurun_out/r04f_micro_rm.log 2>&1
+rc=$?; tail -1 gpurun_out/r04f_micro_rm.log; fatal $rc && exit $rc
+python3 scripts/kstats.py gpurun_out/prof7/run_kernel_stats.csv | head -4; rm -f gpurun_out/prof7/run_kernel_trace.csv
 AKB_GD_CELLS_V1=1 AKB_GD_CLAIM_V1=1 AKB_GD_PATCH_V1=1 timeout -k 10 300 python3 scripts/micro_faithful.py --reps 5 \
     --out /tmp/mf_old.npz > gpurun_out/r04f_micro_old.log 2>&1
 rc=$?; tail -1 gpurun_out/r04f_micro_old.log; fatal $rc && exit $rc
