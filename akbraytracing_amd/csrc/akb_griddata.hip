@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdio.h>
 
 #include <algorithm>
 
@@ -1181,8 +1182,9 @@ __global__ void __launch_bounds__(kBlock) k_gd_ring_chords(Grid g, const double*
 //     per target cell holds the (2K + 4)^2 box around the cell in LDS and runs the K sweeps on the
 //     shrinking square that still influences the cell (x_j on the vertices within K + 1 - j of it);
 //   * the rest (cells near the boundary, pocket triangles): the ring's pocket chords couple vertices
-//     far along a side, so those run the global iteration on the boundary band (depth <= 2K + 2,
-//     one launch per sweep, the chords in the ring kernel), valid to depth K + 3 after K sweeps.
+//     far along a side, so those run the global iteration on the boundary band (depth <= 2K + 3 - j
+//     at sweep j, one launch per sweep, the chords in the ring kernel), valid to depth K + 3 after K
+//     sweeps.
 // Per vertex the edge order and arithmetic are k_gd_grad's / k_gd_grad_ring's, so the result at
 // every target vertex is the global iteration's K-sweep value bit for bit
 // (tests/test_gpu_parity.py::test_gradient_cone_equals_global_sweeps).
@@ -1530,6 +1532,7 @@ struct ConePatch {
     ConeStep st[kConeMaxK + 1];  // st[j] for sweep j = 1 .. K
     double* gout;              // x_K (NV, n, 2): the cells' four corners are written
     unsigned long long* chg;   // largest change measure of one more sweep at the corners (or nullptr)
+    unsigned long long* clk;   // diagnostics (AKB_GD_PATCH_CLOCK): cycles per phase summed over cells, or nullptr
 };
 
 // one workgroup per interior target cell: the (2K + 4)^2 box around it in LDS, K sweeps on the
@@ -1637,10 +1640,11 @@ __global__ void __launch_bounds__(256) k_gd_cone_patch(Grid g, ConePatch<NV> a) 
 // its vertices in order of depth; x_j overwrites x_{j-2} in place (a vertex reads its own predecessor only),
 // so two iterate buffers suffice. The arithmetic is edge_vals / solve_vals' exactly: x_K at the
 // corners equals k_gd_cone_patch's, bit for bit.
+template <bool PF, bool CLK>
 __global__ void __launch_bounds__(1024) k_gd_cone_patch1(Grid g, ConePatch<1> a, int rowmajor) {
     constexpr int P = 33;  // LDS pitch: a column of the box steps 2 banks per row, not 0
     static_assert(kConeBox < P, "box pitch");
-    __shared__ double sx[P * 32], sy[P * 32], sf[P * 32];
+    __shared__ double sxyf[2][3][P * 32];  // x, y, f of the box; two sets (PF: the next cell's DMA)
     __shared__ double2 sg[2][P * 32];
     __shared__ uint8_t sd[P * 32];
     const int K = a.K, W = 2 * K + 4;
@@ -1672,23 +1676,78 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch1(Grid g, ConePatch<1> a,
     }
     const bool mine = dep >= 1;
     const int b = mine ? r * P + c : 0;
-    for (int pid = blockIdx.x; pid < *a.count; pid += gridDim.x) {
+    // the box load. PF: one persistent workgroup walks its cells; x, y, f of the next cell go
+    // global -> LDS by DMA (global_load_lds, no registers) into the other set while this cell's
+    // sweeps run - one wave instruction per box row and array, lane i moving dword i of the row.
+    // The diagonal bytes go through a register (one per thread, row-major). Else everything
+    // through registers, row-major (coalesced), at the top of the cell.
+    const int count = *a.count;
+    const double* const gx_ = g.x;
+    const double* const gy_ = g.y;
+    const double* const gf_ = a.f;
+    const uint8_t* const gd_ = g.diag;
+    const int nh = g.nh;
+    const int wv = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63;
+    const int lr = t / 32, lc = t - (t / 32) * 32;
+    // the next cell's box: the diagonal byte into a register, then x, y, f by DMA (issued after every
+    // load the wave waits on, so no wait before the next cell's top lands on them)
+    auto prefetch = [=](int pid, int st, uint8_t& d) {
+        if (pid >= count) return;
+        const int64_t cell = a.cells[pid];
+        const int iv0 = (int)(cell / (nh - 1)), ih0 = (int)(cell - (int64_t)iv0 * (nh - 1));
+        const int R0 = iv0 - (K + 1), C0 = ih0 - (K + 1);
+        if (lr < W - 1 && lc < W - 1) d = gd_[(int64_t)(R0 + lr) * (nh - 1) + (C0 + lc)];
+#pragma unroll
+        for (int arr = 0; arr < 3; ++arr) {
+            const double* base = arr == 0 ? gx_ : arr == 1 ? gy_ : gf_;
+            for (int row = wv; row < W; row += 16) {
+                const double* src = base + (int64_t)(R0 + row) * nh + C0;
+                if (lane < 2 * W)
+                    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) const char*)src + lane * 4,
+                                                     (__attribute__((address_space(3))) void*)&sxyf[st][arr][row * P],
+                                                     4, 0, 0);
+            }
+        }
+    };
+    uint8_t pd = 0;
+    if (PF) prefetch(blockIdx.x, 0, pd);
+    int set = 0;
+    for (int pid = blockIdx.x; pid < count; pid += gridDim.x, set ^= (PF ? 1 : 0)) {
         const int64_t cell = a.cells[pid];
         const int iv0 = (int)(cell / (g.nh - 1)), ih0 = (int)(cell - (int64_t)iv0 * (g.nh - 1));
         const int R0 = iv0 - (K + 1), C0 = ih0 - (K + 1);
-        __syncthreads();  // the previous cell's reads are done
+        const unsigned long long c0 = CLK ? clock64() : 0;
+        double* const sx = sxyf[set][0];
+        double* const sy = sxyf[set][1];
+        double* const sf = sxyf[set][2];
         {
-            const int lr = t / 32, lc = t - (t / 32) * 32;  // the box load, row-major (coalesced)
+            double nx_ = 0.0, ny_ = 0.0, nf_ = 0.0;
+            uint8_t nd_ = pd;
+            if (!PF && lr < W && lc < W) {
+                const int64_t i = (int64_t)(R0 + lr) * nh + (C0 + lc);
+                nx_ = gx_[i];
+                ny_ = gy_[i];
+                nf_ = gf_[i];
+                nd_ = (lr < W - 1 && lc < W - 1) ? gd_[(int64_t)(R0 + lr) * (nh - 1) + (C0 + lc)] : 0;
+            }
+            if (PF) __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA rows have landed (vmcnt)
+            __syncthreads();  // the previous cell's reads are done; PF: every wave's DMA has landed
             if (lr < W && lc < W) {
-                const int64_t i = (int64_t)(R0 + lr) * g.nh + (C0 + lc);
                 const int q = lr * P + lc;
-                sx[q] = g.x[i];
-                sy[q] = g.y[i];
-                sf[q] = a.f[i];
-                sd[q] = (lr < W - 1 && lc < W - 1) ? g.diag[(int64_t)(R0 + lr) * (g.nh - 1) + (C0 + lc)] : 0;
+                if (!PF) {
+                    sx[q] = nx_;
+                    sy[q] = ny_;
+                    sf[q] = nf_;
+                }
+                sd[q] = nd_;
             }
         }
         __syncthreads();
+        const unsigned long long c1 = CLK ? clock64() : 0;
+        if (PF) {
+            pd = 0;
+            prefetch(pid + gridDim.x, set ^ 1, pd);
+        }
         // this vertex's edges in k_gd_grad's order: left, right, down, up, then the diagonals
         int nb[8];
         unsigned em = 0;
@@ -1730,9 +1789,14 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch1(Grid g, ConePatch<1> a,
             q3 = 4 * q3;
             inv = 1.0 / (q0 * q3 - q1 * q1);
         }
+        if (CLK) __syncthreads();
+        const unsigned long long c2 = CLK ? clock64() : 0;
         // the sums of one sweep from iterate buffer `in` (in < 0: x_0 = 0), solve_vals' solve
         auto sweep_r = [&](int in, double& r0, double& r1) {
             double s0 = 0.0, s1 = 0.0;
+            // (one exposed LDS latency per edge; issuing all eight reads first and selecting the
+            // missing diagonals away measured slower: the work of the missing edges and the
+            // register pressure cost more than the latency)
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 if (!(em & (1u << k))) continue;
@@ -1771,8 +1835,9 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch1(Grid g, ConePatch<1> a,
                 }
                 sg[out][b] = make_double2(ox, oy);
             }
-            __syncthreads();
+            __syncthreads();  // (the first also waits for the next box's DMA: it had setup + sweep 1 to land)
         }
+        const unsigned long long c3 = CLK ? clock64() : 0;
         // the cell's corners (the innermost ring): x_K out, and the change one more (plain-measured)
         // sweep would make
         if (dep == K + 1) {
@@ -1787,6 +1852,13 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch1(Grid g, ConePatch<1> a,
                 const double cm = fmax(fabs(gk.x + r0), fabs(gk.y + r1)) / fmax(1.0, fmax(fabs(r0), fabs(r1)));
                 if (cm > 0) atomicMax(a.chg, (unsigned long long)__double_as_longlong(cm));
             }
+        }
+        if (CLK && t == 0) {
+            atomicAdd(a.clk, c1 - c0);
+            atomicAdd(a.clk + 1, c2 - c1);
+            atomicAdd(a.clk + 2, c3 - c2);
+            atomicAdd(a.clk + 3, clock64() - c3);
+            atomicAdd(a.clk + 4, 1ull);
         }
     }
 }
@@ -2370,6 +2442,28 @@ bool gd_patch_rowmajor() {  // A/B: the register patch kernel's lanes along rows
     static bool b = getenv("AKB_GD_PATCH_ROWMAJOR") != nullptr;
     return b;
 }
+bool gd_patch_prefetch() {  // the next cell's box fetched into registers during the sweeps (A/B: off)
+    static bool b = getenv("AKB_GD_PATCH_NOPREFETCH") == nullptr;
+    return b;
+}
+unsigned gd_cu_count() {  // the device's CUs (one resident 1024-thread patch workgroup each)
+    static unsigned n = [] {
+        int dev = 0, cus = 0;
+        return hipGetDevice(&dev) == hipSuccess &&
+                       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0
+                   ? (unsigned)cus
+                   : 256u;
+    }();
+    return n;
+}
+unsigned long long* gd_patch_clock() {  // diagnostics: per-phase cycle sums of the register patch kernel
+    static unsigned long long* p = [] {
+        unsigned long long* q = nullptr;
+        if (getenv("AKB_GD_PATCH_CLOCK") && hipMalloc(&q, 8 * sizeof(unsigned long long)) != hipSuccess) q = nullptr;
+        return q;
+    }();
+    return p;
+}
 bool gd_patch_v1() {  // A/B: the 256-thread patch kernel for one value set
     static bool b = getenv("AKB_GD_PATCH_V1") != nullptr;
     return b;
@@ -2663,8 +2757,9 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
                                                       assigned);
     int st = launch_status("k_gd_cone_assign");
     if (st) return st;
-    // the boundary band: depth <= 2K + 2 (x_K valid to depth K + 3 >= every band target's corners)
-    const BandMap bm = band_map(g.nv, g.nh, 2 * K + 2);
+    // the boundary band, shrinking like the patches' squares: sweep j forms depth <= 2K + 3 - j, whose
+    // neighbours (depth <= 2K + 4 - j) sweep j - 1 formed, so x_K is the global iteration's to depth
+    // K + 3 >= every band target's corners (the first sweep reads x_0 = 0 only)
     ConeStep steps[kConeMaxK + 1];
     steps[0] = ConeStep{0, 1.0};
     for (int j = 1; j <= K; ++j)
@@ -2677,6 +2772,7 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
             for (int j = 1; j <= K; ++j) {
                 const double* gin = j == 1 ? nullptr : gb[(j - 1) % 3];
                 const double* gprev = j >= 3 ? gb[(j + 1) % 3] : nullptr;
+                const BandMap bm = band_map(g.nv, g.nh, 2 * K + 3 - j);
                 const unsigned nbw = grid_for(bm.total, 1, kStreamGridCap), nrw = grid_for(L * 64);
                 if (nvv == 2) {
                     ConeBand<2> a{fv, gin, gprev, gb[j % 3], ring_acc, steps[j], band};
@@ -2708,7 +2804,32 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
             if (gd_patch_v1())
                 k_gd_cone_patch<1><<<pg, 256, 0, s>>>(g, a);
             else
-                k_gd_cone_patch1<<<pg, 1024, 0, s>>>(g, a, gd_patch_rowmajor() ? 1 : 0);
+            {
+                unsigned long long* clk = gd_patch_clock();
+                if (clk) {
+                    hipMemsetAsync(clk, 0, 8 * sizeof(unsigned long long), s);
+                    a.clk = clk;
+                }
+                const int rm = gd_patch_rowmajor() ? 1 : 0;
+                // prefetching: one persistent workgroup per CU walks its cells (the next one's box
+                // loads during the current one's sweeps); else workgroups per cell
+                const unsigned pp = std::min(pg, gd_cu_count());
+                if (clk) {
+                    if (gd_patch_prefetch()) k_gd_cone_patch1<true, true><<<pp, 1024, 0, s>>>(g, a, rm);
+                    else k_gd_cone_patch1<false, true><<<pg, 1024, 0, s>>>(g, a, rm);
+                } else {
+                    if (gd_patch_prefetch()) k_gd_cone_patch1<true, false><<<pp, 1024, 0, s>>>(g, a, rm);
+                    else k_gd_cone_patch1<false, false><<<pg, 1024, 0, s>>>(g, a, rm);
+                }
+                if (clk) {
+                    unsigned long long h[8];
+                    hipMemcpyAsync(h, clk, sizeof(h), hipMemcpyDeviceToHost, s);
+                    hipStreamSynchronize(s);
+                    const double nc = h[4] ? (double)h[4] : 1.0;
+                    fprintf(stderr, "AKB_GD_PATCH_CLOCK cells %llu cycles/cell: load %.0f setup %.0f sweeps %.0f out %.0f\n",
+                            h[4], h[0] / nc, h[1] / nc, h[2] / nc, h[3] / nc);
+                }
+            }
         }
         if ((st = launch_status("k_gd_cone_patch"))) return st;
         if (cnt)

@@ -39,6 +39,24 @@ from .pupilmap import pupil_post, pupil_post_check
 EUV = 13.5e-9  # option_energy 'EUV' (:1161-1162)
 
 
+def pack_pockets(buf, o, Lr):
+    """Pack a pocket block (akb_gd_pockets' arrays at their capacity offsets o) in place so that
+    what the device reads is one prefix: tri (3 npk) | nbr (3 npk) | edge (L) | xptr (L + 1) | xidx
+    (xptr[L]). Returns (npk, the packed offsets with their total length under "len"); the H2D copy
+    is then that prefix (~half the capacity block at C3) instead of the whole block."""
+    npk = int(buf[o["npk"]])
+    nx = int(buf[o["xptr"] + Lr])
+    nbr = buf[o["nbr"]:o["nbr"] + 3 * npk].copy()
+    rest = np.concatenate([buf[o["edge"]:o["edge"] + Lr], buf[o["xptr"]:o["xptr"] + Lr + 1],
+                           buf[o["xidx"]:o["xidx"] + nx]])
+    p = dict(tri=0, nbr=3 * npk, edge=6 * npk, xptr=6 * npk + Lr, xidx=6 * npk + 2 * Lr + 1)
+    assert o["tri"] == 0
+    buf[p["nbr"]:p["nbr"] + 3 * npk] = nbr
+    buf[p["edge"]:p["edge"] + rest.size] = rest
+    p["len"] = p["edge"] + rest.size
+    return npk, p
+
+
 class Ticket:
     """One run in the pipeline: its slot, the tensors it reads, the pocket job, then its results."""
 
@@ -159,7 +177,8 @@ class FaithfulPupil:
         _lib.check(L.akb_gd_pockets(rb[:Lr].ctypes.data_as(_lib.c_vp), rb[Lr:2 * Lr].ctypes.data_as(_lib.c_vp),
                                     self.nv, self.nh, Lr, hp("npk"), hp("tri"), hp("nbr"), hp("edge"), hp("xptr"),
                                     hp("xidx")))
-        return int(buf[o["npk"]])
+        npk, s["po"] = pack_pockets(buf, o, Lr)
+        return npk
 
     # ------------------------------------------------------------------ stage 2
     def finish(self, t, stream=None, events=None, psf_events=None):
@@ -172,19 +191,19 @@ class FaithfulPupil:
         s = t.slot
         st = torch.cuda.current_stream() if stream is None else stream
         sh = D.stream_handle(st)
-        o, Lr = self._o, self.L
+        o, Lr = s["po"], self.L
         with torch.cuda.stream(st):
             if self._done is not None:  # the shared buffers' last finish, on any stream
                 st.wait_event(self._done)
             if events is not None:
                 events[0].record(st)
-            s["pk"].copy_(s["pk_host"], non_blocking=True)
+            s["pk"][:o["len"]].copy_(s["pk_host"][:o["len"]], non_blocking=True)
             t.h2d = torch.cuda.Event()
             t.h2d.record(st)
             pk = s["pk"]
             k = max(t.npock, 1)
             ptri, pnbr = pk[o["tri"]:o["tri"] + 3 * k], pk[o["nbr"]:o["nbr"] + 3 * k]
-            edge, xptr, xidx = pk[o["edge"]:o["edge"] + Lr], pk[o["xptr"]:o["xptr"] + Lr + 1], pk[o["xidx"]:]
+            edge, xptr, xidx = pk[o["edge"]:o["edge"] + Lr], pk[o["xptr"]:o["xptr"] + Lr + 1], pk[o["xidx"]:o["len"] + 1]
             tri = (D.ptr(t.y), D.ptr(t.z), self.nv, self.nh, D.ptr(s["diag"]), t.npock, D.ptr(ptri), D.ptr(pnbr),
                    D.ptr(edge))
             s["status"].zero_()

@@ -33,6 +33,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
+from .faithful import pack_pockets
 from .griddata import CONE_SWEEPS, _F_NEG, _F_NONCONVEX, _F_NONFINITE, _F_NOT_DELAUNAY, _F_POCKET, _F_POS
 from .wavefront import Shard
 
@@ -399,11 +400,13 @@ class ShardedFaithfulPupil:
             _lib.check(L.akb_gd_pockets(rb[:Lr].ctypes.data_as(_lib.c_vp), rb[Lr:2 * Lr].ctypes.data_as(_lib.c_vp),
                                         self.n, self.n, Lr, hp("npk"), hp("tri"), hp("nbr"), hp("edge"), hp("xptr"),
                                         hp("xidx")))
-            return int(buf[o["npk"]]), None
+            npk, s["po"] = pack_pockets(buf, o, Lr)
+            return npk, None
         except Exception as e:  # noqa: BLE001 - raised again by check()
             buf[o["edge"]:o["edge"] + Lr] = -1  # no pocket neighbours and no chords: every index in range
             buf[o["xptr"]:o["xptr"] + Lr + 1] = 0
             buf[o["npk"]] = 0
+            _, s["po"] = pack_pockets(buf, o, Lr)
             return 0, e
 
     # ------------------------------------------------------------------ stage 2
@@ -434,9 +437,9 @@ class ShardedFaithfulPupil:
             if events is not None:
                 events[0].record(st)
             if p.is_root:
-                o, Lr = self._o, self.Lr
+                o, Lr = s["po"], self.Lr
                 pk = s["pk"]
-                pk.copy_(s["pk_host"], non_blocking=True)
+                pk[:o["len"]].copy_(s["pk_host"][:o["len"]], non_blocking=True)
                 t.h2d = torch.cuda.Event()
                 t.h2d.record(st)
                 pock = (t.npock, D.ptr(pk[o["tri"]:]), D.ptr(pk[o["nbr"]:]), D.ptr(pk[o["edge"]:]))

@@ -167,3 +167,24 @@ def test_halo_and_band_movement_gloo(tmp_path, n, world):
         got = np.load(os.path.join(tmp_path, f"r{r}.npy"))
         assert got.all(), (r, got)
         assert got.size == (3 if r == 0 else 1)
+
+
+def test_pack_pockets_prefix():
+    """faithful.pack_pockets: the device's pocket arrays packed into one prefix of the block
+    (tri | nbr | edge | xptr | xidx[:xptr[L]]), the H2D copy's extent; the empty block too."""
+    from akbraytracing_amd.faithful import pack_pockets
+    rng = np.random.default_rng(3)
+    for Lr, npk in ((10, 4), (37, 0), (64, 50)):
+        cap = Lr
+        o = dict(tri=0, nbr=3 * cap, edge=6 * cap, xptr=6 * cap + Lr, xidx=6 * cap + 2 * Lr + 1)
+        o["npk"] = o["xidx"] + 6 * cap
+        buf = rng.integers(-5, 1000, o["npk"] + 1).astype(np.int32)
+        buf[o["npk"]] = npk
+        xp = np.concatenate([[0], np.cumsum(rng.integers(0, 3, Lr))]) if npk else np.zeros(Lr + 1, np.int64)
+        buf[o["xptr"]:o["xptr"] + Lr + 1] = xp
+        want = {k: buf[o[k]:o[k] + c].copy() for k, c in
+                (("tri", 3 * npk), ("nbr", 3 * npk), ("edge", Lr), ("xptr", Lr + 1), ("xidx", int(xp[-1])))}
+        n, p = pack_pockets(buf, o, Lr)
+        assert n == npk and p["len"] == 6 * npk + 2 * Lr + 1 + int(xp[-1])
+        for k, w in want.items():
+            assert np.array_equal(buf[p[k]:p[k] + w.size], w), k
