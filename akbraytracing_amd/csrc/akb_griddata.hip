@@ -26,6 +26,7 @@
 #include <stdio.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "akb_common.h"
 
@@ -1350,65 +1351,90 @@ __global__ void __launch_bounds__(kBlock) k_gd_cone_band(Grid g, BandMap bm, Con
 
 // the ring vertices of a band sweep: pocket chords (a wave per ring vertex, k_gd_grad_ring's fixed
 // reduction order), then the grid-edge sums the band kernel left, then the solve
+// ring vertex r's lattice index (the ring in k_gd_grad_ring's order)
+__device__ __forceinline__ int64_t ring_vertex(const Grid& g, int64_t r) {
+    const int64_t ra = g.nh - 1, rb = g.nv - 1;
+    if (r < ra) return r;
+    if (r < ra + rb) return (r - ra) * g.nh + (g.nh - 1);
+    if (r < 2 * ra + rb) return (int64_t)(g.nv - 1) * g.nh + (g.nh - 1 - (r - ra - rb));
+    return (int64_t)(g.nv - 1 - (r - 2 * ra - rb)) * g.nh;
+}
+
+// ring vertex r's pocket chords (one per lane of a group of W lanes, W >= the chord count, or
+// strided over a whole wave), reduced over the group by the butterfly k_gd_grad_ring uses over a
+// wave, then (lead lane) the band kernel's grid-edge sums added and the solve. For a count <= W the
+// W-lane tree is the 64-lane tree with its zero partners left out: the same bits.
+template <int NV, int W>
+__device__ __forceinline__ void cone_ring_vertex(const Grid& g, const ConeBand<NV>& a, int64_t r, int sub) {
+    const int64_t n = (int64_t)g.nv * g.nh;
+    const int64_t i = ring_vertex(g, r);
+    const double xi = g.x[i], yi = g.y[i];
+    double fi[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) fi[v] = a.f[v * n + i];
+    GradAcc<NV> A;
+    for (int32_t k = g.xptr[r] + sub; k < g.xptr[r + 1]; k += W) {
+        const int64_t j = g.xidx[k];
+        double fj[NV], gxj[NV], gyj[NV];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            fj[v] = a.f[v * n + j];
+            gxj[v] = a.gin ? a.gin[2 * (v * n + j)] : 0.0;
+            gyj[v] = a.gin ? a.gin[2 * (v * n + j) + 1] : 0.0;
+        }
+        edge_vals<NV>(g.x[j], g.y[j], fj, gxj, gyj, xi, yi, fi, A);
+    }
+    for (int off = W / 2; off > 0; off >>= 1) {
+        A.q0 += __shfl_down(A.q0, off, W);
+        A.q1 += __shfl_down(A.q1, off, W);
+        A.q3 += __shfl_down(A.q3, off, W);
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            A.s0[v] += __shfl_down(A.s0[v], off, W);
+            A.s1[v] += __shfl_down(A.s1[v], off, W);
+        }
+    }
+    if (sub == 0) {
+        const double* d = a.ring_acc + r * (3 + 2 * NV);
+        A.q0 += d[0];
+        A.q1 += d[1];
+        A.q3 += d[2];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            A.s0[v] += d[3 + 2 * v];
+            A.s1[v] += d[4 + 2 * v];
+        }
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            const int64_t o = 2 * (v * n + i);
+            const double gix = a.gin ? a.gin[o] : 0.0, giy = a.gin ? a.gin[o + 1] : 0.0;
+            const double px = a.st.mode == 2 ? a.gprev[o] : 0.0, py = a.st.mode == 2 ? a.gprev[o + 1] : 0.0;
+            double ox, oy;
+            solve_vals<NV>(A, v, gix, giy, a.st, px, py, ox, oy);
+            a.gout[o] = ox;
+            a.gout[o + 1] = oy;
+        }
+    }
+}
+
+// the ring's solve for one sweep: eight ring vertices per wave, eight lanes each (a ring vertex
+// has a few pocket chords); a vertex with more than eight takes the whole wave afterwards
+// (k_gd_grad_ring's 64-lane loop and tree). Either way its bits are k_gd_grad_ring's.
 template <int NV>
 __global__ void __launch_bounds__(kBlock) k_gd_cone_ring(Grid g, ConeBand<NV> a) {
     if (!*a.needed) return;
-    const int64_t n = (int64_t)g.nv * g.nh;
-    const int64_t ra = g.nh - 1, rb = g.nv - 1, L = 2 * ra + 2 * rb;
-    const int lane = threadIdx.x & 63;
-    for (int64_t r = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; r < L;
-         r += ((int64_t)gridDim.x * blockDim.x) >> 6) {
-        int64_t i;
-        if (r < ra) i = r;
-        else if (r < ra + rb) i = (r - ra) * g.nh + (g.nh - 1);
-        else if (r < 2 * ra + rb) i = (int64_t)(g.nv - 1) * g.nh + (g.nh - 1 - (r - ra - rb));
-        else i = (int64_t)(g.nv - 1 - (r - 2 * ra - rb)) * g.nh;
-        const double xi = g.x[i], yi = g.y[i];
-        double fi[NV];
-#pragma unroll
-        for (int v = 0; v < NV; ++v) fi[v] = a.f[v * n + i];
-        GradAcc<NV> A;
-        for (int32_t k = g.xptr[r] + lane; k < g.xptr[r + 1]; k += 64) {
-            const int64_t j = g.xidx[k];
-            double fj[NV], gxj[NV], gyj[NV];
-#pragma unroll
-            for (int v = 0; v < NV; ++v) {
-                fj[v] = a.f[v * n + j];
-                gxj[v] = a.gin ? a.gin[2 * (v * n + j)] : 0.0;
-                gyj[v] = a.gin ? a.gin[2 * (v * n + j) + 1] : 0.0;
-            }
-            edge_vals<NV>(g.x[j], g.y[j], fj, gxj, gyj, xi, yi, fi, A);
-        }
-        for (int off = 32; off > 0; off >>= 1) {
-            A.q0 += __shfl_down(A.q0, off);
-            A.q1 += __shfl_down(A.q1, off);
-            A.q3 += __shfl_down(A.q3, off);
-#pragma unroll
-            for (int v = 0; v < NV; ++v) {
-                A.s0[v] += __shfl_down(A.s0[v], off);
-                A.s1[v] += __shfl_down(A.s1[v], off);
-            }
-        }
-        if (lane == 0) {
-            const double* d = a.ring_acc + r * (3 + 2 * NV);
-            A.q0 += d[0];
-            A.q1 += d[1];
-            A.q3 += d[2];
-#pragma unroll
-            for (int v = 0; v < NV; ++v) {
-                A.s0[v] += d[3 + 2 * v];
-                A.s1[v] += d[4 + 2 * v];
-            }
-#pragma unroll
-            for (int v = 0; v < NV; ++v) {
-                const int64_t o = 2 * (v * n + i);
-                const double gix = a.gin ? a.gin[o] : 0.0, giy = a.gin ? a.gin[o + 1] : 0.0;
-                const double px = a.st.mode == 2 ? a.gprev[o] : 0.0, py = a.st.mode == 2 ? a.gprev[o + 1] : 0.0;
-                double ox, oy;
-                solve_vals<NV>(A, v, gix, giy, a.st, px, py, ox, oy);
-                a.gout[o] = ox;
-                a.gout[o + 1] = oy;
-            }
+    const int64_t L = 2 * (int64_t)(g.nh - 1) + 2 * (int64_t)(g.nv - 1);
+    const int lane = threadIdx.x & 63, sub = lane & 7;
+    for (int64_t r0 = ((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6) * 8; r0 < L;
+         r0 += (((int64_t)gridDim.x * blockDim.x) >> 6) * 8) {
+        const int64_t r = r0 + (lane >> 3);
+        const bool big = r < L && g.xptr[r + 1] - g.xptr[r] > 8;
+        if (r < L && !big) cone_ring_vertex<NV, 8>(g, a, r, sub);
+        unsigned long long m = __ballot(big && sub == 0);
+        while (m) {  // wave-uniform
+            const int q = __builtin_ctzll(m);
+            m &= m - 1;
+            cone_ring_vertex<NV, 64>(g, a, r0 + (q >> 3), lane);
         }
     }
 }
@@ -1711,6 +1737,7 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch1(Grid g, ConePatch<1> a,
     };
     uint8_t pd = 0;
     if (PF) prefetch(blockIdx.x, 0, pd);
+    double cmax = 0.0;  // the corners' change measure over this workgroup's cells: one atomic at the end
     int set = 0;
     for (int pid = blockIdx.x; pid < count; pid += gridDim.x, set ^= (PF ? 1 : 0)) {
         const int64_t cell = a.cells[pid];
@@ -1850,7 +1877,7 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch1(Grid g, ConePatch<1> a,
                 double r0, r1;
                 sweep_r(fin, r0, r1);
                 const double cm = fmax(fabs(gk.x + r0), fabs(gk.y + r1)) / fmax(1.0, fmax(fabs(r0), fabs(r1)));
-                if (cm > 0) atomicMax(a.chg, (unsigned long long)__double_as_longlong(cm));
+                cmax = fmax(cmax, cm);
             }
         }
         if (CLK && t == 0) {
@@ -1861,6 +1888,250 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch1(Grid g, ConePatch<1> a,
             atomicAdd(a.clk + 4, 1ull);
         }
     }
+    if (a.chg && dep == K + 1 && cmax > 0) atomicMax(a.chg, (unsigned long long)__double_as_longlong(cmax));
+}
+
+// vertex `idx` of the box in order of depth from the centre outwards (k_gd_cone_patch1's order):
+// (r, c) and its depth d = min(r, c, W-1-r, W-1-c); indices [0, (W - 2j)^2) are the vertices of
+// depth >= j. dep = 0 past the last (depth-1) vertex.
+__device__ __forceinline__ void depth_order(int W, int idx, int& r, int& c, int& dep) {
+    r = -1;
+    c = -1;
+    dep = 0;
+    int rem = idx;
+    for (int d = W / 2 - 1; d >= 1; --d) {
+        const int s1 = W - 2 * d - 1, cnt = 4 * s1;
+        if (rem < cnt) {
+            if (rem < s1) { r = d; c = d + rem; }
+            else if (rem < 2 * s1) { r = d + (rem - s1); c = d + s1; }
+            else if (rem < 3 * s1) { r = d + s1; c = d + s1 - (rem - 2 * s1); }
+            else { r = d + s1 - (rem - 3 * s1); c = d; }
+            dep = d;
+            return;
+        }
+        rem -= cnt;
+    }
+}
+
+// k_gd_cone_patch1 as a two-stage pipeline over the workgroup's cells: threads [0, N1) hold the
+// (W-2)^2 vertices of depth >= 1 of cell p and run its sweeps 1 .. S, while threads [N1, N1 + N2)
+// hold the N2 = (W - 2S - 2)^2 vertices of depth >= S + 1 of cell p - 1 and run its sweeps
+// S + 1 .. K and its corners' output - the late sweeps, a few waves each, no longer run alone.
+// Each stage's threads compute their vertex's edge constants from that cell's box; box sets rotate
+// over three (stage 1, stage 2, the next cell's DMA) and iterate buffer pairs over two (stage 2
+// reads x_S, x_{S-1} where stage 1 left them). Per vertex the arithmetic is k_gd_cone_patch1's:
+// the same bits. The host picks S (the smallest >= K/2 with N1 + N2 <= 1024).
+template <bool CLK>
+__global__ void __launch_bounds__(1024) k_gd_cone_patch2(Grid g, ConePatch<1> a, int S) {
+    constexpr int P = 33;
+    __shared__ double sxyf[3][3][P * 32];
+    __shared__ double2 sg[2][2][P * 32];
+    __shared__ uint8_t sd[3][P * 32];
+    __shared__ int2 scell[1024];            // this workgroup's cells' box origins (R0, C0), read once
+    __shared__ double sout[4][4];           // stage 2's corner results, stored one step later
+    const int K = a.K, W = 2 * K + 4;
+    const int t = threadIdx.x;
+    const int N1 = (W - 2) * (W - 2), N2 = (W - 2 * S - 2) * (W - 2 * S - 2);
+    const int role = t < N1 ? 1 : (t < N1 + N2 ? 2 : 0);
+    int r, c, dep;
+    depth_order(W, role == 1 ? t : t - N1, r, c, dep);
+    if (role == 0) dep = 0;
+    const int b = dep >= 1 ? r * P + c : 0;
+    const int Q = max(S, K - S);
+    const int count = *a.count;
+    const int my = count > (int)blockIdx.x ? (count - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+    const double* const gx_ = g.x;
+    const double* const gy_ = g.y;
+    const double* const gf_ = a.f;
+    const uint8_t* const gd_ = g.diag;
+    const int nh = g.nh;
+    // the cell list into LDS first (the host keeps it <= 1024 cells per workgroup), so no wait on a
+    // global load sits between a step's barrier and its DMA / setup
+    for (int i = t; i < my; i += 1024) {
+        const int64_t cell = a.cells[blockIdx.x + (int64_t)i * gridDim.x];
+        const int iv0 = (int)(cell / (nh - 1)), ih0 = (int)(cell - (int64_t)iv0 * (nh - 1));
+        scell[i] = make_int2(iv0 - (K + 1), ih0 - (K + 1));
+    }
+    __syncthreads();
+    const int wv = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63;
+    const int lr = t / 32, lc = t - (t / 32) * 32;
+    // cell i's box: diagonal bytes into a register, x, y, f by DMA into box set st (k_gd_cone_patch1).
+    // (The DMA issued at a step's start lands ~10k cycles after that step's sweeps have ended - its
+    // LDS writes seem to queue behind the sweeps' traffic - yet it beats loading the next box
+    // through registers on spare waves during the sweeps: 1.05 ms vs 0.47 ms, each global load's
+    // latency then sits inside a sweep.)
+    auto prefetch = [&](int i, int st, uint8_t& d) {
+        const int2 o = scell[i];
+        const int R0 = o.x, C0 = o.y;
+        if (lr < W - 1 && lc < W - 1) d = gd_[(int64_t)(R0 + lr) * (nh - 1) + (C0 + lc)];
+#pragma unroll
+        for (int arr = 0; arr < 3; ++arr) {
+            const double* base = arr == 0 ? gx_ : arr == 1 ? gy_ : gf_;
+            for (int row = wv; row < W; row += 16) {
+                const double* src = base + (int64_t)(R0 + row) * nh + C0;
+                if (lane < 2 * W)
+                    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) const char*)src + lane * 4,
+                                                     (__attribute__((address_space(3))) void*)&sxyf[st][arr][row * P],
+                                                     4, 0, 0);
+            }
+        }
+    };
+    uint8_t pd = 0;
+    if (my > 0) prefetch(0, 0, pd);
+    // the change measure's running max over this workgroup's cells (threads 0..3), one atomic at the
+    // end: an atomicMax per cell on the one address queued at L2 behind every other workgroup's and
+    // held each step's top (its vmcnt wait) for ~10k cycles
+    double cmax = 0.0;
+    for (int p = 0; p <= my; ++p) {
+        const int s1 = p % 3, s2 = (p + 2) % 3;  // box sets of cell p (stage 1) and cell p - 1 (stage 2)
+        const unsigned long long c0 = CLK ? clock64() : 0;
+        if (p < my && lr < W && lc < W) sd[s1][lr * P + lc] = pd;
+        __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA rows of cell p have landed (vmcnt)
+        const unsigned long long c0b = CLK ? clock64() : 0;
+        __syncthreads();                // every wave's have; the previous step's reads are done
+        const unsigned long long c1 = CLK ? clock64() : 0;
+        if (p + 1 < my) {
+            pd = 0;
+            prefetch(p + 1, (p + 1) % 3, pd);
+        }
+        if (p >= 2 && t < 4) {  // cell p - 2's corners, left by the last step's stage 2
+            const int64_t i = (int64_t)sout[t][2];
+            a.gout[2 * i] = sout[t][0];
+            a.gout[2 * i + 1] = sout[t][1];
+            cmax = fmax(cmax, sout[t][3]);
+        }
+        const bool act = dep >= 1 && (role == 1 ? p < my : p >= 1);
+        const int bs = role == 1 ? s1 : s2;
+        double2(*const gg)[P * 32] = sg[role == 1 ? (p & 1) : ((p + 1) & 1)];
+        const double* const sx = sxyf[bs][0];
+        const double* const sy = sxyf[bs][1];
+        const double* const sf = sxyf[bs][2];
+        const uint8_t* const sdd = sd[bs];
+        int nb[8];
+        unsigned em = 0;
+        double ex[8], ey[8], r3[8], c6[8];
+        double q0 = 0.0, q1 = 0.0, q3 = 0.0, inv = 0.0;
+        if (act) {
+            nb[0] = b - 1;
+            nb[1] = b + 1;
+            nb[2] = b - P;
+            nb[3] = b + P;
+            nb[4] = b - P - 1;
+            nb[5] = b - P + 1;
+            nb[6] = b + P - 1;
+            nb[7] = b + P + 1;
+            em = 0x0fu | (sdd[b - P - 1] == 0 ? 0x10u : 0u) | (sdd[b - P] == 1 ? 0x20u : 0u) |
+                 (sdd[b - 1] == 1 ? 0x40u : 0u) | (sdd[b] == 0 ? 0x80u : 0u);
+            const double xi = sx[b], yi = sy[b], fi = sf[b];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                ex[k] = ey[k] = r3[k] = c6[k] = 0.0;
+                if (!(em & (1u << k))) continue;
+                const int j = nb[k];
+                const double exk = sx[j] - xi, eyk = sy[j] - yi;
+                const double l2 = exk * exk + eyk * eyk;
+                double rr = __builtin_amdgcn_rsq(l2);
+                rr = rr * __builtin_fma(-0.5 * l2 * rr, rr, 1.5);
+                const double r3k = rr * rr * rr;
+                const double wx = exk * r3k, wy = eyk * r3k;
+                q0 = __builtin_fma(exk, wx, q0);
+                q1 = __builtin_fma(exk, wy, q1);
+                q3 = __builtin_fma(eyk, wy, q3);
+                ex[k] = exk;
+                ey[k] = eyk;
+                r3[k] = r3k;
+                c6[k] = 6 * (fi - sf[j]);
+            }
+            q0 = 4 * q0;
+            q1 = 4 * q1;
+            q3 = 4 * q3;
+            inv = 1.0 / (q0 * q3 - q1 * q1);
+        }
+        if (CLK) __syncthreads();
+        const unsigned long long c2 = CLK ? clock64() : 0;
+        auto sweep_r = [&](int in, double& r0, double& r1) {
+            double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                if (!(em & (1u << k))) continue;
+                double gxj = 0.0, gyj = 0.0;
+                if (in >= 0) {
+                    const double2 gj = gg[in][nb[k]];
+                    gxj = gj.x;
+                    gyj = gj.y;
+                }
+                const double df2 = -ex[k] * gxj - ey[k] * gyj;
+                const double w = c6[k] - 2 * df2;
+                const double wx = ex[k] * r3[k], wy = ey[k] * r3[k];
+                s0 = __builtin_fma(w, wx, s0);
+                s1 = __builtin_fma(w, wy, s1);
+            }
+            r0 = (q3 * s0 - q1 * s1) * inv;
+            r1 = (-q1 * s0 + q0 * s1) * inv;
+        };
+        for (int q = 1; q <= Q; ++q) {
+            const int j = role == 1 ? q : S + q;
+            if (act && dep >= j && (role == 1 ? q <= S : j <= K)) {
+                const int in = j == 1 ? -1 : ((j - 1) & 1), out = j & 1;
+                const ConeStep st = a.st[j];
+                double r0, r1;
+                sweep_r(in, r0, r1);
+                double ox, oy;
+                if (st.mode == 2) {
+                    const double2 pv = gg[out][b];  // x_{j-2}, overwritten below
+                    ox = st.omega * (-r0 - pv.x) + pv.x;
+                    oy = st.omega * (-r1 - pv.y) + pv.y;
+                } else if (st.mode == 1) {
+                    ox = st.omega * (-r0 - 0.0) + 0.0;
+                    oy = st.omega * (-r1 - 0.0) + 0.0;
+                } else {
+                    ox = -r0;
+                    oy = -r1;
+                }
+                gg[out][b] = make_double2(ox, oy);
+            }
+            // LDS-only barrier: __syncthreads' fence would also wait (vmcnt) for the next box's DMA
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+        const unsigned long long c3 = CLK ? clock64() : 0;
+        // cell p - 1's corners (stage 2's innermost ring): x_K and the change of one more sweep, into
+        // LDS; threads 0..3 store them after the next step's barrier (or below, after the last step),
+        // so the stores' latency is not waited for at the next step's top
+        if (role == 2 && act && dep == K + 1) {
+            const int2 o = scell[p - 1];
+            const int fin = K & 1;
+            const double2 gk = gg[fin][b];
+            double cm = 0.0;
+            if (a.chg) {
+                double r0, r1;
+                sweep_r(fin, r0, r1);
+                cm = fmax(fabs(gk.x + r0), fabs(gk.y + r1)) / fmax(1.0, fmax(fabs(r0), fabs(r1)));
+            }
+            const int q = t - N1;  // the innermost ring: stage 2's first four threads
+            sout[q][0] = gk.x;
+            sout[q][1] = gk.y;
+            sout[q][2] = (double)((int64_t)(o.x + r) * nh + (o.y + c));
+            sout[q][3] = cm;
+        }
+        if (p == my && my >= 1) {  // the last cell's corners
+            __syncthreads();
+            if (t < 4) {
+                const int64_t i = (int64_t)sout[t][2];
+                a.gout[2 * i] = sout[t][0];
+                a.gout[2 * i + 1] = sout[t][1];
+                cmax = fmax(cmax, sout[t][3]);
+            }
+        }
+        if (CLK && t == 0) {
+            atomicAdd(a.clk, c1 - c0);
+            atomicAdd(a.clk + 1, c2 - c1);
+            atomicAdd(a.clk + 2, c3 - c2);
+            atomicAdd(a.clk + 3, clock64() - c3);
+            atomicAdd(a.clk + 4, 1ull);
+            atomicAdd(a.clk + 5, c0b - c0);
+        }
+    }
+    if (a.chg && t < 4 && cmax > 0) atomicMax(a.chg, (unsigned long long)__double_as_longlong(cmax));
 }
 
 // targets -> interior target cells (the patch list) and whether any target needs the band
@@ -2274,17 +2545,19 @@ __global__ void __launch_bounds__(kBlock) k_gd_claim_hit(Grid g, Targets t, cons
     }
 }
 
-// pocket triangles: long slivers along the boundary whose boxes can hold thousands of targets,
-// so one workgroup per triangle, its threads striding the box
+// pocket triangles: slivers along the boundary whose boxes hold from none to thousands of targets,
+// so one wave per triangle, its lanes striding the box (a workgroup per triangle left most of its
+// threads idle on the common few-target boxes)
 __global__ void __launch_bounds__(kBlock) k_gd_claim_pockets(Grid g, Targets t, int* owner) {
     const int64_t nc2 = 2 * ncells(g);
-    for (int64_t j = blockIdx.x; j < g.npock; j += gridDim.x) {
+    const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+    for (int64_t j = (int64_t)blockIdx.x * nw + (threadIdx.x >> 6); j < g.npock; j += (int64_t)gridDim.x * nw) {
         const Tri T = tri_verts(g, nc2 + j);
         int c0, c1, r0, r1;
         tri_box(g, t, T, c0, c1, r0, r1);
         const int w = c1 - c0;
         const int64_t m = (int64_t)w * (r1 - r0);
-        for (int64_t k = threadIdx.x; k < m; k += blockDim.x) {
+        for (int64_t k = lane; k < m; k += 64) {
             const int r = r0 + (int)(k / w), c = c0 + (int)(k - (int64_t)(k / w) * w);
             claim_one(g, t, T, (int)(nc2 + j), r, c, owner);
         }
@@ -2440,6 +2713,10 @@ bool gd_band_split() {  // the band sweep as two launches (band, then ring); AKB
 }
 bool gd_patch_rowmajor() {  // A/B: the register patch kernel's lanes along rows (not by depth)
     static bool b = getenv("AKB_GD_PATCH_ROWMAJOR") != nullptr;
+    return b;
+}
+bool gd_patch_pipe() {  // the two-stage patch pipeline (A/B: AKB_GD_PATCH_NOPIPE)
+    static bool b = getenv("AKB_GD_PATCH_NOPIPE") == nullptr;
     return b;
 }
 bool gd_patch_prefetch() {  // the next cell's box fetched into registers during the sweeps (A/B: off)
@@ -2673,7 +2950,8 @@ int akb_gd_eval_f64(const double* x, const double* y, int nv, int nh, const uint
     st = launch_status("k_gd_claim");
     if (st) return st;
     if (npock > 0) {
-        k_gd_claim_pockets<<<(unsigned)(npock < 16384 ? npock : 16384), kBlock, 0, s>>>(g, t, owner);
+        const int64_t pw = (npock + kBlock / 64 - 1) / (kBlock / 64);
+        k_gd_claim_pockets<<<(unsigned)(pw < 16384 ? pw : 16384), kBlock, 0, s>>>(g, t, owner);
         st = launch_status("k_gd_claim_pockets");
         if (st) return st;
     }
@@ -2731,7 +3009,8 @@ int cone_claims(const Grid& g, const Targets& t, int with_pockets, int* owner, h
         if ((st = launch_status("k_gd_claim"))) return st;
     }
     if (with_pockets && g.npock > 0) {
-        k_gd_claim_pockets<<<(unsigned)(g.npock < 16384 ? g.npock : 16384), kBlock, 0, s>>>(g, t, owner);
+        const int64_t pw = ((int64_t)g.npock + kBlock / 64 - 1) / (kBlock / 64);
+        k_gd_claim_pockets<<<(unsigned)(pw < 16384 ? pw : 16384), kBlock, 0, s>>>(g, t, owner);
         if ((st = launch_status("k_gd_claim_pockets"))) return st;
     }
     return 0;
@@ -2773,12 +3052,12 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
                 const double* gin = j == 1 ? nullptr : gb[(j - 1) % 3];
                 const double* gprev = j >= 3 ? gb[(j + 1) % 3] : nullptr;
                 const BandMap bm = band_map(g.nv, g.nh, 2 * K + 3 - j);
-                const unsigned nbw = grid_for(bm.total, 1, kStreamGridCap), nrw = grid_for(L * 64);
+                const unsigned nbw = grid_for(bm.total, 1, kStreamGridCap), nrw = grid_for(L * 64), nr8 = grid_for((L + 7) / 8 * 64);
                 if (nvv == 2) {
                     ConeBand<2> a{fv, gin, gprev, gb[j % 3], ring_acc, steps[j], band};
                     if (gd_band_split()) {
                         k_gd_cone_band<2><<<nbw, kBlock, 0, s>>>(g, bm, a);
-                        k_gd_cone_ring<2><<<nrw, kBlock, 0, s>>>(g, a);
+                        k_gd_cone_ring<2><<<nr8, kBlock, 0, s>>>(g, a);
                     } else {
                         k_gd_cone_sweep<2><<<nbw + nrw, kBlock, 0, s>>>(g, bm, a, (int)nbw);
                     }
@@ -2786,7 +3065,7 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
                     ConeBand<1> a{fv, gin, gprev, gb[j % 3], ring_acc, steps[j], band};
                     if (gd_band_split()) {
                         k_gd_cone_band<1><<<nbw, kBlock, 0, s>>>(g, bm, a);
-                        k_gd_cone_ring<1><<<nrw, kBlock, 0, s>>>(g, a);
+                        k_gd_cone_ring<1><<<nr8, kBlock, 0, s>>>(g, a);
                     } else {
                         k_gd_cone_sweep<1><<<nbw + nrw, kBlock, 0, s>>>(g, bm, a, (int)nbw);
                     }
@@ -2807,14 +3086,25 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
             {
                 unsigned long long* clk = gd_patch_clock();
                 if (clk) {
-                    hipMemsetAsync(clk, 0, 8 * sizeof(unsigned long long), s);
+                    (void)hipMemsetAsync(clk, 0, 8 * sizeof(unsigned long long), s);
                     a.clk = clk;
                 }
                 const int rm = gd_patch_rowmajor() ? 1 : 0;
+                // the two-stage pipeline when both stages' vertices fit 1024 threads (K <= 14: always)
+                int S = -1;
+                if (gd_patch_pipe() && !rm) {
+                    const int W = 2 * K + 4;
+                    for (int s2 = (K + 1) / 2; s2 <= K && S < 0; ++s2)
+                        if ((W - 2) * (W - 2) + (W - 2 * s2 - 2) * (W - 2 * s2 - 2) <= 1024) S = s2;
+                }
                 // prefetching: one persistent workgroup per CU walks its cells (the next one's box
                 // loads during the current one's sweeps); else workgroups per cell
                 const unsigned pp = std::min(pg, gd_cu_count());
-                if (clk) {
+                if (S >= 0 && (int64_t)m > 1024 * (int64_t)pp) S = -1;  // the cell list fits LDS
+                if (S >= 0) {
+                    if (clk) k_gd_cone_patch2<true><<<pp, 1024, 0, s>>>(g, a, S);
+                    else k_gd_cone_patch2<false><<<pp, 1024, 0, s>>>(g, a, S);
+                } else if (clk) {
                     if (gd_patch_prefetch()) k_gd_cone_patch1<true, true><<<pp, 1024, 0, s>>>(g, a, rm);
                     else k_gd_cone_patch1<false, true><<<pg, 1024, 0, s>>>(g, a, rm);
                 } else {
@@ -2823,11 +3113,13 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
                 }
                 if (clk) {
                     unsigned long long h[8];
-                    hipMemcpyAsync(h, clk, sizeof(h), hipMemcpyDeviceToHost, s);
-                    hipStreamSynchronize(s);
+                    (void)hipMemcpyAsync(h, clk, sizeof(h), hipMemcpyDeviceToHost, s);
+                    (void)hipStreamSynchronize(s);
                     const double nc = h[4] ? (double)h[4] : 1.0;
-                    fprintf(stderr, "AKB_GD_PATCH_CLOCK cells %llu cycles/cell: load %.0f setup %.0f sweeps %.0f out %.0f\n",
-                            h[4], h[0] / nc, h[1] / nc, h[2] / nc, h[3] / nc);
+                    fprintf(stderr,
+                            "AKB_GD_PATCH_CLOCK cells %llu cycles/cell: load %.0f (own vmem wait %.0f) setup %.0f sweeps "
+                            "%.0f out %.0f\n",
+                            h[4], h[0] / nc, h[5] / nc, h[1] / nc, h[2] / nc, h[3] / nc);
                 }
             }
         }
