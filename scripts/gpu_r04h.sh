@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 fatal() { [ "$1" -ge 124 ]; }
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_faithful_gpu.py tests/test_faithful_dist_gpu.py \
-  -m gpu -x -v -s --timeout 300 --timeout-method thread -k "${PYTEST_K:-cone or gradient or faithful or sharded}" \
+  -m gpu -x -v -s --timeout 300 --timeout-method thread -k "${PYTEST_K:-cone or gradient or faithful or sharded or griddata or claim}" \
   > gpurun_out/r04h_pytest.log 2>&1
 rc=$?; tail -3 gpurun_out/r04h_pytest.log; [ $rc -eq 0 ] || exit $rc
 AKB_GD_PATCH_CLOCK=1 timeout -k 10 300 python3 scripts/micro_faithful.py --reps 2 > gpurun_out/r04h_clk.log 2>&1
