@@ -1290,6 +1290,33 @@ struct ConeBand {
     const int* needed;    // device flag: some target needs the band (else the launch returns at once)
 };
 
+// vertex i's lattice-edge sums of one band sweep (k_gd_grad's edge order: left, right, down, up,
+// then the diagonals present)
+template <int NV>
+__device__ __forceinline__ void band_grid_sums(const Grid& g, const ConeBand<NV>& a, int64_t n, int64_t i, int iv,
+                                               int ih, double xi, double yi, const double (&fi)[NV],
+                                               GradAcc<NV>& A) {
+    auto edge = [&](int64_t j) {
+        double fj[NV], gxj[NV], gyj[NV];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            fj[v] = a.f[v * n + j];
+            gxj[v] = a.gin ? a.gin[2 * (v * n + j)] : 0.0;
+            gyj[v] = a.gin ? a.gin[2 * (v * n + j) + 1] : 0.0;
+        }
+        edge_vals<NV>(g.x[j], g.y[j], fj, gxj, gyj, xi, yi, fi, A);
+    };
+    if (ih > 0) edge(i - 1);
+    if (ih < g.nh - 1) edge(i + 1);
+    if (iv > 0) edge(i - g.nh);
+    if (iv < g.nv - 1) edge(i + g.nh);
+    const int64_t c0 = (int64_t)iv * (g.nh - 1) + ih;
+    if (iv > 0 && ih > 0 && g.diag[c0 - g.nh] == 0) edge(i - g.nh - 1);
+    if (iv > 0 && ih < g.nh - 1 && g.diag[c0 - (g.nh - 1)] == 1) edge(i - g.nh + 1);
+    if (iv < g.nv - 1 && ih > 0 && g.diag[c0 - 1] == 1) edge(i + g.nh - 1);
+    if (iv < g.nv - 1 && ih < g.nh - 1 && g.diag[c0] == 0) edge(i + g.nh + 1);
+}
+
 // one sweep of the band (k_gd_grad's per-vertex body; nothing reads outside the lattice)
 template <int NV>
 __global__ void __launch_bounds__(kBlock) k_gd_cone_band(Grid g, BandMap bm, ConeBand<NV> a) {
@@ -1304,25 +1331,7 @@ __global__ void __launch_bounds__(kBlock) k_gd_cone_band(Grid g, BandMap bm, Con
 #pragma unroll
         for (int v = 0; v < NV; ++v) fi[v] = a.f[v * n + i];
         GradAcc<NV> A;
-        auto edge = [&](int64_t j) {
-            double fj[NV], gxj[NV], gyj[NV];
-#pragma unroll
-            for (int v = 0; v < NV; ++v) {
-                fj[v] = a.f[v * n + j];
-                gxj[v] = a.gin ? a.gin[2 * (v * n + j)] : 0.0;
-                gyj[v] = a.gin ? a.gin[2 * (v * n + j) + 1] : 0.0;
-            }
-            edge_vals<NV>(g.x[j], g.y[j], fj, gxj, gyj, xi, yi, fi, A);
-        };
-        if (ih > 0) edge(i - 1);
-        if (ih < g.nh - 1) edge(i + 1);
-        if (iv > 0) edge(i - g.nh);
-        if (iv < g.nv - 1) edge(i + g.nh);
-        const int64_t c0 = (int64_t)iv * (g.nh - 1) + ih;
-        if (iv > 0 && ih > 0 && g.diag[c0 - g.nh] == 0) edge(i - g.nh - 1);
-        if (iv > 0 && ih < g.nh - 1 && g.diag[c0 - (g.nh - 1)] == 1) edge(i - g.nh + 1);
-        if (iv < g.nv - 1 && ih > 0 && g.diag[c0 - 1] == 1) edge(i + g.nh - 1);
-        if (iv < g.nv - 1 && ih < g.nh - 1 && g.diag[c0] == 0) edge(i + g.nh + 1);
+        band_grid_sums<NV>(g, a, n, i, iv, ih, xi, yi, fi, A);
         const int64_t r = ring_pos(g, iv, ih);
         if (r >= 0) {
             double* d = a.ring_acc + r * (3 + 2 * NV);
@@ -1364,7 +1373,7 @@ __device__ __forceinline__ int64_t ring_vertex(const Grid& g, int64_t r) {
 // strided over a whole wave), reduced over the group by the butterfly k_gd_grad_ring uses over a
 // wave, then (lead lane) the band kernel's grid-edge sums added and the solve. For a count <= W the
 // W-lane tree is the 64-lane tree with its zero partners left out: the same bits.
-template <int NV, int W>
+template <int NV, int W, bool GRID = false>
 __device__ __forceinline__ void cone_ring_vertex(const Grid& g, const ConeBand<NV>& a, int64_t r, int sub) {
     const int64_t n = (int64_t)g.nv * g.nh;
     const int64_t i = ring_vertex(g, r);
@@ -1372,6 +1381,11 @@ __device__ __forceinline__ void cone_ring_vertex(const Grid& g, const ConeBand<N
     double fi[NV];
 #pragma unroll
     for (int v = 0; v < NV; ++v) fi[v] = a.f[v * n + i];
+    GradAcc<NV> D;  // GRID: the lattice-edge sums, formed here by the lead lane (else the band kernel's)
+    if (GRID && sub == 0) {
+        const int iv = (int)(i / g.nh), ih = (int)(i - (int64_t)iv * g.nh);
+        band_grid_sums<NV>(g, a, n, i, iv, ih, xi, yi, fi, D);
+    }
     GradAcc<NV> A;
     for (int32_t k = g.xptr[r] + sub; k < g.xptr[r + 1]; k += W) {
         const int64_t j = g.xidx[k];
@@ -1395,14 +1409,25 @@ __device__ __forceinline__ void cone_ring_vertex(const Grid& g, const ConeBand<N
         }
     }
     if (sub == 0) {
-        const double* d = a.ring_acc + r * (3 + 2 * NV);
-        A.q0 += d[0];
-        A.q1 += d[1];
-        A.q3 += d[2];
+        if (GRID) {
+            A.q0 += D.q0;
+            A.q1 += D.q1;
+            A.q3 += D.q3;
 #pragma unroll
-        for (int v = 0; v < NV; ++v) {
-            A.s0[v] += d[3 + 2 * v];
-            A.s1[v] += d[4 + 2 * v];
+            for (int v = 0; v < NV; ++v) {
+                A.s0[v] += D.s0[v];
+                A.s1[v] += D.s1[v];
+            }
+        } else {
+            const double* d = a.ring_acc + r * (3 + 2 * NV);
+            A.q0 += d[0];
+            A.q1 += d[1];
+            A.q3 += d[2];
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                A.s0[v] += d[3 + 2 * v];
+                A.s1[v] += d[4 + 2 * v];
+            }
         }
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
@@ -1435,6 +1460,57 @@ __global__ void __launch_bounds__(kBlock) k_gd_cone_ring(Grid g, ConeBand<NV> a)
             const int q = __builtin_ctzll(m);
             m &= m - 1;
             cone_ring_vertex<NV, 64>(g, a, r0 + (q >> 3), lane);
+        }
+    }
+}
+
+// one sweep of the band in one launch, the ring in 8-lane groups: workgroups [0, nbw) take the band's
+// vertices off the ring (k_gd_cone_band's body), the rest eight ring vertices per wave - the lead
+// lane forms the vertex's lattice-edge sums itself (band_grid_sums, what k_gd_cone_band would have
+// left in ring_acc), the chords as k_gd_cone_ring. Both halves read x_{j-1} / x_{j-2} only: the
+// two-launch form's bits in one launch per sweep.
+template <int NV>
+__global__ void __launch_bounds__(kBlock) k_gd_cone_sweep8(Grid g, BandMap bm, ConeBand<NV> a, int nbw) {
+    if (!*a.needed) return;
+    const int64_t n = (int64_t)g.nv * g.nh;
+    if ((int)blockIdx.x < nbw) {
+        for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < bm.total;
+             k += (int64_t)nbw * blockDim.x) {
+            const int64_t i = band_vertex(bm, k);
+            const int iv = (int)(i / g.nh), ih = (int)(i - (int64_t)iv * g.nh);
+            if (ring_pos(g, iv, ih) >= 0) continue;
+            const double xi = g.x[i], yi = g.y[i];
+            double fi[NV];
+#pragma unroll
+            for (int v = 0; v < NV; ++v) fi[v] = a.f[v * n + i];
+            GradAcc<NV> A;
+            band_grid_sums<NV>(g, a, n, i, iv, ih, xi, yi, fi, A);
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                const int64_t o = 2 * (v * n + i);
+                const double gix = a.gin ? a.gin[o] : 0.0, giy = a.gin ? a.gin[o + 1] : 0.0;
+                const double px = a.st.mode == 2 ? a.gprev[o] : 0.0, py = a.st.mode == 2 ? a.gprev[o + 1] : 0.0;
+                double ox, oy;
+                solve_vals<NV>(A, v, gix, giy, a.st, px, py, ox, oy);
+                a.gout[o] = ox;
+                a.gout[o + 1] = oy;
+            }
+        }
+        return;
+    }
+    const int64_t L = 2 * (int64_t)(g.nh - 1) + 2 * (int64_t)(g.nv - 1);
+    const int lane = threadIdx.x & 63, sub = lane & 7;
+    const int64_t w0 = ((int64_t)(blockIdx.x - nbw) * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nw = ((int64_t)(gridDim.x - nbw) * blockDim.x) >> 6;
+    for (int64_t r0 = w0 * 8; r0 < L; r0 += nw * 8) {
+        const int64_t r = r0 + (lane >> 3);
+        const bool big = r < L && g.xptr[r + 1] - g.xptr[r] > 8;
+        if (r < L && !big) cone_ring_vertex<NV, 8, true>(g, a, r, sub);
+        unsigned long long m = __ballot(big && sub == 0);
+        while (m) {  // wave-uniform
+            const int q = __builtin_ctzll(m);
+            m &= m - 1;
+            cone_ring_vertex<NV, 64, true>(g, a, r0 + (q >> 3), lane);
         }
     }
 }
@@ -2706,9 +2782,13 @@ int launch_cells(const Grid& g, uint8_t* diag, double tol, unsigned* d_flags, in
     return launch_status("k_gd_cells");
 }
 bool gd_band_split() {  // the band sweep as two launches (band, then ring); AKB_GD_BAND_MERGED: one
-    // (measured slower: 37 us vs 16 + 13 per sweep beside the passes - the ring's grid edges then
-    // wait behind its chord reduction on one lane)
+    // with a wave per ring vertex (measured slower: 37 us vs 16 + 13 per sweep beside the passes -
+    // the ring's grid edges then wait behind its chord reduction on one lane)
     static bool b = getenv("AKB_GD_BAND_MERGED") == nullptr;
+    return b;
+}
+bool gd_band_sweep8() {  // one launch per band sweep, the ring in 8-lane groups (A/B: AKB_GD_BAND_SPLIT)
+    static bool b = getenv("AKB_GD_BAND_SPLIT") == nullptr && getenv("AKB_GD_BAND_MERGED") == nullptr;
     return b;
 }
 bool gd_patch_rowmajor() {  // A/B: the register patch kernel's lanes along rows (not by depth)
@@ -3055,7 +3135,9 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
                 const unsigned nbw = grid_for(bm.total, 1, kStreamGridCap), nrw = grid_for(L * 64), nr8 = grid_for((L + 7) / 8 * 64);
                 if (nvv == 2) {
                     ConeBand<2> a{fv, gin, gprev, gb[j % 3], ring_acc, steps[j], band};
-                    if (gd_band_split()) {
+                    if (gd_band_sweep8()) {
+                        k_gd_cone_sweep8<2><<<nbw + nr8, kBlock, 0, s>>>(g, bm, a, (int)nbw);
+                    } else if (gd_band_split()) {
                         k_gd_cone_band<2><<<nbw, kBlock, 0, s>>>(g, bm, a);
                         k_gd_cone_ring<2><<<nr8, kBlock, 0, s>>>(g, a);
                     } else {
@@ -3063,7 +3145,9 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
                     }
                 } else {
                     ConeBand<1> a{fv, gin, gprev, gb[j % 3], ring_acc, steps[j], band};
-                    if (gd_band_split()) {
+                    if (gd_band_sweep8()) {
+                        k_gd_cone_sweep8<1><<<nbw + nr8, kBlock, 0, s>>>(g, bm, a, (int)nbw);
+                    } else if (gd_band_split()) {
                         k_gd_cone_band<1><<<nbw, kBlock, 0, s>>>(g, bm, a);
                         k_gd_cone_ring<1><<<nr8, kBlock, 0, s>>>(g, a);
                     } else {
@@ -3094,7 +3178,8 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
                 int S = -1;
                 if (gd_patch_pipe() && !rm) {
                     const int W = 2 * K + 4;
-                    for (int s2 = (K + 1) / 2; s2 <= K && S < 0; ++s2)
+                    const char* es = getenv("AKB_GD_PATCH_S");  // A/B: the first sweep stage 2 does is S + 1
+                    for (int s2 = es ? std::max(1, std::min(K, atoi(es))) : (K + 1) / 2; s2 <= K && S < 0; ++s2)
                         if ((W - 2) * (W - 2) + (W - 2 * s2 - 2) * (W - 2 * s2 - 2) <= 1024) S = s2;
                 }
                 // prefetching: one persistent workgroup per CU walks its cells (the next one's box
