@@ -2573,17 +2573,27 @@ __global__ void __launch_bounds__(kBlock) k_gd_claim_scan(Grid g, Targets t, uin
         const int bv = (int)(blk / bh), bc = (int)(blk - (int64_t)bv * bh);
         const int iv0 = r_lo + bv * 8, ih0 = bc * 8;
         const int nr = min(8, r_hi - iv0), nc = min(8, g.nh - 1 - ih0);
+        // the block's extent from its boundary vertices only (32 of 81): on an unfolded lattice of
+        // convex cells an interior vertex lies inside the union of its cells, so no extreme is its
+        // alone - the same box as over all 81. (A folded lattice or a non-finite hit fails the run
+        // from the cell pass's flags; its claims are never used.)
         double xlo = INFINITY, xhi = -INFINITY, ylo = INFINITY, yhi = -INFINITY;
         bool nonfinite = false;
+        auto take = [&](int64_t q) {
+            const double x = g.x[q], y = g.y[q];
+            nonfinite = nonfinite || !isfinite(x) || !isfinite(y);
+            xlo = fmin(xlo, x);
+            xhi = fmax(xhi, x);
+            ylo = fmin(ylo, y);
+            yhi = fmax(yhi, y);
+        };
         for (int vr = 0; vr <= nr; ++vr) {
             const int64_t q0 = (int64_t)(iv0 + vr) * g.nh + ih0;
-            for (int vc = 0; vc <= nc; ++vc) {
-                const double x = g.x[q0 + vc], y = g.y[q0 + vc];
-                nonfinite = nonfinite || !isfinite(x) || !isfinite(y);
-                xlo = fmin(xlo, x);
-                xhi = fmax(xhi, x);
-                ylo = fmin(ylo, y);
-                yhi = fmax(yhi, y);
+            if (vr == 0 || vr == nr) {
+                for (int vc = 0; vc <= nc; ++vc) take(q0 + vc);
+            } else {
+                take(q0);
+                take(q0 + nc);
             }
         }
         bool h = nonfinite;
