@@ -1190,6 +1190,7 @@ __global__ void __launch_bounds__(kBlock) k_gd_ring_chords(Grid g, const double*
 // every target vertex is the global iteration's K-sweep value bit for bit
 // (tests/test_gpu_parity.py::test_gradient_cone_equals_global_sweeps).
 
+constexpr int kClaimAxisLds = 512;                // target axes up to this long go to LDS in k_gd_claim_hit
 constexpr int kConeMaxK = 14;                    // patch box side 2K + 4 <= 32
 constexpr int kConeBox = 2 * kConeMaxK + 4;
 
@@ -2612,10 +2613,20 @@ __global__ void __launch_bounds__(kBlock) k_gd_claim_scan(Grid g, Targets t, uin
     }
 }
 
-__global__ void __launch_bounds__(kBlock) k_gd_claim_hit(Grid g, Targets t, const uint8_t* __restrict__ hit,
+__global__ void __launch_bounds__(kBlock, 5) k_gd_claim_hit(Grid g, Targets t, const uint8_t* __restrict__ hit,
                                                          int* owner) {
     const bool uniform = axes_uniform(t);
     const double inv_dx = inv_step(t.gx, t.mx), inv_dy = inv_step(t.gy, t.my);
+    // the target axes in LDS: the claims' index scans walk them one dependent load at a time
+    __shared__ double sax[2 * kClaimAxisLds];
+    Targets tl = t;
+    if (t.mx <= kClaimAxisLds && t.my <= kClaimAxisLds) {
+        for (int i = threadIdx.x; i < t.mx; i += blockDim.x) sax[i] = t.gx[i];
+        for (int i = threadIdx.x; i < t.my; i += blockDim.x) sax[kClaimAxisLds + i] = t.gy[i];
+        __syncthreads();
+        tl.gx = sax;
+        tl.gy = sax + kClaimAxisLds;
+    }
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
     int64_t nblk;
     int bh, r_lo, r_hi;
@@ -2626,7 +2637,7 @@ __global__ void __launch_bounds__(kBlock) k_gd_claim_hit(Grid g, Targets t, cons
         const int iv0 = r_lo + bv * 8, ih0 = bc * 8;
         const int nr = min(8, r_hi - iv0), nc = min(8, g.nh - 1 - ih0);
         const int rr = lane >> 3, cc = lane & 7;
-        if (rr < nr && cc < nc) claim_cell(g, t, (int64_t)(iv0 + rr) * (g.nh - 1) + (ih0 + cc), uniform, inv_dx, inv_dy,
+        if (rr < nr && cc < nc) claim_cell(g, tl, (int64_t)(iv0 + rr) * (g.nh - 1) + (ih0 + cc), uniform, inv_dx, inv_dy,
                                            owner);
     }
 }
