@@ -2234,9 +2234,11 @@ __global__ void __launch_bounds__(kBlock) k_gd_cone_targets(Grid g, const int* _
 // the driver's target grid axes from the lattice's extent (its extremes lie on the boundary ring):
 // np.linspace(min, max, m) of the ring's x and y - i * step + start, the last point the stop
 // (numpy 2.x's linspace arithmetic) - one workgroup
-__global__ void __launch_bounds__(kBlock) k_gd_axes(const double* __restrict__ rx, const double* __restrict__ ry,
-                                                     int64_t L, int mx, int my, double* gx, double* gy, double* ext) {
-    __shared__ double red[4][kBlock / 64];
+constexpr int kAxesThreads = 1024;  // one workgroup over the ring (4 x kBlock: the loop was its latency)
+__global__ void __launch_bounds__(kAxesThreads) k_gd_axes(const double* __restrict__ rx, const double* __restrict__ ry,
+                                                          int64_t L, int mx, int my, double* gx, double* gy,
+                                                          double* ext) {
+    __shared__ double red[4][kAxesThreads / 64];
     double lo_x = INFINITY, hi_x = -INFINITY, lo_y = INFINITY, hi_y = -INFINITY;
     for (int64_t r = threadIdx.x; r < L; r += blockDim.x) {
         lo_x = fmin(lo_x, rx[r]);
@@ -2260,7 +2262,7 @@ __global__ void __launch_bounds__(kBlock) k_gd_axes(const double* __restrict__ r
     double e[4];
     for (int q = 0; q < 4; ++q) {
         e[q] = red[q][0];
-        for (int w = 1; w < kBlock / 64; ++w) e[q] = (q & 1) ? fmax(e[q], red[q][w]) : fmin(e[q], red[q][w]);
+        for (int w = 1; w < kAxesThreads / 64; ++w) e[q] = (q & 1) ? fmax(e[q], red[q][w]) : fmin(e[q], red[q][w]);
     }
     if (threadIdx.x == 0 && ext) {
         for (int q = 0; q < 4; ++q) ext[q] = e[q];
@@ -3064,7 +3066,7 @@ int akb_gd_axes_f64(const double* ring_x, const double* ring_y, int64_t L, int m
                     double* d_extent, void* stream) {
     clear_error();
     AKB_REQUIRE(ring_x && ring_y && gx && gy && L > 0 && mx > 0 && my > 0, "bad arguments");
-    k_gd_axes<<<1, kBlock, 0, (hipStream_t)stream>>>(ring_x, ring_y, L, mx, my, gx, gy, d_extent);
+    k_gd_axes<<<1, kAxesThreads, 0, (hipStream_t)stream>>>(ring_x, ring_y, L, mx, my, gx, gy, d_extent);
     return launch_status("k_gd_axes");
 }
 
