@@ -1297,6 +1297,39 @@ template <int NV>
 __device__ __forceinline__ void band_grid_sums(const Grid& g, const ConeBand<NV>& a, int64_t n, int64_t i, int iv,
                                                int ih, double xi, double yi, const double (&fi)[NV],
                                                GradAcc<NV>& A) {
+    if constexpr (NV == 1) {
+        // every candidate neighbour's data loaded first (positions off the lattice clamped to i,
+        // the diagonals' presence from their cells' bytes, loaded beside them), then the edges in
+        // the same order and arithmetic: one memory round trip per vertex instead of one per edge
+        const int64_t nh = g.nh;
+        const bool L = ih > 0, R = ih < g.nh - 1, D = iv > 0, U = iv < g.nv - 1;
+        const int64_t jn[8] = {i - 1, i + 1, i - nh, i + nh, i - nh - 1, i - nh + 1, i + nh - 1, i + nh + 1};
+        const bool inb[8] = {L, R, D, U, D && L, D && R, U && L, U && R};
+        const int64_t c0 = (int64_t)iv * (g.nh - 1) + ih;
+        const int64_t dc[4] = {c0 - g.nh, c0 - (g.nh - 1), c0 - 1, c0};
+        uint8_t dg[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) dg[k] = g.diag[inb[4 + k] ? dc[k] : 0];
+        double xs[8], ys[8], fs[8], gxs[8], gys[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int64_t j = inb[k] ? jn[k] : i;
+            xs[k] = g.x[j];
+            ys[k] = g.y[j];
+            fs[k] = a.f[j];
+            gxs[k] = a.gin ? a.gin[2 * j] : 0.0;
+            gys[k] = a.gin ? a.gin[2 * j + 1] : 0.0;
+        }
+        const bool on[8] = {L, R, D, U, inb[4] && dg[0] == 0, inb[5] && dg[1] == 1, inb[6] && dg[2] == 1,
+                            inb[7] && dg[3] == 0};
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (on[k]) {
+                const double fj[1] = {fs[k]}, gxj[1] = {gxs[k]}, gyj[1] = {gys[k]};
+                edge_vals<1>(xs[k], ys[k], fj, gxj, gyj, xi, yi, fi, A);
+            }
+        return;
+    }
     auto edge = [&](int64_t j) {
         double fj[NV], gxj[NV], gyj[NV];
 #pragma unroll
