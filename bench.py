@@ -107,6 +107,9 @@ def parse():
                         "(akbraytracing_amd/faithful.py); standin: RayWave.pupil's ray-index sampler (rounds 1-3)")
     p.add_argument("--cone-sweeps", type=int, default=None,
                    help="Chebyshev sweeps of the faithful pupil's cone solve (default griddata.CONE_SWEEPS)")
+    p.add_argument("--begin-stream", choices=("back", "fin", "copy"), default="back",
+                   help="stream of the faithful pupil's begin (cell pass + ring copy): the back stream, or "
+                        "RayWave's finish / copy stream (N = 1), waiting for the run's back half")
     p.add_argument("--faithful-lag", type=int, default=None,
                    help="faithful runs whose pocket jobs may be in flight before a step waits for the oldest "
                         "(default 3; 6 at N > 1, where the band owner builds configs[3]'s 40k-point ring)")
@@ -480,12 +483,18 @@ def main():
         with torch.cuda.stream(bs):
             out = rw.launch_back(f, stream=bs)
             d2 = out["detcenter2"]
+            cs = bs
+            if args.begin_stream != "back" and world == 1:
+                cs = rw._fin if args.begin_stream == "fin" else rw._copy
+                ready = torch.cuda.Event()
+                ready.record(bs)
+                cs.wait_event(ready)
             if timed:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(bs)
-            tickets.append(fp.begin(d2[1], d2[2], out["wave2"], stream=bs))
+                e0.record(cs)
+            tickets.append(fp.begin(d2[1], d2[2], out["wave2"], stream=cs))
             if timed:
-                e1.record(bs)
+                e1.record(cs)
                 fp_events.append(("begin", e0, e1))
             # N > 1: every rank finishes the same runs (collectives), so by count alone
             while tickets and ((world == 1 and tickets[0].ready()) or len(tickets) > args.faithful_lag):
