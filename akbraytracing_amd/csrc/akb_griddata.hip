@@ -2104,6 +2104,7 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch2(Grid g, ConePatch<1> a,
             pd = 0;
             prefetch(p + 1, (p + 1) % 3, pd);
         }
+        if (p < my && lr < W && lc < W) sg[p & 1][0][lr * P + lc] = make_double2(0.0, 0.0);  // x_0
         if (p >= 2 && t < 4) {  // cell p - 2's corners, left by the last step's stage 2
             const int64_t i = (int64_t)sout[t][2];
             a.gout[2 * i] = sout[t][0];
@@ -2157,20 +2158,21 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch2(Grid g, ConePatch<1> a,
             q3 = 4 * q3;
             inv = 1.0 / (q0 * q3 - q1 * q1);
         }
-        if (CLK) __syncthreads();
+        // x_0 in place for sweep 1 (LDS only: the next box's DMA stays in flight)
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         const unsigned long long c2 = CLK ? clock64() : 0;
+        // the sums of one sweep from iterate buffer `in` (sweep 1 reads x_0 = 0 from buffer 0, zeroed
+        // at the step's top), solve_vals' solve; the buffer's row base is formed once per sweep, so
+        // each edge's read is one LDS instruction with a constant offset
         auto sweep_r = [&](int in, double& r0, double& r1) {
+            constexpr int off[8] = {-1, 1, -P, P, -P - 1, -P + 1, P - 1, P + 1};
             double s0 = 0.0, s1 = 0.0;
+            const double2* const gi = gg[in] + b;
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 if (!(em & (1u << k))) continue;
-                double gxj = 0.0, gyj = 0.0;
-                if (in >= 0) {
-                    const double2 gj = gg[in][nb[k]];
-                    gxj = gj.x;
-                    gyj = gj.y;
-                }
-                const double df2 = -ex[k] * gxj - ey[k] * gyj;
+                const double2 gj = gi[off[k]];
+                const double df2 = -ex[k] * gj.x - ey[k] * gj.y;
                 const double w = c6[k] - 2 * df2;
                 const double wx = ex[k] * r3[k], wy = ey[k] * r3[k];
                 s0 = __builtin_fma(w, wx, s0);
@@ -2182,7 +2184,7 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch2(Grid g, ConePatch<1> a,
         for (int q = 1; q <= Q; ++q) {
             const int j = role == 1 ? q : S + q;
             if (act && dep >= j && (role == 1 ? q <= S : j <= K)) {
-                const int in = j == 1 ? -1 : ((j - 1) & 1), out = j & 1;
+                const int in = (j - 1) & 1, out = j & 1;
                 const ConeStep st = a.st[j];
                 double r0, r1;
                 sweep_r(in, r0, r1);
