@@ -2031,7 +2031,7 @@ __device__ __forceinline__ void depth_order(int W, int idx, int& r, int& c, int&
 // over three (stage 1, stage 2, the next cell's DMA) and iterate buffer pairs over two (stage 2
 // reads x_S, x_{S-1} where stage 1 left them). Per vertex the arithmetic is k_gd_cone_patch1's:
 // the same bits. The host picks S (the smallest >= K/2 with N1 + N2 <= 1024).
-template <bool CLK>
+template <bool CLK, bool RPF>
 __global__ void __launch_bounds__(1024) k_gd_cone_patch2(Grid g, ConePatch<1> a, int S) {
     constexpr int P = 33;
     __shared__ double sxyf[3][3][P * 32];
@@ -2096,20 +2096,39 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch2(Grid g, ConePatch<1> a,
         const int s1 = p % 3, s2 = (p + 2) % 3;  // box sets of cell p (stage 1) and cell p - 1 (stage 2)
         const unsigned long long c0 = CLK ? clock64() : 0;
         if (p < my && lr < W && lc < W) sd[s1][lr * P + lc] = pd;
-        __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA rows of cell p have landed (vmcnt)
+        if (!RPF || p == 0) __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA rows of cell p have landed
         const unsigned long long c0b = CLK ? clock64() : 0;
-        __syncthreads();                // every wave's have; the previous step's reads are done
+        if (RPF) {
+            // cell p's box came through registers to LDS last step: an LDS-only barrier, so no wave
+            // waits here for the acks of its earlier global stores (__syncthreads' fence would)
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        } else {
+            __syncthreads();  // every wave's DMA has landed; the previous step's reads are done
+        }
         const unsigned long long c1 = CLK ? clock64() : 0;
+        double rx_ = 0.0, ry_ = 0.0, rf_ = 0.0;  // RPF: cell p + 1's box point through registers
         if (p + 1 < my) {
             pd = 0;
-            prefetch(p + 1, (p + 1) % 3, pd);
+            if (RPF) {
+                const int2 o = scell[p + 1];
+                if (lr < W && lc < W) {
+                    const int64_t q = (int64_t)(o.x + lr) * nh + (o.y + lc);
+                    rx_ = gx_[q];
+                    ry_ = gy_[q];
+                    rf_ = gf_[q];
+                    if (lr < W - 1 && lc < W - 1) pd = gd_[(int64_t)(o.x + lr) * (nh - 1) + (o.y + lc)];
+                }
+            } else {
+                prefetch(p + 1, (p + 1) % 3, pd);
+            }
         }
         if (p < my && lr < W && lc < W) sg[p & 1][0][lr * P + lc] = make_double2(0.0, 0.0);  // x_0
-        if (p >= 2 && t < 4) {  // cell p - 2's corners, left by the last step's stage 2
-            const int64_t i = (int64_t)sout[t][2];
-            a.gout[2 * i] = sout[t][0];
-            a.gout[2 * i + 1] = sout[t][1];
-            cmax = fmax(cmax, sout[t][3]);
+        if (p >= 2 && t >= 1020) {  // cell p - 2's corners, left by the last step's stage 2 (stored by
+            const int q = t - 1020;    // the last wave: no box loads of its own for K <= 13)
+            const int64_t i = (int64_t)sout[q][2];
+            a.gout[2 * i] = sout[q][0];
+            a.gout[2 * i + 1] = sout[q][1];
+            cmax = fmax(cmax, sout[q][3]);
         }
         const bool act = dep >= 1 && (role == 1 ? p < my : p >= 1);
         const int bs = role == 1 ? s1 : s2;
@@ -2157,6 +2176,12 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch2(Grid g, ConePatch<1> a,
             q1 = 4 * q1;
             q3 = 4 * q3;
             inv = 1.0 / (q0 * q3 - q1 * q1);
+        }
+        if (RPF && p + 1 < my && lr < W && lc < W) {  // after setup: its latency was the setup's time
+            const int q = lr * P + lc, st = (p + 1) % 3;
+            sxyf[st][0][q] = rx_;
+            sxyf[st][1][q] = ry_;
+            sxyf[st][2][q] = rf_;
         }
         // x_0 in place for sweep 1 (LDS only: the next box's DMA stays in flight)
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -2227,11 +2252,12 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch2(Grid g, ConePatch<1> a,
         }
         if (p == my && my >= 1) {  // the last cell's corners
             __syncthreads();
-            if (t < 4) {
-                const int64_t i = (int64_t)sout[t][2];
-                a.gout[2 * i] = sout[t][0];
-                a.gout[2 * i + 1] = sout[t][1];
-                cmax = fmax(cmax, sout[t][3]);
+            if (t >= 1020) {
+                const int q = t - 1020;
+                const int64_t i = (int64_t)sout[q][2];
+                a.gout[2 * i] = sout[q][0];
+                a.gout[2 * i + 1] = sout[q][1];
+                cmax = fmax(cmax, sout[q][3]);
             }
         }
         if (CLK && t == 0) {
@@ -2243,7 +2269,7 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch2(Grid g, ConePatch<1> a,
             atomicAdd(a.clk + 5, c0b - c0);
         }
     }
-    if (a.chg && t < 4 && cmax > 0) atomicMax(a.chg, (unsigned long long)__double_as_longlong(cmax));
+    if (a.chg && t >= 1020 && cmax > 0) atomicMax(a.chg, (unsigned long long)__double_as_longlong(cmax));
 }
 
 // targets -> interior target cells (the patch list) and whether any target needs the band
@@ -2853,6 +2879,11 @@ bool gd_patch_rowmajor() {  // A/B: the register patch kernel's lanes along rows
     static bool b = getenv("AKB_GD_PATCH_ROWMAJOR") != nullptr;
     return b;
 }
+bool gd_patch_rpf() {  // the pipeline's next box through registers over the setup (A/B: AKB_GD_PATCH_DMA,
+    // the LDS DMA issued at the step's top: 433-444 vs 423-426 us, same bits)
+    static bool b = getenv("AKB_GD_PATCH_DMA") == nullptr;
+    return b;
+}
 bool gd_patch_pipe() {  // the two-stage patch pipeline (A/B: AKB_GD_PATCH_NOPIPE)
     static bool b = getenv("AKB_GD_PATCH_NOPIPE") == nullptr;
     return b;
@@ -3245,8 +3276,13 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
                 const unsigned pp = std::min(pg, gd_cu_count());
                 if (S >= 0 && (int64_t)m > 1024 * (int64_t)pp) S = -1;  // the cell list fits LDS
                 if (S >= 0) {
-                    if (clk) k_gd_cone_patch2<true><<<pp, 1024, 0, s>>>(g, a, S);
-                    else k_gd_cone_patch2<false><<<pp, 1024, 0, s>>>(g, a, S);
+                    if (clk) {
+                        if (gd_patch_rpf()) k_gd_cone_patch2<true, true><<<pp, 1024, 0, s>>>(g, a, S);
+                        else k_gd_cone_patch2<true, false><<<pp, 1024, 0, s>>>(g, a, S);
+                    } else {
+                        if (gd_patch_rpf()) k_gd_cone_patch2<false, true><<<pp, 1024, 0, s>>>(g, a, S);
+                        else k_gd_cone_patch2<false, false><<<pp, 1024, 0, s>>>(g, a, S);
+                    }
                 } else if (clk) {
                     if (gd_patch_prefetch()) k_gd_cone_patch1<true, true><<<pp, 1024, 0, s>>>(g, a, rm);
                     else k_gd_cone_patch1<false, true><<<pg, 1024, 0, s>>>(g, a, rm);

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-4 GPU pass 8: pipelined patches with constant-offset neighbour reads (A/B: the one-stage kernel), parity tests,
+# Round-4 GPU pass 8: the pipeline's next box through registers (A/B: by LDS DMA), parity tests,
 # per-phase cycles, kernel times, outputs against the 256-thread patch kernel, then the bench.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -11,13 +11,13 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_faithf
 rc=$?; tail -3 gpurun_out/r04h_pytest.log; [ $rc -eq 0 ] || exit $rc
 AKB_GD_PATCH_CLOCK=1 timeout -k 10 300 python3 scripts/micro_faithful.py --reps 2 > gpurun_out/r04h_clk.log 2>&1
 rc=$?; grep AKB_GD_PATCH_CLOCK gpurun_out/r04h_clk.log | tail -1; fatal $rc && exit $rc; [ $rc -eq 0 ] || exit $rc
-AKB_GD_PATCH_CLOCK=1 AKB_GD_PATCH_NOPIPE=1 timeout -k 10 300 python3 scripts/micro_faithful.py --reps 2 > gpurun_out/r04h_clkpf.log 2>&1
+AKB_GD_PATCH_CLOCK=1 AKB_GD_PATCH_DMA=1 timeout -k 10 300 python3 scripts/micro_faithful.py --reps 2 > gpurun_out/r04h_clkpf.log 2>&1
 rc=$?; grep AKB_GD_PATCH_CLOCK gpurun_out/r04h_clkpf.log | tail -1; fatal $rc && exit $rc; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof10 -o run -- \
     python3 scripts/micro_faithful.py --reps 10 --out /tmp/mf_a.npz > gpurun_out/r04h_micro.log 2>&1
 rc=$?; tail -1 gpurun_out/r04h_micro.log; fatal $rc && exit $rc; [ $rc -eq 0 ] || exit $rc
 python3 scripts/kstats.py gpurun_out/prof10/run_kernel_stats.csv > gpurun_out/r04h_k.txt; head -8 gpurun_out/r04h_k.txt; rm -f gpurun_out/prof10/run_kernel_trace.csv
-AKB_GD_PATCH_NOPIPE=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof11 -o run -- \
+AKB_GD_PATCH_DMA=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof11 -o run -- \
     python3 scripts/micro_faithful.py --reps 10 --out /tmp/mf_b.npz > gpurun_out/r04h_micro_pf.log 2>&1
 rc=$?; tail -1 gpurun_out/r04h_micro_pf.log; fatal $rc && exit $rc; [ $rc -eq 0 ] || exit $rc
 python3 scripts/kstats.py gpurun_out/prof11/run_kernel_stats.csv > gpurun_out/r04h_kpf.txt; head -3 gpurun_out/r04h_kpf.txt; rm -f gpurun_out/prof11/run_kernel_trace.csv
