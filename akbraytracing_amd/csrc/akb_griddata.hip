@@ -3273,7 +3273,9 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
                 }
                 // prefetching: one persistent workgroup per CU walks its cells (the next one's box
                 // loads during the current one's sweeps); else workgroups per cell
-                const unsigned pp = std::min(pg, gd_cu_count());
+                // A/B: AKB_GD_PATCH_GRID leaves CUs to the other streams' kernels while the patches run
+                const char* eg = getenv("AKB_GD_PATCH_GRID");
+                const unsigned pp = std::min(pg, eg ? std::max(1u, (unsigned)atoi(eg)) : gd_cu_count());
                 if (S >= 0 && (int64_t)m > 1024 * (int64_t)pp) S = -1;  // the cell list fits LDS
                 if (S >= 0) {
                     if (clk) {
