@@ -29,6 +29,7 @@
 #include <type_traits>
 
 #include "akb_common.h"
+#include "akb_pairwise.h"
 
 namespace akb {
 namespace {
@@ -2325,13 +2326,8 @@ __global__ void __launch_bounds__(kAxesThreads) k_gd_axes(const double* __restri
         e[q] = red[q][0];
         for (int w = 1; w < kAxesThreads / 64; ++w) e[q] = (q & 1) ? fmax(e[q], red[q][w]) : fmin(e[q], red[q][w]);
     }
-    if (threadIdx.x == 0 && ext) {
+    if (threadIdx.x == 0 && ext)
         for (int q = 0; q < 4; ++q) ext[q] = e[q];
-        // the pupil pitch psf_calc takes (:1176-1177): one step of each axis (before the driver's
-        // mean subtraction, which can move it by an ulp; the normalised PSF does not depend on it)
-        ext[4] = mx > 1 ? fabs((e[1] - e[0]) / (double)(mx - 1)) : 0.0;
-        ext[5] = my > 1 ? fabs((e[3] - e[2]) / (double)(my - 1)) : 0.0;
-    }
     auto lin = [&](double a0, double a1, int m, double* out) {
         if (m == 1) {
             if (threadIdx.x == 0) out[0] = a0;
@@ -2347,6 +2343,24 @@ __global__ void __launch_bounds__(kAxesThreads) k_gd_axes(const double* __restri
     };
     lin(e[0], e[1], mx, gx);
     lin(e[2], e[3], my, gy);
+    if (!ext) return;
+    // the pupil pitch psf_calc takes after the driver's grid_H -= np.mean(grid_H) (:3698, :1176-1177):
+    // dx = |gh[0,1] - gh[0,0]|, dy = |gv[1,0] - gv[0,0]| of the mean-subtracted meshgrids, each mean
+    // numpy's (pairwise over the flattened my x mx meshgrid), waves 0 and 1
+    __shared__ PwTree tree[2];
+    __threadfence_block();
+    __syncthreads();  // the axes are written
+    const int w = threadIdx.x >> 6;
+    if (w < 2) {
+        const long long cnt = (long long)mx * my;
+        const double* a = w == 0 ? gx : gy;
+        const int m = w == 0 ? mx : my;
+        double sum;
+        if (w == 0) sum = pw_sum_wave_get(tree[0], [=](int i) { return gx[i % mx]; }, cnt);
+        else sum = pw_sum_wave_get(tree[1], [=](int i) { return gy[i / mx]; }, cnt);
+        const double mean = sum / (double)cnt;
+        if ((threadIdx.x & 63) == 0) ext[4 + w] = m > 1 ? fabs((a[1] - mean) - (a[0] - mean)) : 0.0;
+    }
 }
 
 // a sharded lattice's targets: this rank forms the interior targets whose cell's p00 lies in its

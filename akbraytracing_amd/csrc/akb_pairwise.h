@@ -131,4 +131,96 @@ static __device__ double pw_tree_wave(PwTree& T, const double* a, int len) {
     return T.val[0][0];
 }
 
+// pw_leaf_lds / pw_tree_wave over a virtual array: element i is get(i) (e.g. a meshgrid's flattened
+// entries formed from its axis), the same split tree and additions, so the same bits as the
+// stored array's sum
+template <class Get>
+__device__ double pw_leaf_get(const Get& get, int o, int n) {
+    if (n < 8) {
+        double res = 0.0;
+        for (int i = 0; i < n; ++i) res = res + get(o + i);
+        return res;
+    }
+    double r[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = get(o + j);
+    int i = 8;
+    for (; i < n - (n % 8); i += 8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[j] = r[j] + get(o + i + j);
+    }
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; ++i) res = res + get(o + i);
+    return res;
+}
+
+template <class Get>
+__device__ double pw_tree_wave_get(PwTree& T, const Get& get, int base, int len) {
+    const int lane = threadIdx.x & 63;
+    if (lane == 0) {
+        T.off[0][0] = 0;
+        T.len[0][0] = len;
+    }
+    int nd[kTreeLevels];
+    nd[0] = 1;
+    int depth = 1;
+    wave_sync();
+#pragma unroll
+    for (int d = 0; d < kTreeLevels; ++d) {
+        if (d < depth) {
+            const bool act = lane < nd[d];
+            int o = 0, l = 0;
+            if (act) {
+                o = T.off[d][lane];
+                l = T.len[d][lane];
+            }
+            const bool split = act && l > kPwLeaf && d + 1 < kTreeLevels;
+            const unsigned long long m = __ballot(split);
+            if (split) {
+                const int pos = 2 * __popcll(m & ((1ull << lane) - 1ull));
+                const int l2 = pw_split(l);
+                T.off[d + 1][pos] = o;
+                T.len[d + 1][pos] = l2;
+                T.off[d + 1][pos + 1] = o + l2;
+                T.len[d + 1][pos + 1] = l - l2;
+                T.child[d][lane] = pos;
+            } else if (act) {
+                T.val[d][lane] = pw_leaf_get(get, base + o, l);
+            }
+            if (m && d + 1 < kTreeLevels) {
+                nd[d + 1] = 2 * __popcll(m);
+                depth = d + 2;
+            }
+            wave_sync();
+        }
+    }
+#pragma unroll
+    for (int d = kTreeLevels - 2; d >= 0; --d) {
+        if (d + 1 < depth) {
+            if (lane < nd[d] && T.len[d][lane] > kPwLeaf) {
+                const int c = T.child[d][lane];
+                T.val[d][lane] = T.val[d + 1][c] + T.val[d + 1][c + 1];
+            }
+            wave_sync();
+        }
+    }
+    return T.val[0][0];
+}
+
+// np.sum of a virtual contiguous float64 array of n elements by one wave: numpy's 8192-element
+// buffers, each summed pairwise, added left to right
+template <class Get>
+__device__ double pw_sum_wave_get(PwTree& T, const Get& get, long long n) {
+    double s = 0.0;
+    bool first = true;
+    for (long long b = 0; b < n; b += 8192) {
+        const int len = (int)((n - b) < 8192 ? (n - b) : 8192);
+        const double v = pw_tree_wave_get(T, get, (int)b, len);
+        s = first ? v : s + v;
+        first = false;
+        wave_sync();
+    }
+    return s;
+}
+
 }  // namespace akb

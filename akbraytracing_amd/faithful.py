@@ -57,10 +57,45 @@ def pack_pockets(buf, o, Lr):
     return npk, p
 
 
+class ErrorLog:
+    """Each finished run's error words, copied device -> pinned host memory at the end of its finish
+    (stream-ordered: no wait on the queuing thread), one row per run. A ticket's check() then reads
+    its own run's words however many runs later it is called - the device buffers they come from
+    (the slot's status word, the shared post parameter block) are rewritten by every later finish.
+    Rows are reused after `cap` finishes; a ticket whose row was reused refuses to report."""
+
+    def __init__(self, width, cap=8192):
+        self.buf = torch.zeros((int(cap), int(width)), dtype=D.F64, pin_memory=True)
+        self.seq = np.full(int(cap), -1, dtype=np.int64)
+        self.count = 0
+
+    def record(self, parts, stream):
+        """Queue the copies of `parts` (float64 device tensors, or int64 ones viewed as float64 bits)
+        into the next row on `stream`. Returns (row, sequence number)."""
+        r = self.count % self.buf.shape[0]
+        seq = self.count
+        self.seq[r] = seq
+        self.count += 1
+        off = 0
+        with torch.cuda.stream(stream):
+            for t in parts:
+                k = t.numel()
+                self.buf[r, off:off + k].copy_(t.reshape(-1), non_blocking=True)
+                off += k
+        return r, seq
+
+    def read(self, row, seq, done):
+        """The row's words once `done` (the run's end event) has passed."""
+        if self.seq[row] != seq:
+            raise RuntimeError(f"the error words of run {seq} were overwritten ({self.buf.shape[0]} runs later)")
+        done.synchronize()
+        return self.buf[row].numpy().copy()
+
+
 class Ticket:
     """One run in the pipeline: its slot, the tensors it reads, the pocket job, then its results."""
 
-    __slots__ = ("slot", "y", "z", "f", "job", "npock", "result", "h2d", "status", "finished", "done")
+    __slots__ = ("slot", "y", "z", "f", "job", "npock", "result", "h2d", "finished", "done", "log", "erow")
 
     def ready(self):
         return self.job.done()
@@ -68,13 +103,15 @@ class Ticket:
     def check(self):
         """Raise as the host chain would (waits for the device): non-finite hits, a lattice that is
         not a convex unfolded grid, pockets that are not locally Delaunay, too few points for the
-        plane fits."""
+        plane fits. Reads this run's own error words (ErrorLog), not the slot's current ones."""
         self.job.result()
-        st = int(self.status.item())
+        if self.erow is None:  # begun, never finished: the pocket job's checks are all there is
+            return
+        w = self.log.read(*self.erow, self.done)
+        st = int(w[:1].view(np.int64)[0])
         if st & (_F_NOT_DELAUNAY | _F_POCKET):
             raise _lib.AKBError("griddata: the grid is too distorted for the structured Delaunay triangulation")
-        if self.result is not None:
-            pupil_post_check(self.result["params"])
+        pupil_post_check(w[1:])
 
 
 class FaithfulPupil:
@@ -121,6 +158,9 @@ class FaithfulPupil:
         self._done = None  # the latest finish's end (finishes share work / map / pupil / psf buffers)
         self._omegas = D.host_f64(chebyshev_weights(max(self.sweeps, 1)))
         self.pool = concurrent.futures.ThreadPoolExecutor(max_workers=int(workers), thread_name_prefix="akb-pockets")
+        # per run: the pocket status word (int64 bits) | the post parameter block's first 18 words
+        self.errors = ErrorLog(1 + 18)
+        self.finished = 0  # runs through finish()
 
     # ------------------------------------------------------------------ stage 1
     def begin(self, y, z, f, stream=None):
@@ -153,7 +193,7 @@ class FaithfulPupil:
             ev.record(st)
         t = Ticket()
         t.slot, t.y, t.z, t.f = s, y, z, f
-        t.npock, t.result, t.h2d, t.status, t.finished, t.done = None, None, None, s["status"], False, None
+        t.npock, t.result, t.h2d, t.finished, t.done, t.log, t.erow = None, None, None, False, None, self.errors, None
         t.job = self.pool.submit(self._pockets, s, ev)
         s["last"] = t
         return t
@@ -187,7 +227,13 @@ class FaithfulPupil:
         the buffers are reused by the next finish on the stream. events: optional (start, end)
         timing events recorded around the device work; psf_events: the same around the PSF alone."""
         L = _lib.lib()
-        t.npock = t.job.result()
+        try:
+            t.npock = t.job.result()
+        except BaseException:
+            # the run failed on the host (check() raises it again); its slot stays usable
+            t.y = t.z = t.f = None
+            t.finished = True
+            raise
         s = t.slot
         st = torch.cuda.current_stream() if stream is None else stream
         sh = D.stream_handle(st)
@@ -228,6 +274,7 @@ class FaithfulPupil:
             self.psf = psf
             if events is not None:
                 events[1].record(st)
+            t.erow = self.errors.record((s["status"].view(D.F64), post["params"][:18]), st)
             t.done = torch.cuda.Event()
             t.done.record(st)
             self._done = t.done
@@ -235,6 +282,7 @@ class FaithfulPupil:
                         params=post["params"], axes=self.axes, change=self.change)
         t.y = t.z = t.f = None
         t.finished = True
+        self.finished += 1
         return t.result
 
     def run(self, y, z, f, stream=None):

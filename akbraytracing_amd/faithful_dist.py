@@ -33,7 +33,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from .faithful import pack_pockets
+from .faithful import ErrorLog, pack_pockets
 from .griddata import CONE_SWEEPS, _F_NEG, _F_NONCONVEX, _F_NONFINITE, _F_NOT_DELAUNAY, _F_POCKET, _F_POS
 from .wavefront import Shard
 
@@ -262,7 +262,7 @@ def _all_reduce_min(comm, t, group=None):
 # ---------------------------------------------------------------------- the pipeline
 
 class DistTicket:
-    __slots__ = ("slot", "job", "npock", "err", "result", "h2d", "finished", "done")
+    __slots__ = ("slot", "job", "npock", "err", "result", "h2d", "finished", "done", "erow")
 
     def ready(self):
         return self.job.done()
@@ -325,6 +325,9 @@ class ShardedFaithfulPupil:
             if p.is_root else None
         self.flags_all = 0
         self._done = None  # the latest finish's end (finishes share work / owner / map / psf buffers)
+        # per run (band owner): every rank's cell flags | the pocket status word | the post block's 18 words
+        self.errors = ErrorLog(comm.world + 1 + 18) if p.is_root else None
+        self.finished = 0
 
     @staticmethod
     def _v(t, elems_off):
@@ -354,7 +357,7 @@ class ShardedFaithfulPupil:
         sh = D.stream_handle(st)
         win, diag = s["win"], s["diag"]
         t = DistTicket()
-        t.slot, t.npock, t.err, t.result, t.h2d, t.finished, t.done = s, 0, None, None, None, False, None
+        t.slot, t.npock, t.err, t.result, t.h2d, t.finished, t.done, t.erow = s, 0, None, None, None, False, None, None
         with torch.cuda.stream(st):
             if s["last"] is not None and s["last"].done is not None:  # the slot's last reader
                 st.wait_event(s["last"].done)
@@ -479,6 +482,7 @@ class ShardedFaithfulPupil:
                 self.psf = psf
                 res = dict(psf=psf, map=self.map[0], corrected=post["corrected"], rotated=post["rotated"],
                            params=post["params"], axes=self.axes, change=self.change)
+                t.erow = self.errors.record((s["rflags"], s["status"].view(D.F64), post["params"][:18]), st)
             if events is not None:
                 events[1].record(st)
             t.done = torch.cuda.Event()
@@ -486,33 +490,37 @@ class ShardedFaithfulPupil:
             self._done = t.done
         t.result = res
         t.finished = True
+        self.finished += 1
         return res
 
     def check(self, t):
         """Raise as the one-process chain would (band owner; waits for the device): non-finite hits, a
         lattice that is not a convex unfolded grid, pockets that are not locally Delaunay, too few
-        points for the plane fits. The other ranks hold no result and return. Valid until t's slot
-        is begun again."""
+        points for the plane fits. The other ranks hold no result and return. Reads t's own error
+        words (faithful.ErrorLog), not the slot's current ones."""
         from . import _lib
         from .pupilmap import pupil_post_check
         if not self.plan.is_root:
             return
-        fl = 0
-        for v in t.slot["rflags"].cpu().numpy():
-            fl |= int(v)
-        self.flags_all = fl
         if t.err is not None:
             raise t.err
+        if t.erow is None:
+            return
+        w = self.errors.read(*t.erow, t.done)
+        world = self.comm.world
+        fl = 0
+        for v in w[:world]:
+            fl |= int(v)
+        self.flags_all = fl
         if fl & _F_NONFINITE:
             raise ValueError("griddata: non-finite point coordinates (a ray that missed)")
         if fl & _F_NONCONVEX or (fl & _F_POS and fl & _F_NEG):
             raise _lib.AKBError("griddata: the points do not form a convex, unfolded lattice")
         if fl & _F_NOT_DELAUNAY:
             raise _lib.AKBError("griddata: the grid is too distorted for the structured Delaunay triangulation")
-        if int(t.slot["status"].item()) & (_F_NOT_DELAUNAY | _F_POCKET):
+        if int(w[world:world + 1].view(np.int64)[0]) & (_F_NOT_DELAUNAY | _F_POCKET):
             raise _lib.AKBError("griddata: the grid is too distorted for the structured Delaunay triangulation")
-        if t.result is not None:
-            pupil_post_check(t.result["params"])
+        pupil_post_check(w[world + 1:])
 
     def run(self, y, z, f, stream=None):
         """begin + finish + check of one run: (result or None, ticket)."""

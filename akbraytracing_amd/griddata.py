@@ -66,7 +66,9 @@ class CubicGrid:
         """diag_override: (cells, splits) - flat cell indices iv * (n_h - 1) + ih and the split each
         takes (0: p00-p11, 1: p01-p10) in place of the exact in-circle one, e.g. qhull's own picks in
         near-cocircular cells (tests/golden/akb_qhull_full.npz); the triangulation then is that one,
-        and the sweeps, claims and patches follow it."""
+        and the sweeps, claims and patches follow it. The override is trusted: the local-Delaunay
+        checks ran on the in-circle splits before it is applied and are not repeated for the cells
+        it changes - it exists for the qhull golden parity tests, not for user input."""
         L = _lib.lib()
         self.dev = D.device()
         self.nv, self.nh = int(n_v), int(n_h)
@@ -269,11 +271,12 @@ class CubicGrid:
         """interp with the gradients of exactly `sweeps` Chebyshev sweeps from zero, formed only where
         the targets read them (akb_gd_cone_eval_f64: a patch per interior target cell, the boundary
         band globally). Equal bit for bit to interp on gradients(maxiter=sweeps, tol=0); one launch
-        sequence, no host synchronisation. self.cone_change: the change one more sweep would make
-        at the interior target cells' corners (device, scipy's measure as ordered double bits)."""
+        sequence; the first call on a grid reads the pocket check's status word (one host
+        synchronisation), and a grid it flagged is refused on every call. self.cone_change: the
+        change one more sweep would make at the interior target cells' corners (device, scipy's
+        measure as ordered double bits)."""
         L = _lib.lib()
-        if not self._checked:
-            self._check_status()
+        self._check_status()  # re-raises on every call for a triangulation the pocket check flagged
         f = _dev(values, self.dev).reshape(-1, self.nv * self.nh).contiguous()
         gx = _dev(gx, self.dev).reshape(-1)
         gy = _dev(gy, self.dev).reshape(-1)

@@ -111,8 +111,8 @@ def parse():
                    help="stream of the faithful pupil's begin (cell pass + ring copy): the back stream, or "
                         "RayWave's finish / copy stream (N = 1), waiting for the run's back half")
     p.add_argument("--faithful-lag", type=int, default=None,
-                   help="faithful runs whose pocket jobs may be in flight before a step waits for the oldest "
-                        "(default 3; 6 at N > 1, where the band owner builds configs[3]'s 40k-point ring)")
+                   help="faithful runs in flight (begun, not finished) after each step: the oldest finishes once "
+                        "more are (default 3; 6 at N > 1, where the band owner builds configs[3]'s 40k-point ring)")
     p.add_argument("--no-ramp-form", action="store_true",
                    help="skip the timed steps before the clock ramp (ms_per_step_no_ramp)")
     p.add_argument("--psf-start", choices=("pupil", "pass1"), default="pupil",
@@ -382,13 +382,32 @@ def _lib_hash():
     return _lib.sources_hash()
 
 
+def launch_ranks(n):
+    """`python bench.py --gpus N` without a launcher: start N ranks (one process per GPU) through
+    torch.distributed.run on 127.0.0.1 and return its exit code. Called before anything touches the
+    GPU, so this process never initialises HIP (the ranks are its children, not an exec)."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     args.warmup = max(args.warmup, 3 if args.fuse >= 2 else 1)
     import torch
     from akbraytracing_amd import build as B
     from akbraytracing_amd import dist as AD
     rank, world, local = AD.init_from_env()
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} ranks")
     if not os.path.exists(B.SO):
         if rank == 0:
             B.build()
@@ -461,6 +480,7 @@ def main():
         args.faithful_lag = 3 if world == 1 else 6
     fp = None
     tickets = []
+    finished = []  # every finished run's ticket: its error words are checked after the timed region
     fp_events = []
     if faithful and world == 1:
         from akbraytracing_amd.faithful import FaithfulPupil
@@ -476,9 +496,9 @@ def main():
 
     def faithful_back(timed, f):
         """The reference's pupil and PSF of the oldest front: its tilt and OPD were fused into later
-        passes 1, so its rows are final; the cell pass and the pocket job start now, and the runs
-        whose pockets are built (or the oldest, once --faithful-lag are in flight) finish on the
-        back stream - griddata, plane correction, psf_calc, PSF - beside the next passes."""
+        passes 1, so its rows are final; the cell pass and the pocket job start now, and the oldest
+        run, once more than --faithful-lag are in flight, finishes on the back stream - griddata,
+        plane correction, psf_calc, PSF - beside the next passes."""
         bs = back_stream
         with torch.cuda.stream(bs):
             out = rw.launch_back(f, stream=bs)
@@ -496,12 +516,16 @@ def main():
             if timed:
                 e1.record(cs)
                 fp_events.append(("begin", e0, e1))
-            # N > 1: every rank finishes the same runs (collectives), so by count alone
-            while tickets and ((world == 1 and tickets[0].ready()) or len(tickets) > args.faithful_lag):
+            # by count alone (every rank finishes the same runs, N > 1: collectives): with
+            # --faithful-lag runs in flight after every step, the timed steps finish exactly as many
+            # runs as they begin (faithful_finishes_timed == steps)
+            while len(tickets) > args.faithful_lag:
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if timed else None
                 pe = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) \
                     if timed and rank == 0 else None
-                fp.finish(tickets.pop(0), stream=bs, events=ev, psf_events=pe)
+                t = tickets.pop(0)
+                fp.finish(t, stream=bs, events=ev, psf_events=pe)
+                finished.append(t)
                 if timed:
                     fp_events.append(("finish", ev[0], ev[1]))
                 if pe is not None:
@@ -559,6 +583,21 @@ def main():
         comm.barrier()
         return time.perf_counter() - t0, hm
 
+    # first use of every kernel, the pocket workers and the pinned buffers of the chain, before any
+    # step: one run and its faithful pupil on their own (outside every timed region; a fresh
+    # process otherwise pays those first launches inside the driver's short W / K form)
+    if fp is not None:
+        o0 = rw.run(geometry=sys_of(0), next_geometry=sys_of(1))
+        d20 = o0["detcenter2"]
+        if world == 1:
+            t0 = fp.begin(d20[1], d20[2], o0["wave2"], stream=back_stream)
+            fp.finish(t0, stream=back_stream)
+            t0.check()
+        else:
+            fp.run(d20[1], d20[2], o0["wave2"], stream=back_stream)
+        del o0, d20
+        torch.cuda.synchronize()
+
     # the driver's form without the clock ramp, in the same process: W warm-up steps, K timed
     no_ramp_ms = None
     if args.ramp_ms > 0 and not args.no_ramp_form:
@@ -590,18 +629,21 @@ def main():
     fp_events.clear()
     psf_events.clear()
     # host_ms: host time spent issuing each step (its waits included): is the host the limit?
+    fin0 = fp.finished if fp is not None else 0
     el, host_ms = timed_steps(args.steps)
+    finishes_timed = (fp.finished - fin0) if fp is not None else None
     while fronts:  # the last front's back half (outside the timed region, like the first one's)
         back(False)
     while tickets:
-        fp.finish(tickets.pop(0), stream=back_stream)
+        t = tickets.pop(0)
+        fp.finish(t, stream=back_stream)
+        finished.append(t)
     torch.cuda.synchronize()
     faithful_checked = None
-    if faithful:  # every run's error words (the reference's raises), read now that nothing waits on them
-        for sl in fp.slots:
-            if sl["last"] is not None:
-                fp.check(sl["last"]) if world > 1 else sl["last"].check()
-        faithful_checked = sum(1 for sl in fp.slots if sl["last"] is not None)
+    if faithful:  # every run's own error words (the reference's raises), read now that nothing waits on them
+        for t in finished:
+            fp.check(t) if world > 1 else t.check()
+        faithful_checked = len(finished)
     psf_alone_ms = psf_device_ms = None
     if rank == 0:  # the PSF's own wall time, nothing beside it (the last pupil: rw.pupil is collective)
         opd, pitch = (fp.post["opd"], None) if faithful else state["pupil"]
@@ -752,11 +794,15 @@ def main():
         "pupil": ("faithful: each step's PSF from the reference's own pupil - griddata(cubic) of Wave2 on the "
                   f"{n}^2 hits (cone solve, {fp.K if world > 1 else fp.sweeps} Chebyshev sweeps), nanmean removal, "
                   "plane correction, psf_calc (rotation, rotate_with_nan, pad 16) - pipelined on the back stream "
-                  + (f"(akbraytracing_amd/faithful.py; {faithful_checked} runs' error words checked)" if world == 1 else
+                  + ("(akbraytracing_amd/faithful.py)" if world == 1 else
                      f"(akbraytracing_amd/faithful_dist.py: each rank grids its own rows, halo of {fp.K + 3} rows "
                      f"from its neighbours, the boundary band ({sum(fp.plan.band_count(r) for r in range(world))} "
-                     f"hits) to rank 0; {faithful_checked} runs' error words checked)") if faithful else
+                     f"hits) to rank 0)") if faithful else
                   "stand-in: RayWave.pupil's ray-index sampler (up to 0.098 nm from the reference's Clough-Tocher)"),
+        # faithful runs finished inside the timed region (count-based lag: equal to steps) and runs
+        # whose own error words were checked after it
+        "faithful_finishes_timed": finishes_timed,
+        "faithful_runs_checked": faithful_checked,
         "faithful_chain_ms": ((sum(fp_begin) + sum(fp_fin)) / max(len(fp_fin), 1)) if fp_fin else None,
         "faithful_finish_ms": (sum(fp_fin) / len(fp_fin)) if fp_fin else None,
         "psf_ms": psf_ms if psf_events else None,

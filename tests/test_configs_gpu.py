@@ -7,13 +7,17 @@ rays), and - given the device's tilt matrices, centre and means, which only a fu
 forms - the tilted detector hits, DistError2 and Wave2 of the sampled rays bit for bit through the
 oracle's own rotation and plane primitives.
 
-C5 (configs[4]): the same at 3163^2 with the Legendre figure-error OPL perturbation on every ray; the
-perturbation against oracle/legendre.py (to the OPL's rounding), the rest as C4. And the config's
-three-wavelength PSF stack sharded one wavelength per rank (dist.psf_stack_sharded, three gloo ranks
-on the one GPU, the real transform): each rank's plane and the gathered stack equal the
-single-process stack bit for bit.
+C5 (configs[4]): the same at its own 10000^2 (1e8 rays) and at 3163^2 with the Legendre figure-error
+OPL perturbation on every ray; the perturbation against oracle/legendre.py (to the OPL's rounding),
+the rest as C4. And the config's three-wavelength PSF stack sharded one wavelength per rank
+(dist.psf_stack_sharded, three gloo ranks on the one GPU, the real transform): each rank's plane and
+the gathered stack equal the single-process stack bit for bit.
 
-AKB_raytrace_20250312.py:2694-2905 (grid, passes, resample), :3583-3677 (tilt, OPD); SURVEY.md §8(d).
+C2 (configs[1]): KB_debug's pair at params = 0 (bench.py --config c2's system) at its own 3163^2,
+20000 sampled rays plus the picks against the oracle as C4.
+
+AKB_raytrace_20250312.py:2694-2905 (grid, passes, resample), :3583-3677 (tilt, OPD), KB_debug
+:10948-10997; legendre_fit.py:45-57; SURVEY.md §8(d).
 """
 import os
 import socket
@@ -86,9 +90,9 @@ def _oracle_opd(g, last_hit, dir_out, opl, params, means):
     return det2, dist_err2, dist_err2 - sph
 
 
-def _check_config(n, perturbation=None, k=20000):
+def _check_config(n, perturbation=None, k=20000, g=None):
     from akbraytracing_amd.wavefront import RayWave, SystemGeometry
-    g = golden_json("akb_geometry.json")
+    g = golden_json("akb_geometry.json") if g is None else g
     rw = RayWave(SystemGeometry.from_dict(g), n, perturbation=perturbation)
     out = rw.run()
     torch.cuda.synchronize()
@@ -119,12 +123,22 @@ def test_c4_1e8_rays_sampled_vs_oracle(gpu):
     _check_config(10000)
 
 
-def test_c5_3163_perturbed_sampled_vs_oracle(gpu):
+@pytest.mark.parametrize("n", [3163, 10000])
+def test_c5_perturbed_sampled_vs_oracle(gpu, n):
+    """configs[4]: the Legendre-perturbed trace at 3163^2 and at the config's own 10000^2 (1e8 rays)."""
     from akbraytracing_amd.legendre import LegendrePerturbation, config5_coefficients
     pert = LegendrePerturbation(config5_coefficients())
-    out = _check_config(3163, perturbation=pert)
-    w = out["wave2"].cpu().numpy()
-    assert np.isfinite(w).all()
+    out = _check_config(n, perturbation=pert)
+    assert bool(torch.isfinite(out["wave2"]).all())
+    del out
+    torch.cuda.empty_cache()
+
+
+def test_c2_3163_kb_sampled_vs_oracle(gpu):
+    """configs[1] at its own 3163^2: KB_debug's pair (bench.py --config c2), sampled rays bit for bit."""
+    import bench
+    out = _check_config(3163, g=bench.geometry_dict("c2"))
+    assert bool(torch.isfinite(out["wave2"]).all())
 
 
 def _free_port():

@@ -141,6 +141,23 @@ def test_bench_two_ranks_runs_to_the_json_line(gpu, tmp_path):
     assert out["n_gpus"] == 2 and out["value"] > 0
 
 
+def test_bench_gpus_flag_launches_the_ranks(gpu):
+    """`python bench.py --gpus 2` with no launcher starts its own two ranks (torch.distributed.run
+    as a child, before anything touches the GPU): the line reports the world it ran, n_gpus == 2.
+    gloo lets both ranks share the one GPU here; the driver's 8-GPU node runs RCCL."""
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["AKB_DIST_BACKEND"] = "gloo"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--rays", "1e5", "--steps", "2",
+           "--warmup", "3", "--ramp-ms", "0", "--no-extras", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["n_gpus"] == 2 and out["steps"] == 2 and out["value"] > 0
+    assert out["config"]["rays_total"] == 447 * 447  # round(sqrt(2 x 1e5))^2: C4's weak-scaling grid
+
+
 def _huygens_field(n, m, seed=3):
     rng = np.random.default_rng(seed)
     T = [rng.random(n) * 2e-6 + o for o in (1.0, 0.0, 0.0)]

@@ -1188,7 +1188,8 @@ def test_griddata_default_tol_margin(gpu):
 
 def test_griddata_flagged_triangulation_stays_refused(gpu):
     """A triangulation the pocket check flags is refused on the first gradient call and on every later
-    one (the failing status is kept, not only the fact that it was read)."""
+    one (the failing status is kept, not only the fact that it was read) - by interp and by the
+    cone solve, whichever comes first."""
     from akbraytracing_amd import _lib
     from akbraytracing_amd.griddata import CubicGrid
     X, Y, F = _lattice(40, 50, 2)
@@ -1198,6 +1199,13 @@ def test_griddata_flagged_triangulation_stays_refused(gpu):
     for _ in range(3):
         with pytest.raises(_lib.AKBError):
             cg.interp(F.ravel(), gx, gy)
+        with pytest.raises(_lib.AKBError):
+            cg.interp_cone(F.ravel(), gx, gy)
+    cg2 = CubicGrid(X.ravel(), Y.ravel(), 40, 50)
+    cg2._status.fill_(2)
+    for _ in range(2):  # the cone solve first: refused on the first call and again on the second
+        with pytest.raises(_lib.AKBError):
+            cg2.interp_cone(F.ravel(), gx, gy)
 
 
 def _interp_k_sweeps(cg, vals, gx, gy, K):
@@ -1307,6 +1315,13 @@ def test_gd_axes_equal_numpy_linspace(gpu):
         assert np.array_equal(gx.cpu().numpy(), np.linspace(rx.min(), rx.max(), mx))
         assert np.array_equal(gy.cpu().numpy(), np.linspace(ry.min(), ry.max(), my))
         assert np.array_equal(ext.cpu().numpy()[:4], [rx.min(), rx.max(), ry.min(), ry.max()])
+        # the pitch psf_calc takes once the driver has subtracted the meshgrids' means (:3698, :1176)
+        gh, gv = np.meshgrid(gx.cpu().numpy(), gy.cpu().numpy())
+        gh, gv = gh - np.mean(gh), gv - np.mean(gv)
+        if mx > 1:
+            assert ext[4].item() == np.abs(gh[0, 1] - gh[0, 0])
+        if my > 1:
+            assert ext[5].item() == np.abs(gv[1, 0] - gv[0, 0])
 
 
 def test_griddata_batched_values_and_errors(gpu):

@@ -2,11 +2,12 @@
 
 configs[1] is KB_debug's pair traced on a 3163 x 3163 grid (1e7 rays) and the Wavecalc driver's
 stages over it: source -> M1 (1e7 targets), M1 -> M2 (1e7 x 1e7 = 1e14 pairs,
-~260 s on one MI355X: not a test), M2 -> image grid. The driver resumes a mirror stage from its
-complex_data_M<k>.npz (Wavecalc_raytrace_fromData_CPU0402.py:261-269, :281-290), which is how the
-chain runs here at full size: M2's field comes from a file, every other stage is propagated on
-the device and checked against the oracle's C sum on sampled targets (<= 1e-9 of max |u|, the
-Huygens bar of tests/test_gpu_parity.py).
+~200 s on one MI355X: run here on 4096 sampled M2 targets, 4e10 pairs, with the real M1 field as
+its sources), M2 -> image grid. The driver resumes a mirror stage from its complex_data_M<k>.npz
+(Wavecalc_raytrace_fromData_CPU0402.py:261-269, :281-290), which is how the chain runs here at
+full size: M2's field comes from a file, every other stage is propagated on the device and checked
+against the oracle's C sum on sampled targets (<= 1e-9 of max |u|, the Huygens bar of
+tests/test_gpu_parity.py). Reference stage: Wavecalc_raytrace_fromData_GPU0402_multi.py:471.
 """
 import os
 
@@ -40,6 +41,20 @@ def test_wave_chain_3163_with_m2_resumed(gpu, tmp_path):
     pick = rng.choice(m1.shape[1], 20000, replace=False)
     want = O.huygens_c(m1[0, pick], m1[1, pick], m1[2, pick], src[0], src[1], src[2], np.ones(1, complex), k)
     assert np.max(np.abs(fields["M1"][pick] - want)) <= 1e-9 * np.max(np.abs(want))
+    # M1 -> M2 (the driver's :471 stage) on 4096 sampled M2 targets: the real M1 field times its dS
+    # as the 1e7 sources (4e10 pairs on the device), 24 of the targets against the oracle's C sum
+    import torch
+    from akbraytracing_amd.wavecalc import propagate
+    dev = torch.device("cuda", 0)
+    t12 = rng.choice(m2.shape[1], 4096, replace=False)
+    tt = [torch.from_numpy(np.ascontiguousarray(m2[r, t12])).to(dev) for r in range(3)]
+    ss = [torch.from_numpy(np.ascontiguousarray(m1[r])).to(dev) for r in range(3)]
+    u1ds = fields["M1"] * m1[3]
+    got = propagate(*tt, *ss, torch.from_numpy(u1ds).to(dev), k).cpu().numpy()
+    chk = np.arange(0, 4096, 171)
+    want = O.huygens_c(m2[0, t12[chk]], m2[1, t12[chk]], m2[2, t12[chk]], m1[0], m1[1], m1[2], u1ds, k)
+    assert np.all(np.isfinite(got)) and np.max(np.abs(got[chk] - want)) <= 1e-9 * np.max(np.abs(want))
+    del tt, ss
     # M2 -> image grid (x2 about its mean, as the driver scales it): 1e7 sources x 2500 targets
     g = img.copy()
     for r in range(3):
