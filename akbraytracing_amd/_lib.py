@@ -43,7 +43,7 @@ EXPORTS = [
     "akb_psf_work_bytes", "akb_psf_f64", "akb_psf_release_plans", "akb_selftest_arith_f64",
     "akb_first_valid_rows_f64", "akb_rotate_work_bytes", "akb_rotate_with_nan_f64", "akb_pupil_post_f64",
     "akb_moments_work_bytes", "akb_map_moments_f64", "akb_plane_subtract_f64", "akb_legendre_rows_f64",
-    "akb_gd_cells_f64", "akb_gd_pockets", "akb_gd_check_pockets", "akb_gd_grad_sweep_f64", "akb_gd_grad_sweeps_f64",
+    "akb_gd_cells_f64", "akb_gd_pockets", "akb_gd_check_pockets", "akb_gd_grad_sweeps_f64",
     "akb_gd_eval_f64", "akb_gd_cone_work_bytes", "akb_gd_cone_eval_f64", "akb_gd_axes_f64",
     "akb_gd_claims_f64", "akb_gd_cone_part_f64", "akb_gd_part_finish_f64", "akb_gd_ring_f64", "akb_gd_cells_window_f64",
     "akb_trace_chain_batch_f64", "akb_focus_eval_work_bytes", "akb_focus_eval_f64", "akb_sep_search_f64",
@@ -173,8 +173,6 @@ def _declare(L):
         "akb_warp_affine_f64": ([c_vp, c_int, c_int, c_vp, c_int, c_vp, c_vp], c_int),
         "akb_gd_check_pockets": ([c_vp, c_vp, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_dbl, c_vp, c_vp],
                                  c_int),
-        "akb_gd_grad_sweep_f64": ([c_vp, c_vp, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
-                                   c_vp, c_vp, c_dbl, c_vp, c_vp, c_vp, c_vp], c_int),
         "akb_gd_grad_sweeps_f64": ([c_vp, c_vp, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
                                     c_vp, c_vp, c_dbl, c_dbl, c_int, c_vp, c_vp, c_vp, c_vp, c_vp], c_int),
         "akb_gd_eval_f64": ([c_vp, c_vp, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int,

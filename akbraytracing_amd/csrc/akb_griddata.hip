@@ -34,8 +34,6 @@
 namespace akb {
 namespace {
 
-constexpr int kStripRowsDefault = 32;
-
 struct Grid {
     const double* x;  // (n,) point x (detcenter2[1])
     const double* y;  // (n,) point y (detcenter2[2])
@@ -48,8 +46,6 @@ struct Grid {
     const int32_t* edge_tri;  // (L) pocket triangle across ring edge e, -1 (hull edge)
     const int32_t* xptr;   // (L + 1) extra neighbours of ring vertex r (pocket chords)
     const int32_t* xidx;
-    int no_xcd;  // 1: plain block order in the sweep (AKB_GD_NOXCD, A/B timing only)
-    int strip_rows = kStripRowsDefault;  // rows per strip workgroup (AKB_GD_ROWS, A/B timing)
     // cell rows [row0, row1) the cell pass and the claims visit (a rank's window of a sharded
     // lattice: x, y, diag are then "virtual" global arrays of which only the window's rows, plus
     // two vertex rows below and above, are backed); row1 < 0: every row
@@ -393,6 +389,20 @@ __global__ void k_gd_check_pockets(Grid g, double tol, unsigned* flags) {
 }
 
 // ------------------------------------------------------------------ gradients
+//
+// scipy's local solve at vertex i (estimate_gradients_2d_global, scipy 1.15 interpolate/_interpnd):
+// over the edges e = p_j - p_i, with r3 = |e|^-3,
+//     Q = 4 sum r3 e e^T,    s = sum (6 (f_i - f_j) + 2 e.g_j) r3 e,    g_i <- -Q^-1 s.
+// With M = r3 e e^T and w = r3 e per edge this is g_i <- c - P S: c = -Q^-1 sum 6 (f_i - f_j) w and
+// P = 2 Q^-1 depend on the geometry and the values only, S = sum M g_j on the iterate. Every kernel
+// below forms them in one arithmetic (edge_geom, acc_edge, vertex_consts, jacobi_y) and one edge
+// order - left, right, down, up, then the diagonals present (those of cells (iv-1, ih-1), (iv-1, ih),
+// (iv, ih-1), (iv, ih)); a ring vertex's pocket chords are summed over lanes and added to those -
+// so any two kernels reach the same iterate bit for bit. A kernel that keeps the geometry (the cone
+// patches) then spends four FMAs per edge and sweep. An edge's M and w are the same from both of
+// its ends (the edge vector only changes sign), and an absent edge taken as M = 0 adds exact zeros
+// (S starts at +0 and a zero product never turns it negative), so the patches may run all eight
+// slots without branches and still give the gather kernels' bits.
 
 __device__ __forceinline__ int64_t ring_pos(const Grid& g, int iv, int ih) {
     const int64_t a = g.nh - 1, b = g.nv - 1;
@@ -403,72 +413,231 @@ __device__ __forceinline__ int64_t ring_pos(const Grid& g, int iv, int ih) {
     return -1;
 }
 
-// sums of the local problem: Q (geometry only, shared by the value sets; the factor 4 applied at
-// the solve) and s per value set
-template <int NV>
-struct GradAcc {
-    double q0 = 0, q1 = 0, q3 = 0;
-    double s0[NV] = {}, s1[NV] = {};
+// ring vertex r's lattice index (the ring in k_gd_ring's order)
+__device__ __forceinline__ int64_t ring_vertex(const Grid& g, int64_t r) {
+    const int64_t ra = g.nh - 1, rb = g.nv - 1;
+    if (r < ra) return r;
+    if (r < ra + rb) return (r - ra) * g.nh + (g.nh - 1);
+    if (r < 2 * ra + rb) return (int64_t)(g.nv - 1) * g.nh + (g.nh - 1 - (r - ra - rb));
+    return (int64_t)(g.nv - 1 - (r - 2 * ra - rb)) * g.nh;
+}
+
+// one edge's geometry: M = r3 e e^T (mxx, mxy, myy) and w = r3 e. r3 from the hardware reciprocal
+// square root and one Newton step (relative error ~1e-16; the solve is an iteration, not
+// reproduced from scipy bit for bit)
+struct EdgeG {
+    double mxx, mxy, myy, wx, wy;
 };
 
-constexpr int64_t kGradChunk = 4 * kBlock;  // vertices per workgroup of a sweep
-
-// one edge (vertex i -> j) of the local problem, NV value sets
-template <int NV>
-__device__ __forceinline__ void grad_edge(const Grid& g, int64_t n, int64_t j, double xi, double yi,
-                                          const double (&fi)[NV], const double* __restrict__ f,
-                                          const double* __restrict__ gin, GradAcc<NV>& A) {
-    const double ex = g.x[j] - xi, ey = g.y[j] - yi;
-    // 1 / L^3 from the hardware reciprocal square root and one Newton step (relative error
-    // ~1e-16: this solve is converged to 1e-10, not reproduced bit for bit)
+__device__ __forceinline__ EdgeG edge_geom(double ex, double ey) {
     const double l2 = ex * ex + ey * ey;
     double r = __builtin_amdgcn_rsq(l2);
     r = r * __builtin_fma(-0.5 * l2 * r, r, 1.5);
     const double r3 = r * r * r;
-    const double wx = ex * r3, wy = ey * r3;
-    A.q0 = __builtin_fma(ex, wx, A.q0);
-    A.q1 = __builtin_fma(ex, wy, A.q1);
-    A.q3 = __builtin_fma(ey, wy, A.q3);
+    EdgeG e;
+    e.wx = ex * r3;
+    e.wy = ey * r3;
+    e.mxx = ex * e.wx;
+    e.mxy = ex * e.wy;
+    e.myy = ey * e.wy;
+    return e;
+}
+
+// a vertex's sums: Q / 4 (geometry, shared by the value sets), c-sums and S per value set. S runs
+// as two chains - the axis edges (and chords) in s, the diagonals in d - folded s + d before use
+// (acc_fold), which halves the dependent FMA chain of a patch sweep
+template <int NV>
+struct GradAcc {
+    double q0 = 0, q1 = 0, q3 = 0;
+    double c0[NV] = {}, c1[NV] = {};
+    double s0[NV] = {}, s1[NV] = {};
+    double d0[NV] = {}, d1[NV] = {};
+};
+
+constexpr int kAccWords(int nv) { return 3 + 4 * nv; }  // a GradAcc in ring_acc / chord buffers
+
+template <int NV, bool kDiag = false>
+__device__ __forceinline__ void acc_edge(GradAcc<NV>& A, const EdgeG& e, const double (&fi)[NV], const double (&fj)[NV],
+                                         const double (&gxj)[NV], const double (&gyj)[NV]) {
+    A.q0 = A.q0 + e.mxx;
+    A.q1 = A.q1 + e.mxy;
+    A.q3 = A.q3 + e.myy;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
-        const double df2 = -ex * gin[2 * (v * n + j)] - ey * gin[2 * (v * n + j) + 1];
-        const double w = 6 * (fi[v] - f[v * n + j]) - 2 * df2;
-        A.s0[v] = __builtin_fma(w, wx, A.s0[v]);
-        A.s1[v] = __builtin_fma(w, wy, A.s1[v]);
+        const double c6 = 6 * (fi[v] - fj[v]);
+        A.c0[v] = __builtin_fma(c6, e.wx, A.c0[v]);
+        A.c1[v] = __builtin_fma(c6, e.wy, A.c1[v]);
+        double& t0 = kDiag ? A.d0[v] : A.s0[v];
+        double& t1 = kDiag ? A.d1[v] : A.s1[v];
+        t0 = __builtin_fma(e.mxy, gyj[v], __builtin_fma(e.mxx, gxj[v], t0));
+        t1 = __builtin_fma(e.myy, gyj[v], __builtin_fma(e.mxy, gxj[v], t1));
     }
 }
 
-// Chebyshev semi-iteration on top of the Jacobi sweep (gprev != nullptr): the new gradient is
-// omega * (y - g_prev) + g_prev with y the Jacobi solve's value, which contracts the error by
-// ~0.27 per sweep instead of Jacobi's ~1/2 (the iteration matrix's spectrum lies in [-1/2, 1/2]:
-// the local problem is block diagonally dominant by a factor 2)
-struct Cheb {
-    const double* gprev;  // the iterate before gin (nullptr: a plain sweep, unless zero_prev)
-    double omega;
-    int zero_prev = 0;    // the previous iterate is zero (a Chebyshev step from x_0 = 0)
+// S = axis chain + diagonal chain (d = 0 after: the sums are then ready to add, store or solve)
+template <int NV>
+__device__ __forceinline__ GradAcc<NV>& acc_fold(GradAcc<NV>& A) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        A.s0[v] = A.s0[v] + A.d0[v];
+        A.s1[v] = A.s1[v] + A.d1[v];
+        A.d0[v] = A.d1[v] = 0.0;
+    }
+    return A;
+}
+
+// A = A + B, every word (chords + lattice edges)
+template <int NV>
+__device__ __forceinline__ void acc_add(GradAcc<NV>& A, const GradAcc<NV>& B) {
+    A.q0 = A.q0 + B.q0;
+    A.q1 = A.q1 + B.q1;
+    A.q3 = A.q3 + B.q3;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        A.c0[v] = A.c0[v] + B.c0[v];
+        A.c1[v] = A.c1[v] + B.c1[v];
+        A.s0[v] = A.s0[v] + B.s0[v];
+        A.s1[v] = A.s1[v] + B.s1[v];
+    }
+}
+
+// the fixed butterfly over W lanes (a lane group's chord sums; zero partners change no bits)
+template <int NV, int W>
+__device__ __forceinline__ void acc_reduce(GradAcc<NV>& A) {
+    for (int off = W / 2; off > 0; off >>= 1) {
+        A.q0 += __shfl_down(A.q0, off, W);
+        A.q1 += __shfl_down(A.q1, off, W);
+        A.q3 += __shfl_down(A.q3, off, W);
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            A.c0[v] += __shfl_down(A.c0[v], off, W);
+            A.c1[v] += __shfl_down(A.c1[v], off, W);
+            A.s0[v] += __shfl_down(A.s0[v], off, W);
+            A.s1[v] += __shfl_down(A.s1[v], off, W);
+        }
+    }
+}
+
+template <int NV>
+__device__ __forceinline__ void acc_store(double* d, const GradAcc<NV>& A) {
+    d[0] = A.q0;
+    d[1] = A.q1;
+    d[2] = A.q3;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        d[3 + 4 * v] = A.c0[v];
+        d[4 + 4 * v] = A.c1[v];
+        d[5 + 4 * v] = A.s0[v];
+        d[6 + 4 * v] = A.s1[v];
+    }
+}
+
+template <int NV>
+__device__ __forceinline__ GradAcc<NV> acc_load(const double* d) {
+    GradAcc<NV> A;
+    A.q0 = d[0];
+    A.q1 = d[1];
+    A.q3 = d[2];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        A.c0[v] = d[3 + 4 * v];
+        A.c1[v] = d[4 + 4 * v];
+        A.s0[v] = d[5 + 4 * v];
+        A.s1[v] = d[6 + 4 * v];
+    }
+    return A;
+}
+
+// the vertex's constants of value set v: c = -Q^-1 csum, P = 2 Q^-1 (symmetric)
+struct VConst {
+    double c0, c1, p00, p01, p11;
 };
 
-// the 2 x 2 solve of value set v; returns the relative change of the Jacobi step (scipy's measure)
 template <int NV>
-__device__ __forceinline__ double grad_solve(const GradAcc<NV>& A, int v, const double* gin, double* gout,
-                                             int64_t o, const Cheb& ch) {
+__device__ __forceinline__ VConst vertex_consts(const GradAcc<NV>& A, int v) {
     const double q0 = 4 * A.q0, q1 = 4 * A.q1, q3 = 4 * A.q3;
     const double inv = 1.0 / (q0 * q3 - q1 * q1);
-    const double r0 = (q3 * A.s0[v] - q1 * A.s1[v]) * inv;
-    const double r1 = (-q1 * A.s0[v] + q0 * A.s1[v]) * inv;
-    const double c = fmax(fabs(gin[o] + r0), fabs(gin[o + 1] + r1)) / fmax(1.0, fmax(fabs(r0), fabs(r1)));
-    if (ch.gprev) {
-        const double p0 = ch.gprev[o], p1 = ch.gprev[o + 1];
-        gout[o] = ch.omega * (-r0 - p0) + p0;
-        gout[o + 1] = ch.omega * (-r1 - p1) + p1;
-    } else if (ch.zero_prev) {
-        gout[o] = ch.omega * (-r0 - 0.0) + 0.0;
-        gout[o + 1] = ch.omega * (-r1 - 0.0) + 0.0;
-    } else {
-        gout[o] = -r0;
-        gout[o + 1] = -r1;
+    VConst k;
+    k.c0 = -((q3 * A.c0[v] - q1 * A.c1[v]) * inv);
+    k.c1 = -((q0 * A.c1[v] - q1 * A.c0[v]) * inv);
+    const double i2 = 2 * inv;
+    k.p00 = q3 * i2;
+    k.p01 = -(q1 * i2);
+    k.p11 = q0 * i2;
+    return k;
+}
+
+// the Jacobi step's new gradient y = c - P S
+__device__ __forceinline__ void jacobi_y(const VConst& k, double s0, double s1, double& y0, double& y1) {
+    y0 = k.c0 - __builtin_fma(k.p01, s1, k.p00 * s0);
+    y1 = k.c1 - __builtin_fma(k.p01, s0, k.p11 * s1);
+}
+
+// scipy's change measure of a Jacobi step from (gx, gy) to y (its stopping rule's quantity)
+__device__ __forceinline__ double change_of(double gx, double gy, double y0, double y1) {
+    return fmax(fabs(gx - y0), fabs(gy - y1)) / fmax(1.0, fmax(fabs(y0), fabs(y1)));
+}
+
+// sweep j's weight and predecessor form: mode 0 plain (y itself), 2 against the predecessor p
+// (omega (y - p) + p), 1 the same against a zero predecessor (the caller passes p = 0)
+struct ConeStep {
+    int mode;
+    double omega;
+};
+
+__device__ __forceinline__ double cheb(const ConeStep& st, double y, double p) {
+    return st.mode == 0 ? y : __builtin_fma(st.omega, y - p, p);  // mode 1: p = 0
+}
+
+// Chebyshev semi-iteration for a Jacobi spectrum in [-1/2, 1/2] (the local problem is block
+// diagonally dominant by a factor 2): ~0.27 error contraction per sweep instead of
+// Jacobi's 1/2. The global kernels' form of ConeStep: gprev = x_{k-1} (mode 2), zero_prev (mode 1).
+struct Cheb {
+    const double* gprev;
+    double omega;
+    int zero_prev = 0;
+};
+
+// the solve of value set v at output offset o (gin nullptr: x_k = 0); returns the change measure
+template <int NV>
+__device__ __forceinline__ double grad_solve(const GradAcc<NV>& A, int v, const double* gin, double* gout, int64_t o,
+                                             const Cheb& ch) {
+    const VConst k = vertex_consts<NV>(A, v);
+    double y0, y1;
+    jacobi_y(k, A.s0[v], A.s1[v], y0, y1);  // A folded by the caller
+    const double gx = gin ? gin[o] : 0.0, gy = gin ? gin[o + 1] : 0.0;
+    const ConeStep st{ch.gprev ? 2 : (ch.zero_prev ? 1 : 0), ch.omega};
+    const double px = ch.gprev ? ch.gprev[o] : 0.0, py = ch.gprev ? ch.gprev[o + 1] : 0.0;
+    gout[o] = cheb(st, y0, px);
+    gout[o + 1] = cheb(st, y1, py);
+    return change_of(gx, gy, y0, y1);
+}
+
+// one edge i -> j read from global memory (gin nullptr: x = 0)
+template <int NV>
+__device__ __forceinline__ void grad_edge(const Grid& g, int64_t n, int64_t j, double xi, double yi,
+                                          const double (&fi)[NV], const double* __restrict__ f,
+                                          const double* __restrict__ gin, GradAcc<NV>& A) {
+    double fj[NV], gxj[NV], gyj[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        fj[v] = f[v * n + j];
+        gxj[v] = gin ? gin[2 * (v * n + j)] : 0.0;
+        gyj[v] = gin ? gin[2 * (v * n + j) + 1] : 0.0;
     }
-    return c;
+    acc_edge<NV>(A, edge_geom(g.x[j] - xi, g.y[j] - yi), fi, fj, gxj, gyj);
+}
+
+// ring vertex r's pocket chords over a group of W lanes (sub: the lane in the group), reduced by the
+// group's butterfly (zeros from the lanes past the chord list)
+template <int NV, int W>
+__device__ __forceinline__ GradAcc<NV> chord_sums(const Grid& g, int64_t n, int64_t r, int sub, double xi, double yi,
+                                                  const double (&fi)[NV], const double* __restrict__ f,
+                                                  const double* __restrict__ gin) {
+    GradAcc<NV> A;
+    for (int32_t k = g.xptr[r] + sub; k < g.xptr[r + 1]; k += W) grad_edge<NV>(g, n, g.xidx[k], xi, yi, fi, f, gin, A);
+    acc_reduce<NV, W>(A);  // (the chords run in the axis chain: d stays 0)
+    return A;
 }
 
 template <int W>
@@ -487,302 +656,51 @@ __device__ __forceinline__ void change_max_n(double worst, unsigned long long* c
     }
 }
 
-__device__ __forceinline__ void change_max(double worst, unsigned long long* chg) {
-    __shared__ double red[kBlock / 64];
-    for (int off = 32; off > 0; off >>= 1) worst = fmax(worst, __shfl_down(worst, off));
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = worst;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int w = 1; w < kBlock / 64; ++w) worst = fmax(worst, red[w]);
-        const unsigned long long bits = (unsigned long long)__double_as_longlong(worst);
-        if (chg && worst > 0 && __hip_atomic_load(chg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < bits)
-            atomicMax(chg, bits);
-    }
-}
-
-// One Jacobi sweep for NV value sets sharing the geometry: gout[i] from gin of the grid
-// neighbours (4 axis + the diagonals of the 4 cells around i). Ring vertices also have pocket
-// chords - a hull vertex can fan out to thousands - so for them this kernel only stores the
-// grid-edge sums in ring_acc and k_gd_grad_ring adds the chords with a whole wave and solves.
-template <int NV>
-__global__ void __launch_bounds__(kBlock) k_gd_grad(Grid g, const double* __restrict__ f,
-                                                    const double* __restrict__ gin, double* __restrict__ gout,
-                                                    double* __restrict__ ring_acc, unsigned long long* chg, Cheb ch) {
-    const int64_t n = (int64_t)g.nv * g.nh;
-    double worst = 0.0;
-    // XCD-aware: the grid is a multiple of 8 and blocks b, b + 8, ... (one XCD, dealt round-robin)
-    // take consecutive chunks, so the rows above and below a chunk are read through the same L2
-    const int64_t per = gridDim.x / 8;
-    const int64_t chunk = g.no_xcd ? (int64_t)blockIdx.x : (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
-    const int64_t i0 = chunk * kGradChunk, i1 = i0 + kGradChunk < n ? i0 + kGradChunk : n;
-    for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-        const int iv = (int)(i / g.nh), ih = (int)(i - (int64_t)iv * g.nh);
-        const double xi = g.x[i], yi = g.y[i];
-        double fi[NV];
-#pragma unroll
-        for (int v = 0; v < NV; ++v) fi[v] = f[v * n + i];
-        GradAcc<NV> A;
-        if (ih > 0) grad_edge<NV>(g, n, i - 1, xi, yi, fi, f, gin, A);
-        if (ih < g.nh - 1) grad_edge<NV>(g, n, i + 1, xi, yi, fi, f, gin, A);
-        if (iv > 0) grad_edge<NV>(g, n, i - g.nh, xi, yi, fi, f, gin, A);
-        if (iv < g.nv - 1) grad_edge<NV>(g, n, i + g.nh, xi, yi, fi, f, gin, A);
-        const int64_t c0 = (int64_t)iv * (g.nh - 1) + ih;  // cell with p00 = i
-        if (iv > 0 && ih > 0 && g.diag[c0 - g.nh] == 0) grad_edge<NV>(g, n, i - g.nh - 1, xi, yi, fi, f, gin, A);
-        if (iv > 0 && ih < g.nh - 1 && g.diag[c0 - (g.nh - 1)] == 1)
-            grad_edge<NV>(g, n, i - g.nh + 1, xi, yi, fi, f, gin, A);
-        if (iv < g.nv - 1 && ih > 0 && g.diag[c0 - 1] == 1) grad_edge<NV>(g, n, i + g.nh - 1, xi, yi, fi, f, gin, A);
-        if (iv < g.nv - 1 && ih < g.nh - 1 && g.diag[c0] == 0) grad_edge<NV>(g, n, i + g.nh + 1, xi, yi, fi, f, gin, A);
-        const int64_t r = ring_pos(g, iv, ih);
-        if (r >= 0) {
-            double* d = ring_acc + r * (3 + 2 * NV);
-            d[0] = A.q0;
-            d[1] = A.q1;
-            d[2] = A.q3;
-#pragma unroll
-            for (int v = 0; v < NV; ++v) {
-                d[3 + 2 * v] = A.s0[v];
-                d[4 + 2 * v] = A.s1[v];
-            }
-            continue;
-        }
-#pragma unroll
-        for (int v = 0; v < NV; ++v) worst = fmax(worst, grad_solve<NV>(A, v, gin, gout, 2 * (v * n + i), ch));
-    }
-    change_max(worst, chg);
-}
-
-// The same sweep with every vertex's data read from HBM once: a workgroup walks down a strip of
-// kStripW columns (plus one halo column each side) over strip_rows rows (default 32), holding three rows of
-// (x, y, f, g) in an LDS ring, the next row already in registers while the current one is solved
-// (its loads in flight across the row's arithmetic). The per-vertex edge order and arithmetic are
-// k_gd_grad's, so both give the same bits; the global version's eight-neighbour gathers (about 50
-// load instructions per vertex through the texture path) become LDS reads.
-
-template <int NV, int W>
-struct StripRow {  // one row of a strip in LDS: column c of the strip at [c + 1], halos at 0 / W + 1
-    double x[W + 2], y[W + 2];
-    double f[NV][W + 2];
-    double gx[NV][W + 2], gy[NV][W + 2];
-    uint8_t d[W + 2];  // the diagonal flags of the cell row below (cells (row, col - 1) at [col])
-};
-
-template <int NV>
-struct StripVals {
-    double x, y, f[NV], gx[NV], gy[NV];
-    int d;  // diag of cell (row, col) (0 outside the cells)
-};
-
-template <int NV>
-__device__ __forceinline__ void strip_load(const Grid& g, int64_t n, const double* __restrict__ f,
-                                           const double* __restrict__ gin, int64_t i, StripVals<NV>& v) {
-    v.x = g.x[i];
-    v.y = g.y[i];
-    const int iv = (int)(i / g.nh), ih = (int)(i - (int64_t)iv * g.nh);
-    v.d = (iv < g.nv - 1 && ih < g.nh - 1) ? g.diag[(int64_t)iv * (g.nh - 1) + ih] : 0;
-#pragma unroll
-    for (int k = 0; k < NV; ++k) {
-        v.f[k] = f[k * n + i];
-        v.gx[k] = gin[2 * (k * n + i)];
-        v.gy[k] = gin[2 * (k * n + i) + 1];
-    }
-}
-
-template <int NV, int W>
-__device__ __forceinline__ void strip_store(StripRow<NV, W>& r, int c, const StripVals<NV>& v) {
-    r.x[c] = v.x;
-    r.y[c] = v.y;
-    r.d[c] = (uint8_t)v.d;
-#pragma unroll
-    for (int k = 0; k < NV; ++k) {
-        r.f[k][c] = v.f[k];
-        r.gx[k][c] = v.gx[k];
-        r.gy[k][c] = v.gy[k];
-    }
-}
-
-// grad_edge with the neighbour's data from an LDS row
-template <int NV, int W>
-__device__ __forceinline__ void grad_edge_lds(const StripRow<NV, W>& r, int c, double xi, double yi,
-                                              const double (&fi)[NV], GradAcc<NV>& A) {
-    const double ex = r.x[c] - xi, ey = r.y[c] - yi;
-    const double l2 = ex * ex + ey * ey;
-    double rr = __builtin_amdgcn_rsq(l2);
-    rr = rr * __builtin_fma(-0.5 * l2 * rr, rr, 1.5);
-    const double r3 = rr * rr * rr;
-    const double wx = ex * r3, wy = ey * r3;
-    A.q0 = __builtin_fma(ex, wx, A.q0);
-    A.q1 = __builtin_fma(ex, wy, A.q1);
-    A.q3 = __builtin_fma(ey, wy, A.q3);
-#pragma unroll
-    for (int v = 0; v < NV; ++v) {
-        const double df2 = -ex * r.gx[v][c] - ey * r.gy[v][c];
-        const double w = 6 * (fi[v] - r.f[v][c]) - 2 * df2;
-        A.s0[v] = __builtin_fma(w, wx, A.s0[v]);
-        A.s1[v] = __builtin_fma(w, wy, A.s1[v]);
-    }
-}
-
-// kGS: a line Gauss-Seidel sweep instead of Jacobi - once row iv is solved, its new gradients
-// replace the old ones in the LDS ring, so row iv + 1 sees its upper neighbours' new values (the
-// way scipy's Gauss-Seidel sweep sees its earlier vertices'); left / right neighbours, the rows
-// outside the chunk, the halo columns and the ring vertices keep the old values. Same local solve,
-// same fixed point, ~1/3 fewer sweeps; deterministic (no value depends on workgroup timing).
-template <int NV, int W, bool kGS = false>
-__global__ void __launch_bounds__(W) k_gd_grad_strip(Grid g, const double* __restrict__ f,
-                                                     const double* __restrict__ gin, double* __restrict__ gout,
-                                                     double* __restrict__ ring_acc, unsigned long long* chg, Cheb ch) {
-    constexpr int kStripW = W;
-    __shared__ StripRow<NV, W> R[3];
-    const int64_t n = (int64_t)g.nv * g.nh;
-    const int nstrips = (g.nh + kStripW - 1) / kStripW;
-    const int strip = blockIdx.x % nstrips, chunk = blockIdx.x / nstrips;
-    const int c0 = strip * kStripW;
-    const int r0 = chunk * g.strip_rows;
-    const int r1 = r0 + g.strip_rows < g.nv ? r0 + g.strip_rows : g.nv;
-    const int t = threadIdx.x;
-    const int ih = c0 + t;
-    const bool col = ih < g.nh;
-    // halo columns: thread 0 the left one, thread 1 the right one (when they exist)
-    const int hcol = t == 0 ? c0 - 1 : c0 + kStripW;
-    const int hslot = t == 0 ? 0 : kStripW + 1;
-    const bool halo = t < 2 && hcol >= 0 && hcol < g.nh;
-    double worst = 0.0;
-    // rows iv + 1 and iv + 2 wait in two register sets (a and b, alternating) while row iv is solved
-    StripVals<NV> a, ah, b, bh;
-    auto load_row = [&](int rr, StripVals<NV>& v, StripVals<NV>& vh) {
-        if (col) strip_load<NV>(g, n, f, gin, (int64_t)rr * g.nh + ih, v);
-        if (halo) strip_load<NV>(g, n, f, gin, (int64_t)rr * g.nh + hcol, vh);
-    };
-    auto store_row = [&](int rr, const StripVals<NV>& v, const StripVals<NV>& vh) {
-        if (col) strip_store<NV, W>(R[rr % 3], t + 1, v);
-        if (halo) strip_store<NV, W>(R[rr % 3], hslot, vh);
-    };
-    // prologue: rows r0 - 1 and r0 into LDS, rows r0 + 1 and r0 + 2 into registers (a row k is
-    // needed while k <= r1: row r1 is the last row's lower neighbour)
-    for (int rr = r0 - 1; rr <= r0; ++rr) {
-        if (rr < 0) continue;
-        load_row(rr, a, ah);
-        store_row(rr, a, ah);
-    }
-    if (r0 + 1 < g.nv) load_row(r0 + 1, a, ah);
-    if (r0 + 2 < g.nv && r0 + 2 <= r1) load_row(r0 + 2, b, bh);
-    double ngx[NV], ngy[NV];
-    bool solved = false;
-    auto step = [&](int iv, StripVals<NV>& nx, StripVals<NV>& nh_) {
-        if (iv + 1 < g.nv) store_row(iv + 1, nx, nh_);  // row iv + 1: registers -> LDS
-        __syncthreads();
-        if (iv + 3 < g.nv && iv + 3 <= r1) load_row(iv + 3, nx, nh_);  // two rows ahead
-        if (col) {
-            const StripRow<NV, W>& up = R[(iv + 2) % 3];  // row iv - 1
-            const StripRow<NV, W>& cur = R[iv % 3];
-            const StripRow<NV, W>& dn = R[(iv + 1) % 3];
-            const int c = t + 1;
-            const int64_t i = (int64_t)iv * g.nh + ih;
-            const double xi = cur.x[c], yi = cur.y[c];
-            double fi[NV];
-#pragma unroll
-            for (int v = 0; v < NV; ++v) fi[v] = cur.f[v][c];
-            GradAcc<NV> A;
-            if (ih > 0) grad_edge_lds<NV, W>(cur, c - 1, xi, yi, fi, A);
-            if (ih < g.nh - 1) grad_edge_lds<NV, W>(cur, c + 1, xi, yi, fi, A);
-            if (iv > 0) grad_edge_lds<NV, W>(up, c, xi, yi, fi, A);
-            if (iv < g.nv - 1) grad_edge_lds<NV, W>(dn, c, xi, yi, fi, A);
-            // the four cells around i: (iv - 1, ih - 1), (iv - 1, ih), (iv, ih - 1), (iv, ih)
-            if (iv > 0 && ih > 0 && up.d[c - 1] == 0) grad_edge_lds<NV, W>(up, c - 1, xi, yi, fi, A);
-            if (iv > 0 && ih < g.nh - 1 && up.d[c] == 1) grad_edge_lds<NV, W>(up, c + 1, xi, yi, fi, A);
-            if (iv < g.nv - 1 && ih > 0 && cur.d[c - 1] == 1) grad_edge_lds<NV, W>(dn, c - 1, xi, yi, fi, A);
-            if (iv < g.nv - 1 && ih < g.nh - 1 && cur.d[c] == 0) grad_edge_lds<NV, W>(dn, c + 1, xi, yi, fi, A);
-            const int64_t r = ring_pos(g, iv, ih);
-            if (r >= 0) {
-                double* d = ring_acc + r * (3 + 2 * NV);
-                d[0] = A.q0;
-                d[1] = A.q1;
-                d[2] = A.q3;
-#pragma unroll
-                for (int v = 0; v < NV; ++v) {
-                    d[3 + 2 * v] = A.s0[v];
-                    d[4 + 2 * v] = A.s1[v];
-                }
-            } else {
-#pragma unroll
-                for (int v = 0; v < NV; ++v) {
-                    const int64_t o = 2 * (v * n + i);
-                    worst = fmax(worst, grad_solve<NV>(A, v, gin, gout, o, ch));
-                    if (kGS) {
-                        ngx[v] = gout[o];
-                        ngy[v] = gout[o + 1];
-                    }
-                }
-                solved = kGS;
-            }
-        }
-        __syncthreads();  // the next step overwrites row iv - 1's slot
-        if (kGS && solved) {  // row iv's new gradients, for row iv + 1 (read after the next sync)
-            StripRow<NV, W>& cur = R[iv % 3];
-#pragma unroll
-            for (int v = 0; v < NV; ++v) {
-                cur.gx[v][t + 1] = ngx[v];
-                cur.gy[v][t + 1] = ngy[v];
-            }
-            solved = false;
-        }
-    };
-    for (int iv = r0; iv < r1; iv += 2) {
-        step(iv, a, ah);
-        if (iv + 1 < r1) step(iv + 1, b, bh);
-    }
-    change_max_n<W>(worst, chg);
-}
-
-// ring vertices: one wave each adds the pocket chords (lanes stride the chord list, fixed-order
-// wave reduction) to the grid-edge sums, then solves
+// ring vertices after k_gd_sweeps' second sweep: one wave each adds the pocket chords of gin to
+// the lattice-edge sums the sweep kernel left in ring_acc, then solves
 template <int NV>
 __global__ void __launch_bounds__(kBlock) k_gd_grad_ring(Grid g, const double* __restrict__ f,
                                                          const double* __restrict__ gin, double* __restrict__ gout,
                                                          const double* __restrict__ ring_acc, unsigned long long* chg,
                                                          Cheb ch) {
     const int64_t n = (int64_t)g.nv * g.nh;
-    const int64_t a = g.nh - 1, b = g.nv - 1, L = 2 * a + 2 * b;
+    const int64_t L = 2 * (int64_t)(g.nh - 1) + 2 * (int64_t)(g.nv - 1);
     const int lane = threadIdx.x & 63;
     double worst = 0.0;
     for (int64_t r = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; r < L;
          r += ((int64_t)gridDim.x * blockDim.x) >> 6) {
-        int64_t i;
-        if (r < a) i = r;
-        else if (r < a + b) i = (r - a) * g.nh + (g.nh - 1);
-        else if (r < 2 * a + b) i = (int64_t)(g.nv - 1) * g.nh + (g.nh - 1 - (r - a - b));
-        else i = (int64_t)(g.nv - 1 - (r - 2 * a - b)) * g.nh;
+        const int64_t i = ring_vertex(g, r);
         const double xi = g.x[i], yi = g.y[i];
         double fi[NV];
 #pragma unroll
         for (int v = 0; v < NV; ++v) fi[v] = f[v * n + i];
-        GradAcc<NV> A;
-        for (int32_t k = g.xptr[r] + lane; k < g.xptr[r + 1]; k += 64) grad_edge<NV>(g, n, g.xidx[k], xi, yi, fi, f, gin, A);
-        for (int off = 32; off > 0; off >>= 1) {
-            A.q0 += __shfl_down(A.q0, off);
-            A.q1 += __shfl_down(A.q1, off);
-            A.q3 += __shfl_down(A.q3, off);
-#pragma unroll
-            for (int v = 0; v < NV; ++v) {
-                A.s0[v] += __shfl_down(A.s0[v], off);
-                A.s1[v] += __shfl_down(A.s1[v], off);
-            }
-        }
+        GradAcc<NV> A = chord_sums<NV, 64>(g, n, r, lane, xi, yi, fi, f, gin);
         if (lane == 0) {
-            const double* d = ring_acc + r * (3 + 2 * NV);
-            A.q0 += d[0];
-            A.q1 += d[1];
-            A.q3 += d[2];
-#pragma unroll
-            for (int v = 0; v < NV; ++v) {
-                A.s0[v] += d[3 + 2 * v];
-                A.s1[v] += d[4 + 2 * v];
-            }
+            acc_add<NV>(A, acc_load<NV>(ring_acc + r * kAccWords(NV)));
 #pragma unroll
             for (int v = 0; v < NV; ++v) worst = fmax(worst, grad_solve<NV>(A, v, gin, gout, 2 * (v * n + i), ch));
         }
     }
-    change_max(worst, chg);
+    change_max_n<kBlock>(worst, chg);
+}
+
+// pocket-chord sums of every ring vertex from gradients gin (nullptr = zeros), one wave each
+template <int NV>
+__global__ void __launch_bounds__(kBlock) k_gd_ring_chords(Grid g, const double* __restrict__ f,
+                                                           const double* __restrict__ gin, double* __restrict__ out) {
+    const int64_t n = (int64_t)g.nv * g.nh;
+    const int64_t L = 2 * (int64_t)(g.nh - 1) + 2 * (int64_t)(g.nv - 1);
+    const int lane = threadIdx.x & 63;
+    for (int64_t r = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; r < L;
+         r += ((int64_t)gridDim.x * blockDim.x) >> 6) {
+        const int64_t i = ring_vertex(g, r);
+        const double xi = g.x[i], yi = g.y[i];
+        double fi[NV];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) fi[v] = f[v * n + i];
+        const GradAcc<NV> A = chord_sums<NV, 64>(g, n, r, lane, xi, yi, fi, f, gin);
+        if (lane == 0) acc_store<NV>(out + r * kAccWords(NV), A);
+    }
 }
 
 // ------------------------------------------------------------------ register sweeps (two per launch)
@@ -795,16 +713,12 @@ __global__ void __launch_bounds__(kBlock) k_gd_grad_ring(Grid g, const double* _
 // the halo so the second has its neighbours, and only x, y, f and the two gradient sets of the
 // rows are read from HBM once per two sweeps. Ring vertices take their pocket chords from
 // k_gd_ring_chords (x_k, before the launch); in the second sweep they only store their grid-edge
-// sums and k_gd_grad_ring adds the chords of x_{k+1} and solves after the launch. Per vertex the
-// edge order and arithmetic are k_gd_grad's, so kK sweeps here give the bits of kK sweeps there.
+// sums and k_gd_grad_ring adds the chords of x_{k+1} and solves after the launch.
 
-// lane l gets lane l - 1's value (DPP wave_shr:1; lane 0 keeps its own) / lane l + 1's (wave_shl:1)
-__device__ __forceinline__ int lane_prev_i(int v) { return __builtin_amdgcn_update_dpp(v, v, 0x138, 0xf, 0xf, false); }
-__device__ __forceinline__ int lane_next_i(int v) { return __builtin_amdgcn_update_dpp(v, v, 0x130, 0xf, 0xf, false); }
-// (the cell flags are loaded per lane rather than shifted: an int shifted this way read the
-// neighbour on the wrong side at a flag change on the MI355X, tests/test_gpu_parity.py's 300 x 280
-// lattice; the doubles' shifts are checked bit for bit against the LDS kernels there)
-// doubles: one v_mov_b32_dpp per half with bound_ctrl (lane 0 / lane 63 read 0: halo lanes)
+// lane l gets lane l - 1's value (DPP wave_shr:1) / lane l + 1's (wave_shl:1); doubles: one
+// v_mov_b32_dpp per half with bound_ctrl (lane 0 / lane 63 read 0: halo lanes). (The cell flags are
+// loaded per lane rather than shifted: an int shifted this way read the neighbour on the wrong side
+// at a flag change on the MI355X.)
 __device__ __forceinline__ double lane_prev(double v) {
     return __hiloint2double(__builtin_amdgcn_mov_dpp(__double2hiint(v), 0x138, 0xf, 0xf, true),
                             __builtin_amdgcn_mov_dpp(__double2loint(v), 0x138, 0xf, 0xf, true));
@@ -835,85 +749,46 @@ __device__ __forceinline__ RV<NV> rv_shift(const RV<NV>& r) {
     return o;
 }
 
-// grad_edge with the neighbour in registers
-template <int NV>
-__device__ __forceinline__ void edge_rv(const RV<NV>& o, double xi, double yi, const double (&fi)[NV],
-                                        GradAcc<NV>& A) {
-    const double ex = o.x - xi, ey = o.y - yi;
-    const double l2 = ex * ex + ey * ey;
-    double rr = __builtin_amdgcn_rsq(l2);
-    rr = rr * __builtin_fma(-0.5 * l2 * rr, rr, 1.5);
-    const double r3 = rr * rr * rr;
-    const double wx = ex * r3, wy = ey * r3;
-    A.q0 = __builtin_fma(ex, wx, A.q0);
-    A.q1 = __builtin_fma(ex, wy, A.q1);
-    A.q3 = __builtin_fma(ey, wy, A.q3);
-#pragma unroll
-    for (int v = 0; v < NV; ++v) {
-        const double df2 = -ex * o.gx[v] - ey * o.gy[v];
-        const double w = 6 * (fi[v] - o.f[v]) - 2 * df2;
-        A.s0[v] = __builtin_fma(w, wx, A.s0[v]);
-        A.s1[v] = __builtin_fma(w, wy, A.s1[v]);
-    }
+template <int NV, bool kDiag>
+__device__ __forceinline__ void edge_rv(const RV<NV>& o, const RV<NV>& c, GradAcc<NV>& A) {
+    acc_edge<NV, kDiag>(A, edge_geom(o.x - c.x, o.y - c.y), c.f, o.f, o.gx, o.gy);
 }
 
-// the grid-edge sums of the vertex in row `cur` (wave-uniform control flow: the lane shifts run in
-// every lane; only the shifts some lane of the wave needs are made)
+// the lattice-edge sums of the vertex in row `cur` (wave-uniform control flow: the lane shifts run
+// in every lane; only the shifts some lane of the wave needs are made)
 template <int NV>
 __device__ __forceinline__ GradAcc<NV> vertex_sums(const RV<NV>& up, const RV<NV>& cur, const RV<NV>& dn,
                                                    bool hl, bool hr, bool hu, bool hd) {
-    // which diagonals exist: cells (iv - 1, ih - 1), (iv - 1, ih), (iv, ih - 1), (iv, ih)
     const bool ul = hu && hl && up.dl == 0, ur = hu && hr && up.d == 1;
     const bool dl = hd && hl && cur.dl == 1, dr = hd && hr && cur.d == 0;
     GradAcc<NV> A;
-    // one shifted neighbour live at a time, the edges in k_gd_grad's order
     {
         const RV<NV> L = rv_shift<NV, false>(cur);
-        if (hl) edge_rv<NV>(L, cur.x, cur.y, cur.f, A);
+        if (hl) edge_rv<NV, false>(L, cur, A);
     }
     {
         const RV<NV> R = rv_shift<NV, true>(cur);
-        if (hr) edge_rv<NV>(R, cur.x, cur.y, cur.f, A);
+        if (hr) edge_rv<NV, false>(R, cur, A);
     }
-    if (hu) edge_rv<NV>(up, cur.x, cur.y, cur.f, A);
-    if (hd) edge_rv<NV>(dn, cur.x, cur.y, cur.f, A);
+    if (hu) edge_rv<NV, false>(up, cur, A);
+    if (hd) edge_rv<NV, false>(dn, cur, A);
     if (__any(ul)) {
         const RV<NV> N = rv_shift<NV, false>(up);
-        if (ul) edge_rv<NV>(N, cur.x, cur.y, cur.f, A);
+        if (ul) edge_rv<NV, true>(N, cur, A);
     }
     if (__any(ur)) {
         const RV<NV> N = rv_shift<NV, true>(up);
-        if (ur) edge_rv<NV>(N, cur.x, cur.y, cur.f, A);
+        if (ur) edge_rv<NV, true>(N, cur, A);
     }
     if (__any(dl)) {
         const RV<NV> N = rv_shift<NV, false>(dn);
-        if (dl) edge_rv<NV>(N, cur.x, cur.y, cur.f, A);
+        if (dl) edge_rv<NV, true>(N, cur, A);
     }
     if (__any(dr)) {
         const RV<NV> N = rv_shift<NV, true>(dn);
-        if (dr) edge_rv<NV>(N, cur.x, cur.y, cur.f, A);
+        if (dr) edge_rv<NV, true>(N, cur, A);
     }
-    return A;
-}
-
-// grad_solve on registers: y = -Q^-1 s, the change against the current value (gi), then the
-// Chebyshev combination with the previous iterate (p; plain: y itself)
-template <int NV>
-__device__ __forceinline__ double solve_rv(const GradAcc<NV>& A, int v, double gix, double giy, bool plain,
-                                           double omega, double px, double py, double& ox, double& oy) {
-    const double q0 = 4 * A.q0, q1 = 4 * A.q1, q3 = 4 * A.q3;
-    const double inv = 1.0 / (q0 * q3 - q1 * q1);  // the same for every v: CSE'd across the unrolled calls
-    const double r0 = (q3 * A.s0[v] - q1 * A.s1[v]) * inv;
-    const double r1 = (-q1 * A.s0[v] + q0 * A.s1[v]) * inv;
-    const double c = fmax(fabs(gix + r0), fabs(giy + r1)) / fmax(1.0, fmax(fabs(r0), fabs(r1)));
-    if (plain) {
-        ox = -r0;
-        oy = -r1;
-    } else {
-        ox = omega * (-r0 - px) + px;
-        oy = omega * (-r1 - py) + py;
-    }
-    return c;
+    return acc_fold<NV>(A);
 }
 
 template <int NV>
@@ -924,13 +799,13 @@ struct SweepArgs {
     double om1, om2;       // the two sweeps' weights
     double* gout1;         // x_{k+1}
     double* gout2;         // x_{k+2} (kK = 2)
-    const double* chords;  // (L, 3 + 2 NV) pocket-chord sums of x_k (k_gd_ring_chords)
-    double* ring_acc;      // (L, 3 + 2 NV) grid-edge sums of x_{k+1} at ring vertices (kK = 2)
+    const double* chords;  // (L, kAccWords) pocket-chord sums of x_k (k_gd_ring_chords)
+    double* ring_acc;      // (L, kAccWords) grid-edge sums of x_{k+1} at ring vertices (kK = 2)
     unsigned long long* chg;  // [2]: largest relative change of each sweep
     int rows;              // rows per wave
 };
 
-template <int NV, int kK, int kWaves, int kDepth = 1>
+template <int NV, int kK, int kWaves>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves)))
 k_gd_sweeps(Grid g, SweepArgs<NV> a) {
     constexpr int kHalo = kK;             // halo lanes on each side
@@ -981,6 +856,7 @@ k_gd_sweeps(Grid g, SweepArgs<NV> a) {
                 py[v] = a.gprev[2 * (v * n + i) + 1];
             }
         };
+        const ConeStep st1{a.gprev ? 2 : 0, a.om1}, st2{2, a.om2};
         // sweep 1 of row i (rows up / cur / dn) -> s (x_{k+1} of row i, NV x 2)
         auto sweep1 = [&](int i, const RV<NV>& up, const RV<NV>& cur, const RV<NV>& dn, const double (&px)[NV],
                           const double (&py)[NV], RV<NV>& s) {
@@ -988,28 +864,23 @@ k_gd_sweeps(Grid g, SweepArgs<NV> a) {
             GradAcc<NV> A = vertex_sums<NV>(up, cur, dn, hl, hr, i > 0, i < g.nv - 1);
             if (!col || i < 0 || i >= g.nv) return;
             const int64_t r = ring_pos(g, i, ih);
-            if (r >= 0) {  // pocket chords of x_k (commutative sum: the bits of k_gd_grad_ring's order)
-                const double* c = a.chords + r * (3 + 2 * NV);
-                A.q0 = c[0] + A.q0;
-                A.q1 = c[1] + A.q1;
-                A.q3 = c[2] + A.q3;
-#pragma unroll
-                for (int v = 0; v < NV; ++v) {
-                    A.s0[v] = c[3 + 2 * v] + A.s0[v];
-                    A.s1[v] = c[4 + 2 * v] + A.s1[v];
-                }
+            if (r >= 0) {  // pocket chords of x_k, then the lattice edges
+                GradAcc<NV> C = acc_load<NV>(a.chords + r * kAccWords(NV));
+                acc_add<NV>(C, A);
+                A = C;
             }
             const bool mine = own && i >= r0 && i < r1;
             const int64_t o = (int64_t)i * g.nh + ih;
 #pragma unroll
             for (int v = 0; v < NV; ++v) {
-                double ox, oy;
-                const double ch = solve_rv<NV>(A, v, cur.gx[v], cur.gy[v], a.gprev == nullptr, a.om1, px[v], py[v],
-                                               ox, oy);
+                const VConst k = vertex_consts<NV>(A, v);
+                double y0, y1;
+                jacobi_y(k, A.s0[v], A.s1[v], y0, y1);
+                const double ox = cheb(st1, y0, px[v]), oy = cheb(st1, y1, py[v]);
                 s.gx[v] = ox;
                 s.gy[v] = oy;
                 if (mine) {
-                    worst1 = fmax(worst1, ch);
+                    worst1 = fmax(worst1, change_of(cur.gx[v], cur.gy[v], y0, y1));
                     a.gout1[2 * (v * n + o)] = ox;
                     a.gout1[2 * (v * n + o) + 1] = oy;
                 }
@@ -1027,29 +898,10 @@ k_gd_sweeps(Grid g, SweepArgs<NV> a) {
         load_prev(first, px, py);
         S0 = G0;
         S1 = G1;
-        // rows i + 2 (and, kDepth = 2, i + 3) in flight across row i's arithmetic: the VGPR budget
-        // of two waves per SIMD holds a second prefetched row
-        RV<NV> P;
-        double sx[NV], sy[NV];
-        if (kDepth == 2) {
-            load(first + 2, P);
-            load_prev(first + 1, sx, sy);
-        }
         for (int i = first; i <= last; ++i) {
             RV<NV> N;
-            if (kDepth == 2) {
-                N = P;
-#pragma unroll
-                for (int v = 0; v < NV; ++v) {
-                    qx[v] = sx[v];
-                    qy[v] = sy[v];
-                }
-                load(i + 3, P);
-                load_prev(i + 2, sx, sy);
-            } else {
-                load(i + 2, N);
-                load_prev(i + 1, qx, qy);
-            }
+            load(i + 2, N);  // row i + 2 in flight across row i's arithmetic
+            load_prev(i + 1, qx, qy);
             sweep1(i, G1, G2, G3, px, py, S2);
             if (kK == 2 && i - 1 >= r0 && i - 1 < r1) {
                 // sweep 2 of row i - 1 from the x_{k+1} rows S0 (i - 2), S1 (i - 1), S2 (i)
@@ -1059,24 +911,17 @@ k_gd_sweeps(Grid g, SweepArgs<NV> a) {
                     const int64_t o = (int64_t)iv * g.nh + ih;
                     const int64_t r = ring_pos(g, iv, ih);
                     if (r >= 0) {  // k_gd_grad_ring adds the chords of x_{k+1} and solves
-                        double* d = a.ring_acc + r * (3 + 2 * NV);
-                        d[0] = A.q0;
-                        d[1] = A.q1;
-                        d[2] = A.q3;
-#pragma unroll
-                        for (int v = 0; v < NV; ++v) {
-                            d[3 + 2 * v] = A.s0[v];
-                            d[4 + 2 * v] = A.s1[v];
-                        }
+                        acc_store<NV>(a.ring_acc + r * kAccWords(NV), A);
                     } else {
 #pragma unroll
                         for (int v = 0; v < NV; ++v) {
-                            double ox, oy;
+                            const VConst k = vertex_consts<NV>(A, v);
+                            double y0, y1;
+                            jacobi_y(k, A.s0[v], A.s1[v], y0, y1);
+                            worst2 = fmax(worst2, change_of(S1.gx[v], S1.gy[v], y0, y1));
                             // Chebyshev against x_k of row i - 1 (G1)
-                            worst2 = fmax(worst2, solve_rv<NV>(A, v, S1.gx[v], S1.gy[v], false, a.om2, G1.gx[v],
-                                                               G1.gy[v], ox, oy));
-                            a.gout2[2 * (v * n + o)] = ox;
-                            a.gout2[2 * (v * n + o) + 1] = oy;
+                            a.gout2[2 * (v * n + o)] = cheb(st2, y0, G1.gx[v]);
+                            a.gout2[2 * (v * n + o) + 1] = cheb(st2, y1, G1.gy[v]);
                         }
                     }
                 }
@@ -1109,70 +954,6 @@ k_gd_sweeps(Grid g, SweepArgs<NV> a) {
     }
 }
 
-// pocket-chord sums of every ring vertex from gradients gin (nullptr = zeros): one wave per ring
-// vertex, lanes striding its chord list, the fixed-order wave reduction of k_gd_grad_ring
-template <int NV>
-__global__ void __launch_bounds__(kBlock) k_gd_ring_chords(Grid g, const double* __restrict__ f,
-                                                           const double* __restrict__ gin, double* __restrict__ out) {
-    const int64_t n = (int64_t)g.nv * g.nh;
-    const int64_t a = g.nh - 1, b = g.nv - 1, L = 2 * a + 2 * b;
-    const int lane = threadIdx.x & 63;
-    for (int64_t r = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; r < L;
-         r += ((int64_t)gridDim.x * blockDim.x) >> 6) {
-        int64_t i;
-        if (r < a) i = r;
-        else if (r < a + b) i = (r - a) * g.nh + (g.nh - 1);
-        else if (r < 2 * a + b) i = (int64_t)(g.nv - 1) * g.nh + (g.nh - 1 - (r - a - b));
-        else i = (int64_t)(g.nv - 1 - (r - 2 * a - b)) * g.nh;
-        const double xi = g.x[i], yi = g.y[i];
-        double fi[NV];
-#pragma unroll
-        for (int v = 0; v < NV; ++v) fi[v] = f[v * n + i];
-        GradAcc<NV> A;
-        for (int32_t k = g.xptr[r] + lane; k < g.xptr[r + 1]; k += 64) {
-            const int64_t j = g.xidx[k];
-            const double ex = g.x[j] - xi, ey = g.y[j] - yi;
-            const double l2 = ex * ex + ey * ey;
-            double rr = __builtin_amdgcn_rsq(l2);
-            rr = rr * __builtin_fma(-0.5 * l2 * rr, rr, 1.5);
-            const double r3 = rr * rr * rr;
-            const double wx = ex * r3, wy = ey * r3;
-            A.q0 = __builtin_fma(ex, wx, A.q0);
-            A.q1 = __builtin_fma(ex, wy, A.q1);
-            A.q3 = __builtin_fma(ey, wy, A.q3);
-#pragma unroll
-            for (int v = 0; v < NV; ++v) {
-                const double gx = gin ? gin[2 * (v * n + j)] : 0.0, gy = gin ? gin[2 * (v * n + j) + 1] : 0.0;
-                const double df2 = -ex * gx - ey * gy;
-                const double w = 6 * (fi[v] - f[v * n + j]) - 2 * df2;
-                A.s0[v] = __builtin_fma(w, wx, A.s0[v]);
-                A.s1[v] = __builtin_fma(w, wy, A.s1[v]);
-            }
-        }
-        for (int off = 32; off > 0; off >>= 1) {
-            A.q0 += __shfl_down(A.q0, off);
-            A.q1 += __shfl_down(A.q1, off);
-            A.q3 += __shfl_down(A.q3, off);
-#pragma unroll
-            for (int v = 0; v < NV; ++v) {
-                A.s0[v] += __shfl_down(A.s0[v], off);
-                A.s1[v] += __shfl_down(A.s1[v], off);
-            }
-        }
-        if (lane == 0) {
-            double* d = out + r * (3 + 2 * NV);
-            d[0] = A.q0;
-            d[1] = A.q1;
-            d[2] = A.q3;
-#pragma unroll
-            for (int v = 0; v < NV; ++v) {
-                d[3 + 2 * v] = A.s0[v];
-                d[4 + 2 * v] = A.s1[v];
-            }
-        }
-    }
-}
-
 // ------------------------------------------------------------------ cone solve (fixed K sweeps)
 //
 // After K Chebyshev sweeps from x_0 = 0 a vertex's gradient depends only on the vertices within K
@@ -1180,71 +961,19 @@ __global__ void __launch_bounds__(kBlock) k_gd_ring_chords(Grid g, const double*
 // iterate before that). The interpolated values need the gradients at the vertices of the
 // triangles that hold targets only, so for a 128^2 target grid over a 1e7-point lattice the global
 // iteration's x_K there is formed from small patches instead of K passes over the whole lattice:
-//   * interior targets (their cell more than K + 1 cells from the lattice boundary): one workgroup
-//     per target cell holds the (2K + 4)^2 box around the cell in LDS and runs the K sweeps on the
-//     shrinking square that still influences the cell (x_j on the vertices within K + 1 - j of it);
+//   * interior targets (their cell more than K + 1 cells from the lattice boundary): the
+//     (2K + 4)^2 box around the cell in LDS, K sweeps on the shrinking square that still influences
+//     the cell (x_j on the vertices within K + 1 - j of it), k_gd_cone_patch;
 //   * the rest (cells near the boundary, pocket triangles): the ring's pocket chords couple vertices
 //     far along a side, so those run the global iteration on the boundary band (depth <= 2K + 3 - j
-//     at sweep j, one launch per sweep, the chords in the ring kernel), valid to depth K + 3 after K
+//     at sweep j, one launch per sweep, the chords in 8-lane groups), valid to depth K + 3 after K
 //     sweeps.
-// Per vertex the edge order and arithmetic are k_gd_grad's / k_gd_grad_ring's, so the result at
-// every target vertex is the global iteration's K-sweep value bit for bit
-// (tests/test_gpu_parity.py::test_gradient_cone_equals_global_sweeps).
+// Both use the gradient arithmetic above, so every target vertex holds the global iteration's
+// K-sweep value bit for bit (tests/test_gpu_parity.py::test_gradient_cone_equals_global_sweeps).
 
 constexpr int kClaimAxisLds = 512;                // target axes up to this long go to LDS in k_gd_claim_hit
 constexpr int kConeMaxK = 14;                    // patch box side 2K + 4 <= 32
-constexpr int kConeBox = 2 * kConeMaxK + 4;
-
-// grad_edge on values: neighbour (xj, yj), its values fj and previous gradients (gxj, gyj)
-template <int NV>
-__device__ __forceinline__ void edge_vals(double xj, double yj, const double (&fj)[NV], const double (&gxj)[NV],
-                                          const double (&gyj)[NV], double xi, double yi, const double (&fi)[NV],
-                                          GradAcc<NV>& A) {
-    const double ex = xj - xi, ey = yj - yi;
-    const double l2 = ex * ex + ey * ey;
-    double r = __builtin_amdgcn_rsq(l2);
-    r = r * __builtin_fma(-0.5 * l2 * r, r, 1.5);
-    const double r3 = r * r * r;
-    const double wx = ex * r3, wy = ey * r3;
-    A.q0 = __builtin_fma(ex, wx, A.q0);
-    A.q1 = __builtin_fma(ex, wy, A.q1);
-    A.q3 = __builtin_fma(ey, wy, A.q3);
-#pragma unroll
-    for (int v = 0; v < NV; ++v) {
-        const double df2 = -ex * gxj[v] - ey * gyj[v];
-        const double w = 6 * (fi[v] - fj[v]) - 2 * df2;
-        A.s0[v] = __builtin_fma(w, wx, A.s0[v]);
-        A.s1[v] = __builtin_fma(w, wy, A.s1[v]);
-    }
-}
-
-// sweep j's weight and predecessor form: j = 1 plain, j = 2 against x_0 = 0, later against x_{j-2}
-struct ConeStep {
-    int mode;  // 0 plain, 1 zero predecessor, 2 predecessor x_{j-2}
-    double omega;
-};
-
-// grad_solve on values: returns scipy's change measure; (ox, oy) = the new gradient
-template <int NV>
-__device__ __forceinline__ double solve_vals(const GradAcc<NV>& A, int v, double gix, double giy, const ConeStep& st,
-                                             double px, double py, double& ox, double& oy) {
-    const double q0 = 4 * A.q0, q1 = 4 * A.q1, q3 = 4 * A.q3;
-    const double inv = 1.0 / (q0 * q3 - q1 * q1);
-    const double r0 = (q3 * A.s0[v] - q1 * A.s1[v]) * inv;
-    const double r1 = (-q1 * A.s0[v] + q0 * A.s1[v]) * inv;
-    const double c = fmax(fabs(gix + r0), fabs(giy + r1)) / fmax(1.0, fmax(fabs(r0), fabs(r1)));
-    if (st.mode == 2) {
-        ox = st.omega * (-r0 - px) + px;
-        oy = st.omega * (-r1 - py) + py;
-    } else if (st.mode == 1) {
-        ox = st.omega * (-r0 - 0.0) + 0.0;
-        oy = st.omega * (-r1 - 0.0) + 0.0;
-    } else {
-        ox = -r0;
-        oy = -r1;
-    }
-    return c;
-}
+constexpr int kConeBox = 2 * kConeMaxK + 4;  // the largest box side: it fits the patches' LDS pitch
 
 // the boundary band: vertices with min(iv, ih, nv - 1 - iv, nh - 1 - ih) <= D, enumerated as the
 // top rows, the bottom rows, then the left / right column pieces of the rows between
@@ -1281,255 +1010,98 @@ __device__ __forceinline__ int64_t band_vertex(const BandMap& b, int64_t k) {
     return (int64_t)r * b.nh + (c < b.cols ? c : b.nh - 2 * b.cols + c);
 }
 
-template <int NV>
 struct ConeBand {
-    const double* f;   // (NV, n)
-    const double* gin;    // x_{j-1} (NV, n, 2) or nullptr (x_0 = 0)
+    const double* f;      // (n) one value set
+    const double* gin;    // x_{j-1} (n, 2) or nullptr (x_0 = 0)
     const double* gprev;  // x_{j-2} (mode 2)
     double* gout;         // x_j
-    double* ring_acc;     // (L, 3 + 2 NV): ring vertices' grid-edge sums, solved by k_gd_cone_ring
     ConeStep st;
     const int* needed;    // device flag: some target needs the band (else the launch returns at once)
 };
 
-// vertex i's lattice-edge sums of one band sweep (k_gd_grad's edge order: left, right, down, up,
-// then the diagonals present)
-template <int NV>
-__device__ __forceinline__ void band_grid_sums(const Grid& g, const ConeBand<NV>& a, int64_t n, int64_t i, int iv,
-                                               int ih, double xi, double yi, const double (&fi)[NV],
-                                               GradAcc<NV>& A) {
-    if constexpr (NV == 1) {
-        // every candidate neighbour's data loaded first (positions off the lattice clamped to i,
-        // the diagonals' presence from their cells' bytes, loaded beside them), then the edges in
-        // the same order and arithmetic: one memory round trip per vertex instead of one per edge
-        const int64_t nh = g.nh;
-        const bool L = ih > 0, R = ih < g.nh - 1, D = iv > 0, U = iv < g.nv - 1;
-        const int64_t jn[8] = {i - 1, i + 1, i - nh, i + nh, i - nh - 1, i - nh + 1, i + nh - 1, i + nh + 1};
-        const bool inb[8] = {L, R, D, U, D && L, D && R, U && L, U && R};
-        const int64_t c0 = (int64_t)iv * (g.nh - 1) + ih;
-        const int64_t dc[4] = {c0 - g.nh, c0 - (g.nh - 1), c0 - 1, c0};
-        uint8_t dg[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) dg[k] = g.diag[inb[4 + k] ? dc[k] : 0];
-        double xs[8], ys[8], fs[8], gxs[8], gys[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int64_t j = inb[k] ? jn[k] : i;
-            xs[k] = g.x[j];
-            ys[k] = g.y[j];
-            fs[k] = a.f[j];
-            gxs[k] = a.gin ? a.gin[2 * j] : 0.0;
-            gys[k] = a.gin ? a.gin[2 * j + 1] : 0.0;
-        }
-        const bool on[8] = {L, R, D, U, inb[4] && dg[0] == 0, inb[5] && dg[1] == 1, inb[6] && dg[2] == 1,
-                            inb[7] && dg[3] == 0};
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-            if (on[k]) {
-                const double fj[1] = {fs[k]}, gxj[1] = {gxs[k]}, gyj[1] = {gys[k]};
-                edge_vals<1>(xs[k], ys[k], fj, gxj, gyj, xi, yi, fi, A);
-            }
-        return;
-    }
-    auto edge = [&](int64_t j) {
-        double fj[NV], gxj[NV], gyj[NV];
-#pragma unroll
-        for (int v = 0; v < NV; ++v) {
-            fj[v] = a.f[v * n + j];
-            gxj[v] = a.gin ? a.gin[2 * (v * n + j)] : 0.0;
-            gyj[v] = a.gin ? a.gin[2 * (v * n + j) + 1] : 0.0;
-        }
-        edge_vals<NV>(g.x[j], g.y[j], fj, gxj, gyj, xi, yi, fi, A);
-    };
-    if (ih > 0) edge(i - 1);
-    if (ih < g.nh - 1) edge(i + 1);
-    if (iv > 0) edge(i - g.nh);
-    if (iv < g.nv - 1) edge(i + g.nh);
+// vertex i's lattice-edge sums of one band sweep: every candidate neighbour's data loaded first
+// (positions off the lattice clamped to i, the diagonals' presence from their cells' bytes, loaded
+// beside them), then the edges in order: one memory round trip per vertex instead of one per edge
+__device__ __forceinline__ void band_grid_sums(const Grid& g, const ConeBand& a, int64_t i, int iv, int ih,
+                                               double xi, double yi, double fi, GradAcc<1>& A) {
+    const int64_t nh = g.nh;
+    const bool L = ih > 0, R = ih < g.nh - 1, D = iv > 0, U = iv < g.nv - 1;
+    const int64_t jn[8] = {i - 1, i + 1, i - nh, i + nh, i - nh - 1, i - nh + 1, i + nh - 1, i + nh + 1};
+    const bool inb[8] = {L, R, D, U, D && L, D && R, U && L, U && R};
     const int64_t c0 = (int64_t)iv * (g.nh - 1) + ih;
-    if (iv > 0 && ih > 0 && g.diag[c0 - g.nh] == 0) edge(i - g.nh - 1);
-    if (iv > 0 && ih < g.nh - 1 && g.diag[c0 - (g.nh - 1)] == 1) edge(i - g.nh + 1);
-    if (iv < g.nv - 1 && ih > 0 && g.diag[c0 - 1] == 1) edge(i + g.nh - 1);
-    if (iv < g.nv - 1 && ih < g.nh - 1 && g.diag[c0] == 0) edge(i + g.nh + 1);
-}
-
-// one sweep of the band (k_gd_grad's per-vertex body; nothing reads outside the lattice)
-template <int NV>
-__global__ void __launch_bounds__(kBlock) k_gd_cone_band(Grid g, BandMap bm, ConeBand<NV> a) {
-    if (!*a.needed) return;
-    const int64_t n = (int64_t)g.nv * g.nh;
-    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < bm.total;
-         k += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t i = band_vertex(bm, k);
-        const int iv = (int)(i / g.nh), ih = (int)(i - (int64_t)iv * g.nh);
-        const double xi = g.x[i], yi = g.y[i];
-        double fi[NV];
+    const int64_t dc[4] = {c0 - g.nh, c0 - (g.nh - 1), c0 - 1, c0};
+    uint8_t dg[4];
 #pragma unroll
-        for (int v = 0; v < NV; ++v) fi[v] = a.f[v * n + i];
-        GradAcc<NV> A;
-        band_grid_sums<NV>(g, a, n, i, iv, ih, xi, yi, fi, A);
-        const int64_t r = ring_pos(g, iv, ih);
-        if (r >= 0) {
-            double* d = a.ring_acc + r * (3 + 2 * NV);
-            d[0] = A.q0;
-            d[1] = A.q1;
-            d[2] = A.q3;
+    for (int k = 0; k < 4; ++k) dg[k] = g.diag[inb[4 + k] ? dc[k] : 0];
+    double xs[8], ys[8], fs[8], gxs[8], gys[8];
 #pragma unroll
-            for (int v = 0; v < NV; ++v) {
-                d[3 + 2 * v] = A.s0[v];
-                d[4 + 2 * v] = A.s1[v];
-            }
-            continue;
-        }
-#pragma unroll
-        for (int v = 0; v < NV; ++v) {
-            const int64_t o = 2 * (v * n + i);
-            const double gix = a.gin ? a.gin[o] : 0.0, giy = a.gin ? a.gin[o + 1] : 0.0;
-            const double px = a.st.mode == 2 ? a.gprev[o] : 0.0, py = a.st.mode == 2 ? a.gprev[o + 1] : 0.0;
-            double ox, oy;
-            solve_vals<NV>(A, v, gix, giy, a.st, px, py, ox, oy);
-            a.gout[o] = ox;
-            a.gout[o + 1] = oy;
-        }
+    for (int k = 0; k < 8; ++k) {
+        const int64_t j = inb[k] ? jn[k] : i;
+        xs[k] = g.x[j];
+        ys[k] = g.y[j];
+        fs[k] = a.f[j];
+        gxs[k] = a.gin ? a.gin[2 * j] : 0.0;
+        gys[k] = a.gin ? a.gin[2 * j + 1] : 0.0;
     }
+    const bool on[8] = {L, R, D, U, inb[4] && dg[0] == 0, inb[5] && dg[1] == 1, inb[6] && dg[2] == 1,
+                        inb[7] && dg[3] == 0};
+    const double fi1[1] = {fi};
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        if (on[k]) {
+            const double fj[1] = {fs[k]}, gxj[1] = {gxs[k]}, gyj[1] = {gys[k]};
+            if (k < 4) acc_edge<1, false>(A, edge_geom(xs[k] - xi, ys[k] - yi), fi1, fj, gxj, gyj);
+            else acc_edge<1, true>(A, edge_geom(xs[k] - xi, ys[k] - yi), fi1, fj, gxj, gyj);
+        }
+    acc_fold<1>(A);
 }
 
-// the ring vertices of a band sweep: pocket chords (a wave per ring vertex, k_gd_grad_ring's fixed
-// reduction order), then the grid-edge sums the band kernel left, then the solve
-// ring vertex r's lattice index (the ring in k_gd_grad_ring's order)
-__device__ __forceinline__ int64_t ring_vertex(const Grid& g, int64_t r) {
-    const int64_t ra = g.nh - 1, rb = g.nv - 1;
-    if (r < ra) return r;
-    if (r < ra + rb) return (r - ra) * g.nh + (g.nh - 1);
-    if (r < 2 * ra + rb) return (int64_t)(g.nv - 1) * g.nh + (g.nh - 1 - (r - ra - rb));
-    return (int64_t)(g.nv - 1 - (r - 2 * ra - rb)) * g.nh;
+// the solve of one band / ring vertex of sweep j, stored to x_j
+__device__ __forceinline__ void band_solve(const ConeBand& a, int64_t i, const GradAcc<1>& A) {
+    const VConst k = vertex_consts<1>(A, 0);
+    double y0, y1;
+    jacobi_y(k, A.s0[0], A.s1[0], y0, y1);
+    const int64_t o = 2 * i;
+    const double px = a.st.mode == 2 ? a.gprev[o] : 0.0, py = a.st.mode == 2 ? a.gprev[o + 1] : 0.0;
+    a.gout[o] = cheb(a.st, y0, px);
+    a.gout[o + 1] = cheb(a.st, y1, py);
 }
 
-// ring vertex r's pocket chords (one per lane of a group of W lanes, W >= the chord count, or
-// strided over a whole wave), reduced over the group by the butterfly k_gd_grad_ring uses over a
-// wave, then (lead lane) the band kernel's grid-edge sums added and the solve. For a count <= W the
-// W-lane tree is the 64-lane tree with its zero partners left out: the same bits.
-template <int NV, int W, bool GRID = false>
-__device__ __forceinline__ void cone_ring_vertex(const Grid& g, const ConeBand<NV>& a, int64_t r, int sub) {
+// ring vertex r of a band sweep over a group of W lanes (sub: the lane in it): the pocket chords
+// (chord_sums: each lane a strided part, the group's butterfly), then the lead lane adds the
+// vertex's lattice-edge sums and solves
+template <int W>
+__device__ __forceinline__ void cone_ring_vertex(const Grid& g, const ConeBand& a, int64_t r, int sub) {
     const int64_t n = (int64_t)g.nv * g.nh;
     const int64_t i = ring_vertex(g, r);
     const double xi = g.x[i], yi = g.y[i];
-    double fi[NV];
-#pragma unroll
-    for (int v = 0; v < NV; ++v) fi[v] = a.f[v * n + i];
-    GradAcc<NV> D;  // GRID: the lattice-edge sums, formed here by the lead lane (else the band kernel's)
-    if (GRID && sub == 0) {
-        const int iv = (int)(i / g.nh), ih = (int)(i - (int64_t)iv * g.nh);
-        band_grid_sums<NV>(g, a, n, i, iv, ih, xi, yi, fi, D);
-    }
-    GradAcc<NV> A;
-    for (int32_t k = g.xptr[r] + sub; k < g.xptr[r + 1]; k += W) {
-        const int64_t j = g.xidx[k];
-        double fj[NV], gxj[NV], gyj[NV];
-#pragma unroll
-        for (int v = 0; v < NV; ++v) {
-            fj[v] = a.f[v * n + j];
-            gxj[v] = a.gin ? a.gin[2 * (v * n + j)] : 0.0;
-            gyj[v] = a.gin ? a.gin[2 * (v * n + j) + 1] : 0.0;
-        }
-        edge_vals<NV>(g.x[j], g.y[j], fj, gxj, gyj, xi, yi, fi, A);
-    }
-    for (int off = W / 2; off > 0; off >>= 1) {
-        A.q0 += __shfl_down(A.q0, off, W);
-        A.q1 += __shfl_down(A.q1, off, W);
-        A.q3 += __shfl_down(A.q3, off, W);
-#pragma unroll
-        for (int v = 0; v < NV; ++v) {
-            A.s0[v] += __shfl_down(A.s0[v], off, W);
-            A.s1[v] += __shfl_down(A.s1[v], off, W);
-        }
-    }
+    const double fi[1] = {a.f[i]};
+    GradAcc<1> D;
     if (sub == 0) {
-        if (GRID) {
-            A.q0 += D.q0;
-            A.q1 += D.q1;
-            A.q3 += D.q3;
-#pragma unroll
-            for (int v = 0; v < NV; ++v) {
-                A.s0[v] += D.s0[v];
-                A.s1[v] += D.s1[v];
-            }
-        } else {
-            const double* d = a.ring_acc + r * (3 + 2 * NV);
-            A.q0 += d[0];
-            A.q1 += d[1];
-            A.q3 += d[2];
-#pragma unroll
-            for (int v = 0; v < NV; ++v) {
-                A.s0[v] += d[3 + 2 * v];
-                A.s1[v] += d[4 + 2 * v];
-            }
-        }
-#pragma unroll
-        for (int v = 0; v < NV; ++v) {
-            const int64_t o = 2 * (v * n + i);
-            const double gix = a.gin ? a.gin[o] : 0.0, giy = a.gin ? a.gin[o + 1] : 0.0;
-            const double px = a.st.mode == 2 ? a.gprev[o] : 0.0, py = a.st.mode == 2 ? a.gprev[o + 1] : 0.0;
-            double ox, oy;
-            solve_vals<NV>(A, v, gix, giy, a.st, px, py, ox, oy);
-            a.gout[o] = ox;
-            a.gout[o + 1] = oy;
-        }
+        const int iv = (int)(i / g.nh), ih = (int)(i - (int64_t)iv * g.nh);
+        band_grid_sums(g, a, i, iv, ih, xi, yi, fi[0], D);
+    }
+    GradAcc<1> A = chord_sums<1, W>(g, n, r, sub, xi, yi, fi, a.f, a.gin);
+    if (sub == 0) {
+        acc_add<1>(A, D);
+        band_solve(a, i, A);
     }
 }
 
-// the ring's solve for one sweep: eight ring vertices per wave, eight lanes each (a ring vertex
-// has a few pocket chords); a vertex with more than eight takes the whole wave afterwards
-// (k_gd_grad_ring's 64-lane loop and tree). Either way its bits are k_gd_grad_ring's.
-template <int NV>
-__global__ void __launch_bounds__(kBlock) k_gd_cone_ring(Grid g, ConeBand<NV> a) {
+// one sweep of the band in one launch: workgroups [0, nbw) take the band's vertices off the ring,
+// the rest eight ring vertices per wave (8-lane groups; a vertex with more than eight chords takes
+// the whole wave afterwards). Both halves read x_{j-1} / x_{j-2} only.
+__global__ void __launch_bounds__(kBlock) k_gd_cone_sweep8(Grid g, BandMap bm, ConeBand a, int nbw) {
     if (!*a.needed) return;
-    const int64_t L = 2 * (int64_t)(g.nh - 1) + 2 * (int64_t)(g.nv - 1);
-    const int lane = threadIdx.x & 63, sub = lane & 7;
-    for (int64_t r0 = ((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6) * 8; r0 < L;
-         r0 += (((int64_t)gridDim.x * blockDim.x) >> 6) * 8) {
-        const int64_t r = r0 + (lane >> 3);
-        const bool big = r < L && g.xptr[r + 1] - g.xptr[r] > 8;
-        if (r < L && !big) cone_ring_vertex<NV, 8>(g, a, r, sub);
-        unsigned long long m = __ballot(big && sub == 0);
-        while (m) {  // wave-uniform
-            const int q = __builtin_ctzll(m);
-            m &= m - 1;
-            cone_ring_vertex<NV, 64>(g, a, r0 + (q >> 3), lane);
-        }
-    }
-}
-
-// one sweep of the band in one launch, the ring in 8-lane groups: workgroups [0, nbw) take the band's
-// vertices off the ring (k_gd_cone_band's body), the rest eight ring vertices per wave - the lead
-// lane forms the vertex's lattice-edge sums itself (band_grid_sums, what k_gd_cone_band would have
-// left in ring_acc), the chords as k_gd_cone_ring. Both halves read x_{j-1} / x_{j-2} only: the
-// two-launch form's bits in one launch per sweep.
-template <int NV>
-__global__ void __launch_bounds__(kBlock) k_gd_cone_sweep8(Grid g, BandMap bm, ConeBand<NV> a, int nbw) {
-    if (!*a.needed) return;
-    const int64_t n = (int64_t)g.nv * g.nh;
     if ((int)blockIdx.x < nbw) {
         for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < bm.total;
              k += (int64_t)nbw * blockDim.x) {
             const int64_t i = band_vertex(bm, k);
             const int iv = (int)(i / g.nh), ih = (int)(i - (int64_t)iv * g.nh);
             if (ring_pos(g, iv, ih) >= 0) continue;
-            const double xi = g.x[i], yi = g.y[i];
-            double fi[NV];
-#pragma unroll
-            for (int v = 0; v < NV; ++v) fi[v] = a.f[v * n + i];
-            GradAcc<NV> A;
-            band_grid_sums<NV>(g, a, n, i, iv, ih, xi, yi, fi, A);
-#pragma unroll
-            for (int v = 0; v < NV; ++v) {
-                const int64_t o = 2 * (v * n + i);
-                const double gix = a.gin ? a.gin[o] : 0.0, giy = a.gin ? a.gin[o + 1] : 0.0;
-                const double px = a.st.mode == 2 ? a.gprev[o] : 0.0, py = a.st.mode == 2 ? a.gprev[o + 1] : 0.0;
-                double ox, oy;
-                solve_vals<NV>(A, v, gix, giy, a.st, px, py, ox, oy);
-                a.gout[o] = ox;
-                a.gout[o + 1] = oy;
-            }
+            GradAcc<1> A;
+            band_grid_sums(g, a, i, iv, ih, g.x[i], g.y[i], a.f[i], A);
+            band_solve(a, i, A);
         }
         return;
     }
@@ -1540,471 +1112,30 @@ __global__ void __launch_bounds__(kBlock) k_gd_cone_sweep8(Grid g, BandMap bm, C
     for (int64_t r0 = w0 * 8; r0 < L; r0 += nw * 8) {
         const int64_t r = r0 + (lane >> 3);
         const bool big = r < L && g.xptr[r + 1] - g.xptr[r] > 8;
-        if (r < L && !big) cone_ring_vertex<NV, 8, true>(g, a, r, sub);
+        if (r < L && !big) cone_ring_vertex<8>(g, a, r, sub);
         unsigned long long m = __ballot(big && sub == 0);
         while (m) {  // wave-uniform
             const int q = __builtin_ctzll(m);
             m &= m - 1;
-            cone_ring_vertex<NV, 64, true>(g, a, r0 + (q >> 3), lane);
+            cone_ring_vertex<64>(g, a, r0 + (q >> 3), lane);
         }
     }
 }
 
-// one sweep of the band in one launch: the band's vertices off the ring (k_gd_cone_band's body) in
-// the first `nb` workgroups, then a wave per ring vertex - the pocket chords reduced over the
-// wave, then the vertex's grid edges (lane 0, k_gd_cone_band's order), added to the chord sums in
-// that order as k_gd_cone_ring adds the band kernel's partial sums - then the solve. Both halves
-// read x_{j-1} / x_{j-2} only, so one launch per sweep gives k_gd_cone_band + k_gd_cone_ring's bits.
-template <int NV>
-__global__ void __launch_bounds__(kBlock) k_gd_cone_sweep(Grid g, BandMap bm, ConeBand<NV> a, int nbw) {
-    if (!*a.needed) return;
-    const int64_t n = (int64_t)g.nv * g.nh;
-    // the grid-edge sums of vertex i (k_gd_cone_band's edge order)
-    auto grid_sums = [&](int64_t i, int iv, int ih, double xi, double yi, const double (&fi)[NV], GradAcc<NV>& A) {
-        auto edge = [&](int64_t j) {
-            double fj[NV], gxj[NV], gyj[NV];
-#pragma unroll
-            for (int v = 0; v < NV; ++v) {
-                fj[v] = a.f[v * n + j];
-                gxj[v] = a.gin ? a.gin[2 * (v * n + j)] : 0.0;
-                gyj[v] = a.gin ? a.gin[2 * (v * n + j) + 1] : 0.0;
-            }
-            edge_vals<NV>(g.x[j], g.y[j], fj, gxj, gyj, xi, yi, fi, A);
-        };
-        if (ih > 0) edge(i - 1);
-        if (ih < g.nh - 1) edge(i + 1);
-        if (iv > 0) edge(i - g.nh);
-        if (iv < g.nv - 1) edge(i + g.nh);
-        const int64_t c0 = (int64_t)iv * (g.nh - 1) + ih;
-        if (iv > 0 && ih > 0 && g.diag[c0 - g.nh] == 0) edge(i - g.nh - 1);
-        if (iv > 0 && ih < g.nh - 1 && g.diag[c0 - (g.nh - 1)] == 1) edge(i - g.nh + 1);
-        if (iv < g.nv - 1 && ih > 0 && g.diag[c0 - 1] == 1) edge(i + g.nh - 1);
-        if (iv < g.nv - 1 && ih < g.nh - 1 && g.diag[c0] == 0) edge(i + g.nh + 1);
-    };
-    auto solve_store = [&](int64_t i, const GradAcc<NV>& A) {
-#pragma unroll
-        for (int v = 0; v < NV; ++v) {
-            const int64_t o = 2 * (v * n + i);
-            const double gix = a.gin ? a.gin[o] : 0.0, giy = a.gin ? a.gin[o + 1] : 0.0;
-            const double px = a.st.mode == 2 ? a.gprev[o] : 0.0, py = a.st.mode == 2 ? a.gprev[o + 1] : 0.0;
-            double ox, oy;
-            solve_vals<NV>(A, v, gix, giy, a.st, px, py, ox, oy);
-            a.gout[o] = ox;
-            a.gout[o + 1] = oy;
-        }
-    };
-    if ((int)blockIdx.x < nbw) {
-        for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < bm.total; k += (int64_t)nbw * blockDim.x) {
-            const int64_t i = band_vertex(bm, k);
-            const int iv = (int)(i / g.nh), ih = (int)(i - (int64_t)iv * g.nh);
-            if (ring_pos(g, iv, ih) >= 0) continue;  // the ring's waves below
-            const double xi = g.x[i], yi = g.y[i];
-            double fi[NV];
-#pragma unroll
-            for (int v = 0; v < NV; ++v) fi[v] = a.f[v * n + i];
-            GradAcc<NV> A;
-            grid_sums(i, iv, ih, xi, yi, fi, A);
-            solve_store(i, A);
-        }
-        return;
-    }
-    const int64_t ra = g.nh - 1, rb = g.nv - 1, L = 2 * ra + 2 * rb;
-    const int lane = threadIdx.x & 63;
-    const int64_t nwave = ((int64_t)(gridDim.x - nbw) * blockDim.x) >> 6;
-    for (int64_t r = (((int64_t)blockIdx.x - nbw) * blockDim.x + threadIdx.x) >> 6; r < L; r += nwave) {
-        int64_t i;
-        if (r < ra) i = r;
-        else if (r < ra + rb) i = (r - ra) * g.nh + (g.nh - 1);
-        else if (r < 2 * ra + rb) i = (int64_t)(g.nv - 1) * g.nh + (g.nh - 1 - (r - ra - rb));
-        else i = (int64_t)(g.nv - 1 - (r - 2 * ra - rb)) * g.nh;
-        const double xi = g.x[i], yi = g.y[i];
-        double fi[NV];
-#pragma unroll
-        for (int v = 0; v < NV; ++v) fi[v] = a.f[v * n + i];
-        GradAcc<NV> A;
-        for (int32_t k = g.xptr[r] + lane; k < g.xptr[r + 1]; k += 64) {
-            const int64_t j = g.xidx[k];
-            double fj[NV], gxj[NV], gyj[NV];
-#pragma unroll
-            for (int v = 0; v < NV; ++v) {
-                fj[v] = a.f[v * n + j];
-                gxj[v] = a.gin ? a.gin[2 * (v * n + j)] : 0.0;
-                gyj[v] = a.gin ? a.gin[2 * (v * n + j) + 1] : 0.0;
-            }
-            edge_vals<NV>(g.x[j], g.y[j], fj, gxj, gyj, xi, yi, fi, A);
-        }
-        for (int off = 32; off > 0; off >>= 1) {
-            A.q0 += __shfl_down(A.q0, off);
-            A.q1 += __shfl_down(A.q1, off);
-            A.q3 += __shfl_down(A.q3, off);
-#pragma unroll
-            for (int v = 0; v < NV; ++v) {
-                A.s0[v] += __shfl_down(A.s0[v], off);
-                A.s1[v] += __shfl_down(A.s1[v], off);
-            }
-        }
-        if (lane == 0) {
-            const int iv = (int)(i / g.nh), ih = (int)(i - (int64_t)iv * g.nh);
-            GradAcc<NV> G;
-            grid_sums(i, iv, ih, xi, yi, fi, G);
-            A.q0 += G.q0;
-            A.q1 += G.q1;
-            A.q3 += G.q3;
-#pragma unroll
-            for (int v = 0; v < NV; ++v) {
-                A.s0[v] += G.s0[v];
-                A.s1[v] += G.s1[v];
-            }
-            solve_store(i, A);
-        }
-    }
-}
-
-template <int NV>
 struct ConePatch {
-    const double* f;           // (NV, n)
+    const double* f;           // (n) one value set
     const int64_t* cells;      // interior target cells (duplicates allowed)
     const int* count;          // how many (device)
     int K;
     ConeStep st[kConeMaxK + 1];  // st[j] for sweep j = 1 .. K
-    double* gout;              // x_K (NV, n, 2): the cells' four corners are written
+    double* gout;              // x_K (n, 2): the cells' four corners are written
     unsigned long long* chg;   // largest change measure of one more sweep at the corners (or nullptr)
-    unsigned long long* clk;   // diagnostics (AKB_GD_PATCH_CLOCK): cycles per phase summed over cells, or nullptr
+    unsigned long long* est;   // largest value-error estimate of a cell (or nullptr; see below)
 };
 
-// one workgroup per interior target cell: the (2K + 4)^2 box around it in LDS, K sweeps on the
-// shrinking square that influences the cell, the corners' x_K to global memory
-template <int NV>
-__global__ void __launch_bounds__(256) k_gd_cone_patch(Grid g, ConePatch<NV> a) {
-    constexpr int B2 = kConeBox * kConeBox;
-    __shared__ double sx[B2], sy[B2], sf[NV][B2];
-    __shared__ double sg[3][NV][B2][2];  // x_{j-2}, x_{j-1}, x_j rotating
-    __shared__ uint8_t sd[B2];
-    const int64_t n = (int64_t)g.nv * g.nh;
-    const int K = a.K, W = 2 * K + 4;
-    for (int pid = blockIdx.x; pid < *a.count; pid += gridDim.x) {
-        const int64_t cell = a.cells[pid];
-        const int iv0 = (int)(cell / (g.nh - 1)), ih0 = (int)(cell - (int64_t)iv0 * (g.nh - 1));
-        const int R0 = iv0 - (K + 1), C0 = ih0 - (K + 1);
-        __syncthreads();  // the previous cell's reads are done
-        for (int idx = threadIdx.x; idx < W * W; idx += blockDim.x) {
-            const int r = idx / W, c = idx - (idx / W) * W;
-            const int64_t i = (int64_t)(R0 + r) * g.nh + (C0 + c);
-            sx[idx] = g.x[i];
-            sy[idx] = g.y[i];
-#pragma unroll
-            for (int v = 0; v < NV; ++v) sf[v][idx] = a.f[v * n + i];
-            sd[idx] = (r < W - 1 && c < W - 1) ? g.diag[(int64_t)(R0 + r) * (g.nh - 1) + (C0 + c)] : 0;
-        }
-        __syncthreads();
-        // the sums of box vertex b from iterate buffer `in` (nullptr role: x_0 = 0)
-        auto sums = [&](int b, int in) {
-            GradAcc<NV> A;
-            double fi[NV];
-#pragma unroll
-            for (int v = 0; v < NV; ++v) fi[v] = sf[v][b];
-            const double xi = sx[b], yi = sy[b];
-            auto edge = [&](int j) {
-                double fj[NV], gxj[NV], gyj[NV];
-#pragma unroll
-                for (int v = 0; v < NV; ++v) {
-                    fj[v] = sf[v][j];
-                    gxj[v] = in < 0 ? 0.0 : sg[in][v][j][0];
-                    gyj[v] = in < 0 ? 0.0 : sg[in][v][j][1];
-                }
-                edge_vals<NV>(sx[j], sy[j], fj, gxj, gyj, xi, yi, fi, A);
-            };
-            // k_gd_grad's order: left, right, down (iv - 1), up (iv + 1), then the diagonals
-            edge(b - 1);
-            edge(b + 1);
-            edge(b - W);
-            edge(b + W);
-            if (sd[b - W - 1] == 0) edge(b - W - 1);
-            if (sd[b - W] == 1) edge(b - W + 1);
-            if (sd[b - 1] == 1) edge(b + W - 1);
-            if (sd[b] == 0) edge(b + W + 1);
-            return A;
-        };
-        for (int j = 1; j <= K; ++j) {
-            const int half = K + 1 - j, side = 2 * half + 2, off = (K + 1) - half;
-            const int in = j == 1 ? -1 : (j - 1) % 3, out = j % 3, prev = (j + 1) % 3;  // x_{j-1}, x_j, x_{j-2}
-            const ConeStep st = a.st[j];
-            for (int idx = threadIdx.x; idx < side * side; idx += blockDim.x) {
-                const int b = (off + idx / side) * W + off + (idx - (idx / side) * side);
-                const GradAcc<NV> A = sums(b, in);
-#pragma unroll
-                for (int v = 0; v < NV; ++v) {
-                    const double gix = in < 0 ? 0.0 : sg[in][v][b][0], giy = in < 0 ? 0.0 : sg[in][v][b][1];
-                    const double px = st.mode == 2 ? sg[prev][v][b][0] : 0.0;
-                    const double py = st.mode == 2 ? sg[prev][v][b][1] : 0.0;
-                    double ox, oy;
-                    solve_vals<NV>(A, v, gix, giy, st, px, py, ox, oy);
-                    sg[out][v][b][0] = ox;
-                    sg[out][v][b][1] = oy;
-                }
-            }
-            __syncthreads();
-        }
-        // the cell's corners: x_K out, and the change one more (plain-measured) sweep would make
-        double worst = 0.0;
-        if (threadIdx.x < 4) {
-            const int cr = K + 1 + (threadIdx.x >> 1), cc = K + 1 + (threadIdx.x & 1);
-            const int b = cr * W + cc, fin = K % 3;
-            const int64_t i = (int64_t)(R0 + cr) * g.nh + (C0 + cc);
-            const GradAcc<NV> A = sums(b, fin);
-#pragma unroll
-            for (int v = 0; v < NV; ++v) {
-                const double gx = sg[fin][v][b][0], gy = sg[fin][v][b][1];
-                a.gout[2 * (v * n + i)] = gx;
-                a.gout[2 * (v * n + i) + 1] = gy;
-                double ox, oy;
-                worst = fmax(worst, solve_vals<NV>(A, v, gx, gy, ConeStep{0, 1.0}, 0.0, 0.0, ox, oy));
-            }
-        }
-        if (a.chg && threadIdx.x < 64) {
-            for (int off = 2; off > 0; off >>= 1) worst = fmax(worst, __shfl_down(worst, off));
-            if (threadIdx.x == 0 && worst > 0) atomicMax(a.chg, (unsigned long long)__double_as_longlong(worst));
-        }
-    }
-}
-
-// k_gd_cone_patch with one thread per box vertex (one value set): the edge geometry of a vertex -
-// (ex, ey), r^-3 and 6 (f_i - f_j) per edge, the local 2 x 2 system and its reciprocal
-// determinant - does not change between sweeps, so each thread forms its own once per cell, in
-// k_gd_grad's expressions and edge order, and keeps it in registers; a sweep then costs per edge
-// one LDS read of the neighbour's iterate and nine operations (against the full edge_vals: a
-// reciprocal square root and ~25 operations, five LDS reads). The box has pitch 32; threads take
-// its vertices in order of depth; x_j overwrites x_{j-2} in place (a vertex reads its own predecessor only),
-// so two iterate buffers suffice. The arithmetic is edge_vals / solve_vals' exactly: x_K at the
-// corners equals k_gd_cone_patch's, bit for bit.
-template <bool PF, bool CLK>
-__global__ void __launch_bounds__(1024) k_gd_cone_patch1(Grid g, ConePatch<1> a, int rowmajor) {
-    constexpr int P = 33;  // LDS pitch: a column of the box steps 2 banks per row, not 0
-    static_assert(kConeBox < P, "box pitch");
-    __shared__ double sxyf[2][3][P * 32];  // x, y, f of the box; two sets (PF: the next cell's DMA)
-    __shared__ double2 sg[2][P * 32];
-    __shared__ uint8_t sd[P * 32];
-    const int K = a.K, W = 2 * K + 4;
-    const int t = threadIdx.x;
-    // this thread's vertex, in order of depth from the box's centre outwards: vertex (r, c) of depth
-    // d = min(r, c, W-1-r, W-1-c) takes part in sweeps 1 .. d, so sweep j's vertices are a prefix of
-    // the threads - its waves are full, the rest idle (row-major lanes would run each sweep's
-    // shrinking square at ~half occupancy). The four innermost are the cell's corners.
-    int r = -1, c = -1, dep = 0;
-    if (rowmajor) {  // A/B: lanes along the box's rows
-        r = t / 32;
-        c = t - (t / 32) * 32;
-        dep = (r < W && c < W) ? min(min(r, c), min(W - 1 - r, W - 1 - c)) : 0;
-        if (dep > K + 1) dep = K + 1;
-    } else {
-        int rem = t;
-        for (int d = W / 2 - 1; d >= 1; --d) {
-            const int s1 = W - 2 * d - 1, cnt = 4 * s1;
-            if (rem < cnt) {
-                if (rem < s1) { r = d; c = d + rem; }
-                else if (rem < 2 * s1) { r = d + (rem - s1); c = d + s1; }
-                else if (rem < 3 * s1) { r = d + s1; c = d + s1 - (rem - 2 * s1); }
-                else { r = d + s1 - (rem - 3 * s1); c = d; }
-                dep = d;
-                break;
-            }
-            rem -= cnt;
-        }
-    }
-    const bool mine = dep >= 1;
-    const int b = mine ? r * P + c : 0;
-    // the box load. PF: one persistent workgroup walks its cells; x, y, f of the next cell go
-    // global -> LDS by DMA (global_load_lds, no registers) into the other set while this cell's
-    // sweeps run - one wave instruction per box row and array, lane i moving dword i of the row.
-    // The diagonal bytes go through a register (one per thread, row-major). Else everything
-    // through registers, row-major (coalesced), at the top of the cell.
-    const int count = *a.count;
-    const double* const gx_ = g.x;
-    const double* const gy_ = g.y;
-    const double* const gf_ = a.f;
-    const uint8_t* const gd_ = g.diag;
-    const int nh = g.nh;
-    const int wv = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63;
-    const int lr = t / 32, lc = t - (t / 32) * 32;
-    // the next cell's box: the diagonal byte into a register, then x, y, f by DMA (issued after every
-    // load the wave waits on, so no wait before the next cell's top lands on them)
-    auto prefetch = [=](int pid, int st, uint8_t& d) {
-        if (pid >= count) return;
-        const int64_t cell = a.cells[pid];
-        const int iv0 = (int)(cell / (nh - 1)), ih0 = (int)(cell - (int64_t)iv0 * (nh - 1));
-        const int R0 = iv0 - (K + 1), C0 = ih0 - (K + 1);
-        if (lr < W - 1 && lc < W - 1) d = gd_[(int64_t)(R0 + lr) * (nh - 1) + (C0 + lc)];
-#pragma unroll
-        for (int arr = 0; arr < 3; ++arr) {
-            const double* base = arr == 0 ? gx_ : arr == 1 ? gy_ : gf_;
-            for (int row = wv; row < W; row += 16) {
-                const double* src = base + (int64_t)(R0 + row) * nh + C0;
-                if (lane < 2 * W)
-                    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) const char*)src + lane * 4,
-                                                     (__attribute__((address_space(3))) void*)&sxyf[st][arr][row * P],
-                                                     4, 0, 0);
-            }
-        }
-    };
-    uint8_t pd = 0;
-    if (PF) prefetch(blockIdx.x, 0, pd);
-    double cmax = 0.0;  // the corners' change measure over this workgroup's cells: one atomic at the end
-    int set = 0;
-    for (int pid = blockIdx.x; pid < count; pid += gridDim.x, set ^= (PF ? 1 : 0)) {
-        const int64_t cell = a.cells[pid];
-        const int iv0 = (int)(cell / (g.nh - 1)), ih0 = (int)(cell - (int64_t)iv0 * (g.nh - 1));
-        const int R0 = iv0 - (K + 1), C0 = ih0 - (K + 1);
-        const unsigned long long c0 = CLK ? clock64() : 0;
-        double* const sx = sxyf[set][0];
-        double* const sy = sxyf[set][1];
-        double* const sf = sxyf[set][2];
-        {
-            double nx_ = 0.0, ny_ = 0.0, nf_ = 0.0;
-            uint8_t nd_ = pd;
-            if (!PF && lr < W && lc < W) {
-                const int64_t i = (int64_t)(R0 + lr) * nh + (C0 + lc);
-                nx_ = gx_[i];
-                ny_ = gy_[i];
-                nf_ = gf_[i];
-                nd_ = (lr < W - 1 && lc < W - 1) ? gd_[(int64_t)(R0 + lr) * (nh - 1) + (C0 + lc)] : 0;
-            }
-            if (PF) __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA rows have landed (vmcnt)
-            __syncthreads();  // the previous cell's reads are done; PF: every wave's DMA has landed
-            if (lr < W && lc < W) {
-                const int q = lr * P + lc;
-                if (!PF) {
-                    sx[q] = nx_;
-                    sy[q] = ny_;
-                    sf[q] = nf_;
-                }
-                sd[q] = nd_;
-            }
-        }
-        __syncthreads();
-        const unsigned long long c1 = CLK ? clock64() : 0;
-        if (PF) {
-            pd = 0;
-            prefetch(pid + gridDim.x, set ^ 1, pd);
-        }
-        // this vertex's edges in k_gd_grad's order: left, right, down, up, then the diagonals
-        int nb[8];
-        unsigned em = 0;
-        double ex[8], ey[8], r3[8], c6[8];
-        double q0 = 0.0, q1 = 0.0, q3 = 0.0, inv = 0.0;
-        if (mine) {
-            nb[0] = b - 1;
-            nb[1] = b + 1;
-            nb[2] = b - P;
-            nb[3] = b + P;
-            nb[4] = b - P - 1;
-            nb[5] = b - P + 1;
-            nb[6] = b + P - 1;
-            nb[7] = b + P + 1;
-            em = 0x0fu | (sd[b - P - 1] == 0 ? 0x10u : 0u) | (sd[b - P] == 1 ? 0x20u : 0u) |
-                 (sd[b - 1] == 1 ? 0x40u : 0u) | (sd[b] == 0 ? 0x80u : 0u);
-            const double xi = sx[b], yi = sy[b], fi = sf[b];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                ex[k] = ey[k] = r3[k] = c6[k] = 0.0;
-                if (!(em & (1u << k))) continue;
-                const int j = nb[k];
-                const double exk = sx[j] - xi, eyk = sy[j] - yi;
-                const double l2 = exk * exk + eyk * eyk;
-                double rr = __builtin_amdgcn_rsq(l2);
-                rr = rr * __builtin_fma(-0.5 * l2 * rr, rr, 1.5);
-                const double r3k = rr * rr * rr;
-                const double wx = exk * r3k, wy = eyk * r3k;
-                q0 = __builtin_fma(exk, wx, q0);
-                q1 = __builtin_fma(exk, wy, q1);
-                q3 = __builtin_fma(eyk, wy, q3);
-                ex[k] = exk;
-                ey[k] = eyk;
-                r3[k] = r3k;
-                c6[k] = 6 * (fi - sf[j]);
-            }
-            q0 = 4 * q0;
-            q1 = 4 * q1;
-            q3 = 4 * q3;
-            inv = 1.0 / (q0 * q3 - q1 * q1);
-        }
-        if (CLK) __syncthreads();
-        const unsigned long long c2 = CLK ? clock64() : 0;
-        // the sums of one sweep from iterate buffer `in` (in < 0: x_0 = 0), solve_vals' solve
-        auto sweep_r = [&](int in, double& r0, double& r1) {
-            double s0 = 0.0, s1 = 0.0;
-            // (one exposed LDS latency per edge; issuing all eight reads first and selecting the
-            // missing diagonals away measured slower: the work of the missing edges and the
-            // register pressure cost more than the latency)
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                if (!(em & (1u << k))) continue;
-                double gxj = 0.0, gyj = 0.0;
-                if (in >= 0) {
-                    const double2 gj = sg[in][nb[k]];
-                    gxj = gj.x;
-                    gyj = gj.y;
-                }
-                const double df2 = -ex[k] * gxj - ey[k] * gyj;
-                const double w = c6[k] - 2 * df2;
-                const double wx = ex[k] * r3[k], wy = ey[k] * r3[k];
-                s0 = __builtin_fma(w, wx, s0);
-                s1 = __builtin_fma(w, wy, s1);
-            }
-            r0 = (q3 * s0 - q1 * s1) * inv;
-            r1 = (-q1 * s0 + q0 * s1) * inv;
-        };
-        for (int j = 1; j <= K; ++j) {
-            if (dep >= j) {  // the square [j, W - 1 - j]^2 (depth >= j)
-                const int in = j == 1 ? -1 : ((j - 1) & 1), out = j & 1;
-                const ConeStep st = a.st[j];
-                double r0, r1;
-                sweep_r(in, r0, r1);
-                double ox, oy;
-                if (st.mode == 2) {
-                    const double2 pv = sg[out][b];  // x_{j-2}, overwritten below
-                    ox = st.omega * (-r0 - pv.x) + pv.x;
-                    oy = st.omega * (-r1 - pv.y) + pv.y;
-                } else if (st.mode == 1) {
-                    ox = st.omega * (-r0 - 0.0) + 0.0;
-                    oy = st.omega * (-r1 - 0.0) + 0.0;
-                } else {
-                    ox = -r0;
-                    oy = -r1;
-                }
-                sg[out][b] = make_double2(ox, oy);
-            }
-            __syncthreads();  // (the first also waits for the next box's DMA: it had setup + sweep 1 to land)
-        }
-        const unsigned long long c3 = CLK ? clock64() : 0;
-        // the cell's corners (the innermost ring): x_K out, and the change one more (plain-measured)
-        // sweep would make
-        if (dep == K + 1) {
-            const int fin = K & 1;
-            const double2 gk = sg[fin][b];
-            const int64_t i = (int64_t)(R0 + r) * g.nh + (C0 + c);
-            a.gout[2 * i] = gk.x;
-            a.gout[2 * i + 1] = gk.y;
-            if (a.chg) {
-                double r0, r1;
-                sweep_r(fin, r0, r1);
-                const double cm = fmax(fabs(gk.x + r0), fabs(gk.y + r1)) / fmax(1.0, fmax(fabs(r0), fabs(r1)));
-                cmax = fmax(cmax, cm);
-            }
-        }
-        if (CLK && t == 0) {
-            atomicAdd(a.clk, c1 - c0);
-            atomicAdd(a.clk + 1, c2 - c1);
-            atomicAdd(a.clk + 2, c3 - c2);
-            atomicAdd(a.clk + 3, clock64() - c3);
-            atomicAdd(a.clk + 4, 1ull);
-        }
-    }
-    if (a.chg && dep == K + 1 && cmax > 0) atomicMax(a.chg, (unsigned long long)__double_as_longlong(cmax));
-}
-
-// vertex `idx` of the box in order of depth from the centre outwards (k_gd_cone_patch1's order):
-// (r, c) and its depth d = min(r, c, W-1-r, W-1-c); indices [0, (W - 2j)^2) are the vertices of
-// depth >= j. dep = 0 past the last (depth-1) vertex.
+// vertex `idx` of the box in order of depth from the centre outwards: (r, c) and its depth d =
+// min(r, c, W-1-r, W-1-c); indices [0, (W - 2j)^2) are the vertices of depth >= j. dep = 0 past the
+// last (depth-1) vertex.
 __device__ __forceinline__ void depth_order(int W, int idx, int& r, int& c, int& dep) {
     r = -1;
     c = -1;
@@ -2024,29 +1155,49 @@ __device__ __forceinline__ void depth_order(int W, int idx, int& r, int& c, int&
     }
 }
 
-// k_gd_cone_patch1 as a two-stage pipeline over the workgroup's cells: threads [0, N1) hold the
-// (W-2)^2 vertices of depth >= 1 of cell p and run its sweeps 1 .. S, while threads [N1, N1 + N2)
-// hold the N2 = (W - 2S - 2)^2 vertices of depth >= S + 1 of cell p - 1 and run its sweeps
-// S + 1 .. K and its corners' output - the late sweeps, a few waves each, no longer run alone.
-// Each stage's threads compute their vertex's edge constants from that cell's box; box sets rotate
-// over three (stage 1, stage 2, the next cell's DMA) and iterate buffer pairs over two (stage 2
-// reads x_S, x_{S-1} where stage 1 left them). Per vertex the arithmetic is k_gd_cone_patch1's:
-// the same bits. The host picks S (the smallest >= K/2 with N1 + N2 <= 1024).
-template <bool CLK, bool RPF>
-__global__ void __launch_bounds__(1024) k_gd_cone_patch2(Grid g, ConePatch<1> a, int S) {
+// The interior target cells' patches: one persistent 1024-thread workgroup per CU walks its cells
+// as a two-stage pipeline. A thread holds one box vertex (the box has pitch 33 in LDS, conflict-free
+// along a column): threads [0, N1) the (W-2)^2 vertices of depth >= 1 of cell p, running its sweeps
+// 1 .. S, threads [N1a, N1a + N2) (N1a: N1 rounded up to a whole wave) the N2 = (W - 2S - 2)^2
+// vertices of depth >= S + 1 of cell p - 1,
+// running its sweeps S + 1 .. K and its corners' output, so the late sweeps (a few waves each) no
+// longer run alone. Vertices are taken in order of depth, so a sweep's shrinking square is a prefix
+// of a stage's threads and fills whole waves. Each thread forms its vertex's constants once per
+// cell - the eight edge slots' M (zero for an absent diagonal) and c, P - so a sweep costs eight
+// LDS reads and 4 FMAs per slot plus the 2 x 2 product and the Chebyshev step. Box sets of x, y, f
+// rotate over three (stage 1, stage 2, the next cell's, loaded through registers during the sweeps
+// and written after them) and iterate pairs over two (stage 2 reads x_S, x_{S-1} where stage 1 left
+// them). The host picks S (the smallest >= K/2 with N1a + N2 <= 1020: threads 1020..1023 store the
+// corners).
+//
+// At the corners (x_K) the kernel also forms the change one more plain sweep would make - scipy's
+// measure (chg) - and a value-error estimate: with the Jacobi spectrum in [-1/2, 1/2] the distance
+// of x_K from the fixed point is at most ~2x the step |y - x_K|, and a Clough-Tocher value moves
+// by at most |dg| x the longest edge it integrates over, so est = 2 sqrt2 max|y - x_K| x the cell's
+// longest side or diagonal (in the map's units; FaithfulPupil checks it against the map's range).
+__device__ __forceinline__ double cell_est(const double (&so)[4][6]) {
+    const double d = fmax(fmax(so[0][4], so[1][4]), fmax(so[2][4], so[3][4]));
+    const double h = fmax(fmax(so[0][5], so[1][5]), fmax(so[2][5], so[3][5]));
+    return 2.0 * 1.4142135623730951 * d * h;
+}
+
+__global__ void __launch_bounds__(1024) k_gd_cone_patch(Grid g, ConePatch a, int S) {
     constexpr int P = 33;
+    static_assert(kConeBox < P, "box pitch");
     __shared__ double sxyf[3][3][P * 32];
     __shared__ double2 sg[2][2][P * 32];
     __shared__ uint8_t sd[3][P * 32];
     __shared__ int2 scell[1024];            // this workgroup's cells' box origins (R0, C0), read once
-    __shared__ double sout[4][4];           // stage 2's corner results, stored one step later
+    __shared__ double sout[4][6];           // stage 2's corner results, stored one step later
     const int K = a.K, W = 2 * K + 4;
     const int t = threadIdx.x;
-    const int N1 = (W - 2) * (W - 2), N2 = (W - 2 * S - 2) * (W - 2 * S - 2);
-    const int role = t < N1 ? 1 : (t < N1 + N2 ? 2 : 0);
+    // stage 2 starts at a wave boundary, so a wave's stage - and with it the sweep it runs - is
+    // uniform: the sweep's weight is a scalar load
+    const int N1 = (W - 2) * (W - 2), N1a = (N1 + 63) & ~63, N2 = (W - 2 * S - 2) * (W - 2 * S - 2);
+    const int role = __builtin_amdgcn_readfirstlane(t < N1a ? 1 : 2);
     int r, c, dep;
-    depth_order(W, role == 1 ? t : t - N1, r, c, dep);
-    if (role == 0) dep = 0;
+    depth_order(W, role == 1 ? t : t - N1a, r, c, dep);
+    if ((role == 1 && t >= N1) || (role == 2 && t - N1a >= N2)) dep = 0;
     const int b = dep >= 1 ? r * P + c : 0;
     const int Q = max(S, K - S);
     const int count = *a.count;
@@ -2057,72 +1208,34 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch2(Grid g, ConePatch<1> a,
     const uint8_t* const gd_ = g.diag;
     const int nh = g.nh;
     // the cell list into LDS first (the host keeps it <= 1024 cells per workgroup), so no wait on a
-    // global load sits between a step's barrier and its DMA / setup
+    // global load sits between a step's barrier and its setup
     for (int i = t; i < my; i += 1024) {
         const int64_t cell = a.cells[blockIdx.x + (int64_t)i * gridDim.x];
         const int iv0 = (int)(cell / (nh - 1)), ih0 = (int)(cell - (int64_t)iv0 * (nh - 1));
         scell[i] = make_int2(iv0 - (K + 1), ih0 - (K + 1));
     }
     __syncthreads();
-    const int wv = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63;
     const int lr = t / 32, lc = t - (t / 32) * 32;
-    // cell i's box: diagonal bytes into a register, x, y, f by DMA into box set st (k_gd_cone_patch1).
-    // (The DMA issued at a step's start lands ~10k cycles after that step's sweeps have ended - its
-    // LDS writes seem to queue behind the sweeps' traffic - yet it beats loading the next box
-    // through registers on spare waves during the sweeps: 1.05 ms vs 0.47 ms, each global load's
-    // latency then sits inside a sweep.)
-    auto prefetch = [&](int i, int st, uint8_t& d) {
-        const int2 o = scell[i];
-        const int R0 = o.x, C0 = o.y;
-        if (lr < W - 1 && lc < W - 1) d = gd_[(int64_t)(R0 + lr) * (nh - 1) + (C0 + lc)];
-#pragma unroll
-        for (int arr = 0; arr < 3; ++arr) {
-            const double* base = arr == 0 ? gx_ : arr == 1 ? gy_ : gf_;
-            for (int row = wv; row < W; row += 16) {
-                const double* src = base + (int64_t)(R0 + row) * nh + C0;
-                if (lane < 2 * W)
-                    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) const char*)src + lane * 4,
-                                                     (__attribute__((address_space(3))) void*)&sxyf[st][arr][row * P],
-                                                     4, 0, 0);
-            }
-        }
-    };
+    // cell 0's box through registers (every later box loads during the step before it)
     uint8_t pd = 0;
-    if (my > 0) prefetch(0, 0, pd);
-    // the change measure's running max over this workgroup's cells (threads 0..3), one atomic at the
-    // end: an atomicMax per cell on the one address queued at L2 behind every other workgroup's and
-    // held each step's top (its vmcnt wait) for ~10k cycles
-    double cmax = 0.0;
+    if (my > 0 && lr < W && lc < W) {
+        const int2 o = scell[0];
+        const int64_t q = (int64_t)(o.x + lr) * nh + (o.y + lc);
+        sxyf[0][0][lr * P + lc] = gx_[q];
+        sxyf[0][1][lr * P + lc] = gy_[q];
+        sxyf[0][2][lr * P + lc] = gf_[q];
+        if (lr < W - 1 && lc < W - 1) pd = gd_[(int64_t)(o.x + lr) * (nh - 1) + (o.y + lc)];
+    }
+    // the corners' running maxima over this workgroup's cells (threads 1020 .. 1023), one atomic each
+    // at the end
+    double cmax = 0.0, emax = 0.0;
+    constexpr int off[8] = {-1, 1, -P, P, -P - 1, -P + 1, P - 1, P + 1};
     for (int p = 0; p <= my; ++p) {
         const int s1 = p % 3, s2 = (p + 2) % 3;  // box sets of cell p (stage 1) and cell p - 1 (stage 2)
-        const unsigned long long c0 = CLK ? clock64() : 0;
         if (p < my && lr < W && lc < W) sd[s1][lr * P + lc] = pd;
-        if (!RPF || p == 0) __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA rows of cell p have landed
-        const unsigned long long c0b = CLK ? clock64() : 0;
-        if (RPF) {
-            // cell p's box came through registers to LDS last step: an LDS-only barrier, so no wave
-            // waits here for the acks of its earlier global stores (__syncthreads' fence would)
-            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        } else {
-            __syncthreads();  // every wave's DMA has landed; the previous step's reads are done
-        }
-        const unsigned long long c1 = CLK ? clock64() : 0;
-        double rx_ = 0.0, ry_ = 0.0, rf_ = 0.0;  // RPF: cell p + 1's box point through registers
-        if (p + 1 < my) {
-            pd = 0;
-            if (RPF) {
-                const int2 o = scell[p + 1];
-                if (lr < W && lc < W) {
-                    const int64_t q = (int64_t)(o.x + lr) * nh + (o.y + lc);
-                    rx_ = gx_[q];
-                    ry_ = gy_[q];
-                    rf_ = gf_[q];
-                    if (lr < W - 1 && lc < W - 1) pd = gd_[(int64_t)(o.x + lr) * (nh - 1) + (o.y + lc)];
-                }
-            } else {
-                prefetch(p + 1, (p + 1) % 3, pd);
-            }
-        }
+        // cell p's box came through registers to LDS last step: an LDS-only barrier, so no wave waits
+        // here for the acks of its earlier global stores (__syncthreads' fence would)
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         if (p < my && lr < W && lc < W) sg[p & 1][0][lr * P + lc] = make_double2(0.0, 0.0);  // x_0
         if (p >= 2 && t >= 1020) {  // cell p - 2's corners, left by the last step's stage 2 (stored by
             const int q = t - 1020;    // the last wave: no box loads of its own for K <= 13)
@@ -2130,6 +1243,7 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch2(Grid g, ConePatch<1> a,
             a.gout[2 * i] = sout[q][0];
             a.gout[2 * i + 1] = sout[q][1];
             cmax = fmax(cmax, sout[q][3]);
+            emax = fmax(emax, cell_est(sout));
         }
         const bool act = dep >= 1 && (role == 1 ? p < my : p >= 1);
         const int bs = role == 1 ? s1 : s2;
@@ -2138,118 +1252,103 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch2(Grid g, ConePatch<1> a,
         const double* const sy = sxyf[bs][1];
         const double* const sf = sxyf[bs][2];
         const uint8_t* const sdd = sd[bs];
-        int nb[8];
-        unsigned em = 0;
-        double ex[8], ey[8], r3[8], c6[8];
-        double q0 = 0.0, q1 = 0.0, q3 = 0.0, inv = 0.0;
+        // this vertex's constants: the eight slots' M in the edge order, c and P
+        double mxx[8], mxy[8], myy[8];
+        VConst kc{0.0, 0.0, 0.0, 0.0, 0.0};
         if (act) {
-            nb[0] = b - 1;
-            nb[1] = b + 1;
-            nb[2] = b - P;
-            nb[3] = b + P;
-            nb[4] = b - P - 1;
-            nb[5] = b - P + 1;
-            nb[6] = b + P - 1;
-            nb[7] = b + P + 1;
-            em = 0x0fu | (sdd[b - P - 1] == 0 ? 0x10u : 0u) | (sdd[b - P] == 1 ? 0x20u : 0u) |
-                 (sdd[b - 1] == 1 ? 0x40u : 0u) | (sdd[b] == 0 ? 0x80u : 0u);
-            const double xi = sx[b], yi = sy[b], fi = sf[b];
+            const unsigned em = 0x0fu | (sdd[b - P - 1] == 0 ? 0x10u : 0u) | (sdd[b - P] == 1 ? 0x20u : 0u) |
+                                (sdd[b - 1] == 1 ? 0x40u : 0u) | (sdd[b] == 0 ? 0x80u : 0u);
+            const double xi = sx[b], yi = sy[b];
+            const double fi[1] = {sf[b]}, zero[1] = {0.0};
+            GradAcc<1> A;
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
-                ex[k] = ey[k] = r3[k] = c6[k] = 0.0;
+                mxx[k] = mxy[k] = myy[k] = 0.0;
                 if (!(em & (1u << k))) continue;
-                const int j = nb[k];
-                const double exk = sx[j] - xi, eyk = sy[j] - yi;
-                const double l2 = exk * exk + eyk * eyk;
-                double rr = __builtin_amdgcn_rsq(l2);
-                rr = rr * __builtin_fma(-0.5 * l2 * rr, rr, 1.5);
-                const double r3k = rr * rr * rr;
-                const double wx = exk * r3k, wy = eyk * r3k;
-                q0 = __builtin_fma(exk, wx, q0);
-                q1 = __builtin_fma(exk, wy, q1);
-                q3 = __builtin_fma(eyk, wy, q3);
-                ex[k] = exk;
-                ey[k] = eyk;
-                r3[k] = r3k;
-                c6[k] = 6 * (fi - sf[j]);
+                const int j = b + off[k];
+                const EdgeG e = edge_geom(sx[j] - xi, sy[j] - yi);
+                const double fj[1] = {sf[j]};
+                acc_edge<1>(A, e, fi, fj, zero, zero);  // (its S part is not used: the sweeps form S)
+                mxx[k] = e.mxx;
+                mxy[k] = e.mxy;
+                myy[k] = e.myy;
             }
-            q0 = 4 * q0;
-            q1 = 4 * q1;
-            q3 = 4 * q3;
-            inv = 1.0 / (q0 * q3 - q1 * q1);
+            kc = vertex_consts<1>(A, 0);
         }
-        if (RPF && p + 1 < my && lr < W && lc < W) {  // after setup: its latency was the setup's time
-            const int q = lr * P + lc, st = (p + 1) % 3;
-            sxyf[st][0][q] = rx_;
-            sxyf[st][1][q] = ry_;
-            sxyf[st][2][q] = rf_;
+        // cell p + 1's box point through registers: issued after the setup (whose temporaries then
+        // are dead), written to LDS after the sweeps, which hide its latency
+        double rx_ = 0.0, ry_ = 0.0, rf_ = 0.0;
+        if (p + 1 < my) {
+            pd = 0;
+            const int2 o = scell[p + 1];
+            if (lr < W && lc < W) {
+                const int64_t q = (int64_t)(o.x + lr) * nh + (o.y + lc);
+                rx_ = gx_[q];
+                ry_ = gy_[q];
+                rf_ = gf_[q];
+                if (lr < W - 1 && lc < W - 1) pd = gd_[(int64_t)(o.x + lr) * (nh - 1) + (o.y + lc)];
+            }
         }
-        // x_0 in place for sweep 1 (LDS only: the next box's DMA stays in flight)
+        // x_0 in place for sweep 1
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        const unsigned long long c2 = CLK ? clock64() : 0;
-        // the sums of one sweep from iterate buffer `in` (sweep 1 reads x_0 = 0 from buffer 0, zeroed
-        // at the step's top), solve_vals' solve; the buffer's row base is formed once per sweep, so
-        // each edge's read is one LDS instruction with a constant offset
-        auto sweep_r = [&](int in, double& r0, double& r1) {
-            constexpr int off[8] = {-1, 1, -P, P, -P - 1, -P + 1, P - 1, P + 1};
-            double s0 = 0.0, s1 = 0.0;
+        // S of one sweep from iterate buffer `in` (sweep 1 reads x_0 = 0 from buffer 0, zeroed at the
+        // step's top) and the Jacobi step's y; the buffer's row base is formed once per sweep, so each
+        // slot's read is one LDS instruction with a constant offset
+        auto sweep_y = [&](int in, double& y0, double& y1) {
+            double s0 = 0.0, s1 = 0.0, d0 = 0.0, d1 = 0.0;  // the axis and the diagonal chains
             const double2* const gi = gg[in] + b;
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
-                if (!(em & (1u << k))) continue;
                 const double2 gj = gi[off[k]];
-                const double df2 = -ex[k] * gj.x - ey[k] * gj.y;
-                const double w = c6[k] - 2 * df2;
-                const double wx = ex[k] * r3[k], wy = ey[k] * r3[k];
-                s0 = __builtin_fma(w, wx, s0);
-                s1 = __builtin_fma(w, wy, s1);
+                double& t0 = k < 4 ? s0 : d0;
+                double& t1 = k < 4 ? s1 : d1;
+                t0 = __builtin_fma(mxy[k], gj.y, __builtin_fma(mxx[k], gj.x, t0));
+                t1 = __builtin_fma(myy[k], gj.y, __builtin_fma(mxy[k], gj.x, t1));
             }
-            r0 = (q3 * s0 - q1 * s1) * inv;
-            r1 = (-q1 * s0 + q0 * s1) * inv;
+            jacobi_y(kc, s0 + d0, s1 + d1, y0, y1);
         };
         for (int q = 1; q <= Q; ++q) {
             const int j = role == 1 ? q : S + q;
             if (act && dep >= j && (role == 1 ? q <= S : j <= K)) {
                 const int in = (j - 1) & 1, out = j & 1;
                 const ConeStep st = a.st[j];
-                double r0, r1;
-                sweep_r(in, r0, r1);
-                double ox, oy;
-                if (st.mode == 2) {
-                    const double2 pv = gg[out][b];  // x_{j-2}, overwritten below
-                    ox = st.omega * (-r0 - pv.x) + pv.x;
-                    oy = st.omega * (-r1 - pv.y) + pv.y;
-                } else if (st.mode == 1) {
-                    ox = st.omega * (-r0 - 0.0) + 0.0;
-                    oy = st.omega * (-r1 - 0.0) + 0.0;
-                } else {
-                    ox = -r0;
-                    oy = -r1;
-                }
-                gg[out][b] = make_double2(ox, oy);
+                double y0, y1;
+                sweep_y(in, y0, y1);
+                const double2 pv = st.mode == 2 ? gg[out][b] : make_double2(0.0, 0.0);  // x_{j-2}, overwritten
+                gg[out][b] = make_double2(cheb(st, y0, pv.x), cheb(st, y1, pv.y));
             }
-            // LDS-only barrier: __syncthreads' fence would also wait (vmcnt) for the next box's DMA
             asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         }
-        const unsigned long long c3 = CLK ? clock64() : 0;
-        // cell p - 1's corners (stage 2's innermost ring): x_K and the change of one more sweep, into
-        // LDS; threads 0..3 store them after the next step's barrier (or below, after the last step),
-        // so the stores' latency is not waited for at the next step's top
+        // cell p - 1's corners (stage 2's innermost ring): x_K, the change of one more plain sweep and
+        // the value-error estimate, into LDS; the last wave stores them after the next step's
+        // barrier (or below, after the last step), so the stores' latency is not waited for at the
+        // next step's top
         if (role == 2 && act && dep == K + 1) {
             const int2 o = scell[p - 1];
             const int fin = K & 1;
             const double2 gk = gg[fin][b];
-            double cm = 0.0;
-            if (a.chg) {
-                double r0, r1;
-                sweep_r(fin, r0, r1);
-                cm = fmax(fabs(gk.x + r0), fabs(gk.y + r1)) / fmax(1.0, fmax(fabs(r0), fabs(r1)));
-            }
-            const int q = t - N1;  // the innermost ring: stage 2's first four threads
+            double y0, y1;
+            sweep_y(fin, y0, y1);
+            // the cell's sides and diagonal at this corner (the corners are (K+1 .. K+2)^2 of the box)
+            const int dr = r == K + 1 ? P : -P, dc = c == K + 1 ? 1 : -1;
+            const double x0 = sx[b], y0c = sy[b];
+            const double h2 = fmax(fmax((sx[b + dr] - x0) * (sx[b + dr] - x0) + (sy[b + dr] - y0c) * (sy[b + dr] - y0c),
+                                        (sx[b + dc] - x0) * (sx[b + dc] - x0) + (sy[b + dc] - y0c) * (sy[b + dc] - y0c)),
+                                   (sx[b + dr + dc] - x0) * (sx[b + dr + dc] - x0) +
+                                       (sy[b + dr + dc] - y0c) * (sy[b + dr + dc] - y0c));
+            const int q = t - N1a;  // the innermost ring: stage 2's first four threads
             sout[q][0] = gk.x;
             sout[q][1] = gk.y;
             sout[q][2] = (double)((int64_t)(o.x + r) * nh + (o.y + c));
-            sout[q][3] = cm;
+            sout[q][3] = a.chg ? change_of(gk.x, gk.y, y0, y1) : 0.0;
+            sout[q][4] = fmax(fabs(gk.x - y0), fabs(gk.y - y1));
+            sout[q][5] = sqrt(h2);
+        }
+        if (p + 1 < my && lr < W && lc < W) {  // set (p + 1) % 3 is read from the next step on
+            const int q = lr * P + lc, st = (p + 1) % 3;
+            sxyf[st][0][q] = rx_;
+            sxyf[st][1][q] = ry_;
+            sxyf[st][2][q] = rf_;
         }
         if (p == my && my >= 1) {  // the last cell's corners
             __syncthreads();
@@ -2259,18 +1358,14 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch2(Grid g, ConePatch<1> a,
                 a.gout[2 * i] = sout[q][0];
                 a.gout[2 * i + 1] = sout[q][1];
                 cmax = fmax(cmax, sout[q][3]);
+                emax = fmax(emax, cell_est(sout));
             }
         }
-        if (CLK && t == 0) {
-            atomicAdd(a.clk, c1 - c0);
-            atomicAdd(a.clk + 1, c2 - c1);
-            atomicAdd(a.clk + 2, c3 - c2);
-            atomicAdd(a.clk + 3, clock64() - c3);
-            atomicAdd(a.clk + 4, 1ull);
-            atomicAdd(a.clk + 5, c0b - c0);
-        }
     }
-    if (a.chg && t >= 1020 && cmax > 0) atomicMax(a.chg, (unsigned long long)__double_as_longlong(cmax));
+    if (t >= 1020) {
+        if (a.chg && cmax > 0) atomicMax(a.chg, (unsigned long long)__double_as_longlong(cmax));
+        if (a.est && emax > 0) atomicMax(a.est, (unsigned long long)__double_as_longlong(emax));
+    }
 }
 
 // targets -> interior target cells (the patch list) and whether any target needs the band
@@ -2356,8 +1451,7 @@ __global__ void __launch_bounds__(kAxesThreads) k_gd_axes(const double* __restri
         const double* a = w == 0 ? gx : gy;
         const int m = w == 0 ? mx : my;
         double sum;
-        if (w == 0) sum = pw_sum_wave_get(tree[0], [=](int i) { return gx[i % mx]; }, cnt);
-        else sum = pw_sum_wave_get(tree[1], [=](int i) { return gy[i / mx]; }, cnt);
+        sum = pw_sum_wave_get(tree[w], MeshgridAxis{w == 0 ? gx : gy, mx, w == 0}, cnt);
         const double mean = sum / (double)cnt;
         if ((threadIdx.x & 63) == 0) ext[4 + w] = m > 1 ? fabs((a[1] - mean) - (a[0] - mean)) : 0.0;
     }
@@ -2845,66 +1939,11 @@ __global__ void k_fill_i32(int* p, int64_t n, int v) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = v;
 }
 
-// A/B knobs (environment, read once): workgroup cap of the sweep / claim launches, and the
-// per-sweep change reduction switched off (timing only)
-int64_t gd_grid_cap() {
-    static int64_t g = [] {
-        const char* e = getenv("AKB_GD_GRID");
-        const long long v = e ? atoll(e) : 0;
-        return (int64_t)(v >= 64 ? v : kStreamGridCap);
-    }();
-    return g;
-}
-int gd_no_xcd() {
-    static int b = getenv("AKB_GD_NOXCD") != nullptr ? 1 : 0;
-    return b;
-}
-bool gd_claim_v1() {  // A/B: the per-cell claim kernel
-    static bool b = getenv("AKB_GD_CLAIM_V1") != nullptr;
-    return b;
-}
-bool gd_cells_v1() {  // A/B: the per-cell (untiled) cell pass
-    static bool b = getenv("AKB_GD_CELLS_V1") != nullptr;
-    return b;
-}
 // the cell pass over the window's `rows` cell rows
 int launch_cells(const Grid& g, uint8_t* diag, double tol, unsigned* d_flags, int rows, hipStream_t s) {
-    const int64_t wc = (int64_t)rows * (g.nh - 1);
-    if (gd_cells_v1()) {
-        k_gd_cells<<<grid_for(wc, 1, kStreamGridCap), kBlock, 0, s>>>(g, diag, tol, d_flags);
-    } else {
-        const int64_t tiles = (int64_t)((rows + kCellTile - 1) / kCellTile) * ((g.nh - 1 + kCellTile - 1) / kCellTile);
-        k_gd_cells_tiled<<<(unsigned)(tiles < 4096 ? tiles : 4096), kCellTile * kCellTile, 0, s>>>(g, diag, tol,
-                                                                                                    d_flags);
-    }
+    const int64_t tiles = (int64_t)((rows + kCellTile - 1) / kCellTile) * ((g.nh - 1 + kCellTile - 1) / kCellTile);
+    k_gd_cells_tiled<<<(unsigned)(tiles < 4096 ? tiles : 4096), kCellTile * kCellTile, 0, s>>>(g, diag, tol, d_flags);
     return launch_status("k_gd_cells");
-}
-bool gd_band_split() {  // the band sweep as two launches (band, then ring); AKB_GD_BAND_MERGED: one
-    // with a wave per ring vertex (measured slower: 37 us vs 16 + 13 per sweep beside the passes -
-    // the ring's grid edges then wait behind its chord reduction on one lane)
-    static bool b = getenv("AKB_GD_BAND_MERGED") == nullptr;
-    return b;
-}
-bool gd_band_sweep8() {  // one launch per band sweep, the ring in 8-lane groups (A/B: AKB_GD_BAND_SPLIT)
-    static bool b = getenv("AKB_GD_BAND_SPLIT") == nullptr && getenv("AKB_GD_BAND_MERGED") == nullptr;
-    return b;
-}
-bool gd_patch_rowmajor() {  // A/B: the register patch kernel's lanes along rows (not by depth)
-    static bool b = getenv("AKB_GD_PATCH_ROWMAJOR") != nullptr;
-    return b;
-}
-bool gd_patch_rpf() {  // the pipeline's next box through registers over the setup (A/B: AKB_GD_PATCH_DMA,
-    // the LDS DMA issued at the step's top: 433-444 vs 423-426 us, same bits)
-    static bool b = getenv("AKB_GD_PATCH_DMA") == nullptr;
-    return b;
-}
-bool gd_patch_pipe() {  // the two-stage patch pipeline (A/B: AKB_GD_PATCH_NOPIPE)
-    static bool b = getenv("AKB_GD_PATCH_NOPIPE") == nullptr;
-    return b;
-}
-bool gd_patch_prefetch() {  // the next cell's box fetched into registers during the sweeps (A/B: off)
-    static bool b = getenv("AKB_GD_PATCH_NOPREFETCH") == nullptr;
-    return b;
 }
 unsigned gd_cu_count() {  // the device's CUs (one resident 1024-thread patch workgroup each)
     static unsigned n = [] {
@@ -2916,22 +1955,8 @@ unsigned gd_cu_count() {  // the device's CUs (one resident 1024-thread patch wo
     }();
     return n;
 }
-unsigned long long* gd_patch_clock() {  // diagnostics: per-phase cycle sums of the register patch kernel
-    static unsigned long long* p = [] {
-        unsigned long long* q = nullptr;
-        if (getenv("AKB_GD_PATCH_CLOCK") && hipMalloc(&q, 8 * sizeof(unsigned long long)) != hipSuccess) q = nullptr;
-        return q;
-    }();
-    return p;
-}
-bool gd_patch_v1() {  // A/B: the 256-thread patch kernel for one value set
-    static bool b = getenv("AKB_GD_PATCH_V1") != nullptr;
-    return b;
-}
-bool gd_no_change() {
-    static bool b = getenv("AKB_GD_NOCHG") != nullptr;
-    return b;
-}
+// the per-triangle claim (tests/test_gpu_parity.py's cross-check of the block claims: AKB_GD_CLAIM_TRI)
+bool gd_claim_tri() { return getenv("AKB_GD_CLAIM_TRI") != nullptr; }
 
 }  // namespace
 }  // namespace akb
@@ -2965,85 +1990,9 @@ int akb_gd_check_pockets(const double* x, const double* y, int nv, int nh, const
     return launch_status("k_gd_check_pockets");
 }
 
-// one Jacobi sweep; d_change: largest relative change (as ordered double bits, zeroed by the
-// caller); nvals value sets strided by n (values) and 2n (gradients); ring_work: 10 L doubles.
-// gprev != NULL: Chebyshev step, gout = omega * (jacobi(gin) - gprev) + gprev (a Jacobi sweep
-// then, whatever AKB_GD_GS says); gprev == NULL with omega == 0: a plain Jacobi sweep
-int akb_gd_grad_sweep_f64(const double* x, const double* y, int nv, int nh, const uint8_t* diag, int npock,
-                          const int32_t* ptri, const int32_t* pnbr, const int32_t* edge_tri, const int32_t* xptr,
-                          const int32_t* xidx, const double* f, int nvals, const double* gin, const double* gprev,
-                          double omega, double* gout, double* ring_work, unsigned long long* d_change, void* stream) {
-    clear_error();
-    AKB_REQUIRE(x && y && diag && f && gin && gout && ring_work && d_change && nvals >= 1, "bad arguments");
-    AKB_REQUIRE(!gprev || (omega > 0 && omega < 2), "Chebyshev weight outside (0, 2)");
-    Grid g{x, y, nv, nh, diag, npock, ptri, pnbr, edge_tri, xptr, xidx, gd_no_xcd()};
-    {
-        const char* re = getenv("AKB_GD_ROWS");
-        const int rows = re ? atoi(re) : 0;
-        if (rows >= 4 && rows <= 256) g.strip_rows = rows;
-    }
-    hipStream_t s = (hipStream_t)stream;
-    const int64_t n = (int64_t)nv * nh;
-    const int64_t L = 2 * (int64_t)(nh - 1) + 2 * (int64_t)(nv - 1);
-    unsigned long long* chg = gd_no_change() ? nullptr : d_change;
-    const int64_t chunks = (n + kGradChunk - 1) / kGradChunk;
-    const unsigned gr = (unsigned)(8 * ((chunks + 7) / 8));  // a multiple of 8 for the XCD mapping
-    const unsigned grr = grid_for(L * 64);
-    // the LDS strip kernel, AKB_GD_STRIP columns wide (64 / 128 / 256; 0: the gather kernel; read
-    // per call: the tests compare them)
-    const char* se = getenv("AKB_GD_STRIP");
-    // 256 by default: 11.9 vs 12.5 / 12.8 ms of sweeps for 128 / 64 on the C3 hits (the row chunk,
-    // 8 ... 64 rows, moves it by < 5 %: the strips are LDS-occupancy bound at 3 waves per SIMD)
-    int strip = se ? atoi(se) : 256;
-    if (strip != 0 && strip != 64 && strip != 128 && strip != 256) strip = 256;
-    // the strip sweeps as line Gauss-Seidel (AKB_GD_GS=0: Jacobi, the gather kernel's bits)
-    const char* ge = getenv("AKB_GD_GS");
-    // Gauss-Seidel only for a plain sweep that asks for it (omega >= 1): Chebyshev iterations pass
-    // omega = 0 for their plain first sweep, which must be the Jacobi one
-    const bool gs_sweep = !(ge && ge[0] == '0') && !gprev && omega > 0;
-    const unsigned gs =
-        strip ? (unsigned)(((nh + strip - 1) / strip) * ((nv + g.strip_rows - 1) / g.strip_rows)) : 0u;
-    for (int v = 0; v < nvals; v += 2) {
-        const double* fv = f + v * n;
-        const double* gi = gin + 2 * v * n;
-        double* go = gout + 2 * v * n;
-        const Cheb ch{gprev ? gprev + 2 * v * n : nullptr, omega};
-        if (nvals - v >= 2) {
-            if (strip == 64)
-                gs_sweep ? k_gd_grad_strip<2, 64, true><<<gs, 64, 0, s>>>(g, fv, gi, go, ring_work, chg, ch)
-                         : k_gd_grad_strip<2, 64><<<gs, 64, 0, s>>>(g, fv, gi, go, ring_work, chg, ch);
-            else if (strip == 128)
-                gs_sweep ? k_gd_grad_strip<2, 128, true><<<gs, 128, 0, s>>>(g, fv, gi, go, ring_work, chg, ch)
-                         : k_gd_grad_strip<2, 128><<<gs, 128, 0, s>>>(g, fv, gi, go, ring_work, chg, ch);
-            else if (strip == 256)
-                gs_sweep ? k_gd_grad_strip<2, 256, true><<<gs, 256, 0, s>>>(g, fv, gi, go, ring_work, chg, ch)
-                         : k_gd_grad_strip<2, 256><<<gs, 256, 0, s>>>(g, fv, gi, go, ring_work, chg, ch);
-            else
-                k_gd_grad<2><<<gr, kBlock, 0, s>>>(g, fv, gi, go, ring_work, chg, ch);
-            k_gd_grad_ring<2><<<grr, kBlock, 0, s>>>(g, fv, gi, go, ring_work, chg, ch);
-        } else {
-            if (strip == 64)
-                gs_sweep ? k_gd_grad_strip<1, 64, true><<<gs, 64, 0, s>>>(g, fv, gi, go, ring_work, chg, ch)
-                         : k_gd_grad_strip<1, 64><<<gs, 64, 0, s>>>(g, fv, gi, go, ring_work, chg, ch);
-            else if (strip == 128)
-                gs_sweep ? k_gd_grad_strip<1, 128, true><<<gs, 128, 0, s>>>(g, fv, gi, go, ring_work, chg, ch)
-                         : k_gd_grad_strip<1, 128><<<gs, 128, 0, s>>>(g, fv, gi, go, ring_work, chg, ch);
-            else if (strip == 256)
-                gs_sweep ? k_gd_grad_strip<1, 256, true><<<gs, 256, 0, s>>>(g, fv, gi, go, ring_work, chg, ch)
-                         : k_gd_grad_strip<1, 256><<<gs, 256, 0, s>>>(g, fv, gi, go, ring_work, chg, ch);
-            else
-                k_gd_grad<1><<<gr, kBlock, 0, s>>>(g, fv, gi, go, ring_work, chg, ch);
-            k_gd_grad_ring<1><<<grr, kBlock, 0, s>>>(g, fv, gi, go, ring_work, chg, ch);
-        }
-        int st = launch_status("k_gd_grad");
-        if (st) return st;
-    }
-    return 0;
-}
-
 // kk = 1 or 2 Jacobi sweeps in one launch of the register kernel, each a Chebyshev step (om1, om2;
 // gprev == NULL: the first is a plain sweep; gin == NULL: x_k = 0). gout1 = x_{k+1}, gout2 =
-// x_{k+2}; d_change[0], [1]: the sweeps' largest relative changes; ring_work: 14 L doubles.
+// x_{k+2}; d_change[0], [1]: the sweeps' largest relative changes; ring_work: 22 L doubles.
 int akb_gd_grad_sweeps_f64(const double* x, const double* y, int nv, int nh, const uint8_t* diag, int npock,
                            const int32_t* ptri, const int32_t* pnbr, const int32_t* edge_tri, const int32_t* xptr,
                            const int32_t* xidx, const double* f, int nvals, const double* gin, const double* gprev,
@@ -3054,21 +2003,11 @@ int akb_gd_grad_sweeps_f64(const double* x, const double* y, int nv, int nh, con
     AKB_REQUIRE(kk == 1 || (kk == 2 && gout2), "kk must be 1, or 2 with gout2");
     AKB_REQUIRE(!gprev || (om1 > 0 && om1 < 2), "Chebyshev weight outside (0, 2)");
     AKB_REQUIRE(kk == 1 || (om2 > 0 && om2 < 2), "Chebyshev weight outside (0, 2)");
-    Grid g{x, y, nv, nh, diag, npock, ptri, pnbr, edge_tri, xptr, xidx, gd_no_xcd()};
-    int rows = 24;  // rows per wave (AKB_GD_ROWS): 24 at 3 waves per SIMD measured best on the C3 hits
-    {
-        const char* re = getenv("AKB_GD_ROWS");
-        const int v = re ? atoi(re) : 0;
-        if (v >= 4 && v <= 1024) rows = v;
-    }
-    // the two-value two-sweep kernel's occupancy variant (AKB_GD_OCC, A/B): 3 waves per SIMD by
-    // default (168 VGPRs, 12 B of scratch: 4.75 vs 5.3 ms for the C3 hits' solve at 2 waves)
-    const char* oe = getenv("AKB_GD_OCC");
-    const int occ = oe ? atoi(oe) : 3;
+    Grid g{x, y, nv, nh, diag, npock, ptri, pnbr, edge_tri, xptr, xidx};
+    const int rows = 24;  // rows per wave: 24 at 3 waves per SIMD measured best on the C3 hits
     hipStream_t s = (hipStream_t)stream;
     const int64_t n = (int64_t)nv * nh;
     const int64_t L = 2 * (int64_t)(nh - 1) + 2 * (int64_t)(nv - 1);
-    unsigned long long* chg = gd_no_change() ? nullptr : d_change;
     const unsigned grr = grid_for(L * 64);
     const int own = 64 - 2 * kk;
     const int64_t waves = (int64_t)((nh + own - 1) / own) * ((nv + rows - 1) / rows);
@@ -3080,27 +2019,21 @@ int akb_gd_grad_sweeps_f64(const double* x, const double* y, int nv, int nh, con
         double* o1 = gout1 + 2 * v * n;
         double* o2 = gout2 ? gout2 + 2 * v * n : nullptr;
         double* chords = ring_work;
-        double* acc = ring_work + 7 * L;
+        double* acc = ring_work + kAccWords(2) * L;
         if (nv2 == 2) {
             k_gd_ring_chords<2><<<grr, kBlock, 0, s>>>(g, fv, gi, chords);
-            SweepArgs<2> a{fv, gi, gprev ? gprev + 2 * v * n : nullptr, om1, om2, o1, o2, chords, acc, chg, rows};
-            if (kk == 2 && occ == 2) k_gd_sweeps<2, 2, 1, 2><<<gw, 256, 0, s>>>(g, a);
-            else if (kk == 2 && occ == 5) k_gd_sweeps<2, 2, 3, 2><<<gw, 256, 0, s>>>(g, a);
-            else if (kk == 2 && occ == 3) k_gd_sweeps<2, 2, 3><<<gw, 256, 0, s>>>(g, a);
-            else if (kk == 2 && occ == 4) k_gd_sweeps<2, 2, 4><<<gw, 256, 0, s>>>(g, a);
-            else if (kk == 2) k_gd_sweeps<2, 2, 1><<<gw, 256, 0, s>>>(g, a);
+            SweepArgs<2> a{fv, gi, gprev ? gprev + 2 * v * n : nullptr, om1, om2, o1, o2, chords, acc, d_change, rows};
+            if (kk == 2) k_gd_sweeps<2, 2, 2><<<gw, 256, 0, s>>>(g, a);  // 180 VGPRs: no spills
             else k_gd_sweeps<2, 1, 1><<<gw, 256, 0, s>>>(g, a);
             if (kk == 2)
-                k_gd_grad_ring<2><<<grr, kBlock, 0, s>>>(g, fv, o1, o2, acc, chg ? chg + 1 : nullptr,
-                                                         Cheb{gi, om2, gi ? 0 : 1});
+                k_gd_grad_ring<2><<<grr, kBlock, 0, s>>>(g, fv, o1, o2, acc, d_change + 1, Cheb{gi, om2, gi ? 0 : 1});
         } else {
             k_gd_ring_chords<1><<<grr, kBlock, 0, s>>>(g, fv, gi, chords);
-            SweepArgs<1> a{fv, gi, gprev ? gprev + 2 * v * n : nullptr, om1, om2, o1, o2, chords, acc, chg, rows};
+            SweepArgs<1> a{fv, gi, gprev ? gprev + 2 * v * n : nullptr, om1, om2, o1, o2, chords, acc, d_change, rows};
             if (kk == 2) k_gd_sweeps<1, 2, 1><<<gw, 256, 0, s>>>(g, a);
             else k_gd_sweeps<1, 1, 1><<<gw, 256, 0, s>>>(g, a);
             if (kk == 2)
-                k_gd_grad_ring<1><<<grr, kBlock, 0, s>>>(g, fv, o1, o2, acc, chg ? chg + 1 : nullptr,
-                                                         Cheb{gi, om2, gi ? 0 : 1});
+                k_gd_grad_ring<1><<<grr, kBlock, 0, s>>>(g, fv, o1, o2, acc, d_change + 1, Cheb{gi, om2, gi ? 0 : 1});
         }
         int st = launch_status("k_gd_sweeps");
         if (st) return st;
@@ -3124,10 +2057,8 @@ int akb_gd_eval_f64(const double* x, const double* y, int nv, int nh, const uint
     int st = launch_status("k_fill_i32");
     if (st) return st;
     const int64_t ntri = 2 * (int64_t)(nv - 1) * (nh - 1) + npock;
-    if (getenv("AKB_GD_CLAIM_TRI"))  // the per-triangle claim (A/B and the tests' cross-check)
-        k_gd_claim<<<grid_for(ntri - npock, 1, gd_grid_cap()), kBlock, 0, s>>>(g, t, owner);
-    else if (gd_claim_v1())
-        k_gd_claim_cells<<<grid_for((ntri - npock) / 2, 1, kStreamGridCap), kBlock, 0, s>>>(g, t, owner);
+    if (gd_claim_tri())  // the per-triangle claim (the tests' cross-check)
+        k_gd_claim<<<grid_for(ntri - npock, 1, kStreamGridCap), kBlock, 0, s>>>(g, t, owner);
     else
         k_gd_claim_blocks<<<grid_for((ntri - npock) / 32 + 1, 1, kStreamGridCap), kBlock, 0, s>>>(g, t, owner);
     st = launch_status("k_gd_claim");
@@ -3179,9 +2110,7 @@ int cone_claims(const Grid& g, const Targets& t, int with_pockets, int* owner, h
     if (st) return st;
     const int64_t wc = (int64_t)((g.row1 < 0 ? g.nv - 1 : g.row1) - g.row0) * (g.nh - 1);
     if (wc > 0) {
-        if (gd_claim_v1()) {
-            k_gd_claim_cells<<<grid_for(wc, 1, kStreamGridCap), kBlock, 0, s>>>(g, t, owner);
-        } else if (scratch) {
+        if (scratch) {
             const int64_t nblk = (int64_t)(((g.row1 < 0 ? g.nv - 1 : g.row1) - g.row0 + 7) / 8) * ((g.nh - 1 + 7) / 8);
             k_gd_claim_scan<<<grid_for(nblk, 1, kStreamGridCap), kBlock, 0, s>>>(g, t, scratch);
             if ((st = launch_status("k_gd_claim_scan"))) return st;
@@ -3200,17 +2129,18 @@ int cone_claims(const Grid& g, const Targets& t, int with_pockets, int* owner, h
 }
 
 // the targets this call forms (own0 .. own1, band_on), their gradients, their values: out / cnt
-// as k_gd_eval_part writes them (cnt == nullptr: k_gd_eval's NaN for unclaimed targets)
+// as k_gd_eval_part writes them (cnt == nullptr: k_gd_eval's NaN for unclaimed targets). Value sets
+// one at a time (a set's iterate does not depend on the others). d_change[0]: the patches' change
+// measure, d_change[1]: their value-error estimate (k_gd_cone_patch), ordered double bits.
 int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int band_on, const double* f, int nvals,
               int K, const double* omegas, void* work, const int* owner, double* out, double* cnt,
               unsigned long long* d_change, hipStream_t s) {
     const int64_t n = (int64_t)g.nv * g.nh, m = (int64_t)t.mx * t.my;
     const int64_t L = 2 * (int64_t)(g.nh - 1) + 2 * (int64_t)(g.nv - 1);
-    const int nv2 = nvals >= 2 ? 2 : 1;
     double* gb[3];
-    for (int k = 0; k < 3; ++k) gb[k] = (double*)work + (int64_t)k * nv2 * n * 2;
-    double* ring_acc = (double*)work + 3 * (int64_t)nv2 * n * 2;
-    int64_t* cells = (int64_t*)(ring_acc + L * 7);
+    for (int k = 0; k < 3; ++k) gb[k] = (double*)work + (int64_t)k * n * 2;
+    const int nv2 = nvals >= 2 ? 2 : 1;  // the work layout's (claim_scratch_offset)
+    int64_t* cells = (int64_t*)((double*)work + 3 * (int64_t)nv2 * n * 2 + L * 7);
     uint8_t* assigned = (uint8_t*)(cells + m);
     int* count = (int*)(((uintptr_t)(assigned + m) + 7) & ~(uintptr_t)7);
     int* band = count + 1;
@@ -3219,112 +2149,43 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
                                                       assigned);
     int st = launch_status("k_gd_cone_assign");
     if (st) return st;
-    // the boundary band, shrinking like the patches' squares: sweep j forms depth <= 2K + 3 - j, whose
-    // neighbours (depth <= 2K + 4 - j) sweep j - 1 formed, so x_K is the global iteration's to depth
-    // K + 3 >= every band target's corners (the first sweep reads x_0 = 0 only)
+    // sweep j's form: 1 plain, 2 against x_0 = 0, later against x_{j-2}
     ConeStep steps[kConeMaxK + 1];
     steps[0] = ConeStep{0, 1.0};
     for (int j = 1; j <= K; ++j)
         steps[j] = j == 1 ? ConeStep{0, 1.0} : j == 2 ? ConeStep{1, omegas[1]} : ConeStep{2, omegas[j - 1]};
-    const unsigned pg = (unsigned)(m < 8192 ? m : 8192);
-    for (int v0 = 0; v0 < nvals; v0 += 2) {
-        const int nvv = nvals - v0 >= 2 ? 2 : 1;
-        const double* fv = f + v0 * n;
+    // the patches' pipeline split: the smallest S >= K / 2 with both stages' vertices in 1020 threads
+    const int W = 2 * K + 4;
+    int S = -1;
+    for (int s2 = (K + 1) / 2; s2 <= K && S < 0; ++s2)
+        if ((((W - 2) * (W - 2) + 63) & ~63) + (W - 2 * s2 - 2) * (W - 2 * s2 - 2) <= 1020) S = s2;
+    const unsigned pp = gd_cu_count();  // one persistent workgroup per CU walks its cells
+    AKB_REQUIRE(S >= 0 && m <= 1024 * (int64_t)pp, "cone patches: K or the target count out of range");
+    for (int v = 0; v < nvals; ++v) {
+        const double* fv = f + v * n;
+        // the boundary band, shrinking like the patches' squares: sweep j forms depth <= 2K + 3 - j,
+        // whose neighbours (depth <= 2K + 4 - j) sweep j - 1 formed, so x_K is the global iteration's
+        // to depth K + 3 >= every band target's corners (the first sweep reads x_0 = 0 only)
         if (band_on) {
             for (int j = 1; j <= K; ++j) {
                 const double* gin = j == 1 ? nullptr : gb[(j - 1) % 3];
                 const double* gprev = j >= 3 ? gb[(j + 1) % 3] : nullptr;
                 const BandMap bm = band_map(g.nv, g.nh, 2 * K + 3 - j);
-                const unsigned nbw = grid_for(bm.total, 1, kStreamGridCap), nrw = grid_for(L * 64), nr8 = grid_for((L + 7) / 8 * 64);
-                if (nvv == 2) {
-                    ConeBand<2> a{fv, gin, gprev, gb[j % 3], ring_acc, steps[j], band};
-                    if (gd_band_sweep8()) {
-                        k_gd_cone_sweep8<2><<<nbw + nr8, kBlock, 0, s>>>(g, bm, a, (int)nbw);
-                    } else if (gd_band_split()) {
-                        k_gd_cone_band<2><<<nbw, kBlock, 0, s>>>(g, bm, a);
-                        k_gd_cone_ring<2><<<nr8, kBlock, 0, s>>>(g, a);
-                    } else {
-                        k_gd_cone_sweep<2><<<nbw + nrw, kBlock, 0, s>>>(g, bm, a, (int)nbw);
-                    }
-                } else {
-                    ConeBand<1> a{fv, gin, gprev, gb[j % 3], ring_acc, steps[j], band};
-                    if (gd_band_sweep8()) {
-                        k_gd_cone_sweep8<1><<<nbw + nr8, kBlock, 0, s>>>(g, bm, a, (int)nbw);
-                    } else if (gd_band_split()) {
-                        k_gd_cone_band<1><<<nbw, kBlock, 0, s>>>(g, bm, a);
-                        k_gd_cone_ring<1><<<nr8, kBlock, 0, s>>>(g, a);
-                    } else {
-                        k_gd_cone_sweep<1><<<nbw + nrw, kBlock, 0, s>>>(g, bm, a, (int)nbw);
-                    }
-                }
-                if ((st = launch_status("k_gd_cone_band"))) return st;
+                const unsigned nbw = grid_for(bm.total, 1, kStreamGridCap), nr8 = grid_for((L + 7) / 8 * 64);
+                const ConeBand a{fv, gin, gprev, gb[j % 3], steps[j], band};
+                k_gd_cone_sweep8<<<nbw + nr8, kBlock, 0, s>>>(g, bm, a, (int)nbw);
+                if ((st = launch_status("k_gd_cone_sweep8"))) return st;
             }
         }
-        if (nvv == 2) {
-            ConePatch<2> a{fv, cells, count, K, {}, gb[K % 3], d_change};
-            for (int j = 0; j <= K; ++j) a.st[j] = steps[j];
-            k_gd_cone_patch<2><<<pg, 256, 0, s>>>(g, a);
-        } else {
-            ConePatch<1> a{fv, cells, count, K, {}, gb[K % 3], d_change};
-            for (int j = 0; j <= K; ++j) a.st[j] = steps[j];
-            if (gd_patch_v1())
-                k_gd_cone_patch<1><<<pg, 256, 0, s>>>(g, a);
-            else
-            {
-                unsigned long long* clk = gd_patch_clock();
-                if (clk) {
-                    (void)hipMemsetAsync(clk, 0, 8 * sizeof(unsigned long long), s);
-                    a.clk = clk;
-                }
-                const int rm = gd_patch_rowmajor() ? 1 : 0;
-                // the two-stage pipeline when both stages' vertices fit 1024 threads (K <= 14: always)
-                int S = -1;
-                if (gd_patch_pipe() && !rm) {
-                    const int W = 2 * K + 4;
-                    const char* es = getenv("AKB_GD_PATCH_S");  // A/B: the first sweep stage 2 does is S + 1
-                    for (int s2 = es ? std::max(1, std::min(K, atoi(es))) : (K + 1) / 2; s2 <= K && S < 0; ++s2)
-                        if ((W - 2) * (W - 2) + (W - 2 * s2 - 2) * (W - 2 * s2 - 2) <= 1024) S = s2;
-                }
-                // prefetching: one persistent workgroup per CU walks its cells (the next one's box
-                // loads during the current one's sweeps); else workgroups per cell
-                // A/B: AKB_GD_PATCH_GRID leaves CUs to the other streams' kernels while the patches run
-                const char* eg = getenv("AKB_GD_PATCH_GRID");
-                const unsigned pp = std::min(pg, eg ? std::max(1u, (unsigned)atoi(eg)) : gd_cu_count());
-                if (S >= 0 && (int64_t)m > 1024 * (int64_t)pp) S = -1;  // the cell list fits LDS
-                if (S >= 0) {
-                    if (clk) {
-                        if (gd_patch_rpf()) k_gd_cone_patch2<true, true><<<pp, 1024, 0, s>>>(g, a, S);
-                        else k_gd_cone_patch2<true, false><<<pp, 1024, 0, s>>>(g, a, S);
-                    } else {
-                        if (gd_patch_rpf()) k_gd_cone_patch2<false, true><<<pp, 1024, 0, s>>>(g, a, S);
-                        else k_gd_cone_patch2<false, false><<<pp, 1024, 0, s>>>(g, a, S);
-                    }
-                } else if (clk) {
-                    if (gd_patch_prefetch()) k_gd_cone_patch1<true, true><<<pp, 1024, 0, s>>>(g, a, rm);
-                    else k_gd_cone_patch1<false, true><<<pg, 1024, 0, s>>>(g, a, rm);
-                } else {
-                    if (gd_patch_prefetch()) k_gd_cone_patch1<true, false><<<pp, 1024, 0, s>>>(g, a, rm);
-                    else k_gd_cone_patch1<false, false><<<pg, 1024, 0, s>>>(g, a, rm);
-                }
-                if (clk) {
-                    unsigned long long h[8];
-                    (void)hipMemcpyAsync(h, clk, sizeof(h), hipMemcpyDeviceToHost, s);
-                    (void)hipStreamSynchronize(s);
-                    const double nc = h[4] ? (double)h[4] : 1.0;
-                    fprintf(stderr,
-                            "AKB_GD_PATCH_CLOCK cells %llu cycles/cell: load %.0f (own vmem wait %.0f) setup %.0f sweeps "
-                            "%.0f out %.0f\n",
-                            h[4], h[0] / nc, h[5] / nc, h[1] / nc, h[2] / nc, h[3] / nc);
-                }
-            }
-        }
+        ConePatch a{fv, cells, count, K, {}, gb[K % 3], d_change, d_change ? d_change + 1 : nullptr};
+        for (int j = 0; j <= K; ++j) a.st[j] = steps[j];
+        k_gd_cone_patch<<<pp, 1024, 0, s>>>(g, a, S);
         if ((st = launch_status("k_gd_cone_patch"))) return st;
         if (cnt)
-            k_gd_eval_part<<<grid_for(m, 1, kStreamGridCap), kBlock, 0, s>>>(g, t, owner, assigned, fv, gb[K % 3], nvv,
-                                                                              out + v0 * m, cnt);
+            k_gd_eval_part<<<grid_for(m, 1, kStreamGridCap), kBlock, 0, s>>>(g, t, owner, assigned, fv, gb[K % 3], 1,
+                                                                              out + v * m, cnt);
         else
-            k_gd_eval<<<grid_for(m, 1, kStreamGridCap), kBlock, 0, s>>>(g, t, owner, fv, gb[K % 3], nvv,
-                                                                         out + v0 * m);
+            k_gd_eval<<<grid_for(m, 1, kStreamGridCap), kBlock, 0, s>>>(g, t, owner, fv, gb[K % 3], 1, out + v * m);
         if ((st = launch_status("k_gd_eval"))) return st;
     }
     return 0;

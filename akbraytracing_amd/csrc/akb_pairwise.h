@@ -131,29 +131,9 @@ static __device__ double pw_tree_wave(PwTree& T, const double* a, int len) {
     return T.val[0][0];
 }
 
-// pw_leaf_lds / pw_tree_wave over a virtual array: element i is get(i) (e.g. a meshgrid's flattened
-// entries formed from its axis), the same split tree and additions, so the same bits as the
-// stored array's sum
-template <class Get>
-__device__ double pw_leaf_get(const Get& get, int o, int n) {
-    if (n < 8) {
-        double res = 0.0;
-        for (int i = 0; i < n; ++i) res = res + get(o + i);
-        return res;
-    }
-    double r[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) r[j] = get(o + j);
-    int i = 8;
-    for (; i < n - (n % 8); i += 8) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) r[j] = r[j] + get(o + i + j);
-    }
-    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-    for (; i < n; ++i) res = res + get(o + i);
-    return res;
-}
-
+// pw_leaf_lds / pw_tree_wave over a virtual array: get.leaf(o, n) is the numpy leaf sum of elements
+// o .. o + n - 1 (8 running sums in order, as pw_leaf_lds), e.g. of a meshgrid's flattened entries
+// formed from its axis; the same split tree and additions, so the same bits as the stored array's sum
 template <class Get>
 __device__ double pw_tree_wave_get(PwTree& T, const Get& get, int base, int len) {
     const int lane = threadIdx.x & 63;
@@ -185,7 +165,7 @@ __device__ double pw_tree_wave_get(PwTree& T, const Get& get, int base, int len)
                 T.len[d + 1][pos + 1] = l - l2;
                 T.child[d][lane] = pos;
             } else if (act) {
-                T.val[d][lane] = pw_leaf_get(get, base + o, l);
+                T.val[d][lane] = get.leaf(base + o, l);
             }
             if (m && d + 1 < kTreeLevels) {
                 nd[d + 1] = 2 * __popcll(m);
@@ -222,5 +202,40 @@ __device__ double pw_sum_wave_get(PwTree& T, const Get& get, long long n) {
     }
     return s;
 }
+
+// the flattened my x mx meshgrid of an axis a as get.leaf wants it: element i is a[i % mx]
+// (np.meshgrid's first output, rows) or a[i / mx] (its second, columns), walked in order
+struct MeshgridAxis {
+    const double* a;
+    int mx;
+    bool rows;
+    __device__ double leaf(int o, int n) const {
+        int r = o / mx, c = o - r * mx;
+        auto next = [&]() {
+            const double v = rows ? a[c] : a[r];
+            if (++c == mx) {
+                c = 0;
+                ++r;
+            }
+            return v;
+        };
+        if (n < 8) {
+            double res = 0.0;
+            for (int i = 0; i < n; ++i) res = res + next();
+            return res;
+        }
+        double acc[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] = next();
+        int i = 8;
+        for (; i < n - (n % 8); i += 8) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[j] = acc[j] + next();
+        }
+        double res = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+        for (; i < n; ++i) res = res + next();
+        return res;
+    }
+};
 
 }  // namespace akb

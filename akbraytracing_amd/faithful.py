@@ -152,7 +152,7 @@ class FaithfulPupil:
         self.owner = torch.empty(m, dtype=torch.int32, device=self.dev)
         self.axes = torch.empty(2 * self.size + 6, dtype=D.F64, device=self.dev)  # gx | gy | extent | pitch
         self.map = torch.empty((1, self.size, self.size), dtype=D.F64, device=self.dev)
-        self.change = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        self.change = torch.zeros(2, dtype=torch.int64, device=self.dev)  # change measure | value-error estimate
         self.post = {}
         self.psf = None
         self._done = None  # the latest finish's end (finishes share work / map / pupil / psf buffers)

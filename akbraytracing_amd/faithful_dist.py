@@ -318,7 +318,7 @@ class ShardedFaithfulPupil:
         # map piece | count | every rank's cell flags (slot r): one SUM reduction to the band owner
         self.red = torch.zeros(2 * m + comm.world, dtype=D.F64, device=self.dev)
         self.map = torch.empty((1, self.size, self.size), dtype=D.F64, device=self.dev)
-        self.change = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        self.change = torch.zeros(2, dtype=torch.int64, device=self.dev)  # change measure | value-error estimate
         self.post, self.psf = {}, None
         self._omegas = D.host_f64(chebyshev_weights(max(self.K, 1)))
         self.pool = concurrent.futures.ThreadPoolExecutor(max_workers=int(workers), thread_name_prefix="akb-pk") \

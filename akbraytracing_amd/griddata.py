@@ -148,83 +148,54 @@ class CubicGrid:
         return (D.ptr(self.x), D.ptr(self.y), self.nv, self.nh, D.ptr(self.diag), self.npock, D.ptr(self.ptri),
                 D.ptr(self.pnbr), D.ptr(self.edge_tri))
 
-    def gradients(self, values, tol=GRADIENT_TOL, maxiter=400, check_every=8, adaptive=True, method=None):
-        """estimate_gradients_2d_global for (nvals, n) values: (nvals, n, 2) device tensor. The sweeps
-        stop after the first batch holding one whose largest relative change (scipy's measure of a
-        Jacobi step) is below tol (GRADIENT_TOL); with adaptive, batches after the first are sized
-        from the observed decay rate.
-
-        method (AKB_GD_ITER overrides the default):
-          "chebyshev"        Jacobi sweeps with Chebyshev semi-iteration for a spectrum in [-1/2, 1/2]
-                             (the local problem is block diagonally dominant by a factor 2), ~0.27 error
-                             contraction per sweep; two sweeps per launch of the register kernel
-                             (k_gd_sweeps). The default.
-          "chebyshev-strip"  the same iterates (the same bits), one sweep per launch of the LDS strip
-                             kernel
-          "sweep"            plain sweeps (line Gauss-Seidel in the LDS strips, Jacobi with AKB_GD_GS=0)"""
-        import os
+    def gradients(self, values, tol=GRADIENT_TOL, maxiter=400, check_every=8, adaptive=True):
+        """estimate_gradients_2d_global for (nvals, n) values: (nvals, n, 2) device tensor. Jacobi
+        sweeps of scipy's local solve with Chebyshev semi-iteration for a spectrum in [-1/2, 1/2] (the
+        local problem is block diagonally dominant by a factor 2), ~0.27 error contraction per sweep,
+        two sweeps per launch of the register kernel (k_gd_sweeps). The sweeps stop after the first
+        batch holding one whose largest relative change (scipy's measure of a Jacobi step) is below
+        tol (GRADIENT_TOL); with adaptive, batches after the first are sized from the observed decay
+        rate."""
         L = _lib.lib()
         if self._checked:
             self._check_status()  # re-raises for a triangulation the pocket check flagged
-        method = method or os.environ.get("AKB_GD_ITER", "chebyshev")
-        if method not in ("chebyshev", "chebyshev-strip", "sweep"):
-            raise ValueError(f"unknown gradient iteration {method!r}")
         f = _dev(values, self.dev)
         f = f.reshape(-1, self.nv * self.nh).contiguous()
         nvals = int(f.shape[0])
         shape = (nvals, self.nv * self.nh, 2)
         change = torch.zeros(maxiter + 1, dtype=torch.int64, device=self.dev)
         s = D.stream_handle()
-        # spectral radius 1/2 (AKB_GD_RHO: an A/B knob)
-        omegas = chebyshev_weights(maxiter, float(os.environ.get("AKB_GD_RHO", "0.5")))
-        if method == "chebyshev":
-            # iterate k in g[k % 4] (a launch reads x_k, x_{k-1} and writes x_{k+1}, x_{k+2}); x_0 = 0
-            g = [torch.empty(shape, dtype=D.F64, device=self.dev) for _ in range(4)]
-            zero = None
-            ring = torch.empty(14 * self.L, dtype=D.F64, device=self.dev)
+        omegas = chebyshev_weights(maxiter)
+        # iterate k in g[k % 4] (a launch reads x_k, x_{k-1} and writes x_{k+1}, x_{k+2}); x_0 = 0
+        g = [torch.empty(shape, dtype=D.F64, device=self.dev) for _ in range(4)]
+        zero = None
+        ring = torch.empty(22 * self.L, dtype=D.F64, device=self.dev)
 
-            def it_ptr(k):
-                return None if k == 0 else D.ptr(g[k % 4])
+        def it_ptr(k):
+            return None if k == 0 else D.ptr(g[k % 4])
 
-            def launch(k, kk):
-                nonlocal zero
-                gprev = None
-                if k == 1:  # x_0 = 0 as a Chebyshev predecessor (only when the first batch is one sweep)
-                    if zero is None:
-                        zero = torch.zeros(shape, dtype=D.F64, device=self.dev)
-                    gprev = D.ptr(zero)
-                elif k >= 2:
-                    gprev = D.ptr(g[(k - 1) % 4])
-                _lib.check(L.akb_gd_grad_sweeps_f64(
-                    *self._tri_args(), D.ptr(self.xptr), D.ptr(self.xidx), D.ptr(f), nvals, it_ptr(k), gprev,
-                    float(omegas[k]), float(omegas[k + 1] if kk == 2 else 1.0), kk, D.ptr(g[(k + 1) % 4]),
-                    D.ptr(g[(k + 2) % 4]) if kk == 2 else None, D.ptr(ring), D.ptr(change[k:]), s))
-        else:
-            cheb = method == "chebyshev-strip"
-            g = [torch.zeros(shape, dtype=D.F64, device=self.dev) for _ in range(3 if cheb else 2)]
-            nb = len(g)
-            ring = torch.empty(10 * self.L, dtype=D.F64, device=self.dev)
-
-            def it_ptr(k):
-                return D.ptr(g[k % nb])
-
-            def launch(k, kk):
-                assert kk == 1
-                gp = D.ptr(g[(k - 1) % nb]) if cheb and k > 0 else None
-                # omega 0: the Chebyshev iteration's plain first sweep is a Jacobi sweep (never Gauss-Seidel)
-                om = (omegas[k] if k > 0 else 0.0) if cheb else 1.0
-                _lib.check(L.akb_gd_grad_sweep_f64(*self._tri_args(), D.ptr(self.xptr), D.ptr(self.xidx), D.ptr(f),
-                                                   nvals, D.ptr(g[k % nb]), gp, float(om),
-                                                   D.ptr(g[(k + 1) % nb]), D.ptr(ring), D.ptr(change[k:]), s))
-        # the first check after 12 Chebyshev sweeps (the C3 hits need ~15 at GRADIENT_TOL), then
-        # batches sized from the observed decay rate: each check is a host round trip
-        it, batch = 0, (max(check_every, 12) if method == "chebyshev" and check_every == 8 else check_every)
+        def launch(k, kk):
+            nonlocal zero
+            gprev = None
+            if k == 1:  # x_0 = 0 as a Chebyshev predecessor (only when the first batch is one sweep)
+                if zero is None:
+                    zero = torch.zeros(shape, dtype=D.F64, device=self.dev)
+                gprev = D.ptr(zero)
+            elif k >= 2:
+                gprev = D.ptr(g[(k - 1) % 4])
+            _lib.check(L.akb_gd_grad_sweeps_f64(
+                *self._tri_args(), D.ptr(self.xptr), D.ptr(self.xidx), D.ptr(f), nvals, it_ptr(k), gprev,
+                float(omegas[k]), float(omegas[k + 1] if kk == 2 else 1.0), kk, D.ptr(g[(k + 1) % 4]),
+                D.ptr(g[(k + 2) % 4]) if kk == 2 else None, D.ptr(ring), D.ptr(change[k:]), s))
+        # the first check after 12 sweeps (the C3 hits need ~15 at GRADIENT_TOL), then batches sized
+        # from the observed decay rate: each check is a host round trip
+        it, batch = 0, (max(check_every, 12) if check_every == 8 else check_every)
         hist = []
         while it < maxiter:
             stop = min(it + batch, maxiter)
             k = it
             while k < stop:
-                kk = 2 if (method == "chebyshev" and stop - k >= 2) else 1
+                kk = 2 if stop - k >= 2 else 1
                 launch(k, kk)
                 k += kk
             if not self._checked:  # the pocket check's word rides on the first batch's copy
@@ -248,9 +219,9 @@ class CubicGrid:
                 batch = int(min(max(need, 1), check_every))
         self.sweeps = it
         self.history = hist  # the largest relative change of each sweep's Jacobi step
-        if method == "chebyshev" and it == 0:
+        if it == 0:
             return torch.zeros(shape, dtype=D.F64, device=self.dev)
-        return g[it % len(g)] if method != "chebyshev" else g[it % 4]
+        return g[it % 4]
 
     def interp(self, values, gx, gy, tol=GRADIENT_TOL):
         """(nvals, n) values -> (nvals, len(gy), len(gx)) on the meshgrid of gx x gy."""
@@ -286,7 +257,8 @@ class CubicGrid:
         work = torch.empty(need // 8 + 1, dtype=D.F64, device=self.dev)
         owner = torch.empty(mx * my, dtype=torch.int32, device=self.dev)
         out = torch.empty((nvals, my, mx), dtype=D.F64, device=self.dev)
-        self.cone_change = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        # [0] the change measure at the interior target cells' corners, [1] the value-error estimate
+        self.cone_change = torch.zeros(2, dtype=torch.int64, device=self.dev)
         om = chebyshev_weights(max(int(sweeps), 1))
         _lib.check(L.akb_gd_cone_eval_f64(*self._tri_args(), D.ptr(self.xptr), D.ptr(self.xidx), D.ptr(gx), mx,
                                           D.ptr(gy), my, D.ptr(f), nvals, int(sweeps), D.host_f64(om), D.ptr(work),

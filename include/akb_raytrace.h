@@ -487,12 +487,11 @@ int akb_warp_affine_f64(const double* img, int ny, int nx, const double* iM, int
  * non-convex cell, bit 1 not locally Delaunay, bit 2 broken pocket adjacency, bits 3 and 4 both
  * set = folded grid) -> akb_gd_pockets (HOST: the triangles between the boundary ring and the
  * convex hull, ring coordinates from akb_gd_cells_f64; ids >= 2 (n_v-1)(n_h-1)) ->
- * akb_gd_check_pockets. Gradients: akb_gd_grad_sweep_f64 (one Jacobi sweep of scipy's
- * estimate_gradients_2d_global local solve, largest relative change of that Jacobi step
- * atomically max-ed into *d_change as double bits; ring_work: 10 * ring-length doubles; with
- * gprev != NULL a Chebyshev step, gout = omega * (jacobi(gin) - gprev) + gprev; gprev == NULL:
- * a plain sweep, line Gauss-Seidel unless AKB_GD_GS=0 or omega == 0) until converged.
- * Values: akb_gd_eval_f64 (NaN outside the hull). */
+ * akb_gd_check_pockets. Gradients: akb_gd_grad_sweeps_f64 (Chebyshev-accelerated Jacobi sweeps of
+ * scipy's estimate_gradients_2d_global local solve, in the edge-matrix form g <- c - P S with
+ * S = sum over the edges of r^-3 e e^T g_j; the largest relative change of each Jacobi step
+ * atomically max-ed into d_change as double bits) until converged. Values: akb_gd_eval_f64 (NaN
+ * outside the hull). */
 int akb_gd_cells_f64(const double* x, const double* y, int nv, int nh, uint8_t* diag, double tol, unsigned* d_flags,
                      double* ring_x, double* ring_y, void* stream);
 int akb_gd_pockets(const double* ring_x, const double* ring_y, int nv, int nh, int cap, int32_t* n_out,
@@ -500,14 +499,11 @@ int akb_gd_pockets(const double* ring_x, const double* ring_y, int nv, int nh, i
 int akb_gd_check_pockets(const double* x, const double* y, int nv, int nh, const uint8_t* diag, int npock,
                          const int32_t* ptri, const int32_t* pnbr, const int32_t* edge_tri, double tol,
                          unsigned* d_flags, void* stream);
-int akb_gd_grad_sweep_f64(const double* x, const double* y, int nv, int nh, const uint8_t* diag, int npock,
-                          const int32_t* ptri, const int32_t* pnbr, const int32_t* edge_tri, const int32_t* xptr,
-                          const int32_t* xidx, const double* f, int nvals, const double* gin, const double* gprev,
-                          double omega, double* gout, double* ring_work, unsigned long long* d_change, void* stream);
 /* kk = 1 or 2 sweeps in one launch (register kernel, wave-shift neighbours, the second sweep one row
  * behind the first): gout1 = x_{k+1}, gout2 = x_{k+2} from gin = x_k (NULL: zeros) and gprev =
- * x_{k-1} (NULL: the first sweep is plain), Chebyshev weights om1, om2; the same bits as kk calls of
- * akb_gd_grad_sweep_f64. d_change[0..kk-1]: the sweeps' changes; ring_work: 14 * ring-length doubles. */
+ * x_{k-1} (NULL: the first sweep is plain), Chebyshev weights om1, om2 (x_{k+1} = om (y - x_{k-1}) +
+ * x_{k-1}, y the Jacobi step). d_change[0..kk-1]: the sweeps' changes; ring_work: 22 * ring-length
+ * doubles. Replaces the gradient loop of scipy/interpolate/_interpnd.pyx. */
 int akb_gd_grad_sweeps_f64(const double* x, const double* y, int nv, int nh, const uint8_t* diag, int npock,
                            const int32_t* ptri, const int32_t* pnbr, const int32_t* edge_tri, const int32_t* xptr,
                            const int32_t* xidx, const double* f, int nvals, const double* gin, const double* gprev,
@@ -523,16 +519,22 @@ int akb_gd_eval_f64(const double* x, const double* y, int nv, int nh, const uint
  * read them: per interior target cell a (2K + 4)^2 patch in LDS, the global iteration on the
  * boundary band (depth 2K + 2, pocket chords included) for the rest. The values equal
  * akb_gd_eval_f64 on the global iteration's K-sweep gradients bit for bit; one call, no host
- * synchronisation. work: akb_gd_cone_work_bytes; d_change (or NULL): the largest change measure
- * (scipy's, as ordered double bits, atomic max) one more sweep would make at the interior target
- * cells' corners. Replaces the gradient loop of scipy's estimate_gradients_2d_global
+ * synchronisation. work: akb_gd_cone_work_bytes; d_change (or NULL, 2 words, ordered double bits,
+ * atomic max): [0] the largest change measure (scipy's) one more sweep would make at the interior
+ * target cells' corners, [1] the largest value-error estimate of an interior target cell (2 sqrt 2 x
+ * the corners' largest |one more plain sweep - x_K| x the cell's longest side or diagonal: the map
+ * units' bound on |value - the converged iteration's value| with the Jacobi spectrum in [-1/2, 1/2];
+ * the boundary-band targets are not covered). Replaces the gradient loop of scipy's
+ * estimate_gradients_2d_global
  * (scipy/interpolate/_interpnd.pyx) where the driver's griddata (AKB_raytrace_20250312.py:3689)
  * feeds a fixed-size pupil. */
 int64_t akb_gd_cone_work_bytes(int nv, int nh, int mx, int my, int nvals);
 /* The driver's target axes (AKB_raytrace_20250312.py:3654-3657): gx = np.linspace(min, max, mx) of
  * the lattice's x (its extremes lie on the boundary ring akb_gd_cells_f64 returns), gy likewise of
- * y; d_extent (or NULL, 6 doubles): [min x, max x, min y, max y, x step, y step] (the steps: the
- * pupil pitch psf_calc hands compute_psf_fft, :1176-1177). One workgroup, device-resident. */
+ * y; d_extent (or NULL, 6 doubles): [min x, max x, min y, max y, dx, dy] with dx = |gh[0,1] - gh[0,0]|,
+ * dy = |gv[1,0] - gv[0,0]| of the meshgrids after the driver's grid_H -= np.mean(grid_H) (numpy's
+ * pairwise mean; :3698): the pupil pitch psf_calc hands compute_psf_fft (:1176-1177). One
+ * workgroup, device-resident. */
 int akb_gd_axes_f64(const double* ring_x, const double* ring_y, int64_t L, int mx, int my, double* gx, double* gy,
                     double* d_extent, void* stream);
 int akb_gd_cone_eval_f64(const double* x, const double* y, int nv, int nh, const uint8_t* diag, int npock,

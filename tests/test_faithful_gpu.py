@@ -56,9 +56,11 @@ def test_faithful_pipeline_vs_host_chain_and_reference(gpu, n):
     assert np.array_equal(x_im, host["x_im"]) and np.array_equal(y_im, host["y_im"])
     fp = golden("akb_psf_full.npz")
     e_ref = float(np.max(np.abs(_crop(P, fp, n) - fp[f"n{n}_psf_crop"])))
-    ch = np.array([int(r["change"].item())]).view(np.float64)[0]
+    ch, est = r["change"].cpu().numpy().view(np.float64)
     print(f"n={n}: pipelined vs host chain: corrected map {e_map:.2e} of the range, PSF {e_psf:.2e} of the peak; "
-          f"vs the reference's PSF {e_ref:.2e}; change at the target corners {ch:.2e}")
+          f"vs the reference's PSF {e_ref:.2e}; change at the target corners {ch:.2e}, value-error estimate "
+          f"{est / rng_:.2e} of the range")
+    assert est <= 1e-6 * rng_
     assert e_map <= 3e-7  # the cone solve's 12 sweeps against the host chain's converged gradients
     assert e_psf <= 1e-7
     assert e_ref <= 1e-6
