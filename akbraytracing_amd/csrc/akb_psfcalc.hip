@@ -7,6 +7,8 @@
 // B-spline sum at each output pixel's source point (oracle/psfcalc.py states the algorithm and
 // its boundary rules). The maps are small (65^2 .. 1k^2): one thread per line for the recursive
 // prefilter, one thread per output pixel for the interpolation, both arrays at once.
+#include <type_traits>
+
 #include "akb_common.h"
 #include "akb_pairwise.h"
 
@@ -150,7 +152,7 @@ struct MomArgs {
 };
 
 // basis5 from per-axis tables (the same X, Y values; tables only for axes of up to kPostBasisMax)
-constexpr int kPostBasisMax = 1024;
+constexpr int kPostBasisMax = 256;
 __device__ __forceinline__ void basis5_tab(const double* bX, const double* bY, int i, int j, int ny, int nx,
                                            double (&f)[5]) {
     const double X = nx <= kPostBasisMax && ny <= kPostBasisMax ? bX[j] : (nx > 1 ? (2.0 * j - (nx - 1)) / (double)(nx - 1) : 0.0);
@@ -356,6 +358,62 @@ __device__ bool solve_small(double* A, double* b, int n) {
     return true;
 }
 
+// solve_small in registers for a fixed n (every index a compile-time one: the pivot row swap is a
+// select per row), the same operations in the same order - thread-local arrays with runtime indices
+// would live in scratch memory, a global-memory round trip per access on this one-thread path
+template <int N>
+__device__ __forceinline__ bool solve_small_reg(double (&A)[N][N], double (&b)[N]) {
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        int p = k;
+        double best = fabs(A[k][k]);
+#pragma unroll
+        for (int i = k + 1; i < N; ++i)
+            if (fabs(A[i][k]) > best) {
+                p = i;
+                best = fabs(A[i][k]);
+            }
+        // the pivot row (the largest magnitude in column k, the first on ties) into row k
+        double pr[N], pb = b[k];
+#pragma unroll
+        for (int j = 0; j < N; ++j) pr[j] = A[k][j];
+#pragma unroll
+        for (int i = k + 1; i < N; ++i)
+            if (i == p) {
+#pragma unroll
+                for (int j = 0; j < N; ++j) pr[j] = A[i][j];
+                pb = b[i];
+            }
+#pragma unroll
+        for (int i = k + 1; i < N; ++i)
+            if (i == p) {
+#pragma unroll
+                for (int j = 0; j < N; ++j) A[i][j] = A[k][j];
+                b[i] = b[k];
+            }
+#pragma unroll
+        for (int j = 0; j < N; ++j) A[k][j] = pr[j];
+        b[k] = pb;
+        if (A[k][k] == 0.0) ok = false;
+#pragma unroll
+        for (int i = k + 1; i < N; ++i) {
+            const double l = A[i][k] / A[k][k];
+#pragma unroll
+            for (int j = k; j < N; ++j) A[i][j] = A[i][j] - l * A[k][j];
+            b[i] = b[i] - l * b[k];
+        }
+    }
+#pragma unroll
+    for (int k = N - 1; k >= 0; --k) {
+        double v = b[k];
+#pragma unroll
+        for (int j = k + 1; j < N; ++j) v = v - A[k][j] * b[j];
+        b[k] = v / A[k][k];
+    }
+    return ok;
+}
+
 constexpr int kPostThreads = 1024;
 constexpr int64_t kPostMax = 65536;  // map points the one-workgroup post handles
 
@@ -392,44 +450,129 @@ __device__ __forceinline__ void block_sum(double (&acc)[Q], double (*red)[Q]) {
     __syncthreads();
 }
 
-// LDS of the post: the nanmean's trees, then the map for the moment passes (maps of up to 16512
-// points; larger ones are read from `corrected`)
-constexpr int kSplineLds = 128 * 129;
+// LDS of the post: the map for the nanmean and the moment passes (maps of up to 16384 points; larger
+// ones are read from global memory and `corrected`)
+constexpr int kPostLds = 16384;
 
-// spline_filter1d along one axis in LDS: a workgroup of 64 threads takes 64 lines of one array
-// (blockIdx.y: map, mask) - a line is a sequential recursion, so through L2 each step would wait
-// for a load; in LDS (pitch lines + 1 against bank conflicts) it waits for LDS only. Lines of up to
-// 256 points; spline_line's arithmetic.
-constexpr int kSplineLines = 64, kSplineMaxLen = 256, kSplineThreads = 256;
+// spline_line's arithmetic on a line in LDS (stride s), in chunks of kCh points: each chunk's values
+// are read at once (independent LDS reads), the pass runs on them in registers with the running
+// value carried across chunks, and the chunk is written back - the same operations in the same
+// order as spline_line, so the same bits, without an LDS write-then-read round trip per point
+template <int kCh>
+__device__ void spline_line_lds(double* c, int n, int s) {
+    const double z = sqrt(3.0) - 2.0;
+    const double gain = (1.0 - z) * (1.0 - 1.0 / z);
+    double v[kCh], u[kCh];
+    for (int i0 = 0; i0 < n; i0 += kCh) {  // the gain
+        const int m = min(kCh, n - i0);
+#pragma unroll
+        for (int k = 0; k < kCh; ++k)
+            if (k < m) v[k] = c[(i0 + k) * s];
+#pragma unroll
+        for (int k = 0; k < kCh; ++k)
+            if (k < m) c[(i0 + k) * s] = v[k] * gain;
+    }
+    if (n == 1) return;
+    const double zn1 = pow(z, (double)(n - 1));
+    // the mirror-symmetric causal initialisation: c0 = c[0] + zn1 c[n-1] + sum_i z^i (c[i] + zn1 c[n-1-i])
+    double c0 = c[0] + zn1 * c[(n - 1) * s];
+    double zi = z;
+    for (int i0 = 1; i0 < n - 1; i0 += kCh) {
+        const int m = min(kCh, n - 1 - i0);
+#pragma unroll
+        for (int k = 0; k < kCh; ++k)
+            if (k < m) {
+                v[k] = c[(i0 + k) * s];
+                u[k] = c[(n - 1 - i0 - k) * s];
+            }
+#pragma unroll
+        for (int k = 0; k < kCh; ++k)
+            if (k < m) {
+                c0 += zi * (v[k] + zn1 * u[k]);
+                zi *= z;
+            }
+    }
+    double prev = c0 / (1.0 - zn1 * zn1);
+    c[0] = prev;
+    for (int i0 = 1; i0 < n; i0 += kCh) {  // causal: c[i] += z c[i-1]
+        const int m = min(kCh, n - i0);
+#pragma unroll
+        for (int k = 0; k < kCh; ++k)
+            if (k < m) v[k] = c[(i0 + k) * s];
+#pragma unroll
+        for (int k = 0; k < kCh; ++k)
+            if (k < m) {
+                v[k] += z * prev;
+                prev = v[k];
+            }
+#pragma unroll
+        for (int k = 0; k < kCh; ++k)
+            if (k < m) c[(i0 + k) * s] = v[k];
+    }
+    // anti-causal: c[n-1] from the last two, then c[i] = z (c[i+1] - c[i]) downwards
+    double next = (z * c[(n - 2) * s] + prev) * z / (z * z - 1.0);
+    c[(n - 1) * s] = next;
+    for (int i0 = n - 2; i0 >= 0; i0 -= kCh) {
+        const int m = min(kCh, i0 + 1);
+#pragma unroll
+        for (int k = 0; k < kCh; ++k)
+            if (k < m) v[k] = c[(i0 - k) * s];
+#pragma unroll
+        for (int k = 0; k < kCh; ++k)
+            if (k < m) {
+                v[k] = z * (next - v[k]);
+                next = v[k];
+            }
+#pragma unroll
+        for (int k = 0; k < kCh; ++k)
+            if (k < m) c[(i0 - k) * s] = v[k];
+    }
+}
+
+// spline_filter1d along one axis in LDS: a workgroup of 256 threads takes kSplineLines lines of
+// one array (blockIdx.y: map, mask), loads them with all its threads (eight independent loads in
+// flight per thread), runs each line's recursion on one thread (spline_line_lds), stores them back.
+// Lines of up to 256 points.
+constexpr int kSplineLines = 16, kSplineMaxLen = 256, kSplineThreads = 256;
 __global__ void __launch_bounds__(kSplineThreads) k_spline_block(double* __restrict__ coef, int ny, int nx, int axis) {
     __shared__ double buf[kSplineMaxLen * (kSplineLines + 1)];
     const int nlines = axis == 0 ? nx : ny, len = axis == 0 ? ny : nx;
     const int l0 = blockIdx.x * kSplineLines, nl = min(kSplineLines, nlines - l0);
     double* base = coef + (int64_t)blockIdx.y * ny * nx;
     const int P = kSplineLines + 1;  // buf[i * P + l]: point i of line l
-    for (int e = threadIdx.x; e < len * nl; e += blockDim.x) {
+    const int total = len * nl;
+    auto gidx = [&](int e, int& bi) {
         int i, l;
-        if (axis == 0) { i = e / nl; l = e - (e / nl) * nl; }  // columns: read along rows (coalesced)
+        if (axis == 0) { i = e / nl; l = e - (e / nl) * nl; }  // columns: read along rows (coalesced pieces)
         else { l = e / len; i = e - (e / len) * len; }         // rows: read along the row
-        const int64_t gi = axis == 0 ? (int64_t)i * nx + (l0 + l) : (int64_t)(l0 + l) * nx + i;
-        buf[i * P + l] = base[gi];
+        bi = i * P + l;
+        return axis == 0 ? (int64_t)i * nx + (l0 + l) : (int64_t)(l0 + l) * nx + i;
+    };
+    for (int e0 = 0; e0 < total; e0 += 8 * kSplineThreads) {
+        double t[8];
+        int bi[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int e = e0 + k * kSplineThreads + (int)threadIdx.x;
+            if (e < total) t[k] = base[gidx(e, bi[k])];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (e0 + k * kSplineThreads + (int)threadIdx.x < total) buf[bi[k]] = t[k];
     }
     __syncthreads();
-    if ((int)threadIdx.x < nl) spline_line(buf + threadIdx.x, len, P);
+    if ((int)threadIdx.x < nl) spline_line_lds<16>(buf + threadIdx.x, len, P);
     __syncthreads();
-    for (int e = threadIdx.x; e < len * nl; e += blockDim.x) {
-        int i, l;
-        if (axis == 0) { i = e / nl; l = e - (e / nl) * nl; }
-        else { l = e / len; i = e - (e / len) * len; }
-        const int64_t gi = axis == 0 ? (int64_t)i * nx + (l0 + l) : (int64_t)(l0 + l) * nx + i;
-        base[gi] = buf[i * P + l];
+    for (int e = threadIdx.x; e < total; e += kSplineThreads) {
+        int bi;
+        const int64_t gi = gidx(e, bi);
+        base[gi] = buf[bi];
     }
 }
 
 __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
-    __shared__ double smem[kSplineLds];  // the nanmean's trees, later one prefilter array
-    static_assert(8 * sizeof(PwTree) <= sizeof(smem), "nanmean trees in the prefilter buffer");
-    PwTree* trees = reinterpret_cast<PwTree*>(smem);
+    __shared__ double smem[kPostLds];  // the map, then matrixWave2 - nanmean (when it fits)
+    __shared__ PwTree trees[2];        // the nanmean's pairwise trees (waves 0 and 1)
     __shared__ double bufsum[8];
     __shared__ int firstrow[2];
     __shared__ double red[kPostThreads / 64][kMomMax];
@@ -446,26 +589,48 @@ __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
         for (int j = tid; j < a.nx; j += kPostThreads) bX[j] = a.nx > 1 ? (2.0 * j - (a.nx - 1)) / (double)(a.nx - 1) : 0.0;
         for (int i = tid; i < a.ny; i += kPostThreads) bY[i] = a.ny > 1 ? (2.0 * i - (a.ny - 1)) / (double)(a.ny - 1) : 0.0;
     }
+    // the map into LDS when it fits: every thread's loads in flight at once (the passes below then
+    // wait for LDS only)
+    const bool in_lds = total <= kPostLds;
+    if (in_lds) {
+        for (int64_t k0 = 0; k0 < total; k0 += 16 * kPostThreads) {
+            double t[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int64_t k = k0 + q * kPostThreads + tid;
+                if (k < total) t[q] = a.m[k];
+            }
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int64_t k = k0 + q * kPostThreads + tid;
+                if (k < total) smem[k] = t[q];
+            }
+        }
+        __syncthreads();
+    }
+    const double* src = in_lds ? smem : a.m;
     // np.nanmean: numpy's pairwise sum of the NaN-zeroed map, one wave per 8192-element buffer
+    // (waves 0 and 1 alternate over the buffers)
     const int nbuf = (int)((total + 8191) / 8192);
-    if (w < nbuf) {
-        const int64_t b0 = (int64_t)w * 8192;
-        const int len = (int)(total - b0 < 8192 ? total - b0 : 8192);
-        const double v = pw_tree_wave<true>(trees[w], a.m + b0, len);
-        if ((tid & 63) == 0) bufsum[w] = v;
+    if (w < 2) {
+        for (int b = w; b < nbuf; b += 2) {
+            const int64_t b0 = (int64_t)b * 8192;
+            const int len = (int)(total - b0 < 8192 ? total - b0 : 8192);
+            const double v = pw_tree_wave<true>(trees[w], src + b0, len);
+            if ((tid & 63) == 0) bufsum[b] = v;
+            wave_sync();
+        }
     }
     double cnt[1] = {0.0};
-    for (int64_t k = tid; k < total; k += kPostThreads) cnt[0] += a.m[k] == a.m[k] ? 1.0 : 0.0;
+    for (int64_t k = tid; k < total; k += kPostThreads) cnt[0] += src[k] == src[k] ? 1.0 : 0.0;
     block_sum<1>(cnt, (double(*)[1])red);
     double tot = 0.0;
     for (int b = 0; b < nbuf; ++b) tot = tot + bufsum[b];
     const double mean = tot / cnt[0];
-    // matrixWave2 - nanmean, the plane correction's input: in LDS when it fits (the trees are done
-    // with; the moment passes then read it there), else in `corrected`
-    const bool in_lds = total <= kSplineLds;
+    // matrixWave2 - nanmean, the plane correction's input: in LDS when it fits, else in `corrected`
     double* cm = in_lds ? smem : a.corrected;
     __syncthreads();
-    for (int64_t k = tid; k < total; k += kPostThreads) cm[k] = a.m[k] - mean;
+    for (int64_t k = tid; k < total; k += kPostThreads) cm[k] = src[k] - mean;
     __syncthreads();
     // plane_correction_with_nan_and_outlier_filter: the four moment passes of k_moments
     auto moments = [&](int nb, const double* cf, double thr, int mode, double mu, double (&acc)[kMomMax]) {
@@ -507,17 +672,21 @@ __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
         block_sum<kMomMax>(acc, red);
     };
     // the normal equations of nb terms from the moment slots (pupilmap._normal_solve) into sys[25..]
-    auto normal_solve = [&](const double (&mom)[kMomMax], int nb, int at) {
+    auto normal_solve = [&](const double (&mom)[kMomMax], auto nbc, int at) {
+        constexpr int nb = decltype(nbc)::value;
         if (tid == 0) {
-            double A[25], b[5];
+            double A[nb][nb], b[nb];
+#pragma unroll
             for (int r = 0; r < nb; ++r) {
+#pragma unroll
                 for (int c = 0; c < nb; ++c) {
                     const int lo = r < c ? r : c, hi = r < c ? c : r;
-                    A[r * nb + c] = mom[lo * 5 - lo * (lo - 1) / 2 + (hi - lo)];
+                    A[r][c] = mom[lo * 5 - lo * (lo - 1) / 2 + (hi - lo)];
                 }
                 b[r] = mom[15 + r];
             }
-            if (!solve_small(A, b, nb)) sflag |= 2;
+            if (!solve_small_reg<nb>(A, b)) sflag |= 2;
+#pragma unroll
             for (int r = 0; r < nb; ++r) sys[at + r] = b[r];
         }
         __syncthreads();
@@ -526,14 +695,14 @@ __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
     double acc[kMomMax];
     moments(5, nullptr, 0.0, 0, 0.0, acc);
     if (tid == 0 && acc[20] < 5) sflag |= 1;  // curve_fit refuses fewer points than parameters
-    normal_solve(acc, 5, 0);                  // c1 = sys[0..5)
+    normal_solve(acc, std::integral_constant<int, 5>{}, 0);  // c1 = sys[0..5)
     moments(5, sys, 0.0, 1, 0.0, acc);
     const double n1 = acc[20], mu = acc[0] / acc[20];
     moments(5, sys, 0.0, 2, mu, acc);
     const double thr = a.sigma * sqrt(acc[0] / n1);
     moments(3, sys, thr, 0, 0.0, acc);
     if (tid == 0 && acc[20] < 3) sflag |= 1;
-    normal_solve(acc, 3, 8);                  // p2 = sys[8..11)
+    normal_solve(acc, std::integral_constant<int, 3>{}, 8);  // p2 = sys[8..11)
     for (int64_t k = tid; k < total; k += kPostThreads) {
         const int i = (int)k / a.nx, j = (int)k - ((int)k / a.nx) * a.nx;
         double f[5];
