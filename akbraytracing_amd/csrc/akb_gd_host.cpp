@@ -19,7 +19,6 @@
 
 #include <algorithm>
 #include <functional>
-#include <thread>
 #include <utility>
 #include <vector>
 
@@ -158,8 +157,7 @@ __attribute__((target("avx512f,avx512dq"))) int64_t best_avx512(const double* X,
 
 // the first m in (p, q) with the smallest cot (a strict '<' scan's pick); best_cot receives it
 int64_t best_chain_point(const double* X, const double* Y, int64_t p, int64_t q, double* tmp, double& best_cot) {
-    static const int isa = getenv("AKB_GD_NO_AVX512") ? 1  // A/B: the two-pass AVX2 scan
-                           : __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512dq") ? 2
+    static const int isa = __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512dq") ? 2
                            : __builtin_cpu_supports("avx2")                                       ? 1
                                                                                                   : 0;
     if (isa == 2) {
@@ -381,27 +379,7 @@ int akb_gd_pockets(const double* rx, const double* ry, int nv, int nh, int cap, 
             chords[2 * (size_t)id + 1] = {q % L, vp};
         }
     };
-    {
-        static const bool threaded = getenv("AKB_GD_POCKET_THREADS") != nullptr;
-        std::vector<std::thread> threads;
-        std::vector<std::vector<Job>> stacks;
-        std::vector<std::vector<double>> cots;
-        if (threaded) {
-            size_t big = 0;
-            for (auto& P : pockets) big += P.q - P.p >= 512;
-            stacks.resize(big);
-            cots.resize(big);
-            size_t k = 0;
-            for (auto& P : pockets)
-                if (P.q - P.p >= 512) {
-                    threads.emplace_back(fill, std::ref(P), std::ref(stacks[k]), std::ref(cots[k]));
-                    ++k;
-                }
-        }
-        for (auto& P : pockets)
-            if (!threaded || P.q - P.p < 512) fill(P, w.stack, w.cot);
-        for (auto& t : threads) t.join();
-    }
+    for (auto& P : pockets) fill(P, w.stack, w.cot);
     for (size_t k = pockets.size(); k-- > 0;) {
         const Pocket& P = pockets[k];
         if (P.err) {

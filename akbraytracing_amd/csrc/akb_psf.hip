@@ -1215,7 +1215,6 @@ static int line_wgs(int ngroups) {
     if (per_cu > by_threads) per_cu = by_threads;
     if (per_cu < 1) per_cu = 1;
     int w = 256 * per_cu;
-    if (const char* e = getenv("AKB_PSF_LINE_WGS")) w = atoi(e) > 0 ? atoi(e) : w;
     if (ngroups < w) w = ngroups >= 8 ? ngroups / 8 * 8 : ngroups;
     return w;
 }

@@ -621,8 +621,27 @@ __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
             wave_sync();
         }
     }
+    // the finite count, and the map's range (np.nanmin / np.nanmax: the cone solve's error estimate
+    // is held to it, FaithfulPupil)
     double cnt[1] = {0.0};
-    for (int64_t k = tid; k < total; k += kPostThreads) cnt[0] += src[k] == src[k] ? 1.0 : 0.0;
+    double lo = INFINITY, hi = -INFINITY;
+    for (int64_t k = tid; k < total; k += kPostThreads) {
+        const double v = src[k];
+        if (v == v) {
+            cnt[0] += 1.0;
+            lo = fmin(lo, v);
+            hi = fmax(hi, v);
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        lo = fmin(lo, __shfl_down(lo, off));
+        hi = fmax(hi, __shfl_down(hi, off));
+    }
+    __shared__ double ext[kPostThreads / 64][2];
+    if ((tid & 63) == 0) {
+        ext[w][0] = lo;
+        ext[w][1] = hi;
+    }
     block_sum<1>(cnt, (double(*)[1])red);
     double tot = 0.0;
     for (int b = 0; b < nbuf; ++b) tot = tot + bufsum[b];
@@ -761,6 +780,13 @@ __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
         P[10] = thr;
         for (int q = 0; q < 6; ++q) P[11 + q] = sys[16 + q];
         P[17] = (double)sflag;
+        double mn = ext[0][0], mx = ext[0][1];
+        for (int q = 1; q < kPostThreads / 64; ++q) {
+            mn = fmin(mn, ext[q][0]);
+            mx = fmax(mx, ext[q][1]);
+        }
+        P[18] = mn;
+        P[19] = mx;
     }
 }
 

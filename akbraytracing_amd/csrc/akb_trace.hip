@@ -1386,45 +1386,13 @@ using namespace akb;
 
 static inline V3In v3in(const double* p, int64_t ld, int64_t inc) { return V3In{p, ld, inc}; }
 
-// occupancy variant of the chain kernels (minimum waves per SIMD the register allocator must
-// allow); AKB_CHAIN_WAVES in the environment selects one for A/B timing, default 4. RayWave's pass
-// 2 (the fixed-output sink variant) has its own knob, AKB_PASS2_WAVES, default 4: 89 VGPRs and no
-// scratch (6 waves: 80 VGPRs and 8 spilled; both 0.358 ms in the 100 / 30-step bench after the
-// wave-guarded division and sqrt; 8 - 64 VGPRs and 160 B of spills - measured slower)
-static int waves_from_env(const char* name, int dflt) {
-    const char* e = getenv(name);
-    const int v = e ? atoi(e) : dflt;
-    return (v == 2 || v == 4 || v == 6 || v == 8) ? v : dflt;
-}
-static int chain_waves() {
-    static int w = waves_from_env("AKB_CHAIN_WAVES", 4);
-    return w;
-}
-static int pass2_waves() {
-    static int w = waves_from_env("AKB_PASS2_WAVES", 4);
-    return w;
-}
-
-// workgroups per chain launch (each walks 256-ray segments grid-stride); AKB_CHAIN_GRID in the
-// environment overrides the default for A/B timing
-static int64_t chain_grid_cap() {
-    static int64_t g = [] {
-        const char* e = getenv("AKB_CHAIN_GRID");
-        const long long v = e ? atoll(e) : 0;
-        return (int64_t)(v >= 256 ? v : 256 * 32);  // 8192: measured best for both passes
-    }();
-    return g;
-}
-
-// workgroup cap of the OPD kernel (AKB_OPD_GRID overrides, for A/B timing)
-static int64_t opd_grid_cap() {
-    static int64_t g = [] {
-        const char* e = getenv("AKB_OPD_GRID");
-        const long long v = e ? atoll(e) : 0;
-        return (int64_t)(v >= 256 ? v : 2048);  // measured best: the extent atomics grow with the grid
-    }();
-    return g;
-}
+// the chain kernels at 4 waves per SIMD (the register allocator's floor; pass 2's fixed-output
+// sink: 89 VGPRs and no scratch; 6 waves spilled 8 VGPRs and was no faster, 8 spilled 160 B and
+// was slower), workgroups capped at 8192 (each walks 256-ray segments grid-stride; measured best
+// for both passes); the OPD kernel at 2048 (its extent atomics grow with the grid)
+constexpr int kChainWaves = 4;
+constexpr int64_t kChainGridCap = 256 * 32;
+constexpr int64_t kOpdGridCap = 2048;
 
 template <bool kGrid, bool kOPL, bool kSink>
 static void launch_chain(int w, unsigned g, hipStream_t s, const ChainArgs& a) {
@@ -1438,36 +1406,18 @@ static void launch_chain(int w, unsigned g, hipStream_t s, const ChainArgs& a) {
     const bool fixed = kGrid && kOPL && point && a.last_hit && a.dir_out && a.opl && !a.det_out && !a.atan_h &&
                        !a.atan_v && !a.samp_h && !a.samp_v && !a.hits;
     if (kSink && fixed) {
-        switch (pass2_waves()) {
-            case 4:
-                k_chain_sink<kGrid, kOPL, 4, kGrid, kGrid && kOPL><<<g, kBlock, 0, s>>>(a);
-                break;
-            case 6:
-                k_chain_sink<kGrid, kOPL, 6, kGrid, kGrid && kOPL><<<g, kBlock, 0, s>>>(a);
-                break;
-            default:
-                k_chain_sink<kGrid, kOPL, 8, kGrid, kGrid && kOPL><<<g, kBlock, 0, s>>>(a);
-        }
+        k_chain_sink<kGrid, kOPL, kChainWaves, kGrid, kGrid && kOPL><<<g, kBlock, 0, s>>>(a);
         return;
     }
-#define AKB_CHAIN_CASE(W)                                                        \
-    case W:                                                                      \
-        if (kSink && point)                                                      \
-            k_chain_sink<kGrid, kOPL, W, kGrid><<<g, kBlock, 0, s>>>(a);         \
-        else if (kSink)                                                          \
-            k_chain_sink<kGrid, kOPL, W, false><<<g, kBlock, 0, s>>>(a);         \
-        else if (point)                                                          \
-            k_chain<kGrid, kOPL, W, false, kGrid><<<g, kBlock, 0, s>>>(a);       \
-        else                                                                     \
-            k_chain<kGrid, kOPL, W, false, false><<<g, kBlock, 0, s>>>(a);       \
-        break;
-    switch (w) {
-        AKB_CHAIN_CASE(2)
-        AKB_CHAIN_CASE(8)
-        default:
-            AKB_CHAIN_CASE(4)
-    }
-#undef AKB_CHAIN_CASE
+    (void)w;
+    if (kSink && point)
+        k_chain_sink<kGrid, kOPL, kChainWaves, kGrid><<<g, kBlock, 0, s>>>(a);
+    else if (kSink)
+        k_chain_sink<kGrid, kOPL, kChainWaves, false><<<g, kBlock, 0, s>>>(a);
+    else if (point)
+        k_chain<kGrid, kOPL, kChainWaves, false, kGrid><<<g, kBlock, 0, s>>>(a);
+    else
+        k_chain<kGrid, kOPL, kChainWaves, false, false><<<g, kBlock, 0, s>>>(a);
 }
 
 extern "C" {
@@ -1702,9 +1652,9 @@ int akb_trace_chain_f64(const akb_chain_desc* d, void* stream) {
     const bool grid = d->dir == nullptr;
     const bool sink = d->sink.nq > 0;
     hipStream_t s = (hipStream_t)stream;
-    const int64_t gcap = chain_grid_cap();
+    const int64_t gcap = kChainGridCap;
     const unsigned gsz = grid_for(d->n_rays, 1, gcap);
-    const int w = chain_waves();
+    const int w = kChainWaves;
     if (sink) {
         const int64_t nseg = (d->n_rays + kLeafSeg - 1) / kLeafSeg;
         const unsigned gs = (unsigned)(nseg < gcap ? nseg : gcap);
@@ -2041,7 +1991,7 @@ static int chain_tilt(const akb_chain_desc* d, const double* d_params, const dou
                         sink);
     if (st != AKB_OK || empty) return st;
     const int64_t nseg = (n + kLeafSeg - 1) / kLeafSeg;
-    const int64_t gcap = chain_grid_cap();
+    const int64_t gcap = kChainGridCap;
     const unsigned gs = (unsigned)(nseg < gcap ? nseg : gcap);
     hipStream_t s = (hipStream_t)stream;
     const OpdRows no{};
@@ -2050,19 +2000,7 @@ static int chain_tilt(const akb_chain_desc* d, const double* d_params, const dou
         k_chain_tilt<W, true><<<gs, kBlock, 0, s>>>(a, b, *o);     \
     else                                                           \
         k_chain_tilt<W, false><<<gs, kBlock, 0, s>>>(a, b, no);
-    switch (chain_waves()) {
-        case 2:
-            AKB_CT(2)
-            break;
-        case 6:
-            AKB_CT(6)
-            break;
-        case 8:
-            AKB_CT(8)
-            break;
-        default:
-            AKB_CT(4)
-    }
+    AKB_CT(kChainWaves)
 #undef AKB_CT
     return launch_status("k_chain_tilt");
 }
@@ -2121,7 +2059,7 @@ int akb_opd_f64(const double* total1, const double* total2, const double* det2, 
     a.sph = sph;
     a.wave = wave;
     a.ext = (unsigned long long*)d_extent_keys;
-    k_opd<<<grid_for(n, 1, opd_grid_cap()), kBlock, 0, s>>>(a);
+    k_opd<<<grid_for(n, 1, kOpdGridCap), kBlock, 0, s>>>(a);
     return launch_status("k_opd");
 }
 

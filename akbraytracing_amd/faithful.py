@@ -31,10 +31,10 @@ import torch
 
 from . import _lib
 from . import device as D
-from .griddata import CONE_SWEEPS, _F_NEG, _F_NONCONVEX, _F_NONFINITE, _F_NOT_DELAUNAY, _F_POCKET, _F_POS
-from .griddata import chebyshev_weights
+from .griddata import CONE_GUARD, CONE_SWEEPS, _F_NEG, _F_NONCONVEX, _F_NONFINITE, _F_NOT_DELAUNAY, _F_POCKET, _F_POS
+from .griddata import ConeNotConverged, CubicGrid, chebyshev_weights
 from .psf import psf_stack
-from .pupilmap import pupil_post, pupil_post_check
+from .pupilmap import POST_PARAMS, pupil_post, pupil_post_check
 
 EUV = 13.5e-9  # option_energy 'EUV' (:1161-1162)
 
@@ -111,7 +111,19 @@ class Ticket:
         st = int(w[:1].view(np.int64)[0])
         if st & (_F_NOT_DELAUNAY | _F_POCKET):
             raise _lib.AKBError("griddata: the grid is too distorted for the structured Delaunay triangulation")
-        pupil_post_check(w[1:])
+        pupil_post_check(w[3:])
+        cone_guard(w[2], w[3:])
+
+
+def cone_guard(est, params):
+    """Raise ConeNotConverged when the cone solve's value-error estimate (k_gd_cone_patch: 2 sqrt2
+    x the corners' one-more-sweep step x the cell size) exceeds CONE_GUARD of the gridded map's
+    range (the post block's nanmin / nanmax)."""
+    rng = float(params[19]) - float(params[18])
+    if not (est <= CONE_GUARD * rng):
+        raise ConeNotConverged(f"griddata: the cone solve's {CONE_SWEEPS}-sweep gradients leave a value error "
+                               f"estimate of {est:.3g} ({est / rng if rng > 0 else float('nan'):.2e} of the map's "
+                               f"range, bar {CONE_GUARD:g}); re-run with the converged gradients")
 
 
 class FaithfulPupil:
@@ -158,8 +170,9 @@ class FaithfulPupil:
         self._done = None  # the latest finish's end (finishes share work / map / pupil / psf buffers)
         self._omegas = D.host_f64(chebyshev_weights(max(self.sweeps, 1)))
         self.pool = concurrent.futures.ThreadPoolExecutor(max_workers=int(workers), thread_name_prefix="akb-pockets")
-        # per run: the pocket status word (int64 bits) | the post parameter block's first 18 words
-        self.errors = ErrorLog(1 + 18)
+        # per run: the pocket status word (int64 bits) | the cone's change and error estimate | the post
+        # parameter block
+        self.errors = ErrorLog(1 + 2 + POST_PARAMS)
         self.finished = 0  # runs through finish()
 
     # ------------------------------------------------------------------ stage 1
@@ -274,7 +287,7 @@ class FaithfulPupil:
             self.psf = psf
             if events is not None:
                 events[1].record(st)
-            t.erow = self.errors.record((s["status"].view(D.F64), post["params"][:18]), st)
+            t.erow = self.errors.record((s["status"].view(D.F64), self.change.view(D.F64), post["params"]), st)
             t.done = torch.cuda.Event()
             t.done.record(st)
             self._done = t.done
@@ -286,8 +299,34 @@ class FaithfulPupil:
         return t.result
 
     def run(self, y, z, f, stream=None):
-        """begin + finish of one run (the pocket job waited for at once)."""
-        return self.finish(self.begin(y, z, f, stream), stream)
+        """begin + finish + check of one run (the pocket job waited for at once). A run whose cone
+        solve fails its guard (ConeNotConverged) is formed again from the converged gradients
+        (CubicGrid.interp: the global sweeps to scipy's tolerance) on the same axes."""
+        t = self.begin(y, z, f, stream)
+        r = self.finish(t, stream)
+        try:
+            t.check()
+        except ConeNotConverged:
+            r = self._converged(y, z, f, stream)
+        return r
+
+    def _converged(self, y, z, f, stream=None):
+        """The run's map from the global gradient iteration (host-synchronous), then the same post
+        and PSF on the device; the result in finish's buffers."""
+        st = torch.cuda.current_stream() if stream is None else stream
+        m = self.size
+        with torch.cuda.stream(st):
+            cg = CubicGrid(y, z, self.nv, self.nh, delaunay_tol=self.tol)
+            ax = self.axes
+            self.map[0].copy_(cg.interp(f.reshape(1, -1), ax[:m], ax[m:2 * m])[0])
+            post = pupil_post(self.map[0], out=self.post, stream=st)
+            self.post = post
+            psf, _, _ = psf_stack(post["opd"], None, self.lams, None, pad_factor=self.pad, stream=st, out=self.psf,
+                                  pitch=ax[2 * m + 4:2 * m + 6])
+            self.psf = psf
+        pupil_post_check(post["params"])
+        return dict(psf=psf, map=self.map[0], corrected=post["corrected"], rotated=post["rotated"],
+                    params=post["params"], axes=self.axes, change=self.change, converged=True)
 
     def close(self):
         self.pool.shutdown(wait=True)

@@ -33,7 +33,8 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from .faithful import ErrorLog, pack_pockets
+from .faithful import ErrorLog, cone_guard, pack_pockets
+from .pupilmap import POST_PARAMS
 from .griddata import CONE_SWEEPS, _F_NEG, _F_NONCONVEX, _F_NONFINITE, _F_NOT_DELAUNAY, _F_POCKET, _F_POS
 from .wavefront import Shard
 
@@ -301,7 +302,7 @@ class ShardedFaithfulPupil:
             s = dict(win=torch.zeros((3, p.nrows * n), dtype=D.F64, device=self.dev),
                      diag=torch.zeros(max(p.nrows - 1, 1) * (n - 1), dtype=torch.uint8, device=self.dev),
                      flags=torch.zeros(1, dtype=torch.int32, device=self.dev),
-                     rflags=torch.zeros(comm.world, dtype=D.F64, device=self.dev), last=None)
+                     rflags=torch.zeros(2 * comm.world, dtype=D.F64, device=self.dev), last=None)
             if p.is_root:
                 s.update(ring=torch.zeros(2 * Lr + 1, dtype=D.F64, device=self.dev),
                          ring_host=torch.empty(2 * Lr + 1, dtype=D.F64, pin_memory=True),
@@ -316,7 +317,8 @@ class ShardedFaithfulPupil:
         self.owner = torch.empty(m, dtype=torch.int32, device=self.dev)
         self.axes = torch.zeros(2 * self.size + 6, dtype=D.F64, device=self.dev)  # gx | gy | extent | pitch
         # map piece | count | every rank's cell flags (slot r): one SUM reduction to the band owner
-        self.red = torch.zeros(2 * m + comm.world, dtype=D.F64, device=self.dev)
+        # | every rank's cone error estimate (slot world + r)
+        self.red = torch.zeros(2 * m + 2 * comm.world, dtype=D.F64, device=self.dev)
         self.map = torch.empty((1, self.size, self.size), dtype=D.F64, device=self.dev)
         self.change = torch.zeros(2, dtype=torch.int64, device=self.dev)  # change measure | value-error estimate
         self.post, self.psf = {}, None
@@ -326,7 +328,7 @@ class ShardedFaithfulPupil:
         self.flags_all = 0
         self._done = None  # the latest finish's end (finishes share work / owner / map / psf buffers)
         # per run (band owner): every rank's cell flags | the pocket status word | the post block's 18 words
-        self.errors = ErrorLog(comm.world + 1 + 18) if p.is_root else None
+        self.errors = ErrorLog(2 * comm.world + 1 + 2 + POST_PARAMS) if p.is_root else None
         self.finished = 0
 
     @staticmethod
@@ -465,6 +467,7 @@ class ShardedFaithfulPupil:
                                               D.ptr(self.change), sh))
             red[2 * mm:].zero_()
             red[2 * mm + p.rank] = s["flags"][0].to(D.F64)
+            red[2 * mm + self.comm.world + p.rank] = self.change.view(D.F64)[1]
             _reduce_sum(self.comm, red, p.root, self.group)
             res = None
             if p.is_root:
@@ -482,7 +485,8 @@ class ShardedFaithfulPupil:
                 self.psf = psf
                 res = dict(psf=psf, map=self.map[0], corrected=post["corrected"], rotated=post["rotated"],
                            params=post["params"], axes=self.axes, change=self.change)
-                t.erow = self.errors.record((s["rflags"], s["status"].view(D.F64), post["params"][:18]), st)
+                t.erow = self.errors.record((s["rflags"], s["status"].view(D.F64), self.change.view(D.F64),
+                                             post["params"]), st)  # rflags: the flags | the estimates
             if events is not None:
                 events[1].record(st)
             t.done = torch.cuda.Event()
@@ -511,6 +515,8 @@ class ShardedFaithfulPupil:
         fl = 0
         for v in w[:world]:
             fl |= int(v)
+        est = float(np.max(w[world:2 * world]))  # every rank's interior targets
+        w = np.concatenate([w[:world], w[2 * world:]])
         self.flags_all = fl
         if fl & _F_NONFINITE:
             raise ValueError("griddata: non-finite point coordinates (a ray that missed)")
@@ -520,7 +526,8 @@ class ShardedFaithfulPupil:
             raise _lib.AKBError("griddata: the grid is too distorted for the structured Delaunay triangulation")
         if int(w[world:world + 1].view(np.int64)[0]) & (_F_NOT_DELAUNAY | _F_POCKET):
             raise _lib.AKBError("griddata: the grid is too distorted for the structured Delaunay triangulation")
-        pupil_post_check(w[world + 1:])
+        pupil_post_check(w[world + 3:])
+        cone_guard(est, w[world + 3:])
 
     def run(self, y, z, f, stream=None):
         """begin + finish + check of one run: (result or None, ticket)."""

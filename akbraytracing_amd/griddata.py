@@ -42,6 +42,16 @@ GRADIENT_TOL = 1e-6
 CONE_SWEEPS = 12
 
 
+# The cone solve's guard (FaithfulPupil, Ticket.check): its value-error estimate at the interior
+# target cells (akb_gd_cone_eval_f64's d_change[1]) must stay within this fraction of the gridded
+# map's range - the parity bar of the gridding against scipy (tests/test_fullsize_gpu.py).
+CONE_GUARD = 1e-6
+
+
+class ConeNotConverged(_lib.AKBError):
+    """The fixed-K cone solve's error estimate exceeds CONE_GUARD of the map's range."""
+
+
 def chebyshev_weights(count, rho=0.5):
     """omegas[k]: the weight of the sweep that reads x_k (omegas[0] unused: a plain first sweep),
     Chebyshev semi-iteration for a Jacobi spectrum in [-rho, rho]."""

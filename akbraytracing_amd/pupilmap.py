@@ -194,7 +194,7 @@ def wave_pupil(detcenter2, wave2, ray_num_H, ray_num_V, grid_num_H=None, grid_nu
     return _plane_corrections([m_wave.contiguous()])[0], grid_H, grid_V, cg.sweeps
 
 
-POST_PARAMS = 18  # akb_pupil_post_f64's parameter block (include/akb_raytrace.h)
+POST_PARAMS = 20  # akb_pupil_post_f64's parameter block (include/akb_raytrace.h)
 
 
 def pupil_post(m, sigma_threshold=3, out=None, stream=None):
@@ -204,7 +204,7 @@ def pupil_post(m, sigma_threshold=3, out=None, stream=None):
     m: (ny, nx) device map, ny * nx <= 65536. out: optional dict of preallocated buffers.
     Returns dict(corrected, rotated, opd, params) of device tensors; params[17] holds error flags
     (bit 0: too few points for the fits, bit 1: a singular normal system), read by the caller when
-    it can wait (pupil_post_check)."""
+    it can wait (pupil_post_check); params[18], [19]: the input map's nanmin and nanmax."""
     L = _lib.lib()
     m = _as_dev(m)
     ny, nx = int(m.shape[0]), int(m.shape[1])

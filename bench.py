@@ -625,7 +625,7 @@ def main():
                 break
     for _ in range(args.warmup):
         step(False)
-    rw.kernel_events = [] if os.environ.get("AKB_BENCH_NO_KEVENTS", "0") == "0" else None
+    rw.kernel_events = []
     fp_events.clear()
     psf_events.clear()
     # host_ms: host time spent issuing each step (its waits included): is the host the limit?

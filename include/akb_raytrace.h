@@ -428,9 +428,9 @@ int akb_rotate_with_nan_f64(const double* m, int ny, int nx, const double rot[4]
  * :1121-1188): corrected = plane_correction_with_nan_and_outlier_filter(map - nanmean(map), sigma),
  * psf_calc's rotation estimate, rotated = rotate_with_nan(corrected, degrees(rot), order 3)
  * (cephes cosdg / sindg for scipy.ndimage.rotate's matrix), opd = rotated * 1e-9. work: 2 ny nx
- * doubles. d_params (18 doubles): nanmean, finite count, the quadratic fit (5), the plane (3), the
+ * doubles. d_params (20 doubles): nanmean, finite count, the quadratic fit (5), the plane (3), the
  * outlier threshold, rot, its degrees, cos, sin, the rotation's offset (2), error flags (bit 0: too
- * few points for curve_fit, bit 1: a singular normal system). Replaces pupilmap._plane_corrections
+ * few points for curve_fit, bit 1: a singular normal system), nanmin and nanmax of the input map. Replaces pupilmap._plane_corrections
  * + psfcalc.rotation_estimate / rotate_with_nan where a pipelined caller cannot wait on the host. */
 int akb_pupil_post_f64(const double* map, int ny, int nx, double sigma, double* corrected, double* rotated,
                        double* opd, void* work, double* d_params, void* stream);

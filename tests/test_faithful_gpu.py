@@ -112,3 +112,57 @@ def test_faithful_pipeline_raises_for_a_missed_ray(gpu):
     with pytest.raises(ValueError):
         fp_.finish(t)
     fp_.close()
+
+
+def _guard_case(geom, n, sweeps=None):
+    """One run of geom at n^2 through FaithfulPupil: (its map and value-error estimate, the map from
+    the converged gradients on the same axes, the map's range)."""
+    from akbraytracing_amd.faithful import FaithfulPupil
+    from akbraytracing_amd.griddata import CubicGrid
+    from akbraytracing_amd.wavefront import RayWave
+    out = RayWave(geom, n).run()
+    y, z, w = out["detcenter2"][1].contiguous(), out["detcenter2"][2].contiguous(), out["wave2"].contiguous()
+    fp = FaithfulPupil(n, n, slots=2, **({"sweeps": sweeps} if sweeps else {}))
+    t = fp.begin(y, z, w)
+    r = fp.finish(t)
+    got = r["map"].cpu().numpy().copy()
+    est = float(r["change"].cpu().numpy().view(np.float64)[1])
+    ax = r["axes"].cpu().numpy()
+    cg = CubicGrid(y, z, n, n)
+    ref = cg.interp(w.reshape(1, -1), ax[:128], ax[128:256], tol=1e-13).cpu().numpy()[0]
+    rng_ = float(np.nanmax(ref) - np.nanmin(ref))
+    return fp, t, got, est, ref, rng_, (y, z, w)
+
+
+@pytest.mark.slow
+def test_cone_guard_on_the_cycled_systems(gpu):
+    """The cone solve's fixed CONE_SWEEPS against the converged gradients on every system the bench
+    cycles (bench.system_variants of the C3 geometry), KB_debug's pair (configs[1]) and the C4 lattice
+    (10000^2): each map within 3e-7 of its range of the converged one, the kernel's value-error
+    estimate at least the error it reports on (interior targets) and inside the guard's bar, so
+    Ticket.check() passes. With too few sweeps the guard trips and FaithfulPupil.run() returns the
+    converged map instead."""
+    import bench
+    from akbraytracing_amd.griddata import CONE_GUARD, CONE_SWEEPS, ConeNotConverged
+    from akbraytracing_amd.wavefront import SystemGeometry
+    c3 = SystemGeometry.from_dict(golden_json("akb_geometry.json"))
+    cases = [(f"c3 system {i}", g, 1001) for i, g in enumerate(bench.system_variants(c3, 8))]
+    cases += [("c2 KB pair", SystemGeometry.from_dict(bench.geometry_dict("c2")), 1001), ("c4 lattice", c3, 10000)]
+    for name, g, n in cases:
+        fp, t, got, est, ref, rng_, _ = _guard_case(g, n)
+        t.check()  # the guard passes at CONE_SWEEPS
+        fp.close()
+        assert np.array_equal(np.isnan(got), np.isnan(ref)), name
+        err = float(np.nanmax(np.abs(got - ref)))
+        print(f"{name} at {n}^2: {CONE_SWEEPS} sweeps vs converged {err / rng_:.2e} of the range, "
+              f"estimate {est / rng_:.2e} (bar {CONE_GUARD:g})")
+        assert err <= 3e-7 * rng_, name
+        assert est <= CONE_GUARD * rng_, name
+    # too few sweeps: the estimate trips the guard; run() then forms the map from the converged gradients
+    fp, t, got, est, ref, rng_, (y, z, w) = _guard_case(c3, 1001, sweeps=3)
+    assert est > CONE_GUARD * rng_ and np.nanmax(np.abs(got - ref)) > 1e-6 * rng_
+    with pytest.raises(ConeNotConverged):
+        t.check()
+    r = fp.run(y, z, w)
+    assert r.get("converged") and np.nanmax(np.abs(r["map"].cpu().numpy() - ref)) <= 1e-6 * rng_
+    fp.close()
