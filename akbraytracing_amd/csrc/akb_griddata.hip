@@ -249,13 +249,247 @@ __global__ void __launch_bounds__(kBlock) k_gd_cells(Grid g, uint8_t* diag, doub
     }
 }
 
+constexpr int kCellTile = 16;
+
+// ------------------------------------------------------------------ targets
+
+struct Targets {
+    const double* gx;  // (mx,) target x axis (grid_H row), ascending
+    const double* gy;  // (my,) target y axis (grid_V column), ascending
+    int mx, my;
+};
+
+// (m - 1) / (a[m-1] - a[0]): the inverse step of a linspace axis (0 for one point)
+__device__ __forceinline__ double inv_step(const double* a, int m) {
+    const double d = a[m - 1] - a[0];
+    return m > 1 && d > 0 ? (m - 1) / d : 0.0;
+}
+
+__device__ __forceinline__ int lower_idx(const double* a, int n, double v) {  // first i with a[i] >= v
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int m = (lo + hi) >> 1;
+        if (a[m] < v) lo = m + 1;
+        else hi = m;
+    }
+    return lo;
+}
+
+// barycentric coordinates of (px, py) in triangle T (origin at its last vertex)
+__device__ __forceinline__ void bary(const Grid& g, const Tri& T, double px, double py, double (&b)[3]) {
+    const double x2 = g.x[T.v[2]], y2 = g.y[T.v[2]];
+    const double a00 = g.x[T.v[0]] - x2, a01 = g.x[T.v[1]] - x2;
+    const double a10 = g.y[T.v[0]] - y2, a11 = g.y[T.v[1]] - y2;
+    const double det = a00 * a11 - a01 * a10;
+    const double t00 = a11 / det, t01 = -a01 / det, t10 = -a10 / det, t11 = a00 / det;
+    const double dx = px - x2, dy = py - y2;
+    b[0] = t00 * dx + t01 * dy;
+    b[1] = t10 * dx + t11 * dy;
+    b[2] = 1.0 - b[0] - b[1];
+}
+
+constexpr double kInsideEps = 100 * 2.220446049250313e-16;
+
+// target index box of triangle T: columns [c0, c1), rows [r0, r1)
+__device__ __forceinline__ void tri_box(const Grid& g, const Targets& t, const Tri& T, int& c0, int& c1, int& r0,
+                                        int& r1) {
+    double xlo = g.x[T.v[0]], xhi = xlo, ylo = g.y[T.v[0]], yhi = ylo;
+    for (int k = 1; k < 3; ++k) {
+        xlo = fmin(xlo, g.x[T.v[k]]);
+        xhi = fmax(xhi, g.x[T.v[k]]);
+        ylo = fmin(ylo, g.y[T.v[k]]);
+        yhi = fmax(yhi, g.y[T.v[k]]);
+    }
+    const double padx = (xhi - xlo) * 1e-9, pady = (yhi - ylo) * 1e-9;
+    c0 = lower_idx(t.gx, t.mx, xlo - padx);
+    c1 = lower_idx(t.gx, t.mx, xhi + padx);
+    r0 = lower_idx(t.gy, t.my, ylo - pady);
+    r1 = lower_idx(t.gy, t.my, yhi + pady);
+}
+
+__device__ __forceinline__ void claim_one(const Grid& g, const Targets& t, const Tri& T, int id, int r, int c,
+                                          int* owner) {
+    double b[3];
+    bary(g, T, t.gx[c], t.gy[r], b);
+    if (b[0] >= -kInsideEps && b[1] >= -kInsideEps && b[2] >= -kInsideEps) atomicMin(&owner[(int64_t)r * t.mx + c], id);
+}
+
+// candidate index range of the targets of an ascending linspace axis a (m points) in [lo, hi):
+// the real-valued indices of lo and hi from the axis's own step, widened by 1e-6 of an index (the
+// axis values sit within a few ulp of a0 + c * step); empty when no integer falls between them
+__device__ __forceinline__ bool axis_range(const double* a, int m, double inv_step, double lo, double hi, int& c0,
+                                           int& c1) {
+    const double a0 = a[0];
+    const double e0 = (lo - a0) * inv_step - 1e-6, e1 = (hi - a0) * inv_step + 1e-6;
+    if (!(e1 >= 0.0) || !(e0 <= (double)(m - 1))) return false;
+    const double f0 = ceil(fmax(e0, 0.0)), f1 = floor(fmin(e1, (double)(m - 1)));
+    if (f0 > f1) return false;
+    c0 = (int)f0;
+    c1 = (int)f1 + 1;
+    return true;
+}
+
+// whether axis a (m points, ascending) is a linspace: strictly increasing and every point within
+// 1e-6 of an index of a0 + i * step (axis_range's widening); one value per thread of the workgroup
+__device__ __forceinline__ bool axis_uniform_part(const double* a, int m, int i) {
+    if (i >= m || m < 2) return true;
+    const double step = (a[m - 1] - a[0]) / (m - 1);
+    if (!(step > 0)) return false;
+    if (i > 0 && !(a[i] > a[i - 1])) return false;
+    return fabs((a[i] - a[0]) / step - i) <= 1e-7;
+}
+
+// the claim kernels' axis test: whether both axes are linspaces (workgroup-wide; every thread)
+__device__ __forceinline__ bool axes_uniform(const Targets& t) {
+    // the index-box estimate needs evenly spaced axes (np.linspace, the driver's); any other
+    // ascending axis takes the exact binary search (lower_idx) of the per-triangle claim
+    bool ok = true;
+    for (int i = threadIdx.x; i < t.mx || i < t.my; i += blockDim.x)
+        ok = ok && axis_uniform_part(t.gx, t.mx, i) && axis_uniform_part(t.gy, t.my, i);
+    return __syncthreads_and(ok) != 0;
+}
+
+// ---- the claims fused into the cell pass (the cone solve's single-process path): while
+// k_gd_cells_tiled holds a tile's vertices and diagonals in LDS, the tile's bounding box is tested
+// against the target axes and only a tile that can hold a target claims, cell by cell - claim_cell
+// on the LDS copies (the same boxes, the same candidate pairs, bary's arithmetic on the same
+// values: the same owners as k_gd_claim_scan + k_gd_claim_hit), with no second pass over the
+// lattice
+struct TileClaims {
+    Targets t;   // the target axes (the device's linspaces, k_gd_axes)
+    int* owner;  // (my, mx), INT32_MAX-filled before the pass
+};
+
+__device__ __forceinline__ void bary_lds(const double* vx, const double* vy, const int (&k)[3], double px, double py,
+                                         double (&b)[3]) {  // bary on LDS copies: the same expressions
+    const double x2 = vx[k[2]], y2 = vy[k[2]];
+    const double a00 = vx[k[0]] - x2, a01 = vx[k[1]] - x2;
+    const double a10 = vy[k[0]] - y2, a11 = vy[k[1]] - y2;
+    const double det = a00 * a11 - a01 * a10;
+    const double t00 = a11 / det, t01 = -a01 / det, t10 = -a10 / det, t11 = a00 / det;
+    const double dx = px - x2, dy = py - y2;
+    b[0] = t00 * dx + t01 * dy;
+    b[1] = t10 * dx + t11 * dy;
+    b[2] = 1.0 - b[0] - b[1];
+}
+
+__device__ void tile_claims(const Grid& g, const TileClaims& tc, bool uniform, double inv_dx, double inv_dy,
+                            const double* vx, const double* vy, const uint8_t* sdg, int iv0, int ih0, int r_hi) {
+    constexpr int T = kCellTile, V = T + 2;
+    __shared__ double sbox[4][T * T / 64];
+    const Targets& t = tc.t;
+    const int tid = threadIdx.x;
+    const int nr = min(T, r_hi - iv0), nc = min(T, g.nh - 1 - ih0);  // the tile's cells
+    // the tile's box over its (nr + 1) x (nc + 1) vertices (a superset of each cell's box; fmin and
+    // fmax pass over a NaN as claim_cell's do, an infinite vertex leaves the tile to the cells)
+    double xlo = INFINITY, xhi = -INFINITY, ylo = INFINITY, yhi = -INFINITY;
+    for (int k = tid; k < (nr + 1) * (nc + 1); k += T * T) {
+        const int r = k / (nc + 1), c = k - (k / (nc + 1)) * (nc + 1);
+        const double x = vx[r * V + c], y = vy[r * V + c];
+        xlo = fmin(xlo, x);
+        xhi = fmax(xhi, x);
+        ylo = fmin(ylo, y);
+        yhi = fmax(yhi, y);
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        xlo = fmin(xlo, __shfl_xor(xlo, off));
+        xhi = fmax(xhi, __shfl_xor(xhi, off));
+        ylo = fmin(ylo, __shfl_xor(ylo, off));
+        yhi = fmax(yhi, __shfl_xor(yhi, off));
+    }
+    if ((tid & 63) == 0) {
+        sbox[0][tid >> 6] = xlo;
+        sbox[1][tid >> 6] = xhi;
+        sbox[2][tid >> 6] = ylo;
+        sbox[3][tid >> 6] = yhi;
+    }
+    __syncthreads();  // (the next tile's writes come after the cell pass's next three barriers)
+    xlo = fmin(fmin(sbox[0][0], sbox[0][1]), fmin(sbox[0][2], sbox[0][3]));
+    xhi = fmax(fmax(sbox[1][0], sbox[1][1]), fmax(sbox[1][2], sbox[1][3]));
+    ylo = fmin(fmin(sbox[2][0], sbox[2][1]), fmin(sbox[2][2], sbox[2][3]));
+    yhi = fmax(fmax(sbox[3][0], sbox[3][1]), fmax(sbox[3][2], sbox[3][3]));
+    if (isfinite(xlo) && isfinite(xhi) && isfinite(ylo) && isfinite(yhi)) {
+        const double padx = (xhi - xlo) * 1e-9, pady = (yhi - ylo) * 1e-9;
+        int c0, c1, r0, r1;
+        const bool hit = uniform ? axis_range(t.gx, t.mx, inv_dx, xlo - padx, xhi + padx, c0, c1) &&
+                                       axis_range(t.gy, t.my, inv_dy, ylo - pady, yhi + pady, r0, r1)
+                                 : lower_idx(t.gx, t.mx, xlo - padx) < lower_idx(t.gx, t.mx, xhi + padx) &&
+                                       lower_idx(t.gy, t.my, ylo - pady) < lower_idx(t.gy, t.my, yhi + pady);
+        if (!hit) return;
+    }
+    const int rr = tid / T, cc = tid - (tid / T) * T;
+    if (rr >= nr || cc >= nc) return;
+    // claim_cell on the LDS copies
+    const int k00 = rr * V + cc, k01 = k00 + 1, k10 = k00 + V, k11 = k10 + 1;
+    const int64_t c = (int64_t)(iv0 + rr) * (g.nh - 1) + (ih0 + cc);
+    const double xa = vx[k00], xb = vx[k01], xc = vx[k10], xd = vx[k11];
+    const double ya = vy[k00], yb = vy[k01], yc = vy[k10], yd = vy[k11];
+    const double cxlo = fmin(fmin(xa, xb), fmin(xc, xd)), cxhi = fmax(fmax(xa, xb), fmax(xc, xd));
+    const double cylo = fmin(fmin(ya, yb), fmin(yc, yd)), cyhi = fmax(fmax(ya, yb), fmax(yc, yd));
+    const double padx = (cxhi - cxlo) * 1e-9, pady = (cyhi - cylo) * 1e-9;
+    int c0, c1, r0, r1;
+    if (uniform) {
+        if (!axis_range(t.gx, t.mx, inv_dx, cxlo - padx, cxhi + padx, c0, c1)) return;
+        if (!axis_range(t.gy, t.my, inv_dy, cylo - pady, cyhi + pady, r0, r1)) return;
+    } else {
+        c0 = lower_idx(t.gx, t.mx, cxlo - padx);
+        c1 = lower_idx(t.gx, t.mx, cxhi + padx);
+        r0 = lower_idx(t.gy, t.my, cylo - pady);
+        r1 = lower_idx(t.gy, t.my, cyhi + pady);
+        if (c0 >= c1 || r0 >= r1) return;
+    }
+    while (c0 < c1 && t.gx[c0] < cxlo - padx) ++c0;
+    while (c1 > c0 && t.gx[c1 - 1] >= cxhi + padx) --c1;
+    if (c0 >= c1) return;
+    while (r0 < r1 && t.gy[r0] < cylo - pady) ++r0;
+    while (r1 > r0 && t.gy[r1 - 1] >= cyhi + pady) --r1;
+    if (r0 >= r1) return;
+    const int d = sdg[rr * (T + 1) + cc];
+    for (int half = 0; half < 2; ++half) {
+        // tri_verts' vertex order: diag 0: (p00, p01, p11), (p00, p11, p10); diag 1: (p00, p01, p10), (p01, p11, p10)
+        int kv[3];
+        if (d == 0) {
+            kv[0] = k00;
+            kv[1] = half == 0 ? k01 : k11;
+            kv[2] = half == 0 ? k11 : k10;
+        } else {
+            kv[0] = half == 0 ? k00 : k01;
+            kv[1] = half == 0 ? k01 : k11;
+            kv[2] = k10;
+        }
+        double txlo = vx[kv[0]], txhi = txlo, tylo = vy[kv[0]], tyhi = tylo;
+        for (int k = 1; k < 3; ++k) {
+            txlo = fmin(txlo, vx[kv[k]]);
+            txhi = fmax(txhi, vx[kv[k]]);
+            tylo = fmin(tylo, vy[kv[k]]);
+            tyhi = fmax(tyhi, vy[kv[k]]);
+        }
+        const double tpx = (txhi - txlo) * 1e-9, tpy = (tyhi - tylo) * 1e-9;
+        int tc0 = c0, tr0 = r0;
+        while (tc0 < c1 && t.gx[tc0] < txlo - tpx) ++tc0;
+        int tc1 = tc0;
+        while (tc1 < c1 && t.gx[tc1] < txhi + tpx) ++tc1;
+        while (tr0 < r1 && t.gy[tr0] < tylo - tpy) ++tr0;
+        int tr1 = tr0;
+        while (tr1 < r1 && t.gy[tr1] < tyhi + tpy) ++tr1;
+        for (int r = tr0; r < tr1; ++r)
+            for (int q = tc0; q < tc1; ++q) {
+                double b[3];
+                bary_lds(vx, vy, kv, t.gx[q], t.gy[r], b);
+                if (b[0] >= -kInsideEps && b[1] >= -kInsideEps && b[2] >= -kInsideEps)
+                    atomicMin(&tc.owner[(int64_t)r * t.mx + q], (int)(2 * c + half));
+            }
+    }
+}
+
 // k_gd_cells on 16 x 16 tiles of the window's cells, one workgroup each: the tile's 18 x 18
 // vertices in LDS (its cells, the next row's and column's), each of its 17 x 17 cells' diagonal
 // formed once (cell_diag's arithmetic on the same values), then each cell's checks from LDS. Per
 // cell: ~1.3 vertex loads and ~3 in-circle tests instead of ~10 and 5. Same diagonals and flags.
-constexpr int kCellTile = 16;
+// With kClaims the tile also claims its targets (tile_claims) before its cells' checks.
+template <bool kClaims = false>
 __global__ void __launch_bounds__(kCellTile * kCellTile) k_gd_cells_tiled(Grid g, uint8_t* diag, double tol,
-                                                                        unsigned* flags) {
+                                                                        unsigned* flags, TileClaims tc = {}) {
     constexpr int T = kCellTile, V = T + 2;
     __shared__ double vx[V * V], vy[V * V];
     __shared__ uint8_t sdg[(T + 1) * (T + 1)];
@@ -263,6 +497,13 @@ __global__ void __launch_bounds__(kCellTile * kCellTile) k_gd_cells_tiled(Grid g
     const int tiles_h = (g.nh - 1 + T - 1) / T;
     const int64_t ntiles = (int64_t)((r_hi - r_lo + T - 1) / T) * tiles_h;
     unsigned acc = 0;
+    bool uniform = false;
+    double inv_dx = 0.0, inv_dy = 0.0;
+    if constexpr (kClaims) {
+        uniform = axes_uniform(tc.t);
+        inv_dx = inv_step(tc.t.gx, tc.t.mx);
+        inv_dy = inv_step(tc.t.gy, tc.t.my);
+    }
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int tv = (int)(tile / tiles_h), th = (int)(tile - (int64_t)tv * tiles_h);
         const int iv0 = r_lo + tv * T, ih0 = th * T;
@@ -310,6 +551,7 @@ __global__ void __launch_bounds__(kCellTile * kCellTile) k_gd_cells_tiled(Grid g
                 (jv < g.nv - 1 && jh < g.nh - 1 && jv <= r_hi) ? (uint8_t)diag_of(r2, c2, nullptr) : (uint8_t)0;
         }
         __syncthreads();
+        if constexpr (kClaims) tile_claims(g, tc, uniform, inv_dx, inv_dy, vx, vy, sdg, iv0, ih0, r_hi);  // (a barrier)
         if (!own) continue;
         const int64_t c = (int64_t)iv * (g.nh - 1) + ih;
         diag[c] = (uint8_t)d;
@@ -1490,69 +1732,6 @@ __global__ void __launch_bounds__(kBlock) k_gd_cone_assign(Grid g, const int* __
     }
 }
 
-// ------------------------------------------------------------------ targets
-
-struct Targets {
-    const double* gx;  // (mx,) target x axis (grid_H row), ascending
-    const double* gy;  // (my,) target y axis (grid_V column), ascending
-    int mx, my;
-};
-
-// (m - 1) / (a[m-1] - a[0]): the inverse step of a linspace axis (0 for one point)
-__device__ __forceinline__ double inv_step(const double* a, int m) {
-    const double d = a[m - 1] - a[0];
-    return m > 1 && d > 0 ? (m - 1) / d : 0.0;
-}
-
-__device__ __forceinline__ int lower_idx(const double* a, int n, double v) {  // first i with a[i] >= v
-    int lo = 0, hi = n;
-    while (lo < hi) {
-        const int m = (lo + hi) >> 1;
-        if (a[m] < v) lo = m + 1;
-        else hi = m;
-    }
-    return lo;
-}
-
-// barycentric coordinates of (px, py) in triangle T (origin at its last vertex)
-__device__ __forceinline__ void bary(const Grid& g, const Tri& T, double px, double py, double (&b)[3]) {
-    const double x2 = g.x[T.v[2]], y2 = g.y[T.v[2]];
-    const double a00 = g.x[T.v[0]] - x2, a01 = g.x[T.v[1]] - x2;
-    const double a10 = g.y[T.v[0]] - y2, a11 = g.y[T.v[1]] - y2;
-    const double det = a00 * a11 - a01 * a10;
-    const double t00 = a11 / det, t01 = -a01 / det, t10 = -a10 / det, t11 = a00 / det;
-    const double dx = px - x2, dy = py - y2;
-    b[0] = t00 * dx + t01 * dy;
-    b[1] = t10 * dx + t11 * dy;
-    b[2] = 1.0 - b[0] - b[1];
-}
-
-constexpr double kInsideEps = 100 * 2.220446049250313e-16;
-
-// target index box of triangle T: columns [c0, c1), rows [r0, r1)
-__device__ __forceinline__ void tri_box(const Grid& g, const Targets& t, const Tri& T, int& c0, int& c1, int& r0,
-                                        int& r1) {
-    double xlo = g.x[T.v[0]], xhi = xlo, ylo = g.y[T.v[0]], yhi = ylo;
-    for (int k = 1; k < 3; ++k) {
-        xlo = fmin(xlo, g.x[T.v[k]]);
-        xhi = fmax(xhi, g.x[T.v[k]]);
-        ylo = fmin(ylo, g.y[T.v[k]]);
-        yhi = fmax(yhi, g.y[T.v[k]]);
-    }
-    const double padx = (xhi - xlo) * 1e-9, pady = (yhi - ylo) * 1e-9;
-    c0 = lower_idx(t.gx, t.mx, xlo - padx);
-    c1 = lower_idx(t.gx, t.mx, xhi + padx);
-    r0 = lower_idx(t.gy, t.my, ylo - pady);
-    r1 = lower_idx(t.gy, t.my, yhi + pady);
-}
-
-__device__ __forceinline__ void claim_one(const Grid& g, const Targets& t, const Tri& T, int id, int r, int c,
-                                          int* owner) {
-    double b[3];
-    bary(g, T, t.gx[c], t.gy[r], b);
-    if (b[0] >= -kInsideEps && b[1] >= -kInsideEps && b[2] >= -kInsideEps) atomicMin(&owner[(int64_t)r * t.mx + c], id);
-}
-
 // cell triangles (ids < 2 * ncells): one thread each, a box of a few targets
 __global__ void __launch_bounds__(kBlock) k_gd_claim(Grid g, Targets t, int* owner) {
     const int64_t ntri = 2 * ncells(g);
@@ -1568,33 +1747,8 @@ __global__ void __launch_bounds__(kBlock) k_gd_claim(Grid g, Targets t, int* own
 // cell triangles, one thread per cell: the targets are sparse against the cells (a 128^2 pupil
 // grid over 1e7 hits), so the cell's target index box is first estimated from the linspace axes
 // (widened by one index each way) and almost every thread stops there; the candidates are then
-// held to each triangle's exact box and barycentric test, so the claims are k_gd_claim's
-// candidate index range of the targets of an ascending linspace axis a (m points) in [lo, hi):
-// the real-valued indices of lo and hi from the axis's own step, widened by 1e-6 of an index (the
-// axis values sit within a few ulp of a0 + c * step); empty when no integer falls between them
-__device__ __forceinline__ bool axis_range(const double* a, int m, double inv_step, double lo, double hi, int& c0,
-                                           int& c1) {
-    const double a0 = a[0];
-    const double e0 = (lo - a0) * inv_step - 1e-6, e1 = (hi - a0) * inv_step + 1e-6;
-    if (!(e1 >= 0.0) || !(e0 <= (double)(m - 1))) return false;
-    const double f0 = ceil(fmax(e0, 0.0)), f1 = floor(fmin(e1, (double)(m - 1)));
-    if (f0 > f1) return false;
-    c0 = (int)f0;
-    c1 = (int)f1 + 1;
-    return true;
-}
-
-// whether axis a (m points, ascending) is a linspace: strictly increasing and every point within
-// 1e-6 of an index of a0 + i * step (axis_range's widening); one value per thread of the workgroup
-__device__ __forceinline__ bool axis_uniform_part(const double* a, int m, int i) {
-    if (i >= m || m < 2) return true;
-    const double step = (a[m - 1] - a[0]) / (m - 1);
-    if (!(step > 0)) return false;
-    if (i > 0 && !(a[i] > a[i - 1])) return false;
-    return fabs((a[i] - a[0]) / step - i) <= 1e-7;
-}
-
-// one cell's claims (its two triangles' targets)
+// held to each triangle's exact box and barycentric test, so the claims are k_gd_claim's.
+// One cell's claims (its two triangles' targets)
 __device__ __forceinline__ void claim_cell(const Grid& g, const Targets& t, int64_t c, bool uniform, double inv_dx,
                                            double inv_dy, int* owner) {
     const int iv = (int)(c / (g.nh - 1)), ih = (int)(c - (int64_t)iv * (g.nh - 1));
@@ -1646,16 +1800,6 @@ __device__ __forceinline__ void claim_cell(const Grid& g, const Targets& t, int6
         for (int r = tr0; r < tr1; ++r)
             for (int cc = tc0; cc < tc1; ++cc) claim_one(g, t, T, (int)id, r, cc, owner);
     }
-}
-
-// the claim kernels' axis test: whether both axes are linspaces (workgroup-wide; every thread)
-__device__ __forceinline__ bool axes_uniform(const Targets& t) {
-    // the index-box estimate needs evenly spaced axes (np.linspace, the driver's); any other
-    // ascending axis takes the exact binary search (lower_idx) of the per-triangle claim
-    bool ok = true;
-    for (int i = threadIdx.x; i < t.mx || i < t.my; i += blockDim.x)
-        ok = ok && axis_uniform_part(t.gx, t.mx, i) && axis_uniform_part(t.gy, t.my, i);
-    return __syncthreads_and(ok) != 0;
 }
 
 __global__ void __launch_bounds__(kBlock) k_gd_claim_cells(Grid g, Targets t, int* owner) {
@@ -1958,6 +2102,20 @@ unsigned gd_cu_count() {  // the device's CUs (one resident 1024-thread patch wo
 // the per-triangle claim (tests/test_gpu_parity.py's cross-check of the block claims: AKB_GD_CLAIM_TRI)
 bool gd_claim_tri() { return getenv("AKB_GD_CLAIM_TRI") != nullptr; }
 
+// diagnostics (akb_gd_patch_timing / akb_gd_patch_times): HIP events around each k_gd_cone_patch
+// launch while enabled, a ring of kPatchEvents pairs, and each launch's cell count (its device word)
+constexpr int kPatchEvents = 1024;
+struct PatchTimer {
+    bool on = false, made = false;
+    hipEvent_t ev[kPatchEvents][2];
+    const int* cnt[kPatchEvents];
+    int64_t launches = 0;
+};
+PatchTimer& patch_timer() {
+    static PatchTimer t;
+    return t;
+}
+
 }  // namespace
 }  // namespace akb
 
@@ -2179,7 +2337,17 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
         }
         ConePatch a{fv, cells, count, K, {}, gb[K % 3], d_change, d_change ? d_change + 1 : nullptr};
         for (int j = 0; j <= K; ++j) a.st[j] = steps[j];
+        PatchTimer& pt = patch_timer();
+        const int slot = (int)(pt.launches % kPatchEvents);
+        if (pt.on) {
+            (void)hipEventRecord(pt.ev[slot][0], s);
+            pt.cnt[slot] = count;
+        }
         k_gd_cone_patch<<<pp, 1024, 0, s>>>(g, a, S);
+        if (pt.on) {
+            (void)hipEventRecord(pt.ev[slot][1], s);
+            ++pt.launches;
+        }
         if ((st = launch_status("k_gd_cone_patch"))) return st;
         if (cnt)
             k_gd_eval_part<<<grid_for(m, 1, kStreamGridCap), kBlock, 0, s>>>(g, t, owner, assigned, fv, gb[K % 3], 1,
@@ -2210,6 +2378,60 @@ int akb_gd_cone_eval_f64(const double* x, const double* y, int nv, int nh, const
     int st = cone_claims(g, t, 1, owner, s, (uint8_t*)work + claim_scratch_offset(nv, nh, mx, my, nvals));
     if (st) return st;
     return cone_part(g, t, 0, (int64_t)nv * nh, 1, f, nvals, K, omegas, work, owner, out, nullptr, d_change, s);
+}
+
+// the single-process cone solve's begin: the target owners filled, then pass 1 with the cells' claims
+// fused in (k_gd_cells_tiled<true>); the axes (akb_gd_axes_f64) before it, the pockets' claims after
+int akb_gd_cells_claims_f64(const double* x, const double* y, int nv, int nh, uint8_t* diag, double tol,
+                            unsigned* d_flags, const double* gx, int mx, const double* gy, int my, int* owner,
+                            void* stream) {
+    clear_error();
+    AKB_REQUIRE(x && y && diag && d_flags && gx && gy && owner && mx > 0 && my > 0, "bad arguments");
+    AKB_REQUIRE(nv >= 2 && nh >= 2, "grid of at least 2 x 2 points");
+    hipStream_t s = (hipStream_t)stream;
+    const int64_t m = (int64_t)mx * my;
+    k_fill_i32<<<grid_for(m, 4), kBlock, 0, s>>>(owner, m, INT32_MAX);
+    int st = launch_status("k_fill_i32");
+    if (st) return st;
+    Grid g{x, y, nv, nh, diag, 0, nullptr, nullptr, nullptr, nullptr, nullptr};
+    const TileClaims tc{Targets{gx, gy, mx, my}, owner};
+    const int64_t tiles = (int64_t)((nv - 1 + kCellTile - 1) / kCellTile) * ((nh - 1 + kCellTile - 1) / kCellTile);
+    k_gd_cells_tiled<true><<<(unsigned)(tiles < 4096 ? tiles : 4096), kCellTile * kCellTile, 0, s>>>(g, diag, tol, d_flags,
+                                                                                                   tc);
+    return launch_status("k_gd_cells_claims");
+}
+
+// the pockets' claims into owners the cells have claimed (akb_gd_cells_claims_f64)
+int akb_gd_claim_pockets_f64(const double* x, const double* y, int nv, int nh, const uint8_t* diag, int npock,
+                             const int32_t* ptri, const double* gx, int mx, const double* gy, int my, int* owner,
+                             void* stream) {
+    clear_error();
+    AKB_REQUIRE(x && y && diag && gx && gy && owner && mx > 0 && my > 0 && nv >= 2 && nh >= 2, "bad arguments");
+    if (npock == 0) return 0;
+    AKB_REQUIRE(ptri, "pockets needed");
+    Grid g{x, y, nv, nh, diag, npock, ptri, nullptr, nullptr, nullptr, nullptr};
+    const int64_t pw = ((int64_t)npock + kBlock / 64 - 1) / (kBlock / 64);
+    k_gd_claim_pockets<<<(unsigned)(pw < 16384 ? pw : 16384), kBlock, 0, (hipStream_t)stream>>>(g, Targets{gx, gy, mx, my},
+                                                                                               owner);
+    return launch_status("k_gd_claim_pockets");
+}
+
+// akb_gd_cone_eval_f64 on claimed owners: the solve and the evaluation only
+int akb_gd_cone_solve_f64(const double* x, const double* y, int nv, int nh, const uint8_t* diag, int npock,
+                          const int32_t* ptri, const int32_t* pnbr, const int32_t* edge_tri, const int32_t* xptr,
+                          const int32_t* xidx, const double* gx, int mx, const double* gy, int my, const double* f,
+                          int nvals, int K, const double* omegas, void* work, const int* owner, double* out,
+                          unsigned long long* d_change, void* stream) {
+    clear_error();
+    AKB_REQUIRE(x && y && diag && gx && gy && f && omegas && work && owner && out && mx > 0 && my > 0 && nvals >= 1,
+                "bad arguments");
+    AKB_REQUIRE(K >= 1 && K <= kConeMaxK, "K sweeps in 1 .. 14");
+    AKB_REQUIRE(nv >= 2 && nh >= 2, "grid of at least 2 x 2 points");
+    AKB_REQUIRE(xptr && xidx && (npock == 0 || (ptri && pnbr && edge_tri)), "the band needs the pockets");
+    for (int j = 2; j <= K; ++j) AKB_REQUIRE(omegas[j - 1] > 0 && omegas[j - 1] < 2, "Chebyshev weight outside (0, 2)");
+    Grid g{x, y, nv, nh, diag, npock, ptri, pnbr, edge_tri, xptr, xidx};
+    return cone_part(g, Targets{gx, gy, mx, my}, 0, (int64_t)nv * nh, 1, f, nvals, K, omegas, work, owner, out, nullptr,
+                     d_change, (hipStream_t)stream);
 }
 
 int akb_gd_claims_f64(const double* x, const double* y, int nv, int nh, const uint8_t* diag, int npock,
@@ -2272,6 +2494,33 @@ int akb_gd_cells_window_f64(const double* x, const double* y, int nv, int nh, in
     const int64_t wc = (int64_t)(row1 - row0) * (nh - 1);
     if (wc == 0) return 0;
     return launch_cells(g, diag, tol, d_flags, row1 - row0, (hipStream_t)stream);
+}
+
+// diagnostics: k_gd_cone_patch launch times (see patch_timer)
+int akb_gd_patch_timing(int enable) {
+    clear_error();
+    PatchTimer& t = patch_timer();
+    if (enable && !t.made) {
+        for (int k = 0; k < kPatchEvents; ++k)
+            for (int q = 0; q < 2; ++q) AKB_HIP_CHECK(hipEventCreate(&t.ev[k][q]));
+        t.made = true;
+    }
+    t.on = enable != 0;
+    t.launches = 0;
+    return 0;
+}
+
+int akb_gd_patch_times(float* ms, int* cells, int max) {
+    clear_error();
+    PatchTimer& t = patch_timer();
+    const int n = (int)std::min<int64_t>(std::min<int64_t>(t.launches, kPatchEvents), max);
+    for (int k = 0; k < n; ++k) {
+        const int slot = (int)((t.launches - n + k) % kPatchEvents);
+        AKB_HIP_CHECK(hipEventSynchronize(t.ev[slot][1]));
+        AKB_HIP_CHECK(hipEventElapsedTime(&ms[k], t.ev[slot][0], t.ev[slot][1]));
+        if (cells) AKB_HIP_CHECK(hipMemcpy(&cells[k], t.cnt[slot], sizeof(int), hipMemcpyDeviceToHost));
+    }
+    return n;
 }
 
 }  // extern "C"

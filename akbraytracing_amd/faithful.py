@@ -9,13 +9,15 @@ plot_result_debug's 'ray_wave' step after the trace (AKB_raytrace_20250312.py:36
 
 FaithfulPupil runs it for run after run without a host wait on the queuing thread:
 
-  begin(y, z)   on the caller's stream: the cell diagonals and checks (akb_gd_cells_f64), the
-                boundary ring to pinned host memory; a worker thread then builds the hull pockets
-                (akb_gd_pockets, host C++ - the only host step, off the GIL);
+  begin(y, z)   on the caller's stream: the boundary ring (akb_gd_ring_f64) to pinned host memory,
+                the target axes from it (akb_gd_axes_f64), then the cell diagonals and checks with
+                the cells' target claims fused in (akb_gd_cells_claims_f64); a worker thread builds
+                the hull pockets from the ring meanwhile (akb_gd_pockets, host C++ - the only host
+                step, off the GIL) and checks the cell flags;
   finish(t, f)  once that ticket's pockets are built: the pocket arrays to the device, their
-                local-Delaunay check, the target axes from the ring (akb_gd_axes_f64), griddata by
-                the cone solve (akb_gd_cone_eval_f64: claims, CONE_SWEEPS Chebyshev sweeps formed
-                only where the targets read them, the Clough-Tocher patches), the nanmean removal,
+                local-Delaunay check and target claims (akb_gd_claim_pockets_f64), griddata by the
+                cone solve (akb_gd_cone_solve_f64: CONE_SWEEPS Chebyshev sweeps formed only where
+                the targets read them, the Clough-Tocher patches), the nanmean removal,
                 plane correction, rotation estimate and rotate_with_nan in one workgroup
                 (akb_pupil_post_f64), and the pad-16 PSF (akb_psf_f64). All on the stream, no host
                 synchronisation; errors the reference would raise surface in Ticket.check().
@@ -156,13 +158,13 @@ class FaithfulPupil:
                 pk_host=torch.zeros(self._pk_len, dtype=torch.int32, pin_memory=True),
                 pk=torch.zeros(self._pk_len, dtype=torch.int32, device=self.dev),
                 status=torch.zeros(1, dtype=torch.int64, device=self.dev),
+                owner=torch.empty(self.size * self.size, dtype=torch.int32, device=self.dev),
+                axes=torch.empty(2 * self.size + 6, dtype=D.F64, device=self.dev),  # gx | gy | extent | pitch
                 last=None))
         self._next = 0
         m = self.size * self.size
         self.work = torch.empty(int(L.akb_gd_cone_work_bytes(self.nv, self.nh, self.size, self.size, 1)) // 8 + 1,
                                 dtype=D.F64, device=self.dev)
-        self.owner = torch.empty(m, dtype=torch.int32, device=self.dev)
-        self.axes = torch.empty(2 * self.size + 6, dtype=D.F64, device=self.dev)  # gx | gy | extent | pitch
         self.map = torch.empty((1, self.size, self.size), dtype=D.F64, device=self.dev)
         self.change = torch.zeros(2, dtype=torch.int64, device=self.dev)  # change measure | value-error estimate
         self.post = {}
@@ -197,26 +199,49 @@ class FaithfulPupil:
             st.wait_event(s["last"].done)
         for a in (y, z, f):  # read on this stream now and in finish: not to be reused before
             a.record_stream(st)
+        m = self.size
+        gx, gy = s["axes"][:m], s["axes"][m:2 * m]
         with torch.cuda.stream(st):
             flags.zero_()
-            _lib.check(L.akb_gd_cells_f64(D.ptr(y), D.ptr(z), self.nv, self.nh, D.ptr(s["diag"]), self.tol,
-                                          D.ptr(flags), D.ptr(ring[:Lr]), D.ptr(ring[Lr:2 * Lr]), sh))
-            s["ring_host"].copy_(ring, non_blocking=True)
+            _lib.check(L.akb_gd_ring_f64(D.ptr(y), D.ptr(z), self.nv, self.nh, D.ptr(ring[:Lr]), D.ptr(ring[Lr:2 * Lr]),
+                                         D.ptr(flags), sh))
+            s["ring_host"][:2 * Lr].copy_(ring[:2 * Lr], non_blocking=True)
+            ev_ring = torch.cuda.Event()
+            ev_ring.record(st)
+            _lib.check(L.akb_gd_axes_f64(D.ptr(ring[:Lr]), D.ptr(ring[Lr:2 * Lr]), Lr, m, m, D.ptr(gx), D.ptr(gy),
+                                         D.ptr(s["axes"][2 * m:]), sh))
+            _lib.check(L.akb_gd_cells_claims_f64(D.ptr(y), D.ptr(z), self.nv, self.nh, D.ptr(s["diag"]), self.tol,
+                                                 D.ptr(flags), D.ptr(gx), m, D.ptr(gy), m, D.ptr(s["owner"]), sh))
+            s["ring_host"][2 * Lr:].copy_(ring[2 * Lr:], non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(st)
         t = Ticket()
         t.slot, t.y, t.z, t.f = s, y, z, f
         t.npock, t.result, t.h2d, t.finished, t.done, t.log, t.erow = None, None, None, False, None, self.errors, None
-        t.job = self.pool.submit(self._pockets, s, ev)
+        t.job = self.pool.submit(self._pockets, s, ev_ring, ev)
         s["last"] = t
         return t
 
-    def _pockets(self, s, ev):
-        """Worker thread: wait for the ring on the host, check the cell flags, build the pockets."""
-        ev.synchronize()
+    def _pockets(self, s, ev_ring, ev):
+        """Worker thread: wait for the ring on the host and build the pockets (while the cell pass
+        runs), then check the cell flags - their errors first, as the host chain raises them."""
+        ev_ring.synchronize()
         L = _lib.lib()
         Lr = self.L
         rb = s["ring_host"].numpy()
+        err, npk = None, None
+        if np.isfinite(rb[:2 * Lr]).all():
+            buf = s["pk_host"].numpy()
+            o = self._o
+            hp = lambda k: buf[o[k]:].ctypes.data_as(_lib.c_vp)  # noqa: E731
+            try:
+                _lib.check(L.akb_gd_pockets(rb[:Lr].ctypes.data_as(_lib.c_vp), rb[Lr:2 * Lr].ctypes.data_as(_lib.c_vp),
+                                            self.nv, self.nh, Lr, hp("npk"), hp("tri"), hp("nbr"), hp("edge"),
+                                            hp("xptr"), hp("xidx")))
+                npk, s["po"] = pack_pockets(buf, o, Lr)
+            except _lib.AKBError as e:
+                err = e
+        ev.synchronize()
         fl = int(rb[2 * Lr:].view(np.int32)[0])
         if fl & _F_NONFINITE:
             raise ValueError("griddata: non-finite point coordinates (a ray that missed)")
@@ -224,20 +249,16 @@ class FaithfulPupil:
             raise _lib.AKBError("griddata: the points do not form a convex, unfolded lattice")
         if fl & _F_NOT_DELAUNAY:
             raise _lib.AKBError("griddata: the grid is too distorted for the structured Delaunay triangulation")
-        buf = s["pk_host"].numpy()
-        o = self._o
-        hp = lambda k: buf[o[k]:].ctypes.data_as(_lib.c_vp)  # noqa: E731
-        _lib.check(L.akb_gd_pockets(rb[:Lr].ctypes.data_as(_lib.c_vp), rb[Lr:2 * Lr].ctypes.data_as(_lib.c_vp),
-                                    self.nv, self.nh, Lr, hp("npk"), hp("tri"), hp("nbr"), hp("edge"), hp("xptr"),
-                                    hp("xidx")))
-        npk, s["po"] = pack_pockets(buf, o, Lr)
+        if err is not None:
+            raise err
         return npk
 
     # ------------------------------------------------------------------ stage 2
     def finish(self, t, stream=None, events=None, psf_events=None):
         """Queue the rest of ticket t's chain on `stream` (waits for its pocket job on the host -
-        normally long done). Returns dict(psf (B, P, P) device, map, corrected, rotated, params);
-        the buffers are reused by the next finish on the stream. events: optional (start, end)
+        normally long done). Returns dict(psf (B, P, P) device, map, corrected, rotated, params,
+        axes, change); the buffers are reused by the next finish on the stream (axes, the slot's, by
+        the slot's next begin). events: optional (start, end)
         timing events recorded around the device work; psf_events: the same around the PSF alone."""
         L = _lib.lib()
         try:
@@ -268,20 +289,20 @@ class FaithfulPupil:
             s["status"].zero_()
             _lib.check(L.akb_gd_check_pockets(*tri, self.tol, D.ptr(s["status"]), sh))
             m = self.size
-            gx, gy = self.axes[:m], self.axes[m:2 * m]
-            ring = s["ring"]
-            _lib.check(L.akb_gd_axes_f64(D.ptr(ring[:Lr]), D.ptr(ring[Lr:2 * Lr]), Lr, m, m, D.ptr(gx), D.ptr(gy),
-                                         D.ptr(self.axes[2 * m:]), sh))
+            axes = s["axes"]
+            gx, gy = axes[:m], axes[m:2 * m]
+            _lib.check(L.akb_gd_claim_pockets_f64(D.ptr(t.y), D.ptr(t.z), self.nv, self.nh, D.ptr(s["diag"]), t.npock,
+                                                  D.ptr(ptri), D.ptr(gx), m, D.ptr(gy), m, D.ptr(s["owner"]), sh))
             self.change.zero_()
-            _lib.check(L.akb_gd_cone_eval_f64(*tri, D.ptr(xptr), D.ptr(xidx), D.ptr(gx), m, D.ptr(gy), m,
-                                              D.ptr(t.f), 1, self.sweeps, self._omegas, D.ptr(self.work),
-                                              D.ptr(self.owner), D.ptr(self.map), D.ptr(self.change), sh))
+            _lib.check(L.akb_gd_cone_solve_f64(*tri, D.ptr(xptr), D.ptr(xidx), D.ptr(gx), m, D.ptr(gy), m,
+                                               D.ptr(t.f), 1, self.sweeps, self._omegas, D.ptr(self.work),
+                                               D.ptr(s["owner"]), D.ptr(self.map), D.ptr(self.change), sh))
             post = pupil_post(self.map[0], out=self.post, stream=st)
             self.post = post
             if psf_events is not None:
                 psf_events[0].record(st)
             psf, _, _ = psf_stack(post["opd"], None, self.lams, None, pad_factor=self.pad, stream=st, out=self.psf,
-                                  pitch=self.axes[2 * m + 4:2 * m + 6])
+                                  pitch=axes[2 * m + 4:2 * m + 6])
             if psf_events is not None:
                 psf_events[1].record(st)
             self.psf = psf
@@ -292,7 +313,7 @@ class FaithfulPupil:
             t.done.record(st)
             self._done = t.done
         t.result = dict(psf=psf, map=self.map[0], corrected=post["corrected"], rotated=post["rotated"],
-                        params=post["params"], axes=self.axes, change=self.change)
+                        params=post["params"], axes=axes, change=self.change)
         t.y = t.z = t.f = None
         t.finished = True
         self.finished += 1
@@ -307,17 +328,16 @@ class FaithfulPupil:
         try:
             t.check()
         except ConeNotConverged:
-            r = self._converged(y, z, f, stream)
+            r = self._converged(y, z, f, t.slot["axes"], stream)
         return r
 
-    def _converged(self, y, z, f, stream=None):
-        """The run's map from the global gradient iteration (host-synchronous), then the same post
-        and PSF on the device; the result in finish's buffers."""
+    def _converged(self, y, z, f, ax, stream=None):
+        """The run's map from the global gradient iteration (host-synchronous) on the run's axes ax,
+        then the same post and PSF on the device; the result in finish's buffers."""
         st = torch.cuda.current_stream() if stream is None else stream
         m = self.size
         with torch.cuda.stream(st):
             cg = CubicGrid(y, z, self.nv, self.nh, delaunay_tol=self.tol)
-            ax = self.axes
             self.map[0].copy_(cg.interp(f.reshape(1, -1), ax[:m], ax[m:2 * m])[0])
             post = pupil_post(self.map[0], out=self.post, stream=st)
             self.post = post
@@ -326,7 +346,7 @@ class FaithfulPupil:
             self.psf = psf
         pupil_post_check(post["params"])
         return dict(psf=psf, map=self.map[0], corrected=post["corrected"], rotated=post["rotated"],
-                    params=post["params"], axes=self.axes, change=self.change, converged=True)
+                    params=post["params"], axes=ax, change=self.change, converged=True)
 
     def close(self):
         self.pool.shutdown(wait=True)

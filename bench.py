@@ -288,6 +288,61 @@ def huygens_rate(out):
     return res
 
 
+def read_faithful_profile():
+    """(summary, file, matches): the newest profiles/*_faithful_roofline.json (scripts/
+    summarize_profiles.py: PMC of the cone solve's kernels) and whether it describes these sources."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    from summarize_profiles import GD_SOURCES, sources_sha256
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_faithful_roofline.json")))
+    if not files:
+        return {}, None, False
+    with open(files[-1]) as f:
+        d = json.load(f)
+    return d, os.path.relpath(files[-1], ROOT), d.get("sources_sha256") == sources_sha256(sources=GD_SOURCES)
+
+
+def faithful_roofline(ms, cells, K, S):
+    """The cone solve's patch kernel (k_gd_cone_patch) over the timed steps: its launch time from HIP
+    events around every launch (akb_gd_patch_times, in the step, sharing the GPU), its work (interior
+    target cells x the box's shrinking squares: sum_j (2K + 4 - 2j)^2 vertex-sweeps; (W - 2)^2 + (W -
+    2S - 2)^2 vertex setups, stage 2 forming its own), its compulsory HBM traffic (the cells' boxes
+    of x, y, f and diagonal bytes in, four corners' gradients out) against 8 TB/s, and - from the
+    committed PMC summary while it describes these sources - its VALU issue against the SIMDs'."""
+    W = 2 * K + 4
+    sweeps = sum((W - 2 * j) ** 2 for j in range(1, K + 1))
+    setups = (W - 2) ** 2 + (W - 2 * S - 2) ** 2
+    avg = sum(ms) / len(ms)
+    byts = cells * (W * W * 24 + (W - 1) * (W - 1) + 4 * 16)
+    prof, pfile, pok = read_faithful_profile()
+    pk = prof.get("kernels", {}).get("cone_patch", {}) if pok else {}
+    valu = pk.get("valu_wave_instructions_per_launch")
+    clock = pk.get("effective_clock_ghz")
+    out = {
+        "kernel": "k_gd_cone_patch (akb_griddata.hip)",
+        "bound": "latency: one 1024-thread workgroup per CU, a barrier per sweep (VALU issue below)",
+        "launches": len(ms),
+        "avg_ms": avg,
+        "cells_per_launch": cells,
+        "vertex_sweeps_per_launch": cells * sweeps,
+        "vertex_setups_per_launch": cells * setups,
+        "vertex_sweeps_per_s": cells * sweeps / (avg * 1e-3),
+        "hbm": {"algorithmic_bytes_per_launch": byts, "achieved": byts / (avg * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": byts / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                "traffic": pk.get("hbm_bytes_per_launch")},
+        "valu_issue": {"wave_instructions_per_launch": valu, "effective_clock_ghz": clock,
+                       "achieved": valu / (avg * 1e-3) if valu else None,
+                       "peak": SIMDS / 4 * clock * 1e9 if clock else None, "unit": "wave-instructions/s",
+                       "frac": (valu / (avg * 1e-3)) / (SIMDS / 4 * clock * 1e9) if valu and clock else None,
+                       "lane_ops_per_vertex_sweep": 64 * valu / (cells * (sweeps + setups)) if valu and cells else None,
+                       "lds_wave_instructions_per_launch": pk.get("lds_wave_instructions_per_launch"),
+                       "lds_bank_conflict_cycles_per_launch": pk.get("lds_bank_conflict_cycles_per_launch"),
+                       "wait_any_frac_profiled": pk.get("wait_any_frac"),
+                       "issue_frac_profiled": pk.get("issue_frac")},
+        "profile": {"file": pfile, "matches_sources": pok},
+    }
+    return out
+
+
 def stage_api(rw, geom, dev, reps=5):
     """The drop-in stage API (SURVEY.md §8(d)'s HBM-bound mode): the reference's per-mirror calls
     on device-resident (3, N) rows of the bench's grid - mirr_ray_intersection, the segment norm,
@@ -630,8 +685,25 @@ def main():
     psf_events.clear()
     # host_ms: host time spent issuing each step (its waits included): is the host the limit?
     fin0 = fp.finished if fp is not None else 0
+    from akbraytracing_amd import _lib as LIBM
+    if fp is not None and world == 1:  # HIP events around each patch launch of the timed steps
+        LIBM.check(LIBM.lib().akb_gd_patch_timing(1))
     el, host_ms = timed_steps(args.steps)
     finishes_timed = (fp.finished - fin0) if fp is not None else None
+    patch = None
+    if fp is not None and world == 1:
+        LIBM.check(LIBM.lib().akb_gd_patch_timing(0))  # (stops new records; the queued ones still land)
+        pms = (ctypes.c_float * 1024)()
+        pcells = (ctypes.c_int * 1024)()
+        k = LIBM.lib().akb_gd_patch_times(pms, pcells, 1024)
+        if k < 0:
+            LIBM.check(k)
+        if k > 0:
+            K = fp.sweeps
+            W = 2 * K + 4
+            S = next(s2 for s2 in range((K + 1) // 2, K + 1)
+                     if (((W - 2) ** 2 + 63) // 64 * 64) + (W - 2 * s2 - 2) ** 2 <= 1020)
+            patch = faithful_roofline(list(pms[:k]), int(pcells[k - 1]), K, S)
     while fronts:  # the last front's back half (outside the timed region, like the first one's)
         back(False)
     while tickets:
@@ -804,6 +876,8 @@ def main():
         "faithful_finishes_timed": finishes_timed,
         "faithful_runs_checked": faithful_checked,
         "faithful_chain_ms": ((sum(fp_begin) + sum(fp_fin)) / max(len(fp_fin), 1)) if fp_fin else None,
+        # the faithful chain's dominant kernel: the cone solve's patches (in the timed steps)
+        "roofline_faithful": patch,
         "faithful_finish_ms": (sum(fp_fin) / len(fp_fin)) if fp_fin else None,
         "psf_ms": psf_ms if psf_events else None,
         "psf_alone_ms": psf_alone_ms,

@@ -529,6 +529,13 @@ int akb_gd_eval_f64(const double* x, const double* y, int nv, int nh, const uint
  * (scipy/interpolate/_interpnd.pyx) where the driver's griddata (AKB_raytrace_20250312.py:3689)
  * feeds a fixed-size pupil. */
 int64_t akb_gd_cone_work_bytes(int nv, int nh, int mx, int my, int nvals);
+/* Diagnostics of the cone solve's patch kernel (k_gd_cone_patch), for bench.py's roofline:
+ * akb_gd_patch_timing(1) records HIP events around every patch launch from then on (the last 1024
+ * launches kept; 0 stops, either resets the count); akb_gd_patch_times waits for them and writes up
+ * to max launch durations (ms, oldest first) and, when cells != NULL, each launch's interior target
+ * cell count; returns how many (or a negative AKB error code). */
+int akb_gd_patch_timing(int enable);
+int akb_gd_patch_times(float* ms, int* cells, int max);
 /* The driver's target axes (AKB_raytrace_20250312.py:3654-3657): gx = np.linspace(min, max, mx) of
  * the lattice's x (its extremes lie on the boundary ring akb_gd_cells_f64 returns), gy likewise of
  * y; d_extent (or NULL, 6 doubles): [min x, max x, min y, max y, dx, dy] with dx = |gh[0,1] - gh[0,0]|,
@@ -542,6 +549,26 @@ int akb_gd_cone_eval_f64(const double* x, const double* y, int nv, int nh, const
                          const int32_t* xidx, const double* gx, int mx, const double* gy, int my, const double* f,
                          int nvals, int K, const double* omegas, void* work, int* owner, double* out,
                          unsigned long long* d_change, void* stream);
+/* The one-process cone solve split at the pockets (FaithfulPupil's begin / finish): the axes from
+ * the ring first (akb_gd_ring_f64 + akb_gd_axes_f64), then
+ *   akb_gd_cells_claims_f64: akb_gd_cells_f64's cell pass (the same diag and flags; no ring) with
+ *     the cells' target claims fused in: owner[] = INT32_MAX, then each 16 x 16 tile of cells
+ *     whose vertex box can hold a target claims from its LDS copy (the same owners as the claims
+ *     of akb_gd_cone_eval_f64);
+ *   akb_gd_claim_pockets_f64: the pocket triangles' claims into those owners (atomicMin);
+ *   akb_gd_cone_solve_f64: akb_gd_cone_eval_f64 on the claimed owners (no claims of its own).
+ * Every target value is akb_gd_cone_eval_f64's bit for bit. */
+int akb_gd_cells_claims_f64(const double* x, const double* y, int nv, int nh, uint8_t* diag, double tol,
+                            unsigned* d_flags, const double* gx, int mx, const double* gy, int my, int* owner,
+                            void* stream);
+int akb_gd_claim_pockets_f64(const double* x, const double* y, int nv, int nh, const uint8_t* diag, int npock,
+                             const int32_t* ptri, const double* gx, int mx, const double* gy, int my, int* owner,
+                             void* stream);
+int akb_gd_cone_solve_f64(const double* x, const double* y, int nv, int nh, const uint8_t* diag, int npock,
+                          const int32_t* ptri, const int32_t* pnbr, const int32_t* edge_tri, const int32_t* xptr,
+                          const int32_t* xidx, const double* gx, int mx, const double* gy, int my, const double* f,
+                          int nvals, int K, const double* omegas, void* work, const int* owner, double* out,
+                          unsigned long long* d_change, void* stream);
 
 /* The cone solve of a lattice sharded over ranks (row-block shards of the flat ray index; each
  * rank passes x, y, diag as "virtual" global arrays of which only its rows plus K + 3 halo rows are

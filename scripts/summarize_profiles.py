@@ -39,13 +39,18 @@ KERNELS = [
      "pass 1 of run k (4 mirrors) + tilt of run k-2 (reads 56 B, writes det2 + total2, 32 B) "
      "+ OPD of run k-3 (reads 32 B, writes 16 B)"),
 ]
+# the faithful chain's kernels (akb_griddata.hip): the cone solve's patch kernel and band sweep
+GD_SOURCES = ["akbraytracing_amd/csrc/akb_griddata.hip", "akbraytracing_amd/csrc/akb_common.h",
+              "akbraytracing_amd/csrc/akb_pairwise.h", "include/akb_raytrace.h"]
+GD_KERNELS = [("cone_patch", "akb::(anonymous namespace)::k_gd_cone_patch("),
+              ("cone_sweep8", "akb::(anonymous namespace)::k_gd_cone_sweep8(")]
 SIMDS = 1024  # 256 CUs x 4 SIMDs
 XCDS = 8
 
 
-def sources_sha256(root=ROOT):
+def sources_sha256(root=ROOT, sources=None):
     h = hashlib.sha256()
-    for rel in TRACE_SOURCES:
+    for rel in (TRACE_SOURCES if sources is None else sources):
         with open(os.path.join(root, rel), "rb") as f:
             h.update(f.read())
     return h.hexdigest()
@@ -151,9 +156,44 @@ def main(tag):
             continue
         tns = next((v for k, v in dur.items() if k.startswith(prefix)), None)
         summary["kernels"][key] = kernel_summary(name, pmc[name], pmc_dur.get(name), tns, bpr, n_rays, label)
-    with open(os.path.join(DST, f"{tag}_roofline.json"), "w") as f:
-        json.dump(summary, f, indent=1)
-    print(json.dumps(summary, indent=1))
+    if summary["kernels"]:
+        with open(os.path.join(DST, f"{tag}_roofline.json"), "w") as f:
+            json.dump(summary, f, indent=1)
+        print(json.dumps(summary, indent=1))
+    gd = {"tag": tag, "sources": GD_SOURCES, "sources_sha256": sources_sha256(sources=GD_SOURCES), "git_head": head,
+          "command": os.environ.get("AKB_PROFILE_CMD", ""), "kernels": {}}
+    for key, prefix in GD_KERNELS:
+        name = next((k for k in pmc if k.startswith(prefix)), None)
+        if name is None:
+            continue
+        d = pmc[name]
+        cycles = d.get("GRBM_GUI_ACTIVE", 0.0) / XCDS
+        valu, lds = d.get("SQ_INSTS_VALU"), d.get("SQ_INSTS_LDS")
+        add, mul = d.get("SQ_INSTS_VALU_ADD_F64", 0.0), d.get("SQ_INSTS_VALU_MUL_F64", 0.0)
+        fma, trans = d.get("SQ_INSTS_VALU_FMA_F64", 0.0), d.get("SQ_INSTS_VALU_TRANS_F64", 0.0)
+        gd["kernels"][key] = {
+            "kernel": name,
+            "avg_duration_ns_kernel_trace": next((v for k, v in dur.items() if k.startswith(prefix)), None),
+            "avg_duration_ns_pmc_runs": pmc_dur.get(name),
+            "effective_clock_ghz": cycles / pmc_dur[name] if pmc_dur.get(name) else None,
+            "hbm_bytes_per_launch": d.get("FETCH_SIZE", 0.0) * 1024 * 2 + d.get("WRITE_SIZE", 0.0) * 1024,
+            "valu_wave_instructions_per_launch": valu,
+            "fp64_flops_per_launch": 64 * (add + mul + trans + 2 * fma),
+            "lds_wave_instructions_per_launch": lds,
+            "lds_bank_conflict_cycles_per_launch": d.get("SQ_LDS_BANK_CONFLICT"),
+            "salu_per_launch": d.get("SQ_INSTS_SALU"),
+            "valu_busy_pct": (100.0 * d["SQ_ACTIVE_INST_VALU"] / 256 / cycles
+                              if d.get("SQ_ACTIVE_INST_VALU") and cycles else None),
+            "issue_frac": (valu * 4 / SIMDS / cycles) if valu and cycles else None,
+            "wait_any_frac": (d["SQ_WAIT_ANY"] / d["SQ_WAVE_CYCLES"]
+                              if d.get("SQ_WAIT_ANY") is not None and d.get("SQ_WAVE_CYCLES") else None),
+            "counters": d,
+        }
+    if gd["kernels"]:
+        with open(os.path.join(DST, f"{tag}_faithful_roofline.json"), "w") as f:
+            json.dump(gd, f, indent=1)
+        print(json.dumps({k: {q: v for q, v in d.items() if q != "counters"} for k, d in gd["kernels"].items()},
+                         indent=1))
 
 
 if __name__ == "__main__":

@@ -1124,6 +1124,56 @@ def test_griddata_cell_claim_equals_triangle_claim(gpu, monkeypatch, nv, nh, m):
     assert np.array_equal(got, want, equal_nan=True)
 
 
+@pytest.mark.parametrize("nv,nh,m,kind", [(97, 113, 40, "linspace"), (280, 300, 128, "linspace"),
+                                          (300, 280, 7, "linspace"), (33, 257, 300, "linspace"),
+                                          (97, 113, 60, "geometric"), (97, 113, 60, "repeated")])
+def test_griddata_fused_cell_claims(gpu, nv, nh, m, kind):
+    """The cell pass with the claims fused in (akb_gd_cells_claims_f64, then the pockets'
+    akb_gd_claim_pockets_f64 - FaithfulPupil's split) gives the two-pass claims' owners
+    (akb_gd_claims_f64) bit for bit, and akb_gd_cells_f64's diagonals and flags."""
+    import torch
+    from akbraytracing_amd import _lib
+    from akbraytracing_amd import device as D
+    from akbraytracing_amd.griddata import CubicGrid
+    L = _lib.lib()
+    X, Y, F = _lattice(nv, nh, nv * 5 + nh)
+    X = X * (nh / nv)
+    lo, hi = X.min(), X.max()
+    if kind == "linspace":
+        gx = np.linspace(lo, hi, m)
+    elif kind == "geometric":
+        gx = lo + (hi - lo) * (np.geomspace(1, 50, m) - 1) / 49
+    else:
+        gx = np.repeat(np.linspace(lo, hi, m // 2), 2)
+    gy = np.linspace(Y.min() - 1e-6, Y.max(), m + 3)
+    cg = CubicGrid(X.ravel(), Y.ravel(), nv, nh)
+    dev = cg.x.device
+    tgx, tgy = torch.tensor(gx, device=dev), torch.tensor(gy, device=dev)
+    mx, my = gx.size, gy.size
+    want = torch.empty(mx * my, dtype=torch.int32, device=dev)
+    _lib.check(L.akb_gd_claims_f64(D.ptr(cg.x), D.ptr(cg.y), nv, nh, D.ptr(cg.diag), cg.npock, D.ptr(cg.ptri),
+                                   D.ptr(cg.pnbr), D.ptr(cg.edge_tri), 0, -1, 1, D.ptr(tgx), mx, D.ptr(tgy), my,
+                                   D.ptr(want), None, None))
+    got = torch.empty_like(want)
+    diag = torch.empty_like(cg.diag)
+    flags = torch.zeros(1, dtype=torch.int32, device=dev)
+    _lib.check(L.akb_gd_cells_claims_f64(D.ptr(cg.x), D.ptr(cg.y), nv, nh, D.ptr(diag), 1e-10, D.ptr(flags),
+                                         D.ptr(tgx), mx, D.ptr(tgy), my, D.ptr(got), None))
+    _lib.check(L.akb_gd_claim_pockets_f64(D.ptr(cg.x), D.ptr(cg.y), nv, nh, D.ptr(diag), cg.npock, D.ptr(cg.ptri),
+                                          D.ptr(tgx), mx, D.ptr(tgy), my, D.ptr(got), None))
+    torch.cuda.synchronize()
+    assert torch.equal(diag, cg.diag)
+    flags2 = torch.zeros(1, dtype=torch.int32, device=dev)
+    ring = torch.empty(2 * cg.L, dtype=torch.float64, device=dev)
+    _lib.check(L.akb_gd_cells_f64(D.ptr(cg.x), D.ptr(cg.y), nv, nh, D.ptr(diag), 1e-10, D.ptr(flags2),
+                                  D.ptr(ring[:cg.L]), D.ptr(ring[cg.L:]), None))
+    torch.cuda.synchronize()
+    assert int(flags.item()) == int(flags2.item())
+    assert torch.equal(got, want)
+    claimed = (want != np.iinfo(np.int32).max).float().mean().item()
+    assert 0.3 < claimed < 1.0  # targets inside and outside the hull
+
+
 @pytest.mark.parametrize("kind", ["geometric", "jittered", "repeated"])
 def test_griddata_nonuniform_axes(gpu, monkeypatch, kind):
     """Target axes that are ascending but not evenly spaced take the binary-search claim inside the
