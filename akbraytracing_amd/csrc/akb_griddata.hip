@@ -350,11 +350,11 @@ __device__ __forceinline__ bool axes_uniform(const Targets& t) {
 }
 
 // ---- the claims fused into the cell pass (the cone solve's single-process path): while
-// k_gd_cells_tiled holds a tile's vertices and diagonals in LDS, the tile's bounding box is tested
-// against the target axes and only a tile that can hold a target claims, cell by cell - claim_cell
-// on the LDS copies (the same boxes, the same candidate pairs, bary's arithmetic on the same
-// values: the same owners as k_gd_claim_scan + k_gd_claim_hit), with no second pass over the
-// lattice
+// k_gd_cells_tiled holds a tile's vertices and diagonals in LDS, the targets in the tile's bounding
+// box (rarely more than one or two: the 128^2 targets sit ~25 cells apart at C3) are tested by
+// every cell of the tile against its two triangles from the LDS copies - claim_cell's box predicate
+// and bary's arithmetic on the same values, so the same owners as k_gd_claim_scan + k_gd_claim_hit,
+// with no second pass over the lattice and no per-cell index search
 struct TileClaims {
     Targets t;   // the target axes (the device's linspaces, k_gd_axes)
     int* owner;  // (my, mx), INT32_MAX-filled before the pass
@@ -366,9 +366,14 @@ __device__ __forceinline__ void bary_lds(const double* vx, const double* vy, con
     const double a00 = vx[k[0]] - x2, a01 = vx[k[1]] - x2;
     const double a10 = vy[k[0]] - y2, a11 = vy[k[1]] - y2;
     const double det = a00 * a11 - a01 * a10;
-    const double t00 = a11 / det, t01 = -a01 / det, t10 = -a10 / det, t11 = a00 / det;
     const double dx = px - x2, dy = py - y2;
+    const double t00 = a11 / det, t01 = -a01 / det;
     b[0] = t00 * dx + t01 * dy;
+    // the second row's divisions after the first's (an empty asm ties det to b[0]): two IEEE
+    // divisions in flight instead of four keep the cell pass at its 8 waves per SIMD
+    double det1 = det;
+    asm volatile("" : "+v"(det1) : "v"(b[0]));
+    const double t10 = -a10 / det1, t11 = a00 / det1;
     b[1] = t10 * dx + t11 * dy;
     b[2] = 1.0 - b[0] - b[1];
 }
@@ -380,8 +385,7 @@ __device__ void tile_claims(const Grid& g, const TileClaims& tc, bool uniform, d
     const Targets& t = tc.t;
     const int tid = threadIdx.x;
     const int nr = min(T, r_hi - iv0), nc = min(T, g.nh - 1 - ih0);  // the tile's cells
-    // the tile's box over its (nr + 1) x (nc + 1) vertices (a superset of each cell's box; fmin and
-    // fmax pass over a NaN as claim_cell's do, an infinite vertex leaves the tile to the cells)
+    // the tile's box over its (nr + 1) x (nc + 1) vertices (fmin / fmax pass over a NaN)
     double xlo = INFINITY, xhi = -INFINITY, ylo = INFINITY, yhi = -INFINITY;
     for (int k = tid; k < (nr + 1) * (nc + 1); k += T * T) {
         const int r = k / (nc + 1), c = k - (k / (nc + 1)) * (nc + 1);
@@ -408,77 +412,60 @@ __device__ void tile_claims(const Grid& g, const TileClaims& tc, bool uniform, d
     xhi = fmax(fmax(sbox[1][0], sbox[1][1]), fmax(sbox[1][2], sbox[1][3]));
     ylo = fmin(fmin(sbox[2][0], sbox[2][1]), fmin(sbox[2][2], sbox[2][3]));
     yhi = fmax(fmax(sbox[3][0], sbox[3][1]), fmax(sbox[3][2], sbox[3][3]));
-    if (isfinite(xlo) && isfinite(xhi) && isfinite(ylo) && isfinite(yhi)) {
-        const double padx = (xhi - xlo) * 1e-9, pady = (yhi - ylo) * 1e-9;
-        int c0, c1, r0, r1;
-        const bool hit = uniform ? axis_range(t.gx, t.mx, inv_dx, xlo - padx, xhi + padx, c0, c1) &&
-                                       axis_range(t.gy, t.my, inv_dy, ylo - pady, yhi + pady, r0, r1)
-                                 : lower_idx(t.gx, t.mx, xlo - padx) < lower_idx(t.gx, t.mx, xhi + padx) &&
-                                       lower_idx(t.gy, t.my, ylo - pady) < lower_idx(t.gy, t.my, yhi + pady);
-        if (!hit) return;
+    // the tile's candidate targets: a superset of every triangle's (a triangle's padded box lies in
+    // the tile's), from the linspace estimate or the exact binary search
+    const double padx = (xhi - xlo) * 1e-9, pady = (yhi - ylo) * 1e-9;
+    int c0, c1, r0, r1;
+    if (uniform) {
+        if (!axis_range(t.gx, t.mx, inv_dx, xlo - padx, xhi + padx, c0, c1)) return;
+        if (!axis_range(t.gy, t.my, inv_dy, ylo - pady, yhi + pady, r0, r1)) return;
+    } else {
+        c0 = lower_idx(t.gx, t.mx, xlo - padx);
+        c1 = lower_idx(t.gx, t.mx, xhi + padx);
+        r0 = lower_idx(t.gy, t.my, ylo - pady);
+        r1 = lower_idx(t.gy, t.my, yhi + pady);
+        if (c0 >= c1 || r0 >= r1) return;
     }
     const int rr = tid / T, cc = tid - (tid / T) * T;
     if (rr >= nr || cc >= nc) return;
-    // claim_cell on the LDS copies
+    // this cell's two triangles (tri_verts' vertex order), formed per candidate target from LDS (a
+    // tile holds one or two: nothing is kept in registers across them). A target is claimed by a
+    // triangle when it lies in the triangle's box as claim_cell bounds it (lo - pad <= coordinate <
+    // hi + pad) and passes bary's test - the same predicate, the same atomicMin, in any order
     const int k00 = rr * V + cc, k01 = k00 + 1, k10 = k00 + V, k11 = k10 + 1;
     const int64_t c = (int64_t)(iv0 + rr) * (g.nh - 1) + (ih0 + cc);
-    const double xa = vx[k00], xb = vx[k01], xc = vx[k10], xd = vx[k11];
-    const double ya = vy[k00], yb = vy[k01], yc = vy[k10], yd = vy[k11];
-    const double cxlo = fmin(fmin(xa, xb), fmin(xc, xd)), cxhi = fmax(fmax(xa, xb), fmax(xc, xd));
-    const double cylo = fmin(fmin(ya, yb), fmin(yc, yd)), cyhi = fmax(fmax(ya, yb), fmax(yc, yd));
-    const double padx = (cxhi - cxlo) * 1e-9, pady = (cyhi - cylo) * 1e-9;
-    int c0, c1, r0, r1;
-    if (uniform) {
-        if (!axis_range(t.gx, t.mx, inv_dx, cxlo - padx, cxhi + padx, c0, c1)) return;
-        if (!axis_range(t.gy, t.my, inv_dy, cylo - pady, cyhi + pady, r0, r1)) return;
-    } else {
-        c0 = lower_idx(t.gx, t.mx, cxlo - padx);
-        c1 = lower_idx(t.gx, t.mx, cxhi + padx);
-        r0 = lower_idx(t.gy, t.my, cylo - pady);
-        r1 = lower_idx(t.gy, t.my, cyhi + pady);
-        if (c0 >= c1 || r0 >= r1) return;
-    }
-    while (c0 < c1 && t.gx[c0] < cxlo - padx) ++c0;
-    while (c1 > c0 && t.gx[c1 - 1] >= cxhi + padx) --c1;
-    if (c0 >= c1) return;
-    while (r0 < r1 && t.gy[r0] < cylo - pady) ++r0;
-    while (r1 > r0 && t.gy[r1 - 1] >= cyhi + pady) --r1;
-    if (r0 >= r1) return;
     const int d = sdg[rr * (T + 1) + cc];
-    for (int half = 0; half < 2; ++half) {
-        // tri_verts' vertex order: diag 0: (p00, p01, p11), (p00, p11, p10); diag 1: (p00, p01, p10), (p01, p11, p10)
-        int kv[3];
-        if (d == 0) {
-            kv[0] = k00;
-            kv[1] = half == 0 ? k01 : k11;
-            kv[2] = half == 0 ? k11 : k10;
-        } else {
-            kv[0] = half == 0 ? k00 : k01;
-            kv[1] = half == 0 ? k01 : k11;
-            kv[2] = k10;
-        }
-        double txlo = vx[kv[0]], txhi = txlo, tylo = vy[kv[0]], tyhi = tylo;
-        for (int k = 1; k < 3; ++k) {
-            txlo = fmin(txlo, vx[kv[k]]);
-            txhi = fmax(txhi, vx[kv[k]]);
-            tylo = fmin(tylo, vy[kv[k]]);
-            tyhi = fmax(tyhi, vy[kv[k]]);
-        }
-        const double tpx = (txhi - txlo) * 1e-9, tpy = (tyhi - tylo) * 1e-9;
-        int tc0 = c0, tr0 = r0;
-        while (tc0 < c1 && t.gx[tc0] < txlo - tpx) ++tc0;
-        int tc1 = tc0;
-        while (tc1 < c1 && t.gx[tc1] < txhi + tpx) ++tc1;
-        while (tr0 < r1 && t.gy[tr0] < tylo - tpy) ++tr0;
-        int tr1 = tr0;
-        while (tr1 < r1 && t.gy[tr1] < tyhi + tpy) ++tr1;
-        for (int r = tr0; r < tr1; ++r)
-            for (int q = tc0; q < tc1; ++q) {
+    for (int r = r0; r < r1; ++r) {
+        for (int q = c0; q < c1; ++q) {
+            asm volatile("" ::: "memory");  // (compiler barrier: the LDS reads stay in the loop)
+            const double px = t.gx[q], py = t.gy[r];
+#pragma unroll 1
+            for (int half = 0; half < 2; ++half) {
+                int kv[3];
+                if (d == 0) {
+                    kv[0] = k00;
+                    kv[1] = half == 0 ? k01 : k11;
+                    kv[2] = half == 0 ? k11 : k10;
+                } else {
+                    kv[0] = half == 0 ? k00 : k01;
+                    kv[1] = half == 0 ? k01 : k11;
+                    kv[2] = k10;
+                }
+                double txlo = vx[kv[0]], txhi = txlo, tylo = vy[kv[0]], tyhi = tylo;
+                for (int k = 1; k < 3; ++k) {
+                    txlo = fmin(txlo, vx[kv[k]]);
+                    txhi = fmax(txhi, vx[kv[k]]);
+                    tylo = fmin(tylo, vy[kv[k]]);
+                    tyhi = fmax(tyhi, vy[kv[k]]);
+                }
+                const double tpx = (txhi - txlo) * 1e-9, tpy = (tyhi - tylo) * 1e-9;
+                if (!(px >= txlo - tpx && px < txhi + tpx && py >= tylo - tpy && py < tyhi + tpy)) continue;
                 double b[3];
-                bary_lds(vx, vy, kv, t.gx[q], t.gy[r], b);
+                bary_lds(vx, vy, kv, px, py, b);
                 if (b[0] >= -kInsideEps && b[1] >= -kInsideEps && b[2] >= -kInsideEps)
                     atomicMin(&tc.owner[(int64_t)r * t.mx + q], (int)(2 * c + half));
             }
+        }
     }
 }
 
@@ -551,36 +538,38 @@ __global__ void __launch_bounds__(kCellTile * kCellTile) k_gd_cells_tiled(Grid g
                 (jv < g.nv - 1 && jh < g.nh - 1 && jv <= r_hi) ? (uint8_t)diag_of(r2, c2, nullptr) : (uint8_t)0;
         }
         __syncthreads();
-        if constexpr (kClaims) tile_claims(g, tc, uniform, inv_dx, inv_dy, vx, vy, sdg, iv0, ih0, r_hi);  // (a barrier)
-        if (!own) continue;
-        const int64_t c = (int64_t)iv * (g.nh - 1) + ih;
-        diag[c] = (uint8_t)d;
-        unsigned f = bad > 0 ? 1u : 0u;
-        const int k00 = rr * V + cc, k01 = k00 + 1, k10 = k00 + V, k11 = k10 + 1;
-        if (!isfinite(vx[k00]) || !isfinite(vy[k00])) f |= 32u;
-        {
-            const double o = orient(vx[k00], vy[k00], vx[k01], vy[k01], vx[k11], vy[k11]);
-            f |= o > 0 ? 8u : (o < 0 ? 16u : 1u);
+        if (own) {
+            const int64_t c = (int64_t)iv * (g.nh - 1) + ih;
+            diag[c] = (uint8_t)d;
+            unsigned f = bad > 0 ? 1u : 0u;
+            const int k00 = rr * V + cc, k01 = k00 + 1, k10 = k00 + V, k11 = k10 + 1;
+            if (!isfinite(vx[k00]) || !isfinite(vy[k00])) f |= 32u;
+            {
+                const double o = orient(vx[k00], vy[k00], vx[k01], vy[k01], vx[k11], vy[k11]);
+                f |= o > 0 ? 8u : (o < 0 ? 16u : 1u);
+            }
+            if (ih + 1 < g.nh - 1) {  // right edge p01-p11 against the next cell's left triangle
+                const int dn = sdg[rr * (T + 1) + cc + 1];
+                const int mine = d == 0 ? k00 : k10, other = dn == 0 ? k11 + 1 : k01 + 1;
+                const double x0 = vx[k01], y0 = vy[k01];
+                const double ax = vx[mine] - x0, ay = vy[mine] - y0, cx = vx[k11] - x0, cy = vy[k11] - y0;
+                const double ox = vx[other] - x0, oy = vy[other] - y0;
+                const double sc = fmax(fmax(fabs(ax), fabs(ay)), fmax(fmax(fabs(cx), fabs(cy)), fmax(fabs(ox), fabs(oy))));
+                if (incircle(0.0, 0.0, ax, ay, cx, cy, ox, oy) > tol * sc * sc * sc * sc) f |= 2u;
+            }
+            if (iv + 1 < g.nv - 1) {  // top edge p10-p11 against the next row's bottom triangle
+                const int dn = sdg[(rr + 1) * (T + 1) + cc];
+                const int mine = d == 0 ? k00 : k01, other = dn == 0 ? k11 + V : k10 + V;
+                const double x0 = vx[k10], y0 = vy[k10];
+                const double ax = vx[mine] - x0, ay = vy[mine] - y0, cx = vx[k11] - x0, cy = vy[k11] - y0;
+                const double ox = vx[other] - x0, oy = vy[other] - y0;
+                const double sc = fmax(fmax(fabs(ax), fabs(ay)), fmax(fmax(fabs(cx), fabs(cy)), fmax(fabs(ox), fabs(oy))));
+                if (incircle(0.0, 0.0, ax, ay, cx, cy, ox, oy) > tol * sc * sc * sc * sc) f |= 2u;
+            }
+            acc |= f;
         }
-        if (ih + 1 < g.nh - 1) {  // right edge p01-p11 against the next cell's left triangle
-            const int dn = sdg[rr * (T + 1) + cc + 1];
-            const int mine = d == 0 ? k00 : k10, other = dn == 0 ? k11 + 1 : k01 + 1;
-            const double x0 = vx[k01], y0 = vy[k01];
-            const double ax = vx[mine] - x0, ay = vy[mine] - y0, cx = vx[k11] - x0, cy = vy[k11] - y0;
-            const double ox = vx[other] - x0, oy = vy[other] - y0;
-            const double sc = fmax(fmax(fabs(ax), fabs(ay)), fmax(fmax(fabs(cx), fabs(cy)), fmax(fabs(ox), fabs(oy))));
-            if (incircle(0.0, 0.0, ax, ay, cx, cy, ox, oy) > tol * sc * sc * sc * sc) f |= 2u;
-        }
-        if (iv + 1 < g.nv - 1) {  // top edge p10-p11 against the next row's bottom triangle
-            const int dn = sdg[(rr + 1) * (T + 1) + cc];
-            const int mine = d == 0 ? k00 : k01, other = dn == 0 ? k11 + V : k10 + V;
-            const double x0 = vx[k10], y0 = vy[k10];
-            const double ax = vx[mine] - x0, ay = vy[mine] - y0, cx = vx[k11] - x0, cy = vy[k11] - y0;
-            const double ox = vx[other] - x0, oy = vy[other] - y0;
-            const double sc = fmax(fmax(fabs(ax), fabs(ay)), fmax(fmax(fabs(cx), fabs(cy)), fmax(fabs(ox), fabs(oy))));
-            if (incircle(0.0, 0.0, ax, ay, cx, cy, ox, oy) > tol * sc * sc * sc * sc) f |= 2u;
-        }
-        acc |= f;
+        // the tile's claims after its checks (their registers are dead by then; a barrier inside)
+        if constexpr (kClaims) tile_claims(g, tc, uniform, inv_dx, inv_dy, vx, vy, sdg, iv0, ih0, r_hi);
     }
     for (int off = 32; off > 0; off >>= 1) acc |= __shfl_down(acc, off);
     if ((threadIdx.x & 63) == 0) {
