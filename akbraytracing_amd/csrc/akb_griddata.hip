@@ -1206,39 +1206,64 @@ constexpr int kClaimAxisLds = 512;                // target axes up to this long
 constexpr int kConeMaxK = 14;                    // patch box side 2K + 4 <= 32
 constexpr int kConeBox = 2 * kConeMaxK + 4;  // the largest box side: it fits the patches' LDS pitch
 
-// the boundary band: vertices with min(iv, ih, nv - 1 - iv, nh - 1 - ih) <= D, enumerated as the
-// top rows, the bottom rows, then the left / right column pieces of the rows between
-struct BandMap {
-    int nv, nh, D;
-    int rows_top, rows_bot, mid0, mid1, cols;  // full rows [0, rows_top), [nv - rows_bot, nv); side columns
-    int64_t n_top, n_bot, n_mid, total;
+// the boundary band: vertices with min(iv, ih, nv - 1 - iv, nh - 1 - ih) <= D, as four regions -
+// the top rows [0, rt), the bottom rows [rb, nv), and between them the left columns [0, cl) and the
+// right columns [cr, nh) - cut into kBandTR x kBandTC tiles (every band vertex in one tile)
+constexpr int kBandTR = 16, kBandTC = 32;
+struct BandTiles {
+    int D, rt, rb, cl, cr;
+    int ncb, top_rb, bot_rb, mid_rb, lcb, rcb;  // column blocks (top / bottom), row blocks, side column blocks
+    int n_top, n_bot, n_left, total;            // tile counts (the right side's are the rest)
 };
 
-inline BandMap band_map(int nv, int nh, int D) {
-    BandMap b{nv, nh, D, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    b.rows_top = std::min(D + 1, nv);
-    b.rows_bot = std::min(D + 1, nv - b.rows_top);
-    b.mid0 = b.rows_top;
-    b.mid1 = nv - b.rows_bot;
-    b.cols = std::min(D + 1, nh / 2);
-    const bool full_mid = 2 * (D + 1) >= nh;
-    b.n_top = (int64_t)b.rows_top * nh;
-    b.n_bot = (int64_t)b.rows_bot * nh;
-    b.n_mid = (int64_t)(b.mid1 - b.mid0) * (full_mid ? nh : 2 * b.cols);
-    if (full_mid) b.cols = -1;
-    b.total = b.n_top + b.n_bot + b.n_mid;
+inline BandTiles band_tiles(int nv, int nh, int D) {
+    BandTiles b{};
+    b.D = D;
+    b.rt = std::min(D + 1, nv);
+    b.rb = std::max(nv - (D + 1), b.rt);
+    b.cl = std::min(D + 1, nh);
+    b.cr = std::max(nh - (D + 1), b.cl);
+    auto cdiv = [](int a, int q) { return (a + q - 1) / q; };
+    b.ncb = cdiv(nh, kBandTC);
+    b.top_rb = cdiv(b.rt, kBandTR);
+    b.bot_rb = cdiv(nv - b.rb, kBandTR);
+    b.mid_rb = cdiv(b.rb - b.rt, kBandTR);
+    b.lcb = cdiv(b.cl, kBandTC);
+    b.rcb = cdiv(nh - b.cr, kBandTC);
+    b.n_top = b.top_rb * b.ncb;
+    b.n_bot = b.bot_rb * b.ncb;
+    b.n_left = b.mid_rb * b.lcb;
+    b.total = b.n_top + b.n_bot + b.n_left + b.mid_rb * b.rcb;
     return b;
 }
 
-__device__ __forceinline__ int64_t band_vertex(const BandMap& b, int64_t k) {
-    if (k < b.n_top) return k;
-    k -= b.n_top;
-    if (k < b.n_bot) return (int64_t)(b.nv - b.rows_bot) * b.nh + k;
-    k -= b.n_bot;
-    if (b.cols < 0) return (int64_t)b.mid0 * b.nh + k;
-    const int w = 2 * b.cols;
-    const int r = b.mid0 + (int)(k / w), c = (int)(k - (int64_t)(k / w) * w);
-    return (int64_t)r * b.nh + (c < b.cols ? c : b.nh - 2 * b.cols + c);
+// tile t's origin and its region's end: rows [r0, r1) x columns [c0, c1) of the tile's vertices
+__device__ __forceinline__ void band_tile(const BandTiles& b, int nv, int nh, int t, int& r0, int& c0, int& r1,
+                                          int& c1) {
+    if (t < b.n_top) {
+        r0 = (t / b.ncb) * kBandTR;
+        c0 = (t % b.ncb) * kBandTC;
+        r1 = b.rt;
+        c1 = nh;
+    } else if ((t -= b.n_top) < b.n_bot) {
+        r0 = b.rb + (t / b.ncb) * kBandTR;
+        c0 = (t % b.ncb) * kBandTC;
+        r1 = nv;
+        c1 = nh;
+    } else if ((t -= b.n_bot) < b.n_left) {
+        r0 = b.rt + (t / b.lcb) * kBandTR;
+        c0 = (t % b.lcb) * kBandTC;
+        r1 = b.rb;
+        c1 = b.cl;
+    } else {
+        t -= b.n_left;
+        r0 = b.rt + (t / b.rcb) * kBandTR;
+        c0 = b.cr + (t % b.rcb) * kBandTC;
+        r1 = b.rb;
+        c1 = nh;
+    }
+    r1 = min(r1, r0 + kBandTR);
+    c1 = min(c1, c0 + kBandTC);
 }
 
 struct ConeBand {
@@ -1249,6 +1274,22 @@ struct ConeBand {
     ConeStep st;
     const int* needed;    // device flag: some target needs the band (else the launch returns at once)
 };
+
+// the lattice edges of a band vertex in the fixed order (left, right, down, up, the diagonals), from
+// its neighbours' data - the one arithmetic of the gather kernel and the tiles
+__device__ __forceinline__ void band_edges(GradAcc<1>& A, double xi, double yi, double fi, const double (&xs)[8],
+                                           const double (&ys)[8], const double (&fs)[8], const double (&gxs)[8],
+                                           const double (&gys)[8], const bool (&on)[8]) {
+    const double fi1[1] = {fi};
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        if (on[k]) {
+            const double fj[1] = {fs[k]}, gxj[1] = {gxs[k]}, gyj[1] = {gys[k]};
+            if (k < 4) acc_edge<1, false>(A, edge_geom(xs[k] - xi, ys[k] - yi), fi1, fj, gxj, gyj);
+            else acc_edge<1, true>(A, edge_geom(xs[k] - xi, ys[k] - yi), fi1, fj, gxj, gyj);
+        }
+    acc_fold<1>(A);
+}
 
 // vertex i's lattice-edge sums of one band sweep: every candidate neighbour's data loaded first
 // (positions off the lattice clamped to i, the diagonals' presence from their cells' bytes, loaded
@@ -1276,15 +1317,7 @@ __device__ __forceinline__ void band_grid_sums(const Grid& g, const ConeBand& a,
     }
     const bool on[8] = {L, R, D, U, inb[4] && dg[0] == 0, inb[5] && dg[1] == 1, inb[6] && dg[2] == 1,
                         inb[7] && dg[3] == 0};
-    const double fi1[1] = {fi};
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-        if (on[k]) {
-            const double fj[1] = {fs[k]}, gxj[1] = {gxs[k]}, gyj[1] = {gys[k]};
-            if (k < 4) acc_edge<1, false>(A, edge_geom(xs[k] - xi, ys[k] - yi), fi1, fj, gxj, gyj);
-            else acc_edge<1, true>(A, edge_geom(xs[k] - xi, ys[k] - yi), fi1, fj, gxj, gyj);
-        }
-    acc_fold<1>(A);
+    band_edges(A, xi, yi, fi, xs, ys, fs, gxs, gys, on);
 }
 
 // the solve of one band / ring vertex of sweep j, stored to x_j
@@ -1319,27 +1352,71 @@ __device__ __forceinline__ void cone_ring_vertex(const Grid& g, const ConeBand& 
     }
 }
 
-// one sweep of the band in one launch: workgroups [0, nbw) take the band's vertices off the ring,
-// the rest eight ring vertices per wave (8-lane groups; a vertex with more than eight chords takes
-// the whole wave afterwards). Both halves read x_{j-1} / x_{j-2} only.
-__global__ void __launch_bounds__(kBlock) k_gd_cone_sweep8(Grid g, BandMap bm, ConeBand a, int nbw) {
+// one sweep of the band in one launch: workgroups [0, nbt) take a band tile each - its vertices
+// and their neighbours' x, y, f and x_{j-1} (and the cells' diagonals) staged in LDS by coalesced
+// row loads, then one thread per vertex off the ring (band_edges from LDS: the gather kernel's
+// arithmetic) - the rest eight ring vertices per wave (8-lane groups; a vertex with more than eight
+// chords takes the whole wave afterwards). Both halves read x_{j-1} / x_{j-2} only.
+constexpr int kBandThreads = kBandTR * kBandTC;
+__global__ void __launch_bounds__(kBandThreads) k_gd_cone_band(Grid g, BandTiles bt, ConeBand a, int nbt) {
     if (!*a.needed) return;
-    if ((int)blockIdx.x < nbw) {
-        for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < bm.total;
-             k += (int64_t)nbw * blockDim.x) {
-            const int64_t i = band_vertex(bm, k);
-            const int iv = (int)(i / g.nh), ih = (int)(i - (int64_t)iv * g.nh);
-            if (ring_pos(g, iv, ih) >= 0) continue;
-            GradAcc<1> A;
-            band_grid_sums(g, a, i, iv, ih, g.x[i], g.y[i], a.f[i], A);
-            band_solve(a, i, A);
+    if ((int)blockIdx.x < nbt) {
+        constexpr int HR = kBandTR + 2, HC = kBandTC + 2, HN = HR * HC, CC = kBandTC + 1;
+        __shared__ double sx[HN], sy[HN], sf[HN], sgx[HN], sgy[HN];
+        __shared__ uint8_t sdg[(kBandTR + 1) * CC];
+        int r0, c0, r1, c1;
+        band_tile(bt, g.nv, g.nh, blockIdx.x, r0, c0, r1, c1);
+        // the tile's vertices with a one-vertex halo (rows r0 - 1 .. r0 + TR, inside the lattice)
+        for (int k = threadIdx.x; k < HN; k += kBandThreads) {
+            const int iv = r0 - 1 + k / HC, ih = c0 - 1 + (k - (k / HC) * HC);
+            if (iv >= 0 && iv < g.nv && ih >= 0 && ih < g.nh) {
+                const int64_t q = (int64_t)iv * g.nh + ih;
+                sx[k] = g.x[q];
+                sy[k] = g.y[q];
+                sf[k] = a.f[q];
+                sgx[k] = a.gin ? a.gin[2 * q] : 0.0;
+                sgy[k] = a.gin ? a.gin[2 * q + 1] : 0.0;
+            }
         }
+        // the diagonals of cells (r0 - 1 .. r0 + TR - 1) x (c0 - 1 .. c0 + TC - 1)
+        for (int k = threadIdx.x; k < (kBandTR + 1) * CC; k += kBandThreads) {
+            const int cv = r0 - 1 + k / CC, ch = c0 - 1 + (k - (k / CC) * CC);
+            sdg[k] = (cv >= 0 && cv < g.nv - 1 && ch >= 0 && ch < g.nh - 1) ? g.diag[(int64_t)cv * (g.nh - 1) + ch] : 0;
+        }
+        __syncthreads();
+        const int tr = threadIdx.x / kBandTC, tc = threadIdx.x - (threadIdx.x / kBandTC) * kBandTC;
+        const int iv = r0 + tr, ih = c0 + tc;
+        if (iv >= r1 || ih >= c1 || ring_pos(g, iv, ih) >= 0) return;
+        const bool L = ih > 0, R = ih < g.nh - 1, D = iv > 0, U = iv < g.nv - 1;
+        const int li = (tr + 1) * HC + (tc + 1);
+        const int jn[8] = {li - 1, li + 1, li - HC, li + HC, li - HC - 1, li - HC + 1, li + HC - 1, li + HC + 1};
+        const bool inb[8] = {L, R, D, U, D && L, D && R, U && L, U && R};
+        const int lc = tr * CC + tc;  // cell (iv - 1, ih - 1)
+        const int dc[4] = {lc, lc + 1, lc + CC, lc + CC + 1};
+        uint8_t dg[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) dg[k] = inb[4 + k] ? sdg[dc[k]] : 0;
+        double xs[8], ys[8], fs[8], gxs[8], gys[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int j = inb[k] ? jn[k] : li;
+            xs[k] = sx[j];
+            ys[k] = sy[j];
+            fs[k] = sf[j];
+            gxs[k] = sgx[j];
+            gys[k] = sgy[j];
+        }
+        const bool on[8] = {L, R, D, U, inb[4] && dg[0] == 0, inb[5] && dg[1] == 1, inb[6] && dg[2] == 1,
+                            inb[7] && dg[3] == 0};
+        GradAcc<1> A;
+        band_edges(A, sx[li], sy[li], sf[li], xs, ys, fs, gxs, gys, on);
+        band_solve(a, (int64_t)iv * g.nh + ih, A);
         return;
     }
     const int64_t L = 2 * (int64_t)(g.nh - 1) + 2 * (int64_t)(g.nv - 1);
     const int lane = threadIdx.x & 63, sub = lane & 7;
-    const int64_t w0 = ((int64_t)(blockIdx.x - nbw) * blockDim.x + threadIdx.x) >> 6;
-    const int64_t nw = ((int64_t)(gridDim.x - nbw) * blockDim.x) >> 6;
+    const int64_t w0 = ((int64_t)(blockIdx.x - nbt) * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nw = ((int64_t)(gridDim.x - nbt) * blockDim.x) >> 6;
     for (int64_t r0 = w0 * 8; r0 < L; r0 += nw * 8) {
         const int64_t r = r0 + (lane >> 3);
         const bool big = r < L && g.xptr[r + 1] - g.xptr[r] > 8;
@@ -1691,6 +1768,16 @@ __global__ void __launch_bounds__(kAxesThreads) k_gd_axes(const double* __restri
 // a sharded lattice's targets: this rank forms the interior targets whose cell's p00 lies in its
 // rays [own0, own1); the band owner forms every band and pocket target. assigned[t] = 1 for the
 // targets formed here; the interior ones' cells go to the patch list
+// whether triangle o lies in an interior target cell (a patch's: its (2K + 4)^2 box clear of the
+// ring by one vertex), and that cell and its p00 vertex; else the boundary band forms its corners
+__device__ __forceinline__ bool cone_interior(const Grid& g, int o, int K, int64_t& c, int64_t& p00) {
+    if (o >= 2 * ncells(g)) return false;
+    c = o >> 1;
+    const int iv = (int)(c / (g.nh - 1)), ih = (int)(c - (int64_t)iv * (g.nh - 1));
+    p00 = (int64_t)iv * g.nh + ih;
+    return iv - K - 1 >= 1 && iv + K + 2 <= g.nv - 2 && ih - K - 1 >= 1 && ih + K + 2 <= g.nh - 2;
+}
+
 __global__ void __launch_bounds__(kBlock) k_gd_cone_assign(Grid g, const int* __restrict__ owner, int64_t m, int K,
                                                             int64_t own0, int64_t own1, int band_on, int64_t* cells,
                                                             int* count, int* band, uint8_t* assigned) {
@@ -1699,14 +1786,8 @@ __global__ void __launch_bounds__(kBlock) k_gd_cone_assign(Grid g, const int* __
         const int o = owner[t];
         uint8_t mine = 0;
         if (o != INT32_MAX) {
-            bool interior = false;
             int64_t c = -1, p00 = -1;
-            if (o < nc2) {
-                c = o >> 1;
-                const int iv = (int)(c / (g.nh - 1)), ih = (int)(c - (int64_t)iv * (g.nh - 1));
-                interior = iv - K - 1 >= 1 && iv + K + 2 <= g.nv - 2 && ih - K - 1 >= 1 && ih + K + 2 <= g.nh - 2;
-                p00 = (int64_t)iv * g.nh + ih;
-            }
+            const bool interior = cone_interior(g, o, K, c, p00);
             if (interior) {
                 if (p00 >= own0 && p00 < own1) {
                     cells[atomicAdd(count, 1)] = c;
@@ -2022,9 +2103,50 @@ __device__ double clough_tocher(const Grid& g, int64_t tid, const Tri& T, const 
 }
 
 // nvals value sets share the triangulation: f / grad / out strided by n / 2n / mx*my
+// The cone solve's estimates at the band's targets (be.y != nullptr: the band's one more plain
+// sweep y from x_K): the patch kernel's change measure and value-error estimate (see cell_est) over
+// the vertices of each target's triangle that is not an interior cell's - the boundary cells' and
+// the pocket triangles', whose long edges carry a gradient error furthest - as ordered double bits
+struct BandEst {
+    const double* y;  // (n, 2) or nullptr
+    int K;
+    unsigned long long* chg;
+    unsigned long long* est;
+};
+
+__device__ __forceinline__ void band_target_est(const Grid& g, const BandEst& be, int o, const Tri& T,
+                                                const double* grad, double& cmax, double& emax) {
+    int64_t c, p00;
+    if (cone_interior(g, o, be.K, c, p00)) return;
+    double d = 0.0, h2 = 0.0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int64_t v = T.v[k], w = T.v[(k + 1) % 3];
+        const double gx = grad[2 * v], gy = grad[2 * v + 1], y0 = be.y[2 * v], y1 = be.y[2 * v + 1];
+        d = fmax(d, fmax(fabs(gx - y0), fabs(gy - y1)));
+        cmax = fmax(cmax, change_of(gx, gy, y0, y1));
+        const double ex = g.x[w] - g.x[v], ey = g.y[w] - g.y[v];
+        h2 = fmax(h2, ex * ex + ey * ey);
+    }
+    emax = fmax(emax, 2.0 * 1.4142135623730951 * d * sqrt(h2));
+}
+
+__device__ __forceinline__ void band_est_store(const BandEst& be, double cmax, double emax) {
+    for (int off = 32; off > 0; off >>= 1) {
+        cmax = fmax(cmax, __shfl_down(cmax, off));
+        emax = fmax(emax, __shfl_down(emax, off));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (be.chg && cmax > 0) atomicMax(be.chg, (unsigned long long)__double_as_longlong(cmax));
+        if (be.est && emax > 0) atomicMax(be.est, (unsigned long long)__double_as_longlong(emax));
+    }
+}
+
 __global__ void __launch_bounds__(kBlock) k_gd_eval(Grid g, Targets t, const int* __restrict__ owner,
-                                                    const double* f, const double* grad, int nvals, double* out) {
+                                                    const double* f, const double* grad, int nvals, double* out,
+                                                    BandEst be = BandEst{nullptr, 0, nullptr, nullptr}) {
     const int64_t m = (int64_t)t.mx * t.my, n = (int64_t)g.nv * g.nh;
+    double cmax = 0.0, emax = 0.0;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
         const int o = owner[i];
         if (o == INT32_MAX) {
@@ -2036,15 +2158,19 @@ __global__ void __launch_bounds__(kBlock) k_gd_eval(Grid g, Targets t, const int
         double b[3];
         bary(g, T, t.gx[c], t.gy[r], b);
         for (int v = 0; v < nvals; ++v) out[v * m + i] = clough_tocher(g, o, T, f + v * n, grad + 2 * v * n, b);
+        if (be.y) band_target_est(g, be, o, T, grad, cmax, emax);
     }
+    if (be.y) band_est_store(be, cmax, emax);
 }
 
 // k_gd_eval for the targets a rank forms (assigned): value and count, zeros elsewhere, so the
 // ranks' pieces add up to the map (a SUM reduction; count 0: outside the hull, NaN)
 __global__ void __launch_bounds__(kBlock) k_gd_eval_part(Grid g, Targets t, const int* __restrict__ owner,
                                                          const uint8_t* __restrict__ assigned, const double* f,
-                                                         const double* grad, int nvals, double* out, double* cnt) {
+                                                         const double* grad, int nvals, double* out, double* cnt,
+                                                         BandEst be = BandEst{nullptr, 0, nullptr, nullptr}) {
     const int64_t m = (int64_t)t.mx * t.my, n = (int64_t)g.nv * g.nh;
+    double cmax = 0.0, emax = 0.0;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
         if (!assigned[i]) {
             for (int v = 0; v < nvals; ++v) out[v * m + i] = 0.0;
@@ -2058,7 +2184,9 @@ __global__ void __launch_bounds__(kBlock) k_gd_eval_part(Grid g, Targets t, cons
         bary(g, T, t.gx[c], t.gy[r], b);
         for (int v = 0; v < nvals; ++v) out[v * m + i] = clough_tocher(g, o, T, f + v * n, grad + 2 * v * n, b);
         cnt[i] = 1.0;
+        if (be.y) band_target_est(g, be, o, T, grad, cmax, emax);
     }
+    if (be.y) band_est_store(be, cmax, emax);
 }
 
 // the assembled pieces: value where some rank formed it, NaN elsewhere (outside the hull)
@@ -2317,13 +2445,21 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
             for (int j = 1; j <= K; ++j) {
                 const double* gin = j == 1 ? nullptr : gb[(j - 1) % 3];
                 const double* gprev = j >= 3 ? gb[(j + 1) % 3] : nullptr;
-                const BandMap bm = band_map(g.nv, g.nh, 2 * K + 3 - j);
-                const unsigned nbw = grid_for(bm.total, 1, kStreamGridCap), nr8 = grid_for((L + 7) / 8 * 64);
+                const BandTiles bt = band_tiles(g.nv, g.nh, 2 * K + 3 - j);
+                const unsigned nr8 = (unsigned)(((L + 7) / 8 * 64 + kBandThreads - 1) / kBandThreads);
                 const ConeBand a{fv, gin, gprev, gb[j % 3], steps[j], band};
-                k_gd_cone_sweep8<<<nbw + nr8, kBlock, 0, s>>>(g, bm, a, (int)nbw);
-                if ((st = launch_status("k_gd_cone_sweep8"))) return st;
+                k_gd_cone_band<<<bt.total + nr8, kBandThreads, 0, s>>>(g, bt, a, bt.total);
+                if ((st = launch_status("k_gd_cone_band"))) return st;
+            }
+            if (d_change) {  // one more plain sweep, y from x_K to depth K + 2 (the band targets' corners)
+                const BandTiles bt = band_tiles(g.nv, g.nh, K + 2);
+                const unsigned nr8 = (unsigned)(((L + 7) / 8 * 64 + kBandThreads - 1) / kBandThreads);
+                const ConeBand a{fv, gb[K % 3], nullptr, gb[(K + 1) % 3], ConeStep{0, 1.0}, band};
+                k_gd_cone_band<<<bt.total + nr8, kBandThreads, 0, s>>>(g, bt, a, bt.total);
+                if ((st = launch_status("k_gd_cone_band"))) return st;
             }
         }
+        const BandEst be{band_on && d_change ? gb[(K + 1) % 3] : nullptr, K, d_change, d_change ? d_change + 1 : nullptr};
         ConePatch a{fv, cells, count, K, {}, gb[K % 3], d_change, d_change ? d_change + 1 : nullptr};
         for (int j = 0; j <= K; ++j) a.st[j] = steps[j];
         PatchTimer& pt = patch_timer();
@@ -2340,9 +2476,9 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
         if ((st = launch_status("k_gd_cone_patch"))) return st;
         if (cnt)
             k_gd_eval_part<<<grid_for(m, 1, kStreamGridCap), kBlock, 0, s>>>(g, t, owner, assigned, fv, gb[K % 3], 1,
-                                                                              out + v * m, cnt);
+                                                                              out + v * m, cnt, be);
         else
-            k_gd_eval<<<grid_for(m, 1, kStreamGridCap), kBlock, 0, s>>>(g, t, owner, fv, gb[K % 3], 1, out + v * m);
+            k_gd_eval<<<grid_for(m, 1, kStreamGridCap), kBlock, 0, s>>>(g, t, owner, fv, gb[K % 3], 1, out + v * m, be);
         if ((st = launch_status("k_gd_eval"))) return st;
     }
     return 0;

@@ -43,7 +43,7 @@ KERNELS = [
 GD_SOURCES = ["akbraytracing_amd/csrc/akb_griddata.hip", "akbraytracing_amd/csrc/akb_common.h",
               "akbraytracing_amd/csrc/akb_pairwise.h", "include/akb_raytrace.h"]
 GD_KERNELS = [("cone_patch", "akb::(anonymous namespace)::k_gd_cone_patch("),
-              ("cone_sweep8", "akb::(anonymous namespace)::k_gd_cone_sweep8(")]
+              ("cone_band", "akb::(anonymous namespace)::k_gd_cone_band(")]
 SIMDS = 1024  # 256 CUs x 4 SIMDs
 XCDS = 8
 
