@@ -177,7 +177,8 @@ def read_profile():
     and whether it describes these kernel sources (its sha256 of them equals theirs now)."""
     sys.path.insert(0, os.path.join(ROOT, "scripts"))
     from summarize_profiles import sources_sha256
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_roofline.json")))
+    files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "*_roofline.json"))
+                   if not f.endswith("_faithful_roofline.json"))
     if not files:
         return {}, None, False
     with open(files[-1]) as f:
@@ -817,7 +818,8 @@ def main():
     inter_launch = len(geom.mirrors) * rw.n_local  # pass 2's intersections per launch
     # VALU-issue roofline of pass 2: the chip issues at most SIMDS / 4 wave-instructions per clock;
     # with the profiled instructions per intersection that caps the intersection rate
-    vpi = (pk["valu_wave_instructions_per_launch"] / pk["intersections_per_launch"]) if pk else None
+    vpi = (pk["valu_wave_instructions_per_launch"] / pk["intersections_per_launch"]
+           if pk.get("valu_wave_instructions_per_launch") and pk.get("intersections_per_launch") else None)
     clock = pk.get("effective_clock_ghz") if pk else None
     issue_peak = (SIMDS / 4 * clock * 1e9 / vpi) if vpi and clock else None
     issue_achieved = inter_launch / (k_avg * 1e-3)

@@ -152,7 +152,9 @@ def main(tag):
                "kernels": {}}
     for key, prefix, bpr, label in KERNELS:
         name = next((k for k in pmc if k.startswith(prefix)), None)
-        if name is None:
+        # only from a profile of the trace kernels (scripts/gpu_pmc.sh); the faithful chain's passes
+        # (scripts/gpu_pmc_faithful.sh) leave them without the issue and traffic counters
+        if name is None or not all(c in pmc[name] for c in ("FETCH_SIZE", "SQ_INSTS_VALU", "GRBM_GUI_ACTIVE")):
             continue
         tns = next((v for k, v in dur.items() if k.startswith(prefix)), None)
         summary["kernels"][key] = kernel_summary(name, pmc[name], pmc_dur.get(name), tns, bpr, n_rays, label)
