@@ -1765,9 +1765,6 @@ __global__ void __launch_bounds__(kAxesThreads) k_gd_axes(const double* __restri
     }
 }
 
-// a sharded lattice's targets: this rank forms the interior targets whose cell's p00 lies in its
-// rays [own0, own1); the band owner forms every band and pocket target. assigned[t] = 1 for the
-// targets formed here; the interior ones' cells go to the patch list
 // whether triangle o lies in an interior target cell (a patch's: its (2K + 4)^2 box clear of the
 // ring by one vertex), and that cell and its p00 vertex; else the boundary band forms its corners
 __device__ __forceinline__ bool cone_interior(const Grid& g, int o, int K, int64_t& c, int64_t& p00) {
@@ -1778,6 +1775,9 @@ __device__ __forceinline__ bool cone_interior(const Grid& g, int o, int K, int64
     return iv - K - 1 >= 1 && iv + K + 2 <= g.nv - 2 && ih - K - 1 >= 1 && ih + K + 2 <= g.nh - 2;
 }
 
+// a sharded lattice's targets: this rank forms the interior targets whose cell's p00 lies in its
+// rays [own0, own1); the band owner forms every band and pocket target. assigned[t] = 1 for the
+// targets formed here; the interior ones' cells go to the patch list
 __global__ void __launch_bounds__(kBlock) k_gd_cone_assign(Grid g, const int* __restrict__ owner, int64_t m, int K,
                                                             int64_t own0, int64_t own1, int band_on, int64_t* cells,
                                                             int* count, int* band, uint8_t* assigned) {
@@ -2104,9 +2104,12 @@ __device__ double clough_tocher(const Grid& g, int64_t tid, const Tri& T, const 
 
 // nvals value sets share the triangulation: f / grad / out strided by n / 2n / mx*my
 // The cone solve's estimates at the band's targets (be.y != nullptr: the band's one more plain
-// sweep y from x_K): the patch kernel's change measure and value-error estimate (see cell_est) over
-// the vertices of each target's triangle that is not an interior cell's - the boundary cells' and
-// the pocket triangles', whose long edges carry a gradient error furthest - as ordered double bits
+// sweep y from x_K), for each target whose triangle is not an interior cell's - the boundary
+// cells' and the pocket triangles': the change measure of that sweep at the triangle's vertices
+// and, as the value-error estimate, twice the value change it makes at the target (the
+// Clough-Tocher value is linear in the gradients and the fixed point lies within ~2x the Jacobi
+// step; a pocket sliver's long edges carry the step furthest, so its value, not a bound through
+// the edge length, is taken), as ordered double bits
 struct BandEst {
     const double* y;  // (n, 2) or nullptr
     int K;
@@ -2115,20 +2118,16 @@ struct BandEst {
 };
 
 __device__ __forceinline__ void band_target_est(const Grid& g, const BandEst& be, int o, const Tri& T,
-                                                const double* grad, double& cmax, double& emax) {
+                                                const double* f, const double* grad, const double (&b)[3], double v0,
+                                                double& cmax, double& emax) {
     int64_t c, p00;
     if (cone_interior(g, o, be.K, c, p00)) return;
-    double d = 0.0, h2 = 0.0;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        const int64_t v = T.v[k], w = T.v[(k + 1) % 3];
-        const double gx = grad[2 * v], gy = grad[2 * v + 1], y0 = be.y[2 * v], y1 = be.y[2 * v + 1];
-        d = fmax(d, fmax(fabs(gx - y0), fabs(gy - y1)));
-        cmax = fmax(cmax, change_of(gx, gy, y0, y1));
-        const double ex = g.x[w] - g.x[v], ey = g.y[w] - g.y[v];
-        h2 = fmax(h2, ex * ex + ey * ey);
+        const int64_t v = T.v[k];
+        cmax = fmax(cmax, change_of(grad[2 * v], grad[2 * v + 1], be.y[2 * v], be.y[2 * v + 1]));
     }
-    emax = fmax(emax, 2.0 * 1.4142135623730951 * d * sqrt(h2));
+    emax = fmax(emax, 2.0 * fabs(clough_tocher(g, o, T, f, be.y, b) - v0));
 }
 
 __device__ __forceinline__ void band_est_store(const BandEst& be, double cmax, double emax) {
@@ -2158,7 +2157,7 @@ __global__ void __launch_bounds__(kBlock) k_gd_eval(Grid g, Targets t, const int
         double b[3];
         bary(g, T, t.gx[c], t.gy[r], b);
         for (int v = 0; v < nvals; ++v) out[v * m + i] = clough_tocher(g, o, T, f + v * n, grad + 2 * v * n, b);
-        if (be.y) band_target_est(g, be, o, T, grad, cmax, emax);
+        if (be.y) band_target_est(g, be, o, T, f, grad, b, out[i], cmax, emax);  // (one value set)
     }
     if (be.y) band_est_store(be, cmax, emax);
 }
@@ -2184,7 +2183,7 @@ __global__ void __launch_bounds__(kBlock) k_gd_eval_part(Grid g, Targets t, cons
         bary(g, T, t.gx[c], t.gy[r], b);
         for (int v = 0; v < nvals; ++v) out[v * m + i] = clough_tocher(g, o, T, f + v * n, grad + 2 * v * n, b);
         cnt[i] = 1.0;
-        if (be.y) band_target_est(g, be, o, T, grad, cmax, emax);
+        if (be.y) band_target_est(g, be, o, T, f, grad, b, out[i], cmax, emax);  // (one value set)
     }
     if (be.y) band_est_store(be, cmax, emax);
 }

@@ -63,7 +63,8 @@ class ErrorLog:
     """Each finished run's error words, copied device -> pinned host memory at the end of its finish
     (stream-ordered: no wait on the queuing thread), one row per run. A ticket's check() then reads
     its own run's words however many runs later it is called - the device buffers they come from
-    (the slot's status word, the shared post parameter block) are rewritten by every later finish.
+    (FaithfulPupil.words: the status word, the change and estimate, the post parameters) are
+    rewritten by every later finish.
     Rows are reused after `cap` finishes; a ticket whose row was reused refuses to report."""
 
     def __init__(self, width, cap=8192):
@@ -118,9 +119,10 @@ class Ticket:
 
 
 def cone_guard(est, params):
-    """Raise ConeNotConverged when the cone solve's value-error estimate (k_gd_cone_patch: 2 sqrt2
-    x the corners' one-more-sweep step x the cell size) exceeds CONE_GUARD of the gridded map's
-    range (the post block's nanmin / nanmax)."""
+    """Raise ConeNotConverged when the cone solve's value-error estimate - interior targets
+    (k_gd_cone_patch): 2 sqrt2 x the corners' one-more-sweep step x the cell's longest side; band
+    and pocket targets (k_gd_eval): twice the value change one more sweep makes there - exceeds
+    CONE_GUARD of the gridded map's range (the post block's nanmin / nanmax)."""
     rng = float(params[19]) - float(params[18])
     if not (est <= CONE_GUARD * rng):
         raise ConeNotConverged(f"griddata: the cone solve's {CONE_SWEEPS}-sweep gradients leave a value error "
@@ -157,7 +159,6 @@ class FaithfulPupil:
                 ring_host=torch.empty(2 * Lr + 1, dtype=D.F64, pin_memory=True),
                 pk_host=torch.zeros(self._pk_len, dtype=torch.int32, pin_memory=True),
                 pk=torch.zeros(self._pk_len, dtype=torch.int32, device=self.dev),
-                status=torch.zeros(1, dtype=torch.int64, device=self.dev),
                 owner=torch.empty(self.size * self.size, dtype=torch.int32, device=self.dev),
                 axes=torch.empty(2 * self.size + 6, dtype=D.F64, device=self.dev),  # gx | gy | extent | pitch
                 last=None))
@@ -166,8 +167,13 @@ class FaithfulPupil:
         self.work = torch.empty(int(L.akb_gd_cone_work_bytes(self.nv, self.nh, self.size, self.size, 1)) // 8 + 1,
                                 dtype=D.F64, device=self.dev)
         self.map = torch.empty((1, self.size, self.size), dtype=D.F64, device=self.dev)
-        self.change = torch.zeros(2, dtype=torch.int64, device=self.dev)  # change measure | value-error estimate
-        self.post = {}
+        # a finish's error words in one block, copied to the ErrorLog in one transfer: the pocket
+        # status word (int64 bits) | the cone's change measure and value-error estimate (ordered
+        # double bits) | pupil_post's parameter block
+        self.words = torch.zeros(1 + 2 + POST_PARAMS, dtype=D.F64, device=self.dev)
+        self.status = self.words[:1].view(torch.int64)
+        self.change = self.words[1:3].view(torch.int64)
+        self.post = {"params": self.words[3:]}
         self.psf = None
         self._done = None  # the latest finish's end (finishes share work / map / pupil / psf buffers)
         self._omegas = D.host_f64(chebyshev_weights(max(self.sweeps, 1)))
@@ -286,14 +292,13 @@ class FaithfulPupil:
             edge, xptr, xidx = pk[o["edge"]:o["edge"] + Lr], pk[o["xptr"]:o["xptr"] + Lr + 1], pk[o["xidx"]:o["len"] + 1]
             tri = (D.ptr(t.y), D.ptr(t.z), self.nv, self.nh, D.ptr(s["diag"]), t.npock, D.ptr(ptri), D.ptr(pnbr),
                    D.ptr(edge))
-            s["status"].zero_()
-            _lib.check(L.akb_gd_check_pockets(*tri, self.tol, D.ptr(s["status"]), sh))
+            self.words[:3].zero_()  # the status word, change and estimate
+            _lib.check(L.akb_gd_check_pockets(*tri, self.tol, D.ptr(self.status), sh))
             m = self.size
             axes = s["axes"]
             gx, gy = axes[:m], axes[m:2 * m]
             _lib.check(L.akb_gd_claim_pockets_f64(D.ptr(t.y), D.ptr(t.z), self.nv, self.nh, D.ptr(s["diag"]), t.npock,
                                                   D.ptr(ptri), D.ptr(gx), m, D.ptr(gy), m, D.ptr(s["owner"]), sh))
-            self.change.zero_()
             _lib.check(L.akb_gd_cone_solve_f64(*tri, D.ptr(xptr), D.ptr(xidx), D.ptr(gx), m, D.ptr(gy), m,
                                                D.ptr(t.f), 1, self.sweeps, self._omegas, D.ptr(self.work),
                                                D.ptr(s["owner"]), D.ptr(self.map), D.ptr(self.change), sh))
@@ -308,7 +313,7 @@ class FaithfulPupil:
             self.psf = psf
             if events is not None:
                 events[1].record(st)
-            t.erow = self.errors.record((s["status"].view(D.F64), self.change.view(D.F64), post["params"]), st)
+            t.erow = self.errors.record((self.words,), st)
             t.done = torch.cuda.Event()
             t.done.record(st)
             self._done = t.done
