@@ -41,7 +41,7 @@ EXPORTS = [
     "akb_leaf_parts_f64", "akb_parts_chain_f64",
     "akb_huygens_splits", "akb_huygens_work_bytes", "akb_huygens_f64", "akb_scale_field_f64",
     "akb_psf_work_bytes", "akb_psf_f64", "akb_psf_release_plans", "akb_selftest_arith_f64",
-    "akb_first_valid_rows_f64", "akb_rotate_work_bytes", "akb_rotate_with_nan_f64", "akb_pupil_post_f64",
+    "akb_first_valid_rows_f64", "akb_rotate_work_bytes", "akb_rotate_with_nan_f64", "akb_pupil_post_f64", "akb_pupil_post_work_bytes",
     "akb_moments_work_bytes", "akb_map_moments_f64", "akb_plane_subtract_f64", "akb_legendre_rows_f64",
     "akb_gd_cells_f64", "akb_gd_pockets", "akb_gd_check_pockets", "akb_gd_grad_sweeps_f64",
     "akb_gd_eval_f64", "akb_gd_cone_work_bytes", "akb_gd_patch_timing", "akb_gd_patch_times", "akb_gd_cone_eval_f64", "akb_gd_axes_f64",
@@ -159,6 +159,7 @@ def _declare(L):
         "akb_rotate_work_bytes": ([c_int, c_int], c_i64),
         "akb_rotate_with_nan_f64": ([c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp], c_int),
         "akb_pupil_post_f64": ([c_vp, c_int, c_int, c_dbl, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp], c_int),
+        "akb_pupil_post_work_bytes": ([c_int, c_int], c_i64),
         "akb_moments_work_bytes": ([], c_i64),
         "akb_map_moments_f64": ([c_vp, c_int, c_int, c_int, c_vp, c_dbl, c_int, c_dbl, c_vp, c_vp, c_vp], c_int),
         "akb_plane_subtract_f64": ([c_vp, c_int, c_int, c_vp, c_vp, c_vp], c_int),
