@@ -1700,6 +1700,7 @@ __global__ void __launch_bounds__(kBlock) k_gd_cone_targets(Grid g, const int* _
 // np.linspace(min, max, m) of the ring's x and y - i * step + start, the last point the stop
 // (numpy 2.x's linspace arithmetic) - one workgroup
 constexpr int kAxesThreads = 1024;  // one workgroup over the ring (4 x kBlock: the loop was its latency)
+constexpr int kAxesLds = 2048;      // axes up to this long are summed from LDS
 __global__ void __launch_bounds__(kAxesThreads) k_gd_axes(const double* __restrict__ rx, const double* __restrict__ ry,
                                                           int64_t L, int mx, int my, double* gx, double* gy,
                                                           double* ext) {
@@ -1731,9 +1732,15 @@ __global__ void __launch_bounds__(kAxesThreads) k_gd_axes(const double* __restri
     }
     if (threadIdx.x == 0 && ext)
         for (int q = 0; q < 4; ++q) ext[q] = e[q];
-    auto lin = [&](double a0, double a1, int m, double* out) {
+    // the axes also into LDS (when they fit) for the pitch's meshgrid sums below
+    __shared__ double sgx[kAxesLds], sgy[kAxesLds];
+    const bool lds = mx <= kAxesLds && my <= kAxesLds;
+    auto lin = [&](double a0, double a1, int m, double* out, double* sout) {
         if (m == 1) {
-            if (threadIdx.x == 0) out[0] = a0;
+            if (threadIdx.x == 0) {
+                out[0] = a0;
+                if (lds) sout[0] = a0;
+            }
             return;
         }
         const double step = (a1 - a0) / (double)(m - 1);
@@ -1742,10 +1749,11 @@ __global__ void __launch_bounds__(kAxesThreads) k_gd_axes(const double* __restri
             if (step == 0) v = (double)i / (double)(m - 1) * (a1 - a0) + a0;  // numpy's zero-step branch
             else v = (double)i * step + a0;
             out[i] = i == m - 1 ? a1 : v;
+            if (lds) sout[i] = i == m - 1 ? a1 : v;
         }
     };
-    lin(e[0], e[1], mx, gx);
-    lin(e[2], e[3], my, gy);
+    lin(e[0], e[1], mx, gx, sgx);
+    lin(e[2], e[3], my, gy, sgy);
     if (!ext) return;
     // the pupil pitch psf_calc takes after the driver's grid_H -= np.mean(grid_H) (:3698, :1176-1177):
     // dx = |gh[0,1] - gh[0,0]|, dy = |gv[1,0] - gv[0,0]| of the mean-subtracted meshgrids, each mean
@@ -1756,10 +1764,10 @@ __global__ void __launch_bounds__(kAxesThreads) k_gd_axes(const double* __restri
     const int w = threadIdx.x >> 6;
     if (w < 2) {
         const long long cnt = (long long)mx * my;
-        const double* a = w == 0 ? gx : gy;
+        const double* a = lds ? (w == 0 ? sgx : sgy) : (w == 0 ? gx : gy);
         const int m = w == 0 ? mx : my;
         double sum;
-        sum = pw_sum_wave_get(tree[w], MeshgridAxis{w == 0 ? gx : gy, mx, w == 0}, cnt);
+        sum = pw_sum_wave_get(tree[w], MeshgridAxis{a, mx, w == 0}, cnt);
         const double mean = sum / (double)cnt;
         if ((threadIdx.x & 63) == 0) ext[4 + w] = m > 1 ? fabs((a[1] - mean) - (a[0] - mean)) : 0.0;
     }
@@ -2033,6 +2041,15 @@ __global__ void __launch_bounds__(kBlock, 5) k_gd_claim_hit(Grid g, Targets t, c
 __global__ void __launch_bounds__(kBlock) k_gd_claim_pockets(Grid g, Targets t, int* owner) {
     const int64_t nc2 = 2 * ncells(g);
     const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+    // the target axes in LDS: tri_box's binary searches walk them one dependent load at a time
+    __shared__ double sax[2 * kClaimAxisLds];
+    if (t.mx <= kClaimAxisLds && t.my <= kClaimAxisLds) {
+        for (int i = threadIdx.x; i < t.mx; i += blockDim.x) sax[i] = t.gx[i];
+        for (int i = threadIdx.x; i < t.my; i += blockDim.x) sax[kClaimAxisLds + i] = t.gy[i];
+        __syncthreads();
+        t.gx = sax;
+        t.gy = sax + kClaimAxisLds;
+    }
     for (int64_t j = (int64_t)blockIdx.x * nw + (threadIdx.x >> 6); j < g.npock; j += (int64_t)gridDim.x * nw) {
         const Tri T = tri_verts(g, nc2 + j);
         int c0, c1, r0, r1;
