@@ -381,51 +381,51 @@ __device__ __forceinline__ void bary_lds(const double* vx, const double* vy, con
 __device__ void tile_claims(const Grid& g, const TileClaims& tc, bool uniform, double inv_dx, double inv_dy,
                             const double* vx, const double* vy, const uint8_t* sdg, int iv0, int ih0, int r_hi) {
     constexpr int T = kCellTile, V = T + 2;
-    __shared__ double sbox[4][T * T / 64];
+    __shared__ int srange[4];  // the tile's candidate targets: columns [0, 1), rows [2, 3)
     const Targets& t = tc.t;
     const int tid = threadIdx.x;
     const int nr = min(T, r_hi - iv0), nc = min(T, g.nh - 1 - ih0);  // the tile's cells
-    // the tile's box over its (nr + 1) x (nc + 1) vertices (fmin / fmax pass over a NaN)
-    double xlo = INFINITY, xhi = -INFINITY, ylo = INFINITY, yhi = -INFINITY;
-    for (int k = tid; k < (nr + 1) * (nc + 1); k += T * T) {
-        const int r = k / (nc + 1), c = k - (k / (nc + 1)) * (nc + 1);
-        const double x = vx[r * V + c], y = vy[r * V + c];
-        xlo = fmin(xlo, x);
-        xhi = fmax(xhi, x);
-        ylo = fmin(ylo, y);
-        yhi = fmax(yhi, y);
-    }
-    for (int off = 32; off > 0; off >>= 1) {
-        xlo = fmin(xlo, __shfl_xor(xlo, off));
-        xhi = fmax(xhi, __shfl_xor(xhi, off));
-        ylo = fmin(ylo, __shfl_xor(ylo, off));
-        yhi = fmax(yhi, __shfl_xor(yhi, off));
-    }
-    if ((tid & 63) == 0) {
-        sbox[0][tid >> 6] = xlo;
-        sbox[1][tid >> 6] = xhi;
-        sbox[2][tid >> 6] = ylo;
-        sbox[3][tid >> 6] = yhi;
+    if (tid < 64) {  // wave 0: the tile's box over its (nr + 1) x (nc + 1) vertices (fmin / fmax pass over a NaN)
+        double xlo = INFINITY, xhi = -INFINITY, ylo = INFINITY, yhi = -INFINITY;
+        for (int k = tid; k < (nr + 1) * (nc + 1); k += 64) {
+            const int r = k / (nc + 1), c = k - (k / (nc + 1)) * (nc + 1);
+            const double x = vx[r * V + c], y = vy[r * V + c];
+            xlo = fmin(xlo, x);
+            xhi = fmax(xhi, x);
+            ylo = fmin(ylo, y);
+            yhi = fmax(yhi, y);
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+            xlo = fmin(xlo, __shfl_xor(xlo, off));
+            xhi = fmax(xhi, __shfl_xor(xhi, off));
+            ylo = fmin(ylo, __shfl_xor(ylo, off));
+            yhi = fmax(yhi, __shfl_xor(yhi, off));
+        }
+        // the candidate targets: a superset of every triangle's (a triangle's padded box lies in the
+        // tile's), from the linspace estimate or the exact binary search; empty: c0 = c1 = 0
+        if (tid == 0) {
+            const double padx = (xhi - xlo) * 1e-9, pady = (yhi - ylo) * 1e-9;
+            int c0, c1, r0, r1;
+            bool hit;
+            if (uniform) {
+                hit = axis_range(t.gx, t.mx, inv_dx, xlo - padx, xhi + padx, c0, c1) &&
+                      axis_range(t.gy, t.my, inv_dy, ylo - pady, yhi + pady, r0, r1);
+            } else {
+                c0 = lower_idx(t.gx, t.mx, xlo - padx);
+                c1 = lower_idx(t.gx, t.mx, xhi + padx);
+                r0 = lower_idx(t.gy, t.my, ylo - pady);
+                r1 = lower_idx(t.gy, t.my, yhi + pady);
+                hit = c0 < c1 && r0 < r1;
+            }
+            srange[0] = hit ? c0 : 0;
+            srange[1] = hit ? c1 : 0;
+            srange[2] = hit ? r0 : 0;
+            srange[3] = hit ? r1 : 0;
+        }
     }
     __syncthreads();  // (the next tile's writes come after the cell pass's next three barriers)
-    xlo = fmin(fmin(sbox[0][0], sbox[0][1]), fmin(sbox[0][2], sbox[0][3]));
-    xhi = fmax(fmax(sbox[1][0], sbox[1][1]), fmax(sbox[1][2], sbox[1][3]));
-    ylo = fmin(fmin(sbox[2][0], sbox[2][1]), fmin(sbox[2][2], sbox[2][3]));
-    yhi = fmax(fmax(sbox[3][0], sbox[3][1]), fmax(sbox[3][2], sbox[3][3]));
-    // the tile's candidate targets: a superset of every triangle's (a triangle's padded box lies in
-    // the tile's), from the linspace estimate or the exact binary search
-    const double padx = (xhi - xlo) * 1e-9, pady = (yhi - ylo) * 1e-9;
-    int c0, c1, r0, r1;
-    if (uniform) {
-        if (!axis_range(t.gx, t.mx, inv_dx, xlo - padx, xhi + padx, c0, c1)) return;
-        if (!axis_range(t.gy, t.my, inv_dy, ylo - pady, yhi + pady, r0, r1)) return;
-    } else {
-        c0 = lower_idx(t.gx, t.mx, xlo - padx);
-        c1 = lower_idx(t.gx, t.mx, xhi + padx);
-        r0 = lower_idx(t.gy, t.my, ylo - pady);
-        r1 = lower_idx(t.gy, t.my, yhi + pady);
-        if (c0 >= c1 || r0 >= r1) return;
-    }
+    const int c0 = srange[0], c1 = srange[1], r0 = srange[2], r1 = srange[3];
+    if (c0 >= c1) return;
     const int rr = tid / T, cc = tid - (tid / T) * T;
     if (rr >= nr || cc >= nc) return;
     // this cell's two triangles (tri_verts' vertex order), formed per candidate target from LDS (a
@@ -473,7 +473,7 @@ __device__ void tile_claims(const Grid& g, const TileClaims& tc, bool uniform, d
 // vertices in LDS (its cells, the next row's and column's), each of its 17 x 17 cells' diagonal
 // formed once (cell_diag's arithmetic on the same values), then each cell's checks from LDS. Per
 // cell: ~1.3 vertex loads and ~3 in-circle tests instead of ~10 and 5. Same diagonals and flags.
-// With kClaims the tile also claims its targets (tile_claims) before its cells' checks.
+// With kClaims the tile also claims its targets (tile_claims) after its cells' checks.
 template <bool kClaims = false>
 __global__ void __launch_bounds__(kCellTile * kCellTile) k_gd_cells_tiled(Grid g, uint8_t* diag, double tol,
                                                                         unsigned* flags, TileClaims tc = {}) {
