@@ -19,7 +19,7 @@ c_int = ctypes.c_int
 c_dbl = ctypes.c_double
 c_vp = ctypes.c_void_p
 MAX_MIRRORS = 7
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 FLAG_MISS = 0x1
 FLAG_ZERO_NORMAL = 0x2

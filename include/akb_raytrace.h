@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define AKB_ABI_VERSION 14
+#define AKB_ABI_VERSION 15
 
 /* status codes */
 #define AKB_OK 0
