@@ -1352,20 +1352,21 @@ __device__ __forceinline__ void cone_ring_vertex(const Grid& g, const ConeBand& 
     }
 }
 
-// one sweep of the band in one launch: workgroups [0, nbt) take a band tile each - its vertices
+// one sweep of the band in one launch: workgroups [0, nr8) eight ring vertices per wave (8-lane
+// groups; a vertex with more than eight chords takes the whole wave afterwards) - first, so the
+// ring's dependent chord loads overlap the tiles - the rest a band tile each - its vertices
 // and their neighbours' x, y, f and x_{j-1} (and the cells' diagonals) staged in LDS by coalesced
 // row loads, then one thread per vertex off the ring (band_edges from LDS: the gather kernel's
-// arithmetic) - the rest eight ring vertices per wave (8-lane groups; a vertex with more than eight
-// chords takes the whole wave afterwards). Both halves read x_{j-1} / x_{j-2} only.
+// arithmetic). Both halves read x_{j-1} / x_{j-2} only.
 constexpr int kBandThreads = kBandTR * kBandTC;
-__global__ void __launch_bounds__(kBandThreads) k_gd_cone_band(Grid g, BandTiles bt, ConeBand a, int nbt) {
+__global__ void __launch_bounds__(kBandThreads) k_gd_cone_band(Grid g, BandTiles bt, ConeBand a, int nr8) {
     if (!*a.needed) return;
-    if ((int)blockIdx.x < nbt) {
+    if ((int)blockIdx.x >= nr8) {
         constexpr int HR = kBandTR + 2, HC = kBandTC + 2, HN = HR * HC, CC = kBandTC + 1;
         __shared__ double sx[HN], sy[HN], sf[HN], sgx[HN], sgy[HN];
         __shared__ uint8_t sdg[(kBandTR + 1) * CC];
         int r0, c0, r1, c1;
-        band_tile(bt, g.nv, g.nh, blockIdx.x, r0, c0, r1, c1);
+        band_tile(bt, g.nv, g.nh, blockIdx.x - nr8, r0, c0, r1, c1);
         // the tile's vertices with a one-vertex halo (rows r0 - 1 .. r0 + TR, inside the lattice)
         for (int k = threadIdx.x; k < HN; k += kBandThreads) {
             const int iv = r0 - 1 + k / HC, ih = c0 - 1 + (k - (k / HC) * HC);
@@ -1415,8 +1416,8 @@ __global__ void __launch_bounds__(kBandThreads) k_gd_cone_band(Grid g, BandTiles
     }
     const int64_t L = 2 * (int64_t)(g.nh - 1) + 2 * (int64_t)(g.nv - 1);
     const int lane = threadIdx.x & 63, sub = lane & 7;
-    const int64_t w0 = ((int64_t)(blockIdx.x - nbt) * blockDim.x + threadIdx.x) >> 6;
-    const int64_t nw = ((int64_t)(gridDim.x - nbt) * blockDim.x) >> 6;
+    const int64_t w0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nw = ((int64_t)nr8 * blockDim.x) >> 6;
     for (int64_t r0 = w0 * 8; r0 < L; r0 += nw * 8) {
         const int64_t r = r0 + (lane >> 3);
         const bool big = r < L && g.xptr[r + 1] - g.xptr[r] > 8;
@@ -2464,14 +2465,14 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
                 const BandTiles bt = band_tiles(g.nv, g.nh, 2 * K + 3 - j);
                 const unsigned nr8 = (unsigned)(((L + 7) / 8 * 64 + kBandThreads - 1) / kBandThreads);
                 const ConeBand a{fv, gin, gprev, gb[j % 3], steps[j], band};
-                k_gd_cone_band<<<bt.total + nr8, kBandThreads, 0, s>>>(g, bt, a, bt.total);
+                k_gd_cone_band<<<bt.total + nr8, kBandThreads, 0, s>>>(g, bt, a, (int)nr8);
                 if ((st = launch_status("k_gd_cone_band"))) return st;
             }
             if (d_change) {  // one more plain sweep, y from x_K to depth K + 2 (the band targets' corners)
                 const BandTiles bt = band_tiles(g.nv, g.nh, K + 2);
                 const unsigned nr8 = (unsigned)(((L + 7) / 8 * 64 + kBandThreads - 1) / kBandThreads);
                 const ConeBand a{fv, gb[K % 3], nullptr, gb[(K + 1) % 3], ConeStep{0, 1.0}, band};
-                k_gd_cone_band<<<bt.total + nr8, kBandThreads, 0, s>>>(g, bt, a, bt.total);
+                k_gd_cone_band<<<bt.total + nr8, kBandThreads, 0, s>>>(g, bt, a, (int)nr8);
                 if ((st = launch_status("k_gd_cone_band"))) return st;
             }
         }
