@@ -435,28 +435,32 @@ struct PostArgs {
     double* part;        // work: (2, kPostG, kPostPart) partials, two banks (a phase reads one, writes the other)
     double* bufsum;      // work: numpy's 8192-element buffer sums of the nanmean (<= 8)
     unsigned* sync;      // work: arrivals, departures, the first valid rows (2), failure bits: zero between launches
+    unsigned long long* clocks;  // work: workgroup 0's wall clock (100 MHz) at the start and after each barrier
     double* params;      // out, kPostParams doubles (layout in akb_raytrace.h)
     int fuse;            // the spline prefilter and the rotation in this launch
 };
 
-// a grid barrier for the post's kPostG co-resident workgroups: stores made visible at device scope,
-// one arrival per workgroup on a counter that only grows within a launch, a bounded wait (bit 2 of
-// the failure word on a timeout: the parameter block's flags then report it)
-__device__ void post_sync(unsigned* sync, unsigned& gen) {
-    __threadfence();
+// a grid barrier for the post's kPostG co-resident workgroups: the workgroup's stores complete
+// (__syncthreads), one thread makes them visible at device scope and arrives on a counter that only
+// grows within a launch (release), then polls it with plain device-scope loads - an acquiring poll
+// would invalidate the caches on every read - and acquires once the count is reached; a bounded
+// wait (bit 2 of the failure word on a timeout: the parameter block's flags then report it)
+__device__ void post_sync(unsigned* sync, unsigned& gen, unsigned long long* clocks) {
     __syncthreads();
     if (threadIdx.x == 0) {
         ++gen;
         __hip_atomic_fetch_add(&sync[0], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned target = gen * gridDim.x;
         unsigned spins = 0;
-        while (__hip_atomic_load(&sync[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
-            __builtin_amdgcn_s_sleep(2);
-            if (++spins == (1u << 24)) {
+        while (__hip_atomic_load(&sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins == (1u << 25)) {
                 atomicOr(&sync[4], 4u);
                 break;
             }
         }
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);  // (agent scope: the default of a HIP fence)
+        if (blockIdx.x == 0) clocks[gen] = wall_clock64();
     }
     __syncthreads();
 }
@@ -614,6 +618,7 @@ __global__ void __launch_bounds__(kPostT) k_pupil_post(PostArgs a) {
     const int64_t S = (int64_t)G * kPostT, gt = (int64_t)wg * kPostT + tid;
     double* P = a.params;
     unsigned gen = 0;
+    if (wg == 0 && tid == 0) a.clocks[0] = wall_clock64();
     if (a.nx <= kPostBasisMax && a.ny <= kPostBasisMax) {
         for (int j = tid; j < a.nx; j += kPostT) bX[j] = a.nx > 1 ? (2.0 * j - (a.nx - 1)) / (double)(a.nx - 1) : 0.0;
         for (int i = tid; i < a.ny; i += kPostT) bY[i] = a.ny > 1 ? (2.0 * i - (a.ny - 1)) / (double)(a.ny - 1) : 0.0;
@@ -676,7 +681,7 @@ __global__ void __launch_bounds__(kPostT) k_pupil_post(PostArgs a) {
         if (wg == 0 && tid < 2)  // the first valid rows (F)
             __hip_atomic_store(&a.sync[2 + tid], (unsigned)a.ny, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    post_sync(a.sync, gen);  // 1
+    post_sync(a.sync, gen, a.clocks);  // 1
     // the partials of bank `bank`, added in workgroup order (thread q < Q forms sum q into red[0][q])
     auto gather = [&](int bank, int Q) {
         if (tid < Q) {
@@ -777,26 +782,26 @@ __global__ void __launch_bounds__(kPostT) k_pupil_post(PostArgs a) {
     double acc[kMomMax];
     moments(5, nullptr, 0.0, 0, 0.0, acc);
     put(1, acc, kMomMax);
-    post_sync(a.sync, gen);  // 2
+    post_sync(a.sync, gen, a.clocks);  // 2
     // ---- C: the quadratic fit, the residual mean's sums
     gather(1, kMomMax);
     if (tid == 0 && red[0][20] < 5) sflag |= 1;  // curve_fit refuses fewer points than parameters
     normal_solve(std::integral_constant<int, 5>{}, 0);  // c1 = sys[0..5)
     moments(5, sys, 0.0, 1, 0.0, acc);
     put(0, acc, kMomMax);
-    post_sync(a.sync, gen);  // 3
+    post_sync(a.sync, gen, a.clocks);  // 3
     // ---- D: the residuals' spread
     gather(0, kMomMax);
     const double n1 = red[0][20], mu = red[0][0] / red[0][20];
     moments(5, sys, 0.0, 2, mu, acc);
     put(1, acc, kMomMax);
-    post_sync(a.sync, gen);  // 4
+    post_sync(a.sync, gen, a.clocks);  // 4
     // ---- E: the 3-sigma filter, the plane's sums
     gather(1, kMomMax);
     const double thr = a.sigma * sqrt(red[0][0] / n1);
     moments(3, sys, thr, 0, 0.0, acc);
     put(0, acc, kMomMax);
-    post_sync(a.sync, gen);  // 5
+    post_sync(a.sync, gen, a.clocks);  // 5
     // ---- F: the plane, corrected = (map - nanmean) - plane, rotate_with_nan's NaN split, and psf_calc's
     // rotation estimate's first valid rows of columns nx / 4 and 3 nx / 4 (:1122-1132)
     gather(0, kMomMax);
@@ -821,7 +826,7 @@ __global__ void __launch_bounds__(kPostT) k_pupil_post(PostArgs a) {
             if (!nan && pj[q] == c3) atomicMin(&a.sync[3], (unsigned)pi[q]);
         }
     }
-    post_sync(a.sync, gen);  // 6
+    post_sync(a.sync, gen, a.clocks);  // 6
     // ---- G: the rotation (workgroup 0) and the parameter block; with fuse, the B-spline prefilter of
     // the map (workgroup 0) and the mask (workgroup 1) in LDS, both axes
     if (wg == 0 && tid == 0) {
@@ -866,7 +871,7 @@ __global__ void __launch_bounds__(kPostT) k_pupil_post(PostArgs a) {
                 base[k] = smem[i * pitch + j];
             }
         }
-        post_sync(a.sync, gen);  // 7
+        post_sync(a.sync, gen, a.clocks);  // 7
         // ---- H: rotate_with_nan's interpolation (k_rotate_post's)
         const RotArgs ra{a.coef, a.ny, a.nx, P[13], P[14], -P[14], P[13], P[15], P[16], a.rotated, a.opd};
 #pragma unroll
@@ -877,6 +882,7 @@ __global__ void __launch_bounds__(kPostT) k_pupil_post(PostArgs a) {
     }
     // the last workgroup out leaves the counters at zero for the next launch
     __syncthreads();
+    if (wg == 0 && tid == 0) a.clocks[15] = wall_clock64();
     if (tid == 0) {
         const unsigned d = __hip_atomic_fetch_add(&a.sync[1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
         if (d == (unsigned)G - 1) {
@@ -1061,9 +1067,9 @@ int akb_plane_subtract_f64(const double* z, int ny, int nx, const double* d_coef
     return launch_status("k_plane_subtract");
 }
 
-// the post's work: sync (4 doubles, first: at the same place for any map size) | partials
-// (2 kPostG kPostPart) | buffer sums (8) | coef (2 ny nx)
-constexpr int64_t kPostHead = 4 + 2 * kPostG * kPostPart + 8;
+// the post's work: sync (4 doubles, first: at the same place for any map size) | phase clocks (16) |
+// partials (2 kPostG kPostPart) | buffer sums (8) | coef (2 ny nx)
+constexpr int64_t kPostHead = 4 + 16 + 2 * kPostG * kPostPart + 8;
 int64_t akb_pupil_post_work_bytes(int ny, int nx) {
     if (ny < 1 || nx < 1) return -1;
     return (kPostHead + 2 * (int64_t)ny * nx) * 8;
@@ -1078,8 +1084,8 @@ int akb_pupil_post_f64(const double* map, int ny, int nx, double sigma, double* 
     double* const head = (double*)work;
     double* const w = head + kPostHead;  // coef
     const int fuse = ny <= kPostFuse && nx <= kPostFuse;
-    PostArgs a{map, ny, nx, sigma, corrected, rotated, opd, w, head + 4, head + 4 + 2 * kPostG * kPostPart,
-               (unsigned*)head, d_params, fuse};
+    PostArgs a{map, ny, nx, sigma, corrected, rotated, opd, w, head + 20, head + 20 + 2 * kPostG * kPostPart,
+               (unsigned*)head, (unsigned long long*)(head + 4), d_params, fuse};
     k_pupil_post<<<kPostG, kPostT, 0, (hipStream_t)stream>>>(a);
     int st = launch_status("k_pupil_post");
     if (st || fuse) return st;
