@@ -491,23 +491,41 @@ __global__ void __launch_bounds__(kCellTile * kCellTile) k_gd_cells_tiled(Grid g
         inv_dx = inv_step(tc.t.gx, tc.t.mx);
         inv_dy = inv_step(tc.t.gy, tc.t.my);
     }
+    // a tile's V x V vertices, two per thread, into registers: the next tile's are loaded while this
+    // one is checked (its loads then wait behind no other work)
+    constexpr int NL = (V * V + T * T - 1) / (T * T);
+    auto load_tile = [&](int64_t tile, double (&px)[NL], double (&py)[NL]) {
+        const int tv = (int)(tile / tiles_h), th = (int)(tile - (int64_t)tv * tiles_h);
+        const int iv0 = r_lo + tv * T, ih0 = th * T;
+#pragma unroll
+        for (int u = 0; u < NL; ++u) {
+            const int k = threadIdx.x + u * T * T;
+            const int rr = k / V, cc = k - (k / V) * V;
+            const int iv = iv0 + rr, ih = ih0 + cc;
+            px[u] = py[u] = 0.0;
+            if (k < V * V && iv < g.nv && ih < g.nh && iv <= r_hi + 1) {
+                const int64_t q = (int64_t)iv * g.nh + ih;
+                px[u] = g.x[q];
+                py[u] = g.y[q];
+            }
+        }
+    };
+    double px[NL], py[NL];
+    if ((int64_t)blockIdx.x < ntiles) load_tile(blockIdx.x, px, py);
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int tv = (int)(tile / tiles_h), th = (int)(tile - (int64_t)tv * tiles_h);
         const int iv0 = r_lo + tv * T, ih0 = th * T;
         __syncthreads();
-        for (int k = threadIdx.x; k < V * V; k += blockDim.x) {
-            const int rr = k / V, cc = k - (k / V) * V;
-            const int iv = iv0 + rr, ih = ih0 + cc;
-            double x = 0.0, y = 0.0;
-            if (iv < g.nv && ih < g.nh && iv <= r_hi + 1) {
-                const int64_t q = (int64_t)iv * g.nh + ih;
-                x = g.x[q];
-                y = g.y[q];
+#pragma unroll
+        for (int u = 0; u < NL; ++u) {
+            const int k = threadIdx.x + u * T * T;
+            if (k < V * V) {
+                vx[k] = px[u];
+                vy[k] = py[u];
             }
-            vx[k] = x;
-            vy[k] = y;
         }
         __syncthreads();
+        if (tile + gridDim.x < ntiles) load_tile(tile + gridDim.x, px, py);
         // the diagonals of the tile's cells and of the next row / column (cell_diag's arithmetic)
         auto diag_of = [&](int rr, int cc, double* viol) {
             const int k00 = rr * V + cc, k01 = k00 + 1, k10 = k00 + V, k11 = k10 + 1;
@@ -866,7 +884,32 @@ __device__ __forceinline__ GradAcc<NV> chord_sums(const Grid& g, int64_t n, int6
                                                   const double (&fi)[NV], const double* __restrict__ f,
                                                   const double* __restrict__ gin) {
     GradAcc<NV> A;
-    for (int32_t k = g.xptr[r] + sub; k < g.xptr[r + 1]; k += W) grad_edge<NV>(g, n, g.xidx[k], xi, yi, fi, f, gin, A);
+    // four of the lane's chords at a time: their indices, then their data, loaded before the first
+    // edge sum (the same edges in the same order; a loop of index-load, data-load, sum waited out
+    // two memory latencies per chord)
+    constexpr int kB = 4;
+    const int32_t k1 = g.xptr[r + 1];
+    for (int32_t k0 = g.xptr[r] + sub; k0 < k1; k0 += kB * W) {
+        int64_t js[kB];
+#pragma unroll
+        for (int b = 0; b < kB; ++b) js[b] = k0 + b * W < k1 ? g.xidx[k0 + b * W] : -1;
+        double xj[kB], yj[kB], fj[kB][NV], gxj[kB][NV], gyj[kB][NV];
+#pragma unroll
+        for (int b = 0; b < kB; ++b) {
+            const int64_t j = js[b] < 0 ? 0 : js[b];
+            xj[b] = g.x[j];
+            yj[b] = g.y[j];
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                fj[b][v] = f[v * n + j];
+                gxj[b][v] = gin ? gin[2 * (v * n + j)] : 0.0;
+                gyj[b][v] = gin ? gin[2 * (v * n + j) + 1] : 0.0;
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < kB; ++b)
+            if (js[b] >= 0) acc_edge<NV>(A, edge_geom(xj[b] - xi, yj[b] - yi), fi, fj[b], gxj[b], gyj[b]);
+    }
     acc_reduce<NV, W>(A);  // (the chords run in the axis chain: d stays 0)
     return A;
 }
@@ -1367,22 +1410,48 @@ __global__ void __launch_bounds__(kBandThreads) k_gd_cone_band(Grid g, BandTiles
         __shared__ uint8_t sdg[(kBandTR + 1) * CC];
         int r0, c0, r1, c1;
         band_tile(bt, g.nv, g.nh, blockIdx.x - nr8, r0, c0, r1, c1);
-        // the tile's vertices with a one-vertex halo (rows r0 - 1 .. r0 + TR, inside the lattice)
-        for (int k = threadIdx.x; k < HN; k += kBandThreads) {
+        // the tile's vertices with a one-vertex halo (rows r0 - 1 .. r0 + TR, inside the lattice) and
+        // the diagonals of cells (r0 - 1 .. r0 + TR - 1) x (c0 - 1 .. c0 + TC - 1): every load of a
+        // thread issued before the first LDS store (one memory latency per tile)
+        constexpr int NQ = (HN + kBandThreads - 1) / kBandThreads, NC = ((kBandTR + 1) * CC + kBandThreads - 1) / kBandThreads;
+        double lx[NQ], ly[NQ], lf[NQ], lgx[NQ], lgy[NQ];
+        uint8_t ld[NC];
+#pragma unroll
+        for (int u = 0; u < NQ; ++u) {
+            const int k = threadIdx.x + u * kBandThreads;
             const int iv = r0 - 1 + k / HC, ih = c0 - 1 + (k - (k / HC) * HC);
-            if (iv >= 0 && iv < g.nv && ih >= 0 && ih < g.nh) {
+            lx[u] = ly[u] = lf[u] = lgx[u] = lgy[u] = 0.0;
+            if (k < HN && iv >= 0 && iv < g.nv && ih >= 0 && ih < g.nh) {
                 const int64_t q = (int64_t)iv * g.nh + ih;
-                sx[k] = g.x[q];
-                sy[k] = g.y[q];
-                sf[k] = a.f[q];
-                sgx[k] = a.gin ? a.gin[2 * q] : 0.0;
-                sgy[k] = a.gin ? a.gin[2 * q + 1] : 0.0;
+                lx[u] = g.x[q];
+                ly[u] = g.y[q];
+                lf[u] = a.f[q];
+                lgx[u] = a.gin ? a.gin[2 * q] : 0.0;
+                lgy[u] = a.gin ? a.gin[2 * q + 1] : 0.0;
             }
         }
-        // the diagonals of cells (r0 - 1 .. r0 + TR - 1) x (c0 - 1 .. c0 + TC - 1)
-        for (int k = threadIdx.x; k < (kBandTR + 1) * CC; k += kBandThreads) {
+#pragma unroll
+        for (int u = 0; u < NC; ++u) {
+            const int k = threadIdx.x + u * kBandThreads;
             const int cv = r0 - 1 + k / CC, ch = c0 - 1 + (k - (k / CC) * CC);
-            sdg[k] = (cv >= 0 && cv < g.nv - 1 && ch >= 0 && ch < g.nh - 1) ? g.diag[(int64_t)cv * (g.nh - 1) + ch] : 0;
+            ld[u] = (k < (kBandTR + 1) * CC && cv >= 0 && cv < g.nv - 1 && ch >= 0 && ch < g.nh - 1)
+                        ? g.diag[(int64_t)cv * (g.nh - 1) + ch] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < NQ; ++u) {
+            const int k = threadIdx.x + u * kBandThreads;
+            if (k < HN) {
+                sx[k] = lx[u];
+                sy[k] = ly[u];
+                sf[k] = lf[u];
+                sgx[k] = lgx[u];
+                sgy[k] = lgy[u];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < NC; ++u) {
+            const int k = threadIdx.x + u * kBandThreads;
+            if (k < (kBandTR + 1) * CC) sdg[k] = ld[u];
         }
         __syncthreads();
         const int tr = threadIdx.x / kBandTC, tc = threadIdx.x - (threadIdx.x / kBandTC) * kBandTC;

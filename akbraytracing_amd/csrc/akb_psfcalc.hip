@@ -671,7 +671,19 @@ __global__ void __launch_bounds__(kPostT) k_pupil_post(PostArgs a) {
         if (wg < nbuf) {
             const int64_t b0 = (int64_t)wg * 8192;
             const int len = (int)(total - b0 < 8192 ? total - b0 : 8192);
-            for (int k = tid; k < len; k += kPostT) smem[k] = a.m[b0 + k];
+            // all 16 of a thread's loads in flight at once (a loop of load-then-store would wait
+            // out each load's latency in turn)
+            double t[8192 / kPostT];
+#pragma unroll
+            for (int q = 0; q < 8192 / kPostT; ++q) {
+                const int k = tid + q * kPostT;
+                t[q] = k < len ? a.m[b0 + k] : 0.0;
+            }
+#pragma unroll
+            for (int q = 0; q < 8192 / kPostT; ++q) {
+                const int k = tid + q * kPostT;
+                if (k < len) smem[k] = t[q];
+            }
             __syncthreads();
             if (tid < 64) {
                 const double v = pw_tree_wave<true>(tree, smem, len);
@@ -683,11 +695,16 @@ __global__ void __launch_bounds__(kPostT) k_pupil_post(PostArgs a) {
     }
     post_sync(a.sync, gen, a.clocks);  // 1
     // the partials of bank `bank`, added in workgroup order (thread q < Q forms sum q into red[0][q])
+    // (the launch has kPostG workgroups; every partial's load is issued before the first add)
     auto gather = [&](int bank, int Q) {
         if (tid < Q) {
             const double* pb = a.part + (int64_t)bank * kPostG * kPostPart + tid;
-            double v = pb[0];
-            for (int b = 1; b < G; ++b) v += pb[(int64_t)b * kPostPart];
+            double t[kPostG];
+#pragma unroll
+            for (int b = 0; b < kPostG; ++b) t[b] = pb[(int64_t)b * kPostPart];
+            double v = t[0];
+#pragma unroll
+            for (int b = 1; b < kPostG; ++b) v += t[b];
             red[0][tid] = v;
         }
         __syncthreads();
@@ -699,16 +716,28 @@ __global__ void __launch_bounds__(kPostT) k_pupil_post(PostArgs a) {
     double mean;
     {
         if (tid == 0) {
-            double c = a.part[0], lo = a.part[1], hi = a.part[2];
-            for (int b = 1; b < G; ++b) {
+            double pc[kPostG], pl[kPostG], ph[kPostG], bs[8];
+#pragma unroll
+            for (int b = 0; b < kPostG; ++b) {
                 const double* pb = a.part + (int64_t)b * kPostPart;
-                c += pb[0];
-                lo = fmin(lo, pb[1]);
-                hi = fmax(hi, pb[2]);
+                pc[b] = pb[0];
+                pl[b] = pb[1];
+                ph[b] = pb[2];
+            }
+            const int nbuf = (int)((total + 8191) / 8192);
+#pragma unroll
+            for (int b = 0; b < 8; ++b) bs[b] = b < nbuf ? a.bufsum[b] : 0.0;
+            double c = pc[0], lo = pl[0], hi = ph[0];
+#pragma unroll
+            for (int b = 1; b < kPostG; ++b) {
+                c += pc[b];
+                lo = fmin(lo, pl[b]);
+                hi = fmax(hi, ph[b]);
             }
             double tot = 0.0;
-            const int nbuf = (int)((total + 8191) / 8192);
-            for (int b = 0; b < nbuf; ++b) tot = tot + a.bufsum[b];
+#pragma unroll
+            for (int b = 0; b < 8; ++b)
+                if (b < nbuf) tot = tot + bs[b];
             sys[24] = tot / c;
             sys[25] = c;
             sys[26] = lo;
@@ -857,9 +886,20 @@ __global__ void __launch_bounds__(kPostT) k_pupil_post(PostArgs a) {
         if (wg < 2) {
             const int pitch = a.nx + 1;  // a column's points on distinct banks
             double* base = a.coef + (int64_t)wg * total;
-            for (int64_t k = tid; k < total; k += kPostT) {
-                const int i = (int)(k / a.nx), j = (int)(k - (int64_t)i * a.nx);
-                smem[i * pitch + j] = base[k];
+            for (int64_t k0 = tid; k0 < total; k0 += 16 * kPostT) {  // 16 loads in flight per thread
+                double t[16];
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const int64_t k = k0 + q * kPostT;
+                    t[q] = k < total ? base[k] : 0.0;
+                }
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const int64_t k = k0 + q * kPostT;
+                    if (k >= total) break;
+                    const int i = (int)(k / a.nx), j = (int)(k - (int64_t)i * a.nx);
+                    smem[i * pitch + j] = t[q];
+                }
             }
             __syncthreads();
             if (tid < a.nx) spline_line_lds<16>(smem + tid, a.ny, pitch);  // axis 0: the columns
