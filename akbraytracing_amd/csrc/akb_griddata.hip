@@ -2119,13 +2119,12 @@ __global__ void __launch_bounds__(kBlock, 5) k_gd_claim_hit(Grid g, Targets t, c
 }
 
 // pocket triangles: slivers along the boundary whose boxes hold from none to thousands of targets,
-// so one thread per triangle for the common boxes of at most kPocketLane targets, and a whole wave
-// (its lanes striding the box) for each larger one, taken in turn after the wave's small ones; the
-// target axes in LDS for tri_box's binary searches
-constexpr int kPocketLane = 4;
+// so one wave per triangle, its lanes striding the box (a workgroup per triangle left most of its
+// threads idle on the common few-target boxes; a thread per triangle left the long slivers' boxes
+// to one lane each: 326 us against 28 at C3); the target axes in LDS for tri_box's binary searches
 __global__ void __launch_bounds__(kBlock) k_gd_claim_pockets(Grid g, Targets t, int* owner) {
     const int64_t nc2 = 2 * ncells(g);
-    const int lane = threadIdx.x & 63;
+    const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
     __shared__ double sax[2 * kClaimAxisLds];
     if (t.mx <= kClaimAxisLds && t.my <= kClaimAxisLds) {
         for (int i = threadIdx.x; i < t.mx; i += blockDim.x) sax[i] = t.gx[i];
@@ -2134,35 +2133,15 @@ __global__ void __launch_bounds__(kBlock) k_gd_claim_pockets(Grid g, Targets t, 
         t.gx = sax;
         t.gy = sax + kClaimAxisLds;
     }
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t j0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); j0 < g.npock; j0 += stride) {
-        const int64_t j = j0 + lane;  // (the loop is wave-uniform)
-        Tri T{};
-        int c0 = 0, c1 = 0, r0 = 0, r1 = 0;
-        if (j < g.npock) {
-            T = tri_verts(g, nc2 + j);
-            tri_box(g, t, T, c0, c1, r0, r1);
-        }
+    for (int64_t j = (int64_t)blockIdx.x * nw + (threadIdx.x >> 6); j < g.npock; j += (int64_t)gridDim.x * nw) {
+        const Tri T = tri_verts(g, nc2 + j);
+        int c0, c1, r0, r1;
+        tri_box(g, t, T, c0, c1, r0, r1);
         const int w = c1 - c0;
-        const int64_t m = c0 < c1 && r0 < r1 ? (int64_t)w * (r1 - r0) : 0;
-        const bool big = m > kPocketLane;
-        if (!big)
-            for (int64_t k = 0; k < m; ++k) {
-                const int r = r0 + (int)(k / w), c = c0 + (int)(k - (int64_t)(k / w) * w);
-                claim_one(g, t, T, (int)(nc2 + j), r, c, owner);
-            }
-        unsigned long long bm = __ballot(big);
-        while (bm) {  // wave-uniform
-            const int q = __builtin_ctzll(bm);
-            bm &= bm - 1;
-            Tri B;
-            for (int k = 0; k < 3; ++k) B.v[k] = __shfl(T.v[k], q);
-            const int bc0 = __shfl(c0, q), bw = __shfl(w, q), br0 = __shfl(r0, q);
-            const int64_t bmn = __shfl(m, q);
-            for (int64_t k = lane; k < bmn; k += 64) {
-                const int r = br0 + (int)(k / bw), c = bc0 + (int)(k - (int64_t)(k / bw) * bw);
-                claim_one(g, t, B, (int)(nc2 + j0 + q), r, c, owner);
-            }
+        const int64_t m = (int64_t)w * (r1 - r0);
+        for (int64_t k = lane; k < m; k += 64) {
+            const int r = r0 + (int)(k / w), c = c0 + (int)(k - (int64_t)(k / w) * w);
+            claim_one(g, t, T, (int)(nc2 + j), r, c, owner);
         }
     }
 }
@@ -2516,7 +2495,8 @@ int cone_claims(const Grid& g, const Targets& t, int with_pockets, int* owner, h
         if ((st = launch_status("k_gd_claim"))) return st;
     }
     if (with_pockets && g.npock > 0) {
-        k_gd_claim_pockets<<<grid_for(g.npock, 1, kStreamGridCap), kBlock, 0, s>>>(g, t, owner);
+        const int64_t pw = ((int64_t)g.npock + kBlock / 64 - 1) / (kBlock / 64);
+        k_gd_claim_pockets<<<(unsigned)(pw < 16384 ? pw : 16384), kBlock, 0, s>>>(g, t, owner);
         if ((st = launch_status("k_gd_claim_pockets"))) return st;
     }
     return 0;
@@ -2654,8 +2634,9 @@ int akb_gd_claim_pockets_f64(const double* x, const double* y, int nv, int nh, c
     if (npock == 0) return 0;
     AKB_REQUIRE(ptri, "pockets needed");
     Grid g{x, y, nv, nh, diag, npock, ptri, nullptr, nullptr, nullptr, nullptr};
-    k_gd_claim_pockets<<<grid_for(npock, 1, kStreamGridCap), kBlock, 0, (hipStream_t)stream>>>(g, Targets{gx, gy, mx, my},
-                                                                                          owner);
+    const int64_t pw = ((int64_t)npock + kBlock / 64 - 1) / (kBlock / 64);
+    k_gd_claim_pockets<<<(unsigned)(pw < 16384 ? pw : 16384), kBlock, 0, (hipStream_t)stream>>>(g, Targets{gx, gy, mx, my},
+                                                                                               owner);
     return launch_status("k_gd_claim_pockets");
 }
 

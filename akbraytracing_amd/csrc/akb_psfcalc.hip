@@ -414,63 +414,29 @@ __device__ __forceinline__ bool solve_small_reg(double (&A)[N][N], double (&b)[N
     return ok;
 }
 
-// ---- the post across workgroups: kPostG workgroups of kPostT threads, each thread a few map
-// points held in registers, the phases separated by grid barriers (post_sync). The reductions add
-// per-workgroup partials in workgroup order - every workgroup forms the same sums and solves, so
-// no phase waits for one workgroup's result but the last.
-constexpr int kPostG = 32, kPostT = 512;
-constexpr int kPostPer = 4;             // map points per thread
-constexpr int64_t kPostMax = (int64_t)kPostG * kPostT * kPostPer;  // 65536
-constexpr int kPostPart = 24;           // a workgroup's partial words
-constexpr int kPostFuse = 128;          // maps up to 128 x 128: the spline prefilter and the rotation in the launch
+// ---- the post: one workgroup over the map (in LDS when it fits) - nanmean, the plane fits, the NaN
+// split, the rotation estimate - then the B-spline prefilter (k_spline_post: a workgroup per array,
+// both axes in LDS, four threads per line) and the rotation (k_rotate_post). A grid of workgroups
+// with a grid barrier between the phases was measured at ~10 us per barrier (the device-scope
+// release and acquire around each), three times the one workgroup's phases.
+constexpr int kPostThreads = 1024;
+constexpr int64_t kPostMax = 65536;  // map points the post handles
+constexpr int kPostFuse = 128;       // arrays up to 128 x 128: the prefilter in LDS, both axes in one launch
 
 struct PostArgs {
     const double* m;     // (ny, nx) gridded map (NaN outside the hull)
     int ny, nx;
     double sigma;        // the outlier filter's threshold in standard deviations (3)
     double* corrected;   // matrixWave2_Corrected
-    double* rotated;     // psf_calc's rotated map (nm, NaN outside)
-    double* opd;         // rotated * 1e-9 (the PSF's opd_m)
-    double* coef;        // work: (2, ny, nx) prefilter coefficients
-    double* part;        // work: (2, kPostG, kPostPart) partials, two banks (a phase reads one, writes the other)
-    double* bufsum;      // work: numpy's 8192-element buffer sums of the nanmean (<= 8)
-    unsigned* sync;      // work: arrivals, departures, the first valid rows (2), failure bits: zero between launches
-    unsigned long long* clocks;  // work: workgroup 0's wall clock (100 MHz) at the start and after each barrier
+    double* coef;        // work: (2, ny, nx) prefilter coefficients (the NaN split)
     double* params;      // out, kPostParams doubles (layout in akb_raytrace.h)
-    int fuse;            // the spline prefilter and the rotation in this launch
+    unsigned long long* clocks;  // work: the wall clock (100 MHz) at the phase ends (diagnostics)
 };
 
-// a grid barrier for the post's kPostG co-resident workgroups: the workgroup's stores complete
-// (__syncthreads), one thread makes them visible at device scope and arrives on a counter that only
-// grows within a launch (release), then polls it with plain device-scope loads - an acquiring poll
-// would invalidate the caches on every read - and acquires once the count is reached; a bounded
-// wait (bit 2 of the failure word on a timeout: the parameter block's flags then report it)
-__device__ void post_sync(unsigned* sync, unsigned& gen, unsigned long long* clocks) {
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        ++gen;
-        __hip_atomic_fetch_add(&sync[0], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned target = gen * gridDim.x;
-        unsigned spins = 0;
-        while (__hip_atomic_load(&sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-            __builtin_amdgcn_s_sleep(1);
-            if (++spins == (1u << 25)) {
-                atomicOr(&sync[4], 4u);
-                break;
-            }
-        }
-        __atomic_thread_fence(__ATOMIC_ACQUIRE);  // (agent scope: the default of a HIP fence)
-        if (blockIdx.x == 0) clocks[gen] = wall_clock64();
-    }
-    __syncthreads();
-}
-
-// a fixed-order workgroup sum of Q values per thread (wave shuffles, then the waves in order);
-// every thread gets the sums
+// fixed-order workgroup sum of q values per thread (wave shuffles, then the waves in order)
 template <int Q>
-__device__ __forceinline__ void wg_sum(double (&acc)[Q], double (*red)[kMomMax]) {
+__device__ __forceinline__ void block_sum(double (&acc)[Q], double (*red)[Q]) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    __syncthreads();  // every thread is past its last read of red
 #pragma unroll
     for (int q = 0; q < Q; ++q)
         for (int off = 32; off > 0; off >>= 1) acc[q] += __shfl_down(acc[q], off);
@@ -480,7 +446,7 @@ __device__ __forceinline__ void wg_sum(double (&acc)[Q], double (*red)[kMomMax])
     __syncthreads();
     if (threadIdx.x < Q) {
         double v = red[0][threadIdx.x];
-        for (int k = 1; k < kPostT / 64; ++k) v += red[k][threadIdx.x];
+        for (int k = 1; k < kPostThreads / 64; ++k) v += red[k][threadIdx.x];
         red[0][threadIdx.x] = v;
     }
     __syncthreads();
@@ -488,6 +454,29 @@ __device__ __forceinline__ void wg_sum(double (&acc)[Q], double (*red)[kMomMax])
     for (int q = 0; q < Q; ++q) acc[q] = red[0][q];
     __syncthreads();
 }
+
+// LDS of the post: the map for the nanmean and the moment passes (maps of up to 16384 points; larger
+// ones are read from global memory and `corrected`)
+constexpr int kPostLds = 16384;
+
+// a thread's map points k = tid + q kPostThreads as (row, column), stepped without divisions
+struct PostIdx {
+    int i, j, di, dj, nx;
+    __device__ PostIdx(int tid, int nx_) : nx(nx_) {
+        i = tid / nx_;
+        j = tid - i * nx_;
+        di = kPostThreads / nx_;
+        dj = kPostThreads - di * nx_;
+    }
+    __device__ void next() {
+        i += di;
+        j += dj;
+        if (j >= nx) {
+            j -= nx;
+            ++i;
+        }
+    }
+};
 
 // spline_line's arithmetic on a line in LDS (stride s), in chunks of kCh points: each chunk's values
 // are read at once (independent LDS reads), the pass runs on them in registers with the running
@@ -605,165 +594,235 @@ __global__ void __launch_bounds__(kSplineThreads) k_spline_block(double* __restr
     }
 }
 
-__global__ void __launch_bounds__(kPostT) k_pupil_post(PostArgs a) {
-    __shared__ double smem[kPostFuse * (kPostFuse + 1)];  // a nanmean buffer, then one spline array
-    __shared__ PwTree tree;
-    __shared__ double red[kPostT / 64][kMomMax];
+// spline_filter1d's recursions on a line in LDS (stride s) split over P consecutive lanes of a wave
+// (sub: the lane's segment of ceil(n / P) points): the gain; the mirror-symmetric initial sum as
+// per-segment parts added in segment order; the causal pass c[i] += z c[i-1] run per segment from
+// zero and corrected by z^(i - b0 + 1) times the true value before the segment (the carries passed
+// up the segments); the anti-causal pass c[i] = z (c[i+1] - c[i]) likewise downwards. The same
+// recursions as spline_line, a different rounding order (~1e-16 relative; |z| = 0.27), a P-th of
+// the sequential steps.
+template <int P>
+__device__ void spline_line_par(double* c, int n, int s, int sub) {
+    const double z = sqrt(3.0) - 2.0;
+    const double gain = (1.0 - z) * (1.0 - 1.0 / z);
+    const int lane = threadIdx.x & 63, base = lane & ~(P - 1);
+    const int seg = (n + P - 1) / P;
+    const int b0 = min(n, sub * seg), b1 = min(n, b0 + seg);
+    for (int i = b0; i < b1; ++i) c[i * s] = c[i * s] * gain;
+    if (n == 1) return;
+    wave_sync();
+    const double zn1 = pow(z, (double)(n - 1));
+    double part = 0.0;
+    {
+        const int i0 = max(b0, 1), i1 = min(b1, n - 1);
+        double zi = i0 < i1 ? pow(z, (double)i0) : 0.0;
+        for (int i = i0; i < i1; ++i) {
+            part += zi * (c[i * s] + zn1 * c[(n - 1 - i) * s]);
+            zi *= z;
+        }
+    }
+    double tot = 0.0;
+#pragma unroll
+    for (int k = 0; k < P; ++k) tot += __shfl(part, base + k);
+    const double y0 = (c[0] + zn1 * c[(n - 1) * s] + tot) / (1.0 - zn1 * zn1);
+    const double zl = pow(z, (double)(b1 - b0));  // z^(segment length), 1 for an empty segment
+    wave_sync();
+    // causal
+    double u = 0.0;
+    if (b0 < b1) {
+        u = b0 == 0 ? y0 : c[b0 * s];
+        c[b0 * s] = u;
+        for (int i = b0 + 1; i < b1; ++i) {
+            u = c[i * s] + z * u;
+            c[i * s] = u;
+        }
+    }
+    double ein = 0.0;  // the true value at b0 - 1
+    {
+        double e = 0.0;
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+            const double uk = __shfl(u, base + k), zk = __shfl(zl, base + k);
+            if (k == sub) ein = e;
+            e = uk + zk * e;
+        }
+    }
+    if (ein != 0.0) {
+        double zk = z;
+        for (int i = b0; i < b1; ++i) {
+            c[i * s] = c[i * s] + zk * ein;
+            zk *= z;
+        }
+    }
+    wave_sync();
+    // anti-causal
+    const double next = (z * c[(n - 2) * s] + c[(n - 1) * s]) * z / (z * z - 1.0);
+    wave_sync();
+    double v = 0.0;
+    if (b0 < b1) {
+        int i = b1 - 1;
+        if (b1 == n) {
+            v = next;
+            c[i * s] = v;
+            --i;
+        }
+        for (; i >= b0; --i) {
+            v = z * (v - c[i * s]);
+            c[i * s] = v;
+        }
+    }
+    double bin = 0.0;  // the true value at b1
+    {
+        double e = 0.0;
+#pragma unroll
+        for (int k = P - 1; k >= 0; --k) {
+            const double vk = __shfl(v, base + k), zk = __shfl(zl, base + k);
+            if (k == sub) bin = e;
+            e = vk + zk * e;
+        }
+    }
+    if (bin != 0.0) {
+        double zk = z;
+        for (int i = b1 - 1; i >= b0; --i) {
+            c[i * s] = c[i * s] + zk * bin;
+            zk *= z;
+        }
+    }
+}
+
+// the post's B-spline prefilter for arrays of up to kPostFuse x kPostFuse: workgroup 0 the map,
+// 1 the mask, each array in LDS (row pitch nx + 1), both axes, four lanes per line
+constexpr int kSplinePostThreads = 4 * kPostFuse;
+__global__ void __launch_bounds__(kSplinePostThreads) k_spline_post(double* __restrict__ coef, int ny, int nx) {
+    __shared__ double a[kPostFuse * (kPostFuse + 1)];
+    const int64_t total = (int64_t)ny * nx;
+    const int pitch = nx + 1, tid = threadIdx.x;
+    double* base = coef + (int64_t)blockIdx.x * total;
+    for (int64_t k0 = tid; k0 < total; k0 += 16 * kSplinePostThreads) {  // 16 loads in flight per thread
+        double t[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int64_t k = k0 + q * kSplinePostThreads;
+            t[q] = k < total ? base[k] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int64_t k = k0 + q * kSplinePostThreads;
+            if (k >= total) break;
+            const int i = (int)(k / nx), j = (int)(k - (int64_t)i * nx);
+            a[i * pitch + j] = t[q];
+        }
+    }
+    __syncthreads();
+    if (tid / 4 < nx) spline_line_par<4>(a + tid / 4, ny, pitch, tid & 3);  // axis 0: the columns
+    __syncthreads();
+    if (tid / 4 < ny) spline_line_par<4>(a + (tid / 4) * pitch, nx, 1, tid & 3);  // axis 1: the rows
+    __syncthreads();
+    for (int64_t k = tid; k < total; k += kSplinePostThreads) {
+        const int i = (int)(k / nx), j = (int)(k - (int64_t)i * nx);
+        base[k] = a[i * pitch + j];
+    }
+}
+
+__global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
+    __shared__ double smem[kPostLds];  // the map, then matrixWave2 - nanmean (when it fits)
+    __shared__ PwTree trees[2];        // the nanmean's pairwise trees (waves 0 and 1)
+    __shared__ double bufsum[8];
+    __shared__ int firstrow[2];
+    __shared__ double red[kPostThreads / 64][kMomMax];
     __shared__ double sys[32];
     __shared__ int sflag;
-    // basis5's X (per column) and Y (per row), each division once
+    // basis5's X (per column) and Y (per row), each division once (the moment passes and the plane
+    // subtraction would repeat two divisions per point each)
     __shared__ double bX[kPostBasisMax], bY[kPostBasisMax];
     const int64_t total = (int64_t)a.ny * a.nx;
-    const int tid = threadIdx.x, G = gridDim.x, wg = blockIdx.x;
-    const int64_t S = (int64_t)G * kPostT, gt = (int64_t)wg * kPostT + tid;
+    const int tid = threadIdx.x, w = tid >> 6;
     double* P = a.params;
-    unsigned gen = 0;
-    if (wg == 0 && tid == 0) a.clocks[0] = wall_clock64();
-    if (a.nx <= kPostBasisMax && a.ny <= kPostBasisMax) {
-        for (int j = tid; j < a.nx; j += kPostT) bX[j] = a.nx > 1 ? (2.0 * j - (a.nx - 1)) / (double)(a.nx - 1) : 0.0;
-        for (int i = tid; i < a.ny; i += kPostT) bY[i] = a.ny > 1 ? (2.0 * i - (a.ny - 1)) / (double)(a.ny - 1) : 0.0;
+    if (tid == 0) a.clocks[0] = wall_clock64();
+    const bool tab = a.nx <= kPostBasisMax && a.ny <= kPostBasisMax;
+    if (tab) {
+        for (int j = tid; j < a.nx; j += kPostThreads) bX[j] = a.nx > 1 ? (2.0 * j - (a.nx - 1)) / (double)(a.nx - 1) : 0.0;
+        for (int i = tid; i < a.ny; i += kPostThreads) bY[i] = a.ny > 1 ? (2.0 * i - (a.ny - 1)) / (double)(a.ny - 1) : 0.0;
     }
-    if (tid == 0) sflag = 0;
-    // this thread's points k = gt + q S (NaN past the map: no point)
-    double z[kPostPer];
-    int pi[kPostPer], pj[kPostPer];
+    // the map into LDS when it fits: every thread's loads in flight at once (the passes below then
+    // wait for LDS only)
+    const bool in_lds = total <= kPostLds;
+    if (in_lds) {
+        for (int64_t k0 = 0; k0 < total; k0 += 16 * kPostThreads) {
+            double t[16];
 #pragma unroll
-    for (int q = 0; q < kPostPer; ++q) {
-        const int64_t k = gt + q * S;
-        z[q] = k < total ? a.m[k] : __builtin_nan("");
-        pi[q] = k < total ? (int)(k / a.nx) : 0;
-        pj[q] = k < total ? (int)(k - (int64_t)pi[q] * a.nx) : 0;
+            for (int q = 0; q < 16; ++q) {
+                const int64_t k = k0 + q * kPostThreads + tid;
+                if (k < total) t[q] = a.m[k];
+            }
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int64_t k = k0 + q * kPostThreads + tid;
+                if (k < total) smem[k] = t[q];
+            }
+        }
+        __syncthreads();
     }
-    // ---- A: the finite count and the range (np.nanmin / np.nanmax: the cone solve's error estimate
-    // is held to it, FaithfulPupil); the nanmean's buffers (numpy's pairwise sum of the NaN-zeroed
-    // map, a buffer per workgroup, one wave summing it from LDS)
-    {
-        double c[1] = {0.0};
-        double lo = INFINITY, hi = -INFINITY;
-#pragma unroll
-        for (int q = 0; q < kPostPer; ++q)
-            if (z[q] == z[q]) {
-                c[0] += 1.0;
-                lo = fmin(lo, z[q]);
-                hi = fmax(hi, z[q]);
-            }
-        for (int off = 32; off > 0; off >>= 1) {
-            lo = fmin(lo, __shfl_down(lo, off));
-            hi = fmax(hi, __shfl_down(hi, off));
-        }
-        __shared__ double ext[kPostT / 64][2];
-        if ((tid & 63) == 0) {
-            ext[tid >> 6][0] = lo;
-            ext[tid >> 6][1] = hi;
-        }
-        wg_sum<1>(c, red);
-        if (tid == 0) {
-            for (int k = 1; k < kPostT / 64; ++k) {
-                lo = fmin(lo, ext[k][0]);
-                hi = fmax(hi, ext[k][1]);
-            }
-            double* pp = a.part + (int64_t)wg * kPostPart;  // bank 0
-            pp[0] = c[0];
-            pp[1] = fmin(lo, ext[0][0]);
-            pp[2] = fmax(hi, ext[0][1]);
-        }
-        const int nbuf = (int)((total + 8191) / 8192);
-        if (wg < nbuf) {
-            const int64_t b0 = (int64_t)wg * 8192;
+    const double* src = in_lds ? smem : a.m;
+    if (tid == 0) a.clocks[1] = wall_clock64();
+    // np.nanmean: numpy's pairwise sum of the NaN-zeroed map, one wave per 8192-element buffer
+    // (waves 0 and 1 alternate over the buffers)
+    const int nbuf = (int)((total + 8191) / 8192);
+    if (w < 2) {
+        for (int b = w; b < nbuf; b += 2) {
+            const int64_t b0 = (int64_t)b * 8192;
             const int len = (int)(total - b0 < 8192 ? total - b0 : 8192);
-            // all 16 of a thread's loads in flight at once (a loop of load-then-store would wait
-            // out each load's latency in turn)
-            double t[8192 / kPostT];
-#pragma unroll
-            for (int q = 0; q < 8192 / kPostT; ++q) {
-                const int k = tid + q * kPostT;
-                t[q] = k < len ? a.m[b0 + k] : 0.0;
-            }
-#pragma unroll
-            for (int q = 0; q < 8192 / kPostT; ++q) {
-                const int k = tid + q * kPostT;
-                if (k < len) smem[k] = t[q];
-            }
-            __syncthreads();
-            if (tid < 64) {
-                const double v = pw_tree_wave<true>(tree, smem, len);
-                if (tid == 0) a.bufsum[wg] = v;
-            }
+            const double v = pw_tree_wave<true>(trees[w], src + b0, len);
+            if ((tid & 63) == 0) bufsum[b] = v;
+            wave_sync();
         }
-        if (wg == 0 && tid < 2)  // the first valid rows (F)
-            __hip_atomic_store(&a.sync[2 + tid], (unsigned)a.ny, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    post_sync(a.sync, gen, a.clocks);  // 1
-    // the partials of bank `bank`, added in workgroup order (thread q < Q forms sum q into red[0][q])
-    // (the launch has kPostG workgroups; every partial's load is issued before the first add)
-    auto gather = [&](int bank, int Q) {
-        if (tid < Q) {
-            const double* pb = a.part + (int64_t)bank * kPostG * kPostPart + tid;
-            double t[kPostG];
-#pragma unroll
-            for (int b = 0; b < kPostG; ++b) t[b] = pb[(int64_t)b * kPostPart];
-            double v = t[0];
-#pragma unroll
-            for (int b = 1; b < kPostG; ++b) v += t[b];
-            red[0][tid] = v;
+    // the finite count, and the map's range (np.nanmin / np.nanmax: the cone solve's error estimate
+    // is held to it, FaithfulPupil)
+    double cnt[1] = {0.0};
+    double lo = INFINITY, hi = -INFINITY;
+    for (int64_t k = tid; k < total; k += kPostThreads) {
+        const double v = src[k];
+        if (v == v) {
+            cnt[0] += 1.0;
+            lo = fmin(lo, v);
+            hi = fmax(hi, v);
         }
-        __syncthreads();
-    };
-    auto put = [&](int bank, const double* acc, int Q) {
-        if (tid < Q) a.part[(int64_t)bank * kPostG * kPostPart + (int64_t)wg * kPostPart + tid] = acc[tid];
-    };
-    // ---- B: mean, matrixWave2 - nanmean, the quadratic fit's sums
-    double mean;
-    {
-        if (tid == 0) {
-            double pc[kPostG], pl[kPostG], ph[kPostG], bs[8];
-#pragma unroll
-            for (int b = 0; b < kPostG; ++b) {
-                const double* pb = a.part + (int64_t)b * kPostPart;
-                pc[b] = pb[0];
-                pl[b] = pb[1];
-                ph[b] = pb[2];
-            }
-            const int nbuf = (int)((total + 8191) / 8192);
-#pragma unroll
-            for (int b = 0; b < 8; ++b) bs[b] = b < nbuf ? a.bufsum[b] : 0.0;
-            double c = pc[0], lo = pl[0], hi = ph[0];
-#pragma unroll
-            for (int b = 1; b < kPostG; ++b) {
-                c += pc[b];
-                lo = fmin(lo, pl[b]);
-                hi = fmax(hi, ph[b]);
-            }
-            double tot = 0.0;
-#pragma unroll
-            for (int b = 0; b < 8; ++b)
-                if (b < nbuf) tot = tot + bs[b];
-            sys[24] = tot / c;
-            sys[25] = c;
-            sys[26] = lo;
-            sys[27] = hi;
-        }
-        __syncthreads();
-        mean = sys[24];
     }
-    double cm[kPostPer];
-#pragma unroll
-    for (int q = 0; q < kPostPer; ++q) cm[q] = z[q] - mean;
-    // plane_correction_with_nan_and_outlier_filter's sums over this thread's points (k_moments' forms)
+    for (int off = 32; off > 0; off >>= 1) {
+        lo = fmin(lo, __shfl_down(lo, off));
+        hi = fmax(hi, __shfl_down(hi, off));
+    }
+    __shared__ double ext[kPostThreads / 64][2];
+    if ((tid & 63) == 0) {
+        ext[w][0] = lo;
+        ext[w][1] = hi;
+    }
+    block_sum<1>(cnt, (double(*)[1])red);
+    double tot = 0.0;
+    for (int b = 0; b < nbuf; ++b) tot = tot + bufsum[b];
+    const double mean = tot / cnt[0];
+    // matrixWave2 - nanmean, the plane correction's input: in LDS when it fits, else in `corrected`
+    double* cm = in_lds ? smem : a.corrected;
+    __syncthreads();
+    for (int64_t k = tid; k < total; k += kPostThreads) cm[k] = src[k] - mean;
+    __syncthreads();
+    if (tid == 0) a.clocks[2] = wall_clock64();
+    // plane_correction_with_nan_and_outlier_filter: the four moment passes of k_moments
     auto moments = [&](int nb, const double* cf, double thr, int mode, double mu, double (&acc)[kMomMax]) {
 #pragma unroll
         for (int q = 0; q < kMomMax; ++q) acc[q] = 0.0;
-#pragma unroll
-        for (int q = 0; q < kPostPer; ++q) {
-            const double zz = cm[q];
-            if (zz != zz) continue;
+        PostIdx ix(tid, a.nx);
+        for (int64_t k = tid; k < total; k += kPostThreads, ix.next()) {
+            const double z = cm[k];
+            if (z != z) continue;
             double f[5];
-            basis5_tab(bX, bY, pi[q], pj[q], a.ny, a.nx, f);
+            basis5_tab(bX, bY, ix.i, ix.j, a.ny, a.nx, f);
             double res = 0.0;
             if (cf || mode > 0) {
                 double mm = 0.0;
                 for (int t = 0; t < 5; ++t) mm = __builtin_fma(cf[t], f[t], mm);
-                res = zz - mm;
+                res = z - mm;
                 if (mode == 0 && !(fabs(res) < thr)) continue;
             }
             if (mode == 1) {
@@ -778,18 +837,18 @@ __global__ void __launch_bounds__(kPostT) k_pupil_post(PostArgs a) {
                 for (int r = 0; r < 5; ++r) {
 #pragma unroll
                     for (int c = r; c < 5; ++c) {
-                        const int qq = r * 5 - r * (r - 1) / 2 + (c - r);
-                        if (nb == 5 || c < 3) acc[qq] = __builtin_fma(f[r], f[c], acc[qq]);
+                        const int q = r * 5 - r * (r - 1) / 2 + (c - r);
+                        if (nb == 5 || c < 3) acc[q] = __builtin_fma(f[r], f[c], acc[q]);
                     }
-                    if (nb == 5 || r < 3) acc[15 + r] = __builtin_fma(f[r], zz, acc[15 + r]);
+                    if (nb == 5 || r < 3) acc[15 + r] = __builtin_fma(f[r], z, acc[15 + r]);
                 }
                 acc[20] += 1.0;
             }
         }
-        wg_sum<kMomMax>(acc, red);
+        block_sum<kMomMax>(acc, red);
     };
-    // the normal equations of nb terms from the gathered sums (red[0]) into sys[at ..]
-    auto normal_solve = [&](auto nbc, int at) {
+    // the normal equations of nb terms from the moment slots (pupilmap._normal_solve) into sys[25..]
+    auto normal_solve = [&](const double (&mom)[kMomMax], auto nbc, int at) {
         constexpr int nb = decltype(nbc)::value;
         if (tid == 0) {
             double A[nb][nb], b[nb];
@@ -798,9 +857,9 @@ __global__ void __launch_bounds__(kPostT) k_pupil_post(PostArgs a) {
 #pragma unroll
                 for (int c = 0; c < nb; ++c) {
                     const int lo = r < c ? r : c, hi = r < c ? c : r;
-                    A[r][c] = red[0][lo * 5 - lo * (lo - 1) / 2 + (hi - lo)];
+                    A[r][c] = mom[lo * 5 - lo * (lo - 1) / 2 + (hi - lo)];
                 }
-                b[r] = red[0][15 + r];
+                b[r] = mom[15 + r];
             }
             if (!solve_small_reg<nb>(A, b)) sflag |= 2;
 #pragma unroll
@@ -808,128 +867,83 @@ __global__ void __launch_bounds__(kPostT) k_pupil_post(PostArgs a) {
         }
         __syncthreads();
     };
+    if (tid == 0) sflag = 0;
     double acc[kMomMax];
     moments(5, nullptr, 0.0, 0, 0.0, acc);
-    put(1, acc, kMomMax);
-    post_sync(a.sync, gen, a.clocks);  // 2
-    // ---- C: the quadratic fit, the residual mean's sums
-    gather(1, kMomMax);
-    if (tid == 0 && red[0][20] < 5) sflag |= 1;  // curve_fit refuses fewer points than parameters
-    normal_solve(std::integral_constant<int, 5>{}, 0);  // c1 = sys[0..5)
+    if (tid == 0 && acc[20] < 5) sflag |= 1;  // curve_fit refuses fewer points than parameters
+    normal_solve(acc, std::integral_constant<int, 5>{}, 0);  // c1 = sys[0..5)
     moments(5, sys, 0.0, 1, 0.0, acc);
-    put(0, acc, kMomMax);
-    post_sync(a.sync, gen, a.clocks);  // 3
-    // ---- D: the residuals' spread
-    gather(0, kMomMax);
-    const double n1 = red[0][20], mu = red[0][0] / red[0][20];
+    const double n1 = acc[20], mu = acc[0] / acc[20];
     moments(5, sys, 0.0, 2, mu, acc);
-    put(1, acc, kMomMax);
-    post_sync(a.sync, gen, a.clocks);  // 4
-    // ---- E: the 3-sigma filter, the plane's sums
-    gather(1, kMomMax);
-    const double thr = a.sigma * sqrt(red[0][0] / n1);
+    const double thr = a.sigma * sqrt(acc[0] / n1);
     moments(3, sys, thr, 0, 0.0, acc);
-    put(0, acc, kMomMax);
-    post_sync(a.sync, gen, a.clocks);  // 5
-    // ---- F: the plane, corrected = (map - nanmean) - plane, rotate_with_nan's NaN split, and psf_calc's
-    // rotation estimate's first valid rows of columns nx / 4 and 3 nx / 4 (:1122-1132)
-    gather(0, kMomMax);
-    if (tid == 0 && red[0][20] < 3) sflag |= 1;
-    normal_solve(std::integral_constant<int, 3>{}, 8);  // p2 = sys[8..11)
+    if (tid == 0 && acc[20] < 3) sflag |= 1;
+    normal_solve(acc, std::integral_constant<int, 3>{}, 8);  // p2 = sys[8..11)
+    if (tid == 0) a.clocks[3] = wall_clock64();
+    // corrected = (map - nanmean) - plane, and rotate_with_nan's NaN split of it
     {
-        const int c1 = a.nx / 4, c3 = a.nx * 3 / 4;
-#pragma unroll
-        for (int q = 0; q < kPostPer; ++q) {
-            const int64_t k = gt + q * S;
-            if (k >= total) continue;
+        PostIdx ix(tid, a.nx);
+        for (int64_t k = tid; k < total; k += kPostThreads, ix.next()) {
             double f[5];
-            basis5_tab(bX, bY, pi[q], pj[q], a.ny, a.nx, f);
+            basis5_tab(bX, bY, ix.i, ix.j, a.ny, a.nx, f);
             const double pl = __builtin_fma(sys[10], f[2], __builtin_fma(sys[9], f[1], sys[8] * f[0]));
-            const double v = cm[q];
+            const double v = cm[k];
             const bool nan = v != v;
             const double o = nan ? v : v - pl;
-            a.corrected[k] = o;
+            cm[k] = o;
+            if (in_lds) a.corrected[k] = o;
             a.coef[k] = nan ? 0.0 : o;
             a.coef[total + k] = nan ? 0.0 : 1.0;
-            if (!nan && pj[q] == c1) atomicMin(&a.sync[2], (unsigned)pi[q]);
-            if (!nan && pj[q] == c3) atomicMin(&a.sync[3], (unsigned)pi[q]);
         }
     }
-    post_sync(a.sync, gen, a.clocks);  // 6
-    // ---- G: the rotation (workgroup 0) and the parameter block; with fuse, the B-spline prefilter of
-    // the map (workgroup 0) and the mask (workgroup 1) in LDS, both axes
-    if (wg == 0 && tid == 0) {
+    __syncthreads();
+    // psf_calc's rotation estimate (:1122-1132): the first valid row of columns nx / 4 and 3 nx / 4
+    // (every row tested at once, the smallest kept)
+    if (tid < 2) firstrow[tid] = a.ny;
+    __syncthreads();
+    {
         const int c1 = a.nx / 4, c3 = a.nx * 3 / 4;
-        const int r1 = (int)__hip_atomic_load(&a.sync[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int r3 = (int)__hip_atomic_load(&a.sync[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const double qv = (r1 < a.ny && r3 < a.ny) ? (double)(r1 - r3) / (double)(c1 - c3) : __builtin_nan("");
-        const double rot = atan(qv);
+        for (int r = tid; r < 2 * a.ny; r += kPostThreads) {
+            const int row = r >> 1, c = (r & 1) ? c3 : c1;
+            const double v = cm[(int64_t)row * a.nx + c];
+            if (v == v) atomicMin(&firstrow[r & 1], row);
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        const int c1 = a.nx / 4, c3 = a.nx * 3 / 4;
+        const int r1 = firstrow[0], r3 = firstrow[1];
+        const double q = (r1 < a.ny && r3 < a.ny) ? (double)(r1 - r3) / (double)(c1 - c3) : __builtin_nan("");
+        const double rot = atan(q);
         const double deg = rot * (180.0 / 3.14159265358979323846);
         const double cs = cos_deg(deg), sn = sin_deg(deg);
         const double cy = (a.ny - 1) / 2.0, cx = (a.nx - 1) / 2.0;
+        sys[16] = rot;
+        sys[17] = deg;
+        sys[18] = cs;
+        sys[19] = sn;
+        sys[20] = cy - (cs * cy + sn * cx);
+        sys[21] = cx - (-sn * cy + cs * cx);
+    }
+    __syncthreads();
+    // rotate_with_nan(order 3): the B-spline prefilter (k_spline_post / k_spline_block) and the
+    // rotation (k_rotate_post) follow as their own launches
+    if (tid == 0) {
         P[0] = mean;
-        P[1] = sys[25];
+        P[1] = cnt[0];
         for (int q = 0; q < 5; ++q) P[2 + q] = sys[q];
         for (int q = 0; q < 3; ++q) P[7 + q] = sys[8 + q];
         P[10] = thr;
-        P[11] = rot;
-        P[12] = deg;
-        P[13] = cs;
-        P[14] = sn;
-        P[15] = cy - (cs * cy + sn * cx);
-        P[16] = cx - (-sn * cy + cs * cx);
-        P[17] = (double)(sflag | (int)__hip_atomic_load(&a.sync[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        P[18] = sys[26];
-        P[19] = sys[27];
-    }
-    if (a.fuse) {
-        if (wg < 2) {
-            const int pitch = a.nx + 1;  // a column's points on distinct banks
-            double* base = a.coef + (int64_t)wg * total;
-            for (int64_t k0 = tid; k0 < total; k0 += 16 * kPostT) {  // 16 loads in flight per thread
-                double t[16];
-#pragma unroll
-                for (int q = 0; q < 16; ++q) {
-                    const int64_t k = k0 + q * kPostT;
-                    t[q] = k < total ? base[k] : 0.0;
-                }
-#pragma unroll
-                for (int q = 0; q < 16; ++q) {
-                    const int64_t k = k0 + q * kPostT;
-                    if (k >= total) break;
-                    const int i = (int)(k / a.nx), j = (int)(k - (int64_t)i * a.nx);
-                    smem[i * pitch + j] = t[q];
-                }
-            }
-            __syncthreads();
-            if (tid < a.nx) spline_line_lds<16>(smem + tid, a.ny, pitch);  // axis 0: the columns
-            __syncthreads();
-            if (tid < a.ny) spline_line_lds<16>(smem + tid * pitch, a.nx, 1);  // axis 1: the rows
-            __syncthreads();
-            for (int64_t k = tid; k < total; k += kPostT) {
-                const int i = (int)(k / a.nx), j = (int)(k - (int64_t)i * a.nx);
-                base[k] = smem[i * pitch + j];
-            }
+        for (int q = 0; q < 6; ++q) P[11 + q] = sys[16 + q];
+        P[17] = (double)sflag;
+        double mn = ext[0][0], mx = ext[0][1];
+        for (int q = 1; q < kPostThreads / 64; ++q) {
+            mn = fmin(mn, ext[q][0]);
+            mx = fmax(mx, ext[q][1]);
         }
-        post_sync(a.sync, gen, a.clocks);  // 7
-        // ---- H: rotate_with_nan's interpolation (k_rotate_post's)
-        const RotArgs ra{a.coef, a.ny, a.nx, P[13], P[14], -P[14], P[13], P[15], P[16], a.rotated, a.opd};
-#pragma unroll
-        for (int q = 0; q < kPostPer; ++q) {
-            const int64_t k = gt + q * S;
-            if (k < total) rotate_pixel(ra, k);
-        }
-    }
-    // the last workgroup out leaves the counters at zero for the next launch
-    __syncthreads();
-    if (wg == 0 && tid == 0) a.clocks[15] = wall_clock64();
-    if (tid == 0) {
-        const unsigned d = __hip_atomic_fetch_add(&a.sync[1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        if (d == (unsigned)G - 1) {
-            __hip_atomic_store(&a.sync[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&a.sync[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&a.sync[4], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        P[18] = mn;
+        P[19] = mx;
+        a.clocks[4] = wall_clock64();
     }
 }
 
@@ -1107,9 +1121,8 @@ int akb_plane_subtract_f64(const double* z, int ny, int nx, const double* d_coef
     return launch_status("k_plane_subtract");
 }
 
-// the post's work: sync (4 doubles, first: at the same place for any map size) | phase clocks (16) |
-// partials (2 kPostG kPostPart) | buffer sums (8) | coef (2 ny nx)
-constexpr int64_t kPostHead = 4 + 16 + 2 * kPostG * kPostPart + 8;
+// the post's work: phase clocks (16 words) | coef (2 ny nx)
+constexpr int64_t kPostHead = 16;
 int64_t akb_pupil_post_work_bytes(int ny, int nx) {
     if (ny < 1 || nx < 1) return -1;
     return (kPostHead + 2 * (int64_t)ny * nx) * 8;
@@ -1120,25 +1133,29 @@ int akb_pupil_post_f64(const double* map, int ny, int nx, double sigma, double* 
     clear_error();
     AKB_REQUIRE(map && corrected && rotated && opd && work && d_params && ny > 1 && nx > 1, "bad arguments");
     AKB_REQUIRE((int64_t)ny * nx <= kPostMax, "the post handles maps of up to 65536 points");
+    hipStream_t s = (hipStream_t)stream;
     const int64_t total = (int64_t)ny * nx;
     double* const head = (double*)work;
     double* const w = head + kPostHead;  // coef
-    const int fuse = ny <= kPostFuse && nx <= kPostFuse;
-    PostArgs a{map, ny, nx, sigma, corrected, rotated, opd, w, head + 20, head + 20 + 2 * kPostG * kPostPart,
-               (unsigned*)head, (unsigned long long*)(head + 4), d_params, fuse};
-    k_pupil_post<<<kPostG, kPostT, 0, (hipStream_t)stream>>>(a);
+    PostArgs a{map, ny, nx, sigma, corrected, w, d_params, (unsigned long long*)head};
+    k_pupil_post<<<1, kPostThreads, 0, s>>>(a);
     int st = launch_status("k_pupil_post");
-    if (st || fuse) return st;
-    for (int axis = 0; axis < 2; ++axis) {
-        const int nlines = axis == 0 ? nx : ny, len = axis == 0 ? ny : nx;
-        if (len <= kSplineMaxLen)
-            k_spline_block<<<dim3((nlines + kSplineLines - 1) / kSplineLines, 2), kSplineThreads, 0,
-                             (hipStream_t)stream>>>(w, ny, nx, axis);
-        else
-            k_spline_lines<<<dim3((nlines + 63) / 64, 2), 64, 0, (hipStream_t)stream>>>(w, ny, nx, axis);
-        if ((st = launch_status("k_spline"))) return st;
+    if (st) return st;
+    if (ny <= kPostFuse && nx <= kPostFuse) {
+        k_spline_post<<<2, kSplinePostThreads, 0, s>>>(w, ny, nx);
+        if ((st = launch_status("k_spline_post"))) return st;
+    } else {
+        for (int axis = 0; axis < 2; ++axis) {
+            const int nlines = axis == 0 ? nx : ny, len = axis == 0 ? ny : nx;
+            if (len <= kSplineMaxLen)
+                k_spline_block<<<dim3((nlines + kSplineLines - 1) / kSplineLines, 2), kSplineThreads, 0, s>>>(w, ny, nx,
+                                                                                                            axis);
+            else
+                k_spline_lines<<<dim3((nlines + 63) / 64, 2), 64, 0, s>>>(w, ny, nx, axis);
+            if ((st = launch_status("k_spline"))) return st;
+        }
     }
-    k_rotate_post<<<grid_for(total, 4, 128), kBlock, 0, (hipStream_t)stream>>>(w, ny, nx, d_params, rotated, opd);
+    k_rotate_post<<<grid_for(total, 4, 128), kBlock, 0, s>>>(w, ny, nx, d_params, rotated, opd);
     return launch_status("k_rotate_post");
 }
 

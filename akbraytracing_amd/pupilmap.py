@@ -198,9 +198,8 @@ POST_PARAMS = 20  # akb_pupil_post_f64's parameter block (include/akb_raytrace.h
 
 
 def pupil_post(m, sigma_threshold=3, out=None, stream=None):
-    """The driver's chain from a gridded Wave2 map to compute_psf_fft's input in one device launch
-    (maps up to 128^2; larger ones add the prefilter and rotation launches), no host round trip
-    (akb_pupil_post_f64): matrixWave2 - nanmean -> plane correction ->
+    """The driver's chain from a gridded Wave2 map to compute_psf_fft's input on the device, no host
+    round trip (akb_pupil_post_f64: the one-workgroup post, the prefilter, the rotation): matrixWave2 - nanmean -> plane correction ->
     psf_calc's rotation estimate and rotate_with_nan (:3690-3700, :9630-9693, :1121-1188).
     m: (ny, nx) device map, ny * nx <= 65536. out: optional dict of preallocated buffers.
     Returns dict(corrected, rotated, opd, params) of device tensors; params[17] holds error flags
@@ -215,7 +214,7 @@ def pupil_post(m, sigma_threshold=3, out=None, stream=None):
             o[k] = torch.empty((ny, nx), dtype=D.F64, device=m.device)
     nw = int(L.akb_pupil_post_work_bytes(ny, nx)) // 8
     if "work" not in o or o["work"].numel() < nw:
-        o["work"] = torch.zeros(nw, dtype=D.F64, device=m.device)  # its barrier words start (and stay) zero
+        o["work"] = torch.empty(nw, dtype=D.F64, device=m.device)
     if "params" not in o:
         o["params"] = torch.empty(POST_PARAMS, dtype=D.F64, device=m.device)
     _lib.check(L.akb_pupil_post_f64(D.ptr(m), ny, nx, float(sigma_threshold), D.ptr(o["corrected"]),
@@ -228,8 +227,6 @@ def pupil_post_check(params):
     """Raise as the host chain would for a pupil_post parameter block (host copy or device tensor)."""
     p = params.cpu().numpy() if isinstance(params, torch.Tensor) else np.asarray(params)
     flags = int(p[17])
-    if flags & 4:
-        raise RuntimeError("pupil_post: a grid barrier of the post timed out (its workgroups were not co-resident)")
     if flags & 1:
         raise TypeError(f"Improper input: the plane fit needs more finite points (N={int(p[1])})")
     if flags & 2:

@@ -427,15 +427,14 @@ int akb_rotate_with_nan_f64(const double* m, int ny, int nx, const double rot[4]
  * on the device, no host round trip (AKB_raytrace_20250312.py:3690-3700, :9630-9693,
  * :1121-1188): corrected = plane_correction_with_nan_and_outlier_filter(map - nanmean(map), sigma),
  * psf_calc's rotation estimate, rotated = rotate_with_nan(corrected, degrees(rot), order 3)
- * (cephes cosdg / sindg for scipy.ndimage.rotate's matrix), opd = rotated * 1e-9. One launch of 32
- * workgroups separated by grid barriers (maps of up to 128 x 128: the B-spline prefilter and the
- * rotation included; larger maps add their launches). work: akb_pupil_post_work_bytes(ny, nx),
- * zero-filled before its first use (the launch leaves its barrier words zero). d_params (20
- * doubles): nanmean, finite count, the quadratic fit (5), the plane (3), the outlier threshold,
- * rot, its degrees, cos, sin, the rotation's offset (2), error flags (bit 0: too few points for
- * curve_fit, bit 1: a singular normal system, bit 2: a grid barrier timed out), nanmin and nanmax
- * of the input map. Replaces pupilmap._plane_corrections + psfcalc.rotation_estimate /
- * rotate_with_nan where a pipelined caller cannot wait on the host. */
+ * (cephes cosdg / sindg for scipy.ndimage.rotate's matrix), opd = rotated * 1e-9. Three launches:
+ * the one-workgroup post, the B-spline prefilter (maps up to 128 x 128: one workgroup per array,
+ * both axes in LDS), the rotation. work: akb_pupil_post_work_bytes(ny, nx). d_params (20 doubles):
+ * nanmean, finite count, the quadratic fit (5), the plane (3), the outlier threshold, rot, its
+ * degrees, cos, sin, the rotation's offset (2), error flags (bit 0: too few points for curve_fit,
+ * bit 1: a singular normal system), nanmin and nanmax of the input map. Replaces
+ * pupilmap._plane_corrections + psfcalc.rotation_estimate / rotate_with_nan where a pipelined
+ * caller cannot wait on the host. */
 int64_t akb_pupil_post_work_bytes(int ny, int nx);
 int akb_pupil_post_f64(const double* map, int ny, int nx, double sigma, double* corrected, double* rotated,
                        double* opd, void* work, double* d_params, void* stream);
