@@ -253,6 +253,8 @@ constexpr int kCellTile = 16;
 
 // ------------------------------------------------------------------ targets
 
+constexpr int kClaimAxisLds = 512;  // target axes up to this long go to LDS in the claim kernels
+
 struct Targets {
     const double* gx;  // (mx,) target x axis (grid_H row), ascending
     const double* gy;  // (my,) target y axis (grid_V column), ascending
@@ -487,6 +489,15 @@ __global__ void __launch_bounds__(kCellTile * kCellTile) k_gd_cells_tiled(Grid g
     bool uniform = false;
     double inv_dx = 0.0, inv_dy = 0.0;
     if constexpr (kClaims) {
+        // the target axes in LDS when they fit: every tile's candidate range and tests read them
+        __shared__ double sax[2 * kClaimAxisLds];
+        if (tc.t.mx <= kClaimAxisLds && tc.t.my <= kClaimAxisLds) {
+            for (int i = threadIdx.x; i < tc.t.mx; i += blockDim.x) sax[i] = tc.t.gx[i];
+            for (int i = threadIdx.x; i < tc.t.my; i += blockDim.x) sax[kClaimAxisLds + i] = tc.t.gy[i];
+            __syncthreads();
+            tc.t.gx = sax;
+            tc.t.gy = sax + kClaimAxisLds;
+        }
         uniform = axes_uniform(tc.t);
         inv_dx = inv_step(tc.t.gx, tc.t.mx);
         inv_dy = inv_step(tc.t.gy, tc.t.my);
@@ -1245,7 +1256,6 @@ k_gd_sweeps(Grid g, SweepArgs<NV> a) {
 // Both use the gradient arithmetic above, so every target vertex holds the global iteration's
 // K-sweep value bit for bit (tests/test_gpu_parity.py::test_gradient_cone_equals_global_sweeps).
 
-constexpr int kClaimAxisLds = 512;                // target axes up to this long go to LDS in k_gd_claim_hit
 constexpr int kConeMaxK = 14;                    // patch box side 2K + 4 <= 32
 constexpr int kConeBox = 2 * kConeMaxK + 4;  // the largest box side: it fits the patches' LDS pitch
 
