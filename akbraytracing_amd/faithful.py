@@ -9,11 +9,11 @@ plot_result_debug's 'ray_wave' step after the trace (AKB_raytrace_20250312.py:36
 
 FaithfulPupil runs it for run after run without a host wait on the queuing thread:
 
-  begin(y, z)   on the caller's stream: the boundary ring (akb_gd_ring_f64) to pinned host memory,
-                the target axes from it (akb_gd_axes_f64), then the cell diagonals and checks with
-                the cells' target claims fused in (akb_gd_cells_claims_f64); a worker thread builds
-                the hull pockets from the ring meanwhile (akb_gd_pockets, host C++ - the only host
-                step, off the GIL) and checks the cell flags;
+  begin(y, z)   on the caller's stream: the boundary ring (akb_gd_ring_f64), the target axes from
+                it (akb_gd_axes_f64), the cell diagonals and checks with the cells' target claims
+                fused in (akb_gd_cells_claims_f64), the ring and the cell flags to pinned host memory
+                in one copy; a worker thread then checks the flags and builds the hull pockets
+                (akb_gd_pockets, host C++ - the only host step, off the GIL);
   finish(t, f)  once that ticket's pockets are built: the pocket arrays to the device, their
                 local-Delaunay check and target claims (akb_gd_claim_pockets_f64), griddata by the
                 cone solve (akb_gd_cone_solve_f64: CONE_SWEEPS Chebyshev sweeps formed only where
@@ -211,27 +211,24 @@ class FaithfulPupil:
             flags.zero_()
             _lib.check(L.akb_gd_ring_f64(D.ptr(y), D.ptr(z), self.nv, self.nh, D.ptr(ring[:Lr]), D.ptr(ring[Lr:2 * Lr]),
                                          D.ptr(flags), sh))
-            s["ring_host"][:2 * Lr].copy_(ring[:2 * Lr], non_blocking=True)
-            ev_ring = torch.cuda.Event()
-            ev_ring.record(st)
             _lib.check(L.akb_gd_axes_f64(D.ptr(ring[:Lr]), D.ptr(ring[Lr:2 * Lr]), Lr, m, m, D.ptr(gx), D.ptr(gy),
                                          D.ptr(s["axes"][2 * m:]), sh))
             _lib.check(L.akb_gd_cells_claims_f64(D.ptr(y), D.ptr(z), self.nv, self.nh, D.ptr(s["diag"]), self.tol,
                                                  D.ptr(flags), D.ptr(gx), m, D.ptr(gy), m, D.ptr(s["owner"]), sh))
-            s["ring_host"][2 * Lr:].copy_(ring[2 * Lr:], non_blocking=True)
+            s["ring_host"].copy_(ring, non_blocking=True)  # the ring and the cell flags, one copy
             ev = torch.cuda.Event()
             ev.record(st)
         t = Ticket()
         t.slot, t.y, t.z, t.f = s, y, z, f
         t.npock, t.result, t.h2d, t.finished, t.done, t.log, t.erow = None, None, None, False, None, self.errors, None
-        t.job = self.pool.submit(self._pockets, s, ev_ring, ev)
+        t.job = self.pool.submit(self._pockets, s, ev)
         s["last"] = t
         return t
 
-    def _pockets(self, s, ev_ring, ev):
-        """Worker thread: wait for the ring on the host and build the pockets (while the cell pass
-        runs), then check the cell flags - their errors first, as the host chain raises them."""
-        ev_ring.synchronize()
+    def _pockets(self, s, ev):
+        """Worker thread: wait for the ring and the cell flags on the host, build the pockets, check
+        the flags - their errors first, as the host chain raises them."""
+        ev.synchronize()
         L = _lib.lib()
         Lr = self.L
         rb = s["ring_host"].numpy()
@@ -247,7 +244,6 @@ class FaithfulPupil:
                 npk, s["po"] = pack_pockets(buf, o, Lr)
             except _lib.AKBError as e:
                 err = e
-        ev.synchronize()
         fl = int(rb[2 * Lr:].view(np.int32)[0])
         if fl & _F_NONFINITE:
             raise ValueError("griddata: non-finite point coordinates (a ray that missed)")
