@@ -1519,6 +1519,8 @@ struct ConePatch {
     double* gout;              // x_K (n, 2): the cells' four corners are written
     unsigned long long* chg;   // largest change measure of one more sweep at the corners (or nullptr)
     unsigned long long* est;   // largest value-error estimate of a cell (or nullptr; see below)
+    unsigned long long* clk;   // diagnostics (or nullptr): workgroup 0's wall clock in its steps' phases -
+                               // setup, sweeps, the rest - summed, and its step count
 };
 
 // vertex `idx` of the box in order of depth from the centre outwards: (r, c) and its depth d =
@@ -1618,8 +1620,15 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch(Grid g, ConePatch a, int
     // at the end
     double cmax = 0.0, emax = 0.0;
     constexpr int off[8] = {-1, 1, -P, P, -P - 1, -P + 1, P - 1, P + 1};
+    const bool clk = a.clk && blockIdx.x == 0 && __builtin_amdgcn_readfirstlane(t >> 6) == 0;  // wave 0 (scalar)
+    unsigned long long c_setup = 0, c_sweeps = 0, c_rest = 0, c0 = clk ? wall_clock64() : 0, c1 = 0;
     for (int p = 0; p <= my; ++p) {
         const int s1 = p % 3, s2 = (p + 2) % 3;  // box sets of cell p (stage 1) and cell p - 1 (stage 2)
+        if (clk && p > 0) {  // the previous step's corners and next box writes
+            const unsigned long long now = wall_clock64();
+            c_rest += now - c0;
+            c0 = now;
+        }
         if (p < my && lr < W && lc < W) sd[s1][lr * P + lc] = pd;
         // cell p's box came through registers to LDS last step: an LDS-only barrier, so no wave waits
         // here for the acks of its earlier global stores (__syncthreads' fence would)
@@ -1679,6 +1688,10 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch(Grid g, ConePatch a, int
         }
         // x_0 in place for sweep 1
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (clk) {
+            c1 = wall_clock64();
+            c_setup += c1 - c0;
+        }
         // S of one sweep from iterate buffer `in` (sweep 1 reads x_0 = 0 from buffer 0, zeroed at the
         // step's top) and the Jacobi step's y; the buffer's row base is formed once per sweep, so each
         // slot's read is one LDS instruction with a constant offset
@@ -1706,6 +1719,10 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch(Grid g, ConePatch a, int
                 gg[out][b] = make_double2(cheb(st, y0, pv.x), cheb(st, y1, pv.y));
             }
             asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+        if (clk) {
+            c0 = wall_clock64();
+            c_sweeps += c0 - c1;
         }
         // cell p - 1's corners (stage 2's innermost ring): x_K, the change of one more plain sweep and
         // the value-error estimate, into LDS; the last wave stores them after the next step's
@@ -1753,6 +1770,12 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch(Grid g, ConePatch a, int
     if (t >= 1020) {
         if (a.chg && cmax > 0) atomicMax(a.chg, (unsigned long long)__double_as_longlong(cmax));
         if (a.est && emax > 0) atomicMax(a.est, (unsigned long long)__double_as_longlong(emax));
+    }
+    if (clk && t == 0) {
+        a.clk[0] += c_setup;
+        a.clk[1] += c_sweeps;
+        a.clk[2] += c_rest;
+        a.clk[3] += (unsigned long long)(my + 1);
     }
 }
 
@@ -2336,6 +2359,7 @@ struct PatchTimer {
     hipEvent_t ev[kPatchEvents][2];
     const int* cnt[kPatchEvents];
     int64_t launches = 0;
+    unsigned long long* clk = nullptr;  // device: workgroup 0's phase clocks, summed over the launches
 };
 PatchTimer& patch_timer() {
     static PatchTimer t;
@@ -2569,7 +2593,8 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
             }
         }
         const BandEst be{band_on && d_change ? gb[(K + 1) % 3] : nullptr, K, d_change, d_change ? d_change + 1 : nullptr};
-        ConePatch a{fv, cells, count, K, {}, gb[K % 3], d_change, d_change ? d_change + 1 : nullptr};
+        ConePatch a{fv, cells, count, K, {}, gb[K % 3], d_change, d_change ? d_change + 1 : nullptr,
+                    patch_timer().on ? patch_timer().clk : nullptr};
         for (int j = 0; j <= K; ++j) a.st[j] = steps[j];
         PatchTimer& pt = patch_timer();
         const int slot = (int)(pt.launches % kPatchEvents);
@@ -2737,10 +2762,25 @@ int akb_gd_patch_timing(int enable) {
     if (enable && !t.made) {
         for (int k = 0; k < kPatchEvents; ++k)
             for (int q = 0; q < 2; ++q) AKB_HIP_CHECK(hipEventCreate(&t.ev[k][q]));
+        AKB_HIP_CHECK(hipMalloc((void**)&t.clk, 4 * sizeof(unsigned long long)));
         t.made = true;
     }
+    if (enable) AKB_HIP_CHECK(hipMemset(t.clk, 0, 4 * sizeof(unsigned long long)));
     t.on = enable != 0;
     t.launches = 0;
+    return 0;
+}
+
+int akb_gd_patch_phases(unsigned long long* out) {
+    clear_error();
+    PatchTimer& t = patch_timer();
+    AKB_REQUIRE(out, "null pointer");
+    if (!t.made) {
+        for (int k = 0; k < 4; ++k) out[k] = 0;
+        return 0;
+    }
+    AKB_HIP_CHECK(hipDeviceSynchronize());
+    AKB_HIP_CHECK(hipMemcpy(out, t.clk, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     return 0;
 }
 
