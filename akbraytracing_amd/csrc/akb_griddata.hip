@@ -506,7 +506,7 @@ __global__ void __launch_bounds__(kCellTile * kCellTile) k_gd_cells_tiled(Grid g
     // one is checked (its loads then wait behind no other work)
     constexpr int NL = (V * V + T * T - 1) / (T * T);
     auto load_tile = [&](int64_t tile, double (&px)[NL], double (&py)[NL]) {
-        const int tv = (int)(tile / tiles_h), th = (int)(tile - (int64_t)tv * tiles_h);
+        const int tv = (int)tile / tiles_h, th = (int)tile - tv * tiles_h;  // (32-bit: a 64-bit division costs ~100 instructions)
         const int iv0 = r_lo + tv * T, ih0 = th * T;
 #pragma unroll
         for (int u = 0; u < NL; ++u) {
@@ -524,7 +524,7 @@ __global__ void __launch_bounds__(kCellTile * kCellTile) k_gd_cells_tiled(Grid g
     double px[NL], py[NL];
     if ((int64_t)blockIdx.x < ntiles) load_tile(blockIdx.x, px, py);
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int tv = (int)(tile / tiles_h), th = (int)(tile - (int64_t)tv * tiles_h);
+        const int tv = (int)tile / tiles_h, th = (int)tile - tv * tiles_h;  // (32-bit: a 64-bit division costs ~100 instructions)
         const int iv0 = r_lo + tv * T, ih0 = th * T;
         __syncthreads();
 #pragma unroll
