@@ -433,14 +433,35 @@ struct PostArgs {
     unsigned long long* clocks;  // work: the wall clock (100 MHz) at the phase ends (diagnostics)
 };
 
-// fixed-order workgroup sum of q values per thread (wave shuffles, then the waves in order)
+// one DPP step of a wave reduction on a double: v + (v moved by the DPP control), rows outside
+// row_mask adding zero
+template <int kCtrl, int kRowMask = 0xf>
+__device__ __forceinline__ double dpp_add(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffLL), kCtrl, kRowMask, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), kCtrl, kRowMask, 0xf, false);
+    return v + __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+
+// the wave's sum in lane 63 (pairs, quads, rows of 16 by rotation, then the rows by broadcast: DPP
+// moves, no LDS traffic; a fixed order, so the same bits every time)
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+    v = dpp_add<0xb1>(v);        // quad_perm [1, 0, 3, 2]
+    v = dpp_add<0x4e>(v);        // quad_perm [2, 3, 0, 1]
+    v = dpp_add<0x124>(v);       // row_ror:4
+    v = dpp_add<0x128>(v);       // row_ror:8
+    v = dpp_add<0x142, 0xa>(v);  // row_bcast:15 into rows 1 and 3
+    v = dpp_add<0x143, 0xc>(v);  // row_bcast:31 into rows 2 and 3
+    return v;
+}
+
+// fixed-order workgroup sum of q values per thread (DPP within the waves, then the waves in order)
 template <int Q>
 __device__ __forceinline__ void block_sum(double (&acc)[Q], double (*red)[Q]) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
-    for (int q = 0; q < Q; ++q)
-        for (int off = 32; off > 0; off >>= 1) acc[q] += __shfl_down(acc[q], off);
-    if (lane == 0)
+    for (int q = 0; q < Q; ++q) acc[q] = wave_sum_dpp(acc[q]);
+    if (lane == 63)
 #pragma unroll
         for (int q = 0; q < Q; ++q) red[w][q] = acc[q];
     __syncthreads();
@@ -601,6 +622,18 @@ __global__ void __launch_bounds__(kSplineThreads) k_spline_block(double* __restr
 // up the segments); the anti-causal pass c[i] = z (c[i+1] - c[i]) likewise downwards. The same
 // recursions as spline_line, a different rounding order (~1e-16 relative; |z| = 0.27), a P-th of
 // the sequential steps.
+// z^k by binary powering (k >= 0): ~2 log2(k) multiplications, where the libm pow of a double
+// costs hundreds of instructions (a few ulp from pow: within spline_line_par's rounding)
+__device__ __forceinline__ double zpow(double z, int k) {
+    double r = 1.0, b = z;
+    while (k > 0) {
+        if (k & 1) r *= b;
+        b *= b;
+        k >>= 1;
+    }
+    return r;
+}
+
 template <int P>
 __device__ void spline_line_par(double* c, int n, int s, int sub) {
     const double z = sqrt(3.0) - 2.0;
@@ -611,11 +644,11 @@ __device__ void spline_line_par(double* c, int n, int s, int sub) {
     for (int i = b0; i < b1; ++i) c[i * s] = c[i * s] * gain;
     if (n == 1) return;
     wave_sync();
-    const double zn1 = pow(z, (double)(n - 1));
+    const double zn1 = zpow(z, n - 1);
     double part = 0.0;
     {
         const int i0 = max(b0, 1), i1 = min(b1, n - 1);
-        double zi = i0 < i1 ? pow(z, (double)i0) : 0.0;
+        double zi = i0 < i1 ? zpow(z, i0) : 0.0;
         for (int i = i0; i < i1; ++i) {
             part += zi * (c[i * s] + zn1 * c[(n - 1 - i) * s]);
             zi *= z;
@@ -625,7 +658,7 @@ __device__ void spline_line_par(double* c, int n, int s, int sub) {
 #pragma unroll
     for (int k = 0; k < P; ++k) tot += __shfl(part, base + k);
     const double y0 = (c[0] + zn1 * c[(n - 1) * s] + tot) / (1.0 - zn1 * zn1);
-    const double zl = pow(z, (double)(b1 - b0));  // z^(segment length), 1 for an empty segment
+    const double zl = zpow(z, b1 - b0);  // z^(segment length), 1 for an empty segment
     wave_sync();
     // causal
     double u = 0.0;
@@ -845,7 +878,23 @@ __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
                 acc[20] += 1.0;
             }
         }
-        block_sum<kMomMax>(acc, red);
+        // only the slots the mode fills: 2 (the residual passes), 10 (the plane's 3 x 3), 21
+        if (mode > 0) {
+            double t[2] = {acc[0], acc[20]};
+            block_sum<2>(t, (double(*)[2])red);
+            acc[0] = t[0];
+            acc[20] = t[1];
+        } else if (nb == 3) {
+            constexpr int slot[10] = {0, 1, 2, 5, 6, 9, 15, 16, 17, 20};
+            double t[10];
+#pragma unroll
+            for (int q = 0; q < 10; ++q) t[q] = acc[slot[q]];
+            block_sum<10>(t, (double(*)[10])red);
+#pragma unroll
+            for (int q = 0; q < 10; ++q) acc[slot[q]] = t[q];
+        } else {
+            block_sum<kMomMax>(acc, red);
+        }
     };
     // the normal equations of nb terms from the moment slots (pupilmap._normal_solve) into sys[25..]
     auto normal_solve = [&](const double (&mom)[kMomMax], auto nbc, int at) {
