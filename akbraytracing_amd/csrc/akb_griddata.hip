@@ -2765,9 +2765,11 @@ int akb_gd_patch_timing(int enable) {
         AKB_HIP_CHECK(hipMalloc((void**)&t.clk, 4 * sizeof(unsigned long long)));
         t.made = true;
     }
-    if (enable) AKB_HIP_CHECK(hipMemset(t.clk, 0, 4 * sizeof(unsigned long long)));
+    if (enable) {  // a new record (stopping keeps the last one for akb_gd_patch_times / _phases)
+        AKB_HIP_CHECK(hipMemset(t.clk, 0, 4 * sizeof(unsigned long long)));
+        t.launches = 0;
+    }
     t.on = enable != 0;
-    t.launches = 0;
     return 0;
 }
 

@@ -535,7 +535,7 @@ int akb_gd_eval_f64(const double* x, const double* y, int nv, int nh, const uint
 int64_t akb_gd_cone_work_bytes(int nv, int nh, int mx, int my, int nvals);
 /* Diagnostics of the cone solve's patch kernel (k_gd_cone_patch), for bench.py's roofline:
  * akb_gd_patch_timing(1) records HIP events around every patch launch from then on (the last 1024
- * launches kept; 0 stops, either resets the count); akb_gd_patch_times waits for them and writes up
+ * launches kept; 0 stops and keeps the record, 1 starts a new one); akb_gd_patch_times waits for them and writes up
  * to max launch durations (ms, oldest first) and, when cells != NULL, each launch's interior target
  * cell count; returns how many (or a negative AKB error code). */
 int akb_gd_patch_timing(int enable);
