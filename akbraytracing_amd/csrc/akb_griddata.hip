@@ -1262,7 +1262,7 @@ constexpr int kConeBox = 2 * kConeMaxK + 4;  // the largest box side: it fits th
 // the boundary band: vertices with min(iv, ih, nv - 1 - iv, nh - 1 - ih) <= D, as four regions -
 // the top rows [0, rt), the bottom rows [rb, nv), and between them the left columns [0, cl) and the
 // right columns [cr, nh) - cut into kBandTR x kBandTC tiles (every band vertex in one tile)
-constexpr int kBandTR = 16, kBandTC = 32;
+constexpr int kBandTR = 32, kBandTC = 32;  // (the depth <= 26 band: one tile deep)
 struct BandTiles {
     int D, rt, rb, cl, cr;
     int ncb, top_rb, bot_rb, mid_rb, lcb, rcb;  // column blocks (top / bottom), row blocks, side column blocks
@@ -1373,15 +1373,18 @@ __device__ __forceinline__ void band_grid_sums(const Grid& g, const ConeBand& a,
     band_edges(A, xi, yi, fi, xs, ys, fs, gxs, gys, on);
 }
 
-// the solve of one band / ring vertex of sweep j, stored to x_j
-__device__ __forceinline__ void band_solve(const ConeBand& a, int64_t i, const GradAcc<1>& A) {
+// the solve of one band / ring vertex of sweep j, stored to x_j (px, py: x_{j-2} there, mode 2)
+__device__ __forceinline__ void band_solve(const ConeBand& a, int64_t i, const GradAcc<1>& A, double px, double py) {
     const VConst k = vertex_consts<1>(A, 0);
     double y0, y1;
     jacobi_y(k, A.s0[0], A.s1[0], y0, y1);
     const int64_t o = 2 * i;
-    const double px = a.st.mode == 2 ? a.gprev[o] : 0.0, py = a.st.mode == 2 ? a.gprev[o + 1] : 0.0;
     a.gout[o] = cheb(a.st, y0, px);
     a.gout[o + 1] = cheb(a.st, y1, py);
+}
+__device__ __forceinline__ void band_solve(const ConeBand& a, int64_t i, const GradAcc<1>& A) {
+    const int64_t o = 2 * i;
+    band_solve(a, i, A, a.st.mode == 2 ? a.gprev[o] : 0.0, a.st.mode == 2 ? a.gprev[o + 1] : 0.0);
 }
 
 // ring vertex r of a band sweep over a group of W lanes (sub: the lane in it): the pocket chords
@@ -1410,8 +1413,9 @@ __device__ __forceinline__ void cone_ring_vertex(const Grid& g, const ConeBand& 
 // ring's dependent chord loads overlap the tiles - the rest a band tile each - its vertices
 // and their neighbours' x, y, f and x_{j-1} (and the cells' diagonals) staged in LDS by coalesced
 // row loads, then one thread per vertex off the ring (band_edges from LDS: the gather kernel's
-// arithmetic). Both halves read x_{j-1} / x_{j-2} only.
-constexpr int kBandThreads = kBandTR * kBandTC;
+// arithmetic, two vertices a thread, x_{j-2} loaded with the tile). Both halves read x_{j-1} /
+// x_{j-2} only.
+constexpr int kBandThreads = 512, kBandVR = kBandTR * kBandTC / kBandThreads;
 __global__ void __launch_bounds__(kBandThreads) k_gd_cone_band(Grid g, BandTiles bt, ConeBand a, int nr8) {
     if (!*a.needed) return;
     if ((int)blockIdx.x >= nr8) {
@@ -1463,34 +1467,50 @@ __global__ void __launch_bounds__(kBandThreads) k_gd_cone_band(Grid g, BandTiles
             const int k = threadIdx.x + u * kBandThreads;
             if (k < (kBandTR + 1) * CC) sdg[k] = ld[u];
         }
-        __syncthreads();
-        const int tr = threadIdx.x / kBandTC, tc = threadIdx.x - (threadIdx.x / kBandTC) * kBandTC;
-        const int iv = r0 + tr, ih = c0 + tc;
-        if (iv >= r1 || ih >= c1 || ring_pos(g, iv, ih) >= 0) return;
-        const bool L = ih > 0, R = ih < g.nh - 1, D = iv > 0, U = iv < g.nv - 1;
-        const int li = (tr + 1) * HC + (tc + 1);
-        const int jn[8] = {li - 1, li + 1, li - HC, li + HC, li - HC - 1, li - HC + 1, li + HC - 1, li + HC + 1};
-        const bool inb[8] = {L, R, D, U, D && L, D && R, U && L, U && R};
-        const int lc = tr * CC + tc;  // cell (iv - 1, ih - 1)
-        const int dc[4] = {lc, lc + 1, lc + CC, lc + CC + 1};
-        uint8_t dg[4];
+        // this thread's vertices: rows tr and tr + TR / 2 of the tile; their x_{j-2} before the barrier
+        const int tr0 = threadIdx.x / kBandTC, tc = threadIdx.x - (threadIdx.x / kBandTC) * kBandTC;
+        double ppx[kBandVR], ppy[kBandVR];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) dg[k] = inb[4 + k] ? sdg[dc[k]] : 0;
-        double xs[8], ys[8], fs[8], gxs[8], gys[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int j = inb[k] ? jn[k] : li;
-            xs[k] = sx[j];
-            ys[k] = sy[j];
-            fs[k] = sf[j];
-            gxs[k] = sgx[j];
-            gys[k] = sgy[j];
+        for (int u = 0; u < kBandVR; ++u) {
+            const int iv = r0 + tr0 + u * (kBandTR / kBandVR), ih = c0 + tc;
+            ppx[u] = ppy[u] = 0.0;
+            if (a.st.mode == 2 && iv < r1 && ih < c1) {
+                const int64_t o = 2 * ((int64_t)iv * g.nh + ih);
+                ppx[u] = a.gprev[o];
+                ppy[u] = a.gprev[o + 1];
+            }
         }
-        const bool on[8] = {L, R, D, U, inb[4] && dg[0] == 0, inb[5] && dg[1] == 1, inb[6] && dg[2] == 1,
-                            inb[7] && dg[3] == 0};
-        GradAcc<1> A;
-        band_edges(A, sx[li], sy[li], sf[li], xs, ys, fs, gxs, gys, on);
-        band_solve(a, (int64_t)iv * g.nh + ih, A);
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < kBandVR; ++u) {
+            const int tr = tr0 + u * (kBandTR / kBandVR);
+            const int iv = r0 + tr, ih = c0 + tc;
+            if (iv >= r1 || ih >= c1 || ring_pos(g, iv, ih) >= 0) continue;
+            const bool L = ih > 0, R = ih < g.nh - 1, D = iv > 0, U = iv < g.nv - 1;
+            const int li = (tr + 1) * HC + (tc + 1);
+            const int jn[8] = {li - 1, li + 1, li - HC, li + HC, li - HC - 1, li - HC + 1, li + HC - 1, li + HC + 1};
+            const bool inb[8] = {L, R, D, U, D && L, D && R, U && L, U && R};
+            const int lc = tr * CC + tc;  // cell (iv - 1, ih - 1)
+            const int dc[4] = {lc, lc + 1, lc + CC, lc + CC + 1};
+            uint8_t dg[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) dg[k] = inb[4 + k] ? sdg[dc[k]] : 0;
+            double xs[8], ys[8], fs[8], gxs[8], gys[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int j = inb[k] ? jn[k] : li;
+                xs[k] = sx[j];
+                ys[k] = sy[j];
+                fs[k] = sf[j];
+                gxs[k] = sgx[j];
+                gys[k] = sgy[j];
+            }
+            const bool on[8] = {L, R, D, U, inb[4] && dg[0] == 0, inb[5] && dg[1] == 1, inb[6] && dg[2] == 1,
+                                inb[7] && dg[3] == 0};
+            GradAcc<1> A;
+            band_edges(A, sx[li], sy[li], sf[li], xs, ys, fs, gxs, gys, on);
+            band_solve(a, (int64_t)iv * g.nh + ih, A, ppx[u], ppy[u]);
+        }
         return;
     }
     const int64_t L = 2 * (int64_t)(g.nh - 1) + 2 * (int64_t)(g.nv - 1);
