@@ -616,15 +616,13 @@ __global__ void __launch_bounds__(kSplineThreads) k_spline_block(double* __restr
 }
 
 // spline_filter1d's recursions on a line in LDS (stride s) split over P consecutive lanes of a wave
-// (sub: the lane's segment of ceil(n / P) points): the gain; the mirror-symmetric initial sum as
-// per-segment parts added in segment order; the causal pass c[i] += z c[i-1] run per segment from
-// zero and corrected by z^(i - b0 + 1) times the true value before the segment (the carries passed
-// up the segments); the anti-causal pass c[i] = z (c[i+1] - c[i]) likewise downwards. The same
-// recursions as spline_line, a different rounding order (~1e-16 relative; |z| = 0.27), a P-th of
-// the sequential steps.
-// z^k by binary powering (k >= 0): ~2 log2(k) multiplications, where the libm pow of a double
-// costs hundreds of instructions (a few ulp from pow: within spline_line_par's rounding)
-__device__ __forceinline__ double zpow(double z, int k) {
+// (sub: the lane's segment of ceil(n / P) <= SEG points, held in registers: one batch of LDS reads,
+// one of writes): the gain; the mirror-symmetric initial sum as per-segment parts added in segment
+// order; the causal pass c[i] += z c[i-1] run per segment from zero and corrected by z^(i - b0 + 1)
+// times the true value before the segment (the carries passed up the segments); the anti-causal
+// pass c[i] = z (c[i+1] - c[i]) likewise downwards. The same recursions as spline_line, a different
+// rounding order (~1e-16 relative; |z| = 0.27), a P-th of the sequential steps.
+__device__ __forceinline__ double zpow(double z, int k) {  // z^k by binary powering (k >= 0)
     double r = 1.0, b = z;
     while (k > 0) {
         if (k & 1) r *= b;
@@ -634,98 +632,121 @@ __device__ __forceinline__ double zpow(double z, int k) {
     return r;
 }
 
-template <int P>
-__device__ void spline_line_par(double* c, int n, int s, int sub) {
+template <int P, int SEG>
+__device__ void spline_line_reg(double* c, int n, int s, int sub) {
     const double z = sqrt(3.0) - 2.0;
     const double gain = (1.0 - z) * (1.0 - 1.0 / z);
     const int lane = threadIdx.x & 63, base = lane & ~(P - 1);
     const int seg = (n + P - 1) / P;
-    const int b0 = min(n, sub * seg), b1 = min(n, b0 + seg);
-    for (int i = b0; i < b1; ++i) c[i * s] = c[i * s] * gain;
-    if (n == 1) return;
-    wave_sync();
-    const double zn1 = zpow(z, n - 1);
-    double part = 0.0;
-    {
-        const int i0 = max(b0, 1), i1 = min(b1, n - 1);
-        double zi = i0 < i1 ? zpow(z, i0) : 0.0;
-        for (int i = i0; i < i1; ++i) {
-            part += zi * (c[i * s] + zn1 * c[(n - 1 - i) * s]);
-            zi *= z;
-        }
-    }
-    double tot = 0.0;
+    const int b0 = min(n, sub * seg), len = min(n, b0 + seg) - b0;
+    double v[SEG];
 #pragma unroll
-    for (int k = 0; k < P; ++k) tot += __shfl(part, base + k);
-    const double y0 = (c[0] + zn1 * c[(n - 1) * s] + tot) / (1.0 - zn1 * zn1);
-    const double zl = zpow(z, b1 - b0);  // z^(segment length), 1 for an empty segment
-    wave_sync();
-    // causal
-    double u = 0.0;
-    if (b0 < b1) {
-        u = b0 == 0 ? y0 : c[b0 * s];
-        c[b0 * s] = u;
-        for (int i = b0 + 1; i < b1; ++i) {
-            u = c[i * s] + z * u;
-            c[i * s] = u;
-        }
-    }
-    double ein = 0.0;  // the true value at b0 - 1
-    {
-        double e = 0.0;
+    for (int k = 0; k < SEG; ++k) v[k] = k < len ? c[(b0 + k) * s] * gain : 0.0;
+    // the gained values at 0, n - 2 and n - 1 (their owners' registers, summed over the group: the
+    // others add zeros)
+    auto at = [&](int idx) {
+        double own = 0.0;
 #pragma unroll
-        for (int k = 0; k < P; ++k) {
-            const double uk = __shfl(u, base + k), zk = __shfl(zl, base + k);
-            if (k == sub) ein = e;
-            e = uk + zk * e;
-        }
-    }
-    if (ein != 0.0) {
-        double zk = z;
-        for (int i = b0; i < b1; ++i) {
-            c[i * s] = c[i * s] + zk * ein;
-            zk *= z;
-        }
-    }
-    wave_sync();
-    // anti-causal
-    const double next = (z * c[(n - 2) * s] + c[(n - 1) * s]) * z / (z * z - 1.0);
-    wave_sync();
-    double v = 0.0;
-    if (b0 < b1) {
-        int i = b1 - 1;
-        if (b1 == n) {
-            v = next;
-            c[i * s] = v;
-            --i;
-        }
-        for (; i >= b0; --i) {
-            v = z * (v - c[i * s]);
-            c[i * s] = v;
-        }
-    }
-    double bin = 0.0;  // the true value at b1
-    {
-        double e = 0.0;
+        for (int k = 0; k < SEG; ++k)
+            if (k < len && b0 + k == idx) own = v[k];
+        double t = 0.0;
 #pragma unroll
-        for (int k = P - 1; k >= 0; --k) {
-            const double vk = __shfl(v, base + k), zk = __shfl(zl, base + k);
-            if (k == sub) bin = e;
-            e = vk + zk * e;
+        for (int q = 0; q < P; ++q) t += __shfl(own, base + q);
+        return t;
+    };
+    if (n > 1) {
+        const double zn1 = zpow(z, n - 1);
+        // the mirror-symmetric initial sum: c0 = c[0] + zn1 c[n-1] + sum_{i=1}^{n-2} z^i (c[i] + zn1 c[n-1-i])
+        double part = 0.0;
+        {
+            double zi = zpow(z, b0);
+#pragma unroll
+            for (int k0 = 0; k0 < SEG; k0 += 8) {  // the mirror values eight reads at a time
+                double mir[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const int i = b0 + k0 + k;
+                    mir[k] = (k0 + k < len && i >= 1 && i <= n - 2) ? c[(n - 1 - i) * s] * gain : 0.0;
+                }
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const int i = b0 + k0 + k;
+                    if (k0 + k < len && i >= 1 && i <= n - 2) part += zi * (v[k0 + k] + zn1 * mir[k]);
+                    zi *= z;
+                }
+            }
+        }
+        double tot = 0.0;
+#pragma unroll
+        for (int q = 0; q < P; ++q) tot += __shfl(part, base + q);
+        const double y0 = (at(0) + zn1 * at(n - 1) + tot) / (1.0 - zn1 * zn1);
+        const double zl = zpow(z, len);  // z^(segment length), 1 for an empty segment
+        // causal
+        double u = 0.0;
+#pragma unroll
+        for (int k = 0; k < SEG; ++k)
+            if (k < len) {
+                u = k == 0 ? (b0 == 0 ? y0 : v[0]) : v[k] + z * u;
+                v[k] = u;
+            }
+        double ein = 0.0;  // the true value at b0 - 1
+        {
+            double e = 0.0;
+#pragma unroll
+            for (int q = 0; q < P; ++q) {
+                const double uq = __shfl(u, base + q), zq = __shfl(zl, base + q);
+                if (q == sub) ein = e;
+                e = uq + zq * e;
+            }
+        }
+        {
+            double zk = z;
+#pragma unroll
+            for (int k = 0; k < SEG; ++k)
+                if (k < len) {
+                    v[k] = v[k] + zk * ein;
+                    zk *= z;
+                }
+        }
+        // anti-causal
+        const double next = (z * at(n - 2) + at(n - 1)) * z / (z * z - 1.0);
+        double w = 0.0;
+        const bool top = b0 + len == n;
+#pragma unroll
+        for (int k = SEG - 1; k >= 0; --k)
+            if (k < len) {
+                w = (top && k == len - 1) ? next : z * (w - v[k]);
+                v[k] = w;
+            }
+        double bin = 0.0;  // the true value at b0 + len
+        {
+            double e = 0.0;
+#pragma unroll
+            for (int q = P - 1; q >= 0; --q) {
+                const double wq = __shfl(w, base + q), zq = __shfl(zl, base + q);
+                if (q == sub) bin = e;
+                e = wq + zq * e;
+            }
+        }
+        {
+            double zk = z;
+#pragma unroll
+            for (int k = SEG - 1; k >= 0; --k)
+                if (k < len) {
+                    v[k] = v[k] + zk * bin;
+                    zk *= z;
+                }
         }
     }
-    if (bin != 0.0) {
-        double zk = z;
-        for (int i = b1 - 1; i >= b0; --i) {
-            c[i * s] = c[i * s] + zk * bin;
-            zk *= z;
-        }
-    }
+    wave_sync();  // every lane's reads (the mirror values) are done before any write
+#pragma unroll
+    for (int k = 0; k < SEG; ++k)
+        if (k < len) c[(b0 + k) * s] = v[k];
 }
 
 // the post's B-spline prefilter for arrays of up to kPostFuse x kPostFuse: workgroup 0 the map,
-// 1 the mask, each array in LDS (row pitch nx + 1), both axes, four lanes per line
-constexpr int kSplinePostThreads = 4 * kPostFuse;
+// 1 the mask, each array in LDS (row pitch nx + 1), both axes, eight lanes per line
+constexpr int kSplineLanes = 8, kSplinePostThreads = kSplineLanes * kPostFuse;
 __global__ void __launch_bounds__(kSplinePostThreads) k_spline_post(double* __restrict__ coef, int ny, int nx) {
     __shared__ double a[kPostFuse * (kPostFuse + 1)];
     const int64_t total = (int64_t)ny * nx;
@@ -747,9 +768,10 @@ __global__ void __launch_bounds__(kSplinePostThreads) k_spline_post(double* __re
         }
     }
     __syncthreads();
-    if (tid / 4 < nx) spline_line_par<4>(a + tid / 4, ny, pitch, tid & 3);  // axis 0: the columns
+    constexpr int Q = kSplineLanes, SEG = kPostFuse / kSplineLanes;
+    if (tid / Q < nx) spline_line_reg<Q, SEG>(a + tid / Q, ny, pitch, tid % Q);  // axis 0: the columns
     __syncthreads();
-    if (tid / 4 < ny) spline_line_par<4>(a + (tid / 4) * pitch, nx, 1, tid & 3);  // axis 1: the rows
+    if (tid / Q < ny) spline_line_reg<Q, SEG>(a + (tid / Q) * pitch, nx, 1, tid % Q);  // axis 1: the rows
     __syncthreads();
     for (int64_t k = tid; k < total; k += kSplinePostThreads) {
         const int i = (int)(k / nx), j = (int)(k - (int64_t)i * nx);
