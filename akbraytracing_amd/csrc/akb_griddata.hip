@@ -1326,6 +1326,8 @@ struct ConeBand {
     double* gout;         // x_j
     ConeStep st;
     const int* needed;    // device flag: some target needs the band (else the launch returns at once)
+    unsigned long long* clk = nullptr;  // diagnostics (or nullptr): the ring / tile workgroups' wall-clock
+                                        // time summed, their counts, their longest (akb_gd_patch_phases)
 };
 
 // the lattice edges of a band vertex in the fixed order (left, right, down, up, the diagonals), from
@@ -1416,8 +1418,20 @@ __device__ __forceinline__ void cone_ring_vertex(const Grid& g, const ConeBand& 
 // arithmetic, two vertices a thread, x_{j-2} loaded with the tile). Both halves read x_{j-1} /
 // x_{j-2} only.
 constexpr int kBandThreads = 512, kBandVR = kBandTR * kBandTC / kBandThreads;
+// a workgroup's wall-clock time into the diagnostics words (ring: k = 0, tile: k = 1)
+__device__ __forceinline__ void band_clock(unsigned long long* clk, int k, unsigned long long t0) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long d = wall_clock64() - t0;
+        atomicAdd(&clk[2 * k], d);
+        atomicAdd(&clk[2 * k + 1], 1ull);
+        atomicMax(&clk[4 + k], d);
+    }
+}
+
 __global__ void __launch_bounds__(kBandThreads) k_gd_cone_band(Grid g, BandTiles bt, ConeBand a, int nr8) {
     if (!*a.needed) return;
+    const unsigned long long t0 = a.clk ? wall_clock64() : 0;
     if ((int)blockIdx.x >= nr8) {
         constexpr int HR = kBandTR + 2, HC = kBandTC + 2, HN = HR * HC, CC = kBandTC + 1;
         __shared__ double sx[HN], sy[HN], sf[HN], sgx[HN], sgy[HN];
@@ -1511,6 +1525,7 @@ __global__ void __launch_bounds__(kBandThreads) k_gd_cone_band(Grid g, BandTiles
             band_edges(A, sx[li], sy[li], sf[li], xs, ys, fs, gxs, gys, on);
             band_solve(a, (int64_t)iv * g.nh + ih, A, ppx[u], ppy[u]);
         }
+        if (a.clk) band_clock(a.clk + 4, 1, t0);
         return;
     }
     const int64_t L = 2 * (int64_t)(g.nh - 1) + 2 * (int64_t)(g.nv - 1);
@@ -1528,6 +1543,7 @@ __global__ void __launch_bounds__(kBandThreads) k_gd_cone_band(Grid g, BandTiles
             cone_ring_vertex<64>(g, a, r0 + (q >> 3), lane);
         }
     }
+    if (a.clk) band_clock(a.clk + 4, 0, t0);
 }
 
 struct ConePatch {
@@ -2374,6 +2390,7 @@ bool gd_claim_tri() { return getenv("AKB_GD_CLAIM_TRI") != nullptr; }
 // diagnostics (akb_gd_patch_timing / akb_gd_patch_times): HIP events around each k_gd_cone_patch
 // launch while enabled, a ring of kPatchEvents pairs, and each launch's cell count (its device word)
 constexpr int kPatchEvents = 1024;
+constexpr int kPatchClk = 10;  // the diagnostics words (akb_gd_patch_phases)
 struct PatchTimer {
     bool on = false, made = false;
     hipEvent_t ev[kPatchEvents][2];
@@ -2600,14 +2617,15 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
                 const double* gprev = j >= 3 ? gb[(j + 1) % 3] : nullptr;
                 const BandTiles bt = band_tiles(g.nv, g.nh, 2 * K + 3 - j);
                 const unsigned nr8 = (unsigned)(((L + 7) / 8 * 64 + kBandThreads - 1) / kBandThreads);
-                const ConeBand a{fv, gin, gprev, gb[j % 3], steps[j], band};
+                const ConeBand a{fv, gin, gprev, gb[j % 3], steps[j], band, patch_timer().on ? patch_timer().clk : nullptr};
                 k_gd_cone_band<<<bt.total + nr8, kBandThreads, 0, s>>>(g, bt, a, (int)nr8);
                 if ((st = launch_status("k_gd_cone_band"))) return st;
             }
             if (d_change) {  // one more plain sweep, y from x_K to depth K + 2 (the band targets' corners)
                 const BandTiles bt = band_tiles(g.nv, g.nh, K + 2);
                 const unsigned nr8 = (unsigned)(((L + 7) / 8 * 64 + kBandThreads - 1) / kBandThreads);
-                const ConeBand a{fv, gb[K % 3], nullptr, gb[(K + 1) % 3], ConeStep{0, 1.0}, band};
+                const ConeBand a{fv, gb[K % 3], nullptr, gb[(K + 1) % 3], ConeStep{0, 1.0}, band,
+                                 patch_timer().on ? patch_timer().clk : nullptr};
                 k_gd_cone_band<<<bt.total + nr8, kBandThreads, 0, s>>>(g, bt, a, (int)nr8);
                 if ((st = launch_status("k_gd_cone_band"))) return st;
             }
@@ -2782,11 +2800,11 @@ int akb_gd_patch_timing(int enable) {
     if (enable && !t.made) {
         for (int k = 0; k < kPatchEvents; ++k)
             for (int q = 0; q < 2; ++q) AKB_HIP_CHECK(hipEventCreate(&t.ev[k][q]));
-        AKB_HIP_CHECK(hipMalloc((void**)&t.clk, 4 * sizeof(unsigned long long)));
+        AKB_HIP_CHECK(hipMalloc((void**)&t.clk, kPatchClk * sizeof(unsigned long long)));
         t.made = true;
     }
     if (enable) {  // a new record (stopping keeps the last one for akb_gd_patch_times / _phases)
-        AKB_HIP_CHECK(hipMemset(t.clk, 0, 4 * sizeof(unsigned long long)));
+        AKB_HIP_CHECK(hipMemset(t.clk, 0, kPatchClk * sizeof(unsigned long long)));
         t.launches = 0;
     }
     t.on = enable != 0;
@@ -2798,11 +2816,11 @@ int akb_gd_patch_phases(unsigned long long* out) {
     PatchTimer& t = patch_timer();
     AKB_REQUIRE(out, "null pointer");
     if (!t.made) {
-        for (int k = 0; k < 4; ++k) out[k] = 0;
+        for (int k = 0; k < kPatchClk; ++k) out[k] = 0;
         return 0;
     }
     AKB_HIP_CHECK(hipDeviceSynchronize());
-    AKB_HIP_CHECK(hipMemcpy(out, t.clk, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    AKB_HIP_CHECK(hipMemcpy(out, t.clk, kPatchClk * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     return 0;
 }
 

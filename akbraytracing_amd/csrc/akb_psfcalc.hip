@@ -747,10 +747,13 @@ __device__ void spline_line_reg(double* c, int n, int s, int sub) {
 // the post's B-spline prefilter for arrays of up to kPostFuse x kPostFuse: workgroup 0 the map,
 // 1 the mask, each array in LDS (row pitch nx + 1), both axes, eight lanes per line
 constexpr int kSplineLanes = 8, kSplinePostThreads = kSplineLanes * kPostFuse;
-__global__ void __launch_bounds__(kSplinePostThreads) k_spline_post(double* __restrict__ coef, int ny, int nx) {
+__global__ void __launch_bounds__(kSplinePostThreads) k_spline_post(double* __restrict__ coef, int ny, int nx,
+                                                                     unsigned long long* clocks) {
     __shared__ double a[kPostFuse * (kPostFuse + 1)];
     const int64_t total = (int64_t)ny * nx;
     const int pitch = nx + 1, tid = threadIdx.x;
+    const bool clk = blockIdx.x == 0 && tid == 0;  // workgroup 0's phase clocks (diagnostics)
+    if (clk) clocks[0] = wall_clock64();
     double* base = coef + (int64_t)blockIdx.x * total;
     for (int64_t k0 = tid; k0 < total; k0 += 16 * kSplinePostThreads) {  // 16 loads in flight per thread
         double t[16];
@@ -768,11 +771,14 @@ __global__ void __launch_bounds__(kSplinePostThreads) k_spline_post(double* __re
         }
     }
     __syncthreads();
+    if (clk) clocks[1] = wall_clock64();
     constexpr int Q = kSplineLanes, SEG = kPostFuse / kSplineLanes;
     if (tid / Q < nx) spline_line_reg<Q, SEG>(a + tid / Q, ny, pitch, tid % Q);  // axis 0: the columns
     __syncthreads();
+    if (clk) clocks[2] = wall_clock64();
     if (tid / Q < ny) spline_line_reg<Q, SEG>(a + (tid / Q) * pitch, nx, 1, tid % Q);  // axis 1: the rows
     __syncthreads();
+    if (clk) clocks[3] = wall_clock64();
     for (int64_t k = tid; k < total; k += kSplinePostThreads) {
         const int i = (int)(k / nx), j = (int)(k - (int64_t)i * nx);
         base[k] = a[i * pitch + j];
@@ -1213,7 +1219,7 @@ int akb_pupil_post_f64(const double* map, int ny, int nx, double sigma, double* 
     int st = launch_status("k_pupil_post");
     if (st) return st;
     if (ny <= kPostFuse && nx <= kPostFuse) {
-        k_spline_post<<<2, kSplinePostThreads, 0, s>>>(w, ny, nx);
+        k_spline_post<<<2, kSplinePostThreads, 0, s>>>(w, ny, nx, (unsigned long long*)head + 8);
         if ((st = launch_status("k_spline_post"))) return st;
     } else {
         for (int axis = 0; axis < 2; ++axis) {

@@ -705,13 +705,16 @@ def main():
             S = next(s2 for s2 in range((K + 1) // 2, K + 1)
                      if (((W - 2) ** 2 + 63) // 64 * 64) + (W - 2 * s2 - 2) ** 2 <= 1020)
             patch = faithful_roofline(list(pms[:k]), int(pcells[k - 1]), K, S)
-            ph = (ctypes.c_ulonglong * 4)()
+            ph = (ctypes.c_ulonglong * 10)()
             LIBM.check(LIBM.lib().akb_gd_patch_phases(ph))
             tot = ph[0] + ph[1] + ph[2]
             if tot:  # workgroup 0's wall clock (10 ns ticks) in its steps' phases
                 patch["workgroup0_phases"] = {"setup_frac": ph[0] / tot, "sweeps_frac": ph[1] / tot,
                                               "rest_frac": ph[2] / tot, "steps": int(ph[3]),
                                               "us_per_step": tot * 0.01 / max(int(ph[3]), 1)}
+            if ph[5] and ph[7]:  # the band sweeps' workgroups (diagnostics)
+                patch["band_workgroups"] = {"ring_avg_us": ph[4] * 0.01 / ph[5], "ring_max_us": ph[8] * 0.01,
+                                            "tile_avg_us": ph[6] * 0.01 / ph[7], "tile_max_us": ph[9] * 0.01}
     while fronts:  # the last front's back half (outside the timed region, like the first one's)
         back(False)
     while tickets:
