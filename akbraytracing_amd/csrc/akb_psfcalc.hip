@@ -785,8 +785,38 @@ __global__ void __launch_bounds__(kSplinePostThreads) k_spline_post(double* __re
     }
 }
 
+// the post's map in LDS with one pad word per 128 (element k at k + k / 128): a numpy leaf is 128
+// consecutive elements, so the nanmean's lanes - a leaf each - then read distinct banks (without the
+// pad every lane of a wave hit the same bank)
+__device__ __forceinline__ int64_t post_lds(int64_t k) { return k + (k >> 7); }
+struct PostLeaf {  // pw_leaf_lds<true>'s sums over the padded map
+    const double* a;
+    __device__ double val(int i) const {
+        const double x = a[post_lds(i)];
+        return x != x ? 0.0 : x;
+    }
+    __device__ double leaf(int o, int n) const {
+        if (n < 8) {
+            double res = 0.0;
+            for (int i = 0; i < n; ++i) res = res + val(o + i);
+            return res;
+        }
+        double r[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[j] = val(o + j);
+        int i = 8;
+        for (; i < n - (n % 8); i += 8) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) r[j] = r[j] + val(o + i + j);
+        }
+        double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+        for (; i < n; ++i) res = res + val(o + i);
+        return res;
+    }
+};
+
 __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
-    __shared__ double smem[kPostLds];  // the map, then matrixWave2 - nanmean (when it fits)
+    __shared__ double smem[kPostLds + kPostLds / 128];  // the map, then matrixWave2 - nanmean (when it fits)
     __shared__ PwTree trees[2];        // the nanmean's pairwise trees (waves 0 and 1)
     __shared__ double bufsum[8];
     __shared__ int firstrow[2];
@@ -819,12 +849,13 @@ __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
                 const int64_t k = k0 + q * kPostThreads + tid;
-                if (k < total) smem[k] = t[q];
+                if (k < total) smem[post_lds(k)] = t[q];
             }
         }
         __syncthreads();
     }
     const double* src = in_lds ? smem : a.m;
+    auto L = [&](int64_t k) { return in_lds ? post_lds(k) : k; };  // a map index in src / cm
     if (tid == 0) a.clocks[1] = wall_clock64();
     // np.nanmean: numpy's pairwise sum of the NaN-zeroed map, one wave per 8192-element buffer
     // (waves 0 and 1 alternate over the buffers)
@@ -833,7 +864,8 @@ __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
         for (int b = w; b < nbuf; b += 2) {
             const int64_t b0 = (int64_t)b * 8192;
             const int len = (int)(total - b0 < 8192 ? total - b0 : 8192);
-            const double v = pw_tree_wave<true>(trees[w], src + b0, len);
+            const double v = in_lds ? pw_tree_wave_get(trees[w], PostLeaf{smem}, (int)b0, len)
+                                    : pw_tree_wave<true>(trees[w], src + b0, len);
             if ((tid & 63) == 0) bufsum[b] = v;
             wave_sync();
         }
@@ -843,7 +875,7 @@ __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
     double cnt[1] = {0.0};
     double lo = INFINITY, hi = -INFINITY;
     for (int64_t k = tid; k < total; k += kPostThreads) {
-        const double v = src[k];
+        const double v = src[L(k)];
         if (v == v) {
             cnt[0] += 1.0;
             lo = fmin(lo, v);
@@ -866,7 +898,7 @@ __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
     // matrixWave2 - nanmean, the plane correction's input: in LDS when it fits, else in `corrected`
     double* cm = in_lds ? smem : a.corrected;
     __syncthreads();
-    for (int64_t k = tid; k < total; k += kPostThreads) cm[k] = src[k] - mean;
+    for (int64_t k = tid; k < total; k += kPostThreads) cm[L(k)] = src[L(k)] - mean;
     __syncthreads();
     if (tid == 0) a.clocks[2] = wall_clock64();
     // plane_correction_with_nan_and_outlier_filter: the four moment passes of k_moments
@@ -875,7 +907,7 @@ __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
         for (int q = 0; q < kMomMax; ++q) acc[q] = 0.0;
         PostIdx ix(tid, a.nx);
         for (int64_t k = tid; k < total; k += kPostThreads, ix.next()) {
-            const double z = cm[k];
+            const double z = cm[L(k)];
             if (z != z) continue;
             double f[5];
             basis5_tab(bX, bY, ix.i, ix.j, a.ny, a.nx, f);
@@ -964,10 +996,10 @@ __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
             double f[5];
             basis5_tab(bX, bY, ix.i, ix.j, a.ny, a.nx, f);
             const double pl = __builtin_fma(sys[10], f[2], __builtin_fma(sys[9], f[1], sys[8] * f[0]));
-            const double v = cm[k];
+            const double v = cm[L(k)];
             const bool nan = v != v;
             const double o = nan ? v : v - pl;
-            cm[k] = o;
+            cm[L(k)] = o;
             if (in_lds) a.corrected[k] = o;
             a.coef[k] = nan ? 0.0 : o;
             a.coef[total + k] = nan ? 0.0 : 1.0;
@@ -982,7 +1014,7 @@ __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
         const int c1 = a.nx / 4, c3 = a.nx * 3 / 4;
         for (int r = tid; r < 2 * a.ny; r += kPostThreads) {
             const int row = r >> 1, c = (r & 1) ? c3 : c1;
-            const double v = cm[(int64_t)row * a.nx + c];
+            const double v = cm[L((int64_t)row * a.nx + c)];
             if (v == v) atomicMin(&firstrow[r & 1], row);
         }
     }
