@@ -633,7 +633,7 @@ __device__ __forceinline__ double zpow(double z, int k) {  // z^k by binary powe
 }
 
 template <int P, int SEG>
-__device__ void spline_line_reg(double* c, int n, int s, int sub) {
+__device__ void spline_line_reg(double* c, int n, int s, int sub, unsigned long long* ck = nullptr) {
     const double z = sqrt(3.0) - 2.0;
     const double gain = (1.0 - z) * (1.0 - 1.0 / z);
     const int lane = threadIdx.x & 63, base = lane & ~(P - 1);
@@ -654,6 +654,7 @@ __device__ void spline_line_reg(double* c, int n, int s, int sub) {
         for (int q = 0; q < P; ++q) t += __shfl(own, base + q);
         return t;
     };
+    if (ck) ck[0] = wall_clock64();
     if (n > 1) {
         const double zn1 = zpow(z, n - 1);
         // the mirror-symmetric initial sum: c0 = c[0] + zn1 c[n-1] + sum_{i=1}^{n-2} z^i (c[i] + zn1 c[n-1-i])
@@ -681,6 +682,7 @@ __device__ void spline_line_reg(double* c, int n, int s, int sub) {
         for (int q = 0; q < P; ++q) tot += __shfl(part, base + q);
         const double y0 = (at(0) + zn1 * at(n - 1) + tot) / (1.0 - zn1 * zn1);
         const double zl = zpow(z, len);  // z^(segment length), 1 for an empty segment
+        if (ck) ck[1] = wall_clock64();
         // causal
         double u = 0.0;
 #pragma unroll
@@ -708,6 +710,7 @@ __device__ void spline_line_reg(double* c, int n, int s, int sub) {
                     zk *= z;
                 }
         }
+        if (ck) ck[2] = wall_clock64();
         // anti-causal
         const double next = (z * at(n - 2) + at(n - 1)) * z / (z * z - 1.0);
         double w = 0.0;
@@ -773,7 +776,8 @@ __global__ void __launch_bounds__(kSplinePostThreads) k_spline_post(double* __re
     __syncthreads();
     if (clk) clocks[1] = wall_clock64();
     constexpr int Q = kSplineLanes, SEG = kPostFuse / kSplineLanes;
-    if (tid / Q < nx) spline_line_reg<Q, SEG>(a + tid / Q, ny, pitch, tid % Q);  // axis 0: the columns
+    if (tid / Q < nx)  // axis 0: the columns
+        spline_line_reg<Q, SEG>(a + tid / Q, ny, pitch, tid % Q, clk ? clocks + 4 : nullptr);
     __syncthreads();
     if (clk) clocks[2] = wall_clock64();
     if (tid / Q < ny) spline_line_reg<Q, SEG>(a + (tid / Q) * pitch, nx, 1, tid % Q);  // axis 1: the rows

@@ -27,7 +27,7 @@ def main():
         torch.cuda.synchronize()
         wall.append(ev[0].elapsed_time(ev[1]) * 1e3)
         clk = o["work"][0:5].cpu().numpy().view(np.uint64).astype(np.int64)
-        sp = o["work"][8:12].cpu().numpy().view(np.uint64).astype(np.int64)
+        sp = o["work"][8:16].cpu().numpy().view(np.uint64).astype(np.int64)
         rows.append(np.concatenate([(clk - clk[0]) * 0.01, (sp - sp[0]) * 0.01]))  # us
     r = np.median(np.array(rows[5:]), axis=0)
     print(json.dumps(dict(wall_us=float(np.median(wall[5:])), phases_us=[round(float(x), 2) for x in r])))
