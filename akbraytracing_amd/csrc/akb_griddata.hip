@@ -890,15 +890,14 @@ __device__ __forceinline__ void grad_edge(const Grid& g, int64_t n, int64_t j, d
 
 // ring vertex r's pocket chords over a group of W lanes (sub: the lane in the group), reduced by the
 // group's butterfly (zeros from the lanes past the chord list)
-template <int NV, int W>
+template <int NV, int W, int kB = 4>
 __device__ __forceinline__ GradAcc<NV> chord_sums(const Grid& g, int64_t n, int64_t r, int sub, double xi, double yi,
                                                   const double (&fi)[NV], const double* __restrict__ f,
                                                   const double* __restrict__ gin) {
     GradAcc<NV> A;
-    // four of the lane's chords at a time: their indices, then their data, loaded before the first
+    // kB of the lane's chords at a time: their indices, then their data, loaded before the first
     // edge sum (the same edges in the same order; a loop of index-load, data-load, sum waited out
     // two memory latencies per chord)
-    constexpr int kB = 4;
     const int32_t k1 = g.xptr[r + 1];
     for (int32_t k0 = g.xptr[r] + sub; k0 < k1; k0 += kB * W) {
         int64_t js[kB];
@@ -1328,6 +1327,7 @@ struct ConeBand {
     const int* needed;    // device flag: some target needs the band (else the launch returns at once)
     unsigned long long* clk = nullptr;  // diagnostics (or nullptr): the ring / tile workgroups' wall-clock
                                         // time summed, their counts, their longest (akb_gd_patch_phases)
+    const int32_t* slots = nullptr;     // (L, 8): ring vertex r's chord neighbours padded with -1 (or nullptr)
 };
 
 // the lattice edges of a band vertex in the fixed order (left, right, down, up, the diagonals), from
@@ -1396,17 +1396,44 @@ template <int W>
 __device__ __forceinline__ void cone_ring_vertex(const Grid& g, const ConeBand& a, int64_t r, int sub) {
     const int64_t n = (int64_t)g.nv * g.nh;
     const int64_t i = ring_vertex(g, r);
+    // every load that needs only r first: the vertex, x_{j-2} there, its chord slot (W = 8 with the
+    // slot table: the chord's index without the xptr level) in flight during the lattice edges,
+    // then the chord's data - two memory latencies for the vertex instead of four
     const double xi = g.x[i], yi = g.y[i];
     const double fi[1] = {a.f[i]};
+    const bool pre = a.st.mode == 2 && sub == 0;
+    const double ppx = pre ? a.gprev[2 * i] : 0.0, ppy = pre ? a.gprev[2 * i + 1] : 0.0;
+    const bool slotted = W == 8 && a.slots;  // (the same chord per lane as chord_sums<1, 8> of at most eight)
+    const int32_t j = slotted ? a.slots[r * 8 + sub] : -1;
     GradAcc<1> D;
     if (sub == 0) {
         const int iv = (int)(i / g.nh), ih = (int)(i - (int64_t)iv * g.nh);
         band_grid_sums(g, a, i, iv, ih, xi, yi, fi[0], D);
     }
-    GradAcc<1> A = chord_sums<1, W>(g, n, r, sub, xi, yi, fi, a.f, a.gin);
+    GradAcc<1> A;
+    if (slotted) {
+        if (j >= 0) {
+            const double fj[1] = {a.f[j]}, gxj[1] = {a.gin ? a.gin[2 * (int64_t)j] : 0.0},
+                         gyj[1] = {a.gin ? a.gin[2 * (int64_t)j + 1] : 0.0};
+            acc_edge<1>(A, edge_geom(g.x[j] - xi, g.y[j] - yi), fi, fj, gxj, gyj);
+        }
+        acc_reduce<1, W>(A);
+    } else {
+        A = chord_sums<1, W, W == 64 ? 1 : 4>(g, n, r, sub, xi, yi, fi, a.f, a.gin);
+    }
     if (sub == 0) {
         acc_add<1>(A, D);
-        band_solve(a, i, A);
+        band_solve(a, i, A, ppx, ppy);
+    }
+}
+
+// the ring's chord slot table for the band sweeps: slots[8 r + k] = ring vertex r's k-th chord
+// neighbour (xidx order), -1 past its chords (a vertex of more than eight keeps the xptr path)
+__global__ void k_gd_chord_slots(Grid g, int32_t* slots, int64_t L) {
+    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < L; r += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t k0 = g.xptr[r], cnt = g.xptr[r + 1] - k0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) slots[r * 8 + k] = k < cnt ? g.xidx[k0 + k] : -1;
     }
 }
 
@@ -1429,7 +1456,7 @@ __device__ __forceinline__ void band_clock(unsigned long long* clk, int k, unsig
     }
 }
 
-__global__ void __launch_bounds__(kBandThreads) k_gd_cone_band(Grid g, BandTiles bt, ConeBand a, int nr8) {
+__global__ void __launch_bounds__(kBandThreads) __attribute__((amdgpu_waves_per_eu(4))) k_gd_cone_band(Grid g, BandTiles bt, ConeBand a, int nr8) {
     if (!*a.needed) return;
     const unsigned long long t0 = a.clk ? wall_clock64() : 0;
     if ((int)blockIdx.x >= nr8) {
@@ -2612,12 +2639,19 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
         // whose neighbours (depth <= 2K + 4 - j) sweep j - 1 formed, so x_K is the global iteration's
         // to depth K + 3 >= every band target's corners (the first sweep reads x_0 = 0 only)
         if (band_on) {
+            // the ring's chord slots (the work's (L, 7)-double region, free in the cone solve)
+            int32_t* slots = (int32_t*)((double*)work + 3 * (int64_t)nv2 * n * 2);
+            if (v == 0) {
+                k_gd_chord_slots<<<grid_for(L), kBlock, 0, s>>>(g, slots, L);
+                if ((st = launch_status("k_gd_chord_slots"))) return st;
+            }
             for (int j = 1; j <= K; ++j) {
                 const double* gin = j == 1 ? nullptr : gb[(j - 1) % 3];
                 const double* gprev = j >= 3 ? gb[(j + 1) % 3] : nullptr;
                 const BandTiles bt = band_tiles(g.nv, g.nh, 2 * K + 3 - j);
                 const unsigned nr8 = (unsigned)(((L + 7) / 8 * 64 + kBandThreads - 1) / kBandThreads);
-                const ConeBand a{fv, gin, gprev, gb[j % 3], steps[j], band, patch_timer().on ? patch_timer().clk : nullptr};
+                const ConeBand a{fv, gin, gprev, gb[j % 3], steps[j], band, patch_timer().on ? patch_timer().clk : nullptr,
+                                 slots};
                 k_gd_cone_band<<<bt.total + nr8, kBandThreads, 0, s>>>(g, bt, a, (int)nr8);
                 if ((st = launch_status("k_gd_cone_band"))) return st;
             }
@@ -2625,7 +2659,7 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
                 const BandTiles bt = band_tiles(g.nv, g.nh, K + 2);
                 const unsigned nr8 = (unsigned)(((L + 7) / 8 * 64 + kBandThreads - 1) / kBandThreads);
                 const ConeBand a{fv, gb[K % 3], nullptr, gb[(K + 1) % 3], ConeStep{0, 1.0}, band,
-                                 patch_timer().on ? patch_timer().clk : nullptr};
+                                 patch_timer().on ? patch_timer().clk : nullptr, slots};
                 k_gd_cone_band<<<bt.total + nr8, kBandThreads, 0, s>>>(g, bt, a, (int)nr8);
                 if ((st = launch_status("k_gd_cone_band"))) return st;
             }
