@@ -2214,14 +2214,13 @@ __global__ void __launch_bounds__(kBlock, 5) k_gd_claim_hit(Grid g, Targets t, c
     }
 }
 
-// pocket triangles: slivers along the boundary whose boxes hold from none to hundreds of targets,
-// so sixteen lanes per triangle, striding its box (a wave each left three of every four waves idle on
-// the common few-target boxes and the grid three rounds deep; a thread each left a long sliver's box
-// to one lane: 326 us against 28 at C3); the target axes in LDS for tri_box's binary searches
-constexpr int kPocketLanes = 16;
+// pocket triangles: slivers along the boundary whose boxes hold from none to thousands of targets,
+// so one wave per triangle, its lanes striding the box (a workgroup per triangle left most of its
+// threads idle on the common few-target boxes; a thread per triangle left the long slivers' boxes
+// to one lane each: 326 us against 28 at C3); the target axes in LDS for tri_box's binary searches
 __global__ void __launch_bounds__(kBlock) k_gd_claim_pockets(Grid g, Targets t, int* owner) {
     const int64_t nc2 = 2 * ncells(g);
-    const int sub = threadIdx.x & (kPocketLanes - 1), ng = blockDim.x / kPocketLanes;
+    const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
     __shared__ double sax[2 * kClaimAxisLds];
     if (t.mx <= kClaimAxisLds && t.my <= kClaimAxisLds) {
         for (int i = threadIdx.x; i < t.mx; i += blockDim.x) sax[i] = t.gx[i];
@@ -2230,13 +2229,13 @@ __global__ void __launch_bounds__(kBlock) k_gd_claim_pockets(Grid g, Targets t, 
         t.gx = sax;
         t.gy = sax + kClaimAxisLds;
     }
-    for (int64_t j = (int64_t)blockIdx.x * ng + threadIdx.x / kPocketLanes; j < g.npock; j += (int64_t)gridDim.x * ng) {
+    for (int64_t j = (int64_t)blockIdx.x * nw + (threadIdx.x >> 6); j < g.npock; j += (int64_t)gridDim.x * nw) {
         const Tri T = tri_verts(g, nc2 + j);
         int c0, c1, r0, r1;
         tri_box(g, t, T, c0, c1, r0, r1);
         const int w = c1 - c0;
         const int64_t m = (int64_t)w * (r1 - r0);
-        for (int64_t k = sub; k < m; k += kPocketLanes) {
+        for (int64_t k = lane; k < m; k += 64) {
             const int r = r0 + (int)(k / w), c = c0 + (int)(k - (int64_t)(k / w) * w);
             claim_one(g, t, T, (int)(nc2 + j), r, c, owner);
         }
@@ -2594,7 +2593,7 @@ int cone_claims(const Grid& g, const Targets& t, int with_pockets, int* owner, h
         if ((st = launch_status("k_gd_claim"))) return st;
     }
     if (with_pockets && g.npock > 0) {
-        const int64_t pw = ((int64_t)g.npock + kBlock / kPocketLanes - 1) / (kBlock / kPocketLanes);
+        const int64_t pw = ((int64_t)g.npock + kBlock / 64 - 1) / (kBlock / 64);
         k_gd_claim_pockets<<<(unsigned)(pw < 16384 ? pw : 16384), kBlock, 0, s>>>(g, t, owner);
         if ((st = launch_status("k_gd_claim_pockets"))) return st;
     }
@@ -2742,7 +2741,7 @@ int akb_gd_claim_pockets_f64(const double* x, const double* y, int nv, int nh, c
     if (npock == 0) return 0;
     AKB_REQUIRE(ptri, "pockets needed");
     Grid g{x, y, nv, nh, diag, npock, ptri, nullptr, nullptr, nullptr, nullptr};
-    const int64_t pw = ((int64_t)npock + kBlock / kPocketLanes - 1) / (kBlock / kPocketLanes);
+    const int64_t pw = ((int64_t)npock + kBlock / 64 - 1) / (kBlock / 64);
     k_gd_claim_pockets<<<(unsigned)(pw < 16384 ? pw : 16384), kBlock, 0, (hipStream_t)stream>>>(g, Targets{gx, gy, mx, my},
                                                                                                owner);
     return launch_status("k_gd_claim_pockets");
