@@ -607,6 +607,226 @@ __global__ void __launch_bounds__(kCellTile * kCellTile) k_gd_cells_tiled(Grid g
     }
 }
 
+// ---- the cell pass as wave strips: a wave's 64 lanes hold 64 consecutive vertex columns and walk
+// a segment of cell rows upwards (as many rows as puts one wave on every resident slot), a vertex row per step (two coalesced loads, issued two steps ahead);
+// the columns h + 1 and h + 2 come from the lanes above by DPP (wave_shl), a cell's right
+// neighbour's diagonal likewise, and the diagonal of the row above is formed one step early - so no
+// LDS, no barrier, each vertex loaded once (plus two halo rows per segment) and each diagonal formed
+// once. Lanes 0 .. 61 own the cells (lane 62 forms the diagonal lane 61's right edge needs). Every
+// test is k_gd_cells_tiled's arithmetic on the same values: the same diagonals and flags. With
+// kClaims each cell claims its targets: the candidates from the cell's own box (axis_range on
+// linspace axes, else the binary search), then tile_claims' per-triangle predicate - the same owners.
+constexpr int kStripCells = 62, kStripThreads = 256;
+
+__device__ __forceinline__ int lane_up(int v) {  // lane i gets lane i + 1's value (lane 63: 0)
+    return __builtin_amdgcn_update_dpp(0, v, 0x130, 0xf, 0xf, false);
+}
+__device__ __forceinline__ double lane_up(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = lane_up((int)(b & 0xffffffffLL)), hi = lane_up((int)(b >> 32));
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+
+struct StripRow {  // a vertex row at the lane's column h and the two columns after it
+    double x, y, x1, y1, x2, y2;
+};
+__device__ __forceinline__ StripRow strip_row(double x, double y) {
+    StripRow r;
+    r.x = x;
+    r.y = y;
+    r.x1 = lane_up(x);
+    r.y1 = lane_up(y);
+    r.x2 = lane_up(r.x1);
+    r.y2 = lane_up(r.y1);
+    return r;
+}
+
+// the diagonal of the cell between rows a (bottom) and b (top) at the lane's column, and whether
+// the split is convex (k_gd_cells_tiled's diag_of)
+__device__ __forceinline__ int strip_diag(const StripRow& a, const StripRow& b, double& viol) {
+    const double x0 = a.x, y0 = a.y;
+    const double bx = a.x1 - x0, by = a.y1 - y0;
+    const double cx = b.x1 - x0, cy = b.y1 - y0;
+    const double dx = b.x - x0, dy = b.y - y0;
+    const double ic = incircle(0.0, 0.0, bx, by, cx, cy, dx, dy);
+    const int d = ic > 0 ? 1 : 0;
+    const double sgn = d == 0 ? orient(0, 0, bx, by, cx, cy) * orient(0, 0, cx, cy, dx, dy)
+                              : orient(0, 0, bx, by, dx, dy) * orient(bx, by, cx, cy, dx, dy);
+    viol = sgn > 0 ? 0.0 : 1.0;
+    return d;
+}
+
+// an edge's local-Delaunay test (k_gd_cells_tiled's): the edge from (x0, y0) to (cxa, cya), the
+// triangle's opposite vertex (mxa, mya), the neighbour's (oxa, oya)
+__device__ __forceinline__ bool strip_edge_bad(double x0, double y0, double mxa, double mya, double cxa, double cya,
+                                               double oxa, double oya, double tol) {
+    const double ax = mxa - x0, ay = mya - y0, cx = cxa - x0, cy = cya - y0;
+    const double ox = oxa - x0, oy = oya - y0;
+    const double sc = fmax(fmax(fabs(ax), fabs(ay)), fmax(fmax(fabs(cx), fabs(cy)), fmax(fabs(ox), fabs(oy))));
+    return incircle(0.0, 0.0, ax, ay, cx, cy, ox, oy) > tol * sc * sc * sc * sc;
+}
+
+// a cell's claims: its corners (p00, p01, p10, p11) in registers, d its diagonal, c its index
+__device__ __forceinline__ void strip_claims(const Targets& t, int* owner, bool uniform, double inv_dx, double inv_dy,
+                                               const double (&vx)[4], const double (&vy)[4], int d, int64_t c) {
+    const double xlo = fmin(fmin(vx[0], vx[1]), fmin(vx[2], vx[3])), xhi = fmax(fmax(vx[0], vx[1]), fmax(vx[2], vx[3]));
+    const double ylo = fmin(fmin(vy[0], vy[1]), fmin(vy[2], vy[3])), yhi = fmax(fmax(vy[0], vy[1]), fmax(vy[2], vy[3]));
+    const double padx = (xhi - xlo) * 1e-9, pady = (yhi - ylo) * 1e-9;
+    int c0, c1, r0, r1;
+    bool hit;
+    if (uniform) {
+        hit = axis_range(t.gx, t.mx, inv_dx, xlo - padx, xhi + padx, c0, c1) &&
+              axis_range(t.gy, t.my, inv_dy, ylo - pady, yhi + pady, r0, r1);
+    } else {
+        c0 = lower_idx(t.gx, t.mx, xlo - padx);
+        c1 = lower_idx(t.gx, t.mx, xhi + padx);
+        r0 = lower_idx(t.gy, t.my, ylo - pady);
+        r1 = lower_idx(t.gy, t.my, yhi + pady);
+        hit = c0 < c1 && r0 < r1;
+    }
+    if (!hit) return;
+    for (int r = r0; r < r1; ++r) {
+        for (int q = c0; q < c1; ++q) {
+            const double px = t.gx[q], py = t.gy[r];
+#pragma unroll 1
+            for (int half = 0; half < 2; ++half) {
+                // tri_verts' vertex order, as corner numbers 0 = p00, 1 = p01, 2 = p10, 3 = p11
+                int kv[3];
+                if (d == 0) {
+                    kv[0] = 0;
+                    kv[1] = half == 0 ? 1 : 3;
+                    kv[2] = half == 0 ? 3 : 2;
+                } else {
+                    kv[0] = half == 0 ? 0 : 1;
+                    kv[1] = half == 0 ? 1 : 3;
+                    kv[2] = 2;
+                }
+                double tx[3], ty[3];
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    tx[k] = kv[k] == 0 ? vx[0] : kv[k] == 1 ? vx[1] : kv[k] == 2 ? vx[2] : vx[3];
+                    ty[k] = kv[k] == 0 ? vy[0] : kv[k] == 1 ? vy[1] : kv[k] == 2 ? vy[2] : vy[3];
+                }
+                double txlo = tx[0], txhi = txlo, tylo = ty[0], tyhi = tylo;
+#pragma unroll
+                for (int k = 1; k < 3; ++k) {
+                    txlo = fmin(txlo, tx[k]);
+                    txhi = fmax(txhi, tx[k]);
+                    tylo = fmin(tylo, ty[k]);
+                    tyhi = fmax(tyhi, ty[k]);
+                }
+                const double tpx = (txhi - txlo) * 1e-9, tpy = (tyhi - tylo) * 1e-9;
+                if (!(px >= txlo - tpx && px < txhi + tpx && py >= tylo - tpy && py < tyhi + tpy)) continue;
+                // bary's expressions
+                const double x2 = tx[2], y2 = ty[2];
+                const double a00 = tx[0] - x2, a01 = tx[1] - x2;
+                const double a10 = ty[0] - y2, a11 = ty[1] - y2;
+                const double det = a00 * a11 - a01 * a10;
+                const double t00 = a11 / det, t01 = -a01 / det, t10 = -a10 / det, t11 = a00 / det;
+                const double dx = px - x2, dy = py - y2;
+                const double b0 = t00 * dx + t01 * dy, b1 = t10 * dx + t11 * dy, b2 = 1.0 - b0 - b1;
+                if (b0 >= -kInsideEps && b1 >= -kInsideEps && b2 >= -kInsideEps)
+                    atomicMin(&owner[(int64_t)r * t.mx + q], (int)(2 * c + half));
+            }
+        }
+    }
+}
+
+template <bool kClaims = false>
+__global__ void __launch_bounds__(kStripThreads) k_gd_cells_strip(Grid g, uint8_t* diag, double tol, unsigned* flags,
+                                                                  int seg_rows, TileClaims tc = {}) {
+    const int r_lo = g.row0, r_hi = g.row1 < 0 ? g.nv - 1 : g.row1;  // window cell rows [r_lo, r_hi)
+    const int nstrip = (g.nh - 1 + kStripCells - 1) / kStripCells;
+    const int nseg = (r_hi - r_lo + seg_rows - 1) / seg_rows;
+    const int lane = threadIdx.x & 63;
+    const int unit = (int)blockIdx.x * (kStripThreads / 64) + (int)(threadIdx.x >> 6);
+    bool uniform = false;
+    double inv_dx = 0.0, inv_dy = 0.0;
+    if constexpr (kClaims) {
+        __shared__ double sax[2 * kClaimAxisLds];
+        if (tc.t.mx <= kClaimAxisLds && tc.t.my <= kClaimAxisLds) {
+            for (int i = threadIdx.x; i < tc.t.mx; i += blockDim.x) sax[i] = tc.t.gx[i];
+            for (int i = threadIdx.x; i < tc.t.my; i += blockDim.x) sax[kClaimAxisLds + i] = tc.t.gy[i];
+            __syncthreads();
+            tc.t.gx = sax;
+            tc.t.gy = sax + kClaimAxisLds;
+        }
+        uniform = axes_uniform(tc.t);
+        inv_dx = inv_step(tc.t.gx, tc.t.mx);
+        inv_dy = inv_step(tc.t.gy, tc.t.my);
+    }
+    if (unit >= nstrip * nseg) return;  // (after the workgroup's barriers)
+    const int seg = unit / nstrip, strip = unit - seg * nstrip;
+    const int ih = strip * kStripCells + lane, iv0 = r_lo + seg * seg_rows;
+    const int iv1 = min(iv0 + seg_rows, r_hi);
+    // vertex row r at this lane's column (0 outside the lattice and past the window's rows + 1)
+    auto load = [&](int r, double& x, double& y) {
+        x = y = 0.0;
+        if (r < g.nv && r <= r_hi + 1 && ih < g.nh) {
+            const int64_t q = (int64_t)r * g.nh + ih;
+            x = g.x[q];
+            y = g.y[q];
+        }
+    };
+    double x0, y0, x1, y1, x2, y2, x3, y3;
+    load(iv0, x0, y0);
+    load(iv0 + 1, x1, y1);
+    load(iv0 + 2, x2, y2);
+    load(iv0 + 3, x3, y3);
+    StripRow A = strip_row(x0, y0), B = strip_row(x1, y1);
+    const bool col_cell = ih < g.nh - 1;                   // a cell at this column
+    const bool own_lane = lane < kStripCells && col_cell;  // (lanes 62 and 63 own none)
+    double bad = 0.0;
+    int d = col_cell ? strip_diag(A, B, bad) : 0;
+    unsigned acc = 0;
+    for (int iv = iv0; iv < iv1; ++iv) {
+        // row iv + 2 arrived (issued two steps ago); row iv + 4 issued now
+        const StripRow C = strip_row(x2, y2);
+        x2 = x3;
+        y2 = y3;
+        load(iv + 4, x3, y3);
+        // the row above's diagonal (this lane's next step) and the right neighbour's on this row
+        const int jv = iv + 1;
+        double bad_up = 0.0;
+        const int dup = (col_cell && jv < g.nv - 1 && jv <= r_hi) ? strip_diag(B, C, bad_up) : 0;
+        const int dn = lane_up(d);
+        if (own_lane) {
+            const int64_t c = (int64_t)iv * (g.nh - 1) + ih;
+            diag[c] = (uint8_t)d;
+            unsigned f = bad > 0 ? 1u : 0u;
+            if (!isfinite(A.x) || !isfinite(A.y)) f |= 32u;
+            {
+                const double o = orient(A.x, A.y, A.x1, A.y1, B.x1, B.y1);
+                f |= o > 0 ? 8u : (o < 0 ? 16u : 1u);
+            }
+            if (ih + 1 < g.nh - 1) {  // right edge p01-p11 against the next cell's left triangle
+                const double mx = d == 0 ? A.x : B.x, my = d == 0 ? A.y : B.y;
+                const double ox = dn == 0 ? B.x2 : A.x2, oy = dn == 0 ? B.y2 : A.y2;
+                if (strip_edge_bad(A.x1, A.y1, mx, my, B.x1, B.y1, ox, oy, tol)) f |= 2u;
+            }
+            if (iv + 1 < g.nv - 1) {  // top edge p10-p11 against the next row's bottom triangle
+                const double mx = d == 0 ? A.x : A.x1, my = d == 0 ? A.y : A.y1;
+                const double ox = dup == 0 ? C.x1 : C.x, oy = dup == 0 ? C.y1 : C.y;
+                if (strip_edge_bad(B.x, B.y, mx, my, B.x1, B.y1, ox, oy, tol)) f |= 2u;
+            }
+            acc |= f;
+            if constexpr (kClaims) {
+                const double vx[4] = {A.x, A.x1, B.x, B.x1}, vy[4] = {A.y, A.y1, B.y, B.y1};
+                strip_claims(tc.t, tc.owner, uniform, inv_dx, inv_dy, vx, vy, d, c);
+            }
+        }
+        A = B;
+        B = C;
+        d = dup;
+        bad = bad_up;
+    }
+    for (int off = 32; off > 0; off >>= 1) acc |= __shfl_down(acc, off);
+    if (lane == 0) {
+        const unsigned cur = __hip_atomic_load(flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((cur | acc) != cur) atomicOr(flags, acc);
+    }
+}
+
 // ring positions -> coordinates, for the host pocket builder (bit 5 of flags: a non-finite one)
 __global__ void k_gd_ring(Grid g, double* rx, double* ry, unsigned* flags) {
     const int64_t a = g.nh - 1, b = g.nv - 1, L = 2 * a + 2 * b;
@@ -2395,10 +2615,26 @@ __global__ void k_fill_i32(int* p, int64_t n, int v) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = v;
 }
 
+// the strip cell pass's grid for `rows` cell rows of a lattice nh points wide: a wave per strip segment,
+// the segments as long as fills the device's wave slots (4 waves per SIMD) once - one round of waves
+unsigned gd_cu_count();
+struct StripGrid {
+    unsigned blocks;
+    int seg_rows;
+};
+StripGrid strip_grid(int nh, int rows) {
+    const int64_t nstrip = (nh - 1 + kStripCells - 1) / kStripCells;
+    const int64_t slots = (int64_t)gd_cu_count() * 16;
+    const int64_t nseg_max = slots / nstrip > 0 ? slots / nstrip : 1;
+    const int seg_rows = (int)((rows + nseg_max - 1) / nseg_max) > 8 ? (int)((rows + nseg_max - 1) / nseg_max) : 8;
+    const int64_t units = nstrip * ((rows + seg_rows - 1) / seg_rows);
+    return StripGrid{(unsigned)((units + kStripThreads / 64 - 1) / (kStripThreads / 64)), seg_rows};
+}
+
 // the cell pass over the window's `rows` cell rows
 int launch_cells(const Grid& g, uint8_t* diag, double tol, unsigned* d_flags, int rows, hipStream_t s) {
-    const int64_t tiles = (int64_t)((rows + kCellTile - 1) / kCellTile) * ((g.nh - 1 + kCellTile - 1) / kCellTile);
-    k_gd_cells_tiled<<<(unsigned)(tiles < 4096 ? tiles : 4096), kCellTile * kCellTile, 0, s>>>(g, diag, tol, d_flags);
+    const StripGrid sg = strip_grid(g.nh, rows);
+    k_gd_cells_strip<<<sg.blocks, kStripThreads, 0, s>>>(g, diag, tol, d_flags, sg.seg_rows);
     return launch_status("k_gd_cells");
 }
 unsigned gd_cu_count() {  // the device's CUs (one resident 1024-thread patch workgroup each)
@@ -2726,9 +2962,8 @@ int akb_gd_cells_claims_f64(const double* x, const double* y, int nv, int nh, ui
     if (st) return st;
     Grid g{x, y, nv, nh, diag, 0, nullptr, nullptr, nullptr, nullptr, nullptr};
     const TileClaims tc{Targets{gx, gy, mx, my}, owner};
-    const int64_t tiles = (int64_t)((nv - 1 + kCellTile - 1) / kCellTile) * ((nh - 1 + kCellTile - 1) / kCellTile);
-    k_gd_cells_tiled<true><<<(unsigned)(tiles < 4096 ? tiles : 4096), kCellTile * kCellTile, 0, s>>>(g, diag, tol, d_flags,
-                                                                                                   tc);
+    const StripGrid sg = strip_grid(nh, nv - 1);
+    k_gd_cells_strip<true><<<sg.blocks, kStripThreads, 0, s>>>(g, diag, tol, d_flags, sg.seg_rows, tc);
     return launch_status("k_gd_cells_claims");
 }
 
