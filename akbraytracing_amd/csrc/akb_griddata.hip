@@ -319,9 +319,8 @@ __device__ __forceinline__ void claim_one(const Grid& g, const Targets& t, const
 // candidate index range of the targets of an ascending linspace axis a (m points) in [lo, hi):
 // the real-valued indices of lo and hi from the axis's own step, widened by 1e-6 of an index (the
 // axis values sit within a few ulp of a0 + c * step); empty when no integer falls between them
-__device__ __forceinline__ bool axis_range(const double* a, int m, double inv_step, double lo, double hi, int& c0,
-                                           int& c1) {
-    const double a0 = a[0];
+__device__ __forceinline__ bool axis_range_at(double a0, int m, double inv_step, double lo, double hi, int& c0,
+                                              int& c1) {
     const double e0 = (lo - a0) * inv_step - 1e-6, e1 = (hi - a0) * inv_step + 1e-6;
     if (!(e1 >= 0.0) || !(e0 <= (double)(m - 1))) return false;
     const double f0 = ceil(fmax(e0, 0.0)), f1 = floor(fmin(e1, (double)(m - 1)));
@@ -329,6 +328,10 @@ __device__ __forceinline__ bool axis_range(const double* a, int m, double inv_st
     c0 = (int)f0;
     c1 = (int)f1 + 1;
     return true;
+}
+__device__ __forceinline__ bool axis_range(const double* a, int m, double inv_step, double lo, double hi, int& c0,
+                                           int& c1) {
+    return axis_range_at(a[0], m, inv_step, lo, hi, c0, c1);
 }
 
 // whether axis a (m points, ascending) is a linspace: strictly increasing and every point within
@@ -608,7 +611,8 @@ __global__ void __launch_bounds__(kCellTile * kCellTile) k_gd_cells_tiled(Grid g
 }
 
 // ---- the cell pass as wave strips: a wave's 64 lanes hold 64 consecutive vertex columns and walk
-// a segment of cell rows upwards (as many rows as puts one wave on every resident slot), a vertex row per step (two coalesced loads, issued two steps ahead);
+// a segment of cell rows upwards (as many rows as puts one wave on every resident slot), a vertex row
+// per step (two coalesced loads, issued kStripAhead steps ahead);
 // the columns h + 1 and h + 2 come from the lanes above by DPP (wave_shl), a cell's right
 // neighbour's diagonal likewise, and the diagonal of the row above is formed one step early - so no
 // LDS, no barrier, each vertex loaded once (plus two halo rows per segment) and each diagonal formed
@@ -616,7 +620,7 @@ __global__ void __launch_bounds__(kCellTile * kCellTile) k_gd_cells_tiled(Grid g
 // test is k_gd_cells_tiled's arithmetic on the same values: the same diagonals and flags. With
 // kClaims each cell claims its targets: the candidates from the cell's own box (axis_range on
 // linspace axes, else the binary search), then tile_claims' per-triangle predicate - the same owners.
-constexpr int kStripCells = 62, kStripThreads = 256;
+constexpr int kStripCells = 62, kStripThreads = 256, kStripAhead = 3;
 
 __device__ __forceinline__ int lane_up(int v) {  // lane i gets lane i + 1's value (lane 63: 0)
     return __builtin_amdgcn_update_dpp(0, v, 0x130, 0xf, 0xf, false);
@@ -667,16 +671,19 @@ __device__ __forceinline__ bool strip_edge_bad(double x0, double y0, double mxa,
 }
 
 // a cell's claims: its corners (p00, p01, p10, p11) in registers, d its diagonal, c its index
+// (ax0, ay0: the axes' first values, read once - a read of the axes here would be a flat load, whose
+// wait drains the row loads in flight)
 __device__ __forceinline__ void strip_claims(const Targets& t, int* owner, bool uniform, double inv_dx, double inv_dy,
-                                               const double (&vx)[4], const double (&vy)[4], int d, int64_t c) {
+                                             double ax0, double ay0, const double (&vx)[4], const double (&vy)[4], int d,
+                                             int64_t c) {
     const double xlo = fmin(fmin(vx[0], vx[1]), fmin(vx[2], vx[3])), xhi = fmax(fmax(vx[0], vx[1]), fmax(vx[2], vx[3]));
     const double ylo = fmin(fmin(vy[0], vy[1]), fmin(vy[2], vy[3])), yhi = fmax(fmax(vy[0], vy[1]), fmax(vy[2], vy[3]));
     const double padx = (xhi - xlo) * 1e-9, pady = (yhi - ylo) * 1e-9;
     int c0, c1, r0, r1;
     bool hit;
     if (uniform) {
-        hit = axis_range(t.gx, t.mx, inv_dx, xlo - padx, xhi + padx, c0, c1) &&
-              axis_range(t.gy, t.my, inv_dy, ylo - pady, yhi + pady, r0, r1);
+        hit = axis_range_at(ax0, t.mx, inv_dx, xlo - padx, xhi + padx, c0, c1) &&
+              axis_range_at(ay0, t.my, inv_dy, ylo - pady, yhi + pady, r0, r1);
     } else {
         c0 = lower_idx(t.gx, t.mx, xlo - padx);
         c1 = lower_idx(t.gx, t.mx, xhi + padx);
@@ -741,7 +748,7 @@ __global__ void __launch_bounds__(kStripThreads) k_gd_cells_strip(Grid g, uint8_
     const int lane = threadIdx.x & 63;
     const int unit = (int)blockIdx.x * (kStripThreads / 64) + (int)(threadIdx.x >> 6);
     bool uniform = false;
-    double inv_dx = 0.0, inv_dy = 0.0;
+    double inv_dx = 0.0, inv_dy = 0.0, ax0 = 0.0, ay0 = 0.0;
     if constexpr (kClaims) {
         __shared__ double sax[2 * kClaimAxisLds];
         if (tc.t.mx <= kClaimAxisLds && tc.t.my <= kClaimAxisLds) {
@@ -754,71 +761,82 @@ __global__ void __launch_bounds__(kStripThreads) k_gd_cells_strip(Grid g, uint8_
         uniform = axes_uniform(tc.t);
         inv_dx = inv_step(tc.t.gx, tc.t.mx);
         inv_dy = inv_step(tc.t.gy, tc.t.my);
+        ax0 = tc.t.gx[0];
+        ay0 = tc.t.gy[0];
     }
     if (unit >= nstrip * nseg) return;  // (after the workgroup's barriers)
     const int seg = unit / nstrip, strip = unit - seg * nstrip;
     const int ih = strip * kStripCells + lane, iv0 = r_lo + seg * seg_rows;
     const int iv1 = min(iv0 + seg_rows, r_hi);
-    // vertex row r at this lane's column (0 outside the lattice and past the window's rows + 1)
+    // vertex row r at this lane's column, the index clamped into the lattice and the window's rows + 1
+    // (no branch: the wait for a slot then counts only the loads issued after it). Clamped values
+    // reach no test: rows past them only feed diagonals that are masked, columns past nh - 1 only
+    // right-edge tests that are skipped.
+    const int r_top = min(g.nv - 1, r_hi + 1), hc = min(ih, g.nh - 1);
     auto load = [&](int r, double& x, double& y) {
-        x = y = 0.0;
-        if (r < g.nv && r <= r_hi + 1 && ih < g.nh) {
-            const int64_t q = (int64_t)r * g.nh + ih;
-            x = g.x[q];
-            y = g.y[q];
-        }
+        const int64_t q = (int64_t)min(r, r_top) * g.nh + hc;
+        x = g.x[q];
+        y = g.y[q];
     };
-    double x0, y0, x1, y1, x2, y2, x3, y3;
+    // rows iv0 + 2 on in a ring of kStripAhead + 1 register slots (row r in slot (r - iv0) % D), three
+    // rows in flight; the step loop unrolled by D, so every slot is a fixed register (a rotation by
+    // moves would wait for each load one step after issuing it)
+    constexpr int D = kStripAhead + 1;
+    double sx[D], sy[D];
+#pragma unroll
+    for (int k = 2; k < 2 + kStripAhead; ++k) load(iv0 + k, sx[k % D], sy[k % D]);
+    double x0, y0, x1, y1;
     load(iv0, x0, y0);
     load(iv0 + 1, x1, y1);
-    load(iv0 + 2, x2, y2);
-    load(iv0 + 3, x3, y3);
     StripRow A = strip_row(x0, y0), B = strip_row(x1, y1);
     const bool col_cell = ih < g.nh - 1;                   // a cell at this column
     const bool own_lane = lane < kStripCells && col_cell;  // (lanes 62 and 63 own none)
     double bad = 0.0;
     int d = col_cell ? strip_diag(A, B, bad) : 0;
     unsigned acc = 0;
-    for (int iv = iv0; iv < iv1; ++iv) {
-        // row iv + 2 arrived (issued two steps ago); row iv + 4 issued now
-        const StripRow C = strip_row(x2, y2);
-        x2 = x3;
-        y2 = y3;
-        load(iv + 4, x3, y3);
-        // the row above's diagonal (this lane's next step) and the right neighbour's on this row
-        const int jv = iv + 1;
-        double bad_up = 0.0;
-        const int dup = (col_cell && jv < g.nv - 1 && jv <= r_hi) ? strip_diag(B, C, bad_up) : 0;
-        const int dn = lane_up(d);
-        if (own_lane) {
-            const int64_t c = (int64_t)iv * (g.nh - 1) + ih;
-            diag[c] = (uint8_t)d;
-            unsigned f = bad > 0 ? 1u : 0u;
-            if (!isfinite(A.x) || !isfinite(A.y)) f |= 32u;
-            {
-                const double o = orient(A.x, A.y, A.x1, A.y1, B.x1, B.y1);
-                f |= o > 0 ? 8u : (o < 0 ? 16u : 1u);
+    for (int j0 = 0; j0 < iv1 - iv0; j0 += D) {
+#pragma unroll
+        for (int u = 0; u < D; ++u) {
+            const int iv = iv0 + j0 + u;
+            if (iv >= iv1) break;
+            // row iv + 2 arrived (issued kStripAhead steps ago); row iv + 2 + kStripAhead issued now
+            const StripRow C = strip_row(sx[(u + 2) % D], sy[(u + 2) % D]);
+            load(iv + 2 + kStripAhead, sx[(u + 2 + kStripAhead) % D], sy[(u + 2 + kStripAhead) % D]);
+            // the row above's diagonal (this lane's next step) and the right neighbour's on this row
+            const int jv = iv + 1;
+            double bad_up = 0.0;
+            const int dup = (col_cell && jv < g.nv - 1 && jv <= r_hi) ? strip_diag(B, C, bad_up) : 0;
+            const int dn = lane_up(d);
+            if (own_lane) {
+                const int64_t c = (int64_t)iv * (g.nh - 1) + ih;
+                diag[c] = (uint8_t)d;
+                unsigned f = bad > 0 ? 1u : 0u;
+                if (!isfinite(A.x) || !isfinite(A.y)) f |= 32u;
+                {
+                    const double o = orient(A.x, A.y, A.x1, A.y1, B.x1, B.y1);
+                    f |= o > 0 ? 8u : (o < 0 ? 16u : 1u);
+                }
+                if (ih + 1 < g.nh - 1) {  // right edge p01-p11 against the next cell's left triangle
+                    const double mx = d == 0 ? A.x : B.x, my = d == 0 ? A.y : B.y;
+                    const double ox = dn == 0 ? B.x2 : A.x2, oy = dn == 0 ? B.y2 : A.y2;
+                    if (strip_edge_bad(A.x1, A.y1, mx, my, B.x1, B.y1, ox, oy, tol)) f |= 2u;
+                }
+                if (iv + 1 < g.nv - 1) {  // top edge p10-p11 against the next row's bottom triangle
+                    const double mx = d == 0 ? A.x : A.x1, my = d == 0 ? A.y : A.y1;
+                    const double ox = dup == 0 ? C.x1 : C.x, oy = dup == 0 ? C.y1 : C.y;
+                    if (strip_edge_bad(B.x, B.y, mx, my, B.x1, B.y1, ox, oy, tol)) f |= 2u;
+                }
+                acc |= f;
+                if constexpr (kClaims) {
+                    const double vx[4] = {A.x, A.x1, B.x, B.x1}, vy[4] = {A.y, A.y1, B.y, B.y1};
+                    strip_claims(tc.t, tc.owner, uniform, inv_dx, inv_dy, ax0, ay0, vx, vy, d, c);
+                }
             }
-            if (ih + 1 < g.nh - 1) {  // right edge p01-p11 against the next cell's left triangle
-                const double mx = d == 0 ? A.x : B.x, my = d == 0 ? A.y : B.y;
-                const double ox = dn == 0 ? B.x2 : A.x2, oy = dn == 0 ? B.y2 : A.y2;
-                if (strip_edge_bad(A.x1, A.y1, mx, my, B.x1, B.y1, ox, oy, tol)) f |= 2u;
-            }
-            if (iv + 1 < g.nv - 1) {  // top edge p10-p11 against the next row's bottom triangle
-                const double mx = d == 0 ? A.x : A.x1, my = d == 0 ? A.y : A.y1;
-                const double ox = dup == 0 ? C.x1 : C.x, oy = dup == 0 ? C.y1 : C.y;
-                if (strip_edge_bad(B.x, B.y, mx, my, B.x1, B.y1, ox, oy, tol)) f |= 2u;
-            }
-            acc |= f;
-            if constexpr (kClaims) {
-                const double vx[4] = {A.x, A.x1, B.x, B.x1}, vy[4] = {A.y, A.y1, B.y, B.y1};
-                strip_claims(tc.t, tc.owner, uniform, inv_dx, inv_dy, vx, vy, d, c);
-            }
+            A = B;
+            B = C;
+            d = dup;
+            bad = bad_up;
         }
-        A = B;
-        B = C;
-        d = dup;
-        bad = bad_up;
     }
     for (int off = 32; off > 0; off >>= 1) acc |= __shfl_down(acc, off);
     if (lane == 0) {

@@ -632,8 +632,28 @@ __device__ __forceinline__ double zpow(double z, int k) {  // z^k by binary powe
     return r;
 }
 
-template <int P, int SEG>
-__device__ void spline_line_reg(double* c, int n, int s, int sub, unsigned long long* ck = nullptr) {
+// a lane group's neighbour values by DPP row shifts (P lanes, P dividing 16): the value of lane
+// sub - 1 (0 for sub 0) and of lane sub + 1 (0 for the top lane)
+template <int kCtrl>
+__device__ __forceinline__ double dpp_mov(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffLL), kCtrl, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), kCtrl, 0xf, 0xf, false);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+template <int P>
+__device__ __forceinline__ double seg_from_below(double v, int sub) {
+    const double t = dpp_mov<0x111>(v);  // row_shr:1
+    return sub == 0 ? 0.0 : t;
+}
+template <int P>
+__device__ __forceinline__ double seg_from_above(double v, int sub) {
+    const double t = dpp_mov<0x101>(v);  // row_shl:1
+    return sub == P - 1 ? 0.0 : t;
+}
+
+template <int P, int SEG, int s>  // s: the line's stride in LDS (a constant: every read an immediate offset)
+__device__ void spline_line_reg(double* c, int n, int sub, unsigned long long* ck = nullptr) {
     const double z = sqrt(3.0) - 2.0;
     const double gain = (1.0 - z) * (1.0 - 1.0 / z);
     const int lane = threadIdx.x & 63, base = lane & ~(P - 1);
@@ -644,15 +664,12 @@ __device__ void spline_line_reg(double* c, int n, int s, int sub, unsigned long 
     for (int k = 0; k < SEG; ++k) v[k] = k < len ? c[(b0 + k) * s] * gain : 0.0;
     // the gained values at 0, n - 2 and n - 1 (their owners' registers, summed over the group: the
     // others add zeros)
-    auto at = [&](int idx) {
+    auto at = [&](int idx) {  // one read from the owner's registers
         double own = 0.0;
 #pragma unroll
         for (int k = 0; k < SEG; ++k)
             if (k < len && b0 + k == idx) own = v[k];
-        double t = 0.0;
-#pragma unroll
-        for (int q = 0; q < P; ++q) t += __shfl(own, base + q);
-        return t;
+        return __shfl(own, base + idx / seg);
     };
     if (ck) ck[0] = wall_clock64();
     if (n > 1) {
@@ -677,9 +694,12 @@ __device__ void spline_line_reg(double* c, int n, int s, int sub, unsigned long 
                 }
             }
         }
-        double tot = 0.0;
+        // the parts summed in segment order (((0 + p0) + p1) + ...): passed up the group, then read
+        // from its top lane
+        double run = 0.0;
 #pragma unroll
-        for (int q = 0; q < P; ++q) tot += __shfl(part, base + q);
+        for (int q = 0; q < P - 1; ++q) run = seg_from_below<P>(run + part, sub);
+        const double tot = __shfl(run + part, base + P - 1);
         const double y0 = (at(0) + zn1 * at(n - 1) + tot) / (1.0 - zn1 * zn1);
         const double zl = zpow(z, len);  // z^(segment length), 1 for an empty segment
         if (ck) ck[1] = wall_clock64();
@@ -691,16 +711,11 @@ __device__ void spline_line_reg(double* c, int n, int s, int sub, unsigned long 
                 u = k == 0 ? (b0 == 0 ? y0 : v[0]) : v[k] + z * u;
                 v[k] = u;
             }
-        double ein = 0.0;  // the true value at b0 - 1
-        {
-            double e = 0.0;
+        // the true value at b0 - 1: e_0 = 0, e_{q+1} = u_q + z^len_q e_q, passed up the group one lane a
+        // step (after step s lanes 0 .. s + 1 hold theirs)
+        double ein = 0.0;
 #pragma unroll
-            for (int q = 0; q < P; ++q) {
-                const double uq = __shfl(u, base + q), zq = __shfl(zl, base + q);
-                if (q == sub) ein = e;
-                e = uq + zq * e;
-            }
-        }
+        for (int q = 0; q < P - 1; ++q) ein = seg_from_below<P>(u + zl * ein, sub);
         {
             double zk = z;
 #pragma unroll
@@ -721,16 +736,10 @@ __device__ void spline_line_reg(double* c, int n, int s, int sub, unsigned long 
                 w = (top && k == len - 1) ? next : z * (w - v[k]);
                 v[k] = w;
             }
-        double bin = 0.0;  // the true value at b0 + len
-        {
-            double e = 0.0;
+        // the true value at b0 + len, passed down the group likewise
+        double bin = 0.0;
 #pragma unroll
-            for (int q = P - 1; q >= 0; --q) {
-                const double wq = __shfl(w, base + q), zq = __shfl(zl, base + q);
-                if (q == sub) bin = e;
-                e = wq + zq * e;
-            }
-        }
+        for (int q = 0; q < P - 1; ++q) bin = seg_from_above<P>(w + zl * bin, sub);
         {
             double zk = z;
 #pragma unroll
@@ -748,13 +757,14 @@ __device__ void spline_line_reg(double* c, int n, int s, int sub, unsigned long 
 }
 
 // the post's B-spline prefilter for arrays of up to kPostFuse x kPostFuse: workgroup 0 the map,
-// 1 the mask, each array in LDS (row pitch nx + 1), both axes, eight lanes per line
+// 1 the mask, each array in LDS (row pitch kPostFuse + 1), both axes, eight lanes per line
 constexpr int kSplineLanes = 8, kSplinePostThreads = kSplineLanes * kPostFuse;
 __global__ void __launch_bounds__(kSplinePostThreads) k_spline_post(double* __restrict__ coef, int ny, int nx,
                                                                      unsigned long long* clocks) {
     __shared__ double a[kPostFuse * (kPostFuse + 1)];
     const int64_t total = (int64_t)ny * nx;
-    const int pitch = nx + 1, tid = threadIdx.x;
+    constexpr int pitch = kPostFuse + 1;
+    const int tid = threadIdx.x;
     const bool clk = blockIdx.x == 0 && tid == 0;  // workgroup 0's phase clocks (diagnostics)
     if (clk) clocks[0] = wall_clock64();
     double* base = coef + (int64_t)blockIdx.x * total;
@@ -777,10 +787,10 @@ __global__ void __launch_bounds__(kSplinePostThreads) k_spline_post(double* __re
     if (clk) clocks[1] = wall_clock64();
     constexpr int Q = kSplineLanes, SEG = kPostFuse / kSplineLanes;
     if (tid / Q < nx)  // axis 0: the columns
-        spline_line_reg<Q, SEG>(a + tid / Q, ny, pitch, tid % Q, clk ? clocks + 4 : nullptr);
+        spline_line_reg<Q, SEG, pitch>(a + tid / Q, ny, tid % Q, clk ? clocks + 4 : nullptr);
     __syncthreads();
     if (clk) clocks[2] = wall_clock64();
-    if (tid / Q < ny) spline_line_reg<Q, SEG>(a + (tid / Q) * pitch, nx, 1, tid % Q);  // axis 1: the rows
+    if (tid / Q < ny) spline_line_reg<Q, SEG, 1>(a + (tid / Q) * pitch, nx, tid % Q);  // axis 1: the rows
     __syncthreads();
     if (clk) clocks[3] = wall_clock64();
     for (int64_t k = tid; k < total; k += kSplinePostThreads) {
