@@ -620,10 +620,10 @@ __global__ void __launch_bounds__(kCellTile * kCellTile) k_gd_cells_tiled(Grid g
 // test is k_gd_cells_tiled's arithmetic on the same values: the same diagonals and flags. With
 // kClaims each cell claims its targets: the candidates from the cell's own box (axis_range on
 // linspace axes, else the binary search), then tile_claims' per-triangle predicate - the same owners.
-constexpr int kStripCells = 62, kStripThreads = 256, kStripAhead = 3;
+constexpr int kStripCells = 62, kStripThreads = 256, kStripAhead = 2;
 
-__device__ __forceinline__ int lane_up(int v) {  // lane i gets lane i + 1's value (lane 63: 0)
-    return __builtin_amdgcn_update_dpp(0, v, 0x130, 0xf, 0xf, false);
+__device__ __forceinline__ int lane_up(int v) {  // lane i gets lane i + 1's value (lane 63: 0, bound_ctrl)
+    return __builtin_amdgcn_mov_dpp(v, 0x130, 0xf, 0xf, true);
 }
 __device__ __forceinline__ double lane_up(double v) {
     const long long b = __double_as_longlong(v);
@@ -681,9 +681,9 @@ __device__ __forceinline__ void strip_claims(const Targets& t, int* owner, bool 
     const double padx = (xhi - xlo) * 1e-9, pady = (yhi - ylo) * 1e-9;
     int c0, c1, r0, r1;
     bool hit;
-    if (uniform) {
-        hit = axis_range_at(ax0, t.mx, inv_dx, xlo - padx, xhi + padx, c0, c1) &&
-              axis_range_at(ay0, t.my, inv_dy, ylo - pady, yhi + pady, r0, r1);
+    if (uniform) {  // the rows first: a target row meets one cell row in ~25 at C3, so most waves skip the rest
+        hit = axis_range_at(ay0, t.my, inv_dy, ylo - pady, yhi + pady, r0, r1) &&
+              axis_range_at(ax0, t.mx, inv_dx, xlo - padx, xhi + padx, c0, c1);
     } else {
         c0 = lower_idx(t.gx, t.mx, xlo - padx);
         c1 = lower_idx(t.gx, t.mx, xhi + padx);
@@ -778,9 +778,9 @@ __global__ void __launch_bounds__(kStripThreads) k_gd_cells_strip(Grid g, uint8_
         x = g.x[q];
         y = g.y[q];
     };
-    // rows iv0 + 2 on in a ring of kStripAhead + 1 register slots (row r in slot (r - iv0) % D), three
-    // rows in flight; the step loop unrolled by D, so every slot is a fixed register (a rotation by
-    // moves would wait for each load one step after issuing it)
+    // rows iv0 + 2 on in a ring of kStripAhead + 1 register slots (row r in slot (r - iv0) % D), two
+    // rows in flight; the step loop unrolled by D = 3, so every slot is a fixed register (a rotation by
+    // moves would wait for each load one step after issuing it) and so are the three rows A, B, C
     constexpr int D = kStripAhead + 1;
     double sx[D], sy[D];
 #pragma unroll
@@ -1641,8 +1641,12 @@ __device__ __forceinline__ void cone_ring_vertex(const Grid& g, const ConeBand& 
     const double fi[1] = {a.f[i]};
     const bool pre = a.st.mode == 2 && sub == 0;
     const double ppx = pre ? a.gprev[2 * i] : 0.0, ppy = pre ? a.gprev[2 * i + 1] : 0.0;
-    const bool slotted = W == 8 && a.slots;  // (the same chord per lane as chord_sums<1, 8> of at most eight)
+    // (slotted: lane sub takes the chords sub and sub + 4 - two for a 4-lane group, their sums added
+    // as the 8-lane butterfly's first level adds them - then the group's butterfly: the same bits as
+    // chord_sums<1, 8> of at most eight)
+    const bool slotted = (W == 8 || W == 4) && a.slots;
     const int32_t j = slotted ? a.slots[r * 8 + sub] : -1;
+    const int32_t j2 = slotted && W == 4 ? a.slots[r * 8 + sub + 4] : -1;
     GradAcc<1> D;
     if (sub == 0) {
         const int iv = (int)(i / g.nh), ih = (int)(i - (int64_t)iv * g.nh);
@@ -1650,10 +1654,18 @@ __device__ __forceinline__ void cone_ring_vertex(const Grid& g, const ConeBand& 
     }
     GradAcc<1> A;
     if (slotted) {
-        if (j >= 0) {
-            const double fj[1] = {a.f[j]}, gxj[1] = {a.gin ? a.gin[2 * (int64_t)j] : 0.0},
-                         gyj[1] = {a.gin ? a.gin[2 * (int64_t)j + 1] : 0.0};
-            acc_edge<1>(A, edge_geom(g.x[j] - xi, g.y[j] - yi), fi, fj, gxj, gyj);
+        auto chord = [&](int32_t c, GradAcc<1>& C) {
+            if (c >= 0) {
+                const double fj[1] = {a.f[c]}, gxj[1] = {a.gin ? a.gin[2 * (int64_t)c] : 0.0},
+                             gyj[1] = {a.gin ? a.gin[2 * (int64_t)c + 1] : 0.0};
+                acc_edge<1>(C, edge_geom(g.x[c] - xi, g.y[c] - yi), fi, fj, gxj, gyj);
+            }
+        };
+        chord(j, A);
+        if (W == 4) {
+            GradAcc<1> B;
+            chord(j2, B);
+            acc_add<1>(A, B);
         }
         acc_reduce<1, W>(A);
     } else {
@@ -1794,20 +1806,28 @@ __global__ void __launch_bounds__(kBandThreads) __attribute__((amdgpu_waves_per_
         return;
     }
     const int64_t L = 2 * (int64_t)(g.nh - 1) + 2 * (int64_t)(g.nv - 1);
-    const int lane = threadIdx.x & 63, sub = lane & 7;
+    const int lane = threadIdx.x & 63;
     const int64_t w0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t nw = ((int64_t)nr8 * blockDim.x) >> 6;
-    for (int64_t r0 = w0 * 8; r0 < L; r0 += nw * 8) {
-        const int64_t r = r0 + (lane >> 3);
-        const bool big = r < L && g.xptr[r + 1] - g.xptr[r] > 8;
-        if (r < L && !big) cone_ring_vertex<8>(g, a, r, sub);
-        unsigned long long m = __ballot(big && sub == 0);
-        while (m) {  // wave-uniform
-            const int q = __builtin_ctzll(m);
-            m &= m - 1;
-            cone_ring_vertex<64>(g, a, r0 + (q >> 3), lane);
+    auto ring = [&](auto gw) {  // vertices of GW lanes each, 64 / GW a wave
+        constexpr int GW = decltype(gw)::value, VPW = 64 / GW;
+        const int sub = lane & (GW - 1);
+        for (int64_t r0 = w0 * VPW; r0 < L; r0 += nw * VPW) {
+            const int64_t r = r0 + lane / GW;
+            const bool big = r < L && g.xptr[r + 1] - g.xptr[r] > 8;
+            if (r < L && !big) cone_ring_vertex<GW>(g, a, r, sub);
+            unsigned long long m = __ballot(big && sub == 0);
+            while (m) {  // wave-uniform
+                const int q = __builtin_ctzll(m);
+                m &= m - 1;
+                cone_ring_vertex<64>(g, a, r0 + q / GW, lane);
+            }
         }
-    }
+    };
+    // with the slot table four lanes a vertex (half the ring's workgroups: with the tiles one round of
+    // workgroups at two per CU)
+    if (a.slots) ring(std::integral_constant<int, 4>{});
+    else ring(std::integral_constant<int, 8>{});
     if (a.clk) band_clock(a.clk + 4, 0, t0);
 }
 
@@ -2903,7 +2923,7 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
                 const double* gin = j == 1 ? nullptr : gb[(j - 1) % 3];
                 const double* gprev = j >= 3 ? gb[(j + 1) % 3] : nullptr;
                 const BandTiles bt = band_tiles(g.nv, g.nh, 2 * K + 3 - j);
-                const unsigned nr8 = (unsigned)(((L + 7) / 8 * 64 + kBandThreads - 1) / kBandThreads);
+                const unsigned nr8 = (unsigned)(((L + 15) / 16 * 64 + kBandThreads - 1) / kBandThreads);  // 4 lanes a vertex
                 const ConeBand a{fv, gin, gprev, gb[j % 3], steps[j], band, patch_timer().on ? patch_timer().clk : nullptr,
                                  slots};
                 k_gd_cone_band<<<bt.total + nr8, kBandThreads, 0, s>>>(g, bt, a, (int)nr8);
@@ -2911,7 +2931,7 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
             }
             if (d_change) {  // one more plain sweep, y from x_K to depth K + 2 (the band targets' corners)
                 const BandTiles bt = band_tiles(g.nv, g.nh, K + 2);
-                const unsigned nr8 = (unsigned)(((L + 7) / 8 * 64 + kBandThreads - 1) / kBandThreads);
+                const unsigned nr8 = (unsigned)(((L + 15) / 16 * 64 + kBandThreads - 1) / kBandThreads);
                 const ConeBand a{fv, gb[K % 3], nullptr, gb[(K + 1) % 3], ConeStep{0, 1.0}, band,
                                  patch_timer().on ? patch_timer().clk : nullptr, slots};
                 k_gd_cone_band<<<bt.total + nr8, kBandThreads, 0, s>>>(g, bt, a, (int)nr8);
