@@ -1631,22 +1631,17 @@ __device__ __forceinline__ void band_solve(const ConeBand& a, int64_t i, const G
 // (chord_sums: each lane a strided part, the group's butterfly), then the lead lane adds the
 // vertex's lattice-edge sums and solves
 template <int W>
-__device__ __forceinline__ void cone_ring_vertex(const Grid& g, const ConeBand& a, int64_t r, int sub) {
+__device__ __forceinline__ void cone_ring_vertex(const Grid& g, const ConeBand& a, int64_t r, int sub, int32_t j = -1) {
     const int64_t n = (int64_t)g.nv * g.nh;
     const int64_t i = ring_vertex(g, r);
-    // every load that needs only r first: the vertex, x_{j-2} there, its chord slot (W = 8 with the
-    // slot table: the chord's index without the xptr level) in flight during the lattice edges,
-    // then the chord's data - two memory latencies for the vertex instead of four
+    // every load that needs only r first: the vertex, x_{j-2} there and the lattice neighbours (with
+    // the slot table the chord j came with the vertex's big test, so its data is in flight with
+    // them: two memory latencies for the vertex)
     const double xi = g.x[i], yi = g.y[i];
     const double fi[1] = {a.f[i]};
     const bool pre = a.st.mode == 2 && sub == 0;
     const double ppx = pre ? a.gprev[2 * i] : 0.0, ppy = pre ? a.gprev[2 * i + 1] : 0.0;
-    // (slotted: lane sub takes the chords sub and sub + 4 - two for a 4-lane group, their sums added
-    // as the 8-lane butterfly's first level adds them - then the group's butterfly: the same bits as
-    // chord_sums<1, 8> of at most eight)
-    const bool slotted = (W == 8 || W == 4) && a.slots;
-    const int32_t j = slotted ? a.slots[r * 8 + sub] : -1;
-    const int32_t j2 = slotted && W == 4 ? a.slots[r * 8 + sub + 4] : -1;
+    const bool slotted = W == 8 && a.slots;  // (the same chord per lane as chord_sums<1, 8> of at most eight)
     GradAcc<1> D;
     if (sub == 0) {
         const int iv = (int)(i / g.nh), ih = (int)(i - (int64_t)iv * g.nh);
@@ -1654,18 +1649,10 @@ __device__ __forceinline__ void cone_ring_vertex(const Grid& g, const ConeBand& 
     }
     GradAcc<1> A;
     if (slotted) {
-        auto chord = [&](int32_t c, GradAcc<1>& C) {
-            if (c >= 0) {
-                const double fj[1] = {a.f[c]}, gxj[1] = {a.gin ? a.gin[2 * (int64_t)c] : 0.0},
-                             gyj[1] = {a.gin ? a.gin[2 * (int64_t)c + 1] : 0.0};
-                acc_edge<1>(C, edge_geom(g.x[c] - xi, g.y[c] - yi), fi, fj, gxj, gyj);
-            }
-        };
-        chord(j, A);
-        if (W == 4) {
-            GradAcc<1> B;
-            chord(j2, B);
-            acc_add<1>(A, B);
+        if (j >= 0) {
+            const double fj[1] = {a.f[j]}, gxj[1] = {a.gin ? a.gin[2 * (int64_t)j] : 0.0},
+                         gyj[1] = {a.gin ? a.gin[2 * (int64_t)j + 1] : 0.0};
+            acc_edge<1>(A, edge_geom(g.x[j] - xi, g.y[j] - yi), fi, fj, gxj, gyj);
         }
         acc_reduce<1, W>(A);
     } else {
@@ -1678,12 +1665,14 @@ __device__ __forceinline__ void cone_ring_vertex(const Grid& g, const ConeBand& 
 }
 
 // the ring's chord slot table for the band sweeps: slots[8 r + k] = ring vertex r's k-th chord
-// neighbour (xidx order), -1 past its chords (a vertex of more than eight keeps the xptr path)
+// neighbour (xidx order), -1 past its chords; a vertex of more than eight (the xptr path, a wave
+// each) has kSlotBig in all eight, so a lane's one slot load also tells it which path its vertex takes
+constexpr int32_t kSlotBig = -2;
 __global__ void k_gd_chord_slots(Grid g, int32_t* slots, int64_t L) {
     for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < L; r += (int64_t)gridDim.x * blockDim.x) {
         const int32_t k0 = g.xptr[r], cnt = g.xptr[r + 1] - k0;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) slots[r * 8 + k] = k < cnt ? g.xidx[k0 + k] : -1;
+        for (int k = 0; k < 8; ++k) slots[r * 8 + k] = cnt > 8 ? kSlotBig : k < cnt ? g.xidx[k0 + k] : -1;
     }
 }
 
@@ -1809,25 +1798,25 @@ __global__ void __launch_bounds__(kBandThreads) __attribute__((amdgpu_waves_per_
     const int lane = threadIdx.x & 63;
     const int64_t w0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t nw = ((int64_t)nr8 * blockDim.x) >> 6;
-    auto ring = [&](auto gw) {  // vertices of GW lanes each, 64 / GW a wave
-        constexpr int GW = decltype(gw)::value, VPW = 64 / GW;
-        const int sub = lane & (GW - 1);
-        for (int64_t r0 = w0 * VPW; r0 < L; r0 += nw * VPW) {
-            const int64_t r = r0 + lane / GW;
-            const bool big = r < L && g.xptr[r + 1] - g.xptr[r] > 8;
-            if (r < L && !big) cone_ring_vertex<GW>(g, a, r, sub);
-            unsigned long long m = __ballot(big && sub == 0);
-            while (m) {  // wave-uniform
-                const int q = __builtin_ctzll(m);
-                m &= m - 1;
-                cone_ring_vertex<64>(g, a, r0 + q / GW, lane);
-            }
+    const int sub = lane & 7;
+    for (int64_t r0 = w0 * 8; r0 < L; r0 += nw * 8) {
+        const int64_t r = r0 + (lane >> 3);
+        int32_t j = -1;
+        bool big;
+        if (a.slots) {  // the slot says whether the vertex is big: no xptr level ahead of the vertex's loads
+            j = r < L ? a.slots[r * 8 + sub] : -1;
+            big = j == kSlotBig;
+        } else {
+            big = r < L && g.xptr[r + 1] - g.xptr[r] > 8;
         }
-    };
-    // with the slot table four lanes a vertex (half the ring's workgroups: with the tiles one round of
-    // workgroups at two per CU)
-    if (a.slots) ring(std::integral_constant<int, 4>{});
-    else ring(std::integral_constant<int, 8>{});
+        if (r < L && !big) cone_ring_vertex<8>(g, a, r, sub, j);
+        unsigned long long m = __ballot(big && sub == 0);
+        while (m) {  // wave-uniform
+            const int q = __builtin_ctzll(m);
+            m &= m - 1;
+            cone_ring_vertex<64>(g, a, r0 + (q >> 3), lane);
+        }
+    }
     if (a.clk) band_clock(a.clk + 4, 0, t0);
 }
 
@@ -2595,6 +2584,35 @@ __device__ __forceinline__ void band_est_store(const BandEst& be, double cmax, d
     }
 }
 
+// a lattice triangle's neighbourhood into the caches, every load at once: the 4 x 4 vertices around
+// its cell (its own and its neighbour triangles' vertices: x, y), f and the gradients (and y) at the
+// cell's corners, the 3 x 3 cells' diagonals. The evaluation's chain - tri_verts, bary, clough_tocher's
+// neighbour triangles, each level waiting on the one before - then waits on cache hits, not on a
+// memory latency per level (a value the asm consumes, so the loads stay)
+__device__ __forceinline__ void warm_cell(const Grid& g, int o, const double* f, const double* grad, const double* y2) {
+    const int64_t c = o >> 1;
+    const int iv = (int)(c / (g.nh - 1)), ih = (int)(c - (int64_t)iv * (g.nh - 1));
+    double acc = 0.0;
+    unsigned d = 0;
+#pragma unroll
+    for (int dr = -1; dr <= 2; ++dr)
+#pragma unroll
+        for (int dc = -1; dc <= 2; ++dc) {
+            const int rv = min(max(iv + dr, 0), g.nv - 1), rh = min(max(ih + dc, 0), g.nh - 1);
+            const int64_t q = (int64_t)rv * g.nh + rh;
+            acc += g.x[q] + g.y[q];
+            if (dr >= 0 && dr <= 1 && dc >= 0 && dc <= 1) {
+                acc += f[q] + grad[2 * q] + grad[2 * q + 1];
+                if (y2) acc += y2[2 * q] + y2[2 * q + 1];
+            }
+            if (dr <= 1 && dc <= 1) {
+                const int cv = min(max(iv + dr, 0), g.nv - 2), ch = min(max(ih + dc, 0), g.nh - 2);
+                d += g.diag[(int64_t)cv * (g.nh - 1) + ch];
+            }
+        }
+    asm volatile("" ::"v"(acc), "v"(d));
+}
+
 __global__ void __launch_bounds__(kBlock) k_gd_eval(Grid g, Targets t, const int* __restrict__ owner,
                                                     const double* f, const double* grad, int nvals, double* out,
                                                     BandEst be = BandEst{nullptr, 0, nullptr, nullptr}) {
@@ -2606,6 +2624,7 @@ __global__ void __launch_bounds__(kBlock) k_gd_eval(Grid g, Targets t, const int
             for (int v = 0; v < nvals; ++v) out[v * m + i] = __builtin_nan("");
             continue;
         }
+        if (nvals == 1 && o < 2 * ncells(g)) warm_cell(g, o, f, grad, be.y);
         const int r = (int)(i / t.mx), c = (int)(i - (int64_t)r * t.mx);
         const Tri T = tri_verts(g, o);
         double b[3];
@@ -2923,7 +2942,7 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
                 const double* gin = j == 1 ? nullptr : gb[(j - 1) % 3];
                 const double* gprev = j >= 3 ? gb[(j + 1) % 3] : nullptr;
                 const BandTiles bt = band_tiles(g.nv, g.nh, 2 * K + 3 - j);
-                const unsigned nr8 = (unsigned)(((L + 15) / 16 * 64 + kBandThreads - 1) / kBandThreads);  // 4 lanes a vertex
+                const unsigned nr8 = (unsigned)(((L + 7) / 8 * 64 + kBandThreads - 1) / kBandThreads);
                 const ConeBand a{fv, gin, gprev, gb[j % 3], steps[j], band, patch_timer().on ? patch_timer().clk : nullptr,
                                  slots};
                 k_gd_cone_band<<<bt.total + nr8, kBandThreads, 0, s>>>(g, bt, a, (int)nr8);
@@ -2931,7 +2950,7 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
             }
             if (d_change) {  // one more plain sweep, y from x_K to depth K + 2 (the band targets' corners)
                 const BandTiles bt = band_tiles(g.nv, g.nh, K + 2);
-                const unsigned nr8 = (unsigned)(((L + 15) / 16 * 64 + kBandThreads - 1) / kBandThreads);
+                const unsigned nr8 = (unsigned)(((L + 7) / 8 * 64 + kBandThreads - 1) / kBandThreads);
                 const ConeBand a{fv, gb[K % 3], nullptr, gb[(K + 1) % 3], ConeStep{0, 1.0}, band,
                                  patch_timer().on ? patch_timer().clk : nullptr, slots};
                 k_gd_cone_band<<<bt.total + nr8, kBandThreads, 0, s>>>(g, bt, a, (int)nr8);
