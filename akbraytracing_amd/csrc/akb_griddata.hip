@@ -2584,35 +2584,6 @@ __device__ __forceinline__ void band_est_store(const BandEst& be, double cmax, d
     }
 }
 
-// a lattice triangle's neighbourhood into the caches, every load at once: the 4 x 4 vertices around
-// its cell (its own and its neighbour triangles' vertices: x, y), f and the gradients (and y) at the
-// cell's corners, the 3 x 3 cells' diagonals. The evaluation's chain - tri_verts, bary, clough_tocher's
-// neighbour triangles, each level waiting on the one before - then waits on cache hits, not on a
-// memory latency per level (a value the asm consumes, so the loads stay)
-__device__ __forceinline__ void warm_cell(const Grid& g, int o, const double* f, const double* grad, const double* y2) {
-    const int64_t c = o >> 1;
-    const int iv = (int)(c / (g.nh - 1)), ih = (int)(c - (int64_t)iv * (g.nh - 1));
-    double acc = 0.0;
-    unsigned d = 0;
-#pragma unroll
-    for (int dr = -1; dr <= 2; ++dr)
-#pragma unroll
-        for (int dc = -1; dc <= 2; ++dc) {
-            const int rv = min(max(iv + dr, 0), g.nv - 1), rh = min(max(ih + dc, 0), g.nh - 1);
-            const int64_t q = (int64_t)rv * g.nh + rh;
-            acc += g.x[q] + g.y[q];
-            if (dr >= 0 && dr <= 1 && dc >= 0 && dc <= 1) {
-                acc += f[q] + grad[2 * q] + grad[2 * q + 1];
-                if (y2) acc += y2[2 * q] + y2[2 * q + 1];
-            }
-            if (dr <= 1 && dc <= 1) {
-                const int cv = min(max(iv + dr, 0), g.nv - 2), ch = min(max(ih + dc, 0), g.nh - 2);
-                d += g.diag[(int64_t)cv * (g.nh - 1) + ch];
-            }
-        }
-    asm volatile("" ::"v"(acc), "v"(d));
-}
-
 __global__ void __launch_bounds__(kBlock) k_gd_eval(Grid g, Targets t, const int* __restrict__ owner,
                                                     const double* f, const double* grad, int nvals, double* out,
                                                     BandEst be = BandEst{nullptr, 0, nullptr, nullptr}) {
@@ -2624,7 +2595,6 @@ __global__ void __launch_bounds__(kBlock) k_gd_eval(Grid g, Targets t, const int
             for (int v = 0; v < nvals; ++v) out[v * m + i] = __builtin_nan("");
             continue;
         }
-        if (nvals == 1 && o < 2 * ncells(g)) warm_cell(g, o, f, grad, be.y);
         const int r = (int)(i / t.mx), c = (int)(i - (int64_t)r * t.mx);
         const Tri T = tri_verts(g, o);
         double b[3];

@@ -883,6 +883,7 @@ __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
             if ((tid & 63) == 0) bufsum[b] = v;
             wave_sync();
         }
+        if (tid == 0) a.clocks[5] = wall_clock64();  // wave 0's pairwise trees done (diagnostics)
     }
     // the finite count, and the map's range (np.nanmin / np.nanmax: the cone solve's error estimate
     // is held to it, FaithfulPupil)
@@ -906,6 +907,7 @@ __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
         ext[w][1] = hi;
     }
     block_sum<1>(cnt, (double(*)[1])red);
+    if (tid == 0) a.clocks[6] = wall_clock64();
     double tot = 0.0;
     for (int b = 0; b < nbuf; ++b) tot = tot + bufsum[b];
     const double mean = tot / cnt[0];
@@ -919,16 +921,32 @@ __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
     auto moments = [&](int nb, const double* cf, double thr, int mode, double mu, double (&acc)[kMomMax]) {
 #pragma unroll
         for (int q = 0; q < kMomMax; ++q) acc[q] = 0.0;
+        double cfr[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+        if (cf)
+#pragma unroll
+            for (int t = 0; t < 5; ++t) cfr[t] = cf[t];
+        // four points a round, their LDS reads (value, basis) issued together before the arithmetic
+        // (one LDS latency a round, not one per point); the points in the same order per thread
+        constexpr int kR = 4;
         PostIdx ix(tid, a.nx);
-        for (int64_t k = tid; k < total; k += kPostThreads, ix.next()) {
-            const double z = cm[L(k)];
+        for (int64_t k0 = tid; k0 < total; k0 += kR * kPostThreads) {
+            double zr[kR], fr[kR][5];
+#pragma unroll
+            for (int u = 0; u < kR; ++u) {
+                const int64_t k = k0 + u * kPostThreads;
+                zr[u] = k < total ? cm[L(k)] : __builtin_nan("");
+                basis5_tab(bX, bY, ix.i, ix.j, a.ny, a.nx, fr[u]);
+                ix.next();
+            }
+#pragma unroll
+            for (int u = 0; u < kR; ++u) {
+            const double z = zr[u];
             if (z != z) continue;
-            double f[5];
-            basis5_tab(bX, bY, ix.i, ix.j, a.ny, a.nx, f);
+            const double (&f)[5] = fr[u];
             double res = 0.0;
             if (cf || mode > 0) {
                 double mm = 0.0;
-                for (int t = 0; t < 5; ++t) mm = __builtin_fma(cf[t], f[t], mm);
+                for (int t = 0; t < 5; ++t) mm = __builtin_fma(cfr[t], f[t], mm);
                 res = z - mm;
                 if (mode == 0 && !(fabs(res) < thr)) continue;
             }
@@ -950,6 +968,7 @@ __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
                     if (nb == 5 || r < 3) acc[15 + r] = __builtin_fma(f[r], z, acc[15 + r]);
                 }
                 acc[20] += 1.0;
+            }
             }
         }
         // only the slots the mode fills: 2 (the residual passes), 10 (the plane's 3 x 3), 21
@@ -991,6 +1010,7 @@ __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
         __syncthreads();
     };
     if (tid == 0) sflag = 0;
+    if (tid < 2) firstrow[tid] = a.ny;  // (the NaN-split pass's minima, after the barriers below)
     double acc[kMomMax];
     moments(5, nullptr, 0.0, 0, 0.0, acc);
     if (tid == 0 && acc[20] < 5) sflag |= 1;  // curve_fit refuses fewer points than parameters
@@ -1003,8 +1023,11 @@ __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
     if (tid == 0 && acc[20] < 3) sflag |= 1;
     normal_solve(acc, std::integral_constant<int, 3>{}, 8);  // p2 = sys[8..11)
     if (tid == 0) a.clocks[3] = wall_clock64();
-    // corrected = (map - nanmean) - plane, and rotate_with_nan's NaN split of it
+    // corrected = (map - nanmean) - plane, and rotate_with_nan's NaN split of it; psf_calc's rotation
+    // estimate (:1122-1132) in the same pass: the first valid row of columns nx / 4 and 3 nx / 4 (every
+    // point of those columns tested, the smallest row kept)
     {
+        const int c1 = a.nx / 4, c3 = a.nx * 3 / 4;
         PostIdx ix(tid, a.nx);
         for (int64_t k = tid; k < total; k += kPostThreads, ix.next()) {
             double f[5];
@@ -1017,22 +1040,15 @@ __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
             if (in_lds) a.corrected[k] = o;
             a.coef[k] = nan ? 0.0 : o;
             a.coef[total + k] = nan ? 0.0 : 1.0;
+            if (o == o) {
+                if (ix.j == c1) atomicMin(&firstrow[0], ix.i);
+                if (ix.j == c3) atomicMin(&firstrow[1], ix.i);
+            }
         }
     }
-    __syncthreads();
-    // psf_calc's rotation estimate (:1122-1132): the first valid row of columns nx / 4 and 3 nx / 4
-    // (every row tested at once, the smallest kept)
-    if (tid < 2) firstrow[tid] = a.ny;
-    __syncthreads();
-    {
-        const int c1 = a.nx / 4, c3 = a.nx * 3 / 4;
-        for (int r = tid; r < 2 * a.ny; r += kPostThreads) {
-            const int row = r >> 1, c = (r & 1) ? c3 : c1;
-            const double v = cm[L((int64_t)row * a.nx + c)];
-            if (v == v) atomicMin(&firstrow[r & 1], row);
-        }
-    }
-    __syncthreads();
+    // (an LDS-only barrier: nothing here reads the global stores above, so no wave waits for their
+    // acknowledgements as __syncthreads' fence would make it)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     if (tid == 0) {
         const int c1 = a.nx / 4, c3 = a.nx * 3 / 4;
         const int r1 = firstrow[0], r3 = firstrow[1];
