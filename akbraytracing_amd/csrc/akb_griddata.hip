@@ -197,60 +197,6 @@ __device__ int64_t tri_nbr(const Grid& g, int64_t t, int k) {
 // flags: bit 0 a non-convex or degenerate cell, bit 1 an edge that is not locally Delaunay,
 // bit 2 a broken pocket adjacency, bits 3 / 4 cells of positive / negative orientation, bit 5 a
 // non-finite point
-__global__ void __launch_bounds__(kBlock) k_gd_cells(Grid g, uint8_t* diag, double tol, unsigned* flags) {
-    const int64_t nc = win_cell1(g);
-    unsigned acc = 0;
-    for (int64_t c = win_cell0(g) + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < nc;
-         c += (int64_t)gridDim.x * blockDim.x) {
-        const int iv = (int)(c / (g.nh - 1)), ih = (int)(c - (int64_t)iv * (g.nh - 1));
-        double bad = 0.0;
-        const int d = cell_diag(g, iv, ih, &bad);
-        diag[c] = (uint8_t)d;
-        unsigned f = bad > 0 ? 1u : 0u;
-        {   // bit 5: a non-finite point (a ray that missed); the ring kernel covers the last row / column
-            const int64_t q = (int64_t)iv * g.nh + ih;
-            if (!isfinite(g.x[q]) || !isfinite(g.y[q])) f |= 32u;
-        }
-        {   // every cell must share the grid's orientation (bits 3 / 4 both set: a folded grid)
-            const int64_t q00 = (int64_t)iv * g.nh + ih;
-            const double o = orient(g.x[q00], g.y[q00], g.x[q00 + 1], g.y[q00 + 1], g.x[q00 + g.nh + 1], g.y[q00 + g.nh + 1]);
-            f |= o > 0 ? 8u : (o < 0 ? 16u : 1u);
-        }
-        const int64_t p00 = (int64_t)iv * g.nh + ih, p01 = p00 + 1, p10 = p00 + g.nh, p11 = p10 + 1;
-        // right edge p01-p11 against the next cell's left triangle
-        if (ih + 1 < g.nh - 1) {
-            const int dn = cell_diag(g, iv, ih + 1, nullptr);
-            const int64_t mine = d == 0 ? p00 : p10;           // opposite vertex of my right-edge triangle
-            const int64_t other = dn == 0 ? p11 + 1 : p01 + 1;  // opposite vertex of its left-edge triangle
-            const double x0 = g.x[p01], y0 = g.y[p01];
-            const double ax = g.x[mine] - x0, ay = g.y[mine] - y0, cx = g.x[p11] - x0, cy = g.y[p11] - y0;
-            const double ox = g.x[other] - x0, oy = g.y[other] - y0;
-            const double s = fmax(fmax(fabs(ax), fabs(ay)), fmax(fmax(fabs(cx), fabs(cy)), fmax(fabs(ox), fabs(oy))));
-            if (incircle(0.0, 0.0, ax, ay, cx, cy, ox, oy) > tol * s * s * s * s) f |= 2u;
-        }
-        // top edge p10-p11 against the next row's bottom triangle
-        if (iv + 1 < g.nv - 1) {
-            const int dn = cell_diag(g, iv + 1, ih, nullptr);
-            const int64_t mine = d == 0 ? p00 : p01;
-            const int64_t other = dn == 0 ? p11 + g.nh : p10 + g.nh;
-            const double x0 = g.x[p10], y0 = g.y[p10];
-            const double ax = g.x[mine] - x0, ay = g.y[mine] - y0, cx = g.x[p11] - x0, cy = g.y[p11] - y0;
-            const double ox = g.x[other] - x0, oy = g.y[other] - y0;
-            const double s = fmax(fmax(fabs(ax), fabs(ay)), fmax(fmax(fabs(cx), fabs(cy)), fmax(fabs(ox), fabs(oy))));
-            if (incircle(0.0, 0.0, ax, ay, cx, cy, ox, oy) > tol * s * s * s * s) f |= 2u;
-        }
-        acc |= f;
-    }
-    // one atomic per wave, only for bits not yet set (every cell sets an orientation bit)
-    for (int off = 32; off > 0; off >>= 1) acc |= __shfl_down(acc, off);
-    if ((threadIdx.x & 63) == 0) {
-        const unsigned cur = __hip_atomic_load(flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((cur | acc) != cur) atomicOr(flags, acc);
-    }
-}
-
-constexpr int kCellTile = 16;
-
 // ------------------------------------------------------------------ targets
 
 constexpr int kClaimAxisLds = 512;  // target axes up to this long go to LDS in the claim kernels
@@ -354,261 +300,15 @@ __device__ __forceinline__ bool axes_uniform(const Targets& t) {
     return __syncthreads_and(ok) != 0;
 }
 
-// ---- the claims fused into the cell pass (the cone solve's single-process path): while
-// k_gd_cells_tiled holds a tile's vertices and diagonals in LDS, the targets in the tile's bounding
-// box (rarely more than one or two: the 128^2 targets sit ~25 cells apart at C3) are tested by
-// every cell of the tile against its two triangles from the LDS copies - claim_cell's box predicate
-// and bary's arithmetic on the same values, so the same owners as k_gd_claim_scan + k_gd_claim_hit,
-// with no second pass over the lattice and no per-cell index search
+// ---- the claims fused into the cell pass (the cone solve's single-process path, k_gd_cells_strip<true>):
+// each cell tests the targets in its own box (rarely any: the 128^2 targets sit ~25 cells apart at C3)
+// against its two triangles from the values it holds - claim_cell's box predicate and bary's
+// arithmetic on the same values, so the same owners as k_gd_claim_scan + k_gd_claim_hit, with no
+// second pass over the lattice
 struct TileClaims {
     Targets t;   // the target axes (the device's linspaces, k_gd_axes)
     int* owner;  // (my, mx), INT32_MAX-filled before the pass
 };
-
-__device__ __forceinline__ void bary_lds(const double* vx, const double* vy, const int (&k)[3], double px, double py,
-                                         double (&b)[3]) {  // bary on LDS copies: the same expressions
-    const double x2 = vx[k[2]], y2 = vy[k[2]];
-    const double a00 = vx[k[0]] - x2, a01 = vx[k[1]] - x2;
-    const double a10 = vy[k[0]] - y2, a11 = vy[k[1]] - y2;
-    const double det = a00 * a11 - a01 * a10;
-    const double dx = px - x2, dy = py - y2;
-    const double t00 = a11 / det, t01 = -a01 / det;
-    b[0] = t00 * dx + t01 * dy;
-    // the second row's divisions after the first's (an empty asm ties det to b[0]): two IEEE
-    // divisions in flight instead of four keep the cell pass at its 8 waves per SIMD
-    double det1 = det;
-    asm volatile("" : "+v"(det1) : "v"(b[0]));
-    const double t10 = -a10 / det1, t11 = a00 / det1;
-    b[1] = t10 * dx + t11 * dy;
-    b[2] = 1.0 - b[0] - b[1];
-}
-
-__device__ void tile_claims(const Grid& g, const TileClaims& tc, bool uniform, double inv_dx, double inv_dy,
-                            const double* vx, const double* vy, const uint8_t* sdg, int iv0, int ih0, int r_hi) {
-    constexpr int T = kCellTile, V = T + 2;
-    __shared__ int srange[4];  // the tile's candidate targets: columns [0, 1), rows [2, 3)
-    const Targets& t = tc.t;
-    const int tid = threadIdx.x;
-    const int nr = min(T, r_hi - iv0), nc = min(T, g.nh - 1 - ih0);  // the tile's cells
-    if (tid < 64) {  // wave 0: the tile's box over its (nr + 1) x (nc + 1) vertices (fmin / fmax pass over a NaN)
-        double xlo = INFINITY, xhi = -INFINITY, ylo = INFINITY, yhi = -INFINITY;
-        for (int k = tid; k < (nr + 1) * (nc + 1); k += 64) {
-            const int r = k / (nc + 1), c = k - (k / (nc + 1)) * (nc + 1);
-            const double x = vx[r * V + c], y = vy[r * V + c];
-            xlo = fmin(xlo, x);
-            xhi = fmax(xhi, x);
-            ylo = fmin(ylo, y);
-            yhi = fmax(yhi, y);
-        }
-        for (int off = 32; off > 0; off >>= 1) {
-            xlo = fmin(xlo, __shfl_xor(xlo, off));
-            xhi = fmax(xhi, __shfl_xor(xhi, off));
-            ylo = fmin(ylo, __shfl_xor(ylo, off));
-            yhi = fmax(yhi, __shfl_xor(yhi, off));
-        }
-        // the candidate targets: a superset of every triangle's (a triangle's padded box lies in the
-        // tile's), from the linspace estimate or the exact binary search; empty: c0 = c1 = 0
-        if (tid == 0) {
-            const double padx = (xhi - xlo) * 1e-9, pady = (yhi - ylo) * 1e-9;
-            int c0, c1, r0, r1;
-            bool hit;
-            if (uniform) {
-                hit = axis_range(t.gx, t.mx, inv_dx, xlo - padx, xhi + padx, c0, c1) &&
-                      axis_range(t.gy, t.my, inv_dy, ylo - pady, yhi + pady, r0, r1);
-            } else {
-                c0 = lower_idx(t.gx, t.mx, xlo - padx);
-                c1 = lower_idx(t.gx, t.mx, xhi + padx);
-                r0 = lower_idx(t.gy, t.my, ylo - pady);
-                r1 = lower_idx(t.gy, t.my, yhi + pady);
-                hit = c0 < c1 && r0 < r1;
-            }
-            srange[0] = hit ? c0 : 0;
-            srange[1] = hit ? c1 : 0;
-            srange[2] = hit ? r0 : 0;
-            srange[3] = hit ? r1 : 0;
-        }
-    }
-    __syncthreads();  // (the next tile's writes come after the cell pass's next three barriers)
-    const int c0 = srange[0], c1 = srange[1], r0 = srange[2], r1 = srange[3];
-    if (c0 >= c1) return;
-    const int rr = tid / T, cc = tid - (tid / T) * T;
-    if (rr >= nr || cc >= nc) return;
-    // this cell's two triangles (tri_verts' vertex order), formed per candidate target from LDS (a
-    // tile holds one or two: nothing is kept in registers across them). A target is claimed by a
-    // triangle when it lies in the triangle's box as claim_cell bounds it (lo - pad <= coordinate <
-    // hi + pad) and passes bary's test - the same predicate, the same atomicMin, in any order
-    const int k00 = rr * V + cc, k01 = k00 + 1, k10 = k00 + V, k11 = k10 + 1;
-    const int64_t c = (int64_t)(iv0 + rr) * (g.nh - 1) + (ih0 + cc);
-    const int d = sdg[rr * (T + 1) + cc];
-    for (int r = r0; r < r1; ++r) {
-        for (int q = c0; q < c1; ++q) {
-            asm volatile("" ::: "memory");  // (compiler barrier: the LDS reads stay in the loop)
-            const double px = t.gx[q], py = t.gy[r];
-#pragma unroll 1
-            for (int half = 0; half < 2; ++half) {
-                int kv[3];
-                if (d == 0) {
-                    kv[0] = k00;
-                    kv[1] = half == 0 ? k01 : k11;
-                    kv[2] = half == 0 ? k11 : k10;
-                } else {
-                    kv[0] = half == 0 ? k00 : k01;
-                    kv[1] = half == 0 ? k01 : k11;
-                    kv[2] = k10;
-                }
-                double txlo = vx[kv[0]], txhi = txlo, tylo = vy[kv[0]], tyhi = tylo;
-                for (int k = 1; k < 3; ++k) {
-                    txlo = fmin(txlo, vx[kv[k]]);
-                    txhi = fmax(txhi, vx[kv[k]]);
-                    tylo = fmin(tylo, vy[kv[k]]);
-                    tyhi = fmax(tyhi, vy[kv[k]]);
-                }
-                const double tpx = (txhi - txlo) * 1e-9, tpy = (tyhi - tylo) * 1e-9;
-                if (!(px >= txlo - tpx && px < txhi + tpx && py >= tylo - tpy && py < tyhi + tpy)) continue;
-                double b[3];
-                bary_lds(vx, vy, kv, px, py, b);
-                if (b[0] >= -kInsideEps && b[1] >= -kInsideEps && b[2] >= -kInsideEps)
-                    atomicMin(&tc.owner[(int64_t)r * t.mx + q], (int)(2 * c + half));
-            }
-        }
-    }
-}
-
-// k_gd_cells on 16 x 16 tiles of the window's cells, one workgroup each: the tile's 18 x 18
-// vertices in LDS (its cells, the next row's and column's), each of its 17 x 17 cells' diagonal
-// formed once (cell_diag's arithmetic on the same values), then each cell's checks from LDS. Per
-// cell: ~1.3 vertex loads and ~3 in-circle tests instead of ~10 and 5. Same diagonals and flags.
-// With kClaims the tile also claims its targets (tile_claims) after its cells' checks.
-template <bool kClaims = false>
-__global__ void __launch_bounds__(kCellTile * kCellTile) k_gd_cells_tiled(Grid g, uint8_t* diag, double tol,
-                                                                        unsigned* flags, TileClaims tc = {}) {
-    constexpr int T = kCellTile, V = T + 2;
-    __shared__ double vx[V * V], vy[V * V];
-    __shared__ uint8_t sdg[(T + 1) * (T + 1)];
-    const int r_lo = g.row0, r_hi = g.row1 < 0 ? g.nv - 1 : g.row1;  // window cell rows [r_lo, r_hi)
-    const int tiles_h = (g.nh - 1 + T - 1) / T;
-    const int64_t ntiles = (int64_t)((r_hi - r_lo + T - 1) / T) * tiles_h;
-    unsigned acc = 0;
-    bool uniform = false;
-    double inv_dx = 0.0, inv_dy = 0.0;
-    if constexpr (kClaims) {
-        // the target axes in LDS when they fit: every tile's candidate range and tests read them
-        __shared__ double sax[2 * kClaimAxisLds];
-        if (tc.t.mx <= kClaimAxisLds && tc.t.my <= kClaimAxisLds) {
-            for (int i = threadIdx.x; i < tc.t.mx; i += blockDim.x) sax[i] = tc.t.gx[i];
-            for (int i = threadIdx.x; i < tc.t.my; i += blockDim.x) sax[kClaimAxisLds + i] = tc.t.gy[i];
-            __syncthreads();
-            tc.t.gx = sax;
-            tc.t.gy = sax + kClaimAxisLds;
-        }
-        uniform = axes_uniform(tc.t);
-        inv_dx = inv_step(tc.t.gx, tc.t.mx);
-        inv_dy = inv_step(tc.t.gy, tc.t.my);
-    }
-    // a tile's V x V vertices, two per thread, into registers: the next tile's are loaded while this
-    // one is checked (its loads then wait behind no other work)
-    constexpr int NL = (V * V + T * T - 1) / (T * T);
-    auto load_tile = [&](int64_t tile, double (&px)[NL], double (&py)[NL]) {
-        const int tv = (int)tile / tiles_h, th = (int)tile - tv * tiles_h;  // (32-bit: a 64-bit division costs ~100 instructions)
-        const int iv0 = r_lo + tv * T, ih0 = th * T;
-#pragma unroll
-        for (int u = 0; u < NL; ++u) {
-            const int k = threadIdx.x + u * T * T;
-            const int rr = k / V, cc = k - (k / V) * V;
-            const int iv = iv0 + rr, ih = ih0 + cc;
-            px[u] = py[u] = 0.0;
-            if (k < V * V && iv < g.nv && ih < g.nh && iv <= r_hi + 1) {
-                const int64_t q = (int64_t)iv * g.nh + ih;
-                px[u] = g.x[q];
-                py[u] = g.y[q];
-            }
-        }
-    };
-    double px[NL], py[NL];
-    if ((int64_t)blockIdx.x < ntiles) load_tile(blockIdx.x, px, py);
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int tv = (int)tile / tiles_h, th = (int)tile - tv * tiles_h;  // (32-bit: a 64-bit division costs ~100 instructions)
-        const int iv0 = r_lo + tv * T, ih0 = th * T;
-        __syncthreads();
-#pragma unroll
-        for (int u = 0; u < NL; ++u) {
-            const int k = threadIdx.x + u * T * T;
-            if (k < V * V) {
-                vx[k] = px[u];
-                vy[k] = py[u];
-            }
-        }
-        __syncthreads();
-        if (tile + gridDim.x < ntiles) load_tile(tile + gridDim.x, px, py);
-        // the diagonals of the tile's cells and of the next row / column (cell_diag's arithmetic)
-        auto diag_of = [&](int rr, int cc, double* viol) {
-            const int k00 = rr * V + cc, k01 = k00 + 1, k10 = k00 + V, k11 = k10 + 1;
-            const double x0 = vx[k00], y0 = vy[k00];
-            const double bx = vx[k01] - x0, by = vy[k01] - y0;
-            const double cx = vx[k11] - x0, cy = vy[k11] - y0;
-            const double dx = vx[k10] - x0, dy = vy[k10] - y0;
-            const double ic = incircle(0.0, 0.0, bx, by, cx, cy, dx, dy);
-            const int d = ic > 0 ? 1 : 0;
-            if (viol) {
-                const double sgn = d == 0 ? orient(0, 0, bx, by, cx, cy) * orient(0, 0, cx, cy, dx, dy)
-                                          : orient(0, 0, bx, by, dx, dy) * orient(bx, by, cx, cy, dx, dy);
-                *viol = sgn > 0 ? 0.0 : 1.0;
-            }
-            return d;
-        };
-        double bad = 0.0;
-        const int rr = threadIdx.x / T, cc = threadIdx.x - (threadIdx.x / T) * T;
-        const int iv = iv0 + rr, ih = ih0 + cc;
-        const bool own = iv < r_hi && ih < g.nh - 1;
-        const int d = own ? diag_of(rr, cc, &bad) : 0;
-        sdg[rr * (T + 1) + cc] = (uint8_t)d;
-        if (threadIdx.x < 2 * T + 1) {  // the next row (T + 1 cells) and column (T cells)
-            const int r2 = threadIdx.x <= T ? T : (int)threadIdx.x - (T + 1);
-            const int c2 = threadIdx.x <= T ? (int)threadIdx.x : T;
-            const int jv = iv0 + r2, jh = ih0 + c2;
-            sdg[r2 * (T + 1) + c2] =
-                (jv < g.nv - 1 && jh < g.nh - 1 && jv <= r_hi) ? (uint8_t)diag_of(r2, c2, nullptr) : (uint8_t)0;
-        }
-        __syncthreads();
-        if (own) {
-            const int64_t c = (int64_t)iv * (g.nh - 1) + ih;
-            diag[c] = (uint8_t)d;
-            unsigned f = bad > 0 ? 1u : 0u;
-            const int k00 = rr * V + cc, k01 = k00 + 1, k10 = k00 + V, k11 = k10 + 1;
-            if (!isfinite(vx[k00]) || !isfinite(vy[k00])) f |= 32u;
-            {
-                const double o = orient(vx[k00], vy[k00], vx[k01], vy[k01], vx[k11], vy[k11]);
-                f |= o > 0 ? 8u : (o < 0 ? 16u : 1u);
-            }
-            if (ih + 1 < g.nh - 1) {  // right edge p01-p11 against the next cell's left triangle
-                const int dn = sdg[rr * (T + 1) + cc + 1];
-                const int mine = d == 0 ? k00 : k10, other = dn == 0 ? k11 + 1 : k01 + 1;
-                const double x0 = vx[k01], y0 = vy[k01];
-                const double ax = vx[mine] - x0, ay = vy[mine] - y0, cx = vx[k11] - x0, cy = vy[k11] - y0;
-                const double ox = vx[other] - x0, oy = vy[other] - y0;
-                const double sc = fmax(fmax(fabs(ax), fabs(ay)), fmax(fmax(fabs(cx), fabs(cy)), fmax(fabs(ox), fabs(oy))));
-                if (incircle(0.0, 0.0, ax, ay, cx, cy, ox, oy) > tol * sc * sc * sc * sc) f |= 2u;
-            }
-            if (iv + 1 < g.nv - 1) {  // top edge p10-p11 against the next row's bottom triangle
-                const int dn = sdg[(rr + 1) * (T + 1) + cc];
-                const int mine = d == 0 ? k00 : k01, other = dn == 0 ? k11 + V : k10 + V;
-                const double x0 = vx[k10], y0 = vy[k10];
-                const double ax = vx[mine] - x0, ay = vy[mine] - y0, cx = vx[k11] - x0, cy = vy[k11] - y0;
-                const double ox = vx[other] - x0, oy = vy[other] - y0;
-                const double sc = fmax(fmax(fabs(ax), fabs(ay)), fmax(fmax(fabs(cx), fabs(cy)), fmax(fabs(ox), fabs(oy))));
-                if (incircle(0.0, 0.0, ax, ay, cx, cy, ox, oy) > tol * sc * sc * sc * sc) f |= 2u;
-            }
-            acc |= f;
-        }
-        // the tile's claims after its checks (their registers are dead by then; a barrier inside)
-        if constexpr (kClaims) tile_claims(g, tc, uniform, inv_dx, inv_dy, vx, vy, sdg, iv0, ih0, r_hi);
-    }
-    for (int off = 32; off > 0; off >>= 1) acc |= __shfl_down(acc, off);
-    if ((threadIdx.x & 63) == 0) {
-        const unsigned cur = __hip_atomic_load(flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((cur | acc) != cur) atomicOr(flags, acc);
-    }
-}
 
 // ---- the cell pass as wave strips: a wave's 64 lanes hold 64 consecutive vertex columns and walk
 // a segment of cell rows upwards (as many rows as puts one wave on every resident slot), a vertex row
@@ -617,9 +317,9 @@ __global__ void __launch_bounds__(kCellTile * kCellTile) k_gd_cells_tiled(Grid g
 // neighbour's diagonal likewise, and the diagonal of the row above is formed one step early - so no
 // LDS, no barrier, each vertex loaded once (plus two halo rows per segment) and each diagonal formed
 // once. Lanes 0 .. 61 own the cells (lane 62 forms the diagonal lane 61's right edge needs). Every
-// test is k_gd_cells_tiled's arithmetic on the same values: the same diagonals and flags. With
-// kClaims each cell claims its targets: the candidates from the cell's own box (axis_range on
-// linspace axes, else the binary search), then tile_claims' per-triangle predicate - the same owners.
+// test is cell_diag's and the Delaunay checks' arithmetic (the oracle's): the same diagonals and
+// flags. With kClaims each cell claims its targets: the candidates from the cell's own box (axis_range
+// on linspace axes, else the binary search), then the per-triangle predicate - the same owners.
 constexpr int kStripCells = 62, kStripThreads = 256, kStripAhead = 2;
 
 __device__ __forceinline__ int lane_up(int v) {  // lane i gets lane i + 1's value (lane 63: 0, bound_ctrl)
@@ -646,7 +346,7 @@ __device__ __forceinline__ StripRow strip_row(double x, double y) {
 }
 
 // the diagonal of the cell between rows a (bottom) and b (top) at the lane's column, and whether
-// the split is convex (k_gd_cells_tiled's diag_of)
+// the split is convex (cell_diag's arithmetic)
 __device__ __forceinline__ int strip_diag(const StripRow& a, const StripRow& b, double& viol) {
     const double x0 = a.x, y0 = a.y;
     const double bx = a.x1 - x0, by = a.y1 - y0;
@@ -660,7 +360,7 @@ __device__ __forceinline__ int strip_diag(const StripRow& a, const StripRow& b, 
     return d;
 }
 
-// an edge's local-Delaunay test (k_gd_cells_tiled's): the edge from (x0, y0) to (cxa, cya), the
+// an edge's local-Delaunay test (the tolerance-scaled in-circle): the edge from (x0, y0) to (cxa, cya), the
 // triangle's opposite vertex (mxa, mya), the neighbour's (oxa, oya)
 __device__ __forceinline__ bool strip_edge_bad(double x0, double y0, double mxa, double mya, double cxa, double cya,
                                                double oxa, double oya, double tol) {
@@ -2975,7 +2675,7 @@ int akb_gd_cone_eval_f64(const double* x, const double* y, int nv, int nh, const
 }
 
 // the single-process cone solve's begin: the target owners filled, then pass 1 with the cells' claims
-// fused in (k_gd_cells_tiled<true>); the axes (akb_gd_axes_f64) before it, the pockets' claims after
+// fused in (k_gd_cells_strip<true>); the axes (akb_gd_axes_f64) before it, the pockets' claims after
 int akb_gd_cells_claims_f64(const double* x, const double* y, int nv, int nh, uint8_t* diag, double tol,
                             unsigned* d_flags, const double* gx, int mx, const double* gy, int my, int* owner,
                             void* stream) {

@@ -253,7 +253,7 @@ def test_dropin_psf_module_exports():
 # ----------------------------------------------------------------------------- griddata triangulation
 
 def _cell_tris_np(X, Y):
-    """Cell split by the in-circle test (the rule k_gd_cells applies), as vertex triples."""
+    """Cell split by the in-circle test (the rule the device cell pass applies), as vertex triples."""
     nv, nh = X.shape
     x0, y0 = X[:-1, :-1], Y[:-1, :-1]
     bx, by = X[:-1, 1:] - x0, Y[:-1, 1:] - y0
