@@ -829,6 +829,25 @@ struct PostLeaf {  // pw_leaf_lds<true>'s sums over the padded map
     }
 };
 
+// PostLeaf::leaf(o, 128): numpy's eight accumulators over a 128-element leaf of the padded map, the
+// reads issued 8 at a time (fully unrolled: no loop branch between the batches)
+__device__ __noinline__ double post_leaf128(const double* smem, int o) {
+    const PostLeaf P{smem};
+    double r[8];
+#pragma unroll
+    for (int blk = 0; blk < 16; ++blk) {
+        double t[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) t[q] = P.val(o + 8 * blk + q);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int idx = 8 * blk + q;
+            r[idx & 7] = idx < 8 ? t[q] : r[idx & 7] + t[q];
+        }
+    }
+    return ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+}
+
 __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
     __shared__ double smem[kPostLds + kPostLds / 128];  // the map, then matrixWave2 - nanmean (when it fits)
     __shared__ PwTree trees[2];        // the nanmean's pairwise trees (waves 0 and 1)
@@ -878,8 +897,17 @@ __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
         for (int b = w; b < nbuf; b += 2) {
             const int64_t b0 = (int64_t)b * 8192;
             const int len = (int)(total - b0 < 8192 ? total - b0 : 8192);
-            const double v = in_lds ? pw_tree_wave_get(trees[w], PostLeaf{smem}, (int)b0, len)
-                                    : pw_tree_wave<true>(trees[w], src + b0, len);
+            double v;
+            if (in_lds && len == 8192) {
+                // a full buffer: numpy's split tree is balanced down to 64 leaves of 128 - a lane's
+                // leaf (its 128 reads issued in four batches), then the levels left + right as a
+                // butterfly (lane 0 ends with the buffer's sum, in the tree's order)
+                v = post_leaf128(smem, (int)b0 + 128 * (tid & 63));
+                for (int off = 1; off < 64; off <<= 1) v = v + __shfl_down(v, off);
+            } else {
+                v = in_lds ? pw_tree_wave_get(trees[w], PostLeaf{smem}, (int)b0, len)
+                           : pw_tree_wave<true>(trees[w], src + b0, len);
+            }
             if ((tid & 63) == 0) bufsum[b] = v;
             wave_sync();
         }
@@ -914,7 +942,19 @@ __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
     // matrixWave2 - nanmean, the plane correction's input: in LDS when it fits, else in `corrected`
     double* cm = in_lds ? smem : a.corrected;
     __syncthreads();
-    for (int64_t k = tid; k < total; k += kPostThreads) cm[L(k)] = src[L(k)] - mean;
+    for (int64_t k0 = tid; k0 < total; k0 += 4 * kPostThreads) {  // four reads in flight a round
+        double t[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t k = k0 + u * kPostThreads;
+            t[u] = k < total ? src[L(k)] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t k = k0 + u * kPostThreads;
+            if (k < total) cm[L(k)] = t[u] - mean;
+        }
+    }
     __syncthreads();
     if (tid == 0) a.clocks[2] = wall_clock64();
     // plane_correction_with_nan_and_outlier_filter: the four moment passes of k_moments
@@ -1015,6 +1055,7 @@ __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
     moments(5, nullptr, 0.0, 0, 0.0, acc);
     if (tid == 0 && acc[20] < 5) sflag |= 1;  // curve_fit refuses fewer points than parameters
     normal_solve(acc, std::integral_constant<int, 5>{}, 0);  // c1 = sys[0..5)
+    if (tid == 0) a.clocks[7] = wall_clock64();  // the first fit solved (diagnostics)
     moments(5, sys, 0.0, 1, 0.0, acc);
     const double n1 = acc[20], mu = acc[0] / acc[20];
     moments(5, sys, 0.0, 2, mu, acc);

@@ -1,6 +1,6 @@
 """The pupil post's phases on the device: akb_pupil_post_f64 on the reference's 1001^2 gridded map
 (128^2), the post kernel's wall clock (100 MHz) at its start, after the map's load, after the
-nanmean, after the plane fits, at its end, after wave 0's pairwise trees and after the count's sum, and the prefilter's after its load and each axis (the
+nanmean, after the plane fits, at its end, after wave 0's pairwise trees, after the count's sum and after the first plane fit, and the prefilter's after its load and each axis (the
 work buffer's clock words), medians over repeated launches, beside the three launches' wall time. Study script (GPU):
 python scripts/study_post.py"""
 import json
@@ -26,7 +26,7 @@ def main():
         ev[1].record()
         torch.cuda.synchronize()
         wall.append(ev[0].elapsed_time(ev[1]) * 1e3)
-        clk = o["work"][0:7].cpu().numpy().view(np.uint64).astype(np.int64)
+        clk = o["work"][0:8].cpu().numpy().view(np.uint64).astype(np.int64)
         sp = o["work"][8:16].cpu().numpy().view(np.uint64).astype(np.int64)
         rows.append(np.concatenate([(clk - clk[0]) * 0.01, (sp - sp[0]) * 0.01]))  # us
     r = np.median(np.array(rows[5:]), axis=0)
