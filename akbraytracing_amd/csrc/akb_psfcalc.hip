@@ -374,27 +374,24 @@ __device__ __forceinline__ bool solve_small_reg(double (&A)[N][N], double (&b)[N
                 p = i;
                 best = fabs(A[i][k]);
             }
-        // the pivot row (the largest magnitude in column k, the first on ties) into row k
-        double pr[N], pb = b[k];
+        // the pivot row (the largest magnitude in column k, the first on ties) into row k: a
+        // conditional exchange of rows k and i for each i, on a flag the compiler cannot relate to
+        // p (else it folds the selects into a row index - an array in scratch memory, a memory
+        // round trip per pivot on this one-thread path)
 #pragma unroll
-        for (int j = 0; j < N; ++j) pr[j] = A[k][j];
+        for (int i = k + 1; i < N; ++i) {
+            int sw = i == p;
+            asm volatile("" : "+v"(sw));
 #pragma unroll
-        for (int i = k + 1; i < N; ++i)
-            if (i == p) {
-#pragma unroll
-                for (int j = 0; j < N; ++j) pr[j] = A[i][j];
-                pb = b[i];
+            for (int j = 0; j < N; ++j) {
+                const double rk = A[k][j], ri = A[i][j];
+                A[k][j] = sw ? ri : rk;
+                A[i][j] = sw ? rk : ri;
             }
-#pragma unroll
-        for (int i = k + 1; i < N; ++i)
-            if (i == p) {
-#pragma unroll
-                for (int j = 0; j < N; ++j) A[i][j] = A[k][j];
-                b[i] = b[k];
-            }
-#pragma unroll
-        for (int j = 0; j < N; ++j) A[k][j] = pr[j];
-        b[k] = pb;
+            const double bk = b[k], bi = b[i];
+            b[k] = sw ? bi : bk;
+            b[i] = sw ? bk : bi;
+        }
         if (A[k][k] == 0.0) ok = false;
 #pragma unroll
         for (int i = k + 1; i < N; ++i) {
