@@ -137,6 +137,14 @@ static __device__ double pw_tree_wave(PwTree& T, const double* a, int len) {
 template <class Get>
 __device__ double pw_tree_wave_get(PwTree& T, const Get& get, int base, int len) {
     const int lane = threadIdx.x & 63;
+    if (len == 64 * kPwLeaf) {
+        // a full 8192-element buffer: numpy's split tree is balanced down to 64 leaves of 128 - a
+        // leaf a lane, then the levels left + right as a butterfly in the tree's order (no tree
+        // bookkeeping in LDS); every lane gets the root
+        double v = get.leaf(base + kPwLeaf * lane, kPwLeaf);
+        for (int off = 1; off < 64; off <<= 1) v = v + __shfl_down(v, off);
+        return __shfl(v, 0);
+    }
     if (lane == 0) {
         T.off[0][0] = 0;
         T.len[0][0] = len;
