@@ -2189,18 +2189,40 @@ __global__ void __launch_bounds__(kBlock) k_gd_claim_pockets(Grid g, Targets t, 
     }
 }
 
-__device__ double clough_tocher(const Grid& g, int64_t tid, const Tri& T, const double* f, const double* grad,
-                                const double (&b)[3]) {
-    const double p0x = g.x[T.v[0]], p0y = g.y[T.v[0]];
-    const double p1x = g.x[T.v[1]], p1y = g.y[T.v[1]];
-    const double p2x = g.x[T.v[2]], p2y = g.y[T.v[2]];
+// the values clough_tocher reads for a triangle: its vertices' positions, f and gradients, and its
+// three neighbour triangles' centroids (nb false: a hull edge)
+struct CTIn {
+    double px[3], py[3], f[3], gx[3], gy[3];
+    double cx[3], cy[3];
+    bool nb[3];
+};
+
+// bary's arithmetic on the triangle's vertex values
+__device__ __forceinline__ void bary_v(const double (&x)[3], const double (&y)[3], double px, double py,
+                                       double (&b)[3]) {
+    const double x2 = x[2], y2 = y[2];
+    const double a00 = x[0] - x2, a01 = x[1] - x2;
+    const double a10 = y[0] - y2, a11 = y[1] - y2;
+    const double det = a00 * a11 - a01 * a10;
+    const double t00 = a11 / det, t01 = -a01 / det, t10 = -a10 / det, t11 = a00 / det;
+    const double dx = px - x2, dy = py - y2;
+    b[0] = t00 * dx + t01 * dy;
+    b[1] = t10 * dx + t11 * dy;
+    b[2] = 1.0 - b[0] - b[1];
+}
+
+// scipy's Clough-Tocher patch at barycentric b from the gathered values
+__device__ double ct_eval(const CTIn& in, const double (&b)[3]) {
+    const double p0x = in.px[0], p0y = in.py[0];
+    const double p1x = in.px[1], p1y = in.py[1];
+    const double p2x = in.px[2], p2y = in.py[2];
     const double e12x = p1x - p0x, e12y = p1y - p0y;
     const double e23x = p2x - p1x, e23y = p2y - p1y;
     const double e31x = p0x - p2x, e31y = p0y - p2y;
-    const double f1 = f[T.v[0]], f2 = f[T.v[1]], f3 = f[T.v[2]];
-    const double g0x = grad[2 * T.v[0]], g0y = grad[2 * T.v[0] + 1];
-    const double g1x = grad[2 * T.v[1]], g1y = grad[2 * T.v[1] + 1];
-    const double g2x = grad[2 * T.v[2]], g2y = grad[2 * T.v[2] + 1];
+    const double f1 = in.f[0], f2 = in.f[1], f3 = in.f[2];
+    const double g0x = in.gx[0], g0y = in.gy[0];
+    const double g1x = in.gx[1], g1y = in.gy[1];
+    const double g2x = in.gx[2], g2y = in.gy[2];
     const double df12 = +(g0x * e12x + g0y * e12y);
     const double df21 = -(g1x * e12x + g1y * e12y);
     const double df23 = +(g1x * e23x + g1y * e23y);
@@ -2215,16 +2237,12 @@ __device__ double clough_tocher(const Grid& g, int64_t tid, const Tri& T, const 
     const double c0021 = (c1020 + c0120 + c0030) / 3;
     double gk[3];
     for (int k = 0; k < 3; ++k) {
-        const int64_t n = tri_nbr(g, tid, k);
-        if (n < 0) {
+        if (!in.nb[k]) {
             gk[k] = -0.5;
             continue;
         }
-        const Tri N = tri_verts(g, n);
-        const double cx = (g.x[N.v[0]] + g.x[N.v[1]] + g.x[N.v[2]]) / 3;
-        const double cy = (g.y[N.v[0]] + g.y[N.v[1]] + g.y[N.v[2]]) / 3;
         double c[3];
-        bary(g, T, cx, cy, c);
+        bary_v(in.px, in.py, in.cx[k], in.cy[k], c);
         if (k == 0) gk[k] = (2 * c[2] + c[1] - 1) / (2 - 3 * c[2] - 3 * c[1]);
         else if (k == 1) gk[k] = (2 * c[0] + c[2] - 1) / (2 - 3 * c[0] - 3 * c[2]);
         else gk[k] = (2 * c[1] + c[0] - 1) / (2 - 3 * c[1] - 3 * c[0]);
@@ -2243,6 +2261,105 @@ __device__ double clough_tocher(const Grid& g, int64_t tid, const Tri& T, const 
            3 * b1 * b4 * b4 * c1002 + b2 * b2 * b2 * c0300 + 3 * b2 * b2 * b3 * c0210 + 3 * b2 * b2 * b4 * c0201 +
            3 * b2 * b3 * b3 * c0120 + 6 * b2 * b3 * b4 * c0111 + 3 * b2 * b4 * b4 * c0102 + b3 * b3 * b3 * c0030 +
            3 * b3 * b3 * b4 * c0021 + 3 * b3 * b4 * b4 * c0012 + b4 * b4 * b4 * c0003;
+}
+
+
+// the generic gather (any triangle: lattice cells at the boundary, pockets) through tri_nbr / tri_verts
+__device__ void ct_gather(const Grid& g, int64_t tid, const Tri& T, const double* f, const double* grad, CTIn& in) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        in.px[k] = g.x[T.v[k]];
+        in.py[k] = g.y[T.v[k]];
+        in.f[k] = f[T.v[k]];
+        in.gx[k] = grad[2 * T.v[k]];
+        in.gy[k] = grad[2 * T.v[k] + 1];
+    }
+    for (int k = 0; k < 3; ++k) {
+        const int64_t n = tri_nbr(g, tid, k);
+        in.nb[k] = n >= 0;
+        if (n < 0) continue;
+        const Tri N = tri_verts(g, n);
+        in.cx[k] = (g.x[N.v[0]] + g.x[N.v[1]] + g.x[N.v[2]]) / 3;
+        in.cy[k] = (g.y[N.v[0]] + g.y[N.v[1]] + g.y[N.v[2]]) / 3;
+    }
+}
+
+__device__ double clough_tocher(const Grid& g, int64_t tid, const Tri& T, const double* f, const double* grad,
+                                const double (&b)[3]) {
+    CTIn in;
+    ct_gather(g, tid, T, f, grad, in);
+    return ct_eval(in, b);
+}
+
+// a cell triangle's vertices (tri_verts' order) from its cell's first corner, diagonal and half
+__device__ __forceinline__ void cell_tri(int64_t p00, int64_t nh, int d, int half, int64_t (&v)[3]) {
+    const int64_t p01 = p00 + 1, p10 = p00 + nh, p11 = p10 + 1;
+    if (d == 0) {
+        v[0] = p00;
+        v[1] = half == 0 ? p01 : p11;
+        v[2] = half == 0 ? p11 : p10;
+    } else {
+        v[0] = half == 0 ? p00 : p01;
+        v[1] = half == 0 ? p01 : p11;
+        v[2] = p10;
+    }
+}
+
+// ct_gather for a lattice triangle whose cell is one cell clear of the ring (its four neighbour
+// cells are lattice cells, so tri_nbr takes no ring edge or pocket): the five cells' diagonals in
+// one batch, then every vertex value - the triangle's and its neighbours' - in a second, instead of
+// tri_verts -> tri_nbr -> across_side -> tri_verts one dependent load after another. The same
+// triangles and the same values, so ct_eval gives clough_tocher's bits. y2 (or nullptr): a second
+// gradient set (the band's extra sweep) into gy2x / gy2y. false: not such a triangle.
+__device__ __forceinline__ bool ct_gather_lattice(const Grid& g, int o, const double* f, const double* grad,
+                                                  const double* y2, CTIn& in, double (&g2x)[3], double (&g2y)[3],
+                                                  Tri& T) {
+    const int64_t nc2 = 2 * ncells(g);
+    if (o >= nc2) return false;
+    const int64_t c = o >> 1;
+    const int half = o & 1;
+    const int64_t w = g.nh - 1;
+    const int iv = (int)(c / w), ih = (int)(c - (int64_t)iv * w);
+    if (iv < 1 || iv > g.nv - 3 || ih < 1 || ih > g.nh - 3) return false;
+    const int d = g.diag[c], dB = g.diag[c - w], dT = g.diag[c + w], dL = g.diag[c - 1], dR = g.diag[c + 1];
+    const int64_t p00 = (int64_t)iv * g.nh + ih;
+    cell_tri(p00, g.nh, d, half, T.v);
+    // the neighbour across the side opposite vertex k (tri_nbr's table and across_side's cells)
+    constexpr uint64_t kSide = (2ull << 0) | (0ull << 3) | (1ull << 6) | (3ull << 9) | (4ull << 12) | (0ull << 15) |
+                               (0ull << 18) | (4ull << 21) | (1ull << 24) | (3ull << 27) | (0ull << 30) | (2ull << 33);
+    int64_t nv_[3][3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int side = (int)((kSide >> (3 * ((d * 2 + half) * 3 + k))) & 7u) - 1;
+        if (side < 0) cell_tri(p00, g.nh, d, 1 - half, nv_[k]);                    // the cell's other half
+        else if (side == 0) cell_tri(p00 - g.nh, g.nh, dB, 1, nv_[k]);             // below: its top edge
+        else if (side == 2) cell_tri(p00 + g.nh, g.nh, dT, 0, nv_[k]);             // above: its bottom edge
+        else if (side == 1) cell_tri(p00 + 1, g.nh, dR, dR == 0 ? 1 : 0, nv_[k]);  // right: its left edge
+        else cell_tri(p00 - 1, g.nh, dL, dL == 0 ? 0 : 1, nv_[k]);                 // left: its right edge
+    }
+    double nx[3][3], ny[3][3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        in.px[k] = g.x[T.v[k]];
+        in.py[k] = g.y[T.v[k]];
+        in.f[k] = f[T.v[k]];
+        in.gx[k] = grad[2 * T.v[k]];
+        in.gy[k] = grad[2 * T.v[k] + 1];
+        g2x[k] = y2 ? y2[2 * T.v[k]] : 0.0;
+        g2y[k] = y2 ? y2[2 * T.v[k] + 1] : 0.0;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            nx[k][q] = g.x[nv_[k][q]];
+            ny[k][q] = g.y[nv_[k][q]];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        in.nb[k] = true;
+        in.cx[k] = (nx[k][0] + nx[k][1] + nx[k][2]) / 3;
+        in.cy[k] = (ny[k][0] + ny[k][1] + ny[k][2]) / 3;
+    }
+    return true;
 }
 
 // nvals value sets share the triangulation: f / grad / out strided by n / 2n / mx*my
@@ -2296,6 +2413,29 @@ __global__ void __launch_bounds__(kBlock) k_gd_eval(Grid g, Targets t, const int
             continue;
         }
         const int r = (int)(i / t.mx), c = (int)(i - (int64_t)r * t.mx);
+        if (nvals == 1) {  // the cone solve's: the batched gather where it applies
+            CTIn in;
+            double g2x[3], g2y[3];
+            Tri T;
+            if (ct_gather_lattice(g, o, f, grad, be.y, in, g2x, g2y, T)) {
+                double b[3];
+                bary_v(in.px, in.py, t.gx[c], t.gy[r], b);
+                const double v0 = ct_eval(in, b);
+                out[i] = v0;
+                int64_t cc, p00;
+                if (be.y && !cone_interior(g, o, be.K, cc, p00)) {  // band_target_est on the gathered values
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) cmax = fmax(cmax, change_of(in.gx[k], in.gy[k], g2x[k], g2y[k]));
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) {
+                        in.gx[k] = g2x[k];
+                        in.gy[k] = g2y[k];
+                    }
+                    emax = fmax(emax, 2.0 * fabs(ct_eval(in, b) - v0));
+                }
+                continue;
+            }
+        }
         const Tri T = tri_verts(g, o);
         double b[3];
         bary(g, T, t.gx[c], t.gy[r], b);
