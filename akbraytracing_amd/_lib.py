@@ -29,8 +29,7 @@ FLAG_CHAIN_DIR = 1 << 28
 
 # every symbol the header declares (tests check the library exports all of them)
 EXPORTS = [
-    "akb_last_error", "akb_abi_version", "akb_sources_hash", "akb_device_count", "akb_stream_create_reserving",
-    "akb_stream_destroy",
+    "akb_last_error", "akb_abi_version", "akb_sources_hash", "akb_device_count",
     "akb_isect_f64", "akb_normal_f64", "akb_reflect_f64", "akb_normalize_f64", "akb_plane_isect_f64",
     "akb_seglen_f64", "akb_rotate_f64", "akb_fill_nan_f64",
     "akb_trace_chain_f64", "akb_chain_desc_size", "akb_tilt_opd_f64", "akb_tilt_params_f64",
