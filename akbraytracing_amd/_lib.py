@@ -19,7 +19,7 @@ c_int = ctypes.c_int
 c_dbl = ctypes.c_double
 c_vp = ctypes.c_void_p
 MAX_MIRRORS = 7
-ABI_VERSION = 16
+ABI_VERSION = 15
 
 FLAG_MISS = 0x1
 FLAG_ZERO_NORMAL = 0x2
@@ -200,8 +200,6 @@ def _declare(L):
                                      c_vp], c_int),
         "akb_gd_claim_pockets_f64": ([c_vp, c_vp, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_int, c_vp,
                                       c_vp], c_int),
-        "akb_stream_create_reserving": ([c_int, c_vp], c_int),
-        "akb_stream_destroy": ([c_vp], c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

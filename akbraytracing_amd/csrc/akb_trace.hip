@@ -1434,37 +1434,6 @@ int akb_device_count(void) {
     return n;
 }
 
-int akb_stream_create_reserving(int reserve, void** stream) {
-    clear_error();
-    AKB_REQUIRE(stream && reserve >= 0, "bad arguments");
-    int dev = 0, cus = 0;
-    AKB_REQUIRE(hipGetDevice(&dev) == hipSuccess &&
-                    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0,
-                "no device");
-    AKB_REQUIRE(reserve < cus, "cannot reserve every CU");
-    std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0u);
-    for (int i = 0; i < cus - reserve; ++i) mask[(size_t)i / 32] |= 1u << (i % 32);
-    hipStream_t s = nullptr;
-    const hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data());
-    if (e != hipSuccess) {
-        set_error("hipExtStreamCreateWithCUMask: %s", hipGetErrorString(e));
-        return AKB_E_HIP;
-    }
-    *stream = (void*)s;
-    return 0;
-}
-
-int akb_stream_destroy(void* stream) {
-    clear_error();
-    if (!stream) return 0;
-    const hipError_t e = hipStreamDestroy((hipStream_t)stream);
-    if (e != hipSuccess) {
-        set_error("hipStreamDestroy: %s", hipGetErrorString(e));
-        return AKB_E_HIP;
-    }
-    return 0;
-}
-
 int akb_isect_f64(const double coeffs[10], const double* dir, int64_t dir_ld, int64_t dir_inc,
                   const double* org, int64_t org_ld, int64_t org_inc, int negative, int64_t n,
                   double* out, int64_t out_ld, int32_t* flags, void* stream) {

@@ -94,9 +94,6 @@ def parse():
     p.add_argument("--back-stream", type=int, default=1,
                    help="1: queue each step's tilt / OPD / pupil on a second stream, concurrent with the "
                         "next step's FP64-bound pass 1 (0: behind it on one stream)")
-    p.add_argument("--reserve-cus", type=int, default=8,
-                   help="CUs the trace passes leave free (their stream's CU mask): the faithful chain's "
-                        "one-workgroup kernels then start at once instead of waiting for a pass to drain; 0: off")
     p.add_argument("--back-priority", type=int, default=0,
                    help="torch stream priority of the back stream (lower = higher priority; 0 = normal)")
     p.add_argument("--fuse", type=int, default=2,
@@ -490,15 +487,6 @@ def main():
         from akbraytracing_amd.legendre import LegendrePerturbation, config5_coefficients
         pert = LegendrePerturbation(config5_coefficients(lams[0]))
         lams = [13.5e-9, 1.35e-9, 1.35e-10]  # EUV, softXray, hardXray (:1161-1166)
-    main_stream = None
-    if args.reserve_cus > 0:
-        # the trace passes' stream: every CU but the last --reserve-cus of its mask (the streams the
-        # faithful chain, the PSF and the finishes run on keep every CU)
-        from akbraytracing_amd import _lib as LIBR
-        hs = ctypes.c_void_p()
-        LIBR.check(LIBR.lib().akb_stream_create_reserving(int(args.reserve_cus), ctypes.byref(hs)))
-        main_stream = torch.cuda.ExternalStream(hs.value, device=dev)
-        torch.cuda.set_stream(main_stream)
     rw = RayWave(geom, n, shard=shard, comm=comm, perturbation=pert)
     nsteps = [0]  # steps launched so far (which system the next one traces)
 
@@ -853,7 +841,6 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "clock_ramp": {"ms": args.ramp_ms, "untimed_steps": ramp_steps},
-        "reserved_cus": args.reserve_cus,
         "ms_per_step": el / args.steps * 1e3,
         # the same K steps timed in this process after the W warm-up steps alone, before the clock
         # ramp: the driver's plain W / K form (null with --no-ramp-form or --ramp-ms 0)

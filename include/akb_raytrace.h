@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define AKB_ABI_VERSION 16
+#define AKB_ABI_VERSION 15
 
 /* status codes */
 #define AKB_OK 0
@@ -70,12 +70,6 @@ int akb_abi_version(void);
 const char* akb_sources_hash(void);
 /* number of visible HIP devices (0 on a host without GPU; never fails) */
 int akb_device_count(void);
-/* a stream on the current device whose kernels use every CU but the last `reserve` of its CU mask
- * (hipExtStreamCreateWithCUMask): bench.py runs the trace passes on it, so the faithful chain's
- * one-workgroup kernels on the other streams always find a whole CU free instead of waiting for a
- * pass to drain. Release with akb_stream_destroy. */
-int akb_stream_create_reserving(int reserve, void** stream);
-int akb_stream_destroy(void* stream);
 
 /* ---------------- stage primitives (drop-in boundary, one reference call each) ---------------- */
 
