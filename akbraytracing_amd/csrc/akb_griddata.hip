@@ -2401,7 +2401,7 @@ __device__ __forceinline__ void band_est_store(const BandEst& be, double cmax, d
     }
 }
 
-__global__ void __launch_bounds__(kBlock) k_gd_eval(Grid g, Targets t, const int* __restrict__ owner,
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) k_gd_eval(Grid g, Targets t, const int* __restrict__ owner,
                                                     const double* f, const double* grad, int nvals, double* out,
                                                     BandEst be = BandEst{nullptr, 0, nullptr, nullptr}) {
     const int64_t m = (int64_t)t.mx * t.my, n = (int64_t)g.nv * g.nh;
