@@ -908,7 +908,8 @@ __device__ __forceinline__ void tilt_params_wave(const double* s5, const int64_t
 // to right, the short buffer last - numpy's order - then wave 0 forms the parameter block. No
 // cross-workgroup hand-off inside a kernel, so no device-scope fences.
 constexpr int kFinBPB = 32;      // buffers per k_fin_buffers block (8 per wave)
-constexpr int kFinTile = 2048;   // buffer sums staged per LDS round and wave
+constexpr int kFinTile = 512;    // buffer sums staged per LDS round and wave (20 KB of LDS: the
+                                 // kernel then fits beside the trace passes instead of waiting for a CU to drain)
 
 __global__ void __launch_bounds__(256) k_fin_buffers(akb_leaf_sink S, int64_t nfull, double* __restrict__ part,
                                                      long long* __restrict__ part_cnt) {
