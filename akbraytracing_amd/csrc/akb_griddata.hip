@@ -1330,18 +1330,27 @@ __device__ __forceinline__ void band_solve(const ConeBand& a, int64_t i, const G
 // ring vertex r of a band sweep over a group of W lanes (sub: the lane in it): the pocket chords
 // (chord_sums: each lane a strided part, the group's butterfly), then the lead lane adds the
 // vertex's lattice-edge sums and solves
+// the ring's chord slot table for the band sweeps, kChordSlots a vertex: a vertex of at most eight
+// chords has them in xidx order (-1 past them); one of nine to kChordSlots has them encoded
+// -(j + 3) (-1 past them), so a lane's first slot tells it the vertex is big; one of more has
+// kSlotBig in every slot (the xptr path, a wave for the vertex)
+constexpr int kChordSlots = 32;
+constexpr int32_t kSlotBig = -2;
+__device__ __forceinline__ int32_t slot_chord(int32_t v) { return v >= 0 ? v : v <= -3 ? -v - 3 : -1; }
+
 template <int W>
-__device__ __forceinline__ void cone_ring_vertex(const Grid& g, const ConeBand& a, int64_t r, int sub, int32_t j = -1) {
+__device__ __forceinline__ void cone_ring_vertex(const Grid& g, const ConeBand& a, int64_t r, int sub,
+                                                 const int32_t (&js)[4] = {-1, -1, -1, -1}) {
     const int64_t n = (int64_t)g.nv * g.nh;
     const int64_t i = ring_vertex(g, r);
     // every load that needs only r first: the vertex, x_{j-2} there and the lattice neighbours (with
-    // the slot table the chord j came with the vertex's big test, so its data is in flight with
+    // the slot table the chords came with the vertex's big test, so their data is in flight with
     // them: two memory latencies for the vertex)
     const double xi = g.x[i], yi = g.y[i];
     const double fi[1] = {a.f[i]};
     const bool pre = a.st.mode == 2 && sub == 0;
     const double ppx = pre ? a.gprev[2 * i] : 0.0, ppy = pre ? a.gprev[2 * i + 1] : 0.0;
-    const bool slotted = W == 8 && a.slots;  // (the same chord per lane as chord_sums<1, 8> of at most eight)
+    const bool slotted = W == 8 && a.slots;
     GradAcc<1> D;
     if (sub == 0) {
         const int iv = (int)(i / g.nh), ih = (int)(i - (int64_t)iv * g.nh);
@@ -1349,10 +1358,33 @@ __device__ __forceinline__ void cone_ring_vertex(const Grid& g, const ConeBand& 
     }
     GradAcc<1> A;
     if (slotted) {
-        if (j >= 0) {
-            const double fj[1] = {a.f[j]}, gxj[1] = {a.gin ? a.gin[2 * (int64_t)j] : 0.0},
-                         gyj[1] = {a.gin ? a.gin[2 * (int64_t)j + 1] : 0.0};
-            acc_edge<1>(A, edge_geom(g.x[j] - xi, g.y[j] - yi), fi, fj, gxj, gyj);
+        auto chord = [&](int32_t c, GradAcc<1>& C) {
+            if (c >= 0) {
+                const double fj[1] = {a.f[c]}, gxj[1] = {a.gin ? a.gin[2 * (int64_t)c] : 0.0},
+                             gyj[1] = {a.gin ? a.gin[2 * (int64_t)c + 1] : 0.0};
+                acc_edge<1>(C, edge_geom(g.x[c] - xi, g.y[c] - yi), fi, fj, gxj, gyj);
+            }
+        };
+        if (js[0] <= -3) {
+            // nine to 32 chords: chord_sums<1, 64>'s lanes sub, sub + 8, ..., sub + 56 (a chord each,
+            // zeros past them) combined as its butterfly's first three levels combine them, then the
+            // group's butterfly its last three - the 64-lane path's bits, without a wave per vertex
+            GradAcc<1> c0, c8, c16, c24;
+            const GradAcc<1> z;
+            chord(slot_chord(js[0]), c0);
+            chord(slot_chord(js[1]), c8);
+            chord(slot_chord(js[2]), c16);
+            chord(slot_chord(js[3]), c24);
+            acc_add<1>(c0, z);    // lane sub + 32
+            acc_add<1>(c16, z);   // lane sub + 48
+            acc_add<1>(c0, c16);  // (lane sub) + (lane sub + 16)
+            acc_add<1>(c8, z);
+            acc_add<1>(c24, z);
+            acc_add<1>(c8, c24);
+            acc_add<1>(c0, c8);
+            A = c0;
+        } else {  // at most eight: one chord a lane (chord_sums<1, 8>'s order)
+            chord(js[0], A);
         }
         acc_reduce<1, W>(A);
     } else {
@@ -1364,15 +1396,15 @@ __device__ __forceinline__ void cone_ring_vertex(const Grid& g, const ConeBand& 
     }
 }
 
-// the ring's chord slot table for the band sweeps: slots[8 r + k] = ring vertex r's k-th chord
-// neighbour (xidx order), -1 past its chords; a vertex of more than eight (the xptr path, a wave
-// each) has kSlotBig in all eight, so a lane's one slot load also tells it which path its vertex takes
-constexpr int32_t kSlotBig = -2;
 __global__ void k_gd_chord_slots(Grid g, int32_t* slots, int64_t L) {
     for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < L; r += (int64_t)gridDim.x * blockDim.x) {
         const int32_t k0 = g.xptr[r], cnt = g.xptr[r + 1] - k0;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) slots[r * 8 + k] = cnt > 8 ? kSlotBig : k < cnt ? g.xidx[k0 + k] : -1;
+        int32_t* sr = slots + r * kChordSlots;
+        for (int k = 0; k < kChordSlots; ++k)
+            sr[k] = cnt > kChordSlots ? kSlotBig
+                    : k >= cnt        ? -1
+                    : cnt > 8         ? -g.xidx[k0 + k] - 3
+                                      : g.xidx[k0 + k];
     }
 }
 
@@ -1501,15 +1533,18 @@ __global__ void __launch_bounds__(kBandThreads) __attribute__((amdgpu_waves_per_
     const int sub = lane & 7;
     for (int64_t r0 = w0 * 8; r0 < L; r0 += nw * 8) {
         const int64_t r = r0 + (lane >> 3);
-        int32_t j = -1;
+        int32_t js[4] = {-1, -1, -1, -1};
         bool big;
-        if (a.slots) {  // the slot says whether the vertex is big: no xptr level ahead of the vertex's loads
-            j = r < L ? a.slots[r * 8 + sub] : -1;
-            big = j == kSlotBig;
+        if (a.slots) {  // the slots say whether the vertex is big: no xptr level ahead of the vertex's loads
+            if (r < L) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) js[k] = a.slots[r * kChordSlots + sub + 8 * k];
+            }
+            big = js[0] == kSlotBig;
         } else {
             big = r < L && g.xptr[r + 1] - g.xptr[r] > 8;
         }
-        if (r < L && !big) cone_ring_vertex<8>(g, a, r, sub, j);
+        if (r < L && !big) cone_ring_vertex<8>(g, a, r, sub, js);
         unsigned long long m = __ballot(big && sub == 0);
         while (m) {  // wave-uniform
             const int q = __builtin_ctzll(m);
@@ -2667,7 +2702,7 @@ static int64_t claim_scratch_offset(int nv, int nh, int mx, int my, int nvals) {
     const int64_t n = (int64_t)nv * nh, L = 2 * (int64_t)(nh - 1) + 2 * (int64_t)(nv - 1);
     const int nv2 = nvals >= 2 ? 2 : 1;
     const int64_t m = (int64_t)mx * my;
-    return (3 * (int64_t)nv2 * n * 2 * 8 + L * 7 * 8 + m * 8 + m + 64 + 63) / 64 * 64;
+    return (3 * (int64_t)nv2 * n * 2 * 8 + L * 16 * 8 + m * 8 + m + 64 + 63) / 64 * 64;
 }
 
 int64_t akb_gd_cone_work_bytes(int nv, int nh, int mx, int my, int nvals) {
@@ -2715,7 +2750,7 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
     double* gb[3];
     for (int k = 0; k < 3; ++k) gb[k] = (double*)work + (int64_t)k * n * 2;
     const int nv2 = nvals >= 2 ? 2 : 1;  // the work layout's (claim_scratch_offset)
-    int64_t* cells = (int64_t*)((double*)work + 3 * (int64_t)nv2 * n * 2 + L * 7);
+    int64_t* cells = (int64_t*)((double*)work + 3 * (int64_t)nv2 * n * 2 + L * 16);
     uint8_t* assigned = (uint8_t*)(cells + m);
     int* count = (int*)(((uintptr_t)(assigned + m) + 7) & ~(uintptr_t)7);
     int* band = count + 1;
@@ -2742,7 +2777,7 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
         // whose neighbours (depth <= 2K + 4 - j) sweep j - 1 formed, so x_K is the global iteration's
         // to depth K + 3 >= every band target's corners (the first sweep reads x_0 = 0 only)
         if (band_on) {
-            // the ring's chord slots (the work's (L, 7)-double region, free in the cone solve)
+            // the ring's chord slots (the work's (L, 16)-double region: kChordSlots int32 a vertex)
             int32_t* slots = (int32_t*)((double*)work + 3 * (int64_t)nv2 * n * 2);
             if (v == 0) {
                 k_gd_chord_slots<<<grid_for(L), kBlock, 0, s>>>(g, slots, L);
