@@ -1408,9 +1408,10 @@ __global__ void k_gd_chord_slots(Grid g, int32_t* slots, int64_t L) {
     }
 }
 
-// one sweep of the band in one launch: workgroups [0, nr8) eight ring vertices per wave (8-lane
-// groups; a vertex with more than eight chords takes the whole wave afterwards) - first, so the
-// ring's dependent chord loads overlap the tiles - the rest a band tile each - its vertices
+// one sweep of the band in one launch: the band tiles first, then nr8 workgroups of ring vertices,
+// eight a wave (8-lane groups; a vertex of more than 32 chords takes the whole wave afterwards):
+// the grid is more than one round at two workgroups a CU, and the ring's workgroups, the shorter,
+// then fill the slots the tiles free. A band tile workgroup: its vertices
 // and their neighbours' x, y, f and x_{j-1} (and the cells' diagonals) staged in LDS by coalesced
 // row loads, then one thread per vertex off the ring (band_edges from LDS: the gather kernel's
 // arithmetic, two vertices a thread, x_{j-2} loaded with the tile). Both halves read x_{j-1} /
@@ -1430,12 +1431,13 @@ __device__ __forceinline__ void band_clock(unsigned long long* clk, int k, unsig
 __global__ void __launch_bounds__(kBandThreads) __attribute__((amdgpu_waves_per_eu(4))) k_gd_cone_band(Grid g, BandTiles bt, ConeBand a, int nr8) {
     if (!*a.needed) return;
     const unsigned long long t0 = a.clk ? wall_clock64() : 0;
-    if ((int)blockIdx.x >= nr8) {
+    const int ntile = (int)gridDim.x - nr8;
+    if ((int)blockIdx.x < ntile) {
         constexpr int HR = kBandTR + 2, HC = kBandTC + 2, HN = HR * HC, CC = kBandTC + 1;
         __shared__ double sx[HN], sy[HN], sf[HN], sgx[HN], sgy[HN];
         __shared__ uint8_t sdg[(kBandTR + 1) * CC];
         int r0, c0, r1, c1;
-        band_tile(bt, g.nv, g.nh, blockIdx.x - nr8, r0, c0, r1, c1);
+        band_tile(bt, g.nv, g.nh, blockIdx.x, r0, c0, r1, c1);
         // the tile's vertices with a one-vertex halo (rows r0 - 1 .. r0 + TR, inside the lattice) and
         // the diagonals of cells (r0 - 1 .. r0 + TR - 1) x (c0 - 1 .. c0 + TC - 1): every load of a
         // thread issued before the first LDS store (one memory latency per tile)
@@ -1528,7 +1530,7 @@ __global__ void __launch_bounds__(kBandThreads) __attribute__((amdgpu_waves_per_
     }
     const int64_t L = 2 * (int64_t)(g.nh - 1) + 2 * (int64_t)(g.nv - 1);
     const int lane = threadIdx.x & 63;
-    const int64_t w0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t w0 = ((int64_t)(blockIdx.x - ntile) * blockDim.x + threadIdx.x) >> 6;
     const int64_t nw = ((int64_t)nr8 * blockDim.x) >> 6;
     const int sub = lane & 7;
     for (int64_t r0 = w0 * 8; r0 < L; r0 += nw * 8) {
