@@ -1263,7 +1263,7 @@ struct ConeBand {
     double* gout;         // x_j
     ConeStep st;
     const int* needed;    // device flag: some target needs the band (else the launch returns at once)
-    unsigned long long* clk = nullptr;  // diagnostics (or nullptr): the ring / tile workgroups' wall-clock
+    unsigned long long* clk = nullptr;  // diagnostics (or nullptr): the ring-only / tile workgroups' wall-clock
                                         // time summed, their counts, their longest (akb_gd_patch_phases)
     const int32_t* slots = nullptr;     // (L, 8): ring vertex r's chord neighbours padded with -1 (or nullptr)
 };
@@ -1408,16 +1408,17 @@ __global__ void k_gd_chord_slots(Grid g, int32_t* slots, int64_t L) {
     }
 }
 
-// one sweep of the band in one launch: the band tiles first, then nr8 workgroups of ring vertices,
-// eight a wave (8-lane groups; a vertex of more than 32 chords takes the whole wave afterwards):
-// the grid is more than one round at two workgroups a CU, and the ring's workgroups, the shorter,
-// then fill the slots the tiles free. A band tile workgroup: its vertices
-// and their neighbours' x, y, f and x_{j-1} (and the cells' diagonals) staged in LDS by coalesced
-// row loads, then one thread per vertex off the ring (band_edges from LDS: the gather kernel's
-// arithmetic, two vertices a thread, x_{j-2} loaded with the tile). Both halves read x_{j-1} /
-// x_{j-2} only.
-constexpr int kBandThreads = 512, kBandVR = kBandTR * kBandTC / kBandThreads;
-// a workgroup's wall-clock time into the diagnostics words (ring: k = 0, tile: k = 1)
+// one sweep of the band in one launch, one round of workgroups at two a CU: workgroup b takes ring
+// vertices [32 b, 32 b + 32) on its first four waves (8-lane groups: a vertex's chords over the
+// group, its lattice edges on the lead lane; a vertex of more than 32 chords takes its whole wave
+// afterwards) and, for b < the tile count, band tile b on its last four - the tile's vertices and
+// their neighbours' x, y, f and x_{j-1} (and the cells' diagonals), and x_{j-2} of its vertices,
+// staged in LDS by all eight waves with coalesced row loads, then four vertices a thread off the
+// ring (band_edges from LDS: the gather kernel's arithmetic). The ring's dependent loads and the
+// tile's arithmetic overlap inside the workgroup. Both halves read x_{j-1} / x_{j-2} only.
+constexpr int kBandThreads = 512, kBandRingWaves = 4, kBandRingPer = 8 * kBandRingWaves;
+constexpr int kBandTileThreads = kBandThreads - 64 * kBandRingWaves, kBandVR = kBandTR * kBandTC / kBandTileThreads;
+// a workgroup's wall-clock time into the diagnostics words (ring only: k = 0, with a tile: k = 1)
 __device__ __forceinline__ void band_clock(unsigned long long* clk, int k, unsigned long long t0) {
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1427,22 +1428,29 @@ __device__ __forceinline__ void band_clock(unsigned long long* clk, int k, unsig
         atomicMax(&clk[4 + k], d);
     }
 }
+// the band launch's workgroups: every tile, and enough for the ring at kBandRingPer a workgroup
+inline unsigned band_grid(const BandTiles& bt, int64_t L) {
+    const int64_t nr = (L + kBandRingPer - 1) / kBandRingPer;
+    return (unsigned)(bt.total > nr ? bt.total : nr);
+}
 
-__global__ void __launch_bounds__(kBandThreads) __attribute__((amdgpu_waves_per_eu(4))) k_gd_cone_band(Grid g, BandTiles bt, ConeBand a, int nr8) {
+__global__ void __launch_bounds__(kBandThreads) __attribute__((amdgpu_waves_per_eu(4))) k_gd_cone_band(Grid g, BandTiles bt, ConeBand a) {
     if (!*a.needed) return;
     const unsigned long long t0 = a.clk ? wall_clock64() : 0;
-    const int ntile = (int)gridDim.x - nr8;
-    if ((int)blockIdx.x < ntile) {
-        constexpr int HR = kBandTR + 2, HC = kBandTC + 2, HN = HR * HC, CC = kBandTC + 1;
-        __shared__ double sx[HN], sy[HN], sf[HN], sgx[HN], sgy[HN];
-        __shared__ uint8_t sdg[(kBandTR + 1) * CC];
-        int r0, c0, r1, c1;
+    constexpr int HR = kBandTR + 2, HC = kBandTC + 2, HN = HR * HC, CC = kBandTC + 1;
+    __shared__ double sx[HN], sy[HN], sf[HN], sgx[HN], sgy[HN];
+    __shared__ double spx[kBandTR * kBandTC], spy[kBandTR * kBandTC];  // x_{j-2} of the tile's vertices
+    __shared__ uint8_t sdg[(kBandTR + 1) * CC];
+    const bool has_tile = (int)blockIdx.x < bt.total;  // (workgroup-uniform)
+    int r0 = 0, c0 = 0, r1 = 0, c1 = 0;
+    if (has_tile) {
         band_tile(bt, g.nv, g.nh, blockIdx.x, r0, c0, r1, c1);
-        // the tile's vertices with a one-vertex halo (rows r0 - 1 .. r0 + TR, inside the lattice) and
-        // the diagonals of cells (r0 - 1 .. r0 + TR - 1) x (c0 - 1 .. c0 + TC - 1): every load of a
-        // thread issued before the first LDS store (one memory latency per tile)
+        // the tile's vertices with a one-vertex halo (rows r0 - 1 .. r0 + TR, inside the lattice), the
+        // diagonals of cells (r0 - 1 .. r0 + TR - 1) x (c0 - 1 .. c0 + TC - 1) and x_{j-2} of the tile's
+        // vertices: every load of a thread issued before the first LDS store (one memory latency)
         constexpr int NQ = (HN + kBandThreads - 1) / kBandThreads, NC = ((kBandTR + 1) * CC + kBandThreads - 1) / kBandThreads;
-        double lx[NQ], ly[NQ], lf[NQ], lgx[NQ], lgy[NQ];
+        constexpr int NP = kBandTR * kBandTC / kBandThreads;
+        double lx[NQ], ly[NQ], lf[NQ], lgx[NQ], lgy[NQ], lpx[NP], lpy[NP];
         uint8_t ld[NC];
 #pragma unroll
         for (int u = 0; u < NQ; ++u) {
@@ -1466,6 +1474,17 @@ __global__ void __launch_bounds__(kBandThreads) __attribute__((amdgpu_waves_per_
                         ? g.diag[(int64_t)cv * (g.nh - 1) + ch] : 0;
         }
 #pragma unroll
+        for (int u = 0; u < NP; ++u) {
+            const int k = threadIdx.x + u * kBandThreads;
+            const int iv = r0 + k / kBandTC, ih = c0 + (k - (k / kBandTC) * kBandTC);
+            lpx[u] = lpy[u] = 0.0;
+            if (a.st.mode == 2 && iv < r1 && ih < c1) {
+                const int64_t o = 2 * ((int64_t)iv * g.nh + ih);
+                lpx[u] = a.gprev[o];
+                lpy[u] = a.gprev[o + 1];
+            }
+        }
+#pragma unroll
         for (int u = 0; u < NQ; ++u) {
             const int k = threadIdx.x + u * kBandThreads;
             if (k < HN) {
@@ -1481,21 +1500,43 @@ __global__ void __launch_bounds__(kBandThreads) __attribute__((amdgpu_waves_per_
             const int k = threadIdx.x + u * kBandThreads;
             if (k < (kBandTR + 1) * CC) sdg[k] = ld[u];
         }
-        // this thread's vertices: rows tr and tr + TR / 2 of the tile; their x_{j-2} before the barrier
-        const int tr0 = threadIdx.x / kBandTC, tc = threadIdx.x - (threadIdx.x / kBandTC) * kBandTC;
-        double ppx[kBandVR], ppy[kBandVR];
 #pragma unroll
-        for (int u = 0; u < kBandVR; ++u) {
-            const int iv = r0 + tr0 + u * (kBandTR / kBandVR), ih = c0 + tc;
-            ppx[u] = ppy[u] = 0.0;
-            if (a.st.mode == 2 && iv < r1 && ih < c1) {
-                const int64_t o = 2 * ((int64_t)iv * g.nh + ih);
-                ppx[u] = a.gprev[o];
-                ppy[u] = a.gprev[o + 1];
-            }
+        for (int u = 0; u < NP; ++u) {
+            const int k = threadIdx.x + u * kBandThreads;
+            spx[k] = lpx[u];
+            spy[k] = lpy[u];
         }
         __syncthreads();
+    }
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (w < kBandRingWaves) {
+        const int64_t L = 2 * (int64_t)(g.nh - 1) + 2 * (int64_t)(g.nv - 1);
+        const int sub = lane & 7;
+        for (int64_t q0 = (int64_t)blockIdx.x * kBandRingPer + 8 * w; q0 < L; q0 += (int64_t)gridDim.x * kBandRingPer) {
+            const int64_t r = q0 + (lane >> 3);
+            int32_t js[4] = {-1, -1, -1, -1};
+            bool big;
+            if (a.slots) {  // the slots say whether the vertex is big: no xptr level ahead of the vertex's loads
+                if (r < L) {
 #pragma unroll
+                    for (int k = 0; k < 4; ++k) js[k] = a.slots[r * kChordSlots + sub + 8 * k];
+                }
+                big = js[0] == kSlotBig;
+            } else {
+                big = r < L && g.xptr[r + 1] - g.xptr[r] > 8;
+            }
+            if (r < L && !big) cone_ring_vertex<8>(g, a, r, sub, js);
+            unsigned long long m = __ballot(big && sub == 0);
+            while (m) {  // wave-uniform
+                const int q = __builtin_ctzll(m);
+                m &= m - 1;
+                cone_ring_vertex<64>(g, a, q0 + (q >> 3), lane);
+            }
+        }
+    } else if (has_tile) {
+        const int tt = threadIdx.x - 64 * kBandRingWaves;
+        const int tr0 = tt / kBandTC, tc = tt - (tt / kBandTC) * kBandTC;
+#pragma unroll 1
         for (int u = 0; u < kBandVR; ++u) {
             const int tr = tr0 + u * (kBandTR / kBandVR);
             const int iv = r0 + tr, ih = c0 + tc;
@@ -1523,38 +1564,11 @@ __global__ void __launch_bounds__(kBandThreads) __attribute__((amdgpu_waves_per_
                                 inb[7] && dg[3] == 0};
             GradAcc<1> A;
             band_edges(A, sx[li], sy[li], sf[li], xs, ys, fs, gxs, gys, on);
-            band_solve(a, (int64_t)iv * g.nh + ih, A, ppx[u], ppy[u]);
-        }
-        if (a.clk) band_clock(a.clk + 4, 1, t0);
-        return;
-    }
-    const int64_t L = 2 * (int64_t)(g.nh - 1) + 2 * (int64_t)(g.nv - 1);
-    const int lane = threadIdx.x & 63;
-    const int64_t w0 = ((int64_t)(blockIdx.x - ntile) * blockDim.x + threadIdx.x) >> 6;
-    const int64_t nw = ((int64_t)nr8 * blockDim.x) >> 6;
-    const int sub = lane & 7;
-    for (int64_t r0 = w0 * 8; r0 < L; r0 += nw * 8) {
-        const int64_t r = r0 + (lane >> 3);
-        int32_t js[4] = {-1, -1, -1, -1};
-        bool big;
-        if (a.slots) {  // the slots say whether the vertex is big: no xptr level ahead of the vertex's loads
-            if (r < L) {
-#pragma unroll
-                for (int k = 0; k < 4; ++k) js[k] = a.slots[r * kChordSlots + sub + 8 * k];
-            }
-            big = js[0] == kSlotBig;
-        } else {
-            big = r < L && g.xptr[r + 1] - g.xptr[r] > 8;
-        }
-        if (r < L && !big) cone_ring_vertex<8>(g, a, r, sub, js);
-        unsigned long long m = __ballot(big && sub == 0);
-        while (m) {  // wave-uniform
-            const int q = __builtin_ctzll(m);
-            m &= m - 1;
-            cone_ring_vertex<64>(g, a, r0 + (q >> 3), lane);
+            const int pk = tr * kBandTC + tc;
+            band_solve(a, (int64_t)iv * g.nh + ih, A, spx[pk], spy[pk]);
         }
     }
-    if (a.clk) band_clock(a.clk + 4, 0, t0);
+    if (a.clk) band_clock(a.clk + 4, has_tile ? 1 : 0, t0);
 }
 
 struct ConePatch {
@@ -2789,18 +2803,16 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
                 const double* gin = j == 1 ? nullptr : gb[(j - 1) % 3];
                 const double* gprev = j >= 3 ? gb[(j + 1) % 3] : nullptr;
                 const BandTiles bt = band_tiles(g.nv, g.nh, 2 * K + 3 - j);
-                const unsigned nr8 = (unsigned)(((L + 7) / 8 * 64 + kBandThreads - 1) / kBandThreads);
                 const ConeBand a{fv, gin, gprev, gb[j % 3], steps[j], band, patch_timer().on ? patch_timer().clk : nullptr,
                                  slots};
-                k_gd_cone_band<<<bt.total + nr8, kBandThreads, 0, s>>>(g, bt, a, (int)nr8);
+                k_gd_cone_band<<<band_grid(bt, L), kBandThreads, 0, s>>>(g, bt, a);
                 if ((st = launch_status("k_gd_cone_band"))) return st;
             }
             if (d_change) {  // one more plain sweep, y from x_K to depth K + 2 (the band targets' corners)
                 const BandTiles bt = band_tiles(g.nv, g.nh, K + 2);
-                const unsigned nr8 = (unsigned)(((L + 7) / 8 * 64 + kBandThreads - 1) / kBandThreads);
                 const ConeBand a{fv, gb[K % 3], nullptr, gb[(K + 1) % 3], ConeStep{0, 1.0}, band,
                                  patch_timer().on ? patch_timer().clk : nullptr, slots};
-                k_gd_cone_band<<<bt.total + nr8, kBandThreads, 0, s>>>(g, bt, a, (int)nr8);
+                k_gd_cone_band<<<band_grid(bt, L), kBandThreads, 0, s>>>(g, bt, a);
                 if ((st = launch_status("k_gd_cone_band"))) return st;
             }
         }

@@ -712,9 +712,10 @@ def main():
                 patch["workgroup0_phases"] = {"setup_frac": ph[0] / tot, "sweeps_frac": ph[1] / tot,
                                               "rest_frac": ph[2] / tot, "steps": int(ph[3]),
                                               "us_per_step": tot * 0.01 / max(int(ph[3]), 1)}
-            if ph[5] and ph[7]:  # the band sweeps' workgroups (diagnostics)
-                patch["band_workgroups"] = {"ring_avg_us": ph[4] * 0.01 / ph[5], "ring_max_us": ph[8] * 0.01,
-                                            "tile_avg_us": ph[6] * 0.01 / ph[7], "tile_max_us": ph[9] * 0.01}
+            if ph[7]:  # the band sweeps' workgroups (diagnostics): with a tile (and its ring share), ring only
+                patch["band_workgroups"] = {"tile_avg_us": ph[6] * 0.01 / ph[7], "tile_max_us": ph[9] * 0.01,
+                                            "ring_only_avg_us": ph[4] * 0.01 / ph[5] if ph[5] else None,
+                                            "ring_only_max_us": ph[8] * 0.01 if ph[5] else None}
     while fronts:  # the last front's back half (outside the timed region, like the first one's)
         back(False)
     while tickets:

@@ -543,8 +543,8 @@ int akb_gd_patch_times(float* ms, int* cells, int max);
 /* while timing (100 MHz wall-clock ticks, summed over the launches since akb_gd_patch_timing(1);
  * waits for the device), out[0..9]: the patch kernel's workgroup 0 in its steps' phases - the
  * setup (box in, vertex constants), the sweeps, the rest (corners, next box) - and its step count;
- * the band sweeps' ring workgroups' time and count, their tile workgroups' time and count, the
- * longest ring and tile workgroup */
+ * the band sweeps' ring-only workgroups' time and count, their workgroups with a tile (and a share
+ * of the ring) time and count, the longest of each */
 int akb_gd_patch_phases(unsigned long long* out);
 /* The driver's target axes (AKB_raytrace_20250312.py:3654-3657): gx = np.linspace(min, max, mx) of
  * the lattice's x (its extremes lie on the boundary ring akb_gd_cells_f64 returns), gy likewise of
