@@ -625,6 +625,16 @@ struct LineShape {
     static_assert(Q >= 1 && Q2 <= SIG && PAD % SIG == 0, "line transform shape");
 };
 
+// threads of a workgroup: the 1024-point fp64 lines run two lanes j and j + 512 per thread in
+// 512-thread workgroups (a 1024-thread workgroup caps a thread at 128 VGPRs, and a lane's sixteen
+// outputs held across the second chunk's transform spilled past it; at 512 the cap is 256)
+template <int N, int PAD, int MODE>
+struct LineThreads {
+    static constexpr int kLanes = (N >= 1024 && MODE != kLinePeak32) ? 2 : 1;
+    static constexpr int kThreads = LineShape<N, PAD>::kThreads / kLanes;
+    static_assert(kLanes == 1 || (LineShape<N, PAD>::LINES == 1 && kThreads % PAD == 0), "lane split");
+};
+
 struct PsfLineArgs {
     const double* opd;
     const double* amp;
@@ -670,8 +680,9 @@ constexpr int kSelRows = 256;
 constexpr double kBoundMarginSel = 1.0 + 0x1p-20;
 
 template <int N, int PAD, int MODE>
-__global__ void __launch_bounds__((LineShape<N, PAD>::kThreads)) k_psf_line(PsfLineArgs A) {
+__global__ void __launch_bounds__((LineThreads<N, PAD, MODE>::kThreads)) k_psf_line(PsfLineArgs A) {
     using S = LineShape<N, PAD>;
+    constexpr int LPT = LineThreads<N, PAD, MODE>::kLanes, NT = LineThreads<N, PAD, MODE>::kThreads;
     using R = typename std::conditional<MODE == kLinePeak32, float, double>::type;
     using V = typename Cx<R>::T;
     constexpr int SIG = S::SIG, Q = S::Q, Q2 = S::Q2, LINES = S::LINES, TS = S::TS;
@@ -679,7 +690,7 @@ __global__ void __launch_bounds__((LineShape<N, PAD>::kThreads)) k_psf_line(PsfL
     __shared__ V Yc[LINES * SIG * N];
     __shared__ V gl[LINES * N];
     __shared__ V tab[S::kTab];
-    __shared__ double wm[S::kThreads / 64];
+    __shared__ double wm[NT / 64];
     // select route (pass 1 of planes up to 4096 rows: per-workgroup row sums; the peak pass: its rows)
     constexpr int BS = (MODE == kLinePupil && N * PAD <= 4096) ? N * PAD : 1;
     constexpr bool kSelPeak = MODE == kLinePeak;
@@ -694,8 +705,9 @@ __global__ void __launch_bounds__((LineShape<N, PAD>::kThreads)) k_psf_line(PsfL
     const int b = blockIdx.y;
     const bool sel1 = BS > 1 && A.bpart != nullptr;  // pass 1 leaves the select route's parts
     const double2* WP = MODE == kLinePupil ? A.Wy : A.Wx;
-    const int line = threadIdx.x / N, i = threadIdx.x % N;
-    const int t = i % PAD, q2 = i / TS;
+    const int line = threadIdx.x / N, i0 = threadIdx.x % N;
+    int i = i0, q2 = i0 / TS;  // the current lane (below: lane(h)) and its four-step row
+    int t = i0 % PAD;          // the same for every lane of a thread (NT is a multiple of PAD)
     // lines of this pass: pupil columns (pass 1), psf rows, or the fp64 peak pass's row list
     int nl = MODE == kLinePupil ? g.nx2 : g.py;
     const int* rows = nullptr;
@@ -727,10 +739,10 @@ __global__ void __launch_bounds__((LineShape<N, PAD>::kThreads)) k_psf_line(PsfL
     };
     double2 sacc = make_double2(0.0, 0.0);
     if (sel1) {
-        for (int k = threadIdx.x; k < BS; k += S::kThreads) Bsum[k] = 0.0;
+        for (int k = threadIdx.x; k < BS; k += NT) Bsum[k] = 0.0;
         if (group_at(0) < 0) {  // no columns here: its parts are zero
             double* bp = A.bpart + ((int64_t)b * A.npart + blockIdx.x) * g.py;
-            for (int k = threadIdx.x; k < g.py; k += S::kThreads) bp[k] = 0.0;
+            for (int k = threadIdx.x; k < g.py; k += NT) bp[k] = 0.0;
             if (threadIdx.x < kSel) A.spart[((int64_t)b * A.npart + blockIdx.x) * 32 + threadIdx.x] = sacc;
             return;
         }
@@ -744,10 +756,10 @@ __global__ void __launch_bounds__((LineShape<N, PAD>::kThreads)) k_psf_line(PsfL
         int nmine = 0;
         for (int k = 0; group_at(k) >= 0; ++k) nmine += LINES;
         const bool fits = nmine <= kSelRows;
-        for (int e = threadIdx.x; e < 3 * kSel + kSelRows; e += S::kThreads) ssum[e] = 0.0;
+        for (int e = threadIdx.x; e < 3 * kSel + kSelRows; e += NT) ssum[e] = 0.0;
         if (threadIdx.x == 0) lcount = 0;
         __syncthreads();
-        for (int e = threadIdx.x; e < kSel * np; e += S::kThreads) {
+        for (int e = threadIdx.x; e < kSel * np; e += NT) {
             const int k = e % kSel, w = e / kSel;
             const double2 tv = A.spart[(pb + w) * 32 + k];
             atomicAdd(&ssum[k], tv.x);
@@ -755,7 +767,7 @@ __global__ void __launch_bounds__((LineShape<N, PAD>::kThreads)) k_psf_line(PsfL
             atomicAdd(&ssum[2 * kSel + k], A.bpart[(pb + w) * g.py + g.py / 2 - 2 + k / 5]);
         }
         if (fits)
-            for (int e = threadIdx.x; e < nmine * np; e += S::kThreads) {
+            for (int e = threadIdx.x; e < nmine * np; e += NT) {
                 const int q = e / np, w = e - (e / np) * np;
                 const int row = group_at(q / LINES) * LINES + q % LINES;
                 if (row < nl) atomicAdd(&ssum[3 * kSel + q], A.bpart[(pb + w) * g.py + row]);
@@ -776,7 +788,7 @@ __global__ void __launch_bounds__((LineShape<N, PAD>::kThreads)) k_psf_line(PsfL
         const bool all = !(M > 0.0) || !isfinite(M);
         // this workgroup's rows (the all-rows pass's assignment): keep those with B >= M_low
         if (!all && fits) {
-            for (int q = threadIdx.x; q < nmine; q += S::kThreads) {
+            for (int q = threadIdx.x; q < nmine; q += NT) {
                 const int row = group_at(q / LINES) * LINES + q % LINES;
                 const double bs = ssum[3 * kSel + q];
                 if (row < nl && !((bs * bs) * kBoundMarginSel < M)) lrows[atomicAdd(&lcount, 1)] = row;
@@ -797,7 +809,7 @@ __global__ void __launch_bounds__((LineShape<N, PAD>::kThreads)) k_psf_line(PsfL
     V* TA = tab;
     V* TB = tab + Q2 * PAD;
     V* TQ = tab + Q2 * PAD + SIG * PAD;
-    for (int e = threadIdx.x; e < S::kTab; e += S::kThreads) {
+    for (int e = threadIdx.x; e < S::kTab; e += NT) {
         int m;
         if (S::kFour) {
             if (e < Q2 * PAD)
@@ -875,39 +887,158 @@ __global__ void __launch_bounds__((LineShape<N, PAD>::kThreads)) k_psf_line(PsfL
 
     double m = 0.0, nan_sum = 0.0;
     unsigned m32 = 0u;
+    auto lane = [&](int h) {  // lane h of this thread: j = i0 + h NT
+        int x = i0;
+        // two lanes: the lane index opaque at each phase, so the LDS addresses derived from it are
+        // formed where they are used instead of hoisted out of the line loop (four phases x eight
+        // addresses x two lanes held across every line would fill the registers)
+        if constexpr (LPT > 1) asm volatile("" : "+v"(x));
+        i = x + h * NT;
+        q2 = i / TS;
+        t = i % PAD;
+    };
     int grp = group_at(0);
-    double2 pre = fetch(line_of(grp));
+    double2 pre[LPT];
+#pragma unroll
+    for (int h = 0; h < LPT; ++h) {
+        lane(h);
+        pre[h] = fetch(line_of(grp));
+    }
     for (int k = 0; grp >= 0; ++k) {
         const int L = line_of(grp);
         const int next = group_at(k + 1);
         __syncthreads();  // the previous group is done with gl / Yc / wm (and the tables are in)
-        gl[line * N + i] = input(pre, L);
-        pre = fetch(line_of(next));
+#pragma unroll
+        for (int h = 0; h < LPT; ++h) {
+            lane(h);
+            gl[line * N + i] = input(pre[h], L);
+            pre[h] = fetch(line_of(next));
+        }
         __syncthreads();
-        V v[PAD];
-        const double2 w1d = WP[i];  // W_P^j (reloaded per line: fewer registers held across it)
-        const V w1 = Cx<R>::mk((R)w1d.x, (R)w1d.y);
-        const V wch = S::CH == 1 ? w1 : cmul_r<R>(w1, w1);
+        V v[LPT][PAD];
+        // a lane's outputs, formed as soon as its last chunk is done (its registers then free for
+        // the next lane)
+        auto emit = [&](const V (&vh)[PAD]) {
+            if constexpr (MODE == kLinePupil) {
+                if (L >= 0) {
+                    double2* Gl = A.G + ((int64_t)b * g.nx2 + L) * g.py + i;
+#pragma unroll
+                    for (int r = 0; r < PAD; ++r) Gl[(int64_t)N * r] = vh[r];
+                }
+                if constexpr (BS > 1) {
+                    if (sel1) {
+                        // |G| into the row sums, one line after the other (a fixed order); the sample
+                        // rows' values to LDS
+                        for (int ln = 0; ln < LINES; ++ln) {
+                            __syncthreads();
+                            if (line == ln && L >= 0) {
+#pragma unroll
+                                for (int r = 0; r < PAD; ++r) Bsum[i + N * r] += sqrt(fma(vh[r].x, vh[r].x, vh[r].y * vh[r].y));
+                            }
+                        }
+                        if (i == 0) Lc[line] = L;
+#pragma unroll
+                        for (int r = 0; r < PAD; ++r) {
+                            const int d = i + N * r - (N * PAD / 2 - 2);
+                            if (d >= 0 && d < 5) Gs[line][d] = L >= 0 ? vh[r] : make_double2(0.0, 0.0);
+                        }
+                        __syncthreads();
+                        if (threadIdx.x < kSel) {  // sample (ko = py/2 - 2 + k / 5, lo = px/2 - 2 + k % 5)
+                            const int dk = threadIdx.x / 5, lo = g.px / 2 - 2 + threadIdx.x % 5;
+                            for (int ln = 0; ln < LINES; ++ln) {
+                                const int x = Lc[ln];
+                                if (x < 0) continue;
+                                double2 t = cmul(Gs[ln][dk], A.Wx[((int64_t)lo * x) % g.px]);
+                                if (x & 1) t = make_double2(-t.x, -t.y);
+                                sacc.x += t.x;
+                                sacc.y += t.y;
+                            }
+                        }
+                    }
+                }
+            } else if constexpr (MODE == kLinePeak32) {
+                // this row's max (uint order of non-negative floats is numeric, NaN above +inf)
+                unsigned mr = 0u;
+#pragma unroll
+                for (int r = 0; r < PAD; ++r) {
+                    const float U = fmaf(vh[r].x, vh[r].x, vh[r].y * vh[r].y);
+                    mr = max(mr, __float_as_uint(U));
+                }
+                constexpr int W = N < 64 ? N : 64;
+#pragma unroll
+                for (int off = 1; off < W; off <<= 1) mr = max(mr, (unsigned)__shfl_xor((int)mr, off));
+                if (N > 64) {
+                    if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = (double)__uint_as_float(mr);
+                    __syncthreads();
+                    if (i == 0)
+                        for (int w = 1; w < N / 64; ++w) mr = max(mr, __float_as_uint((float)wm[(threadIdx.x >> 6) + w]));
+                }
+                if (i == 0 && L >= 0) {
+                    A.rowmax32[(int64_t)b * g.py + L] = __uint_as_float(mr);
+                    m32 = max(m32, mr);
+                }
+            } else {
+              if (L >= 0) {
+                double* Pr = A.psf + ((int64_t)b * g.py + L) * g.px + i;
+                double2* Er = A.efield + ((int64_t)b * g.py + L) * g.px + i;
+#pragma unroll
+                for (int r = 0; r < PAD; ++r) {
+                    const double U = fma(vh[r].x, vh[r].x, vh[r].y * vh[r].y);
+                    if (MODE == kLinePeak) {
+                        m = fmax(m, U);
+                        nan_sum += U;  // NaN iff some U is NaN (U >= 0): numpy's max propagates it
+                    } else {
+                        if (AKB_PSF_NT)
+                            __builtin_nontemporal_store(U * scale, Pr + N * r);
+                        else
+                            Pr[N * r] = U * scale;
+                        if (MODE == kLineWriteE) {
+                            const double re = vh[r].x * dA, im = vh[r].y * dA;
+                            const int lo = i + N * r;
+                            const double2 py_ph = A.Wy[((int64_t)L * (g.ny2 / 2)) % g.py];
+                            const double2 px_ph = A.Wx[((int64_t)lo * (g.nx2 / 2)) % g.px];
+                            double2 e = cmul(make_double2(re, im), make_double2(py_ph.x, -py_ph.y));
+                            e = cmul(e, make_double2(px_ph.x, -px_ph.y));
+                            Er[N * r] = make_double2(sgn * e.x / sq, sgn * e.y / sq);
+                        }
+                    }
+                }
+              }
+            }
+        };
+        V w1[LPT], wch[LPT];
+#pragma unroll
+        for (int h = 0; h < LPT; ++h) {
+            const double2 w1d = WP[i0 + h * NT];  // W_P^j (reloaded per line: fewer registers held across it)
+            w1[h] = Cx<R>::mk((R)w1d.x, (R)w1d.y);
+            wch[h] = S::CH == 1 ? w1[h] : cmul_r<R>(w1[h], w1[h]);
+        }
         V* Yl = Yc + line * SIG * N;
         const V* gll = gl + line * N;
 #pragma unroll
         for (int c = 0; c < S::CH; ++c) {
             if constexpr (!S::kFour) {
 #pragma unroll
-                for (int kk = 0; kk < SIG / Q; ++kk) {
-                    const int s_l = (i + kk * N) / PAD, s = S::CH * s_l + c;
-                    V w[Q];
+                for (int h = 0; h < LPT; ++h) {
+                    lane(h);
 #pragma unroll
-                    for (int q = 0; q < Q; ++q) {
-                        const V x = gll[PAD * q + s];
-                        w[bitrev_c(q, LQ)] = q ? cmul_r<R>(x, tab[q * PAD + t]) : x;
+                    for (int kk = 0; kk < SIG / Q; ++kk) {
+                        const int s_l = (i + kk * N) / PAD, s = S::CH * s_l + c;
+                        V w[Q];
+#pragma unroll
+                        for (int q = 0; q < Q; ++q) {
+                            const V x = gll[PAD * q + s];
+                            w[bitrev_c(q, LQ)] = q ? cmul_r<R>(x, tab[q * PAD + t]) : x;
+                        }
+                        dft_br<Q, R>(w);
+#pragma unroll
+                        for (int u = 0; u < Q; ++u) Yl[s_l * N + t + PAD * u] = w[u];
                     }
-                    dft_br<Q, R>(w);
-#pragma unroll
-                    for (int u = 0; u < Q; ++u) Yl[s_l * N + t + PAD * u] = w[u];
                 }
             } else {
-                {
+#pragma unroll
+                for (int h = 0; h < LPT; ++h) {
+                    lane(h);
                     const int task = i % TS;
                     const int s_l = task / PAD, s = S::CH * s_l + c;
                     V w[SIG];
@@ -923,148 +1054,80 @@ __global__ void __launch_bounds__((LineShape<N, PAD>::kThreads)) k_psf_line(PsfL
                         const V tw = k1 ? cmul_r<R>(tw0, TQ[q2 * SIG + k1]) : tw0;
                         Yl[(k1 * Q2 + q2) * TS + task] = cmul_r<R>(w[k1], tw);
                     }
+                    if (h + 1 < LPT) __builtin_amdgcn_sched_barrier(0);
                 }
                 __syncthreads();
                 {
-                    const int task = i % TS, kg = i / TS;
-                    const int s_l = task / PAD;
-                    V w[SIG / Q2][Q2];
+                    V w[LPT][SIG / Q2][Q2];
 #pragma unroll
-                    for (int e = 0; e < SIG / Q2; ++e) {
-                        const int k1 = kg + Q2 * e;
+                    for (int h = 0; h < LPT; ++h) {
+                        lane(h);
+                        const int task = i % TS, kg = i / TS;
 #pragma unroll
-                        for (int ii = 0; ii < Q2; ++ii) w[e][ii] = Yl[(k1 * Q2 + bitrev_c(ii, LQ2)) * TS + task];
+                        for (int e = 0; e < SIG / Q2; ++e) {
+                            const int k1 = kg + Q2 * e;
+#pragma unroll
+                            for (int ii = 0; ii < Q2; ++ii)
+                                w[h][e][ii] = Yl[(k1 * Q2 + bitrev_c(ii, LQ2)) * TS + task];
+                        }
                     }
                     __syncthreads();
 #pragma unroll
-                    for (int e = 0; e < SIG / Q2; ++e) {
-                        dft_br<Q2, R>(w[e]);
-                        const int k1 = kg + Q2 * e;
+                    for (int h = 0; h < LPT; ++h) {
+                        lane(h);
+                        const int task = i % TS, kg = i / TS;
+                        const int s_l = task / PAD;
 #pragma unroll
-                        for (int k2 = 0; k2 < Q2; ++k2) Yl[s_l * N + t + PAD * (k1 + SIG * k2)] = w[e][k2];
+                        for (int e = 0; e < SIG / Q2; ++e) {
+                            dft_br<Q2, R>(w[h][e]);
+                            const int k1 = kg + Q2 * e;
+#pragma unroll
+                            for (int k2 = 0; k2 < Q2; ++k2) Yl[s_l * N + t + PAD * (k1 + SIG * k2)] = w[h][e][k2];
+                        }
+                        if (h + 1 < LPT) __builtin_amdgcn_sched_barrier(0);
                     }
                 }
             }
             __syncthreads();
             // stage 2 of this chunk's s = CH s' + c: W_P^(s j) as powers of W_P^(CH j) (at most
             // SIG - 1 roundings), the SIG-point DFT over s'
-            V a[SIG];
-            {
-                V p = c ? w1 : Cx<R>::mk((R)1, (R)0);
 #pragma unroll
-                for (int s_l = 0; s_l < SIG; ++s_l) {
-                    const V y = Yl[s_l * N + i];
-                    a[bitrev_c(s_l, LS)] = (c == 0 && s_l == 0) ? y : cmul_r<R>(y, p);
-                    if (s_l + 1 < SIG) p = (c == 0 && s_l == 0) ? wch : cmul_r<R>(p, wch);
+            for (int h = 0; h < LPT; ++h) {
+                lane(h);
+                V a[SIG];
+                {
+                    V p = c ? w1[h] : Cx<R>::mk((R)1, (R)0);
+#pragma unroll
+                    for (int s_l = 0; s_l < SIG; ++s_l) {
+                        const V y = Yl[s_l * N + i];
+                        a[bitrev_c(s_l, LS)] = (c == 0 && s_l == 0) ? y : cmul_r<R>(y, p);
+                        if (s_l + 1 < SIG) p = (c == 0 && s_l == 0) ? wch[h] : cmul_r<R>(p, wch[h]);
+                    }
                 }
+                dft_br<SIG, R>(a);
+                if constexpr (S::CH == 1) {
+#pragma unroll
+                    for (int r = 0; r < SIG; ++r) v[h][r] = a[r];
+                } else {
+                    // PAD = 2 SIG: X[r] = A0[r] + W_PAD^r A1[r], X[r + SIG] = A0[r] - W_PAD^r A1[r]
+                    if (c == 0) {
+#pragma unroll
+                        for (int r = 0; r < SIG; ++r) v[h][r] = a[r];
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < SIG; ++r) {
+                            const int wi = r * (32 / PAD);
+                            const V tt = r ? cmul_r<R>(a[r], Cx<R>::mk((R)kW32re[wi], (R)kW32im[wi])) : a[r];
+                            const V x0 = v[h][r];
+                            v[h][r] = Cx<R>::mk(x0.x + tt.x, x0.y + tt.y);
+                            v[h][r + SIG] = Cx<R>::mk(x0.x - tt.x, x0.y - tt.y);
+                        }
+                    }
+                }
+                if (c + 1 == S::CH) emit(v[h]);
+                if (h + 1 < LPT) __builtin_amdgcn_sched_barrier(0);  // one lane after the other
             }
-            dft_br<SIG, R>(a);
             if (c + 1 < S::CH) __syncthreads();
-            if constexpr (S::CH == 1) {
-#pragma unroll
-                for (int r = 0; r < SIG; ++r) v[r] = a[r];
-            } else {
-                // PAD = 2 SIG: X[r] = A0[r] + W_PAD^r A1[r], X[r + SIG] = A0[r] - W_PAD^r A1[r]
-                if (c == 0) {
-#pragma unroll
-                    for (int r = 0; r < SIG; ++r) v[r] = a[r];
-                } else {
-#pragma unroll
-                    for (int r = 0; r < SIG; ++r) {
-                        const int wi = r * (32 / PAD);
-                        const V tt = r ? cmul_r<R>(a[r], Cx<R>::mk((R)kW32re[wi], (R)kW32im[wi])) : a[r];
-                        const V x0 = v[r];
-                        v[r] = Cx<R>::mk(x0.x + tt.x, x0.y + tt.y);
-                        v[r + SIG] = Cx<R>::mk(x0.x - tt.x, x0.y - tt.y);
-                    }
-                }
-            }
-        }
-        if constexpr (MODE == kLinePupil) {
-            if (L >= 0) {
-                double2* Gl = A.G + ((int64_t)b * g.nx2 + L) * g.py + i;
-#pragma unroll
-                for (int r = 0; r < PAD; ++r) Gl[(int64_t)N * r] = v[r];
-            }
-            if constexpr (BS > 1) {
-                if (sel1) {
-                    // |G| into the row sums, one line after the other (a fixed order); the sample
-                    // rows' values to LDS
-                    for (int ln = 0; ln < LINES; ++ln) {
-                        __syncthreads();
-                        if (line == ln && L >= 0) {
-#pragma unroll
-                            for (int r = 0; r < PAD; ++r) Bsum[i + N * r] += sqrt(fma(v[r].x, v[r].x, v[r].y * v[r].y));
-                        }
-                    }
-                    if (i == 0) Lc[line] = L;
-#pragma unroll
-                    for (int r = 0; r < PAD; ++r) {
-                        const int d = i + N * r - (N * PAD / 2 - 2);
-                        if (d >= 0 && d < 5) Gs[line][d] = L >= 0 ? v[r] : make_double2(0.0, 0.0);
-                    }
-                    __syncthreads();
-                    if (threadIdx.x < kSel) {  // sample (ko = py/2 - 2 + k / 5, lo = px/2 - 2 + k % 5)
-                        const int dk = threadIdx.x / 5, lo = g.px / 2 - 2 + threadIdx.x % 5;
-                        for (int ln = 0; ln < LINES; ++ln) {
-                            const int x = Lc[ln];
-                            if (x < 0) continue;
-                            double2 t = cmul(Gs[ln][dk], A.Wx[((int64_t)lo * x) % g.px]);
-                            if (x & 1) t = make_double2(-t.x, -t.y);
-                            sacc.x += t.x;
-                            sacc.y += t.y;
-                        }
-                    }
-                }
-            }
-        } else if constexpr (MODE == kLinePeak32) {
-            // this row's max (uint order of non-negative floats is numeric, NaN above +inf)
-            unsigned mr = 0u;
-#pragma unroll
-            for (int r = 0; r < PAD; ++r) {
-                const float U = fmaf(v[r].x, v[r].x, v[r].y * v[r].y);
-                mr = max(mr, __float_as_uint(U));
-            }
-            constexpr int W = N < 64 ? N : 64;
-#pragma unroll
-            for (int off = 1; off < W; off <<= 1) mr = max(mr, (unsigned)__shfl_xor((int)mr, off));
-            if (N > 64) {
-                if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = (double)__uint_as_float(mr);
-                __syncthreads();
-                if (i == 0)
-                    for (int w = 1; w < N / 64; ++w) mr = max(mr, __float_as_uint((float)wm[(threadIdx.x >> 6) + w]));
-            }
-            if (i == 0 && L >= 0) {
-                A.rowmax32[(int64_t)b * g.py + L] = __uint_as_float(mr);
-                m32 = max(m32, mr);
-            }
-        } else {
-          if (L >= 0) {
-            double* Pr = A.psf + ((int64_t)b * g.py + L) * g.px + i;
-            double2* Er = A.efield + ((int64_t)b * g.py + L) * g.px + i;
-#pragma unroll
-            for (int r = 0; r < PAD; ++r) {
-                const double U = fma(v[r].x, v[r].x, v[r].y * v[r].y);
-                if (MODE == kLinePeak) {
-                    m = fmax(m, U);
-                    nan_sum += U;  // NaN iff some U is NaN (U >= 0): numpy's max propagates it
-                } else {
-                    if (AKB_PSF_NT)
-                        __builtin_nontemporal_store(U * scale, Pr + N * r);
-                    else
-                        Pr[N * r] = U * scale;
-                    if (MODE == kLineWriteE) {
-                        const double re = v[r].x * dA, im = v[r].y * dA;
-                        const int lo = i + N * r;
-                        const double2 py_ph = A.Wy[((int64_t)L * (g.ny2 / 2)) % g.py];
-                        const double2 px_ph = A.Wx[((int64_t)lo * (g.nx2 / 2)) % g.px];
-                        double2 e = cmul(make_double2(re, im), make_double2(py_ph.x, -py_ph.y));
-                        e = cmul(e, make_double2(px_ph.x, -px_ph.y));
-                        Er[N * r] = make_double2(sgn * e.x / sq, sgn * e.y / sq);
-                    }
-                }
-            }
-          }
         }
         grp = next;
     }
@@ -1072,7 +1135,7 @@ __global__ void __launch_bounds__((LineShape<N, PAD>::kThreads)) k_psf_line(PsfL
         if (sel1) {
             __syncthreads();
             double* bp = A.bpart + ((int64_t)b * A.npart + blockIdx.x) * g.py;
-            for (int k = threadIdx.x; k < g.py; k += S::kThreads) bp[k] = Bsum[k];
+            for (int k = threadIdx.x; k < g.py; k += NT) bp[k] = Bsum[k];
             if (threadIdx.x < kSel) A.spart[((int64_t)b * A.npart + blockIdx.x) * 32 + threadIdx.x] = sacc;
         }
     }
@@ -1083,7 +1146,7 @@ __global__ void __launch_bounds__((LineShape<N, PAD>::kThreads)) k_psf_line(PsfL
         if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
         __syncthreads();
         if (threadIdx.x == 0) {
-            for (int w = 1; w < S::kThreads / 64; ++w) m = dmax_nan(m, wm[w]);
+            for (int w = 1; w < NT / 64; ++w) m = dmax_nan(m, wm[w]);
             atomic_max_nonneg(A.umax + b, m);
         }
     } else if (MODE == kLinePeak32) {
@@ -1206,12 +1269,12 @@ __global__ void __launch_bounds__(1024) k_psf_bound_rows2(PsfLineArgs A) {
 }
 
 // persistent workgroups per pass: the resident count (LDS / threads) x 256 CUs, a multiple of 8
-template <int N, int PAD, typename R>
+template <int N, int PAD, typename R, int NT = LineShape<N, PAD>::kThreads>
 static int line_wgs(int ngroups) {
     using S = LineShape<N, PAD>;
     const int lds = (int)(2 * sizeof(R)) * (S::LINES * S::SIG * N + S::LINES * N + S::kTab);
     int per_cu = (160 * 1024) / lds;
-    const int by_threads = 2048 / S::kThreads;
+    const int by_threads = 2048 / NT;
     if (per_cu > by_threads) per_cu = by_threads;
     if (per_cu < 1) per_cu = 1;
     int w = 256 * per_cu;
@@ -1224,7 +1287,8 @@ static int launch_psf_line(PsfLineArgs fa, int nlines, int batch, hipStream_t s)
     using S = LineShape<N, PAD>;
     using R = typename std::conditional<MODE == kLinePeak32, float, double>::type;
     fa.ngroups = (nlines + S::LINES - 1) / S::LINES;
-    k_psf_line<N, PAD, MODE><<<dim3(line_wgs<N, PAD, R>(fa.ngroups), batch), S::kThreads, 0, s>>>(fa);
+    using T = LineThreads<N, PAD, MODE>;
+    k_psf_line<N, PAD, MODE><<<dim3(line_wgs<N, PAD, R, T::kThreads>(fa.ngroups), batch), T::kThreads, 0, s>>>(fa);
     return launch_status(MODE == kLinePupil  ? "k_psf_line(pupil)"
                          : MODE == kLinePeak32 ? "k_psf_line(peak32)"
                          : MODE == kLinePeak   ? "k_psf_line(peak)"
@@ -1235,7 +1299,7 @@ static int launch_psf_line(PsfLineArgs fa, int nlines, int batch, hipStream_t s)
 template <int N, int PAD>
 static int pupil_pass_wgs(int nlines) {
     using S = LineShape<N, PAD>;
-    return line_wgs<N, PAD, double>((nlines + S::LINES - 1) / S::LINES);
+    return line_wgs<N, PAD, double, LineThreads<N, PAD, kLinePupil>::kThreads>((nlines + S::LINES - 1) / S::LINES);
 }
 
 // pad 16: lines of 16..1024; pad 8: 8..512 (Q = N / PAD <= 64)
