@@ -735,7 +735,8 @@ def test_psf_stack_equals_single(gpu):
                                                (512, 512, 8, False, True), (1024, 32, 8, True, False),
                                                (15, 16, 16, False, True), (16, 8, 8, True, True),
                                                (256, 64, 16, True, True), (64, 512, 16, False, False),
-                                               (1024, 16, 16, False, True), (127, 1024, 16, True, False)])
+                                               (1024, 16, 16, False, True), (127, 1024, 16, True, False),
+                                               (32, 1024, 16, False, True)])
 def test_psf_pruned_transform(gpu, ny, nx, pad, win, eff, monkeypatch):
     """Power-of-two pupils take the pruned transform (the padded plane is never built): against
     the oracle (numpy fft2 on the padded plane), the rocFFT path on the same input and, at pad 8
@@ -773,6 +774,31 @@ def test_psf_pruned_transform(gpu, ny, nx, pad, win, eff, monkeypatch):
     slow = G.psf_stack(o, None, [lam], dx, dy, pad_factor=pad, window="hann" if win else None,
                        workspace=G.PsfWorkspace())
     assert np.max(np.abs(slow[0][0].cpu().numpy() - got)) <= 1e-12
+
+
+def test_psf_line_1024_stack_equals_single(gpu, monkeypatch):
+    """1024-point lines (two output columns a thread, 512-thread workgroups) batched over three
+    wavelengths, with the E-field: each entry the single-wavelength run's bits, on every peak route."""
+    from akbraytracing_amd import psf as G
+    rng = np.random.default_rng(1024)
+    opd = rng.standard_normal((32, 1024)) * 3e-9
+    opd[rng.random((32, 1024)) < 0.03] = np.nan
+    o = torch.from_numpy(opd).to(gpu)
+    lams = [13.5e-9, 1.35e-9, 6.7e-9]
+    base = None
+    for mode in ("select", "bound", "f64", "f32"):
+        monkeypatch.setenv("AKB_PSF_PEAK", mode)
+        st, ef, imax = G.psf_stack(o, None, lams, 5e-6, 4e-6, pad_factor=16, return_efield=True,
+                                   workspace=G.PsfWorkspace())
+        if base is None:
+            base = st
+            for b, lam in enumerate(lams):
+                one, e1, im1 = G.psf_stack(o, None, [lam], 5e-6, 4e-6, pad_factor=16, return_efield=True,
+                                           workspace=G.PsfWorkspace())
+                assert torch.equal(st[b], one[0]) and torch.equal(ef[b], e1[0])
+                assert float(imax[b]) == float(im1[0])
+        else:
+            assert torch.equal(st, base), mode
 
 
 @pytest.mark.parametrize("n", [128, 512])
