@@ -45,6 +45,7 @@ import glob
 import json
 import math
 import os
+import re
 import sys
 import time
 
@@ -172,18 +173,35 @@ def cpu_baseline(seconds, g):
             "sample_1thread": f"same pipeline, 1 thread, {n1}x{n1} grid, {reps1} reps in {el1:.1f} s"}
 
 
-def read_profile():
-    """(summary, file, matches): the newest profiles/*_roofline.json (scripts/summarize_profiles.py)
-    and whether it describes these kernel sources (its sha256 of them equals theirs now)."""
-    sys.path.insert(0, os.path.join(ROOT, "scripts"))
-    from summarize_profiles import sources_sha256
-    files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "*_roofline.json"))
-                   if not f.endswith("_faithful_roofline.json"))
+def _tag_key(path):
+    """Order of profile tags: rNN then the run letters a .. z, aa .. zz (so r05y < r05aa)."""
+    m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(path))
+    return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
+
+
+def _pick_profile(files, sha):
+    """(summary, file, matches) of the newest of files whose sources_sha256 is sha, else of the
+    newest one."""
+    files = sorted(files, key=_tag_key, reverse=True)
     if not files:
         return {}, None, False
-    with open(files[-1]) as f:
-        d = json.load(f)
-    return d, os.path.relpath(files[-1], ROOT), d.get("sources_sha256") == sources_sha256()
+    docs = []
+    for f in files:
+        with open(f) as fh:
+            docs.append(json.load(fh))
+        if docs[-1].get("sources_sha256") == sha:
+            return docs[-1], os.path.relpath(f, ROOT), True
+    return docs[0], os.path.relpath(files[0], ROOT), False
+
+
+def read_profile():
+    """(summary, file, matches): the newest profiles/*_roofline.json (scripts/summarize_profiles.py)
+    that describes these kernel sources (its sha256 of them equals theirs now), else the newest."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    from summarize_profiles import sources_sha256
+    files = [f for f in glob.glob(os.path.join(ROOT, "profiles", "*_roofline.json"))
+             if not f.endswith("_faithful_roofline.json")]
+    return _pick_profile(files, sources_sha256())
 
 
 def system_variants(geom, k):
@@ -271,10 +289,9 @@ def huygens_rate(out):
     # instruction mix of the committed PMC summary (scripts/summarize_huygens.py) while it describes
     # this kernel source
     import hashlib
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_huygens.json")))
     src = os.path.join(ROOT, "akbraytracing_amd", "csrc", "akb_huygens.hip")
-    prof = json.load(open(files[-1])) if files else {}
-    ok = prof.get("sources_sha256") == hashlib.sha256(open(src, "rb").read()).hexdigest()
+    prof, pfile, ok = _pick_profile(glob.glob(os.path.join(ROOT, "profiles", "*_huygens.json")),
+                                    hashlib.sha256(open(src, "rb").read()).hexdigest())
     if ok:
         lane_ops = prof["valu_lane_ops_per_pair"]
         peak = SIMDS / 4 * prof["effective_clock_ghz"] * 1e9 * 64 / lane_ops
@@ -285,21 +302,18 @@ def huygens_rate(out):
                            "fp64_frac_of_peak_profiled": prof["fp64_frac_of_peak"],
                            "issue_frac_profiled": prof["issue_frac"],
                            "effective_clock_ghz": prof["effective_clock_ghz"]}
-    res["profile"] = {"file": os.path.relpath(files[-1], ROOT) if files else None, "matches_sources": ok}
+    res["profile"] = {"file": pfile, "matches_sources": ok}
     return res
 
 
 def read_faithful_profile():
     """(summary, file, matches): the newest profiles/*_faithful_roofline.json (scripts/
-    summarize_profiles.py: PMC of the cone solve's kernels) and whether it describes these sources."""
+    summarize_profiles.py: PMC of the cone solve's kernels) that describes these sources, else the
+    newest."""
     sys.path.insert(0, os.path.join(ROOT, "scripts"))
     from summarize_profiles import GD_SOURCES, sources_sha256
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_faithful_roofline.json")))
-    if not files:
-        return {}, None, False
-    with open(files[-1]) as f:
-        d = json.load(f)
-    return d, os.path.relpath(files[-1], ROOT), d.get("sources_sha256") == sources_sha256(sources=GD_SOURCES)
+    return _pick_profile(glob.glob(os.path.join(ROOT, "profiles", "*_faithful_roofline.json")),
+                         sources_sha256(sources=GD_SOURCES))
 
 
 def faithful_roofline(ms, cells, K, S):
