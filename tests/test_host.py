@@ -326,3 +326,24 @@ def test_pockets_refuse_a_cut_corner():
     X[0, 0], Y[0, 0] = -0.5, -0.5   # the corner pulled inside the hull
     with pytest.raises(_lib.AKBError):
         _pockets(X, Y)
+
+
+def test_bench_picks_the_newest_profile_that_matches_the_sources(tmp_path, monkeypatch):
+    """bench.py's profile lookup: tags order r05y < r05aa < r05an < r06a, and the newest file whose
+    sources hash matches wins over a newer stale one (else the newest, flagged as not matching)."""
+    import json
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    files = []
+    for tag, sha in (("r04n", "a"), ("r05y", "b"), ("r05aa", "a"), ("r05an", "a"), ("r06a", "c")):
+        f = tmp_path / f"{tag}_roofline.json"
+        f.write_text(json.dumps({"tag": tag, "sources_sha256": sha}))
+        files.append(str(f))
+    assert sorted(reversed(files), key=bench._tag_key) == files
+    d, name, ok = bench._pick_profile(files, "a")
+    assert (d["tag"], name, ok) == ("r05an", "r05an_roofline.json", True)
+    d, name, ok = bench._pick_profile(files, "zzz")
+    assert (d["tag"], ok) == ("r06a", False)
+    assert bench._pick_profile([], "a") == ({}, None, False)
