@@ -4,6 +4,7 @@ The library is loaded lazily on first use. torch is imported first so the proces
 HIP runtime (libamdhip64.so.7 is matched by SONAME), which keeps the device pointers and stream
 handles that torch hands us valid inside the library.
 """
+import atexit
 import ctypes
 import os
 
@@ -19,7 +20,7 @@ c_int = ctypes.c_int
 c_dbl = ctypes.c_double
 c_vp = ctypes.c_void_p
 MAX_MIRRORS = 7
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 FLAG_MISS = 0x1
 FLAG_ZERO_NORMAL = 0x2
@@ -40,11 +41,11 @@ EXPORTS = [
     "akb_leaf_sink_bytes", "akb_leaf_sink_layout", "akb_leaf_finish_work_bytes", "akb_leaf_finish_f64",
     "akb_leaf_parts_f64", "akb_parts_chain_f64",
     "akb_huygens_splits", "akb_huygens_work_bytes", "akb_huygens_f64", "akb_scale_field_f64",
-    "akb_psf_work_bytes", "akb_psf_f64", "akb_psf_release_plans", "akb_selftest_arith_f64",
+    "akb_psf_work_bytes", "akb_psf_f64", "akb_psf_release_plans", "akb_release_all", "akb_selftest_arith_f64",
     "akb_first_valid_rows_f64", "akb_rotate_work_bytes", "akb_rotate_with_nan_f64", "akb_pupil_post_f64", "akb_pupil_post_work_bytes",
     "akb_moments_work_bytes", "akb_map_moments_f64", "akb_plane_subtract_f64", "akb_legendre_rows_f64",
     "akb_gd_cells_f64", "akb_gd_pockets", "akb_gd_check_pockets", "akb_gd_grad_sweeps_f64",
-    "akb_gd_eval_f64", "akb_gd_cone_work_bytes", "akb_gd_patch_timing", "akb_gd_patch_times", "akb_gd_patch_phases", "akb_gd_cone_eval_f64", "akb_gd_axes_f64",
+    "akb_gd_eval_f64", "akb_gd_cone_work_bytes", "akb_gd_patch_timing", "akb_gd_patch_times", "akb_gd_band_times", "akb_gd_patch_phases", "akb_gd_cone_eval_f64", "akb_gd_axes_f64",
     "akb_gd_cells_claims_f64", "akb_gd_claim_pockets_f64", "akb_gd_cone_solve_f64",
     "akb_gd_claims_f64", "akb_gd_cone_part_f64", "akb_gd_part_finish_f64", "akb_gd_ring_f64", "akb_gd_cells_window_f64",
     "akb_trace_chain_batch_f64", "akb_focus_eval_work_bytes", "akb_focus_eval_f64", "akb_sep_search_f64",
@@ -154,6 +155,7 @@ def _declare(L):
         "akb_psf_f64": ([c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_dbl, c_dbl, c_vp, c_vp, c_dbl, c_vp,
                          c_vp, c_vp, c_vp, c_vp, c_vp], c_int),
         "akb_psf_release_plans": ([], None),
+        "akb_release_all": ([], None),
         "akb_selftest_arith_f64": ([c_vp, c_vp, c_i64, c_vp, c_vp], c_int),
         "akb_first_valid_rows_f64": ([c_vp, c_int, c_int, c_vp, c_vp], c_int),
         "akb_rotate_work_bytes": ([c_int, c_int], c_i64),
@@ -182,6 +184,7 @@ def _declare(L):
         "akb_gd_cone_work_bytes": ([c_int, c_int, c_int, c_int, c_int], c_i64),
         "akb_gd_patch_timing": ([c_int], c_int),
         "akb_gd_patch_times": ([c_vp, c_vp, c_int], c_int),
+        "akb_gd_band_times": ([c_vp, c_int], c_int),
         "akb_gd_patch_phases": ([c_vp], c_int),
         "akb_gd_axes_f64": ([c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp], c_int),
         "akb_gd_claims_f64": ([c_vp, c_vp, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp,
@@ -232,7 +235,18 @@ def lib():
         if L.akb_chain_desc_size() != ctypes.sizeof(ChainDesc):
             raise AKBError("akb_chain_desc layout mismatch between include/akb_raytrace.h and _lib.py")
         _LIB = L
+        # the library's cached plans, device tables, pinned buffers and events are freed while the
+        # HIP runtime is still up: Python's exit hooks run before the C runtime's static destructors
+        # (left to those, rocFFT's teardown can run after HIP's)
+        atexit.register(_release_all, L)
     return _LIB
+
+
+def _release_all(L):
+    try:
+        L.akb_release_all()
+    except Exception:  # exit path: never mask the process's own status
+        pass
 
 
 def sources_hash():

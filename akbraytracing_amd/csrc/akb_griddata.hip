@@ -1199,7 +1199,7 @@ constexpr int kConeBox = 2 * kConeMaxK + 4;  // the largest box side: it fits th
 // the boundary band: vertices with min(iv, ih, nv - 1 - iv, nh - 1 - ih) <= D, as four regions -
 // the top rows [0, rt), the bottom rows [rb, nv), and between them the left columns [0, cl) and the
 // right columns [cr, nh) - cut into kBandTR x kBandTC tiles (every band vertex in one tile)
-constexpr int kBandTR = 32, kBandTC = 32;  // (the depth <= 26 band: one tile deep)
+constexpr int kBandTR = 16, kBandTC = 32;  // (33 KB of LDS a tile: four workgroups a CU, 128 VGPRs a wave)
 struct BandTiles {
     int D, rt, rb, cl, cr;
     int ncb, top_rb, bot_rb, mid_rb, lcb, rcb;  // column blocks (top / bottom), row blocks, side column blocks
@@ -1408,16 +1408,16 @@ __global__ void k_gd_chord_slots(Grid g, int32_t* slots, int64_t L) {
     }
 }
 
-// one sweep of the band in one launch, one round of workgroups at two a CU: workgroup b takes ring
-// vertices [32 b, 32 b + 32) on its first four waves (8-lane groups: a vertex's chords over the
-// group, its lattice edges on the lead lane; a vertex of more than 32 chords takes its whole wave
-// afterwards) and, for b < the tile count, band tile b on its last four - the tile's vertices and
-// their neighbours' x, y, f and x_{j-1} (and the cells' diagonals), and x_{j-2} of its vertices,
-// staged in LDS by all eight waves with coalesced row loads, then four vertices a thread off the
-// ring (band_edges from LDS: the gather kernel's arithmetic). The ring's dependent loads and the
-// tile's arithmetic overlap inside the workgroup. Both halves read x_{j-1} / x_{j-2} only.
-constexpr int kBandThreads = 512, kBandRingWaves = 4, kBandRingPer = 8 * kBandRingWaves;
-constexpr int kBandTileThreads = kBandThreads - 64 * kBandRingWaves, kBandVR = kBandTR * kBandTC / kBandTileThreads;
+// one sweep of the band in one launch, one round of 256-thread workgroups (a wave per SIMD, so a
+// workgroup fits beside a pass-2 workgroup's four waves a SIMD instead of waiting for a CU to drain):
+// the first ceil(L / 32) take ring vertices [32 b, 32 b + 32) (8-lane groups: a vertex's chords over
+// the group, its lattice edges on the lead lane; a vertex of more than 32 chords takes its whole wave
+// afterwards), the others band tile b - ceil(L / 32) - the tile's vertices and their neighbours' x,
+// y, f and x_{j-1} (and the cells' diagonals), and x_{j-2} of its vertices, staged in LDS with
+// coalesced row loads, then four vertices a thread off the ring (band_edges from LDS: the gather
+// kernel's arithmetic). Both read x_{j-1} / x_{j-2} only.
+constexpr int kBandThreads = 256, kBandRingWaves = kBandThreads / 64, kBandRingPer = 8 * kBandRingWaves;
+constexpr int kBandTileThreads = kBandThreads, kBandVR = kBandTR * kBandTC / kBandTileThreads;
 // a workgroup's wall-clock time into the diagnostics words (ring only: k = 0, with a tile: k = 1)
 __device__ __forceinline__ void band_clock(unsigned long long* clk, int k, unsigned long long t0) {
     __syncthreads();
@@ -1428,11 +1428,9 @@ __device__ __forceinline__ void band_clock(unsigned long long* clk, int k, unsig
         atomicMax(&clk[4 + k], d);
     }
 }
-// the band launch's workgroups: every tile, and enough for the ring at kBandRingPer a workgroup
-inline unsigned band_grid(const BandTiles& bt, int64_t L) {
-    const int64_t nr = (L + kBandRingPer - 1) / kBandRingPer;
-    return (unsigned)(bt.total > nr ? bt.total : nr);
-}
+// the band launch's ring workgroups (the tiles' follow them)
+inline unsigned band_ring_wgs(int64_t L) { return (unsigned)((L + kBandRingPer - 1) / kBandRingPer); }
+inline unsigned band_grid(const BandTiles& bt, int64_t L) { return band_ring_wgs(L) + (unsigned)bt.total; }
 
 __global__ void __launch_bounds__(kBandThreads) __attribute__((amdgpu_waves_per_eu(4))) k_gd_cone_band(Grid g, BandTiles bt, ConeBand a) {
     if (!*a.needed) return;
@@ -1441,10 +1439,37 @@ __global__ void __launch_bounds__(kBandThreads) __attribute__((amdgpu_waves_per_
     __shared__ double sx[HN], sy[HN], sf[HN], sgx[HN], sgy[HN];
     __shared__ double spx[kBandTR * kBandTC], spy[kBandTR * kBandTC];  // x_{j-2} of the tile's vertices
     __shared__ uint8_t sdg[(kBandTR + 1) * CC];
-    const bool has_tile = (int)blockIdx.x < bt.total;  // (workgroup-uniform)
+    const int64_t L = 2 * (int64_t)(g.nh - 1) + 2 * (int64_t)(g.nv - 1);
+    const int nr = (int)((L + kBandRingPer - 1) / kBandRingPer);
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if ((int)blockIdx.x < nr) {  // (workgroup-uniform) ring vertices
+        const int sub = lane & 7;
+        const int64_t q0 = (int64_t)blockIdx.x * kBandRingPer + 8 * w;
+        const int64_t r = q0 + (lane >> 3);
+        int32_t js[4] = {-1, -1, -1, -1};
+        bool big;
+        if (a.slots) {  // the slots say whether the vertex is big: no xptr level ahead of the vertex's loads
+            if (r < L) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) js[k] = a.slots[r * kChordSlots + sub + 8 * k];
+            }
+            big = js[0] == kSlotBig;
+        } else {
+            big = r < L && g.xptr[r + 1] - g.xptr[r] > 8;
+        }
+        if (r < L && !big) cone_ring_vertex<8>(g, a, r, sub, js);
+        unsigned long long m = __ballot(big && sub == 0);
+        while (m) {  // wave-uniform
+            const int q = __builtin_ctzll(m);
+            m &= m - 1;
+            cone_ring_vertex<64>(g, a, q0 + (q >> 3), lane);
+        }
+        if (a.clk) band_clock(a.clk + 4, 0, t0);
+        return;
+    }
     int r0 = 0, c0 = 0, r1 = 0, c1 = 0;
-    if (has_tile) {
-        band_tile(bt, g.nv, g.nh, blockIdx.x, r0, c0, r1, c1);
+    band_tile(bt, g.nv, g.nh, (int)blockIdx.x - nr, r0, c0, r1, c1);
+    {
         // the tile's vertices with a one-vertex halo (rows r0 - 1 .. r0 + TR, inside the lattice), the
         // diagonals of cells (r0 - 1 .. r0 + TR - 1) x (c0 - 1 .. c0 + TC - 1) and x_{j-2} of the tile's
         // vertices: every load of a thread issued before the first LDS store (one memory latency)
@@ -1508,67 +1533,40 @@ __global__ void __launch_bounds__(kBandThreads) __attribute__((amdgpu_waves_per_
         }
         __syncthreads();
     }
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (w < kBandRingWaves) {
-        const int64_t L = 2 * (int64_t)(g.nh - 1) + 2 * (int64_t)(g.nv - 1);
-        const int sub = lane & 7;
-        for (int64_t q0 = (int64_t)blockIdx.x * kBandRingPer + 8 * w; q0 < L; q0 += (int64_t)gridDim.x * kBandRingPer) {
-            const int64_t r = q0 + (lane >> 3);
-            int32_t js[4] = {-1, -1, -1, -1};
-            bool big;
-            if (a.slots) {  // the slots say whether the vertex is big: no xptr level ahead of the vertex's loads
-                if (r < L) {
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) js[k] = a.slots[r * kChordSlots + sub + 8 * k];
-                }
-                big = js[0] == kSlotBig;
-            } else {
-                big = r < L && g.xptr[r + 1] - g.xptr[r] > 8;
-            }
-            if (r < L && !big) cone_ring_vertex<8>(g, a, r, sub, js);
-            unsigned long long m = __ballot(big && sub == 0);
-            while (m) {  // wave-uniform
-                const int q = __builtin_ctzll(m);
-                m &= m - 1;
-                cone_ring_vertex<64>(g, a, q0 + (q >> 3), lane);
-            }
-        }
-    } else if (has_tile) {
-        const int tt = threadIdx.x - 64 * kBandRingWaves;
-        const int tr0 = tt / kBandTC, tc = tt - (tt / kBandTC) * kBandTC;
+    const int tt = threadIdx.x;
+    const int tr0 = tt / kBandTC, tc = tt - (tt / kBandTC) * kBandTC;
 #pragma unroll 1
-        for (int u = 0; u < kBandVR; ++u) {
-            const int tr = tr0 + u * (kBandTR / kBandVR);
-            const int iv = r0 + tr, ih = c0 + tc;
-            if (iv >= r1 || ih >= c1 || ring_pos(g, iv, ih) >= 0) continue;
-            const bool L = ih > 0, R = ih < g.nh - 1, D = iv > 0, U = iv < g.nv - 1;
-            const int li = (tr + 1) * HC + (tc + 1);
-            const int jn[8] = {li - 1, li + 1, li - HC, li + HC, li - HC - 1, li - HC + 1, li + HC - 1, li + HC + 1};
-            const bool inb[8] = {L, R, D, U, D && L, D && R, U && L, U && R};
-            const int lc = tr * CC + tc;  // cell (iv - 1, ih - 1)
-            const int dc[4] = {lc, lc + 1, lc + CC, lc + CC + 1};
-            uint8_t dg[4];
+    for (int u = 0; u < kBandVR; ++u) {
+        const int tr = tr0 + u * (kBandTR / kBandVR);
+        const int iv = r0 + tr, ih = c0 + tc;
+        if (iv >= r1 || ih >= c1 || ring_pos(g, iv, ih) >= 0) continue;
+        const bool L_ = ih > 0, R = ih < g.nh - 1, D = iv > 0, U = iv < g.nv - 1;
+        const int li = (tr + 1) * HC + (tc + 1);
+        const int jn[8] = {li - 1, li + 1, li - HC, li + HC, li - HC - 1, li - HC + 1, li + HC - 1, li + HC + 1};
+        const bool inb[8] = {L_, R, D, U, D && L_, D && R, U && L_, U && R};
+        const int lc = tr * CC + tc;  // cell (iv - 1, ih - 1)
+        const int dc[4] = {lc, lc + 1, lc + CC, lc + CC + 1};
+        uint8_t dg[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) dg[k] = inb[4 + k] ? sdg[dc[k]] : 0;
-            double xs[8], ys[8], fs[8], gxs[8], gys[8];
+        for (int k = 0; k < 4; ++k) dg[k] = inb[4 + k] ? sdg[dc[k]] : 0;
+        double xs[8], ys[8], fs[8], gxs[8], gys[8];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const int j = inb[k] ? jn[k] : li;
-                xs[k] = sx[j];
-                ys[k] = sy[j];
-                fs[k] = sf[j];
-                gxs[k] = sgx[j];
-                gys[k] = sgy[j];
-            }
-            const bool on[8] = {L, R, D, U, inb[4] && dg[0] == 0, inb[5] && dg[1] == 1, inb[6] && dg[2] == 1,
-                                inb[7] && dg[3] == 0};
-            GradAcc<1> A;
-            band_edges(A, sx[li], sy[li], sf[li], xs, ys, fs, gxs, gys, on);
-            const int pk = tr * kBandTC + tc;
-            band_solve(a, (int64_t)iv * g.nh + ih, A, spx[pk], spy[pk]);
+        for (int k = 0; k < 8; ++k) {
+            const int j = inb[k] ? jn[k] : li;
+            xs[k] = sx[j];
+            ys[k] = sy[j];
+            fs[k] = sf[j];
+            gxs[k] = sgx[j];
+            gys[k] = sgy[j];
         }
+        const bool on[8] = {L_, R, D, U, inb[4] && dg[0] == 0, inb[5] && dg[1] == 1, inb[6] && dg[2] == 1,
+                            inb[7] && dg[3] == 0};
+        GradAcc<1> A;
+        band_edges(A, sx[li], sy[li], sf[li], xs, ys, fs, gxs, gys, on);
+        const int pk = tr * kBandTC + tc;
+        band_solve(a, (int64_t)iv * g.nh + ih, A, spx[pk], spy[pk]);
     }
-    if (a.clk) band_clock(a.clk + 4, has_tile ? 1 : 0, t0);
+    if (a.clk) band_clock(a.clk + 4, 1, t0);
 }
 
 struct ConePatch {
@@ -1606,50 +1604,98 @@ __device__ __forceinline__ void depth_order(int W, int idx, int& r, int& c, int&
     }
 }
 
-// The interior target cells' patches: one persistent 1024-thread workgroup per CU walks its cells
-// as a two-stage pipeline. A thread holds one box vertex (the box has pitch 33 in LDS, conflict-free
-// along a column): threads [0, N1) the (W-2)^2 vertices of depth >= 1 of cell p, running its sweeps
-// 1 .. S, threads [N1a, N1a + N2) (N1a: N1 rounded up to a whole wave) the N2 = (W - 2S - 2)^2
-// vertices of depth >= S + 1 of cell p - 1,
-// running its sweeps S + 1 .. K and its corners' output, so the late sweeps (a few waves each) no
-// longer run alone. Vertices are taken in order of depth, so a sweep's shrinking square is a prefix
-// of a stage's threads and fills whole waves. Each thread forms its vertex's constants once per
-// cell - the eight edge slots' M (zero for an absent diagonal) and c, P - so a sweep costs eight
-// LDS reads and 4 FMAs per slot plus the 2 x 2 product and the Chebyshev step. Box sets of x, y, f
-// rotate over three (stage 1, stage 2, the next cell's, loaded through registers during the sweeps
-// and written after them) and iterate pairs over two (stage 2 reads x_S, x_{S-1} where stage 1 left
-// them). The host picks S (the smallest >= K/2 with N1a + N2 <= 1020: threads 1020..1023 store the
-// corners).
+// The interior target cells' patches: one persistent workgroup per CU walks its cells as a
+// two-stage pipeline. A thread holds one box vertex (the box has pitch 33 in LDS) and that
+// vertex's constants - the eight edge slots' M (zero for an absent diagonal) and c, P - in
+// registers, so a sweep costs eight LDS reads and 4 FMAs per slot plus the 2 x 2 product and the
+// Chebyshev step. Three thread sets, in order of depth from the centre outwards within each:
+//   * inner A = threads [0, N2), inner B = [N2, 2 N2): the N2 = (W - 2S - 2)^2 vertices of depth
+//     >= S + 1, the ones the late sweeps S + 1 .. K still update;
+//   * outer = [2 N2, N1 + N2): the vertices of depth 1 .. S (N1 = (W - 2)^2 of depth >= 1 in all).
+// Step p sets cell p up on the outer threads and on inner set p & 1, which run its sweeps 1 .. S;
+// the other inner set, whose registers still hold cell p - 1's constants from the step before,
+// runs that cell's sweeps S + 1 .. K and its corners' output beside them. So every vertex's
+// constants are formed once per cell, and the late sweeps (a few waves each) never run alone.
+// A sweep's shrinking square is a prefix of each set's threads. Sweep 1 reads nothing: x_0 = 0
+// makes S = +0, the same bits as summing the zero iterate. A box whose cells all take the same
+// diagonal (about two in three at C3) runs the sweeps over its six present slots (an absent
+// slot adds exact zeros, so the bits are the eight-slot sum's); a wave reads that from the
+// boxes' orientation words. Box sets of x, y, f rotate over two (cell p's, read by its setup;
+// cell p + 1's, loaded through registers during the sweeps and written after them: the old set
+// keeps the little geometry its corners need in registers), iterate pairs over two (cell p - 1's
+// x_S, x_{S-1} stay where its sweeps left them). The host picks S (the smallest >= K/2 with
+// N1 + N2 + 4 threads in a workgroup: threads N1 + N2 .. + 3 store the corners).
 //
 // At the corners (x_K) the kernel also forms the change one more plain sweep would make - scipy's
 // measure (chg) - and a value-error estimate: with the Jacobi spectrum in [-1/2, 1/2] the distance
 // of x_K from the fixed point is at most ~2x the step |y - x_K|, and a Clough-Tocher value moves
 // by at most |dg| x the longest edge it integrates over, so est = 2 sqrt2 max|y - x_K| x the cell's
 // longest side or diagonal (in the map's units; FaithfulPupil checks it against the map's range).
+// A NaN step makes the estimate NaN, which the max keeps (fmax would drop it) and the guard
+// refuses.
+__device__ __forceinline__ double nan_max(double a, double b) { return (a != a || b != b) ? (a + b) : fmax(a, b); }
+
 __device__ __forceinline__ double cell_est(const double (&so)[4][6]) {
-    const double d = fmax(fmax(so[0][4], so[1][4]), fmax(so[2][4], so[3][4]));
+    const double d = nan_max(nan_max(so[0][4], so[1][4]), nan_max(so[2][4], so[3][4]));
     const double h = fmax(fmax(so[0][5], so[1][5]), fmax(so[2][5], so[3][5]));
     return 2.0 * 1.4142135623730951 * d * h;
 }
 
+// the patch workgroup's size for K and S (every vertex thread, the four corner-store threads, and
+// the 32-wide box-load rows)
+__host__ __device__ constexpr int patch_threads(int K, int S) {
+    return ((((2 * K + 2) * (2 * K + 2) + (2 * K + 2 - 2 * S) * (2 * K + 2 - 2 * S) + 4) >
+                     32 * (2 * K + 4)
+                 ? ((2 * K + 2) * (2 * K + 2) + (2 * K + 2 - 2 * S) * (2 * K + 2 - 2 * S) + 4)
+                 : 32 * (2 * K + 4)) +
+            63) &
+           ~63;
+}
+
+// S of one sweep: the slots of kMask (bit k: slot k) summed from the iterate at gi (the vertex's
+// buffer entry, minus P + 1 so that every slot's offset is a positive immediate), in the fixed
+// order - the axis chain s, the diagonal chain d - then s + d
+template <int kMask, int P>
+__device__ __forceinline__ void patch_sums(const double2* __restrict__ buf, int i0, const double (&mxx)[8],
+                                           const double (&mxy)[8], const double (&myy)[8], double& s0, double& s1) {
+    constexpr int off[8] = {P, P + 2, 1, 2 * P + 1, 0, 2, 2 * P, 2 * P + 2};
+    asm volatile("" : "+v"(i0));  // i0 = b - P - 1 as computed: the slots' offsets stay immediates
+    double2 gj[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        if (kMask & (1 << k)) gj[k] = buf[i0 + off[k]];
+    double a0 = 0.0, a1 = 0.0, d0 = 0.0, d1 = 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        if (!(kMask & (1 << k))) continue;
+        double& t0 = k < 4 ? a0 : d0;
+        double& t1 = k < 4 ? a1 : d1;
+        t0 = __builtin_fma(mxy[k], gj[k].y, __builtin_fma(mxx[k], gj[k].x, t0));
+        t1 = __builtin_fma(myy[k], gj[k].y, __builtin_fma(mxy[k], gj[k].x, t1));
+    }
+    s0 = a0 + d0;
+    s1 = a1 + d1;
+}
+constexpr int kSlotsAll = 0xff, kSlotsDiag0 = 0x9f, kSlotsDiag1 = 0x6f;  // diagonal 0: slots 4, 7; 1: 5, 6
+
 __global__ void __launch_bounds__(1024) k_gd_cone_patch(Grid g, ConePatch a, int S) {
     constexpr int P = 33;
     static_assert(kConeBox < P, "box pitch");
-    __shared__ double sxyf[3][3][P * 32];
+    __shared__ double sxyf[2][3][P * 32];
     __shared__ double2 sg[2][2][P * 32];
-    __shared__ uint8_t sd[3][P * 32];
-    __shared__ int2 scell[1024];            // this workgroup's cells' box origins (R0, C0), read once
-    __shared__ double sout[4][6];           // stage 2's corner results, stored one step later
+    __shared__ uint8_t sd[2][P * 32];
+    __shared__ int2 scell[1024];   // this workgroup's cells' box origins (R0, C0), read once
+    __shared__ double sout[4][6];  // the old set's corner results, stored one step later
+    __shared__ unsigned sori[2];   // per box set: bit 0 some cell takes diagonal 0, bit 1 some diagonal 1
+    __shared__ double somg[kConeMaxK + 1];  // sweep j's Chebyshev weight
+    __shared__ double shc[2][4];   // per iterate pair: the corners' longest cell side or diagonal
     const int K = a.K, W = 2 * K + 4;
     const int t = threadIdx.x;
-    // stage 2 starts at a wave boundary, so a wave's stage - and with it the sweep it runs - is
-    // uniform: the sweep's weight is a scalar load
-    const int N1 = (W - 2) * (W - 2), N1a = (N1 + 63) & ~63, N2 = (W - 2 * S - 2) * (W - 2 * S - 2);
-    const int role = __builtin_amdgcn_readfirstlane(t < N1a ? 1 : 2);
-    int r, c, dep;
-    depth_order(W, role == 1 ? t : t - N1a, r, c, dep);
-    if ((role == 1 && t >= N1) || (role == 2 && t - N1a >= N2)) dep = 0;
-    const int b = dep >= 1 ? r * P + c : 0;
+    const int N1 = (W - 2) * (W - 2), N2 = (W - 2 * S - 2) * (W - 2 * S - 2), T0 = N1 + N2;
+    const int role = t < N2 ? 0 : t < 2 * N2 ? 1 : t < T0 ? 2 : 3;  // inner A, inner B, outer, corner / idle
+    int r = -1, c = -1, dep = 0;
+    if (role < 3) depth_order(W, role == 0 ? t : t - N2, r, c, dep);
+    const int b = dep >= 1 ? r * P + c : P + 1;  // (idle threads: a harmless in-range base)
     const int Q = max(S, K - S);
     const int count = *a.count;
     const int my = count > (int)blockIdx.x ? (count - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
@@ -1660,71 +1706,104 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch(Grid g, ConePatch a, int
     const int nh = g.nh;
     // the cell list into LDS first (the host keeps it <= 1024 cells per workgroup), so no wait on a
     // global load sits between a step's barrier and its setup
-    for (int i = t; i < my; i += 1024) {
+    for (int i = t; i < my; i += blockDim.x) {
         const int64_t cell = a.cells[blockIdx.x + (int64_t)i * gridDim.x];
         const int iv0 = (int)(cell / (nh - 1)), ih0 = (int)(cell - (int64_t)iv0 * (nh - 1));
         scell[i] = make_int2(iv0 - (K + 1), ih0 - (K + 1));
     }
+    if (t < 2) sori[t] = 0u;
+    if (t <= kConeMaxK) somg[t] = a.st[t].omega;
     __syncthreads();
-    const int lr = t / 32, lc = t - (t / 32) * 32;
+    // the box loaders' row and column: re-formed where used (from an opaque copy of t), so that their
+    // addresses are not held in registers across the sweeps
+    auto lrc = [&](int& lr, int& lc) {
+        int tt = t;
+        asm volatile("" : "+v"(tt));
+        lr = tt >> 5;
+        lc = tt & 31;
+    };
+    int lr, lc;
+    lrc(lr, lc);
+    const bool loader = lr < W && lc < W, cell_loader = lr < W - 1 && lc < W - 1;
     // cell 0's box through registers (every later box loads during the step before it)
     uint8_t pd = 0;
-    if (my > 0 && lr < W && lc < W) {
+    if (my > 0 && loader) {
         const int2 o = scell[0];
         const int64_t q = (int64_t)(o.x + lr) * nh + (o.y + lc);
         sxyf[0][0][lr * P + lc] = gx_[q];
         sxyf[0][1][lr * P + lc] = gy_[q];
         sxyf[0][2][lr * P + lc] = gf_[q];
-        if (lr < W - 1 && lc < W - 1) pd = gd_[(int64_t)(o.x + lr) * (nh - 1) + (o.y + lc)];
+        if (cell_loader) pd = gd_[(int64_t)(o.x + lr) * (nh - 1) + (o.y + lc)];
     }
-    // the corners' running maxima over this workgroup's cells (threads 1020 .. 1023), one atomic each
+    // the corners' running maxima over this workgroup's cells (threads T0 .. T0 + 3), one atomic each
     // at the end
     double cmax = 0.0, emax = 0.0;
     constexpr int off[8] = {-1, 1, -P, P, -P - 1, -P + 1, P - 1, P + 1};
     const bool clk = a.clk && blockIdx.x == 0 && __builtin_amdgcn_readfirstlane(t >> 6) == 0;  // wave 0 (scalar)
     unsigned long long c_setup = 0, c_sweeps = 0, c_rest = 0, c0 = clk ? wall_clock64() : 0, c1 = 0;
+    // the vertex's constants (kept across two steps by the inner sets), its box's orientation word and,
+    // at a corner, the cell's longest side or diagonal there
+    double mxx[8], mxy[8], myy[8];
+    VConst kc{0.0, 0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) mxx[k] = mxy[k] = myy[k] = 0.0;
+    unsigned ori = 3u;
     for (int p = 0; p <= my; ++p) {
-        const int s1 = p % 3, s2 = (p + 2) % 3;  // box sets of cell p (stage 1) and cell p - 1 (stage 2)
+        const int s1 = p & 1;  // cell p's box set and iterate pair
         if (clk && p > 0) {  // the previous step's corners and next box writes
             const unsigned long long now = wall_clock64();
             c_rest += now - c0;
             c0 = now;
         }
-        if (p < my && lr < W && lc < W) sd[s1][lr * P + lc] = pd;
+        if (p < my && loader) {
+            lrc(lr, lc);
+            sd[s1][lr * P + lc] = pd;
+        }
+        {  // the box's diagonal orientations: one LDS atomic a wave
+            const bool cv = p < my && cell_loader;
+            const unsigned long long b0 = __ballot(cv && pd == 0), b1 = __ballot(cv && pd != 0);
+            if ((t & 63) == 0 && (b0 | b1)) atomicOr(&sori[s1], (b0 ? 1u : 0u) | (b1 ? 2u : 0u));
+        }
         // cell p's box came through registers to LDS last step: an LDS-only barrier, so no wave waits
         // here for the acks of its earlier global stores (__syncthreads' fence would)
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        if (p < my && lr < W && lc < W) sg[p & 1][0][lr * P + lc] = make_double2(0.0, 0.0);  // x_0
-        if (p >= 2 && t >= 1020) {  // cell p - 2's corners, left by the last step's stage 2 (stored by
-            const int q = t - 1020;    // the last wave: no box loads of its own for K <= 13)
+        if (p >= 2 && role == 3 && t < T0 + 4) {  // cell p - 2's corners, left by the last step's old set
+            const int q = t - T0;
             const int64_t i = (int64_t)sout[q][2];
             a.gout[2 * i] = sout[q][0];
             a.gout[2 * i + 1] = sout[q][1];
             cmax = fmax(cmax, sout[q][3]);
-            emax = fmax(emax, cell_est(sout));
+            emax = nan_max(emax, cell_est(sout));
         }
-        const bool act = dep >= 1 && (role == 1 ? p < my : p >= 1);
-        const int bs = role == 1 ? s1 : s2;
-        double2(*const gg)[P * 32] = sg[role == 1 ? (p & 1) : ((p + 1) & 1)];
-        const double* const sx = sxyf[bs][0];
-        const double* const sy = sxyf[bs][1];
-        const double* const sf = sxyf[bs][2];
-        const uint8_t* const sdd = sd[bs];
-        // this vertex's constants: the eight slots' M in the edge order, c and P
-        double mxx[8], mxy[8], myy[8];
-        VConst kc{0.0, 0.0, 0.0, 0.0, 0.0};
-        if (act) {
+        const bool fresh = role == 2 || role == s1;  // this step: cell p (sweeps 1 .. S), else cell p - 1
+        const bool act = dep >= 1 && (fresh ? p < my : p >= 1);
+        if (act && fresh) {  // cell p's constants: the eight slots' M in the edge order, c and P
+            const double* const sx = sxyf[s1][0];
+            const double* const sy = sxyf[s1][1];
+            const double* const sf = sxyf[s1][2];
+            const uint8_t* const sdd = sd[s1];
+            ori = sori[s1];
             const unsigned em = 0x0fu | (sdd[b - P - 1] == 0 ? 0x10u : 0u) | (sdd[b - P] == 1 ? 0x20u : 0u) |
                                 (sdd[b - 1] == 1 ? 0x40u : 0u) | (sdd[b] == 0 ? 0x80u : 0u);
             const double xi = sx[b], yi = sy[b];
             const double fi[1] = {sf[b]}, zero[1] = {0.0};
+            // a corner (the corners are (K+1 .. K+2)^2 of the box) also takes the cell's two sides and
+            // its diagonal there: the slots toward the cell's other corners
+            const bool up = r == K + 1, rt = c == K + 1;
+            const unsigned cm = dep == K + 1 ? (up ? 0x08u : 0x04u) | (rt ? 0x02u : 0x01u) |
+                                                   (up ? (rt ? 0x80u : 0x40u) : (rt ? 0x20u : 0x10u))
+                                             : 0u;
+            double h2 = 0.0;
             GradAcc<1> A;
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 mxx[k] = mxy[k] = myy[k] = 0.0;
-                if (!(em & (1u << k))) continue;
+                if (!((em | cm) & (1u << k))) continue;
                 const int j = b + off[k];
-                const EdgeG e = edge_geom(sx[j] - xi, sy[j] - yi);
+                const double ex = sx[j] - xi, ey = sy[j] - yi;
+                if (cm & (1u << k)) h2 = fmax(h2, ex * ex + ey * ey);
+                if (!(em & (1u << k))) continue;
+                const EdgeG e = edge_geom(ex, ey);
                 const double fj[1] = {sf[j]};
                 acc_edge<1>(A, e, fi, fj, zero, zero);  // (its S part is not used: the sweeps form S)
                 mxx[k] = e.mxx;
@@ -1732,6 +1811,7 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch(Grid g, ConePatch a, int
                 myy[k] = e.myy;
             }
             kc = vertex_consts<1>(A, 0);
+            if (cm) shc[s1][role == 0 ? t : t - N2] = sqrt(h2);
         }
         // cell p + 1's box point through registers: issued after the setup (whose temporaries then
         // are dead), written to LDS after the sweeps, which hide its latency
@@ -1739,45 +1819,41 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch(Grid g, ConePatch a, int
         if (p + 1 < my) {
             pd = 0;
             const int2 o = scell[p + 1];
-            if (lr < W && lc < W) {
+            if (loader) {
+                lrc(lr, lc);
                 const int64_t q = (int64_t)(o.x + lr) * nh + (o.y + lc);
                 rx_ = gx_[q];
                 ry_ = gy_[q];
                 rf_ = gf_[q];
-                if (lr < W - 1 && lc < W - 1) pd = gd_[(int64_t)(o.x + lr) * (nh - 1) + (o.y + lc)];
+                if (cell_loader) pd = gd_[(int64_t)(o.x + lr) * (nh - 1) + (o.y + lc)];
             }
         }
-        // x_0 in place for sweep 1
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (t == 0) sori[s1 ^ 1] = 0u;  // cell p + 1's word (cell p - 1's was read in its own setup)
         if (clk) {
             c1 = wall_clock64();
             c_setup += c1 - c0;
         }
-        // S of one sweep from iterate buffer `in` (sweep 1 reads x_0 = 0 from buffer 0, zeroed at the
-        // step's top) and the Jacobi step's y; the buffer's row base is formed once per sweep, so each
-        // slot's read is one LDS instruction with a constant offset
-        auto sweep_y = [&](int in, double& y0, double& y1) {
-            double s0 = 0.0, s1 = 0.0, d0 = 0.0, d1 = 0.0;  // the axis and the diagonal chains
-            const double2* const gi = gg[in] + b;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const double2 gj = gi[off[k]];
-                double& t0 = k < 4 ? s0 : d0;
-                double& t1 = k < 4 ? s1 : d1;
-                t0 = __builtin_fma(mxy[k], gj.y, __builtin_fma(mxx[k], gj.x, t0));
-                t1 = __builtin_fma(myy[k], gj.y, __builtin_fma(mxy[k], gj.x, t1));
-            }
-            jacobi_y(kc, s0 + d0, s1 + d1, y0, y1);
-        };
+        double2(*const gg)[P * 32] = sg[fresh ? s1 : s1 ^ 1];  // this thread's cell's iterate pair
+        // the wave's slot set: six slots when every active lane's box takes one diagonal throughout
+        const bool w0 = __ballot(act && ori != 1u) == 0, w1 = __ballot(act && ori != 2u) == 0;
         for (int q = 1; q <= Q; ++q) {
-            const int j = role == 1 ? q : S + q;
-            if (act && dep >= j && (role == 1 ? q <= S : j <= K)) {
+            const int j = fresh ? q : S + q;
+            if (act && dep >= j && j <= (fresh ? S : K)) {
+                // sweep j's form (the host's steps): 1 plain, 2 against x_0 = 0, later against x_{j-2}
+                const double om = somg[j];
                 const int in = (j - 1) & 1, out = j & 1;
-                const ConeStep st = a.st[j];
+                const double2 pv = j >= 3 ? gg[out][b] : make_double2(0.0, 0.0);  // x_{j-2}, overwritten
+                double s0 = 0.0, s1v = 0.0;  // sweep 1: x_0 = 0, S = +0
+                if (j >= 2) {
+                    if (w0) patch_sums<kSlotsDiag0, P>(gg[in], b - P - 1, mxx, mxy, myy, s0, s1v);
+                    else if (w1) patch_sums<kSlotsDiag1, P>(gg[in], b - P - 1, mxx, mxy, myy, s0, s1v);
+                    else patch_sums<kSlotsAll, P>(gg[in], b - P - 1, mxx, mxy, myy, s0, s1v);
+                }
                 double y0, y1;
-                sweep_y(in, y0, y1);
-                const double2 pv = st.mode == 2 ? gg[out][b] : make_double2(0.0, 0.0);  // x_{j-2}, overwritten
-                gg[out][b] = make_double2(cheb(st, y0, pv.x), cheb(st, y1, pv.y));
+                jacobi_y(kc, s0, s1v, y0, y1);
+                gg[out][b] = j == 1 ? make_double2(y0, y1)
+                                    : make_double2(__builtin_fma(om, y0 - pv.x, pv.x), __builtin_fma(om, y1 - pv.y, pv.y));
             }
             asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         }
@@ -1785,52 +1861,49 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch(Grid g, ConePatch a, int
             c0 = wall_clock64();
             c_sweeps += c0 - c1;
         }
-        // cell p - 1's corners (stage 2's innermost ring): x_K, the change of one more plain sweep and
-        // the value-error estimate, into LDS; the last wave stores them after the next step's
-        // barrier (or below, after the last step), so the stores' latency is not waited for at the
-        // next step's top
-        if (role == 2 && act && dep == K + 1) {
+        // cell p - 1's corners (the old set's innermost ring): x_K, the change of one more plain
+        // sweep and the value-error estimate, into LDS; the corner-store threads store them after the
+        // next step's barrier (or below, after the last step), so the stores' latency is not waited
+        // for at the next step's top
+        if (!fresh && act && dep == K + 1) {
             const int2 o = scell[p - 1];
             const int fin = K & 1;
             const double2 gk = gg[fin][b];
-            double y0, y1;
-            sweep_y(fin, y0, y1);
-            // the cell's sides and diagonal at this corner (the corners are (K+1 .. K+2)^2 of the box)
-            const int dr = r == K + 1 ? P : -P, dc = c == K + 1 ? 1 : -1;
-            const double x0 = sx[b], y0c = sy[b];
-            const double h2 = fmax(fmax((sx[b + dr] - x0) * (sx[b + dr] - x0) + (sy[b + dr] - y0c) * (sy[b + dr] - y0c),
-                                        (sx[b + dc] - x0) * (sx[b + dc] - x0) + (sy[b + dc] - y0c) * (sy[b + dc] - y0c)),
-                                   (sx[b + dr + dc] - x0) * (sx[b + dr + dc] - x0) +
-                                       (sy[b + dr + dc] - y0c) * (sy[b + dr + dc] - y0c));
-            const int q = t - N1a;  // the innermost ring: stage 2's first four threads
+            double s0, s1v, y0, y1;
+            patch_sums<kSlotsAll, P>(gg[fin], b - P - 1, mxx, mxy, myy, s0, s1v);
+            jacobi_y(kc, s0, s1v, y0, y1);
+            const int q = role == 0 ? t : t - N2;  // the innermost ring: a set's first four threads
             sout[q][0] = gk.x;
             sout[q][1] = gk.y;
             sout[q][2] = (double)((int64_t)(o.x + r) * nh + (o.y + c));
             sout[q][3] = a.chg ? change_of(gk.x, gk.y, y0, y1) : 0.0;
-            sout[q][4] = fmax(fabs(gk.x - y0), fabs(gk.y - y1));
-            sout[q][5] = sqrt(h2);
+            sout[q][4] = nan_max(fabs(gk.x - y0), fabs(gk.y - y1));
+            sout[q][5] = shc[s1 ^ 1][q];
         }
-        if (p + 1 < my && lr < W && lc < W) {  // set (p + 1) % 3 is read from the next step on
-            const int q = lr * P + lc, st = (p + 1) % 3;
+        if (p + 1 < my && loader) {  // set (p + 1) & 1 is read from the next step on
+            lrc(lr, lc);
+            const int q = lr * P + lc, st = s1 ^ 1;
             sxyf[st][0][q] = rx_;
             sxyf[st][1][q] = ry_;
             sxyf[st][2][q] = rf_;
         }
         if (p == my && my >= 1) {  // the last cell's corners
             __syncthreads();
-            if (t >= 1020) {
-                const int q = t - 1020;
+            if (role == 3 && t < T0 + 4) {
+                const int q = t - T0;
                 const int64_t i = (int64_t)sout[q][2];
                 a.gout[2 * i] = sout[q][0];
                 a.gout[2 * i + 1] = sout[q][1];
                 cmax = fmax(cmax, sout[q][3]);
-                emax = fmax(emax, cell_est(sout));
+                emax = nan_max(emax, cell_est(sout));
             }
         }
     }
-    if (t >= 1020) {
+    if (role == 3 && t < T0 + 4) {
         if (a.chg && cmax > 0) atomicMax(a.chg, (unsigned long long)__double_as_longlong(cmax));
-        if (a.est && emax > 0) atomicMax(a.est, (unsigned long long)__double_as_longlong(emax));
+        // a NaN estimate as +inf (ordered bits: the guard sees an estimate above any bar)
+        if (a.est && (emax > 0 || emax != emax))
+            atomicMax(a.est, (unsigned long long)__double_as_longlong(emax != emax ? HUGE_VAL : emax));
     }
     if (clk && t == 0) {
         a.clk[0] += c_setup;
@@ -1966,7 +2039,6 @@ __device__ __forceinline__ bool cone_interior(const Grid& g, int o, int K, int64
 __global__ void __launch_bounds__(kBlock) k_gd_cone_assign(Grid g, const int* __restrict__ owner, int64_t m, int K,
                                                             int64_t own0, int64_t own1, int band_on, int64_t* cells,
                                                             int* count, int* band, uint8_t* assigned) {
-    const int64_t nc2 = 2 * ncells(g);
     for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < m; t += (int64_t)gridDim.x * blockDim.x) {
         const int o = owner[t];
         uint8_t mine = 0;
@@ -2576,6 +2648,8 @@ struct PatchTimer {
     bool on = false, made = false;
     hipEvent_t ev[kPatchEvents][2];
     const int* cnt[kPatchEvents];
+    hipEvent_t bev[kPatchEvents][2];  // around each value set's band sweeps (the guard's extra sweep included)
+    int64_t band_launches = 0;
     int64_t launches = 0;
     unsigned long long* clk = nullptr;  // device: workgroup 0's phase clocks, summed over the launches
 };
@@ -2780,11 +2854,12 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
     steps[0] = ConeStep{0, 1.0};
     for (int j = 1; j <= K; ++j)
         steps[j] = j == 1 ? ConeStep{0, 1.0} : j == 2 ? ConeStep{1, omegas[1]} : ConeStep{2, omegas[j - 1]};
-    // the patches' pipeline split: the smallest S >= K / 2 with both stages' vertices in 1020 threads
+    // the patches' pipeline split: the smallest S >= K / 2 with the three thread sets (two inner, one
+    // outer) and the four corner-store threads in one workgroup
     const int W = 2 * K + 4;
     int S = -1;
     for (int s2 = (K + 1) / 2; s2 <= K && S < 0; ++s2)
-        if ((((W - 2) * (W - 2) + 63) & ~63) + (W - 2 * s2 - 2) * (W - 2 * s2 - 2) <= 1020) S = s2;
+        if ((W - 2) * (W - 2) + (W - 2 * s2 - 2) * (W - 2 * s2 - 2) + 4 <= 1024) S = s2;
     const unsigned pp = gd_cu_count();  // one persistent workgroup per CU walks its cells
     AKB_REQUIRE(S >= 0 && m <= 1024 * (int64_t)pp, "cone patches: K or the target count out of range");
     for (int v = 0; v < nvals; ++v) {
@@ -2792,7 +2867,14 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
         // the boundary band, shrinking like the patches' squares: sweep j forms depth <= 2K + 3 - j,
         // whose neighbours (depth <= 2K + 4 - j) sweep j - 1 formed, so x_K is the global iteration's
         // to depth K + 3 >= every band target's corners (the first sweep reads x_0 = 0 only)
+#ifdef AKB_EXP_NOBAND  // (measurement only: the band's share of the step; results wrong)
+        if (false) {
+#else
         if (band_on) {
+#endif
+            PatchTimer& bt0 = patch_timer();
+            const int bslot = (int)(bt0.band_launches % kPatchEvents);
+            if (bt0.on) (void)hipEventRecord(bt0.bev[bslot][0], s);
             // the ring's chord slots (the work's (L, 16)-double region: kChordSlots int32 a vertex)
             int32_t* slots = (int32_t*)((double*)work + 3 * (int64_t)nv2 * n * 2);
             if (v == 0) {
@@ -2815,6 +2897,10 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
                 k_gd_cone_band<<<band_grid(bt, L), kBandThreads, 0, s>>>(g, bt, a);
                 if ((st = launch_status("k_gd_cone_band"))) return st;
             }
+            if (bt0.on) {
+                (void)hipEventRecord(bt0.bev[bslot][1], s);
+                ++bt0.band_launches;
+            }
         }
         const BandEst be{band_on && d_change ? gb[(K + 1) % 3] : nullptr, K, d_change, d_change ? d_change + 1 : nullptr};
         ConePatch a{fv, cells, count, K, {}, gb[K % 3], d_change, d_change ? d_change + 1 : nullptr,
@@ -2826,7 +2912,9 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
             (void)hipEventRecord(pt.ev[slot][0], s);
             pt.cnt[slot] = count;
         }
-        k_gd_cone_patch<<<pp, 1024, 0, s>>>(g, a, S);
+#ifndef AKB_EXP_NOPATCH  // (measurement only: the patches' share of the step; results wrong)
+        k_gd_cone_patch<<<pp, patch_threads(K, S), 0, s>>>(g, a, S);
+#endif
         if (pt.on) {
             (void)hipEventRecord(pt.ev[slot][1], s);
             ++pt.launches;
@@ -2978,19 +3066,38 @@ int akb_gd_cells_window_f64(const double* x, const double* y, int nv, int nh, in
     return launch_cells(g, diag, tol, d_flags, row1 - row0, (hipStream_t)stream);
 }
 
+// the patch timer's events and clock words (akb_release_all)
+void akb_gd_release(void) {
+    PatchTimer& t = patch_timer();
+    if (!t.made) return;
+    for (int k = 0; k < kPatchEvents; ++k)
+        for (int q = 0; q < 2; ++q) {
+            (void)hipEventDestroy(t.ev[k][q]);
+            (void)hipEventDestroy(t.bev[k][q]);
+        }
+    (void)hipFree(t.clk);
+    t.clk = nullptr;
+    t.made = t.on = false;
+    t.launches = t.band_launches = 0;
+}
+
 // diagnostics: k_gd_cone_patch launch times (see patch_timer)
 int akb_gd_patch_timing(int enable) {
     clear_error();
     PatchTimer& t = patch_timer();
     if (enable && !t.made) {
         for (int k = 0; k < kPatchEvents; ++k)
-            for (int q = 0; q < 2; ++q) AKB_HIP_CHECK(hipEventCreate(&t.ev[k][q]));
+            for (int q = 0; q < 2; ++q) {
+                AKB_HIP_CHECK(hipEventCreate(&t.ev[k][q]));
+                AKB_HIP_CHECK(hipEventCreate(&t.bev[k][q]));
+            }
         AKB_HIP_CHECK(hipMalloc((void**)&t.clk, kPatchClk * sizeof(unsigned long long)));
         t.made = true;
     }
     if (enable) {  // a new record (stopping keeps the last one for akb_gd_patch_times / _phases)
         AKB_HIP_CHECK(hipMemset(t.clk, 0, kPatchClk * sizeof(unsigned long long)));
         t.launches = 0;
+        t.band_launches = 0;
     }
     t.on = enable != 0;
     return 0;
@@ -3018,6 +3125,18 @@ int akb_gd_patch_times(float* ms, int* cells, int max) {
         AKB_HIP_CHECK(hipEventSynchronize(t.ev[slot][1]));
         AKB_HIP_CHECK(hipEventElapsedTime(&ms[k], t.ev[slot][0], t.ev[slot][1]));
         if (cells) AKB_HIP_CHECK(hipMemcpy(&cells[k], t.cnt[slot], sizeof(int), hipMemcpyDeviceToHost));
+    }
+    return n;
+}
+
+int akb_gd_band_times(float* ms, int max) {
+    clear_error();
+    PatchTimer& t = patch_timer();
+    const int n = (int)std::min<int64_t>(std::min<int64_t>(t.band_launches, kPatchEvents), max);
+    for (int k = 0; k < n; ++k) {
+        const int slot = (int)((t.band_launches - n + k) % kPatchEvents);
+        AKB_HIP_CHECK(hipEventSynchronize(t.bev[slot][1]));
+        AKB_HIP_CHECK(hipEventElapsedTime(&ms[k], t.bev[slot][0], t.bev[slot][1]));
     }
     return n;
 }

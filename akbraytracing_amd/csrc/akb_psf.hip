@@ -1641,6 +1641,10 @@ void akb_psf_release_plans(void) {
         std::lock_guard<std::mutex> lk(g_plan_mu);
         for (auto& kv : g_plans) rocfft_plan_destroy(kv.second.plan);
         g_plans.clear();
+        if (g_rocfft_ready) {  // rocFFT's own caches too, before the HIP runtime's teardown
+            rocfft_cleanup();
+            g_rocfft_ready = false;
+        }
     }
     std::lock_guard<std::mutex> lk(g_tw_mu);
     for (auto& kv : g_tw) (void)hipFree(kv.second);

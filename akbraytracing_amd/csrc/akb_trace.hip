@@ -1701,6 +1701,28 @@ std::mutex g_ring_mu;
 ArgRing g_rings[64];
 }  // namespace
 
+void akb_gd_release(void);  // akb_griddata.hip: the patch-timing events and clock words
+
+// every cache of device / pinned resources, freed while the HIP runtime is up (see the header)
+void akb_release_all(void) {
+    {
+        std::lock_guard<std::mutex> lock(g_ring_mu);
+        for (ArgRing& R : g_rings)
+            for (ArgSlot& S : R.slot) {
+                if (S.done) {
+                    (void)hipEventSynchronize(S.done);
+                    (void)hipEventDestroy(S.done);
+                    S.done = nullptr;
+                }
+                if (S.host) (void)hipHostFree(S.host);
+                S.host = nullptr;
+                S.cap = 0;
+            }
+    }
+    akb_psf_release_plans();
+    akb_gd_release();
+}
+
 // copy `bytes` of host data to a fresh stream-ordered device allocation (*d_out, freed by the
 // caller with hipFreeAsync on the same stream after its launch)
 static int stage_args(const void* src, size_t bytes, hipStream_t s, void** d_out) {

@@ -3,6 +3,8 @@
 All hot-path data is float64 struct-of-arrays, (3, N) row-major, like the reference's arrays.
 """
 import ctypes
+import threading
+import time
 
 import numpy as np
 import torch
@@ -58,3 +60,39 @@ def empty(shape, dev=None):
 
 def flags_tensor(dev=None):
     return torch.zeros(1, dtype=torch.int32, device=dev or device())
+
+
+# ---- host wait clock: wall time the issuing (main) thread spends blocked on the device or on a
+# worker (events not yet reached, the pocket job), so a caller can tell its own issue cost from its
+# waits (bench.py: host_issue_ms_per_step = host_wait_ms_per_step + the pure issue time)
+_HOST_WAIT = [0.0]
+
+
+def host_wait_s():
+    """Seconds the main thread has spent in wait_event / wait_result so far."""
+    return _HOST_WAIT[0]
+
+
+def _clock(t0):
+    if threading.current_thread() is threading.main_thread():
+        _HOST_WAIT[0] += time.perf_counter() - t0
+
+
+def wait_event(ev):
+    """ev.synchronize(), its blocked time on the host wait clock (nothing when ev has passed)."""
+    if ev.query():
+        return
+    t0 = time.perf_counter()
+    ev.synchronize()
+    _clock(t0)
+
+
+def wait_result(fut):
+    """fut.result(), its blocked time on the host wait clock."""
+    if fut.done():
+        return fut.result()
+    t0 = time.perf_counter()
+    try:
+        return fut.result()
+    finally:
+        _clock(t0)

@@ -27,6 +27,7 @@ API for single calls; tests/test_faithful_gpu.py holds this pipeline to them and
 reference's own PSF.
 """
 import concurrent.futures
+import time
 
 import numpy as np
 import torch
@@ -182,6 +183,7 @@ class FaithfulPupil:
         # parameter block
         self.errors = ErrorLog(1 + 2 + POST_PARAMS)
         self.finished = 0  # runs through finish()
+        self.pocket_ms = []  # host time of each run's pocket triangulation (worker threads)
 
     # ------------------------------------------------------------------ stage 1
     def begin(self, y, z, f, stream=None):
@@ -195,7 +197,7 @@ class FaithfulPupil:
             if not prev.finished:
                 raise RuntimeError("FaithfulPupil: more runs begun than slots before a finish")
             if prev.h2d is not None:
-                prev.h2d.synchronize()
+                D.wait_event(prev.h2d)
         sh = D.stream_handle(stream)
         Lr = self.L
         ring = s["ring"]
@@ -238,10 +240,12 @@ class FaithfulPupil:
             o = self._o
             hp = lambda k: buf[o[k]:].ctypes.data_as(_lib.c_vp)  # noqa: E731
             try:
+                t0 = time.perf_counter()
                 _lib.check(L.akb_gd_pockets(rb[:Lr].ctypes.data_as(_lib.c_vp), rb[Lr:2 * Lr].ctypes.data_as(_lib.c_vp),
                                             self.nv, self.nh, Lr, hp("npk"), hp("tri"), hp("nbr"), hp("edge"),
                                             hp("xptr"), hp("xidx")))
                 npk, s["po"] = pack_pockets(buf, o, Lr)
+                self.pocket_ms.append((time.perf_counter() - t0) * 1e3)  # (the host's pocket job, bench.py)
             except _lib.AKBError as e:
                 err = e
         fl = int(rb[2 * Lr:].view(np.int32)[0])
@@ -256,15 +260,16 @@ class FaithfulPupil:
         return npk
 
     # ------------------------------------------------------------------ stage 2
-    def finish(self, t, stream=None, events=None, psf_events=None):
+    def finish(self, t, stream=None, events=None, psf_events=None, post_events=None):
         """Queue the rest of ticket t's chain on `stream` (waits for its pocket job on the host -
         normally long done). Returns dict(psf (B, P, P) device, map, corrected, rotated, params,
         axes, change); the buffers are reused by the next finish on the stream (axes, the slot's, by
         the slot's next begin). events: optional (start, end)
-        timing events recorded around the device work; psf_events: the same around the PSF alone."""
+        timing events recorded around the device work; psf_events: the same around the PSF alone;
+        post_events: around the post (nanmean, plane fits, prefilter, rotation)."""
         L = _lib.lib()
         try:
-            t.npock = t.job.result()
+            t.npock = D.wait_result(t.job)
         except BaseException:
             # the run failed on the host (check() raises it again); its slot stays usable
             t.y = t.z = t.f = None
@@ -298,7 +303,11 @@ class FaithfulPupil:
             _lib.check(L.akb_gd_cone_solve_f64(*tri, D.ptr(xptr), D.ptr(xidx), D.ptr(gx), m, D.ptr(gy), m,
                                                D.ptr(t.f), 1, self.sweeps, self._omegas, D.ptr(self.work),
                                                D.ptr(s["owner"]), D.ptr(self.map), D.ptr(self.change), sh))
+            if post_events is not None:
+                post_events[0].record(st)
             post = pupil_post(self.map[0], out=self.post, stream=st)
+            if post_events is not None:
+                post_events[1].record(st)
             self.post = post
             if psf_events is not None:
                 psf_events[0].record(st)
@@ -345,6 +354,10 @@ class FaithfulPupil:
             psf, _, _ = psf_stack(post["opd"], None, self.lams, None, pad_factor=self.pad, stream=st, out=self.psf,
                                   pitch=ax[2 * m + 4:2 * m + 6])
             self.psf = psf
+            # the shared map / post / psf buffers' last writer: a later finish on another stream waits
+            # for this one, not for the run's own (earlier) finish
+            self._done = torch.cuda.Event()
+            self._done.record(st)
         pupil_post_check(post["params"])
         return dict(psf=psf, map=self.map[0], corrected=post["corrected"], rotated=post["rotated"],
                     params=post["params"], axes=ax, change=self.change, converged=True)

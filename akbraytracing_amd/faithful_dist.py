@@ -530,11 +530,62 @@ class ShardedFaithfulPupil:
         cone_guard(est, w[world + 3:])
 
     def run(self, y, z, f, stream=None):
-        """begin + finish + check of one run: (result or None, ticket)."""
+        """begin + finish + check of one run: (result or None, ticket). The band owner's guard verdict
+        is broadcast, so every rank takes the same path: a run whose cone solve fails its guard
+        (ConeNotConverged; FaithfulPupil.run's fallback) is formed again from the converged gradients -
+        the ranks' hits gathered to the band owner, which grids the whole lattice with the global
+        sweeps to scipy's tolerance on the run's axes; the other ranks return None, as for every
+        run. Any other error raises on the band owner only (after the run's collectives, so the
+        group stays in step)."""
+        from .griddata import ConeNotConverged
         t = self.begin(y, z, f, stream)
         res = self.finish(t, stream)
-        self.check(t)
+        verdict, err = 0, None
+        if self.plan.is_root:
+            try:
+                self.check(t)
+            except ConeNotConverged as e:
+                verdict, err = 1, e
+            except BaseException as e:  # raised below, after the verdict's collective
+                verdict, err = 2, e
+        v = torch.tensor([float(verdict)], dtype=torch.float64, device=self.dev)
+        _broadcast(self.comm, v, self.plan.root, self.group)
+        verdict = int(v.item())
+        if verdict == 1:
+            res = self._converged(y, z, f, stream)
+        elif verdict == 2 and err is not None:
+            raise err
         return res, t
+
+    def _converged(self, y, z, f, stream=None):
+        """The guard's fallback (collective): every rank's rows to the band owner, which forms the
+        run's map from the global gradient iteration (CubicGrid.interp) on the run's axes, then the
+        same post and PSF; None on the other ranks."""
+        from . import device as D
+        from .dist import gather_to_root
+        from .griddata import CubicGrid
+        from .pupilmap import pupil_post, pupil_post_check
+        from .psf import psf_stack
+        p, m = self.plan, self.size
+        counts = [sh.count for sh in p.shards]
+        got = gather_to_root(self.comm, [y.contiguous(), z.contiguous(), f.contiguous()], counts, p.root)
+        if got is None:
+            return None
+        st = torch.cuda.current_stream() if stream is None else stream
+        with torch.cuda.stream(st):
+            ya, za, fa = got
+            cg = CubicGrid(ya, za, self.n, self.n, delaunay_tol=self.tol)
+            self.map[0].copy_(cg.interp(fa.reshape(1, -1), self.axes[:m], self.axes[m:2 * m])[0])
+            post = pupil_post(self.map[0], out=self.post, stream=st)
+            self.post = post
+            psf, _, _ = psf_stack(post["opd"], None, self.lams, None, pad_factor=self.pad, stream=st,
+                                  out=self.psf, pitch=self.axes[2 * m + 4:2 * m + 6])
+            self.psf = psf
+            self._done = torch.cuda.Event()  # the shared buffers' last writer (see FaithfulPupil._converged)
+            self._done.record(st)
+        pupil_post_check(post["params"])
+        return dict(psf=psf, map=self.map[0], corrected=post["corrected"], rotated=post["rotated"],
+                    params=post["params"], axes=self.axes, change=self.change, converged=True)
 
     def close(self):
         if self.pool is not None:

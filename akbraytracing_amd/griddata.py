@@ -42,9 +42,10 @@ GRADIENT_TOL = 1e-6
 CONE_SWEEPS = 12
 
 
-# The cone solve's guard (FaithfulPupil, Ticket.check): its value-error estimate at the interior
-# target cells (akb_gd_cone_eval_f64's d_change[1]) must stay within this fraction of the gridded
-# map's range - the parity bar of the gridding against scipy (tests/test_fullsize_gpu.py).
+# The cone solve's guard (FaithfulPupil, Ticket.check): its value-error estimate (akb_gd_cone_eval_f64's
+# d_change[1]: the interior target cells' corner bound from the patches, and the band and pocket
+# targets' value change of one more band sweep, from k_gd_eval) must stay within this fraction of
+# the gridded map's range - the parity bar of the gridding against scipy (tests/test_fullsize_gpu.py).
 CONE_GUARD = 1e-6
 
 

@@ -1,14 +1,16 @@
-"""Fraunhofer PSF by FFT on rocFFT: the reference's psf_fft module, device-backed.
+"""Fraunhofer PSF of a pupil: the reference's psf_fft module, device-backed.
 
 compute_psf_fft / psf_to_db / ensure_even_size keep psf_fft.py's signatures, argument checks
 (ValueError on a shape mismatch, a bad pad_factor, an unknown window: psf_fft.py:74-77, :92) and
 return values (numpy arrays). psf_stack() is the device API: one batched 2-D transform over a
 stack of wavelengths (config 5's multi-lambda PSF), inputs and outputs as device tensors.
 
-On the device (libakb_hip.so, akb_psf_f64): one kernel builds the padded, ifftshift-ed pupil
-field straight into the FFT buffer (NaN mask, exp(i 2pi/lambda opd), optional Hann, even-size
-pad, centred zero-pad), rocFFT runs the in-place complex transform, and one kernel applies
-fftshift, dA, |U|^2 and the per-wavelength peak, followed by the normalisation pass.
+On the device (libakb_hip.so, akb_psf_f64) the padded plane is never built: it is zero outside
+the pupil block, so at pad 8 and 16 (every caller's pad) the transform runs as pruned line
+transforms (k_psf_line: the pupil's columns, the peak rows, then the normalised write - DESIGN.md
+§4.1); other pads of small pupils take the column-pass transform, and only the remaining shapes
+build the padded, ifftshift-ed field and run rocFFT's in-place complex transform, then fftshift,
+dA, |U|^2, the per-wavelength peak and the normalisation pass.
 """
 import numpy as np
 import torch

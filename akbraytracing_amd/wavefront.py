@@ -292,6 +292,7 @@ class RayWave:
         self._opd_buf = None
         self.last = {}
         self.kernel_events = None  # set to a list to time the pass-2 chain launch (bench.py)
+        self.pass1_events = None  # set to a list to time the pass-1 launch (fused or not; bench.py)
         # prepared launches. The resample picks come from a prepass that traces only the rays
         # they read (akb_trace_chain_samples_f64, every rank all of them); the pick buffer ends
         # with one double-sized slot holding that prepass's flag word, so one copy brings both to
@@ -407,13 +408,13 @@ class RayWave:
         next_geometry) is dropped and redone for g."""
         g = g if g is not None else self.g
         if self._next_picks is not None and self._next_picks[2] != geometry_key(g):
-            self._next_picks[0].synchronize()  # its host buffer is about to be reused
+            D.wait_event(self._next_picks[0])  # its host buffer is about to be reused
             self._next_picks = None
         if self._next_picks is None:
             self._queue_picks(g)
         ev, x, _ = self._next_picks
         self._next_picks = None
-        ev.synchronize()
+        D.wait_event(ev)
         hb, he, _ = self._plan
         host = x.numpy()
         nh = he - hb
@@ -427,12 +428,19 @@ class RayWave:
         d = self._p1.desc
         d.copy_src, d.copy_dst, d.copy_n = D.ptr(self._tan2_host[slot]), D.ptr(self._tan2[slot]), 2 * self.n
         d.flags = D.ptr(self._flagw[slot, 0:1])
+        tev = None
+        if self.pass1_events is not None:  # (on the stream the kernel runs on: the current one)
+            tev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            tev[0].record()
         if fuse is None:
             self._p1.launch(stream=stream, reset_flags=False)
             ev = torch.cuda.Event()
             ev.record()
         else:
             ev = self._fused_pass1(fuse, stream, fuse_opd)  # one event after the kernel serves both
+        if tev is not None:
+            tev[1].record()
+            self.pass1_events.append((tev[0], tev[1], fuse is not None, fuse_opd is not None))
         self._staged[slot] = ev
 
     def _pass2(self, want_rows=False, stream=None, slot=0):
@@ -533,7 +541,7 @@ class RayWave:
             torch.cuda.synchronize()
             raise _lib.AKBError(self._pass1_error(sflags))
         if self._staged[slot] is not None:  # the pass 1 that last copied this slot's host tables
-            self._staged[slot].synchronize()
+            D.wait_event(self._staged[slot])
             self._staged[slot] = None
         th = self._tan2_host[slot].numpy()
         if self.resample_pass:
@@ -608,13 +616,12 @@ class RayWave:
         on the host: a pipelined caller runs ahead of the device, so the wait costs the device
         nothing, while a cross-queue wait on the device puts a barrier packet ahead of the next
         trace kernel (measured 0.810 -> 0.803 ms per step)."""
-        if not ev.query():
-            ev.synchronize()
+        D.wait_event(ev)
 
     def _flags_of(self, f):
         """f's (pass 1, pass 2) trace flag words (waits for its pass 2 if still running)."""
         if f.flags is None:
-            f.flag_ev.synchronize()
+            D.wait_event(f.flag_ev)
             h = self._f_host[f.slot]
             f.flags = (int(h[0]), int(h[1]))
         return f.flags

@@ -319,13 +319,13 @@ def read_faithful_profile():
 def faithful_roofline(ms, cells, K, S):
     """The cone solve's patch kernel (k_gd_cone_patch) over the timed steps: its launch time from HIP
     events around every launch (akb_gd_patch_times, in the step, sharing the GPU), its work (interior
-    target cells x the box's shrinking squares: sum_j (2K + 4 - 2j)^2 vertex-sweeps; (W - 2)^2 + (W -
-    2S - 2)^2 vertex setups, stage 2 forming its own), its compulsory HBM traffic (the cells' boxes
+    target cells x the box's shrinking squares: sum_j (2K + 4 - 2j)^2 vertex-sweeps; (W - 2)^2 vertex
+    setups, each vertex's constants formed once per cell), its compulsory HBM traffic (the cells' boxes
     of x, y, f and diagonal bytes in, four corners' gradients out) against 8 TB/s, and - from the
     committed PMC summary while it describes these sources - its VALU issue against the SIMDs'."""
     W = 2 * K + 4
     sweeps = sum((W - 2 * j) ** 2 for j in range(1, K + 1))
-    setups = (W - 2) ** 2 + (W - 2 * S - 2) ** 2
+    setups = (W - 2) ** 2
     avg = sum(ms) / len(ms)
     byts = cells * (W * W * 24 + (W - 1) * (W - 1) + 4 * 16)
     prof, pfile, pok = read_faithful_profile()
@@ -334,7 +334,8 @@ def faithful_roofline(ms, cells, K, S):
     clock = pk.get("effective_clock_ghz")
     out = {
         "kernel": "k_gd_cone_patch (akb_griddata.hip)",
-        "bound": "latency: one 1024-thread workgroup per CU, a barrier per sweep (VALU issue below)",
+        "bound": "latency: one workgroup of (W-2)^2 + (W-2S-2)^2 vertex threads per CU, a barrier per sweep "
+                 "(VALU issue below)",
         "launches": len(ms),
         "avg_ms": avg,
         "cells_per_launch": cells,
@@ -356,6 +357,115 @@ def faithful_roofline(ms, cells, K, S):
         "profile": {"file": pfile, "matches_sources": pok},
     }
     return out
+
+
+# bytes pass 1 moves per ray besides its 2n-entry tables: the fused tilt of run k-2 reads the last
+# hit and exit direction (48) + total OPL (8) and writes detector-2 hit (24) + total OPL 2 (8); the
+# fused OPD of run k-3 reads t2 + detector-2 hit (32) and writes DistError2 and Wave2 (16)
+PASS1_TILT_BYTES_PER_RAY = 88
+PASS1_OPD_BYTES_PER_RAY = 48
+
+
+def pass1_roofline(launches, rays, prof, fuse):
+    """The pass-1 kernel of the timed steps: HIP-event time per launch (the steady-state launches:
+    tilt and OPD fused when --fuse 2), its algorithmic bytes against 8 TB/s, and - from the committed
+    PMC summary (its pass1_fused entry) while it describes these sources - its HBM traffic, VALU issue
+    and wait fractions. Pass 1 is VALU-issue bound (4 mirrors of FP64 quadric solves per ray); its
+    HBM bytes are the fused tilt / OPD rows it carries."""
+    if not launches:
+        return None
+    full = [ms for ms, ft, fo in launches if ft and fo] if fuse >= 2 else \
+           [ms for ms, ft, fo in launches if ft] if fuse == 1 else [ms for ms, _, _ in launches]
+    ms = full or [ms for ms, _, _ in launches]
+    avg = sum(ms) / len(ms)
+    per_ray = (PASS1_TILT_BYTES_PER_RAY if fuse >= 1 else 0) + (PASS1_OPD_BYTES_PER_RAY if fuse >= 2 else 0)
+    byts = per_ray * rays
+    pk = prof.get("kernels", {}).get("pass1_fused", {}) if fuse >= 2 else {}
+    clock = pk.get("effective_clock_ghz")
+    valu = pk.get("valu_wave_instructions_per_launch")
+    return {
+        "kernel": "k_chain_tilt<4,true> (pass 1 + tilt of run k-2 + OPD of run k-3)" if fuse >= 2 else
+                  "k_chain_tilt<4,false> (pass 1 + tilt of run k-2)" if fuse == 1 else "k_chain (pass 1, flags only)",
+        "launches": len(ms),
+        "avg_ms": avg,
+        "rays_per_launch": rays,
+        "hbm": {"bound": "hbm", "algorithmic_bytes_per_launch": byts,
+                "achieved": byts / (avg * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": byts / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": pk.get("hbm_bytes_per_launch")},
+        "valu_issue": {"bound": "valu-issue", "wave_instructions_per_launch": valu, "effective_clock_ghz": clock,
+                       "achieved": valu / (avg * 1e-3) if valu else None,
+                       "peak": SIMDS / 4 * clock * 1e9 if clock else None, "unit": "wave-instructions/s",
+                       "frac": (valu / (avg * 1e-3)) / (SIMDS / 4 * clock * 1e9) if valu and clock else None,
+                       "issue_frac_profiled": pk.get("issue_frac"), "wait_any_frac_profiled": pk.get("wait_any_frac"),
+                       "non_fp64_share": pk.get("non_fp64_share")},
+        "fusion_ab": "--fuse 2 / 1 / 0 (this kernel fused with tilt + OPD / tilt only / neither): 1.63 / 1.66 / "
+                     "1.83 ms per step, two interleaved rounds (profiles/r06a_fuse_ab.json)",
+    }
+
+
+def rank0_tail(n=10000, reps=3, size=128, pad=16, lams=(13.5e-9,), workers=4):
+    """C4's band owner's extra work per run, measured on one GPU. At N > 1 every rank
+    traces its rows and forms the interior targets of its own cells (faithful_dist.py); rank 0 alone
+    also iterates the boundary band (K + 1 launches), builds the pockets on the host (worker threads),
+    and runs the post and the PSF. Here the one-process chain runs on configs[3]'s whole n^2 = 1e8-ray
+    lattice (one trace of the C3 system) and its device phases are timed with HIP events: the band
+    iteration (akb_gd_band_times), the post, the PSF, and the finish as a whole (with every interior
+    patch: finish - patches bounds rank 0's device share from above); the pocket job's host time
+    comes from its worker. Medians over reps runs after one first-use run."""
+    import torch
+    from akbraytracing_amd import _lib as LIBM
+    from akbraytracing_amd.faithful import FaithfulPupil
+    from akbraytracing_amd.wavefront import RayWave, SystemGeometry
+    L = LIBM.lib()
+    rw = RayWave(SystemGeometry.from_dict(geometry_dict("c3")), n)
+    out = rw.run()
+    d2, w2 = out["detcenter2"], out["wave2"]
+    fp = FaithfulPupil(n, n, size=size, pad=pad, wavelengths=list(lams), slots=2, workers=workers)
+
+    def ev():
+        return torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
+    rows = []
+    try:
+        for i in range(reps + 1):
+            if i == 1:
+                LIBM.check(L.akb_gd_patch_timing(1))
+            e_fin, e_psf, e_post = ev(), ev(), ev()
+            t = fp.begin(d2[1], d2[2], w2)
+            fp.finish(t, events=e_fin, psf_events=e_psf, post_events=e_post)
+            t.check()
+            torch.cuda.synchronize()
+            if i >= 1:
+                rows.append({"finish": e_fin[0].elapsed_time(e_fin[1]), "psf": e_psf[0].elapsed_time(e_psf[1]),
+                             "post": e_post[0].elapsed_time(e_post[1])})
+        LIBM.check(L.akb_gd_patch_timing(0))
+        bms = (ctypes.c_float * 64)()
+        nb = L.akb_gd_band_times(bms, 64)
+        pms = (ctypes.c_float * 64)()
+        npch = L.akb_gd_patch_times(pms, None, 64)
+        if nb < 0 or npch < 0:
+            LIBM.check(min(nb, npch))
+        pockets = list(fp.pocket_ms[1:])
+    finally:
+        fp.close()
+    del rw, out, d2, w2, fp
+    torch.cuda.empty_cache()
+
+    def med(v):
+        v = sorted(v)
+        return v[len(v) // 2] if v else None
+
+    band, patch = med(list(bms[:nb])), med(list(pms[:npch]))
+    post, psf, fin = med([r["post"] for r in rows]), med([r["psf"] for r in rows]), med([r["finish"] for r in rows])
+    return {"lattice": f"{n}^2 (configs[3]'s 1e8 rays, one GPU)", "runs": len(rows),
+            "rank0_tail_ms": band + post + psf,
+            "band_iteration_ms": band, "post_ms": post, "psf_ms": psf,
+            "finish_ms": fin, "patches_ms": patch, "finish_minus_patches_ms": fin - patch,
+            "pocket_job_host_ms": med(pockets), "pocket_workers": workers,
+            "what": "rank0_tail_ms = the band owner's device-only work per run (band iteration + post + PSF), "
+                    "alone on the GPU; finish_minus_patches_ms also holds the claims and the evaluation every "
+                    "rank shares; the pocket job runs on the host beside the passes (pocket_job_host_ms / "
+                    "pocket_workers per run of throughput)"}
 
 
 def stage_api(rw, geom, dev, reps=5):
@@ -550,7 +660,23 @@ def main():
         args.faithful_lag = 3 if world == 1 else 6
     fp = None
     tickets = []
-    finished = []  # every finished run's ticket: its error words are checked after the timed region
+    finished = []  # finished runs' tickets whose error words are still to be checked
+    checked = {"runs": 0, "guard_trips": 0}
+
+    def check_finished(block):
+        """Each finished run's own error words (the reference's raises): those whose device work is
+        done (block False: never waits - the timed steps' form), or all of them (block True). A cone
+        guard trip (the cone solve's estimate over its bar: FaithfulPupil.run would re-form that map
+        from the converged gradients) is counted, not raised; any other error raises."""
+        from akbraytracing_amd.griddata import ConeNotConverged
+        while finished and (block or finished[0].done is None or finished[0].done.query()):
+            t = finished.pop(0)
+            try:
+                fp.check(t) if world > 1 else t.check()
+            except ConeNotConverged:
+                checked["guard_trips"] += 1
+            checked["runs"] += 1
+
     fp_events = []
     if faithful and world == 1:
         from akbraytracing_amd.faithful import FaithfulPupil
@@ -596,6 +722,8 @@ def main():
                 t = tickets.pop(0)
                 fp.finish(t, stream=bs, events=ev, psf_events=pe)
                 finished.append(t)
+                if len(finished) > 1024:  # (the error log keeps 8192 runs: check the ones already done)
+                    check_finished(False)
                 if timed:
                     fp_events.append(("finish", ev[0], ev[1]))
                 if pe is not None:
@@ -640,15 +768,18 @@ def main():
         else:
             fronts.append(rw.launch_front(overlap=(lambda: back(timed)) if fronts else None, **kw))
 
+    from akbraytracing_amd import device as DEVM
+
     def timed_steps(k):
         comm.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         hm = []
         for _ in range(k):
-            h0 = time.perf_counter()
+            h0, w0 = time.perf_counter(), DEVM.host_wait_s()
             step(True)
-            hm.append((time.perf_counter() - h0) * 1e3)
+            # (host time issuing the step, of it blocked on events / the pocket job)
+            hm.append(((time.perf_counter() - h0) * 1e3, (DEVM.host_wait_s() - w0) * 1e3))
         torch.cuda.synchronize()
         comm.barrier()
         return time.perf_counter() - t0, hm
@@ -677,6 +808,7 @@ def main():
         t = comm.allreduce_max(torch.tensor([el0], dtype=torch.float64, device=dev))
         no_ramp_ms = float(t.item()) / args.steps * 1e3
         rw.kernel_events = None
+        rw.pass1_events = None
         fp_events.clear()
         psf_events.clear()
 
@@ -696,6 +828,7 @@ def main():
     for _ in range(args.warmup):
         step(False)
     rw.kernel_events = []
+    rw.pass1_events = []
     fp_events.clear()
     psf_events.clear()
     # host_ms: host time spent issuing each step (its waits included): is the host the limit?
@@ -717,7 +850,7 @@ def main():
             K = fp.sweeps
             W = 2 * K + 4
             S = next(s2 for s2 in range((K + 1) // 2, K + 1)
-                     if (((W - 2) ** 2 + 63) // 64 * 64) + (W - 2 * s2 - 2) ** 2 <= 1020)
+                     if (W - 2) ** 2 + (W - 2 * s2 - 2) ** 2 + 4 <= 1024)
             patch = faithful_roofline(list(pms[:k]), int(pcells[k - 1]), K, S)
             ph = (ctypes.c_ulonglong * 10)()
             LIBM.check(LIBM.lib().akb_gd_patch_phases(ph))
@@ -739,9 +872,8 @@ def main():
     torch.cuda.synchronize()
     faithful_checked = None
     if faithful:  # every run's own error words (the reference's raises), read now that nothing waits on them
-        for t in finished:
-            fp.check(t) if world > 1 else t.check()
-        faithful_checked = len(finished)
+        check_finished(True)
+        faithful_checked = checked["runs"]
     psf_alone_ms = psf_device_ms = None
     if rank == 0:  # the PSF's own wall time, nothing beside it (the last pupil: rw.pupil is collective)
         opd, pitch = (fp.post["opd"], None) if faithful else state["pupil"]
@@ -826,11 +958,30 @@ def main():
     if world == 1 and not args.no_extras:
         stage = stage_api(rw, geom, dev)
 
+    # N > 1: every rank's median faithful finish (device time on its back stream, in the timed steps):
+    # rank 0's excess over the others is the band owner's tail inside the step (rank0_tail below)
+    tail_in_step = None
+    if world > 1 and faithful:
+        mine = sorted(a.elapsed_time(b) for k, a, b in fp_events if k == "finish")
+        v = torch.zeros(world, dtype=torch.float64, device=dev)
+        v[rank] = mine[len(mine) // 2] if mine else float("nan")
+        v = comm.allreduce_sums(v).cpu().numpy()
+        others = sorted(float(x) for x in v[1:])
+        tail_in_step = {"rank0_finish_ms": float(v[0]), "other_ranks_finish_ms_median": others[len(others) // 2],
+                        "other_ranks_finish_ms_max": others[-1],
+                        "rank0_tail_ms": float(v[0]) - others[len(others) // 2],
+                        "what": "median device time of a faithful finish per rank in the timed steps (HIP events "
+                                "on its back stream, sharing the GPU with its passes); rank 0 adds the band "
+                                "iteration, the post and the PSF"}
+
     if rank != 0:
         return
     k_ms = [a.elapsed_time(b) for a, b in rw.kernel_events] if rw.kernel_events else [float('nan')]
     k_avg = sum(k_ms) / len(k_ms)
     psf_ms = sum(a.elapsed_time(b) for a, b in psf_events) / max(len(psf_events), 1)
+    # pass 1 (fused with run k-2's tilt and run k-3's OPD at --fuse 2): its own HIP events
+    p1 = [(a.elapsed_time(b), ft, fo) for a, b, ft, fo in (rw.pass1_events or [])]
+    roof_p1 = pass1_roofline(p1, rw.n_local, read_profile()[0] if args.config != "c2" else {}, args.fuse)
     # the faithful chain's device time per step on the back stream (cell pass + finish), and the
     # finishes alone (griddata, plane correction, psf_calc, PSF), sharing the GPU with the passes
     fp_begin = [a.elapsed_time(b) for k, a, b in fp_events if k == "begin"]
@@ -889,7 +1040,13 @@ def main():
                                      len(lams) > 1 else ""),
             "parallelism": f"ray-row shards x{world}",
         },
-        "host_issue_ms_per_step": sorted(host_ms)[len(host_ms) // 2],
+        # the host's share of a step (medians over the timed steps): its whole time per step, the part
+        # blocked on the device (event waits) or on the pocket workers, and the rest - the host's own
+        # issue cost (launch calls, the resample, Python). A step time near host_pure_issue would mean
+        # the host bounds the step; near the waits' sum, the device does
+        "host_issue_ms_per_step": sorted(h for h, _ in host_ms)[len(host_ms) // 2],
+        "host_wait_ms_per_step": sorted(w for _, w in host_ms)[len(host_ms) // 2],
+        "host_pure_issue_ms_per_step": sorted(h - w for h, w in host_ms)[len(host_ms) // 2],
         "pupil": ("faithful: each step's PSF from the reference's own pupil - griddata(cubic) of Wave2 on the "
                   f"{n}^2 hits (cone solve, {fp.K if world > 1 else fp.sweeps} Chebyshev sweeps), nanmean removal, "
                   "plane correction, psf_calc (rotation, rotate_with_nan, pad 16) - pipelined on the back stream "
@@ -902,6 +1059,7 @@ def main():
         # whose own error words were checked after it
         "faithful_finishes_timed": finishes_timed,
         "faithful_runs_checked": faithful_checked,
+        "cone_guard_trips": checked["guard_trips"] if faithful else None,
         "faithful_chain_ms": ((sum(fp_begin) + sum(fp_fin)) / max(len(fp_fin), 1)) if fp_fin else None,
         # the faithful chain's dominant kernel: the cone solve's patches (in the timed steps)
         "roofline_faithful": patch,
@@ -926,6 +1084,8 @@ def main():
             "traffic": pk.get("hbm_bytes_per_launch"),
             "algorithmic_bytes_per_launch": launch_bytes,
         },
+        # the fused pass 1 (the step's longest trace kernel at --fuse 2)
+        "roofline_pass1": roof_p1,
         # what bounds pass 2: VALU issue. Peak = intersections/s the chip would reach issuing one
         # wave-instruction per SIMD every 4 cycles at the profiled clock, with the profiled VALU
         # wave-instructions per intersection; frac = this run's rate over it
@@ -962,6 +1122,8 @@ def main():
         out["faithful_psf_chain_ms"] = faithful_dist_ms
         out["faithful_psf_route"] = (f"sharded over the {world} ray shards (faithful_dist.py): halo rows and the "
                                      "boundary band move, not the hits; one run alone, between barriers")
+    if tail_in_step is not None:
+        out["rank0_tail"] = tail_in_step
     if world > 1:
         out["note_multi_gpu"] = ("shards are aligned to numpy's 8192-element sum buffers and the ranks' buffer sums "
                                  "are chained in numpy's order: N ranks give one process's bits "
@@ -989,6 +1151,8 @@ def main():
             out["faithful_step"] = faithful_steps
         if stage is not None:
             out["stage_api"] = stage
+        if not args.no_extras and args.config == "c3":
+            out["rank0_tail"] = rank0_tail()
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, gdict)
     print(json.dumps(out), flush=True)

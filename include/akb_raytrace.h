@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define AKB_ABI_VERSION 15
+#define AKB_ABI_VERSION 16
 
 /* status codes */
 #define AKB_OK 0
@@ -540,6 +540,9 @@ int64_t akb_gd_cone_work_bytes(int nv, int nh, int mx, int my, int nvals);
  * cell count; returns how many (or a negative AKB error code). */
 int akb_gd_patch_timing(int enable);
 int akb_gd_patch_times(float* ms, int* cells, int max);
+/* the same record of the boundary band's sweeps: one duration (ms) per value set's band iteration
+ * (the K sweep launches and the guard's extra sweep, events around all of them) */
+int akb_gd_band_times(float* ms, int max);
 /* while timing (100 MHz wall-clock ticks, summed over the launches since akb_gd_patch_timing(1);
  * waits for the device), out[0..9]: the patch kernel's workgroup 0 in its steps' phases - the
  * setup (box in, vertex constants), the sweeps, the rest (corners, next box) - and its step count;
@@ -619,8 +622,14 @@ int akb_gd_part_finish_f64(double* out, const double* cnt, int64_t m, int nvals,
 #define AKB_SELFTEST_COLS 13
 int akb_selftest_arith_f64(const double* a, const double* b, int64_t n, double* out, void* stream);
 
-/* release cached rocFFT plans (also done at unload) */
+/* release the cached rocFFT plans (and rocFFT itself) and the device twiddle tables */
 void akb_psf_release_plans(void);
+
+/* release every device / pinned resource the library caches between calls - rocFFT plans and
+ * twiddle tables, the staged-argument ring's pinned buffers and events, the patch-timing events -
+ * while the HIP runtime is still up (bindings call it from an exit hook: the Python package's
+ * atexit). No HIP call is made for a cache that was never filled; the library stays usable */
+void akb_release_all(void);
 
 #ifdef __cplusplus
 }

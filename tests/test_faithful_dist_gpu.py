@@ -110,3 +110,57 @@ def test_sharded_faithful_pupil_equals_one_process(gpu, tmp_path, n, world):
     raised = [open(os.path.join(tmp_path, f"raised{r}.txt")).read() for r in range(world)]
     assert "non-finite" in raised[0]
     assert all(r == "none" for r in raised[1:])
+
+
+def guard_worker(rank, world, port, n, out_dir, sweeps):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), AKB_DIST_BACKEND="gloo")
+    import torch.distributed as dist
+    from akbraytracing_amd import dist as AD
+    from akbraytracing_amd.faithful_dist import ShardedFaithfulPupil
+    from akbraytracing_amd.wavefront import RayWave, Shard
+    AD.init_from_env()
+    try:
+        dev = torch.device("cuda", torch.cuda.current_device())
+        comm = AD.TorchComm(dev)
+        rw = RayWave(_geom(), n, shard=Shard.split(n, world, rank), comm=comm)
+        out = rw.run()
+        d2, w2 = out["detcenter2"], out["wave2"]
+        sp = ShardedFaithfulPupil(n, comm, size=128, slots=2, sweeps=sweeps)
+        r, _ = sp.run(d2[1], d2[2], w2)  # every rank returns: the guard's verdict is broadcast
+        if rank == 0:
+            assert r.get("converged")
+            save_result(os.path.join(out_dir, "guard.npz"), r)
+        else:
+            assert r is None
+        r2, _ = sp.run(d2[1], d2[2], w2)  # and the group is still in step for the next run
+        if rank == 0:
+            save_result(os.path.join(out_dir, "guard2.npz"), r2)
+        with open(os.path.join(out_dir, f"guard{rank}.txt"), "w") as f:
+            f.write("ok")
+        sp.close()
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_cone_guard_trip_falls_back_on_every_rank(gpu, tmp_path):
+    """A cone solve of 3 sweeps trips the guard on the band owner: the verdict is
+    broadcast, the ranks' hits meet on the band owner, which forms the map from the converged
+    gradients - FaithfulPupil.run's fallback, bit for bit - and every rank returns normally and
+    runs the next run's collectives."""
+    from akbraytracing_amd.faithful import FaithfulPupil
+    from akbraytracing_amd.wavefront import RayWave
+    n, world = 1001, 3
+    out = RayWave(_geom(), n).run()
+    fp = FaithfulPupil(n, n, slots=2, sweeps=3)
+    want = fp.run(out["detcenter2"][1], out["detcenter2"][2], out["wave2"])
+    assert want.get("converged")
+    want = {k: want[k].clone() for k in KEYS}
+    torch.cuda.synchronize()
+    fp.close()
+    mp.start_processes(guard_worker, args=(world, _free_port(), n, str(tmp_path), 3), nprocs=world, join=True,
+                       start_method="spawn")
+    assert all(open(os.path.join(tmp_path, f"guard{r}.txt")).read() == "ok" for r in range(world))
+    assert_same(os.path.join(tmp_path, "guard.npz"), want)
+    assert_same(os.path.join(tmp_path, "guard2.npz"), want)

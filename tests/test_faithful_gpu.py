@@ -166,3 +166,57 @@ def test_cone_guard_on_the_cycled_systems(gpu):
     r = fp.run(y, z, w)
     assert r.get("converged") and np.nanmax(np.abs(r["map"].cpu().numpy() - ref)) <= 1e-6 * rng_
     fp.close()
+
+
+# The moves the reference's alignment loops sweep (Legendrealignment calls, AKB_raytrace_20250312.py:
+# 14664-14851; the loops themselves :13853-14043): params indices moved together, and the widest
+# range each is swept over
+ALIGN_MOVES = [((8, 20), 2e-3), ((10, 22), 1e-3), ((12, 24), 2e-3), ((9, 21), 1e-5), ((2, 14), 2e-5),
+               ((2,), 1e-4), ((3,), 1e-5), ((4,), 1e-4), ((5,), 1e-6), ((7,), 1e-6), ((10,), 1e-5), ((11,), 1e-4),
+               ((12,), 1e-5), ((14,), 1e-5), ((15,), 1e-5), ((16,), 1e-5), ((17,), 1e-5), ((19,), 1e-6),
+               ((20,), 1e-4), ((21,), 1e-4), ((22,), 1e-4), ((23,), 1e-4), ((24,), 1e-5)]
+
+
+@pytest.mark.slow
+def test_cone_guard_on_drawn_misalignments(gpu):
+    """the guard's value-error estimate bounds the actual error of the 12-sweep map
+    (against the converged gradients on the same axes) on 50 systems drawn from the misalignments the
+    reference's alignment loops sweep: each system 1-3 of ALIGN_MOVES, each uniform over its range,
+    built by geometry.build_akb (the reference's plot_result_debug system) at 1001^2. A system the
+    reference could not trace (np.inf) or whose lattice the device refuses is redrawn and counted."""
+    from akbraytracing_amd import _lib
+    from akbraytracing_amd import geometry as G
+    from akbraytracing_amd.driver import ray_wave_conditions
+    from akbraytracing_amd.griddata import CONE_GUARD
+    from akbraytracing_amd.wavefront import SystemGeometry
+    rng = np.random.default_rng(20260618)
+    defocus_wave, _ = ray_wave_conditions(True)
+    done, skipped, trips, ratios = 0, 0, 0, []
+    while done < 50:
+        assert skipped <= 50, "too many drawn systems refused"
+        params = np.zeros(26)
+        for k in rng.choice(len(ALIGN_MOVES), size=int(rng.integers(1, 4)), replace=False):
+            idx, span = ALIGN_MOVES[k]
+            params[list(idx)] += rng.uniform(-span, span)
+        b = G.build_akb(params)
+        if not isinstance(b, dict):
+            skipped += 1
+            continue
+        det2 = np.zeros(10)
+        det2[6] = 1
+        det2[9] = -(np.float64(b["s2f_middle"]) + np.float64(b["defocus"]) + defocus_wave)
+        geom = SystemGeometry.from_dict(dict(b, det2=[float(x) for x in det2], defocus_wave_m=defocus_wave))
+        try:
+            fp, t, got, est, ref, rng_, _ = _guard_case(geom, 1001)
+        except (_lib.AKBError, ValueError):  # a ray missed, or a folded lattice: no pupil to grid
+            skipped += 1
+            continue
+        fp.close()
+        assert np.array_equal(np.isnan(got), np.isnan(ref))
+        err = float(np.nanmax(np.abs(got - ref)))
+        assert err <= est, (params.tolist(), err, est)
+        ratios.append(est / err if err > 0 else np.inf)
+        trips += int(not (est <= CONE_GUARD * rng_))
+        done += 1
+    print(f"{done} drawn systems ({skipped} redrawn): estimate / actual error min {min(ratios):.2f}, "
+          f"median {np.median(ratios):.2f}; guard trips {trips}")
