@@ -20,7 +20,7 @@ c_int = ctypes.c_int
 c_dbl = ctypes.c_double
 c_vp = ctypes.c_void_p
 MAX_MIRRORS = 7
-ABI_VERSION = 16
+ABI_VERSION = 17
 
 FLAG_MISS = 0x1
 FLAG_ZERO_NORMAL = 0x2
@@ -31,6 +31,7 @@ FLAG_CHAIN_DIR = 1 << 28
 # every symbol the header declares (tests check the library exports all of them)
 EXPORTS = [
     "akb_last_error", "akb_abi_version", "akb_sources_hash", "akb_device_count",
+    "akb_stream_create_reserved", "akb_stream_destroy",
     "akb_isect_f64", "akb_normal_f64", "akb_reflect_f64", "akb_normalize_f64", "akb_plane_isect_f64",
     "akb_seglen_f64", "akb_rotate_f64", "akb_fill_nan_f64",
     "akb_trace_chain_f64", "akb_chain_desc_size", "akb_tilt_opd_f64", "akb_tilt_params_f64",
@@ -103,6 +104,8 @@ def _declare(L):
         "akb_abi_version": ([], c_int),
         "akb_sources_hash": ([], ctypes.c_char_p),
         "akb_device_count": ([], c_int),
+        "akb_stream_create_reserved": ([c_int, c_vp], c_int),
+        "akb_stream_destroy": ([c_vp], c_int),
         "akb_isect_f64": ([c_vp] + v3 + v3 + [c_int, c_i64, c_vp, c_i64, c_vp, c_vp], c_int),
         "akb_normal_f64": ([c_vp] + v3 + [c_i64, c_vp, c_i64, c_int, c_vp, c_vp], c_int),
         "akb_reflect_f64": (v3 + v3 + [c_i64, c_vp, c_i64, c_int, c_vp, c_vp], c_int),

@@ -13,6 +13,16 @@
 
 #include "../../include/akb_raytrace.h"
 
+// Wave priority of the latency-bound kernels (the faithful chain's, the trace's sums and tilt
+// parameters, the PSF): in a pipelined step they run on the critical path while the trace passes'
+// FP64-bound waves share their SIMDs, so each of their waves issues first (s_setprio); the passes,
+// throughput work with slack in the step, take the remaining issue slots.
+#ifndef AKB_NO_CHAIN_PRIO
+#define AKB_CHAIN_PRIORITY() __builtin_amdgcn_s_setprio(3)
+#else
+#define AKB_CHAIN_PRIORITY() ((void)0)
+#endif
+
 namespace akb {
 
 // thread-local last error, surfaced by akb_last_error()

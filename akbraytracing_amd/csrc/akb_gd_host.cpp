@@ -304,8 +304,7 @@ int akb_gd_pockets(const double* rx, const double* ry, int nv, int nh, int cap, 
     // the pockets, one per hull edge that skips ring points. They are independent (disjoint chains
     // and ring edges); triangle ids and chord order are those of one LIFO walk over all of them
     // (the last hull edge's pocket first). One thread walks them in that order (a call is one job of
-    // the caller's pool); AKB_GD_POCKET_THREADS=1 gives the large ones threads of their own, with
-    // the same result
+    // the caller's pool: FaithfulPupil's workers run the runs' calls side by side)
     std::vector<Pocket>& pockets = w.pockets;
     pockets.clear();
     for (size_t k = 0; k < hv.size(); ++k) {

@@ -442,6 +442,7 @@ __device__ __forceinline__ void strip_claims(const Targets& t, int* owner, bool 
 template <bool kClaims = false>
 __global__ void __launch_bounds__(kStripThreads) k_gd_cells_strip(Grid g, uint8_t* diag, double tol, unsigned* flags,
                                                                   int seg_rows, TileClaims tc = {}) {
+    AKB_CHAIN_PRIORITY();
     const int r_lo = g.row0, r_hi = g.row1 < 0 ? g.nv - 1 : g.row1;  // window cell rows [r_lo, r_hi)
     const int nstrip = (g.nh - 1 + kStripCells - 1) / kStripCells;
     const int nseg = (r_hi - r_lo + seg_rows - 1) / seg_rows;
@@ -547,6 +548,7 @@ __global__ void __launch_bounds__(kStripThreads) k_gd_cells_strip(Grid g, uint8_
 
 // ring positions -> coordinates, for the host pocket builder (bit 5 of flags: a non-finite one)
 __global__ void k_gd_ring(Grid g, double* rx, double* ry, unsigned* flags) {
+    AKB_CHAIN_PRIORITY();
     const int64_t a = g.nh - 1, b = g.nv - 1, L = 2 * a + 2 * b;
     for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < L; r += (int64_t)gridDim.x * blockDim.x) {
         int64_t v;
@@ -562,6 +564,7 @@ __global__ void k_gd_ring(Grid g, double* rx, double* ry, unsigned* flags) {
 
 // the pockets against the triangles they border: every pocket edge locally Delaunay (bit 1)
 __global__ void k_gd_check_pockets(Grid g, double tol, unsigned* flags) {
+    AKB_CHAIN_PRIORITY();
     const int64_t nc2 = 2 * ncells(g);
     for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < g.npock; j += (int64_t)gridDim.x * blockDim.x) {
         const Tri T = tri_verts(g, nc2 + j);
@@ -1199,7 +1202,7 @@ constexpr int kConeBox = 2 * kConeMaxK + 4;  // the largest box side: it fits th
 // the boundary band: vertices with min(iv, ih, nv - 1 - iv, nh - 1 - ih) <= D, as four regions -
 // the top rows [0, rt), the bottom rows [rb, nv), and between them the left columns [0, cl) and the
 // right columns [cr, nh) - cut into kBandTR x kBandTC tiles (every band vertex in one tile)
-constexpr int kBandTR = 16, kBandTC = 32;  // (33 KB of LDS a tile: four workgroups a CU, 128 VGPRs a wave)
+constexpr int kBandTR = 16, kBandTC = 32;  // (33 KB of LDS a tile, 126 VGPRs: a workgroup fits beside the passes')
 struct BandTiles {
     int D, rt, rb, cl, cr;
     int ncb, top_rb, bot_rb, mid_rb, lcb, rcb;  // column blocks (top / bottom), row blocks, side column blocks
@@ -1397,6 +1400,7 @@ __device__ __forceinline__ void cone_ring_vertex(const Grid& g, const ConeBand& 
 }
 
 __global__ void k_gd_chord_slots(Grid g, int32_t* slots, int64_t L) {
+    AKB_CHAIN_PRIORITY();
     for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < L; r += (int64_t)gridDim.x * blockDim.x) {
         const int32_t k0 = g.xptr[r], cnt = g.xptr[r + 1] - k0;
         int32_t* sr = slots + r * kChordSlots;
@@ -1433,6 +1437,7 @@ inline unsigned band_ring_wgs(int64_t L) { return (unsigned)((L + kBandRingPer -
 inline unsigned band_grid(const BandTiles& bt, int64_t L) { return band_ring_wgs(L) + (unsigned)bt.total; }
 
 __global__ void __launch_bounds__(kBandThreads) __attribute__((amdgpu_waves_per_eu(4))) k_gd_cone_band(Grid g, BandTiles bt, ConeBand a) {
+    AKB_CHAIN_PRIORITY();
     if (!*a.needed) return;
     const unsigned long long t0 = a.clk ? wall_clock64() : 0;
     constexpr int HR = kBandTR + 2, HC = kBandTC + 2, HN = HR * HC, CC = kBandTC + 1;
@@ -1689,6 +1694,7 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch(Grid g, ConePatch a, int
     __shared__ unsigned sori[2];   // per box set: bit 0 some cell takes diagonal 0, bit 1 some diagonal 1
     __shared__ double somg[kConeMaxK + 1];  // sweep j's Chebyshev weight
     __shared__ double shc[2][4];   // per iterate pair: the corners' longest cell side or diagonal
+    __shared__ double smax[2];     // the corners' running maxima over this workgroup's cells: change, estimate
     const int K = a.K, W = 2 * K + 4;
     const int t = threadIdx.x;
     const int N1 = (W - 2) * (W - 2), N2 = (W - 2 * S - 2) * (W - 2 * S - 2), T0 = N1 + N2;
@@ -1711,7 +1717,10 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch(Grid g, ConePatch a, int
         const int iv0 = (int)(cell / (nh - 1)), ih0 = (int)(cell - (int64_t)iv0 * (nh - 1));
         scell[i] = make_int2(iv0 - (K + 1), ih0 - (K + 1));
     }
-    if (t < 2) sori[t] = 0u;
+    if (t < 2) {
+        sori[t] = 0u;
+        smax[t] = 0.0;
+    }
     if (t <= kConeMaxK) somg[t] = a.st[t].omega;
     __syncthreads();
     // the box loaders' row and column: re-formed where used (from an opaque copy of t), so that their
@@ -1735,9 +1744,6 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch(Grid g, ConePatch a, int
         sxyf[0][2][lr * P + lc] = gf_[q];
         if (cell_loader) pd = gd_[(int64_t)(o.x + lr) * (nh - 1) + (o.y + lc)];
     }
-    // the corners' running maxima over this workgroup's cells (threads T0 .. T0 + 3), one atomic each
-    // at the end
-    double cmax = 0.0, emax = 0.0;
     constexpr int off[8] = {-1, 1, -P, P, -P - 1, -P + 1, P - 1, P + 1};
     const bool clk = a.clk && blockIdx.x == 0 && __builtin_amdgcn_readfirstlane(t >> 6) == 0;  // wave 0 (scalar)
     unsigned long long c_setup = 0, c_sweeps = 0, c_rest = 0, c0 = clk ? wall_clock64() : 0, c1 = 0;
@@ -1772,8 +1778,10 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch(Grid g, ConePatch a, int
             const int64_t i = (int64_t)sout[q][2];
             a.gout[2 * i] = sout[q][0];
             a.gout[2 * i + 1] = sout[q][1];
-            cmax = fmax(cmax, sout[q][3]);
-            emax = nan_max(emax, cell_est(sout));
+            if (q == 0) {  // the running maxima (in LDS: no register held across the steps)
+                smax[0] = fmax(fmax(smax[0], fmax(sout[0][3], sout[1][3])), fmax(sout[2][3], sout[3][3]));
+                smax[1] = nan_max(smax[1], cell_est(sout));
+            }
         }
         const bool fresh = role == 2 || role == s1;  // this step: cell p (sweeps 1 .. S), else cell p - 1
         const bool act = dep >= 1 && (fresh ? p < my : p >= 1);
@@ -1787,23 +1795,13 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch(Grid g, ConePatch a, int
                                 (sdd[b - 1] == 1 ? 0x40u : 0u) | (sdd[b] == 0 ? 0x80u : 0u);
             const double xi = sx[b], yi = sy[b];
             const double fi[1] = {sf[b]}, zero[1] = {0.0};
-            // a corner (the corners are (K+1 .. K+2)^2 of the box) also takes the cell's two sides and
-            // its diagonal there: the slots toward the cell's other corners
-            const bool up = r == K + 1, rt = c == K + 1;
-            const unsigned cm = dep == K + 1 ? (up ? 0x08u : 0x04u) | (rt ? 0x02u : 0x01u) |
-                                                   (up ? (rt ? 0x80u : 0x40u) : (rt ? 0x20u : 0x10u))
-                                             : 0u;
-            double h2 = 0.0;
             GradAcc<1> A;
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 mxx[k] = mxy[k] = myy[k] = 0.0;
-                if (!((em | cm) & (1u << k))) continue;
-                const int j = b + off[k];
-                const double ex = sx[j] - xi, ey = sy[j] - yi;
-                if (cm & (1u << k)) h2 = fmax(h2, ex * ex + ey * ey);
                 if (!(em & (1u << k))) continue;
-                const EdgeG e = edge_geom(ex, ey);
+                const int j = b + off[k];
+                const EdgeG e = edge_geom(sx[j] - xi, sy[j] - yi);
                 const double fj[1] = {sf[j]};
                 acc_edge<1>(A, e, fi, fj, zero, zero);  // (its S part is not used: the sweeps form S)
                 mxx[k] = e.mxx;
@@ -1811,7 +1809,18 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch(Grid g, ConePatch a, int
                 myy[k] = e.myy;
             }
             kc = vertex_consts<1>(A, 0);
-            if (cm) shc[s1][role == 0 ? t : t - N2] = sqrt(h2);
+            if (dep == K + 1) {  // a corner (the corners are (K+1 .. K+2)^2 of the box): the cell's two
+                                 // sides and its diagonal there, for the value-error estimate
+                int tb = t;
+                asm volatile("" : "+v"(tb));  // (its addresses formed here, not held across the step)
+                const int bq = b + (tb - t);
+                const int dr = r == K + 1 ? P : -P, dc = c == K + 1 ? 1 : -1;
+                auto l2 = [&](int j) {
+                    const double ex = sx[j] - xi, ey = sy[j] - yi;
+                    return ex * ex + ey * ey;
+                };
+                shc[s1][role == 0 ? t : t - N2] = sqrt(fmax(fmax(l2(bq + dr), l2(bq + dc)), l2(bq + dr + dc)));
+            }
         }
         // cell p + 1's box point through registers: issued after the setup (whose temporaries then
         // are dead), written to LDS after the sweeps, which hide its latency
@@ -1852,8 +1861,10 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch(Grid g, ConePatch a, int
                 }
                 double y0, y1;
                 jacobi_y(kc, s0, s1v, y0, y1);
-                gg[out][b] = j == 1 ? make_double2(y0, y1)
-                                    : make_double2(__builtin_fma(om, y0 - pv.x, pv.x), __builtin_fma(om, y1 - pv.y, pv.y));
+                if (j == 1)  // (a branch: only the first sweep's step takes it, and then the whole wave)
+                    gg[out][b] = make_double2(y0, y1);
+                else
+                    gg[out][b] = make_double2(__builtin_fma(om, y0 - pv.x, pv.x), __builtin_fma(om, y1 - pv.y, pv.y));
             }
             asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         }
@@ -1894,12 +1905,15 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch(Grid g, ConePatch a, int
                 const int64_t i = (int64_t)sout[q][2];
                 a.gout[2 * i] = sout[q][0];
                 a.gout[2 * i + 1] = sout[q][1];
-                cmax = fmax(cmax, sout[q][3]);
-                emax = nan_max(emax, cell_est(sout));
+                if (q == 0) {
+                    smax[0] = fmax(fmax(smax[0], fmax(sout[0][3], sout[1][3])), fmax(sout[2][3], sout[3][3]));
+                    smax[1] = nan_max(smax[1], cell_est(sout));
+                }
             }
         }
     }
-    if (role == 3 && t < T0 + 4) {
+    if (t == T0) {
+        const double cmax = smax[0], emax = smax[1];
         if (a.chg && cmax > 0) atomicMax(a.chg, (unsigned long long)__double_as_longlong(cmax));
         // a NaN estimate as +inf (ordered bits: the guard sees an estimate above any bar)
         if (a.est && (emax > 0 || emax != emax))
@@ -1916,6 +1930,7 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch(Grid g, ConePatch a, int
 // targets -> interior target cells (the patch list) and whether any target needs the band
 __global__ void __launch_bounds__(kBlock) k_gd_cone_targets(Grid g, const int* __restrict__ owner, int64_t m, int K,
                                                              int64_t* cells, int* count, int* band) {
+    AKB_CHAIN_PRIORITY();
     const int64_t nc2 = 2 * ncells(g);
     for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < m; t += (int64_t)gridDim.x * blockDim.x) {
         const int o = owner[t];
@@ -1941,6 +1956,7 @@ constexpr int kAxesLds = 2048;      // axes up to this long are summed from LDS
 __global__ void __launch_bounds__(kAxesThreads) k_gd_axes(const double* __restrict__ rx, const double* __restrict__ ry,
                                                           int64_t L, int mx, int my, double* gx, double* gy,
                                                           double* ext) {
+    AKB_CHAIN_PRIORITY();
     __shared__ double red[4][kAxesThreads / 64];
     double lo_x = INFINITY, hi_x = -INFINITY, lo_y = INFINITY, hi_y = -INFINITY;
     // the ring's points in batches of 16 loads per thread in flight (one memory latency per batch,
@@ -2039,6 +2055,7 @@ __device__ __forceinline__ bool cone_interior(const Grid& g, int o, int K, int64
 __global__ void __launch_bounds__(kBlock) k_gd_cone_assign(Grid g, const int* __restrict__ owner, int64_t m, int K,
                                                             int64_t own0, int64_t own1, int band_on, int64_t* cells,
                                                             int* count, int* band, uint8_t* assigned) {
+    AKB_CHAIN_PRIORITY();
     for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < m; t += (int64_t)gridDim.x * blockDim.x) {
         const int o = owner[t];
         uint8_t mine = 0;
@@ -2061,6 +2078,7 @@ __global__ void __launch_bounds__(kBlock) k_gd_cone_assign(Grid g, const int* __
 
 // cell triangles (ids < 2 * ncells): one thread each, a box of a few targets
 __global__ void __launch_bounds__(kBlock) k_gd_claim(Grid g, Targets t, int* owner) {
+    AKB_CHAIN_PRIORITY();
     const int64_t ntri = 2 * ncells(g);
     for (int64_t id = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; id < ntri; id += (int64_t)gridDim.x * blockDim.x) {
         const Tri T = tri_verts(g, id);
@@ -2130,6 +2148,7 @@ __device__ __forceinline__ void claim_cell(const Grid& g, const Targets& t, int6
 }
 
 __global__ void __launch_bounds__(kBlock) k_gd_claim_cells(Grid g, Targets t, int* owner) {
+    AKB_CHAIN_PRIORITY();
     const bool uniform = axes_uniform(t);
     const double inv_dx = inv_step(t.gx, t.mx), inv_dy = inv_step(t.gy, t.my);
     for (int64_t c = win_cell0(g) + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < win_cell1(g);
@@ -2143,6 +2162,7 @@ __global__ void __launch_bounds__(kBlock) k_gd_claim_cells(Grid g, Targets t, in
 // sparse against the cells (a 128^2 grid over 1e7 cells: ~85 % of the blocks hold none), so most
 // cells are settled by one 81-vertex load per block. Same claims as k_gd_claim_cells.
 __global__ void __launch_bounds__(kBlock) k_gd_claim_blocks(Grid g, Targets t, int* owner) {
+    AKB_CHAIN_PRIORITY();
     const bool uniform = axes_uniform(t);
     const double inv_dx = inv_step(t.gx, t.mx), inv_dy = inv_step(t.gy, t.my);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
@@ -2206,6 +2226,7 @@ __device__ __forceinline__ void claim_block_dims(const Grid& g, int64_t& nblk, i
 }
 
 __global__ void __launch_bounds__(kBlock) k_gd_claim_scan(Grid g, Targets t, uint8_t* hit) {
+    AKB_CHAIN_PRIORITY();
     const bool uniform = axes_uniform(t);
     const double inv_dx = inv_step(t.gx, t.mx), inv_dy = inv_step(t.gy, t.my);
     int64_t nblk;
@@ -2257,6 +2278,7 @@ __global__ void __launch_bounds__(kBlock) k_gd_claim_scan(Grid g, Targets t, uin
 
 __global__ void __launch_bounds__(kBlock, 5) k_gd_claim_hit(Grid g, Targets t, const uint8_t* __restrict__ hit,
                                                          int* owner) {
+    AKB_CHAIN_PRIORITY();
     const bool uniform = axes_uniform(t);
     const double inv_dx = inv_step(t.gx, t.mx), inv_dy = inv_step(t.gy, t.my);
     // the target axes in LDS: the claims' index scans walk them one dependent load at a time
@@ -2289,6 +2311,7 @@ __global__ void __launch_bounds__(kBlock, 5) k_gd_claim_hit(Grid g, Targets t, c
 // threads idle on the common few-target boxes; a thread per triangle left the long slivers' boxes
 // to one lane each: 326 us against 28 at C3); the target axes in LDS for tri_box's binary searches
 __global__ void __launch_bounds__(kBlock) k_gd_claim_pockets(Grid g, Targets t, int* owner) {
+    AKB_CHAIN_PRIORITY();
     const int64_t nc2 = 2 * ncells(g);
     const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
     __shared__ double sax[2 * kClaimAxisLds];
@@ -2510,23 +2533,26 @@ __device__ __forceinline__ void band_target_est(const Grid& g, const BandEst& be
         const int64_t v = T.v[k];
         cmax = fmax(cmax, change_of(grad[2 * v], grad[2 * v + 1], be.y[2 * v], be.y[2 * v + 1]));
     }
-    emax = fmax(emax, 2.0 * fabs(clough_tocher(g, o, T, f, be.y, b) - v0));
+    emax = nan_max(emax, 2.0 * fabs(clough_tocher(g, o, T, f, be.y, b) - v0));  // (a NaN kept: refused)
 }
 
 __device__ __forceinline__ void band_est_store(const BandEst& be, double cmax, double emax) {
     for (int off = 32; off > 0; off >>= 1) {
         cmax = fmax(cmax, __shfl_down(cmax, off));
-        emax = fmax(emax, __shfl_down(emax, off));
+        emax = nan_max(emax, __shfl_down(emax, off));
     }
     if ((threadIdx.x & 63) == 0) {
         if (be.chg && cmax > 0) atomicMax(be.chg, (unsigned long long)__double_as_longlong(cmax));
-        if (be.est && emax > 0) atomicMax(be.est, (unsigned long long)__double_as_longlong(emax));
+        // a NaN estimate (a non-finite value at a band target) as +inf: above any bar
+        if (be.est && (emax > 0 || emax != emax))
+            atomicMax(be.est, (unsigned long long)__double_as_longlong(emax != emax ? HUGE_VAL : emax));
     }
 }
 
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) k_gd_eval(Grid g, Targets t, const int* __restrict__ owner,
                                                     const double* f, const double* grad, int nvals, double* out,
                                                     BandEst be = BandEst{nullptr, 0, nullptr, nullptr}) {
+    AKB_CHAIN_PRIORITY();
     const int64_t m = (int64_t)t.mx * t.my, n = (int64_t)g.nv * g.nh;
     double cmax = 0.0, emax = 0.0;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
@@ -2554,7 +2580,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
                         in.gx[k] = g2x[k];
                         in.gy[k] = g2y[k];
                     }
-                    emax = fmax(emax, 2.0 * fabs(ct_eval(in, b) - v0));
+                    emax = nan_max(emax, 2.0 * fabs(ct_eval(in, b) - v0));
                 }
                 continue;
             }
@@ -2574,6 +2600,7 @@ __global__ void __launch_bounds__(kBlock) k_gd_eval_part(Grid g, Targets t, cons
                                                          const uint8_t* __restrict__ assigned, const double* f,
                                                          const double* grad, int nvals, double* out, double* cnt,
                                                          BandEst be = BandEst{nullptr, 0, nullptr, nullptr}) {
+    AKB_CHAIN_PRIORITY();
     const int64_t m = (int64_t)t.mx * t.my, n = (int64_t)g.nv * g.nh;
     double cmax = 0.0, emax = 0.0;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
@@ -2596,12 +2623,14 @@ __global__ void __launch_bounds__(kBlock) k_gd_eval_part(Grid g, Targets t, cons
 
 // the assembled pieces: value where some rank formed it, NaN elsewhere (outside the hull)
 __global__ void k_gd_part_finish(double* out, const double* cnt, int64_t m, int nvals) {
+    AKB_CHAIN_PRIORITY();
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x)
         if (!(cnt[i] > 0))
             for (int v = 0; v < nvals; ++v) out[v * m + i] = __builtin_nan("");
 }
 
 __global__ void k_fill_i32(int* p, int64_t n, int v) {
+    AKB_CHAIN_PRIORITY();
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = v;
 }
 
@@ -2646,6 +2675,7 @@ constexpr int kPatchEvents = 1024;
 constexpr int kPatchClk = 10;  // the diagnostics words (akb_gd_patch_phases)
 struct PatchTimer {
     bool on = false, made = false;
+    bool band_clk = false;  // the band workgroups' clocks too (akb_gd_patch_timing(2): their atomics cost the step)
     hipEvent_t ev[kPatchEvents][2];
     const int* cnt[kPatchEvents];
     hipEvent_t bev[kPatchEvents][2];  // around each value set's band sweeps (the guard's extra sweep included)
@@ -2867,11 +2897,7 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
         // the boundary band, shrinking like the patches' squares: sweep j forms depth <= 2K + 3 - j,
         // whose neighbours (depth <= 2K + 4 - j) sweep j - 1 formed, so x_K is the global iteration's
         // to depth K + 3 >= every band target's corners (the first sweep reads x_0 = 0 only)
-#ifdef AKB_EXP_NOBAND  // (measurement only: the band's share of the step; results wrong)
-        if (false) {
-#else
         if (band_on) {
-#endif
             PatchTimer& bt0 = patch_timer();
             const int bslot = (int)(bt0.band_launches % kPatchEvents);
             if (bt0.on) (void)hipEventRecord(bt0.bev[bslot][0], s);
@@ -2885,7 +2911,7 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
                 const double* gin = j == 1 ? nullptr : gb[(j - 1) % 3];
                 const double* gprev = j >= 3 ? gb[(j + 1) % 3] : nullptr;
                 const BandTiles bt = band_tiles(g.nv, g.nh, 2 * K + 3 - j);
-                const ConeBand a{fv, gin, gprev, gb[j % 3], steps[j], band, patch_timer().on ? patch_timer().clk : nullptr,
+                const ConeBand a{fv, gin, gprev, gb[j % 3], steps[j], band, patch_timer().band_clk ? patch_timer().clk : nullptr,
                                  slots};
                 k_gd_cone_band<<<band_grid(bt, L), kBandThreads, 0, s>>>(g, bt, a);
                 if ((st = launch_status("k_gd_cone_band"))) return st;
@@ -2893,7 +2919,7 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
             if (d_change) {  // one more plain sweep, y from x_K to depth K + 2 (the band targets' corners)
                 const BandTiles bt = band_tiles(g.nv, g.nh, K + 2);
                 const ConeBand a{fv, gb[K % 3], nullptr, gb[(K + 1) % 3], ConeStep{0, 1.0}, band,
-                                 patch_timer().on ? patch_timer().clk : nullptr, slots};
+                                 patch_timer().band_clk ? patch_timer().clk : nullptr, slots};
                 k_gd_cone_band<<<band_grid(bt, L), kBandThreads, 0, s>>>(g, bt, a);
                 if ((st = launch_status("k_gd_cone_band"))) return st;
             }
@@ -2912,9 +2938,7 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
             (void)hipEventRecord(pt.ev[slot][0], s);
             pt.cnt[slot] = count;
         }
-#ifndef AKB_EXP_NOPATCH  // (measurement only: the patches' share of the step; results wrong)
         k_gd_cone_patch<<<pp, patch_threads(K, S), 0, s>>>(g, a, S);
-#endif
         if (pt.on) {
             (void)hipEventRecord(pt.ev[slot][1], s);
             ++pt.launches;
@@ -3100,6 +3124,7 @@ int akb_gd_patch_timing(int enable) {
         t.band_launches = 0;
     }
     t.on = enable != 0;
+    t.band_clk = enable == 2;
     return 0;
 }
 

@@ -192,6 +192,7 @@ __device__ __forceinline__ double2 cmul(double2 a, double2 b) {
 }
 
 __global__ void __launch_bounds__(kBlock) k_psf_twiddle(double2* W, int P) {
+    AKB_CHAIN_PRIORITY();
     for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < P; t += gridDim.x * blockDim.x) {
         double sn, cs;
         sincospi(2.0 * (double)t / (double)P, &sn, &cs);
@@ -681,6 +682,7 @@ constexpr double kBoundMarginSel = 1.0 + 0x1p-20;
 
 template <int N, int PAD, int MODE>
 __global__ void __launch_bounds__((LineThreads<N, PAD, MODE>::kThreads)) k_psf_line(PsfLineArgs A) {
+    AKB_CHAIN_PRIORITY();
     using S = LineShape<N, PAD>;
     constexpr int LPT = LineThreads<N, PAD, MODE>::kLanes, NT = LineThreads<N, PAD, MODE>::kThreads;
     using R = typename std::conditional<MODE == kLinePeak32, float, double>::type;

@@ -124,6 +124,7 @@ __global__ void k_rotate_cubic(RotArgs a) {
 // rotate_with_nan's interpolation after k_pupil_post: scipy.ndimage.rotate's matrix and offsets
 // from its parameter block (cos, sin, offsets at [13 .. 17), akb_raytrace.h)
 __global__ void k_rotate_post(const double* coef, int ny, int nx, const double* P, double* rotated, double* opd) {
+    AKB_CHAIN_PRIORITY();
     const RotArgs ra{coef, ny, nx, P[13], P[14], -P[14], P[13], P[15], P[16], rotated, opd};
     const int64_t total = (int64_t)ny * nx;
     for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < total; k += (int64_t)gridDim.x * blockDim.x)
@@ -758,6 +759,7 @@ __device__ void spline_line_reg(double* c, int n, int sub, unsigned long long* c
 constexpr int kSplineLanes = 8, kSplinePostThreads = kSplineLanes * kPostFuse;
 __global__ void __launch_bounds__(kSplinePostThreads) k_spline_post(double* __restrict__ coef, int ny, int nx,
                                                                      unsigned long long* clocks) {
+    AKB_CHAIN_PRIORITY();
     __shared__ double a[kPostFuse * (kPostFuse + 1)];
     const int64_t total = (int64_t)ny * nx;
     constexpr int pitch = kPostFuse + 1;
@@ -846,6 +848,7 @@ __device__ __noinline__ double post_leaf128(const double* smem, int o) {
 }
 
 __global__ void __launch_bounds__(kPostThreads) k_pupil_post(PostArgs a) {
+    AKB_CHAIN_PRIORITY();
     __shared__ double smem[kPostLds + kPostLds / 128];  // the map, then matrixWave2 - nanmean (when it fits)
     __shared__ PwTree trees[2];        // the nanmean's pairwise trees (waves 0 and 1)
     __shared__ double bufsum[8];

@@ -30,6 +30,7 @@ constexpr int kFinalTile = 4096;
 __global__ void __launch_bounds__(kPwThreads) k_pw_chunks(const double* __restrict__ x, int64_t ld, int nan_mask,
                                                           int part_ld, double* __restrict__ part,
                                                           long long* __restrict__ part_cnt) {
+    AKB_CHAIN_PRIORITY();
     __shared__ double s[(kPwBuf / kPwLeaf) * kPwStride];
     __shared__ double leafv[kPwBuf / kPwLeaf];
     __shared__ long long wcnt[kPwThreads / 64];
@@ -96,6 +97,7 @@ __global__ void __launch_bounds__(64) k_leaf_chunks(const double* __restrict__ l
                                                     const int* __restrict__ leaf_cnt, int64_t nleaves,
                                                     int part_ld, double* __restrict__ part,
                                                     long long* __restrict__ part_cnt) {
+    AKB_CHAIN_PRIORITY();
     const int q = blockIdx.y;
     const int c = blockIdx.x;
     const int lane = threadIdx.x;
@@ -127,6 +129,7 @@ __global__ void __launch_bounds__(kPwThreads) k_pw_final(const double* __restric
                                                          int64_t tail_ld, int tail_len, int nan_mask,
                                                          double* __restrict__ out, int64_t* __restrict__ cnt_out,
                                                          int tile) {
+    AKB_CHAIN_PRIORITY();
     extern __shared__ double dyn[];
     double* const t = dyn;
     double* const tl = dyn + tile;

@@ -913,6 +913,7 @@ constexpr int kFinTile = 512;    // buffer sums staged per LDS round and wave (2
 
 __global__ void __launch_bounds__(256) k_fin_buffers(akb_leaf_sink S, int64_t nfull, double* __restrict__ part,
                                                      long long* __restrict__ part_cnt) {
+    AKB_CHAIN_PRIORITY();
     extern __shared__ double tl[];  // the short buffer (its length in doubles)
     __shared__ PwTree T;
     const int q = blockIdx.y;
@@ -975,6 +976,7 @@ __global__ void __launch_bounds__(320) k_fin_params(akb_leaf_sink S, int64_t nfu
                                                     const long long* __restrict__ part_cnt, double* __restrict__ sum5,
                                                     int64_t* __restrict__ cnt5, double* __restrict__ P,
                                                     unsigned long long* keys, int32_t* clear, int nclear) {
+    AKB_CHAIN_PRIORITY();
     __shared__ double tile[5][kFinTile];
     __shared__ double s5[8];
     __shared__ int64_t c5[8];
@@ -1433,6 +1435,34 @@ int akb_device_count(void) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
     return n;
+}
+
+int akb_stream_create_reserved(int reserve, void** stream) {
+    clear_error();
+    AKB_REQUIRE(stream, "null pointer");
+    AKB_REQUIRE(reserve >= 0 && reserve <= 32 && reserve % 8 == 0, "reserve must be 0, 8, 16, 24 or 32");
+    int dev = 0, ncu = 0;
+    AKB_HIP_CHECK(hipGetDevice(&dev));
+    AKB_HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    AKB_REQUIRE(ncu >= 64 && ncu % 32 == 0, "CU count not a multiple of 32");
+    std::vector<uint32_t> mask((size_t)ncu / 32, 0xffffffffu);
+    // bit x*32 + x + 8k (x < 8, k < reserve/8): per XCD the same count whether the driver maps
+    // mask bits to XCDs in blocks of 32 or round-robin (bit % 8)
+    for (int x = 0; x < 8; ++x)
+        for (int k = 0; k < reserve / 8; ++k) {
+            const int b = x * 32 + x + 8 * k;
+            mask[b / 32] &= ~(1u << (b % 32));
+        }
+    hipStream_t st = nullptr;
+    AKB_HIP_CHECK(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
+    *stream = st;
+    return AKB_OK;
+}
+
+int akb_stream_destroy(void* stream) {
+    clear_error();
+    if (stream) AKB_HIP_CHECK(hipStreamDestroy((hipStream_t)stream));
+    return AKB_OK;
 }
 
 int akb_isect_f64(const double coeffs[10], const double* dir, int64_t dir_ld, int64_t dir_inc,
@@ -2018,11 +2048,15 @@ static int chain_tilt(const akb_chain_desc* d, const double* d_params, const dou
     const unsigned gs = (unsigned)(nseg < gcap ? nseg : gcap);
     hipStream_t s = (hipStream_t)stream;
     const OpdRows no{};
+    // 22 KB of dynamic LDS beside its 18.6 KB static: three pass-1 workgroups a CU (their VGPRs
+    // would allow four) leave every SIMD a wave of 128 VGPRs and 38 KB of LDS, where the faithful
+    // chain's 256-thread workgroups run beside the pass instead of waiting for it to drain a CU
+    constexpr size_t kPass1LdsPad = 22528;
 #define AKB_CT(W)                                                  \
     if (o)                                                         \
-        k_chain_tilt<W, true><<<gs, kBlock, 0, s>>>(a, b, *o);     \
+        k_chain_tilt<W, true><<<gs, kBlock, kPass1LdsPad, s>>>(a, b, *o);     \
     else                                                           \
-        k_chain_tilt<W, false><<<gs, kBlock, 0, s>>>(a, b, no);
+        k_chain_tilt<W, false><<<gs, kBlock, kPass1LdsPad, s>>>(a, b, no);
     AKB_CT(kChainWaves)
 #undef AKB_CT
     return launch_status("k_chain_tilt");

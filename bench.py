@@ -97,6 +97,10 @@ def parse():
                         "next step's FP64-bound pass 1 (0: behind it on one stream)")
     p.add_argument("--back-priority", type=int, default=0,
                    help="torch stream priority of the back stream (lower = higher priority; 0 = normal)")
+    p.add_argument("--reserve-cus", type=int, default=0,
+                   help="CUs (0, 8, 16, 24, 32: the same number on every XCD) the main stream's passes leave "
+                        "to the other streams (akb_stream_create_reserved), where the faithful chain's "
+                        "single-workgroup kernels then start without waiting for a CU to drain")
     p.add_argument("--fuse", type=int, default=2,
                    help="2: step k's pass-1 kernel also tilts step k-2 and forms step k-3's OPD maps (their loads "
                         "hidden behind the chain's FP64 arithmetic), step k-3's pupil / PSF on the back stream; "
@@ -596,6 +600,13 @@ def main():
     from akbraytracing_amd.wavefront import RayWave, Shard, SystemGeometry
 
     dev = torch.device("cuda", torch.cuda.current_device())
+    if args.reserve_cus:
+        import akbraytracing_amd
+        from akbraytracing_amd import _lib
+        L = akbraytracing_amd.lib()
+        sp = ctypes.c_void_p()
+        _lib.check(L.akb_stream_create_reserved(args.reserve_cus, ctypes.byref(sp)))
+        torch.cuda.set_stream(torch.cuda.ExternalStream(sp.value, device=dev))
     gdict = geometry_dict(args.config)
     geom = SystemGeometry.from_dict(gdict)
     if args.rays is None:

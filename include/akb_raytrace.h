@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define AKB_ABI_VERSION 16
+#define AKB_ABI_VERSION 17
 
 /* status codes */
 #define AKB_OK 0
@@ -70,6 +70,12 @@ int akb_abi_version(void);
 const char* akb_sources_hash(void);
 /* number of visible HIP devices (0 on a host without GPU; never fails) */
 int akb_device_count(void);
+/* a stream on the current device whose kernels leave `reserve` CUs (0, 8, 16, 24 or 32; the same
+ * number on every XCD) to the device's other streams: the trace's passes run on it so that the
+ * faithful chain's single-workgroup kernels find a free CU at once instead of waiting for one to
+ * drain of pass workgroups. *stream receives the hipStream_t; release it with akb_stream_destroy. */
+int akb_stream_create_reserved(int reserve, void** stream);
+int akb_stream_destroy(void* stream);
 
 /* ---------------- stage primitives (drop-in boundary, one reference call each) ---------------- */
 
@@ -527,15 +533,18 @@ int akb_gd_eval_f64(const double* x, const double* y, int nv, int nh, const uint
  * atomic max): [0] the largest change measure (scipy's) one more sweep would make at the interior
  * target cells' corners, [1] the largest value-error estimate of an interior target cell (2 sqrt 2 x
  * the corners' largest |one more plain sweep - x_K| x the cell's longest side or diagonal: the map
- * units' bound on |value - the converged iteration's value| with the Jacobi spectrum in [-1/2, 1/2];
- * the boundary-band targets are not covered). Replaces the gradient loop of scipy's
+ * units' bound on |value - the converged iteration's value| with the Jacobi spectrum in [-1/2, 1/2]),
+ * maxed with the boundary-band and pocket targets' own estimate (twice the value change one more plain
+ * band sweep makes there, k_gd_eval; a NaN estimate is stored as +inf). Replaces the gradient loop of scipy's
  * estimate_gradients_2d_global
  * (scipy/interpolate/_interpnd.pyx) where the driver's griddata (AKB_raytrace_20250312.py:3689)
  * feeds a fixed-size pupil. */
 int64_t akb_gd_cone_work_bytes(int nv, int nh, int mx, int my, int nvals);
 /* Diagnostics of the cone solve's patch kernel (k_gd_cone_patch), for bench.py's roofline:
  * akb_gd_patch_timing(1) records HIP events around every patch launch from then on (the last 1024
- * launches kept; 0 stops and keeps the record, 1 starts a new one); akb_gd_patch_times waits for them and writes up
+ * launches kept; 0 stops and keeps the record, 1 starts a new one; 2 also clocks every band sweep
+ * workgroup - device atomics in each, which lengthen the step: never inside a timed region);
+ * akb_gd_patch_times waits for them and writes up
  * to max launch durations (ms, oldest first) and, when cells != NULL, each launch's interior target
  * cell count; returns how many (or a negative AKB error code). */
 int akb_gd_patch_timing(int enable);
