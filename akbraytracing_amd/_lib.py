@@ -31,7 +31,7 @@ FLAG_CHAIN_DIR = 1 << 28
 # every symbol the header declares (tests check the library exports all of them)
 EXPORTS = [
     "akb_last_error", "akb_abi_version", "akb_sources_hash", "akb_device_count",
-    "akb_stream_create_reserved", "akb_stream_destroy",
+    "akb_stream_create_reserved", "akb_stream_destroy", "akb_reserved_cu_mask",
     "akb_isect_f64", "akb_normal_f64", "akb_reflect_f64", "akb_normalize_f64", "akb_plane_isect_f64",
     "akb_seglen_f64", "akb_rotate_f64", "akb_fill_nan_f64",
     "akb_trace_chain_f64", "akb_chain_desc_size", "akb_tilt_opd_f64", "akb_tilt_params_f64",
@@ -106,6 +106,7 @@ def _declare(L):
         "akb_device_count": ([], c_int),
         "akb_stream_create_reserved": ([c_int, c_vp], c_int),
         "akb_stream_destroy": ([c_vp], c_int),
+        "akb_reserved_cu_mask": ([c_int, c_int, c_vp], c_int),
         "akb_isect_f64": ([c_vp] + v3 + v3 + [c_int, c_i64, c_vp, c_i64, c_vp, c_vp], c_int),
         "akb_normal_f64": ([c_vp] + v3 + [c_i64, c_vp, c_i64, c_int, c_vp, c_vp], c_int),
         "akb_reflect_f64": (v3 + v3 + [c_i64, c_vp, c_i64, c_int, c_vp, c_vp], c_int),

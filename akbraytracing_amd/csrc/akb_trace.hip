@@ -1437,31 +1437,69 @@ int akb_device_count(void) {
     return n;
 }
 
+int akb_reserved_cu_mask(int reserve, int ncu, uint32_t* mask) {
+    clear_error();
+    AKB_REQUIRE(mask, "null pointer");
+    AKB_REQUIRE(ncu >= 256 && ncu % 32 == 0, "CU count not a multiple of 32 of at least 256");
+    AKB_REQUIRE(reserve >= 0 && reserve <= 128 && reserve % 8 == 0, "reserve must be a multiple of 8 up to 128");
+    for (int w = 0; w < ncu / 32; ++w) mask[w] = 0xffffffffu;
+    // bits x*32 + (x + o_k) % 32 (x < 8, k < reserve/8, fixed offsets o_k = 8 (k % 4) + k / 4):
+    // per XCD the same count whether the driver maps mask bits to XCDs in blocks of 32 or
+    // round-robin (bit % 8): over x, (x + o_k) % 8 takes every residue once
+    for (int x = 0; x < 8; ++x)
+        for (int k = 0; k < reserve / 8; ++k) {
+            const int b = x * 32 + (x + 8 * (k % 4) + k / 4) % 32;
+            mask[b / 32] &= ~(1u << (b % 32));
+        }
+    return AKB_OK;
+}
+
+}  // extern "C"
+
+namespace {
+// reserved streams still alive: destroyed when the library unloads (the C runtime's exit, after
+// the interpreter's own teardown has freed every tensor that recorded work on them, and before
+// the HIP runtime's teardown, which this library depends on and so outlives it)
+struct ReservedStreams {
+    std::vector<hipStream_t> live;
+    ~ReservedStreams() {
+        for (hipStream_t s : live) (void)hipStreamDestroy(s);
+    }
+};
+ReservedStreams& reserved_streams() {
+    static ReservedStreams r;
+    return r;
+}
+}  // namespace
+
+extern "C" {
+
 int akb_stream_create_reserved(int reserve, void** stream) {
     clear_error();
     AKB_REQUIRE(stream, "null pointer");
-    AKB_REQUIRE(reserve >= 0 && reserve <= 32 && reserve % 8 == 0, "reserve must be 0, 8, 16, 24 or 32");
     int dev = 0, ncu = 0;
     AKB_HIP_CHECK(hipGetDevice(&dev));
     AKB_HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-    AKB_REQUIRE(ncu >= 64 && ncu % 32 == 0, "CU count not a multiple of 32");
-    std::vector<uint32_t> mask((size_t)ncu / 32, 0xffffffffu);
-    // bit x*32 + x + 8k (x < 8, k < reserve/8): per XCD the same count whether the driver maps
-    // mask bits to XCDs in blocks of 32 or round-robin (bit % 8)
-    for (int x = 0; x < 8; ++x)
-        for (int k = 0; k < reserve / 8; ++k) {
-            const int b = x * 32 + x + 8 * k;
-            mask[b / 32] &= ~(1u << (b % 32));
-        }
+    AKB_REQUIRE(ncu >= 256 && ncu % 32 == 0, "CU count not a multiple of 32 of at least 256");
+    std::vector<uint32_t> mask((size_t)ncu / 32);
+    if (int st = akb_reserved_cu_mask(reserve, ncu, mask.data())) return st;
     hipStream_t st = nullptr;
     AKB_HIP_CHECK(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
+    reserved_streams().live.push_back(st);
     *stream = st;
     return AKB_OK;
 }
 
 int akb_stream_destroy(void* stream) {
     clear_error();
-    if (stream) AKB_HIP_CHECK(hipStreamDestroy((hipStream_t)stream));
+    if (!stream) return AKB_OK;
+    auto& v = reserved_streams().live;
+    for (size_t i = 0; i < v.size(); ++i)
+        if (v[i] == (hipStream_t)stream) {
+            v.erase(v.begin() + (int64_t)i);
+            break;
+        }
+    AKB_HIP_CHECK(hipStreamDestroy((hipStream_t)stream));
     return AKB_OK;
 }
 

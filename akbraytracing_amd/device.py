@@ -2,6 +2,7 @@
 
 All hot-path data is float64 struct-of-arrays, (3, N) row-major, like the reference's arrays.
 """
+import atexit
 import ctypes
 import threading
 import time
@@ -30,6 +31,29 @@ def stream_handle(stream=None):
         return stream
     s = stream if stream is not None else torch.cuda.current_stream()
     return ctypes.c_void_p(s.cuda_stream)
+
+
+def reserved_stream(reserve, dev=None):
+    """A torch stream whose kernels leave `reserve` CUs (a multiple of 8, the same number on every
+    XCD) to the device's other streams (akb_stream_create_reserved). The trace's passes run on it
+    so the faithful chain's single-workgroup kernels on the back stream start on a free CU instead
+    of waiting for one to drain of pass workgroups. It lives until the library unloads: tensors
+    freed during the interpreter's teardown may still record events on it."""
+    require_gpu()
+    dev = dev if dev is not None else device()
+    L = _lib.lib()
+    sp = ctypes.c_void_p()
+    _lib.check(L.akb_stream_create_reserved(int(reserve), ctypes.byref(sp)))
+    atexit.register(_quiesce_reserved, dev)
+    return torch.cuda.ExternalStream(sp.value, device=dev)
+
+
+def _quiesce_reserved(dev):
+    try:
+        torch.cuda.synchronize(dev)
+        torch.cuda.set_stream(torch.cuda.default_stream(dev))
+    except Exception:  # exit path: never mask the process's own status
+        pass
 
 
 def ptr(t):

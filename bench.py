@@ -97,10 +97,11 @@ def parse():
                         "next step's FP64-bound pass 1 (0: behind it on one stream)")
     p.add_argument("--back-priority", type=int, default=0,
                    help="torch stream priority of the back stream (lower = higher priority; 0 = normal)")
-    p.add_argument("--reserve-cus", type=int, default=0,
-                   help="CUs (0, 8, 16, 24, 32: the same number on every XCD) the main stream's passes leave "
+    p.add_argument("--reserve-cus", type=int, default=None,
+                   help="CUs (a multiple of 8 up to 128, the same number on every XCD) the main stream's passes leave "
                         "to the other streams (akb_stream_create_reserved), where the faithful chain's "
-                        "single-workgroup kernels then start without waiting for a CU to drain")
+                        "single-workgroup kernels then start without waiting for a CU to drain (default 40 at "
+                        "N = 1, measured best of 0..96; 0 at N > 1, unmeasured there)")
     p.add_argument("--fuse", type=int, default=2,
                    help="2: step k's pass-1 kernel also tilts step k-2 and forms step k-3's OPD maps (their loads "
                         "hidden behind the chain's FP64 arithmetic), step k-3's pupil / PSF on the back stream; "
@@ -124,6 +125,20 @@ def parse():
                    help="side-stream PSF starts as soon as the previous pupil is ready, beside pass 1 "
                         "(default; measured faster), or after this step's pass 1")
     return p.parse_args()
+
+
+def workload_label(config, world, faithful):
+    """config.workload: the configuration, what a step runs, and the pupil route"""
+    pupil = (" + the reference's pupil (griddata cubic, nanmean, plane correction, psf_calc)"
+             + (" sharded with the rays" if world > 1 else "")) if faithful else ""
+    shards = ", ray-row shards" if world > 1 else ""
+    if config == "c2":
+        return f"C2: 2-mirror KB ray trace (2 passes, tilt, OPD){shards}{pupil} + 2048^2 PSF"
+    if config == "c3":
+        name = "C3" if world == 1 else "C4"
+        return f"{name}: 4-mirror AKB ray_wave trace (2 passes, tilt, OPD){shards}{pupil} + 2048^2 PSF"
+    return ("C5: 4-mirror AKB ray_wave trace with per-ray Legendre OPL perturbation" + shards + pupil
+            + " + 3-wavelength 2048^2 PSF stack")
 
 
 def geometry_dict(config):
@@ -600,13 +615,11 @@ def main():
     from akbraytracing_amd.wavefront import RayWave, Shard, SystemGeometry
 
     dev = torch.device("cuda", torch.cuda.current_device())
+    if args.reserve_cus is None:
+        args.reserve_cus = 40 if world == 1 else 0
     if args.reserve_cus:
-        import akbraytracing_amd
-        from akbraytracing_amd import _lib
-        L = akbraytracing_amd.lib()
-        sp = ctypes.c_void_p()
-        _lib.check(L.akb_stream_create_reserved(args.reserve_cus, ctypes.byref(sp)))
-        torch.cuda.set_stream(torch.cuda.ExternalStream(sp.value, device=dev))
+        from akbraytracing_amd.device import reserved_stream
+        torch.cuda.set_stream(reserved_stream(args.reserve_cus, dev))
     gdict = geometry_dict(args.config)
     geom = SystemGeometry.from_dict(gdict)
     if args.rays is None:
@@ -1030,19 +1043,7 @@ def main():
         "data": "synthetic: deterministic ray grid through the reference's "
                 + ("KB" if args.config == "c2" else "AKB") + " geometry (recorded fixture)",
         "config": {
-            "workload": ("C2: 2-mirror KB ray trace (2 passes, tilt, OPD) + 2048^2 PSF"
-                         + (", ray-row shards" if world > 1 else "") if args.config == "c2" else
-                         "C3: 4-mirror AKB ray_wave trace (2 passes, tilt, OPD) + the reference's pupil (griddata "
-                         "cubic, nanmean, plane correction, psf_calc) + 2048^2 PSF" if args.config == "c3"
-                         and world == 1 and faithful else
-                         "C3: 4-mirror AKB ray_wave trace (2 passes, tilt, OPD) + 2048^2 PSF" if args.config == "c3"
-                         and world == 1 else
-                         "C4: 4-mirror AKB ray_wave trace, ray-row shards, + the reference's pupil (griddata cubic, "
-                         "nanmean, plane correction, psf_calc) sharded with the rays + 2048^2 PSF"
-                         if args.config == "c3" and faithful else
-                         "C4: 4-mirror AKB ray_wave trace, ray-row shards, + 2048^2 PSF" if args.config == "c3" else
-                         "C5: 4-mirror AKB ray_wave trace with per-ray Legendre OPL perturbation + "
-                         "3-wavelength 2048^2 PSF stack"),
+            "workload": workload_label(args.config, world, faithful),
             "rays_per_gpu": rw.n_local, "rays_total": n * n, "grid": n, "v_rows_per_rank": round(shard.count / n, 1),
             "mirrors": len(geom.mirrors), "systems_cycled": len(systems),
             "intersections_per_step": 2 * len(geom.mirrors) * n * n,
@@ -1050,6 +1051,7 @@ def main():
                    "DFT (pruned)" + (f", wavelength-sharded over {min(world, len(lams))} ranks" if world > 1 and
                                      len(lams) > 1 else ""),
             "parallelism": f"ray-row shards x{world}",
+            "reserved_cus": args.reserve_cus,
         },
         # the host's share of a step (medians over the timed steps): its whole time per step, the part
         # blocked on the device (event waits) or on the pocket workers, and the rest - the host's own

@@ -70,11 +70,14 @@ int akb_abi_version(void);
 const char* akb_sources_hash(void);
 /* number of visible HIP devices (0 on a host without GPU; never fails) */
 int akb_device_count(void);
-/* a stream on the current device whose kernels leave `reserve` CUs (0, 8, 16, 24 or 32; the same
- * number on every XCD) to the device's other streams: the trace's passes run on it so that the
+/* a stream on the current device whose kernels leave `reserve` CUs (a multiple of 8 up to 128;
+ * the same number on every XCD) to the device's other streams: the trace's passes run on it so that the
  * faithful chain's single-workgroup kernels find a free CU at once instead of waiting for one to
- * drain of pass workgroups. *stream receives the hipStream_t; release it with akb_stream_destroy. */
+ * drain of pass workgroups. *stream receives the hipStream_t; release it with akb_stream_destroy
+ * (a stream still alive when the library unloads is destroyed then). */
 int akb_stream_create_reserved(int reserve, void** stream);
+/* the CU mask such a stream gets on a device of ncu CUs (ncu / 32 words; host only, no device call) */
+int akb_reserved_cu_mask(int reserve, int ncu, uint32_t* mask);
 int akb_stream_destroy(void* stream);
 
 /* ---------------- stage primitives (drop-in boundary, one reference call each) ---------------- */

@@ -406,6 +406,23 @@ def test_two_stream_pipeline_equals_sequential_runs(gpu, n):
         assert torch.equal(opd, want_opd)
 
 
+def test_reserved_cu_stream_gives_the_same_bits(gpu):
+    """bench.py's default at one GPU: the passes on a stream that leaves 40 CUs to the back stream
+    (akb_stream_create_reserved) - the same bits as on torch's default stream."""
+    from akbraytracing_amd.device import reserved_stream
+    from akbraytracing_amd.wavefront import RayWave
+    rw = RayWave(_geom(), 1001)
+    seq = rw.run()
+    want = {k: seq[k].clone() for k in ("wave2", "dist_err2", "detcenter2")}
+    rs = reserved_stream(40)
+    with torch.cuda.stream(rs):
+        for _ in range(2):
+            out = rw.run()
+            for k, v in want.items():
+                assert torch.equal(out[k], v), k
+    torch.cuda.synchronize()
+
+
 @pytest.mark.parametrize("n", [65, 1001])
 def test_fused_pipeline_equals_sequential_runs(gpu, n):
     """bench.py's default pipeline: each run's tilt inside the next run's pass-1 kernel

@@ -63,6 +63,21 @@ def test_invalid_arguments_are_reported_not_crashed():
     assert L.akb_pairwise_work_bytes(3, 10_000_000) == 3 * 1221 * 16
 
 
+@pytest.mark.parametrize("reserve", [0, 8, 40, 64, 128])
+def test_reserved_cu_mask_is_even_over_xcds_under_either_bit_mapping(reserve):
+    from akbraytracing_amd import _lib
+    L = _lib.lib()
+    m = np.zeros(8, dtype=np.uint32)
+    assert L.akb_reserved_cu_mask(reserve, 256, m.ctypes.data) == 0
+    off = [b for b in range(256) if not (int(m[b // 32]) >> (b % 32)) & 1]
+    assert len(off) == reserve
+    per = reserve // 8
+    # blocks of 32 bits per XCD, or bit % 8 round-robin: the same count on each of the eight
+    assert all(sum(1 for b in off if b // 32 == x) == per for x in range(8))
+    assert all(sum(1 for b in off if b % 8 == x) == per for x in range(8))
+    assert L.akb_reserved_cu_mask(12, 256, m.ctypes.data) == -1
+
+
 def test_header_comments_cite_reference_lines():
     with open(os.path.join(ROOT, "include", "akb_raytrace.h")) as f:
         hdr = f.read()
