@@ -119,6 +119,9 @@ def parse():
     p.add_argument("--faithful-lag", type=int, default=None,
                    help="faithful runs in flight (begun, not finished) after each step: the oldest finishes once "
                         "more are (default 3; 6 at N > 1, where the band owner builds configs[3]'s 40k-point ring)")
+    p.add_argument("--step-log", action="store_true",
+                   help="add step_log to the line: per timed step, when its main-stream and back-stream work "
+                        "completed (ms after the region's start, device events) and its host time / wait")
     p.add_argument("--no-ramp-form", action="store_true",
                    help="skip the timed steps before the clock ramp (ms_per_step_no_ramp)")
     p.add_argument("--psf-start", choices=("pupil", "pass1"), default="pupil",
@@ -794,19 +797,35 @@ def main():
 
     from akbraytracing_amd import device as DEVM
 
+    step_log = []
+
     def timed_steps(k):
         comm.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         hm = []
+        evs = []
+        if args.step_log:
+            e_start = torch.cuda.Event(enable_timing=True)
+            e_start.record()
         for _ in range(k):
             h0, w0 = time.perf_counter(), DEVM.host_wait_s()
             step(True)
             # (host time issuing the step, of it blocked on events / the pocket job)
             hm.append(((time.perf_counter() - h0) * 1e3, (DEVM.host_wait_s() - w0) * 1e3))
+            if args.step_log:
+                em, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                em.record()
+                eb.record(back_stream)
+                evs.append((em, eb))
         torch.cuda.synchronize()
         comm.barrier()
-        return time.perf_counter() - t0, hm
+        el = time.perf_counter() - t0
+        if args.step_log:
+            step_log.clear()
+            step_log.extend([round(e_start.elapsed_time(em), 4), round(e_start.elapsed_time(eb), 4),
+                             round(h, 4), round(w, 4)] for (em, eb), (h, w) in zip(evs, hm))
+        return el, hm
 
     # first use of every kernel, the pocket workers and the pinned buffers of the chain, before any
     # step: one run and its faithful pupil on their own (outside every timed region; a fresh
@@ -1166,6 +1185,9 @@ def main():
             out["stage_api"] = stage
         if not args.no_extras and args.config == "c3":
             out["rank0_tail"] = rank0_tail()
+    if step_log:
+        out["step_log"] = {"columns": ["main_done_ms", "back_done_ms", "host_ms", "host_wait_ms"],
+                           "steps": step_log}
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, gdict)
     print(json.dumps(out), flush=True)
