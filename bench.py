@@ -882,6 +882,7 @@ def main():
     el, host_ms = timed_steps(args.steps)
     finishes_timed = (fp.finished - fin0) if fp is not None else None
     patch = None
+    patch_launch_ms = []
     if fp is not None and world == 1:
         LIBM.check(LIBM.lib().akb_gd_patch_timing(0))  # (stops new records; the queued ones still land)
         pms = (ctypes.c_float * 1024)()
@@ -895,6 +896,7 @@ def main():
             S = next(s2 for s2 in range((K + 1) // 2, K + 1)
                      if (W - 2) ** 2 + (W - 2 * s2 - 2) ** 2 + 4 <= 1024)
             patch = faithful_roofline(list(pms[:k]), int(pcells[k - 1]), K, S)
+            patch_launch_ms = list(pms[:k])
             ph = (ctypes.c_ulonglong * 10)()
             LIBM.check(LIBM.lib().akb_gd_patch_phases(ph))
             tot = ph[0] + ph[1] + ph[2]
@@ -1187,7 +1189,11 @@ def main():
             out["rank0_tail"] = rank0_tail()
     if step_log:
         out["step_log"] = {"columns": ["main_done_ms", "back_done_ms", "host_ms", "host_wait_ms"],
-                           "steps": step_log}
+                           "steps": step_log,
+                           # the same timed steps' kernels in launch order (HIP events)
+                           "pass1_ms": [round(a.elapsed_time(b), 4) for a, b, _, _ in (rw.pass1_events or [])],
+                           "pass2_ms": [round(a.elapsed_time(b), 4) for a, b in (rw.kernel_events or [])],
+                           "patch_ms": [round(float(x), 4) for x in patch_launch_ms]}
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, gdict)
     print(json.dumps(out), flush=True)
