@@ -366,8 +366,12 @@ __device__ __forceinline__ bool strip_edge_bad(double x0, double y0, double mxa,
                                                double oxa, double oya, double tol) {
     const double ax = mxa - x0, ay = mya - y0, cx = cxa - x0, cy = cya - y0;
     const double ox = oxa - x0, oy = oya - y0;
+    const double ic = incircle(0.0, 0.0, ax, ay, cx, cy, ox, oy);
+    // a non-positive (or NaN) in-circle value never exceeds a non-negative tolerance: the scale only
+    // where it can decide (almost never on a Delaunay lattice: its ten FP64 operations a test skipped)
+    if (tol >= 0.0 && !(ic > 0.0)) return false;
     const double sc = fmax(fmax(fabs(ax), fabs(ay)), fmax(fmax(fabs(cx), fabs(cy)), fmax(fabs(ox), fabs(oy))));
-    return incircle(0.0, 0.0, ax, ay, cx, cy, ox, oy) > tol * sc * sc * sc * sc;
+    return ic > tol * sc * sc * sc * sc;
 }
 
 // a cell's claims: its corners (p00, p01, p10, p11) in registers, d its diagonal, c its index
