@@ -1693,7 +1693,9 @@ inline int patch_order_upload() {
 // runs that cell's sweeps S + 1 .. K and its corners' output beside them. So every vertex's
 // constants are formed once per cell, and the late sweeps (a few waves each) never run alone.
 // A sweep's shrinking square is a prefix of each set's threads. Sweep 1 reads nothing: x_0 = 0
-// makes S = +0, the same bits as summing the zero iterate. A box whose cells all take the same
+// makes S = +0, the same bits as summing the zero iterate, so each fresh thread runs it right
+// after its constants, and the old set runs its sweep S + 1 (its own iterate only) during that
+// setup: the barrier-separated loop then holds max(S - 1, K - S - 1) sweeps. A box whose cells all take the same
 // diagonal (about two in three at C3) runs the sweeps over its six present slots (an absent
 // slot adds exact zeros, so the bits are the eight-slot sum's); a wave reads that from the
 // boxes' orientation words. Box sets of x, y, f rotate over two (cell p's, read by its setup;
@@ -1778,7 +1780,7 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch(Grid g, ConePatch a, int
         dep = min(min(r, c), min(W - 1 - r, W - 1 - c));
     }
     const int b = dep >= 1 ? r * P + c : P + 1;  // (idle threads: a harmless in-range base)
-    const int Q = max(S, K - S);
+    const int Q = max(S - 1, K - S - 1);  // the step loop's sweeps (sweeps 1 and S + 1 run beside the setup)
     const int count = *a.count;
     const int my = count > (int)blockIdx.x ? (count - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
     const double* const gx_ = g.x;
@@ -1861,6 +1863,27 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch(Grid g, ConePatch a, int
         }
         const bool fresh = role == 2 || role == s1;  // this step: cell p (sweeps 1 .. S), else cell p - 1
         const bool act = dep >= 1 && (fresh ? p < my : p >= 1);
+        double2(*const gg)[P * 32] = sg[fresh ? s1 : s1 ^ 1];  // this thread's cell's iterate pair
+        // sweep j at this thread's vertex, its form the host's steps: 1 plain (x_0 = 0: S = +0, no
+        // reads), 2 against x_0 = 0, later against x_{j-2}; w0 / w1: the wave's slot set is six slots
+        // (every active lane's box takes one diagonal throughout)
+        auto sweep = [&](int j, bool w0, bool w1) {
+            const double om = somg[j];
+            const int in = (j - 1) & 1, out = j & 1;
+            const double2 pv = j >= 3 ? gg[out][b] : make_double2(0.0, 0.0);  // x_{j-2}, overwritten
+            double s0 = 0.0, s1v = 0.0;
+            if (j >= 2) {
+                if (w0) patch_sums<kSlotsDiag0, P>(gg[in], b - P - 1, mxx, mxy, myy, s0, s1v);
+                else if (w1) patch_sums<kSlotsDiag1, P>(gg[in], b - P - 1, mxx, mxy, myy, s0, s1v);
+                else patch_sums<kSlotsAll, P>(gg[in], b - P - 1, mxx, mxy, myy, s0, s1v);
+            }
+            double y0, y1;
+            jacobi_y(kc, s0, s1v, y0, y1);
+            if (j == 1)
+                gg[out][b] = make_double2(y0, y1);
+            else
+                gg[out][b] = make_double2(__builtin_fma(om, y0 - pv.x, pv.x), __builtin_fma(om, y1 - pv.y, pv.y));
+        };
         if (act && fresh) {  // cell p's constants: the eight slots' M in the edge order, c and P
             const double* const sx = sxyf[s1][0];
             const double* const sy = sxyf[s1][1];
@@ -1872,13 +1895,21 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch(Grid g, ConePatch a, int
             const double xi = sx[b], yi = sy[b];
             const double fi[1] = {sf[b]}, zero[1] = {0.0};
             GradAcc<1> A;
+            // every slot's neighbour read up front (the box holds them all): one LDS latency for the
+            // eight, not one per present diagonal behind its branch
+            double nx[8], ny[8], nf[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                nx[k] = sx[b + off[k]];
+                ny[k] = sy[b + off[k]];
+                nf[k] = sf[b + off[k]];
+            }
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 mxx[k] = mxy[k] = myy[k] = 0.0;
                 if (!(em & (1u << k))) continue;
-                const int j = b + off[k];
-                const EdgeG e = edge_geom(sx[j] - xi, sy[j] - yi);
-                const double fj[1] = {sf[j]};
+                const EdgeG e = edge_geom(nx[k] - xi, ny[k] - yi);
+                const double fj[1] = {nf[k]};
                 acc_edge<1>(A, e, fi, fj, zero, zero);  // (its S part is not used: the sweeps form S)
                 mxx[k] = e.mxx;
                 mxy[k] = e.mxy;
@@ -1897,6 +1928,12 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch(Grid g, ConePatch a, int
                 };
                 shc[s1][role == 0 ? t : t - N2] = sqrt(fmax(fmax(l2(bq + dr), l2(bq + dc)), l2(bq + dr + dc)));
             }
+            sweep(1, false, false);  // reads nothing: no barrier between the constants and x_1
+        } else if (act && S < K) {
+            // the old set's first late sweep, S + 1, beside the setup (it reads only its own cell's
+            // iterate pair, complete since the last step's sweeps): the step loop then runs
+            // max(S - 1, K - S - 1) sweeps, one fewer than the two sets' sweep counts would need
+            sweep(S + 1, __ballot(ori != 1u) == 0, __ballot(ori != 2u) == 0);
         }
         // cell p + 1's box point through registers: issued after the setup (whose temporaries then
         // are dead), written to LDS after the sweeps, which hide its latency
@@ -1919,29 +1956,11 @@ __global__ void __launch_bounds__(1024) k_gd_cone_patch(Grid g, ConePatch a, int
             c1 = wall_clock64();
             c_setup += c1 - c0;
         }
-        double2(*const gg)[P * 32] = sg[fresh ? s1 : s1 ^ 1];  // this thread's cell's iterate pair
         // the wave's slot set: six slots when every active lane's box takes one diagonal throughout
         const bool w0 = __ballot(act && ori != 1u) == 0, w1 = __ballot(act && ori != 2u) == 0;
         for (int q = 1; q <= Q; ++q) {
-            const int j = fresh ? q : S + q;
-            if (act && dep >= j && j <= (fresh ? S : K)) {
-                // sweep j's form (the host's steps): 1 plain, 2 against x_0 = 0, later against x_{j-2}
-                const double om = somg[j];
-                const int in = (j - 1) & 1, out = j & 1;
-                const double2 pv = j >= 3 ? gg[out][b] : make_double2(0.0, 0.0);  // x_{j-2}, overwritten
-                double s0 = 0.0, s1v = 0.0;  // sweep 1: x_0 = 0, S = +0
-                if (j >= 2) {
-                    if (w0) patch_sums<kSlotsDiag0, P>(gg[in], b - P - 1, mxx, mxy, myy, s0, s1v);
-                    else if (w1) patch_sums<kSlotsDiag1, P>(gg[in], b - P - 1, mxx, mxy, myy, s0, s1v);
-                    else patch_sums<kSlotsAll, P>(gg[in], b - P - 1, mxx, mxy, myy, s0, s1v);
-                }
-                double y0, y1;
-                jacobi_y(kc, s0, s1v, y0, y1);
-                if (j == 1)  // (a branch: only the first sweep's step takes it, and then the whole wave)
-                    gg[out][b] = make_double2(y0, y1);
-                else
-                    gg[out][b] = make_double2(__builtin_fma(om, y0 - pv.x, pv.x), __builtin_fma(om, y1 - pv.y, pv.y));
-            }
+            const int j = fresh ? q + 1 : S + 1 + q;
+            if (act && dep >= j && j <= (fresh ? S : K)) sweep(j, w0, w1);
             asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         }
         if (clk) {
