@@ -46,7 +46,7 @@ EXPORTS = [
     "akb_first_valid_rows_f64", "akb_rotate_work_bytes", "akb_rotate_with_nan_f64", "akb_pupil_post_f64", "akb_pupil_post_work_bytes",
     "akb_moments_work_bytes", "akb_map_moments_f64", "akb_plane_subtract_f64", "akb_legendre_rows_f64",
     "akb_gd_cells_f64", "akb_gd_pockets", "akb_gd_check_pockets", "akb_gd_grad_sweeps_f64",
-    "akb_gd_eval_f64", "akb_gd_cone_work_bytes", "akb_gd_patch_timing", "akb_gd_patch_times", "akb_gd_band_times", "akb_gd_patch_phases", "akb_gd_cone_eval_f64", "akb_gd_axes_f64",
+    "akb_gd_eval_f64", "akb_gd_cone_work_bytes", "akb_gd_patch_timing", "akb_gd_patch_times", "akb_gd_band_times", "akb_gd_patch_phases", "akb_gd_patch_order", "akb_gd_cone_eval_f64", "akb_gd_axes_f64",
     "akb_gd_cells_claims_f64", "akb_gd_claim_pockets_f64", "akb_gd_cone_solve_f64",
     "akb_gd_claims_f64", "akb_gd_cone_part_f64", "akb_gd_part_finish_f64", "akb_gd_ring_f64", "akb_gd_cells_window_f64",
     "akb_trace_chain_batch_f64", "akb_focus_eval_work_bytes", "akb_focus_eval_f64", "akb_sep_search_f64",
@@ -187,6 +187,7 @@ def _declare(L):
                              c_vp, c_vp, c_int, c_vp, c_vp, c_vp], c_int),
         "akb_gd_cone_work_bytes": ([c_int, c_int, c_int, c_int, c_int], c_i64),
         "akb_gd_patch_timing": ([c_int], c_int),
+        "akb_gd_patch_order": ([c_int, c_vp], c_int),
         "akb_gd_patch_times": ([c_vp, c_vp, c_int], c_int),
         "akb_gd_band_times": ([c_vp, c_int], c_int),
         "akb_gd_patch_phases": ([c_vp], c_int),

@@ -3224,6 +3224,15 @@ int akb_gd_patch_timing(int enable) {
     return 0;
 }
 
+int akb_gd_patch_order(int K, uint16_t* out) {
+    clear_error();
+    AKB_REQUIRE(out && K >= 1 && K <= kConeMaxK, "K in 1 .. 14 and an output of 1024 entries");
+    const int S = patch_split(K);
+    AKB_REQUIRE(S >= 0, "no thread split for this K");
+    patch_order_table(K, S, out);
+    return S;
+}
+
 int akb_gd_patch_phases(unsigned long long* out) {
     clear_error();
     PatchTimer& t = patch_timer();

@@ -561,6 +561,12 @@ int akb_gd_band_times(float* ms, int max);
  * the band sweeps' ring-only workgroups' time and count, their workgroups with a tile (and a share
  * of the ring) time and count, the longest of each */
 int akb_gd_patch_phases(unsigned long long* out);
+/* The patch kernel's thread -> box vertex table for K sweeps (host only, no device call): out[t] =
+ * r | c << 8 of thread t's vertex in the (2K + 4)^2 box, 0xffff for the corner-store and idle
+ * threads; writes 1024 entries and returns the kernel's split S (the thread sets: inner A = [0, N2),
+ * inner B = [N2, 2 N2), outer = [2 N2, N1 + N2) with N1 = (2K + 2)^2, N2 = (2K + 2 - 2S)^2), or a
+ * negative AKB error code for K outside 1 .. 14. */
+int akb_gd_patch_order(int K, uint16_t* out);
 /* The driver's target axes (AKB_raytrace_20250312.py:3654-3657): gx = np.linspace(min, max, mx) of
  * the lattice's x (its extremes lie on the boundary ring akb_gd_cells_f64 returns), gy likewise of
  * y; d_extent (or NULL, 6 doubles): [min x, max x, min y, max y, dx, dy] with dx = |gh[0,1] - gh[0,0]|,
