@@ -1270,6 +1270,11 @@ __global__ void __launch_bounds__(1024) k_psf_bound_rows2(PsfLineArgs A) {
     if (threadIdx.x == 0) A.cand_n[b] = cnt;
 }
 
+#ifndef AKB_PSF_SEL_WGS
+#define AKB_PSF_SEL_WGS 128
+#endif
+constexpr int kSelPeakWgs = AKB_PSF_SEL_WGS;  // the select route's peak-pass grid (0: line_wgs)
+
 // persistent workgroups per pass: the resident count (LDS / threads) x 256 CUs, a multiple of 8
 template <int N, int PAD, typename R, int NT = LineShape<N, PAD>::kThreads>
 static int line_wgs(int ngroups) {
@@ -1290,7 +1295,13 @@ static int launch_psf_line(PsfLineArgs fa, int nlines, int batch, hipStream_t s)
     using R = typename std::conditional<MODE == kLinePeak32, float, double>::type;
     fa.ngroups = (nlines + S::LINES - 1) / S::LINES;
     using T = LineThreads<N, PAD, MODE>;
-    k_psf_line<N, PAD, MODE><<<dim3(line_wgs<N, PAD, R, T::kThreads>(fa.ngroups), batch), T::kThreads, 0, s>>>(fa);
+    int wgs = line_wgs<N, PAD, R, T::kThreads>(fa.ngroups);
+    // the select route's peak pass: most of its workgroups only sum the bounds of their few rows
+    // and leave (a focused PSF's peak rows are a handful), yet each needs a CU slot with its LDS
+    // while the trace passes hold the CUs; a small grid (a multiple of 8: the XCD shares) takes
+    // the slots the chain's reserved CUs have in one round
+    if (MODE == kLinePeak && fa.bpart && !fa.cand && kSelPeakWgs > 0 && wgs > kSelPeakWgs) wgs = kSelPeakWgs;
+    k_psf_line<N, PAD, MODE><<<dim3(wgs, batch), T::kThreads, 0, s>>>(fa);
     return launch_status(MODE == kLinePupil  ? "k_psf_line(pupil)"
                          : MODE == kLinePeak32 ? "k_psf_line(peak32)"
                          : MODE == kLinePeak   ? "k_psf_line(peak)"
