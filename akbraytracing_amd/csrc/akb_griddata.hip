@@ -354,8 +354,11 @@ __device__ __forceinline__ int strip_diag(const StripRow& a, const StripRow& b, 
     const double dx = b.x - x0, dy = b.y - y0;
     const double ic = incircle(0.0, 0.0, bx, by, cx, cy, dx, dy);
     const int d = ic > 0 ? 1 : 0;
-    const double sgn = d == 0 ? orient(0, 0, bx, by, cx, cy) * orient(0, 0, cx, cy, dx, dy)
-                              : orient(0, 0, bx, by, dx, dy) * orient(bx, by, cx, cy, dx, dy);
+    // d = 0: orient(0, b, c) orient(0, c, d); d = 1: orient(0, b, d) orient(b, c, d) - one form with
+    // its inputs selected (x - 0.0 is x bit for bit), two orientations a cell instead of four
+    const double px = d == 0 ? cx : dx, py = d == 0 ? cy : dy;
+    const double ox = d == 0 ? 0.0 : bx, oy = d == 0 ? 0.0 : by;
+    const double sgn = (bx * py - by * px) * ((cx - ox) * (dy - oy) - (cy - oy) * (dx - ox));
     viol = sgn > 0 ? 0.0 : 1.0;
     return d;
 }
@@ -380,15 +383,23 @@ __device__ __forceinline__ bool strip_edge_bad(double x0, double y0, double mxa,
 __device__ __forceinline__ void strip_claims(const Targets& t, int* owner, bool uniform, double inv_dx, double inv_dy,
                                              double ax0, double ay0, const double (&vx)[4], const double (&vy)[4], int d,
                                              int64_t c) {
-    const double xlo = fmin(fmin(vx[0], vx[1]), fmin(vx[2], vx[3])), xhi = fmax(fmax(vx[0], vx[1]), fmax(vx[2], vx[3]));
     const double ylo = fmin(fmin(vy[0], vy[1]), fmin(vy[2], vy[3])), yhi = fmax(fmax(vy[0], vy[1]), fmax(vy[2], vy[3]));
-    const double padx = (xhi - xlo) * 1e-9, pady = (yhi - ylo) * 1e-9;
+    const double pady = (yhi - ylo) * 1e-9;
     int c0, c1, r0, r1;
     bool hit;
-    if (uniform) {  // the rows first: a target row meets one cell row in ~25 at C3, so most waves skip the rest
-        hit = axis_range_at(ay0, t.my, inv_dy, ylo - pady, yhi + pady, r0, r1) &&
-              axis_range_at(ax0, t.mx, inv_dx, xlo - padx, xhi + padx, c0, c1);
+    if (uniform) {  // the rows first: a target row meets one cell row in ~25 at C3, so most waves skip the
+                    // rest, the x extent included
+        hit = axis_range_at(ay0, t.my, inv_dy, ylo - pady, yhi + pady, r0, r1);
+        if (hit) {
+            const double xlo = fmin(fmin(vx[0], vx[1]), fmin(vx[2], vx[3]));
+            const double xhi = fmax(fmax(vx[0], vx[1]), fmax(vx[2], vx[3]));
+            const double padx = (xhi - xlo) * 1e-9;
+            hit = axis_range_at(ax0, t.mx, inv_dx, xlo - padx, xhi + padx, c0, c1);
+        }
     } else {
+        const double xlo = fmin(fmin(vx[0], vx[1]), fmin(vx[2], vx[3]));
+        const double xhi = fmax(fmax(vx[0], vx[1]), fmax(vx[2], vx[3]));
+        const double padx = (xhi - xlo) * 1e-9;
         c0 = lower_idx(t.gx, t.mx, xlo - padx);
         c1 = lower_idx(t.gx, t.mx, xhi + padx);
         r0 = lower_idx(t.gy, t.my, ylo - pady);
