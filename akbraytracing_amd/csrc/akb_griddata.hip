@@ -26,6 +26,7 @@
 #include <stdio.h>
 
 #include <algorithm>
+#include <mutex>
 #include <type_traits>
 
 #include "akb_common.h"
@@ -1676,18 +1677,35 @@ inline int patch_split(int K) {
     return -1;
 }
 
-// every K's table into constant memory, once per process (before the first patch launch)
-inline int patch_order_upload() {
-    static int status = [] {
-        static uint16_t tab[kConeMaxK + 1][1024];
+// every K's table into the constant memory of the device stream s runs on, once per device and
+// process (before that device's first patch launch: a module's constant memory is per device, and
+// the thread-per-GPU callers run the solve on several devices from one process)
+inline int patch_order_upload(hipStream_t s) {
+    static std::mutex mu;
+    static uint16_t tab[kConeMaxK + 1][1024];
+    static bool built = false;
+    static uint64_t done = 0;  // devices (bit d) whose copy holds the tables
+    int dev = 0, cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess) return 1;
+    dev = cur;
+    if (s != nullptr && hipStreamGetDevice(s, &dev) != hipSuccess) return 1;
+    if (dev < 0 || dev >= 64) return 1;
+    std::lock_guard<std::mutex> lk(mu);
+    if ((done >> dev) & 1u) return 0;
+    if (!built) {
         for (int K = 0; K <= kConeMaxK; ++K) {
             const int S = K >= 1 ? patch_split(K) : -1;
             if (S >= 0) patch_order_table(K, S, tab[K]);
             else std::fill(tab[K], tab[K] + 1024, (uint16_t)0xffff);
         }
-        return hipMemcpyToSymbol(HIP_SYMBOL(c_patch_order), tab, sizeof(tab)) == hipSuccess ? 0 : 1;
-    }();
-    return status;
+        built = true;
+    }
+    if (dev != cur && hipSetDevice(dev) != hipSuccess) return 1;
+    const bool ok = hipMemcpyToSymbol(HIP_SYMBOL(c_patch_order), tab, sizeof(tab)) == hipSuccess;
+    if (dev != cur) (void)hipSetDevice(cur);
+    if (!ok) return 1;
+    done |= 1ull << dev;
+    return 0;
 }
 
 // The interior target cells' patches: one persistent workgroup per CU walks its cells as a
@@ -2995,7 +3013,7 @@ int cone_part(const Grid& g, const Targets& t, int64_t own0, int64_t own1, int b
     const int S = patch_split(K);
     const unsigned pp = gd_cu_count();  // one persistent workgroup per CU walks its cells
     AKB_REQUIRE(S >= 0 && m <= 1024 * (int64_t)pp, "cone patches: K or the target count out of range");
-    if (patch_order_upload()) {
+    if (patch_order_upload(s)) {
         set_error("cone patches: the vertex order table did not reach constant memory");
         return AKB_E_HIP;
     }
